@@ -1,0 +1,192 @@
+"""Builds the native pieces in-tree (no pip, no JIT cache; the .so files travel with
+the repo snapshot to the GPU box):
+
+* ``k8s_gpu_device_plugin_amd/_native*.so``   C++17 core (amdsmi backend, fixture
+  backend, xGMI allocator, protobuf hot paths, exporter, epoll httpd, inotify,
+  native HTTP/2 gRPC server) + pybind11 bindings, linked against ``libamd_smi``.
+* ``k8s_gpu_device_plugin_amd/ops/libamdgpu_canary.so``  HIP/CDNA4 health canary,
+  ``hipcc --offload-arch=gfx950``.
+* ``build/native_selftest[-asan|-tsan]``  standalone C++ self-test (no Python) for
+  sanitizer runs.
+
+Usage: ``python -m k8s_gpu_device_plugin_amd._build [--force] [--sanitize address|thread]``
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG_DIR)
+NATIVE_DIR = os.path.join(ROOT, "native")
+BUILD_DIR = os.path.join(ROOT, "build")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+OFFLOAD_ARCH = "gfx950"
+
+CORE_SOURCES = [
+    "common.cpp",
+    "fixture_backend.cpp",
+    "amdsmi_backend.cpp",
+    "allocator.cpp",
+    "device_table.cpp",
+    "health.cpp",
+    "telemetry.cpp",
+    "httpd.cpp",
+    "watch.cpp",
+]
+BINDING_SOURCES = ["bindings.cpp"]
+CANARY_SOURCE = os.path.join(PKG_DIR, "ops", "canary.hip")
+CANARY_LIB = os.path.join(PKG_DIR, "ops", "libamdgpu_canary.so")
+
+
+def native_ext_path() -> str:
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return os.path.join(PKG_DIR, "_native" + suffix)
+
+
+def _headers():
+    return [os.path.join(NATIVE_DIR, f) for f in os.listdir(NATIVE_DIR) if f.endswith(".h")]
+
+
+def _stale(target: str, deps) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def _run(cmd, what: str) -> None:
+    proc = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if proc.returncode != 0:
+        raise RuntimeError("%s failed (%d):\n%s\n%s" % (what, proc.returncode, " ".join(cmd), proc.stdout))
+
+
+def _cxx() -> str:
+    return os.environ.get("CXX", "g++")
+
+
+def _common_flags(sanitize: str | None):
+    flags = ["-std=c++17", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter", "-pthread",
+             "-I" + NATIVE_DIR, "-I" + os.path.join(ROCM, "include")]
+    if sanitize:
+        flags += ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=" + sanitize]
+        if sanitize == "address":
+            flags.append("-fsanitize=undefined")
+    else:
+        flags += ["-O2", "-g1"]
+    return flags
+
+
+def _link_libs():
+    return ["-L" + os.path.join(ROCM, "lib"), "-lamd_smi", "-Wl,-rpath," + os.path.join(ROCM, "lib"),
+            "-pthread"]
+
+
+def _compile_objects(sources, obj_dir, extra_flags, force, jobs):
+    os.makedirs(obj_dir, exist_ok=True)
+    hdrs = _headers()
+    todo, objs = [], []
+    for s in sources:
+        src = os.path.join(NATIVE_DIR, s)
+        obj = os.path.join(obj_dir, s.rsplit(".", 1)[0] + ".o")
+        objs.append(obj)
+        if force or _stale(obj, [src] + hdrs):
+            todo.append((src, obj))
+
+    def one(pair):
+        src, obj = pair
+        _run([_cxx()] + extra_flags + ["-c", src, "-o", obj], "compile " + os.path.basename(src))
+
+    if todo:
+        with concurrent.futures.ThreadPoolExecutor(max_workers=jobs) as ex:
+            list(ex.map(one, todo))
+    return objs, bool(todo)
+
+
+def build_native(force: bool = False, jobs: int | None = None, verbose: bool = True) -> str:
+    import pybind11
+
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    out = native_ext_path()
+    flags = _common_flags(None)
+    core_objs, core_changed = _compile_objects(CORE_SOURCES, os.path.join(BUILD_DIR, "obj"), flags, force, jobs)
+    py_flags = flags + ["-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"],
+                        "-fvisibility=hidden"]
+    bind_objs, bind_changed = _compile_objects(BINDING_SOURCES, os.path.join(BUILD_DIR, "obj_py"), py_flags,
+                                               force, jobs)
+    if force or core_changed or bind_changed or not os.path.exists(out):
+        tmp = out + ".tmp"
+        _run([_cxx(), "-shared", "-o", tmp] + bind_objs + core_objs + _link_libs(), "link _native")
+        os.replace(tmp, out)
+        if verbose:
+            print("built", os.path.relpath(out, ROOT))
+    return out
+
+
+def build_selftest(sanitize: str | None = None, force: bool = False) -> str:
+    """Standalone C++ self-test binary (optionally ASan+UBSan or TSan instrumented)."""
+    tag = {"address": "-asan", "thread": "-tsan", None: ""}[sanitize]
+    obj_dir = os.path.join(BUILD_DIR, "obj_selftest" + tag)
+    flags = _common_flags(sanitize)
+    objs, changed = _compile_objects(CORE_SOURCES + ["selftest.cpp"], obj_dir, flags, force,
+                                     min(8, os.cpu_count() or 4))
+    exe = os.path.join(BUILD_DIR, "native_selftest" + tag)
+    if force or changed or not os.path.exists(exe):
+        link = [_cxx()] + (["-fsanitize=" + sanitize] if sanitize else [])
+        if sanitize == "address":
+            link.append("-fsanitize=undefined")
+        _run(link + ["-o", exe] + objs + _link_libs(), "link selftest")
+    return exe
+
+
+def hipcc_path() -> str | None:
+    p = os.path.join(ROCM, "bin", "hipcc")
+    return p if os.path.exists(p) else shutil.which("hipcc")
+
+
+def build_canary(force: bool = False, verbose: bool = True) -> str:
+    """hipcc the CDNA4 health-canary kernel library for gfx950 only."""
+    hipcc = hipcc_path()
+    if hipcc is None:
+        raise RuntimeError("hipcc not found under %s/bin" % ROCM)
+    if force or _stale(CANARY_LIB, [CANARY_SOURCE]):
+        tmp = CANARY_LIB + ".tmp"
+        _run([hipcc, "--offload-arch=" + OFFLOAD_ARCH, "-O3", "-std=c++17", "-shared", "-fPIC",
+              "-Wall", "-o", tmp, CANARY_SOURCE], "hipcc canary")
+        os.replace(tmp, CANARY_LIB)
+        if verbose:
+            print("built", os.path.relpath(CANARY_LIB, ROOT))
+    return CANARY_LIB
+
+
+def build_all(force: bool = False) -> None:
+    build_native(force=force)
+    build_canary(force=force)
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--sanitize", choices=["address", "thread"], default=None,
+                    help="build the native self-test with a sanitizer instead")
+    ap.add_argument("--selftest", action="store_true", help="also build (and run) the native self-test")
+    ap.add_argument("--no-canary", action="store_true")
+    args = ap.parse_args(argv)
+    if args.sanitize or args.selftest:
+        exe = build_selftest(args.sanitize, force=args.force)
+        print("built", os.path.relpath(exe, ROOT))
+        r = subprocess.run([exe])
+        return r.returncode
+    build_native(force=args.force)
+    if not args.no_canary:
+        build_canary(force=args.force)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

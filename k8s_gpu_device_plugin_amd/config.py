@@ -1,0 +1,256 @@
+"""Configuration: YAML file + defaults + environment overrides, validated early.
+
+Reference: ``config/config.go:9-22`` (struct + viper defaults), ``config.yml:1-13``,
+``main.go:31-52`` (``--configFile`` flag, ``./<name>.yml`` lookup, non-fatal read
+error).  Kept: the same keys (``webListenAddress``, ``migStrategy``, ``benchmark``,
+``log.level``, ``log.fileDir``) and file lookup.  Fixed: D11 (code default listen
+address ``"9002"`` has no colon -> ``0.0.0.0:9100``), strategy validated at load
+time instead of deep inside device-map building (§5.6).  Added keys for the MI355X
+build (plugin dir, backend, partition/resource options, telemetry, health, servers).
+
+Environment overrides: ``AMDGPU_DP_<UPPER_SNAKE_KEY>`` for top-level scalars, e.g.
+``AMDGPU_DP_WEB_LISTEN_ADDRESS=127.0.0.1:0``, ``AMDGPU_DP_BACKEND=fixture``.
+"""
+from __future__ import annotations
+
+import copy
+import dataclasses
+import os
+import re
+from dataclasses import dataclass, field
+from typing import Any
+
+import yaml
+
+from .api import v1beta1
+
+STRATEGIES = ("none", "single", "mixed")
+
+
+@dataclass
+class LogConfig:
+    level: str = "debug"
+    fileDir: str = "./logs"
+    console: bool = True
+
+
+@dataclass
+class ResourceSpec:
+    pattern: str = "*"
+    name: str = "gpu"
+
+
+@dataclass
+class SharingConfig:
+    replicas: int = 1            # >1: advertise "<id>::<n>" time-sliced replicas
+    renameByDefault: bool = False  # rename amd.com/gpu -> amd.com/gpu.shared when shared
+
+
+@dataclass
+class TelemetryConfig:
+    enabled: bool = True
+    intervalMs: int = 1000
+
+
+@dataclass
+class HealthConfig:
+    enabled: bool = True
+    lostAfterFailures: int = 3
+    canary: bool = False          # run the HIP canary before advertising / after reset
+    canaryBytes: int = 256 << 20
+    rejectUnhealthyAllocate: bool = True
+
+
+@dataclass
+class HttpConfig:
+    threads: int = 2
+    accessLog: bool = True
+    server: str = "native"       # native | python
+
+
+@dataclass
+class GrpcConfig:
+    server: str = "native"       # native (C++ HTTP/2) | python (grpcio)
+    threads: int = 4
+
+
+@dataclass
+class Config:
+    webListenAddress: str = "0.0.0.0:9100"
+    migStrategy: str = "none"            # alias partitionStrategy (none|single|mixed)
+    benchmark: bool = False
+    benchmarkDir: str = ""
+    log: LogConfig = field(default_factory=LogConfig)
+    pluginDir: str = v1beta1.DEVICE_PLUGIN_PATH
+    backend: str = "auto"                 # auto | amdsmi | fixture
+    fixture: str = "2gpu_spx"             # builtin name or path, used by backend=fixture
+    devices: str = ""                     # physical GPU filter, e.g. "0-3" ("" = all)
+    resourcePrefix: str = "amd.com"
+    resources: list = field(default_factory=list)  # [ResourceSpec]
+    visibleDevicesEnv: str = "AMD_VISIBLE_DEVICES"
+    mountCardNodes: bool = False
+    cdi: bool = False
+    sharing: SharingConfig = field(default_factory=SharingConfig)
+    telemetry: TelemetryConfig = field(default_factory=TelemetryConfig)
+    health: HealthConfig = field(default_factory=HealthConfig)
+    http: HttpConfig = field(default_factory=HttpConfig)
+    grpc: GrpcConfig = field(default_factory=GrpcConfig)
+    retrySeconds: float = 30.0            # plugin start retry (plugin/manager.go:135-138)
+
+    @property
+    def strategy(self) -> str:
+        return self.migStrategy
+
+    @property
+    def kubelet_socket(self) -> str:
+        return os.path.join(self.pluginDir, v1beta1.KUBELET_SOCKET_NAME)
+
+    def listen_host_port(self) -> tuple[str, int]:
+        return split_host_port(self.webListenAddress)
+
+    def to_dict(self) -> dict:
+        return dataclasses.asdict(self)
+
+
+class ConfigError(ValueError):
+    pass
+
+
+def split_host_port(addr: str) -> tuple[str, int]:
+    addr = str(addr).strip()
+    m = re.fullmatch(r"\[?([^\]]*)\]?:(\d+)", addr)
+    if not m:
+        raise ConfigError("webListenAddress %r must be host:port (e.g. 0.0.0.0:9100)" % addr)
+    host = m.group(1) or "0.0.0.0"
+    return host, int(m.group(2))
+
+
+_NESTED = {"log": LogConfig, "sharing": SharingConfig, "telemetry": TelemetryConfig,
+           "health": HealthConfig, "http": HttpConfig, "grpc": GrpcConfig}
+
+
+def _ci_lookup(d: dict, name: str):
+    """viper/mapstructure match keys case-insensitively (§5.6)."""
+    for k, v in d.items():
+        if str(k).lower() == name.lower():
+            return True, v
+    return False, None
+
+
+def _coerce(value: Any, default: Any):
+    if isinstance(default, bool):
+        if isinstance(value, str):
+            return value.strip().lower() in ("1", "true", "yes", "on")
+        return bool(value)
+    if isinstance(default, int) and not isinstance(default, bool):
+        return int(value)
+    if isinstance(default, float):
+        return float(value)
+    if isinstance(default, str):
+        return str(value)
+    return value
+
+
+def from_dict(raw: dict | None) -> Config:
+    cfg = Config()
+    raw = raw or {}
+    if not isinstance(raw, dict):
+        raise ConfigError("config root must be a mapping")
+    found, ps = _ci_lookup(raw, "partitionStrategy")
+    if found and ps is not None:
+        raw = dict(raw)
+        raw["migStrategy"] = ps
+    for f in dataclasses.fields(Config):
+        found, v = _ci_lookup(raw, f.name)
+        if not found or v is None:
+            continue
+        if f.name in _NESTED:
+            sub = getattr(cfg, f.name)
+            if not isinstance(v, dict):
+                raise ConfigError("%s must be a mapping" % f.name)
+            for sf in dataclasses.fields(sub):
+                sfound, sv = _ci_lookup(v, sf.name)
+                if sfound and sv is not None:
+                    setattr(sub, sf.name, _coerce(sv, getattr(sub, sf.name)))
+        elif f.name == "resources":
+            specs = []
+            for item in v or []:
+                if not isinstance(item, dict) or "name" not in item:
+                    raise ConfigError("resources entries need {pattern, name}")
+                specs.append(ResourceSpec(pattern=str(item.get("pattern", "*")), name=str(item["name"])))
+            cfg.resources = specs
+        else:
+            setattr(cfg, f.name, _coerce(v, getattr(cfg, f.name)))
+    return cfg
+
+
+def apply_env(cfg: Config, environ=None) -> Config:
+    environ = os.environ if environ is None else environ
+    for f in dataclasses.fields(Config):
+        if f.name in _NESTED or f.name == "resources":
+            continue
+        env = "AMDGPU_DP_" + re.sub(r"(?<!^)(?=[A-Z])", "_", f.name).upper()
+        if env in environ:
+            setattr(cfg, f.name, _coerce(environ[env], getattr(cfg, f.name)))
+    for name in ("LOG_LEVEL", "LOG_FILE_DIR"):
+        if "AMDGPU_DP_" + name in environ:
+            val = environ["AMDGPU_DP_" + name]
+            if name == "LOG_LEVEL":
+                cfg.log.level = val
+            else:
+                cfg.log.fileDir = val
+    if "AMDGPU_DP_GRPC_SERVER" in environ:
+        cfg.grpc.server = environ["AMDGPU_DP_GRPC_SERVER"]
+    if "AMDGPU_DP_HTTP_SERVER" in environ:
+        cfg.http.server = environ["AMDGPU_DP_HTTP_SERVER"]
+    return cfg
+
+
+def validate(cfg: Config) -> Config:
+    cfg.migStrategy = str(cfg.migStrategy).strip().lower()
+    if cfg.migStrategy not in STRATEGIES:
+        raise ConfigError("invalid partition (MIG) strategy %r: want one of %s" % (cfg.migStrategy, STRATEGIES))
+    split_host_port(cfg.webListenAddress)
+    from .utils.log import parse_level
+    try:
+        parse_level(cfg.log.level)
+    except ValueError as e:
+        raise ConfigError(str(e)) from None
+    if cfg.backend not in ("auto", "amdsmi", "fixture"):
+        raise ConfigError("backend must be auto|amdsmi|fixture, got %r" % cfg.backend)
+    if cfg.sharing.replicas < 1:
+        raise ConfigError("sharing.replicas must be >= 1")
+    if cfg.grpc.server not in ("native", "python"):
+        raise ConfigError("grpc.server must be native|python")
+    if cfg.http.server not in ("native", "python"):
+        raise ConfigError("http.server must be native|python")
+    if cfg.telemetry.intervalMs < 10:
+        raise ConfigError("telemetry.intervalMs must be >= 10")
+    if not cfg.resourcePrefix or "/" in cfg.resourcePrefix:
+        raise ConfigError("resourcePrefix must be a DNS-like prefix without '/'")
+    return cfg
+
+
+def load(config_file: str | None = "config", search_dirs=(".",), environ=None, required: bool = False) -> Config:
+    """Loads ``<dir>/<config_file>.yml`` (reference lookup, ``main.go:39-41``), or an
+    explicit path when ``config_file`` has a ``.yml``/``.yaml`` suffix or a '/'.  A
+    missing file is not fatal (``main.go:42-45``) unless ``required``."""
+    raw: dict = {}
+    path = None
+    if config_file:
+        if config_file.endswith((".yml", ".yaml")) or os.sep in config_file:
+            candidates = [config_file]
+        else:
+            candidates = [os.path.join(d, config_file + ext) for d in search_dirs for ext in (".yml", ".yaml")]
+        for c in candidates:
+            if os.path.isfile(c):
+                path = c
+                break
+        if path is None and required:
+            raise ConfigError("config file not found: %s" % candidates)
+    if path:
+        with open(path, "r", encoding="utf-8") as f:
+            raw = yaml.safe_load(f) or {}
+    cfg = from_dict(copy.deepcopy(raw))
+    apply_env(cfg, environ)
+    return validate(cfg)

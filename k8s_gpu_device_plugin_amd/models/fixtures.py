@@ -1,0 +1,149 @@
+"""Hardware node models for the fixture backend (MI355X nodes without the hardware).
+
+An MI355X node (OAM, 8 GPUs) is a full xGMI mesh: each GPU has 7 links, one direct
+link to every peer.  Each GPU has 8 XCDs x 32 CUs and 288 GB HBM3E
+(MI355X_MICROARCH.md); compute partitioning splits the XCDs: SPX 1, DPX 2, QPX 4,
+CPX 8 partitions.  Memory partitioning is NPS1 or NPS2 on MI355X; the BASELINE config
+names "CPX+NPS4", so ``8gpu_cpx_nps4`` is modelled too, with its caps declared so the
+plugin's capability checks can be exercised (SURVEY.md §7.5 hard part 3).
+
+A node model is a plain dict (also loadable from JSON/YAML)::
+
+    {"gpus": [{"compute_partition": "CPX", "memory_partition": "NPS2",
+               "numa_node": 0, ...}, ...],
+     "links": {"type": "xgmi", "down": [[0, 5]]},
+     "events": [{"at": 2.0, "kind": "pre_reset", "gpu": 3}, ...],
+     "seed": 1}
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import yaml
+
+from .. import native
+
+PARTITIONS = {"SPX": 1, "DPX": 2, "TPX": 3, "QPX": 4, "CPX": 8}
+NPS_BITS = {"NPS1": 1, "NPS2": 2, "NPS4": 4, "NPS8": 8}
+MI355X_HBM_BYTES = 288 * 10**9
+MI355X_CUS = 256
+MI355X_NAME = "AMD Instinct MI355X"
+
+EVENT_KINDS = {
+    "pre_reset": "EVT_PRE_RESET", "post_reset": "EVT_POST_RESET",
+    "ecc_uncorrectable": "EVT_ECC_UNCORRECTABLE", "link_down": "EVT_LINK_DOWN",
+    "link_up": "EVT_LINK_UP", "thermal": "EVT_THERMAL", "vm_fault": "EVT_VM_FAULT",
+    "device_lost": "EVT_DEVICE_LOST", "device_recovered": "EVT_DEVICE_RECOVERED",
+}
+
+
+def fixture_uuid(seed: int, gpu: int) -> str:
+    return "%08x-0000-1000-80%02x-%012x" % (0x5a000000 + seed, gpu, 0x355000 + gpu)
+
+
+def mi355x_node(num_gpus: int = 8, compute: str = "SPX", memory: str = "NPS1", gpus_per_numa: int = 4,
+                nps_caps=("NPS1", "NPS2"), down_links=(), seed: int = 1, events=()) -> dict:
+    gpus = []
+    for g in range(num_gpus):
+        gpus.append({"compute_partition": compute, "memory_partition": memory,
+                     "numa_node": g // max(1, gpus_per_numa), "nps_caps": list(nps_caps)})
+    return {"gpus": gpus, "links": {"type": "xgmi", "down": [list(p) for p in down_links]},
+            "events": list(events), "seed": seed}
+
+
+BUILTIN = {
+    "1gpu_spx": lambda: mi355x_node(1),
+    "2gpu_spx": lambda: mi355x_node(2),
+    "4gpu_spx": lambda: mi355x_node(4),
+    "8gpu_spx_mesh": lambda: mi355x_node(8),
+    "8gpu_dpx_nps2": lambda: mi355x_node(8, "DPX", "NPS2"),
+    "8gpu_qpx_nps2": lambda: mi355x_node(8, "QPX", "NPS2"),
+    "8gpu_cpx_nps2": lambda: mi355x_node(8, "CPX", "NPS2"),
+    "8gpu_cpx_nps4": lambda: mi355x_node(8, "CPX", "NPS4", nps_caps=("NPS1", "NPS2", "NPS4")),
+    "8gpu_spx_degraded": lambda: mi355x_node(8, down_links=[(0, 5), (2, 3)]),
+}
+
+
+def load_model(spec) -> dict:
+    """``spec``: builtin name, path to .json/.yaml, or a dict."""
+    if isinstance(spec, dict):
+        return spec
+    if spec in BUILTIN:
+        return BUILTIN[spec]()
+    m = None
+    if isinstance(spec, str) and os.path.isfile(spec):
+        with open(spec, "r", encoding="utf-8") as f:
+            m = json.load(f) if spec.endswith(".json") else yaml.safe_load(f)
+    if m is None:
+        # "<n>gpu_<mode>_<nps>" shorthand, e.g. 3gpu_qpx_nps2
+        parts = str(spec).split("_")
+        if len(parts) >= 2 and parts[0].endswith("gpu") and parts[0][:-3].isdigit():
+            mode = parts[1].upper()
+            nps = parts[2].upper() if len(parts) > 2 else "NPS1"
+            if mode in PARTITIONS and nps in NPS_BITS:
+                return mi355x_node(int(parts[0][:-3]), mode, nps,
+                                   nps_caps=tuple(sorted({"NPS1", "NPS2", nps}, key=lambda s: NPS_BITS[s])))
+        raise ValueError("unknown fixture %r (builtins: %s)" % (spec, ", ".join(sorted(BUILTIN))))
+    return m
+
+
+def build_backend(spec):
+    """Creates a native FixtureBackend populated from a node model."""
+    n = native.load()
+    model = load_model(spec)
+    seed = int(model.get("seed", 1))
+    be = n.FixtureBackend(seed)
+    gpus = model.get("gpus", [])
+    render = 128
+    card = 0
+    for gi, g in enumerate(gpus):
+        info = n.GpuInfo()
+        info.uuid = g.get("uuid") or fixture_uuid(seed, gi)
+        info.bdf = g.get("bdf") or "0000:%02x:00.0" % (0x05 + 0x10 * gi)
+        info.market_name = g.get("name", MI355X_NAME)
+        info.gfx_target = g.get("gfx_target", "gfx950")
+        info.serial = g.get("serial", "FIXTURE%04d" % gi)
+        info.numa_node = int(g.get("numa_node", 0))
+        info.vram_total_bytes = int(g.get("vram_bytes", MI355X_HBM_BYTES))
+        info.compute_partition = str(g.get("compute_partition", "SPX")).upper()
+        info.memory_partition = str(g.get("memory_partition", "NPS1")).upper()
+        caps = 0
+        for c in g.get("nps_caps", ["NPS1", "NPS2"]):
+            caps |= {1: 1, 2: 2, 4: 4, 8: 8}[NPS_BITS[str(c).upper()]]
+        info.nps_caps = caps
+        info.num_compute_units = int(g.get("num_cus", MI355X_CUS))
+        nparts = int(g.get("num_partitions", PARTITIONS.get(info.compute_partition, 1)))
+        info.num_xgmi_links = max(0, len(gpus) - 1)
+        parts = []
+        for p in range(nparts):
+            pi = n.PartitionInfo()
+            pi.gpu = gi
+            pi.index = p
+            pi.uuid = info.uuid if nparts == 1 else "%s-%d" % (info.uuid, p)
+            pi.id = info.uuid if nparts == 1 else "%s-xcp%d" % (info.uuid, p)
+            pi.render_minor = render
+            pi.card_minor = card
+            pi.hip_id = gi * nparts + p
+            pi.hsa_id = gi * nparts + p
+            pi.kfd_node = 1 + gi * nparts + p
+            pi.numa_node = info.numa_node
+            pi.vram_bytes = info.vram_total_bytes // nparts
+            render += 1
+            card += 1
+            parts.append(pi)
+        info.partitions = parts
+        be.add_gpu(info)
+    links = model.get("links", {}) or {}
+    ltype = {"xgmi": n.LINK_XGMI, "pcie": n.LINK_PCIE}.get(str(links.get("type", "xgmi")).lower(), n.LINK_XGMI)
+    down = {tuple(sorted(p)) for p in links.get("down", [])}
+    for a in range(len(gpus)):
+        for b in range(a + 1, len(gpus)):
+            be.set_link(a, b, n.Link(type=ltype, hops=1, weight=15 if ltype == n.LINK_XGMI else 40,
+                                     up=(a, b) not in down, p2p=True))
+    for ev in model.get("events", []) or []:
+        kind = getattr(n, EVENT_KINDS[str(ev["kind"]).lower()])
+        be.schedule_event(float(ev.get("at", 0.0)),
+                          n.HwEvent(kind, int(ev.get("gpu", -1)), int(ev.get("partition", -1)),
+                                    int(ev.get("peer", -1)), str(ev.get("message", "scripted"))))
+    return be

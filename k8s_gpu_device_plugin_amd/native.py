@@ -1,0 +1,49 @@
+"""Loads the in-tree C++ core (``_native*.so``), building it first when it is missing
+or older than ``native/*.cpp|h`` (g++ is part of the plugin's build image).
+
+There is deliberately no pure-Python fallback for the core: if the extension cannot
+be loaded the plugin fails loudly (a silently slower or partial plugin is worse than a
+crash-looping DaemonSet pod that shows the error).
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import threading
+
+_lock = threading.Lock()
+_mod = None
+
+
+def _stale() -> bool:
+    from . import _build
+    so = _build.native_ext_path()
+    if not os.path.exists(so):
+        return True
+    if not os.path.isdir(_build.NATIVE_DIR):
+        return False  # installed without sources: use what ships
+    t = os.path.getmtime(so)
+    for f in os.listdir(_build.NATIVE_DIR):
+        if f.endswith((".cpp", ".h")) and f != "selftest.cpp":
+            if os.path.getmtime(os.path.join(_build.NATIVE_DIR, f)) > t:
+                return True
+    return False
+
+
+def load():
+    """Returns the ``_native`` module (building it if needed)."""
+    global _mod
+    if _mod is not None:
+        return _mod
+    with _lock:
+        if _mod is not None:
+            return _mod
+        if os.environ.get("AMDGPU_DP_NO_AUTOBUILD", "") not in ("1", "true") and _stale():
+            from . import _build
+            _build.build_native(verbose=False)
+        try:
+            _mod = importlib.import_module("k8s_gpu_device_plugin_amd._native")
+        except ImportError as e:  # pragma: no cover - exercised only on broken installs
+            raise RuntimeError("native core k8s_gpu_device_plugin_amd._native is not built/loadable: %s "
+                               "(run: python -m k8s_gpu_device_plugin_amd._build)" % e) from e
+        return _mod

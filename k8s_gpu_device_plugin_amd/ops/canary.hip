@@ -1,0 +1,270 @@
+// MI355X (gfx950 / CDNA4) partition health canary.
+//
+// The reference has no device-level health check at all: its health channel has no
+// producer (plugin/plugin.go:181, SURVEY.md defect D9).  Before a partition is
+// advertised (and after a GPU_POST_RESET) the plugin can run this canary on it, in a
+// short-lived child process so the plugin daemon itself never holds a HIP context:
+//
+//   1. HBM pattern test  - every 16-byte word gets an address-derived pattern
+//      (catches stuck bits and aliasing/addressing faults), written and read back
+//      with 16 B/lane vector accesses over a grid >> 256 CUs; mismatches are
+//      reduced per wave (64-lane shuffles) then per block in LDS, one atomic/block.
+//      Write and read passes are timed separately -> achieved HBM GB/s.
+//   2. MFMA exactness    - v_mfma_f32_32x32x16_bf16 on small-integer operands
+//      (exact in bf16 and fp32) checked lane-by-lane against a scalar reference
+//      using the documented gfx950 fragment maps (cdna_hip_programming.md §3).
+//   3. MFMA throughput   - register-resident 32x32x16 bf16 MFMA chains, 4 waves
+//      per block (one per SIMD), 8 blocks per CU -> dense bf16 TFLOP/s.
+//
+// C ABI for ctypes (k8s_gpu_device_plugin_amd/ops/canary.py).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+
+namespace {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ uint32_t mix32(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return static_cast<uint32_t>(x);
+}
+
+__device__ __forceinline__ uint4 pattern(uint64_t idx, uint32_t seed) {
+  const uint64_t b = (idx << 2) ^ (static_cast<uint64_t>(seed) << 40);
+  return make_uint4(mix32(b), mix32(b + 1), mix32(b + 2), mix32(b + 3));
+}
+
+__global__ void __launch_bounds__(256) hbm_write(uint4* __restrict__ buf, uint64_t n, uint32_t seed) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  // 4 independent 16 B stores in flight per lane per iteration
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    buf[i] = pattern(i, seed);
+    buf[i + stride] = pattern(i + stride, seed);
+    buf[i + 2 * stride] = pattern(i + 2 * stride, seed);
+    buf[i + 3 * stride] = pattern(i + 3 * stride, seed);
+  }
+  for (; i < n; i += stride) buf[i] = pattern(i, seed);
+}
+
+__device__ __forceinline__ uint32_t diff(const uint4& a, const uint4& b) {
+  return (a.x != b.x) + (a.y != b.y) + (a.z != b.z) + (a.w != b.w);
+}
+
+__global__ void __launch_bounds__(256) hbm_verify(const uint4* __restrict__ buf, uint64_t n, uint32_t seed,
+                                                  unsigned long long* __restrict__ errors) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  uint32_t bad = 0;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    const uint4 v0 = buf[i], v1 = buf[i + stride], v2 = buf[i + 2 * stride], v3 = buf[i + 3 * stride];
+    bad += diff(v0, pattern(i, seed)) + diff(v1, pattern(i + stride, seed)) + diff(v2, pattern(i + 2 * stride, seed)) +
+           diff(v3, pattern(i + 3 * stride, seed));
+  }
+  for (; i < n; i += stride) bad += diff(buf[i], pattern(i, seed));
+  // 64-lane wave reduction, then one LDS slot per wave, one atomic per block
+  for (int off = kWave / 2; off > 0; off >>= 1) bad += __shfl_down(bad, off, kWave);
+  __shared__ uint32_t wave_bad[256 / kWave];
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  if (lane == 0) wave_bad[wid] = bad;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < static_cast<int>(blockDim.x / kWave); ++w) t += wave_bad[w];
+    if (t) atomicAdd(errors, static_cast<unsigned long long>(t));
+  }
+}
+
+using bf16x8 = __attribute__((ext_vector_type(8))) short;
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+
+// small integer in [-4, 4] from a hash: exactly representable in bf16
+__device__ __forceinline__ int small_int(uint64_t key) { return static_cast<int>(mix32(key) % 9u) - 4; }
+
+__device__ __forceinline__ short bf16_of_int(int v) {
+  const float f = static_cast<float>(v);
+  uint32_t u;
+  __builtin_memcpy(&u, &f, 4);
+  return static_cast<short>(u >> 16);  // exact for small integers
+}
+
+__device__ __forceinline__ int a_val(uint32_t blk, int row, int k) {
+  return small_int((static_cast<uint64_t>(blk) << 40) ^ (static_cast<uint64_t>(row) << 20) ^ static_cast<uint64_t>(k));
+}
+__device__ __forceinline__ int b_val(uint32_t blk, int k, int col) {
+  return small_int(0x5555ull ^ (static_cast<uint64_t>(blk) << 40) ^ (static_cast<uint64_t>(k) << 20) ^
+                   static_cast<uint64_t>(col) ^ (1ull << 62));
+}
+
+// One wave per block computes C[32x32] = A[32xK] * B[Kx32] with K = 16 * ksteps, then
+// every lane checks its 16 accumulator registers against a scalar integer reference.
+__global__ void __launch_bounds__(64) mfma_exact(int ksteps, unsigned long long* __restrict__ errors) {
+  const int lane = threadIdx.x;
+  const int r = lane & 31, h = lane >> 5;
+  const uint32_t blk = blockIdx.x;
+  f32x16 acc;
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  for (int s = 0; s < ksteps; ++s) {
+    bf16x8 a, b;
+    for (int j = 0; j < 8; ++j) {
+      const int k = s * 16 + 8 * h + j;  // lane l holds A[r][8h+j], B[8h+j][r]
+      a[j] = bf16_of_int(a_val(blk, r, k));
+      b[j] = bf16_of_int(b_val(blk, k, r));
+    }
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+  }
+  uint32_t bad = 0;
+  const int col = lane & 31;
+  for (int reg = 0; reg < 16; ++reg) {
+    const int row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);  // C/D map of 32x32x16
+    int ref = 0;
+    for (int k = 0; k < ksteps * 16; ++k) ref += a_val(blk, row, k) * b_val(blk, k, col);
+    bad += acc[reg] != static_cast<float>(ref);
+  }
+  for (int off = kWave / 2; off > 0; off >>= 1) bad += __shfl_down(bad, off, kWave);
+  if (lane == 0 && bad) atomicAdd(errors, static_cast<unsigned long long>(bad));
+}
+
+// Throughput: register-resident operands, two independent accumulator chains per wave.
+__global__ void __launch_bounds__(256) mfma_rate(int iters, float* __restrict__ sink) {
+  const int lane = threadIdx.x & 63;
+  bf16x8 a, b;
+  for (int j = 0; j < 8; ++j) {
+    a[j] = bf16_of_int(((lane + j) % 5) - 2);
+    b[j] = bf16_of_int(((lane * 3 + j) % 7) - 3);
+  }
+  f32x16 acc0, acc1;
+  for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.f;
+  for (int it = 0; it < iters; ++it) {
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b, a, acc1, 0, 0, 0);
+  }
+  float s = 0.f;
+  for (int i = 0; i < 16; ++i) s += acc0[i] + acc1[i];
+  if (s == 1234.5f) sink[blockIdx.x * blockDim.x + threadIdx.x] = s;  // keeps the chain live
+}
+
+}  // namespace
+
+extern "C" {
+
+struct amdgpu_canary_result {
+  int ok;
+  int device;
+  unsigned long long hbm_bytes;
+  unsigned long long hbm_errors;
+  unsigned long long mfma_errors;
+  double write_gbps;
+  double read_gbps;
+  double mfma_tflops;
+  double elapsed_ms;
+  int num_cus;
+  char arch[64];
+  char error[256];
+};
+
+int amdgpu_canary_device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return -1;
+  return n;
+}
+
+#define CANARY_CHECK(expr)                                                                   \
+  do {                                                                                       \
+    hipError_t e_ = (expr);                                                                  \
+    if (e_ != hipSuccess) {                                                                  \
+      std::snprintf(out->error, sizeof(out->error), "%s: %s", #expr, hipGetErrorString(e_)); \
+      goto done;                                                                             \
+    }                                                                                        \
+  } while (0)
+
+// hbm_bytes: size of the pattern buffer (rounded down to 16 B); passes: timed
+// write+verify repetitions; mfma_iters: MFMA pairs per wave for the rate test.
+int amdgpu_canary_run(int device, unsigned long long hbm_bytes, int passes, int mfma_iters,
+                      amdgpu_canary_result* out) {
+  std::memset(out, 0, sizeof(*out));
+  out->device = device;
+  uint4* buf = nullptr;
+  unsigned long long* d_err = nullptr;
+  float* sink = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
+  hipDeviceProp_t prop;
+  const uint64_t n = hbm_bytes / sizeof(uint4);
+  unsigned long long h_err[2] = {0, 0};
+  float t_write = 0, t_read = 0, t_mfma = 0;
+  const int t0_dummy = 0;
+  (void)t0_dummy;
+  int blocks = 0;
+  CANARY_CHECK(hipSetDevice(device));
+  CANARY_CHECK(hipGetDeviceProperties(&prop, device));
+  out->num_cus = prop.multiProcessorCount;
+  std::snprintf(out->arch, sizeof(out->arch), "%s", prop.gcnArchName);
+  out->hbm_bytes = n * sizeof(uint4);
+  if (passes < 1) passes = 1;
+  CANARY_CHECK(hipMalloc(&buf, n * sizeof(uint4) + 16));
+  CANARY_CHECK(hipMalloc(&d_err, 2 * sizeof(unsigned long long)));
+  CANARY_CHECK(hipMemset(d_err, 0, 2 * sizeof(unsigned long long)));
+  CANARY_CHECK(hipEventCreate(&e0));
+  CANARY_CHECK(hipEventCreate(&e1));
+  CANARY_CHECK(hipEventCreate(&e2));
+  blocks = prop.multiProcessorCount * 8;  // >> #CUs, 8 blocks of 256 threads per CU
+  // warm-up (first-touch page mapping) outside the timed region
+  hipLaunchKernelGGL(hbm_write, dim3(blocks), dim3(256), 0, 0, buf, n, 0x1234u);
+  CANARY_CHECK(hipGetLastError());
+  CANARY_CHECK(hipDeviceSynchronize());
+  for (int p = 0; p < passes; ++p) {
+    const uint32_t seed = 0xA5A5u + p;
+    float tw = 0, tr = 0;
+    CANARY_CHECK(hipEventRecord(e0, 0));
+    hipLaunchKernelGGL(hbm_write, dim3(blocks), dim3(256), 0, 0, buf, n, seed);
+    CANARY_CHECK(hipEventRecord(e1, 0));
+    hipLaunchKernelGGL(hbm_verify, dim3(blocks), dim3(256), 0, 0, buf, n, seed, d_err);
+    CANARY_CHECK(hipEventRecord(e2, 0));
+    CANARY_CHECK(hipEventSynchronize(e2));
+    CANARY_CHECK(hipGetLastError());
+    CANARY_CHECK(hipEventElapsedTime(&tw, e0, e1));
+    CANARY_CHECK(hipEventElapsedTime(&tr, e1, e2));
+    t_write += tw;
+    t_read += tr;
+  }
+  // MFMA exactness: 2 * #CUs single-wave blocks, K = 16 * 32
+  hipLaunchKernelGGL(mfma_exact, dim3(prop.multiProcessorCount * 2), dim3(64), 0, 0, 32, d_err + 1);
+  CANARY_CHECK(hipGetLastError());
+  // MFMA rate
+  CANARY_CHECK(hipMalloc(&sink, static_cast<size_t>(prop.multiProcessorCount) * 8 * 256 * sizeof(float)));
+  hipLaunchKernelGGL(mfma_rate, dim3(prop.multiProcessorCount * 8), dim3(256), 0, 0, 16, sink);  // warm-up
+  CANARY_CHECK(hipEventRecord(e0, 0));
+  hipLaunchKernelGGL(mfma_rate, dim3(prop.multiProcessorCount * 8), dim3(256), 0, 0, mfma_iters, sink);
+  CANARY_CHECK(hipEventRecord(e1, 0));
+  CANARY_CHECK(hipEventSynchronize(e1));
+  CANARY_CHECK(hipGetLastError());
+  CANARY_CHECK(hipEventElapsedTime(&t_mfma, e0, e1));
+  CANARY_CHECK(hipMemcpy(h_err, d_err, sizeof(h_err), hipMemcpyDeviceToHost));
+  out->hbm_errors = h_err[0];
+  out->mfma_errors = h_err[1];
+  out->write_gbps = static_cast<double>(n) * sizeof(uint4) * passes / (t_write * 1e-3) / 1e9;
+  out->read_gbps = static_cast<double>(n) * sizeof(uint4) * passes / (t_read * 1e-3) / 1e9;
+  {
+    const double flops = 2.0 * 32 * 32 * 16 * 2.0 /*chains*/ * mfma_iters * (prop.multiProcessorCount * 8.0 * 4 /*waves*/);
+    out->mfma_tflops = flops / (t_mfma * 1e-3) / 1e12;
+  }
+  out->elapsed_ms = t_write + t_read + t_mfma;
+  out->ok = (out->hbm_errors == 0 && out->mfma_errors == 0) ? 1 : 0;
+done:
+  if (e0) hipEventDestroy(e0);
+  if (e1) hipEventDestroy(e1);
+  if (e2) hipEventDestroy(e2);
+  if (sink) hipFree(sink);
+  if (d_err) hipFree(d_err);
+  if (buf) hipFree(buf);
+  return out->error[0] ? -1 : 0;
+}
+
+}  // extern "C"

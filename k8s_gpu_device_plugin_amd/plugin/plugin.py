@@ -1,0 +1,317 @@
+"""One kubelet DevicePlugin endpoint per resource name.
+
+Reference ``plugin/plugin.go`` (``NvidiaDevicePlugin``):
+  * socket ``<DevicePluginPath>/nvidia-<name>.sock`` (``:46-51``) -> ``amd-<name>.sock``
+  * ``Serve`` (``:100-137``): remove stale socket, listen, serve with a crash-restart
+    loop (fatal after >5 crashes within 1 h), then a blocking self-dial check (5 s)
+  * ``Register`` (``:140-162``): dial ``kubelet.sock``, ``RegisterRequest{v1beta1,
+    endpoint, resource, GetPreferredAllocationAvailable}``
+  * RPCs ``GetDevicePluginOptions``/``ListAndWatch``/``GetPreferredAllocation``/
+    ``Allocate``/``PreStartContainer`` (``:165-229``)
+
+MI355X design: the device set, health, topology, allocator and the protobuf encoding
+of every hot response live in a native ``DeviceTable`` (C++).  Two interchangeable
+servers put it on the kubelet socket:
+  * ``native`` - C++ HTTP/2 gRPC server (``native/grpc_h2.cpp``): no Python and no
+    GIL on the request path.
+  * ``python`` - grpcio generic handlers with identity (de)serialisers, so request
+    bytes go straight into the native table and its bytes straight back out.
+Health changes bump the table version and wake every ListAndWatch stream; devices can
+become Healthy again (reference only ever marks Unhealthy, ``:181-186``).
+Lifecycle is idempotent: ``stop()`` twice, or after a failed ``start()``, is safe
+(defects D5/D6/D10).
+"""
+from __future__ import annotations
+
+import concurrent.futures
+import os
+import threading
+import time
+
+import grpc
+
+from .. import native
+from ..api import v1beta1
+from ..device import Devices
+from ..resource import ResourceName
+from ..utils.log import get_logger
+
+log = get_logger("plugin")
+
+SERVE_CRASH_LIMIT = 5          # plugin/plugin.go:110
+SERVE_CRASH_WINDOW_S = 3600.0  # plugin/plugin.go:122
+DIAL_TIMEOUT_S = 5.0           # plugin/plugin.go:130,141
+
+
+def socket_name(resource: ResourceName, vendor: str = "amd") -> str:
+    return "%s-%s.sock" % (vendor, ResourceName(resource).get_resource_name())
+
+
+def _unix_target(path: str) -> str:
+    return "unix://" + os.path.abspath(path)
+
+
+def dial(path: str, timeout: float = DIAL_TIMEOUT_S) -> grpc.Channel:
+    """Blocking dial of a unix socket (reference ``dial`` ``plugin/plugin.go:231-246``)."""
+    ch = grpc.insecure_channel(_unix_target(path), options=[("grpc.enable_http_proxy", 0)])
+    try:
+        grpc.channel_ready_future(ch).result(timeout=timeout)
+    except grpc.FutureTimeoutError:
+        ch.close()
+        raise TimeoutError("timed out dialing %s after %.1fs" % (path, timeout)) from None
+    return ch
+
+
+def make_table(resource: str, devices: Devices, topology, cfg) -> "object":
+    """Builds the native DeviceTable for a resource from the Python device view."""
+    n = native.load()
+    tc = n.TableConfig()
+    tc.resource_name = str(resource)
+    tc.visible_env = cfg.visibleDevicesEnv if cfg is not None else "AMD_VISIBLE_DEVICES"
+    tc.cdi = bool(cfg.cdi) if cfg is not None else False
+    tc.cdi_prefix = str(resource) + "="
+    tc.reject_unhealthy = bool(cfg.health.rejectUnhealthyAllocate) if cfg is not None else True
+    tds = [n.TableDevice(d.id, d.gpu, d.partition, d.numa_node if d.numa_node is not None else -1, d.replica,
+                         list(d.paths), d.health == v1beta1.HEALTHY) for d in devices]
+    return n.DeviceTable(tc, tds, topology)
+
+
+class AmdDevicePlugin:
+    """kubelet DevicePlugin for one ``amd.com/*`` resource."""
+
+    def __init__(self, resource: str, devices: Devices, topology, cfg=None, plugin_dir: str | None = None,
+                 server_kind: str | None = None) -> None:
+        self.resource = ResourceName(resource)
+        self._devices = devices
+        self.cfg = cfg
+        self.plugin_dir = plugin_dir or (cfg.pluginDir if cfg is not None else v1beta1.DEVICE_PLUGIN_PATH)
+        self.socket = os.path.join(self.plugin_dir, socket_name(self.resource))
+        self.kubelet_socket = os.path.join(self.plugin_dir, v1beta1.KUBELET_SOCKET_NAME)
+        self.server_kind = server_kind or (cfg.grpc.server if cfg is not None else "python")
+        self.table = make_table(str(self.resource), devices, topology, cfg)
+        self._lock = threading.RLock()
+        self._cv = threading.Condition()
+        self._server = None
+        self._native_server = None
+        self._serving = False
+        self._stopping = False
+        self._supervisor: threading.Thread | None = None
+        self.fatal_error: str | None = None
+        self.registered = False
+
+    # ------------------------------------------------------------------ views
+    def devices(self) -> Devices:
+        return self._devices
+
+    def __len__(self) -> int:
+        return len(self._devices)
+
+    # ------------------------------------------------------------------ lifecycle
+    def start(self) -> None:
+        """Serve then register; on register failure the server is stopped again
+        (reference ``Start`` ``plugin/plugin.go:68-83``)."""
+        self.serve()
+        log.info("Starting to serve", extra={"resourceName": str(self.resource), "socket": self.socket})
+        try:
+            self.register()
+        except Exception as e:
+            log.info("Could not register device plugin", extra={"resourceName": str(self.resource), "error": str(e)})
+            self.stop()
+            raise
+        log.info("Registered device plugin", extra={"resourceName": str(self.resource)})
+
+    def stop(self) -> None:
+        with self._lock:
+            self._stopping = True
+            server, self._server = self._server, None
+            nserver, self._native_server = self._native_server, None
+            was_serving, self._serving = self._serving, False
+        self.notify()
+        if server is not None:
+            server.stop(grace=0.5).wait(2.0)
+        if nserver is not None:
+            nserver.stop()
+        if was_serving:
+            log.info("Stopped serving", extra={"resourceName": str(self.resource), "socket": self.socket})
+        try:
+            os.remove(self.socket)
+        except FileNotFoundError:
+            pass
+        self.registered = False
+
+    @property
+    def serving(self) -> bool:
+        return self._serving
+
+    def serve(self) -> None:
+        with self._lock:
+            if self._serving:
+                return
+            self._stopping = False
+            os.makedirs(self.plugin_dir, exist_ok=True)
+            try:
+                os.remove(self.socket)
+            except FileNotFoundError:
+                pass
+            if self.server_kind == "native":
+                self._start_native_server()
+            else:
+                self._start_grpcio_server()
+            self._serving = True
+        # blocking self-dial (plugin/plugin.go:130-134)
+        try:
+            dial(self.socket, DIAL_TIMEOUT_S).close()
+        except Exception:
+            self.stop()
+            raise
+
+    def _start_native_server(self) -> None:
+        n = native.load()
+        srv = n.GrpcServer(self.socket, max(1, self.cfg.grpc.threads if self.cfg is not None else 2))
+        srv.add_table(self.table)
+        srv.start()
+        self._native_server = srv
+
+    def _start_grpcio_server(self) -> None:
+        server = grpc.server(concurrent.futures.ThreadPoolExecutor(
+            max_workers=max(4, self.cfg.grpc.threads if self.cfg is not None else 4),
+            thread_name_prefix="dp-" + self.resource.get_resource_name()))
+        server.add_generic_rpc_handlers((self._handler(),))
+        if server.add_insecure_port(_unix_target(self.socket)) == 0:
+            raise OSError("cannot listen on %s" % self.socket)
+        server.start()
+        self._server = server
+        self._supervisor = threading.Thread(target=self._supervise, args=(server,), daemon=True,
+                                            name="dp-supervise-" + self.resource.get_resource_name())
+        self._supervisor.start()
+
+    def _supervise(self, server) -> None:
+        """grpcio analogue of the Serve crash-restart loop (``plugin/plugin.go:107-129``):
+        an unexpected termination restarts the server, >5 crashes within an hour is fatal."""
+        crashes, last = 0, time.monotonic()
+        while True:
+            server.wait_for_termination()
+            with self._lock:
+                if self._stopping or self._server is not server:
+                    return
+            now = time.monotonic()
+            crashes = 0 if now - last > SERVE_CRASH_WINDOW_S else crashes + 1
+            last = now
+            log.error("gRPC server for %s terminated unexpectedly", self.resource)
+            if crashes > SERVE_CRASH_LIMIT:
+                self.fatal_error = "gRPC server for '%s' has repeatedly crashed recently" % self.resource
+                log.critical(self.fatal_error)
+                return
+            with self._lock:
+                self._serving = False
+                try:
+                    self._start_grpcio_server_locked_restart()
+                except Exception as e:  # pragma: no cover
+                    log.error("restart failed: %s", e)
+                return
+
+    def _start_grpcio_server_locked_restart(self) -> None:
+        try:
+            os.remove(self.socket)
+        except FileNotFoundError:
+            pass
+        self._start_grpcio_server()
+        self._serving = True
+
+    def register(self) -> None:
+        ch = dial(self.kubelet_socket, DIAL_TIMEOUT_S)
+        try:
+            req = v1beta1.RegisterRequest(version=v1beta1.VERSION, endpoint=os.path.basename(self.socket),
+                                          resource_name=str(self.resource), options=v1beta1.plugin_options())
+            call = ch.unary_unary(v1beta1.METHOD_REGISTER, request_serializer=v1beta1.RegisterRequest.SerializeToString,
+                                  response_deserializer=v1beta1.Empty.FromString)
+            call(req, timeout=DIAL_TIMEOUT_S)
+            self.registered = True
+        finally:
+            ch.close()
+
+    # ------------------------------------------------------------------ health
+    def notify(self) -> None:
+        """Wakes ListAndWatch streams (health or stop)."""
+        with self._cv:
+            self._cv.notify_all()
+
+    def set_gpu_health(self, gpu: int, partition: int, healthy: bool) -> int:
+        changed = self.table.set_gpu_health(gpu, partition, healthy)
+        if changed:
+            for d in self._devices:
+                if d.gpu == gpu and (partition < 0 or d.partition < 0 or d.partition == partition):
+                    d.health = v1beta1.HEALTHY if healthy else v1beta1.UNHEALTHY
+            self.notify()
+        return changed
+
+    def set_device_health(self, device_id: str, healthy: bool) -> bool:
+        changed = self.table.set_health(device_id, healthy)
+        if changed:
+            d = self._devices.get_by_id(device_id)
+            if d is not None:
+                d.health = v1beta1.HEALTHY if healthy else v1beta1.UNHEALTHY
+            self.notify()
+        return changed
+
+    def set_link_up(self, a: int, b: int, up: bool) -> None:
+        self.table.set_link_up(a, b, up)
+
+    # ------------------------------------------------------------------ RPCs (grpcio)
+    def _handler(self):
+        n = native.load()
+        table = self.table
+        rpc_opt, rpc_law, rpc_pref, rpc_alloc, rpc_pre = (n.RPC_OPTIONS, n.RPC_LIST_AND_WATCH, n.RPC_PREFERRED,
+                                                          n.RPC_ALLOCATE, n.RPC_PRE_START)
+        perf = time.perf_counter
+        opts = table.options()
+
+        def get_options(req: bytes, ctx) -> bytes:
+            t0 = perf()
+            table.observe(rpc_opt, perf() - t0, False)
+            return opts
+
+        def allocate(req: bytes, ctx) -> bytes:
+            t0 = perf()
+            ok, out = table.allocate(req)
+            table.observe(rpc_alloc, perf() - t0, not ok)
+            if not ok:
+                ctx.abort(grpc.StatusCode.UNKNOWN, out)
+            return out
+
+        def preferred(req: bytes, ctx) -> bytes:
+            t0 = perf()
+            ok, out = table.preferred(req)
+            table.observe(rpc_pref, perf() - t0, not ok)
+            if not ok:
+                ctx.abort(grpc.StatusCode.UNKNOWN, out)
+            return out
+
+        def pre_start(req: bytes, ctx) -> bytes:
+            table.observe(rpc_pre, 0.0, False)
+            return b""
+
+        def list_and_watch(req: bytes, ctx):
+            version = table.version
+            t0 = perf()
+            payload = table.list_and_watch()
+            table.observe(rpc_law, perf() - t0, False)
+            yield payload
+            while True:
+                with self._cv:
+                    while table.version == version and not self._stopping and ctx.is_active():
+                        self._cv.wait(0.5)
+                if self._stopping or not ctx.is_active():
+                    return
+                version = table.version
+                log.info("'%s' device health changed; sending update", self.resource)
+                yield table.list_and_watch()
+
+        u = grpc.unary_unary_rpc_method_handler
+        return grpc.method_handlers_generic_handler(v1beta1.DEVICE_PLUGIN_SERVICE, {
+            "GetDevicePluginOptions": u(get_options),
+            "ListAndWatch": grpc.unary_stream_rpc_method_handler(list_and_watch),
+            "GetPreferredAllocation": u(preferred),
+            "Allocate": u(allocate),
+            "PreStartContainer": u(pre_start),
+        })

@@ -1,0 +1,268 @@
+#include "allocator.h"
+
+#include <algorithm>
+#include <map>
+#include <numeric>
+#include <set>
+#include <unordered_map>
+
+namespace amdgpu_dp {
+
+int pair_score(const Topology& topo, const AllocDevice& a, const AllocDevice& b) {
+  const bool same_numa = a.numa >= 0 && a.numa == b.numa;
+  if (a.gpu == b.gpu) return 100 + 5;  // partitions of one GPU: on-package fabric
+  if (a.gpu < 0 || b.gpu < 0 || a.gpu >= topo.n || b.gpu >= topo.n) return 5;
+  const Link& l = topo.at(a.gpu, b.gpu);
+  int s;
+  switch (l.type) {
+    case kLinkXgmi:
+      s = l.up ? (l.hops <= 1 ? 60 : 40) : 10;
+      break;
+    case kLinkPcie:
+      s = 20;
+      break;
+    default:
+      s = 5;
+  }
+  return s + (same_numa ? 5 : 0);
+}
+
+namespace {
+
+struct Ctx {
+  const Topology& topo;
+  const std::vector<AllocDevice>& devs;
+  std::vector<char> is_avail;   // device index -> available
+  std::vector<int> gpu_total;   // devices per gpu (all)
+  std::vector<int> gpu_avail;   // available devices per gpu
+  std::vector<int> gpu_numa;
+  int ngpu = 0;
+  int parts_per_gpu = 1;
+
+  Ctx(const Topology& t, const std::vector<AllocDevice>& d, const std::vector<int>& avail) : topo(t), devs(d) {
+    is_avail.assign(d.size(), 0);
+    for (int i : avail) is_avail[i] = 1;
+    for (auto& x : d) ngpu = std::max(ngpu, x.gpu + 1);
+    gpu_total.assign(ngpu, 0);
+    gpu_avail.assign(ngpu, 0);
+    gpu_numa.assign(ngpu, -1);
+    for (size_t i = 0; i < d.size(); ++i) {
+      if (d[i].gpu < 0) continue;
+      gpu_total[d[i].gpu]++;
+      gpu_avail[d[i].gpu] += is_avail[i];
+      gpu_numa[d[i].gpu] = d[i].numa;
+    }
+    for (int g = 0; g < ngpu; ++g) parts_per_gpu = std::max(parts_per_gpu, gpu_total[g]);
+  }
+
+  // score of choosing set S (device indices) out of the available pool
+  double score(const std::vector<int>& S) const {
+    double s = 0;
+    for (size_t i = 0; i < S.size(); ++i)
+      for (size_t j = i + 1; j < S.size(); ++j) s += pair_score(topo, devs[S[i]], devs[S[j]]);
+    // per-gpu usage after taking S
+    std::vector<int> taken(ngpu, 0);
+    for (int i : S)
+      if (devs[i].gpu >= 0) taken[devs[i].gpu]++;
+    bool multi_gpu = false;
+    int first_gpu = -2;
+    for (int i : S) {
+      if (first_gpu == -2) first_gpu = devs[i].gpu;
+      else if (devs[i].gpu != first_gpu) multi_gpu = true;
+    }
+    for (int g = 0; g < ngpu; ++g) {
+      if (!taken[g]) continue;
+      const bool busy = gpu_avail[g] < gpu_total[g];  // other pods already on this GPU
+      if (busy && gpu_total[g] > 1) s += 6.0 * taken[g];  // pack into partially used GPUs
+      if (busy && multi_gpu) s -= 4.0;  // cross-GPU traffic would share this GPU's links
+    }
+    // fragmentation of the remainder: concentrate leftovers, keep whole GPUs per NUMA free
+    std::map<int, int> whole_free_per_numa;
+    double frag = 0;
+    for (int g = 0; g < ngpu; ++g) {
+      const int f = gpu_avail[g] - taken[g];
+      frag += static_cast<double>(f) * f / parts_per_gpu;
+      if (gpu_total[g] > 0 && f == gpu_total[g]) whole_free_per_numa[gpu_numa[g]]++;
+    }
+    for (auto& kv : whole_free_per_numa) frag += static_cast<double>(kv.second) * kv.second;
+    return s + frag;
+  }
+};
+
+double n_choose_k(int n, int k) {
+  if (k < 0 || k > n) return 0;
+  double r = 1;
+  for (int i = 1; i <= k; ++i) r = r * (n - k + i) / i;
+  return r;
+}
+
+}  // namespace
+
+AllocResult aligned_alloc(const Topology& topo, const std::vector<AllocDevice>& devs, const std::vector<int>& avail_in,
+                          const std::vector<int>& required_in, int size) {
+  AllocResult res;
+  const int ndev = static_cast<int>(devs.size());
+  std::vector<int> avail, required;
+  std::vector<char> seen(ndev, 0);
+  for (int i : required_in)
+    if (i >= 0 && i < ndev && !seen[i]) {
+      seen[i] = 1;
+      required.push_back(i);
+    }
+  std::vector<char> in_avail(ndev, 0);
+  for (int i : avail_in)
+    if (i >= 0 && i < ndev && !in_avail[i]) {
+      in_avail[i] = 1;
+      avail.push_back(i);
+    }
+  for (int i : required)
+    if (!in_avail[i]) {
+      in_avail[i] = 1;
+      avail.push_back(i);
+    }
+  std::sort(avail.begin(), avail.end());
+  const int need = size - static_cast<int>(required.size());
+  if (size <= 0 || need <= 0) {
+    res.chosen = required;
+    return res;
+  }
+  std::vector<int> cand;
+  for (int i : avail)
+    if (!seen[i]) cand.push_back(i);
+  if (static_cast<int>(cand.size()) < need) {
+    res.ok = false;
+    res.error = "not enough available devices to satisfy allocation";
+    return res;
+  }
+  std::vector<int> best;
+  if (static_cast<int>(cand.size()) == need) {
+    best = cand;
+  } else {
+    Ctx ctx(topo, devs, avail);
+    double best_score = -1e300;
+    auto consider = [&](std::vector<int>& S) {
+      const double sc = ctx.score(S);
+      if (sc > best_score + 1e-9) {
+        best_score = sc;
+        best.assign(S.begin() + required.size(), S.end());
+      }
+    };
+    if (n_choose_k(static_cast<int>(cand.size()), need) <= 20000) {
+      // exhaustive, lexicographic order => deterministic tie-break (first best wins)
+      std::vector<int> idx(need);
+      std::iota(idx.begin(), idx.end(), 0);
+      const int m = static_cast<int>(cand.size());
+      std::vector<int> S(required);
+      S.resize(required.size() + need);
+      for (;;) {
+        for (int k = 0; k < need; ++k) S[required.size() + k] = cand[idx[k]];
+        consider(S);
+        int k = need - 1;
+        while (k >= 0 && idx[k] == m - need + k) --k;
+        if (k < 0) break;
+        ++idx[k];
+        for (int j = k + 1; j < need; ++j) idx[j] = idx[j - 1] + 1;
+      }
+    } else {
+      // seeds: (a) whole request from one GPU (partition packing), (b) greedy growth
+      std::map<int, std::vector<int>> by_gpu;
+      for (int c : cand) by_gpu[devs[c].gpu].push_back(c);
+      for (auto& kv : by_gpu) {
+        if (static_cast<int>(kv.second.size()) < need) continue;
+        std::vector<int> S(required);
+        S.insert(S.end(), kv.second.begin(), kv.second.begin() + need);
+        consider(S);
+      }
+      std::vector<int> S(required);
+      std::vector<char> used(ndev, 0);
+      for (int i : required) used[i] = 1;
+      while (static_cast<int>(S.size()) < size) {
+        int pick = -1;
+        double ps = -1e300;
+        S.push_back(-1);
+        for (int c : cand) {
+          if (used[c]) continue;
+          S.back() = c;
+          const double sc = ctx.score(S);
+          if (sc > ps + 1e-9) {
+            ps = sc;
+            pick = c;
+          }
+        }
+        S.back() = pick;
+        used[pick] = 1;
+      }
+      // 1-swap local search (bounded)
+      double cur = ctx.score(S);
+      for (int pass = 0; pass < 4; ++pass) {
+        bool improved = false;
+        for (size_t k = required.size(); k < S.size(); ++k) {
+          for (int c : cand) {
+            if (used[c]) continue;
+            const int old = S[k];
+            S[k] = c;
+            const double sc = ctx.score(S);
+            if (sc > cur + 1e-9) {
+              cur = sc;
+              used[old] = 0;
+              used[c] = 1;
+              improved = true;
+            } else {
+              S[k] = old;
+            }
+          }
+        }
+        if (!improved) break;
+      }
+      consider(S);
+    }
+  }
+  std::sort(best.begin(), best.end());
+  res.chosen = required;
+  res.chosen.insert(res.chosen.end(), best.begin(), best.end());
+  return res;
+}
+
+AllocResult distributed_alloc(const std::vector<AllocDevice>& devs, const std::vector<int>& avail,
+                              const std::vector<int>& required, int size) {
+  AllocResult res;
+  const int ndev = static_cast<int>(devs.size());
+  std::vector<char> is_req(ndev, 0);
+  for (int i : required)
+    if (i >= 0 && i < ndev) is_req[i] = 1;
+  std::vector<int> cand;
+  std::vector<char> seen(ndev, 0);
+  for (int i : avail)
+    if (i >= 0 && i < ndev && !is_req[i] && !seen[i]) {
+      seen[i] = 1;
+      cand.push_back(i);
+    }
+  const int needed = size - static_cast<int>(required.size());
+  if (static_cast<int>(cand.size()) < needed) {
+    res.ok = false;
+    res.error = "not enough available devices to satisfy allocation";
+    return res;
+  }
+  // replica accounting per base device id (plugin/plugin.go:292-306)
+  std::unordered_map<std::string, std::pair<int, int>> rep;  // base -> (total, available)
+  for (int c : cand) rep[devs[c].base_id].second++;
+  for (const auto& d : devs) {
+    auto it = rep.find(d.base_id);
+    if (it != rep.end()) it->second.first++;
+  }
+  res.chosen = required;
+  for (int i = 0; i < needed; ++i) {
+    std::stable_sort(cand.begin(), cand.end(), [&](int a, int b) {
+      const auto& ra = rep[devs[a].base_id];
+      const auto& rb = rep[devs[b].base_id];
+      return (ra.first - ra.second) < (rb.first - rb.second);
+    });
+    const int pick = cand.front();
+    rep[devs[pick].base_id].second--;
+    res.chosen.push_back(pick);
+    cand.erase(cand.begin());
+  }
+  return res;
+}
+
+}  // namespace amdgpu_dp

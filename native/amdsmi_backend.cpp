@@ -1,0 +1,435 @@
+// Real MI355X backend over libamd_smi (ROCm 7.2).
+//
+// Replaces: NVML device queries (reference device/device.go:37-181), NVML MIG
+// enumeration (device/device_map.go:78-98, resource/resources.go:22-51), the
+// sysfs NUMA lookup (device/device.go:69-93) and go-gpuallocator's NVLink graph
+// (plugin/plugin.go:259-264).  Every amdsmi call is serialised behind one mutex
+// (SURVEY.md §7.5 hard part 6) except the blocking event wait.
+#include <amd_smi/amdsmi.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "backend.h"
+
+namespace amdgpu_dp {
+
+namespace {
+
+std::mutex g_init_mu;
+int g_init_refs = 0;
+
+std::string status_str(amdsmi_status_t st) {
+  const char* s = nullptr;
+  if (amdsmi_status_code_to_string(st, &s) == AMDSMI_STATUS_SUCCESS && s) return s;
+  return "amdsmi status " + std::to_string(static_cast<int>(st));
+}
+
+void check(amdsmi_status_t st, const char* what) {
+  if (st != AMDSMI_STATUS_SUCCESS) throw std::runtime_error(std::string(what) + ": " + status_str(st));
+}
+
+std::string bdf_str(const amdsmi_bdf_t& b) {
+  char buf[32];
+  std::snprintf(buf, sizeof(buf), "%04llx:%02x:%02x.%x", static_cast<unsigned long long>(b.domain_number),
+                static_cast<unsigned>(b.bus_number), static_cast<unsigned>(b.device_number),
+                static_cast<unsigned>(b.function_number));
+  return buf;
+}
+
+uint64_t bdf_key(const amdsmi_bdf_t& b) {  // physical device key (function masked)
+  return (static_cast<uint64_t>(b.domain_number) << 16) | (static_cast<uint64_t>(b.bus_number) << 8) |
+         (static_cast<uint64_t>(b.device_number) << 3);
+}
+
+// target_graphics_version: KFD encoding major*10000 + minor*100 + stepping (90500 ->
+// gfx950); older amdsmi returned the hex gfx id (0x950).
+std::string gfx_name(uint64_t v) {
+  if (v == 0 || v == ~0ull) return "";
+  char buf[32];
+  if (v >= 10000) {
+    const unsigned major = static_cast<unsigned>(v / 10000), minor = static_cast<unsigned>((v / 100) % 100),
+                   step = static_cast<unsigned>(v % 100);
+    std::snprintf(buf, sizeof(buf), "gfx%u%x%x", major, minor, step);
+  } else {
+    std::snprintf(buf, sizeof(buf), "gfx%llx", static_cast<unsigned long long>(v));
+  }
+  return buf;
+}
+
+int sysfs_numa(const std::string& bdf) {
+  std::ifstream f("/sys/bus/pci/devices/" + bdf + "/numa_node");
+  int n = -1;
+  if (f >> n) return n;
+  return -1;
+}
+
+bool valid16(uint16_t v) { return v != 0xFFFF; }
+bool valid64(uint64_t v) { return v != ~0ull; }
+
+struct Proc {
+  amdsmi_processor_handle h;
+  amdsmi_bdf_t bdf;
+  uint32_t partition_id;
+};
+
+}  // namespace
+
+bool amdsmi_available() {
+  std::lock_guard<std::mutex> lk(g_init_mu);
+  if (g_init_refs > 0) return true;
+  if (amdsmi_init(AMDSMI_INIT_AMD_GPUS) != AMDSMI_STATUS_SUCCESS) return false;
+  uint32_t n = 0;
+  const bool ok = amdsmi_get_socket_handles(&n, nullptr) == AMDSMI_STATUS_SUCCESS && n > 0;
+  amdsmi_shut_down();
+  return ok;
+}
+
+class AmdSmiBackend : public Backend {
+ public:
+  AmdSmiBackend() {
+    std::lock_guard<std::mutex> lk(g_init_mu);
+    if (g_init_refs == 0) check(amdsmi_init(AMDSMI_INIT_AMD_GPUS), "amdsmi_init");
+    ++g_init_refs;
+  }
+  ~AmdSmiBackend() override { shutdown(); }
+
+  std::string name() const override { return "amdsmi"; }
+
+  void shutdown() override {
+    std::lock_guard<std::mutex> lk(mu_);
+    disarm_locked();
+    if (!closed_) {
+      closed_ = true;
+      std::lock_guard<std::mutex> ilk(g_init_mu);
+      if (--g_init_refs == 0) amdsmi_shut_down();
+    }
+  }
+
+  void discover(std::vector<GpuInfo>* gpus, Topology* topo) override {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (closed_) throw std::runtime_error("amdsmi backend is shut down");
+    disarm_locked();
+    uint32_t nsock = 0;
+    check(amdsmi_get_socket_handles(&nsock, nullptr), "amdsmi_get_socket_handles(count)");
+    std::vector<amdsmi_socket_handle> socks(nsock);
+    check(amdsmi_get_socket_handles(&nsock, socks.data()), "amdsmi_get_socket_handles");
+    std::map<uint64_t, std::vector<Proc>> groups;  // ordered by BDF -> deterministic indices
+    for (uint32_t s = 0; s < nsock; ++s) {
+      uint32_t np = 0;
+      if (amdsmi_get_processor_handles(socks[s], &np, nullptr) != AMDSMI_STATUS_SUCCESS || np == 0) continue;
+      std::vector<amdsmi_processor_handle> ph(np);
+      check(amdsmi_get_processor_handles(socks[s], &np, ph.data()), "amdsmi_get_processor_handles");
+      for (uint32_t i = 0; i < np; ++i) {
+        processor_type_t t = AMDSMI_PROCESSOR_TYPE_UNKNOWN;
+        if (amdsmi_get_processor_type(ph[i], &t) != AMDSMI_STATUS_SUCCESS || t != AMDSMI_PROCESSOR_TYPE_AMD_GPU)
+          continue;
+        Proc p{ph[i], {}, 0};
+        check(amdsmi_get_gpu_device_bdf(ph[i], &p.bdf), "amdsmi_get_gpu_device_bdf");
+        amdsmi_kfd_info_t kfd{};
+        p.partition_id = (amdsmi_get_gpu_kfd_info(ph[i], &kfd) == AMDSMI_STATUS_SUCCESS &&
+                          kfd.current_partition_id != 0xFFFFFFFFu)
+                             ? kfd.current_partition_id
+                             : static_cast<uint32_t>(p.bdf.function_number);
+        groups[bdf_key(p.bdf)].push_back(p);
+      }
+    }
+    gpus->clear();
+    procs_.clear();
+    for (auto& kv : groups) {
+      auto& plist = kv.second;
+      std::stable_sort(plist.begin(), plist.end(),
+                       [](const Proc& a, const Proc& b) { return a.partition_id < b.partition_id; });
+      GpuInfo g;
+      g.index = static_cast<int>(gpus->size());
+      amdsmi_processor_handle h0 = plist.front().h;
+      amdsmi_bdf_t b0 = plist.front().bdf;
+      b0.function_number = 0;
+      g.bdf = bdf_str(b0);
+      g.uuid = uuid_of(h0);
+      amdsmi_asic_info_t asic{};
+      if (amdsmi_get_gpu_asic_info(h0, &asic) == AMDSMI_STATUS_SUCCESS) {
+        g.market_name = asic.market_name;
+        g.serial = asic.asic_serial;
+        g.gfx_target = gfx_name(asic.target_graphics_version);
+        if (asic.num_of_compute_units != 0xFFFFFFFFu) g.num_compute_units = static_cast<int>(asic.num_of_compute_units);
+      }
+      if (g.market_name.empty()) g.market_name = "AMD Instinct";
+      amdsmi_vram_info_t vram{};
+      if (amdsmi_get_gpu_vram_info(h0, &vram) == AMDSMI_STATUS_SUCCESS)
+        g.vram_total_bytes = static_cast<uint64_t>(vram.vram_size) << 20;
+      char buf[64] = {0};
+      if (amdsmi_get_gpu_compute_partition(h0, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS) g.compute_partition = buf;
+      std::memset(buf, 0, sizeof(buf));
+      if (amdsmi_get_gpu_memory_partition(h0, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS) g.memory_partition = buf;
+      amdsmi_memory_partition_config_t mcfg{};
+      if (amdsmi_get_gpu_memory_partition_config(h0, &mcfg) == AMDSMI_STATUS_SUCCESS)
+        g.nps_caps = mcfg.partition_caps.nps_cap_mask & 0xF;
+      if (g.compute_partition.empty()) g.compute_partition = plist.size() == 1 ? "SPX" : "UNKNOWN";
+      if (g.memory_partition.empty()) g.memory_partition = "NPS1";
+      int32_t numa = -1;
+      if (amdsmi_get_gpu_topo_numa_affinity(h0, &numa) != AMDSMI_STATUS_SUCCESS || numa < 0) numa = sysfs_numa(g.bdf);
+      g.numa_node = numa;
+      std::vector<amdsmi_processor_handle> handles;
+      for (size_t k = 0; k < plist.size(); ++k) {
+        const Proc& p = plist[k];
+        PartitionInfo part;
+        part.gpu = g.index;
+        part.index = static_cast<int>(k);
+        part.uuid = uuid_of(p.h);
+        part.id = plist.size() == 1 ? g.uuid : g.uuid + "-xcp" + std::to_string(k);
+        amdsmi_enumeration_info_t en{};
+        if (amdsmi_get_gpu_enumeration_info(p.h, &en) == AMDSMI_STATUS_SUCCESS) {
+          part.render_minor = static_cast<int>(en.drm_render);
+          part.card_minor = static_cast<int>(en.drm_card);
+          part.hip_id = static_cast<int>(en.hip_id);
+          part.hsa_id = static_cast<int>(en.hsa_id);
+        }
+        amdsmi_kfd_info_t kfd{};
+        if (amdsmi_get_gpu_kfd_info(p.h, &kfd) == AMDSMI_STATUS_SUCCESS && kfd.node_id != 0xFFFFFFFFu)
+          part.kfd_node = kfd.node_id;
+        part.numa_node = g.numa_node;
+        amdsmi_vram_usage_t vu{};
+        if (amdsmi_get_gpu_vram_usage(p.h, &vu) == AMDSMI_STATUS_SUCCESS)
+          part.vram_bytes = static_cast<uint64_t>(vu.vram_total) << 20;
+        if (part.vram_bytes == 0 && !plist.empty()) part.vram_bytes = g.vram_total_bytes / plist.size();
+        g.partitions.push_back(part);
+        handles.push_back(p.h);
+      }
+      procs_.push_back(handles);
+      gpus->push_back(std::move(g));
+    }
+    const int n = static_cast<int>(gpus->size());
+    topo->resize(n);
+    for (int a = 0; a < n; ++a) {
+      for (int b = 0; b < n; ++b) {
+        if (a == b) continue;
+        Link l;
+        uint64_t hops = 0;
+        amdsmi_link_type_t t = AMDSMI_LINK_TYPE_UNKNOWN;
+        if (amdsmi_topo_get_link_type(procs_[a][0], procs_[b][0], &hops, &t) == AMDSMI_STATUS_SUCCESS) {
+          l.type = static_cast<int>(t);
+          l.hops = static_cast<int>(hops);
+        }
+        uint64_t w = 0;
+        if (amdsmi_topo_get_link_weight(procs_[a][0], procs_[b][0], &w) == AMDSMI_STATUS_SUCCESS) l.weight = w;
+        amdsmi_link_type_t pt;
+        amdsmi_p2p_capability_t cap{};
+        if (amdsmi_topo_get_p2p_status(procs_[a][0], procs_[b][0], &pt, &cap) == AMDSMI_STATUS_SUCCESS)
+          l.p2p = true;
+        topo->at(a, b) = l;
+      }
+    }
+    // xGMI per-link health: link metrics name the peer BDF of each physical link.
+    for (int a = 0; a < n; ++a) {
+      GpuSample s;
+      link_state_locked(a, &s);
+      (*gpus)[a].num_xgmi_links = s.num_links;
+      for (int k = 0; k < s.num_links; ++k)
+        if (s.link_peer[k] >= 0 && s.link_up[k] == 0) topo->at(a, s.link_peer[k]).up = topo->at(s.link_peer[k], a).up = false;
+    }
+    gpus_ = *gpus;
+  }
+
+  bool sample(int gpu, GpuSample* s) override {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (closed_ || gpu < 0 || gpu >= static_cast<int>(procs_.size())) return false;
+    amdsmi_processor_handle h0 = procs_[gpu][0];
+    s->ts_ns = now_ns();
+    amdsmi_gpu_metrics_t m;
+    std::memset(&m, 0, sizeof(m));
+    if (amdsmi_get_gpu_metrics_info(h0, &m) == AMDSMI_STATUS_SUCCESS) {
+      s->ok = true;
+      if (valid16(m.current_socket_power) && m.current_socket_power != 0) s->power_w = m.current_socket_power;
+      else if (valid16(m.average_socket_power)) s->power_w = m.average_socket_power;
+      if (valid64(m.energy_accumulator)) s->energy_j = m.energy_accumulator * 15.259e-6;  // 15.259 uJ / count
+      if (valid16(m.temperature_edge) && m.temperature_edge != 0) s->temp_edge_c = m.temperature_edge;
+      if (valid16(m.temperature_hotspot)) s->temp_hotspot_c = m.temperature_hotspot;
+      if (valid16(m.temperature_mem)) s->temp_mem_c = m.temperature_mem;
+      s->num_hbm = 0;
+      for (int i = 0; i < AMDSMI_NUM_HBM_INSTANCES && i < kMaxHbm; ++i)
+        if (valid16(m.temperature_hbm[i]) && m.temperature_hbm[i] != 0) s->temp_hbm_c[s->num_hbm++] = m.temperature_hbm[i];
+      if (valid16(m.average_gfx_activity)) s->gfx_activity_pct = m.average_gfx_activity;
+      if (valid16(m.average_umc_activity)) s->umc_activity_pct = m.average_umc_activity;
+      if (valid16(m.current_gfxclks[0]) && m.current_gfxclks[0] != 0) s->gfxclk_mhz = m.current_gfxclks[0];
+      else if (valid16(m.average_gfxclk_frequency)) s->gfxclk_mhz = m.average_gfxclk_frequency;
+      if (valid16(m.current_uclk)) s->uclk_mhz = m.current_uclk;
+      if (m.throttle_status != 0xFFFFFFFFu) s->throttle_status = m.throttle_status;
+      const int nparts = static_cast<int>(procs_[gpu].size());
+      s->num_partitions = std::min(nparts, kMaxPartitions);
+      for (int p = 0; p < s->num_partitions && p < AMDSMI_MAX_NUM_XCP; ++p) {
+        double sum = 0;
+        int cnt = 0;
+        for (int x = 0; x < AMDSMI_MAX_NUM_XCC; ++x) {
+          const uint16_t v = m.xcp_stats[p].gfx_busy_inst[x];
+          if (valid16(v)) {
+            sum += v;
+            ++cnt;
+          }
+        }
+        s->partition_gfx_busy_pct[p] = cnt ? sum / cnt : (nparts == 1 ? s->gfx_activity_pct : -1);
+      }
+    }
+    double used = 0, total = 0;
+    bool have_vram = false;
+    for (size_t p = 0; p < procs_[gpu].size(); ++p) {
+      amdsmi_vram_usage_t vu{};
+      if (amdsmi_get_gpu_vram_usage(procs_[gpu][p], &vu) == AMDSMI_STATUS_SUCCESS) {
+        have_vram = true;
+        used += static_cast<double>(vu.vram_used) * 1048576.0;
+        total += static_cast<double>(vu.vram_total) * 1048576.0;
+        if (static_cast<int>(p) < kMaxPartitions) s->partition_vram_used_bytes[p] = static_cast<double>(vu.vram_used) * 1048576.0;
+        // partitions share one VRAM pool in NPS1; do not double count
+        if (gpus_.size() > static_cast<size_t>(gpu) && gpus_[gpu].memory_partition == "NPS1") break;
+      }
+    }
+    if (have_vram) {
+      s->vram_used_bytes = used;
+      s->vram_total_bytes = total;
+      s->ok = true;
+    }
+    amdsmi_error_count_t ec{};
+    if (amdsmi_get_gpu_total_ecc_count(h0, &ec) == AMDSMI_STATUS_SUCCESS) {
+      s->ecc_correctable = static_cast<int64_t>(ec.correctable_count);
+      s->ecc_uncorrectable = static_cast<int64_t>(ec.uncorrectable_count);
+    }
+    link_state_locked(gpu, s);
+    return s->ok;
+  }
+
+  void arm_events() override {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (armed_ || closed_) return;
+    const uint64_t mask = AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_GPU_PRE_RESET) |
+                          AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_GPU_POST_RESET) |
+                          AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_THERMAL_THROTTLE) |
+                          AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_VMFAULT);
+    armed_handles_.clear();
+    for (auto& handles : procs_) {
+      for (auto h : handles) {
+        if (amdsmi_init_gpu_event_notification(h) != AMDSMI_STATUS_SUCCESS) continue;
+        if (amdsmi_set_gpu_event_notification_mask(h, mask) != AMDSMI_STATUS_SUCCESS) {
+          amdsmi_stop_gpu_event_notification(h);
+          continue;
+        }
+        armed_handles_.push_back(h);
+      }
+    }
+    armed_ = true;
+  }
+
+  int wait_events(int timeout_ms, std::vector<HwEvent>* out) override {
+    bool armed;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      armed = armed_ && !armed_handles_.empty() && !closed_;
+    }
+    if (!armed) {
+      // nothing armed (e.g. unprivileged container): the health monitor polls instead
+      struct timespec ts{timeout_ms / 1000, (timeout_ms % 1000) * 1000000L};
+      nanosleep(&ts, nullptr);
+      return 0;
+    }
+    amdsmi_evt_notification_data_t data[16];
+    uint32_t num = 16;
+    amdsmi_status_t st = amdsmi_get_gpu_event_notification(timeout_ms, &num, data);
+    if (st != AMDSMI_STATUS_SUCCESS) return 0;
+    int added = 0;
+    std::lock_guard<std::mutex> lk(mu_);
+    for (uint32_t i = 0; i < num; ++i) {
+      HwEvent e;
+      e.ts_ns = now_ns();
+      e.message = data[i].message;
+      switch (data[i].event) {
+        case AMDSMI_EVT_NOTIF_GPU_PRE_RESET: e.kind = kEvtPreReset; break;
+        case AMDSMI_EVT_NOTIF_GPU_POST_RESET: e.kind = kEvtPostReset; break;
+        case AMDSMI_EVT_NOTIF_THERMAL_THROTTLE: e.kind = kEvtThermal; break;
+        case AMDSMI_EVT_NOTIF_VMFAULT: e.kind = kEvtVmFault; break;
+        default: continue;
+      }
+      locate(data[i].processor_handle, &e.gpu, &e.partition);
+      out->push_back(e);
+      ++added;
+    }
+    return added;
+  }
+
+ private:
+  std::string uuid_of(amdsmi_processor_handle h) {
+    char ubuf[AMDSMI_MAX_STRING_LENGTH] = {0};
+    unsigned int ulen = sizeof(ubuf);
+    if (amdsmi_get_gpu_device_uuid(h, &ulen, ubuf) == AMDSMI_STATUS_SUCCESS && ubuf[0]) return ubuf;
+    amdsmi_bdf_t b{};
+    amdsmi_get_gpu_device_bdf(h, &b);
+    return "amdgpu-" + bdf_str(b);
+  }
+
+  void locate(amdsmi_processor_handle h, int* gpu, int* part) {
+    for (size_t g = 0; g < procs_.size(); ++g)
+      for (size_t p = 0; p < procs_[g].size(); ++p)
+        if (procs_[g][p] == h) {
+          *gpu = static_cast<int>(g);
+          *part = procs_[g].size() == 1 ? -1 : static_cast<int>(p);
+          return;
+        }
+  }
+
+  int gpu_of_bdf(const amdsmi_bdf_t& b) {
+    const uint64_t k = bdf_key(b);
+    for (size_t g = 0; g < procs_.size(); ++g) {
+      amdsmi_bdf_t gb{};
+      if (amdsmi_get_gpu_device_bdf(procs_[g][0], &gb) == AMDSMI_STATUS_SUCCESS && bdf_key(gb) == k)
+        return static_cast<int>(g);
+    }
+    return -1;
+  }
+
+  // Fills per-link peer/up/read/write from amdsmi link metrics + xgmi link status.
+  void link_state_locked(int gpu, GpuSample* s) {
+    amdsmi_link_metrics_t lm;
+    std::memset(&lm, 0, sizeof(lm));
+    s->num_links = 0;
+    if (amdsmi_get_link_metrics(procs_[gpu][0], &lm) != AMDSMI_STATUS_SUCCESS) return;
+    amdsmi_xgmi_link_status_t ls;
+    std::memset(&ls, 0, sizeof(ls));
+    const bool have_status = amdsmi_get_gpu_xgmi_link_status(procs_[gpu][0], &ls) == AMDSMI_STATUS_SUCCESS;
+    const uint32_t nl = std::min<uint32_t>(lm.num_links, kMaxXgmiLinks);
+    for (uint32_t k = 0; k < nl; ++k) {
+      if (lm.links[k].link_type != AMDSMI_LINK_TYPE_XGMI) continue;
+      const int i = s->num_links++;
+      s->link_peer[i] = gpu_of_bdf(lm.links[k].bdf);
+      s->link_read_kb[i] = static_cast<double>(lm.links[k].read);
+      s->link_write_kb[i] = static_cast<double>(lm.links[k].write);
+      if (have_status && k < ls.total_links)
+        s->link_up[i] = ls.status[k] == AMDSMI_XGMI_LINK_UP ? 1 : (ls.status[k] == AMDSMI_XGMI_LINK_DOWN ? 0 : -1);
+      else
+        s->link_up[i] = -1;
+    }
+  }
+
+  void disarm_locked() {
+    if (!armed_) return;
+    for (auto h : armed_handles_) amdsmi_stop_gpu_event_notification(h);
+    armed_handles_.clear();
+    armed_ = false;
+  }
+
+  std::mutex mu_;
+  std::vector<std::vector<amdsmi_processor_handle>> procs_;
+  std::vector<GpuInfo> gpus_;
+  std::vector<amdsmi_processor_handle> armed_handles_;
+  bool armed_ = false;
+  bool closed_ = false;
+};
+
+std::shared_ptr<Backend> make_amdsmi_backend() { return std::make_shared<AmdSmiBackend>(); }
+
+}  // namespace amdgpu_dp

@@ -1,0 +1,166 @@
+// Hardware backend interface of the MI355X device plugin.
+//
+// Replaces the reference's NVML + go-nvlib stack (reference: plugin/manager.go:44
+// nvml.New(), device/device.go:37-181 per-device NVML queries, device/device_map.go:
+// 48-98 VisitDevices/VisitMigDevices).  One physical MI355X (an amdsmi *socket*) owns
+// 1..8 compute partitions (SPX..CPX, amdsmi *processors*); each partition is a KFD node
+// with its own DRM render node, which is what a container needs mounted.
+//
+// Two implementations:
+//   * AmdSmiBackend  (amdsmi_backend.cpp)  - real gfx950 hardware via libamd_smi
+//   * FixtureBackend (fixture_backend.cpp) - scripted topologies / telemetry / faults
+//                                             for CPU tests and the 8x8 CPX configs
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace amdgpu_dp {
+
+// Link classes between two physical GPUs (mirrors amdsmi_link_type_t values).
+enum LinkType : int {
+  kLinkInternal = 0,  // same physical GPU (on-package Infinity Fabric)
+  kLinkPcie = 1,
+  kLinkXgmi = 2,
+  kLinkNotApplicable = 3,
+  kLinkUnknown = 4,
+};
+
+struct PartitionInfo {
+  int gpu = -1;           // physical GPU index (socket order, sorted by BDF)
+  int index = 0;          // partition index inside the GPU (0..num_partitions-1)
+  std::string id;         // stable device id advertised to kubelet
+  std::string uuid;       // amdsmi uuid of this processor
+  int render_minor = -1;  // /dev/dri/renderD<render_minor>
+  int card_minor = -1;    // /dev/dri/card<card_minor>
+  int hip_id = -1;
+  int hsa_id = -1;
+  int64_t kfd_node = -1;
+  int numa_node = -1;
+  uint64_t vram_bytes = 0;
+};
+
+struct GpuInfo {
+  int index = -1;
+  std::string uuid;
+  std::string bdf;            // dddd:bb:dd.f
+  std::string market_name;    // e.g. "AMD Instinct MI355X"
+  std::string gfx_target;     // e.g. "gfx950"
+  std::string serial;
+  int numa_node = -1;
+  uint64_t vram_total_bytes = 0;
+  std::string compute_partition;  // SPX/DPX/TPX/QPX/CPX
+  std::string memory_partition;   // NPS1/NPS2/NPS4/NPS8
+  uint32_t nps_caps = 0;          // bit0 NPS1, bit1 NPS2, bit2 NPS4, bit3 NPS8
+  int num_compute_units = 0;
+  int num_xgmi_links = 0;
+  std::vector<PartitionInfo> partitions;
+};
+
+struct Link {
+  int type = kLinkUnknown;
+  int hops = 0;
+  uint64_t weight = 0;  // amdsmi link weight (lower = closer)
+  bool up = true;       // all physical xGMI links between the pair are up
+  bool p2p = false;
+};
+
+struct Topology {
+  int n = 0;
+  std::vector<Link> links;  // n*n, row-major; diagonal = internal
+  const Link& at(int a, int b) const { return links[static_cast<size_t>(a) * n + b]; }
+  Link& at(int a, int b) { return links[static_cast<size_t>(a) * n + b]; }
+  void resize(int count) {
+    n = count;
+    links.assign(static_cast<size_t>(count) * count, Link{});
+    for (int i = 0; i < count; ++i) {
+      at(i, i).type = kLinkInternal;
+      at(i, i).p2p = true;
+    }
+  }
+};
+
+constexpr int kMaxXgmiLinks = 8;
+constexpr int kMaxHbm = 8;
+constexpr int kMaxPartitions = 8;
+
+// One telemetry sample of a physical GPU.  NaN / negative = unavailable.
+struct GpuSample {
+  int64_t ts_ns = 0;
+  double power_w = -1;
+  double energy_j = -1;            // accumulated
+  double temp_edge_c = -1;
+  double temp_hotspot_c = -1;
+  double temp_mem_c = -1;
+  int num_hbm = 0;
+  double temp_hbm_c[kMaxHbm] = {};
+  double gfx_activity_pct = -1;
+  double umc_activity_pct = -1;
+  double gfxclk_mhz = -1;
+  double uclk_mhz = -1;
+  double vram_used_bytes = -1;
+  double vram_total_bytes = -1;
+  int64_t ecc_correctable = -1;
+  int64_t ecc_uncorrectable = -1;
+  int64_t throttle_status = -1;
+  int num_links = 0;
+  int link_peer[kMaxXgmiLinks] = {};  // physical GPU index of the peer, -1 unknown
+  int link_up[kMaxXgmiLinks] = {};    // 1 up, 0 down, -1 unknown/disabled
+  double link_read_kb[kMaxXgmiLinks] = {};
+  double link_write_kb[kMaxXgmiLinks] = {};
+  int num_partitions = 0;
+  double partition_gfx_busy_pct[kMaxPartitions] = {};
+  double partition_vram_used_bytes[kMaxPartitions] = {};
+  bool ok = false;
+};
+
+// Health-relevant hardware event.
+enum EventKind : int {
+  kEvtNone = 0,
+  kEvtPreReset = 1,     // GPU_PRE_RESET  -> Unhealthy
+  kEvtPostReset = 2,    // GPU_POST_RESET -> re-probe -> Healthy
+  kEvtEccUncorrectable = 3,
+  kEvtLinkDown = 4,
+  kEvtLinkUp = 5,
+  kEvtThermal = 6,      // informational
+  kEvtVmFault = 7,      // informational
+  kEvtDeviceLost = 8,   // device disappeared / unrecoverable -> Unhealthy
+  kEvtDeviceRecovered = 9,
+};
+
+const char* event_kind_name(int kind);
+
+struct HwEvent {
+  int64_t ts_ns = 0;
+  int kind = kEvtNone;
+  int gpu = -1;        // physical GPU (-1 = all)
+  int partition = -1;  // -1 = whole GPU
+  int peer = -1;       // for link events
+  std::string message;
+};
+
+class Backend {
+ public:
+  virtual ~Backend() = default;
+  virtual std::string name() const = 0;
+  // (Re)discover GPUs/partitions/topology.  Throws std::runtime_error on failure.
+  virtual void discover(std::vector<GpuInfo>* gpus, Topology* topo) = 0;
+  // Telemetry for physical GPU `gpu`; returns false when unavailable.
+  virtual bool sample(int gpu, GpuSample* out) = 0;
+  // Block up to timeout_ms for hardware events; append to *out.  Returns count.
+  virtual int wait_events(int timeout_ms, std::vector<HwEvent>* out) = 0;
+  // Arm event delivery for the discovered GPUs (idempotent).
+  virtual void arm_events() {}
+  virtual void shutdown() {}
+};
+
+std::shared_ptr<Backend> make_amdsmi_backend();
+bool amdsmi_available();
+
+int64_t now_ns();
+int64_t mono_ns();
+
+}  // namespace amdgpu_dp

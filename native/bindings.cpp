@@ -1,0 +1,449 @@
+// pybind11 module `k8s_gpu_device_plugin_amd._native`.
+// Long-blocking calls (health pop, inotify read, server stop, scrapes) release the GIL.
+#include <pybind11/functional.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "allocator.h"
+#include "backend.h"
+#include "device_table.h"
+#include "fixture_backend.h"
+#include "health.h"
+#include "httpd.h"
+#include "telemetry.h"
+#include "watch.h"
+
+namespace py = pybind11;
+using namespace amdgpu_dp;
+
+namespace {
+
+py::tuple ok_bytes(bool ok, const std::string& s) {
+  if (ok) return py::make_tuple(true, py::bytes(s));
+  return py::make_tuple(false, py::str(s));
+}
+
+std::string to_str(const py::bytes& b) { return std::string(b); }
+
+}  // namespace
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "MI355X device plugin native core (amdsmi backend, allocator, exporter, httpd)";
+
+  py::class_<PartitionInfo>(m, "PartitionInfo")
+      .def(py::init<>())
+      .def_readwrite("gpu", &PartitionInfo::gpu)
+      .def_readwrite("index", &PartitionInfo::index)
+      .def_readwrite("id", &PartitionInfo::id)
+      .def_readwrite("uuid", &PartitionInfo::uuid)
+      .def_readwrite("render_minor", &PartitionInfo::render_minor)
+      .def_readwrite("card_minor", &PartitionInfo::card_minor)
+      .def_readwrite("hip_id", &PartitionInfo::hip_id)
+      .def_readwrite("hsa_id", &PartitionInfo::hsa_id)
+      .def_readwrite("kfd_node", &PartitionInfo::kfd_node)
+      .def_readwrite("numa_node", &PartitionInfo::numa_node)
+      .def_readwrite("vram_bytes", &PartitionInfo::vram_bytes);
+
+  py::class_<GpuInfo>(m, "GpuInfo")
+      .def(py::init<>())
+      .def_readwrite("index", &GpuInfo::index)
+      .def_readwrite("uuid", &GpuInfo::uuid)
+      .def_readwrite("bdf", &GpuInfo::bdf)
+      .def_readwrite("market_name", &GpuInfo::market_name)
+      .def_readwrite("gfx_target", &GpuInfo::gfx_target)
+      .def_readwrite("serial", &GpuInfo::serial)
+      .def_readwrite("numa_node", &GpuInfo::numa_node)
+      .def_readwrite("vram_total_bytes", &GpuInfo::vram_total_bytes)
+      .def_readwrite("compute_partition", &GpuInfo::compute_partition)
+      .def_readwrite("memory_partition", &GpuInfo::memory_partition)
+      .def_readwrite("nps_caps", &GpuInfo::nps_caps)
+      .def_readwrite("num_compute_units", &GpuInfo::num_compute_units)
+      .def_readwrite("num_xgmi_links", &GpuInfo::num_xgmi_links)
+      .def_readwrite("partitions", &GpuInfo::partitions);
+
+  py::class_<Link>(m, "Link")
+      .def(py::init<>())
+      .def(py::init([](int type, int hops, uint64_t weight, bool up, bool p2p) {
+             Link l;
+             l.type = type;
+             l.hops = hops;
+             l.weight = weight;
+             l.up = up;
+             l.p2p = p2p;
+             return l;
+           }),
+           py::arg("type") = static_cast<int>(kLinkXgmi), py::arg("hops") = 1, py::arg("weight") = 15,
+           py::arg("up") = true, py::arg("p2p") = true)
+      .def_readwrite("type", &Link::type)
+      .def_readwrite("hops", &Link::hops)
+      .def_readwrite("weight", &Link::weight)
+      .def_readwrite("up", &Link::up)
+      .def_readwrite("p2p", &Link::p2p);
+
+  py::class_<Topology>(m, "Topology")
+      .def(py::init<>())
+      .def(py::init([](int n) {
+        Topology t;
+        t.resize(n);
+        return t;
+      }))
+      .def_readonly("n", &Topology::n)
+      .def("link", [](const Topology& t, int a, int b) {
+        if (a < 0 || b < 0 || a >= t.n || b >= t.n) throw py::index_error("gpu index");
+        return t.at(a, b);
+      })
+      .def("set_link", [](Topology& t, int a, int b, const Link& l) {
+        if (a < 0 || b < 0 || a >= t.n || b >= t.n) throw py::index_error("gpu index");
+        t.at(a, b) = l;
+        t.at(b, a) = l;
+      });
+
+  py::class_<GpuSample>(m, "GpuSample")
+      .def(py::init<>())
+      .def_readonly("ts_ns", &GpuSample::ts_ns)
+      .def_readonly("ok", &GpuSample::ok)
+      .def_readonly("power_w", &GpuSample::power_w)
+      .def_readonly("energy_j", &GpuSample::energy_j)
+      .def_readonly("temp_edge_c", &GpuSample::temp_edge_c)
+      .def_readonly("temp_hotspot_c", &GpuSample::temp_hotspot_c)
+      .def_readonly("temp_mem_c", &GpuSample::temp_mem_c)
+      .def_property_readonly("temp_hbm_c", [](const GpuSample& s) {
+        return std::vector<double>(s.temp_hbm_c, s.temp_hbm_c + s.num_hbm);
+      })
+      .def_readonly("gfx_activity_pct", &GpuSample::gfx_activity_pct)
+      .def_readonly("umc_activity_pct", &GpuSample::umc_activity_pct)
+      .def_readonly("gfxclk_mhz", &GpuSample::gfxclk_mhz)
+      .def_readonly("uclk_mhz", &GpuSample::uclk_mhz)
+      .def_readonly("vram_used_bytes", &GpuSample::vram_used_bytes)
+      .def_readonly("vram_total_bytes", &GpuSample::vram_total_bytes)
+      .def_readonly("ecc_correctable", &GpuSample::ecc_correctable)
+      .def_readonly("ecc_uncorrectable", &GpuSample::ecc_uncorrectable)
+      .def_readonly("throttle_status", &GpuSample::throttle_status)
+      .def_property_readonly("links", [](const GpuSample& s) {
+        py::list l;
+        for (int k = 0; k < s.num_links; ++k)
+          l.append(py::make_tuple(s.link_peer[k], s.link_up[k], s.link_read_kb[k], s.link_write_kb[k]));
+        return l;
+      })
+      .def_property_readonly("partition_gfx_busy_pct", [](const GpuSample& s) {
+        return std::vector<double>(s.partition_gfx_busy_pct, s.partition_gfx_busy_pct + s.num_partitions);
+      });
+
+  m.attr("EVT_PRE_RESET") = static_cast<int>(kEvtPreReset);
+  m.attr("EVT_POST_RESET") = static_cast<int>(kEvtPostReset);
+  m.attr("EVT_ECC_UNCORRECTABLE") = static_cast<int>(kEvtEccUncorrectable);
+  m.attr("EVT_LINK_DOWN") = static_cast<int>(kEvtLinkDown);
+  m.attr("EVT_LINK_UP") = static_cast<int>(kEvtLinkUp);
+  m.attr("EVT_THERMAL") = static_cast<int>(kEvtThermal);
+  m.attr("EVT_VM_FAULT") = static_cast<int>(kEvtVmFault);
+  m.attr("EVT_DEVICE_LOST") = static_cast<int>(kEvtDeviceLost);
+  m.attr("EVT_DEVICE_RECOVERED") = static_cast<int>(kEvtDeviceRecovered);
+  m.attr("LINK_INTERNAL") = static_cast<int>(kLinkInternal);
+  m.attr("LINK_PCIE") = static_cast<int>(kLinkPcie);
+  m.attr("LINK_XGMI") = static_cast<int>(kLinkXgmi);
+  m.attr("LINK_UNKNOWN") = static_cast<int>(kLinkUnknown);
+  m.def("event_kind_name", &event_kind_name);
+
+  py::class_<HwEvent>(m, "HwEvent")
+      .def(py::init([](int kind, int gpu, int partition, int peer, const std::string& msg) {
+             HwEvent e;
+             e.kind = kind;
+             e.gpu = gpu;
+             e.partition = partition;
+             e.peer = peer;
+             e.message = msg;
+             return e;
+           }),
+           py::arg("kind"), py::arg("gpu") = -1, py::arg("partition") = -1, py::arg("peer") = -1,
+           py::arg("message") = "")
+      .def_readwrite("kind", &HwEvent::kind)
+      .def_readwrite("gpu", &HwEvent::gpu)
+      .def_readwrite("partition", &HwEvent::partition)
+      .def_readwrite("peer", &HwEvent::peer)
+      .def_readwrite("message", &HwEvent::message)
+      .def_readwrite("ts_ns", &HwEvent::ts_ns);
+
+  py::class_<Backend, std::shared_ptr<Backend>>(m, "Backend")
+      .def_property_readonly("name", &Backend::name)
+      .def("discover",
+           [](Backend& b) {
+             std::vector<GpuInfo> g;
+             Topology t;
+             {
+               py::gil_scoped_release rel;
+               b.discover(&g, &t);
+             }
+             return py::make_tuple(g, t);
+           })
+      .def("sample",
+           [](Backend& b, int gpu) -> py::object {
+             GpuSample s;
+             bool ok;
+             {
+               py::gil_scoped_release rel;
+               ok = b.sample(gpu, &s);
+             }
+             if (!ok) return py::none();
+             return py::cast(s);
+           })
+      .def("arm_events", &Backend::arm_events, py::call_guard<py::gil_scoped_release>())
+      .def("shutdown", &Backend::shutdown, py::call_guard<py::gil_scoped_release>());
+
+  py::class_<FixtureBackend, Backend, std::shared_ptr<FixtureBackend>>(m, "FixtureBackend")
+      .def(py::init<uint64_t>(), py::arg("seed") = 1)
+      .def("add_gpu", &FixtureBackend::add_gpu)
+      .def("clear", &FixtureBackend::clear)
+      .def("set_link", &FixtureBackend::set_link)
+      .def("set_link_up", &FixtureBackend::set_link_up)
+      .def("schedule_event", &FixtureBackend::schedule_event)
+      .def("inject_event", &FixtureBackend::inject_event)
+      .def("set_fail_discovery", &FixtureBackend::set_fail_discovery)
+      .def("set_ecc_uncorrectable", &FixtureBackend::set_ecc_uncorrectable)
+      .def("set_gpu_present", &FixtureBackend::set_gpu_present)
+      .def_property_readonly("discover_calls", &FixtureBackend::discover_calls);
+
+  m.def("make_amdsmi_backend", &make_amdsmi_backend, py::call_guard<py::gil_scoped_release>());
+  m.def("amdsmi_available", &amdsmi_available, py::call_guard<py::gil_scoped_release>());
+
+  // ---- allocator (raw, for tests / Python policies) ----
+  py::class_<AllocDevice>(m, "AllocDevice")
+      .def(py::init([](int gpu, int partition, int numa, const std::string& base_id, bool annotated) {
+             AllocDevice d;
+             d.gpu = gpu;
+             d.partition = partition;
+             d.numa = numa;
+             d.base_id = base_id;
+             d.annotated = annotated;
+             return d;
+           }),
+           py::arg("gpu"), py::arg("partition") = -1, py::arg("numa") = -1, py::arg("base_id") = "",
+           py::arg("annotated") = false)
+      .def_readwrite("gpu", &AllocDevice::gpu)
+      .def_readwrite("partition", &AllocDevice::partition)
+      .def_readwrite("numa", &AllocDevice::numa)
+      .def_readwrite("base_id", &AllocDevice::base_id);
+  m.def("pair_score", &pair_score);
+  m.def("aligned_alloc", [](const Topology& t, const std::vector<AllocDevice>& d, const std::vector<int>& avail,
+                            const std::vector<int>& req, int size) {
+    AllocResult r = aligned_alloc(t, d, avail, req, size);
+    if (!r.ok) throw std::runtime_error(r.error);
+    return r.chosen;
+  });
+  m.def("distributed_alloc", [](const std::vector<AllocDevice>& d, const std::vector<int>& avail,
+                                const std::vector<int>& req, int size) {
+    AllocResult r = distributed_alloc(d, avail, req, size);
+    if (!r.ok) throw std::runtime_error(r.error);
+    return r.chosen;
+  });
+
+  // ---- device table ----
+  py::class_<TableDevice>(m, "TableDevice")
+      .def(py::init([](const std::string& id, int gpu, int partition, int numa, int replica,
+                       const std::vector<std::string>& paths, bool healthy) {
+             TableDevice d;
+             d.id = id;
+             d.gpu = gpu;
+             d.partition = partition;
+             d.numa = numa;
+             d.replica = replica;
+             d.host_paths = paths;
+             d.healthy = healthy;
+             return d;
+           }),
+           py::arg("id"), py::arg("gpu"), py::arg("partition") = -1, py::arg("numa") = -1, py::arg("replica") = -1,
+           py::arg("host_paths") = std::vector<std::string>{}, py::arg("healthy") = true)
+      .def_readonly("id", &TableDevice::id)
+      .def_readonly("gpu", &TableDevice::gpu)
+      .def_readonly("partition", &TableDevice::partition)
+      .def_readonly("numa", &TableDevice::numa)
+      .def_readonly("replica", &TableDevice::replica)
+      .def_readonly("host_paths", &TableDevice::host_paths)
+      .def_readonly("healthy", &TableDevice::healthy);
+
+  py::class_<TableConfig>(m, "TableConfig")
+      .def(py::init<>())
+      .def_readwrite("resource_name", &TableConfig::resource_name)
+      .def_readwrite("visible_env", &TableConfig::visible_env)
+      .def_readwrite("extra_envs", &TableConfig::extra_envs)
+      .def_readwrite("mount_kfd", &TableConfig::mount_kfd)
+      .def_readwrite("kfd_path", &TableConfig::kfd_path)
+      .def_readwrite("permissions", &TableConfig::permissions)
+      .def_readwrite("cdi", &TableConfig::cdi)
+      .def_readwrite("cdi_prefix", &TableConfig::cdi_prefix)
+      .def_readwrite("reject_unhealthy", &TableConfig::reject_unhealthy);
+
+  m.attr("RPC_OPTIONS") = static_cast<int>(kRpcOptions);
+  m.attr("RPC_LIST_AND_WATCH") = static_cast<int>(kRpcListAndWatch);
+  m.attr("RPC_PREFERRED") = static_cast<int>(kRpcPreferred);
+  m.attr("RPC_ALLOCATE") = static_cast<int>(kRpcAllocate);
+  m.attr("RPC_PRE_START") = static_cast<int>(kRpcPreStart);
+
+  py::class_<DeviceTable, std::shared_ptr<DeviceTable>>(m, "DeviceTable")
+      .def(py::init<TableConfig, std::vector<TableDevice>, Topology>())
+      .def_property_readonly("resource_name", [](const DeviceTable& t) { return t.config().resource_name; })
+      .def("__len__", &DeviceTable::size)
+      .def("device", [](const DeviceTable& t, size_t i) {
+        if (i >= t.size()) throw py::index_error();
+        return t.device(i);
+      })
+      .def("ids", &DeviceTable::ids)
+      .def("index_of", [](const DeviceTable& t, const std::string& id) { return t.index_of(id); })
+      .def("contains", &DeviceTable::contains)
+      .def_property_readonly("aligned_supported", &DeviceTable::aligned_supported)
+      .def("set_health", [](DeviceTable& t, const std::string& id, bool h) { return t.set_health(id, h); })
+      .def("set_gpu_health", &DeviceTable::set_gpu_health)
+      .def("healthy", [](const DeviceTable& t, const std::string& id) { return t.healthy(id); })
+      .def("healthy_count", &DeviceTable::healthy_count)
+      .def("set_link_up", &DeviceTable::set_link_up)
+      .def("topology", &DeviceTable::topology)
+      .def_property_readonly("version", &DeviceTable::version)
+      .def("list_and_watch", [](const DeviceTable& t) { return py::bytes(t.list_and_watch()); })
+      .def("options", [](const DeviceTable& t) { return py::bytes(t.options_bytes()); })
+      .def("allocate",
+           [](const DeviceTable& t, const py::bytes& req) {
+             std::string out;
+             const bool ok = t.allocate(std::string_view(PyBytes_AS_STRING(req.ptr()), PyBytes_GET_SIZE(req.ptr())), &out);
+             return ok_bytes(ok, out);
+           })
+      .def("preferred",
+           [](const DeviceTable& t, const py::bytes& req) {
+             std::string out;
+             const bool ok = t.preferred(std::string_view(PyBytes_AS_STRING(req.ptr()), PyBytes_GET_SIZE(req.ptr())), &out);
+             return ok_bytes(ok, out);
+           })
+      .def("preferred_ids",
+           [](const DeviceTable& t, const std::vector<std::string>& avail, const std::vector<std::string>& must,
+              int size) {
+             std::vector<std::string> ids;
+             AllocResult r = t.preferred_ids(avail, must, size, &ids);
+             if (!r.ok) throw std::runtime_error(r.error);
+             return ids;
+           })
+      .def("observe", &DeviceTable::observe)
+      .def("render_metrics", [](const DeviceTable& t) {
+        std::string s;
+        t.render_metrics(&s, true);
+        return s;
+      });
+
+  // ---- health ----
+  py::class_<HealthUpdate>(m, "HealthUpdate")
+      .def_readonly("ts_ns", &HealthUpdate::ts_ns)
+      .def_readonly("kind", &HealthUpdate::kind)
+      .def_readonly("gpu", &HealthUpdate::gpu)
+      .def_readonly("partition", &HealthUpdate::partition)
+      .def_readonly("healthy", &HealthUpdate::healthy)
+      .def_readonly("peer", &HealthUpdate::peer)
+      .def_readonly("link_up", &HealthUpdate::link_up)
+      .def_readonly("reason", &HealthUpdate::reason)
+      .def("__repr__", [](const HealthUpdate& u) {
+        return "<HealthUpdate " + std::string(event_kind_name(u.kind)) + " gpu=" + std::to_string(u.gpu) +
+               " healthy=" + std::to_string(u.healthy) + " " + u.reason + ">";
+      });
+
+  py::class_<HealthMonitor, std::shared_ptr<HealthMonitor>>(m, "HealthMonitor")
+      .def(py::init<std::shared_ptr<Backend>, int>(), py::arg("backend"), py::arg("lost_after_failures") = 3)
+      .def("set_gpu_count", &HealthMonitor::set_gpu_count)
+      .def("start", &HealthMonitor::start, py::call_guard<py::gil_scoped_release>())
+      .def("stop", &HealthMonitor::stop, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("running", &HealthMonitor::running)
+      .def("process", &HealthMonitor::process, py::call_guard<py::gil_scoped_release>())
+      .def("pop", &HealthMonitor::pop, py::call_guard<py::gil_scoped_release>(), py::arg("timeout_ms") = 200)
+      .def("gpu_healthy", &HealthMonitor::gpu_healthy)
+      .def_property_readonly("events_seen", &HealthMonitor::events_seen);
+
+  // ---- exporter ----
+  py::class_<PartitionLabel>(m, "PartitionLabel")
+      .def(py::init([](int gpu, int partition, const std::string& device_id, const std::string& resource) {
+        PartitionLabel l;
+        l.gpu = gpu;
+        l.partition = partition;
+        l.device_id = device_id;
+        l.resource = resource;
+        return l;
+      }));
+
+  py::class_<Exporter, std::shared_ptr<Exporter>>(m, "Exporter")
+      .def(py::init<>())
+      .def("set_inventory", &Exporter::set_inventory)
+      .def("set_partition_labels", &Exporter::set_partition_labels)
+      .def("set_build_info", &Exporter::set_build_info)
+      .def("set_tables", &Exporter::set_tables)
+      .def("set_extra", &Exporter::set_extra)
+      .def("start", &Exporter::start, py::arg("backend"), py::arg("interval_ms"), py::arg("monitor") = nullptr,
+           py::call_guard<py::gil_scoped_release>())
+      .def("stop", &Exporter::stop, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("running", &Exporter::running)
+      .def("sample_once", &Exporter::sample_once, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("samples_total", &Exporter::samples_total)
+      .def("last_sample", &Exporter::last_sample)
+      .def("render", [](const Exporter& e) {
+        std::string s;
+        {
+          py::gil_scoped_release rel;
+          e.render(&s);
+        }
+        return s;
+      });
+
+  // ---- http ----
+  py::class_<HttpConfig>(m, "HttpConfig")
+      .def(py::init<>())
+      .def_readwrite("host", &HttpConfig::host)
+      .def_readwrite("port", &HttpConfig::port)
+      .def_readwrite("threads", &HttpConfig::threads)
+      .def_readwrite("access_log", &HttpConfig::access_log)
+      .def_readwrite("idle_timeout_s", &HttpConfig::idle_timeout_s)
+      .def_readwrite("read_timeout_s", &HttpConfig::read_timeout_s)
+      .def_readwrite("version", &HttpConfig::version);
+
+  py::class_<HttpServer, std::shared_ptr<HttpServer>>(m, "HttpServer")
+      .def(py::init<HttpConfig, std::shared_ptr<Exporter>>())
+      .def("start", &HttpServer::start, py::call_guard<py::gil_scoped_release>())
+      .def("stop", &HttpServer::stop, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("running", &HttpServer::running)
+      .def_property_readonly("port", &HttpServer::port)
+      .def_property_readonly("requests_total", &HttpServer::requests_total)
+      .def("render_http_metrics", [](const HttpServer& s) {
+        std::string o;
+        s.render_http_metrics(&o);
+        return o;
+      })
+      .def("set_restart_hook", [](HttpServer& s, py::object fn) {
+        if (fn.is_none()) {
+          s.set_restart_hook(nullptr);
+          return;
+        }
+        // keep the callable alive; destroy it only while holding the GIL
+        auto holder = std::shared_ptr<py::object>(new py::object(fn), [](py::object* o) {
+          py::gil_scoped_acquire g;
+          delete o;
+        });
+        s.set_restart_hook([holder]() {
+          py::gil_scoped_acquire g;
+          try {
+            (*holder)();
+          } catch (py::error_already_set& e) {
+            e.discard_as_unraisable("restart hook");
+          }
+        });
+      });
+
+  // ---- fs watch ----
+  py::class_<DirWatcher, std::shared_ptr<DirWatcher>>(m, "DirWatcher")
+      .def(py::init<const std::string&>())
+      .def("read",
+           [](DirWatcher& w, int timeout_ms) {
+             std::vector<FsEvent> evs;
+             {
+               py::gil_scoped_release rel;
+               evs = w.read(timeout_ms);
+             }
+             py::list out;
+             for (auto& e : evs) out.append(py::make_tuple(e.name, e.mask, e.create(), e.remove()));
+             return out;
+           },
+           py::arg("timeout_ms") = 200)
+      .def("close", &DirWatcher::close)
+      .def_property_readonly("dir", &DirWatcher::dir);
+}

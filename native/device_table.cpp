@@ -1,0 +1,313 @@
+#include "device_table.h"
+
+#include <algorithm>
+#include <mutex>
+
+#include "pbwire.h"
+
+namespace amdgpu_dp {
+
+const char* rpc_name(int rpc) {
+  switch (rpc) {
+    case kRpcOptions: return "GetDevicePluginOptions";
+    case kRpcListAndWatch: return "ListAndWatch";
+    case kRpcPreferred: return "GetPreferredAllocation";
+    case kRpcAllocate: return "Allocate";
+    case kRpcPreStart: return "PreStartContainer";
+    default: return "unknown";
+  }
+}
+
+namespace {
+std::string map_entry(std::string_view k, std::string_view v) {
+  std::string e;
+  pb::put_bytes(&e, 1, k);
+  pb::put_bytes(&e, 2, v);
+  return e;
+}
+std::string device_spec(std::string_view container, std::string_view host, std::string_view perms) {
+  std::string s;
+  pb::put_string_nz(&s, 1, container);
+  pb::put_string_nz(&s, 2, host);
+  pb::put_string_nz(&s, 3, perms);
+  return s;
+}
+std::string base_of(const std::string& id) {
+  const size_t p = id.find("::");
+  return p == std::string::npos ? id : id.substr(0, p);
+}
+}  // namespace
+
+DeviceTable::DeviceTable(TableConfig cfg, std::vector<TableDevice> devices, Topology topo)
+    : cfg_(std::move(cfg)), devs_(std::move(devices)), topo_(std::move(topo)) {
+  for (int r = 0; r < kRpcCount; ++r) {
+    hist_[r] = std::make_unique<Histogram>(rpc_buckets());
+    errors_[r].store(0);
+  }
+  for (size_t i = 0; i < devs_.size(); ++i) {
+    const auto& d = devs_[i];
+    index_.emplace(std::string_view(devs_[i].id), static_cast<int>(i));
+    AllocDevice a;
+    a.gpu = d.gpu;
+    a.partition = d.partition;
+    a.numa = d.numa;
+    a.base_id = base_of(d.id);
+    a.annotated = d.id.find("::") != std::string::npos;
+    if (a.annotated) aligned_ok_ = false;
+    alloc_devs_.push_back(a);
+    std::string frag;
+    for (const auto& p : d.host_paths) pb::put_bytes(&frag, 3, device_spec(p, p, cfg_.permissions));
+    spec_frag_.push_back(std::move(frag));
+  }
+  if (cfg_.mount_kfd) pb::put_bytes(&kfd_frag_, 3, device_spec(cfg_.kfd_path, cfg_.kfd_path, cfg_.permissions));
+  for (const auto& kv : cfg_.extra_envs) pb::put_bytes(&env_extra_frag_, 1, map_entry(kv.first, kv.second));
+  std::unique_lock<std::shared_mutex> lk(mu_);
+  rebuild_law_locked();
+}
+
+std::vector<std::string> DeviceTable::ids() const {
+  std::vector<std::string> out;
+  out.reserve(devs_.size());
+  for (const auto& d : devs_) out.push_back(d.id);
+  return out;
+}
+
+int DeviceTable::index_of(std::string_view id) const {
+  auto it = index_.find(id);
+  return it == index_.end() ? -1 : it->second;
+}
+
+bool DeviceTable::contains(const std::vector<std::string>& ids) const {
+  for (const auto& id : ids)
+    if (index_of(id) < 0) return false;
+  return true;
+}
+
+void DeviceTable::rebuild_law_locked() {
+  std::string out;
+  for (const auto& d : devs_) {
+    std::string dev;
+    pb::put_string_nz(&dev, 1, d.id);
+    pb::put_string_nz(&dev, 2, d.healthy ? "Healthy" : "Unhealthy");
+    if (d.numa >= 0) {
+      std::string node, topo;
+      pb::put_int_nz(&node, 1, d.numa);
+      pb::put_bytes(&topo, 1, node);
+      pb::put_bytes(&dev, 3, topo);
+    }
+    pb::put_bytes(&out, 1, dev);
+  }
+  law_.swap(out);
+}
+
+bool DeviceTable::set_health(std::string_view id, bool healthy) {
+  std::unique_lock<std::shared_mutex> lk(mu_);
+  const int i = index_of(id);
+  if (i < 0 || devs_[i].healthy == healthy) return false;
+  devs_[i].healthy = healthy;
+  rebuild_law_locked();
+  version_.fetch_add(1, std::memory_order_acq_rel);
+  return true;
+}
+
+int DeviceTable::set_gpu_health(int gpu, int partition, bool healthy) {
+  std::unique_lock<std::shared_mutex> lk(mu_);
+  int changed = 0;
+  for (auto& d : devs_) {
+    if (d.gpu != gpu) continue;
+    // a partition event hits that partition (and the whole-GPU device containing it)
+    if (partition >= 0 && d.partition >= 0 && d.partition != partition) continue;
+    if (d.healthy != healthy) {
+      d.healthy = healthy;
+      ++changed;
+    }
+  }
+  if (changed) {
+    rebuild_law_locked();
+    version_.fetch_add(1, std::memory_order_acq_rel);
+  }
+  return changed;
+}
+
+bool DeviceTable::healthy(std::string_view id) const {
+  std::shared_lock<std::shared_mutex> lk(mu_);
+  const int i = index_of(id);
+  return i >= 0 && devs_[i].healthy;
+}
+
+int DeviceTable::healthy_count() const {
+  std::shared_lock<std::shared_mutex> lk(mu_);
+  int n = 0;
+  for (const auto& d : devs_) n += d.healthy;
+  return n;
+}
+
+void DeviceTable::set_link_up(int a, int b, bool up) {
+  std::unique_lock<std::shared_mutex> lk(mu_);
+  if (a < 0 || b < 0 || a >= topo_.n || b >= topo_.n) return;
+  topo_.at(a, b).up = up;
+  topo_.at(b, a).up = up;
+}
+
+Topology DeviceTable::topology() const {
+  std::shared_lock<std::shared_mutex> lk(mu_);
+  return topo_;
+}
+
+std::string DeviceTable::list_and_watch() const {
+  std::shared_lock<std::shared_mutex> lk(mu_);
+  return law_;
+}
+
+std::string DeviceTable::options_bytes() const {
+  std::string s;
+  pb::put_bool_nz(&s, 2, true);  // get_preferred_allocation_available
+  return s;
+}
+
+std::string DeviceTable::encode_container_alloc(const std::vector<int>& idx) const {
+  std::string joined;
+  for (size_t k = 0; k < idx.size(); ++k) {
+    if (k) joined.push_back(',');
+    joined.append(devs_[idx[k]].id);
+  }
+  std::string c;
+  if (!cfg_.visible_env.empty()) pb::put_bytes(&c, 1, map_entry(cfg_.visible_env, joined));
+  c.append(env_extra_frag_);
+  c.append(kfd_frag_);
+  // de-duplicate device nodes (replicas of one partition share its render node)
+  std::vector<int> seen_base;
+  for (int i : idx) {
+    bool dup = false;
+    for (int j : seen_base)
+      if (spec_frag_[j] == spec_frag_[i]) {
+        dup = true;
+        break;
+      }
+    if (dup) continue;
+    seen_base.push_back(i);
+    c.append(spec_frag_[i]);
+  }
+  if (cfg_.cdi) {
+    for (int i : idx) {
+      std::string cdi;
+      pb::put_bytes(&cdi, 1, cfg_.cdi_prefix + alloc_devs_[i].base_id);
+      pb::put_bytes(&c, 5, cdi);
+    }
+  }
+  return c;
+}
+
+bool DeviceTable::allocate(std::string_view req, std::string* out) const {
+  std::vector<std::vector<std::string_view>> reqs;
+  try {
+    reqs = pb::decode_allocate_request(req);
+  } catch (const pb::DecodeError& e) {
+    *out = std::string("malformed AllocateRequest: ") + e.what();
+    return false;
+  }
+  std::shared_lock<std::shared_mutex> lk(mu_);
+  std::string resp;
+  std::vector<int> idx;
+  for (const auto& ids : reqs) {
+    idx.clear();
+    for (const auto& id : ids) {
+      const int i = index_of(id);
+      if (i < 0) {
+        *out = "invalid allocation request for '" + cfg_.resource_name + "': unknown device: " + std::string(id);
+        return false;
+      }
+      if (cfg_.reject_unhealthy && !devs_[i].healthy) {
+        *out = "invalid allocation request for '" + cfg_.resource_name + "': device is Unhealthy: " + std::string(id);
+        return false;
+      }
+      idx.push_back(i);
+    }
+    pb::put_bytes(&resp, 1, encode_container_alloc(idx));
+  }
+  out->swap(resp);
+  return true;
+}
+
+AllocResult DeviceTable::preferred_ids(const std::vector<std::string>& avail, const std::vector<std::string>& must,
+                                       int size, std::vector<std::string>* out_ids) const {
+  std::vector<int> a, m;
+  bool any_annotated = false;
+  for (const auto& id : avail) {
+    if (id.find("::") != std::string::npos) any_annotated = true;
+    const int i = index_of(id);
+    if (i >= 0) a.push_back(i);
+  }
+  for (const auto& id : must) {
+    const int i = index_of(id);
+    if (i < 0) {
+      AllocResult r;
+      r.ok = false;
+      r.error = "unknown device in must_include_deviceIDs: " + id;
+      return r;
+    }
+    m.push_back(i);
+  }
+  AllocResult r;
+  {
+    std::shared_lock<std::shared_mutex> lk(mu_);
+    if (aligned_ok_ && !any_annotated) r = aligned_alloc(topo_, alloc_devs_, a, m, size);
+    else r = distributed_alloc(alloc_devs_, a, m, size);
+  }
+  if (r.ok && out_ids) {
+    out_ids->clear();
+    for (int i : r.chosen) out_ids->push_back(devs_[i].id);
+  }
+  return r;
+}
+
+bool DeviceTable::preferred(std::string_view req, std::string* out) const {
+  std::vector<pb::PreferredRequest> reqs;
+  try {
+    reqs = pb::decode_preferred_request(req);
+  } catch (const pb::DecodeError& e) {
+    *out = std::string("malformed PreferredAllocationRequest: ") + e.what();
+    return false;
+  }
+  std::string resp;
+  std::vector<std::string> avail, must, ids;
+  for (const auto& r : reqs) {
+    avail.assign(r.available.begin(), r.available.end());
+    must.assign(r.must_include.begin(), r.must_include.end());
+    AllocResult ar = preferred_ids(avail, must, r.size, &ids);
+    if (!ar.ok) {
+      *out = "error getting list of preferred allocation devices: " + ar.error;
+      return false;
+    }
+    std::string c;
+    for (const auto& id : ids) pb::put_bytes(&c, 1, id);
+    pb::put_bytes(&resp, 1, c);
+  }
+  out->swap(resp);
+  return true;
+}
+
+void DeviceTable::observe(int rpc, double seconds, bool error) const {
+  if (rpc < 0 || rpc >= kRpcCount) return;
+  hist_[rpc]->observe(seconds);
+  if (error) errors_[rpc].fetch_add(1, std::memory_order_relaxed);
+}
+
+void DeviceTable::render_metric_headers(std::string* out) {
+  append_header(out, "amdgpu_device_plugin_rpc_duration_seconds",
+                "Latency of kubelet DevicePlugin RPCs served by this plugin.", "histogram");
+}
+
+void DeviceTable::render_metrics(std::string* out, bool with_headers) const {
+  if (with_headers) render_metric_headers(out);
+  std::string labels;
+  for (int r = 0; r < kRpcCount; ++r) {
+    if (hist_[r]->count() == 0) continue;
+    labels.assign("resource=\"");
+    append_label_value(&labels, cfg_.resource_name);
+    labels.append("\",rpc=\"").append(rpc_name(r)).append("\",");
+    hist_[r]->render(out, "amdgpu_device_plugin_rpc_duration_seconds", labels);
+  }
+}
+
+}  // namespace amdgpu_dp

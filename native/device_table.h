@@ -1,0 +1,119 @@
+// Per-resource device table: the data behind one kubelet DevicePlugin endpoint.
+//
+// Reference equivalents: device.Devices map + set algebra (device/devices.go:32-209),
+// NvidiaDevicePlugin.ListAndWatch/GetPreferredAllocation/Allocate
+// (plugin/plugin.go:173-225).  Differences by design:
+//   * deterministic insertion order (reference iterates Go maps: defect D14)
+//   * Allocate returns DeviceSpecs (/dev/kfd + the partition's render node) instead of
+//     only an env var (defect D17), refuses Unhealthy devices
+//   * responses are encoded from pre-built per-device protobuf fragments
+//   * ListAndWatch bytes are cached and versioned; health changes bump the version
+#pragma once
+
+#include <atomic>
+#include <memory>
+#include <shared_mutex>
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "allocator.h"
+#include "backend.h"
+#include "metrics.h"
+
+namespace amdgpu_dp {
+
+struct TableDevice {
+  std::string id;
+  int gpu = -1;
+  int partition = -1;  // -1 = whole physical GPU
+  int numa = -1;
+  int replica = -1;    // >=0 when advertised as "<base>::<replica>"
+  std::vector<std::string> host_paths;  // device nodes to expose (render/card)
+  bool healthy = true;
+};
+
+struct TableConfig {
+  std::string resource_name = "amd.com/gpu";
+  std::string visible_env = "AMD_VISIBLE_DEVICES";
+  std::vector<std::pair<std::string, std::string>> extra_envs;
+  bool mount_kfd = true;
+  std::string kfd_path = "/dev/kfd";
+  std::string permissions = "rw";
+  bool cdi = false;
+  std::string cdi_prefix = "amd.com/gpu=";
+  bool reject_unhealthy = true;
+};
+
+enum Rpc : int {
+  kRpcOptions = 0,
+  kRpcListAndWatch,
+  kRpcPreferred,
+  kRpcAllocate,
+  kRpcPreStart,
+  kRpcCount
+};
+
+const char* rpc_name(int rpc);
+
+class DeviceTable {
+ public:
+  DeviceTable(TableConfig cfg, std::vector<TableDevice> devices, Topology topo);
+
+  const TableConfig& config() const { return cfg_; }
+  size_t size() const { return devs_.size(); }
+  const TableDevice& device(size_t i) const { return devs_[i]; }
+  std::vector<std::string> ids() const;
+  int index_of(std::string_view id) const;
+  bool contains(const std::vector<std::string>& ids) const;
+  bool aligned_supported() const { return aligned_ok_; }
+
+  // Health: return true if anything changed (ListAndWatch version bumps).
+  bool set_health(std::string_view id, bool healthy);
+  int set_gpu_health(int gpu, int partition, bool healthy);
+  bool healthy(std::string_view id) const;
+  int healthy_count() const;
+  void set_link_up(int a, int b, bool up);
+  Topology topology() const;
+
+  uint64_t version() const { return version_.load(std::memory_order_acquire); }
+  std::string list_and_watch() const;  // ListAndWatchResponse bytes (cached)
+
+  // RPC bodies.  Return true and response bytes in *out, or false and an error message.
+  bool allocate(std::string_view req, std::string* out) const;
+  bool preferred(std::string_view req, std::string* out) const;
+  std::string options_bytes() const;  // DevicePluginOptions
+
+  // Convenience for Python callers / tests
+  AllocResult preferred_ids(const std::vector<std::string>& avail, const std::vector<std::string>& must, int size,
+                            std::vector<std::string>* out_ids) const;
+
+  void observe(int rpc, double seconds, bool error) const;
+  void render_metrics(std::string* out, bool with_headers) const;
+  static void render_metric_headers(std::string* out);
+
+ private:
+  void rebuild_law_locked();
+  std::string encode_container_alloc(const std::vector<int>& idx) const;
+
+  TableConfig cfg_;
+  std::vector<TableDevice> devs_;
+  std::vector<AllocDevice> alloc_devs_;
+  std::unordered_map<std::string_view, int> index_;
+  std::vector<std::string> spec_frag_;  // per device: encoded DeviceSpec fields (tag 3)
+  std::string kfd_frag_;
+  std::string env_extra_frag_;
+  bool aligned_ok_ = true;
+
+  mutable std::shared_mutex mu_;
+  Topology topo_;
+  std::string law_;  // cached ListAndWatchResponse
+  std::atomic<uint64_t> version_{1};
+
+  mutable std::unique_ptr<Histogram> hist_[kRpcCount];
+  mutable std::atomic<uint64_t> errors_[kRpcCount];
+};
+
+}  // namespace amdgpu_dp

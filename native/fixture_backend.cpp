@@ -1,0 +1,228 @@
+#include "fixture_backend.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <stdexcept>
+
+namespace amdgpu_dp {
+
+namespace {
+// splitmix64: cheap deterministic noise for the telemetry generators
+uint64_t mix(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+double unit(uint64_t x) { return (mix(x) >> 11) * (1.0 / 9007199254740992.0); }
+}  // namespace
+
+FixtureBackend::FixtureBackend(uint64_t seed) : seed_(seed) {}
+
+void FixtureBackend::add_gpu(const GpuInfo& g) {
+  std::lock_guard<std::mutex> lk(mu_);
+  GpuInfo copy = g;
+  copy.index = static_cast<int>(gpus_.size());
+  for (auto& p : copy.partitions) p.gpu = copy.index;
+  gpus_.push_back(copy);
+  Topology old = topo_;
+  topo_.resize(static_cast<int>(gpus_.size()));
+  for (int a = 0; a < old.n; ++a)
+    for (int b = 0; b < old.n; ++b) topo_.at(a, b) = old.at(a, b);
+  ecc_ue_.push_back(0);
+  present_.push_back(true);
+}
+
+void FixtureBackend::clear() {
+  std::lock_guard<std::mutex> lk(mu_);
+  gpus_.clear();
+  topo_.resize(0);
+  ecc_ue_.clear();
+  present_.clear();
+  scheduled_.clear();
+  pending_.clear();
+}
+
+void FixtureBackend::set_link(int a, int b, const Link& l) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (a < 0 || b < 0 || a >= topo_.n || b >= topo_.n) throw std::out_of_range("set_link: bad gpu index");
+  topo_.at(a, b) = l;
+  topo_.at(b, a) = l;
+}
+
+void FixtureBackend::set_link_up(int a, int b, bool up) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (a < 0 || b < 0 || a >= topo_.n || b >= topo_.n) throw std::out_of_range("set_link_up: bad gpu index");
+    topo_.at(a, b).up = up;
+    topo_.at(b, a).up = up;
+    HwEvent e;
+    e.ts_ns = now_ns();
+    e.kind = up ? kEvtLinkUp : kEvtLinkDown;
+    e.gpu = a;
+    e.peer = b;
+    e.message = std::string("fixture xgmi link ") + std::to_string(a) + "-" + std::to_string(b) + (up ? " up" : " down");
+    pending_.push_back(e);
+  }
+  cv_.notify_all();
+}
+
+void FixtureBackend::set_ecc_uncorrectable(int gpu, int64_t count) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (gpu < 0 || gpu >= static_cast<int>(ecc_ue_.size())) throw std::out_of_range("bad gpu");
+  ecc_ue_[gpu] = count;
+}
+
+void FixtureBackend::set_gpu_present(int gpu, bool present) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (gpu < 0 || gpu >= static_cast<int>(present_.size())) throw std::out_of_range("bad gpu");
+  present_[gpu] = present;
+}
+
+void FixtureBackend::discover(std::vector<GpuInfo>* gpus, Topology* topo) {
+  std::lock_guard<std::mutex> lk(mu_);
+  ++discover_calls_;
+  if (fail_discovery_) throw std::runtime_error("fixture: discovery failure injected");
+  gpus->clear();
+  // A GPU that "fell off the bus" disappears from discovery, like a real one.
+  std::vector<int> remap(gpus_.size(), -1);
+  for (size_t i = 0; i < gpus_.size(); ++i) {
+    if (!present_[i]) continue;
+    remap[i] = static_cast<int>(gpus->size());
+    GpuInfo g = gpus_[i];
+    g.index = remap[i];
+    for (auto& p : g.partitions) p.gpu = g.index;
+    gpus->push_back(std::move(g));
+  }
+  topo->resize(static_cast<int>(gpus->size()));
+  for (size_t a = 0; a < gpus_.size(); ++a)
+    for (size_t b = 0; b < gpus_.size(); ++b)
+      if (remap[a] >= 0 && remap[b] >= 0) topo->at(remap[a], remap[b]) = topo_.at(a, b);
+}
+
+bool FixtureBackend::sample(int gpu, GpuSample* s) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (gpu < 0 || gpu >= static_cast<int>(gpus_.size()) || !present_[gpu]) return false;
+  const GpuInfo& g = gpus_[gpu];
+  const int64_t t = now_ns();
+  const double ts = t * 1e-9;
+  const uint64_t tick = static_cast<uint64_t>(ts * 10);  // noise changes at 10 Hz
+  const uint64_t key = seed_ * 1000003ull + gpu * 7919ull;
+  s->ts_ns = t;
+  const double load = 0.5 + 0.45 * std::sin(ts * 0.7 + gpu);
+  s->power_w = 220.0 + 1100.0 * load + 10.0 * unit(key ^ tick);
+  s->energy_j = 1e6 + ts * 700.0;
+  s->temp_edge_c = 40 + 30 * load;
+  s->temp_hotspot_c = 45 + 45 * load + 2 * unit(key + 1 + tick);
+  s->temp_mem_c = 42 + 35 * load;
+  s->num_hbm = 8;
+  for (int h = 0; h < 8; ++h) s->temp_hbm_c[h] = 44 + 33 * load + unit(key + 10 + h + tick);
+  s->gfx_activity_pct = 100.0 * load;
+  s->umc_activity_pct = 70.0 * load;
+  s->gfxclk_mhz = 1500 + 900 * load;
+  s->uclk_mhz = 1900;
+  s->vram_total_bytes = static_cast<double>(g.vram_total_bytes);
+  s->vram_used_bytes = g.vram_total_bytes * 0.6 * load;
+  s->ecc_correctable = static_cast<int64_t>(ts) % 3;
+  s->ecc_uncorrectable = ecc_ue_[gpu];
+  s->throttle_status = 0;
+  s->num_links = 0;
+  for (int peer = 0; peer < topo_.n && s->num_links < kMaxXgmiLinks; ++peer) {
+    if (peer == gpu || topo_.at(gpu, peer).type != kLinkXgmi) continue;
+    const int k = s->num_links++;
+    s->link_peer[k] = peer;
+    s->link_up[k] = topo_.at(gpu, peer).up ? 1 : 0;
+    s->link_read_kb[k] = 1e6 * ts * load;
+    s->link_write_kb[k] = 0.9e6 * ts * load;
+  }
+  s->num_partitions = std::min<int>(static_cast<int>(g.partitions.size()), kMaxPartitions);
+  for (int p = 0; p < s->num_partitions; ++p) {
+    s->partition_gfx_busy_pct[p] = 100.0 * (0.5 + 0.45 * std::sin(ts * 0.7 + gpu + 0.3 * p));
+    s->partition_vram_used_bytes[p] = s->vram_used_bytes / std::max(1, s->num_partitions);
+  }
+  s->ok = true;
+  return true;
+}
+
+void FixtureBackend::arm_events() {
+  std::lock_guard<std::mutex> lk(mu_);
+  armed_at_ns_ = mono_ns();
+  shutdown_ = false;
+}
+
+void FixtureBackend::schedule_event(double delay_s, const HwEvent& e) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    scheduled_.push_back({delay_s, e});
+    std::stable_sort(scheduled_.begin(), scheduled_.end(),
+                     [](const Scheduled& a, const Scheduled& b) { return a.delay_s < b.delay_s; });
+  }
+  cv_.notify_all();
+}
+
+void FixtureBackend::inject_event(const HwEvent& e) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    HwEvent copy = e;
+    if (copy.ts_ns == 0) copy.ts_ns = now_ns();
+    pending_.push_back(copy);
+  }
+  cv_.notify_all();
+}
+
+void FixtureBackend::shutdown() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    shutdown_ = true;
+  }
+  cv_.notify_all();
+}
+
+int FixtureBackend::wait_events(int timeout_ms, std::vector<HwEvent>* out) {
+  std::unique_lock<std::mutex> lk(mu_);
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+  for (;;) {
+    // promote due scheduled events
+    if (armed_at_ns_ != 0) {
+      const double elapsed = (mono_ns() - armed_at_ns_) * 1e-9;
+      while (!scheduled_.empty() && scheduled_.front().delay_s <= elapsed) {
+        HwEvent e = scheduled_.front().ev;
+        e.ts_ns = now_ns();
+        if (e.kind == kEvtEccUncorrectable && e.gpu >= 0 && e.gpu < static_cast<int>(ecc_ue_.size()))
+          ecc_ue_[e.gpu] += 1;
+        if ((e.kind == kEvtLinkDown || e.kind == kEvtLinkUp) && e.gpu >= 0 && e.peer >= 0 &&
+            e.gpu < topo_.n && e.peer < topo_.n) {
+          topo_.at(e.gpu, e.peer).up = topo_.at(e.peer, e.gpu).up = (e.kind == kEvtLinkUp);
+        }
+        pending_.push_back(e);
+        scheduled_.erase(scheduled_.begin());
+      }
+    }
+    if (!pending_.empty()) {
+      int n = 0;
+      while (!pending_.empty()) {
+        out->push_back(pending_.front());
+        pending_.pop_front();
+        ++n;
+      }
+      return n;
+    }
+    if (shutdown_) return 0;
+    auto wake = deadline;
+    if (armed_at_ns_ != 0 && !scheduled_.empty()) {
+      const double elapsed = (mono_ns() - armed_at_ns_) * 1e-9;
+      const auto due = std::chrono::steady_clock::now() +
+                       std::chrono::microseconds(static_cast<int64_t>((scheduled_.front().delay_s - elapsed) * 1e6) + 1);
+      if (due < wake) wake = due;
+    }
+    if (cv_.wait_until(lk, wake) == std::cv_status::timeout && std::chrono::steady_clock::now() >= deadline) {
+      // one last promotion pass happens on the next loop iteration only if due; exit now
+      if (armed_at_ns_ == 0 || scheduled_.empty() ||
+          scheduled_.front().delay_s > (mono_ns() - armed_at_ns_) * 1e-9)
+        return 0;
+    }
+  }
+}
+
+}  // namespace amdgpu_dp

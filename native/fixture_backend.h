@@ -1,0 +1,59 @@
+// Scripted hardware backend: N fake MI355X GPUs x {SPX..CPX} x {NPS1..NPS8},
+// an xGMI link matrix with per-link health, deterministic telemetry generators and
+// timed fault scripts.  The reference has no fake NVML at all; this is
+// the seam every CPU test and the BASELINE "Mock-device backend" config run on.
+#pragma once
+
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+
+#include "backend.h"
+
+namespace amdgpu_dp {
+
+class FixtureBackend : public Backend {
+ public:
+  explicit FixtureBackend(uint64_t seed = 1);
+  std::string name() const override { return "fixture"; }
+  void discover(std::vector<GpuInfo>* gpus, Topology* topo) override;
+  bool sample(int gpu, GpuSample* out) override;
+  int wait_events(int timeout_ms, std::vector<HwEvent>* out) override;
+  void arm_events() override;
+  void shutdown() override;
+
+  // --- configuration (called before / between discoveries) ---
+  void add_gpu(const GpuInfo& g);
+  void clear();
+  void set_link(int a, int b, const Link& l);  // symmetric
+  void set_link_up(int a, int b, bool up);      // also emits LinkDown/LinkUp events
+  // Event `kind` fires `delay_s` seconds after arm_events().
+  void schedule_event(double delay_s, const HwEvent& e);
+  // Event fires immediately (wakes wait_events).
+  void inject_event(const HwEvent& e);
+  void set_fail_discovery(bool fail) { fail_discovery_ = fail; }
+  void set_ecc_uncorrectable(int gpu, int64_t count);
+  void set_gpu_present(int gpu, bool present);
+  int discover_calls() const { return discover_calls_; }
+
+ private:
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<GpuInfo> gpus_;
+  Topology topo_;
+  std::deque<HwEvent> pending_;
+  struct Scheduled {
+    double delay_s;
+    HwEvent ev;
+  };
+  std::vector<Scheduled> scheduled_;
+  std::vector<int64_t> ecc_ue_;
+  std::vector<bool> present_;
+  int64_t armed_at_ns_ = 0;
+  uint64_t seed_;
+  bool fail_discovery_ = false;
+  bool shutdown_ = false;
+  int discover_calls_ = 0;
+};
+
+}  // namespace amdgpu_dp

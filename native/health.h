@@ -1,0 +1,83 @@
+// Device health monitor: the producer the reference never had.
+//
+// Reference: plugin/plugin.go:40,53,181-186 declare a `health` channel consumed by
+// ListAndWatch, but nothing ever sends on it (defect D9; README "driver monitoring"
+// unimplemented).  Here two native sources feed one de-duplicated state machine:
+//   * hardware events (amdsmi_get_gpu_event_notification: PRE/POST_RESET, thermal,
+//     VM faults; or the fixture's scripted faults)        -> event thread
+//   * telemetry polling (ECC uncorrectable deltas, xGMI link up/down, device lost)
+//                                                          -> sampler thread
+// Transitions go both ways (Unhealthy *and* back to Healthy) and are queued for the
+// plugin manager, which pushes a fresh ListAndWatch response.
+#pragma once
+
+#include <condition_variable>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "backend.h"
+
+namespace amdgpu_dp {
+
+struct HealthUpdate {
+  int64_t ts_ns = 0;
+  int kind = kEvtNone;
+  int gpu = -1;
+  int partition = -1;
+  int healthy = -1;  // 1 healthy, 0 unhealthy, -1 = not a health change (link/info)
+  int peer = -1;     // link events
+  int link_up = -1;
+  std::string reason;
+};
+
+class HealthMonitor {
+ public:
+  explicit HealthMonitor(std::shared_ptr<Backend> backend, int lost_after_failures = 3);
+  ~HealthMonitor();
+
+  void set_gpu_count(int n);
+  void start();
+  void stop();
+  bool running() const { return running_; }
+
+  // Called by the telemetry sampler after every sample of `gpu`.
+  void on_sample(int gpu, bool ok, const GpuSample& s);
+  // Feed an event as if it came from the backend (tests, canary failures).
+  void process(const HwEvent& e);
+
+  // Blocks up to timeout_ms; returns queued updates (possibly empty).
+  std::vector<HealthUpdate> pop(int timeout_ms);
+  bool gpu_healthy(int gpu) const;
+  uint64_t events_seen() const { return events_seen_; }
+
+ private:
+  struct GpuState {
+    bool resetting = false;
+    bool ecc_bad = false;
+    bool lost = false;
+    int failures = 0;
+    int64_t last_ue = -1;
+    bool reported_healthy = true;
+    std::map<int, int> link_up;  // peer -> 1/0
+  };
+  void loop();
+  void emit_locked(HealthUpdate u);
+  void reconcile_locked(int gpu, int kind, const std::string& reason);
+
+  std::shared_ptr<Backend> backend_;
+  int lost_after_;
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<HealthUpdate> queue_;
+  std::vector<GpuState> state_;
+  std::thread thread_;
+  volatile bool running_ = false;
+  bool stop_ = false;
+  uint64_t events_seen_ = 0;
+};
+
+}  // namespace amdgpu_dp

@@ -1,0 +1,550 @@
+#include "httpd.h"
+
+#include <arpa/inet.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/epoll.h>
+#include <sys/socket.h>
+#include <sys/uio.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <ctime>
+#include <stdexcept>
+#include <unordered_map>
+
+namespace amdgpu_dp {
+
+namespace {
+
+const char* kMethodNames[] = {"GET", "POST", "PUT", "DELETE", "PATCH", "HEAD", "OPTIONS", "OTHER"};
+const char* kHandlerNames[] = {"/", "/metrics", "/health", "/restart", "/not-found"};
+const char* kStatusNames[] = {"1xx", "2xx", "3xx", "4xx", "5xx"};
+
+int method_index(const std::string& m) {
+  for (int i = 0; i < 7; ++i)
+    if (m == kMethodNames[i]) return i;
+  return 7;
+}
+
+int status_class(int status) {  // middleware/echo_metric.go:50-61
+  if (status < 200) return 0;
+  if (status < 300) return 1;
+  if (status < 400) return 2;
+  if (status < 500) return 3;
+  return 4;
+}
+
+const char* reason(int status) {
+  switch (status) {
+    case 200: return "OK";
+    case 400: return "Bad Request";
+    case 404: return "Not Found";
+    case 405: return "Method Not Allowed";
+    case 413: return "Request Entity Too Large";
+    case 431: return "Request Header Fields Too Large";
+    case 500: return "Internal Server Error";
+    case 501: return "Not Implemented";
+    default: return "Unknown";
+  }
+}
+
+// echo_http_request_duration_seconds buckets (middleware/echo_metric.go:25-48)
+std::vector<double> echo_buckets() {
+  return {0.0005, 0.001, 0.002, 0.005, 0.01, 0.02, 0.05, 0.1, 0.2, 0.5, 1.0, 2.0, 5.0, 10.0, 15.0, 20.0, 30.0};
+}
+
+bool ieq(const char* a, size_t n, const char* b) {
+  if (std::strlen(b) != n) return false;
+  for (size_t i = 0; i < n; ++i)
+    if (std::tolower(static_cast<unsigned char>(a[i])) != std::tolower(static_cast<unsigned char>(b[i]))) return false;
+  return true;
+}
+
+std::string http_date() {
+  char buf[64];
+  time_t t = time(nullptr);
+  struct tm tmv;
+  gmtime_r(&t, &tmv);
+  const size_t n = strftime(buf, sizeof(buf), "%a, %d %b %Y %H:%M:%S GMT", &tmv);
+  return std::string(buf, n);
+}
+
+struct Conn {
+  int fd = -1;
+  std::string in;
+  std::string out;
+  size_t out_off = 0;
+  int64_t last_ns = 0;
+  std::string remote;
+  bool close_after = false;
+  bool want_out = false;
+};
+
+}  // namespace
+
+struct HttpServer::Worker {
+  int ep = -1;
+  std::unordered_map<int, std::unique_ptr<Conn>> conns;
+};
+
+HttpServer::HttpServer(HttpConfig cfg, std::shared_ptr<Exporter> exporter)
+    : cfg_(std::move(cfg)), exporter_(std::move(exporter)) {
+  for (auto& a : counts_)
+    for (auto& b : a)
+      for (auto& c : b) c.store(0);
+  for (auto& row : hist_)
+    for (auto& h : row) h = std::make_unique<Histogram>(echo_buckets());
+}
+
+HttpServer::~HttpServer() { stop(); }
+
+void HttpServer::set_restart_hook(std::function<void()> hook) {
+  std::lock_guard<std::mutex> lk(hook_mu_);
+  restart_hook_ = std::move(hook);
+}
+
+int HttpServer::start() {
+  if (running_) return bound_port_;
+  struct addrinfo hints {};
+  hints.ai_family = AF_UNSPEC;
+  hints.ai_socktype = SOCK_STREAM;
+  hints.ai_flags = AI_PASSIVE | AI_NUMERICSERV;
+  struct addrinfo* res = nullptr;
+  const std::string port = std::to_string(cfg_.port);
+  const char* host = cfg_.host.empty() ? nullptr : cfg_.host.c_str();
+  if (getaddrinfo(host, port.c_str(), &hints, &res) != 0 || !res)
+    throw std::runtime_error("httpd: cannot resolve listen address " + cfg_.host + ":" + port);
+  int fd = -1;
+  for (auto* ai = res; ai; ai = ai->ai_next) {
+    fd = socket(ai->ai_family, ai->ai_socktype | SOCK_NONBLOCK | SOCK_CLOEXEC, ai->ai_protocol);
+    if (fd < 0) continue;
+    int one = 1;
+    setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    if (bind(fd, ai->ai_addr, ai->ai_addrlen) == 0 && listen(fd, 1024) == 0) break;
+    close(fd);
+    fd = -1;
+  }
+  freeaddrinfo(res);
+  if (fd < 0) throw std::runtime_error("httpd: bind/listen failed on " + cfg_.host + ":" + port + ": " + strerror(errno));
+  struct sockaddr_storage ss {};
+  socklen_t sl = sizeof(ss);
+  getsockname(fd, reinterpret_cast<sockaddr*>(&ss), &sl);
+  bound_port_ = ntohs(ss.ss_family == AF_INET6 ? reinterpret_cast<sockaddr_in6*>(&ss)->sin6_port
+                                               : reinterpret_cast<sockaddr_in*>(&ss)->sin_port);
+  listen_fd_ = fd;
+  stop_ = false;
+  running_ = true;
+  const int nthreads = std::max(1, cfg_.threads);
+  for (int t = 0; t < nthreads; ++t) {
+    auto w = std::make_unique<Worker>();
+    w->ep = epoll_create1(EPOLL_CLOEXEC);
+    struct epoll_event ev {};
+    ev.events = EPOLLIN | EPOLLEXCLUSIVE;
+    ev.data.fd = listen_fd_;
+    epoll_ctl(w->ep, EPOLL_CTL_ADD, listen_fd_, &ev);
+    workers_.push_back(std::move(w));
+  }
+  for (int t = 0; t < nthreads; ++t) {
+    Worker* w = workers_[t].get();
+    threads_.emplace_back([this, w] {
+      std::vector<epoll_event> evs(128);
+      char rbuf[16384];
+      int64_t last_sweep = mono_ns();
+      auto close_conn = [&](int cfd) {
+        epoll_ctl(w->ep, EPOLL_CTL_DEL, cfd, nullptr);
+        close(cfd);
+        w->conns.erase(cfd);
+      };
+      auto flush = [&](Conn* c) -> bool {  // false => connection closed
+        while (c->out_off < c->out.size()) {
+          const ssize_t n = send(c->fd, c->out.data() + c->out_off, c->out.size() - c->out_off, MSG_NOSIGNAL);
+          if (n > 0) {
+            c->out_off += static_cast<size_t>(n);
+          } else if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+            break;
+          } else if (n < 0 && errno == EINTR) {
+            continue;
+          } else {
+            close_conn(c->fd);
+            return false;
+          }
+        }
+        if (c->out_off >= c->out.size()) {
+          c->out.clear();
+          c->out_off = 0;
+          if (c->close_after) {
+            close_conn(c->fd);
+            return false;
+          }
+        }
+        const bool want = c->out_off < c->out.size() || !c->out.empty();
+        if (want != c->want_out) {
+          struct epoll_event ev {};
+          ev.events = EPOLLIN | EPOLLRDHUP | (want ? EPOLLOUT : 0);
+          ev.data.fd = c->fd;
+          epoll_ctl(w->ep, EPOLL_CTL_MOD, c->fd, &ev);
+          c->want_out = want;
+        }
+        return true;
+      };
+      while (!stop_.load(std::memory_order_relaxed)) {
+        const int n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), 200);
+        const int64_t now = mono_ns();
+        for (int i = 0; i < n; ++i) {
+          const int fd = evs[i].data.fd;
+          if (fd == listen_fd_) {
+            for (;;) {
+              struct sockaddr_storage peer {};
+              socklen_t pl = sizeof(peer);
+              const int cfd = accept4(listen_fd_, reinterpret_cast<sockaddr*>(&peer), &pl, SOCK_NONBLOCK | SOCK_CLOEXEC);
+              if (cfd < 0) break;
+              int one = 1;
+              setsockopt(cfd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+              auto c = std::make_unique<Conn>();
+              c->fd = cfd;
+              c->last_ns = now;
+              char ip[INET6_ADDRSTRLEN] = {0};
+              if (peer.ss_family == AF_INET)
+                inet_ntop(AF_INET, &reinterpret_cast<sockaddr_in*>(&peer)->sin_addr, ip, sizeof(ip));
+              else if (peer.ss_family == AF_INET6)
+                inet_ntop(AF_INET6, &reinterpret_cast<sockaddr_in6*>(&peer)->sin6_addr, ip, sizeof(ip));
+              c->remote = ip;
+              struct epoll_event ev {};
+              ev.events = EPOLLIN | EPOLLRDHUP;
+              ev.data.fd = cfd;
+              epoll_ctl(w->ep, EPOLL_CTL_ADD, cfd, &ev);
+              w->conns.emplace(cfd, std::move(c));
+            }
+            continue;
+          }
+          auto it = w->conns.find(fd);
+          if (it == w->conns.end()) continue;
+          Conn* c = it->second.get();
+          c->last_ns = now;
+          if (evs[i].events & EPOLLERR) {
+            close_conn(fd);
+            continue;
+          }
+          bool peer_closed = false;
+          if (evs[i].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP)) {
+            for (;;) {
+              const ssize_t r = recv(fd, rbuf, sizeof(rbuf), 0);
+              if (r > 0) {
+                c->in.append(rbuf, static_cast<size_t>(r));
+                if (c->in.size() > (1u << 20)) break;
+                if (static_cast<size_t>(r) < sizeof(rbuf)) break;
+              } else if (r == 0) {
+                peer_closed = true;
+                break;
+              } else if (errno == EINTR) {
+                continue;
+              } else {
+                if (errno != EAGAIN && errno != EWOULDBLOCK) peer_closed = true;
+                break;
+              }
+            }
+            // parse and answer every complete request in the buffer (pipelining)
+            size_t pos = 0;
+            while (!c->close_after) {
+              const size_t hdr_end = c->in.find("\r\n\r\n", pos);
+              if (hdr_end == std::string::npos) {
+                if (c->in.size() - pos > 65536) {  // header block too large
+                  std::string o;
+                  int st = 431;
+                  size_t bytes = 0;
+                  handle("", "", "", false, false, &o, &st, &bytes);
+                  c->out.append(o);
+                  c->close_after = true;
+                }
+                break;
+              }
+              const char* p = c->in.data() + pos;
+              const size_t hlen = hdr_end - pos;
+              const char* le = static_cast<const char*>(memchr(p, '\n', hlen + 2));
+              std::string reqline(p, le ? static_cast<size_t>(le - p) : hlen);
+              if (!reqline.empty() && reqline.back() == '\r') reqline.pop_back();
+              const size_t sp1 = reqline.find(' ');
+              const size_t sp2 = sp1 == std::string::npos ? std::string::npos : reqline.find(' ', sp1 + 1);
+              std::string method, uri, proto;
+              if (sp1 != std::string::npos && sp2 != std::string::npos) {
+                method = reqline.substr(0, sp1);
+                uri = reqline.substr(sp1 + 1, sp2 - sp1 - 1);
+                proto = reqline.substr(sp2 + 1);
+              }
+              std::string origin, hosth, ua;
+              size_t content_len = 0;
+              bool conn_close = false, conn_keep = false, chunked = false;
+              const char* q = le ? le + 1 : p + hlen;
+              const char* hend = p + hlen;
+              while (q < hend) {
+                const char* e = static_cast<const char*>(memchr(q, '\n', static_cast<size_t>(hend - q)));
+                if (!e) e = hend;
+                const char* colon = static_cast<const char*>(memchr(q, ':', static_cast<size_t>(e - q)));
+                if (colon) {
+                  const size_t nlen = static_cast<size_t>(colon - q);
+                  const char* v = colon + 1;
+                  while (v < e && (*v == ' ' || *v == '\t')) ++v;
+                  const char* ve = e;
+                  while (ve > v && (ve[-1] == '\r' || ve[-1] == ' ')) --ve;
+                  std::string val(v, static_cast<size_t>(ve - v));
+                  if (ieq(q, nlen, "origin")) origin = val;
+                  else if (ieq(q, nlen, "host")) hosth = val;
+                  else if (ieq(q, nlen, "user-agent")) ua = val;
+                  else if (ieq(q, nlen, "content-length")) content_len = std::strtoull(val.c_str(), nullptr, 10);
+                  else if (ieq(q, nlen, "transfer-encoding")) chunked = true;
+                  else if (ieq(q, nlen, "connection")) {
+                    std::string lv = val;
+                    std::transform(lv.begin(), lv.end(), lv.begin(), ::tolower);
+                    if (lv.find("close") != std::string::npos) conn_close = true;
+                    if (lv.find("keep-alive") != std::string::npos) conn_keep = true;
+                  }
+                }
+                q = e + 1;
+              }
+              const size_t body_start = hdr_end + 4;
+              if (content_len > (1u << 20)) {
+                std::string o;
+                int st = 413;
+                size_t bytes = 0;
+                handle("", "", origin, false, false, &o, &st, &bytes);
+                c->out.append(o);
+                c->close_after = true;
+                break;
+              }
+              if (c->in.size() < body_start + content_len) break;  // wait for the body
+              const bool http10 = proto == "HTTP/1.0";
+              const bool keep = !chunked && !method.empty() && (http10 ? conn_keep : !conn_close);
+              const int64_t t0 = mono_ns();
+              std::string o;
+              int status = 0;
+              size_t body_bytes = 0;
+              if (method.empty() || chunked) {
+                status = method.empty() ? 400 : 501;
+                handle("", "", origin, false, http10, &o, &status, &body_bytes);
+              } else {
+                const size_t qm = uri.find('?');
+                handle(method, qm == std::string::npos ? uri : uri.substr(0, qm), origin, keep, http10, &o, &status,
+                       &body_bytes);
+              }
+              const double dt = (mono_ns() - t0) * 1e-9;
+              requests_.fetch_add(1, std::memory_order_relaxed);
+              if (cfg_.access_log && method != "OPTIONS" && !method.empty())
+                log_access(c->remote, hosth, method, uri, ua, status, dt, content_len, body_bytes);
+              c->out.append(o);
+              pos = body_start + content_len;
+              if (!keep) c->close_after = true;
+            }
+            c->in.erase(0, pos);
+          }
+          if (!c->out.empty() || (evs[i].events & EPOLLOUT)) {
+            if (!flush(c)) continue;
+          }
+          if (peer_closed && c->out.empty()) close_conn(fd);
+        }
+        if (now - last_sweep > 1000000000LL) {  // idle / slow-client sweep
+          last_sweep = now;
+          std::vector<int> dead;
+          for (auto& kv : w->conns) {
+            const int64_t idle = now - kv.second->last_ns;
+            const int64_t limit = kv.second->in.empty() ? cfg_.idle_timeout_s : cfg_.read_timeout_s;
+            if (idle > limit * 1000000000LL) dead.push_back(kv.first);
+          }
+          for (int fd : dead) close_conn(fd);
+        }
+      }
+      for (auto& kv : w->conns) close(kv.first);
+      w->conns.clear();
+    });
+  }
+  if (cfg_.access_log) {
+    log_thread_ = std::thread([this] {
+      while (!stop_.load()) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(100));
+        flush_log();
+      }
+      flush_log();
+    });
+  }
+  return bound_port_;
+}
+
+void HttpServer::stop() {
+  if (!running_.exchange(false)) return;
+  stop_ = true;
+  for (auto& t : threads_)
+    if (t.joinable()) t.join();
+  threads_.clear();
+  if (log_thread_.joinable()) log_thread_.join();
+  for (auto& w : workers_)
+    if (w->ep >= 0) close(w->ep);
+  workers_.clear();
+  if (listen_fd_ >= 0) close(listen_fd_);
+  listen_fd_ = -1;
+}
+
+void HttpServer::record(int mi, int hi, int status, double seconds) {
+  hist_[mi][hi]->observe(seconds);
+  counts_[status_class(status)][mi][hi].fetch_add(1, std::memory_order_relaxed);
+}
+
+void HttpServer::handle(const std::string& method, const std::string& path, const std::string& origin,
+                        bool keep_alive, bool http10, std::string* out, int* status_out, size_t* body_bytes_out) {
+  const int64_t t0 = mono_ns();
+  int status = 200;
+  std::string body;
+  const char* ctype = "application/json";
+  int handler = -1;
+  const bool cors = true;
+  if (method.empty()) {
+    status = *status_out ? *status_out : 400;
+    body = std::string("{\"message\":\"") + reason(status) + "\"}\n";
+  } else if (method == "OPTIONS") {
+    // server/server.go:92-94: Cros answers every OPTIONS with HTTPError(200); echo's
+    // error handler renders {"message":"OK"}.  Logger/Metrics are not reached.
+    body = "{\"message\":\"OK\"}\n";
+  } else {
+    if (path == "/") handler = 0;
+    else if (path == "/metrics") handler = 1;
+    else if (path == "/health") handler = 2;
+    else if (path == "/restart") handler = 3;
+    if (handler < 0) {
+      status = 404;
+      body = "{\"message\":\"Not Found\"}\n";
+      handler = 4;
+    } else if (method != "GET") {
+      status = 405;
+      body = "{\"message\":\"Method Not Allowed\"}\n";
+    } else if (handler == 0) {  // router/api.go:40-42
+      body = "{\"code\":0,\"data\":\"version : " + cfg_.version + "\",\"msg\":\"success\"}\n";
+    } else if (handler == 2) {  // router/api.go:45-47
+      body = "{\"code\":0,\"data\":\"ok\",\"msg\":\"success\"}\n";
+    } else if (handler == 3) {  // router/api.go:50-54
+      std::function<void()> hook;
+      {
+        std::lock_guard<std::mutex> lk(hook_mu_);
+        hook = restart_hook_;
+      }
+      if (hook) hook();
+      body = "{\"code\":0,\"data\":\"ok\",\"msg\":\"success\"}\n";
+    } else {  // /metrics
+      ctype = "text/plain; version=0.0.4; charset=utf-8";
+      body.reserve(64 * 1024);
+      if (exporter_) exporter_->render(&body);
+      render_http_metrics(&body);
+    }
+    const double dt = (mono_ns() - t0) * 1e-9;
+    record(method_index(method), handler, status, dt);
+  }
+  static thread_local std::string date;
+  static thread_local int64_t date_ns = 0;
+  const int64_t now = mono_ns();
+  if (now - date_ns > 500000000LL) {
+    date = http_date();
+    date_ns = now;
+  }
+  std::string& o = *out;
+  o.reserve(o.size() + body.size() + 512);
+  o.append(http10 ? "HTTP/1.0 " : "HTTP/1.1 ").append(std::to_string(status)).append(" ").append(reason(status)).append("\r\n");
+  if (cors) {  // server/server.go:77-96
+    o.append("Access-Control-Allow-Credentials: true\r\n");
+    o.append("Access-Control-Allow-Headers: Content-Type, Content-Length, Accept-Encoding, Authorization, Origin\r\n");
+    o.append("Access-Control-Allow-Methods: POST, GET, OPTIONS, PATCH, PUT, DELETE\r\n");
+    o.append("Access-Control-Allow-Origin: ").append(origin.empty() ? std::string("*") : origin).append("\r\n");
+  }
+  if (!keep_alive) o.append("Connection: close\r\n");
+  else if (http10) o.append("Connection: keep-alive\r\n");
+  o.append("Content-Length: ").append(std::to_string(body.size())).append("\r\n");
+  o.append("Content-Type: ").append(ctype).append("\r\n");
+  o.append("Date: ").append(date).append("\r\n\r\n");
+  o.append(body);
+  *status_out = status;
+  *body_bytes_out = body.size();
+}
+
+void HttpServer::render_http_metrics(std::string* out) const {
+  // middleware/echo_metric.go:80-93 family names / help strings
+  bool any = false;
+  for (int s = 0; s < kStatus; ++s)
+    for (int m = 0; m < kMethods; ++m)
+      for (int h = 0; h < kHandlers; ++h) {
+        const uint64_t v = counts_[s][m][h].load(std::memory_order_relaxed);
+        if (!v) continue;
+        if (!any) {
+          append_header(out, "echo_http_requests_total", "Number of HTTP operations", "counter");
+          any = true;
+        }
+        out->append("echo_http_requests_total{handler=\"").append(kHandlerNames[h]).append("\",method=\"")
+            .append(kMethodNames[m]).append("\",status=\"").append(kStatusNames[s]).append("\"} ");
+        append_u64(out, v);
+        out->push_back('\n');
+      }
+  any = false;
+  std::string labels;
+  for (int m = 0; m < kMethods; ++m)
+    for (int h = 0; h < kHandlers; ++h) {
+      if (!hist_[m][h]->count()) continue;
+      if (!any) {
+        append_header(out, "echo_http_request_duration_seconds", "Spend time by processing a route", "histogram");
+        any = true;
+      }
+      labels.assign("handler=\"").append(kHandlerNames[h]).append("\",method=\"").append(kMethodNames[m]).append("\",");
+      hist_[m][h]->render(out, "echo_http_request_duration_seconds", labels);
+    }
+}
+
+void HttpServer::log_access(const std::string& remote, const std::string& host, const std::string& method,
+                            const std::string& uri, const std::string& ua, int status, double seconds, size_t bytes_in,
+                            size_t bytes_out) {
+  // echo middleware.Logger() default JSON format (server/server.go:42)
+  char ts[64];
+  struct timespec tsv;
+  clock_gettime(CLOCK_REALTIME, &tsv);
+  struct tm tmv;
+  gmtime_r(&tsv.tv_sec, &tmv);
+  const size_t n = strftime(ts, sizeof(ts), "%Y-%m-%dT%H:%M:%S", &tmv);
+  std::snprintf(ts + n, sizeof(ts) - n, ".%09ldZ", tsv.tv_nsec);
+  std::string line;
+  line.reserve(256);
+  line.append("{\"time\":\"").append(ts).append("\",\"id\":\"\",\"remote_ip\":\"");
+  append_label_value(&line, remote);
+  line.append("\",\"host\":\"");
+  append_label_value(&line, host);
+  line.append("\",\"method\":\"").append(method).append("\",\"uri\":\"");
+  append_label_value(&line, uri);
+  line.append("\",\"user_agent\":\"");
+  append_label_value(&line, ua);
+  line.append("\",\"status\":").append(std::to_string(status)).append(",\"error\":\"\",\"latency\":");
+  line.append(std::to_string(static_cast<long long>(seconds * 1e9)));
+  char human[32];
+  std::snprintf(human, sizeof(human), "%.3fµs", seconds * 1e6);
+  line.append(",\"latency_human\":\"").append(human).append("\",\"bytes_in\":").append(std::to_string(bytes_in));
+  line.append(",\"bytes_out\":").append(std::to_string(bytes_out)).append("}\n");
+  std::lock_guard<std::mutex> lk(log_mu_);
+  log_buf_.append(line);
+  if (log_buf_.size() > (256u << 10)) {
+    fwrite(log_buf_.data(), 1, log_buf_.size(), stdout);
+    fflush(stdout);
+    log_buf_.clear();
+  }
+}
+
+void HttpServer::flush_log() {
+  std::string buf;
+  {
+    std::lock_guard<std::mutex> lk(log_mu_);
+    buf.swap(log_buf_);
+  }
+  if (!buf.empty()) {
+    fwrite(buf.data(), 1, buf.size(), stdout);
+    fflush(stdout);
+  }
+}
+
+}  // namespace amdgpu_dp

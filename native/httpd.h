@@ -1,0 +1,87 @@
+// Native HTTP/1.1 ops server: GET / /metrics /health /restart.
+//
+// Reference: echo v4 server (server/server.go:35-69) with middleware chain
+// Recover -> Cros -> Logger -> MetricsMiddleware (server/server.go:39-43,
+// middleware/echo_metric.go:78-124) and routes from router/api.go:27-54.
+// Wire behaviour kept byte-compatible: JSON envelope {"code":0,"data":..,"msg":"success"},
+// echo's error bodies {"message":"Not Found"}, CORS headers, OPTIONS -> 200, and the
+// echo_http_requests_total / echo_http_request_duration_seconds families with the same
+// labels and buckets.  Implementation: epoll workers sharing one listening socket
+// (EPOLLEXCLUSIVE), keep-alive + pipelining, lock-free metric atomics, buffered access
+// log, and /metrics served from the exporter's pre-rendered bytes without the GIL.
+#pragma once
+
+#include <atomic>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "metrics.h"
+#include "telemetry.h"
+
+namespace amdgpu_dp {
+
+struct HttpConfig {
+  std::string host = "0.0.0.0";
+  int port = 9100;
+  int threads = 2;
+  bool access_log = true;
+  int idle_timeout_s = 60;
+  int read_timeout_s = 30;
+  std::string version = "0.1.0";
+};
+
+class HttpServer {
+ public:
+  HttpServer(HttpConfig cfg, std::shared_ptr<Exporter> exporter);
+  ~HttpServer();
+  // Returns the bound port (cfg.port may be 0 = ephemeral).  Throws on bind failure.
+  int start();
+  void stop();
+  bool running() const { return running_.load(); }
+  int port() const { return bound_port_; }
+  void set_restart_hook(std::function<void()> hook);
+  uint64_t requests_total() const { return requests_.load(); }
+  // Renders the echo_http_* families (exposed for tests).
+  void render_http_metrics(std::string* out) const;
+
+  // Internal, public for the worker implementation
+  struct Worker;
+
+ private:
+  friend struct Worker;
+  void handle(const std::string& method, const std::string& path, const std::string& origin, bool keep_alive,
+              bool http10, std::string* out, int* status_out, size_t* body_bytes_out);
+  void record(int method_idx, int handler_idx, int status, double seconds);
+  void log_access(const std::string& remote, const std::string& host, const std::string& method,
+                  const std::string& uri, const std::string& ua, int status, double seconds, size_t bytes_in,
+                  size_t bytes_out);
+  void flush_log();
+
+  HttpConfig cfg_;
+  std::shared_ptr<Exporter> exporter_;
+  std::function<void()> restart_hook_;
+  std::mutex hook_mu_;
+  int listen_fd_ = -1;
+  int bound_port_ = 0;
+  std::atomic<bool> running_{false};
+  std::atomic<bool> stop_{false};
+  std::vector<std::thread> threads_;
+  std::vector<std::unique_ptr<Worker>> workers_;
+  std::thread log_thread_;
+  std::atomic<uint64_t> requests_{0};
+
+  static constexpr int kMethods = 8;
+  static constexpr int kHandlers = 5;
+  static constexpr int kStatus = 5;
+  std::atomic<uint64_t> counts_[kStatus][kMethods][kHandlers];
+  std::unique_ptr<Histogram> hist_[kMethods][kHandlers];
+
+  std::mutex log_mu_;
+  std::string log_buf_;
+};
+
+}  // namespace amdgpu_dp

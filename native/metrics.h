@@ -1,0 +1,146 @@
+// Lock-free Prometheus primitives + text-format (0.0.4) helpers.
+//
+// Reference: client_golang counters/histograms registered by promauto
+// (middleware/echo_metric.go:80-93) and rendered by promhttp (router/api.go:32).
+// Here every hot-path observation is a couple of relaxed atomic adds; rendering
+// happens only on scrape.
+#pragma once
+
+#include <atomic>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <string_view>
+#include <vector>
+
+namespace amdgpu_dp {
+
+// Shortest round-trip decimal, matching Go's strconv.FormatFloat(v, 'g', -1, 64)
+// closely enough for Prometheus consumers ("0.0005", "30", "1e+06", "+Inf").
+inline void append_float(std::string* out, double v) {
+  if (std::isnan(v)) {
+    out->append("NaN");
+    return;
+  }
+  if (std::isinf(v)) {
+    out->append(v > 0 ? "+Inf" : "-Inf");
+    return;
+  }
+  if (v == std::floor(v) && std::fabs(v) < 1e15) {
+    char buf[32];
+    int n = std::snprintf(buf, sizeof(buf), "%lld", static_cast<long long>(v));
+    if (std::fabs(v) >= 1e21) n = std::snprintf(buf, sizeof(buf), "%g", v);
+    out->append(buf, n);
+    return;
+  }
+  char buf[40];
+  for (int prec = 1; prec <= 17; ++prec) {
+    const int n = std::snprintf(buf, sizeof(buf), "%.*g", prec, v);
+    if (std::strtod(buf, nullptr) == v) {
+      out->append(buf, n);
+      return;
+    }
+  }
+  out->append(buf);
+}
+
+inline void append_label_value(std::string* out, std::string_view s) {
+  for (char c : s) {
+    if (c == '\\') out->append("\\\\");
+    else if (c == '"') out->append("\\\"");
+    else if (c == '\n') out->append("\\n");
+    else out->push_back(c);
+  }
+}
+
+inline void append_u64(std::string* out, uint64_t v) {
+  char buf[24];
+  const int n = std::snprintf(buf, sizeof(buf), "%llu", static_cast<unsigned long long>(v));
+  out->append(buf, n);
+}
+
+inline void append_header(std::string* out, const char* name, const char* help, const char* type) {
+  out->append("# HELP ").append(name).append(" ").append(help).append("\n# TYPE ").append(name).append(" ")
+      .append(type).append("\n");
+}
+
+class AtomicDouble {
+ public:
+  void add(double d) {
+    uint64_t old = bits_.load(std::memory_order_relaxed);
+    for (;;) {
+      double cur;
+      std::memcpy(&cur, &old, sizeof(cur));
+      const double nv = cur + d;
+      uint64_t nb;
+      std::memcpy(&nb, &nv, sizeof(nb));
+      if (bits_.compare_exchange_weak(old, nb, std::memory_order_relaxed)) return;
+    }
+  }
+  double load() const {
+    const uint64_t b = bits_.load(std::memory_order_relaxed);
+    double d;
+    std::memcpy(&d, &b, sizeof(d));
+    return d;
+  }
+
+ private:
+  std::atomic<uint64_t> bits_{0};
+};
+
+class Histogram {
+ public:
+  explicit Histogram(std::vector<double> bounds) : bounds_(std::move(bounds)), counts_(bounds_.size() + 1) {}
+  Histogram(const Histogram&) = delete;
+  void observe(double v) {
+    size_t i = 0;
+    while (i < bounds_.size() && v > bounds_[i]) ++i;
+    counts_[i].fetch_add(1, std::memory_order_relaxed);
+    sum_.add(v);
+  }
+  uint64_t count() const {
+    uint64_t c = 0;
+    for (auto& x : counts_) c += x.load(std::memory_order_relaxed);
+    return c;
+  }
+  // labels: already-formatted `k="v",` prefix (may be empty)
+  void render(std::string* out, const char* name, std::string_view labels) const {
+    uint64_t cum = 0;
+    for (size_t i = 0; i <= bounds_.size(); ++i) {
+      cum += counts_[i].load(std::memory_order_relaxed);
+      out->append(name).append("_bucket{").append(labels.data(), labels.size()).append("le=\"");
+      if (i < bounds_.size()) append_float(out, bounds_[i]);
+      else out->append("+Inf");
+      out->append("\"} ");
+      append_u64(out, cum);
+      out->push_back('\n');
+    }
+    std::string_view lab = labels;
+    if (!lab.empty() && lab.back() == ',') lab.remove_suffix(1);
+    out->append(name).append("_sum");
+    if (!lab.empty()) out->append("{").append(lab.data(), lab.size()).append("}");
+    out->push_back(' ');
+    append_float(out, sum_.load());
+    out->push_back('\n');
+    out->append(name).append("_count");
+    if (!lab.empty()) out->append("{").append(lab.data(), lab.size()).append("}");
+    out->push_back(' ');
+    append_u64(out, cum);
+    out->push_back('\n');
+  }
+
+ private:
+  std::vector<double> bounds_;
+  std::vector<std::atomic<uint64_t>> counts_;
+  AtomicDouble sum_;
+};
+
+// RPC latency buckets: 5 us .. 1 s (the echo buckets start at 500 us, too coarse
+// for a microsecond-scale Allocate).
+inline std::vector<double> rpc_buckets() {
+  return {5e-6, 1e-5, 2e-5, 5e-5, 1e-4, 2e-4, 5e-4, 1e-3, 2e-3, 5e-3, 1e-2, 5e-2, 0.1, 0.5, 1.0};
+}
+
+}  // namespace amdgpu_dp

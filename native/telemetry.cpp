@@ -1,0 +1,444 @@
+#include "telemetry.h"
+
+#include <unistd.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <dirent.h>
+#include <fstream>
+#include <sys/resource.h>
+
+namespace amdgpu_dp {
+
+Exporter::Exporter()
+    : sample_hist_({1e-4, 2.5e-4, 5e-4, 1e-3, 2.5e-3, 5e-3, 1e-2, 2.5e-2, 5e-2, 0.1, 0.25, 0.5, 1.0}) {
+  start_time_s_ = now_ns() / 1000000000LL;
+  extra_ = std::make_shared<const std::string>();
+  gpu_text_ = std::make_shared<const std::string>();
+}
+
+Exporter::~Exporter() { stop(); }
+
+void Exporter::set_inventory(const std::vector<GpuInfo>& gpus) {
+  std::lock_guard<std::mutex> lk(mu_);
+  gpus_ = gpus;
+  last_.assign(gpus.size(), GpuSample{});
+}
+
+void Exporter::set_partition_labels(const std::vector<PartitionLabel>& labels) {
+  std::lock_guard<std::mutex> lk(mu_);
+  labels_ = labels;
+}
+
+void Exporter::set_build_info(const std::string& rendered) {
+  std::lock_guard<std::mutex> lk(mu_);
+  build_info_ = rendered;
+}
+
+void Exporter::set_tables(const std::vector<std::shared_ptr<DeviceTable>>& tables) {
+  std::lock_guard<std::mutex> lk(mu_);
+  tables_ = tables;
+}
+
+void Exporter::set_extra(const std::string& rendered) {
+  auto p = std::make_shared<const std::string>(rendered);
+  std::lock_guard<std::mutex> lk(mu_);
+  extra_ = p;
+}
+
+void Exporter::start(std::shared_ptr<Backend> backend, int interval_ms, std::shared_ptr<HealthMonitor> monitor) {
+  stop();
+  backend_ = std::move(backend);
+  monitor_ = std::move(monitor);
+  interval_ms_ = interval_ms > 0 ? interval_ms : 1000;
+  stop_ = false;
+  running_ = true;
+  thread_ = std::thread([this] { loop(); });
+}
+
+void Exporter::stop() {
+  if (!running_.load()) return;
+  stop_ = true;
+  if (thread_.joinable()) thread_.join();
+  running_ = false;
+}
+
+void Exporter::loop() {
+  while (!stop_.load()) {
+    const int64_t t0 = mono_ns();
+    sample_once();
+    const int64_t spent_ms = (mono_ns() - t0) / 1000000;
+    int64_t left = interval_ms_ - spent_ms;
+    while (left > 0 && !stop_.load()) {  // sleep in slices so stop() is prompt
+      const int64_t slice = left < 50 ? left : 50;
+      std::this_thread::sleep_for(std::chrono::milliseconds(slice));
+      left -= slice;
+    }
+  }
+}
+
+void Exporter::sample_once() {
+  std::lock_guard<std::mutex> slk(sample_mu_);
+  std::shared_ptr<Backend> be = backend_;
+  size_t n;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    n = gpus_.size();
+  }
+  std::vector<GpuSample> samples(n);
+  std::vector<char> ok(n, 0);
+  const int64_t t0 = mono_ns();
+  for (size_t g = 0; g < n; ++g) {
+    if (be) ok[g] = be->sample(static_cast<int>(g), &samples[g]) ? 1 : 0;
+    if (!ok[g]) sample_errors_.fetch_add(1, std::memory_order_relaxed);
+    if (monitor_) monitor_->on_sample(static_cast<int>(g), ok[g], samples[g]);
+  }
+  const double dt = (mono_ns() - t0) * 1e-9;
+  if (be) {
+    sample_hist_.observe(dt);
+    samples_.fetch_add(1, std::memory_order_relaxed);
+  }
+  render_gpu_text(samples, ok, dt);
+}
+
+namespace {
+
+struct Fam {
+  std::string* out;
+  const char* name;
+  bool started = false;
+  void begin(const char* help, const char* type) {
+    if (started) return;
+    append_header(out, name, help, type);
+    started = true;
+  }
+};
+
+void gpu_labels(std::string* out, int gpu) {
+  out->append("gpu=\"");
+  append_u64(out, static_cast<uint64_t>(gpu));
+  out->append("\"");
+}
+
+void line(std::string* out, const char* name, const std::string& labels, double v) {
+  out->append(name).append("{").append(labels).append("} ");
+  append_float(out, v);
+  out->push_back('\n');
+}
+
+}  // namespace
+
+void Exporter::render_gpu_text(const std::vector<GpuSample>& samples, const std::vector<char>& ok, double) {
+  std::vector<GpuInfo> gpus;
+  std::vector<PartitionLabel> labels;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    gpus = gpus_;
+    labels = labels_;
+    for (size_t g = 0; g < samples.size() && g < last_.size(); ++g)
+      if (ok[g]) last_[g] = samples[g];
+  }
+  std::string o;
+  o.reserve(4096 + gpus.size() * 4096);
+  std::vector<std::string> gl(gpus.size());
+  for (size_t g = 0; g < gpus.size(); ++g) gpu_labels(&gl[g], static_cast<int>(g));
+
+  append_header(&o, "amdgpu_info", "Static inventory of each physical AMD GPU (value is always 1).", "gauge");
+  for (size_t g = 0; g < gpus.size(); ++g) {
+    const GpuInfo& gi = gpus[g];
+    std::string l = gl[g];
+    l.append(",uuid=\"");
+    append_label_value(&l, gi.uuid);
+    l.append("\",bdf=\"");
+    append_label_value(&l, gi.bdf);
+    l.append("\",name=\"");
+    append_label_value(&l, gi.market_name);
+    l.append("\",gfx_target=\"");
+    append_label_value(&l, gi.gfx_target);
+    l.append("\",compute_partition=\"");
+    append_label_value(&l, gi.compute_partition);
+    l.append("\",memory_partition=\"");
+    append_label_value(&l, gi.memory_partition);
+    l.append("\",numa_node=\"").append(std::to_string(gi.numa_node)).append("\"");
+    line(&o, "amdgpu_info", l, 1);
+  }
+  append_header(&o, "amdgpu_telemetry_up", "1 if the last telemetry sample of the GPU succeeded.", "gauge");
+  for (size_t g = 0; g < gpus.size(); ++g) line(&o, "amdgpu_telemetry_up", gl[g], ok[g] ? 1 : 0);
+
+  auto per_gpu = [&](const char* name, const char* help, const char* type, auto getter) {
+    bool hdr = false;
+    for (size_t g = 0; g < gpus.size(); ++g) {
+      if (!ok[g]) continue;
+      const double v = getter(samples[g]);
+      if (v < 0) continue;
+      if (!hdr) {
+        append_header(&o, name, help, type);
+        hdr = true;
+      }
+      line(&o, name, gl[g], v);
+    }
+  };
+  per_gpu("amdgpu_power_watts", "Current socket power in watts.", "gauge",
+          [](const GpuSample& s) { return s.power_w; });
+  per_gpu("amdgpu_energy_joules_total", "Accumulated socket energy in joules.", "counter",
+          [](const GpuSample& s) { return s.energy_j; });
+  per_gpu("amdgpu_gfx_activity_percent", "Average graphics/compute engine activity.", "gauge",
+          [](const GpuSample& s) { return s.gfx_activity_pct; });
+  per_gpu("amdgpu_umc_activity_percent", "Average memory controller (HBM) activity.", "gauge",
+          [](const GpuSample& s) { return s.umc_activity_pct; });
+  per_gpu("amdgpu_vram_used_bytes", "VRAM in use.", "gauge", [](const GpuSample& s) { return s.vram_used_bytes; });
+  per_gpu("amdgpu_vram_total_bytes", "VRAM capacity.", "gauge", [](const GpuSample& s) { return s.vram_total_bytes; });
+  per_gpu("amdgpu_throttle_status", "Raw throttle status bitmask.", "gauge",
+          [](const GpuSample& s) { return static_cast<double>(s.throttle_status); });
+
+  {  // temperatures
+    bool hdr = false;
+    for (size_t g = 0; g < gpus.size(); ++g) {
+      if (!ok[g]) continue;
+      const GpuSample& s = samples[g];
+      auto emit = [&](const char* sensor, double v) {
+        if (v < 0) return;
+        if (!hdr) {
+          append_header(&o, "amdgpu_temperature_celsius", "Temperature by sensor (edge, hotspot, mem, hbmN).", "gauge");
+          hdr = true;
+        }
+        line(&o, "amdgpu_temperature_celsius", gl[g] + ",sensor=\"" + sensor + "\"", v);
+      };
+      emit("edge", s.temp_edge_c);
+      emit("hotspot", s.temp_hotspot_c);
+      emit("mem", s.temp_mem_c);
+      for (int h = 0; h < s.num_hbm; ++h) emit(("hbm" + std::to_string(h)).c_str(), s.temp_hbm_c[h]);
+    }
+  }
+  {  // clocks
+    bool hdr = false;
+    for (size_t g = 0; g < gpus.size(); ++g) {
+      if (!ok[g]) continue;
+      const GpuSample& s = samples[g];
+      for (int k = 0; k < 2; ++k) {
+        const double v = k == 0 ? s.gfxclk_mhz : s.uclk_mhz;
+        if (v < 0) continue;
+        if (!hdr) {
+          append_header(&o, "amdgpu_clock_mhz", "Current clock frequency in MHz.", "gauge");
+          hdr = true;
+        }
+        line(&o, "amdgpu_clock_mhz", gl[g] + (k == 0 ? ",clock=\"gfx\"" : ",clock=\"mem\""), v);
+      }
+    }
+  }
+  {  // ECC
+    bool hdr = false;
+    for (size_t g = 0; g < gpus.size(); ++g) {
+      if (!ok[g] || samples[g].ecc_correctable < 0) continue;
+      if (!hdr) {
+        append_header(&o, "amdgpu_ecc_errors_total", "Accumulated ECC error counts.", "counter");
+        hdr = true;
+      }
+      line(&o, "amdgpu_ecc_errors_total", gl[g] + ",type=\"correctable\"",
+           static_cast<double>(samples[g].ecc_correctable));
+      line(&o, "amdgpu_ecc_errors_total", gl[g] + ",type=\"uncorrectable\"",
+           static_cast<double>(samples[g].ecc_uncorrectable));
+    }
+  }
+  {  // xGMI
+    std::string up, rd, wr;
+    for (size_t g = 0; g < gpus.size(); ++g) {
+      if (!ok[g]) continue;
+      const GpuSample& s = samples[g];
+      for (int k = 0; k < s.num_links; ++k) {
+        const std::string l = gl[g] + ",link=\"" + std::to_string(k) + "\",peer=\"" +
+                              (s.link_peer[k] >= 0 ? std::to_string(s.link_peer[k]) : std::string("unknown")) + "\"";
+        if (s.link_up[k] >= 0) line(&up, "amdgpu_xgmi_link_up", l, s.link_up[k]);
+        line(&rd, "amdgpu_xgmi_read_bytes_total", l, s.link_read_kb[k] * 1024.0);
+        line(&wr, "amdgpu_xgmi_write_bytes_total", l, s.link_write_kb[k] * 1024.0);
+      }
+    }
+    if (!up.empty()) {
+      append_header(&o, "amdgpu_xgmi_link_up", "1 if the xGMI link to the peer GPU is up.", "gauge");
+      o.append(up);
+    }
+    if (!rd.empty()) {
+      append_header(&o, "amdgpu_xgmi_read_bytes_total", "Bytes received over the xGMI link.", "counter");
+      o.append(rd);
+      append_header(&o, "amdgpu_xgmi_write_bytes_total", "Bytes sent over the xGMI link.", "counter");
+      o.append(wr);
+    }
+  }
+  {  // partitions
+    std::string info, busy, vram;
+    for (const auto& pl : labels) {
+      if (pl.gpu < 0 || pl.gpu >= static_cast<int>(gpus.size())) continue;
+      std::string l = gl[pl.gpu];
+      l.append(",partition=\"").append(std::to_string(pl.partition < 0 ? 0 : pl.partition)).append("\",device_id=\"");
+      append_label_value(&l, pl.device_id);
+      l.append("\",resource=\"");
+      append_label_value(&l, pl.resource);
+      l.append("\"");
+      line(&info, "amdgpu_partition_info", l, 1);
+      if (!ok[pl.gpu]) continue;
+      const GpuSample& s = samples[pl.gpu];
+      const int p = pl.partition < 0 ? 0 : pl.partition;
+      if (p < s.num_partitions && s.partition_gfx_busy_pct[p] >= 0)
+        line(&busy, "amdgpu_partition_gfx_busy_percent", l, s.partition_gfx_busy_pct[p]);
+      if (p < s.num_partitions && s.partition_vram_used_bytes[p] > 0)
+        line(&vram, "amdgpu_partition_vram_used_bytes", l, s.partition_vram_used_bytes[p]);
+    }
+    if (!info.empty()) {
+      append_header(&o, "amdgpu_partition_info",
+                    "Advertised compute partition -> kubelet device id / resource (value 1).", "gauge");
+      o.append(info);
+    }
+    if (!busy.empty()) {
+      append_header(&o, "amdgpu_partition_gfx_busy_percent", "Per-partition (XCP) compute busy.", "gauge");
+      o.append(busy);
+    }
+    if (!vram.empty()) {
+      append_header(&o, "amdgpu_partition_vram_used_bytes", "Per-partition VRAM in use.", "gauge");
+      o.append(vram);
+    }
+  }
+  auto p = std::make_shared<const std::string>(std::move(o));
+  std::lock_guard<std::mutex> lk(mu_);
+  gpu_text_ = p;
+}
+
+std::shared_ptr<const std::string> Exporter::gpu_text() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return gpu_text_;
+}
+
+GpuSample Exporter::last_sample(int gpu) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (gpu < 0 || gpu >= static_cast<int>(last_.size())) return GpuSample{};
+  return last_[gpu];
+}
+
+void Exporter::render_process(std::string* out) const {
+  std::lock_guard<std::mutex> lk(proc_mu_);
+  const int64_t now = mono_ns();
+  if (now - proc_cache_ns_ < 1000000000LL && !proc_cache_.empty()) {  // /proc reads cached 1 s
+    out->append(proc_cache_);
+    return;
+  }
+  std::string o;
+  double utime = 0, stime = 0, vsize = 0, rss = 0;
+  long long starttime = 0;
+  {
+    std::ifstream f("/proc/self/stat");
+    std::string s((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    const size_t rp = s.rfind(')');
+    if (rp != std::string::npos) {
+      std::vector<std::string> fields;
+      size_t i = rp + 2;
+      while (i < s.size()) {
+        size_t j = s.find(' ', i);
+        if (j == std::string::npos) j = s.size();
+        fields.push_back(s.substr(i, j - i));
+        i = j + 1;
+      }
+      // fields[0] = state (field 3); utime=14, stime=15, starttime=22, vsize=23, rss=24
+      if (fields.size() > 22) {
+        const double hz = static_cast<double>(sysconf(_SC_CLK_TCK));
+        utime = std::stod(fields[11]) / hz;
+        stime = std::stod(fields[12]) / hz;
+        starttime = std::stoll(fields[19]);
+        vsize = std::stod(fields[20]);
+        rss = std::stod(fields[21]) * sysconf(_SC_PAGESIZE);
+        (void)starttime;
+      }
+    }
+  }
+  int fds = 0;
+  if (DIR* d = opendir("/proc/self/fd")) {
+    while (readdir(d)) ++fds;
+    closedir(d);
+    fds -= 3;  // ., .., the dir fd itself
+  }
+  struct rlimit rl {};
+  getrlimit(RLIMIT_NOFILE, &rl);
+  append_header(&o, "process_cpu_seconds_total", "Total user and system CPU time spent in seconds.", "counter");
+  o.append("process_cpu_seconds_total ");
+  append_float(&o, utime + stime);
+  o.push_back('\n');
+  append_header(&o, "process_resident_memory_bytes", "Resident memory size in bytes.", "gauge");
+  o.append("process_resident_memory_bytes ");
+  append_float(&o, rss);
+  o.push_back('\n');
+  append_header(&o, "process_virtual_memory_bytes", "Virtual memory size in bytes.", "gauge");
+  o.append("process_virtual_memory_bytes ");
+  append_float(&o, vsize);
+  o.push_back('\n');
+  append_header(&o, "process_open_fds", "Number of open file descriptors.", "gauge");
+  o.append("process_open_fds ");
+  append_float(&o, fds);
+  o.push_back('\n');
+  append_header(&o, "process_max_fds", "Maximum number of open file descriptors.", "gauge");
+  o.append("process_max_fds ");
+  append_float(&o, static_cast<double>(rl.rlim_cur));
+  o.push_back('\n');
+  append_header(&o, "process_start_time_seconds", "Start time of the process since unix epoch in seconds.", "gauge");
+  o.append("process_start_time_seconds ");
+  append_float(&o, static_cast<double>(start_time_s_));
+  o.push_back('\n');
+  proc_cache_ = o;
+  proc_cache_ns_ = now;
+  out->append(o);
+}
+
+void Exporter::render(std::string* out) const {
+  std::shared_ptr<const std::string> gt, extra;
+  std::vector<std::shared_ptr<DeviceTable>> tables;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    gt = gpu_text_;
+    extra = extra_;
+    tables = tables_;
+    out->append(build_info_);
+  }
+  out->append(*gt);
+  append_header(out, "amdgpu_telemetry_samples_total", "Telemetry sampling passes completed.", "counter");
+  out->append("amdgpu_telemetry_samples_total ");
+  append_u64(out, samples_.load());
+  out->push_back('\n');
+  append_header(out, "amdgpu_telemetry_sample_errors_total", "Per-GPU telemetry sample failures.", "counter");
+  out->append("amdgpu_telemetry_sample_errors_total ");
+  append_u64(out, sample_errors_.load());
+  out->push_back('\n');
+  if (sample_hist_.count()) {
+    append_header(out, "amdgpu_telemetry_sample_duration_seconds", "Wall time of one sampling pass over all GPUs.",
+                  "histogram");
+    sample_hist_.render(out, "amdgpu_telemetry_sample_duration_seconds", "");
+  }
+  if (!tables.empty()) {
+    append_header(out, "amdgpu_device_plugin_device_health",
+                  "1 if the advertised device is Healthy, 0 if Unhealthy.", "gauge");
+    std::string l;
+    for (const auto& t : tables) {
+      for (size_t i = 0; i < t->size(); ++i) {
+        const TableDevice& d = t->device(i);
+        l.assign("resource=\"");
+        append_label_value(&l, t->config().resource_name);
+        l.append("\",device_id=\"");
+        append_label_value(&l, d.id);
+        l.append("\"");
+        line(out, "amdgpu_device_plugin_device_health", l, t->healthy(d.id) ? 1 : 0);
+      }
+    }
+    bool any = false;
+    for (const auto& t : tables) {
+      std::string tmp;
+      t->render_metrics(&tmp, false);
+      if (tmp.empty()) continue;
+      if (!any) {
+        DeviceTable::render_metric_headers(out);
+        any = true;
+      }
+      out->append(tmp);
+    }
+  }
+  out->append(*extra);
+  render_process(out);
+}
+
+}  // namespace amdgpu_dp
