@@ -1,0 +1,288 @@
+"""Headline benchmark: Allocate() p50 latency + /metrics scrape RPS with N MI355X advertised.
+
+Metric and configs come from BASELINE.json.  One rank per GPU (``torch.distributed.run
+--nproc-per-node N``); rank 0 launches the plugin daemon as a child process *before*
+anything touches the GPU, advertising the node's first N physical GPUs (amdsmi backend
+on MI355X, an N-GPU fixture node model elsewhere) and an in-process kubelet stub for it
+to register with.  Every rank then acts as one kubelet-side client for "its" GPU:
+
+  step = ALLOCS Allocate RPCs through a compiled HTTP/2 gRPC client (kubelet-like)
+       + ALLOCS Allocate RPCs through a persistent grpcio client (BASELINE.md method)
+       + PREFS GetPreferredAllocation RPCs over the whole advertised set (each timed)
+       + SCRAPES GET /metrics on a keep-alive connection (each timed)
+
+W warm-up steps, then K timed steps bracketed by barrier + torch.cuda.synchronize().
+Work per rank is fixed as N grows (weak scaling).  ``value`` = Allocate p50 in
+microseconds over every compiled-client Allocate of every rank in the timed window (lower
+is better; kubelet is a compiled grpc-go client, and a Python client's own ~80 us per
+call would hide the plugin); the grpcio-client p50/p99 are reported alongside;
+``scrape_rps`` = all ranks' scrapes / the slowest rank's scrape time.  Before timing,
+each rank validates its allocation: the returned render node exists and the gfx950
+canary (HBM pattern + MFMA exactness/throughput) passes on that device.
+
+The reference publishes no numbers, so ``vs_baseline`` is null.
+"""
+from __future__ import annotations
+
+import argparse
+import http.client
+import json
+import os
+import shutil
+import signal
+import socket
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+ALLOCS, PREFS, SCRAPES = 256, 32, 32
+METRIC = "Allocate() p50 latency + /metrics scrape RPS at 1/2/4/8 MI355X advertised"
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _pct(xs, q):
+    if not xs:
+        return None
+    xs = sorted(xs)
+    return xs[min(len(xs) - 1, int(q * len(xs)))]
+
+
+def _wait_http(port: int, timeout: float) -> None:
+    deadline = time.time() + timeout
+    while time.time() < deadline:
+        try:
+            c = http.client.HTTPConnection("127.0.0.1", port, timeout=1)
+            c.request("GET", "/health")
+            if c.getresponse().status == 200:
+                c.close()
+                return
+        except OSError:
+            pass
+        time.sleep(0.1)
+    raise TimeoutError("plugin web server did not come up on port %d" % port)
+
+
+def start_daemon(n_gpus: int, grpc_server: str, workdir: str):
+    """Rank 0: kubelet stub + plugin daemon subprocess.  Must run before GPU init."""
+    from k8s_gpu_device_plugin_amd import native
+    from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import KubeletStub
+
+    n = native.load()
+    backend = "amdsmi" if n.amdsmi_available() else "fixture"
+    plugin_dir = os.path.join(workdir, "device-plugins")
+    os.makedirs(plugin_dir, exist_ok=True)
+    kubelet = KubeletStub(plugin_dir).start()
+    port = _free_port()
+    cfg_path = os.path.join(workdir, "bench-config.yml")
+    with open(cfg_path, "w") as f:
+        f.write("webListenAddress: \"127.0.0.1:%d\"\nmigStrategy: none\nbackend: %s\nfixture: %dgpu_spx\n"
+                "devices: \"0-%d\"\npluginDir: \"%s\"\nlog:\n  level: info\n  fileDir: \"\"\n"
+                "http:\n  accessLog: false\n  threads: 4\ngrpc:\n  server: %s\n  threads: 4\n"
+                "telemetry:\n  intervalMs: 1000\n"
+                % (port, backend, n_gpus, n_gpus - 1, plugin_dir, grpc_server))
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    log = open(os.path.join(workdir, "daemon.log"), "w")
+    proc = subprocess.Popen([sys.executable, "-m", "k8s_gpu_device_plugin_amd", "--configFile", cfg_path],
+                            cwd=workdir, env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
+    regs = kubelet.wait_for_registrations(1, timeout=60)
+    _wait_http(port, 30)
+    return proc, kubelet, port, regs[0], backend
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--grpc-server", choices=["native", "python"], default="native")
+    ap.add_argument("--no-canary", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    n_gpus = args.gpus
+    if world > 1 and world != n_gpus:
+        print("warning: WORLD_SIZE=%d != --gpus %d" % (world, n_gpus), file=sys.stderr)
+
+    from k8s_gpu_device_plugin_amd import native
+    n = native.load()
+    if args.grpc_server == "native" and not hasattr(n, "GrpcServer"):
+        args.grpc_server = "python"
+
+    master_port = os.environ.get("MASTER_PORT", "0")
+    workdir = os.path.join(tempfile.gettempdir(), "amdgpu-dp-bench-%s-%d" % (master_port, os.getuid()))
+    proc = kubelet = None
+    info = None
+    if rank == 0:  # daemon first: nothing has touched the GPU in this process yet
+        shutil.rmtree(workdir, ignore_errors=True)
+        os.makedirs(workdir)
+        proc, kubelet, port, reg, backend = start_daemon(n_gpus, args.grpc_server, workdir)
+        info = {"port": port, "endpoint": reg.endpoint, "resource": reg.resource_name, "backend": backend,
+                "plugin_dir": os.path.join(workdir, "device-plugins")}
+
+    import torch
+    import torch.distributed as dist
+
+    use_cuda = torch.cuda.is_available()
+    if world > 1:
+        if use_cuda:
+            torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl" if use_cuda else "gloo",
+                                device_id=torch.device("cuda", local_rank) if use_cuda else None)
+        obj = [info]
+        dist.broadcast_object_list(obj, src=0)
+        info = obj[0]
+    elif use_cuda:
+        torch.cuda.set_device(local_rank)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        if use_cuda:
+            torch.cuda.synchronize()
+
+    from k8s_gpu_device_plugin_amd.api import v1beta1
+    from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import DevicePluginClient
+
+    client = DevicePluginClient(os.path.join(info["plugin_dir"], info["endpoint"]))
+    law = client.list_and_watch()
+    first = next(iter(law))
+    law.cancel()
+    ids = [d.ID for d in first.devices]
+    my_id = ids[rank % len(ids)]
+    alloc_req = v1beta1.AllocateRequest(container_requests=[
+        v1beta1.ContainerAllocateRequest(devices_ids=[my_id])]).SerializeToString()
+    pref_req = v1beta1.PreferredAllocationRequest(container_requests=[
+        v1beta1.ContainerPreferredAllocationRequest(available_deviceIDs=ids, must_include_deviceIDs=[my_id],
+                                                    allocation_size=min(2, len(ids)))]).SerializeToString()
+    alloc_raw, pref_raw = client.allocate_raw, client.preferred_raw
+    h2 = n.H2Client(os.path.join(info["plugin_dir"], info["endpoint"]))  # compiled, kubelet-like client
+
+    # ---- validate the allocation on the real device (untimed) ----
+    resp = v1beta1.AllocateResponse.FromString(alloc_raw(alloc_req))
+    specs = [s.host_path for s in resp.container_responses[0].devices]
+    canary_res = None
+    if info["backend"] == "amdsmi":
+        missing = [p for p in specs if not os.path.exists(p)]
+        if missing:
+            raise RuntimeError("allocated device nodes missing: %s" % missing)
+    if use_cuda and not args.no_canary:
+        from k8s_gpu_device_plugin_amd.ops import canary
+        canary_res = canary.run(torch.cuda.current_device(), hbm_bytes=1 << 30, passes=3, mfma_iters=8192)
+        if not canary_res["ok"]:
+            raise RuntimeError("canary failed on rank %d: %s" % (rank, canary_res))
+
+    conn = http.client.HTTPConnection("127.0.0.1", info["port"], timeout=10)
+    perf = time.perf_counter
+
+    def step(rec):
+        a, p, s, an = rec
+        an.extend(h2.bench_unary(v1beta1.METHOD_ALLOCATE, alloc_req, ALLOCS))
+        for _ in range(ALLOCS):
+            t0 = perf()
+            alloc_raw(alloc_req)
+            a.append(perf() - t0)
+        for _ in range(PREFS):
+            t0 = perf()
+            pref_raw(pref_req)
+            p.append(perf() - t0)
+        t_s = perf()
+        for _ in range(SCRAPES):
+            t0 = perf()
+            conn.request("GET", "/metrics")
+            body = conn.getresponse().read()
+            s.append(perf() - t0)
+        return perf() - t_s, len(body)
+
+    junk = ([], [], [], [])
+    for _ in range(args.warmup):
+        step(junk)
+    barrier()
+    rec = ([], [], [], [])
+    scrape_time = 0.0
+    t_start = perf()
+    for _ in range(args.steps):
+        st, body_len = step(rec)
+        scrape_time += st
+    barrier()
+    elapsed = perf() - t_start
+    mine = {"elapsed": elapsed, "scrape_time": scrape_time, "alloc": rec[0], "pref": rec[1], "scrape": rec[2],
+            "alloc_native": rec[3],
+            "canary": canary_res, "body": body_len}
+    if world > 1:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, mine)
+    else:
+        gathered = [mine]
+    rc = 0
+    if rank == 0:
+        allocs = [x for g in gathered for x in g["alloc"]]
+        allocs_native = [x for g in gathered for x in g["alloc_native"]]
+        prefs = [x for g in gathered for x in g["pref"]]
+        scrapes = [x for g in gathered for x in g["scrape"]]
+        t_max = max(g["elapsed"] for g in gathered)
+        scrape_t = max(g["scrape_time"] for g in gathered)
+        p50 = _pct(allocs_native, 0.5) * 1e6
+        p50_grpcio = _pct(allocs, 0.5) * 1e6
+        can = [g["canary"] for g in gathered if g["canary"]]
+        out = {
+            "metric": METRIC, "value": round(p50, 2), "unit": "us (Allocate p50, compiled h2 client; lower is better)",
+            "n_gpus": n_gpus, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(t_max / args.steps * 1e3, 3), "higher_is_better": False, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic kubelet allocation workload (%d Allocate + %d GetPreferredAllocation + %d /metrics "
+                    "per rank per step) against %s-discovered devices" % (ALLOCS, PREFS, SCRAPES, info["backend"]),
+            "config": {"model": "MI355X device plugin, %s, strategy=none (SPX/NPS1 whole GPUs)" % info["resource"],
+                       "global_batch": ALLOCS * world, "seq_len": 0,
+                       "parallelism": "%d kubelet-client rank(s), 1 plugin daemon" % world,
+                       "backend": info["backend"], "grpc_server": args.grpc_server},
+            "allocate_p50_us": round(p50, 2), "allocate_p99_us": round(_pct(allocs_native, 0.99) * 1e6, 2),
+            "allocate_p50_us_grpcio_client": round(p50_grpcio, 2),
+            "allocate_p99_us_grpcio_client": round(_pct(allocs, 0.99) * 1e6, 2),
+            "preferred_p50_us": round(_pct(prefs, 0.5) * 1e6, 2),
+            "scrape_p50_us": round(_pct(scrapes, 0.5) * 1e6, 2),
+            "scrape_rps": round(len(scrapes) / scrape_t, 1) if scrape_t > 0 else None,
+            "allocate_calls": len(allocs) + len(allocs_native),
+            "metrics_bytes": gathered[0]["body"],
+            "canary": ({"arch": can[0]["arch"], "hbm_read_gbps": round(min(c["read_gbps"] for c in can), 1),
+                        "hbm_write_gbps": round(min(c["write_gbps"] for c in can), 1),
+                        "mfma_bf16_tflops": round(min(c["mfma_tflops"] for c in can), 1)} if can else None),
+        }
+        print(json.dumps(out), flush=True)
+    client.close()
+    h2.close()
+    conn.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        if proc is not None:
+            try:
+                os.killpg(proc.pid, signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+            try:
+                proc.wait(15)
+            except subprocess.TimeoutExpired:
+                os.killpg(proc.pid, signal.SIGKILL)
+        if kubelet is not None:
+            kubelet.stop()
+        shutil.rmtree(workdir, ignore_errors=True)
+    return rc
+
+
+if __name__ == "__main__":
+    sys.exit(main())

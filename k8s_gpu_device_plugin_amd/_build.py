@@ -38,6 +38,8 @@ CORE_SOURCES = [
     "telemetry.cpp",
     "httpd.cpp",
     "watch.cpp",
+    "hpack.cpp",
+    "grpc_h2.cpp",
 ]
 BINDING_SOURCES = ["bindings.cpp"]
 CANARY_SOURCE = os.path.join(PKG_DIR, "ops", "canary.hip")

@@ -1,0 +1,122 @@
+"""Process bootstrap / supervisor: ``python -m k8s_gpu_device_plugin_amd``.
+
+Reference ``main.go:30-162``: ``--configFile`` flag, viper config, logger, plugin
+manager, web server, ``oklog/run`` group of three actors (signal handler, manager,
+web server gated on ``pluginReady``) and an optional pprof benchmark.
+
+Kept: the flag (``--configFile``, lookup ``./<name>.yml``), SIGHUP/SIGINT/SIGQUIT/
+SIGTERM -> graceful exit, "first actor to finish stops the others".  Fixed: the web
+server is not gated on the plugins being ready (D20: /health must come up even when
+no GPU is usable), profiles are flushed on every exit path (D19), and the process
+exit code reports a fatal manager error.
+"""
+from __future__ import annotations
+
+import argparse
+import signal
+import sys
+import threading
+
+from . import config as config_mod
+from .utils.log import get_logger, init_logger
+from .utils.util import CloseOnce
+from .utils.version import APP_NAME, VERSION
+
+
+def parse_args(argv=None) -> argparse.Namespace:
+    ap = argparse.ArgumentParser(prog="k8s_gpu_device_plugin_amd",
+                                 description="MI355X Kubernetes device plugin (amd.com/gpu)")
+    ap.add_argument("--configFile", default="config", help="name of config file (without extension) or a path")
+    ap.add_argument("--configDir", default=".", help="directory searched for <configFile>.yml")
+    ap.add_argument("--backend", choices=["auto", "amdsmi", "fixture"], help="override config backend")
+    ap.add_argument("--fixture", help="fixture node model (builtin name or file) for backend=fixture")
+    ap.add_argument("--plugin-dir", dest="pluginDir", help="kubelet device-plugin directory")
+    ap.add_argument("--web-listen-address", dest="webListenAddress", help="host:port of the HTTP ops server")
+    ap.add_argument("--strategy", dest="migStrategy", choices=["none", "single", "mixed"])
+    ap.add_argument("--log-level")
+    ap.add_argument("--log-dir")
+    ap.add_argument("--devices", help="physical GPU indices to advertise, e.g. 0-3")
+    ap.add_argument("--version", action="store_true")
+    return ap.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    if args.version:
+        print("%s %s" % (APP_NAME, VERSION))
+        return 0
+    try:
+        cfg = config_mod.load(args.configFile, search_dirs=(args.configDir,))
+    except config_mod.ConfigError as e:
+        print("fatal config error: %s" % e, file=sys.stderr)
+        return 2
+    for k in ("backend", "fixture", "pluginDir", "webListenAddress", "migStrategy", "devices"):
+        v = getattr(args, k)
+        if v is not None:
+            setattr(cfg, k, v)
+    if args.log_level:
+        cfg.log.level = args.log_level
+    if args.log_dir is not None:
+        cfg.log.fileDir = args.log_dir
+    config_mod.validate(cfg)
+    init_logger(cfg.log.level, cfg.log.fileDir or None, APP_NAME, console=cfg.log.console)
+    log = get_logger()
+    log.info("Starting %s %s", APP_NAME, VERSION)
+
+    from .plugin.manager import PluginManager
+    from .server.web import WebServer
+
+    ready = CloseOnce()
+    manager = PluginManager(cfg, ready)
+    web = WebServer(cfg, manager)
+    bench = None
+    if cfg.benchmark:
+        from .benchmark.profiling import Benchmark
+        bench = Benchmark(cfg.benchmarkDir, render_metrics=manager.exporter.render)
+        bench.run()
+
+    done = threading.Event()
+    reason = {"why": ""}
+
+    def on_signal(signum, _frame):
+        reason["why"] = "messaged %s, exiting gracefully..." % signal.Signals(signum).name
+        done.set()
+
+    for s in (signal.SIGHUP, signal.SIGINT, signal.SIGQUIT, signal.SIGTERM):
+        signal.signal(s, on_signal)
+
+    def run_manager():
+        try:
+            manager.start()
+        except Exception as e:  # pragma: no cover
+            log.exception("plugin manager crashed: %s", e)
+            manager.fatal_error = str(e)
+        finally:
+            reason["why"] = reason["why"] or "plugin manager stopped"
+            done.set()
+
+    mt = threading.Thread(target=run_manager, name="plugin-manager", daemon=True)
+    rc = 0
+    try:
+        web.start()
+        mt.start()
+        while not done.wait(0.5):
+            pass
+    except Exception as e:
+        log.error("error starting web server: %s", e)
+        rc = 1
+    finally:
+        log.info(reason["why"] or "shutting down")
+        web.stop()
+        manager.stop()
+        mt.join(10)
+        if bench is not None:
+            bench.stop()
+    if manager.fatal_error:
+        rc = 1
+    log.info("see you next time!")
+    return rc
+
+
+if __name__ == "__main__":
+    sys.exit(main())

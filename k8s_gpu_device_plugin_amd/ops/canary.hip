@@ -151,6 +151,32 @@ __global__ void __launch_bounds__(256) mfma_rate(int iters, float* __restrict__ 
   if (s == 1234.5f) sink[blockIdx.x * blockDim.x + threadIdx.x] = s;  // keeps the chain live
 }
 
+// Plain MFMA GEMM used by the numerics test: C[MxN] (fp32) = A[MxK] * B[KxN] (bf16,
+// row-major).  One wave per 32x32 output tile, K stepped 16 at a time through
+// v_mfma_f32_32x32x16_bf16 with the gfx950 operand maps: lane l (r = l&31, h = l>>5)
+// feeds A[r][k0+8h+j] and B[k0+8h+j][r]; accumulator reg i of lane l is
+// C[(i&3) + 8*(i>>2) + 4*h][l&31].  M, N multiples of 32, K multiple of 16 (host-checked).
+__global__ void __launch_bounds__(64) mfma_gemm(const short* __restrict__ A, const short* __restrict__ B,
+                                                float* __restrict__ C, int M, int N, int K) {
+  const int lane = threadIdx.x;
+  const int r = lane & 31, h = lane >> 5;
+  const int tm = blockIdx.y * 32, tn = blockIdx.x * 32;
+  f32x16 acc;
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+  for (int k0 = 0; k0 < K; k0 += 16) {
+    bf16x8 a, b;
+    for (int j = 0; j < 8; ++j) {
+      a[j] = A[static_cast<size_t>(tm + r) * K + k0 + 8 * h + j];
+      b[j] = B[static_cast<size_t>(k0 + 8 * h + j) * N + tn + r];
+    }
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+  }
+  for (int i = 0; i < 16; ++i) {
+    const int row = tm + (i & 3) + 8 * (i >> 2) + 4 * h;
+    C[static_cast<size_t>(row) * N + tn + r] = acc[i];
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -199,8 +225,6 @@ int amdgpu_canary_run(int device, unsigned long long hbm_bytes, int passes, int 
   const uint64_t n = hbm_bytes / sizeof(uint4);
   unsigned long long h_err[2] = {0, 0};
   float t_write = 0, t_read = 0, t_mfma = 0;
-  const int t0_dummy = 0;
-  (void)t0_dummy;
   int blocks = 0;
   CANARY_CHECK(hipSetDevice(device));
   CANARY_CHECK(hipGetDeviceProperties(&prop, device));
@@ -258,13 +282,43 @@ int amdgpu_canary_run(int device, unsigned long long hbm_bytes, int passes, int 
   out->elapsed_ms = t_write + t_read + t_mfma;
   out->ok = (out->hbm_errors == 0 && out->mfma_errors == 0) ? 1 : 0;
 done:
-  if (e0) hipEventDestroy(e0);
-  if (e1) hipEventDestroy(e1);
-  if (e2) hipEventDestroy(e2);
-  if (sink) hipFree(sink);
-  if (d_err) hipFree(d_err);
-  if (buf) hipFree(buf);
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (e2) (void)hipEventDestroy(e2);
+  if (sink) (void)hipFree(sink);
+  if (d_err) (void)hipFree(d_err);
+  if (buf) (void)hipFree(buf);
   return out->error[0] ? -1 : 0;
+}
+
+// Host wrapper for the numerics test: inputs/outputs in host memory.
+int amdgpu_canary_mfma_gemm(int device, const unsigned short* a_host, const unsigned short* b_host, float* c_host,
+                            int M, int N, int K, char* err, int err_len) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % 32 || N % 32 || K % 16) {
+    std::snprintf(err, err_len, "shape (%d,%d,%d) must be M,N %% 32 == 0 and K %% 16 == 0", M, N, K);
+    return -1;
+  }
+  short *a = nullptr, *b = nullptr;
+  float* c = nullptr;
+  hipError_t e = hipSetDevice(device);
+  const size_t sa = static_cast<size_t>(M) * K * 2, sb = static_cast<size_t>(K) * N * 2,
+               sc = static_cast<size_t>(M) * N * 4;
+  if (e == hipSuccess) e = hipMalloc(&a, sa);
+  if (e == hipSuccess) e = hipMalloc(&b, sb);
+  if (e == hipSuccess) e = hipMalloc(&c, sc);
+  if (e == hipSuccess) e = hipMemcpy(a, a_host, sa, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(b, b_host, sb, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(mfma_gemm, dim3(N / 32, M / 32), dim3(64), 0, 0, a, b, c, M, N, K);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(c_host, c, sc, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) std::snprintf(err, err_len, "%s", hipGetErrorString(e));
+  if (a) (void)hipFree(a);
+  if (b) (void)hipFree(b);
+  if (c) (void)hipFree(c);
+  return e == hipSuccess ? 0 : -1;
 }
 
 }  // extern "C"

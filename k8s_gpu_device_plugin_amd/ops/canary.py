@@ -1,0 +1,116 @@
+"""Python face of the gfx950 health canary (``ops/canary.hip``).
+
+``run(device)`` loads ``libamdgpu_canary.so`` with ctypes (no torch needed) and runs
+the HBM pattern test + MFMA exactness/throughput probe on one HIP device (= one
+compute partition).  ``run_isolated(device)`` does the same in a child process so the
+long-lived plugin daemon never creates a HIP context on GPUs it hands to pods.
+
+CLI: ``python -m k8s_gpu_device_plugin_amd.ops.canary --device 0 [--bytes N]`` prints
+one JSON line.  Missing library => loud ``RuntimeError`` (never a silent pass).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import subprocess
+import sys
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libamdgpu_canary.so")
+
+
+class CanaryResult(ctypes.Structure):
+    _fields_ = [("ok", ctypes.c_int), ("device", ctypes.c_int), ("hbm_bytes", ctypes.c_ulonglong),
+                ("hbm_errors", ctypes.c_ulonglong), ("mfma_errors", ctypes.c_ulonglong),
+                ("write_gbps", ctypes.c_double), ("read_gbps", ctypes.c_double), ("mfma_tflops", ctypes.c_double),
+                ("elapsed_ms", ctypes.c_double), ("num_cus", ctypes.c_int), ("arch", ctypes.c_char * 64),
+                ("error", ctypes.c_char * 256)]
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            from .. import _build
+            _build.build_canary(verbose=False)
+        lib = ctypes.CDLL(LIB_PATH)
+        lib.amdgpu_canary_run.argtypes = [ctypes.c_int, ctypes.c_ulonglong, ctypes.c_int, ctypes.c_int,
+                                          ctypes.POINTER(CanaryResult)]
+        lib.amdgpu_canary_run.restype = ctypes.c_int
+        lib.amdgpu_canary_device_count.restype = ctypes.c_int
+        lib.amdgpu_canary_mfma_gemm.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
+                                                ctypes.c_int]
+        lib.amdgpu_canary_mfma_gemm.restype = ctypes.c_int
+        _lib = lib
+    return _lib
+
+
+def device_count() -> int:
+    return load().amdgpu_canary_device_count()
+
+
+def run(device: int = 0, hbm_bytes: int = 1 << 30, passes: int = 3, mfma_iters: int = 8192) -> dict:
+    r = CanaryResult()
+    rc = load().amdgpu_canary_run(int(device), int(hbm_bytes), int(passes), int(mfma_iters), ctypes.byref(r))
+    out = {f[0]: getattr(r, f[0]) for f in CanaryResult._fields_}
+    out["arch"] = r.arch.decode(errors="replace")
+    out["error"] = r.error.decode(errors="replace")
+    out["ok"] = bool(r.ok) and rc == 0
+    return out
+
+
+def mfma_gemm(a_bf16_bits, b_bf16_bits, device: int = 0):
+    """C = A @ B through the canary's MFMA kernel.  ``a``/``b``: uint16 numpy arrays of
+    bf16 bit patterns (row-major, M,N % 32 == 0, K % 16 == 0); returns float32 [M, N]."""
+    import numpy as np
+
+    a = np.ascontiguousarray(a_bf16_bits, dtype=np.uint16)
+    b = np.ascontiguousarray(b_bf16_bits, dtype=np.uint16)
+    (m, k), (k2, nn) = a.shape, b.shape
+    if k != k2:
+        raise ValueError("inner dimensions differ: %d vs %d" % (k, k2))
+    c = np.empty((m, nn), dtype=np.float32)
+    err = ctypes.create_string_buffer(256)
+    rc = load().amdgpu_canary_mfma_gemm(int(device), a.ctypes.data, b.ctypes.data, c.ctypes.data, m, nn, k, err, 256)
+    if rc != 0:
+        raise RuntimeError("mfma_gemm failed: " + err.value.decode(errors="replace"))
+    return c
+
+
+def run_isolated(device: int, hbm_bytes: int = 256 << 20, timeout: float = 120.0) -> dict:
+    cmd = [sys.executable, "-m", "k8s_gpu_device_plugin_amd.ops.canary", "--device", str(device),
+           "--bytes", str(hbm_bytes), "--passes", "1"]
+    env = dict(os.environ)
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
+    try:
+        p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=timeout, env=env)
+    except subprocess.TimeoutExpired:
+        return {"ok": False, "device": device, "error": "canary timed out after %.0fs" % timeout}
+    for line in reversed(p.stdout.strip().splitlines()):
+        try:
+            return json.loads(line)
+        except ValueError:
+            continue
+    return {"ok": False, "device": device, "error": "canary exited %d: %s" % (p.returncode, p.stderr[-500:])}
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description="MI355X partition health canary")
+    ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--bytes", type=int, default=1 << 30)
+    ap.add_argument("--passes", type=int, default=3)
+    ap.add_argument("--mfma-iters", type=int, default=8192)
+    a = ap.parse_args(argv)
+    res = run(a.device, a.bytes, a.passes, a.mfma_iters)
+    print(json.dumps(res))
+    return 0 if res["ok"] else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,327 @@
+"""Plugin lifecycle manager.
+
+Reference ``plugin/manager.go``: owns the NVML handle, resources, device map and
+plugins; ``Start`` watches the device-plugin dir, loads + starts plugins, then loops
+over restart timer / ``kubelet.sock`` CREATE / watcher errors / ctx done / a
+``default:`` branch polling a ``restart`` bool.
+
+Defects fixed here:
+  D1  the ready latch is stored and closed once
+  D4  no busy loop: a blocking ``queue.Queue`` carries every event
+  D5  stop returns from the loop exactly once; stop is idempotent
+  D6  restart stops the *old* plugins, then starts the freshly loaded ones
+  D7  ``restart()`` is a thread-safe enqueue, not an unsynchronised bool
+  D9  a real health producer (native HealthMonitor) feeds ListAndWatch
+  D20 a failed load does not end the process; it retries every ``retrySeconds``
+Event sources: native inotify thread (kubelet restarts), native health monitor,
+HTTP ``/restart``, retry timer, ``stop()``.
+"""
+from __future__ import annotations
+
+import os
+import platform
+import queue
+import threading
+import time
+
+from .. import native
+from ..device import build_device_map
+from ..device.backend import make_backend
+from ..resource import new_resources
+from ..utils.log import get_logger
+from ..utils.util import CloseOnce, parse_index_list
+from ..utils.version import APP_NAME, VERSION
+from .plugin import AmdDevicePlugin
+
+log = get_logger("manager")
+
+EV_STOP, EV_RESTART, EV_RETRY, EV_KUBELET, EV_HEALTH = "stop", "restart", "retry", "kubelet", "health"
+
+
+def build_info_text() -> str:
+    return ("# HELP k8s_gpu_device_plugin_build_info Build information of the MI355X device plugin.\n"
+            "# TYPE k8s_gpu_device_plugin_build_info gauge\n"
+            'k8s_gpu_device_plugin_build_info{app="%s",version="%s",python="%s",native="%s"} 1\n'
+            % (APP_NAME, VERSION, platform.python_version(), "cxx17"))
+
+
+class PluginManager:
+    def __init__(self, cfg, ready: CloseOnce | None = None, backend=None) -> None:
+        n = native.load()
+        self.cfg = cfg
+        self.ready = ready if ready is not None else CloseOnce()
+        self.backend = backend if backend is not None else make_backend(cfg)
+        self.exporter = n.Exporter()
+        self.exporter.set_build_info(build_info_text())
+        self.monitor = n.HealthMonitor(self.backend, cfg.health.lostAfterFailures)
+        self.events: "queue.Queue[tuple]" = queue.Queue()
+        self.plugins: list[AmdDevicePlugin] = []
+        self.gpus: list = []
+        self.topology = None
+        self.device_map = None
+        self._retry_timer: threading.Timer | None = None
+        self._threads: list[threading.Thread] = []
+        self._running = threading.Event()
+        self._stopped = threading.Event()
+        self._lock = threading.Lock()
+        self.fatal_error: str | None = None
+        self.counters = {"restarts_api": 0, "restarts_kubelet": 0, "restarts_retry": 0, "registrations": 0,
+                         "load_failures": 0, "health_events": 0}
+        self.health_log: list[tuple[float, int, int, str]] = []  # (t, gpu, healthy, reason)
+
+    # ------------------------------------------------------------ public API
+    def restart(self) -> None:
+        """Thread-safe restart request (``GET /restart``; reference ``Restart`` sets a racy bool)."""
+        self.events.put((EV_RESTART, "api"))
+
+    def stop(self) -> None:
+        self.events.put((EV_STOP,))
+
+    @property
+    def running(self) -> bool:
+        return self._running.is_set()
+
+    def wait_stopped(self, timeout: float | None = None) -> bool:
+        return self._stopped.wait(timeout)
+
+    def start(self) -> None:
+        """Runs the manager loop in the calling thread until ``stop()``."""
+        os.makedirs(self.cfg.pluginDir, exist_ok=True)
+        self._running.set()
+        try:
+            self._start_watch()
+            try:
+                self.load_plugins()
+                self.start_plugins()
+            except Exception as e:
+                self.counters["load_failures"] += 1
+                log.error("failed to load plugins: %s; retrying in %.0fs", e, self.cfg.retrySeconds)
+                self._arm_retry()
+            self._start_telemetry()
+            self.ready.close()
+            self._loop()
+        finally:
+            self._shutdown()
+
+    def start_background(self) -> threading.Thread:
+        t = threading.Thread(target=self.start, name="plugin-manager", daemon=True)
+        t.start()
+        self.ready.wait(30)
+        return t
+
+    # ------------------------------------------------------------ loop
+    def _loop(self) -> None:
+        while True:
+            try:
+                ev = self.events.get(timeout=1.0)
+            except queue.Empty:
+                for p in self.plugins:
+                    if p.fatal_error:
+                        self.fatal_error = p.fatal_error
+                        log.critical("fatal: %s", p.fatal_error)
+                        return
+                continue
+            kind = ev[0]
+            if kind == EV_STOP:
+                log.info("plugin server stopped")
+                return
+            try:
+                if kind == EV_RESTART:
+                    self.counters["restarts_" + ev[1]] = self.counters.get("restarts_" + ev[1], 0) + 1
+                    log.info("restarting plugins (%s)", ev[1])
+                    self.restart_plugins()
+                elif kind == EV_KUBELET:
+                    self.counters["restarts_kubelet"] += 1
+                    log.info("kubelet.sock re-created: kubelet restarted; re-registering")
+                    self.restart_plugins()
+                elif kind == EV_RETRY:
+                    self.counters["restarts_retry"] += 1
+                    self._retry_timer = None
+                    if not self.plugins:
+                        self.load_plugins()
+                    self.start_plugins()
+                elif kind == EV_HEALTH:
+                    self._apply_health(ev[1])
+            except Exception as e:
+                self.counters["load_failures"] += 1
+                log.error("event %s failed: %s; retrying in %.0fs", kind, e, self.cfg.retrySeconds)
+                self._arm_retry()
+            self._publish_metrics()
+
+    # ------------------------------------------------------------ plugins
+    def load_plugins(self) -> None:
+        gpus, topo = self.backend.discover()
+        wanted = parse_index_list(self.cfg.devices)
+        if wanted is not None:
+            gpus = [g for g in gpus if g.index in wanted]
+        self.gpus, self.topology = gpus, topo
+        resources = new_resources(gpus, self.cfg.strategy, self.cfg.resourcePrefix, self.cfg.resources)
+        self.device_map = build_device_map(gpus, resources, self.cfg.strategy, self.cfg.mountCardNodes,
+                                           self.cfg.sharing.replicas, self.cfg.sharing.renameByDefault)
+        plugins = [AmdDevicePlugin(name, devs, topo, self.cfg) for name, devs in self.device_map.items()]
+        # health state survives a reload: re-apply what the monitor currently reports
+        for p in plugins:
+            for g in gpus:
+                if self.monitor.running and not self.monitor.gpu_healthy(g.index):
+                    p.set_gpu_health(g.index, -1, False)
+        self.plugins = plugins
+        n = native.load()
+        labels = []
+        for name, devs in self.device_map.items():
+            for d in devs:
+                if d.replica <= 0:
+                    labels.append(n.PartitionLabel(d.gpu, d.partition, d.get_uuid(), name))
+        self.exporter.set_inventory(gpus)
+        self.exporter.set_partition_labels(labels)
+        self.exporter.set_tables([p.table for p in plugins])
+        self.monitor.set_gpu_count(max([g.index for g in gpus], default=-1) + 1)
+        log.info("loaded %d GPU(s), resources: %s", len(gpus),
+                 ", ".join("%s=%d" % (k, len(v)) for k, v in self.device_map.items()) or "none")
+
+    def start_plugins(self) -> None:
+        started = 0
+        for p in self.plugins:
+            if len(p) == 0 or p.registered:
+                continue
+            try:
+                p.start()
+                started += 1
+                self.counters["registrations"] += 1
+            except Exception as e:
+                log.error("failed to start plugin %s: %s", p.resource, e)
+                log.info("Failed to start one or more plugins. Retrying in %.0fs...", self.cfg.retrySeconds)
+                self._arm_retry()
+                return
+        if not any(len(p) for p in self.plugins):
+            log.info("No devices found. Waiting indefinitely.")
+        elif started:
+            log.info("All plugins started.")
+
+    def stop_plugins(self) -> None:
+        for p in self.plugins:
+            try:
+                p.stop()
+            except Exception as e:  # pragma: no cover
+                log.error("failed to stop plugin %s: %s", p.resource, e)
+
+    def restart_plugins(self) -> None:
+        self._cancel_retry()
+        self.stop_plugins()
+        self.plugins = []
+        self.load_plugins()
+        self.start_plugins()
+
+    # ------------------------------------------------------------ health
+    def _apply_health(self, u) -> None:
+        self.counters["health_events"] += 1
+        if u.healthy in (0, 1):
+            healthy = bool(u.healthy)
+            if healthy and self.cfg.health.canary:
+                healthy = self._canary_ok(u.gpu)
+            for p in self.plugins:
+                p.set_gpu_health(u.gpu, u.partition, healthy)
+            self.health_log.append((time.monotonic(), u.gpu, int(healthy), u.reason))
+            (log.info if healthy else log.warning)("GPU %d marked %s: %s", u.gpu,
+                                                   "Healthy" if healthy else "Unhealthy", u.reason)
+        elif u.link_up in (0, 1):
+            for p in self.plugins:
+                p.set_link_up(u.gpu, u.peer, bool(u.link_up))
+            log.warning("xGMI link %d<->%d %s", u.gpu, u.peer, "up" if u.link_up else "down")
+        else:
+            log.info("GPU event on %d: %s", u.gpu, u.reason)
+
+    def _canary_ok(self, gpu: int) -> bool:
+        from ..ops import canary
+        for g in self.gpus:
+            if g.index != gpu:
+                continue
+            for part in g.partitions:
+                res = canary.run_isolated(part.hip_id, self.cfg.health.canaryBytes)
+                if not res.get("ok"):
+                    log.error("canary failed on GPU %d partition %d: %s", gpu, part.index, res)
+                    return False
+        return True
+
+    # ------------------------------------------------------------ threads
+    def _start_watch(self) -> None:
+        n = native.load()
+        try:
+            watcher = n.DirWatcher(self.cfg.pluginDir)
+        except Exception as e:
+            log.error("failed to create FS watcher on %s: %s", self.cfg.pluginDir, e)
+            watcher = None
+
+        def watch_loop():
+            while self._running.is_set() and watcher is not None:
+                for name, _mask, created, _removed in watcher.read(200):
+                    if name == "kubelet.sock" and created:
+                        self.events.put((EV_KUBELET,))
+            if watcher is not None:
+                watcher.close()
+
+        def health_loop():
+            while self._running.is_set():
+                if not self.monitor.running:
+                    time.sleep(0.1)
+                    continue
+                for u in self.monitor.pop(200):
+                    self.events.put((EV_HEALTH, u))
+
+        for fn, name in ((watch_loop, "fs-watch"), (health_loop, "health-pump")):
+            t = threading.Thread(target=fn, name=name, daemon=True)
+            t.start()
+            self._threads.append(t)
+
+    def _start_telemetry(self) -> None:
+        if self.cfg.health.enabled:
+            self.monitor.start()
+        if self.cfg.telemetry.enabled:
+            self.exporter.sample_once()
+            self.exporter.start(self.backend, self.cfg.telemetry.intervalMs,
+                                self.monitor if self.cfg.health.enabled else None)
+        self._publish_metrics()
+
+    def _arm_retry(self) -> None:
+        with self._lock:
+            if self._retry_timer is not None:
+                return
+            t = threading.Timer(self.cfg.retrySeconds, lambda: self.events.put((EV_RETRY,)))
+            t.daemon = True
+            self._retry_timer = t
+            t.start()
+
+    def _cancel_retry(self) -> None:
+        with self._lock:
+            if self._retry_timer is not None:
+                self._retry_timer.cancel()
+                self._retry_timer = None
+
+    def _publish_metrics(self) -> None:
+        lines = ["# HELP amdgpu_device_plugin_events_total Plugin manager lifecycle events.",
+                 "# TYPE amdgpu_device_plugin_events_total counter"]
+        for k in sorted(self.counters):
+            lines.append('amdgpu_device_plugin_events_total{event="%s"} %d' % (k, self.counters[k]))
+        lines += ["# HELP amdgpu_device_plugin_devices Devices advertised per resource and health.",
+                  "# TYPE amdgpu_device_plugin_devices gauge"]
+        for p in self.plugins:
+            healthy = p.table.healthy_count()
+            lines.append('amdgpu_device_plugin_devices{resource="%s",health="Healthy"} %d' % (p.resource, healthy))
+            lines.append('amdgpu_device_plugin_devices{resource="%s",health="Unhealthy"} %d'
+                         % (p.resource, len(p) - healthy))
+        lines += ["# HELP amdgpu_device_plugin_registered 1 if the resource is registered with kubelet.",
+                  "# TYPE amdgpu_device_plugin_registered gauge"]
+        for p in self.plugins:
+            lines.append('amdgpu_device_plugin_registered{resource="%s"} %d' % (p.resource, int(p.registered)))
+        self.exporter.set_extra("\n".join(lines) + "\n")
+
+    def _shutdown(self) -> None:
+        self._cancel_retry()
+        self._running.clear()
+        self.stop_plugins()
+        self.exporter.stop()
+        self.monitor.stop()
+        for t in self._threads:
+            t.join(2.0)
+        self._threads.clear()
+        self._stopped.set()
+        self.ready.close()

@@ -168,7 +168,7 @@ class AmdDevicePlugin:
     def _start_native_server(self) -> None:
         n = native.load()
         srv = n.GrpcServer(self.socket, max(1, self.cfg.grpc.threads if self.cfg is not None else 2))
-        srv.add_table(self.table)
+        srv.set_table(self.table)
         srv.start()
         self._native_server = srv
 
@@ -235,6 +235,9 @@ class AmdDevicePlugin:
         """Wakes ListAndWatch streams (health or stop)."""
         with self._cv:
             self._cv.notify_all()
+        srv = self._native_server
+        if srv is not None:
+            srv.notify()
 
     def set_gpu_health(self, gpu: int, partition: int, healthy: bool) -> int:
         changed = self.table.set_gpu_health(gpu, partition, healthy)

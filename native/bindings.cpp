@@ -8,6 +8,8 @@
 #include "backend.h"
 #include "device_table.h"
 #include "fixture_backend.h"
+#include "grpc_h2.h"
+#include "hpack.h"
 #include "health.h"
 #include "httpd.h"
 #include "telemetry.h"
@@ -446,4 +448,87 @@ PYBIND11_MODULE(_native, m) {
            py::arg("timeout_ms") = 200)
       .def("close", &DirWatcher::close)
       .def_property_readonly("dir", &DirWatcher::dir);
+
+  // ---- native gRPC (HTTP/2) server + client ----
+  py::class_<GrpcServer, std::shared_ptr<GrpcServer>>(m, "GrpcServer")
+      .def(py::init<std::string, int>(), py::arg("socket_path"), py::arg("threads") = 2)
+      .def("set_table", &GrpcServer::set_table)
+      .def("add_table", &GrpcServer::set_table)
+      .def("start", &GrpcServer::start, py::call_guard<py::gil_scoped_release>())
+      .def("stop", &GrpcServer::stop, py::call_guard<py::gil_scoped_release>())
+      .def("notify", &GrpcServer::notify)
+      .def_property_readonly("running", &GrpcServer::running)
+      .def_property_readonly("requests", &GrpcServer::requests)
+      .def_property_readonly("connections", &GrpcServer::connections)
+      .def_property_readonly("socket_path", &GrpcServer::socket_path);
+
+  py::class_<H2Client>(m, "H2Client")
+      .def(py::init<std::string, double>(), py::arg("socket_path"), py::arg("timeout_s") = 5.0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("unary",
+           [](H2Client& c, const std::string& path, const py::bytes& req) {
+             std::string r(req), resp, msg;
+             int st;
+             {
+               py::gil_scoped_release rel;
+               st = c.unary(path, r, &resp, &msg);
+             }
+             return py::make_tuple(st, py::bytes(resp), msg);
+           })
+      .def("first_stream_message",
+           [](H2Client& c, const std::string& path, const py::bytes& req) {
+             std::string r(req), resp;
+             {
+               py::gil_scoped_release rel;
+               c.first_stream_message(path, r, &resp);
+             }
+             return py::bytes(resp);
+           })
+      .def("bench_unary",
+           [](H2Client& c, const std::string& path, const py::bytes& req, int n) {
+             std::string r(req), resp, msg;
+             std::vector<double> out;
+             out.reserve(static_cast<size_t>(n));
+             py::gil_scoped_release rel;
+             for (int i = 0; i < n; ++i) {
+               const int64_t t0 = mono_ns();
+               const int st = c.unary(path, r, &resp, &msg);
+               out.push_back((mono_ns() - t0) * 1e-9);
+               if (st != 0) throw std::runtime_error("grpc-status " + std::to_string(st) + ": " + msg);
+             }
+             return out;
+           })
+      .def("close", &H2Client::close);
+
+  m.def("h2_bench_unary",
+        [](const std::string& sock, const std::string& path, const py::bytes& req, int n) {
+          std::string r(req);
+          py::gil_scoped_release rel;
+          return h2_bench_unary(sock, path, r, n);
+        });
+
+  // hpack (exposed for tests)
+  m.def("hpack_huffman_encode", [](const std::string& s) {
+    std::string o;
+    hpack::huffman_encode(s, &o);
+    return py::bytes(o);
+  });
+  m.def("hpack_huffman_decode", [](const py::bytes& b) -> py::object {
+    std::string in(b), out;
+    if (!hpack::huffman_decode(reinterpret_cast<const uint8_t*>(in.data()), in.size(), &out)) return py::none();
+    return py::bytes(out);
+  });
+  py::class_<hpack::Decoder>(m, "HpackDecoder")
+      .def(py::init<size_t>(), py::arg("max_table_size") = 4096)
+      .def("decode",
+           [](hpack::Decoder& d, const py::bytes& b) -> py::object {
+             std::string in(b);
+             std::vector<hpack::Header> hs;
+             if (!d.decode(reinterpret_cast<const uint8_t*>(in.data()), in.size(), &hs)) return py::none();
+             py::list l;
+             for (auto& h : hs) l.append(py::make_tuple(h.name, h.value));
+             return l;
+           })
+      .def_property_readonly("table_size", &hpack::Decoder::table_size)
+      .def_property_readonly("table_entries", &hpack::Decoder::table_entries);
 }

@@ -18,7 +18,7 @@ uint64_t mix(uint64_t x) {
 double unit(uint64_t x) { return (mix(x) >> 11) * (1.0 / 9007199254740992.0); }
 }  // namespace
 
-FixtureBackend::FixtureBackend(uint64_t seed) : seed_(seed) {}
+FixtureBackend::FixtureBackend(uint64_t seed) : seed_(seed), t0_ns_(mono_ns()) {}
 
 void FixtureBackend::add_gpu(const GpuInfo& g) {
   std::lock_guard<std::mutex> lk(mu_);
@@ -106,7 +106,7 @@ bool FixtureBackend::sample(int gpu, GpuSample* s) {
   if (gpu < 0 || gpu >= static_cast<int>(gpus_.size()) || !present_[gpu]) return false;
   const GpuInfo& g = gpus_[gpu];
   const int64_t t = now_ns();
-  const double ts = t * 1e-9;
+  const double ts = (mono_ns() - t0_ns_) * 1e-9;  // seconds since the fixture was created
   const uint64_t tick = static_cast<uint64_t>(ts * 10);  // noise changes at 10 Hz
   const uint64_t key = seed_ * 1000003ull + gpu * 7919ull;
   s->ts_ns = t;

@@ -51,6 +51,7 @@ class FixtureBackend : public Backend {
   std::vector<bool> present_;
   int64_t armed_at_ns_ = 0;
   uint64_t seed_;
+  int64_t t0_ns_;
   bool fail_discovery_ = false;
   bool shutdown_ = false;
   int discover_calls_ = 0;

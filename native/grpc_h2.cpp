@@ -1,0 +1,898 @@
+#include "grpc_h2.h"
+
+#include <errno.h>
+#include <fcntl.h>
+#include <poll.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <sys/stat.h>
+#include <sys/un.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <unordered_map>
+
+namespace amdgpu_dp {
+
+namespace {
+
+constexpr char kPreface[] = "PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n";
+constexpr size_t kPrefaceLen = 24;
+
+enum FrameType : uint8_t {
+  kData = 0,
+  kHeaders = 1,
+  kPriority = 2,
+  kRstStream = 3,
+  kSettings = 4,
+  kPushPromise = 5,
+  kPing = 6,
+  kGoaway = 7,
+  kWindowUpdate = 8,
+  kContinuation = 9,
+};
+enum Flags : uint8_t { kEndStream = 0x1, kAck = 0x1, kEndHeaders = 0x4, kPadded = 0x8, kPriorityFlag = 0x20 };
+enum H2Error : uint32_t { kNoError = 0, kProtocolError = 1, kFlowControlError = 3, kFrameSizeError = 6,
+                          kRefusedStream = 7, kCompressionError = 9 };
+
+constexpr uint32_t kMaxFrame = 16384;           // our SETTINGS_MAX_FRAME_SIZE (default)
+constexpr int64_t kLocalWindow = 1 << 20;        // stream + connection receive windows we grant
+constexpr size_t kMaxMessage = 4u << 20;         // grpc default max receive message size
+constexpr size_t kMaxStreams = 1024;
+
+void put_u32(std::string* o, uint32_t v) {
+  o->push_back(static_cast<char>(v >> 24));
+  o->push_back(static_cast<char>(v >> 16));
+  o->push_back(static_cast<char>(v >> 8));
+  o->push_back(static_cast<char>(v));
+}
+
+uint32_t get_u32(const uint8_t* p) {
+  return (static_cast<uint32_t>(p[0]) << 24) | (static_cast<uint32_t>(p[1]) << 16) |
+         (static_cast<uint32_t>(p[2]) << 8) | p[3];
+}
+
+void frame(std::string* o, uint32_t len, uint8_t type, uint8_t flags, uint32_t sid) {
+  o->push_back(static_cast<char>(len >> 16));
+  o->push_back(static_cast<char>(len >> 8));
+  o->push_back(static_cast<char>(len));
+  o->push_back(static_cast<char>(type));
+  o->push_back(static_cast<char>(flags));
+  put_u32(o, sid & 0x7FFFFFFFu);
+}
+
+void window_update(std::string* o, uint32_t sid, uint32_t inc) {
+  frame(o, 4, kWindowUpdate, 0, sid);
+  put_u32(o, inc & 0x7FFFFFFFu);
+}
+
+void grpc_prefix(std::string* o, size_t len) {
+  o->push_back(0);
+  put_u32(o, static_cast<uint32_t>(len));
+}
+
+std::string pct_encode(std::string_view s) {
+  static const char* hex = "0123456789ABCDEF";
+  std::string o;
+  for (unsigned char c : s) {
+    if (c >= 0x20 && c <= 0x7E && c != '%') {
+      o.push_back(static_cast<char>(c));
+    } else {
+      o.push_back('%');
+      o.push_back(hex[c >> 4]);
+      o.push_back(hex[c & 15]);
+    }
+  }
+  return o;
+}
+
+const std::string& response_headers() {
+  static const std::string h = [] {
+    std::string s;
+    hpack::encode_indexed(&s, 8);                              // :status 200
+    hpack::encode_literal_name_index(&s, 31, "application/grpc");  // content-type
+    return s;
+  }();
+  return h;
+}
+
+const std::string& ok_trailers() {
+  static const std::string t = [] {
+    std::string s;
+    hpack::encode_literal(&s, "grpc-status", "0");
+    return s;
+  }();
+  return t;
+}
+
+enum Method { kMUnknown = -1, kMOptions = 0, kMLaw, kMPreferred, kMAllocate, kMPreStart };
+
+Method method_of(std::string_view path) {
+  static const std::string_view base = "/v1beta1.DevicePlugin/";
+  if (path.size() <= base.size() || path.substr(0, base.size()) != base) return kMUnknown;
+  const std::string_view m = path.substr(base.size());
+  if (m == "Allocate") return kMAllocate;
+  if (m == "GetPreferredAllocation") return kMPreferred;
+  if (m == "ListAndWatch") return kMLaw;
+  if (m == "GetDevicePluginOptions") return kMOptions;
+  if (m == "PreStartContainer") return kMPreStart;
+  return kMUnknown;
+}
+
+struct Stream {
+  std::string path;
+  std::string data;
+  bool headers_done = false;
+  int64_t send_window = 65535;
+  int64_t recv_unacked = 0;
+  std::string pend;         // queued DATA payload (flow-controlled)
+  bool trailers_after = false;
+  std::string trailers;     // header block sent (END_STREAM) once pend drains
+  bool law = false;
+  uint64_t law_version = 0;
+  bool done = false;
+};
+
+}  // namespace
+
+struct GrpcServer::Worker {
+  int ep = -1;
+  int efd = -1;
+  struct Conn {
+    int fd = -1;
+    std::string in;
+    std::string out;
+    size_t out_off = 0;
+    bool preface = false;
+    hpack::Decoder dec{4096};
+    std::unordered_map<uint32_t, Stream> streams;
+    int64_t send_window = 65535;
+    int64_t peer_init_window = 65535;
+    uint32_t peer_max_frame = 16384;
+    uint32_t cont_sid = 0;
+    uint8_t cont_flags = 0;
+    std::string hblock;
+    int64_t recv_unacked = 0;
+    uint32_t last_sid = 0;
+    bool closing = false;
+    bool want_out = false;
+  };
+  std::unordered_map<int, std::unique_ptr<Conn>> conns;
+};
+
+using Conn = GrpcServer::Worker::Conn;
+
+namespace {
+
+void goaway(Conn& c, uint32_t code) {
+  frame(&c.out, 8, kGoaway, 0, 0);
+  put_u32(&c.out, c.last_sid);
+  put_u32(&c.out, code);
+  c.closing = true;
+}
+
+void rst_stream(Conn& c, uint32_t sid, uint32_t code) {
+  frame(&c.out, 4, kRstStream, 0, sid);
+  put_u32(&c.out, code);
+}
+
+// Drain a stream's pending DATA within the flow-control windows, then its trailers.
+void flush_stream(Conn& c, uint32_t sid, Stream& s) {
+  while (!s.pend.empty()) {
+    const int64_t n = std::min<int64_t>({static_cast<int64_t>(s.pend.size()), c.send_window, s.send_window,
+                                         static_cast<int64_t>(c.peer_max_frame)});
+    if (n <= 0) return;
+    frame(&c.out, static_cast<uint32_t>(n), kData, 0, sid);
+    c.out.append(s.pend.data(), static_cast<size_t>(n));
+    s.pend.erase(0, static_cast<size_t>(n));
+    c.send_window -= n;
+    s.send_window -= n;
+  }
+  if (s.trailers_after) {
+    frame(&c.out, static_cast<uint32_t>(s.trailers.size()), kHeaders, kEndHeaders | kEndStream, sid);
+    c.out.append(s.trailers);
+    s.trailers_after = false;
+    s.done = true;
+  }
+}
+
+void send_message(Conn& c, uint32_t sid, Stream& s, std::string_view payload, bool with_ok_trailers) {
+  grpc_prefix(&s.pend, payload.size());
+  s.pend.append(payload.data(), payload.size());
+  if (with_ok_trailers) {
+    s.trailers = ok_trailers();
+    s.trailers_after = true;
+  }
+  flush_stream(c, sid, s);
+}
+
+void send_error(Conn& c, uint32_t sid, Stream& s, int code, std::string_view msg) {
+  std::string h = response_headers();
+  hpack::encode_literal(&h, "grpc-status", std::to_string(code));
+  if (!msg.empty()) hpack::encode_literal(&h, "grpc-message", pct_encode(msg));
+  frame(&c.out, static_cast<uint32_t>(h.size()), kHeaders, kEndHeaders | kEndStream, sid);
+  c.out.append(h);
+  s.done = true;
+}
+
+void send_headers(Conn& c, uint32_t sid) {
+  const std::string& h = response_headers();
+  frame(&c.out, static_cast<uint32_t>(h.size()), kHeaders, kEndHeaders, sid);
+  c.out.append(h);
+}
+
+}  // namespace
+
+GrpcServer::GrpcServer(std::string socket_path, int threads) : path_(std::move(socket_path)), nthreads_(threads) {}
+
+GrpcServer::~GrpcServer() { stop(); }
+
+void GrpcServer::set_table(std::shared_ptr<DeviceTable> t) {
+  std::lock_guard<std::mutex> lk(mu_);
+  table_ = std::move(t);
+}
+
+void GrpcServer::start() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (running_) return;
+  if (!table_) throw std::runtime_error("GrpcServer: no device table");
+  struct sockaddr_un addr {};
+  addr.sun_family = AF_UNIX;
+  if (path_.size() >= sizeof(addr.sun_path)) throw std::runtime_error("GrpcServer: socket path too long: " + path_);
+  std::memcpy(addr.sun_path, path_.c_str(), path_.size() + 1);
+  ::unlink(path_.c_str());
+  const int fd = socket(AF_UNIX, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+  if (fd < 0) throw std::runtime_error(std::string("GrpcServer: socket: ") + strerror(errno));
+  if (bind(fd, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) != 0 || listen(fd, 256) != 0) {
+    const int e = errno;
+    ::close(fd);
+    throw std::runtime_error("GrpcServer: bind/listen " + path_ + ": " + strerror(e));
+  }
+  listen_fd_ = fd;
+  stop_ = false;
+  running_ = true;
+  const int n = std::max(1, nthreads_);
+  for (int i = 0; i < n; ++i) {
+    auto w = std::make_unique<Worker>();
+    w->ep = epoll_create1(EPOLL_CLOEXEC);
+    w->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    struct epoll_event ev {};
+    ev.events = EPOLLIN | EPOLLEXCLUSIVE;
+    ev.data.fd = listen_fd_;
+    epoll_ctl(w->ep, EPOLL_CTL_ADD, listen_fd_, &ev);
+    struct epoll_event ev2 {};
+    ev2.events = EPOLLIN;
+    ev2.data.fd = w->efd;
+    epoll_ctl(w->ep, EPOLL_CTL_ADD, w->efd, &ev2);
+    workers_.push_back(std::move(w));
+  }
+  for (auto& w : workers_) threads_.emplace_back([this, wp = w.get()] { run(wp); });
+}
+
+void GrpcServer::notify() {
+  for (auto& w : workers_) {
+    const uint64_t one = 1;
+    if (w->efd >= 0) (void)!write(w->efd, &one, sizeof(one));
+  }
+}
+
+void GrpcServer::stop() {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (!running_.exchange(false)) return;
+  stop_ = true;
+  notify();
+  for (auto& t : threads_)
+    if (t.joinable()) t.join();
+  threads_.clear();
+  for (auto& w : workers_) {
+    if (w->ep >= 0) ::close(w->ep);
+    if (w->efd >= 0) ::close(w->efd);
+  }
+  workers_.clear();
+  if (listen_fd_ >= 0) ::close(listen_fd_);
+  listen_fd_ = -1;
+  ::unlink(path_.c_str());
+}
+
+void GrpcServer::run(Worker* w) {
+  std::vector<epoll_event> evs(128);
+  char rbuf[32768];
+  std::shared_ptr<DeviceTable> table;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    table = table_;
+  }
+  auto close_conn = [&](int fd) {
+    epoll_ctl(w->ep, EPOLL_CTL_DEL, fd, nullptr);
+    ::close(fd);
+    w->conns.erase(fd);
+    conns_.fetch_sub(1);
+  };
+  // returns false if the connection was closed
+  auto flush = [&](Conn* c) -> bool {
+    while (c->out_off < c->out.size()) {
+      const ssize_t n = send(c->fd, c->out.data() + c->out_off, c->out.size() - c->out_off, MSG_NOSIGNAL);
+      if (n > 0) {
+        c->out_off += static_cast<size_t>(n);
+      } else if (n < 0 && errno == EINTR) {
+        continue;
+      } else if (n < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
+        break;
+      } else {
+        close_conn(c->fd);
+        return false;
+      }
+    }
+    if (c->out_off >= c->out.size()) {
+      c->out.clear();
+      c->out_off = 0;
+      if (c->closing) {
+        close_conn(c->fd);
+        return false;
+      }
+    }
+    const bool want = !c->out.empty();
+    if (want != c->want_out) {
+      struct epoll_event ev {};
+      ev.events = EPOLLIN | EPOLLRDHUP | (want ? EPOLLOUT : 0);
+      ev.data.fd = c->fd;
+      epoll_ctl(w->ep, EPOLL_CTL_MOD, c->fd, &ev);
+      c->want_out = want;
+    }
+    return true;
+  };
+  auto push_law = [&](Conn* c) {
+    const uint64_t v = table->version();
+    std::string payload;
+    for (auto& kv : c->streams) {
+      Stream& s = kv.second;
+      if (!s.law || s.done || s.law_version == v) continue;
+      if (payload.empty()) payload = table->list_and_watch();
+      s.law_version = v;
+      send_message(*c, kv.first, s, payload, false);
+    }
+  };
+  auto dispatch = [&](Conn& c, uint32_t sid, Stream& s) {
+    const int64_t t0 = mono_ns();
+    requests_.fetch_add(1, std::memory_order_relaxed);
+    const Method m = method_of(s.path);
+    if (m == kMUnknown) {
+      send_error(c, sid, s, 12, "unknown method " + s.path);  // UNIMPLEMENTED
+      return;
+    }
+    if (s.data.size() < 5) {
+      send_error(c, sid, s, 13, "missing gRPC message");  // INTERNAL
+      return;
+    }
+    const uint8_t* d = reinterpret_cast<const uint8_t*>(s.data.data());
+    if (d[0] != 0) {
+      send_error(c, sid, s, 12, "compressed gRPC messages are not supported");
+      return;
+    }
+    const uint32_t len = get_u32(d + 1);
+    if (len != s.data.size() - 5) {
+      send_error(c, sid, s, 13, "unary request must carry exactly one message");
+      return;
+    }
+    const std::string_view msg(s.data.data() + 5, len);
+    std::string out;
+    bool ok = true;
+    int rpc = kRpcAllocate;
+    switch (m) {
+      case kMAllocate:
+        ok = table->allocate(msg, &out);
+        break;
+      case kMPreferred:
+        rpc = kRpcPreferred;
+        ok = table->preferred(msg, &out);
+        break;
+      case kMOptions:
+        rpc = kRpcOptions;
+        out = table->options_bytes();
+        break;
+      case kMPreStart:
+        rpc = kRpcPreStart;
+        break;
+      case kMLaw: {
+        rpc = kRpcListAndWatch;
+        s.law = true;
+        s.law_version = table->version();
+        send_headers(c, sid);
+        send_message(c, sid, s, table->list_and_watch(), false);
+        table->observe(rpc, (mono_ns() - t0) * 1e-9, false);
+        return;
+      }
+      default:
+        break;
+    }
+    if (ok) {
+      send_headers(c, sid);
+      send_message(c, sid, s, out, true);
+    } else {
+      send_error(c, sid, s, 2, out);  // UNKNOWN, like a plain Go error from a handler
+    }
+    table->observe(rpc, (mono_ns() - t0) * 1e-9, !ok);
+  };
+  auto on_headers_block = [&](Conn& c, uint32_t sid, uint8_t flags) -> bool {
+    std::vector<hpack::Header> hs;
+    if (!c.dec.decode(reinterpret_cast<const uint8_t*>(c.hblock.data()), c.hblock.size(), &hs)) {
+      goaway(c, kCompressionError);
+      return false;
+    }
+    c.hblock.clear();
+    auto it = c.streams.find(sid);
+    if (it == c.streams.end()) {
+      if ((sid & 1) == 0 || sid <= c.last_sid) {  // must be a new, odd, increasing stream id
+        goaway(c, kProtocolError);
+        return false;
+      }
+      c.last_sid = sid;
+      if (c.streams.size() >= kMaxStreams) {
+        rst_stream(c, sid, kRefusedStream);
+        return true;
+      }
+      Stream s;
+      s.send_window = c.peer_init_window;
+      for (auto& h : hs)
+        if (h.name == ":path") s.path = h.value;
+      s.headers_done = true;
+      it = c.streams.emplace(sid, std::move(s)).first;
+    }
+    if (flags & kEndStream) dispatch(c, sid, it->second);
+    return true;
+  };
+  auto process = [&](Conn& c) -> bool {  // false = fatal, close after flushing
+    size_t pos = 0;
+    if (!c.preface) {
+      if (c.in.size() < kPrefaceLen) return true;
+      if (std::memcmp(c.in.data(), kPreface, kPrefaceLen) != 0) {
+        goaway(c, kProtocolError);
+        return false;
+      }
+      pos = kPrefaceLen;
+      c.preface = true;
+    }
+    while (c.in.size() - pos >= 9) {
+      const uint8_t* h = reinterpret_cast<const uint8_t*>(c.in.data() + pos);
+      const uint32_t len = (static_cast<uint32_t>(h[0]) << 16) | (static_cast<uint32_t>(h[1]) << 8) | h[2];
+      const uint8_t type = h[3], flags = h[4];
+      const uint32_t sid = get_u32(h + 5) & 0x7FFFFFFFu;
+      if (len > kMaxFrame) {
+        goaway(c, kFrameSizeError);
+        return false;
+      }
+      if (c.in.size() - pos < 9 + len) break;
+      const uint8_t* p = h + 9;
+      pos += 9 + len;
+      if (c.cont_sid && type != kContinuation) {
+        goaway(c, kProtocolError);
+        return false;
+      }
+      switch (type) {
+        case kSettings: {
+          if (sid != 0 || (!(flags & kAck) && len % 6)) {
+            goaway(c, kProtocolError);
+            return false;
+          }
+          if (flags & kAck) break;
+          for (uint32_t i = 0; i + 6 <= len; i += 6) {
+            const uint16_t id = static_cast<uint16_t>((p[i] << 8) | p[i + 1]);
+            const uint32_t v = get_u32(p + i + 2);
+            if (id == 4) {  // INITIAL_WINDOW_SIZE: adjust every open stream by the delta
+              if (v > 0x7FFFFFFFu) {
+                goaway(c, kFlowControlError);
+                return false;
+              }
+              const int64_t delta = static_cast<int64_t>(v) - c.peer_init_window;
+              c.peer_init_window = v;
+              for (auto& kv : c.streams) kv.second.send_window += delta;
+            } else if (id == 5) {
+              if (v < 16384 || v > 16777215) {
+                goaway(c, kProtocolError);
+                return false;
+              }
+              c.peer_max_frame = v;
+            }
+          }
+          frame(&c.out, 0, kSettings, kAck, 0);
+          for (auto& kv : c.streams) flush_stream(c, kv.first, kv.second);
+          break;
+        }
+        case kPing:
+          if (len != 8) {
+            goaway(c, kFrameSizeError);
+            return false;
+          }
+          if (!(flags & kAck)) {
+            frame(&c.out, 8, kPing, kAck, 0);
+            c.out.append(reinterpret_cast<const char*>(p), 8);
+          }
+          break;
+        case kWindowUpdate: {
+          if (len != 4) {
+            goaway(c, kFrameSizeError);
+            return false;
+          }
+          const uint32_t inc = get_u32(p) & 0x7FFFFFFFu;
+          if (sid == 0) {
+            c.send_window += inc;
+            for (auto& kv : c.streams) flush_stream(c, kv.first, kv.second);
+          } else {
+            auto it = c.streams.find(sid);
+            if (it != c.streams.end()) {
+              it->second.send_window += inc;
+              flush_stream(c, sid, it->second);
+            }
+          }
+          break;
+        }
+        case kHeaders: {
+          size_t off = 0, pad = 0;
+          if (flags & kPadded) {
+            if (len < 1) return goaway(c, kProtocolError), false;
+            pad = p[0];
+            off = 1;
+          }
+          if (flags & kPriorityFlag) off += 5;
+          if (off + pad > len) {
+            goaway(c, kProtocolError);
+            return false;
+          }
+          c.hblock.assign(reinterpret_cast<const char*>(p + off), len - off - pad);
+          if (flags & kEndHeaders) {
+            if (!on_headers_block(c, sid, flags)) return false;
+          } else {
+            c.cont_sid = sid;
+            c.cont_flags = flags;
+          }
+          break;
+        }
+        case kContinuation:
+          if (sid != c.cont_sid || c.hblock.size() + len > (1u << 20)) {
+            goaway(c, kProtocolError);
+            return false;
+          }
+          c.hblock.append(reinterpret_cast<const char*>(p), len);
+          if (flags & kEndHeaders) {
+            const uint32_t s = c.cont_sid;
+            c.cont_sid = 0;
+            if (!on_headers_block(c, s, c.cont_flags)) return false;
+          }
+          break;
+        case kData: {
+          size_t off = 0, pad = 0;
+          if (flags & kPadded) {
+            if (len < 1) return goaway(c, kProtocolError), false;
+            pad = p[0];
+            off = 1;
+          }
+          if (off + pad > len) {
+            goaway(c, kProtocolError);
+            return false;
+          }
+          c.recv_unacked += len;
+          auto it = c.streams.find(sid);
+          if (it != c.streams.end() && !it->second.done) {
+            Stream& s = it->second;
+            s.data.append(reinterpret_cast<const char*>(p + off), len - off - pad);
+            s.recv_unacked += len;
+            if (s.data.size() > kMaxMessage + 5) {
+              send_error(c, sid, s, 8, "request exceeds 4 MiB");  // RESOURCE_EXHAUSTED
+            } else if (flags & kEndStream) {
+              dispatch(c, sid, s);
+            } else if (s.recv_unacked > kLocalWindow / 2) {
+              window_update(&c.out, sid, static_cast<uint32_t>(s.recv_unacked));
+              s.recv_unacked = 0;
+            }
+          }
+          if (c.recv_unacked > kLocalWindow / 2) {
+            window_update(&c.out, 0, static_cast<uint32_t>(c.recv_unacked));
+            c.recv_unacked = 0;
+          }
+          break;
+        }
+        case kRstStream:
+          c.streams.erase(sid);
+          break;
+        case kGoaway:
+          c.closing = true;
+          break;
+        default:  // PRIORITY, PUSH_PROMISE (invalid from clients; ignored), unknown
+          break;
+      }
+    }
+    c.in.erase(0, pos);
+    for (auto it = c.streams.begin(); it != c.streams.end();)
+      it = it->second.done && it->second.pend.empty() ? c.streams.erase(it) : std::next(it);
+    return true;
+  };
+
+  uint64_t seen_version = table->version();
+  while (!stop_.load(std::memory_order_relaxed)) {
+    const int n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), 100);
+    bool law_tick = false;
+    for (int i = 0; i < n; ++i) {
+      const int fd = evs[i].data.fd;
+      if (fd == w->efd) {
+        uint64_t x;
+        while (read(w->efd, &x, sizeof(x)) > 0) {
+        }
+        law_tick = true;
+        continue;
+      }
+      if (fd == listen_fd_) {
+        for (;;) {
+          const int cfd = accept4(listen_fd_, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+          if (cfd < 0) break;
+          auto c = std::make_unique<Conn>();
+          c->fd = cfd;
+          // server preface: SETTINGS(MAX_CONCURRENT_STREAMS, INITIAL_WINDOW_SIZE) + conn window
+          frame(&c->out, 12, kSettings, 0, 0);
+          c->out.push_back(0);
+          c->out.push_back(3);
+          put_u32(&c->out, kMaxStreams);
+          c->out.push_back(0);
+          c->out.push_back(4);
+          put_u32(&c->out, static_cast<uint32_t>(kLocalWindow));
+          window_update(&c->out, 0, static_cast<uint32_t>(kLocalWindow - 65535));
+          struct epoll_event ev {};
+          ev.events = EPOLLIN | EPOLLRDHUP;
+          ev.data.fd = cfd;
+          epoll_ctl(w->ep, EPOLL_CTL_ADD, cfd, &ev);
+          Conn* cp = c.get();
+          w->conns.emplace(cfd, std::move(c));
+          conns_.fetch_add(1);
+          flush(cp);
+        }
+        continue;
+      }
+      auto it = w->conns.find(fd);
+      if (it == w->conns.end()) continue;
+      Conn* c = it->second.get();
+      if (evs[i].events & EPOLLERR) {
+        close_conn(fd);
+        continue;
+      }
+      bool peer_closed = false;
+      if (evs[i].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP)) {
+        for (;;) {
+          const ssize_t r = recv(fd, rbuf, sizeof(rbuf), 0);
+          if (r > 0) {
+            c->in.append(rbuf, static_cast<size_t>(r));
+            if (static_cast<size_t>(r) < sizeof(rbuf)) break;
+          } else if (r == 0) {
+            peer_closed = true;
+            break;
+          } else if (errno == EINTR) {
+            continue;
+          } else {
+            if (errno != EAGAIN && errno != EWOULDBLOCK) peer_closed = true;
+            break;
+          }
+        }
+        if (!process(*c)) c->closing = true;
+      }
+      if (!flush(c)) continue;
+      if (peer_closed) close_conn(fd);
+    }
+    // ListAndWatch: push on notify() and on any version change seen by the poll tick
+    const uint64_t v = table->version();
+    if (law_tick || v != seen_version) {
+      seen_version = v;
+      std::vector<int> fds;
+      for (auto& kv : w->conns) fds.push_back(kv.first);
+      for (int fd : fds) {
+        auto it = w->conns.find(fd);
+        if (it == w->conns.end()) continue;
+        push_law(it->second.get());
+        flush(it->second.get());
+      }
+    }
+  }
+  // shutdown: finish open streams with OK trailers (like the reference's ListAndWatch
+  // returning nil on stop), GOAWAY, best-effort flush, close.
+  for (auto& kv : w->conns) {
+    Conn* c = kv.second.get();
+    for (auto& s : c->streams) {
+      if (s.second.done) continue;
+      frame(&c->out, static_cast<uint32_t>(ok_trailers().size()), kHeaders, kEndHeaders | kEndStream, s.first);
+      c->out.append(ok_trailers());
+    }
+    goaway(*c, kNoError);
+    (void)!send(c->fd, c->out.data() + c->out_off, c->out.size() - c->out_off, MSG_NOSIGNAL | MSG_DONTWAIT);
+    ::close(c->fd);
+    conns_.fetch_sub(1);
+  }
+  w->conns.clear();
+}
+
+// ------------------------------------------------------------------- client
+
+H2Client::H2Client(const std::string& socket_path, double timeout_s)
+    : timeout_ms_(static_cast<int>(timeout_s * 1000)) {
+  struct sockaddr_un addr {};
+  addr.sun_family = AF_UNIX;
+  if (socket_path.size() >= sizeof(addr.sun_path)) throw std::runtime_error("socket path too long");
+  std::memcpy(addr.sun_path, socket_path.c_str(), socket_path.size() + 1);
+  fd_ = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  if (fd_ < 0 || connect(fd_, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) != 0) {
+    const int e = errno;
+    close();
+    throw std::runtime_error("H2Client: connect " + socket_path + ": " + strerror(e));
+  }
+  std::string o(kPreface, kPrefaceLen);
+  frame(&o, 6, kSettings, 0, 0);
+  o.push_back(0);
+  o.push_back(4);
+  put_u32(&o, static_cast<uint32_t>(kLocalWindow));
+  window_update(&o, 0, static_cast<uint32_t>(kLocalWindow - 65535));
+  send_all(o);
+}
+
+H2Client::~H2Client() { close(); }
+
+void H2Client::close() {
+  if (fd_ >= 0) ::close(fd_);
+  fd_ = -1;
+}
+
+void H2Client::send_all(const std::string& s) {
+  size_t off = 0;
+  while (off < s.size()) {
+    const ssize_t n = send(fd_, s.data() + off, s.size() - off, MSG_NOSIGNAL);
+    if (n < 0) {
+      if (errno == EINTR) continue;
+      throw std::runtime_error(std::string("H2Client: send: ") + strerror(errno));
+    }
+    off += static_cast<size_t>(n);
+  }
+}
+
+bool H2Client::read_frame(uint8_t* type, uint8_t* flags, uint32_t* sid, std::string* payload) {
+  char buf[32768];
+  for (;;) {
+    if (in_.size() >= 9) {
+      const uint8_t* h = reinterpret_cast<const uint8_t*>(in_.data());
+      const uint32_t len = (static_cast<uint32_t>(h[0]) << 16) | (static_cast<uint32_t>(h[1]) << 8) | h[2];
+      if (in_.size() >= 9 + len) {
+        *type = h[3];
+        *flags = h[4];
+        *sid = get_u32(h + 5) & 0x7FFFFFFFu;
+        payload->assign(in_.data() + 9, len);
+        in_.erase(0, 9 + len);
+        return true;
+      }
+    }
+    struct pollfd pf {fd_, POLLIN, 0};
+    if (poll(&pf, 1, timeout_ms_) <= 0) throw std::runtime_error("H2Client: timed out waiting for response");
+    const ssize_t r = recv(fd_, buf, sizeof(buf), 0);
+    if (r <= 0) {
+      if (r < 0 && errno == EINTR) continue;
+      return false;
+    }
+    in_.append(buf, static_cast<size_t>(r));
+  }
+}
+
+namespace {
+std::string request_headers(std::string_view path) {
+  std::string h;
+  hpack::encode_indexed(&h, 3);  // :method POST
+  hpack::encode_indexed(&h, 6);  // :scheme http
+  hpack::encode_literal_name_index(&h, 4, path);          // :path
+  hpack::encode_literal_name_index(&h, 1, "localhost");   // :authority
+  hpack::encode_literal_name_index(&h, 31, "application/grpc");
+  hpack::encode_literal(&h, "te", "trailers");
+  return h;
+}
+}  // namespace
+
+int H2Client::unary(std::string_view path, std::string_view req, std::string* resp, std::string* message) {
+  const uint32_t sid = next_sid_;
+  next_sid_ += 2;
+  std::string o;
+  const std::string h = request_headers(path);
+  frame(&o, static_cast<uint32_t>(h.size()), kHeaders, kEndHeaders, sid);
+  o.append(h);
+  frame(&o, static_cast<uint32_t>(req.size() + 5), kData, kEndStream, sid);
+  grpc_prefix(&o, req.size());
+  o.append(req.data(), req.size());
+  send_all(o);
+  std::string data;
+  int status = -1;
+  uint8_t type, flags;
+  uint32_t fsid;
+  std::string payload;
+  for (;;) {
+    if (!read_frame(&type, &flags, &fsid, &payload)) throw std::runtime_error("H2Client: connection closed");
+    std::string ctl;
+    if (type == kSettings && !(flags & kAck)) {
+      frame(&ctl, 0, kSettings, kAck, 0);
+    } else if (type == kPing && !(flags & kAck)) {
+      frame(&ctl, 8, kPing, kAck, 0);
+      ctl.append(payload);
+    } else if (type == kGoaway) {
+      throw std::runtime_error("H2Client: GOAWAY");
+    } else if (fsid == sid && type == kData) {
+      data.append(payload);
+      conn_consumed_ += static_cast<int64_t>(payload.size());
+    } else if (fsid == sid && type == kHeaders) {
+      std::vector<hpack::Header> hs;
+      if (!dec_.decode(reinterpret_cast<const uint8_t*>(payload.data()), payload.size(), &hs))
+        throw std::runtime_error("H2Client: bad HPACK from server");
+      for (auto& x : hs) {
+        if (x.name == "grpc-status") status = std::atoi(x.value.c_str());
+        else if (x.name == "grpc-message" && message) *message = x.value;
+      }
+    } else if (fsid == sid && type == kRstStream) {
+      throw std::runtime_error("H2Client: stream reset");
+    }
+    if (conn_consumed_ > kLocalWindow / 2) {
+      window_update(&ctl, 0, static_cast<uint32_t>(conn_consumed_));
+      conn_consumed_ = 0;
+    }
+    if (!ctl.empty()) send_all(ctl);
+    if (fsid == sid && (flags & kEndStream) && (type == kHeaders || type == kData)) break;
+  }
+  if (resp) {
+    resp->clear();
+    if (data.size() >= 5) resp->assign(data.data() + 5, data.size() - 5);
+  }
+  return status;
+}
+
+int H2Client::first_stream_message(std::string_view path, std::string_view req, std::string* resp) {
+  const uint32_t sid = next_sid_;
+  next_sid_ += 2;
+  std::string o;
+  const std::string h = request_headers(path);
+  frame(&o, static_cast<uint32_t>(h.size()), kHeaders, kEndHeaders, sid);
+  o.append(h);
+  frame(&o, static_cast<uint32_t>(req.size() + 5), kData, kEndStream, sid);
+  grpc_prefix(&o, req.size());
+  o.append(req.data(), req.size());
+  send_all(o);
+  std::string data;
+  uint8_t type, flags;
+  uint32_t fsid;
+  std::string payload;
+  for (;;) {
+    if (!read_frame(&type, &flags, &fsid, &payload)) throw std::runtime_error("H2Client: connection closed");
+    if (type == kSettings && !(flags & kAck)) {
+      std::string ctl;
+      frame(&ctl, 0, kSettings, kAck, 0);
+      send_all(ctl);
+    }
+    if (fsid == sid && type == kData) {
+      data.append(payload);
+      if (data.size() >= 5 && data.size() >= 5 + get_u32(reinterpret_cast<const uint8_t*>(data.data()) + 1)) break;
+    }
+    if (fsid == sid && (flags & kEndStream)) break;
+  }
+  std::string rst;
+  frame(&rst, 4, kRstStream, 0, sid);
+  put_u32(&rst, 8);  // CANCEL
+  send_all(rst);
+  if (resp && data.size() >= 5) resp->assign(data.data() + 5, data.size() - 5);
+  return 0;
+}
+
+std::vector<double> h2_bench_unary(const std::string& socket_path, const std::string& path, const std::string& req,
+                                   int n) {
+  H2Client c(socket_path);
+  std::vector<double> out;
+  out.reserve(static_cast<size_t>(n));
+  std::string resp, msg;
+  for (int i = 0; i < n; ++i) {
+    const int64_t t0 = mono_ns();
+    const int st = c.unary(path, req, &resp, &msg);
+    out.push_back((mono_ns() - t0) * 1e-9);
+    if (st != 0) throw std::runtime_error("h2_bench_unary: grpc-status " + std::to_string(st) + ": " + msg);
+  }
+  return out;
+}
+
+}  // namespace amdgpu_dp

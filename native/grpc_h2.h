@@ -1,0 +1,83 @@
+// Native gRPC-over-HTTP/2 (h2c, unix socket) server for the kubelet DevicePlugin API.
+//
+// Reference: each NvidiaDevicePlugin owns a grpc-go server on its unix socket
+// (plugin/plugin.go:52,100-137).  The kubelet-facing RPCs are tiny, so their latency
+// is framework overhead (SURVEY.md §3.4, §7.5 hard part 2); this server removes Python
+// and the GIL from that path entirely: epoll workers parse HTTP/2 frames, decode HPACK,
+// hand the protobuf bytes to the native DeviceTable and write one response burst
+// (HEADERS + DATA + trailers) per call.  ListAndWatch streams stay open and are
+// re-sent whenever the table's health version changes (eventfd wake-up).
+//
+// Also: H2Client, a minimal blocking client used as the load generator in bench.py
+// and by tests (it speaks full HPACK, so it can talk to grpcio / grpc-go servers too).
+#pragma once
+
+#include <atomic>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <string_view>
+#include <thread>
+#include <vector>
+
+#include "device_table.h"
+#include "hpack.h"
+
+namespace amdgpu_dp {
+
+class GrpcServer {
+ public:
+  GrpcServer(std::string socket_path, int threads);
+  ~GrpcServer();
+  void set_table(std::shared_ptr<DeviceTable> t);
+  void start();  // throws std::runtime_error on bind/listen failure
+  void stop();   // idempotent: trailers for open streams, GOAWAY, close, unlink socket
+  void notify(); // wake ListAndWatch streams now (health changed)
+  bool running() const { return running_.load(); }
+  uint64_t requests() const { return requests_.load(); }
+  int connections() const { return conns_.load(); }
+  const std::string& socket_path() const { return path_; }
+
+  struct Worker;
+
+ private:
+  void run(Worker* w);
+  std::string path_;
+  int nthreads_;
+  std::shared_ptr<DeviceTable> table_;
+  int listen_fd_ = -1;
+  std::atomic<bool> running_{false};
+  std::atomic<bool> stop_{false};
+  std::atomic<uint64_t> requests_{0};
+  std::atomic<int> conns_{0};
+  std::vector<std::unique_ptr<Worker>> workers_;
+  std::vector<std::thread> threads_;
+  std::mutex mu_;
+};
+
+class H2Client {
+ public:
+  explicit H2Client(const std::string& socket_path, double timeout_s = 5.0);
+  ~H2Client();
+  // Unary call. Returns the grpc-status (0 = OK), response message in *resp.
+  int unary(std::string_view path, std::string_view req, std::string* resp, std::string* message);
+  // Opens a server stream and returns its first message (ListAndWatch probe).
+  int first_stream_message(std::string_view path, std::string_view req, std::string* resp);
+  void close();
+
+ private:
+  void send_all(const std::string& s);
+  bool read_frame(uint8_t* type, uint8_t* flags, uint32_t* sid, std::string* payload);
+  int fd_ = -1;
+  uint32_t next_sid_ = 1;
+  hpack::Decoder dec_;
+  std::string in_;
+  int64_t conn_consumed_ = 0;
+  int timeout_ms_;
+};
+
+// n sequential unary calls on one connection; per-call latency in seconds.
+std::vector<double> h2_bench_unary(const std::string& socket_path, const std::string& path, const std::string& req,
+                                   int n);
+
+}  // namespace amdgpu_dp

@@ -1,0 +1,26 @@
+#!/bin/bash
+# One gpurun call: GPU tests, smoke, bench, rocprof of the canary kernels.
+# Ordinary test failures (rc 1) do not stop the script; faults/timeouts/aborts do.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export PYTHONPATH="$PWD:$PYTHONPATH"
+OUT="$PWD/gpurun_out"
+mkdir -p "$OUT"
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 tmo=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$tmo" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -n 5 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "=== stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for s in ${STEPS:-pytest smoke bench prof}; do
+  case $s in
+    pytest) step pytest_gpu 420 python -m pytest tests -q -m gpu -s -p no:cacheprovider ;;
+    smoke)  step smoke 240 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)  step bench 300 python bench.py ${BENCH_ARGS:-} ;;
+    prof)   (cd /tmp && export TMPDIR=/tmp && step rocprof_canary 240 rocprofv3 --kernel-trace --stats -d "$OUT/prof_canary" -o canary --output-format csv -- python3 -m k8s_gpu_device_plugin_amd.ops.canary --device 0 --bytes 2147483648 --passes 3) ;;
+  esac
+done
+echo "=== done"
