@@ -219,6 +219,8 @@ class AmdDevicePlugin:
         self._serving = True
 
     def register(self) -> None:
+        if not os.path.exists(self.kubelet_socket):  # fail fast instead of a 5 s dial timeout
+            raise FileNotFoundError("kubelet socket %s does not exist" % self.kubelet_socket)
         ch = dial(self.kubelet_socket, DIAL_TIMEOUT_S)
         try:
             req = v1beta1.RegisterRequest(version=v1beta1.VERSION, endpoint=os.path.basename(self.socket),

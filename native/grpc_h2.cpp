@@ -136,6 +136,17 @@ struct Stream {
   bool done = false;
 };
 
+std::string request_headers(std::string_view path) {
+  std::string h;
+  hpack::encode_indexed(&h, 3);  // :method POST
+  hpack::encode_indexed(&h, 6);  // :scheme http
+  hpack::encode_literal_name_index(&h, 4, path);          // :path
+  hpack::encode_literal_name_index(&h, 1, "localhost");   // :authority
+  hpack::encode_literal_name_index(&h, 31, "application/grpc");
+  hpack::encode_literal(&h, "te", "trailers");
+  return h;
+}
+
 }  // namespace
 
 struct GrpcServer::Worker {
@@ -777,30 +788,81 @@ bool H2Client::read_frame(uint8_t* type, uint8_t* flags, uint32_t* sid, std::str
   }
 }
 
-namespace {
-std::string request_headers(std::string_view path) {
-  std::string h;
-  hpack::encode_indexed(&h, 3);  // :method POST
-  hpack::encode_indexed(&h, 6);  // :scheme http
-  hpack::encode_literal_name_index(&h, 4, path);          // :path
-  hpack::encode_literal_name_index(&h, 1, "localhost");   // :authority
-  hpack::encode_literal_name_index(&h, 31, "application/grpc");
-  hpack::encode_literal(&h, "te", "trailers");
-  return h;
-}
-}  // namespace
 
-int H2Client::unary(std::string_view path, std::string_view req, std::string* resp, std::string* message) {
-  const uint32_t sid = next_sid_;
-  next_sid_ += 2;
+bool H2Client::handle_control(uint8_t type, uint8_t flags, uint32_t sid, const std::string& payload) {
+  std::string ctl;
+  if (type == kSettings) {
+    if (!(flags & kAck)) {
+      for (size_t i = 0; i + 6 <= payload.size(); i += 6) {
+        const uint8_t* p = reinterpret_cast<const uint8_t*>(payload.data()) + i;
+        const uint16_t id = static_cast<uint16_t>((p[0] << 8) | p[1]);
+        const uint32_t v = get_u32(p + 2);
+        if (id == 4) {
+          stream_window_ += static_cast<int64_t>(v) - stream_window_init_;
+          stream_window_init_ = v;
+        } else if (id == 5) {
+          peer_max_frame_ = v;
+        }
+      }
+      frame(&ctl, 0, kSettings, kAck, 0);
+    }
+  } else if (type == kPing) {
+    if (!(flags & kAck)) {
+      frame(&ctl, 8, kPing, kAck, 0);
+      ctl.append(payload);
+    }
+  } else if (type == kWindowUpdate && payload.size() == 4) {
+    const uint32_t inc = get_u32(reinterpret_cast<const uint8_t*>(payload.data())) & 0x7FFFFFFFu;
+    if (sid == 0) send_window_ += inc;
+    else if (sid == cur_sid_) stream_window_ += inc;
+  } else if (type == kGoaway) {
+    throw std::runtime_error("H2Client: GOAWAY");
+  } else {
+    return false;
+  }
+  if (!ctl.empty()) send_all(ctl);
+  return true;
+}
+
+void H2Client::send_request(uint32_t sid, std::string_view path, std::string_view req) {
+  cur_sid_ = sid;
+  stream_window_ = stream_window_init_;
   std::string o;
   const std::string h = request_headers(path);
   frame(&o, static_cast<uint32_t>(h.size()), kHeaders, kEndHeaders, sid);
   o.append(h);
-  frame(&o, static_cast<uint32_t>(req.size() + 5), kData, kEndStream, sid);
-  grpc_prefix(&o, req.size());
-  o.append(req.data(), req.size());
+  std::string body;
+  grpc_prefix(&body, req.size());
+  body.append(req.data(), req.size());
+  size_t off = 0;
+  while (off < body.size()) {
+    int64_t n = std::min<int64_t>({static_cast<int64_t>(body.size() - off), send_window_, stream_window_,
+                                   static_cast<int64_t>(peer_max_frame_)});
+    if (n <= 0) {  // blocked on flow control: flush what we have, wait for WINDOW_UPDATE
+      send_all(o);
+      o.clear();
+      uint8_t type, flags;
+      uint32_t fsid;
+      std::string payload;
+      if (!read_frame(&type, &flags, &fsid, &payload)) throw std::runtime_error("H2Client: connection closed");
+      if (!handle_control(type, flags, fsid, payload) && fsid == sid && (type == kRstStream))
+        throw std::runtime_error("H2Client: stream reset while sending");
+      continue;
+    }
+    const bool last = off + static_cast<size_t>(n) == body.size();
+    frame(&o, static_cast<uint32_t>(n), kData, last ? kEndStream : 0, sid);
+    o.append(body.data() + off, static_cast<size_t>(n));
+    off += static_cast<size_t>(n);
+    send_window_ -= n;
+    stream_window_ -= n;
+  }
   send_all(o);
+}
+
+int H2Client::unary(std::string_view path, std::string_view req, std::string* resp, std::string* message) {
+  const uint32_t sid = next_sid_;
+  next_sid_ += 2;
+  send_request(sid, path, req);
   std::string data;
   int status = -1;
   uint8_t type, flags;
@@ -808,15 +870,8 @@ int H2Client::unary(std::string_view path, std::string_view req, std::string* re
   std::string payload;
   for (;;) {
     if (!read_frame(&type, &flags, &fsid, &payload)) throw std::runtime_error("H2Client: connection closed");
-    std::string ctl;
-    if (type == kSettings && !(flags & kAck)) {
-      frame(&ctl, 0, kSettings, kAck, 0);
-    } else if (type == kPing && !(flags & kAck)) {
-      frame(&ctl, 8, kPing, kAck, 0);
-      ctl.append(payload);
-    } else if (type == kGoaway) {
-      throw std::runtime_error("H2Client: GOAWAY");
-    } else if (fsid == sid && type == kData) {
+    if (handle_control(type, flags, fsid, payload)) continue;
+    if (fsid == sid && type == kData) {
       data.append(payload);
       conn_consumed_ += static_cast<int64_t>(payload.size());
     } else if (fsid == sid && type == kHeaders) {
@@ -831,10 +886,11 @@ int H2Client::unary(std::string_view path, std::string_view req, std::string* re
       throw std::runtime_error("H2Client: stream reset");
     }
     if (conn_consumed_ > kLocalWindow / 2) {
+      std::string ctl;
       window_update(&ctl, 0, static_cast<uint32_t>(conn_consumed_));
       conn_consumed_ = 0;
+      send_all(ctl);
     }
-    if (!ctl.empty()) send_all(ctl);
     if (fsid == sid && (flags & kEndStream) && (type == kHeaders || type == kData)) break;
   }
   if (resp) {
@@ -847,27 +903,17 @@ int H2Client::unary(std::string_view path, std::string_view req, std::string* re
 int H2Client::first_stream_message(std::string_view path, std::string_view req, std::string* resp) {
   const uint32_t sid = next_sid_;
   next_sid_ += 2;
-  std::string o;
-  const std::string h = request_headers(path);
-  frame(&o, static_cast<uint32_t>(h.size()), kHeaders, kEndHeaders, sid);
-  o.append(h);
-  frame(&o, static_cast<uint32_t>(req.size() + 5), kData, kEndStream, sid);
-  grpc_prefix(&o, req.size());
-  o.append(req.data(), req.size());
-  send_all(o);
+  send_request(sid, path, req);
   std::string data;
   uint8_t type, flags;
   uint32_t fsid;
   std::string payload;
   for (;;) {
     if (!read_frame(&type, &flags, &fsid, &payload)) throw std::runtime_error("H2Client: connection closed");
-    if (type == kSettings && !(flags & kAck)) {
-      std::string ctl;
-      frame(&ctl, 0, kSettings, kAck, 0);
-      send_all(ctl);
-    }
+    if (handle_control(type, flags, fsid, payload)) continue;
     if (fsid == sid && type == kData) {
       data.append(payload);
+      conn_consumed_ += static_cast<int64_t>(payload.size());
       if (data.size() >= 5 && data.size() >= 5 + get_u32(reinterpret_cast<const uint8_t*>(data.data()) + 1)) break;
     }
     if (fsid == sid && (flags & kEndStream)) break;

@@ -68,6 +68,15 @@ class H2Client {
  private:
   void send_all(const std::string& s);
   bool read_frame(uint8_t* type, uint8_t* flags, uint32_t* sid, std::string* payload);
+  // Sends HEADERS + gRPC-framed request DATA (split into frames, within flow control).
+  void send_request(uint32_t sid, std::string_view path, std::string_view req);
+  // Handles connection-level frames (SETTINGS/PING/WINDOW_UPDATE); true if consumed.
+  bool handle_control(uint8_t type, uint8_t flags, uint32_t sid, const std::string& payload);
+  int64_t send_window_ = 65535;          // connection send window
+  int64_t stream_window_init_ = 65535;   // server's SETTINGS_INITIAL_WINDOW_SIZE
+  int64_t stream_window_ = 0;            // current request stream's send window
+  uint32_t cur_sid_ = 0;
+  uint32_t peer_max_frame_ = 16384;
   int fd_ = -1;
   uint32_t next_sid_ = 1;
   hpack::Decoder dec_;

@@ -1,0 +1,158 @@
+"""xGMI-aware GetPreferredAllocation policies.
+
+Contract (go-gpuallocator BestEffortPolicy, used at reference plugin/plugin.go:276):
+result ⊆ available ∪ required, ⊇ required, |result| = size, deterministic.
+MI355X specifics: partition packing, healthy-link cliques, NUMA,
+fragmentation.  The distributed (replica) policy mirrors plugin/plugin.go:284-326."""
+import itertools
+
+import pytest
+from hypothesis import given, settings, strategies as st
+
+from k8s_gpu_device_plugin_amd.models import fixtures
+
+
+def _topo(n, ngpu, down=()):
+    t = n.Topology(ngpu)
+    for a in range(ngpu):
+        for b in range(a + 1, ngpu):
+            t.set_link(a, b, n.Link(type=n.LINK_XGMI, hops=1, up=(a, b) not in down))
+    return t
+
+
+def _whole(n, ngpu, per_numa=4):
+    return [n.AllocDevice(g, -1, g // per_numa, "g%d" % g) for g in range(ngpu)]
+
+
+def _parts(n, ngpu, nparts, per_numa=4):
+    return [n.AllocDevice(g, p, g // per_numa, "g%dp%d" % (g, p)) for g in range(ngpu) for p in range(nparts)]
+
+
+def test_pair_scores(n):
+    t = _topo(n, 8, down={(0, 5)})
+    d = _whole(n, 8)
+    same_gpu = n.pair_score(t, n.AllocDevice(0, 0, 0, "a"), n.AllocDevice(0, 1, 0, "b"))
+    xgmi_same_numa = n.pair_score(t, d[0], d[1])
+    xgmi_cross_numa = n.pair_score(t, d[0], d[4])
+    down = n.pair_score(t, d[0], d[5])
+    assert same_gpu > xgmi_same_numa > xgmi_cross_numa > down
+
+
+def test_whole_gpu_numa_packing_sequence(n):
+    """2+2 requests fill NUMA node 0 first, leaving node 1's four GPUs for a 4-GPU job."""
+    t, d = _topo(n, 8), _whole(n, 8)
+    avail = list(range(8))
+    a = n.aligned_alloc(t, d, avail, [], 2)
+    assert a == [0, 1]
+    avail = [x for x in avail if x not in a]
+    b = n.aligned_alloc(t, d, avail, [], 2)
+    assert b == [2, 3]
+    avail = [x for x in avail if x not in b]
+    c = n.aligned_alloc(t, d, avail, [], 4)
+    assert c == [4, 5, 6, 7]
+
+
+def test_avoids_down_links(n):
+    t, d = _topo(n, 8, down={(0, 1), (0, 2), (0, 3)}), _whole(n, 8)
+    r = n.aligned_alloc(t, d, [0, 1, 2, 3], [0], 2)
+    assert r[0] == 0 and len(r) == 2  # forced: 0 plus someone (all links from 0 down)
+    r = n.aligned_alloc(t, d, list(range(8)), [], 4)
+    assert 0 not in r or all(x not in r for x in (1, 2, 3))
+    r = n.aligned_alloc(t, d, [0, 1, 2, 3], [], 3)
+    assert r == [1, 2, 3]
+
+
+def test_partition_packing_best_fit(n):
+    t, d = _topo(n, 8), _parts(n, 8, 8)
+    # GPU 0 has 3 free partitions, GPU 1 is completely free: a 2-partition job goes to GPU 0
+    avail = [i for i in range(len(d)) if (d[i].gpu == 0 and d[i].partition >= 5) or d[i].gpu >= 1]
+    r = n.aligned_alloc(t, d, avail, [], 2)
+    assert {d[i].gpu for i in r} == {0}
+    # a 4-partition job cannot fit GPU 0 (3 free) -> one whole other GPU, not split across two
+    r = n.aligned_alloc(t, d, avail, [], 4)
+    assert len({d[i].gpu for i in r}) == 1 and d[r[0]].gpu != 0
+
+
+def test_must_include_is_honoured_and_first(n):
+    t, d = _topo(n, 8), _parts(n, 8, 8)
+    r = n.aligned_alloc(t, d, list(range(64)), [17], 4)
+    assert r[0] == 17 and len(r) == 4 and {d[i].gpu for i in r} == {2}
+
+
+def test_errors_and_edge_cases(n):
+    t, d = _topo(n, 4), _whole(n, 4)
+    with pytest.raises(RuntimeError, match="not enough"):
+        n.aligned_alloc(t, d, [0, 1], [], 3)
+    assert n.aligned_alloc(t, d, [0, 1, 2], [2, 1], 2) == [2, 1]
+    assert n.aligned_alloc(t, d, [0, 1, 2], [], 0) == []
+    assert n.aligned_alloc(t, d, [3, 1], [], 2) == [1, 3]
+
+
+@settings(max_examples=150, deadline=None)
+@given(st.data())
+def test_aligned_invariants(n, data):
+    ngpu = data.draw(st.integers(1, 8))
+    nparts = data.draw(st.sampled_from([1, 2, 4, 8]))
+    d = _parts(n, ngpu, nparts) if nparts > 1 else _whole(n, ngpu)
+    down = set(data.draw(st.lists(st.tuples(st.integers(0, 7), st.integers(0, 7)), max_size=4)))
+    down = {tuple(sorted(x)) for x in down if x[0] != x[1]}
+    t = _topo(n, ngpu, down)
+    avail = sorted(data.draw(st.sets(st.integers(0, len(d) - 1), min_size=1)))
+    req = data.draw(st.lists(st.sampled_from(avail), max_size=min(3, len(avail)), unique=True))
+    size = data.draw(st.integers(len(req), len(avail)))
+    r = n.aligned_alloc(t, d, avail, req, size)
+    assert len(r) == size == len(set(r))
+    assert set(r) <= set(avail) and r[:len(req)] == req
+    assert n.aligned_alloc(t, d, avail, req, size) == r  # deterministic
+
+
+def test_exhaustive_matches_bruteforce_optimum(n):
+    """For small sets the chosen set has the best pairwise link score."""
+    t, d = _topo(n, 6, down={(0, 1), (2, 3), (1, 4)}), _whole(n, 6, per_numa=3)
+    r = n.aligned_alloc(t, d, list(range(6)), [], 3)
+
+    def pairs(s):
+        return sum(n.pair_score(t, d[a], d[b]) for a, b in itertools.combinations(s, 2))
+    best = max(pairs(s) for s in itertools.combinations(range(6), 3))
+    assert pairs(r) == best
+
+
+def test_large_partition_pool_is_fast_and_packed(n):
+    import time
+    t, d = _topo(n, 8), _parts(n, 8, 8)
+    t0 = time.perf_counter()
+    r = n.aligned_alloc(t, d, list(range(64)), [], 8)
+    dt = time.perf_counter() - t0
+    assert len({d[i].gpu for i in r}) == 1   # a whole GPU's partitions, not 8 GPUs
+    assert dt < 0.5, dt
+
+
+def test_distributed_policy_spreads_replicas(n):
+    # 3 GPUs x 2 replicas; replicas of g0 are already in use by someone else
+    d = [n.AllocDevice(g, -1, 0, "g%d" % g, True) for g in range(3) for _ in range(2)]
+    avail = [2, 3, 4, 5]  # g0's replicas (0, 1) are taken
+    r = n.distributed_alloc(d, avail, [], 2)
+    assert sorted({d[i].base_id for i in r}) == ["g1", "g2"]  # one replica on each free GPU
+    r2 = n.distributed_alloc(d, [1, 2, 3, 4, 5], [], 1)
+    assert d[r2[0]].base_id in ("g1", "g2")  # least-used GPUs first
+    assert n.distributed_alloc(d, avail, [4], 2)[0] == 4
+    with pytest.raises(RuntimeError):
+        n.distributed_alloc(d, [2], [], 2)
+
+
+def test_table_switches_policy_on_annotations(n):
+    from k8s_gpu_device_plugin_amd.device import build_device_map
+    from k8s_gpu_device_plugin_amd.plugin.plugin import make_table
+    from k8s_gpu_device_plugin_amd.resource import new_resources
+    g, topo = fixtures.build_backend("4gpu_spx").discover()
+    dm = build_device_map(g, new_resources(g, "single"), "single", replicas=2)
+    t = make_table("amd.com/gpu", dm["amd.com/gpu"], topo, None)
+    assert not t.aligned_supported
+    ids = t.ids()
+    got = t.preferred_ids(ids[2:], [], 2)
+    assert len({x.split("::")[0] for x in got}) == 2
+    dm2 = build_device_map(g, new_resources(g, "single"), "single")
+    t2 = make_table("amd.com/gpu", dm2["amd.com/gpu"], topo, None)
+    assert t2.aligned_supported
+    t2.set_link_up(0, 1, False)
+    assert t2.preferred_ids(t2.ids()[:3], [], 2) != t2.ids()[:2]

@@ -1,0 +1,209 @@
+"""Native HTTP/2 gRPC server protocol behaviour (flow control, errors, streams),
+exercised with the native H2Client, raw sockets and grpcio."""
+import os
+import socket
+import struct
+import threading
+import time
+
+import grpc
+import pytest
+
+from k8s_gpu_device_plugin_amd.api import v1beta1
+
+PREFACE = b"PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n"
+
+
+@pytest.fixture
+def server(n, plugin_dir):
+    tc = n.TableConfig()
+    devs = [n.TableDevice("dev-%03d" % i, i // 8, i % 8, i // 32, -1, ["/dev/dri/renderD%d" % (128 + i)], True)
+            for i in range(64)]
+    table = n.DeviceTable(tc, devs, n.Topology(8))
+    path = os.path.join(plugin_dir, "amd-gpu.sock")
+    srv = n.GrpcServer(path, 2)
+    srv.set_table(table)
+    srv.start()
+    yield srv, table, path
+    srv.stop()
+
+
+def test_unary_and_status_codes(n, server):
+    srv, table, path = server
+    c = n.H2Client(path)
+    req = v1beta1.AllocateRequest(container_requests=[v1beta1.ContainerAllocateRequest(
+        devices_ids=["dev-001"])]).SerializeToString()
+    st, body, msg = c.unary(v1beta1.METHOD_ALLOCATE, req)
+    assert st == 0 and v1beta1.AllocateResponse.FromString(body).container_responses[0].envs["AMD_VISIBLE_DEVICES"] \
+        == "dev-001"
+    st, _, msg = c.unary("/v1beta1.DevicePlugin/Bogus", b"")
+    assert st == 12 and "unknown method" in msg
+    st, _, msg = c.unary("/other.Service/Allocate", b"")
+    assert st == 12
+    st, _, msg = c.unary(v1beta1.METHOD_ALLOCATE, v1beta1.AllocateRequest(container_requests=[
+        v1beta1.ContainerAllocateRequest(devices_ids=["zzz"])]).SerializeToString())
+    assert st == 2 and "unknown device: zzz" in msg
+    st, body, _ = c.unary(v1beta1.METHOD_GET_OPTIONS, b"")
+    assert st == 0 and v1beta1.DevicePluginOptions.FromString(body).get_preferred_allocation_available
+    st, body, _ = c.unary(v1beta1.METHOD_PRE_START, b"")
+    assert st == 0 and body == b""
+    assert srv.requests >= 6 and srv.connections == 1
+    c.close()
+
+
+def test_large_request_exercises_flow_control(n, server):
+    """A GetPreferredAllocation with ~200 KB of ids spans many DATA frames and both windows."""
+    srv, table, path = server
+    ids = ["dev-%03d" % (i % 64) for i in range(12000)]
+    req = v1beta1.PreferredAllocationRequest(container_requests=[v1beta1.ContainerPreferredAllocationRequest(
+        available_deviceIDs=ids, allocation_size=4)]).SerializeToString()
+    assert len(req) > 100_000
+    c = n.H2Client(path)
+    for _ in range(12):  # > 1 MiB total: needs connection-level WINDOW_UPDATEs from the server
+        st, body, msg = c.unary(v1beta1.METHOD_GET_PREFERRED, req)
+        assert st == 0, msg
+        assert len(v1beta1.PreferredAllocationResponse.FromString(body).container_responses[0].deviceIDs) == 4
+    c.close()
+
+
+def test_large_response_respects_peer_window(n, plugin_dir):
+    """64 KiB default client window: a ListAndWatch over 2000 devices (>64 KiB) must be
+    split and continued only after WINDOW_UPDATE (grpcio client handles that)."""
+    tc = n.TableConfig()
+    devs = [n.TableDevice("a-very-long-device-identifier-%05d" % i, 0, -1, 0, -1, [], True) for i in range(2000)]
+    table = n.DeviceTable(tc, devs, n.Topology(1))
+    path = os.path.join(plugin_dir, "big.sock")
+    srv = n.GrpcServer(path, 1)
+    srv.set_table(table)
+    srv.start()
+    try:
+        assert len(table.list_and_watch()) > 65535
+        ch = grpc.insecure_channel("unix://" + path)
+        law = ch.unary_stream(v1beta1.METHOD_LIST_AND_WATCH, request_serializer=v1beta1.Empty.SerializeToString,
+                              response_deserializer=v1beta1.ListAndWatchResponse.FromString)
+        it = law(v1beta1.Empty())
+        first = next(it)
+        assert len(first.devices) == 2000
+        table.set_health(devs[5].id, False)
+        srv.notify()
+        second = next(it)
+        assert second.devices[5].health == "Unhealthy"
+        it.cancel()
+        ch.close()
+    finally:
+        srv.stop()
+
+
+def test_list_and_watch_push_without_notify(n, server):
+    """Version polling pushes updates even if nobody calls notify()."""
+    srv, table, path = server
+    ch = grpc.insecure_channel("unix://" + path)
+    law = ch.unary_stream(v1beta1.METHOD_LIST_AND_WATCH, request_serializer=v1beta1.Empty.SerializeToString,
+                          response_deserializer=v1beta1.ListAndWatchResponse.FromString)
+    it = law(v1beta1.Empty())
+    assert len(next(it).devices) == 64
+    t0 = time.monotonic()
+    table.set_gpu_health(2, -1, False)
+    upd = next(it)
+    assert sum(d.health == "Unhealthy" for d in upd.devices) == 8 and time.monotonic() - t0 < 1.0
+    it.cancel()
+    ch.close()
+
+
+def test_server_stop_ends_streams_cleanly(n, server):
+    srv, table, path = server
+    ch = grpc.insecure_channel("unix://" + path)
+    law = ch.unary_stream(v1beta1.METHOD_LIST_AND_WATCH, request_serializer=v1beta1.Empty.SerializeToString,
+                          response_deserializer=v1beta1.ListAndWatchResponse.FromString)
+    it = law(v1beta1.Empty())
+    next(it)
+    srv.stop()
+    with pytest.raises(StopIteration):
+        next(it)  # OK trailers, like the reference's ListAndWatch returning nil on stop
+    ch.close()
+    assert not os.path.exists(path)
+    srv.stop()  # idempotent
+
+
+def _frame(ftype, flags, sid, payload=b""):
+    return struct.pack(">I", len(payload))[1:] + bytes([ftype, flags]) + struct.pack(">I", sid) + payload
+
+
+def _read_frames(s, until_type=None, timeout=2.0):
+    s.settimeout(timeout)
+    buf, frames = b"", []
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline:
+        try:
+            chunk = s.recv(65536)
+        except socket.timeout:
+            break
+        if not chunk:
+            break
+        buf += chunk
+        while len(buf) >= 9:
+            ln = int.from_bytes(buf[:3], "big")
+            if len(buf) < 9 + ln:
+                break
+            frames.append((buf[3], buf[4], int.from_bytes(buf[5:9], "big") & 0x7FFFFFFF, buf[9:9 + ln]))
+            buf = buf[9 + ln:]
+        if until_type is not None and any(f[0] == until_type for f in frames):
+            break
+    return frames
+
+
+def test_raw_protocol_ping_settings_and_bad_preface(server):
+    srv, table, path = server
+    s = socket.socket(socket.AF_UNIX)
+    s.connect(path)
+    s.sendall(PREFACE + _frame(4, 0, 0) + _frame(6, 0, 0, b"12345678"))
+    frames = _read_frames(s, until_type=6)
+    types = [(f[0], f[1]) for f in frames]
+    assert (4, 0) in types and (4, 1) in types  # server SETTINGS + ACK of ours
+    assert any(f[0] == 6 and f[1] == 1 and f[3] == b"12345678" for f in frames)  # PING ACK echoes payload
+    s.close()
+    s = socket.socket(socket.AF_UNIX)
+    s.connect(path)
+    s.sendall(b"GET / HTTP/1.1\r\nHost: x\r\n\r\n")
+    frames = _read_frames(s, until_type=7)
+    assert any(f[0] == 7 and struct.unpack(">I", f[3][4:8])[0] == 1 for f in frames)  # GOAWAY PROTOCOL_ERROR
+    s.close()
+
+
+def test_oversized_frame_is_rejected(server):
+    srv, table, path = server
+    s = socket.socket(socket.AF_UNIX)
+    s.connect(path)
+    s.sendall(PREFACE + b"\x00\x80\x00" + bytes([0, 0]) + b"\x00\x00\x00\x01" + b"x" * 100)
+    frames = _read_frames(s, until_type=7)
+    assert any(f[0] == 7 and struct.unpack(">I", f[3][4:8])[0] == 6 for f in frames)  # FRAME_SIZE_ERROR
+    s.close()
+
+
+def test_many_connections_and_threads(n, server):
+    srv, table, path = server
+    req = v1beta1.AllocateRequest(container_requests=[v1beta1.ContainerAllocateRequest(
+        devices_ids=["dev-010"])]).SerializeToString()
+    errs = []
+
+    def run():
+        try:
+            lat = n.h2_bench_unary(path, v1beta1.METHOD_ALLOCATE, req, 500)
+            assert len(lat) == 500
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+    ts = [threading.Thread(target=run) for _ in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs and srv.requests >= 4000
+
+
+def test_first_stream_message_helper(n, server):
+    srv, table, path = server
+    c = n.H2Client(path)
+    body = c.first_stream_message(v1beta1.METHOD_LIST_AND_WATCH, b"")
+    assert len(v1beta1.ListAndWatchResponse.FromString(body).devices) == 64
+    st, _, _ = c.unary(v1beta1.METHOD_GET_OPTIONS, b"")  # connection still usable after RST_STREAM
+    assert st == 0

@@ -1,0 +1,214 @@
+"""Plugin manager lifecycle: registration, kubelet restart, /restart, retries, health
+events (fault injection via the fixture backend), idempotent stop, no busy loop."""
+import os
+import threading
+import time
+
+import pytest
+
+from k8s_gpu_device_plugin_amd.models import fixtures
+from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import KubeletStub
+from k8s_gpu_device_plugin_amd.plugin.manager import PluginManager
+
+
+def _wait(pred, timeout=5.0, step=0.02):
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline:
+        if pred():
+            return True
+        time.sleep(step)
+    return False
+
+
+@pytest.fixture
+def run_manager():
+    started = []
+
+    def _run(cfg, backend=None):
+        m = PluginManager(cfg, backend=backend)
+        t = m.start_background()
+        started.append((m, t))
+        return m
+    yield _run
+    for m, t in started:
+        m.stop()
+        t.join(10)
+        assert not t.is_alive()
+
+
+@pytest.mark.parametrize("grpc_server", ["native", "python"])
+def test_starts_registers_and_serves(make_cfg, plugin_dir, run_manager, grpc_server):
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(grpc={"server": grpc_server}))
+        regs = k.wait_for_registrations(1)
+        assert regs[0].resource_name == "amd.com/gpu"
+        assert m.ready.closed and m.running
+        _, devs = k.watch(regs[0].endpoint).next()
+        assert len(devs) == 2
+        text = m.exporter.render()
+        assert 'amdgpu_device_plugin_registered{resource="amd.com/gpu"} 1' in text
+
+
+def test_kubelet_restart_triggers_reregistration(make_cfg, plugin_dir, run_manager):
+    k = KubeletStub(plugin_dir).start()
+    try:
+        m = run_manager(make_cfg())
+        k.wait_for_registrations(1)
+        k.restart()  # deletes + recreates kubelet.sock -> inotify CREATE
+        k.wait_for_registrations(2, timeout=10)
+        assert _wait(lambda: m.counters["restarts_kubelet"] >= 1)
+        c = k.client("amd-gpu.sock")
+        assert c.get_options().get_preferred_allocation_available
+    finally:
+        k.stop()
+
+
+def test_restart_api_reloads(make_cfg, plugin_dir, run_manager):
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg())
+        k.wait_for_registrations(1)
+        calls = m.backend.discover_calls
+        m.restart()
+        m.restart()
+        k.wait_for_registrations(2, timeout=10)
+        assert _wait(lambda: m.backend.discover_calls >= calls + 1)
+        assert _wait(lambda: m.counters["restarts_api"] == 2)
+
+
+def test_retry_until_kubelet_appears(make_cfg, plugin_dir, run_manager):
+    m = run_manager(make_cfg(retrySeconds=0.3))
+    assert m.ready.wait(5)  # ready even though registration failed (D20)
+    time.sleep(0.5)
+    assert m.plugins and not m.plugins[0].registered
+    with KubeletStub(plugin_dir) as k:
+        k.wait_for_registrations(1, timeout=10)  # kubelet CREATE event or the retry timer
+
+
+def test_discovery_failure_is_retried(make_cfg, plugin_dir, run_manager):
+    be = fixtures.build_backend("2gpu_spx")
+    be.set_fail_discovery(True)
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(retrySeconds=0.2), backend=be)
+        assert m.ready.wait(5)
+        assert _wait(lambda: m.counters["load_failures"] >= 1)
+        be.set_fail_discovery(False)
+        k.wait_for_registrations(1, timeout=10)
+
+
+def test_scripted_reset_marks_unhealthy_then_healthy(make_cfg, plugin_dir, run_manager):
+    model = fixtures.mi355x_node(4, events=[{"at": 0.3, "kind": "pre_reset", "gpu": 2},
+                                            {"at": 0.8, "kind": "post_reset", "gpu": 2}])
+    be = fixtures.build_backend(model)
+    with KubeletStub(plugin_dir) as k:
+        run_manager(make_cfg(), backend=be)
+        w = k.watch(k.wait_for_registrations(1)[0].endpoint)
+        _, devs = w.next()
+        assert all(h == "Healthy" for _, h, _ in devs)
+        _, devs = w.next(timeout=5)
+        assert [h for _, h, _ in devs] == ["Healthy", "Healthy", "Unhealthy", "Healthy"]
+        _, devs = w.next(timeout=5)
+        assert all(h == "Healthy" for _, h, _ in devs)
+
+
+def test_ecc_uncorrectable_via_telemetry_polling(make_cfg, plugin_dir, run_manager):
+    be = fixtures.build_backend("2gpu_spx")
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(telemetry={"intervalMs": 50}), backend=be)
+        w = k.watch(k.wait_for_registrations(1)[0].endpoint)
+        w.next()
+        time.sleep(0.2)  # baseline ECC sample
+        be.set_ecc_uncorrectable(1, 3)
+        _, devs = w.next(timeout=5)
+        assert [h for _, h, _ in devs] == ["Healthy", "Unhealthy"]
+        assert any("ecc_uncorrectable" in r for _, _, _, r in m.health_log)
+        assert 'amdgpu_ecc_errors_total{gpu="1",type="uncorrectable"} 3' in m.exporter.render()
+
+
+def test_device_lost_and_recovered(make_cfg, plugin_dir, run_manager):
+    be = fixtures.build_backend("2gpu_spx")
+    with KubeletStub(plugin_dir) as k:
+        run_manager(make_cfg(telemetry={"intervalMs": 30}, health={"lostAfterFailures": 2}), backend=be)
+        w = k.watch(k.wait_for_registrations(1)[0].endpoint)
+        w.next()
+        be.set_gpu_present(0, False)
+        _, devs = w.next(timeout=5)
+        assert devs[0][1] == "Unhealthy"
+        be.set_gpu_present(0, True)
+        _, devs = w.next(timeout=5)
+        assert devs[0][1] == "Healthy"
+
+
+def test_link_down_updates_allocator_topology(make_cfg, plugin_dir, run_manager):
+    be = fixtures.build_backend("4gpu_spx")
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(telemetry={"intervalMs": 50}), backend=be)
+        reg = k.wait_for_registrations(1)[0]
+        c = k.client(reg.endpoint)
+        ids = m.plugins[0].table.ids()
+        assert list(c.preferred(ids, [ids[0]], 2).container_responses[0].deviceIDs) == ids[:2]
+        be.set_link_up(0, 1, False)
+        assert _wait(lambda: not m.plugins[0].table.topology().link(0, 1).up)
+        got = list(c.preferred(ids, [ids[0]], 2).container_responses[0].deviceIDs)
+        assert got[0] == ids[0] and got[1] != ids[1]
+
+
+def test_stop_is_idempotent_and_quick(make_cfg, plugin_dir):
+    with KubeletStub(plugin_dir):
+        m = PluginManager(make_cfg())
+        t = m.start_background()
+        m.stop()
+        m.stop()
+        t.join(5)
+        assert not t.is_alive() and m.wait_stopped(1)
+        assert not os.path.exists(os.path.join(plugin_dir, "amd-gpu.sock"))
+
+
+def test_event_loop_does_not_spin(make_cfg, plugin_dir, run_manager):
+    """Reference defect D4: the manager's `default:` branch pins a CPU core."""
+    with KubeletStub(plugin_dir) as k:
+        run_manager(make_cfg(telemetry={"intervalMs": 1000}))
+        k.wait_for_registrations(1)
+        t0, c0 = time.monotonic(), time.process_time()
+        time.sleep(1.0)
+        cpu = (time.process_time() - c0) / (time.monotonic() - t0)
+        assert cpu < 0.25, cpu  # the whole process, all threads
+
+
+def test_device_filter(make_cfg, plugin_dir, run_manager):
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(fixture="8gpu_spx_mesh", devices="0-3"))
+        _, devs = k.watch(k.wait_for_registrations(1)[0].endpoint).next()
+        assert len(devs) == 4 and [g.index for g in m.gpus] == [0, 1, 2, 3]
+
+
+def test_mixed_strategy_registers_one_plugin_per_resource(make_cfg, plugin_dir, run_manager):
+    model = fixtures.mi355x_node(2)
+    model["gpus"].append({"compute_partition": "CPX", "memory_partition": "NPS2", "numa_node": 1})
+    with KubeletStub(plugin_dir) as k:
+        run_manager(make_cfg(migStrategy="mixed"), backend=fixtures.build_backend(model))
+        regs = k.wait_for_registrations(2)
+        assert sorted((r.resource_name, r.endpoint) for r in regs) == [
+            ("amd.com/cpx_nps2", "amd-cpx_nps2.sock"), ("amd.com/gpu", "amd-gpu.sock")]
+        _, devs = k.watch("amd-cpx_nps2.sock").next()
+        assert len(devs) == 8
+
+
+def test_no_devices_waits(make_cfg, plugin_dir, run_manager, n):
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(), backend=n.FixtureBackend(1))
+        assert m.ready.wait(5)
+        time.sleep(0.3)
+        assert not k.requests and m.running
+
+
+def test_concurrent_restart_requests_are_serialized(make_cfg, plugin_dir, run_manager):
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg())
+        k.wait_for_registrations(1)
+        ts = [threading.Thread(target=m.restart) for _ in range(10)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert _wait(lambda: m.counters["restarts_api"] == 10, timeout=20)
+        assert k.client("amd-gpu.sock").get_options().get_preferred_allocation_available

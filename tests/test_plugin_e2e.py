@@ -1,0 +1,153 @@
+"""DevicePlugin endpoint end-to-end against the in-process kubelet stub, for both gRPC
+servers (native C++ HTTP/2 and grpcio).  BASELINE config 1: mock backend, 2 fake GPUs."""
+import os
+import time
+
+import grpc
+import pytest
+
+from k8s_gpu_device_plugin_amd.api import v1beta1
+from k8s_gpu_device_plugin_amd.device import build_device_map
+from k8s_gpu_device_plugin_amd.models import fixtures
+from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import KubeletStub
+from k8s_gpu_device_plugin_amd.plugin.plugin import AmdDevicePlugin, socket_name
+from k8s_gpu_device_plugin_amd.resource import new_resources
+
+
+@pytest.fixture(params=["native", "python"])
+def server_kind(request):
+    return request.param
+
+
+def _plugin(plugin_dir, kind, spec="2gpu_spx", strategy="none", **kw):
+    g, topo = fixtures.build_backend(spec).discover()
+    dm = build_device_map(g, new_resources(g, strategy), strategy, **kw)
+    name, devs = next(iter(dm.items()))
+    return AmdDevicePlugin(name, devs, topo, plugin_dir=plugin_dir, server_kind=kind), g
+
+
+def test_socket_name():
+    assert socket_name("amd.com/gpu") == "amd-gpu.sock"
+    assert socket_name("amd.com/cpx_nps2") == "amd-cpx_nps2.sock"
+
+
+def test_register_and_serve(plugin_dir, server_kind):
+    with KubeletStub(plugin_dir) as k:
+        p, g = _plugin(plugin_dir, server_kind)
+        p.start()
+        try:
+            reg = k.wait_for_registrations(1)[0]
+            assert (reg.version, reg.endpoint, reg.resource_name) == ("v1beta1", "amd-gpu.sock", "amd.com/gpu")
+            assert reg.options.get_preferred_allocation_available and not reg.options.pre_start_required
+            c = k.client(reg.endpoint)
+            assert c.get_options().get_preferred_allocation_available
+            assert c.pre_start([g[0].uuid]) == v1beta1.PreStartContainerResponse()
+            _, devs = k.watch(reg.endpoint).next()
+            assert [d[0] for d in devs] == [g[0].uuid, g[1].uuid]
+            assert all(h == "Healthy" for _, h, _ in devs) and devs[0][2] == [0]
+            r = c.allocate([g[1].uuid], [g[0].uuid, g[1].uuid])
+            c0, c1 = r.container_responses
+            assert dict(c0.envs) == {"AMD_VISIBLE_DEVICES": g[1].uuid}
+            assert [s.host_path for s in c0.devices] == ["/dev/kfd", "/dev/dri/renderD129"]
+            assert [s.host_path for s in c1.devices] == ["/dev/kfd", "/dev/dri/renderD128", "/dev/dri/renderD129"]
+            pref = c.preferred([g[0].uuid, g[1].uuid], [g[1].uuid], 1)
+            assert list(pref.container_responses[0].deviceIDs) == [g[1].uuid]
+        finally:
+            p.stop()
+    assert not os.path.exists(p.socket)
+
+
+def test_allocate_errors(plugin_dir, server_kind):
+    with KubeletStub(plugin_dir) as k:
+        p, g = _plugin(plugin_dir, server_kind)
+        p.start()
+        try:
+            c = k.client("amd-gpu.sock")
+            with pytest.raises(grpc.RpcError) as e:
+                c.allocate(["not-a-device"])
+            assert e.value.code() == grpc.StatusCode.UNKNOWN
+            assert "invalid allocation request for 'amd.com/gpu'" in e.value.details()
+            p.set_gpu_health(0, -1, False)
+            with pytest.raises(grpc.RpcError) as e:
+                c.allocate([g[0].uuid])
+            assert "Unhealthy" in e.value.details()
+            with pytest.raises(grpc.RpcError):
+                c.preferred([g[0].uuid], [], 5)
+        finally:
+            p.stop()
+
+
+def test_health_updates_both_ways(plugin_dir, server_kind):
+    with KubeletStub(plugin_dir) as k:
+        p, g = _plugin(plugin_dir, server_kind, "8gpu_cpx_nps2", "single")
+        p.start()
+        try:
+            w = k.watch("amd-gpu.sock")
+            t0, devs = w.next()
+            assert len(devs) == 64
+            t_set = time.monotonic()
+            assert p.set_gpu_health(3, -1, False) == 8
+            t1, devs = w.next()
+            bad = [i for i, h, _ in devs if h == "Unhealthy"]
+            assert len(bad) == 8 and all(i.startswith(g[3].uuid) for i in bad)
+            assert t1 - t_set < 1.0
+            assert p.set_gpu_health(3, 2, True) == 1  # one partition recovers
+            _, devs = w.next()
+            assert sum(h == "Unhealthy" for _, h, _ in devs) == 7
+            assert p.set_device_health(g[3].partitions[0].id, True)
+            _, devs = w.next()
+            assert sum(h == "Unhealthy" for _, h, _ in devs) == 6
+            assert not p.set_device_health("nope", True)
+        finally:
+            p.stop()
+
+
+def test_stop_is_idempotent_and_restartable(plugin_dir, server_kind):
+    with KubeletStub(plugin_dir) as k:
+        p, _ = _plugin(plugin_dir, server_kind)
+        p.stop()  # before start
+        p.start()
+        w = k.watch("amd-gpu.sock")
+        w.next()
+        p.stop()
+        p.stop()
+        assert not p.serving
+        p.start()  # same object can serve again (D6/D10)
+        k.wait_for_registrations(2)
+        assert k.client("amd-gpu.sock") is not None
+        p.stop()
+
+
+def test_register_fails_without_kubelet(plugin_dir, server_kind):
+    p, _ = _plugin(plugin_dir, server_kind)
+    with pytest.raises(Exception):
+        p.start()
+    assert not p.serving and not os.path.exists(p.socket)
+
+
+def test_concurrent_clients(plugin_dir, server_kind):
+    import threading
+    with KubeletStub(plugin_dir) as k:
+        p, g = _plugin(plugin_dir, server_kind, "8gpu_spx_mesh")
+        p.start()
+        errors = []
+
+        def worker(i):
+            from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import DevicePluginClient
+            c = DevicePluginClient(p.socket)
+            try:
+                for _ in range(50):
+                    r = c.allocate([g[i].uuid])
+                    if dict(r.container_responses[0].envs)["AMD_VISIBLE_DEVICES"] != g[i].uuid:
+                        errors.append(i)
+            except Exception as e:  # pragma: no cover
+                errors.append(e)
+            finally:
+                c.close()
+        ts = [threading.Thread(target=worker, args=(i,)) for i in range(8)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        p.stop()
+        assert not errors
