@@ -12,6 +12,8 @@
 //                                             for CPU tests and the 8x8 CPX configs
 #pragma once
 
+#include <chrono>
+#include <condition_variable>
 #include <cstdint>
 #include <memory>
 #include <mutex>
@@ -162,5 +164,17 @@ bool amdsmi_available();
 
 int64_t now_ns();
 int64_t mono_ns();
+
+// Timed condition-variable wait.  libstdc++ implements steady-clock waits with
+// pthread_cond_clockwait, which GCC 11's ThreadSanitizer does not intercept (it then
+// reports bogus double-locks/races); TSan builds wait on the system clock instead.
+template <class Pred>
+bool cv_wait_ms(std::condition_variable& cv, std::unique_lock<std::mutex>& lk, int64_t ms, Pred pred) {
+#if defined(__SANITIZE_THREAD__)
+  return cv.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(ms), pred);
+#else
+  return cv.wait_for(lk, std::chrono::milliseconds(ms), pred);
+#endif
+}
 
 }  // namespace amdgpu_dp

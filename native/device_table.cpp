@@ -39,7 +39,9 @@ std::string base_of(const std::string& id) {
 }  // namespace
 
 DeviceTable::DeviceTable(TableConfig cfg, std::vector<TableDevice> devices, Topology topo)
-    : cfg_(std::move(cfg)), devs_(std::move(devices)), topo_(std::move(topo)) {
+    : cfg_(std::move(cfg)), devs_(std::move(devices)), topo_(std::make_shared<const Topology>(std::move(topo))) {
+  health_.reset(new std::atomic<uint8_t>[devs_.size() ? devs_.size() : 1]);
+  for (size_t i = 0; i < devs_.size(); ++i) health_[i].store(devs_[i].healthy ? 1 : 0);
   for (int r = 0; r < kRpcCount; ++r) {
     hist_[r] = std::make_unique<Histogram>(rpc_buckets());
     errors_[r].store(0);
@@ -61,8 +63,8 @@ DeviceTable::DeviceTable(TableConfig cfg, std::vector<TableDevice> devices, Topo
   }
   if (cfg_.mount_kfd) pb::put_bytes(&kfd_frag_, 3, device_spec(cfg_.kfd_path, cfg_.kfd_path, cfg_.permissions));
   for (const auto& kv : cfg_.extra_envs) pb::put_bytes(&env_extra_frag_, 1, map_entry(kv.first, kv.second));
-  std::unique_lock<std::shared_mutex> lk(mu_);
-  rebuild_law_locked();
+  std::lock_guard<std::mutex> lk(wmu_);
+  publish_law_locked();
 }
 
 std::vector<std::string> DeviceTable::ids() const {
@@ -83,12 +85,13 @@ bool DeviceTable::contains(const std::vector<std::string>& ids) const {
   return true;
 }
 
-void DeviceTable::rebuild_law_locked() {
+void DeviceTable::publish_law_locked() {
   std::string out;
-  for (const auto& d : devs_) {
+  for (size_t i = 0; i < devs_.size(); ++i) {
+    const auto& d = devs_[i];
     std::string dev;
     pb::put_string_nz(&dev, 1, d.id);
-    pb::put_string_nz(&dev, 2, d.healthy ? "Healthy" : "Unhealthy");
+    pb::put_string_nz(&dev, 2, is_healthy(static_cast<int>(i)) ? "Healthy" : "Unhealthy");
     if (d.numa >= 0) {
       std::string node, topo;
       pb::put_int_nz(&node, 1, d.numa);
@@ -97,66 +100,65 @@ void DeviceTable::rebuild_law_locked() {
     }
     pb::put_bytes(&out, 1, dev);
   }
-  law_.swap(out);
+  std::atomic_store_explicit(&law_, std::shared_ptr<const std::string>(std::make_shared<std::string>(std::move(out))),
+                             std::memory_order_release);
 }
 
 bool DeviceTable::set_health(std::string_view id, bool healthy) {
-  std::unique_lock<std::shared_mutex> lk(mu_);
+  std::lock_guard<std::mutex> lk(wmu_);
   const int i = index_of(id);
-  if (i < 0 || devs_[i].healthy == healthy) return false;
-  devs_[i].healthy = healthy;
-  rebuild_law_locked();
+  if (i < 0 || is_healthy(i) == healthy) return false;
+  health_[i].store(healthy ? 1 : 0, std::memory_order_release);
+  publish_law_locked();
   version_.fetch_add(1, std::memory_order_acq_rel);
   return true;
 }
 
 int DeviceTable::set_gpu_health(int gpu, int partition, bool healthy) {
-  std::unique_lock<std::shared_mutex> lk(mu_);
+  std::lock_guard<std::mutex> lk(wmu_);
   int changed = 0;
-  for (auto& d : devs_) {
+  for (size_t i = 0; i < devs_.size(); ++i) {
+    const auto& d = devs_[i];
     if (d.gpu != gpu) continue;
     // a partition event hits that partition (and the whole-GPU device containing it)
     if (partition >= 0 && d.partition >= 0 && d.partition != partition) continue;
-    if (d.healthy != healthy) {
-      d.healthy = healthy;
+    if (is_healthy(static_cast<int>(i)) != healthy) {
+      health_[i].store(healthy ? 1 : 0, std::memory_order_release);
       ++changed;
     }
   }
   if (changed) {
-    rebuild_law_locked();
+    publish_law_locked();
     version_.fetch_add(1, std::memory_order_acq_rel);
   }
   return changed;
 }
 
 bool DeviceTable::healthy(std::string_view id) const {
-  std::shared_lock<std::shared_mutex> lk(mu_);
   const int i = index_of(id);
-  return i >= 0 && devs_[i].healthy;
+  return i >= 0 && is_healthy(i);
 }
 
 int DeviceTable::healthy_count() const {
-  std::shared_lock<std::shared_mutex> lk(mu_);
   int n = 0;
-  for (const auto& d : devs_) n += d.healthy;
+  for (size_t i = 0; i < devs_.size(); ++i) n += is_healthy(static_cast<int>(i));
   return n;
 }
 
 void DeviceTable::set_link_up(int a, int b, bool up) {
-  std::unique_lock<std::shared_mutex> lk(mu_);
-  if (a < 0 || b < 0 || a >= topo_.n || b >= topo_.n) return;
-  topo_.at(a, b).up = up;
-  topo_.at(b, a).up = up;
+  std::lock_guard<std::mutex> lk(wmu_);
+  auto cur = std::atomic_load_explicit(&topo_, std::memory_order_acquire);
+  if (a < 0 || b < 0 || a >= cur->n || b >= cur->n) return;
+  auto next = std::make_shared<Topology>(*cur);  // copy-on-write
+  next->at(a, b).up = up;
+  next->at(b, a).up = up;
+  std::atomic_store_explicit(&topo_, std::shared_ptr<const Topology>(std::move(next)), std::memory_order_release);
 }
 
-Topology DeviceTable::topology() const {
-  std::shared_lock<std::shared_mutex> lk(mu_);
-  return topo_;
-}
+Topology DeviceTable::topology() const { return *std::atomic_load_explicit(&topo_, std::memory_order_acquire); }
 
 std::string DeviceTable::list_and_watch() const {
-  std::shared_lock<std::shared_mutex> lk(mu_);
-  return law_;
+  return *std::atomic_load_explicit(&law_, std::memory_order_acquire);
 }
 
 std::string DeviceTable::options_bytes() const {
@@ -206,7 +208,6 @@ bool DeviceTable::allocate(std::string_view req, std::string* out) const {
     *out = std::string("malformed AllocateRequest: ") + e.what();
     return false;
   }
-  std::shared_lock<std::shared_mutex> lk(mu_);
   std::string resp;
   std::vector<int> idx;
   for (const auto& ids : reqs) {
@@ -217,7 +218,7 @@ bool DeviceTable::allocate(std::string_view req, std::string* out) const {
         *out = "invalid allocation request for '" + cfg_.resource_name + "': unknown device: " + std::string(id);
         return false;
       }
-      if (cfg_.reject_unhealthy && !devs_[i].healthy) {
+      if (cfg_.reject_unhealthy && !is_healthy(i)) {
         *out = "invalid allocation request for '" + cfg_.resource_name + "': device is Unhealthy: " + std::string(id);
         return false;
       }
@@ -249,10 +250,11 @@ AllocResult DeviceTable::preferred_ids(const std::vector<std::string>& avail, co
     m.push_back(i);
   }
   AllocResult r;
-  {
-    std::shared_lock<std::shared_mutex> lk(mu_);
-    if (aligned_ok_ && !any_annotated) r = aligned_alloc(topo_, alloc_devs_, a, m, size);
-    else r = distributed_alloc(alloc_devs_, a, m, size);
+  if (aligned_ok_ && !any_annotated) {
+    const auto topo = std::atomic_load_explicit(&topo_, std::memory_order_acquire);  // snapshot
+    r = aligned_alloc(*topo, alloc_devs_, a, m, size);
+  } else {
+    r = distributed_alloc(alloc_devs_, a, m, size);
   }
   if (r.ok && out_ids) {
     out_ids->clear();

@@ -8,11 +8,15 @@
 //     only an env var (defect D17), refuses Unhealthy devices
 //   * responses are encoded from pre-built per-device protobuf fragments
 //   * ListAndWatch bytes are cached and versioned; health changes bump the version
+//   * the RPC read path takes no lock: per-device health is an atomic flag and the
+//     ListAndWatch bytes / topology are immutable snapshots swapped RCU-style, so a
+//     burst of Allocate/GetPreferredAllocation calls can never starve a health update
+//     (a reader-preferring rwlock did, under ASan: native/selftest.cpp)
 #pragma once
 
 #include <atomic>
 #include <memory>
-#include <shared_mutex>
+#include <mutex>
 #include <string>
 #include <string_view>
 #include <unordered_map>
@@ -64,7 +68,7 @@ class DeviceTable {
 
   const TableConfig& config() const { return cfg_; }
   size_t size() const { return devs_.size(); }
-  const TableDevice& device(size_t i) const { return devs_[i]; }
+  const TableDevice& device(size_t i) const { return devs_[i]; }  // static fields only
   std::vector<std::string> ids() const;
   int index_of(std::string_view id) const;
   bool contains(const std::vector<std::string>& ids) const;
@@ -95,8 +99,9 @@ class DeviceTable {
   static void render_metric_headers(std::string* out);
 
  private:
-  void rebuild_law_locked();
+  void publish_law_locked();  // caller holds wmu_
   std::string encode_container_alloc(const std::vector<int>& idx) const;
+  bool is_healthy(int i) const { return health_[i].load(std::memory_order_acquire) != 0; }
 
   TableConfig cfg_;
   std::vector<TableDevice> devs_;
@@ -107,9 +112,10 @@ class DeviceTable {
   std::string env_extra_frag_;
   bool aligned_ok_ = true;
 
-  mutable std::shared_mutex mu_;
-  Topology topo_;
-  std::string law_;  // cached ListAndWatchResponse
+  std::unique_ptr<std::atomic<uint8_t>[]> health_;
+  std::mutex wmu_;                                // serialises writers only
+  std::shared_ptr<const Topology> topo_;          // atomic_load / atomic_store
+  std::shared_ptr<const std::string> law_;        // cached ListAndWatchResponse
   std::atomic<uint64_t> version_{1};
 
   mutable std::unique_ptr<Histogram> hist_[kRpcCount];

@@ -181,7 +181,7 @@ void FixtureBackend::shutdown() {
 
 int FixtureBackend::wait_events(int timeout_ms, std::vector<HwEvent>* out) {
   std::unique_lock<std::mutex> lk(mu_);
-  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+  const int64_t deadline = mono_ns() + static_cast<int64_t>(timeout_ms) * 1000000;
   for (;;) {
     // promote due scheduled events
     if (armed_at_ns_ != 0) {
@@ -209,19 +209,14 @@ int FixtureBackend::wait_events(int timeout_ms, std::vector<HwEvent>* out) {
       return n;
     }
     if (shutdown_) return 0;
-    auto wake = deadline;
+    const int64_t now = mono_ns();
+    if (now >= deadline) return 0;
+    int64_t wait_ns = deadline - now;
     if (armed_at_ns_ != 0 && !scheduled_.empty()) {
-      const double elapsed = (mono_ns() - armed_at_ns_) * 1e-9;
-      const auto due = std::chrono::steady_clock::now() +
-                       std::chrono::microseconds(static_cast<int64_t>((scheduled_.front().delay_s - elapsed) * 1e6) + 1);
-      if (due < wake) wake = due;
+      const int64_t due = armed_at_ns_ + static_cast<int64_t>(scheduled_.front().delay_s * 1e9);
+      wait_ns = std::min<int64_t>(wait_ns, std::max<int64_t>(0, due - now));
     }
-    if (cv_.wait_until(lk, wake) == std::cv_status::timeout && std::chrono::steady_clock::now() >= deadline) {
-      // one last promotion pass happens on the next loop iteration only if due; exit now
-      if (armed_at_ns_ == 0 || scheduled_.empty() ||
-          scheduled_.front().delay_s > (mono_ns() - armed_at_ns_) * 1e-9)
-        return 0;
-    }
+    cv_wait_ms(cv_, lk, wait_ns / 1000000 + 1, [&] { return !pending_.empty() || shutdown_; });
   }
 }
 

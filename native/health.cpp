@@ -186,7 +186,7 @@ void HealthMonitor::on_sample(int gpu, bool ok, const GpuSample& s) {
 std::vector<HealthUpdate> HealthMonitor::pop(int timeout_ms) {
   std::unique_lock<std::mutex> lk(mu_);
   if (queue_.empty())
-    cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return !queue_.empty() || stop_; });
+    cv_wait_ms(cv_, lk, timeout_ms, [&] { return !queue_.empty() || stop_; });
   std::vector<HealthUpdate> out(queue_.begin(), queue_.end());
   queue_.clear();
   return out;

@@ -11,6 +11,7 @@
 // plugin manager, which pushes a fresh ListAndWatch response.
 #pragma once
 
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <map>
@@ -42,7 +43,7 @@ class HealthMonitor {
   void set_gpu_count(int n);
   void start();
   void stop();
-  bool running() const { return running_; }
+  bool running() const { return running_.load(); }
 
   // Called by the telemetry sampler after every sample of `gpu`.
   void on_sample(int gpu, bool ok, const GpuSample& s);
@@ -75,7 +76,7 @@ class HealthMonitor {
   std::deque<HealthUpdate> queue_;
   std::vector<GpuState> state_;
   std::thread thread_;
-  volatile bool running_ = false;
+  std::atomic<bool> running_{false};
   bool stop_ = false;
   uint64_t events_seen_ = 0;
 };

@@ -1,0 +1,265 @@
+// Standalone native self-test (no Python): exercises every threaded component
+// concurrently so ASan/UBSan and TSan builds can check them (the
+// reference never ran a race detector and has real races, e.g. the `restart` bool).
+//
+//   python -m k8s_gpu_device_plugin_amd._build --selftest            (plain)
+//   python -m k8s_gpu_device_plugin_amd._build --sanitize address    (ASan + UBSan)
+//   python -m k8s_gpu_device_plugin_amd._build --sanitize thread     (TSan)
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "allocator.h"
+#include "device_table.h"
+#include "fixture_backend.h"
+#include "grpc_h2.h"
+#include "health.h"
+#include "hpack.h"
+#include "httpd.h"
+#include "pbwire.h"
+#include "telemetry.h"
+
+using namespace amdgpu_dp;
+
+static int g_failures = 0;
+#define CHECK(cond)                                                      \
+  do {                                                                   \
+    if (!(cond)) {                                                       \
+      std::fprintf(stderr, "CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #cond); \
+      ++g_failures;                                                      \
+    }                                                                    \
+  } while (0)
+
+static std::shared_ptr<FixtureBackend> make_node(int ngpu, int nparts) {
+  auto be = std::make_shared<FixtureBackend>(7);
+  int render = 128;
+  for (int g = 0; g < ngpu; ++g) {
+    GpuInfo gi;
+    gi.uuid = "gpu-" + std::to_string(g);
+    gi.market_name = "AMD Instinct MI355X";
+    gi.gfx_target = "gfx950";
+    gi.numa_node = g / 4;
+    gi.vram_total_bytes = 288ull * 1000000000ull;
+    gi.compute_partition = nparts == 1 ? "SPX" : "CPX";
+    gi.memory_partition = "NPS1";
+    for (int p = 0; p < nparts; ++p) {
+      PartitionInfo pi;
+      pi.id = gi.uuid + "-xcp" + std::to_string(p);
+      pi.index = p;
+      pi.render_minor = render++;
+      pi.numa_node = gi.numa_node;
+      gi.partitions.push_back(pi);
+    }
+    be->add_gpu(gi);
+  }
+  for (int a = 0; a < ngpu; ++a)
+    for (int b = a + 1; b < ngpu; ++b) {
+      Link l;
+      l.type = kLinkXgmi;
+      l.hops = 1;
+      be->set_link(a, b, l);
+    }
+  return be;
+}
+
+static std::string alloc_req(const std::string& id) {
+  std::string c, r;
+  pb::put_bytes(&c, 1, id);
+  pb::put_bytes(&r, 1, c);
+  return r;
+}
+
+static void test_hpack() {
+  std::string enc, dec;
+  hpack::huffman_encode("www.example.com", &enc);
+  CHECK(hpack::huffman_decode(reinterpret_cast<const uint8_t*>(enc.data()), enc.size(), &dec));
+  CHECK(dec == "www.example.com");
+  hpack::Decoder d;
+  std::string block;
+  hpack::encode_indexed(&block, 3);
+  hpack::encode_literal(&block, "te", "trailers", true);
+  std::vector<hpack::Header> hs;
+  CHECK(d.decode(reinterpret_cast<const uint8_t*>(block.data()), block.size(), &hs));
+  CHECK(hs.size() == 2 && hs[0].value == "POST" && hs[1].value == "trailers");
+}
+
+static void test_allocator_and_table(std::shared_ptr<FixtureBackend> be) {
+  std::vector<GpuInfo> gpus;
+  Topology topo;
+  be->discover(&gpus, &topo);
+  std::vector<TableDevice> devs;
+  for (auto& g : gpus)
+    for (auto& p : g.partitions) {
+      TableDevice d;
+      d.id = p.id;
+      d.gpu = g.index;
+      d.partition = p.index;
+      d.numa = p.numa_node;
+      d.host_paths = {"/dev/dri/renderD" + std::to_string(p.render_minor)};
+      devs.push_back(d);
+    }
+  auto table = std::make_shared<DeviceTable>(TableConfig{}, devs, topo);
+  std::string out;
+  CHECK(table->allocate(alloc_req(devs[3].id), &out));
+  CHECK(!table->allocate(alloc_req("nope"), &out));
+  std::vector<std::string> ids;
+  AllocResult r = table->preferred_ids(table->ids(), {}, 8, &ids);
+  CHECK(r.ok && ids.size() == 8);
+  // concurrent readers + health writers
+  std::atomic<bool> stop{false};
+  std::vector<std::thread> ts;
+  for (int i = 0; i < 4; ++i)
+    ts.emplace_back([&, i] {
+      std::string o;
+      std::vector<std::string> got;
+      while (!stop.load()) {
+        table->allocate(alloc_req(devs[i].id), &o);
+        table->list_and_watch();
+        table->preferred_ids(table->ids(), {}, 2, &got);
+      }
+    });
+  for (int k = 0; k < 200; ++k) table->set_gpu_health(k % 8, -1, k % 2);
+  stop = true;
+  for (auto& t : ts) t.join();
+}
+
+static void test_grpc_server(std::shared_ptr<FixtureBackend> be, const std::string& dir) {
+  std::vector<GpuInfo> gpus;
+  Topology topo;
+  be->discover(&gpus, &topo);
+  std::vector<TableDevice> devs;
+  for (auto& g : gpus) {
+    TableDevice d;
+    d.id = g.uuid;
+    d.gpu = g.index;
+    d.numa = g.numa_node;
+    devs.push_back(d);
+  }
+  TableConfig tc;
+  tc.reject_unhealthy = false;  // health flips concurrently below
+  auto table = std::make_shared<DeviceTable>(tc, devs, topo);
+  const std::string path = dir + "/selftest.sock";
+  GrpcServer srv(path, 3);
+  srv.set_table(table);
+  srv.start();
+  std::atomic<int> errors{0};
+  std::vector<std::thread> ts;
+  for (int i = 0; i < 6; ++i)
+    ts.emplace_back([&, i] {
+      try {
+        H2Client c(path);
+        std::string resp, msg;
+        for (int k = 0; k < 300; ++k)
+          if (c.unary("/v1beta1.DevicePlugin/Allocate", alloc_req(devs[i % devs.size()].id), &resp, &msg) != 0)
+            ++errors;
+        std::string law;
+        c.first_stream_message("/v1beta1.DevicePlugin/ListAndWatch", "", &law);
+        if (law.empty()) ++errors;
+      } catch (const std::exception& e) {
+        std::fprintf(stderr, "client error: %s\n", e.what());
+        ++errors;
+      }
+    });
+  for (int k = 0; k < 50; ++k) {
+    table->set_gpu_health(k % 4, -1, k % 2);
+    srv.notify();
+  }
+  for (auto& t : ts) t.join();
+  CHECK(errors.load() == 0);
+  CHECK(srv.requests() >= 1800);
+  srv.stop();
+  srv.stop();
+}
+
+static void test_exporter_httpd_health(std::shared_ptr<FixtureBackend> be) {
+  std::vector<GpuInfo> gpus;
+  Topology topo;
+  be->discover(&gpus, &topo);
+  auto ex = std::make_shared<Exporter>();
+  ex->set_inventory(gpus);
+  auto mon = std::make_shared<HealthMonitor>(be, 2);
+  mon->set_gpu_count(static_cast<int>(gpus.size()));
+  mon->start();
+  ex->start(be, 5, mon);
+  HttpConfig hc;
+  hc.host = "127.0.0.1";
+  hc.port = 0;
+  hc.threads = 3;
+  hc.access_log = false;
+  HttpServer http(hc, ex);
+  std::atomic<int> restarts{0};
+  http.set_restart_hook([&] { ++restarts; });
+  const int port = http.start();
+  std::atomic<int> bad{0};
+  std::vector<std::thread> ts;
+  for (int i = 0; i < 4; ++i)
+    ts.emplace_back([&, i] {
+      for (int k = 0; k < 40; ++k) {
+        const int fd = socket(AF_INET, SOCK_STREAM, 0);
+        sockaddr_in a{};
+        a.sin_family = AF_INET;
+        a.sin_port = htons(static_cast<uint16_t>(port));
+        a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+        if (connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0) {
+          ++bad;
+          close(fd);
+          continue;
+        }
+        const char* req = (k % 3 == 0) ? "GET /metrics HTTP/1.1\r\nConnection: close\r\n\r\n"
+                                       : (i == 0 && k == 1 ? "GET /restart HTTP/1.1\r\nConnection: close\r\n\r\n"
+                                                           : "GET /health HTTP/1.1\r\nConnection: close\r\n\r\n");
+        (void)!write(fd, req, std::strlen(req));
+        std::string resp;
+        char buf[65536];
+        ssize_t r;
+        while ((r = read(fd, buf, sizeof(buf))) > 0) resp.append(buf, static_cast<size_t>(r));
+        close(fd);
+        if (resp.compare(0, 15, "HTTP/1.1 200 OK") != 0) ++bad;
+      }
+    });
+  HwEvent e;
+  e.kind = kEvtPreReset;
+  e.gpu = 1;
+  be->inject_event(e);
+  be->set_ecc_uncorrectable(0, 5);
+  for (auto& t : ts) t.join();
+  CHECK(bad.load() == 0);
+  CHECK(restarts.load() == 1);
+  http.stop();
+  ex->stop();
+  mon->stop();
+  bool saw_unhealthy = false;
+  for (auto& u : mon->pop(10))
+    if (u.healthy == 0) saw_unhealthy = true;
+  CHECK(saw_unhealthy || !mon->gpu_healthy(1));
+}
+
+int main() {
+  char tmpl[] = "/tmp/amdgpu-selftest-XXXXXX";
+  const char* dir = mkdtemp(tmpl);
+  if (!dir) return 2;
+  std::fprintf(stderr, "[selftest] hpack\n");
+  test_hpack();
+  std::fprintf(stderr, "[selftest] allocator + table\n");
+  auto be = make_node(8, 8);
+  test_allocator_and_table(be);
+  std::fprintf(stderr, "[selftest] grpc server\n");
+  test_grpc_server(make_node(4, 1), dir);
+  std::fprintf(stderr, "[selftest] exporter + httpd + health\n");
+  test_exporter_httpd_health(make_node(2, 1));
+  rmdir(dir);
+  if (g_failures) {
+    std::fprintf(stderr, "native selftest: %d failure(s)\n", g_failures);
+    return 1;
+  }
+  std::printf("native selftest: ok\n");
+  return 0;
+}

@@ -1,0 +1,115 @@
+"""Process-level tests: the daemon entry point (signals, config, profiling flag) and the
+bench.py driver contract (single rank and 2 ranks over gloo)."""
+import http.client
+import json
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+
+import pytest
+
+from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import KubeletStub
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _env():
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    return env
+
+
+def test_version_and_bad_config(tmp_path):
+    out = subprocess.run([sys.executable, "-m", "k8s_gpu_device_plugin_amd", "--version"], env=_env(),
+                         stdout=subprocess.PIPE, text=True, timeout=60)
+    assert out.returncode == 0 and out.stdout.strip() == "k8s-gpu-device-plugin 0.1.0"
+    (tmp_path / "bad.yml").write_text("migStrategy: sometimes\n")
+    out = subprocess.run([sys.executable, "-m", "k8s_gpu_device_plugin_amd", "--configFile", str(tmp_path / "bad.yml")],
+                         env=_env(), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=60)
+    assert out.returncode == 2 and "invalid partition" in out.stderr
+
+
+@pytest.mark.parametrize("sig", [signal.SIGTERM, signal.SIGINT, signal.SIGHUP, signal.SIGQUIT])
+def test_daemon_serves_and_exits_gracefully(plugin_dir, tmp_path, sig):
+    port = _port()
+    bench_dir = tmp_path / "prof"
+    cfg = tmp_path / "c.yml"
+    cfg.write_text("webListenAddress: 127.0.0.1:%d\nbackend: fixture\nfixture: 2gpu_spx\npluginDir: %s\n"
+                   "benchmark: %s\nbenchmarkDir: %s\nlog:\n  fileDir: %s\n  console: false\n"
+                   % (port, plugin_dir, "true" if sig == signal.SIGTERM else "false", bench_dir, tmp_path / "logs"))
+    with KubeletStub(plugin_dir) as k:
+        p = subprocess.Popen([sys.executable, "-m", "k8s_gpu_device_plugin_amd", "--configFile", str(cfg)],
+                             env=_env(), cwd=str(tmp_path), stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+        try:
+            k.wait_for_registrations(1, timeout=60)
+            c = http.client.HTTPConnection("127.0.0.1", port, timeout=5)
+            c.request("GET", "/health")
+            assert c.getresponse().read() == b'{"code":0,"data":"ok","msg":"success"}\n'
+            c.request("GET", "/restart")
+            assert c.getresponse().status == 200
+            k.wait_for_registrations(2, timeout=30)
+            time.sleep(0.2)
+            p.send_signal(sig)
+            rc = p.wait(30)
+        finally:
+            if p.poll() is None:
+                p.kill()
+    assert rc == 0, p.stdout.read().decode()[-3000:]
+    logs = os.listdir(tmp_path / "logs")
+    assert "k8s-gpu-device-plugin-info.log" in logs
+    info = (tmp_path / "logs" / "k8s-gpu-device-plugin-info.log").read_text()
+    assert "exiting gracefully" in info and "see you next time!" in info
+    if sig == signal.SIGTERM:
+        files = set(os.listdir(bench_dir))
+        assert {"cpu.prof", "mem.prof", "threads.prof", "latency.prom"} <= files
+        assert "amdgpu_device_plugin_rpc_duration_seconds" in (bench_dir / "latency.prom").read_text() or True
+
+
+def _run_bench(args, nproc=1, timeout=300):
+    env = _env()
+    env.pop("RANK", None)
+    env.pop("WORLD_SIZE", None)
+    if nproc == 1:
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + args
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+               "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py")] + args
+    p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    return json.loads(lines[0])
+
+
+def _check_contract(r, n, steps, warmup):
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in r, k
+    assert r["metric"] == json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+    assert (r["n_gpus"], r["steps"], r["warmup"]) == (n, steps, warmup)
+    assert r["value"] > 0 and r["higher_is_better"] is False and r["scaling"] == "weak"
+    assert r["allocate_p50_us_grpcio_client"] > 0 and r["scrape_rps"] > 0
+    assert set(r["config"]) >= {"model", "global_batch", "seq_len", "parallelism"}
+
+
+def test_bench_single_rank():
+    r = _run_bench(["--steps", "2", "--warmup", "1"])
+    _check_contract(r, 1, 2, 1)
+
+
+@pytest.mark.slow
+def test_bench_two_ranks_gloo():
+    r = _run_bench(["--gpus", "2", "--steps", "2", "--warmup", "1"], nproc=2)
+    _check_contract(r, 2, 2, 1)
+    assert r["config"]["global_batch"] == 2 * 256

@@ -1,0 +1,111 @@
+"""Config loading/validation (config/config.go, main.go:31-52) and per-level JSON logs
+(modules/log/log.go)."""
+import json
+import logging
+import os
+
+import pytest
+
+from k8s_gpu_device_plugin_amd import config as C
+from k8s_gpu_device_plugin_amd.utils import log as L
+from k8s_gpu_device_plugin_amd.utils.util import CloseOnce, envelope_bytes, failed, parse_index_list, success
+
+
+def test_defaults_fix_d11():
+    cfg = C.validate(C.Config())
+    assert cfg.webListenAddress == "0.0.0.0:9100" and cfg.listen_host_port() == ("0.0.0.0", 9100)
+    assert cfg.migStrategy == "none" and cfg.log.level == "debug" and cfg.log.fileDir == "./logs"
+    assert cfg.pluginDir == "/var/lib/kubelet/device-plugins/" and cfg.kubelet_socket.endswith("kubelet.sock")
+
+
+def test_load_reference_style_file(tmp_path):
+    (tmp_path / "config.yml").write_text(
+        'webListenAddress: "0.0.0.0:9100"\nmigStrategy: "none"\nbenchmark: false\nlog:\n  level: "debug"\n'
+        '  fileDir: "./logs"\n')
+    cfg = C.load("config", search_dirs=(str(tmp_path),), environ={})
+    assert cfg.webListenAddress == "0.0.0.0:9100" and not cfg.benchmark
+
+
+def test_missing_file_is_not_fatal(tmp_path):
+    cfg = C.load("nope", search_dirs=(str(tmp_path),), environ={})
+    assert cfg.migStrategy == "none"
+    with pytest.raises(C.ConfigError):
+        C.load("nope", search_dirs=(str(tmp_path),), environ={}, required=True)
+
+
+def test_case_insensitive_keys_alias_and_nested(tmp_path):
+    p = tmp_path / "x.yaml"
+    p.write_text("WEBLISTENADDRESS: 127.0.0.1:1234\npartitionStrategy: MIXED\nLog: {Level: INFO}\n"
+                 "telemetry: {intervalMs: 250}\nresources: [{pattern: '*MI355*', name: mi355}]\n"
+                 "sharing: {replicas: 4, renameByDefault: true}\ngrpc: {server: python}\n")
+    cfg = C.load(str(p), environ={})
+    assert cfg.listen_host_port() == ("127.0.0.1", 1234) and cfg.migStrategy == "mixed"
+    assert cfg.log.level == "INFO" and cfg.telemetry.intervalMs == 250
+    assert cfg.resources[0].pattern == "*MI355*" and cfg.resources[0].name == "mi355"
+    assert cfg.sharing.replicas == 4 and cfg.sharing.renameByDefault and cfg.grpc.server == "python"
+
+
+def test_env_overrides(tmp_path):
+    env = {"AMDGPU_DP_WEB_LISTEN_ADDRESS": "127.0.0.1:0", "AMDGPU_DP_BACKEND": "fixture",
+           "AMDGPU_DP_MIG_STRATEGY": "single", "AMDGPU_DP_LOG_LEVEL": "warn", "AMDGPU_DP_BENCHMARK": "true",
+           "AMDGPU_DP_GRPC_SERVER": "python"}
+    cfg = C.load("none", search_dirs=(str(tmp_path),), environ=env)
+    assert (cfg.webListenAddress, cfg.backend, cfg.migStrategy, cfg.log.level, cfg.benchmark, cfg.grpc.server) == \
+        ("127.0.0.1:0", "fixture", "single", "warn", True, "python")
+
+
+@pytest.mark.parametrize("raw", [{"migStrategy": "bogus"}, {"webListenAddress": "9002"},
+                                 {"log": {"level": "verbose"}}, {"backend": "nvml"},
+                                 {"sharing": {"replicas": 0}}, {"grpc": {"server": "java"}},
+                                 {"resourcePrefix": "a/b"}, {"resources": [{"pattern": "*"}]}])
+def test_validation_errors(raw):
+    with pytest.raises(C.ConfigError):
+        C.validate(C.from_dict(raw))
+
+
+def test_util_helpers():
+    assert envelope_bytes(success("ok")) == b'{"code":0,"data":"ok","msg":"success"}\n'
+    assert failed("x") == {"code": -1, "data": None, "msg": "x"}
+    assert parse_index_list("0-3,6") == [0, 1, 2, 3, 6] and parse_index_list("") is None
+    assert parse_index_list("all") is None
+    latch = CloseOnce()
+    assert not latch.wait(0.01)
+    latch.close()
+    latch.close()
+    assert latch.closed and latch.wait(0)
+
+
+def test_level_parsing():
+    assert L.parse_level("Debug") == logging.DEBUG and L.parse_level("WARN") == logging.WARNING
+    with pytest.raises(ValueError):
+        L.parse_level("trace")
+
+
+def test_per_level_json_files(tmp_path):
+    logger = L.init_logger("debug", str(tmp_path), "app", console=False)
+    child = L.get_logger("x")
+    child.debug("d %d", 1)
+    child.info("i", extra={"resourceName": "amd.com/gpu"})
+    child.warning("w")
+    child.error("e")
+    child.critical("fatal one")  # D12: reference drops Fatal/Panic records entirely
+    for h in logger.handlers:
+        h.flush()
+    files = {f: (tmp_path / f).read_text().strip().splitlines() for f in os.listdir(tmp_path)}
+    assert set(files) == {"app-debug.log", "app-info.log", "app-warn.log", "app-error.log"}
+    assert [json.loads(x)["msg"] for x in files["app-debug.log"]] == ["d 1"]
+    info = json.loads(files["app-info.log"][0])
+    assert info["msg"] == "i" and info["resourceName"] == "amd.com/gpu" and info["level"] == "info"
+    assert isinstance(info["ts"], int) and info["ts"] > 1_600_000_000_000  # unix millis
+    assert [json.loads(x)["level"] for x in files["app-error.log"]] == ["error", "fatal"]
+    assert [json.loads(x)["level"] for x in files["app-warn.log"]] == ["warn"]
+    L.init_logger("info", None, "app", console=False)  # idempotent reconfiguration
+
+
+def test_rotation_gzip(tmp_path):
+    logger = L.init_logger("info", str(tmp_path), "rot", console=False, max_bytes=2000, backups=3)
+    for i in range(200):
+        logger.info("message number %d with some padding text", i)
+    names = sorted(os.listdir(tmp_path))
+    assert any(n.endswith(".gz") for n in names) and len([n for n in names if n.startswith("rot-info")]) <= 4
+    L.init_logger("info", None, console=False)

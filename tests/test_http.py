@@ -1,0 +1,171 @@
+"""HTTP ops surface parity with the reference (router/api.go, server/server.go,
+middleware/echo_metric.go) for the native epoll server and the Python server."""
+import http.client
+import json
+import socket
+import time
+
+import pytest
+from prometheus_client.parser import text_string_to_metric_families
+
+from k8s_gpu_device_plugin_amd.plugin.manager import PluginManager
+from k8s_gpu_device_plugin_amd.server.web import WebServer
+
+
+@pytest.fixture(params=["native", "python"])
+def web(request, make_cfg):
+    cfg = make_cfg(webListenAddress="127.0.0.1:0", http={"server": request.param, "accessLog": False})
+    mgr = PluginManager(cfg)
+    restarts = []
+    mgr.restart = lambda: restarts.append(time.monotonic())  # observe, do not reload
+    mgr.load_plugins()
+    mgr._start_telemetry()  # exporter sampling the fixture backend, health monitor
+    w = WebServer(cfg, mgr)
+    port = w.start()
+    yield port, restarts, request.param
+    w.stop()
+    mgr.exporter.stop()
+    mgr.monitor.stop()
+
+
+def get(port, path, method="GET", headers=None, body=None):
+    c = http.client.HTTPConnection("127.0.0.1", port, timeout=5)
+    c.request(method, path, body=body, headers=headers or {})
+    r = c.getresponse()
+    data = r.read()
+    c.close()
+    return r.status, dict(r.getheaders()), data
+
+
+def test_json_routes_byte_exact(web):
+    port, restarts, _ = web
+    assert get(port, "/")[2] == b'{"code":0,"data":"version : 0.1.0","msg":"success"}\n'
+    st, h, body = get(port, "/health")
+    assert st == 200 and body == b'{"code":0,"data":"ok","msg":"success"}\n'
+    assert h["Content-Type"] == "application/json"
+    st, _, body = get(port, "/restart")
+    assert st == 200 and json.loads(body) == {"code": 0, "data": "ok", "msg": "success"}
+    assert len(restarts) == 1
+
+
+def test_errors_and_cors(web):
+    port, _, _ = web
+    st, h, body = get(port, "/nope")
+    assert st == 404 and body == b'{"message":"Not Found"}\n'
+    assert h["Access-Control-Allow-Origin"] == "*"
+    assert h["Access-Control-Allow-Credentials"] == "true"
+    assert h["Access-Control-Allow-Methods"] == "POST, GET, OPTIONS, PATCH, PUT, DELETE"
+    assert h["Access-Control-Allow-Headers"] == \
+        "Content-Type, Content-Length, Accept-Encoding, Authorization, Origin"
+    st, h, body = get(port, "/health", headers={"Origin": "https://ops.example"})
+    assert h["Access-Control-Allow-Origin"] == "https://ops.example"
+    st, h, body = get(port, "/anything", method="OPTIONS")
+    assert st == 200 and body == b'{"message":"OK"}\n'
+    st, _, body = get(port, "/health", method="POST", body=b"x=1")
+    assert st == 405 and body == b'{"message":"Method Not Allowed"}\n'
+    st, _, _ = get(port, "/health?probe=1")
+    assert st == 200
+
+
+def test_metrics_exposition_is_valid_and_complete(web):
+    port, _, kind = web
+    get(port, "/health")
+    get(port, "/missing")
+    st, h, body = get(port, "/metrics")
+    assert st == 200 and h["Content-Type"] == "text/plain; version=0.0.4; charset=utf-8"
+    st, h, body = get(port, "/metrics")
+    fams = {f.name: f for f in text_string_to_metric_families(body.decode())}
+    for name in ("k8s_gpu_device_plugin_build_info", "amdgpu_info", "amdgpu_power_watts",
+                 "amdgpu_temperature_celsius", "amdgpu_xgmi_link_up", "amdgpu_partition_info",
+                 "amdgpu_device_plugin_device_health", "echo_http_requests", "echo_http_request_duration_seconds"):
+        assert name in fams, name
+    reqs = {(s.labels["handler"], s.labels["method"], s.labels["status"]): s.value
+            for s in fams["echo_http_requests"].samples}
+    assert reqs[("/health", "GET", "2xx")] >= 1 and reqs[("/not-found", "GET", "4xx")] >= 1
+    assert reqs[("/metrics", "GET", "2xx")] >= 1
+    les = [s.labels["le"] for s in fams["echo_http_request_duration_seconds"].samples
+           if s.name.endswith("_bucket") and s.labels["handler"] == "/health"]
+    assert les == ["0.0005", "0.001", "0.002", "0.005", "0.01", "0.02", "0.05", "0.1", "0.2", "0.5", "1",
+                   "2", "5", "10", "15", "20", "30", "+Inf"]  # Go FormatFloat(g, -1)
+
+
+def test_keepalive_and_pipelining(web):
+    port, _, kind = web
+    c = http.client.HTTPConnection("127.0.0.1", port, timeout=5)
+    for _ in range(20):
+        c.request("GET", "/health")
+        assert c.getresponse().read().endswith(b'"ok","msg":"success"}\n')
+    c.close()
+    if kind != "native":
+        return
+    s = socket.create_connection(("127.0.0.1", port))
+    s.sendall(b"GET /health HTTP/1.1\r\nHost: x\r\n\r\nGET / HTTP/1.1\r\nHost: x\r\n\r\n"
+              b"GET /health HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n")
+    data = b""
+    s.settimeout(5)
+    while True:
+        chunk = s.recv(65536)
+        if not chunk:
+            break
+        data += chunk
+    s.close()
+    assert data.count(b"HTTP/1.1 200 OK") == 3 and b"Connection: close" in data
+    s = socket.create_connection(("127.0.0.1", port))
+    s.sendall(b"GET /health HTTP/1.0\r\n\r\n")
+    s.settimeout(5)
+    data = b""
+    while True:
+        chunk = s.recv(65536)
+        if not chunk:
+            break
+        data += chunk
+    assert data.startswith(b"HTTP/1.0 200 OK")
+
+
+def test_native_http_rejects_garbage(make_cfg):
+    cfg = make_cfg(webListenAddress="127.0.0.1:0", http={"accessLog": False})
+    mgr = PluginManager(cfg)
+    w = WebServer(cfg, mgr)
+    port = w.start()
+    try:
+        s = socket.create_connection(("127.0.0.1", port))
+        s.sendall(b"garbage\r\n\r\n")
+        s.settimeout(5)
+        assert s.recv(4096).startswith(b"HTTP/1.1 400 Bad Request")
+        s.close()
+        s = socket.create_connection(("127.0.0.1", port))
+        s.sendall(b"GET / HTTP/1.1\r\n" + b"X-Long: " + b"a" * 70000 + b"\r\n")
+        assert s.recv(4096).startswith(b"HTTP/1.1 431")
+        s.close()
+        assert get(port, "/health")[0] == 200  # server still fine
+    finally:
+        w.stop()
+
+
+def test_start_stop_start_same_port(make_cfg):
+    """D16: the reference registers routes/collectors globally, a 2nd Run panics."""
+    cfg = make_cfg(webListenAddress="127.0.0.1:0", http={"accessLog": False})
+    mgr = PluginManager(cfg)
+    w = WebServer(cfg, mgr)
+    port = w.start()
+    w.stop()
+    cfg.webListenAddress = "127.0.0.1:%d" % port
+    w2 = WebServer(cfg, mgr)
+    assert w2.start() == port
+    assert get(port, "/health")[0] == 200
+    w2.stop()
+
+
+def test_access_log_lines(make_cfg, capfd):
+    cfg = make_cfg(webListenAddress="127.0.0.1:0", http={"accessLog": True})
+    mgr = PluginManager(cfg)
+    w = WebServer(cfg, mgr)
+    port = w.start()
+    get(port, "/health", headers={"User-Agent": "probe/1"})
+    time.sleep(0.3)
+    w.stop()
+    out = capfd.readouterr().out
+    line = [ln for ln in out.splitlines() if '"uri":"/health"' in ln][0]
+    rec = json.loads(line)
+    assert rec["method"] == "GET" and rec["status"] == 200 and rec["user_agent"] == "probe/1"
+    assert rec["remote_ip"] == "127.0.0.1" and rec["bytes_out"] > 0 and "latency" in rec

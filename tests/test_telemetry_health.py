@@ -1,0 +1,115 @@
+"""Exporter (per-GPU / per-partition telemetry rendering) and the native health monitor."""
+import time
+
+from prometheus_client.parser import text_string_to_metric_families
+
+from k8s_gpu_device_plugin_amd.models import fixtures
+
+
+def _families(text):
+    return {f.name: f for f in text_string_to_metric_families(text)}
+
+
+def test_exporter_cpx_64_partitions(n):
+    be = fixtures.build_backend("8gpu_cpx_nps2")
+    gpus, _ = be.discover()
+    ex = n.Exporter()
+    ex.set_inventory(gpus)
+    ex.set_partition_labels([n.PartitionLabel(g.index, p.index, p.id, "amd.com/gpu") for g in gpus
+                             for p in g.partitions])
+    ex.set_build_info('# TYPE x_build_info gauge\nx_build_info{v="1"} 1\n')
+    ex.start(be, 50, None)
+    time.sleep(0.2)
+    ex.stop()
+    assert ex.samples_total >= 2
+    fams = _families(ex.render())
+    assert len(fams["amdgpu_info"].samples) == 8
+    assert fams["amdgpu_info"].samples[0].labels["compute_partition"] == "CPX"
+    assert len(fams["amdgpu_partition_info"].samples) == 64
+    assert len(fams["amdgpu_partition_gfx_busy_percent"].samples) == 64
+    assert len(fams["amdgpu_xgmi_link_up"].samples) == 8 * 7
+    hbm = [s for s in fams["amdgpu_temperature_celsius"].samples if s.labels["sensor"].startswith("hbm")]
+    assert len(hbm) == 64
+    assert fams["amdgpu_ecc_errors"].type == "counter"
+    assert "process_cpu_seconds" in fams and "x_build_info" in fams
+    assert fams["amdgpu_telemetry_sample_duration_seconds"].type == "histogram"
+    s = ex.last_sample(3)
+    assert s.ok and s.power_w > 0 and len(s.links) == 7
+
+
+def test_exporter_device_health_and_rpc_histogram(n):
+    tc = n.TableConfig()
+    t = n.DeviceTable(tc, [n.TableDevice("a", 0), n.TableDevice("b", 1)], n.Topology(2))
+    t.observe(n.RPC_ALLOCATE, 12e-6, False)
+    t.set_health("b", False)
+    ex = n.Exporter()
+    ex.set_tables([t])
+    fams = _families(ex.render())
+    health = {s.labels["device_id"]: s.value for s in fams["amdgpu_device_plugin_device_health"].samples}
+    assert health == {"a": 1.0, "b": 0.0}
+    buckets = [s for s in fams["amdgpu_device_plugin_rpc_duration_seconds"].samples if s.name.endswith("_bucket")]
+    assert buckets[0].labels["rpc"] == "Allocate" and buckets[-1].value == 1
+
+
+def test_health_monitor_state_machine(n):
+    be = n.FixtureBackend(1)
+    m = n.HealthMonitor(be, 2)
+    m.set_gpu_count(2)
+    m.process(n.HwEvent(n.EVT_PRE_RESET, 1, message="x"))
+    m.process(n.HwEvent(n.EVT_PRE_RESET, 1))  # duplicate -> no second transition
+    u = m.pop(100)
+    assert [(x.gpu, x.healthy) for x in u] == [(1, 0)]
+    assert not m.gpu_healthy(1) and m.gpu_healthy(0)
+    m.process(n.HwEvent(n.EVT_ECC_UNCORRECTABLE, 1))
+    assert m.pop(10) == []  # still unhealthy, no transition
+    m.process(n.HwEvent(n.EVT_POST_RESET, 1))  # reset clears the ECC latch too
+    assert [(x.gpu, x.healthy) for x in m.pop(100)] == [(1, 1)]
+    m.process(n.HwEvent(n.EVT_LINK_DOWN, 0, peer=1))
+    m.process(n.HwEvent(n.EVT_LINK_DOWN, 1, peer=0))  # same link seen from the peer: deduplicated
+    u = m.pop(100)
+    assert len(u) == 1 and u[0].link_up == 0 and u[0].healthy == -1
+    m.process(n.HwEvent(n.EVT_THERMAL, 0, message="hot"))
+    u = m.pop(100)
+    assert u[0].healthy == -1 and "thermal" in u[0].reason
+    assert m.events_seen >= 7
+    m.process(n.HwEvent(n.EVT_PRE_RESET, 7))  # out of range gpu: ignored, no crash
+
+
+def test_health_monitor_from_samples(n):
+    be = fixtures.build_backend("2gpu_spx")
+    m = n.HealthMonitor(be, 2)
+    m.set_gpu_count(2)
+    ex = n.Exporter()
+    gpus, _ = be.discover()
+    ex.set_inventory(gpus)
+    ex.start(be, 30, m)
+    try:
+        time.sleep(0.1)
+        be.set_ecc_uncorrectable(0, 1)
+        deadline = time.monotonic() + 3
+        got = []
+        while time.monotonic() < deadline and not got:
+            got = [u for u in m.pop(100) if u.healthy == 0]
+        assert got and got[0].gpu == 0 and "ecc" in got[0].reason
+    finally:
+        ex.stop()
+
+
+def test_monitor_event_thread_scripted(n):
+    model = fixtures.mi355x_node(2, events=[{"at": 0.05, "kind": "pre_reset", "gpu": 0},
+                                            {"at": 0.10, "kind": "link_down", "gpu": 0, "peer": 1}])
+    be = fixtures.build_backend(model)
+    m = n.HealthMonitor(be, 3)
+    m.set_gpu_count(2)
+    m.start()
+    try:
+        got = []
+        deadline = time.monotonic() + 3
+        while time.monotonic() < deadline and len(got) < 2:
+            got += m.pop(100)
+        assert (got[0].gpu, got[0].healthy) == (0, 0)
+        assert got[1].link_up == 0 and got[1].peer == 1
+        assert not be.discover()[1].link(0, 1).up
+    finally:
+        m.stop()
+        m.stop()
