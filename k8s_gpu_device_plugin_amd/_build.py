@@ -40,6 +40,7 @@ CORE_SOURCES = [
     "watch.cpp",
     "hpack.cpp",
     "grpc_h2.cpp",
+    "loadgen.cpp",
 ]
 BINDING_SOURCES = ["bindings.cpp"]
 CANARY_SOURCE = os.path.join(PKG_DIR, "ops", "canary.hip")

@@ -36,9 +36,14 @@ __device__ __forceinline__ uint32_t mix32(uint64_t x) {
   return static_cast<uint32_t>(x);
 }
 
+// Address-derived 16-byte pattern, ~5 integer ops per word so the verify pass stays
+// HBM-bound: lo * odd constant is a bijection mod 2^32, so no two words of a <=64 GiB
+// buffer share a pattern (aliasing / addressing faults are caught), and every data bit
+// takes both values across the buffer (stuck-at faults are caught).
 __device__ __forceinline__ uint4 pattern(uint64_t idx, uint32_t seed) {
-  const uint64_t b = (idx << 2) ^ (static_cast<uint64_t>(seed) << 40);
-  return make_uint4(mix32(b), mix32(b + 1), mix32(b + 2), mix32(b + 3));
+  const uint32_t lo = static_cast<uint32_t>(idx), hi = static_cast<uint32_t>(idx >> 32);
+  const uint32_t b = lo * 0x9E3779B1u ^ (hi + seed) * 0x85EBCA77u;
+  return make_uint4(b, b ^ 0xA5A5A5A5u, ~b, b * 3u + 0x6A09E667u);
 }
 
 __global__ void __launch_bounds__(256) hbm_write(uint4* __restrict__ buf, uint64_t n, uint32_t seed) {
@@ -289,6 +294,42 @@ done:
   if (d_err) (void)hipFree(d_err);
   if (buf) (void)hipFree(buf);
   return out->error[0] ? -1 : 0;
+}
+
+// Fault-injection self-check of the HBM verifier: writes the pattern, corrupts
+// `flips` 4-byte words at spread-out offsets behind the kernel's back (hipMemcpy), and
+// returns how many mismatching words the verify kernel reports (expected == flips).
+long long amdgpu_canary_detects_corruption(int device, unsigned long long hbm_bytes, int flips) {
+  uint4* buf = nullptr;
+  unsigned long long* d_err = nullptr;
+  unsigned long long h_err = 0;
+  const uint64_t n = hbm_bytes / sizeof(uint4);
+  hipDeviceProp_t prop;
+  if (n == 0 || flips < 0 || hipSetDevice(device) != hipSuccess ||
+      hipGetDeviceProperties(&prop, device) != hipSuccess)
+    return -1;
+  const int blocks = prop.multiProcessorCount * 8;
+  long long rc = -1;
+  if (hipMalloc(&buf, n * sizeof(uint4)) == hipSuccess && hipMalloc(&d_err, sizeof(h_err)) == hipSuccess &&
+      hipMemset(d_err, 0, sizeof(h_err)) == hipSuccess) {
+    hipLaunchKernelGGL(hbm_write, dim3(blocks), dim3(256), 0, 0, buf, n, 77u);
+    bool ok = hipDeviceSynchronize() == hipSuccess;
+    for (int f = 0; ok && f < flips; ++f) {
+      const uint64_t word = (static_cast<uint64_t>(f) * 2654435761ull) % n;
+      const uint32_t junk = 0xDEADBEEFu ^ static_cast<uint32_t>(f);
+      ok = hipMemcpy(reinterpret_cast<char*>(buf + word) + 4 * (f & 3), &junk, 4, hipMemcpyHostToDevice) ==
+           hipSuccess;
+    }
+    if (ok) {
+      hipLaunchKernelGGL(hbm_verify, dim3(blocks), dim3(256), 0, 0, buf, n, 77u, d_err);
+      if (hipDeviceSynchronize() == hipSuccess &&
+          hipMemcpy(&h_err, d_err, sizeof(h_err), hipMemcpyDeviceToHost) == hipSuccess)
+        rc = static_cast<long long>(h_err);
+    }
+  }
+  if (d_err) (void)hipFree(d_err);
+  if (buf) (void)hipFree(buf);
+  return rc;
 }
 
 // Host wrapper for the numerics test: inputs/outputs in host memory.

@@ -46,6 +46,8 @@ def load():
                                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
                                                 ctypes.c_int]
         lib.amdgpu_canary_mfma_gemm.restype = ctypes.c_int
+        lib.amdgpu_canary_detects_corruption.argtypes = [ctypes.c_int, ctypes.c_ulonglong, ctypes.c_int]
+        lib.amdgpu_canary_detects_corruption.restype = ctypes.c_longlong
         _lib = lib
     return _lib
 
@@ -62,6 +64,11 @@ def run(device: int = 0, hbm_bytes: int = 1 << 30, passes: int = 3, mfma_iters: 
     out["error"] = r.error.decode(errors="replace")
     out["ok"] = bool(r.ok) and rc == 0
     return out
+
+
+def detects_corruption(device: int = 0, hbm_bytes: int = 64 << 20, flips: int = 5) -> int:
+    """Fault-injection check of the HBM verifier; returns the mismatches it found."""
+    return int(load().amdgpu_canary_detects_corruption(int(device), int(hbm_bytes), int(flips)))
 
 
 def mfma_gemm(a_bf16_bits, b_bf16_bits, device: int = 0):

@@ -36,6 +36,8 @@ struct Ctx {
   std::vector<int> gpu_total;   // devices per gpu (all)
   std::vector<int> gpu_avail;   // available devices per gpu
   std::vector<int> gpu_numa;
+  std::vector<uint64_t> adj;       // healthy direct-link adjacency bitmask per GPU
+  std::vector<int> numa_ids;       // distinct NUMA nodes
   int ngpu = 0;
   int parts_per_gpu = 1;
 
@@ -53,6 +55,31 @@ struct Ctx {
       gpu_numa[d[i].gpu] = d[i].numa;
     }
     for (int g = 0; g < ngpu; ++g) parts_per_gpu = std::max(parts_per_gpu, gpu_total[g]);
+    adj.assign(ngpu, 0);
+    for (int a = 0; a < ngpu && a < 64; ++a)
+      for (int b = 0; b < ngpu && b < 64; ++b)
+        if (a != b && a < t.n && b < t.n && t.at(a, b).up &&
+            (t.at(a, b).type == kLinkXgmi || t.at(a, b).type == kLinkPcie))
+          adj[a] |= 1ull << b;
+    for (int g = 0; g < ngpu; ++g)
+      if (std::find(numa_ids.begin(), numa_ids.end(), gpu_numa[g]) == numa_ids.end()) numa_ids.push_back(gpu_numa[g]);
+  }
+
+  // Largest set of GPUs in `mask` that are pairwise connected by healthy links.
+  int max_clique(uint64_t mask) const {
+    int best = 0;
+    // enumerate subsets of mask (callers pass <= 8-16 GPUs of one NUMA node)
+    for (uint64_t sub = mask; sub; sub = (sub - 1) & mask) {
+      const int pc = __builtin_popcountll(sub);
+      if (pc <= best) continue;
+      bool ok = true;
+      for (uint64_t rest = sub; rest && ok; rest &= rest - 1) {
+        const int v = __builtin_ctzll(rest);
+        ok = (sub & ~(adj[v] | (1ull << v))) == 0;
+      }
+      if (ok) best = pc;
+    }
+    return best;
   }
 
   // score of choosing set S (device indices) out of the available pool
@@ -76,15 +103,23 @@ struct Ctx {
       if (busy && gpu_total[g] > 1) s += 6.0 * taken[g];  // pack into partially used GPUs
       if (busy && multi_gpu) s -= 4.0;  // cross-GPU traffic would share this GPU's links
     }
-    // fragmentation of the remainder: concentrate leftovers, keep whole GPUs per NUMA free
-    std::map<int, int> whole_free_per_numa;
+    // fragmentation of the remainder: concentrate leftovers, and keep the largest
+    // healthy-link clique of whole free GPUs per NUMA node (what a future multi-GPU
+    // RCCL job needs) - on a healthy mesh this is just the whole-free count.
     double frag = 0;
+    std::vector<uint64_t> whole_free(numa_ids.size(), 0);
     for (int g = 0; g < ngpu; ++g) {
       const int f = gpu_avail[g] - taken[g];
       frag += static_cast<double>(f) * f / parts_per_gpu;
-      if (gpu_total[g] > 0 && f == gpu_total[g]) whole_free_per_numa[gpu_numa[g]]++;
+      if (gpu_total[g] > 0 && f == gpu_total[g] && g < 64) {
+        const size_t ni = std::find(numa_ids.begin(), numa_ids.end(), gpu_numa[g]) - numa_ids.begin();
+        whole_free[ni] |= 1ull << g;
+      }
     }
-    for (auto& kv : whole_free_per_numa) frag += static_cast<double>(kv.second) * kv.second;
+    for (uint64_t m : whole_free) {
+      const int c = __builtin_popcountll(m) <= 16 ? max_clique(m) : __builtin_popcountll(m);
+      frag += static_cast<double>(c) * c;
+    }
     return s + frag;
   }
 };
@@ -147,7 +182,26 @@ AllocResult aligned_alloc(const Topology& topo, const std::vector<AllocDevice>& 
         best.assign(S.begin() + required.size(), S.end());
       }
     };
-    if (n_choose_k(static_cast<int>(cand.size()), need) <= 20000) {
+    // Partition packing shortcut: if one GPU can hold the whole request (together with
+    // every required device), a single-GPU set dominates - each split pair loses >= 40
+    // pair-score points while the fragmentation/packing terms move by < 40 in total.
+    std::map<int, std::vector<int>> by_gpu;
+    for (int c : cand) by_gpu[devs[c].gpu].push_back(c);
+    int req_gpu = -2;
+    for (int i : required) req_gpu = (req_gpu == -2 || req_gpu == devs[i].gpu) ? devs[i].gpu : -3;
+    bool single_gpu_done = false;
+    if (need >= 1 && req_gpu != -3) {
+      for (auto& kv : by_gpu) {
+        if (static_cast<int>(kv.second.size()) < need || (req_gpu >= 0 && kv.first != req_gpu)) continue;
+        std::vector<int> S(required);
+        S.insert(S.end(), kv.second.begin(), kv.second.begin() + need);
+        consider(S);
+        single_gpu_done = true;
+      }
+    }
+    if (single_gpu_done && ctx.parts_per_gpu > 1) {
+      // best single-GPU placement already chosen
+    } else if (n_choose_k(static_cast<int>(cand.size()), need) <= 4000) {
       // exhaustive, lexicographic order => deterministic tie-break (first best wins)
       std::vector<int> idx(need);
       std::iota(idx.begin(), idx.end(), 0);
@@ -164,15 +218,6 @@ AllocResult aligned_alloc(const Topology& topo, const std::vector<AllocDevice>& 
         for (int j = k + 1; j < need; ++j) idx[j] = idx[j - 1] + 1;
       }
     } else {
-      // seeds: (a) whole request from one GPU (partition packing), (b) greedy growth
-      std::map<int, std::vector<int>> by_gpu;
-      for (int c : cand) by_gpu[devs[c].gpu].push_back(c);
-      for (auto& kv : by_gpu) {
-        if (static_cast<int>(kv.second.size()) < need) continue;
-        std::vector<int> S(required);
-        S.insert(S.end(), kv.second.begin(), kv.second.begin() + need);
-        consider(S);
-      }
       std::vector<int> S(required);
       std::vector<char> used(ndev, 0);
       for (int i : required) used[i] = 1;

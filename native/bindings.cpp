@@ -12,6 +12,7 @@
 #include "hpack.h"
 #include "health.h"
 #include "httpd.h"
+#include "loadgen.h"
 #include "telemetry.h"
 #include "watch.h"
 
@@ -531,4 +532,39 @@ PYBIND11_MODULE(_native, m) {
            })
       .def_property_readonly("table_size", &hpack::Decoder::table_size)
       .def_property_readonly("table_entries", &hpack::Decoder::table_entries);
+
+  // ---- load generators (bench / BASELINE protocol) ----
+  auto load_dict = [](const LoadResult& r) {
+    py::dict d;
+    d["ok"] = r.ok;
+    d["errors"] = r.errors;
+    d["bytes"] = r.bytes;
+    d["elapsed_s"] = r.elapsed_s;
+    d["latencies_s"] = r.latencies_s;
+    return d;
+  };
+  m.def("http_load",
+        [load_dict](const std::string& host, int port, const std::string& path, int conns, double duration_s,
+                    double target_rps) {
+          LoadResult r;
+          {
+            py::gil_scoped_release rel;
+            r = http_load(host, port, path, conns, duration_s, target_rps);
+          }
+          return load_dict(r);
+        },
+        py::arg("host"), py::arg("port"), py::arg("path") = "/metrics", py::arg("conns") = 4,
+        py::arg("duration_s") = 2.0, py::arg("target_rps") = 0.0);
+  m.def("grpc_load",
+        [load_dict](const std::string& sock, const std::string& method, const py::bytes& req, int conns,
+                    double duration_s) {
+          std::string rq(req);
+          LoadResult r;
+          {
+            py::gil_scoped_release rel;
+            r = grpc_load(sock, method, rq, conns, duration_s);
+          }
+          return load_dict(r);
+        },
+        py::arg("socket_path"), py::arg("method"), py::arg("req"), py::arg("conns") = 4, py::arg("duration_s") = 2.0);
 }

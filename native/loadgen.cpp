@@ -1,0 +1,172 @@
+#include "loadgen.h"
+
+#include <arpa/inet.h>
+#include <errno.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <thread>
+
+#include "backend.h"
+#include "grpc_h2.h"
+
+namespace amdgpu_dp {
+
+namespace {
+
+int tcp_connect(const std::string& host, int port) {
+  struct addrinfo hints {};
+  hints.ai_family = AF_UNSPEC;
+  hints.ai_socktype = SOCK_STREAM;
+  struct addrinfo* res = nullptr;
+  if (getaddrinfo(host.c_str(), std::to_string(port).c_str(), &hints, &res) != 0) return -1;
+  int fd = -1;
+  for (auto* ai = res; ai; ai = ai->ai_next) {
+    fd = socket(ai->ai_family, ai->ai_socktype | SOCK_CLOEXEC, ai->ai_protocol);
+    if (fd < 0) continue;
+    if (connect(fd, ai->ai_addr, ai->ai_addrlen) == 0) break;
+    close(fd);
+    fd = -1;
+  }
+  freeaddrinfo(res);
+  if (fd >= 0) {
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  }
+  return fd;
+}
+
+// Reads one HTTP/1.1 response (Content-Length framed) from fd; `buf` keeps leftovers.
+bool read_response(int fd, std::string* buf, size_t* body_len, int* status) {
+  char tmp[65536];
+  for (;;) {
+    const size_t he = buf->find("\r\n\r\n");
+    if (he != std::string::npos) {
+      *status = std::atoi(buf->c_str() + 9);
+      size_t cl = 0;
+      const size_t p = buf->find("Content-Length:");
+      if (p != std::string::npos && p < he) cl = std::strtoull(buf->c_str() + p + 15, nullptr, 10);
+      if (buf->size() >= he + 4 + cl) {
+        *body_len = cl;
+        buf->erase(0, he + 4 + cl);
+        return true;
+      }
+    }
+    const ssize_t r = recv(fd, tmp, sizeof(tmp), 0);
+    if (r <= 0) {
+      if (r < 0 && errno == EINTR) continue;
+      return false;
+    }
+    buf->append(tmp, static_cast<size_t>(r));
+  }
+}
+
+}  // namespace
+
+LoadResult http_load(const std::string& host, int port, const std::string& path, int conns, double duration_s,
+                     double target_rps) {
+  LoadResult total;
+  std::mutex mu;
+  std::vector<std::thread> ts;
+  const int64_t t0 = mono_ns() + 2000000;  // common start 2 ms out
+  const int64_t t_end = t0 + static_cast<int64_t>(duration_s * 1e9);
+  const std::string req = "GET " + path + " HTTP/1.1\r\nHost: " + host + "\r\nUser-Agent: amdgpu-dp-loadgen\r\n\r\n";
+  for (int c = 0; c < conns; ++c) {
+    ts.emplace_back([&, c] {
+      LoadResult r;
+      int fd = tcp_connect(host, port);
+      std::string buf;
+      // open loop: this connection's requests are scheduled every conns/target_rps seconds
+      const double interval_ns = target_rps > 0 ? 1e9 * conns / target_rps : 0;
+      int64_t next = t0 + static_cast<int64_t>(interval_ns * c / std::max(1, conns));
+      while (mono_ns() < t0) {
+      }
+      for (;;) {
+        int64_t sched = mono_ns();
+        if (interval_ns > 0) {
+          while (mono_ns() < next) std::this_thread::sleep_for(std::chrono::microseconds(20));
+          sched = next;
+          next += static_cast<int64_t>(interval_ns);
+        }
+        if (sched >= t_end) break;
+        if (fd < 0) fd = tcp_connect(host, port);
+        size_t body = 0;
+        int status = 0;
+        bool ok = fd >= 0 && send(fd, req.data(), req.size(), MSG_NOSIGNAL) == static_cast<ssize_t>(req.size()) &&
+                  read_response(fd, &buf, &body, &status) && status == 200;
+        const int64_t done = mono_ns();
+        if (ok) {
+          ++r.ok;
+          r.bytes += body;
+          r.latencies_s.push_back((done - sched) * 1e-9);
+        } else {
+          ++r.errors;
+          if (fd >= 0) close(fd);
+          fd = -1;
+          buf.clear();
+        }
+      }
+      if (fd >= 0) close(fd);
+      std::lock_guard<std::mutex> lk(mu);
+      total.ok += r.ok;
+      total.errors += r.errors;
+      total.bytes += r.bytes;
+      total.latencies_s.insert(total.latencies_s.end(), r.latencies_s.begin(), r.latencies_s.end());
+    });
+  }
+  for (auto& t : ts) t.join();
+  total.elapsed_s = duration_s;  // every connection issues requests over [t0, t_end)
+  return total;
+}
+
+LoadResult grpc_load(const std::string& socket_path, const std::string& method, const std::string& req, int conns,
+                     double duration_s) {
+  LoadResult total;
+  std::mutex mu;
+  std::vector<std::thread> ts;
+  const int64_t t0 = mono_ns() + 2000000;
+  const int64_t t_end = t0 + static_cast<int64_t>(duration_s * 1e9);
+  for (int c = 0; c < conns; ++c) {
+    ts.emplace_back([&] {
+      LoadResult r;
+      try {
+        H2Client cl(socket_path);
+        std::string resp, msg;
+        while (mono_ns() < t0) {
+        }
+        for (;;) {
+          const int64_t s = mono_ns();
+          if (s >= t_end) break;
+          const int st = cl.unary(method, req, &resp, &msg);
+          const int64_t e = mono_ns();
+          if (st == 0) {
+            ++r.ok;
+            r.bytes += resp.size();
+            r.latencies_s.push_back((e - s) * 1e-9);
+          } else {
+            ++r.errors;
+          }
+        }
+      } catch (const std::exception&) {
+        ++r.errors;
+      }
+      std::lock_guard<std::mutex> lk(mu);
+      total.ok += r.ok;
+      total.errors += r.errors;
+      total.bytes += r.bytes;
+      total.latencies_s.insert(total.latencies_s.end(), r.latencies_s.begin(), r.latencies_s.end());
+    });
+  }
+  for (auto& t : ts) t.join();
+  total.elapsed_s = duration_s;
+  return total;
+}
+
+}  // namespace amdgpu_dp

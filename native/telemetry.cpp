@@ -411,19 +411,33 @@ void Exporter::render(std::string* out) const {
     sample_hist_.render(out, "amdgpu_telemetry_sample_duration_seconds", "");
   }
   if (!tables.empty()) {
-    append_header(out, "amdgpu_device_plugin_device_health",
-                  "1 if the advertised device is Healthy, 0 if Unhealthy.", "gauge");
-    std::string l;
+    std::vector<uint64_t> key;
+    key.reserve(tables.size() * 2);
     for (const auto& t : tables) {
-      for (size_t i = 0; i < t->size(); ++i) {
-        const TableDevice& d = t->device(i);
-        l.assign("resource=\"");
-        append_label_value(&l, t->config().resource_name);
-        l.append("\",device_id=\"");
-        append_label_value(&l, d.id);
-        l.append("\"");
-        line(out, "amdgpu_device_plugin_device_health", l, t->healthy(d.id) ? 1 : 0);
+      key.push_back(reinterpret_cast<uintptr_t>(t.get()));
+      key.push_back(t->version());
+    }
+    {
+      std::lock_guard<std::mutex> hk(health_mu_);
+      if (key != health_key_) {
+        health_cache_.clear();
+        append_header(&health_cache_, "amdgpu_device_plugin_device_health",
+                      "1 if the advertised device is Healthy, 0 if Unhealthy.", "gauge");
+        std::string l;
+        for (const auto& t : tables) {
+          for (size_t i = 0; i < t->size(); ++i) {
+            const TableDevice& d = t->device(i);
+            l.assign("resource=\"");
+            append_label_value(&l, t->config().resource_name);
+            l.append("\",device_id=\"");
+            append_label_value(&l, d.id);
+            l.append("\"");
+            line(&health_cache_, "amdgpu_device_plugin_device_health", l, t->healthy(d.id) ? 1 : 0);
+          }
+        }
+        health_key_ = key;
       }
+      out->append(health_cache_);
     }
     bool any = false;
     for (const auto& t : tables) {

@@ -78,6 +78,10 @@ class Exporter {
   std::atomic<uint64_t> sample_errors_{0};
   Histogram sample_hist_;
   int64_t start_time_s_ = 0;
+  // device-health block, re-rendered only when a table's version changes
+  mutable std::mutex health_mu_;
+  mutable std::vector<uint64_t> health_key_;
+  mutable std::string health_cache_;
   mutable std::mutex proc_mu_;
   mutable std::string proc_cache_;
   mutable int64_t proc_cache_ns_ = 0;

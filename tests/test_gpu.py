@@ -87,6 +87,12 @@ def test_mfma_gemm_matches_torch_fp32(shape):
     assert err < 1e-5, err  # same bf16 inputs, fp32 accumulate: only summation-order rounding
 
 
+def test_canary_verifier_catches_injected_corruption():
+    from k8s_gpu_device_plugin_amd.ops import canary
+    assert canary.detects_corruption(0, 64 << 20, 0) == 0
+    assert canary.detects_corruption(0, 64 << 20, 7) == 7
+
+
 def test_canary_isolated_subprocess():
     from k8s_gpu_device_plugin_amd.ops import canary
     r = canary.run_isolated(0, 128 << 20)
