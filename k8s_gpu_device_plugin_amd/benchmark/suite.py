@@ -131,6 +131,7 @@ def config2():
     try:
         ids = node.ids()
         g = node.mgr.gpus[0]
+        time.sleep(2.5)  # a few 1 s sampling ticks of real amdsmi telemetry
         text = node.mgr.exporter.render()
         sample = [ln for ln in text.splitlines() if ln.startswith("amdgpu_telemetry_sample_duration_seconds_")]
         sums = {ln.split()[0]: float(ln.split()[1]) for ln in sample if "_sum" in ln or "_count" in ln}

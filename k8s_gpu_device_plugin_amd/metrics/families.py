@@ -1,0 +1,88 @@
+"""The /metrics contract: every metric family the plugin exposes.
+
+The reference's ``metrics`` package is empty (``metrics/metrics.go:1``); its /metrics
+carries only the Go runtime/process collectors, ``go_build_info`` (``main.go:26-28``)
+and the echo HTTP families (``middleware/echo_metric.go:80-93``).  This registry is the
+single place that documents the MI355X plugin's families; ``tests/test_metrics_contract``
+checks the native exporter against it in both directions.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+
+@dataclass(frozen=True)
+class Family:
+    name: str
+    type: str
+    labels: tuple
+    source: str
+    help: str
+
+
+GPU = ("gpu",)
+PART = ("gpu", "partition", "device_id", "resource")
+
+FAMILIES = (
+    # --- reference-compatible ---
+    Family("echo_http_requests_total", "counter", ("handler", "method", "status"), "httpd",
+           "Number of HTTP operations (reference middleware/echo_metric.go)"),
+    Family("echo_http_request_duration_seconds", "histogram", ("handler", "method"), "httpd",
+           "Spend time by processing a route; buckets .0005..30 s as the reference"),
+    Family("k8s_gpu_device_plugin_build_info", "gauge", ("app", "version", "python", "native"), "manager",
+           "Build information (the go_build_info analogue)"),
+    Family("process_cpu_seconds_total", "counter", (), "exporter", "Process CPU time"),
+    Family("process_resident_memory_bytes", "gauge", (), "exporter", "Resident memory"),
+    Family("process_virtual_memory_bytes", "gauge", (), "exporter", "Virtual memory"),
+    Family("process_open_fds", "gauge", (), "exporter", "Open file descriptors"),
+    Family("process_max_fds", "gauge", (), "exporter", "File descriptor limit"),
+    Family("process_start_time_seconds", "gauge", (), "exporter", "Process start time"),
+    # --- per-GPU amdsmi telemetry ---
+    Family("amdgpu_info", "gauge", GPU + ("uuid", "bdf", "name", "gfx_target", "compute_partition",
+                                          "memory_partition", "numa_node"), "exporter", "Static inventory (value 1)"),
+    Family("amdgpu_telemetry_up", "gauge", GPU, "exporter", "Last sample succeeded"),
+    Family("amdgpu_power_watts", "gauge", GPU, "exporter", "Socket power"),
+    Family("amdgpu_energy_joules_total", "counter", GPU, "exporter", "Accumulated energy"),
+    Family("amdgpu_gfx_activity_percent", "gauge", GPU, "exporter", "Compute engine activity"),
+    Family("amdgpu_umc_activity_percent", "gauge", GPU, "exporter", "HBM controller activity"),
+    Family("amdgpu_vram_used_bytes", "gauge", GPU, "exporter", "VRAM used"),
+    Family("amdgpu_vram_total_bytes", "gauge", GPU, "exporter", "VRAM capacity"),
+    Family("amdgpu_throttle_status", "gauge", GPU, "exporter", "Throttle status bitmask"),
+    Family("amdgpu_temperature_celsius", "gauge", GPU + ("sensor",), "exporter",
+           "Temperature by sensor: edge, hotspot, mem, hbm0..N"),
+    Family("amdgpu_clock_mhz", "gauge", GPU + ("clock",), "exporter", "gfx / mem clocks"),
+    Family("amdgpu_ecc_errors_total", "counter", GPU + ("type",), "exporter", "ECC (un)correctable counts"),
+    Family("amdgpu_xgmi_link_up", "gauge", GPU + ("link", "peer"), "exporter", "xGMI link to peer is up"),
+    Family("amdgpu_xgmi_read_bytes_total", "counter", GPU + ("link", "peer"), "exporter", "xGMI bytes received"),
+    Family("amdgpu_xgmi_write_bytes_total", "counter", GPU + ("link", "peer"), "exporter", "xGMI bytes sent"),
+    # --- per-partition ---
+    Family("amdgpu_partition_info", "gauge", PART, "exporter", "Partition -> device id / resource (value 1)"),
+    Family("amdgpu_partition_gfx_busy_percent", "gauge", PART, "exporter", "Per-XCP compute busy"),
+    Family("amdgpu_partition_vram_used_bytes", "gauge", PART, "exporter", "Per-partition VRAM used"),
+    # --- sampler / plugin ---
+    Family("amdgpu_telemetry_samples_total", "counter", (), "exporter", "Sampling passes"),
+    Family("amdgpu_telemetry_sample_errors_total", "counter", (), "exporter", "Per-GPU sample failures"),
+    Family("amdgpu_telemetry_sample_duration_seconds", "histogram", (), "exporter", "One sampling pass"),
+    Family("amdgpu_device_plugin_device_health", "gauge", ("resource", "device_id"), "exporter",
+           "1 Healthy / 0 Unhealthy per advertised device"),
+    Family("amdgpu_device_plugin_rpc_duration_seconds", "histogram", ("resource", "rpc"), "device_table",
+           "kubelet RPC latency (5 us .. 1 s buckets)"),
+    Family("amdgpu_device_plugin_events_total", "counter", ("event",), "manager",
+           "Lifecycle events: restarts (api/kubelet/retry), registrations, load failures, health events"),
+    Family("amdgpu_device_plugin_devices", "gauge", ("resource", "health"), "manager",
+           "Advertised devices per resource and health"),
+    Family("amdgpu_device_plugin_registered", "gauge", ("resource",), "manager",
+           "Resource registered with kubelet"),
+)
+
+BY_NAME = {f.name: f for f in FAMILIES}
+
+
+def family_of(sample_name: str) -> Family | None:
+    """Maps a sample name (``x_bucket``/``x_sum``/``x_count``/``x``) to its family."""
+    if sample_name in BY_NAME:
+        return BY_NAME[sample_name]
+    for suffix in ("_bucket", "_sum", "_count"):
+        if sample_name.endswith(suffix) and sample_name[: -len(suffix)] in BY_NAME:
+            return BY_NAME[sample_name[: -len(suffix)]]
+    return None

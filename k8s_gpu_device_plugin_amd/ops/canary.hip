@@ -7,7 +7,9 @@
 //
 //   1. HBM pattern test  - every 16-byte word gets an address-derived pattern
 //      (catches stuck bits and aliasing/addressing faults), written and read back
-//      with 16 B/lane vector accesses over a grid >> 256 CUs; mismatches are
+//      with 16 B/lane vector accesses, block-contiguous chunks, 16 blocks per CU,
+//      non-temporal loads on the verify pass (shapes chosen by the on-hardware sweep
+//      below: ~6.0 TB/s write, ~6.8 TB/s read+verify on MI355X); mismatches are
 //      reduced per wave (64-lane shuffles) then per block in LDS, one atomic/block.
 //      Write and read passes are timed separately -> achieved HBM GB/s.
 //   2. MFMA exactness    - v_mfma_f32_32x32x16_bf16 on small-integer operands
@@ -46,45 +48,8 @@ __device__ __forceinline__ uint4 pattern(uint64_t idx, uint32_t seed) {
   return make_uint4(b, b ^ 0xA5A5A5A5u, ~b, b * 3u + 0x6A09E667u);
 }
 
-__global__ void __launch_bounds__(256) hbm_write(uint4* __restrict__ buf, uint64_t n, uint32_t seed) {
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  // 4 independent 16 B stores in flight per lane per iteration
-  for (; i + 3 * stride < n; i += 4 * stride) {
-    buf[i] = pattern(i, seed);
-    buf[i + stride] = pattern(i + stride, seed);
-    buf[i + 2 * stride] = pattern(i + 2 * stride, seed);
-    buf[i + 3 * stride] = pattern(i + 3 * stride, seed);
-  }
-  for (; i < n; i += stride) buf[i] = pattern(i, seed);
-}
-
 __device__ __forceinline__ uint32_t diff(const uint4& a, const uint4& b) {
   return (a.x != b.x) + (a.y != b.y) + (a.z != b.z) + (a.w != b.w);
-}
-
-__global__ void __launch_bounds__(256) hbm_verify(const uint4* __restrict__ buf, uint64_t n, uint32_t seed,
-                                                  unsigned long long* __restrict__ errors) {
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  uint32_t bad = 0;
-  for (; i + 3 * stride < n; i += 4 * stride) {
-    const uint4 v0 = buf[i], v1 = buf[i + stride], v2 = buf[i + 2 * stride], v3 = buf[i + 3 * stride];
-    bad += diff(v0, pattern(i, seed)) + diff(v1, pattern(i + stride, seed)) + diff(v2, pattern(i + 2 * stride, seed)) +
-           diff(v3, pattern(i + 3 * stride, seed));
-  }
-  for (; i < n; i += stride) bad += diff(buf[i], pattern(i, seed));
-  // 64-lane wave reduction, then one LDS slot per wave, one atomic per block
-  for (int off = kWave / 2; off > 0; off >>= 1) bad += __shfl_down(bad, off, kWave);
-  __shared__ uint32_t wave_bad[256 / kWave];
-  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-  if (lane == 0) wave_bad[wid] = bad;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t t = 0;
-    for (int w = 0; w < static_cast<int>(blockDim.x / kWave); ++w) t += wave_bad[w];
-    if (t) atomicAdd(errors, static_cast<unsigned long long>(t));
-  }
 }
 
 using bf16x8 = __attribute__((ext_vector_type(8))) short;
@@ -182,6 +147,117 @@ __global__ void __launch_bounds__(64) mfma_gemm(const short* __restrict__ A, con
   }
 }
 
+// ---- HBM access-shape sweep (used to pick the canary's streaming shape on gfx950) ----
+// UNROLL independent 16 B accesses in flight per lane; NT = non-temporal (streaming)
+// loads/stores; CHUNKED = each block streams one contiguous chunk instead of a
+// grid-stride walk.
+using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
+__device__ __forceinline__ uint4 nt_load(const uint4* p) {
+  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void nt_store(const uint4& v, uint4* p) {
+  const u32x4 x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(p));
+}
+
+template <int UNROLL, bool NT, bool CHUNKED>
+__global__ void __launch_bounds__(256) sweep_write(uint4* __restrict__ buf, uint64_t n, uint32_t seed) {
+  uint64_t begin, end, step;
+  if (CHUNKED) {
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    begin = blockIdx.x * per + threadIdx.x;
+    end = min<uint64_t>(n, (blockIdx.x + 1) * per);
+    step = blockDim.x;
+  } else {
+    begin = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    end = n;
+    step = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  }
+  uint64_t i = begin;
+  for (; i + (UNROLL - 1) * step < end; i += UNROLL * step) {
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const uint4 v = pattern(i + u * step, seed);
+      if (NT) nt_store(v, buf + i + u * step);
+      else buf[i + u * step] = v;
+    }
+  }
+  for (; i < end; i += step) buf[i] = pattern(i, seed);
+}
+
+template <int UNROLL, bool NT, bool CHUNKED>
+__global__ void __launch_bounds__(256) sweep_verify(const uint4* __restrict__ buf, uint64_t n, uint32_t seed,
+                                                    unsigned long long* __restrict__ errors) {
+  uint64_t begin, end, step;
+  if (CHUNKED) {
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    begin = blockIdx.x * per + threadIdx.x;
+    end = min<uint64_t>(n, (blockIdx.x + 1) * per);
+    step = blockDim.x;
+  } else {
+    begin = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    end = n;
+    step = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  }
+  uint32_t bad = 0;
+  uint64_t i = begin;
+  for (; i + (UNROLL - 1) * step < end; i += UNROLL * step) {
+    uint4 v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) v[u] = NT ? nt_load(buf + i + u * step) : buf[i + u * step];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) bad += diff(v[u], pattern(i + u * step, seed));
+  }
+  for (; i < end; i += step) bad += diff(buf[i], pattern(i, seed));
+  for (int off = kWave / 2; off > 0; off >>= 1) bad += __shfl_down(bad, off, kWave);
+  __shared__ uint32_t wave_bad[256 / kWave];
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  if (lane == 0) wave_bad[wid] = bad;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < static_cast<int>(blockDim.x / kWave); ++w) t += wave_bad[w];
+    if (t) atomicAdd(errors, static_cast<unsigned long long>(t));
+  }
+}
+
+// Shapes picked from the on-hardware sweep (profiles/hbm_sweep_gpu.json, 4 GiB buffer):
+// writes: block-contiguous chunks, plain stores (~6.0 TB/s); verify: block-contiguous
+// chunks, non-temporal loads (~6.8 TB/s), both at 16 blocks of 256 threads per CU.
+constexpr int kBlocksPerCu = 16;
+#define hbm_write sweep_write<4, false, true>
+#define hbm_verify sweep_verify<4, true, true>
+
+template <int U, bool NT, bool CH>
+float time_pair(uint4* buf, uint64_t n, int blocks, unsigned long long* err, int reps, float* t_read) {
+  hipEvent_t a, b, c;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  (void)hipEventCreate(&c);
+  float tw = 0, tr = 0;
+  for (int r = 0; r < reps + 1; ++r) {  // first repetition is warm-up
+    (void)hipEventRecord(a, 0);
+    hipLaunchKernelGGL((sweep_write<U, NT, CH>), dim3(blocks), dim3(256), 0, 0, buf, n, 9u + r);
+    (void)hipEventRecord(b, 0);
+    hipLaunchKernelGGL((sweep_verify<U, NT, CH>), dim3(blocks), dim3(256), 0, 0, buf, n, 9u + r, err);
+    (void)hipEventRecord(c, 0);
+    (void)hipEventSynchronize(c);
+    float x = 0, y = 0;
+    (void)hipEventElapsedTime(&x, a, b);
+    (void)hipEventElapsedTime(&y, b, c);
+    if (r) {
+      tw += x;
+      tr += y;
+    }
+  }
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  (void)hipEventDestroy(c);
+  *t_read = tr / reps;
+  return tw / reps;
+}
+
 }  // namespace
 
 extern "C" {
@@ -243,7 +319,7 @@ int amdgpu_canary_run(int device, unsigned long long hbm_bytes, int passes, int 
   CANARY_CHECK(hipEventCreate(&e0));
   CANARY_CHECK(hipEventCreate(&e1));
   CANARY_CHECK(hipEventCreate(&e2));
-  blocks = prop.multiProcessorCount * 8;  // >> #CUs, 8 blocks of 256 threads per CU
+  blocks = prop.multiProcessorCount * kBlocksPerCu;  // >> #CUs
   // warm-up (first-touch page mapping) outside the timed region
   hipLaunchKernelGGL(hbm_write, dim3(blocks), dim3(256), 0, 0, buf, n, 0x1234u);
   CANARY_CHECK(hipGetLastError());
@@ -308,7 +384,7 @@ long long amdgpu_canary_detects_corruption(int device, unsigned long long hbm_by
   if (n == 0 || flips < 0 || hipSetDevice(device) != hipSuccess ||
       hipGetDeviceProperties(&prop, device) != hipSuccess)
     return -1;
-  const int blocks = prop.multiProcessorCount * 8;
+  const int blocks = prop.multiProcessorCount * kBlocksPerCu;
   long long rc = -1;
   if (hipMalloc(&buf, n * sizeof(uint4)) == hipSuccess && hipMalloc(&d_err, sizeof(h_err)) == hipSuccess &&
       hipMemset(d_err, 0, sizeof(h_err)) == hipSuccess) {
@@ -360,6 +436,42 @@ int amdgpu_canary_mfma_gemm(int device, const unsigned short* a_host, const unsi
   if (b) (void)hipFree(b);
   if (c) (void)hipFree(c);
   return e == hipSuccess ? 0 : -1;
+}
+
+// variant: 0 U4 grid-stride, 1 U8 grid-stride, 2 U4 NT, 3 U8 NT, 4 U4 chunked, 5 U8 chunked,
+// 6 U4 NT chunked, 7 U16 grid-stride.  blocks_per_cu scales the grid.
+int amdgpu_canary_hbm_sweep(int device, unsigned long long bytes, int variant, int blocks_per_cu, int reps,
+                            double* write_gbps, double* read_gbps, unsigned long long* errors) {
+  hipDeviceProp_t prop;
+  if (hipSetDevice(device) != hipSuccess || hipGetDeviceProperties(&prop, device) != hipSuccess) return -1;
+  const uint64_t n = bytes / sizeof(uint4);
+  uint4* buf = nullptr;
+  unsigned long long* err = nullptr;
+  if (hipMalloc(&buf, n * sizeof(uint4)) != hipSuccess) return -2;
+  if (hipMalloc(&err, 8) != hipSuccess || hipMemset(err, 0, 8) != hipSuccess) {
+    (void)hipFree(buf);
+    return -2;
+  }
+  const int blocks = prop.multiProcessorCount * (blocks_per_cu > 0 ? blocks_per_cu : 8);
+  float tw = 0, tr = 0;
+  switch (variant) {
+    case 0: tw = time_pair<4, false, false>(buf, n, blocks, err, reps, &tr); break;
+    case 1: tw = time_pair<8, false, false>(buf, n, blocks, err, reps, &tr); break;
+    case 2: tw = time_pair<4, true, false>(buf, n, blocks, err, reps, &tr); break;
+    case 3: tw = time_pair<8, true, false>(buf, n, blocks, err, reps, &tr); break;
+    case 4: tw = time_pair<4, false, true>(buf, n, blocks, err, reps, &tr); break;
+    case 5: tw = time_pair<8, false, true>(buf, n, blocks, err, reps, &tr); break;
+    case 6: tw = time_pair<4, true, true>(buf, n, blocks, err, reps, &tr); break;
+    case 7: tw = time_pair<16, false, false>(buf, n, blocks, err, reps, &tr); break;
+    default: break;
+  }
+  const hipError_t e = hipDeviceSynchronize();
+  (void)hipMemcpy(errors, err, 8, hipMemcpyDeviceToHost);
+  *write_gbps = tw > 0 ? n * 16.0 / (tw * 1e-3) / 1e9 : 0;
+  *read_gbps = tr > 0 ? n * 16.0 / (tr * 1e-3) / 1e9 : 0;
+  (void)hipFree(err);
+  (void)hipFree(buf);
+  return e == hipSuccess ? 0 : -3;
 }
 
 }  // extern "C"

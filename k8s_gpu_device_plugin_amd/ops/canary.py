@@ -48,6 +48,10 @@ def load():
         lib.amdgpu_canary_mfma_gemm.restype = ctypes.c_int
         lib.amdgpu_canary_detects_corruption.argtypes = [ctypes.c_int, ctypes.c_ulonglong, ctypes.c_int]
         lib.amdgpu_canary_detects_corruption.restype = ctypes.c_longlong
+        lib.amdgpu_canary_hbm_sweep.argtypes = [ctypes.c_int, ctypes.c_ulonglong, ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                                ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_ulonglong)]
+        lib.amdgpu_canary_hbm_sweep.restype = ctypes.c_int
         _lib = lib
     return _lib
 
@@ -69,6 +73,24 @@ def run(device: int = 0, hbm_bytes: int = 1 << 30, passes: int = 3, mfma_iters: 
 def detects_corruption(device: int = 0, hbm_bytes: int = 64 << 20, flips: int = 5) -> int:
     """Fault-injection check of the HBM verifier; returns the mismatches it found."""
     return int(load().amdgpu_canary_detects_corruption(int(device), int(hbm_bytes), int(flips)))
+
+
+SWEEP_VARIANTS = {0: "u4 grid-stride", 1: "u8 grid-stride", 2: "u4 nontemporal", 3: "u8 nontemporal",
+                  4: "u4 chunked", 5: "u8 chunked", 6: "u4 nt chunked", 7: "u16 grid-stride"}
+
+
+def hbm_sweep(device: int = 0, nbytes: int = 4 << 30, variants=tuple(SWEEP_VARIANTS), blocks_per_cu=(4, 8, 16),
+              reps: int = 5) -> list:
+    """Times write+verify for each access shape; returns rows of GB/s (HBM-resident buffer)."""
+    rows = []
+    for v in variants:
+        for b in blocks_per_cu:
+            w, r, e = ctypes.c_double(), ctypes.c_double(), ctypes.c_ulonglong()
+            rc = load().amdgpu_canary_hbm_sweep(device, nbytes, v, b, reps, ctypes.byref(w), ctypes.byref(r),
+                                                ctypes.byref(e))
+            rows.append({"variant": SWEEP_VARIANTS[v], "blocks_per_cu": b, "write_gbps": round(w.value, 1),
+                         "read_verify_gbps": round(r.value, 1), "errors": e.value, "rc": rc})
+    return rows
 
 
 def mfma_gemm(a_bf16_bits, b_bf16_bits, device: int = 0):

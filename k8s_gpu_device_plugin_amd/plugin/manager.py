@@ -276,7 +276,6 @@ class PluginManager:
         if self.cfg.health.enabled:
             self.monitor.start()
         if self.cfg.telemetry.enabled:
-            self.exporter.sample_once()
             self.exporter.start(self.backend, self.cfg.telemetry.intervalMs,
                                 self.monitor if self.cfg.health.enabled else None)
         self._publish_metrics()

@@ -2,6 +2,7 @@
 
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -54,6 +55,7 @@ void Exporter::start(std::shared_ptr<Backend> backend, int interval_ms, std::sha
   interval_ms_ = interval_ms > 0 ? interval_ms : 1000;
   stop_ = false;
   running_ = true;
+  sample_once();  // first sample synchronously: /metrics is populated before start() returns
   thread_ = std::thread([this] { loop(); });
 }
 
@@ -65,16 +67,17 @@ void Exporter::stop() {
 }
 
 void Exporter::loop() {
+  int64_t next = mono_ns() + static_cast<int64_t>(interval_ms_) * 1000000;
   while (!stop_.load()) {
-    const int64_t t0 = mono_ns();
-    sample_once();
-    const int64_t spent_ms = (mono_ns() - t0) / 1000000;
-    int64_t left = interval_ms_ - spent_ms;
-    while (left > 0 && !stop_.load()) {  // sleep in slices so stop() is prompt
-      const int64_t slice = left < 50 ? left : 50;
-      std::this_thread::sleep_for(std::chrono::milliseconds(slice));
-      left -= slice;
+    const int64_t now = mono_ns();
+    if (now < next) {  // sleep in slices so stop() is prompt
+      const int64_t slice_ms = std::min<int64_t>(50, (next - now) / 1000000 + 1);
+      std::this_thread::sleep_for(std::chrono::milliseconds(slice_ms));
+      continue;
     }
+    sample_once();
+    next += static_cast<int64_t>(interval_ms_) * 1000000;  // fixed cadence, no drift
+    if (next < mono_ns()) next = mono_ns() + static_cast<int64_t>(interval_ms_) * 1000000;
   }
 }
 
