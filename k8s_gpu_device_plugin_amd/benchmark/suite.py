@@ -257,12 +257,36 @@ def scaling():
     return {"config": "scaling curve (fixture nodes, strategy none)", "rows": rows}
 
 
-RUNNERS = {"1": config1, "2": config2, "3": config3, "4": config4, "5": config5, "scaling": scaling}
+def health_propagation(events=60):
+    """Hardware event -> Unhealthy/Healthy visible to a kubelet ListAndWatch stream."""
+    nat = native.load()
+    node = Node("fixture", "8gpu_spx_mesh")
+    try:
+        w = node.kubelet.watch(node.regs[0].endpoint)
+        w.next(10)
+        for kind in (nat.EVT_PRE_RESET, nat.EVT_POST_RESET):  # warm-up pair (first-use costs)
+            node.mgr.backend.inject_event(nat.HwEvent(kind, 3, message="warm-up"))
+            w.next(10)
+        lat = []
+        for i in range(events):
+            kind = nat.EVT_PRE_RESET if i % 2 == 0 else nat.EVT_POST_RESET
+            t0 = time.monotonic()
+            node.mgr.backend.inject_event(nat.HwEvent(kind, 3, message="suite"))
+            t1, devs = w.next(10)
+            lat.append(t1 - t0)
+            assert devs[3][1] == ("Unhealthy" if i % 2 == 0 else "Healthy")
+        return {"config": "health event -> ListAndWatch update (fixture PRE/POST_RESET on GPU 3)",
+                "events": events, "p50_us": us(pct(lat, 0.5)), "p99_us": us(pct(lat, 0.99))}
+    finally:
+        node.close()
+
+
+RUNNERS = {"health": health_propagation, "1": config1, "2": config2, "3": config3, "4": config4, "5": config5, "scaling": scaling}
 
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
-    ap.add_argument("--configs", default="1,2,3,4,5,scaling")
+    ap.add_argument("--configs", default="1,2,3,4,5,scaling,health")
     ap.add_argument("--json", default="")
     a = ap.parse_args(argv)
     from ..utils.log import init_logger

@@ -56,8 +56,10 @@ class TelemetryConfig:
 class HealthConfig:
     enabled: bool = True
     lostAfterFailures: int = 3
-    canary: bool = False          # run the HIP canary before advertising / after reset
+    canary: bool = False          # gfx950 canary before re-advertising a GPU after a reset
+    canaryOnStart: bool = False   # ... and on every partition before the first advertisement
     canaryBytes: int = 256 << 20
+    canaryTimeoutS: float = 120.0
     rejectUnhealthyAllocate: bool = True
 
 

@@ -158,12 +158,15 @@ class PluginManager:
         resources = new_resources(gpus, self.cfg.strategy, self.cfg.resourcePrefix, self.cfg.resources)
         self.device_map = build_device_map(gpus, resources, self.cfg.strategy, self.cfg.mountCardNodes,
                                            self.cfg.sharing.replicas, self.cfg.sharing.renameByDefault)
+        failed = self._startup_canary(gpus) if self.cfg.health.canaryOnStart else set()
         plugins = [AmdDevicePlugin(name, devs, topo, self.cfg) for name, devs in self.device_map.items()]
         # health state survives a reload: re-apply what the monitor currently reports
         for p in plugins:
             for g in gpus:
                 if self.monitor.running and not self.monitor.gpu_healthy(g.index):
                     p.set_gpu_health(g.index, -1, False)
+            for gpu, part in failed:
+                p.set_gpu_health(gpu, part, False)
         self.plugins = plugins
         n = native.load()
         labels = []
@@ -230,13 +233,35 @@ class PluginManager:
         else:
             log.info("GPU event on %d: %s", u.gpu, u.reason)
 
+    def _startup_canary(self, gpus) -> set:
+        """Runs the gfx950 canary on every partition (one child process per partition, all
+        GPUs in parallel) before the first advertisement; returns failing (gpu, partition)."""
+        import concurrent.futures
+
+        from ..ops import canary
+        jobs = [(g.index, p.index if len(g.partitions) > 1 else -1, p.hip_id) for g in gpus for p in g.partitions]
+        failed = set()
+        with concurrent.futures.ThreadPoolExecutor(max_workers=max(1, min(8, len(jobs)))) as ex:
+            futs = {ex.submit(canary.run_isolated, max(0, hip), self.cfg.health.canaryBytes,
+                              self.cfg.health.canaryTimeoutS): (gpu, part) for gpu, part, hip in jobs}
+            for f in concurrent.futures.as_completed(futs):
+                gpu, part = futs[f]
+                res = f.result()
+                self.counters["canary_runs"] = self.counters.get("canary_runs", 0) + 1
+                if not res.get("ok"):
+                    failed.add((gpu, part))
+                    self.counters["canary_failures"] = self.counters.get("canary_failures", 0) + 1
+                    log.error("start-up canary failed on GPU %d partition %d: %s", gpu, part, res.get("error") or res)
+        return failed
+
     def _canary_ok(self, gpu: int) -> bool:
         from ..ops import canary
         for g in self.gpus:
             if g.index != gpu:
                 continue
             for part in g.partitions:
-                res = canary.run_isolated(part.hip_id, self.cfg.health.canaryBytes)
+                res = canary.run_isolated(max(0, part.hip_id), self.cfg.health.canaryBytes,
+                                          self.cfg.health.canaryTimeoutS)
                 if not res.get("ok"):
                     log.error("canary failed on GPU %d partition %d: %s", gpu, part.index, res)
                     return False

@@ -26,8 +26,6 @@ py::tuple ok_bytes(bool ok, const std::string& s) {
   return py::make_tuple(false, py::str(s));
 }
 
-std::string to_str(const py::bytes& b) { return std::string(b); }
-
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {

@@ -361,9 +361,11 @@ void GrpcServer::run(Worker* w) {
     for (auto& kv : c->streams) {
       Stream& s = kv.second;
       if (!s.law || s.done || s.law_version == v) continue;
+      const int64_t t0 = mono_ns();
       if (payload.empty()) payload = table->list_and_watch();
       s.law_version = v;
       send_message(*c, kv.first, s, payload, false);
+      table->observe(kRpcListAndWatch, (mono_ns() - t0) * 1e-9, false);
     }
   };
   auto dispatch = [&](Conn& c, uint32_t sid, Stream& s) {

@@ -107,17 +107,6 @@ void Exporter::sample_once() {
 
 namespace {
 
-struct Fam {
-  std::string* out;
-  const char* name;
-  bool started = false;
-  void begin(const char* help, const char* type) {
-    if (started) return;
-    append_header(out, name, help, type);
-    started = true;
-  }
-};
-
 void gpu_labels(std::string* out, int gpu) {
   out->append("gpu=\"");
   append_u64(out, static_cast<uint64_t>(gpu));

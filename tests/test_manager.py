@@ -212,3 +212,20 @@ def test_concurrent_restart_requests_are_serialized(make_cfg, plugin_dir, run_ma
             t.join()
         assert _wait(lambda: m.counters["restarts_api"] == 10, timeout=20)
         assert k.client("amd-gpu.sock").get_options().get_preferred_allocation_available
+
+
+def test_startup_canary_marks_failing_partition_unhealthy(make_cfg, plugin_dir, run_manager, monkeypatch):
+    from k8s_gpu_device_plugin_amd.ops import canary
+    calls = []
+
+    def fake_run_isolated(device, nbytes, timeout=120.0):
+        calls.append(device)
+        return {"ok": device != 9, "device": device, "error": "" if device != 9 else "hbm mismatch"}
+    monkeypatch.setattr(canary, "run_isolated", fake_run_isolated)
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(fixture="2gpu_cpx_nps2", migStrategy="single", health={"canaryOnStart": True}))
+        _, devs = k.watch(k.wait_for_registrations(1)[0].endpoint).next()
+        assert sorted(calls) == list(range(16))
+        bad = [i for i, (_, h, _) in enumerate(devs) if h == "Unhealthy"]
+        assert bad == [9]  # GPU 1, partition 1 (hip id 9)
+        assert m.counters["canary_failures"] == 1 and m.counters["canary_runs"] == 16
