@@ -1,0 +1,60 @@
+"""Container Device Interface (CDI) spec for the advertised devices.
+
+With ``cdi: true`` the Allocate response names devices as ``amd.com/gpu=<device id>``
+(``ContainerAllocateResponse.cdi_devices``) instead of relying only on DeviceSpecs; a
+CDI-enabled runtime (containerd >= 1.7, CRI-O) resolves those names through a spec file
+in ``/var/run/cdi``.  The reference has no CDI support (its Allocate returns only an env
+var, ``plugin/plugin.go:217-221``).
+
+One spec per resource kind, e.g. ``/var/run/cdi/amd.com-gpu.json``::
+
+    {"cdiVersion": "0.6.0", "kind": "amd.com/gpu",
+     "containerEdits": {"deviceNodes": [{"path": "/dev/kfd"}]},
+     "devices": [{"name": "<id>", "containerEdits": {"deviceNodes": [{"path": "/dev/dri/renderD128"}],
+                  "env": ["AMD_VISIBLE_DEVICES=<id>"]}}]}
+"""
+from __future__ import annotations
+
+import json
+import os
+import tempfile
+
+CDI_VERSION = "0.6.0"
+
+
+def _node(path: str) -> dict:
+    return {"path": path, "permissions": "rw"}
+
+
+def build_spec(kind: str, devices, kfd_path: str = "/dev/kfd", visible_env: str = "AMD_VISIBLE_DEVICES") -> dict:
+    out = []
+    for d in devices:
+        edits = {"deviceNodes": [_node(p) for p in d.paths]}
+        if visible_env:
+            edits["env"] = ["%s=%s" % (visible_env, d.get_uuid())]
+        out.append({"name": d.get_uuid(), "containerEdits": edits})
+    # replicas share one CDI device (the name is the base id)
+    uniq, seen = [], set()
+    for d in out:
+        if d["name"] not in seen:
+            seen.add(d["name"])
+            uniq.append(d)
+    return {"cdiVersion": CDI_VERSION, "kind": kind,
+            "containerEdits": {"deviceNodes": [_node(kfd_path)] if kfd_path else []},
+            "devices": uniq}
+
+
+def spec_path(spec_dir: str, kind: str) -> str:
+    return os.path.join(spec_dir, kind.replace("/", "-") + ".json")
+
+
+def write_spec(spec_dir: str, spec: dict) -> str:
+    """Atomic write (temp file + rename) so a runtime never reads a torn spec."""
+    os.makedirs(spec_dir, exist_ok=True)
+    path = spec_path(spec_dir, spec["kind"])
+    fd, tmp = tempfile.mkstemp(prefix=".cdi-", dir=spec_dir)
+    with os.fdopen(fd, "w") as f:
+        json.dump(spec, f, indent=1, sort_keys=True)
+    os.chmod(tmp, 0o644)
+    os.replace(tmp, path)
+    return path

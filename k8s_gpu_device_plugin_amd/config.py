@@ -92,6 +92,8 @@ class Config:
     visibleDevicesEnv: str = "AMD_VISIBLE_DEVICES"
     mountCardNodes: bool = False
     cdi: bool = False
+    cdiSpecDir: str = "/var/run/cdi"
+    rediscoverIntervalS: float = 60.0     # detect partition-mode / device-set changes (0 = off)
     sharing: SharingConfig = field(default_factory=SharingConfig)
     telemetry: TelemetryConfig = field(default_factory=TelemetryConfig)
     health: HealthConfig = field(default_factory=HealthConfig)

@@ -88,6 +88,37 @@ def load_model(spec) -> dict:
     return m
 
 
+def _partitions(n, gpu_index: int, uuid: str, nparts: int, numa: int, vram: int, first_render: int):
+    parts = []
+    for p in range(nparts):
+        pi = n.PartitionInfo()
+        pi.gpu = gpu_index
+        pi.index = p
+        pi.uuid = uuid if nparts == 1 else "%s-%d" % (uuid, p)
+        pi.id = uuid if nparts == 1 else "%s-xcp%d" % (uuid, p)
+        pi.render_minor = first_render + p
+        pi.card_minor = first_render - 128 + p
+        pi.hip_id = gpu_index * nparts + p
+        pi.hsa_id = gpu_index * nparts + p
+        pi.kfd_node = 1 + gpu_index * nparts + p
+        pi.numa_node = numa
+        pi.vram_bytes = vram // nparts
+        parts.append(pi)
+    return parts
+
+
+def set_gpu_mode(backend, gpu_index: int, compute: str, memory: str = "NPS1", first_render: int = 200) -> None:
+    """Simulates an operator re-partitioning one GPU (amd-smi set --compute-partition):
+    the GPU's partitions (and their render nodes) are replaced."""
+    n = native.load()
+    gpus, _ = backend.discover()
+    g = gpus[gpu_index]
+    g.compute_partition, g.memory_partition = compute.upper(), memory.upper()
+    g.partitions = _partitions(n, gpu_index, g.uuid, PARTITIONS[g.compute_partition], g.numa_node,
+                               g.vram_total_bytes, first_render)
+    backend.replace_gpu(gpu_index, g)
+
+
 def build_backend(spec):
     """Creates a native FixtureBackend populated from a node model."""
     n = native.load()
@@ -96,7 +127,6 @@ def build_backend(spec):
     be = n.FixtureBackend(seed)
     gpus = model.get("gpus", [])
     render = 128
-    card = 0
     for gi, g in enumerate(gpus):
         info = n.GpuInfo()
         info.uuid = g.get("uuid") or fixture_uuid(seed, gi)
@@ -115,24 +145,8 @@ def build_backend(spec):
         info.num_compute_units = int(g.get("num_cus", MI355X_CUS))
         nparts = int(g.get("num_partitions", PARTITIONS.get(info.compute_partition, 1)))
         info.num_xgmi_links = max(0, len(gpus) - 1)
-        parts = []
-        for p in range(nparts):
-            pi = n.PartitionInfo()
-            pi.gpu = gi
-            pi.index = p
-            pi.uuid = info.uuid if nparts == 1 else "%s-%d" % (info.uuid, p)
-            pi.id = info.uuid if nparts == 1 else "%s-xcp%d" % (info.uuid, p)
-            pi.render_minor = render
-            pi.card_minor = card
-            pi.hip_id = gi * nparts + p
-            pi.hsa_id = gi * nparts + p
-            pi.kfd_node = 1 + gi * nparts + p
-            pi.numa_node = info.numa_node
-            pi.vram_bytes = info.vram_total_bytes // nparts
-            render += 1
-            card += 1
-            parts.append(pi)
-        info.partitions = parts
+        info.partitions = _partitions(n, gi, info.uuid, nparts, info.numa_node, info.vram_total_bytes, render)
+        render += nparts
         be.add_gpu(info)
     links = model.get("links", {}) or {}
     ltype = {"xgmi": n.LINK_XGMI, "pcie": n.LINK_PCIE}.get(str(links.get("type", "xgmi")).lower(), n.LINK_XGMI)

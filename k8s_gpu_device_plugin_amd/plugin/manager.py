@@ -35,7 +35,14 @@ from .plugin import AmdDevicePlugin
 
 log = get_logger("manager")
 
-EV_STOP, EV_RESTART, EV_RETRY, EV_KUBELET, EV_HEALTH = "stop", "restart", "retry", "kubelet", "health"
+EV_STOP, EV_RESTART, EV_RETRY, EV_KUBELET, EV_HEALTH, EV_REDISCOVER = (
+    "stop", "restart", "retry", "kubelet", "health", "rediscover")
+
+
+def inventory_signature(gpus) -> tuple:
+    """What must stay identical for the advertised device set to stay valid."""
+    return tuple((g.index, g.uuid, g.compute_partition, g.memory_partition,
+                  tuple((p.id, p.render_minor) for p in g.partitions)) for g in gpus)
 
 
 def build_info_text() -> str:
@@ -63,6 +70,8 @@ class PluginManager:
         self._threads: list[threading.Thread] = []
         self._running = threading.Event()
         self._stopped = threading.Event()
+        self._stop_flag = threading.Event()
+        self.signature = None
         self._lock = threading.Lock()
         self.fatal_error: str | None = None
         self.counters = {"restarts_api": 0, "restarts_kubelet": 0, "restarts_retry": 0, "registrations": 0,
@@ -142,6 +151,8 @@ class PluginManager:
                     self.start_plugins()
                 elif kind == EV_HEALTH:
                     self._apply_health(ev[1])
+                elif kind == EV_REDISCOVER:
+                    self._check_inventory()
             except Exception as e:
                 self.counters["load_failures"] += 1
                 log.error("event %s failed: %s; retrying in %.0fs", kind, e, self.cfg.retrySeconds)
@@ -155,6 +166,7 @@ class PluginManager:
         if wanted is not None:
             gpus = [g for g in gpus if g.index in wanted]
         self.gpus, self.topology = gpus, topo
+        self.signature = inventory_signature(gpus)
         resources = new_resources(gpus, self.cfg.strategy, self.cfg.resourcePrefix, self.cfg.resources)
         self.device_map = build_device_map(gpus, resources, self.cfg.strategy, self.cfg.mountCardNodes,
                                            self.cfg.sharing.replicas, self.cfg.sharing.renameByDefault)
@@ -174,6 +186,13 @@ class PluginManager:
             for d in devs:
                 if d.replica <= 0:
                     labels.append(n.PartitionLabel(d.gpu, d.partition, d.get_uuid(), name))
+        if self.cfg.cdi:
+            from ..cdi import build_spec, write_spec
+            for name, devs in self.device_map.items():
+                try:
+                    write_spec(self.cfg.cdiSpecDir, build_spec(name, devs, visible_env=self.cfg.visibleDevicesEnv))
+                except OSError as e:
+                    log.error("cannot write CDI spec for %s to %s: %s", name, self.cfg.cdiSpecDir, e)
         self.exporter.set_inventory(gpus)
         self.exporter.set_partition_labels(labels)
         self.exporter.set_tables([p.table for p in plugins])
@@ -254,6 +273,18 @@ class PluginManager:
                     log.error("start-up canary failed on GPU %d partition %d: %s", gpu, part, res.get("error") or res)
         return failed
 
+    def _check_inventory(self) -> None:
+        """Periodic re-discovery: a compute/memory partition-mode change (SPX->CPX, ...) or a
+        GPU appearing/disappearing changes the device set; re-advertise when it does."""
+        gpus, _ = self.backend.discover()
+        wanted = parse_index_list(self.cfg.devices)
+        if wanted is not None:
+            gpus = [g for g in gpus if g.index in wanted]
+        if inventory_signature(gpus) != getattr(self, "signature", None):
+            self.counters["restarts_inventory"] = self.counters.get("restarts_inventory", 0) + 1
+            log.warning("device inventory changed (partition mode or GPU set); re-advertising")
+            self.restart_plugins()
+
     def _canary_ok(self, gpu: int) -> bool:
         from ..ops import canary
         for g in self.gpus:
@@ -292,7 +323,12 @@ class PluginManager:
                 for u in self.monitor.pop(200):
                     self.events.put((EV_HEALTH, u))
 
-        for fn, name in ((watch_loop, "fs-watch"), (health_loop, "health-pump")):
+        def rediscover_loop():
+            interval = float(self.cfg.rediscoverIntervalS)
+            while interval > 0 and not self._stop_flag.wait(interval):
+                self.events.put((EV_REDISCOVER,))
+
+        for fn, name in ((watch_loop, "fs-watch"), (health_loop, "health-pump"), (rediscover_loop, "rediscover")):
             t = threading.Thread(target=fn, name=name, daemon=True)
             t.start()
             self._threads.append(t)
@@ -340,6 +376,7 @@ class PluginManager:
 
     def _shutdown(self) -> None:
         self._cancel_retry()
+        self._stop_flag.set()
         self._running.clear()
         self.stop_plugins()
         self.exporter.stop()

@@ -193,6 +193,7 @@ PYBIND11_MODULE(_native, m) {
   py::class_<FixtureBackend, Backend, std::shared_ptr<FixtureBackend>>(m, "FixtureBackend")
       .def(py::init<uint64_t>(), py::arg("seed") = 1)
       .def("add_gpu", &FixtureBackend::add_gpu)
+      .def("replace_gpu", &FixtureBackend::replace_gpu)
       .def("clear", &FixtureBackend::clear)
       .def("set_link", &FixtureBackend::set_link)
       .def("set_link_up", &FixtureBackend::set_link_up)

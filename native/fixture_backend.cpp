@@ -34,6 +34,15 @@ void FixtureBackend::add_gpu(const GpuInfo& g) {
   present_.push_back(true);
 }
 
+void FixtureBackend::replace_gpu(int index, const GpuInfo& g) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (index < 0 || index >= static_cast<int>(gpus_.size())) throw std::out_of_range("replace_gpu: bad gpu index");
+  GpuInfo copy = g;
+  copy.index = index;
+  for (auto& p : copy.partitions) p.gpu = index;
+  gpus_[index] = copy;
+}
+
 void FixtureBackend::clear() {
   std::lock_guard<std::mutex> lk(mu_);
   gpus_.clear();

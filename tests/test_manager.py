@@ -229,3 +229,34 @@ def test_startup_canary_marks_failing_partition_unhealthy(make_cfg, plugin_dir, 
         bad = [i for i, (_, h, _) in enumerate(devs) if h == "Unhealthy"]
         assert bad == [9]  # GPU 1, partition 1 (hip id 9)
         assert m.counters["canary_failures"] == 1 and m.counters["canary_runs"] == 16
+
+
+def test_partition_mode_change_is_rediscovered(make_cfg, plugin_dir, run_manager):
+    be = fixtures.build_backend("2gpu_spx")
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(migStrategy="single", rediscoverIntervalS=0.2), backend=be)
+        _, devs = k.watch(k.wait_for_registrations(1)[0].endpoint).next()
+        assert len(devs) == 2
+        fixtures.set_gpu_mode(be, 1, "CPX", "NPS2")  # operator switches GPU 1 to CPX
+        k.wait_for_registrations(2, timeout=10)
+        assert _wait(lambda: m.counters.get("restarts_inventory", 0) >= 1)
+        c = k.client("amd-gpu.sock")
+        ids = m.plugins[0].table.ids()
+        assert len(ids) == 9 and ids[1].endswith("-xcp0")
+        r = c.allocate([ids[4]])
+        assert [s.host_path for s in r.container_responses[0].devices] == ["/dev/kfd", "/dev/dri/renderD203"]
+
+
+def test_cdi_spec_written_and_allocate_names(make_cfg, plugin_dir, run_manager, tmp_path):
+    import json
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(cdi=True, cdiSpecDir=str(tmp_path / "cdi")))
+        k.wait_for_registrations(1)
+        spec = json.load(open(tmp_path / "cdi" / "amd.com-gpu.json"))
+        assert spec["kind"] == "amd.com/gpu" and spec["cdiVersion"] == "0.6.0"
+        assert spec["containerEdits"]["deviceNodes"][0]["path"] == "/dev/kfd"
+        ids = m.plugins[0].table.ids()
+        assert [d["name"] for d in spec["devices"]] == ids
+        assert spec["devices"][1]["containerEdits"]["deviceNodes"][0]["path"] == "/dev/dri/renderD129"
+        r = k.client("amd-gpu.sock").allocate([ids[1]])
+        assert [d.name for d in r.container_responses[0].cdi_devices] == ["amd.com/gpu=" + ids[1]]
