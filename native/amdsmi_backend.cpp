@@ -117,7 +117,16 @@ class AmdSmiBackend : public Backend {
   void discover(std::vector<GpuInfo>* gpus, Topology* topo) override {
     std::lock_guard<std::mutex> lk(mu_);
     if (closed_) throw std::runtime_error("amdsmi backend is shut down");
+    // periodic re-discovery must not silently drop event delivery: re-arm afterwards
+    const bool was_armed = armed_;
     disarm_locked();
+    struct Rearm {
+      AmdSmiBackend* self;
+      bool on;
+      ~Rearm() {
+        if (on) self->arm_locked();
+      }
+    } rearm{this, was_armed};
     uint32_t nsock = 0;
     check(amdsmi_get_socket_handles(&nsock, nullptr), "amdsmi_get_socket_handles(count)");
     std::vector<amdsmi_socket_handle> socks(nsock);
@@ -307,6 +316,10 @@ class AmdSmiBackend : public Backend {
 
   void arm_events() override {
     std::lock_guard<std::mutex> lk(mu_);
+    arm_locked();
+  }
+
+  void arm_locked() {
     if (armed_ || closed_) return;
     const uint64_t mask = AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_GPU_PRE_RESET) |
                           AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_GPU_POST_RESET) |
@@ -324,6 +337,11 @@ class AmdSmiBackend : public Backend {
       }
     }
     armed_ = true;
+  }
+
+  int armed_event_sources() const override {
+    std::lock_guard<std::mutex> lk(mu_);
+    return static_cast<int>(armed_handles_.size());
   }
 
   int wait_events(int timeout_ms, std::vector<HwEvent>* out) override {
@@ -422,7 +440,7 @@ class AmdSmiBackend : public Backend {
     armed_ = false;
   }
 
-  std::mutex mu_;
+  mutable std::mutex mu_;
   std::vector<std::vector<amdsmi_processor_handle>> procs_;
   std::vector<GpuInfo> gpus_;
   std::vector<amdsmi_processor_handle> armed_handles_;

@@ -156,6 +156,8 @@ class Backend {
   virtual int wait_events(int timeout_ms, std::vector<HwEvent>* out) = 0;
   // Arm event delivery for the discovered GPUs (idempotent).
   virtual void arm_events() {}
+  // Number of processors with hardware event delivery armed (0 = polling only).
+  virtual int armed_event_sources() const { return 0; }
   virtual void shutdown() {}
 };
 

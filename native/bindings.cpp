@@ -188,6 +188,7 @@ PYBIND11_MODULE(_native, m) {
              return py::cast(s);
            })
       .def("arm_events", &Backend::arm_events, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("armed_event_sources", &Backend::armed_event_sources)
       .def("shutdown", &Backend::shutdown, py::call_guard<py::gil_scoped_release>());
 
   py::class_<FixtureBackend, Backend, std::shared_ptr<FixtureBackend>>(m, "FixtureBackend")

@@ -20,6 +20,7 @@ class FixtureBackend : public Backend {
   bool sample(int gpu, GpuSample* out) override;
   int wait_events(int timeout_ms, std::vector<HwEvent>* out) override;
   void arm_events() override;
+  int armed_event_sources() const override { return armed_at_ns_ != 0 ? 1 : 0; }
   void shutdown() override;
 
   // --- configuration (called before / between discoveries) ---

@@ -152,3 +152,24 @@ def test_native_grpc_server_on_gpu_box(make_cfg, plugin_dir, n):
         mgr.stop()
         t.join(10)
         k.stop()
+
+
+def test_amdsmi_health_monitor_runs_and_stops(n, amdsmi_backend):
+    gpus, _ = amdsmi_backend.discover()
+    mon = n.HealthMonitor(amdsmi_backend, 3)
+    mon.set_gpu_count(len(gpus))
+    t0 = time.monotonic()
+    mon.start()
+    time.sleep(0.5)
+    print("amdsmi event sources armed:", amdsmi_backend.armed_event_sources)
+    assert mon.running and mon.gpu_healthy(0)
+    mon.stop()
+    assert not mon.running and time.monotonic() - t0 < 5
+    assert [u for u in mon.pop(10) if u.healthy == 0] == []
+
+
+def test_amdsmi_inventory_signature_is_stable(amdsmi_backend):
+    from k8s_gpu_device_plugin_amd.plugin.manager import inventory_signature
+    a = inventory_signature(amdsmi_backend.discover()[0])
+    b = inventory_signature(amdsmi_backend.discover()[0])
+    assert a == b  # no spurious re-advertisement from periodic re-discovery
