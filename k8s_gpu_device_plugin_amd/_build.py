@@ -8,8 +8,12 @@ the repo snapshot to the GPU box):
   ``hipcc --offload-arch=gfx950``.
 * ``build/native_selftest[-asan|-tsan]``  standalone C++ self-test (no Python) for
   sanitizer runs.
+* ``build/fuzz/fuzz_<target>``  libFuzzer + ASan + UBSan binaries (amdclang++) for
+  every parser that faces a peer: ``pbwire`` (kubelet protobuf + allocator contract),
+  ``hpack``, ``grpc`` (HTTP/2 server on its socket), ``http`` (HTTP/1.1 ops server).
 
-Usage: ``python -m k8s_gpu_device_plugin_amd._build [--force] [--sanitize address|thread]``
+Usage: ``python -m k8s_gpu_device_plugin_amd._build [--force] [--sanitize address|thread]
+[--fuzz TARGET... --fuzz-seconds N]``
 """
 from __future__ import annotations
 
@@ -43,6 +47,8 @@ CORE_SOURCES = [
     "loadgen.cpp",
 ]
 BINDING_SOURCES = ["bindings.cpp"]
+FUZZ_TARGETS = ("pbwire", "hpack", "grpc", "http")
+FUZZ_DIR = os.path.join(NATIVE_DIR, "fuzz")
 CANARY_SOURCE = os.path.join(PKG_DIR, "ops", "canary.hip")
 CANARY_LIB = os.path.join(PKG_DIR, "ops", "libamdgpu_canary.so")
 
@@ -90,12 +96,13 @@ def _link_libs():
             "-pthread"]
 
 
-def _compile_objects(sources, obj_dir, extra_flags, force, jobs):
+def _compile_objects(sources, obj_dir, extra_flags, force, jobs, cxx=None, src_dir=NATIVE_DIR):
     os.makedirs(obj_dir, exist_ok=True)
     hdrs = _headers()
+    cxx = cxx or _cxx()
     todo, objs = [], []
     for s in sources:
-        src = os.path.join(NATIVE_DIR, s)
+        src = os.path.join(src_dir, s)
         obj = os.path.join(obj_dir, s.rsplit(".", 1)[0] + ".o")
         objs.append(obj)
         if force or _stale(obj, [src] + hdrs):
@@ -103,7 +110,7 @@ def _compile_objects(sources, obj_dir, extra_flags, force, jobs):
 
     def one(pair):
         src, obj = pair
-        _run([_cxx()] + extra_flags + ["-c", src, "-o", obj], "compile " + os.path.basename(src))
+        _run([cxx] + extra_flags + ["-c", src, "-o", obj], "compile " + os.path.basename(src))
 
     if todo:
         with concurrent.futures.ThreadPoolExecutor(max_workers=jobs) as ex:
@@ -147,6 +154,59 @@ def build_selftest(sanitize: str | None = None, force: bool = False) -> str:
     return exe
 
 
+def clangxx_path() -> str:
+    p = os.path.join(ROCM, "lib", "llvm", "bin", "clang++")
+    if not os.path.exists(p):
+        raise RuntimeError("libFuzzer builds need ROCm's clang++ (%s)" % p)
+    return p
+
+
+def build_fuzzer(target: str, force: bool = False) -> str:
+    """libFuzzer binary for one target, ASan + UBSan, coverage on the core sources too.
+
+    ``-mllvm -asan-globals=0``: ROCm's clang + libstdc++ 11 trips ASan's global
+    alignment/ODR check on merged string literals (a false positive); heap, stack and
+    UB checks are unaffected."""
+    if target not in FUZZ_TARGETS:
+        raise ValueError("unknown fuzz target %r (have %s)" % (target, ", ".join(FUZZ_TARGETS)))
+    cxx = clangxx_path()
+    san = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-mllvm", "-asan-globals=0",
+           "-fno-sanitize-recover=undefined"]
+    base = [f for f in _common_flags(None) if f not in ("-O2", "-g1")] + san
+    core, core_changed = _compile_objects(CORE_SOURCES, os.path.join(BUILD_DIR, "obj_fuzz"),
+                                          base + ["-fsanitize=fuzzer-no-link"], force, min(8, os.cpu_count() or 4),
+                                          cxx=cxx)
+    harness, h_changed = _compile_objects(["fuzz_%s.cpp" % target], os.path.join(BUILD_DIR, "obj_fuzz"),
+                                          base + ["-fsanitize=fuzzer-no-link", "-I" + FUZZ_DIR], force, 1,
+                                          cxx=cxx, src_dir=FUZZ_DIR)
+    exe = os.path.join(BUILD_DIR, "fuzz", "fuzz_" + target)
+    os.makedirs(os.path.dirname(exe), exist_ok=True)
+    if force or core_changed or h_changed or not os.path.exists(exe):
+        _run([cxx, "-fsanitize=fuzzer,address,undefined", "-o", exe] + harness + core + _link_libs(),
+             "link fuzz_" + target)
+    return exe
+
+
+def run_fuzzer(target: str, seconds: float = 10.0, force: bool = False, extra_args=()) -> subprocess.CompletedProcess:
+    """Builds ``target``, writes its seed corpus, fuzzes for ``seconds``.  Crashes /
+    hangs are saved under ``build/fuzz/artifacts/`` and make the return code non-zero."""
+    exe = build_fuzzer(target, force=force)
+    corpus = os.path.join(BUILD_DIR, "fuzz", "corpus", target)
+    artifacts = os.path.join(BUILD_DIR, "fuzz", "artifacts") + os.sep
+    os.makedirs(corpus, exist_ok=True)
+    os.makedirs(artifacts, exist_ok=True)
+    seeded = subprocess.run([exe], env=dict(os.environ, FUZZ_WRITE_SEEDS=corpus), stdout=subprocess.PIPE,
+                            stderr=subprocess.STDOUT, text=True)
+    if seeded.returncode != 0:
+        raise RuntimeError("fuzz_%s: writing seeds failed:\n%s" % (target, seeded.stdout[-2000:]))
+    env = dict(os.environ)
+    env["ASAN_OPTIONS"] = "detect_leaks=0:halt_on_error=1:abort_on_error=1"
+    env["UBSAN_OPTIONS"] = "halt_on_error=1:print_stacktrace=1"
+    cmd = [exe, corpus, "-max_total_time=%d" % max(1, int(seconds)), "-timeout=10", "-rss_limit_mb=4096",
+           "-max_len=8192", "-print_final_stats=1", "-artifact_prefix=" + artifacts + target + "-"] + list(extra_args)
+    return subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
+
+
 def hipcc_path() -> str | None:
     p = os.path.join(ROCM, "bin", "hipcc")
     return p if os.path.exists(p) else shutil.which("hipcc")
@@ -179,7 +239,18 @@ def main(argv=None) -> int:
                     help="build the native self-test with a sanitizer instead")
     ap.add_argument("--selftest", action="store_true", help="also build (and run) the native self-test")
     ap.add_argument("--no-canary", action="store_true")
+    ap.add_argument("--fuzz", nargs="*", choices=FUZZ_TARGETS, default=None,
+                    help="build and run libFuzzer targets (all when none named)")
+    ap.add_argument("--fuzz-seconds", type=float, default=30.0)
     args = ap.parse_args(argv)
+    if args.fuzz is not None:
+        rc = 0
+        for t in args.fuzz or FUZZ_TARGETS:
+            p = run_fuzzer(t, args.fuzz_seconds, force=args.force)
+            tail = [ln for ln in p.stdout.splitlines() if ln.startswith(("#", "Done", "stat::", "=="))][-4:]
+            print("fuzz_%s: rc=%d\n  %s" % (t, p.returncode, "\n  ".join(tail)))
+            rc = rc or p.returncode
+        return rc
     if args.sanitize or args.selftest:
         exe = build_selftest(args.sanitize, force=args.force)
         print("built", os.path.relpath(exe, ROOT))

@@ -247,9 +247,21 @@ AllocResult DeviceTable::preferred_ids(const std::vector<std::string>& avail, co
       r.error = "unknown device in must_include_deviceIDs: " + id;
       return r;
     }
-    m.push_back(i);
+    if (std::find(m.begin(), m.end(), i) == m.end()) m.push_back(i);
   }
   AllocResult r;
+  // Contract (go-gpuallocator BestEffort): a non-positive size yields no devices; a size
+  // below |must_include| cannot be honoured and is an error rather than a larger set.
+  if (size <= 0) {
+    if (out_ids) out_ids->clear();
+    return r;
+  }
+  if (static_cast<size_t>(size) < m.size()) {
+    r.ok = false;
+    r.error = "allocation_size " + std::to_string(size) + " is smaller than must_include_deviceIDs (" +
+              std::to_string(m.size()) + ")";
+    return r;
+  }
   if (aligned_ok_ && !any_annotated) {
     const auto topo = std::atomic_load_explicit(&topo_, std::memory_order_acquire);  // snapshot
     r = aligned_alloc(*topo, alloc_devs_, a, m, size);

@@ -35,13 +35,16 @@ enum FrameType : uint8_t {
   kContinuation = 9,
 };
 enum Flags : uint8_t { kEndStream = 0x1, kAck = 0x1, kEndHeaders = 0x4, kPadded = 0x8, kPriorityFlag = 0x20 };
-enum H2Error : uint32_t { kNoError = 0, kProtocolError = 1, kFlowControlError = 3, kFrameSizeError = 6,
-                          kRefusedStream = 7, kCompressionError = 9 };
+enum H2Error : uint32_t { kNoError = 0, kProtocolError = 1, kFlowControlError = 3, kStreamClosed = 5,
+                          kFrameSizeError = 6, kRefusedStream = 7, kCompressionError = 9 };
 
 constexpr uint32_t kMaxFrame = 16384;           // our SETTINGS_MAX_FRAME_SIZE (default)
 constexpr int64_t kLocalWindow = 1 << 20;        // stream + connection receive windows we grant
 constexpr size_t kMaxMessage = 4u << 20;         // grpc default max receive message size
 constexpr size_t kMaxStreams = 1024;
+constexpr int64_t kMaxWindow = 0x7FFFFFFF;       // RFC 9113 §6.9.1
+constexpr size_t kMaxPendingOut = 16u << 20;     // a peer that never reads is dropped
+constexpr size_t kMaxBuffered = 16u << 20;       // request bytes buffered per connection
 
 void put_u32(std::string* o, uint32_t v) {
   o->push_back(static_cast<char>(v >> 24));
@@ -133,6 +136,7 @@ struct Stream {
   std::string trailers;     // header block sent (END_STREAM) once pend drains
   bool law = false;
   uint64_t law_version = 0;
+  bool dispatched = false;  // request half-closed; later DATA/HEADERS are stream errors
   bool done = false;
 };
 
@@ -168,6 +172,7 @@ struct GrpcServer::Worker {
     std::string hblock;
     int64_t recv_unacked = 0;
     uint32_t last_sid = 0;
+    size_t buffered = 0;  // request bytes held across all streams
     bool closing = false;
     bool want_out = false;
   };
@@ -188,6 +193,11 @@ void goaway(Conn& c, uint32_t code) {
 void rst_stream(Conn& c, uint32_t sid, uint32_t code) {
   frame(&c.out, 4, kRstStream, 0, sid);
   put_u32(&c.out, code);
+}
+
+void drop_data(Conn& c, Stream& s) {
+  c.buffered -= s.data.size();
+  std::string().swap(s.data);
 }
 
 // Drain a stream's pending DATA within the flow-control windows, then its trailers.
@@ -369,6 +379,12 @@ void GrpcServer::run(Worker* w) {
     }
   };
   auto dispatch = [&](Conn& c, uint32_t sid, Stream& s) {
+    if (s.dispatched) {  // END_STREAM seen twice (trailers or DATA after the request)
+      rst_stream(c, sid, kStreamClosed);
+      s.done = true;
+      return;
+    }
+    s.dispatched = true;
     const int64_t t0 = mono_ns();
     requests_.fetch_add(1, std::memory_order_relaxed);
     const Method m = method_of(s.path);
@@ -454,7 +470,10 @@ void GrpcServer::run(Worker* w) {
       s.headers_done = true;
       it = c.streams.emplace(sid, std::move(s)).first;
     }
-    if (flags & kEndStream) dispatch(c, sid, it->second);
+    if (flags & kEndStream) {
+      dispatch(c, sid, it->second);
+      drop_data(c, it->second);
+    }
     return true;
   };
   auto process = [&](Conn& c) -> bool {  // false = fatal, close after flushing
@@ -501,7 +520,13 @@ void GrpcServer::run(Worker* w) {
               }
               const int64_t delta = static_cast<int64_t>(v) - c.peer_init_window;
               c.peer_init_window = v;
-              for (auto& kv : c.streams) kv.second.send_window += delta;
+              for (auto& kv : c.streams) {
+                kv.second.send_window += delta;
+                if (kv.second.send_window > kMaxWindow) {
+                  goaway(c, kFlowControlError);
+                  return false;
+                }
+              }
             } else if (id == 5) {
               if (v < 16384 || v > 16777215) {
                 goaway(c, kProtocolError);
@@ -532,17 +557,32 @@ void GrpcServer::run(Worker* w) {
           const uint32_t inc = get_u32(p) & 0x7FFFFFFFu;
           if (sid == 0) {
             c.send_window += inc;
+            if (inc == 0 || c.send_window > kMaxWindow) {
+              goaway(c, inc == 0 ? kProtocolError : kFlowControlError);
+              return false;
+            }
             for (auto& kv : c.streams) flush_stream(c, kv.first, kv.second);
           } else {
             auto it = c.streams.find(sid);
             if (it != c.streams.end()) {
               it->second.send_window += inc;
-              flush_stream(c, sid, it->second);
+              if (inc == 0 || it->second.send_window > kMaxWindow) {
+                rst_stream(c, sid, inc == 0 ? kProtocolError : kFlowControlError);
+                it->second.done = true;
+                it->second.pend.clear();
+                it->second.trailers_after = false;
+              } else {
+                flush_stream(c, sid, it->second);
+              }
             }
           }
           break;
         }
         case kHeaders: {
+          if (sid == 0) {
+            goaway(c, kProtocolError);
+            return false;
+          }
           size_t off = 0, pad = 0;
           if (flags & kPadded) {
             if (len < 1) return goaway(c, kProtocolError), false;
@@ -576,6 +616,10 @@ void GrpcServer::run(Worker* w) {
           }
           break;
         case kData: {
+          if (sid == 0) {
+            goaway(c, kProtocolError);
+            return false;
+          }
           size_t off = 0, pad = 0;
           if (flags & kPadded) {
             if (len < 1) return goaway(c, kProtocolError), false;
@@ -588,14 +632,20 @@ void GrpcServer::run(Worker* w) {
           }
           c.recv_unacked += len;
           auto it = c.streams.find(sid);
-          if (it != c.streams.end() && !it->second.done) {
+          if (it != c.streams.end() && it->second.dispatched && !it->second.done) {
+            rst_stream(c, sid, kStreamClosed);  // DATA after the request half-closed
+            it->second.done = true;
+          } else if (it != c.streams.end() && !it->second.done) {
             Stream& s = it->second;
             s.data.append(reinterpret_cast<const char*>(p + off), len - off - pad);
+            c.buffered += len - off - pad;
             s.recv_unacked += len;
-            if (s.data.size() > kMaxMessage + 5) {
-              send_error(c, sid, s, 8, "request exceeds 4 MiB");  // RESOURCE_EXHAUSTED
+            if (s.data.size() > kMaxMessage + 5 || c.buffered > kMaxBuffered) {
+              send_error(c, sid, s, 8, "request exceeds the receive limit");  // RESOURCE_EXHAUSTED
+              drop_data(c, s);
             } else if (flags & kEndStream) {
               dispatch(c, sid, s);
+              drop_data(c, s);
             } else if (s.recv_unacked > kLocalWindow / 2) {
               window_update(&c.out, sid, static_cast<uint32_t>(s.recv_unacked));
               s.recv_unacked = 0;
@@ -607,9 +657,14 @@ void GrpcServer::run(Worker* w) {
           }
           break;
         }
-        case kRstStream:
-          c.streams.erase(sid);
+        case kRstStream: {
+          auto it = c.streams.find(sid);
+          if (it != c.streams.end()) {
+            drop_data(c, it->second);
+            c.streams.erase(it);
+          }
           break;
+        }
         case kGoaway:
           c.closing = true;
           break;
@@ -619,7 +674,12 @@ void GrpcServer::run(Worker* w) {
     }
     c.in.erase(0, pos);
     for (auto it = c.streams.begin(); it != c.streams.end();)
-      it = it->second.done && it->second.pend.empty() ? c.streams.erase(it) : std::next(it);
+      if (it->second.done && it->second.pend.empty()) {
+        drop_data(c, it->second);
+        it = c.streams.erase(it);
+      } else {
+        ++it;
+      }
     return true;
   };
 
@@ -687,6 +747,10 @@ void GrpcServer::run(Worker* w) {
           }
         }
         if (!process(*c)) c->closing = true;
+      }
+      if (c->out.size() - c->out_off > kMaxPendingOut) {  // e.g. a PING flood that is never read
+        close_conn(fd);
+        continue;
       }
       if (!flush(c)) continue;
       if (peer_closed) close_conn(fd);

@@ -207,3 +207,64 @@ def test_first_stream_message_helper(n, server):
     assert len(v1beta1.ListAndWatchResponse.FromString(body).devices) == 64
     st, _, _ = c.unary(v1beta1.METHOD_GET_OPTIONS, b"")  # connection still usable after RST_STREAM
     assert st == 0
+
+
+def _grpc_call_frames(sid, path, msg, end_stream=True):
+    hb = bytes([0x83, 0x86]) + bytes([0x44, len(path)]) + path.encode() + bytes([0x5f, 16]) + b"application/grpc"
+    body = b"\x00" + struct.pack(">I", len(msg)) + msg
+    return _frame(1, 0x4, sid, hb) + _frame(0, 0x1 if end_stream else 0, sid, body)
+
+
+def _goaway_code(frames):
+    codes = [struct.unpack(">I", f[3][4:8])[0] for f in frames if f[0] == 7]
+    return codes[0] if codes else None
+
+
+def test_data_after_end_stream_is_stream_closed(server):
+    """Found by fuzz_grpc: a second END_STREAM on a dispatched stream used to dispatch the
+    request again (duplicate response HEADERS).  It is now RST_STREAM(STREAM_CLOSED)."""
+    srv, table, path = server
+    s = socket.socket(socket.AF_UNIX)
+    s.connect(path)
+    law = _grpc_call_frames(1, v1beta1.METHOD_LIST_AND_WATCH, b"")
+    s.sendall(PREFACE + _frame(4, 0, 0) + law + _frame(0, 0x1, 1, b"\x00\x00\x00\x00\x00"))
+    frames = _read_frames(s, until_type=3)
+    assert [f for f in frames if f[0] == 3 and f[2] == 1 and struct.unpack(">I", f[3])[0] == 5]
+    assert sum(1 for f in frames if f[0] == 1 and f[2] == 1) == 1  # response HEADERS sent once
+    s.close()
+
+
+@pytest.mark.parametrize("bad,code", [
+    (_frame(8, 0, 0, struct.pack(">I", 0x7FFFFFFF)), 3),  # connection window overflow -> FLOW_CONTROL
+    (_frame(8, 0, 0, struct.pack(">I", 0)), 1),           # zero increment -> PROTOCOL_ERROR
+    (_frame(1, 0x5, 0, b"\x83"), 1),                      # HEADERS on stream 0
+    (_frame(0, 0x1, 0, b"x"), 1),                         # DATA on stream 0
+])
+def test_connection_errors(server, bad, code):
+    srv, table, path = server
+    s = socket.socket(socket.AF_UNIX)
+    s.connect(path)
+    s.sendall(PREFACE + _frame(4, 0, 0) + bad)
+    assert _goaway_code(_read_frames(s, until_type=7)) == code
+    s.close()
+
+
+def test_preferred_size_contract(n, server):
+    """Found by fuzz_pbwire: allocation_size below |must_include| returned a larger set.
+    Now: size <= 0 -> empty answer, size < |must| -> error; must ids are de-duplicated."""
+    srv, table, path = server
+    c = n.H2Client(path)
+
+    def pref(avail, must, size):
+        return c.unary(v1beta1.METHOD_GET_PREFERRED, v1beta1.PreferredAllocationRequest(container_requests=[
+            v1beta1.ContainerPreferredAllocationRequest(available_deviceIDs=avail, must_include_deviceIDs=must,
+                                                        allocation_size=size)]).SerializeToString())
+    st, body, _ = pref(["dev-000", "dev-001"], [], 0)
+    assert st == 0 and list(v1beta1.PreferredAllocationResponse.FromString(body).container_responses[0].deviceIDs) \
+        == []
+    st, _, msg = pref(["dev-000", "dev-001", "dev-002"], ["dev-000", "dev-001"], 1)
+    assert st == 2 and "smaller than must_include" in msg
+    st, body, _ = pref(["dev-000", "dev-001", "dev-009"], ["dev-001", "dev-001"], 2)
+    ids = list(v1beta1.PreferredAllocationResponse.FromString(body).container_responses[0].deviceIDs)
+    assert st == 0 and len(ids) == 2 and len(set(ids)) == 2 and "dev-001" in ids
+    c.close()
