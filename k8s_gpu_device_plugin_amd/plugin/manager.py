@@ -18,6 +18,8 @@ HTTP ``/restart``, retry timer, ``stop()``.
 """
 from __future__ import annotations
 
+import collections
+import concurrent.futures
 import os
 import platform
 import queue
@@ -35,8 +37,9 @@ from .plugin import AmdDevicePlugin
 
 log = get_logger("manager")
 
-EV_STOP, EV_RESTART, EV_RETRY, EV_KUBELET, EV_HEALTH, EV_REDISCOVER = (
-    "stop", "restart", "retry", "kubelet", "health", "rediscover")
+EV_STOP, EV_RESTART, EV_RETRY, EV_KUBELET, EV_HEALTH, EV_REDISCOVER, EV_VERIFIED = (
+    "stop", "restart", "retry", "kubelet", "health", "rediscover", "verified")
+HEALTH_LOG_LEN = 4096
 
 
 def inventory_signature(gpus) -> tuple:
@@ -76,7 +79,15 @@ class PluginManager:
         self.fatal_error: str | None = None
         self.counters = {"restarts_api": 0, "restarts_kubelet": 0, "restarts_retry": 0, "registrations": 0,
                          "load_failures": 0, "health_events": 0}
-        self.health_log: list[tuple[float, int, int, str]] = []  # (t, gpu, healthy, reason)
+        # (t, gpu, healthy, reason); bounded so a flapping GPU cannot grow it forever
+        self.health_log: "collections.deque[tuple[float, int, int, str]]" = collections.deque(maxlen=HEALTH_LOG_LEN)
+        # Recovery canaries run off the manager thread; a per-GPU generation drops a
+        # verdict that an Unhealthy event overtook while the canary was running.
+        self._health_gen: dict[int, int] = {}
+        # GPUs the manager holds Unhealthy although the monitor reports them healthy:
+        # recovery canary pending or failed.  Survives plugin reloads.
+        self._held_unhealthy: set[int] = set()
+        self._verify_pool: concurrent.futures.ThreadPoolExecutor | None = None
 
     # ------------------------------------------------------------ public API
     def restart(self) -> None:
@@ -151,6 +162,8 @@ class PluginManager:
                     self.start_plugins()
                 elif kind == EV_HEALTH:
                     self._apply_health(ev[1])
+                elif kind == EV_VERIFIED:
+                    self._apply_verified(*ev[1:])
                 elif kind == EV_REDISCOVER:
                     self._check_inventory()
             except Exception as e:
@@ -175,7 +188,7 @@ class PluginManager:
         # health state survives a reload: re-apply what the monitor currently reports
         for p in plugins:
             for g in gpus:
-                if self.monitor.running and not self.monitor.gpu_healthy(g.index):
+                if (self.monitor.running and not self.monitor.gpu_healthy(g.index)) or g.index in self._held_unhealthy:
                     p.set_gpu_health(g.index, -1, False)
             for gpu, part in failed:
                 p.set_gpu_health(gpu, part, False)
@@ -238,19 +251,48 @@ class PluginManager:
         self.counters["health_events"] += 1
         if u.healthy in (0, 1):
             healthy = bool(u.healthy)
+            gen = self._health_gen[u.gpu] = self._health_gen.get(u.gpu, 0) + 1
             if healthy and self.cfg.health.canary:
-                healthy = self._canary_ok(u.gpu)
-            for p in self.plugins:
-                p.set_gpu_health(u.gpu, u.partition, healthy)
-            self.health_log.append((time.monotonic(), u.gpu, int(healthy), u.reason))
-            (log.info if healthy else log.warning)("GPU %d marked %s: %s", u.gpu,
-                                                   "Healthy" if healthy else "Unhealthy", u.reason)
+                # stay Unhealthy until the canary passes; do not block the event loop on it
+                if self._verify_pool is None:
+                    self._verify_pool = concurrent.futures.ThreadPoolExecutor(max_workers=4,
+                                                                              thread_name_prefix="canary")
+                log.info("GPU %d reports healthy (%s); verifying with the canary", u.gpu, u.reason)
+                self._held_unhealthy.add(u.gpu)
+                self._verify_pool.submit(self._verify_and_post, u, gen)
+                return
+            if healthy:
+                self._held_unhealthy.discard(u.gpu)
+            self._set_health(u.gpu, u.partition, healthy, u.reason)
         elif u.link_up in (0, 1):
             for p in self.plugins:
                 p.set_link_up(u.gpu, u.peer, bool(u.link_up))
             log.warning("xGMI link %d<->%d %s", u.gpu, u.peer, "up" if u.link_up else "down")
         else:
             log.info("GPU event on %d: %s", u.gpu, u.reason)
+
+    def _set_health(self, gpu: int, partition: int, healthy: bool, reason: str) -> None:
+        for p in self.plugins:
+            p.set_gpu_health(gpu, partition, healthy)
+        self.health_log.append((time.monotonic(), gpu, int(healthy), reason))
+        (log.info if healthy else log.warning)("GPU %d marked %s: %s", gpu, "Healthy" if healthy else "Unhealthy",
+                                               reason)
+
+    def _verify_and_post(self, u, gen: int) -> None:
+        try:
+            ok = self._canary_ok(u.gpu)
+        except Exception as e:  # a canary that cannot run does not prove health
+            log.error("recovery canary on GPU %d could not run: %s", u.gpu, e)
+            ok = False
+        self.events.put((EV_VERIFIED, u, gen, ok))
+
+    def _apply_verified(self, u, gen: int, ok: bool) -> None:
+        if self._health_gen.get(u.gpu) != gen:
+            log.info("dropping stale canary verdict for GPU %d (newer health event)", u.gpu)
+            return
+        if ok:
+            self._held_unhealthy.discard(u.gpu)
+        self._set_health(u.gpu, u.partition, ok, u.reason + ("" if ok else "; canary failed"))
 
     def _startup_canary(self, gpus) -> set:
         """Runs the gfx950 canary on every partition (one child process per partition, all
@@ -376,6 +418,8 @@ class PluginManager:
 
     def _shutdown(self) -> None:
         self._cancel_retry()
+        if self._verify_pool is not None:
+            self._verify_pool.shutdown(wait=False, cancel_futures=True)
         self._stop_flag.set()
         self._running.clear()
         self.stop_plugins()

@@ -24,7 +24,9 @@ for s in ${STEPS:-pytest smoke bench prof}; do
     sweep)  step hbm_sweep 300 python -c "import json; from k8s_gpu_device_plugin_amd.ops import canary; rows = canary.hbm_sweep(0); print(json.dumps(rows, indent=1)); json.dump(rows, open('$OUT/hbm_sweep.json', 'w'), indent=1)" ;;
     prof)   (cd /tmp && export TMPDIR=/tmp && step rocprof_canary 240 rocprofv3 --kernel-trace --stats -d "$OUT/prof_canary" -o canary --output-format csv -- python3 -m k8s_gpu_device_plugin_amd.ops.canary --device 0 --bytes 2147483648 --passes 3) ;;
     pmc)    # one derived counter per pass ("exceeds the capabilities" otherwise); short limits
-            for ctr in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES"; do
+            # PMC_CTRS="A;B C" overrides the list (';' separates passes)
+            IFS=';' read -r -a ctrs <<< "${PMC_CTRS:-FETCH_SIZE;WRITE_SIZE;TCC_HIT_sum TCC_MISS_sum;SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES}"
+            for ctr in "${ctrs[@]}"; do
               tag=$(echo "$ctr" | tr ' ' '_')
               (cd /tmp && export TMPDIR=/tmp && step "pmc_$tag" 90 rocprofv3 --pmc $ctr --kernel-trace --stats -d "$OUT/pmc_$tag" -o canary --output-format csv -- python3 -m k8s_gpu_device_plugin_amd.ops.canary --device 0 --bytes 1073741824 --passes 1) || exit $?
             done ;;

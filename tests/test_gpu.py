@@ -173,3 +173,56 @@ def test_amdsmi_inventory_signature_is_stable(amdsmi_backend):
     a = inventory_signature(amdsmi_backend.discover()[0])
     b = inventory_signature(amdsmi_backend.discover()[0])
     assert a == b  # no spurious re-advertisement from periodic re-discovery
+
+
+def _bdf_of_render_node(path):
+    """/dev/dri/renderD<N> -> PCI BDF of the GPU behind it (sysfs, no GPU call)."""
+    dev = os.path.realpath("/sys/class/drm/%s/device" % os.path.basename(path))
+    return os.path.basename(dev).lower()
+
+
+def test_allocation_maps_to_the_right_physical_gpu(make_cfg, plugin_dir, amdsmi_backend):
+    """SURVEY.md §7.3 minimum-slice validation: Allocate's DeviceSpecs name the render
+    node of the advertised GPU (checked through sysfs), and a child process restricted
+    to the allocated device (HIP_VISIBLE_DEVICES from the partition's HIP id, as a
+    container that only sees that render node would be) runs a GEMM on the GPU whose
+    PCI address matches the allocation."""
+    import json
+    import subprocess
+    import sys
+
+    from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import KubeletStub
+    from k8s_gpu_device_plugin_amd.plugin.manager import PluginManager
+
+    gpus, _ = amdsmi_backend.discover()
+    by_id = {p.id: (g, p) for g in gpus for p in g.partitions}
+    cfg = make_cfg(backend="amdsmi", migStrategy="single")
+    k = KubeletStub(plugin_dir).start()
+    mgr = PluginManager(cfg)
+    t = mgr.start_background()
+    try:
+        regs = k.wait_for_registrations(1, 20)
+        _, devs = k.watch(regs[0].endpoint).next(10)
+        dev_id = devs[0][0]
+        g, part = by_id[dev_id]
+        resp = k.client(regs[0].endpoint).allocate([dev_id])
+    finally:
+        mgr.stop()
+        t.join(10)
+        k.stop()
+    renders = [s.host_path for s in resp.container_responses[0].devices if "renderD" in s.host_path]
+    assert renders == ["/dev/dri/renderD%d" % part.render_minor], renders
+    assert _bdf_of_render_node(renders[0]) == g.bdf.lower(), (renders[0], g.bdf)
+    code = ("import json, torch; p = torch.cuda.get_device_properties(0); "
+            "a = torch.randn(512, 512, device='cuda', dtype=torch.bfloat16); "
+            "c = (a @ a.T).float(); ref = a.float() @ a.float().T; "
+            "print(json.dumps({'n': torch.cuda.device_count(), 'bus': p.pci_bus_id, 'dom': p.pci_domain_id, "
+            "'dev': p.pci_device_id, 'err': float((c - ref).abs().max() / ref.abs().max())}))")
+    env = dict(os.environ, HIP_VISIBLE_DEVICES=str(part.hip_id))
+    out = subprocess.run([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    bdf = "%04x:%02x:%02x" % (r["dom"], r["bus"], r["dev"])
+    assert r["n"] == 1 and g.bdf.lower().startswith(bdf), (r, g.bdf)
+    assert r["err"] < 2e-2, r

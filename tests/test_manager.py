@@ -260,3 +260,65 @@ def test_cdi_spec_written_and_allocate_names(make_cfg, plugin_dir, run_manager, 
         assert spec["devices"][1]["containerEdits"]["deviceNodes"][0]["path"] == "/dev/dri/renderD129"
         r = k.client("amd-gpu.sock").allocate([ids[1]])
         assert [d.name for d in r.container_responses[0].cdi_devices] == ["amd.com/gpu=" + ids[1]]
+
+
+def _gate_canary(monkeypatch, verdicts):
+    """Replaces the isolated canary with one that blocks until released."""
+    from k8s_gpu_device_plugin_amd.ops import canary
+    gate = threading.Event()
+    calls = []
+
+    def fake_run_isolated(device, nbytes, timeout=120.0):
+        calls.append(device)
+        gate.wait(10)
+        return {"ok": verdicts.pop(0) if verdicts else True, "device": device}
+    monkeypatch.setattr(canary, "run_isolated", fake_run_isolated)
+    return gate, calls
+
+
+def test_recovery_canary_runs_off_the_event_loop(make_cfg, plugin_dir, run_manager, monkeypatch):
+    """post_reset with health.canary: the GPU stays Unhealthy until the canary passes,
+    and the manager keeps serving other events (here /restart) while it runs."""
+    gate, calls = _gate_canary(monkeypatch, [True])
+    be = fixtures.build_backend("2gpu_spx")
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(health={"canary": True}), backend=be)
+        w = k.watch(k.wait_for_registrations(1)[0].endpoint)
+        w.next()
+        be.inject_event(be_event(m, "EVT_PRE_RESET", 1))
+        _, devs = w.next(timeout=5)
+        assert [h for _, h, _ in devs] == ["Healthy", "Unhealthy"]
+        be.inject_event(be_event(m, "EVT_POST_RESET", 1))
+        assert _wait(lambda: calls == [1])
+        m.restart()  # handled while the canary is still blocked
+        assert _wait(lambda: m.counters["restarts_api"] == 1)
+        k.wait_for_registrations(2, timeout=10)
+        time.sleep(0.2)
+        assert m.plugins[0].table.healthy_count() == 1  # reloaded, GPU 1 still held until verified
+        gate.set()
+        assert _wait(lambda: m.plugins and m.plugins[0].table.healthy_count() == 2)
+
+
+def test_stale_canary_verdict_is_dropped(make_cfg, plugin_dir, run_manager, monkeypatch):
+    """A new Unhealthy event while the recovery canary runs wins over its (passing) verdict."""
+    gate, calls = _gate_canary(monkeypatch, [True])
+    be = fixtures.build_backend("2gpu_spx")
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(health={"canary": True}), backend=be)
+        k.wait_for_registrations(1)
+        be.inject_event(be_event(m, "EVT_PRE_RESET", 0))
+        assert _wait(lambda: m.plugins[0].table.healthy_count() == 1)
+        be.inject_event(be_event(m, "EVT_POST_RESET", 0))
+        assert _wait(lambda: calls == [0])
+        be.inject_event(be_event(m, "EVT_PRE_RESET", 0))
+        assert _wait(lambda: m.counters["health_events"] >= 3)
+        gate.set()
+        time.sleep(0.3)
+        assert m.plugins[0].table.healthy_count() == 1
+        assert list(m.health_log)[-1][2] == 0
+
+
+def be_event(m, kind, gpu):
+    from k8s_gpu_device_plugin_amd import native
+    n = native.load()
+    return n.HwEvent(getattr(n, kind), gpu, -1, -1, "test")
