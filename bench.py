@@ -8,15 +8,18 @@ to register with.  Every rank then acts as one kubelet-side client for "its" GPU
 
   step = ALLOCS Allocate RPCs through a compiled HTTP/2 gRPC client (kubelet-like)
        + ALLOCS Allocate RPCs through a persistent grpcio client (BASELINE.md method)
-       + PREFS GetPreferredAllocation RPCs over the whole advertised set (each timed)
-       + SCRAPES GET /metrics on a keep-alive connection (each timed)
+       + PREFS GetPreferredAllocation RPCs over the whole advertised set, compiled
+         client and grpcio client (each timed)
+       + SCRAPE_S seconds of closed-loop GET /metrics on SCRAPE_CONNS keep-alive
+         connections from the compiled load generator (native/loadgen.cpp)
 
 W warm-up steps, then K timed steps bracketed by barrier + torch.cuda.synchronize().
 Work per rank is fixed as N grows (weak scaling).  ``value`` = Allocate p50 in
 microseconds over every compiled-client Allocate of every rank in the timed window (lower
 is better; kubelet is a compiled grpc-go client, and a Python client's own ~80 us per
 call would hide the plugin); the grpcio-client p50/p99 are reported alongside;
-``scrape_rps`` = all ranks' scrapes / the slowest rank's scrape time.  Before timing,
+``scrape_rps`` = all ranks' completed scrapes / the slowest rank's scrape window (the
+ranks scrape concurrently, so this is the daemon's aggregate throughput).  Before timing,
 each rank validates its allocation: the returned render node exists and the gfx950
 canary (HBM pattern + MFMA exactness/throughput) passes on that device.
 
@@ -39,7 +42,8 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-ALLOCS, PREFS, SCRAPES = 256, 32, 32
+ALLOCS, PREFS = 256, 32
+SCRAPE_S, SCRAPE_CONNS = 0.05, 2
 METRIC = "Allocate() p50 latency + /metrics scrape RPS at 1/2/4/8 MI355X advertised"
 
 
@@ -85,12 +89,13 @@ def start_daemon(n_gpus: int, grpc_server: str, workdir: str):
     kubelet = KubeletStub(plugin_dir).start()
     port = _free_port()
     cfg_path = os.path.join(workdir, "bench-config.yml")
+    threads = max(4, n_gpus)  # one server worker per concurrent kubelet-client rank
     with open(cfg_path, "w") as f:
         f.write("webListenAddress: \"127.0.0.1:%d\"\nmigStrategy: none\nbackend: %s\nfixture: %dgpu_spx\n"
                 "devices: \"0-%d\"\npluginDir: \"%s\"\nlog:\n  level: info\n  fileDir: \"\"\n"
-                "http:\n  accessLog: false\n  threads: 4\ngrpc:\n  server: %s\n  threads: 4\n"
+                "http:\n  accessLog: false\n  threads: %d\ngrpc:\n  server: %s\n  threads: %d\n"
                 "telemetry:\n  intervalMs: 1000\n"
-                % (port, backend, n_gpus, n_gpus - 1, plugin_dir, grpc_server))
+                % (port, backend, n_gpus, n_gpus - 1, plugin_dir, threads, grpc_server, threads))
     env = dict(os.environ)
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
     log = open(os.path.join(workdir, "daemon.log"), "w")
@@ -189,8 +194,9 @@ def main() -> int:
     perf = time.perf_counter
 
     def step(rec):
-        a, p, s, an = rec
+        a, p, s, an, pn = rec
         an.extend(h2.bench_unary(v1beta1.METHOD_ALLOCATE, alloc_req, ALLOCS))
+        pn.extend(h2.bench_unary(v1beta1.METHOD_GET_PREFERRED, pref_req, PREFS))
         for _ in range(ALLOCS):
             t0 = perf()
             alloc_raw(alloc_req)
@@ -199,19 +205,21 @@ def main() -> int:
             t0 = perf()
             pref_raw(pref_req)
             p.append(perf() - t0)
-        t_s = perf()
-        for _ in range(SCRAPES):
-            t0 = perf()
-            conn.request("GET", "/metrics")
-            body = conn.getresponse().read()
-            s.append(perf() - t0)
-        return perf() - t_s, len(body)
+        r = n.http_load("127.0.0.1", info["port"], "/metrics", SCRAPE_CONNS, SCRAPE_S, 0.0)
+        if r["errors"]:
+            raise RuntimeError("%d /metrics scrape errors" % r["errors"])
+        s.extend(r["latencies_s"])
+        return r["elapsed_s"], r["bytes"] // max(1, r["ok"])
 
-    junk = ([], [], [], [])
+    conn.request("GET", "/metrics")
+    body = conn.getresponse().read()
+    if b"amdgpu_info{" not in body:
+        raise RuntimeError("/metrics lacks the GPU inventory")
+    junk = ([], [], [], [], [])
     for _ in range(args.warmup):
         step(junk)
     barrier()
-    rec = ([], [], [], [])
+    rec = ([], [], [], [], [])
     scrape_time = 0.0
     t_start = perf()
     for _ in range(args.steps):
@@ -220,7 +228,7 @@ def main() -> int:
     barrier()
     elapsed = perf() - t_start
     mine = {"elapsed": elapsed, "scrape_time": scrape_time, "alloc": rec[0], "pref": rec[1], "scrape": rec[2],
-            "alloc_native": rec[3],
+            "alloc_native": rec[3], "pref_native": rec[4],
             "canary": canary_res, "body": body_len}
     if world > 1:
         gathered = [None] * world
@@ -232,6 +240,7 @@ def main() -> int:
         allocs = [x for g in gathered for x in g["alloc"]]
         allocs_native = [x for g in gathered for x in g["alloc_native"]]
         prefs = [x for g in gathered for x in g["pref"]]
+        prefs_native = [x for g in gathered for x in g["pref_native"]]
         scrapes = [x for g in gathered for x in g["scrape"]]
         t_max = max(g["elapsed"] for g in gathered)
         scrape_t = max(g["scrape_time"] for g in gathered)
@@ -243,8 +252,9 @@ def main() -> int:
             "n_gpus": n_gpus, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(t_max / args.steps * 1e3, 3), "higher_is_better": False, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16",
-            "data": "synthetic kubelet allocation workload (%d Allocate + %d GetPreferredAllocation + %d /metrics "
-                    "per rank per step) against %s-discovered devices" % (ALLOCS, PREFS, SCRAPES, info["backend"]),
+            "data": "synthetic kubelet allocation workload (%d Allocate + %d GetPreferredAllocation per client "
+                    "per rank per step, %d ms of /metrics scraping on %d connections per rank per step) against "
+                    "%s-discovered devices" % (ALLOCS, PREFS, SCRAPE_S * 1e3, SCRAPE_CONNS, info["backend"]),
             "config": {"model": "MI355X device plugin, %s, strategy=none (SPX/NPS1 whole GPUs)" % info["resource"],
                        "global_batch": ALLOCS * world, "seq_len": 0,
                        "parallelism": "%d kubelet-client rank(s), 1 plugin daemon" % world,
@@ -252,9 +262,13 @@ def main() -> int:
             "allocate_p50_us": round(p50, 2), "allocate_p99_us": round(_pct(allocs_native, 0.99) * 1e6, 2),
             "allocate_p50_us_grpcio_client": round(p50_grpcio, 2),
             "allocate_p99_us_grpcio_client": round(_pct(allocs, 0.99) * 1e6, 2),
-            "preferred_p50_us": round(_pct(prefs, 0.5) * 1e6, 2),
+            "preferred_p50_us": round(_pct(prefs_native, 0.5) * 1e6, 2),
+            "preferred_p99_us": round(_pct(prefs_native, 0.99) * 1e6, 2),
+            "preferred_p50_us_grpcio_client": round(_pct(prefs, 0.5) * 1e6, 2),
             "scrape_p50_us": round(_pct(scrapes, 0.5) * 1e6, 2),
             "scrape_rps": round(len(scrapes) / scrape_t, 1) if scrape_t > 0 else None,
+            "scrape_p99_us": round(_pct(scrapes, 0.99) * 1e6, 2),
+            "scrapes": len(scrapes),
             "allocate_calls": len(allocs) + len(allocs_native),
             "metrics_bytes": gathered[0]["body"],
             "canary": ({"arch": can[0]["arch"], "hbm_read_gbps": round(min(c["read_gbps"] for c in can), 1),
