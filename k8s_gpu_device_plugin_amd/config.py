@@ -188,6 +188,24 @@ def from_dict(raw: dict | None) -> Config:
     return cfg
 
 
+def unknown_keys(raw: dict | None) -> list[str]:
+    """Keys the loader ignores (viper ignores them silently; a typo such as
+    ``migStratgy`` would otherwise fall back to a default without a trace)."""
+    out: list[str] = []
+    if not isinstance(raw, dict):
+        return out
+    top = {f.name.lower() for f in dataclasses.fields(Config)} | {"partitionstrategy"}
+    for k, v in raw.items():
+        if str(k).lower() not in top:
+            out.append(str(k))
+            continue
+        for name, cls in _NESTED.items():
+            if str(k).lower() == name.lower() and isinstance(v, dict):
+                sub = {f.name.lower() for f in dataclasses.fields(cls)}
+                out += ["%s.%s" % (k, sk) for sk in v if str(sk).lower() not in sub]
+    return out
+
+
 def apply_env(cfg: Config, environ=None) -> Config:
     environ = os.environ if environ is None else environ
     for f in dataclasses.fields(Config):
@@ -255,6 +273,10 @@ def load(config_file: str | None = "config", search_dirs=(".",), environ=None, r
     if path:
         with open(path, "r", encoding="utf-8") as f:
             raw = yaml.safe_load(f) or {}
+    unknown = unknown_keys(raw)
+    if unknown:
+        from .utils.log import get_logger
+        get_logger("config").warning("ignoring unknown config key(s) in %s: %s", path, ", ".join(unknown))
     cfg = from_dict(copy.deepcopy(raw))
     apply_env(cfg, environ)
     return validate(cfg)

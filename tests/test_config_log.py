@@ -109,3 +109,20 @@ def test_rotation_gzip(tmp_path):
     names = sorted(os.listdir(tmp_path))
     assert any(n.endswith(".gz") for n in names) and len([n for n in names if n.startswith("rot-info")]) <= 4
     L.init_logger("info", None, console=False)
+
+
+def test_unknown_keys_are_reported(tmp_path, caplog):
+    assert C.unknown_keys({"migStratgy": "single", "Log": {"levle": "info", "level": "info"},
+                           "partitionStrategy": "none", "health": {"canary": True}}) == ["migStratgy", "Log.levle"]
+    p = tmp_path / "c.yml"
+    p.write_text("webListenAddress: 127.0.0.1:9\nmigStratgy: single\n")
+    logger = logging.getLogger(L.LOGGER_NAME)
+    old = logger.propagate
+    logger.propagate = True
+    try:
+        with caplog.at_level(logging.WARNING, logger=L.LOGGER_NAME):
+            cfg = C.load(str(p), environ={})
+    finally:
+        logger.propagate = old
+    assert cfg.migStrategy == "none"
+    assert any("migStratgy" in r.getMessage() for r in caplog.records)
