@@ -93,7 +93,7 @@ def _common_flags(sanitize: str | None):
 
 def _link_libs():
     return ["-L" + os.path.join(ROCM, "lib"), "-lamd_smi", "-Wl,-rpath," + os.path.join(ROCM, "lib"),
-            "-pthread"]
+            "-lz", "-pthread"]
 
 
 def _compile_objects(sources, obj_dir, extra_flags, force, jobs, cxx=None, src_dir=NATIVE_DIR):
@@ -204,7 +204,10 @@ def run_fuzzer(target: str, seconds: float = 10.0, force: bool = False, extra_ar
     env["UBSAN_OPTIONS"] = "halt_on_error=1:print_stacktrace=1"
     cmd = [exe, corpus, "-max_total_time=%d" % max(1, int(seconds)), "-timeout=10", "-rss_limit_mb=4096",
            "-max_len=8192", "-print_final_stats=1", "-artifact_prefix=" + artifacts + target + "-"] + list(extra_args)
-    return subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env)
+    with open(os.path.join(BUILD_DIR, "fuzz", "fuzz_%s.log" % target), "w") as f:
+        f.write(p.stdout)
+    return p
 
 
 def hipcc_path() -> str | None:

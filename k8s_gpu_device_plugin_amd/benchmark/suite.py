@@ -103,12 +103,12 @@ def rpc_latency(node, method, req, n_native=10000, n_grpcio=2000):
     return out
 
 
-def scrape(node, conns=4, seconds=2.0, rate=0.0):
-    r = native.load().http_load("127.0.0.1", node.port, "/metrics", conns, seconds, rate)
+def scrape(node, conns=4, seconds=2.0, rate=0.0, gzip=False):
+    r = native.load().http_load("127.0.0.1", node.port, "/metrics", conns, seconds, rate, gzip)
     lat = r["latencies_s"]
     return {"rps": round(r["ok"] / r["elapsed_s"], 1), "errors": r["errors"], "p50_us": us(pct(lat, 0.5)),
             "p99_us": us(pct(lat, 0.99)), "bytes": r["bytes"] // max(1, r["ok"]), "conns": conns,
-            "target_rps": rate or "max", "seconds": seconds}
+            "target_rps": rate or "max", "seconds": seconds, "gzip": gzip}
 
 
 def config1():
@@ -237,7 +237,9 @@ def config5(seconds=10.0):
         return {"config": "Sustained /metrics at 1k RPS, 8 GPUs x 8 partitions, per-partition telemetry",
                 "backend": "fixture:8gpu_cpx_nps4",
                 "sustained_1k": scrape(node, 4, seconds, 1000.0),
-                "max_rate_8conns": scrape(node, 8, 3.0)}
+                "sustained_1k_gzip": scrape(node, 4, seconds, 1000.0, gzip=True),
+                "max_rate_8conns": scrape(node, 8, 3.0),
+                "max_rate_8conns_gzip": scrape(node, 8, 3.0, gzip=True)}
     finally:
         node.close()
 

@@ -12,6 +12,7 @@ reference implementation and for hosts where the native core is being debugged.
 """
 from __future__ import annotations
 
+import gzip
 import http.server
 import socketserver
 import threading
@@ -68,6 +69,11 @@ class WebServer:
         if impl is not None:
             impl.stop()
             log.info("web server stopped")
+
+
+def accepts_gzip(header: str) -> bool:
+    """promhttp ``gzipAccepted``: a comma-separated part equal to ``gzip`` or ``gzip;...``."""
+    return any(p.strip() == "gzip" or p.strip().startswith("gzip;") for p in header.split(","))
 
 
 class _Metrics:
@@ -130,11 +136,13 @@ class PyWebServer:
             def log_message(self, fmt, *args):  # access log goes through our logger
                 log.debug("%s %s", self.address_string(), fmt % args)
 
-            def _send(self, status: int, body: bytes, ctype: str = "application/json") -> None:
+            def _send(self, status: int, body: bytes, ctype: str = "application/json", gz: bool = False) -> None:
                 self.send_response_only(status, {200: "OK", 404: "Not Found", 405: "Method Not Allowed"}.get(status))
                 for k, v in CORS_HEADERS:
                     self.send_header(k, v)
                 self.send_header("Access-Control-Allow-Origin", self.headers.get("Origin") or "*")
+                if gz:
+                    self.send_header("Content-Encoding", "gzip")
                 self.send_header("Content-Length", str(len(body)))
                 self.send_header("Content-Type", ctype)
                 self.send_header("Date", self.date_time_string())
@@ -149,6 +157,7 @@ class PyWebServer:
                 if method == "OPTIONS":
                     return self._send(200, b'{"message":"OK"}\n')
                 t0 = time.perf_counter()
+                gz = False
                 handler = path if path in ROUTES else "/not-found"
                 if handler == "/not-found":
                     status, body, ctype = 404, b'{"message":"Not Found"}\n', "application/json"
@@ -164,8 +173,10 @@ class PyWebServer:
                 else:
                     text = outer.manager.exporter.render() + outer.metrics.render()
                     status, body, ctype = 200, text.encode(), METRICS_CTYPE
+                    if accepts_gzip(self.headers.get("Accept-Encoding", "")):
+                        body, gz = gzip.compress(body, compresslevel=1), True
                 outer.metrics.observe(method, handler, status, time.perf_counter() - t0)
-                self._send(status, body, ctype)
+                self._send(status, body, ctype, gz)
 
             def do_GET(self):
                 self._route("GET")

@@ -545,16 +545,16 @@ PYBIND11_MODULE(_native, m) {
   };
   m.def("http_load",
         [load_dict](const std::string& host, int port, const std::string& path, int conns, double duration_s,
-                    double target_rps) {
+                    double target_rps, bool accept_gzip) {
           LoadResult r;
           {
             py::gil_scoped_release rel;
-            r = http_load(host, port, path, conns, duration_s, target_rps);
+            r = http_load(host, port, path, conns, duration_s, target_rps, accept_gzip);
           }
           return load_dict(r);
         },
         py::arg("host"), py::arg("port"), py::arg("path") = "/metrics", py::arg("conns") = 4,
-        py::arg("duration_s") = 2.0, py::arg("target_rps") = 0.0);
+        py::arg("duration_s") = 2.0, py::arg("target_rps") = 0.0, py::arg("accept_gzip") = false);
   m.def("grpc_load",
         [load_dict](const std::string& sock, const std::string& method, const py::bytes& req, int conns,
                     double duration_s) {

@@ -11,6 +11,8 @@
 #include <sys/un.h>
 #include <unistd.h>
 
+#include <dirent.h>
+
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -22,6 +24,27 @@
 using namespace amdgpu_dp;
 
 namespace {
+
+// Every connection the harness opened has been closed by then; a growing count means
+// the server leaks descriptors (or connections it never closes).
+int open_fds() {
+  int n = 0;
+  if (DIR* d = opendir("/proc/self/fd")) {
+    while (readdir(d)) ++n;
+    closedir(d);
+  }
+  return n;
+}
+int g_fd_baseline = -1;
+
+void check_fds() {
+  const int n = open_fds();
+  if (g_fd_baseline < 0) g_fd_baseline = n;
+  if (n > g_fd_baseline + 64) {
+    std::fprintf(stderr, "descriptor leak: %d open fds (baseline %d)\n", n, g_fd_baseline);
+    std::abort();
+  }
+}
 
 std::unique_ptr<GrpcServer> g_srv;
 std::string g_path;
@@ -119,6 +142,9 @@ extern "C" int LLVMFuzzerInitialize(int*, char***) {
 
 extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
   one_connection(data, size);
-  if ((++g_iter & 255) == 0) liveness_check();
+  if ((++g_iter & 255) == 0) {
+    liveness_check();
+    check_fds();
+  }
   return 0;
 }

@@ -12,6 +12,8 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <dirent.h>
+
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -24,6 +26,27 @@
 using namespace amdgpu_dp;
 
 namespace {
+
+// Every connection the harness opened has been closed by then; a growing count means
+// the server leaks descriptors (or connections it never closes).
+int open_fds() {
+  int n = 0;
+  if (DIR* d = opendir("/proc/self/fd")) {
+    while (readdir(d)) ++n;
+    closedir(d);
+  }
+  return n;
+}
+int g_fd_baseline = -1;
+
+void check_fds() {
+  const int n = open_fds();
+  if (g_fd_baseline < 0) g_fd_baseline = n;
+  if (n > g_fd_baseline + 64) {
+    std::fprintf(stderr, "descriptor leak: %d open fds (baseline %d)\n", n, g_fd_baseline);
+    std::abort();
+  }
+}
 
 std::shared_ptr<Exporter> g_ex;
 std::unique_ptr<HttpServer> g_http;
@@ -77,6 +100,8 @@ extern "C" int LLVMFuzzerInitialize(int*, char***) {
     fuzzutil::write_seed(dir, "post_body", "POST /health HTTP/1.1\r\nContent-Length: 5\r\n\r\nhelloGET /nope HTTP/1.0\r\n\r\n");
     fuzzutil::write_seed(dir, "keepalive_10", "GET /health HTTP/1.0\r\nConnection: keep-alive\r\n\r\n"
                                               "DELETE /metrics HTTP/1.1\r\nConnection: close\r\n\r\n");
+    fuzzutil::write_seed(dir, "metrics_gzip", "GET /metrics HTTP/1.1\r\nAccept-Encoding: deflate, gzip;q=1\r\n\r\n"
+                                              "GET /metrics HTTP/1.1\r\naccept-encoding: br\r\n\r\n");
     fuzzutil::write_seed(dir, "chunked", "PUT / HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n5\r\nhello\r\n0\r\n\r\n");
     std::exit(0);
   }
@@ -109,6 +134,7 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
     std::abort();
   }
   if ((++g_iter & 255) == 0) {
+    check_fds();
     static const char kHealth[] = "GET /health HTTP/1.1\r\nConnection: close\r\n\r\n";
     const std::string r = roundtrip(kHealth, sizeof(kHealth) - 1);
     if (r.compare(0, 15, "HTTP/1.1 200 OK") != 0) {

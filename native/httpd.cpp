@@ -67,6 +67,23 @@ bool ieq(const char* a, size_t n, const char* b) {
   return true;
 }
 
+// promhttp's gzipAccepted: any comma-separated part equal to "gzip" or starting with
+// "gzip;" (q-values are not weighed, as in the reference's client_golang v1.19).
+bool accepts_gzip(const std::string& v) {
+  size_t i = 0;
+  while (i <= v.size()) {
+    size_t j = v.find(',', i);
+    if (j == std::string::npos) j = v.size();
+    size_t a = i, b = j;
+    while (a < b && (v[a] == ' ' || v[a] == '\t')) ++a;
+    while (b > a && (v[b - 1] == ' ' || v[b - 1] == '\t')) --b;
+    const std::string part = v.substr(a, b - a);
+    if (part == "gzip" || part.compare(0, 5, "gzip;") == 0) return true;
+    i = j + 1;
+  }
+  return false;
+}
+
 std::string http_date() {
   char buf[64];
   time_t t = time(nullptr);
@@ -280,7 +297,7 @@ int HttpServer::start() {
               }
               std::string origin, hosth, ua;
               size_t content_len = 0;
-              bool conn_close = false, conn_keep = false, chunked = false;
+              bool conn_close = false, conn_keep = false, chunked = false, gzip_ok = false;
               const char* q = le ? le + 1 : p + hlen;
               const char* hend = p + hlen;
               while (q < hend) {
@@ -299,6 +316,7 @@ int HttpServer::start() {
                   else if (ieq(q, nlen, "user-agent")) ua = val;
                   else if (ieq(q, nlen, "content-length")) content_len = std::strtoull(val.c_str(), nullptr, 10);
                   else if (ieq(q, nlen, "transfer-encoding")) chunked = true;
+                  else if (ieq(q, nlen, "accept-encoding")) gzip_ok = gzip_ok || accepts_gzip(val);
                   else if (ieq(q, nlen, "connection")) {
                     std::string lv = val;
                     std::transform(lv.begin(), lv.end(), lv.begin(), ::tolower);
@@ -331,7 +349,7 @@ int HttpServer::start() {
               } else {
                 const size_t qm = uri.find('?');
                 handle(method, qm == std::string::npos ? uri : uri.substr(0, qm), origin, keep, http10, &o, &status,
-                       &body_bytes);
+                       &body_bytes, gzip_ok);
               }
               const double dt = (mono_ns() - t0) * 1e-9;
               requests_.fetch_add(1, std::memory_order_relaxed);
@@ -395,13 +413,15 @@ void HttpServer::record(int mi, int hi, int status, double seconds) {
 }
 
 void HttpServer::handle(const std::string& method, const std::string& path, const std::string& origin,
-                        bool keep_alive, bool http10, std::string* out, int* status_out, size_t* body_bytes_out) {
+                        bool keep_alive, bool http10, std::string* out, int* status_out, size_t* body_bytes_out,
+                        bool gzip_ok) {
   const int64_t t0 = mono_ns();
   int status = 200;
   std::string body;
   const char* ctype = "application/json";
   int handler = -1;
   const bool cors = true;
+  bool gz = false;
   if (method.empty()) {
     status = *status_out ? *status_out : 400;
     body = std::string("{\"message\":\"") + reason(status) + "\"}\n";
@@ -435,9 +455,17 @@ void HttpServer::handle(const std::string& method, const std::string& path, cons
       body = "{\"code\":0,\"data\":\"ok\",\"msg\":\"success\"}\n";
     } else {  // /metrics
       ctype = "text/plain; version=0.0.4; charset=utf-8";
-      body.reserve(64 * 1024);
-      if (exporter_) exporter_->render(&body);
-      render_http_metrics(&body);
+      if (gzip_ok) {  // promhttp compresses when the scraper accepts gzip (Prometheus does)
+        std::string httpm;
+        render_http_metrics(&httpm);
+        if (exporter_) exporter_->render_gzip(&body, httpm);
+        else gzip_member(httpm.data(), httpm.size(), &body);
+        gz = true;
+      } else {
+        body.reserve(64 * 1024);
+        if (exporter_) exporter_->render(&body);
+        render_http_metrics(&body);
+      }
     }
     const double dt = (mono_ns() - t0) * 1e-9;
     record(method_index(method), handler, status, dt);
@@ -460,9 +488,12 @@ void HttpServer::handle(const std::string& method, const std::string& path, cons
   }
   if (!keep_alive) o.append("Connection: close\r\n");
   else if (http10) o.append("Connection: keep-alive\r\n");
+  if (gz) o.append("Content-Encoding: gzip\r\n");
   o.append("Content-Length: ").append(std::to_string(body.size())).append("\r\n");
   o.append("Content-Type: ").append(ctype).append("\r\n");
-  o.append("Date: ").append(date).append("\r\n\r\n");
+  o.append("Date: ").append(date).append("\r\n");
+  if (handler == 1) o.append("Vary: Accept-Encoding\r\n");
+  o.append("\r\n");
   o.append(body);
   *status_out = status;
   *body_bytes_out = body.size();

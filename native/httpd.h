@@ -54,7 +54,7 @@ class HttpServer {
  private:
   friend struct Worker;
   void handle(const std::string& method, const std::string& path, const std::string& origin, bool keep_alive,
-              bool http10, std::string* out, int* status_out, size_t* body_bytes_out);
+              bool http10, std::string* out, int* status_out, size_t* body_bytes_out, bool gzip_ok = false);
   void record(int method_idx, int handler_idx, int status, double seconds);
   void log_access(const std::string& remote, const std::string& host, const std::string& method,
                   const std::string& uri, const std::string& ua, int status, double seconds, size_t bytes_in,

@@ -71,13 +71,14 @@ bool read_response(int fd, std::string* buf, size_t* body_len, int* status) {
 }  // namespace
 
 LoadResult http_load(const std::string& host, int port, const std::string& path, int conns, double duration_s,
-                     double target_rps) {
+                     double target_rps, bool accept_gzip) {
   LoadResult total;
   std::mutex mu;
   std::vector<std::thread> ts;
   const int64_t t0 = mono_ns() + 2000000;  // common start 2 ms out
   const int64_t t_end = t0 + static_cast<int64_t>(duration_s * 1e9);
-  const std::string req = "GET " + path + " HTTP/1.1\r\nHost: " + host + "\r\nUser-Agent: amdgpu-dp-loadgen\r\n\r\n";
+  const std::string req = "GET " + path + " HTTP/1.1\r\nHost: " + host + "\r\nUser-Agent: amdgpu-dp-loadgen\r\n" +
+                          (accept_gzip ? "Accept-Encoding: gzip\r\n" : "") + "\r\n";
   for (int c = 0; c < conns; ++c) {
     ts.emplace_back([&, c] {
       LoadResult r;

@@ -21,7 +21,7 @@ struct LoadResult {
 };
 
 LoadResult http_load(const std::string& host, int port, const std::string& path, int conns, double duration_s,
-                     double target_rps);
+                     double target_rps, bool accept_gzip = false);
 
 LoadResult grpc_load(const std::string& socket_path, const std::string& method, const std::string& req, int conns,
                      double duration_s);

@@ -213,7 +213,8 @@ static void test_exporter_httpd_health(std::shared_ptr<FixtureBackend> be) {
           close(fd);
           continue;
         }
-        const char* req = (k % 3 == 0) ? "GET /metrics HTTP/1.1\r\nConnection: close\r\n\r\n"
+        const char* req = (k % 3 == 0) ? (k % 2 ? "GET /metrics HTTP/1.1\r\nAccept-Encoding: gzip\r\nConnection: close\r\n\r\n"
+                                                : "GET /metrics HTTP/1.1\r\nConnection: close\r\n\r\n")
                                        : (i == 0 && k == 1 ? "GET /restart HTTP/1.1\r\nConnection: close\r\n\r\n"
                                                            : "GET /health HTTP/1.1\r\nConnection: close\r\n\r\n");
         (void)!write(fd, req, std::strlen(req));

@@ -1,5 +1,7 @@
 #include "telemetry.h"
 
+#include <zlib.h>
+
 #include <unistd.h>
 
 #include <algorithm>
@@ -11,6 +13,47 @@
 #include <sys/resource.h>
 
 namespace amdgpu_dp {
+
+namespace {
+
+// deflateInit2 allocates and clears ~256 KiB of state; a scrape-path compressor reuses
+// one stream per thread (deflateReset) instead.
+struct ThreadDeflater {
+  z_stream zs{};
+  int level = -100;
+  bool live = false;
+  ~ThreadDeflater() {
+    if (live) deflateEnd(&zs);
+  }
+  z_stream* get(int lvl) {
+    if (live && level == lvl) {
+      deflateReset(&zs);
+      return &zs;
+    }
+    if (live) deflateEnd(&zs);
+    zs = z_stream{};
+    live = deflateInit2(&zs, lvl, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) == Z_OK;
+    if (!live) throw std::runtime_error("deflateInit2 failed");
+    level = lvl;
+    return &zs;
+  }
+};
+
+}  // namespace
+
+void gzip_member(const char* data, size_t n, std::string* out, int level) {
+  static thread_local ThreadDeflater td;
+  z_stream* zs = td.get(level);
+  const size_t base = out->size();
+  out->resize(base + deflateBound(zs, static_cast<uLong>(n)));
+  zs->next_in = reinterpret_cast<Bytef*>(const_cast<char*>(data));
+  zs->avail_in = static_cast<uInt>(n);
+  zs->next_out = reinterpret_cast<Bytef*>(&(*out)[base]);
+  zs->avail_out = static_cast<uInt>(out->size() - base);
+  const int rc = deflate(zs, Z_FINISH);
+  out->resize(base + zs->total_out);
+  if (rc != Z_STREAM_END) throw std::runtime_error("deflate did not finish");
+}
 
 Exporter::Exporter()
     : sample_hist_({1e-4, 2.5e-4, 5e-4, 1e-3, 2.5e-3, 5e-3, 1e-2, 2.5e-2, 5e-2, 0.1, 0.25, 0.5, 1.0}) {
@@ -35,6 +78,7 @@ void Exporter::set_partition_labels(const std::vector<PartitionLabel>& labels) {
 void Exporter::set_build_info(const std::string& rendered) {
   std::lock_guard<std::mutex> lk(mu_);
   build_info_ = rendered;
+  ++build_info_version_;
 }
 
 void Exporter::set_tables(const std::vector<std::shared_ptr<DeviceTable>>& tables) {
@@ -378,7 +422,11 @@ void Exporter::render_process(std::string* out) const {
   out->append(o);
 }
 
-void Exporter::render(std::string* out) const {
+// The exposition is assembled from segments so the gzip path can cache the big,
+// slowly-changing ones: [inventory + per-tick GPU text] changes once per sampling
+// tick, [device health] once per table version; the rest is small and per-scrape.
+void Exporter::render_parts(std::shared_ptr<const std::string>* head, std::string* counters,
+                            std::shared_ptr<const std::string>* health, std::string* tail) const {
   std::shared_ptr<const std::string> gt, extra;
   std::vector<std::shared_ptr<DeviceTable>> tables;
   {
@@ -386,22 +434,30 @@ void Exporter::render(std::string* out) const {
     gt = gpu_text_;
     extra = extra_;
     tables = tables_;
-    out->append(build_info_);
+    if (head_src_ != gt || head_build_ != build_info_version_) {
+      auto h = std::make_shared<std::string>();
+      h->reserve(build_info_.size() + gt->size());
+      h->append(build_info_).append(*gt);
+      head_ = std::move(h);
+      head_src_ = gt;
+      head_build_ = build_info_version_;
+    }
+    *head = head_;
   }
-  out->append(*gt);
-  append_header(out, "amdgpu_telemetry_samples_total", "Telemetry sampling passes completed.", "counter");
-  out->append("amdgpu_telemetry_samples_total ");
-  append_u64(out, samples_.load());
-  out->push_back('\n');
-  append_header(out, "amdgpu_telemetry_sample_errors_total", "Per-GPU telemetry sample failures.", "counter");
-  out->append("amdgpu_telemetry_sample_errors_total ");
-  append_u64(out, sample_errors_.load());
-  out->push_back('\n');
+  append_header(counters, "amdgpu_telemetry_samples_total", "Telemetry sampling passes completed.", "counter");
+  counters->append("amdgpu_telemetry_samples_total ");
+  append_u64(counters, samples_.load());
+  counters->push_back('\n');
+  append_header(counters, "amdgpu_telemetry_sample_errors_total", "Per-GPU telemetry sample failures.", "counter");
+  counters->append("amdgpu_telemetry_sample_errors_total ");
+  append_u64(counters, sample_errors_.load());
+  counters->push_back('\n');
   if (sample_hist_.count()) {
-    append_header(out, "amdgpu_telemetry_sample_duration_seconds", "Wall time of one sampling pass over all GPUs.",
+    append_header(counters, "amdgpu_telemetry_sample_duration_seconds", "Wall time of one sampling pass over all GPUs.",
                   "histogram");
-    sample_hist_.render(out, "amdgpu_telemetry_sample_duration_seconds", "");
+    sample_hist_.render(counters, "amdgpu_telemetry_sample_duration_seconds", "");
   }
+  health->reset();
   if (!tables.empty()) {
     std::vector<uint64_t> key;
     key.reserve(tables.size() * 2);
@@ -411,9 +467,9 @@ void Exporter::render(std::string* out) const {
     }
     {
       std::lock_guard<std::mutex> hk(health_mu_);
-      if (key != health_key_) {
-        health_cache_.clear();
-        append_header(&health_cache_, "amdgpu_device_plugin_device_health",
+      if (key != health_key_ || !health_cache_) {
+        auto hc = std::make_shared<std::string>();
+        append_header(hc.get(), "amdgpu_device_plugin_device_health",
                       "1 if the advertised device is Healthy, 0 if Unhealthy.", "gauge");
         std::string l;
         for (const auto& t : tables) {
@@ -424,12 +480,13 @@ void Exporter::render(std::string* out) const {
             l.append("\",device_id=\"");
             append_label_value(&l, d.id);
             l.append("\"");
-            line(&health_cache_, "amdgpu_device_plugin_device_health", l, t->healthy(d.id) ? 1 : 0);
+            line(hc.get(), "amdgpu_device_plugin_device_health", l, t->healthy(d.id) ? 1 : 0);
           }
         }
+        health_cache_ = std::move(hc);
         health_key_ = key;
       }
-      out->append(health_cache_);
+      *health = health_cache_;
     }
     bool any = false;
     for (const auto& t : tables) {
@@ -437,14 +494,53 @@ void Exporter::render(std::string* out) const {
       t->render_metrics(&tmp, false);
       if (tmp.empty()) continue;
       if (!any) {
-        DeviceTable::render_metric_headers(out);
+        DeviceTable::render_metric_headers(tail);
         any = true;
       }
-      out->append(tmp);
+      tail->append(tmp);
     }
   }
-  out->append(*extra);
-  render_process(out);
+  tail->append(*extra);
+  render_process(tail);
+}
+
+void Exporter::render(std::string* out) const {
+  std::shared_ptr<const std::string> head, health;
+  std::string counters, tail;
+  render_parts(&head, &counters, &health, &tail);
+  out->append(*head).append(counters);
+  if (health) out->append(*health);
+  out->append(tail);
+}
+
+void Exporter::render_gzip(std::string* out, std::string_view trailer) const {
+  std::shared_ptr<const std::string> head, health;
+  std::string dyn, tail;
+  render_parts(&head, &dyn, &health, &tail);
+  {
+    std::lock_guard<std::mutex> lk(gz_mu_);
+    if (gz_head_src_ != head) {
+      gz_head_.clear();
+      gzip_member(head->data(), head->size(), &gz_head_);
+      gz_head_src_ = head;
+    }
+    out->append(gz_head_);
+    if (health) {
+      if (gz_health_src_ != health) {
+        gz_health_.clear();
+        gzip_member(health->data(), health->size(), &gz_health_);
+        gz_health_src_ = health;
+      }
+    }
+  }
+  // members must follow the plain-text order: head, counters, health, tail + trailer
+  gzip_member(dyn.data(), dyn.size(), out);
+  if (health) {
+    std::lock_guard<std::mutex> lk(gz_mu_);
+    out->append(gz_health_);
+  }
+  tail.append(trailer.data(), trailer.size());
+  gzip_member(tail.data(), tail.size(), out);
 }
 
 }  // namespace amdgpu_dp

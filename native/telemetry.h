@@ -12,6 +12,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <string_view>
 #include <thread>
 #include <vector>
 
@@ -21,6 +22,10 @@
 #include "metrics.h"
 
 namespace amdgpu_dp {
+
+// Appends one complete gzip member (RFC 1952) of data[0, n).  Concatenated members
+// form a valid multi-member gzip stream (Go's gzip.Reader, Python's gzip, curl).
+void gzip_member(const char* data, size_t n, std::string* out, int level = 1);
 
 struct PartitionLabel {
   int gpu = -1;
@@ -51,12 +56,19 @@ class Exporter {
   GpuSample last_sample(int gpu) const;
   // Full exposition (everything except the HTTP server's own echo_http_* families).
   void render(std::string* out) const;
+  // Same exposition + `trailer` (the HTTP server's families) as a multi-member gzip
+  // stream.  The inventory/GPU-text member is compressed once per sampling tick and
+  // the device-health member once per table version; only the small per-scrape parts
+  // are compressed on the request path.
+  void render_gzip(std::string* out, std::string_view trailer) const;
   uint64_t samples_total() const { return samples_.load(); }
 
  private:
   void loop();
   void render_gpu_text(const std::vector<GpuSample>& samples, const std::vector<char>& ok, double sample_s);
   void render_process(std::string* out) const;
+  void render_parts(std::shared_ptr<const std::string>* head, std::string* counters,
+                    std::shared_ptr<const std::string>* health, std::string* tail) const;
 
   mutable std::mutex mu_;
   std::vector<GpuInfo> gpus_;
@@ -64,6 +76,10 @@ class Exporter {
   std::vector<GpuSample> last_;
   std::vector<std::shared_ptr<DeviceTable>> tables_;
   std::string build_info_;
+  uint64_t build_info_version_ = 0;
+  mutable std::shared_ptr<const std::string> head_;      // build_info_ + *gpu_text_
+  mutable std::shared_ptr<const std::string> head_src_;  // gpu_text_ that head_ was built from
+  mutable uint64_t head_build_ = 0;
   std::shared_ptr<const std::string> extra_;
   std::shared_ptr<const std::string> gpu_text_;
 
@@ -81,7 +97,11 @@ class Exporter {
   // device-health block, re-rendered only when a table's version changes
   mutable std::mutex health_mu_;
   mutable std::vector<uint64_t> health_key_;
-  mutable std::string health_cache_;
+  mutable std::shared_ptr<const std::string> health_cache_;
+  // gzip members cached against the exact segment objects they were compressed from
+  mutable std::mutex gz_mu_;
+  mutable std::string gz_head_, gz_health_;
+  mutable std::shared_ptr<const std::string> gz_head_src_, gz_health_src_;
   mutable std::mutex proc_mu_;
   mutable std::string proc_cache_;
   mutable int64_t proc_cache_ns_ = 0;

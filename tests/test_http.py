@@ -89,6 +89,34 @@ def test_metrics_exposition_is_valid_and_complete(web):
                    "2", "5", "10", "15", "20", "30", "+Inf"]  # Go FormatFloat(g, -1)
 
 
+def test_metrics_gzip_negotiation(web):
+    """promhttp compresses /metrics for scrapers sending Accept-Encoding: gzip (Prometheus
+    does).  The native server sends a multi-member gzip stream whose large members are
+    cached per sampling tick; it must decode to the same exposition as a plain scrape."""
+    import gzip
+    port, _, kind = web
+    get(port, "/health")  # so the echo_http families exist in every scrape below
+    st, h, plain = get(port, "/metrics")
+    assert "Content-Encoding" not in h
+    for ae in ("gzip", "deflate, gzip;q=1.0", "br,gzip"):
+        st, h, body = get(port, "/metrics", headers={"Accept-Encoding": ae})
+        assert st == 200 and h["Content-Encoding"] == "gzip", (ae, h)
+        text = gzip.decompress(body).decode()
+        fams = {f.name for f in text_string_to_metric_families(text)}
+        assert fams == {f.name for f in text_string_to_metric_families(plain.decode())}
+        # everything but the per-request counters is identical
+        strip = lambda t: [ln for ln in t.splitlines() if not ln.startswith(("echo_http", "process_"))]  # noqa: E731
+        assert strip(text) == strip(plain.decode())
+        assert len(body) < len(plain) / 3
+    st, h, body = get(port, "/metrics", headers={"Accept-Encoding": "identity, gzipx"})
+    assert "Content-Encoding" not in h and body.startswith(b"# HELP")
+    if kind == "native":  # cached head member: byte-identical across scrapes within a tick
+        a = get(port, "/metrics", headers={"Accept-Encoding": "gzip"})[2]
+        b = get(port, "/metrics", headers={"Accept-Encoding": "gzip"})[2]
+        head = min(len(a), len(b)) // 2
+        assert a[:head] == b[:head]
+
+
 def test_keepalive_and_pipelining(web):
     port, _, kind = web
     c = http.client.HTTPConnection("127.0.0.1", port, timeout=5)
