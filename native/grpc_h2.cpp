@@ -410,32 +410,38 @@ void GrpcServer::run(Worker* w) {
     std::string out;
     bool ok = true;
     int rpc = kRpcAllocate;
-    switch (m) {
-      case kMAllocate:
-        ok = table->allocate(msg, &out);
-        break;
-      case kMPreferred:
-        rpc = kRpcPreferred;
-        ok = table->preferred(msg, &out);
-        break;
-      case kMOptions:
-        rpc = kRpcOptions;
-        out = table->options_bytes();
-        break;
-      case kMPreStart:
-        rpc = kRpcPreStart;
-        break;
-      case kMLaw: {
-        rpc = kRpcListAndWatch;
-        s.law = true;
-        s.law_version = table->version();
-        send_headers(c, sid);
-        send_message(c, sid, s, table->list_and_watch(), false);
-        table->observe(rpc, (mono_ns() - t0) * 1e-9, false);
-        return;
+    try {
+      switch (m) {
+        case kMAllocate:
+          ok = table->allocate(msg, &out);
+          break;
+        case kMPreferred:
+          rpc = kRpcPreferred;
+          ok = table->preferred(msg, &out);
+          break;
+        case kMOptions:
+          rpc = kRpcOptions;
+          out = table->options_bytes();
+          break;
+        case kMPreStart:
+          rpc = kRpcPreStart;
+          break;
+        case kMLaw: {
+          rpc = kRpcListAndWatch;
+          s.law = true;
+          s.law_version = table->version();
+          send_headers(c, sid);
+          send_message(c, sid, s, table->list_and_watch(), false);
+          table->observe(rpc, (mono_ns() - t0) * 1e-9, false);
+          return;
+        }
+        default:
+          break;
       }
-      default:
-        break;
+    } catch (const std::exception& e) {  // e.g. bad_alloc on a hostile request: INTERNAL, keep serving
+      send_error(c, sid, s, 13, std::string("internal error: ") + e.what());
+      table->observe(rpc, (mono_ns() - t0) * 1e-9, true);
+      return;
     }
     if (ok) {
       send_headers(c, sid);

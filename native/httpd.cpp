@@ -429,7 +429,7 @@ void HttpServer::handle(const std::string& method, const std::string& path, cons
     // server/server.go:92-94: Cros answers every OPTIONS with HTTPError(200); echo's
     // error handler renders {"message":"OK"}.  Logger/Metrics are not reached.
     body = "{\"message\":\"OK\"}\n";
-  } else {
+  } else try {
     if (path == "/") handler = 0;
     else if (path == "/metrics") handler = 1;
     else if (path == "/health") handler = 2;
@@ -469,6 +469,13 @@ void HttpServer::handle(const std::string& method, const std::string& path, cons
     }
     const double dt = (mono_ns() - t0) * 1e-9;
     record(method_index(method), handler, status, dt);
+  } catch (const std::exception& e) {  // echo's Recover middleware: a failing handler is a 500, not a crash
+    status = 500;
+    body = "{\"message\":\"Internal Server Error\"}\n";
+    ctype = "application/json";
+    gz = false;
+    std::fprintf(stderr, "httpd: handler for %s %s failed: %s\n", method.c_str(), path.c_str(), e.what());
+    if (handler >= 0) record(method_index(method), handler, status, (mono_ns() - t0) * 1e-9);
   }
   static thread_local std::string date;
   static thread_local int64_t date_ns = 0;
