@@ -8,6 +8,7 @@
 #include <amd_smi/amdsmi.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -81,6 +82,16 @@ struct Proc {
   uint32_t partition_id;
 };
 
+// Processors a compute-partition mode implies on CDNA3/4 (8 XCDs on MI355X); 0 = unknown.
+int partitions_of_mode(const std::string& mode) {
+  if (mode == "SPX") return 1;
+  if (mode == "DPX") return 2;
+  if (mode == "TPX") return 3;
+  if (mode == "QPX") return 4;
+  if (mode == "CPX") return 8;
+  return 0;
+}
+
 }  // namespace
 
 bool amdsmi_available() {
@@ -117,16 +128,54 @@ class AmdSmiBackend : public Backend {
   void discover(std::vector<GpuInfo>* gpus, Topology* topo) override {
     std::lock_guard<std::mutex> lk(mu_);
     if (closed_) throw std::runtime_error("amdsmi backend is shut down");
-    // periodic re-discovery must not silently drop event delivery: re-arm afterwards
+    discover_locked(gpus, topo);
+    // amdsmi enumerates processors once, at amdsmi_init.  After an operator switches a
+    // GPU's compute partition mode (amd-smi set --compute-partition), the cached handle
+    // list no longer matches the mode the GPU reports: re-initialise and enumerate again.
+    bool stale = false;
+    for (const auto& g : *gpus) {
+      const int want = partitions_of_mode(g.compute_partition);
+      if (want > 0 && want != static_cast<int>(g.partitions.size())) stale = true;
+    }
+    if (stale && reinit_locked()) discover_locked(gpus, topo);
+    // keep event delivery armed across periodic re-discovery; re-arm only when the
+    // processor set changed (handles from a re-init are new objects)
+    std::vector<amdsmi_processor_handle> flat;
+    for (const auto& hs : procs_) flat.insert(flat.end(), hs.begin(), hs.end());
+    if (armed_ && flat != armed_for_) {
+      disarm_locked();
+      arm_locked();
+    }
+  }
+
+  bool reinit() override {
+    std::lock_guard<std::mutex> lk(mu_);
+    return !closed_ && reinit_locked();
+  }
+
+  int reinit_count() const override {
+    std::lock_guard<std::mutex> lk(mu_);
+    return reinits_;
+  }
+
+ private:
+  // amdsmi is process-global: only the sole owner may shut it down and start it again.
+  bool reinit_locked() {
+    std::lock_guard<std::mutex> ilk(g_init_mu);
+    if (g_init_refs != 1) return false;
     const bool was_armed = armed_;
     disarm_locked();
-    struct Rearm {
-      AmdSmiBackend* self;
-      bool on;
-      ~Rearm() {
-        if (on) self->arm_locked();
-      }
-    } rearm{this, was_armed};
+    procs_.clear();
+    std::lock_guard<std::mutex> ek(evt_mu_);  // no event wait may run across shut-down/init
+    amdsmi_shut_down();
+    check(amdsmi_init(AMDSMI_INIT_AMD_GPUS), "amdsmi_init (re-init)");
+    ++reinits_;
+    armed_ = false;
+    if (was_armed) want_rearm_ = true;
+    return true;
+  }
+
+  void discover_locked(std::vector<GpuInfo>* gpus, Topology* topo) {
     uint32_t nsock = 0;
     check(amdsmi_get_socket_handles(&nsock, nullptr), "amdsmi_get_socket_handles(count)");
     std::vector<amdsmi_socket_handle> socks(nsock);
@@ -246,8 +295,13 @@ class AmdSmiBackend : public Backend {
         if (s.link_peer[k] >= 0 && s.link_up[k] == 0) topo->at(a, s.link_peer[k]).up = topo->at(s.link_peer[k], a).up = false;
     }
     gpus_ = *gpus;
+    if (want_rearm_) {
+      want_rearm_ = false;
+      arm_locked();
+    }
   }
 
+ public:
   bool sample(int gpu, GpuSample* s) override {
     std::lock_guard<std::mutex> lk(mu_);
     if (closed_ || gpu < 0 || gpu >= static_cast<int>(procs_.size())) return false;
@@ -326,7 +380,9 @@ class AmdSmiBackend : public Backend {
                           AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_THERMAL_THROTTLE) |
                           AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_VMFAULT);
     armed_handles_.clear();
+    armed_for_.clear();
     for (auto& handles : procs_) {
+      armed_for_.insert(armed_for_.end(), handles.begin(), handles.end());
       for (auto h : handles) {
         if (amdsmi_init_gpu_event_notification(h) != AMDSMI_STATUS_SUCCESS) continue;
         if (amdsmi_set_gpu_event_notification_mask(h, mask) != AMDSMI_STATUS_SUCCESS) {
@@ -337,6 +393,7 @@ class AmdSmiBackend : public Backend {
       }
     }
     armed_ = true;
+    evt_live_.store(!armed_handles_.empty());
   }
 
   int armed_event_sources() const override {
@@ -344,21 +401,27 @@ class AmdSmiBackend : public Backend {
     return static_cast<int>(armed_handles_.size());
   }
 
+  // Lock order: mu_ -> evt_mu_ (disarm/re-init); the blocking wait holds only evt_mu_
+  // and takes mu_ after releasing it, so disarming waits for an in-flight wait to
+  // return instead of stopping notification underneath it.
   int wait_events(int timeout_ms, std::vector<HwEvent>* out) override {
-    bool armed;
+    amdsmi_evt_notification_data_t data[16];
+    uint32_t num = 16;
+    amdsmi_status_t st = AMDSMI_STATUS_NOT_INIT;
+    bool waited = false;
     {
-      std::lock_guard<std::mutex> lk(mu_);
-      armed = armed_ && !armed_handles_.empty() && !closed_;
+      std::lock_guard<std::mutex> ek(evt_mu_);
+      if (evt_live_.load()) {
+        st = amdsmi_get_gpu_event_notification(timeout_ms, &num, data);
+        waited = true;
+      }
     }
-    if (!armed) {
+    if (!waited) {
       // nothing armed (e.g. unprivileged container): the health monitor polls instead
       struct timespec ts{timeout_ms / 1000, (timeout_ms % 1000) * 1000000L};
       nanosleep(&ts, nullptr);
       return 0;
     }
-    amdsmi_evt_notification_data_t data[16];
-    uint32_t num = 16;
-    amdsmi_status_t st = amdsmi_get_gpu_event_notification(timeout_ms, &num, data);
     if (st != AMDSMI_STATUS_SUCCESS) return 0;
     int added = 0;
     std::lock_guard<std::mutex> lk(mu_);
@@ -435,16 +498,23 @@ class AmdSmiBackend : public Backend {
 
   void disarm_locked() {
     if (!armed_) return;
+    evt_live_.store(false);
+    std::lock_guard<std::mutex> ek(evt_mu_);
     for (auto h : armed_handles_) amdsmi_stop_gpu_event_notification(h);
     armed_handles_.clear();
     armed_ = false;
   }
 
   mutable std::mutex mu_;
+  std::mutex evt_mu_;                   // held across the blocking event wait
+  std::atomic<bool> evt_live_{false};   // armed with at least one source
   std::vector<std::vector<amdsmi_processor_handle>> procs_;
   std::vector<GpuInfo> gpus_;
   std::vector<amdsmi_processor_handle> armed_handles_;
+  std::vector<amdsmi_processor_handle> armed_for_;  // processor set at arming time
   bool armed_ = false;
+  bool want_rearm_ = false;
+  int reinits_ = 0;
   bool closed_ = false;
 };
 

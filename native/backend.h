@@ -158,6 +158,11 @@ class Backend {
   virtual void arm_events() {}
   // Number of processors with hardware event delivery armed (0 = polling only).
   virtual int armed_event_sources() const { return 0; }
+  // Drop cached device handles so the next discover() enumerates afresh (a compute
+  // partition change creates new processors).  Returns false when not possible.
+  virtual bool reinit() { return true; }
+  // Times the backend re-initialised its hardware library (stale-handle recovery).
+  virtual int reinit_count() const { return 0; }
   virtual void shutdown() {}
 };
 

@@ -189,6 +189,8 @@ PYBIND11_MODULE(_native, m) {
            })
       .def("arm_events", &Backend::arm_events, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("armed_event_sources", &Backend::armed_event_sources)
+      .def("reinit", &Backend::reinit, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("reinit_count", &Backend::reinit_count)
       .def("shutdown", &Backend::shutdown, py::call_guard<py::gil_scoped_release>());
 
   py::class_<FixtureBackend, Backend, std::shared_ptr<FixtureBackend>>(m, "FixtureBackend")

@@ -10,8 +10,11 @@
 // inputs built with the same encoders the production code uses into <dir> and exits.
 #pragma once
 
+#include <poll.h>
+#include <sys/socket.h>
 #include <sys/stat.h>
 
+#include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
@@ -126,6 +129,39 @@ inline std::string h2_call(uint32_t sid, const std::string& path, const std::str
   h2_frame(&o, 0x1, 0x4, sid, grpc_headers(path, huffman));
   h2_frame(&o, 0x0, 0x1, sid, grpc_body(msg));
   return o;
+}
+
+// ---- sockets ----
+// libFuzzer's -timeout watchdog is a 1 s SIGALRM, so every blocking call here can see
+// EINTR; an interrupted connect() keeps connecting in the background.
+inline bool connect_retry(int fd, const sockaddr* addr, socklen_t len) {
+  if (connect(fd, addr, len) == 0) return true;
+  if (errno != EINTR && errno != EINPROGRESS) return false;
+  for (;;) {
+    struct pollfd p {fd, POLLOUT, 0};
+    const int r = poll(&p, 1, 5000);
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) return false;
+    int err = 0;
+    socklen_t el = sizeof(err);
+    getsockopt(fd, SOL_SOCKET, SO_ERROR, &err, &el);
+    return err == 0;
+  }
+}
+
+// Reads until the peer closes.  false = nothing arrived for 5 s (the server is stuck).
+inline bool drain_until_close(int fd, std::string* into) {
+  char buf[65536];
+  for (;;) {
+    struct pollfd p {fd, POLLIN, 0};
+    const int r = poll(&p, 1, 5000);
+    if (r < 0 && errno == EINTR) continue;
+    if (r == 0) return false;
+    const ssize_t n = recv(fd, buf, sizeof(buf), 0);
+    if (n < 0 && errno == EINTR) continue;
+    if (n <= 0) return true;
+    if (into) into->append(buf, static_cast<size_t>(n));
+  }
 }
 
 // ---- seed corpus ----

@@ -61,6 +61,7 @@ std::string client_prefix() {
 bool write_all(int fd, const char* p, size_t n) {
   while (n > 0) {
     const ssize_t w = send(fd, p, n, MSG_NOSIGNAL);
+    if (w < 0 && errno == EINTR) continue;
     if (w <= 0) return false;  // the server closed early (GOAWAY): fine
     p += w;
     n -= static_cast<size_t>(w);
@@ -73,23 +74,16 @@ void one_connection(const uint8_t* data, size_t size) {
   struct sockaddr_un addr {};
   addr.sun_family = AF_UNIX;
   std::memcpy(addr.sun_path, g_path.c_str(), g_path.size() + 1);
-  if (connect(fd, reinterpret_cast<sockaddr*>(&addr), sizeof(addr)) != 0) {
+  if (!fuzzutil::connect_retry(fd, reinterpret_cast<sockaddr*>(&addr), sizeof(addr))) {
     std::fprintf(stderr, "connect failed: %s\n", std::strerror(errno));
     std::abort();
   }
   const std::string pre = client_prefix();
   if (write_all(fd, pre.data(), pre.size())) write_all(fd, reinterpret_cast<const char*>(data), size);
   shutdown(fd, SHUT_WR);
-  char buf[65536];
-  for (;;) {
-    struct pollfd pfd {fd, POLLIN, 0};
-    const int r = poll(&pfd, 1, 5000);
-    if (r == 0) {
-      std::fprintf(stderr, "server did not close a half-closed connection within 5 s\n");
-      std::abort();
-    }
-    const ssize_t n = recv(fd, buf, sizeof(buf), 0);
-    if (n <= 0) break;
+  if (!fuzzutil::drain_until_close(fd, nullptr)) {
+    std::fprintf(stderr, "server did not close a half-closed connection within 5 s\n");
+    std::abort();
   }
   close(fd);
 }

@@ -59,28 +59,22 @@ std::string roundtrip(const char* data, size_t size) {
   a.sin_family = AF_INET;
   a.sin_port = htons(static_cast<uint16_t>(g_port));
   a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
-  if (connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0) {
+  if (!fuzzutil::connect_retry(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a))) {
     std::fprintf(stderr, "connect failed: %s\n", std::strerror(errno));
     std::abort();
   }
   size_t off = 0;
   while (off < size) {
     const ssize_t w = send(fd, data + off, size - off, MSG_NOSIGNAL);
+    if (w < 0 && errno == EINTR) continue;
     if (w <= 0) break;  // server answered 4xx and closed early: fine
     off += static_cast<size_t>(w);
   }
   shutdown(fd, SHUT_WR);
   std::string resp;
-  char buf[65536];
-  for (;;) {
-    struct pollfd pfd {fd, POLLIN, 0};
-    if (poll(&pfd, 1, 5000) == 0) {
-      std::fprintf(stderr, "server did not close a half-closed connection within 5 s\n");
-      std::abort();
-    }
-    const ssize_t n = recv(fd, buf, sizeof(buf), 0);
-    if (n <= 0) break;
-    resp.append(buf, static_cast<size_t>(n));
+  if (!fuzzutil::drain_until_close(fd, &resp)) {
+    std::fprintf(stderr, "server did not close a half-closed connection within 5 s\n");
+    std::abort();
   }
   // Linger-free close: the fuzzer opens tens of thousands of connections.
   struct linger lg {1, 0};

@@ -226,3 +226,42 @@ def test_allocation_maps_to_the_right_physical_gpu(make_cfg, plugin_dir, amdsmi_
     bdf = "%04x:%02x:%02x" % (r["dom"], r["bus"], r["dev"])
     assert r["n"] == 1 and g.bdf.lower().startswith(bdf), (r, g.bdf)
     assert r["err"] < 2e-2, r
+
+
+_REINIT_CHILD = """
+import json, time
+from k8s_gpu_device_plugin_amd import native
+from k8s_gpu_device_plugin_amd.plugin.manager import inventory_signature
+n = native.load()
+be = n.make_amdsmi_backend()
+gpus, _ = be.discover()
+before = inventory_signature(gpus)
+mon = n.HealthMonitor(be, 3)
+mon.set_gpu_count(len(gpus))
+mon.start()
+time.sleep(0.3)
+armed = be.armed_event_sources
+ok = be.reinit()
+gpus2, _ = be.discover()
+out = {"reinit": ok, "count": be.reinit_count, "same": inventory_signature(gpus2) == before,
+       "armed_before": armed, "armed_after": be.armed_event_sources, "sample_ok": be.sample(0).ok}
+mon.stop()
+be.shutdown()
+print(json.dumps(out))
+"""
+
+
+def test_amdsmi_reinit_keeps_inventory_and_events():
+    """Stale-handle recovery (a compute-partition switch needs a fresh amdsmi
+    enumeration): in a process that solely owns the amdsmi session, re-initialising
+    yields the same inventory and event delivery is re-armed on the new handles."""
+    import json
+    import subprocess
+    import sys
+    out = subprocess.run([sys.executable, "-c", _REINIT_CHILD], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                         text=True, timeout=120, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    print("reinit", r)
+    assert r["reinit"] and r["count"] == 1 and r["same"] and r["sample_ok"]
+    assert r["armed_after"] == r["armed_before"]
