@@ -10,8 +10,11 @@ One spec per resource kind, e.g. ``/var/run/cdi/amd.com-gpu.json``::
 
     {"cdiVersion": "0.6.0", "kind": "amd.com/gpu",
      "containerEdits": {"deviceNodes": [{"path": "/dev/kfd"}]},
-     "devices": [{"name": "<id>", "containerEdits": {"deviceNodes": [{"path": "/dev/dri/renderD128"}],
-                  "env": ["AMD_VISIBLE_DEVICES=<id>"]}}]}
+     "devices": [{"name": "<id>", "containerEdits": {"deviceNodes": [{"path": "/dev/dri/renderD128"}]}}]}
+
+Per-device edits carry no env: with two devices in one container, two
+``AMD_VISIBLE_DEVICES=<id>`` edits would conflict (last one wins).  The visible-devices
+list comes from Allocate's env, which names every allocated device.
 """
 from __future__ import annotations
 
@@ -26,13 +29,10 @@ def _node(path: str) -> dict:
     return {"path": path, "permissions": "rw"}
 
 
-def build_spec(kind: str, devices, kfd_path: str = "/dev/kfd", visible_env: str = "AMD_VISIBLE_DEVICES") -> dict:
+def build_spec(kind: str, devices, kfd_path: str = "/dev/kfd") -> dict:
     out = []
     for d in devices:
-        edits = {"deviceNodes": [_node(p) for p in d.paths]}
-        if visible_env:
-            edits["env"] = ["%s=%s" % (visible_env, d.get_uuid())]
-        out.append({"name": d.get_uuid(), "containerEdits": edits})
+        out.append({"name": d.get_uuid(), "containerEdits": {"deviceNodes": [_node(p) for p in d.paths]}})
     # replicas share one CDI device (the name is the base id)
     uniq, seen = [], set()
     for d in out:

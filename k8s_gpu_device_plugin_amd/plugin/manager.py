@@ -203,7 +203,7 @@ class PluginManager:
             from ..cdi import build_spec, write_spec
             for name, devs in self.device_map.items():
                 try:
-                    write_spec(self.cfg.cdiSpecDir, build_spec(name, devs, visible_env=self.cfg.visibleDevicesEnv))
+                    write_spec(self.cfg.cdiSpecDir, build_spec(name, devs))
                 except OSError as e:
                     log.error("cannot write CDI spec for %s to %s: %s", name, self.cfg.cdiSpecDir, e)
         self.exporter.set_inventory(gpus)
