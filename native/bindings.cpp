@@ -13,6 +13,7 @@
 #include "health.h"
 #include "httpd.h"
 #include "loadgen.h"
+#include "metrics.h"
 #include "telemetry.h"
 #include "watch.h"
 
@@ -510,6 +511,11 @@ PYBIND11_MODULE(_native, m) {
           return h2_bench_unary(sock, path, r, n);
         });
 
+  m.def("format_float", [](double v) {  // Prometheus number formatting (exposed for tests)
+    std::string s;
+    append_float(&s, v);
+    return s;
+  });
   // hpack (exposed for tests)
   m.def("hpack_huffman_encode", [](const std::string& s) {
     std::string o;

@@ -7,6 +7,7 @@
 #pragma once
 
 #include <atomic>
+#include <charconv>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -17,8 +18,20 @@
 
 namespace amdgpu_dp {
 
-// Shortest round-trip decimal, matching Go's strconv.FormatFloat(v, 'g', -1, 64)
-// closely enough for Prometheus consumers ("0.0005", "30", "1e+06", "+Inf").
+inline void append_u64(std::string* out, uint64_t v) {
+  char buf[24];
+  char* p = buf + sizeof(buf);
+  do {
+    *--p = static_cast<char>('0' + v % 10);
+    v /= 10;
+  } while (v);
+  out->append(p, static_cast<size_t>(buf + sizeof(buf) - p));
+}
+
+// Shortest round-trip decimal in %g style, like Go's strconv.FormatFloat(v, 'g', -1,
+// 64) that promhttp uses ("0.0005", "30", "1e-05", "+Inf"); integral values below 1e15
+// print as plain integers.  std::to_chars (Ryu) keeps this off the snprintf path: a
+// scrape formats hundreds of numbers.
 inline void append_float(std::string* out, double v) {
   if (std::isnan(v)) {
     out->append("NaN");
@@ -29,21 +42,17 @@ inline void append_float(std::string* out, double v) {
     return;
   }
   if (v == std::floor(v) && std::fabs(v) < 1e15) {
-    char buf[32];
-    int n = std::snprintf(buf, sizeof(buf), "%lld", static_cast<long long>(v));
-    if (std::fabs(v) >= 1e21) n = std::snprintf(buf, sizeof(buf), "%g", v);
-    out->append(buf, n);
+    if (v < 0) {
+      out->push_back('-');
+      append_u64(out, static_cast<uint64_t>(-v));
+    } else {
+      append_u64(out, static_cast<uint64_t>(v));
+    }
     return;
   }
   char buf[40];
-  for (int prec = 1; prec <= 17; ++prec) {
-    const int n = std::snprintf(buf, sizeof(buf), "%.*g", prec, v);
-    if (std::strtod(buf, nullptr) == v) {
-      out->append(buf, n);
-      return;
-    }
-  }
-  out->append(buf);
+  const auto r = std::to_chars(buf, buf + sizeof(buf), v, std::chars_format::general);
+  out->append(buf, static_cast<size_t>(r.ptr - buf));
 }
 
 inline void append_label_value(std::string* out, std::string_view s) {
@@ -53,12 +62,6 @@ inline void append_label_value(std::string* out, std::string_view s) {
     else if (c == '\n') out->append("\\n");
     else out->push_back(c);
   }
-}
-
-inline void append_u64(std::string* out, uint64_t v) {
-  char buf[24];
-  const int n = std::snprintf(buf, sizeof(buf), "%llu", static_cast<unsigned long long>(v));
-  out->append(buf, n);
 }
 
 inline void append_header(std::string* out, const char* name, const char* help, const char* type) {
@@ -92,7 +95,14 @@ class AtomicDouble {
 
 class Histogram {
  public:
-  explicit Histogram(std::vector<double> bounds) : bounds_(std::move(bounds)), counts_(bounds_.size() + 1) {}
+  explicit Histogram(std::vector<double> bounds) : bounds_(std::move(bounds)), counts_(bounds_.size() + 1) {
+    for (double b : bounds_) {  // the le="..." strings never change: format them once
+      std::string s;
+      append_float(&s, b);
+      le_.push_back(std::move(s));
+    }
+    le_.push_back("+Inf");
+  }
   Histogram(const Histogram&) = delete;
   void observe(double v) {
     size_t i = 0;
@@ -107,13 +117,12 @@ class Histogram {
   }
   // labels: already-formatted `k="v",` prefix (may be empty)
   void render(std::string* out, const char* name, std::string_view labels) const {
+    std::string prefix(name);
+    prefix.append("_bucket{").append(labels.data(), labels.size()).append("le=\"");
     uint64_t cum = 0;
     for (size_t i = 0; i <= bounds_.size(); ++i) {
       cum += counts_[i].load(std::memory_order_relaxed);
-      out->append(name).append("_bucket{").append(labels.data(), labels.size()).append("le=\"");
-      if (i < bounds_.size()) append_float(out, bounds_[i]);
-      else out->append("+Inf");
-      out->append("\"} ");
+      out->append(prefix).append(le_[i]).append("\"} ");
       append_u64(out, cum);
       out->push_back('\n');
     }
@@ -133,6 +142,7 @@ class Histogram {
 
  private:
   std::vector<double> bounds_;
+  std::vector<std::string> le_;
   std::vector<std::atomic<uint64_t>> counts_;
   AtomicDouble sum_;
 };

@@ -1,6 +1,8 @@
 """Exporter (per-GPU / per-partition telemetry rendering) and the native health monitor."""
 import time
 
+from hypothesis import given, settings, strategies as st
+
 from prometheus_client.parser import text_string_to_metric_families
 
 from k8s_gpu_device_plugin_amd.models import fixtures
@@ -113,3 +115,21 @@ def test_monitor_event_thread_scripted(n):
     finally:
         m.stop()
         m.stop()
+
+
+def test_prometheus_number_formatting(n):
+    """Shortest round-trip %g formatting (Go strconv.FormatFloat 'g' -1 as used by
+    promhttp) on the Ryu fast path; integers print as integers."""
+    import math
+    cases = {0.0005: "0.0005", 1e-05: "1e-05", 30.0: "30", 0.1: "0.1", 1.5e-07: "1.5e-07", -0.5: "-0.5",
+             2.5: "2.5", 0.0: "0", 1e6: "1000000", -3.0: "-3", float("inf"): "+Inf", float("-inf"): "-Inf",
+             123.456: "123.456", 1e-4: "0.0001"}
+    for v, want in cases.items():
+        assert n.format_float(v) == want, (v, n.format_float(v))
+    assert n.format_float(float("nan")) == "NaN"
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.floats(allow_nan=False, allow_infinity=False))
+def test_prometheus_number_round_trips(n, v):
+    assert float(n.format_float(v)) == v
