@@ -103,8 +103,8 @@ def rpc_latency(node, method, req, n_native=10000, n_grpcio=2000):
     return out
 
 
-def scrape(node, conns=4, seconds=2.0, rate=0.0, gzip=False):
-    r = native.load().http_load("127.0.0.1", node.port, "/metrics", conns, seconds, rate, gzip)
+def scrape(node, conns=4, seconds=2.0, rate=0.0, gzip=False, path="/metrics"):
+    r = native.load().http_load("127.0.0.1", node.port, path, conns, seconds, rate, gzip)
     lat = r["latencies_s"]
     return {"rps": round(r["ok"] / r["elapsed_s"], 1), "errors": r["errors"], "p50_us": us(pct(lat, 0.5)),
             "p99_us": us(pct(lat, 0.99)), "bytes": r["bytes"] // max(1, r["ok"]), "conns": conns,
@@ -145,6 +145,8 @@ def config2():
                 "advertised": len(ids),
                 "allocate": rpc_latency(node, v1beta1.METHOD_ALLOCATE, alloc_req(ids[:1])),
                 "scrape_max": scrape(node, 4, 2.0),
+                "scrape_1conn": scrape(node, 1, 1.0),
+                "health_route_1conn": scrape(node, 1, 1.0, path="/health"),
                 "telemetry_sample_cost_us": us(cost)}
     finally:
         node.close()
