@@ -86,3 +86,35 @@ def family_of(sample_name: str) -> Family | None:
         if sample_name.endswith(suffix) and sample_name[: -len(suffix)] in BY_NAME:
             return BY_NAME[sample_name[: -len(suffix)]]
     return None
+
+
+PROMQL_EXAMPLES = (
+    ("Socket power seen per advertised partition (join on the physical GPU)",
+     "amdgpu_power_watts * on(gpu) group_right amdgpu_partition_info"),
+    ("Hottest HBM stack per GPU", 'max by (gpu) (amdgpu_temperature_celsius{sensor=~"hbm.*"})'),
+    ("Unhealthy advertised devices per resource", "count by (resource) (amdgpu_device_plugin_device_health == 0)"),
+    ("Allocate p99 over 5 minutes",
+     'histogram_quantile(0.99, sum by (le) (rate(amdgpu_device_plugin_rpc_duration_seconds_bucket{rpc="Allocate"}[5m])))'),
+    ("Down xGMI links", "amdgpu_xgmi_link_up == 0"),
+    ("xGMI traffic per link (bytes/s)", "rate(amdgpu_xgmi_read_bytes_total[1m]) + rate(amdgpu_xgmi_write_bytes_total[1m])"),
+)
+
+
+def markdown() -> str:
+    """docs/METRICS.md, generated from FAMILIES (tests keep the file in sync)."""
+    out = ["# /metrics reference", "",
+           "Generated by `python -m k8s_gpu_device_plugin_amd.metrics.families`. Do not edit by hand.",
+           "`tests/test_topology_model.py` checks this list against a live exporter in both",
+           "directions.", "",
+           "| Family | Type | Labels | Source | Meaning |", "|---|---|---|---|---|"]
+    for f in FAMILIES:
+        out.append("| `%s` | %s | %s | %s | %s |" % (f.name, f.type, ", ".join("`%s`" % x for x in f.labels) or "—",
+                                                  f.source, f.help))
+    out += ["", "## PromQL examples", ""]
+    for title, q in PROMQL_EXAMPLES:
+        out += ["%s:" % title, "", "```promql", q, "```", ""]
+    return "\n".join(out)
+
+
+if __name__ == "__main__":
+    print(markdown(), end="")

@@ -86,3 +86,10 @@ def test_metrics_contract_both_ways(n):
     missing = {f.name for f in families.FAMILIES} - seen
     # per-partition VRAM needs real usage; everything else must be present on the fixture node
     assert missing <= {"amdgpu_partition_vram_used_bytes"}, missing
+
+
+def test_metrics_doc_is_generated_from_the_registry():
+    import os
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "docs", "METRICS.md")
+    with open(path, encoding="utf-8") as f:
+        assert f.read() == families.markdown(), "regenerate: python -m k8s_gpu_device_plugin_amd.metrics.families"
