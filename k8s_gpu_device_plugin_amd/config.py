@@ -93,6 +93,7 @@ class Config:
     mountCardNodes: bool = False
     cdi: bool = False
     cdiSpecDir: str = "/var/run/cdi"
+    nodeFeatureFile: str = ""             # NFD local feature file ("" = off), see labels/nfd.py
     rediscoverIntervalS: float = 60.0     # detect partition-mode / device-set changes (0 = off)
     sharing: SharingConfig = field(default_factory=SharingConfig)
     telemetry: TelemetryConfig = field(default_factory=TelemetryConfig)

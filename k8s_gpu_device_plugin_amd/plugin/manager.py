@@ -206,6 +206,12 @@ class PluginManager:
                     write_spec(self.cfg.cdiSpecDir, build_spec(name, devs))
                 except OSError as e:
                     log.error("cannot write CDI spec for %s to %s: %s", name, self.cfg.cdiSpecDir, e)
+        if self.cfg.nodeFeatureFile:
+            from ..labels import node_labels, write_feature_file
+            try:
+                write_feature_file(self.cfg.nodeFeatureFile, node_labels(gpus))
+            except OSError as e:
+                log.error("cannot write node feature file %s: %s", self.cfg.nodeFeatureFile, e)
         self.exporter.set_inventory(gpus)
         self.exporter.set_partition_labels(labels)
         self.exporter.set_tables([p.table for p in plugins])

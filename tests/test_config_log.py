@@ -126,3 +126,23 @@ def test_unknown_keys_are_reported(tmp_path, caplog):
         logger.propagate = old
     assert cfg.migStrategy == "none"
     assert any("migStratgy" in r.getMessage() for r in caplog.records)
+
+
+def test_shipped_configs_are_valid():
+    """config.yml and the DaemonSet's embedded config load with no unknown keys."""
+    import yaml
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "config.yml")) as f:
+        raw = yaml.safe_load(f)
+    assert C.unknown_keys(raw) == []
+    C.validate(C.from_dict(raw))
+    with open(os.path.join(root, "deploy", "daemonset.yaml")) as f:
+        docs = list(yaml.safe_load_all(f))
+    raw = yaml.safe_load(docs[0]["data"]["config.yml"])
+    assert C.unknown_keys(raw) == []
+    cfg = C.validate(C.from_dict(raw))
+    assert cfg.backend == "amdsmi" and cfg.nodeFeatureFile.endswith("features.d/amd-gpu")
+    ds = docs[1]["spec"]["template"]["spec"]
+    mounts = {m["mountPath"] for m in ds["containers"][0]["volumeMounts"]}
+    assert {"/var/lib/kubelet/device-plugins", "/dev/kfd", "/dev/dri"} <= mounts
+    assert os.path.dirname(cfg.nodeFeatureFile) in mounts

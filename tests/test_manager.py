@@ -322,3 +322,23 @@ def be_event(m, kind, gpu):
     from k8s_gpu_device_plugin_amd import native
     n = native.load()
     return n.HwEvent(getattr(n, kind), gpu, -1, -1, "test")
+
+
+def test_node_feature_file_tracks_partition_mode(make_cfg, plugin_dir, run_manager, tmp_path):
+    """Optional NFD local-feature labels; rewritten when the partition mode changes."""
+    path = tmp_path / "features.d" / "amd-gpu"
+    be = fixtures.build_backend("2gpu_spx")
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(migStrategy="single", rediscoverIntervalS=0.2, nodeFeatureFile=str(path)),
+                        backend=be)
+        k.wait_for_registrations(1)
+        labels = dict(ln.split("=", 1) for ln in path.read_text().splitlines())
+        assert labels["amd.com/gpu.count"] == "2" and labels["amd.com/gpu.compute-partition"] == "SPX"
+        assert labels["amd.com/gpu.product"] == "AMD_Instinct_MI355X" and labels["amd.com/gpu.family"] == "gfx950"
+        assert labels["amd.com/gpu.vram-gb"] == "288" and labels["amd.com/gpu.partitions"] == "2"
+        fixtures.set_gpu_mode(be, 0, "CPX", "NPS2")
+        fixtures.set_gpu_mode(be, 1, "CPX", "NPS2")
+        assert _wait(lambda: "gpu.compute-partition=CPX" in path.read_text(), timeout=10)
+        labels = dict(ln.split("=", 1) for ln in path.read_text().splitlines())
+        assert labels["amd.com/gpu.partitions"] == "16" and labels["amd.com/gpu.memory-partition"] == "NPS2"
+        assert m.counters.get("restarts_inventory", 0) >= 1
