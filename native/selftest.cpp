@@ -11,8 +11,10 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 #include <thread>
 #include <vector>
@@ -243,6 +245,114 @@ static void test_exporter_httpd_health(std::shared_ptr<FixtureBackend> be) {
   CHECK(saw_unhealthy || !mon->gpu_healthy(1));
 }
 
+// A plugin reload (manager.load_plugins) swaps the exporter's inventory, partition
+// labels and device tables while HTTP workers render /metrics (plain and gzip) and the
+// sampler ticks; a server stop races open ListAndWatch streams.
+static std::string http_get(int port, const char* req) {
+  const int fd = socket(AF_INET, SOCK_STREAM, 0);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons(static_cast<uint16_t>(port));
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  std::string resp;
+  if (connect(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) == 0) {
+    (void)!write(fd, req, std::strlen(req));
+    char buf[65536];
+    ssize_t r;
+    while ((r = read(fd, buf, sizeof(buf))) > 0) resp.append(buf, static_cast<size_t>(r));
+  }
+  close(fd);
+  return resp;
+}
+
+static std::shared_ptr<DeviceTable> table_of(const std::vector<GpuInfo>& gpus, const Topology& topo) {
+  std::vector<TableDevice> devs;
+  for (auto& g : gpus)
+    for (auto& p : g.partitions) {
+      TableDevice d;
+      d.id = p.id;
+      d.gpu = g.index;
+      d.partition = p.index;
+      devs.push_back(d);
+    }
+  return std::make_shared<DeviceTable>(TableConfig{}, devs, topo);
+}
+
+static void test_reload_races(const std::string& dir) {
+  auto be_a = make_node(2, 1), be_b = make_node(4, 8);
+  std::vector<GpuInfo> ga, gb;
+  Topology ta, tb;
+  be_a->discover(&ga, &ta);
+  be_b->discover(&gb, &tb);
+  auto ex = std::make_shared<Exporter>();
+  ex->set_inventory(ga);
+  ex->set_tables({table_of(ga, ta)});
+  ex->start(be_a, 2, nullptr);
+  HttpConfig hc;
+  hc.host = "127.0.0.1";
+  hc.port = 0;
+  hc.threads = 3;
+  hc.access_log = false;
+  HttpServer http(hc, ex);
+  const int port = http.start();
+  std::atomic<bool> stop{false};
+  std::atomic<int> bad{0};
+  std::vector<std::thread> ts;
+  for (int i = 0; i < 3; ++i)
+    ts.emplace_back([&, i] {
+      while (!stop.load()) {
+        const std::string r = http_get(port, i % 2 ? "GET /metrics HTTP/1.1\r\nAccept-Encoding: gzip\r\nConnection: close\r\n\r\n"
+                                                   : "GET /metrics HTTP/1.1\r\nConnection: close\r\n\r\n");
+        if (r.compare(0, 15, "HTTP/1.1 200 OK") != 0) ++bad;
+      }
+    });
+  for (int k = 0; k < 60; ++k) {  // reloads flip between a 2-GPU SPX and a 4-GPU CPX node
+    const bool b = k % 2;
+    std::vector<PartitionLabel> labels;
+    for (auto& g : b ? gb : ga)
+      for (auto& p : g.partitions) labels.push_back({g.index, p.index, p.id, "amd.com/gpu"});
+    ex->set_inventory(b ? gb : ga);
+    ex->set_partition_labels(labels);
+    ex->set_tables({table_of(b ? gb : ga, b ? tb : ta)});
+    ex->set_extra("# extra " + std::to_string(k) + "\n");
+    std::this_thread::sleep_for(std::chrono::milliseconds(2));
+  }
+  stop = true;
+  for (auto& t : ts) t.join();
+  CHECK(bad.load() == 0);
+  http.stop();
+  ex->stop();
+
+  // server stop with ListAndWatch streams open and clients still calling
+  auto table = table_of(ga, ta);
+  const std::string path = dir + "/reload.sock";
+  for (int round = 0; round < 3; ++round) {
+    GrpcServer srv(path, 2);
+    srv.set_table(table);
+    srv.start();
+    std::atomic<bool> done{false};
+    std::vector<std::thread> cs;
+    for (int i = 0; i < 3; ++i)
+      cs.emplace_back([&] {
+        try {
+          H2Client c(path, 2.0);
+          std::string law;
+          c.first_stream_message("/v1beta1.DevicePlugin/ListAndWatch", "", &law);
+          std::string resp, msg;
+          while (!done.load()) c.unary("/v1beta1.DevicePlugin/Allocate", alloc_req(ga[0].partitions[0].id), &resp, &msg);
+        } catch (const std::exception&) {
+          // the server going away mid-call is the point of this test
+        }
+      });
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    table->set_gpu_health(0, -1, round % 2);
+    srv.notify();
+    srv.stop();
+    done = true;
+    for (auto& t : cs) t.join();
+  }
+}
+
 int main() {
   char tmpl[] = "/tmp/amdgpu-selftest-XXXXXX";
   const char* dir = mkdtemp(tmpl);
@@ -256,6 +366,8 @@ int main() {
   test_grpc_server(make_node(4, 1), dir);
   std::fprintf(stderr, "[selftest] exporter + httpd + health\n");
   test_exporter_httpd_health(make_node(2, 1));
+  std::fprintf(stderr, "[selftest] reload races\n");
+  test_reload_races(dir);
   rmdir(dir);
   if (g_failures) {
     std::fprintf(stderr, "native selftest: %d failure(s)\n", g_failures);
