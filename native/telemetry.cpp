@@ -68,6 +68,7 @@ void Exporter::set_inventory(const std::vector<GpuInfo>& gpus) {
   std::lock_guard<std::mutex> lk(mu_);
   gpus_ = gpus;
   last_.assign(gpus.size(), GpuSample{});
+  ++inventory_gen_;
 }
 
 void Exporter::set_partition_labels(const std::vector<PartitionLabel>& labels) {
@@ -129,9 +130,11 @@ void Exporter::sample_once() {
   std::lock_guard<std::mutex> slk(sample_mu_);
   std::shared_ptr<Backend> be = backend_;
   size_t n;
+  uint64_t gen;
   {
     std::lock_guard<std::mutex> lk(mu_);
     n = gpus_.size();
+    gen = inventory_gen_;
   }
   std::vector<GpuSample> samples(n);
   std::vector<char> ok(n, 0);
@@ -146,7 +149,7 @@ void Exporter::sample_once() {
     sample_hist_.observe(dt);
     samples_.fetch_add(1, std::memory_order_relaxed);
   }
-  render_gpu_text(samples, ok, dt);
+  render_gpu_text(samples, ok, gen);
 }
 
 namespace {
@@ -165,11 +168,14 @@ void line(std::string* out, const char* name, const std::string& labels, double 
 
 }  // namespace
 
-void Exporter::render_gpu_text(const std::vector<GpuSample>& samples, const std::vector<char>& ok, double) {
+void Exporter::render_gpu_text(const std::vector<GpuSample>& samples, const std::vector<char>& ok, uint64_t gen) {
   std::vector<GpuInfo> gpus;
   std::vector<PartitionLabel> labels;
   {
     std::lock_guard<std::mutex> lk(mu_);
+    // A reload replaced the inventory while this pass sampled the old one: its samples
+    // belong to other GPUs (or more/fewer of them).  Drop the pass; the next tick renders.
+    if (gen != inventory_gen_) return;
     gpus = gpus_;
     labels = labels_;
     for (size_t g = 0; g < samples.size() && g < last_.size(); ++g)

@@ -65,13 +65,14 @@ class Exporter {
 
  private:
   void loop();
-  void render_gpu_text(const std::vector<GpuSample>& samples, const std::vector<char>& ok, double sample_s);
+  void render_gpu_text(const std::vector<GpuSample>& samples, const std::vector<char>& ok, uint64_t inventory_gen);
   void render_process(std::string* out) const;
   void render_parts(std::shared_ptr<const std::string>* head, std::string* counters,
                     std::shared_ptr<const std::string>* health, std::string* tail) const;
 
   mutable std::mutex mu_;
   std::vector<GpuInfo> gpus_;
+  uint64_t inventory_gen_ = 0;  // bumped by set_inventory; a sampling pass is tied to one
   std::vector<PartitionLabel> labels_;
   std::vector<GpuSample> last_;
   std::vector<std::shared_ptr<DeviceTable>> tables_;
