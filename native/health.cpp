@@ -1,5 +1,6 @@
 #include "health.h"
 
+#include <algorithm>
 #include <chrono>
 
 namespace amdgpu_dp {
@@ -10,8 +11,11 @@ HealthMonitor::HealthMonitor(std::shared_ptr<Backend> backend, int lost_after_fa
 HealthMonitor::~HealthMonitor() { stop(); }
 
 void HealthMonitor::set_gpu_count(int n) {
+  // Called on every plugin (re)load: keep the state of GPUs that are still there, or a
+  // GPU that is mid-reset when kubelet restarts would be forgotten as healthy and its
+  // POST_RESET would never produce the Healthy update.
   std::lock_guard<std::mutex> lk(mu_);
-  state_.assign(n, GpuState{});
+  state_.resize(static_cast<size_t>(std::max(0, n)));
 }
 
 void HealthMonitor::start() {

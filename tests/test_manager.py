@@ -342,3 +342,20 @@ def test_node_feature_file_tracks_partition_mode(make_cfg, plugin_dir, run_manag
         labels = dict(ln.split("=", 1) for ln in path.read_text().splitlines())
         assert labels["amd.com/gpu.partitions"] == "16" and labels["amd.com/gpu.memory-partition"] == "NPS2"
         assert m.counters.get("restarts_inventory", 0) >= 1
+
+
+def test_reset_state_survives_a_reload(make_cfg, plugin_dir, run_manager):
+    """A GPU mid-reset when kubelet restarts (full reload) must still come back Healthy
+    on POST_RESET: the monitor keeps per-GPU state across reloads."""
+    be = fixtures.build_backend("2gpu_spx")
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(), backend=be)
+        k.wait_for_registrations(1)
+        be.inject_event(be_event(m, "EVT_PRE_RESET", 1))
+        assert _wait(lambda: m.plugins[0].table.healthy_count() == 1)
+        m.restart()
+        k.wait_for_registrations(2, timeout=10)
+        assert _wait(lambda: m.counters["restarts_api"] == 1)
+        assert m.plugins[0].table.healthy_count() == 1  # still held Unhealthy after the reload
+        be.inject_event(be_event(m, "EVT_POST_RESET", 1))
+        assert _wait(lambda: m.plugins[0].table.healthy_count() == 2)
