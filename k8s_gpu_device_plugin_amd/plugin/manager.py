@@ -215,6 +215,7 @@ class PluginManager:
         self.exporter.set_inventory(gpus)
         self.exporter.set_partition_labels(labels)
         self.exporter.set_tables([p.table for p in plugins])
+        self.monitor.set_fast_tables([p.table for p in plugins])  # Unhealthy applied natively, at once
         self.monitor.set_gpu_count(max([g.index for g in gpus], default=-1) + 1)
         log.info("loaded %d GPU(s), resources: %s", len(gpus),
                  ", ".join("%s=%d" % (k, len(v)) for k, v in self.device_map.items()) or "none")

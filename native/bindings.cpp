@@ -356,6 +356,7 @@ PYBIND11_MODULE(_native, m) {
       .def("process", &HealthMonitor::process, py::call_guard<py::gil_scoped_release>())
       .def("pop", &HealthMonitor::pop, py::call_guard<py::gil_scoped_release>(), py::arg("timeout_ms") = 200)
       .def("gpu_healthy", &HealthMonitor::gpu_healthy)
+      .def("set_fast_tables", &HealthMonitor::set_fast_tables)
       .def_property_readonly("events_seen", &HealthMonitor::events_seen);
 
   // ---- exporter ----
@@ -488,6 +489,25 @@ PYBIND11_MODULE(_native, m) {
              }
              return py::bytes(resp);
            })
+      .def("open_stream",
+           [](H2Client& c, const std::string& path, const py::bytes& req) {
+             std::string r(req);
+             py::gil_scoped_release rel;
+             c.open_stream(path, r);
+           })
+      .def(
+          "next_stream_message",
+          [](H2Client& c, double timeout_s) -> py::object {
+            std::string resp;
+            int st;
+            {
+              py::gil_scoped_release rel;
+              st = c.next_stream_message(&resp, static_cast<int>(timeout_s * 1000));
+            }
+            if (st != 0) return py::none();
+            return py::bytes(resp);
+          },
+          py::arg("timeout_s") = 5.0)
       .def("bench_unary",
            [](H2Client& c, const std::string& path, const py::bytes& req, int n) {
              std::string r(req), resp, msg;
@@ -563,6 +583,15 @@ PYBIND11_MODULE(_native, m) {
         },
         py::arg("host"), py::arg("port"), py::arg("path") = "/metrics", py::arg("conns") = 4,
         py::arg("duration_s") = 2.0, py::arg("target_rps") = 0.0, py::arg("accept_gzip") = false);
+  m.def(
+      "health_propagation",
+      [](std::shared_ptr<Backend> be, const std::string& sock, int gpu, int events) {
+        auto* fx = dynamic_cast<FixtureBackend*>(be.get());
+        if (!fx) throw std::invalid_argument("health_propagation needs a fixture backend");
+        py::gil_scoped_release rel;
+        return health_propagation(*fx, sock, gpu, events);
+      },
+      py::arg("backend"), py::arg("socket_path"), py::arg("gpu"), py::arg("events") = 60);
   m.def("grpc_load",
         [load_dict](const std::string& sock, const std::string& method, const py::bytes& req, int conns,
                     double duration_s) {

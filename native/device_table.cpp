@@ -104,18 +104,39 @@ void DeviceTable::publish_law_locked() {
                              std::memory_order_release);
 }
 
+void DeviceTable::add_listener(std::weak_ptr<TableListener> l) {
+  std::lock_guard<std::mutex> lk(lmu_);
+  listeners_.erase(std::remove_if(listeners_.begin(), listeners_.end(),
+                                  [](const std::weak_ptr<TableListener>& w) { return w.expired(); }),
+                   listeners_.end());
+  listeners_.push_back(std::move(l));
+}
+
+void DeviceTable::notify_listeners() {
+  std::vector<std::shared_ptr<TableListener>> live;
+  {
+    std::lock_guard<std::mutex> lk(lmu_);
+    for (const auto& w : listeners_)
+      if (auto sp = w.lock()) live.push_back(std::move(sp));
+  }
+  for (const auto& l : live) l->on_table_change();
+}
+
 bool DeviceTable::set_health(std::string_view id, bool healthy) {
-  std::lock_guard<std::mutex> lk(wmu_);
-  const int i = index_of(id);
-  if (i < 0 || is_healthy(i) == healthy) return false;
-  health_[i].store(healthy ? 1 : 0, std::memory_order_release);
-  publish_law_locked();
-  version_.fetch_add(1, std::memory_order_acq_rel);
+  {
+    std::lock_guard<std::mutex> lk(wmu_);
+    const int i = index_of(id);
+    if (i < 0 || is_healthy(i) == healthy) return false;
+    health_[i].store(healthy ? 1 : 0, std::memory_order_release);
+    publish_law_locked();
+    version_.fetch_add(1, std::memory_order_acq_rel);
+  }
+  notify_listeners();
   return true;
 }
 
 int DeviceTable::set_gpu_health(int gpu, int partition, bool healthy) {
-  std::lock_guard<std::mutex> lk(wmu_);
+  std::unique_lock<std::mutex> lk(wmu_);
   int changed = 0;
   for (size_t i = 0; i < devs_.size(); ++i) {
     const auto& d = devs_[i];
@@ -130,6 +151,8 @@ int DeviceTable::set_gpu_health(int gpu, int partition, bool healthy) {
   if (changed) {
     publish_law_locked();
     version_.fetch_add(1, std::memory_order_acq_rel);
+    lk.unlock();
+    notify_listeners();
   }
   return changed;
 }

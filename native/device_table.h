@@ -62,6 +62,14 @@ enum Rpc : int {
 
 const char* rpc_name(int rpc);
 
+// Woken after every published health change, e.g. a GrpcServer pushing ListAndWatch.
+// Tables hold listeners weakly, so a destroyed server is simply skipped.
+class TableListener {
+ public:
+  virtual ~TableListener() = default;
+  virtual void on_table_change() = 0;
+};
+
 class DeviceTable {
  public:
   DeviceTable(TableConfig cfg, std::vector<TableDevice> devices, Topology topo);
@@ -83,6 +91,7 @@ class DeviceTable {
   Topology topology() const;
 
   uint64_t version() const { return version_.load(std::memory_order_acquire); }
+  void add_listener(std::weak_ptr<TableListener> l);
   std::string list_and_watch() const;  // ListAndWatchResponse bytes (cached)
 
   // RPC bodies.  Return true and response bytes in *out, or false and an error message.
@@ -100,6 +109,7 @@ class DeviceTable {
 
  private:
   void publish_law_locked();  // caller holds wmu_
+  void notify_listeners();    // caller must NOT hold wmu_
   std::string encode_container_alloc(const std::vector<int>& idx) const;
   bool is_healthy(int i) const { return health_[i].load(std::memory_order_acquire) != 0; }
 
@@ -114,6 +124,8 @@ class DeviceTable {
 
   std::unique_ptr<std::atomic<uint8_t>[]> health_;
   std::mutex wmu_;                                // serialises writers only
+  std::mutex lmu_;                                // listeners_
+  std::vector<std::weak_ptr<TableListener>> listeners_;
   std::shared_ptr<const Topology> topo_;          // atomic_load / atomic_store
   std::shared_ptr<const std::string> law_;        // cached ListAndWatchResponse
   std::atomic<uint64_t> version_{1};

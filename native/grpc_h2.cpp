@@ -254,6 +254,7 @@ GrpcServer::~GrpcServer() { stop(); }
 void GrpcServer::set_table(std::shared_ptr<DeviceTable> t) {
   std::lock_guard<std::mutex> lk(mu_);
   table_ = std::move(t);
+  table_->add_listener(notifier_);
 }
 
 void GrpcServer::start() {
@@ -291,6 +292,8 @@ void GrpcServer::start() {
     workers_.push_back(std::move(w));
   }
   for (auto& w : workers_) threads_.emplace_back([this, wp = w.get()] { run(wp); });
+  std::lock_guard<std::mutex> nk(notifier_->mu);
+  notifier_->srv = this;
 }
 
 void GrpcServer::notify() {
@@ -303,6 +306,10 @@ void GrpcServer::notify() {
 void GrpcServer::stop() {
   std::lock_guard<std::mutex> lk(mu_);
   if (!running_.exchange(false)) return;
+  {
+    std::lock_guard<std::mutex> nk(notifier_->mu);  // no table change may notify from here on
+    notifier_->srv = nullptr;
+  }
   stop_ = true;
   notify();
   for (auto& t : threads_)
@@ -996,6 +1003,60 @@ int H2Client::first_stream_message(std::string_view path, std::string_view req, 
   send_all(rst);
   if (resp && data.size() >= 5) resp->assign(data.data() + 5, data.size() - 5);
   return 0;
+}
+
+void H2Client::open_stream(std::string_view path, std::string_view req) {
+  watch_sid_ = next_sid_;
+  next_sid_ += 2;
+  watch_buf_.clear();
+  watch_consumed_ = 0;
+  send_request(watch_sid_, path, req);
+}
+
+int H2Client::next_stream_message(std::string* resp, int timeout_ms) {
+  if (watch_sid_ == 0) throw std::runtime_error("H2Client: no open stream");
+  const int saved = timeout_ms_;
+  timeout_ms_ = timeout_ms;
+  struct Restore {
+    int* p;
+    int v;
+    ~Restore() { *p = v; }
+  } restore{&timeout_ms_, saved};
+  uint8_t type, flags;
+  uint32_t fsid;
+  std::string payload;
+  for (;;) {
+    if (watch_buf_.size() >= 5) {
+      const uint32_t len = get_u32(reinterpret_cast<const uint8_t*>(watch_buf_.data()) + 1);
+      if (watch_buf_.size() >= 5 + static_cast<size_t>(len)) {
+        if (resp) resp->assign(watch_buf_.data() + 5, len);
+        watch_buf_.erase(0, 5 + static_cast<size_t>(len));
+        return 0;
+      }
+    }
+    if (!read_frame(&type, &flags, &fsid, &payload)) throw std::runtime_error("H2Client: connection closed");
+    if (handle_control(type, flags, fsid, payload)) continue;
+    if (fsid != watch_sid_) continue;
+    if (type == kData) {
+      watch_buf_.append(payload);
+      conn_consumed_ += static_cast<int64_t>(payload.size());
+      watch_consumed_ += static_cast<int64_t>(payload.size());
+      std::string ctl;  // a long watch must keep both receive windows open
+      if (conn_consumed_ > kLocalWindow / 2) {
+        window_update(&ctl, 0, static_cast<uint32_t>(conn_consumed_));
+        conn_consumed_ = 0;
+      }
+      if (watch_consumed_ > kLocalWindow / 2) {
+        window_update(&ctl, watch_sid_, static_cast<uint32_t>(watch_consumed_));
+        watch_consumed_ = 0;
+      }
+      if (!ctl.empty()) send_all(ctl);
+    }
+    if (type == kRstStream || (flags & kEndStream)) {
+      watch_sid_ = 0;
+      return -1;  // the server ended the stream (plugin stopped)
+    }
+  }
 }
 
 std::vector<double> h2_bench_unary(const std::string& socket_path, const std::string& path, const std::string& req,

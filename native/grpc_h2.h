@@ -41,7 +41,18 @@ class GrpcServer {
   struct Worker;
 
  private:
+  // Table listener: pushes ListAndWatch as soon as the table changes, from whichever
+  // thread changed it.  Live only between start() and stop().
+  struct Notifier : TableListener {
+    std::mutex mu;
+    GrpcServer* srv = nullptr;
+    void on_table_change() override {
+      std::lock_guard<std::mutex> lk(mu);
+      if (srv) srv->notify();
+    }
+  };
   void run(Worker* w);
+  std::shared_ptr<Notifier> notifier_ = std::make_shared<Notifier>();
   std::string path_;
   int nthreads_;
   std::shared_ptr<DeviceTable> table_;
@@ -63,6 +74,11 @@ class H2Client {
   int unary(std::string_view path, std::string_view req, std::string* resp, std::string* message);
   // Opens a server stream and returns its first message (ListAndWatch probe).
   int first_stream_message(std::string_view path, std::string_view req, std::string* resp);
+  // A long-lived server stream (a kubelet-like ListAndWatch watcher): open it, then
+  // read one message at a time.  next_stream_message returns 0 with a message, -1 when
+  // the server ended the stream; throws on timeout.
+  void open_stream(std::string_view path, std::string_view req);
+  int next_stream_message(std::string* resp, int timeout_ms);
   void close();
 
  private:
@@ -82,6 +98,9 @@ class H2Client {
   hpack::Decoder dec_;
   std::string in_;
   int64_t conn_consumed_ = 0;
+  uint32_t watch_sid_ = 0;
+  std::string watch_buf_;
+  int64_t watch_consumed_ = 0;
   int timeout_ms_;
 };
 

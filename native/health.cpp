@@ -64,6 +64,8 @@ void HealthMonitor::reconcile_locked(int gpu, int kind, const std::string& reaso
   const bool healthy = !st.resetting && !st.ecc_bad && !st.lost;
   if (healthy == st.reported_healthy) return;
   st.reported_healthy = healthy;
+  if (!healthy)
+    for (const auto& t : fast_tables_) t->set_gpu_health(gpu, -1, false);
   HealthUpdate u;
   u.kind = kind;
   u.gpu = gpu;
@@ -194,6 +196,11 @@ std::vector<HealthUpdate> HealthMonitor::pop(int timeout_ms) {
   std::vector<HealthUpdate> out(queue_.begin(), queue_.end());
   queue_.clear();
   return out;
+}
+
+void HealthMonitor::set_fast_tables(std::vector<std::shared_ptr<DeviceTable>> tables) {
+  std::lock_guard<std::mutex> lk(mu_);
+  fast_tables_ = std::move(tables);
 }
 
 bool HealthMonitor::gpu_healthy(int gpu) const {

@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "backend.h"
+#include "device_table.h"
 
 namespace amdgpu_dp {
 
@@ -53,6 +54,11 @@ class HealthMonitor {
   // Blocks up to timeout_ms; returns queued updates (possibly empty).
   std::vector<HealthUpdate> pop(int timeout_ms);
   bool gpu_healthy(int gpu) const;
+  // Fail-fast path: an Unhealthy transition is applied to these tables from the
+  // monitor thread itself (their gRPC servers push ListAndWatch at once), before the
+  // update reaches the Python manager.  Healthy transitions stay with the manager,
+  // which may hold a GPU back for the recovery canary.
+  void set_fast_tables(std::vector<std::shared_ptr<DeviceTable>> tables);
   uint64_t events_seen() const { return events_seen_; }
 
  private:
@@ -75,6 +81,7 @@ class HealthMonitor {
   std::condition_variable cv_;
   std::deque<HealthUpdate> queue_;
   std::vector<GpuState> state_;
+  std::vector<std::shared_ptr<DeviceTable>> fast_tables_;
   std::thread thread_;
   std::atomic<bool> running_{false};
   bool stop_ = false;

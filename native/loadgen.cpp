@@ -15,6 +15,7 @@
 #include <thread>
 
 #include "backend.h"
+#include "fixture_backend.h"
 #include "grpc_h2.h"
 
 namespace amdgpu_dp {
@@ -168,6 +169,41 @@ LoadResult grpc_load(const std::string& socket_path, const std::string& method, 
   for (auto& t : ts) t.join();
   total.elapsed_s = duration_s;
   return total;
+}
+
+namespace {
+
+int count_unhealthy(const std::string& law) {
+  int n = 0;
+  for (size_t p = law.find("Unhealthy"); p != std::string::npos; p = law.find("Unhealthy", p + 9)) ++n;
+  return n;
+}
+
+}  // namespace
+
+std::vector<std::pair<int, double>> health_propagation(FixtureBackend& be, const std::string& socket_path, int gpu,
+                                                       int events) {
+  H2Client c(socket_path);
+  c.open_stream("/v1beta1.DevicePlugin/ListAndWatch", "");
+  std::string msg;
+  if (c.next_stream_message(&msg, 10000) != 0) throw std::runtime_error("ListAndWatch ended");
+  const int base = count_unhealthy(msg);
+  std::vector<std::pair<int, double>> out;
+  for (int i = 0; i < events; ++i) {
+    const bool down = i % 2 == 0;
+    HwEvent e;
+    e.kind = down ? kEvtPreReset : kEvtPostReset;
+    e.gpu = gpu;
+    e.message = "propagation bench";
+    const int64_t t0 = mono_ns();
+    be.inject_event(e);
+    for (;;) {
+      if (c.next_stream_message(&msg, 10000) != 0) throw std::runtime_error("ListAndWatch ended");
+      if ((count_unhealthy(msg) > base) == down) break;
+    }
+    out.emplace_back(down ? 1 : 0, (mono_ns() - t0) * 1e-9);
+  }
+  return out;
 }
 
 }  // namespace amdgpu_dp

@@ -26,4 +26,14 @@ LoadResult http_load(const std::string& host, int port, const std::string& path,
 LoadResult grpc_load(const std::string& socket_path, const std::string& method, const std::string& req, int conns,
                      double duration_s);
 
+class FixtureBackend;
+
+// Health propagation as a kubelet sees it: inject alternating PRE_RESET / POST_RESET
+// events for `gpu` into a fixture backend and time each until a ListAndWatch message
+// with the matching health arrives on a compiled watcher.  Runs without the GIL, so the
+// Python side of the plugin is measured, not the measuring client.  Returns
+// (1 = Unhealthy transition / 0 = Healthy, seconds) per event.
+std::vector<std::pair<int, double>> health_propagation(FixtureBackend& be, const std::string& socket_path, int gpu,
+                                                       int events);
+
 }  // namespace amdgpu_dp

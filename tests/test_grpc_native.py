@@ -268,3 +268,20 @@ def test_preferred_size_contract(n, server):
     ids = list(v1beta1.PreferredAllocationResponse.FromString(body).container_responses[0].deviceIDs)
     assert st == 0 and len(ids) == 2 and len(set(ids)) == 2 and "dev-001" in ids
     c.close()
+
+
+def test_native_watch_client_follows_list_and_watch(n, server):
+    """The compiled client can hold a ListAndWatch stream like kubelet does; a table
+    change reaches it through the table -> server listener (no notify() call)."""
+    srv, table, path = server
+    c = n.H2Client(path)
+    c.open_stream(v1beta1.METHOD_LIST_AND_WATCH, b"")
+    first = v1beta1.ListAndWatchResponse.FromString(c.next_stream_message(5.0))
+    assert len(first.devices) == 64 and all(d.health == "Healthy" for d in first.devices)
+    for k in range(40):  # more than one receive window of pushes overall
+        table.set_gpu_health((k // 2) % 8, -1, k % 2 == 1)
+        upd = v1beta1.ListAndWatchResponse.FromString(c.next_stream_message(5.0))
+        assert sum(d.health == "Unhealthy" for d in upd.devices) == (0 if k % 2 else 8)
+    srv.stop()
+    assert c.next_stream_message(5.0) is None  # OK trailers end the stream
+    c.close()
