@@ -344,11 +344,16 @@ static void test_reload_races(const std::string& dir) {
           // the server going away mid-call is the point of this test
         }
       });
+    // health flips (table -> server listener pushes) race the server's stop
+    std::thread flipper([&] {
+      for (int k = 0; !done.load(); ++k) table->set_gpu_health(k % 2, -1, k % 3 == 0);
+    });
     std::this_thread::sleep_for(std::chrono::milliseconds(20));
     table->set_gpu_health(0, -1, round % 2);
     srv.notify();
     srv.stop();
     done = true;
+    flipper.join();
     for (auto& t : cs) t.join();
   }
 }
