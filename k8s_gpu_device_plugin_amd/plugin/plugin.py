@@ -90,7 +90,6 @@ class AmdDevicePlugin:
         self.server_kind = server_kind or (cfg.grpc.server if cfg is not None else "python")
         self.table = make_table(str(self.resource), devices, topology, cfg)
         self._lock = threading.RLock()
-        self._cv = threading.Condition()
         self._server = None
         self._native_server = None
         self._serving = False
@@ -235,18 +234,19 @@ class AmdDevicePlugin:
     # ------------------------------------------------------------------ health
     def notify(self) -> None:
         """Wakes ListAndWatch streams (health or stop)."""
-        with self._cv:
-            self._cv.notify_all()
+        self.table.wake()  # grpcio ListAndWatch generators block in table.wait_change
         srv = self._native_server
         if srv is not None:
             srv.notify()
 
     def set_gpu_health(self, gpu: int, partition: int, healthy: bool) -> int:
         changed = self.table.set_gpu_health(gpu, partition, healthy)
+        # The table is the source of truth (the monitor thread may already have applied
+        # an Unhealthy transition natively): mirror it into the Python device view.
+        for d in self._devices:
+            if d.gpu == gpu and (partition < 0 or d.partition < 0 or d.partition == partition):
+                d.health = v1beta1.HEALTHY if self.table.healthy(d.id) else v1beta1.UNHEALTHY
         if changed:
-            for d in self._devices:
-                if d.gpu == gpu and (partition < 0 or d.partition < 0 or d.partition == partition):
-                    d.health = v1beta1.HEALTHY if healthy else v1beta1.UNHEALTHY
             self.notify()
         return changed
 
@@ -303,9 +303,10 @@ class AmdDevicePlugin:
             table.observe(rpc_law, perf() - t0, False)
             yield payload
             while True:
-                with self._cv:
-                    while table.version == version and not self._stopping and ctx.is_active():
-                        self._cv.wait(0.5)
+                # native wait (GIL released): woken by any table change, including the
+                # monitor thread's fail-fast Unhealthy path, or by stop() -> table.wake()
+                while table.version == version and not self._stopping and ctx.is_active():
+                    table.wait_change(version, 500)
                 if self._stopping or not ctx.is_active():
                     return
                 version = table.version

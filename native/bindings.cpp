@@ -285,6 +285,9 @@ PYBIND11_MODULE(_native, m) {
   m.attr("RPC_PRE_START") = static_cast<int>(kRpcPreStart);
 
   py::class_<DeviceTable, std::shared_ptr<DeviceTable>>(m, "DeviceTable")
+      .def("wait_change", &DeviceTable::wait_change, py::call_guard<py::gil_scoped_release>(), py::arg("seen"),
+           py::arg("timeout_ms") = 500)
+      .def("wake", &DeviceTable::wake)
       .def(py::init<TableConfig, std::vector<TableDevice>, Topology>())
       .def_property_readonly("resource_name", [](const DeviceTable& t) { return t.config().resource_name; })
       .def("__len__", &DeviceTable::size)

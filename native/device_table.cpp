@@ -112,7 +112,26 @@ void DeviceTable::add_listener(std::weak_ptr<TableListener> l) {
   listeners_.push_back(std::move(l));
 }
 
+uint64_t DeviceTable::wait_change(uint64_t seen, int timeout_ms) const {
+  std::unique_lock<std::mutex> lk(vmu_);
+  const uint64_t w0 = wakes_;
+  cv_wait_ms(vcv_, lk, timeout_ms, [&] { return version() != seen || wakes_ != w0; });
+  return version();
+}
+
+void DeviceTable::wake() const {
+  {
+    std::lock_guard<std::mutex> lk(vmu_);
+    ++wakes_;
+  }
+  vcv_.notify_all();
+}
+
 void DeviceTable::notify_listeners() {
+  {
+    std::lock_guard<std::mutex> lk(vmu_);  // pairs with wait_change's predicate check
+  }
+  vcv_.notify_all();
   std::vector<std::shared_ptr<TableListener>> live;
   {
     std::lock_guard<std::mutex> lk(lmu_);

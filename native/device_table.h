@@ -15,6 +15,7 @@
 #pragma once
 
 #include <atomic>
+#include <condition_variable>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -92,6 +93,11 @@ class DeviceTable {
 
   uint64_t version() const { return version_.load(std::memory_order_acquire); }
   void add_listener(std::weak_ptr<TableListener> l);
+  // Blocks until version() != seen, wake() is called or timeout_ms passes; returns the
+  // current version.  For waiters that cannot be native listeners (the grpcio server's
+  // ListAndWatch generators), called with the GIL released.
+  uint64_t wait_change(uint64_t seen, int timeout_ms) const;
+  void wake() const;
   std::string list_and_watch() const;  // ListAndWatchResponse bytes (cached)
 
   // RPC bodies.  Return true and response bytes in *out, or false and an error message.
@@ -125,6 +131,9 @@ class DeviceTable {
   std::unique_ptr<std::atomic<uint8_t>[]> health_;
   std::mutex wmu_;                                // serialises writers only
   std::mutex lmu_;                                // listeners_
+  mutable std::mutex vmu_;                        // version waiters
+  mutable std::condition_variable vcv_;
+  mutable uint64_t wakes_ = 0;
   std::vector<std::weak_ptr<TableListener>> listeners_;
   std::shared_ptr<const Topology> topo_;          // atomic_load / atomic_store
   std::shared_ptr<const std::string> law_;        // cached ListAndWatchResponse

@@ -151,3 +151,23 @@ def test_concurrent_clients(plugin_dir, server_kind):
             t.join()
         p.stop()
         assert not errors
+
+
+def test_native_table_change_reaches_watchers_without_notify(plugin_dir, server_kind):
+    """The monitor thread's fail-fast path changes the table directly (no Python
+    notify): both servers must push it at once (native: table listener; grpcio: the
+    generator blocks in table.wait_change), and the Python device view follows."""
+    with KubeletStub(plugin_dir) as k:
+        p, g = _plugin(plugin_dir, server_kind, "2gpu_spx", "none")
+        p.start()
+        try:
+            w = k.watch("amd-gpu.sock")
+            w.next()
+            t0 = time.monotonic()
+            assert p.table.set_gpu_health(1, -1, False) == 1  # bypasses AmdDevicePlugin
+            t1, devs = w.next()
+            assert [h for _, h, _ in devs] == ["Healthy", "Unhealthy"] and t1 - t0 < 0.25
+            assert p.set_gpu_health(1, -1, False) == 0  # manager catching up: no change, no push
+            assert p.devices()[devs[1][0]].health == v1beta1.UNHEALTHY
+        finally:
+            p.stop()
