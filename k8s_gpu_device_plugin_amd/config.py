@@ -77,6 +77,13 @@ class GrpcConfig:
 
 
 @dataclass
+class PodResourcesConfig:
+    enabled: bool = False        # poll kubelet's PodResources API -> allocation_info metric
+    socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"
+    intervalS: float = 10.0
+
+
+@dataclass
 class Config:
     webListenAddress: str = "0.0.0.0:9100"
     migStrategy: str = "none"            # alias partitionStrategy (none|single|mixed)
@@ -100,6 +107,7 @@ class Config:
     health: HealthConfig = field(default_factory=HealthConfig)
     http: HttpConfig = field(default_factory=HttpConfig)
     grpc: GrpcConfig = field(default_factory=GrpcConfig)
+    podResources: PodResourcesConfig = field(default_factory=PodResourcesConfig)
     retrySeconds: float = 30.0            # plugin start retry (plugin/manager.go:135-138)
 
     @property
@@ -131,7 +139,7 @@ def split_host_port(addr: str) -> tuple[str, int]:
 
 
 _NESTED = {"log": LogConfig, "sharing": SharingConfig, "telemetry": TelemetryConfig,
-           "health": HealthConfig, "http": HttpConfig, "grpc": GrpcConfig}
+           "health": HealthConfig, "http": HttpConfig, "grpc": GrpcConfig, "podResources": PodResourcesConfig}
 
 
 def _ci_lookup(d: dict, name: str):
@@ -247,6 +255,8 @@ def validate(cfg: Config) -> Config:
         raise ConfigError("grpc.server must be native|python")
     if cfg.http.server not in ("native", "python"):
         raise ConfigError("http.server must be native|python")
+    if cfg.podResources.intervalS <= 0:
+        raise ConfigError("podResources.intervalS must be > 0")
     if cfg.telemetry.intervalMs < 10:
         raise ConfigError("telemetry.intervalMs must be >= 10")
     if not cfg.resourcePrefix or "/" in cfg.resourcePrefix:

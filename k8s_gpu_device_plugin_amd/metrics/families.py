@@ -73,6 +73,11 @@ FAMILIES = (
            "Advertised devices per resource and health"),
     Family("amdgpu_device_plugin_registered", "gauge", ("resource",), "manager",
            "Resource registered with kubelet"),
+    # --- kubelet PodResources (podResources.enabled) ---
+    Family("amdgpu_device_plugin_allocation_info", "gauge", ("resource", "device_id", "namespace", "pod", "container"),
+           "manager", "Advertised device held by a container (value 1)"),
+    Family("amdgpu_device_plugin_pod_resources_up", "gauge", (), "manager",
+           "Last kubelet PodResources List succeeded"),
 )
 
 BY_NAME = {f.name: f for f in FAMILIES}
@@ -96,6 +101,9 @@ PROMQL_EXAMPLES = (
     ("Allocate p99 over 5 minutes",
      'histogram_quantile(0.99, sum by (le) (rate(amdgpu_device_plugin_rpc_duration_seconds_bucket{rpc="Allocate"}[5m])))'),
     ("Down xGMI links", "amdgpu_xgmi_link_up == 0"),
+    ("Partition busy per workload (podResources.enabled)",
+     "amdgpu_partition_gfx_busy_percent * on(device_id) group_left(namespace, pod, container) "
+     "amdgpu_device_plugin_allocation_info"),
     ("xGMI traffic per link (bytes/s)", "rate(amdgpu_xgmi_read_bytes_total[1m]) + rate(amdgpu_xgmi_write_bytes_total[1m])"),
 )
 

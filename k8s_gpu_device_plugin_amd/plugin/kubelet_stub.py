@@ -172,3 +172,56 @@ class KubeletStub:
 
     def __exit__(self, *exc) -> None:
         self.stop()
+
+
+class PodResourcesStub:
+    """In-process kubelet PodResources ``v1`` server (``List`` only) on a unix socket.
+    ``set_pods([(namespace, pod, [(container, resource, [device ids])])])``."""
+
+    def __init__(self, socket_path: str) -> None:
+        from ..api import podresources_v1 as pr
+        self._pr = pr
+        self.socket_path = socket_path
+        self._resp = pr.ListPodResourcesResponse()
+        self._lock = threading.Lock()
+        self.calls = 0
+        self._server = None
+
+    def set_pods(self, pods) -> None:
+        pr = self._pr
+        resp = pr.ListPodResourcesResponse()
+        for ns, name, containers in pods:
+            p = resp.pod_resources.add(name=name, namespace=ns)
+            for cname, resource, ids in containers:
+                c = p.containers.add(name=cname)
+                c.devices.add(resource_name=resource, device_ids=list(ids))
+        with self._lock:
+            self._resp = resp
+
+    def start(self) -> "PodResourcesStub":
+        pr = self._pr
+
+        def list_(req, ctx):
+            with self._lock:
+                self.calls += 1
+                return self._resp
+
+        handler = grpc.method_handlers_generic_handler(pr.SERVICE, {
+            "List": grpc.unary_unary_rpc_method_handler(
+                list_, request_deserializer=pr.ListPodResourcesRequest.FromString,
+                response_serializer=pr.ListPodResourcesResponse.SerializeToString)})
+        os.makedirs(os.path.dirname(self.socket_path), exist_ok=True)
+        self._server = grpc.server(concurrent.futures.ThreadPoolExecutor(max_workers=2))
+        self._server.add_generic_rpc_handlers((handler,))
+        self._server.add_insecure_port("unix://" + self.socket_path)
+        self._server.start()
+        return self
+
+    def stop(self) -> None:
+        if self._server is not None:
+            self._server.stop(grace=0.2).wait(2.0)
+            self._server = None
+        try:
+            os.remove(self.socket_path)
+        except FileNotFoundError:
+            pass

@@ -37,8 +37,8 @@ from .plugin import AmdDevicePlugin
 
 log = get_logger("manager")
 
-EV_STOP, EV_RESTART, EV_RETRY, EV_KUBELET, EV_HEALTH, EV_REDISCOVER, EV_VERIFIED = (
-    "stop", "restart", "retry", "kubelet", "health", "rediscover", "verified")
+EV_STOP, EV_RESTART, EV_RETRY, EV_KUBELET, EV_HEALTH, EV_REDISCOVER, EV_VERIFIED, EV_PODRES = (
+    "stop", "restart", "retry", "kubelet", "health", "rediscover", "verified", "podresources")
 HEALTH_LOG_LEN = 4096
 
 
@@ -88,6 +88,7 @@ class PluginManager:
         # recovery canary pending or failed.  Survives plugin reloads.
         self._held_unhealthy: set[int] = set()
         self._verify_pool: concurrent.futures.ThreadPoolExecutor | None = None
+        self.podres = None  # PodResourcesWatcher when podResources.enabled
 
     # ------------------------------------------------------------ public API
     def restart(self) -> None:
@@ -164,6 +165,8 @@ class PluginManager:
                     self._apply_health(ev[1])
                 elif kind == EV_VERIFIED:
                     self._apply_verified(*ev[1:])
+                elif kind == EV_PODRES:
+                    pass  # allocation map changed: _publish_metrics below re-renders it
                 elif kind == EV_REDISCOVER:
                     self._check_inventory()
             except Exception as e:
@@ -381,6 +384,11 @@ class PluginManager:
             t = threading.Thread(target=fn, name=name, daemon=True)
             t.start()
             self._threads.append(t)
+        if self.cfg.podResources.enabled:
+            from .podresources import PodResourcesWatcher
+            self.podres = PodResourcesWatcher(self.cfg.podResources.socket, self.cfg.podResources.intervalS,
+                                              self.cfg.resourcePrefix, lambda: self.events.put((EV_PODRES,)))
+            self.podres.start()
 
     def _start_telemetry(self) -> None:
         if self.cfg.health.enabled:
@@ -421,6 +429,10 @@ class PluginManager:
                   "# TYPE amdgpu_device_plugin_registered gauge"]
         for p in self.plugins:
             lines.append('amdgpu_device_plugin_registered{resource="%s"} %d' % (p.resource, int(p.registered)))
+        if self.podres is not None:
+            from .podresources import render
+            allocs, up = self.podres.snapshot()
+            lines += render(allocs, up)
         self.exporter.set_extra("\n".join(lines) + "\n")
 
     def _shutdown(self) -> None:
@@ -429,6 +441,8 @@ class PluginManager:
             self._verify_pool.shutdown(wait=False, cancel_futures=True)
         self._stop_flag.set()
         self._running.clear()
+        if self.podres is not None:
+            self.podres.stop()
         self.stop_plugins()
         self.exporter.stop()
         self.monitor.stop()

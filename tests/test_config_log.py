@@ -146,3 +146,4 @@ def test_shipped_configs_are_valid():
     mounts = {m["mountPath"] for m in ds["containers"][0]["volumeMounts"]}
     assert {"/var/lib/kubelet/device-plugins", "/dev/kfd", "/dev/dri"} <= mounts
     assert os.path.dirname(cfg.nodeFeatureFile) in mounts
+    assert cfg.podResources.enabled and os.path.dirname(cfg.podResources.socket) in mounts

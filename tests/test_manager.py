@@ -359,3 +359,32 @@ def test_reset_state_survives_a_reload(make_cfg, plugin_dir, run_manager):
         assert m.plugins[0].table.healthy_count() == 1  # still held Unhealthy after the reload
         be.inject_event(be_event(m, "EVT_POST_RESET", 1))
         assert _wait(lambda: m.plugins[0].table.healthy_count() == 2)
+
+
+def test_pod_resources_allocation_metric(make_cfg, plugin_dir, run_manager, tmp_path):
+    """podResources.enabled: the kubelet PodResources List is polled and every held
+    device of ours appears as allocation_info{namespace,pod,container}; other vendors'
+    resources are ignored; a kubelet outage flips pod_resources_up to 0."""
+    from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import PodResourcesStub
+    sock = str(tmp_path / "pod-resources" / "kubelet.sock")
+    stub = PodResourcesStub(sock).start()
+    try:
+        with KubeletStub(plugin_dir) as k:
+            m = run_manager(make_cfg(podResources={"enabled": True, "socket": sock, "intervalS": 0.05}))
+            k.wait_for_registrations(1)
+            ids = m.plugins[0].table.ids()
+            stub.set_pods([("ml", "trainer-0", [("main", "amd.com/gpu", ids[:1]), ("side", "nvidia.com/gpu", ["x"])]),
+                           ("ml", "trainer-1", [("main", "amd.com/gpu", ids[1:2])])])
+            want0 = ('amdgpu_device_plugin_allocation_info{resource="amd.com/gpu",device_id="%s",namespace="ml",'
+                     'pod="trainer-0",container="main"} 1' % ids[0])
+            assert _wait(lambda: want0 in m.exporter.render())
+            text = m.exporter.render()
+            assert "amdgpu_device_plugin_pod_resources_up 1" in text
+            assert 'pod="trainer-1"' in text and "nvidia.com" not in text
+            stub.set_pods([("ml", "trainer-1", [("main", "amd.com/gpu", ids[1:2])])])  # trainer-0 finished
+            assert _wait(lambda: 'pod="trainer-0"' not in m.exporter.render())
+            stub.stop()
+            assert _wait(lambda: "amdgpu_device_plugin_pod_resources_up 0" in m.exporter.render())
+            assert 'pod="trainer-1"' in m.exporter.render()  # last known map is kept
+    finally:
+        stub.stop()

