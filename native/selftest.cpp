@@ -170,11 +170,22 @@ static void test_grpc_server(std::shared_ptr<FixtureBackend> be, const std::stri
         ++errors;
       }
     });
+  // the monitor thread's fail-fast path pushes through the table listener while the
+  // main thread also flips health and clients call in
+  auto mon = std::make_shared<HealthMonitor>(be, 2);
+  mon->set_gpu_count(static_cast<int>(gpus.size()));
+  mon->set_fast_tables({table});
+  mon->start();
   for (int k = 0; k < 50; ++k) {
     table->set_gpu_health(k % 4, -1, k % 2);
     srv.notify();
+    HwEvent e;
+    e.kind = k % 2 ? kEvtPostReset : kEvtPreReset;
+    e.gpu = k % 4;
+    be->inject_event(e);
   }
   for (auto& t : ts) t.join();
+  mon->stop();
   CHECK(errors.load() == 0);
   CHECK(srv.requests() >= 1800);
   srv.stop();
