@@ -6,6 +6,7 @@
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
+#include <sys/time.h>
 #include <sys/stat.h>
 #include <sys/un.h>
 #include <unistd.h>
@@ -813,6 +814,7 @@ H2Client::H2Client(const std::string& socket_path, double timeout_s)
     close();
     throw std::runtime_error("H2Client: connect " + socket_path + ": " + strerror(e));
   }
+  set_recv_timeout(timeout_ms_);
   std::string o(kPreface, kPrefaceLen);
   frame(&o, 6, kSettings, 0, 0);
   o.push_back(0);
@@ -827,6 +829,13 @@ H2Client::~H2Client() { close(); }
 void H2Client::close() {
   if (fd_ >= 0) ::close(fd_);
   fd_ = -1;
+}
+
+void H2Client::set_recv_timeout(int ms) {
+  struct timeval tv;
+  tv.tv_sec = ms / 1000;
+  tv.tv_usec = (ms % 1000) * 1000;
+  setsockopt(fd_, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
 }
 
 void H2Client::send_all(const std::string& s) {
@@ -856,11 +865,12 @@ bool H2Client::read_frame(uint8_t* type, uint8_t* flags, uint32_t* sid, std::str
         return true;
       }
     }
-    struct pollfd pf {fd_, POLLIN, 0};
-    if (poll(&pf, 1, timeout_ms_) <= 0) throw std::runtime_error("H2Client: timed out waiting for response");
+    // blocking recv bounded by SO_RCVTIMEO: one syscall per response instead of poll + recv
     const ssize_t r = recv(fd_, buf, sizeof(buf), 0);
     if (r <= 0) {
       if (r < 0 && errno == EINTR) continue;
+      if (r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK))
+        throw std::runtime_error("H2Client: timed out waiting for response");
       return false;
     }
     in_.append(buf, static_cast<size_t>(r));
@@ -1015,13 +1025,11 @@ void H2Client::open_stream(std::string_view path, std::string_view req) {
 
 int H2Client::next_stream_message(std::string* resp, int timeout_ms) {
   if (watch_sid_ == 0) throw std::runtime_error("H2Client: no open stream");
-  const int saved = timeout_ms_;
-  timeout_ms_ = timeout_ms;
+  set_recv_timeout(timeout_ms);
   struct Restore {
-    int* p;
-    int v;
-    ~Restore() { *p = v; }
-  } restore{&timeout_ms_, saved};
+    H2Client* c;
+    ~Restore() { c->set_recv_timeout(c->timeout_ms_); }
+  } restore{this};
   uint8_t type, flags;
   uint32_t fsid;
   std::string payload;

@@ -83,6 +83,7 @@ class H2Client {
 
  private:
   void send_all(const std::string& s);
+  void set_recv_timeout(int ms);
   bool read_frame(uint8_t* type, uint8_t* flags, uint32_t* sid, std::string* payload);
   // Sends HEADERS + gRPC-framed request DATA (split into frames, within flow control).
   void send_request(uint32_t sid, std::string_view path, std::string_view req);
