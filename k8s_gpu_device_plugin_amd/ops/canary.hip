@@ -131,6 +131,7 @@ __global__ void __launch_bounds__(64) mfma_gemm(const short* __restrict__ A, con
   const int lane = threadIdx.x;
   const int r = lane & 31, h = lane >> 5;
   const int tm = blockIdx.y * 32, tn = blockIdx.x * 32;
+  if (tm + 32 > M || tn + 32 > N) return;  // host checks shapes; never touch memory past them
   f32x16 acc;
   for (int i = 0; i < 16; ++i) acc[i] = 0.f;
   for (int k0 = 0; k0 < K; k0 += 16) {
