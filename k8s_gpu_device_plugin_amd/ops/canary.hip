@@ -75,7 +75,10 @@ __device__ __forceinline__ int b_val(uint32_t blk, int k, int col) {
 
 // One wave per block computes C[32x32] = A[32xK] * B[Kx32] with K = 16 * ksteps, then
 // every lane checks its 16 accumulator registers against a scalar integer reference.
-__global__ void __launch_bounds__(64) mfma_exact(int ksteps, unsigned long long* __restrict__ errors) {
+// Blocks below `inject_blocks` perturb one A operand (lane 0, first k-step): the fault
+// injection that proves the verifier sees a wrong matrix-core result.
+__global__ void __launch_bounds__(64) mfma_exact(int ksteps, int inject_blocks,
+                                                 unsigned long long* __restrict__ errors) {
   const int lane = threadIdx.x;
   const int r = lane & 31, h = lane >> 5;
   const uint32_t blk = blockIdx.x;
@@ -85,7 +88,8 @@ __global__ void __launch_bounds__(64) mfma_exact(int ksteps, unsigned long long*
     bf16x8 a, b;
     for (int j = 0; j < 8; ++j) {
       const int k = s * 16 + 8 * h + j;  // lane l holds A[r][8h+j], B[8h+j][r]
-      a[j] = bf16_of_int(a_val(blk, r, k));
+      a[j] = bf16_of_int(a_val(blk, r, k) + ((s == 0 && j == 0 && lane == 0 && static_cast<int>(blk) < inject_blocks)
+                                                   ? 1 : 0));
       b[j] = bf16_of_int(b_val(blk, k, r));
     }
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
@@ -341,7 +345,7 @@ int amdgpu_canary_run(int device, unsigned long long hbm_bytes, int passes, int 
     t_read += tr;
   }
   // MFMA exactness: 2 * #CUs single-wave blocks, K = 16 * 32
-  hipLaunchKernelGGL(mfma_exact, dim3(prop.multiProcessorCount * 2), dim3(64), 0, 0, 32, d_err + 1);
+  hipLaunchKernelGGL(mfma_exact, dim3(prop.multiProcessorCount * 2), dim3(64), 0, 0, 32, 0, d_err + 1);
   CANARY_CHECK(hipGetLastError());
   // MFMA rate
   CANARY_CHECK(hipMalloc(&sink, static_cast<size_t>(prop.multiProcessorCount) * 8 * 256 * sizeof(float)));
@@ -406,6 +410,26 @@ long long amdgpu_canary_detects_corruption(int device, unsigned long long hbm_by
   }
   if (d_err) (void)hipFree(d_err);
   if (buf) (void)hipFree(buf);
+  return rc;
+}
+
+// Fault-injection check of the MFMA verifier: `inject_blocks` of the 2 * #CUs exactness
+// blocks compute with one perturbed operand.  Returns the mismatching accumulator
+// registers found (0 expected without injection), -1 on a HIP error.
+long long amdgpu_canary_mfma_detects(int device, int inject_blocks) {
+  unsigned long long* d_err = nullptr;
+  unsigned long long h_err = 0;
+  hipDeviceProp_t prop;
+  if (inject_blocks < 0 || hipSetDevice(device) != hipSuccess || hipGetDeviceProperties(&prop, device) != hipSuccess)
+    return -1;
+  long long rc = -1;
+  if (hipMalloc(&d_err, sizeof(h_err)) == hipSuccess && hipMemset(d_err, 0, sizeof(h_err)) == hipSuccess) {
+    hipLaunchKernelGGL(mfma_exact, dim3(prop.multiProcessorCount * 2), dim3(64), 0, 0, 32, inject_blocks, d_err);
+    if (hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+        hipMemcpy(&h_err, d_err, sizeof(h_err), hipMemcpyDeviceToHost) == hipSuccess)
+      rc = static_cast<long long>(h_err);
+  }
+  if (d_err) (void)hipFree(d_err);
   return rc;
 }
 

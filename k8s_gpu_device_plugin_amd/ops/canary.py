@@ -48,6 +48,8 @@ def load():
         lib.amdgpu_canary_mfma_gemm.restype = ctypes.c_int
         lib.amdgpu_canary_detects_corruption.argtypes = [ctypes.c_int, ctypes.c_ulonglong, ctypes.c_int]
         lib.amdgpu_canary_detects_corruption.restype = ctypes.c_longlong
+        lib.amdgpu_canary_mfma_detects.argtypes = [ctypes.c_int, ctypes.c_int]
+        lib.amdgpu_canary_mfma_detects.restype = ctypes.c_longlong
         lib.amdgpu_canary_hbm_sweep.argtypes = [ctypes.c_int, ctypes.c_ulonglong, ctypes.c_int, ctypes.c_int,
                                                 ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                                 ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_ulonglong)]
@@ -73,6 +75,12 @@ def run(device: int = 0, hbm_bytes: int = 1 << 30, passes: int = 3, mfma_iters: 
 def detects_corruption(device: int = 0, hbm_bytes: int = 64 << 20, flips: int = 5) -> int:
     """Fault-injection check of the HBM verifier; returns the mismatches it found."""
     return int(load().amdgpu_canary_detects_corruption(int(device), int(hbm_bytes), int(flips)))
+
+
+def mfma_detects_corruption(device: int = 0, inject_blocks: int = 3) -> int:
+    """Fault-injection check of the MFMA exactness verifier; returns the wrong
+    accumulator registers it found (0 expected with inject_blocks=0)."""
+    return int(load().amdgpu_canary_mfma_detects(int(device), int(inject_blocks)))
 
 
 SWEEP_VARIANTS = {0: "u4 grid-stride", 1: "u8 grid-stride", 2: "u4 nontemporal", 3: "u8 nontemporal",

@@ -93,6 +93,14 @@ def test_canary_verifier_catches_injected_corruption():
     assert canary.detects_corruption(0, 64 << 20, 7) == 7
 
 
+def test_canary_mfma_verifier_catches_injected_fault():
+    """One perturbed bf16 operand in 3 of the exactness blocks must surface as wrong
+    accumulator registers; none without injection."""
+    from k8s_gpu_device_plugin_amd.ops import canary
+    assert canary.mfma_detects_corruption(0, 0) == 0
+    assert canary.mfma_detects_corruption(0, 3) > 0
+
+
 def test_canary_isolated_subprocess():
     from k8s_gpu_device_plugin_amd.ops import canary
     r = canary.run_isolated(0, 128 << 20)
