@@ -17,7 +17,7 @@ step() {  # step <name> <timeout> <cmd...>
 }
 for s in ${STEPS:-pytest smoke bench prof}; do
   case $s in
-    pytest) step pytest_gpu 420 python -m pytest tests -q -m gpu -s -p no:cacheprovider ;;
+    pytest) step pytest_gpu 420 python -u -m pytest tests -x -v -m gpu -s -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     smoke)  step smoke 240 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  step bench 300 python bench.py ${BENCH_ARGS:-} ;;
     suite)  step suite 600 python -m k8s_gpu_device_plugin_amd.benchmark.suite --json "$OUT/baseline_suite_gpu.json" ;;
