@@ -230,6 +230,11 @@ def main() -> int:
     mine = {"elapsed": elapsed, "scrape_time": scrape_time, "alloc": rec[0], "pref": rec[1], "scrape": rec[2],
             "alloc_native": rec[3], "pref_native": rec[4],
             "canary": canary_res, "body": body_len}
+    # Untimed speed-of-light reference: the same send/epoll_wait/recv/send/recv exchange
+    # between two threads with no HTTP/2, HPACK or protobuf work (sizes ~ this Allocate's).
+    alloc_resp_len = len(alloc_raw(alloc_req))
+    floor = n.uds_pingpong(10000, 500, 9 + 80 + 9 + 5 + len(alloc_req), 9 + 20 + 9 + 5 + alloc_resp_len + 9 + 16)
+    mine["uds_floor_p50"] = _pct(floor, 0.5)
     if world > 1:
         gathered = [None] * world
         dist.all_gather_object(gathered, mine)
@@ -260,6 +265,7 @@ def main() -> int:
                        "parallelism": "%d kubelet-client rank(s), 1 plugin daemon" % world,
                        "backend": info["backend"], "grpc_server": args.grpc_server},
             "allocate_p50_us": round(p50, 2), "allocate_p99_us": round(_pct(allocs_native, 0.99) * 1e6, 2),
+            "uds_roundtrip_floor_p50_us": round(gathered[0]["uds_floor_p50"] * 1e6, 2),
             "allocate_p50_us_grpcio_client": round(p50_grpcio, 2),
             "allocate_p99_us_grpcio_client": round(_pct(allocs, 0.99) * 1e6, 2),
             "preferred_p50_us": round(_pct(prefs_native, 0.5) * 1e6, 2),

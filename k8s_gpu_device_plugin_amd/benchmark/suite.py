@@ -283,12 +283,21 @@ def health_propagation(events=60):
         node.close()
 
 
-RUNNERS = {"health": health_propagation, "1": config1, "2": config2, "3": config3, "4": config4, "5": config5, "scaling": scaling}
+def uds_floor():
+    """Speed-of-light reference for one kubelet RPC: two threads exchange Allocate-sized
+    messages over a unix socket with the server's exact syscalls (epoll_wait, recv, send)
+    and no protocol work.  Allocate p50 minus this is the plugin's own cost."""
+    lat = native.load().uds_pingpong(20000, 1000, 140, 250)
+    return {"config": "unix-socket round trip floor (no HTTP/2, HPACK, protobuf or table work)",
+            "p50_us": us(pct(lat, 0.5)), "p99_us": us(pct(lat, 0.99)), "round_trips": len(lat)}
+
+
+RUNNERS = {"floor": uds_floor, "health": health_propagation, "1": config1, "2": config2, "3": config3, "4": config4, "5": config5, "scaling": scaling}
 
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
-    ap.add_argument("--configs", default="1,2,3,4,5,scaling,health")
+    ap.add_argument("--configs", default="floor,1,2,3,4,5,scaling,health")
     ap.add_argument("--json", default="")
     a = ap.parse_args(argv)
     from ..utils.log import init_logger

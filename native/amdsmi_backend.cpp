@@ -202,7 +202,9 @@ class AmdSmiBackend : public Backend {
     }
     gpus->clear();
     procs_.clear();
+    bdf_keys_.clear();
     for (auto& kv : groups) {
+      bdf_keys_.push_back(kv.first);
       auto& plist = kv.second;
       std::stable_sort(plist.begin(), plist.end(),
                        [](const Proc& a, const Proc& b) { return a.partition_id < b.partition_id; });
@@ -463,14 +465,11 @@ class AmdSmiBackend : public Backend {
         }
   }
 
-  int gpu_of_bdf(const amdsmi_bdf_t& b) {
-    const uint64_t k = bdf_key(b);
-    for (size_t g = 0; g < procs_.size(); ++g) {
-      amdsmi_bdf_t gb{};
-      if (amdsmi_get_gpu_device_bdf(procs_[g][0], &gb) == AMDSMI_STATUS_SUCCESS && bdf_key(gb) == k)
-        return static_cast<int>(g);
-    }
-    return -1;
+  // Peer lookup for every xGMI link of every sample: BDF keys are cached at discovery
+  // (7 links x 8 GPUs per tick would otherwise re-query amdsmi 8 times per link).
+  int gpu_of_bdf(const amdsmi_bdf_t& b) const {
+    const auto it = std::find(bdf_keys_.begin(), bdf_keys_.end(), bdf_key(b));
+    return it == bdf_keys_.end() ? -1 : static_cast<int>(it - bdf_keys_.begin());
   }
 
   // Fills per-link peer/up/read/write from amdsmi link metrics + xgmi link status.
@@ -509,6 +508,7 @@ class AmdSmiBackend : public Backend {
   std::mutex evt_mu_;                   // held across the blocking event wait
   std::atomic<bool> evt_live_{false};   // armed with at least one source
   std::vector<std::vector<amdsmi_processor_handle>> procs_;
+  std::vector<uint64_t> bdf_keys_;  // physical-device BDF key per GPU index (procs_ order)
   std::vector<GpuInfo> gpus_;
   std::vector<amdsmi_processor_handle> armed_handles_;
   std::vector<amdsmi_processor_handle> armed_for_;  // processor set at arming time

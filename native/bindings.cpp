@@ -595,6 +595,12 @@ PYBIND11_MODULE(_native, m) {
         return health_propagation(*fx, sock, gpu, events);
       },
       py::arg("backend"), py::arg("socket_path"), py::arg("gpu"), py::arg("events") = 60);
+  m.def("uds_pingpong",
+        [](int n, int warmup, int req_bytes, int resp_bytes) {
+          py::gil_scoped_release rel;
+          return uds_pingpong(n, warmup, req_bytes, resp_bytes);
+        },
+        py::arg("n") = 10000, py::arg("warmup") = 500, py::arg("req_bytes") = 128, py::arg("resp_bytes") = 256);
   m.def("grpc_load",
         [load_dict](const std::string& sock, const std::string& method, const py::bytes& req, int conns,
                     double duration_s) {

@@ -4,7 +4,9 @@
 #include <errno.h>
 #include <netdb.h>
 #include <netinet/in.h>
+#include <fcntl.h>
 #include <netinet/tcp.h>
+#include <sys/epoll.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -169,6 +171,92 @@ LoadResult grpc_load(const std::string& socket_path, const std::string& method, 
   for (auto& t : ts) t.join();
   total.elapsed_s = duration_s;
   return total;
+}
+
+std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_bytes) {
+  if (n < 0 || warmup < 0 || req_bytes <= 0 || resp_bytes <= 0 || req_bytes > (1 << 20) || resp_bytes > (1 << 20))
+    throw std::invalid_argument("uds_pingpong: bad sizes");
+  int sv[2];
+  if (socketpair(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0, sv) != 0)
+    throw std::runtime_error(std::string("socketpair: ") + strerror(errno));
+  const int cfd = sv[0], sfd = sv[1];
+  fcntl(sfd, F_SETFL, fcntl(sfd, F_GETFL) | O_NONBLOCK);
+  struct timeval tv {5, 0};  // a dead server thread ends the client's recv, not the process
+  setsockopt(cfd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+  const int ep = epoll_create1(EPOLL_CLOEXEC);
+  struct epoll_event ev {};
+  ev.events = EPOLLIN | EPOLLRDHUP;
+  ev.data.fd = sfd;
+  epoll_ctl(ep, EPOLL_CTL_ADD, sfd, &ev);
+  std::thread server([&] {  // the plugin server's syscall pattern: epoll_wait, recv, send
+    std::vector<char> in(static_cast<size_t>(req_bytes) + 65536), out(static_cast<size_t>(resp_bytes), 'r');
+    size_t have = 0;
+    epoll_event evs[4];
+    for (;;) {
+      const int k = epoll_wait(ep, evs, 4, 1000);
+      if (k < 0 && errno != EINTR) return;
+      if (k <= 0) continue;
+      bool closed = false;
+      for (;;) {
+        const ssize_t r = recv(sfd, in.data() + have, in.size() - have, 0);
+        if (r > 0) {
+          have += static_cast<size_t>(r);
+          if (have >= in.size()) break;
+        } else if (r < 0 && errno == EINTR) {
+          continue;
+        } else {
+          if (r == 0 || errno != EAGAIN) closed = true;
+          break;
+        }
+      }
+      while (have >= static_cast<size_t>(req_bytes)) {
+        have -= static_cast<size_t>(req_bytes);
+        size_t off = 0;
+        while (off < out.size()) {
+          const ssize_t w = send(sfd, out.data() + off, out.size() - off, MSG_NOSIGNAL);
+          if (w > 0)
+            off += static_cast<size_t>(w);
+          else if (w < 0 && (errno == EAGAIN || errno == EINTR))
+            continue;
+          else
+            return;
+        }
+      }
+      if (closed) return;
+    }
+  });
+  std::vector<double> lat;
+  lat.reserve(static_cast<size_t>(n));
+  const std::string req(static_cast<size_t>(req_bytes), 'q');
+  std::vector<char> buf(static_cast<size_t>(resp_bytes));
+  bool failed = false;
+  for (int i = 0; i < n + warmup && !failed; ++i) {
+    const int64_t t0 = mono_ns();
+    if (send(cfd, req.data(), req.size(), MSG_NOSIGNAL) != static_cast<ssize_t>(req.size())) {
+      failed = true;
+      break;
+    }
+    size_t got = 0;
+    while (got < buf.size()) {
+      const ssize_t r = recv(cfd, buf.data() + got, buf.size() - got, 0);
+      if (r > 0) {
+        got += static_cast<size_t>(r);
+      } else if (r < 0 && errno == EINTR) {
+        continue;
+      } else {
+        failed = true;
+        break;
+      }
+    }
+    if (i >= warmup && !failed) lat.push_back((mono_ns() - t0) * 1e-9);
+  }
+  shutdown(cfd, SHUT_RDWR);  // the server sees EOF and leaves its loop
+  server.join();
+  close(cfd);
+  close(sfd);
+  close(ep);
+  if (failed) throw std::runtime_error("uds_pingpong: socket error");
+  return lat;
 }
 
 namespace {

@@ -26,6 +26,14 @@ LoadResult http_load(const std::string& host, int port, const std::string& path,
 LoadResult grpc_load(const std::string& socket_path, const std::string& method, const std::string& req, int conns,
                      double duration_s);
 
+// Speed-of-light reference for one unary RPC on a unix socket: a client thread and an
+// epoll server thread exchange `req_bytes` / `resp_bytes` with exactly the syscalls the
+// plugin's Allocate path makes (client send + blocking recv; server epoll_wait + recv +
+// send) and no protocol work at all.  Per-round-trip latency in seconds, n samples after
+// `warmup` untimed ones.  Allocate p50 minus this p50 is what HTTP/2 + HPACK + protobuf +
+// the device table cost.
+std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_bytes);
+
 class FixtureBackend;
 
 // Health propagation as a kubelet sees it: inject alternating PRE_RESET / POST_RESET

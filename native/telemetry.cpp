@@ -129,20 +129,23 @@ void Exporter::loop() {
 void Exporter::sample_once() {
   std::lock_guard<std::mutex> slk(sample_mu_);
   std::shared_ptr<Backend> be = backend_;
-  size_t n;
+  // The inventory may be a subset of the node (`devices: "4-7"`): sample, report health
+  // for and label each GPU by its backend index, never by its position in the subset.
+  std::vector<int> index;
   uint64_t gen;
   {
     std::lock_guard<std::mutex> lk(mu_);
-    n = gpus_.size();
+    for (const auto& g : gpus_) index.push_back(g.index);
     gen = inventory_gen_;
   }
+  const size_t n = index.size();
   std::vector<GpuSample> samples(n);
   std::vector<char> ok(n, 0);
   const int64_t t0 = mono_ns();
   for (size_t g = 0; g < n; ++g) {
-    if (be) ok[g] = be->sample(static_cast<int>(g), &samples[g]) ? 1 : 0;
+    if (be) ok[g] = be->sample(index[g], &samples[g]) ? 1 : 0;
     if (!ok[g]) sample_errors_.fetch_add(1, std::memory_order_relaxed);
-    if (monitor_) monitor_->on_sample(static_cast<int>(g), ok[g], samples[g]);
+    if (monitor_) monitor_->on_sample(index[g], ok[g], samples[g]);
   }
   const double dt = (mono_ns() - t0) * 1e-9;
   if (be) {
@@ -184,7 +187,7 @@ void Exporter::render_gpu_text(const std::vector<GpuSample>& samples, const std:
   std::string o;
   o.reserve(4096 + gpus.size() * 4096);
   std::vector<std::string> gl(gpus.size());
-  for (size_t g = 0; g < gpus.size(); ++g) gpu_labels(&gl[g], static_cast<int>(g));
+  for (size_t g = 0; g < gpus.size(); ++g) gpu_labels(&gl[g], gpus[g].index);
 
   append_header(&o, "amdgpu_info", "Static inventory of each physical AMD GPU (value is always 1).", "gauge");
   for (size_t g = 0; g < gpus.size(); ++g) {
@@ -309,17 +312,24 @@ void Exporter::render_gpu_text(const std::vector<GpuSample>& samples, const std:
   }
   {  // partitions
     std::string info, busy, vram;
+    std::vector<int> pos;  // backend GPU index -> position in this (possibly subset) inventory
+    for (size_t g = 0; g < gpus.size(); ++g) {
+      if (gpus[g].index < 0) continue;
+      if (static_cast<size_t>(gpus[g].index) >= pos.size()) pos.resize(gpus[g].index + 1, -1);
+      pos[gpus[g].index] = static_cast<int>(g);
+    }
     for (const auto& pl : labels) {
-      if (pl.gpu < 0 || pl.gpu >= static_cast<int>(gpus.size())) continue;
-      std::string l = gl[pl.gpu];
+      if (pl.gpu < 0 || pl.gpu >= static_cast<int>(pos.size()) || pos[pl.gpu] < 0) continue;
+      const int g = pos[pl.gpu];
+      std::string l = gl[g];
       l.append(",partition=\"").append(std::to_string(pl.partition < 0 ? 0 : pl.partition)).append("\",device_id=\"");
       append_label_value(&l, pl.device_id);
       l.append("\",resource=\"");
       append_label_value(&l, pl.resource);
       l.append("\"");
       line(&info, "amdgpu_partition_info", l, 1);
-      if (!ok[pl.gpu]) continue;
-      const GpuSample& s = samples[pl.gpu];
+      if (!ok[g]) continue;
+      const GpuSample& s = samples[g];
       const int p = pl.partition < 0 ? 0 : pl.partition;
       if (p < s.num_partitions && s.partition_gfx_busy_pct[p] >= 0)
         line(&busy, "amdgpu_partition_gfx_busy_percent", l, s.partition_gfx_busy_pct[p]);
@@ -351,9 +361,10 @@ std::shared_ptr<const std::string> Exporter::gpu_text() const {
 }
 
 GpuSample Exporter::last_sample(int gpu) const {
-  std::lock_guard<std::mutex> lk(mu_);
-  if (gpu < 0 || gpu >= static_cast<int>(last_.size())) return GpuSample{};
-  return last_[gpu];
+  std::lock_guard<std::mutex> lk(mu_);  // `gpu` is the backend (node) index
+  for (size_t g = 0; g < gpus_.size() && g < last_.size(); ++g)
+    if (gpus_[g].index == gpu) return last_[g];
+  return GpuSample{};
 }
 
 void Exporter::render_process(std::string* out) const {
