@@ -550,6 +550,12 @@ PYBIND11_MODULE(_native, m) {
     if (!hpack::huffman_decode(reinterpret_cast<const uint8_t*>(in.data()), in.size(), &out)) return py::none();
     return py::bytes(out);
   });
+  m.def("hpack_huffman_decode_bitwise", [](const py::bytes& b) -> py::object {
+    std::string in(b), out;
+    if (!hpack::huffman_decode_bitwise(reinterpret_cast<const uint8_t*>(in.data()), in.size(), &out))
+      return py::none();
+    return py::bytes(out);
+  });
   py::class_<hpack::Decoder>(m, "HpackDecoder")
       .def(py::init<size_t>(), py::arg("max_table_size") = 4096)
       .def("decode",
@@ -560,6 +566,18 @@ PYBIND11_MODULE(_native, m) {
              py::list l;
              for (auto& h : hs) l.append(py::make_tuple(h.name, h.value));
              return l;
+           })
+      .def("decode_visit",  // the server's non-allocating path; same result contract as decode
+           [](hpack::Decoder& d, const py::bytes& b) -> py::object {
+             std::string in(b);
+             std::vector<std::pair<std::string, std::string>> hs;
+             auto fn = [](void* ctx, std::string_view name, std::string_view value) {
+               static_cast<std::vector<std::pair<std::string, std::string>>*>(ctx)->emplace_back(name, value);
+             };
+             if (!d.decode(reinterpret_cast<const uint8_t*>(in.data()), in.size(), fn, &hs)) return py::none();
+             py::list out;
+             for (auto& h : hs) out.append(py::make_tuple(h.first, h.second));
+             return out;
            })
       .def_property_readonly("table_size", &hpack::Decoder::table_size)
       .def_property_readonly("table_entries", &hpack::Decoder::table_entries);

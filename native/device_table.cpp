@@ -209,52 +209,93 @@ std::string DeviceTable::options_bytes() const {
   return s;
 }
 
-std::string DeviceTable::encode_container_alloc(const std::vector<int>& idx) const {
-  std::string joined;
-  for (size_t k = 0; k < idx.size(); ++k) {
+namespace {
+
+size_t varint_len(uint64_t v) {
+  size_t n = 1;
+  while (v >= 0x80) {
+    v >>= 7;
+    ++n;
+  }
+  return n;
+}
+
+// map<string,string> entry (field `field`) written in place, no temporary message
+void put_map_entry(std::string* out, uint32_t field, std::string_view k, std::string_view v) {
+  const size_t inner = 1 + varint_len(k.size()) + k.size() + 1 + varint_len(v.size()) + v.size();
+  pb::put_tag(out, field, 2);
+  pb::put_varint(out, inner);
+  pb::put_bytes(out, 1, k);
+  pb::put_bytes(out, 2, v);
+}
+
+}  // namespace
+
+void DeviceTable::encode_container_alloc(const int* idx, size_t n, std::string* c) const {
+  thread_local std::string joined;
+  joined.clear();
+  for (size_t k = 0; k < n; ++k) {
     if (k) joined.push_back(',');
     joined.append(devs_[idx[k]].id);
   }
-  std::string c;
-  if (!cfg_.visible_env.empty()) pb::put_bytes(&c, 1, map_entry(cfg_.visible_env, joined));
-  c.append(env_extra_frag_);
-  c.append(kfd_frag_);
+  if (!cfg_.visible_env.empty()) put_map_entry(c, 1, cfg_.visible_env, joined);
+  c->append(env_extra_frag_);
+  c->append(kfd_frag_);
   // de-duplicate device nodes (replicas of one partition share its render node)
-  std::vector<int> seen_base;
-  for (int i : idx) {
+  for (size_t k = 0; k < n; ++k) {
+    const int i = idx[k];
     bool dup = false;
-    for (int j : seen_base)
-      if (spec_frag_[j] == spec_frag_[i]) {
-        dup = true;
-        break;
-      }
-    if (dup) continue;
-    seen_base.push_back(i);
-    c.append(spec_frag_[i]);
+    for (size_t j = 0; j < k && !dup; ++j) dup = spec_frag_[idx[j]] == spec_frag_[i];
+    if (!dup) c->append(spec_frag_[i]);
   }
   if (cfg_.cdi) {
-    for (int i : idx) {
-      std::string cdi;
-      pb::put_bytes(&cdi, 1, cfg_.cdi_prefix + alloc_devs_[i].base_id);
-      pb::put_bytes(&c, 5, cdi);
+    for (size_t k = 0; k < n; ++k) {
+      const std::string& base = alloc_devs_[idx[k]].base_id;
+      const size_t name_len = cfg_.cdi_prefix.size() + base.size();
+      pb::put_tag(c, 5, 2);  // CDIDevice{ name = 1 }
+      pb::put_varint(c, 1 + varint_len(name_len) + name_len);
+      pb::put_tag(c, 1, 2);
+      pb::put_varint(c, name_len);
+      c->append(cfg_.cdi_prefix).append(base);
     }
   }
-  return c;
 }
 
 bool DeviceTable::allocate(std::string_view req, std::string* out) const {
-  std::vector<std::vector<std::string_view>> reqs;
+  // Flat, reused decode state: one pass validates the whole request (a malformed
+  // message is reported as such before any lookup), with no per-call allocation.
+  thread_local std::vector<std::string_view> ids;
+  thread_local std::vector<size_t> ends;  // ids[ends[k-1], ends[k]) belong to container k
+  thread_local std::vector<int> idx;
+  thread_local std::string c;
+  ids.clear();
+  ends.clear();
   try {
-    reqs = pb::decode_allocate_request(req);
+    pb::Reader r(req);
+    uint32_t f, w;
+    while (r.next(&f, &w)) {
+      if (f == 1 && w == 2) {
+        pb::Reader cr(r.bytes());
+        uint32_t cf, cw;
+        while (cr.next(&cf, &cw)) {
+          if (cf == 1 && cw == 2) ids.push_back(cr.bytes());
+          else cr.skip(cw);
+        }
+        ends.push_back(ids.size());
+      } else {
+        r.skip(w);
+      }
+    }
   } catch (const pb::DecodeError& e) {
     *out = std::string("malformed AllocateRequest: ") + e.what();
     return false;
   }
-  std::string resp;
-  std::vector<int> idx;
-  for (const auto& ids : reqs) {
+  out->clear();
+  size_t begin = 0;
+  for (const size_t end : ends) {
     idx.clear();
-    for (const auto& id : ids) {
+    for (size_t k = begin; k < end; ++k) {
+      const std::string_view id = ids[k];
       const int i = index_of(id);
       if (i < 0) {
         *out = "invalid allocation request for '" + cfg_.resource_name + "': unknown device: " + std::string(id);
@@ -266,9 +307,11 @@ bool DeviceTable::allocate(std::string_view req, std::string* out) const {
       }
       idx.push_back(i);
     }
-    pb::put_bytes(&resp, 1, encode_container_alloc(idx));
+    begin = end;
+    c.clear();
+    encode_container_alloc(idx.data(), idx.size(), &c);
+    pb::put_bytes(out, 1, c);
   }
-  out->swap(resp);
   return true;
 }
 

@@ -116,7 +116,7 @@ class DeviceTable {
  private:
   void publish_law_locked();  // caller holds wmu_
   void notify_listeners();    // caller must NOT hold wmu_
-  std::string encode_container_alloc(const std::vector<int>& idx) const;
+  void encode_container_alloc(const int* idx, size_t n, std::string* out) const;  // appends
   bool is_healthy(int i) const { return health_[i].load(std::memory_order_acquire) != 0; }
 
   TableConfig cfg_;

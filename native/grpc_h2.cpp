@@ -127,7 +127,8 @@ Method method_of(std::string_view path) {
 }
 
 struct Stream {
-  std::string path;
+  int method = -1;          // Method, resolved from :path while decoding the header block
+  std::string path;         // kept only for an unknown method's error message
   std::string data;
   bool headers_done = false;
   int64_t send_window = 65535;
@@ -222,6 +223,23 @@ void flush_stream(Conn& c, uint32_t sid, Stream& s) {
 }
 
 void send_message(Conn& c, uint32_t sid, Stream& s, std::string_view payload, bool with_ok_trailers) {
+  const int64_t len = static_cast<int64_t>(payload.size()) + 5;
+  if (s.pend.empty() && len <= c.send_window && len <= s.send_window && len <= c.peer_max_frame) {
+    // common case (every unary response): one DATA frame straight into the output,
+    // trailers right behind it - no per-stream queue
+    frame(&c.out, static_cast<uint32_t>(len), kData, 0, sid);
+    grpc_prefix(&c.out, payload.size());
+    c.out.append(payload.data(), payload.size());
+    c.send_window -= len;
+    s.send_window -= len;
+    if (with_ok_trailers) {
+      const std::string& t = ok_trailers();
+      frame(&c.out, static_cast<uint32_t>(t.size()), kHeaders, kEndHeaders | kEndStream, sid);
+      c.out.append(t);
+      s.done = true;
+    }
+    return;
+  }
   grpc_prefix(&s.pend, payload.size());
   s.pend.append(payload.data(), payload.size());
   if (with_ok_trailers) {
@@ -373,6 +391,7 @@ void GrpcServer::run(Worker* w) {
     }
     return true;
   };
+  std::string scratch;
   auto push_law = [&](Conn* c) {
     const uint64_t v = table->version();
     std::string payload;
@@ -386,7 +405,7 @@ void GrpcServer::run(Worker* w) {
       table->observe(kRpcListAndWatch, (mono_ns() - t0) * 1e-9, false);
     }
   };
-  auto dispatch = [&](Conn& c, uint32_t sid, Stream& s) {
+  auto dispatch = [&](Conn& c, uint32_t sid, Stream& s, std::string_view body) {
     if (s.dispatched) {  // END_STREAM seen twice (trailers or DATA after the request)
       rst_stream(c, sid, kStreamClosed);
       s.done = true;
@@ -395,27 +414,28 @@ void GrpcServer::run(Worker* w) {
     s.dispatched = true;
     const int64_t t0 = mono_ns();
     requests_.fetch_add(1, std::memory_order_relaxed);
-    const Method m = method_of(s.path);
+    const Method m = static_cast<Method>(s.method);
     if (m == kMUnknown) {
       send_error(c, sid, s, 12, "unknown method " + s.path);  // UNIMPLEMENTED
       return;
     }
-    if (s.data.size() < 5) {
+    if (body.size() < 5) {
       send_error(c, sid, s, 13, "missing gRPC message");  // INTERNAL
       return;
     }
-    const uint8_t* d = reinterpret_cast<const uint8_t*>(s.data.data());
+    const uint8_t* d = reinterpret_cast<const uint8_t*>(body.data());
     if (d[0] != 0) {
       send_error(c, sid, s, 12, "compressed gRPC messages are not supported");
       return;
     }
     const uint32_t len = get_u32(d + 1);
-    if (len != s.data.size() - 5) {
+    if (len != body.size() - 5) {
       send_error(c, sid, s, 13, "unary request must carry exactly one message");
       return;
     }
-    const std::string_view msg(s.data.data() + 5, len);
-    std::string out;
+    const std::string_view msg(body.data() + 5, len);
+    std::string& out = scratch;  // per-worker response buffer, capacity reused
+    out.clear();
     bool ok = true;
     int rpc = kRpcAllocate;
     try {
@@ -459,9 +479,21 @@ void GrpcServer::run(Worker* w) {
     }
     table->observe(rpc, (mono_ns() - t0) * 1e-9, !ok);
   };
+  struct PathSink {
+    bool seen = false;
+    int method = kMUnknown;
+    std::string unknown;
+  };
+  auto on_header = [](void* ctx, std::string_view name, std::string_view value) {
+    if (name != ":path") return;
+    auto* ps = static_cast<PathSink*>(ctx);
+    ps->seen = true;
+    ps->method = method_of(value);
+    if (ps->method == kMUnknown) ps->unknown.assign(value.data(), value.size());
+  };
   auto on_headers_block = [&](Conn& c, uint32_t sid, uint8_t flags) -> bool {
-    std::vector<hpack::Header> hs;
-    if (!c.dec.decode(reinterpret_cast<const uint8_t*>(c.hblock.data()), c.hblock.size(), &hs)) {
+    PathSink ps;
+    if (!c.dec.decode(reinterpret_cast<const uint8_t*>(c.hblock.data()), c.hblock.size(), on_header, &ps)) {
       goaway(c, kCompressionError);
       return false;
     }
@@ -479,13 +511,13 @@ void GrpcServer::run(Worker* w) {
       }
       Stream s;
       s.send_window = c.peer_init_window;
-      for (auto& h : hs)
-        if (h.name == ":path") s.path = h.value;
+      s.method = ps.method;
+      s.path = std::move(ps.unknown);
       s.headers_done = true;
       it = c.streams.emplace(sid, std::move(s)).first;
     }
     if (flags & kEndStream) {
-      dispatch(c, sid, it->second);
+      dispatch(c, sid, it->second, it->second.data);
       drop_data(c, it->second);
     }
     return true;
@@ -649,6 +681,12 @@ void GrpcServer::run(Worker* w) {
           if (it != c.streams.end() && it->second.dispatched && !it->second.done) {
             rst_stream(c, sid, kStreamClosed);  // DATA after the request half-closed
             it->second.done = true;
+          } else if (it != c.streams.end() && !it->second.done && it->second.data.empty() &&
+                     (flags & kEndStream)) {
+            // the whole request in one DATA frame (every kubelet unary call): dispatch
+            // from the frame in place, no per-stream copy
+            dispatch(c, sid, it->second,
+                     std::string_view(reinterpret_cast<const char*>(p + off), len - off - pad));
           } else if (it != c.streams.end() && !it->second.done) {
             Stream& s = it->second;
             s.data.append(reinterpret_cast<const char*>(p + off), len - off - pad);
@@ -658,7 +696,7 @@ void GrpcServer::run(Worker* w) {
               send_error(c, sid, s, 8, "request exceeds the receive limit");  // RESOURCE_EXHAUSTED
               drop_data(c, s);
             } else if (flags & kEndStream) {
-              dispatch(c, sid, s);
+              dispatch(c, sid, s, s.data);
               drop_data(c, s);
             } else if (s.recv_unacked > kLocalWindow / 2) {
               window_update(&c.out, sid, static_cast<uint32_t>(s.recv_unacked));
@@ -916,11 +954,16 @@ bool H2Client::handle_control(uint8_t type, uint8_t flags, uint32_t sid, const s
 void H2Client::send_request(uint32_t sid, std::string_view path, std::string_view req) {
   cur_sid_ = sid;
   stream_window_ = stream_window_init_;
-  std::string o;
-  const std::string h = request_headers(path);
-  frame(&o, static_cast<uint32_t>(h.size()), kHeaders, kEndHeaders, sid);
-  o.append(h);
-  std::string body;
+  std::string& o = out_buf_;  // capacity reused across calls
+  o.clear();
+  if (path != hpath_) {  // a client calls one or two methods: keep the encoded block
+    hpath_.assign(path.data(), path.size());
+    hblock_ = request_headers(path);
+  }
+  frame(&o, static_cast<uint32_t>(hblock_.size()), kHeaders, kEndHeaders, sid);
+  o.append(hblock_);
+  std::string& body = body_buf_;
+  body.clear();
   grpc_prefix(&body, req.size());
   body.append(req.data(), req.size());
   size_t off = 0;
@@ -952,11 +995,12 @@ int H2Client::unary(std::string_view path, std::string_view req, std::string* re
   const uint32_t sid = next_sid_;
   next_sid_ += 2;
   send_request(sid, path, req);
-  std::string data;
+  std::string& data = data_buf_;
+  data.clear();
   int status = -1;
   uint8_t type, flags;
   uint32_t fsid;
-  std::string payload;
+  std::string& payload = frame_buf_;
   for (;;) {
     if (!read_frame(&type, &flags, &fsid, &payload)) throw std::runtime_error("H2Client: connection closed");
     if (handle_control(type, flags, fsid, payload)) continue;
@@ -964,13 +1008,25 @@ int H2Client::unary(std::string_view path, std::string_view req, std::string* re
       data.append(payload);
       conn_consumed_ += static_cast<int64_t>(payload.size());
     } else if (fsid == sid && type == kHeaders) {
-      std::vector<hpack::Header> hs;
-      if (!dec_.decode(reinterpret_cast<const uint8_t*>(payload.data()), payload.size(), &hs))
+      struct Sink {
+        int* status;
+        std::string* message;
+      } sink{&status, message};
+      auto fn = [](void* ctx, std::string_view name, std::string_view value) {
+        auto* k = static_cast<Sink*>(ctx);
+        if (name == "grpc-status") {
+          int v = 0;
+          for (char ch : value) {
+            if (ch < '0' || ch > '9') break;
+            v = v * 10 + (ch - '0');
+          }
+          *k->status = v;
+        } else if (name == "grpc-message" && k->message) {
+          k->message->assign(value.data(), value.size());
+        }
+      };
+      if (!dec_.decode(reinterpret_cast<const uint8_t*>(payload.data()), payload.size(), fn, &sink))
         throw std::runtime_error("H2Client: bad HPACK from server");
-      for (auto& x : hs) {
-        if (x.name == "grpc-status") status = std::atoi(x.value.c_str());
-        else if (x.name == "grpc-message" && message) *message = x.value;
-      }
     } else if (fsid == sid && type == kRstStream) {
       throw std::runtime_error("H2Client: stream reset");
     }

@@ -103,6 +103,8 @@ class H2Client {
   std::string watch_buf_;
   int64_t watch_consumed_ = 0;
   int timeout_ms_;
+  std::string hpath_, hblock_;  // last request path and its encoded header block
+  std::string out_buf_, body_buf_, data_buf_, frame_buf_;  // per-call scratch, capacity reused
 };
 
 // n sequential unary calls on one connection; per-call latency in seconds.

@@ -70,7 +70,7 @@ const Canon& canon() {
 
 }  // namespace
 
-bool huffman_decode(const uint8_t* p, size_t n, std::string* out) {
+bool huffman_decode_bitwise(const uint8_t* p, size_t n, std::string* out) {
   const Canon& c = canon();
   uint32_t code = 0;
   uint32_t len = 0;
@@ -91,6 +91,84 @@ bool huffman_decode(const uint8_t* p, size_t n, std::string* out) {
   // padding: < 8 bits, all ones (the most significant bits of EOS)
   if (len >= 8) return false;
   return code == ((1u << len) - 1u);
+}
+
+namespace {
+
+// Primary lookup on the next kPeek bits: every code of length <= kPeek (all of
+// printable ASCII except a few symbols) resolves in one step; longer codes fall back
+// to the canonical first/count search from length kPeek+1.
+constexpr int kPeek = 10;
+
+struct FastTable {
+  uint16_t sym[1 << kPeek];
+  uint8_t len[1 << kPeek];  // 0 = no code of length <= kPeek has this prefix
+  FastTable() {
+    for (int i = 0; i < (1 << kPeek); ++i) len[i] = 0;
+    for (int s = 0; s < 257; ++s) {
+      const int L = static_cast<int>(kHuff[s].len);
+      if (L > kPeek) continue;
+      const uint32_t base = kHuff[s].code << (kPeek - L);
+      for (uint32_t k = 0; k < (1u << (kPeek - L)); ++k) {
+        sym[base + k] = static_cast<uint16_t>(s);
+        len[base + k] = static_cast<uint8_t>(L);
+      }
+    }
+  }
+};
+
+const FastTable& fast_table() {
+  static const FastTable t;
+  return t;
+}
+
+}  // namespace
+
+bool huffman_decode(const uint8_t* p, size_t n, std::string* out) {
+  const FastTable& ft = fast_table();
+  const Canon& c = canon();
+  uint64_t acc = 0;  // bit buffer, the next `bits` bits right-aligned
+  int bits = 0;
+  size_t i = 0;
+  out->reserve(out->size() + n * 8 / 5 + 1);
+  for (;;) {
+    while (bits <= 56 && i < n) {
+      acc = (acc << 8) | p[i++];
+      bits += 8;
+    }
+    if (bits == 0) return true;
+    // peek kPeek bits; past the end pad with ones (EOS prefix), as a valid string's padding is
+    const uint32_t peek = bits >= kPeek
+                              ? static_cast<uint32_t>(acc >> (bits - kPeek)) & ((1u << kPeek) - 1)
+                              : static_cast<uint32_t>(((acc << (kPeek - bits)) | ((1u << (kPeek - bits)) - 1)) &
+                                                      ((1u << kPeek) - 1));
+    int L = ft.len[peek];
+    uint16_t sym = ft.sym[peek];
+    if (L == 0) {  // code longer than kPeek bits
+      L = -1;
+      for (int len = kPeek + 1; len <= 30 && len <= bits; ++len) {
+        const uint32_t code = static_cast<uint32_t>(acc >> (bits - len)) & ((1u << len) - 1);
+        if (c.count[len] && code >= c.first[len] && code - c.first[len] < c.count[len]) {
+          sym = c.syms[c.offset[len] + (code - c.first[len])];
+          L = len;
+          break;
+        }
+      }
+      if (L < 0) {  // not enough bits left for any code: must be padding
+        if (i < n) return false;  // (cannot happen with 56+ bits buffered)
+        if (bits >= 8) return false;
+        return (acc & ((1u << bits) - 1)) == ((1u << bits) - 1);
+      }
+    }
+    if (L > bits) {  // the match used padding ones: the rest is padding
+      if (bits >= 8) return false;
+      return (acc & ((1u << bits) - 1)) == ((1u << bits) - 1);
+    }
+    if (sym == 256) return false;  // EOS inside a string is an error
+    out->push_back(static_cast<char>(sym));
+    bits -= L;
+    acc &= bits ? ((uint64_t{1} << bits) - 1) : 0;
+  }
 }
 
 size_t huffman_encoded_len(std::string_view s) {
@@ -232,6 +310,102 @@ void Decoder::insert(Header h) {
   size_ += sz;
   dyn_.push_front(std::move(h));
   evict();
+}
+
+bool Decoder::name_of(uint64_t index, std::string_view* name) const {
+  if (index == 0) return false;
+  if (index <= 61) {
+    *name = kStatic[index - 1][0];
+    return true;
+  }
+  const uint64_t d = index - 62;
+  if (d >= dyn_.size()) return false;
+  *name = dyn_[static_cast<size_t>(d)].name;
+  return true;
+}
+
+bool Decoder::entry(uint64_t index, std::string_view* name, std::string_view* value) const {
+  if (index == 0) return false;
+  if (index <= 61) {
+    *name = kStatic[index - 1][0];
+    *value = kStatic[index - 1][1];
+    return true;
+  }
+  const uint64_t d = index - 62;
+  if (d >= dyn_.size()) return false;
+  const Header& h = dyn_[static_cast<size_t>(d)];
+  *name = h.name;
+  *value = h.value;
+  return true;
+}
+
+namespace {
+
+// A string literal as a view: raw bytes in place, Huffman decoded into `scratch`.
+bool string_view_of(const uint8_t*& p, const uint8_t* end, std::string* scratch, std::string_view* out) {
+  if (p >= end) return false;
+  const bool huff = (*p & 0x80) != 0;
+  uint64_t len;
+  if (!decode_int(p, end, 7, &len)) return false;
+  if (len > static_cast<uint64_t>(end - p)) return false;
+  if (huff) {
+    scratch->clear();
+    if (!huffman_decode(p, static_cast<size_t>(len), scratch)) return false;
+    *out = *scratch;
+  } else {
+    *out = std::string_view(reinterpret_cast<const char*>(p), static_cast<size_t>(len));
+  }
+  p += len;
+  return true;
+}
+
+}  // namespace
+
+bool Decoder::decode(const uint8_t* p, size_t n, HeaderFn fn, void* ctx) {
+  const uint8_t* end = p + n;
+  bool header_seen = false;
+  while (p < end) {
+    const uint8_t b = *p;
+    std::string_view name, value;
+    if (b & 0x80) {  // indexed
+      uint64_t idx;
+      if (!decode_int(p, end, 7, &idx) || !entry(idx, &name, &value)) return false;
+      fn(ctx, name, value);
+      header_seen = true;
+    } else if ((b & 0xE0) == 0x20) {  // dynamic table size update
+      if (header_seen) return false;
+      uint64_t sz;
+      if (!decode_int(p, end, 5, &sz) || sz > limit_) return false;
+      max_ = static_cast<size_t>(sz);
+      evict();
+    } else {
+      const bool indexing = (b & 0xC0) == 0x40;  // else without indexing / never indexed
+      uint64_t idx;
+      if (!decode_int(p, end, indexing ? 6 : 4, &idx)) return false;
+      if (idx) {
+        if (!name_of(idx, &name)) return false;
+      } else if (!string_view_of(p, end, &name_buf_, &name)) {
+        return false;
+      }
+      if (!string_view_of(p, end, &value_buf_, &value)) return false;
+      if (indexing) {  // table state must follow the encoder: copy first (views may
+                       // point into entries the insertion evicts), insert, view the entry
+        Header h{std::string(name), std::string(value)};
+        if (h.name.size() + h.value.size() + 32 <= max_) {
+          insert(std::move(h));
+          fn(ctx, dyn_.front().name, dyn_.front().value);
+        } else {  // larger than the table: delivered, and the table is emptied (§4.4)
+          fn(ctx, h.name, h.value);
+          dyn_.clear();
+          size_ = 0;
+        }
+      } else {
+        fn(ctx, name, value);
+      }
+      header_seen = true;
+    }
+  }
+  return true;
 }
 
 bool Decoder::decode(const uint8_t* p, size_t n, std::vector<Header>* out) {

@@ -35,11 +35,23 @@ void encode_literal(std::string* out, std::string_view name, std::string_view va
 void encode_literal_name_index(std::string* out, int static_name_index, std::string_view value, bool huffman = false);
 int static_index(std::string_view name, std::string_view value, bool* value_match);
 
+// Bit-by-bit canonical decoder: the reference the table-driven huffman_decode is
+// tested against.
+bool huffman_decode_bitwise(const uint8_t* p, size_t n, std::string* out);
+
+// Visitor for Decoder::decode: name/value views are valid only during the call (they
+// point into the static table, the dynamic table, the input block or scratch space).
+using HeaderFn = void (*)(void* ctx, std::string_view name, std::string_view value);
+
 class Decoder {
  public:
   explicit Decoder(size_t max_table_size = 4096) : limit_(max_table_size), max_(max_table_size) {}
   // Decodes one complete header block.  false = COMPRESSION_ERROR (connection fatal).
   bool decode(const uint8_t* p, size_t n, std::vector<Header>* out);
+  // Same, without materialising headers: static-table and dynamic-table entries and
+  // raw literals are passed as views (no allocation); Huffman literals decode into
+  // reused scratch buffers.  The request hot path of the gRPC server.
+  bool decode(const uint8_t* p, size_t n, HeaderFn fn, void* ctx);
   size_t table_size() const { return size_; }
   size_t table_entries() const { return dyn_.size(); }
 
@@ -47,7 +59,10 @@ class Decoder {
   bool get(uint64_t index, Header* h) const;
   void insert(Header h);
   void evict();
+  bool name_of(uint64_t index, std::string_view* name) const;
+  bool entry(uint64_t index, std::string_view* name, std::string_view* value) const;
   std::deque<Header> dyn_;  // front = most recent (index 62)
+  std::string name_buf_, value_buf_;  // Huffman scratch for the visitor decode
   size_t size_ = 0;
   size_t limit_;  // SETTINGS_HEADER_TABLE_SIZE we advertised
   size_t max_;    // current max set by the encoder's size updates

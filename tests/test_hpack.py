@@ -77,3 +77,39 @@ def test_integer_prefix_examples(n):
     name = "a" * 1337
     block = b"\x00" + bytes([0x7F, 0xBA, 0x09]) + name.encode() + b"\x01x"  # 127 + 1210 = 1337 (7-bit prefix)
     assert d.decode(block) == [(name, "x")]
+
+
+@settings(max_examples=500, deadline=None)
+@given(st.binary(max_size=64))
+def test_table_huffman_decoder_matches_bitwise_reference(n, blob):
+    """Arbitrary bytes (mostly invalid codes/padding): the table-driven decoder used on
+    the request path accepts and rejects exactly what the bit-by-bit decoder does."""
+    assert n.hpack_huffman_decode(blob) == n.hpack_huffman_decode_bitwise(blob)
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.binary(max_size=300))
+def test_table_huffman_decoder_roundtrip_long_codes(n, data):
+    enc = n.hpack_huffman_encode(data)  # bytes >= 0x80 use the long (> 10 bit) codes
+    assert n.hpack_huffman_decode(enc) == data == n.hpack_huffman_decode_bitwise(enc)
+
+
+def test_visitor_decode_matches_vector_decode(n):
+    """The server's non-allocating decode keeps the same dynamic-table state and yields
+    the same headers as the vector decode, across RFC C.3-C.5 sequences (incl. eviction)."""
+    seqs = [(4096, ["828684410f7777772e6578616d706c652e636f6d", "828684be58086e6f2d6361636865",
+                    "828785bf400a637573746f6d2d6b65790c637573746f6d2d76616c7565"]),
+            (4096, ["828684418cf1e3c2e5f23a6ba0ab90f4ff", "828684be5886a8eb10649cbf",
+                    "828785bf408825a849e95ba97d7f8925a849e95bb8e8b4bf"]),
+            (256, ["4803333032580770726976617465611d4d6f6e2c203231204f637420323031332032303a31333a323120474d"
+                   "546e1768747470733a2f2f7777772e6578616d706c652e636f6d", "4803333037c1c0bf"])]
+    for size, blocks in seqs:
+        a, b = n.HpackDecoder(size), n.HpackDecoder(size)
+        for hx in blocks:
+            assert a.decode(bytes.fromhex(hx)) == b.decode_visit(bytes.fromhex(hx))
+            assert (a.table_size, a.table_entries) == (b.table_size, b.table_entries)
+    d = n.HpackDecoder(64)  # an entry larger than the table is delivered and empties it
+    big = b"\x40\x01a" + bytes([60]) + b"v" * 60
+    assert d.decode_visit(big) == [("a", "v" * 60)] and d.table_entries == 0
+    for bad in (b"\x80", b"\xbf", b"\x82\x20"):
+        assert n.HpackDecoder(4096).decode_visit(bad) is None
