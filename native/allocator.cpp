@@ -38,8 +38,12 @@ struct Ctx {
   std::vector<int> gpu_numa;
   std::vector<uint64_t> adj;       // healthy direct-link adjacency bitmask per GPU
   std::vector<int> numa_ids;       // distinct NUMA nodes
+  std::vector<int> gpu_numa_slot;  // gpu -> index into numa_ids
   int ngpu = 0;
   int parts_per_gpu = 1;
+  // score() scratch, reused across the (up to thousands of) candidate evaluations
+  mutable std::vector<int> taken;
+  mutable std::vector<uint64_t> whole_free;
 
   Ctx(const Topology& t, const std::vector<AllocDevice>& d, const std::vector<int>& avail) : topo(t), devs(d) {
     is_avail.assign(d.size(), 0);
@@ -61,8 +65,14 @@ struct Ctx {
         if (a != b && a < t.n && b < t.n && t.at(a, b).up &&
             (t.at(a, b).type == kLinkXgmi || t.at(a, b).type == kLinkPcie))
           adj[a] |= 1ull << b;
-    for (int g = 0; g < ngpu; ++g)
-      if (std::find(numa_ids.begin(), numa_ids.end(), gpu_numa[g]) == numa_ids.end()) numa_ids.push_back(gpu_numa[g]);
+    gpu_numa_slot.assign(ngpu, 0);
+    for (int g = 0; g < ngpu; ++g) {
+      auto it = std::find(numa_ids.begin(), numa_ids.end(), gpu_numa[g]);
+      if (it == numa_ids.end()) it = numa_ids.insert(numa_ids.end(), gpu_numa[g]);
+      gpu_numa_slot[g] = static_cast<int>(it - numa_ids.begin());
+    }
+    taken.assign(ngpu, 0);
+    whole_free.assign(numa_ids.size(), 0);
   }
 
   // Largest set of GPUs in `mask` that are pairwise connected by healthy links.
@@ -88,7 +98,7 @@ struct Ctx {
     for (size_t i = 0; i < S.size(); ++i)
       for (size_t j = i + 1; j < S.size(); ++j) s += pair_score(topo, devs[S[i]], devs[S[j]]);
     // per-gpu usage after taking S
-    std::vector<int> taken(ngpu, 0);
+    std::fill(taken.begin(), taken.end(), 0);
     for (int i : S)
       if (devs[i].gpu >= 0) taken[devs[i].gpu]++;
     bool multi_gpu = false;
@@ -107,14 +117,11 @@ struct Ctx {
     // healthy-link clique of whole free GPUs per NUMA node (what a future multi-GPU
     // RCCL job needs) - on a healthy mesh this is just the whole-free count.
     double frag = 0;
-    std::vector<uint64_t> whole_free(numa_ids.size(), 0);
+    std::fill(whole_free.begin(), whole_free.end(), 0);
     for (int g = 0; g < ngpu; ++g) {
       const int f = gpu_avail[g] - taken[g];
       frag += static_cast<double>(f) * f / parts_per_gpu;
-      if (gpu_total[g] > 0 && f == gpu_total[g] && g < 64) {
-        const size_t ni = std::find(numa_ids.begin(), numa_ids.end(), gpu_numa[g]) - numa_ids.begin();
-        whole_free[ni] |= 1ull << g;
-      }
+      if (gpu_total[g] > 0 && f == gpu_total[g] && g < 64) whole_free[gpu_numa_slot[g]] |= 1ull << g;
     }
     for (uint64_t m : whole_free) {
       const int c = __builtin_popcountll(m) <= 16 ? max_clique(m) : __builtin_popcountll(m);
@@ -185,18 +192,26 @@ AllocResult aligned_alloc(const Topology& topo, const std::vector<AllocDevice>& 
     // Partition packing shortcut: if one GPU can hold the whole request (together with
     // every required device), a single-GPU set dominates - each split pair loses >= 40
     // pair-score points while the fragmentation/packing terms move by < 40 in total.
-    std::map<int, std::vector<int>> by_gpu;
-    for (int c : cand) by_gpu[devs[c].gpu].push_back(c);
+    // candidates grouped by GPU (ascending GPU, then device index): runs in `grouped`
+    thread_local std::vector<int> grouped;
+    grouped.assign(cand.begin(), cand.end());
+    std::stable_sort(grouped.begin(), grouped.end(), [&](int x, int y) { return devs[x].gpu < devs[y].gpu; });
     int req_gpu = -2;
     for (int i : required) req_gpu = (req_gpu == -2 || req_gpu == devs[i].gpu) ? devs[i].gpu : -3;
     bool single_gpu_done = false;
     if (need >= 1 && req_gpu != -3) {
-      for (auto& kv : by_gpu) {
-        if (static_cast<int>(kv.second.size()) < need || (req_gpu >= 0 && kv.first != req_gpu)) continue;
-        std::vector<int> S(required);
-        S.insert(S.end(), kv.second.begin(), kv.second.begin() + need);
-        consider(S);
-        single_gpu_done = true;
+      std::vector<int> S;
+      for (size_t b = 0; b < grouped.size();) {
+        size_t e = b;
+        while (e < grouped.size() && devs[grouped[e]].gpu == devs[grouped[b]].gpu) ++e;
+        const int gpu = devs[grouped[b]].gpu;
+        if (static_cast<int>(e - b) >= need && !(req_gpu >= 0 && gpu != req_gpu)) {
+          S.assign(required.begin(), required.end());
+          S.insert(S.end(), grouped.begin() + b, grouped.begin() + b + need);
+          consider(S);
+          single_gpu_done = true;
+        }
+        b = e;
       }
     }
     if (single_gpu_done && ctx.parts_per_gpu > 1) {

@@ -315,33 +315,33 @@ bool DeviceTable::allocate(std::string_view req, std::string* out) const {
   return true;
 }
 
-AllocResult DeviceTable::preferred_ids(const std::vector<std::string>& avail, const std::vector<std::string>& must,
-                                       int size, std::vector<std::string>* out_ids) const {
-  std::vector<int> a, m;
+AllocResult DeviceTable::preferred_core(const std::string_view* avail, size_t n_avail, const std::string_view* must,
+                                        size_t n_must, int size) const {
+  thread_local std::vector<int> a, m;
+  a.clear();
+  m.clear();
   bool any_annotated = false;
-  for (const auto& id : avail) {
-    if (id.find("::") != std::string::npos) any_annotated = true;
-    const int i = index_of(id);
-    if (i >= 0) a.push_back(i);
+  for (size_t k = 0; k < n_avail; ++k) {
+    const int i = index_of(avail[k]);
+    if (i < 0) continue;
+    a.push_back(i);
+    any_annotated |= alloc_devs_[i].annotated;
   }
-  for (const auto& id : must) {
-    const int i = index_of(id);
+  for (size_t k = 0; k < n_must; ++k) {
+    const int i = index_of(must[k]);
     if (i < 0) {
       AllocResult r;
       r.ok = false;
-      r.error = "unknown device in must_include_deviceIDs: " + id;
+      r.error = "unknown device in must_include_deviceIDs: " + std::string(must[k]);
       return r;
     }
     if (std::find(m.begin(), m.end(), i) == m.end()) m.push_back(i);
   }
-  AllocResult r;
   // Contract (go-gpuallocator BestEffort): a non-positive size yields no devices; a size
   // below |must_include| cannot be honoured and is an error rather than a larger set.
-  if (size <= 0) {
-    if (out_ids) out_ids->clear();
-    return r;
-  }
+  if (size <= 0) return AllocResult{};
   if (static_cast<size_t>(size) < m.size()) {
+    AllocResult r;
     r.ok = false;
     r.error = "allocation_size " + std::to_string(size) + " is smaller than must_include_deviceIDs (" +
               std::to_string(m.size()) + ")";
@@ -349,10 +349,15 @@ AllocResult DeviceTable::preferred_ids(const std::vector<std::string>& avail, co
   }
   if (aligned_ok_ && !any_annotated) {
     const auto topo = std::atomic_load_explicit(&topo_, std::memory_order_acquire);  // snapshot
-    r = aligned_alloc(*topo, alloc_devs_, a, m, size);
-  } else {
-    r = distributed_alloc(alloc_devs_, a, m, size);
+    return aligned_alloc(*topo, alloc_devs_, a, m, size);
   }
+  return distributed_alloc(alloc_devs_, a, m, size);
+}
+
+AllocResult DeviceTable::preferred_ids(const std::vector<std::string>& avail, const std::vector<std::string>& must,
+                                       int size, std::vector<std::string>* out_ids) const {
+  std::vector<std::string_view> av(avail.begin(), avail.end()), mu(must.begin(), must.end());
+  AllocResult r = preferred_core(av.data(), av.size(), mu.data(), mu.size(), size);
   if (r.ok && out_ids) {
     out_ids->clear();
     for (int i : r.chosen) out_ids->push_back(devs_[i].id);
@@ -361,28 +366,54 @@ AllocResult DeviceTable::preferred_ids(const std::vector<std::string>& avail, co
 }
 
 bool DeviceTable::preferred(std::string_view req, std::string* out) const {
-  std::vector<pb::PreferredRequest> reqs;
+  // One validating pass into flat reused vectors (malformed => error before any work).
+  struct Span {
+    size_t av_end, mu_end;
+    int32_t size;
+  };
+  thread_local std::vector<std::string_view> av, mu;
+  thread_local std::vector<Span> spans;
+  thread_local std::string c;
+  av.clear();
+  mu.clear();
+  spans.clear();
   try {
-    reqs = pb::decode_preferred_request(req);
+    pb::Reader r(req);
+    uint32_t f, w;
+    while (r.next(&f, &w)) {
+      if (f == 1 && w == 2) {
+        pb::Reader cr(r.bytes());
+        int32_t size = 0;
+        uint32_t cf, cw;
+        while (cr.next(&cf, &cw)) {
+          if (cf == 1 && cw == 2) av.push_back(cr.bytes());
+          else if (cf == 2 && cw == 2) mu.push_back(cr.bytes());
+          else if (cf == 3 && cw == 0) size = static_cast<int32_t>(cr.varint());
+          else cr.skip(cw);
+        }
+        spans.push_back({av.size(), mu.size(), size});
+      } else {
+        r.skip(w);
+      }
+    }
   } catch (const pb::DecodeError& e) {
     *out = std::string("malformed PreferredAllocationRequest: ") + e.what();
     return false;
   }
-  std::string resp;
-  std::vector<std::string> avail, must, ids;
-  for (const auto& r : reqs) {
-    avail.assign(r.available.begin(), r.available.end());
-    must.assign(r.must_include.begin(), r.must_include.end());
-    AllocResult ar = preferred_ids(avail, must, r.size, &ids);
+  out->clear();
+  size_t av0 = 0, mu0 = 0;
+  for (const Span& sp : spans) {
+    AllocResult ar = preferred_core(av.data() + av0, sp.av_end - av0, mu.data() + mu0, sp.mu_end - mu0, sp.size);
+    av0 = sp.av_end;
+    mu0 = sp.mu_end;
     if (!ar.ok) {
       *out = "error getting list of preferred allocation devices: " + ar.error;
       return false;
     }
-    std::string c;
-    for (const auto& id : ids) pb::put_bytes(&c, 1, id);
-    pb::put_bytes(&resp, 1, c);
+    c.clear();
+    for (int i : ar.chosen) pb::put_bytes(&c, 1, devs_[i].id);
+    pb::put_bytes(out, 1, c);
   }
-  out->swap(resp);
   return true;
 }
 

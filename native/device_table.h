@@ -16,6 +16,7 @@
 
 #include <atomic>
 #include <condition_variable>
+#include <cstring>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -108,6 +109,9 @@ class DeviceTable {
   // Convenience for Python callers / tests
   AllocResult preferred_ids(const std::vector<std::string>& avail, const std::vector<std::string>& must, int size,
                             std::vector<std::string>* out_ids) const;
+  // Core of both: ids as views, result as device indices in r->chosen.
+  AllocResult preferred_core(const std::string_view* avail, size_t n_avail, const std::string_view* must,
+                             size_t n_must, int size) const;
 
   void observe(int rpc, double seconds, bool error) const;
   void render_metrics(std::string* out, bool with_headers) const;
@@ -122,7 +126,30 @@ class DeviceTable {
   TableConfig cfg_;
   std::vector<TableDevice> devs_;
   std::vector<AllocDevice> alloc_devs_;
-  std::unordered_map<std::string_view, int> index_;
+  // Device ids are long (UUID + "-xcpN"); hashing three 8-byte words and the length
+  // is enough to spread them and several times cheaper than hashing every byte.
+  struct IdHash {
+    size_t operator()(std::string_view s) const noexcept {
+      uint64_t h = 0x9E3779B97F4A7C15ull ^ s.size();
+      auto word = [&](size_t off) {
+        uint64_t w = 0;
+        std::memcpy(&w, s.data() + off, 8);
+        return w;
+      };
+      if (s.size() >= 8) {
+        const uint64_t ws[3] = {word(0), word((s.size() - 8) / 2), word(s.size() - 8)};
+        for (uint64_t w : ws) {
+          h ^= w;
+          h *= 0xBF58476D1CE4E5B9ull;
+          h ^= h >> 31;
+        }
+      } else {
+        for (unsigned char ch : s) h = (h ^ ch) * 0x100000001B3ull;
+      }
+      return static_cast<size_t>(h ^ (h >> 29));
+    }
+  };
+  std::unordered_map<std::string_view, int, IdHash> index_;
   std::vector<std::string> spec_frag_;  // per device: encoded DeviceSpec fields (tag 3)
   std::string kfd_frag_;
   std::string env_extra_frag_;
