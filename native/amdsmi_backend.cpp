@@ -304,6 +304,14 @@ class AmdSmiBackend : public Backend {
   }
 
  public:
+  std::vector<CallCost> sample_costs() const override {
+    std::lock_guard<std::mutex> lk(mu_);
+    std::vector<CallCost> out;
+    for (int c = 0; c < kCallCount; ++c)
+      out.push_back({kCallNames[c], cost_ns_[c] * 1e-9, cost_n_[c]});
+    return out;
+  }
+
   bool sample(int gpu, GpuSample* s) override {
     std::lock_guard<std::mutex> lk(mu_);
     if (closed_ || gpu < 0 || gpu >= static_cast<int>(procs_.size())) return false;
@@ -311,7 +319,10 @@ class AmdSmiBackend : public Backend {
     s->ts_ns = now_ns();
     amdsmi_gpu_metrics_t m;
     std::memset(&m, 0, sizeof(m));
-    if (amdsmi_get_gpu_metrics_info(h0, &m) == AMDSMI_STATUS_SUCCESS) {
+    int64_t t = mono_ns();
+    const amdsmi_status_t mst = amdsmi_get_gpu_metrics_info(h0, &m);
+    t = charge(kCallGpuMetrics, t);
+    if (mst == AMDSMI_STATUS_SUCCESS) {
       s->ok = true;
       if (valid16(m.current_socket_power) && m.current_socket_power != 0) s->power_w = m.current_socket_power;
       else if (valid16(m.average_socket_power)) s->power_w = m.average_socket_power;
@@ -343,6 +354,7 @@ class AmdSmiBackend : public Backend {
         s->partition_gfx_busy_pct[p] = cnt ? sum / cnt : (nparts == 1 ? s->gfx_activity_pct : -1);
       }
     }
+    t = mono_ns();
     double used = 0, total = 0;
     bool have_vram = false;
     for (size_t p = 0; p < procs_[gpu].size(); ++p) {
@@ -361,12 +373,15 @@ class AmdSmiBackend : public Backend {
       s->vram_total_bytes = total;
       s->ok = true;
     }
+    t = charge(kCallVram, t);
     amdsmi_error_count_t ec{};
     if (amdsmi_get_gpu_total_ecc_count(h0, &ec) == AMDSMI_STATUS_SUCCESS) {
       s->ecc_correctable = static_cast<int64_t>(ec.correctable_count);
       s->ecc_uncorrectable = static_cast<int64_t>(ec.uncorrectable_count);
     }
+    t = charge(kCallEcc, t);
     link_state_locked(gpu, s);
+    charge(kCallLinks, t);
     return s->ok;
   }
 
@@ -503,6 +518,18 @@ class AmdSmiBackend : public Backend {
     armed_handles_.clear();
     armed_ = false;
   }
+
+  // per-call cost accounting for sample() (guarded by mu_)
+  enum SampleCall { kCallGpuMetrics, kCallVram, kCallEcc, kCallLinks, kCallCount };
+  static constexpr const char* kCallNames[kCallCount] = {"gpu_metrics", "vram_usage", "ecc_count", "xgmi_links"};
+  int64_t charge(int call, int64_t since) {
+    const int64_t now = mono_ns();
+    cost_ns_[call] += now - since;
+    ++cost_n_[call];
+    return now;
+  }
+  int64_t cost_ns_[kCallCount] = {};
+  uint64_t cost_n_[kCallCount] = {};
 
   mutable std::mutex mu_;
   std::mutex evt_mu_;                   // held across the blocking event wait

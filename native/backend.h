@@ -163,6 +163,13 @@ class Backend {
   virtual bool reinit() { return true; }
   // Times the backend re-initialised its hardware library (stale-handle recovery).
   virtual int reinit_count() const { return 0; }
+  // Cumulative cost of the hardware calls inside sample(): (call, seconds, calls).
+  struct CallCost {
+    std::string call;
+    double seconds = 0;
+    uint64_t calls = 0;
+  };
+  virtual std::vector<CallCost> sample_costs() const { return {}; }
   virtual void shutdown() {}
 };
 

@@ -167,6 +167,12 @@ PYBIND11_MODULE(_native, m) {
 
   py::class_<Backend, std::shared_ptr<Backend>>(m, "Backend")
       .def_property_readonly("name", &Backend::name)
+      .def("sample_costs",
+           [](const Backend& b) {
+             py::dict d;
+             for (const auto& c : b.sample_costs()) d[py::str(c.call)] = py::make_tuple(c.seconds, c.calls);
+             return d;
+           })
       .def("discover",
            [](Backend& b) {
              std::vector<GpuInfo> g;
