@@ -46,6 +46,21 @@ def test_amdsmi_telemetry(amdsmi_backend):
     print("sample", s.power_w, s.temp_hotspot_c, s.temp_hbm_c, s.gfx_activity_pct, s.vram_used_bytes, s.links)
 
 
+def test_amdsmi_sample_cost_breakdown(amdsmi_backend):
+    """Where one telemetry pass spends its time (it runs once per GPU per tick, off the
+    request path, but 8 GPUs x 8 partitions must fit a 1 s tick with room to spare)."""
+    amdsmi_backend.discover()
+    before = amdsmi_backend.sample_costs()
+    for _ in range(20):
+        assert amdsmi_backend.sample(0).ok
+    after = amdsmi_backend.sample_costs()
+    per = {k: (after[k][0] - before[k][0]) / 20 * 1e6 for k in after}
+    print("amdsmi sample cost per GPU (us):", {k: round(v, 1) for k, v in per.items()},
+          "total %.1f us" % sum(per.values()))
+    assert set(per) == {"gpu_metrics", "vram_usage", "ecc_count", "xgmi_links"}
+    assert sum(per.values()) < 50e3
+
+
 def test_exporter_renders_real_metrics(n, amdsmi_backend):
     gpus, _ = amdsmi_backend.discover()
     ex = n.Exporter()
