@@ -14,6 +14,7 @@ to register with.  Every rank then acts as one kubelet-side client for "its" GPU
          connections from the compiled load generator (native/loadgen.cpp)
 
 W warm-up steps, then K timed steps bracketed by barrier + torch.cuda.synchronize().
+With N > 1 the ranks also barrier between a step's RPC phase and its scrape phase.
 Work per rank is fixed as N grows (weak scaling).  ``value`` = Allocate p50 in
 microseconds over every compiled-client Allocate of every rank in the timed window (lower
 is better; kubelet is a compiled grpc-go client, and a Python client's own ~80 us per
@@ -193,8 +194,16 @@ def main() -> int:
     conn = http.client.HTTPConnection("127.0.0.1", info["port"], timeout=10)
     perf = time.perf_counter
 
+    def phase_sync():
+        # Ranks move through a step's phases together: the kubelet RPC phase is measured
+        # under N concurrent kubelet-like clients, not under N-1 other ranks' max-rate
+        # scrapers, and every rank's scrape window overlaps (aggregate daemon throughput).
+        if world > 1:
+            dist.barrier()
+
     def step(rec):
         a, p, s, an, pn = rec
+        phase_sync()
         an.extend(h2.bench_unary(v1beta1.METHOD_ALLOCATE, alloc_req, ALLOCS))
         pn.extend(h2.bench_unary(v1beta1.METHOD_GET_PREFERRED, pref_req, PREFS))
         for _ in range(ALLOCS):
@@ -205,6 +214,7 @@ def main() -> int:
             t0 = perf()
             pref_raw(pref_req)
             p.append(perf() - t0)
+        phase_sync()
         r = n.http_load("127.0.0.1", info["port"], "/metrics", SCRAPE_CONNS, SCRAPE_S, 0.0)
         if r["errors"]:
             raise RuntimeError("%d /metrics scrape errors" % r["errors"])
