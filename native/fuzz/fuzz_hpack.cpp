@@ -4,7 +4,11 @@
 //  * a block that decodes re-encodes (literal, never-indexed, Huffman or not) into a
 //    block that a fresh decoder decodes to the same header list;
 //  * Huffman encode -> decode is the identity on arbitrary bytes;
-//  * the dynamic table never exceeds the advertised 4096-octet limit.
+//  * the dynamic table never exceeds the advertised 4096-octet limit;
+//  * the server's visitor decode (views, no header strings) accepts/rejects the same
+//    blocks, yields the same headers and leaves the same dynamic-table state as the
+//    vector decode;
+//  * the table-driven Huffman decoder agrees with the bit-by-bit reference.
 // The first input byte splits the rest into two header blocks decoded on one decoder,
 // so dynamic-table state carried across blocks (and size updates) is exercised.
 #include <cstdint>
@@ -51,6 +55,34 @@ extern "C" int LLVMFuzzerTestOneInput(const uint8_t* data, size_t size) {
       for (size_t i = 0; i < back.size(); ++i)
         if (back[i].name != h1[i].name || back[i].value != h1[i].value) std::abort();
     }
+  }
+  {  // differential: visitor decode vs vector decode, over the same two blocks
+    hpack::Decoder a, b;
+    std::vector<hpack::Header> va;
+    std::vector<std::pair<std::string, std::string>> vb;
+    auto sink = [](void* ctx, std::string_view n, std::string_view v) {
+      static_cast<std::vector<std::pair<std::string, std::string>>*>(ctx)->emplace_back(n, v);
+    };
+    const uint8_t* blocks[2] = {p, p + split};
+    const size_t lens[2] = {split, size - 1 - split};
+    for (int k = 0; k < 2; ++k) {
+      va.clear();
+      vb.clear();
+      const bool ra = a.decode(blocks[k], lens[k], &va);
+      const bool rb = b.decode(blocks[k], lens[k], sink, &vb);
+      if (ra != rb) std::abort();
+      if (!ra) break;
+      if (va.size() != vb.size() || a.table_size() != b.table_size() || a.table_entries() != b.table_entries())
+        std::abort();
+      for (size_t i = 0; i < va.size(); ++i)
+        if (va[i].name != vb[i].first || va[i].value != vb[i].second) std::abort();
+    }
+  }
+  {
+    std::string x, y;
+    const bool rx = hpack::huffman_decode(p, size - 1, &x);
+    const bool ry = hpack::huffman_decode_bitwise(p, size - 1, &y);
+    if (rx != ry || (rx && x != y)) std::abort();
   }
   const std::string_view raw(reinterpret_cast<const char*>(p), size - 1);
   std::string enc, dec;
