@@ -61,6 +61,9 @@ class HealthConfig:
     canaryBytes: int = 256 << 20
     canaryTimeoutS: float = 120.0
     rejectUnhealthyAllocate: bool = True
+    # retired + pending HBM pages at which a GPU goes Unhealthy: 0 = the GPU's own RAS
+    # threshold when readable (root), -1 = never, N > 0 = N
+    badPageThreshold: int = 0
 
 
 @dataclass

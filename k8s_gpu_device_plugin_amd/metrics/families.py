@@ -52,6 +52,10 @@ FAMILIES = (
            "Temperature by sensor: edge, hotspot, mem, hbm0..N"),
     Family("amdgpu_clock_mhz", "gauge", GPU + ("clock",), "exporter", "gfx / mem clocks"),
     Family("amdgpu_ecc_errors_total", "counter", GPU + ("type",), "exporter", "ECC (un)correctable counts"),
+    Family("amdgpu_retired_pages", "gauge", GPU + ("status",), "exporter",
+           "RAS retired HBM pages: reserved / pending / unreservable"),
+    Family("amdgpu_retired_pages_threshold", "gauge", GPU, "exporter",
+           "Retired + pending pages that make the GPU Unhealthy (health.badPageThreshold or the GPU's RAS threshold)"),
     Family("amdgpu_xgmi_link_up", "gauge", GPU + ("link", "peer"), "exporter", "xGMI link to peer is up"),
     Family("amdgpu_xgmi_read_bytes_total", "counter", GPU + ("link", "peer"), "exporter", "xGMI bytes received"),
     Family("amdgpu_xgmi_write_bytes_total", "counter", GPU + ("link", "peer"), "exporter", "xGMI bytes sent"),

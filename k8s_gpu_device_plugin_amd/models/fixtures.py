@@ -143,6 +143,7 @@ def build_backend(spec):
             caps |= {1: 1, 2: 2, 4: 4, 8: 8}[NPS_BITS[str(c).upper()]]
         info.nps_caps = caps
         info.num_compute_units = int(g.get("num_cus", MI355X_CUS))
+        info.bad_page_threshold = int(g.get("bad_page_threshold", -1))  # -1: RAS threshold not readable
         nparts = int(g.get("num_partitions", PARTITIONS.get(info.compute_partition, 1)))
         info.num_xgmi_links = max(0, len(gpus) - 1)
         info.partitions = _partitions(n, gi, info.uuid, nparts, info.numa_node, info.vram_total_bytes, render)

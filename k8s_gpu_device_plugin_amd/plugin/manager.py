@@ -215,6 +215,14 @@ class PluginManager:
                 write_feature_file(self.cfg.nodeFeatureFile, node_labels(gpus))
             except OSError as e:
                 log.error("cannot write node feature file %s: %s", self.cfg.nodeFeatureFile, e)
+        # retired-page limit per GPU: config override, else the GPU's own RAS threshold
+        limit = int(self.cfg.health.badPageThreshold)
+        for g in gpus:
+            g.bad_page_threshold = limit if limit > 0 else (g.bad_page_threshold if limit == 0 else -1)
+        thresholds = [-1] * (max([g.index for g in gpus], default=-1) + 1)
+        for g in gpus:
+            thresholds[g.index] = g.bad_page_threshold
+        self.monitor.set_bad_page_thresholds(thresholds)
         self.exporter.set_inventory(gpus)
         self.exporter.set_partition_labels(labels)
         self.exporter.set_tables([p.table for p in plugins])

@@ -235,6 +235,8 @@ class AmdSmiBackend : public Backend {
         g.nps_caps = mcfg.partition_caps.nps_cap_mask & 0xF;
       if (g.compute_partition.empty()) g.compute_partition = plist.size() == 1 ? "SPX" : "UNKNOWN";
       if (g.memory_partition.empty()) g.memory_partition = "NPS1";
+      uint32_t thr = 0;  // needs root; -1 when not readable
+      if (amdsmi_get_gpu_bad_page_threshold(h0, &thr) == AMDSMI_STATUS_SUCCESS) g.bad_page_threshold = static_cast<int>(thr);
       int32_t numa = -1;
       if (amdsmi_get_gpu_topo_numa_affinity(h0, &numa) != AMDSMI_STATUS_SUCCESS || numa < 0) numa = sysfs_numa(g.bdf);
       g.numa_node = numa;
@@ -381,7 +383,9 @@ class AmdSmiBackend : public Backend {
     }
     t = charge(kCallEcc, t);
     link_state_locked(gpu, s);
-    charge(kCallLinks, t);
+    t = charge(kCallLinks, t);
+    bad_pages_locked(gpu, h0, s);
+    charge(kCallBadPages, t);
     return s->ok;
   }
 
@@ -482,6 +486,38 @@ class AmdSmiBackend : public Backend {
 
   // Peer lookup for every xGMI link of every sample: BDF keys are cached at discovery
   // (7 links x 8 GPUs per tick would otherwise re-query amdsmi 8 times per link).
+  // RAS retired-page records change only when the driver retires a page: re-read them
+  // every kBadPageRefreshNs and report the cached counts in between.
+  static constexpr int64_t kBadPageRefreshNs = 10'000'000'000LL;
+  void bad_pages_locked(int gpu, amdsmi_processor_handle h, GpuSample* s) {
+    if (bad_pages_.size() != procs_.size()) bad_pages_.assign(procs_.size(), BadPages{});
+    BadPages& bp = bad_pages_[gpu];
+    const int64_t now = mono_ns();
+    if (bp.read_ns == 0 || now - bp.read_ns >= kBadPageRefreshNs) {
+      bp.read_ns = now;
+      bp.reserved = bp.pending = bp.unreservable = -1;
+      uint32_t n = 0;
+      if (amdsmi_get_gpu_bad_page_info(h, &n, nullptr) == AMDSMI_STATUS_SUCCESS) {
+        bp.reserved = bp.pending = bp.unreservable = 0;
+        if (n > 0) {
+          std::vector<amdsmi_retired_page_record_t> rec(n);
+          if (amdsmi_get_gpu_bad_page_info(h, &n, rec.data()) == AMDSMI_STATUS_SUCCESS) {
+            for (uint32_t i = 0; i < n && i < rec.size(); ++i) {
+              if (rec[i].status == AMDSMI_MEM_PAGE_STATUS_PENDING) ++bp.pending;
+              else if (rec[i].status == AMDSMI_MEM_PAGE_STATUS_UNRESERVABLE) ++bp.unreservable;
+              else ++bp.reserved;
+            }
+          } else {
+            bp.reserved = n;  // count known, statuses not
+          }
+        }
+      }
+    }
+    s->retired_pages = bp.reserved;
+    s->pending_pages = bp.pending;
+    s->unreservable_pages = bp.unreservable;
+  }
+
   int gpu_of_bdf(const amdsmi_bdf_t& b) const {
     const auto it = std::find(bdf_keys_.begin(), bdf_keys_.end(), bdf_key(b));
     return it == bdf_keys_.end() ? -1 : static_cast<int>(it - bdf_keys_.begin());
@@ -520,8 +556,14 @@ class AmdSmiBackend : public Backend {
   }
 
   // per-call cost accounting for sample() (guarded by mu_)
-  enum SampleCall { kCallGpuMetrics, kCallVram, kCallEcc, kCallLinks, kCallCount };
-  static constexpr const char* kCallNames[kCallCount] = {"gpu_metrics", "vram_usage", "ecc_count", "xgmi_links"};
+  enum SampleCall { kCallGpuMetrics, kCallVram, kCallEcc, kCallLinks, kCallBadPages, kCallCount };
+  static constexpr const char* kCallNames[kCallCount] = {"gpu_metrics", "vram_usage", "ecc_count", "xgmi_links",
+                                                         "bad_pages"};
+  struct BadPages {
+    int64_t read_ns = 0;
+    int64_t reserved = -1, pending = -1, unreservable = -1;
+  };
+  std::vector<BadPages> bad_pages_;  // per GPU, guarded by mu_
   int64_t charge(int call, int64_t since) {
     const int64_t now = mono_ns();
     cost_ns_[call] += now - since;

@@ -59,6 +59,7 @@ struct GpuInfo {
   uint32_t nps_caps = 0;          // bit0 NPS1, bit1 NPS2, bit2 NPS4, bit3 NPS8
   int num_compute_units = 0;
   int num_xgmi_links = 0;
+  int bad_page_threshold = -1;    // RAS retired-page threshold (-1 = not readable)
   std::vector<PartitionInfo> partitions;
 };
 
@@ -108,6 +109,11 @@ struct GpuSample {
   int64_t ecc_correctable = -1;
   int64_t ecc_uncorrectable = -1;
   int64_t throttle_status = -1;
+  // RAS retired (bad) HBM pages by status; -1 = unavailable.  Refreshed at a slower
+  // cadence than the rest of the sample (the page table rarely changes).
+  int64_t retired_pages = -1;
+  int64_t pending_pages = -1;
+  int64_t unreservable_pages = -1;
   int num_links = 0;
   int link_peer[kMaxXgmiLinks] = {};  // physical GPU index of the peer, -1 unknown
   int link_up[kMaxXgmiLinks] = {};    // 1 up, 0 down, -1 unknown/disabled
@@ -131,6 +137,8 @@ enum EventKind : int {
   kEvtVmFault = 7,      // informational
   kEvtDeviceLost = 8,   // device disappeared / unrecoverable -> Unhealthy
   kEvtDeviceRecovered = 9,
+  kEvtRetiredPagesExceeded = 10,  // retired + pending pages >= threshold -> Unhealthy
+  kEvtRetiredPagesCleared = 11,   // back below the threshold (threshold raised, GPU swapped)
 };
 
 const char* event_kind_name(int kind);

@@ -61,6 +61,7 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("nps_caps", &GpuInfo::nps_caps)
       .def_readwrite("num_compute_units", &GpuInfo::num_compute_units)
       .def_readwrite("num_xgmi_links", &GpuInfo::num_xgmi_links)
+      .def_readwrite("bad_page_threshold", &GpuInfo::bad_page_threshold)
       .def_readwrite("partitions", &GpuInfo::partitions);
 
   py::class_<Link>(m, "Link")
@@ -120,6 +121,9 @@ PYBIND11_MODULE(_native, m) {
       .def_readonly("vram_total_bytes", &GpuSample::vram_total_bytes)
       .def_readonly("ecc_correctable", &GpuSample::ecc_correctable)
       .def_readonly("ecc_uncorrectable", &GpuSample::ecc_uncorrectable)
+      .def_readonly("retired_pages", &GpuSample::retired_pages)
+      .def_readonly("pending_pages", &GpuSample::pending_pages)
+      .def_readonly("unreservable_pages", &GpuSample::unreservable_pages)
       .def_readonly("throttle_status", &GpuSample::throttle_status)
       .def_property_readonly("links", [](const GpuSample& s) {
         py::list l;
@@ -140,6 +144,8 @@ PYBIND11_MODULE(_native, m) {
   m.attr("EVT_VM_FAULT") = static_cast<int>(kEvtVmFault);
   m.attr("EVT_DEVICE_LOST") = static_cast<int>(kEvtDeviceLost);
   m.attr("EVT_DEVICE_RECOVERED") = static_cast<int>(kEvtDeviceRecovered);
+  m.attr("EVT_RETIRED_PAGES_EXCEEDED") = static_cast<int>(kEvtRetiredPagesExceeded);
+  m.attr("EVT_RETIRED_PAGES_CLEARED") = static_cast<int>(kEvtRetiredPagesCleared);
   m.attr("LINK_INTERNAL") = static_cast<int>(kLinkInternal);
   m.attr("LINK_PCIE") = static_cast<int>(kLinkPcie);
   m.attr("LINK_XGMI") = static_cast<int>(kLinkXgmi);
@@ -211,6 +217,8 @@ PYBIND11_MODULE(_native, m) {
       .def("inject_event", &FixtureBackend::inject_event)
       .def("set_fail_discovery", &FixtureBackend::set_fail_discovery)
       .def("set_ecc_uncorrectable", &FixtureBackend::set_ecc_uncorrectable)
+      .def("set_retired_pages", &FixtureBackend::set_retired_pages, py::arg("gpu"), py::arg("reserved"),
+           py::arg("pending") = 0)
       .def("set_gpu_present", &FixtureBackend::set_gpu_present)
       .def_property_readonly("discover_calls", &FixtureBackend::discover_calls);
 
@@ -366,6 +374,9 @@ PYBIND11_MODULE(_native, m) {
       .def("pop", &HealthMonitor::pop, py::call_guard<py::gil_scoped_release>(), py::arg("timeout_ms") = 200)
       .def("gpu_healthy", &HealthMonitor::gpu_healthy)
       .def("set_fast_tables", &HealthMonitor::set_fast_tables)
+      .def("set_bad_page_thresholds", &HealthMonitor::set_bad_page_thresholds)
+      .def("on_sample", &HealthMonitor::on_sample, py::arg("gpu"), py::arg("ok"), py::arg("sample"),
+           py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("events_seen", &HealthMonitor::events_seen);
 
   // ---- exporter ----

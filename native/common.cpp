@@ -27,6 +27,8 @@ const char* event_kind_name(int kind) {
     case kEvtVmFault: return "vm_fault";
     case kEvtDeviceLost: return "device_lost";
     case kEvtDeviceRecovered: return "device_recovered";
+    case kEvtRetiredPagesExceeded: return "retired_pages_threshold";
+    case kEvtRetiredPagesCleared: return "retired_pages_below_threshold";
     default: return "none";
   }
 }

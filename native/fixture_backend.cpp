@@ -31,6 +31,7 @@ void FixtureBackend::add_gpu(const GpuInfo& g) {
   for (int a = 0; a < old.n; ++a)
     for (int b = 0; b < old.n; ++b) topo_.at(a, b) = old.at(a, b);
   ecc_ue_.push_back(0);
+  pages_.emplace_back(0, 0);
   present_.push_back(true);
 }
 
@@ -48,6 +49,7 @@ void FixtureBackend::clear() {
   gpus_.clear();
   topo_.resize(0);
   ecc_ue_.clear();
+  pages_.clear();
   present_.clear();
   scheduled_.clear();
   pending_.clear();
@@ -81,6 +83,12 @@ void FixtureBackend::set_ecc_uncorrectable(int gpu, int64_t count) {
   std::lock_guard<std::mutex> lk(mu_);
   if (gpu < 0 || gpu >= static_cast<int>(ecc_ue_.size())) throw std::out_of_range("bad gpu");
   ecc_ue_[gpu] = count;
+}
+
+void FixtureBackend::set_retired_pages(int gpu, int64_t reserved, int64_t pending) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (gpu < 0 || gpu >= static_cast<int>(pages_.size())) throw std::out_of_range("bad gpu");
+  pages_[gpu] = {reserved, pending};
 }
 
 void FixtureBackend::set_gpu_present(int gpu, bool present) {
@@ -135,6 +143,9 @@ bool FixtureBackend::sample(int gpu, GpuSample* s) {
   s->vram_used_bytes = g.vram_total_bytes * 0.6 * load;
   s->ecc_correctable = static_cast<int64_t>(ts) % 3;
   s->ecc_uncorrectable = ecc_ue_[gpu];
+  s->retired_pages = pages_[gpu].first;
+  s->pending_pages = pages_[gpu].second;
+  s->unreservable_pages = 0;
   s->throttle_status = 0;
   s->num_links = 0;
   for (int peer = 0; peer < topo_.n && s->num_links < kMaxXgmiLinks; ++peer) {

@@ -36,6 +36,7 @@ class FixtureBackend : public Backend {
   void inject_event(const HwEvent& e);
   void set_fail_discovery(bool fail) { fail_discovery_ = fail; }
   void set_ecc_uncorrectable(int gpu, int64_t count);
+  void set_retired_pages(int gpu, int64_t reserved, int64_t pending);
   void set_gpu_present(int gpu, bool present);
   int discover_calls() const { return discover_calls_; }
 
@@ -51,6 +52,7 @@ class FixtureBackend : public Backend {
   };
   std::vector<Scheduled> scheduled_;
   std::vector<int64_t> ecc_ue_;
+  std::vector<std::pair<int64_t, int64_t>> pages_;  // (reserved, pending) per GPU
   std::vector<bool> present_;
   int64_t armed_at_ns_ = 0;
   uint64_t seed_;

@@ -61,7 +61,7 @@ void HealthMonitor::emit_locked(HealthUpdate u) {
 
 void HealthMonitor::reconcile_locked(int gpu, int kind, const std::string& reason) {
   GpuState& st = state_[gpu];
-  const bool healthy = !st.resetting && !st.ecc_bad && !st.lost;
+  const bool healthy = !st.resetting && !st.ecc_bad && !st.lost && !st.pages_bad;
   if (healthy == st.reported_healthy) return;
   st.reported_healthy = healthy;
   if (!healthy)
@@ -106,6 +106,12 @@ void HealthMonitor::process(const HwEvent& e) {
       if (!valid(e.gpu)) return;
       state_[e.gpu].lost = false;
       state_[e.gpu].failures = 0;
+      reconcile_locked(e.gpu, e.kind, why);
+      return;
+    case kEvtRetiredPagesExceeded:
+    case kEvtRetiredPagesCleared:
+      if (!valid(e.gpu)) return;
+      state_[e.gpu].pages_bad = e.kind == kEvtRetiredPagesExceeded;
       reconcile_locked(e.gpu, e.kind, why);
       return;
     case kEvtLinkDown:
@@ -171,6 +177,18 @@ void HealthMonitor::on_sample(int gpu, bool ok, const GpuSample& s) {
         }
         st.last_ue = s.ecc_uncorrectable;
       }
+      const int thr = gpu < static_cast<int>(page_thresholds_.size()) ? page_thresholds_[gpu] : 0;
+      if (s.retired_pages >= 0) {
+        const int64_t bad = s.retired_pages + std::max<int64_t>(0, s.pending_pages);
+        const bool over = thr > 0 && bad >= thr;
+        if (over != st.pages_bad) {
+          HwEvent e;
+          e.kind = over ? kEvtRetiredPagesExceeded : kEvtRetiredPagesCleared;
+          e.gpu = gpu;
+          e.message = std::to_string(bad) + " retired/pending HBM pages, threshold " + std::to_string(thr);
+          derived.push_back(e);
+        }
+      }
       for (int k = 0; k < s.num_links; ++k) {
         if (s.link_peer[k] < 0 || s.link_up[k] < 0) continue;
         auto it = st.link_up.find(s.link_peer[k]);
@@ -201,6 +219,11 @@ std::vector<HealthUpdate> HealthMonitor::pop(int timeout_ms) {
 void HealthMonitor::set_fast_tables(std::vector<std::shared_ptr<DeviceTable>> tables) {
   std::lock_guard<std::mutex> lk(mu_);
   fast_tables_ = std::move(tables);
+}
+
+void HealthMonitor::set_bad_page_thresholds(std::vector<int> thresholds) {
+  std::lock_guard<std::mutex> lk(mu_);
+  page_thresholds_ = std::move(thresholds);
 }
 
 bool HealthMonitor::gpu_healthy(int gpu) const {

@@ -59,6 +59,8 @@ class HealthMonitor {
   // update reaches the Python manager.  Healthy transitions stay with the manager,
   // which may hold a GPU back for the recovery canary.
   void set_fast_tables(std::vector<std::shared_ptr<DeviceTable>> tables);
+  // Per-GPU retired-page limits (index = GPU; <= 0 disables the check for that GPU).
+  void set_bad_page_thresholds(std::vector<int> thresholds);
   uint64_t events_seen() const { return events_seen_; }
 
  private:
@@ -66,6 +68,7 @@ class HealthMonitor {
     bool resetting = false;
     bool ecc_bad = false;
     bool lost = false;
+    bool pages_bad = false;  // retired + pending pages at/over the threshold (not cleared by a reset)
     int failures = 0;
     int64_t last_ue = -1;
     bool reported_healthy = true;
@@ -82,6 +85,7 @@ class HealthMonitor {
   std::deque<HealthUpdate> queue_;
   std::vector<GpuState> state_;
   std::vector<std::shared_ptr<DeviceTable>> fast_tables_;
+  std::vector<int> page_thresholds_;
   std::thread thread_;
   std::atomic<bool> running_{false};
   bool stop_ = false;

@@ -286,6 +286,31 @@ void Exporter::render_gpu_text(const std::vector<GpuSample>& samples, const std:
            static_cast<double>(samples[g].ecc_uncorrectable));
     }
   }
+  {  // RAS retired pages (+ the threshold that makes a GPU Unhealthy)
+    bool hdr = false;
+    for (size_t g = 0; g < gpus.size(); ++g) {
+      const GpuSample& s = samples[g];
+      if (!ok[g] || s.retired_pages < 0) continue;
+      if (!hdr) {
+        append_header(&o, "amdgpu_retired_pages", "RAS retired (bad) HBM pages by status.", "gauge");
+        hdr = true;
+      }
+      line(&o, "amdgpu_retired_pages", gl[g] + ",status=\"reserved\"", static_cast<double>(s.retired_pages));
+      line(&o, "amdgpu_retired_pages", gl[g] + ",status=\"pending\"", static_cast<double>(std::max<int64_t>(0, s.pending_pages)));
+      line(&o, "amdgpu_retired_pages", gl[g] + ",status=\"unreservable\"",
+           static_cast<double>(std::max<int64_t>(0, s.unreservable_pages)));
+    }
+    hdr = false;
+    for (size_t g = 0; g < gpus.size(); ++g) {
+      if (gpus[g].bad_page_threshold <= 0) continue;
+      if (!hdr) {
+        append_header(&o, "amdgpu_retired_pages_threshold",
+                      "Retired + pending pages at which the GPU is advertised Unhealthy.", "gauge");
+        hdr = true;
+      }
+      line(&o, "amdgpu_retired_pages_threshold", gl[g], gpus[g].bad_page_threshold);
+    }
+  }
   {  // xGMI
     std::string up, rd, wr;
     for (size_t g = 0; g < gpus.size(); ++g) {

@@ -57,8 +57,20 @@ def test_amdsmi_sample_cost_breakdown(amdsmi_backend):
     per = {k: (after[k][0] - before[k][0]) / 20 * 1e6 for k in after}
     print("amdsmi sample cost per GPU (us):", {k: round(v, 1) for k, v in per.items()},
           "total %.1f us" % sum(per.values()))
-    assert set(per) == {"gpu_metrics", "vram_usage", "ecc_count", "xgmi_links"}
+    assert set(per) == {"gpu_metrics", "vram_usage", "ecc_count", "xgmi_links", "bad_pages"}
     assert sum(per.values()) < 50e3
+
+
+def test_amdsmi_retired_pages(amdsmi_backend):
+    """RAS retired-page records read through amdsmi (0 on a healthy GPU); the threshold
+    is root-only, so -1 is accepted for it."""
+    gpus, _ = amdsmi_backend.discover()
+    s = amdsmi_backend.sample(0)
+    print("retired pages", s.retired_pages, s.pending_pages, s.unreservable_pages,
+          "threshold", gpus[0].bad_page_threshold)
+    assert s.retired_pages >= 0 or s.retired_pages == -1
+    assert s.retired_pages <= 0 or s.retired_pages < 10**6
+    assert gpus[0].bad_page_threshold == -1 or gpus[0].bad_page_threshold > 0
 
 
 def test_exporter_renders_real_metrics(n, amdsmi_backend):

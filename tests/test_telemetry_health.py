@@ -133,3 +133,67 @@ def test_prometheus_number_formatting(n):
 @given(st.floats(allow_nan=False, allow_infinity=False))
 def test_prometheus_number_round_trips(n, v):
     assert float(n.format_float(v)) == v
+
+
+def test_retired_pages_threshold_state_machine(n):
+    """Retired + pending HBM pages at the threshold latch Unhealthy; a reset does not
+    clear it (retired pages persist), dropping below the threshold does."""
+    be = fixtures.build_backend("2gpu_spx")
+    m = n.HealthMonitor(be, 3)
+    m.set_gpu_count(2)
+    m.set_bad_page_thresholds([10, 0])
+    ok = be.sample(1)
+    assert ok.retired_pages == 0 and ok.pending_pages == 0
+    be.set_retired_pages(0, 8, 2)
+    be.set_retired_pages(1, 500, 0)  # threshold 0 on GPU 1: check disabled
+    for g in (0, 1):
+        m.on_sample(g, True, be.sample(g))
+    u = m.pop(100)
+    assert [(x.gpu, x.healthy) for x in u] == [(0, 0)] and "retired" in u[0].reason
+    m.process(n.HwEvent(n.EVT_PRE_RESET, 0))
+    m.process(n.HwEvent(n.EVT_POST_RESET, 0))
+    m.on_sample(0, True, be.sample(0))
+    assert m.pop(50) == [] and not m.gpu_healthy(0)
+    be.set_retired_pages(0, 9, 0)
+    m.on_sample(0, True, be.sample(0))
+    assert [(x.gpu, x.healthy) for x in m.pop(100)] == [(0, 1)]
+
+
+def test_retired_pages_exported_and_gate_advertisement(make_cfg, plugin_dir):
+    import time as _t
+    from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import KubeletStub
+    from k8s_gpu_device_plugin_amd.plugin.manager import PluginManager
+    model = fixtures.mi355x_node(2)
+    for g in model["gpus"]:
+        g["bad_page_threshold"] = 64  # what a root-readable RAS threshold would report
+    be = fixtures.build_backend(model)
+    with KubeletStub(plugin_dir) as k:
+        m = PluginManager(make_cfg(telemetry={"intervalMs": 40}), backend=be)
+        t = m.start_background()
+        try:
+            w = k.watch(k.wait_for_registrations(1)[0].endpoint)
+            w.next()
+            be.set_retired_pages(1, 60, 4)
+            _, devs = w.next(timeout=5)
+            assert [h for _, h, _ in devs] == ["Healthy", "Unhealthy"]
+            _t.sleep(0.1)
+            fams = _families(m.exporter.render())
+            pages = {(s.labels["gpu"], s.labels["status"]): s.value for s in fams["amdgpu_retired_pages"].samples}
+            assert pages[("1", "reserved")] == 60 and pages[("1", "pending")] == 4 and pages[("0", "reserved")] == 0
+            thr = {s.labels["gpu"]: s.value for s in fams["amdgpu_retired_pages_threshold"].samples}
+            assert thr == {"0": 64.0, "1": 64.0}
+        finally:
+            m.stop()
+            t.join(10)
+    # health.badPageThreshold overrides the hardware value; -1 turns the check off
+    be = fixtures.build_backend(model)
+    be.set_retired_pages(0, 1000, 0)
+    m = PluginManager(make_cfg(health={"badPageThreshold": -1}, telemetry={"intervalMs": 40}), backend=be)
+    t = m.start_background()
+    try:
+        _t.sleep(0.2)
+        assert all(p.table.healthy_count() == len(p) for p in m.plugins)
+        assert "amdgpu_retired_pages_threshold" not in m.exporter.render()
+    finally:
+        m.stop()
+        t.join(10)
