@@ -292,12 +292,54 @@ def uds_floor():
             "p50_us": us(pct(lat, 0.5)), "p99_us": us(pct(lat, 0.99)), "round_trips": len(lat)}
 
 
-RUNNERS = {"floor": uds_floor, "health": health_propagation, "1": config1, "2": config2, "3": config3, "4": config4, "5": config5, "scaling": scaling}
+def startup(runs=5):
+    """Plugin start-up as kubelet sees it: process spawn -> Registration.Register
+    received -> first ListAndWatch answered (fresh process each run, so Python start,
+    imports, hardware discovery and the native servers are all inside).  The reference
+    publishes no start-up figure."""
+    import subprocess
+    import sys
+    nat = native.load()
+    backend = "amdsmi" if nat.amdsmi_available() else "fixture"
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    reg_t, law_t = [], []
+    for _ in range(runs):
+        d = tempfile.mkdtemp(prefix="dp-start-", dir="/tmp")
+        kubelet = KubeletStub(d).start()
+        env = dict(os.environ, PYTHONPATH=root + os.pathsep + os.environ.get("PYTHONPATH", ""))
+        cmd = [sys.executable, "-m", "k8s_gpu_device_plugin_amd", "--configFile", "none", "--backend", backend,
+               "--fixture", "8gpu_spx_mesh", "--plugin-dir", d, "--web-listen-address", "127.0.0.1:0",
+               "--log-dir", "", "--log-level", "warn"]
+        t0 = time.perf_counter()
+        proc = subprocess.Popen(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                                start_new_session=True)
+        try:
+            reg = kubelet.wait_for_registrations(1, timeout=60)[0]
+            reg_t.append(time.perf_counter() - t0)
+            c = nat.H2Client(os.path.join(d, reg.endpoint))
+            c.first_stream_message(v1beta1.METHOD_LIST_AND_WATCH, b"")
+            law_t.append(time.perf_counter() - t0)
+            c.close()
+        finally:
+            proc.terminate()
+            try:
+                proc.wait(15)
+            except subprocess.TimeoutExpired:
+                proc.kill()
+            kubelet.stop()
+            shutil.rmtree(d, ignore_errors=True)
+    ms = lambda x: None if x is None else round(x * 1e3, 1)  # noqa: E731
+    return {"config": "process spawn -> Register -> first ListAndWatch (%s backend)" % backend, "runs": runs,
+            "register_p50_ms": ms(pct(reg_t, 0.5)), "register_max_ms": ms(max(reg_t)),
+            "first_list_and_watch_p50_ms": ms(pct(law_t, 0.5))}
+
+
+RUNNERS = {"floor": uds_floor, "startup": startup, "health": health_propagation, "1": config1, "2": config2, "3": config3, "4": config4, "5": config5, "scaling": scaling}
 
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
-    ap.add_argument("--configs", default="floor,1,2,3,4,5,scaling,health")
+    ap.add_argument("--configs", default="floor,startup,1,2,3,4,5,scaling,health")
     ap.add_argument("--json", default="")
     a = ap.parse_args(argv)
     from ..utils.log import init_logger
