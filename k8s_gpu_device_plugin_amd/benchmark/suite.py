@@ -337,6 +337,7 @@ def startup(runs=5):
             node.kubelet.restart()
             node.kubelet.wait_for_registrations(i + 2, timeout=30)
             rereg.append(time.perf_counter() - t0)
+            time.sleep(0.05)  # let the plugin's Register call return before the next restart
     finally:
         node.close()
     ms = lambda x: None if x is None else round(x * 1e3, 1)  # noqa: E731
