@@ -78,7 +78,7 @@ def _wait_http(port: int, timeout: float) -> None:
     raise TimeoutError("plugin web server did not come up on port %d" % port)
 
 
-def start_daemon(n_gpus: int, grpc_server: str, workdir: str):
+def start_daemon(n_gpus: int, grpc_server: str, workdir: str, profile_dir: str = ""):
     """Rank 0: kubelet stub + plugin daemon subprocess.  Must run before GPU init."""
     from k8s_gpu_device_plugin_amd import native
     from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import KubeletStub
@@ -97,6 +97,8 @@ def start_daemon(n_gpus: int, grpc_server: str, workdir: str):
                 "http:\n  accessLog: false\n  threads: %d\ngrpc:\n  server: %s\n  threads: %d\n"
                 "telemetry:\n  intervalMs: 1000\n"
                 % (port, backend, n_gpus, n_gpus - 1, plugin_dir, threads, grpc_server, threads))
+        if profile_dir:  # benchmark: true -> cpu/mem/threads/native profiles when the daemon exits
+            f.write("benchmark: true\nbenchmarkDir: \"%s\"\n" % os.path.abspath(profile_dir))
     env = dict(os.environ)
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
     log = open(os.path.join(workdir, "daemon.log"), "w")
@@ -114,6 +116,7 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--grpc-server", choices=["native", "python"], default="native")
     ap.add_argument("--no-canary", action="store_true")
+    ap.add_argument("--profile-dir", default="", help="run the daemon with benchmark: true, profiles here")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -135,7 +138,7 @@ def main() -> int:
     if rank == 0:  # daemon first: nothing has touched the GPU in this process yet
         shutil.rmtree(workdir, ignore_errors=True)
         os.makedirs(workdir)
-        proc, kubelet, port, reg, backend = start_daemon(n_gpus, args.grpc_server, workdir)
+        proc, kubelet, port, reg, backend = start_daemon(n_gpus, args.grpc_server, workdir, args.profile_dir)
         info = {"port": port, "endpoint": reg.endpoint, "resource": reg.resource_name, "backend": backend,
                 "plugin_dir": os.path.join(workdir, "device-plugins")}
 

@@ -45,6 +45,7 @@ CORE_SOURCES = [
     "hpack.cpp",
     "grpc_h2.cpp",
     "loadgen.cpp",
+    "profiler.cpp",
 ]
 BINDING_SOURCES = ["bindings.cpp"]
 FUZZ_TARGETS = ("pbwire", "hpack", "grpc", "http")

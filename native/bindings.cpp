@@ -14,6 +14,7 @@
 #include "httpd.h"
 #include "loadgen.h"
 #include "metrics.h"
+#include "profiler.h"
 #include "telemetry.h"
 #include "watch.h"
 
@@ -630,6 +631,23 @@ PYBIND11_MODULE(_native, m) {
         return health_propagation(*fx, sock, gpu, events);
       },
       py::arg("backend"), py::arg("socket_path"), py::arg("gpu"), py::arg("events") = 60);
+  // ---- whole-process CPU sampling profiler (benchmark: true) ----
+  m.def("prof_start", &prof::start, py::arg("hz") = 997);
+  m.def("prof_stop", &prof::stop);
+  m.def("prof_running", &prof::running);
+  m.def("prof_dropped", &prof::dropped);
+  m.def("prof_histogram", []() {
+    py::list out;  // (module, offset, exported symbol or "", samples)
+    for (const auto& kv : prof::histogram()) {
+      std::string path, sym;
+      uintptr_t base = 0;
+      if (prof::module_of(kv.first, &path, &base, &sym))
+        out.append(py::make_tuple(path, static_cast<uint64_t>(kv.first - base), sym, kv.second));
+      else
+        out.append(py::make_tuple(std::string("?"), static_cast<uint64_t>(kv.first), std::string(), kv.second));
+    }
+    return out;
+  });
   m.def("uds_pingpong",
         [](int n, int warmup, int req_bytes, int resp_bytes) {
           py::gil_scoped_release rel;

@@ -72,7 +72,9 @@ def test_daemon_serves_and_exits_gracefully(plugin_dir, tmp_path, sig):
     assert "exiting gracefully" in info and "see you next time!" in info
     if sig == signal.SIGTERM:
         files = set(os.listdir(bench_dir))
-        assert {"cpu.prof", "mem.prof", "threads.prof", "latency.prom"} <= files
+        assert {"cpu.prof", "mem.prof", "threads.prof", "latency.prom", "native.prof"} <= files
+        native_prof = (bench_dir / "native.prof").read_text()
+        assert native_prof.startswith("# whole-process CPU samples")
         assert "amdgpu_device_plugin_rpc_duration_seconds" in (bench_dir / "latency.prom").read_text() or True
 
 

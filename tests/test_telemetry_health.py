@@ -197,3 +197,21 @@ def test_retired_pages_exported_and_gate_advertisement(make_cfg, plugin_dir):
     finally:
         m.stop()
         t.join(10)
+
+
+def test_native_sampling_profiler_sees_native_threads(n):
+    """The benchmark harness's pprof analogue samples every thread, including native
+    threads Python cannot see, and resolves internal C++ functions."""
+    from k8s_gpu_device_plugin_amd.benchmark.profiling import symbolize
+    assert n.prof_start(2000) and n.prof_running()
+    assert not n.prof_start(2000)  # one profile at a time
+    t0 = time.monotonic()
+    while time.monotonic() - t0 < 0.6:
+        n.uds_pingpong(2000, 0, 128, 256)  # client + epoll server threads, no GIL
+    n.prof_stop()
+    n.prof_stop()
+    assert not n.prof_running()
+    rows = symbolize(n.prof_histogram())
+    assert sum(c for _, _, c in rows) >= 20
+    text = " ".join(fn for fn, _, _ in rows)
+    assert any(k in text for k in ("send", "recv", "epoll_wait", "uds_pingpong")), rows[:10]
