@@ -35,7 +35,8 @@ def list_allocations(socket_path: str, resource_prefix: str, timeout: float = 5.
                               response_deserializer=pr.ListPodResourcesResponse.FromString)
         resp = call(pr.ListPodResourcesRequest(), timeout=timeout)
     finally:
-        ch.close()
+        from .plugin import close_async
+        close_async(ch)  # Channel.close() would block the poller ~200 ms per poll
     out: Allocation = {}
     prefix = resource_prefix.rstrip("/") + "/"
     for pod in resp.pod_resources:
