@@ -58,6 +58,7 @@ class HealthConfig:
     lostAfterFailures: int = 3
     canary: bool = False          # gfx950 canary before re-advertising a GPU after a reset
     canaryOnStart: bool = False   # ... and on every partition before the first advertisement
+    canaryOnPreStart: bool = False  # pre_start_required: canary the allocated partitions before each container
     canaryBytes: int = 256 << 20
     canaryTimeoutS: float = 120.0
     rejectUnhealthyAllocate: bool = True

@@ -37,8 +37,8 @@ from .plugin import AmdDevicePlugin
 
 log = get_logger("manager")
 
-EV_STOP, EV_RESTART, EV_RETRY, EV_KUBELET, EV_HEALTH, EV_REDISCOVER, EV_VERIFIED, EV_PODRES = (
-    "stop", "restart", "retry", "kubelet", "health", "rediscover", "verified", "podresources")
+EV_STOP, EV_RESTART, EV_RETRY, EV_KUBELET, EV_HEALTH, EV_REDISCOVER, EV_VERIFIED, EV_PODRES, EV_PRESTART_FAIL = (
+    "stop", "restart", "retry", "kubelet", "health", "rediscover", "verified", "podresources", "prestart_fail")
 HEALTH_LOG_LEN = 4096
 
 
@@ -167,6 +167,9 @@ class PluginManager:
                     self._apply_verified(*ev[1:])
                 elif kind == EV_PODRES:
                     pass  # allocation map changed: _publish_metrics below re-renders it
+                elif kind == EV_PRESTART_FAIL:
+                    self.counters["prestart_failures"] = self.counters.get("prestart_failures", 0) + 1
+                    self._set_health(ev[1], ev[2], False, ev[3])
                 elif kind == EV_REDISCOVER:
                     self._check_inventory()
             except Exception as e:
@@ -188,6 +191,9 @@ class PluginManager:
                                            self.cfg.sharing.replicas, self.cfg.sharing.renameByDefault)
         failed = self._startup_canary(gpus) if self.cfg.health.canaryOnStart else set()
         plugins = [AmdDevicePlugin(name, devs, topo, self.cfg) for name, devs in self.device_map.items()]
+        if self.cfg.health.canaryOnPreStart:
+            for p in plugins:
+                p.prestart_check = self._prestart_check
         # health state survives a reload: re-apply what the monitor currently reports
         for p in plugins:
             for g in gpus:
@@ -332,6 +338,42 @@ class PluginManager:
                     self.counters["canary_failures"] = self.counters.get("canary_failures", 0) + 1
                     log.error("start-up canary failed on GPU %d partition %d: %s", gpu, part, res.get("error") or res)
         return failed
+
+    def _prestart_check(self, ids) -> str:
+        """PreStartContainer verifier (health.canaryOnPreStart): the gfx950 canary on
+        every partition the container is about to get, all in parallel child processes,
+        right before it starts.  A failing partition is marked Unhealthy and the
+        container start is refused.  Runs on the plugin's verifier pool, never on a
+        server thread."""
+        from ..ops import canary
+        want = set(ids)
+        gpus = {g.index: g for g in self.gpus}
+        targets = {}  # (gpu, partition) -> HIP device ids to check
+        for p in self.plugins:
+            for d in p.devices():
+                if d.id not in want or d.gpu not in gpus:
+                    continue
+                parts = gpus[d.gpu].partitions
+                sel = parts if d.partition < 0 else [x for x in parts if x.index == d.partition]
+                targets[(d.gpu, d.partition)] = [max(0, x.hip_id) for x in sel]
+        jobs = [(key, hip) for key, hips in targets.items() for hip in hips]
+        if not jobs:
+            return ""
+        failures = {}
+        with concurrent.futures.ThreadPoolExecutor(max_workers=min(8, len(jobs))) as ex:
+            futs = {ex.submit(canary.run_isolated, hip, self.cfg.health.canaryBytes,
+                              self.cfg.health.canaryTimeoutS): key for key, hip in jobs}
+            for f in concurrent.futures.as_completed(futs):
+                res = f.result()
+                self.counters["canary_runs"] = self.counters.get("canary_runs", 0) + 1
+                if not res.get("ok"):
+                    failures.setdefault(futs[f], res.get("error") or "canary reported errors")
+        for (gpu, part), why in sorted(failures.items()):
+            self.events.put((EV_PRESTART_FAIL, gpu, part, "PreStartContainer canary failed: %s" % why))
+        if failures:
+            return "PreStartContainer: gfx950 canary failed on %s" % ", ".join(
+                "GPU %d%s" % (g, "" if p < 0 else " partition %d" % p) for g, p in sorted(failures))
+        return ""
 
     def _check_inventory(self) -> None:
         """Periodic re-discovery: a compute/memory partition-mode change (SPX->CPX, ...) or a

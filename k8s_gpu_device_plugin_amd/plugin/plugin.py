@@ -90,6 +90,7 @@ def make_table(resource: str, devices: Devices, topology, cfg) -> "object":
     tc.cdi = bool(cfg.cdi) if cfg is not None else False
     tc.cdi_prefix = str(resource) + "="
     tc.reject_unhealthy = bool(cfg.health.rejectUnhealthyAllocate) if cfg is not None else True
+    tc.pre_start_required = bool(cfg.health.canaryOnPreStart) if cfg is not None else False
     tds = [n.TableDevice(d.id, d.gpu, d.partition, d.numa_node if d.numa_node is not None else -1, d.replica,
                          list(d.paths), d.health == v1beta1.HEALTHY) for d in devices]
     return n.DeviceTable(tc, tds, topology)
@@ -116,6 +117,10 @@ class AmdDevicePlugin:
         self._supervisor: threading.Thread | None = None
         self.fatal_error: str | None = None
         self.registered = False
+        # PreStartContainer verifier: fn(device ids) -> "" (pass) or an error message
+        self.prestart_check = None
+        self._prestart_thread: threading.Thread | None = None
+        self._prestart_pool: concurrent.futures.ThreadPoolExecutor | None = None
 
     # ------------------------------------------------------------------ views
     def devices(self) -> Devices:
@@ -138,7 +143,29 @@ class AmdDevicePlugin:
             raise
         log.info("Registered device plugin", extra={"resourceName": str(self.resource)})
 
+    def _prestart_loop(self) -> None:
+        """Pops PreStartContainer jobs from the table (either server enqueues them) and
+        runs the verifier off the server threads; several containers verify in parallel."""
+        while not self._stopping:
+            for job_id, ids in self.table.pop_prestart(200):
+                self._prestart_pool.submit(self._run_prestart, job_id, ids)
+
+    def _run_prestart(self, job_id: int, ids) -> None:
+        try:
+            err = self.prestart_check(list(ids)) if self.prestart_check else ""
+        except Exception as e:  # a verifier that cannot run does not pass the devices
+            err = "PreStartContainer check failed to run: %s" % e
+        self.table.complete_prestart(job_id, not err, err or "")
+
     def stop(self) -> None:
+        self.table.cancel_prestart("device plugin for %s is stopping" % self.resource)
+        if self._prestart_thread is not None:
+            self._stopping = True
+            self._prestart_thread.join(2.0)
+            self._prestart_thread = None
+        if self._prestart_pool is not None:
+            self._prestart_pool.shutdown(wait=False, cancel_futures=True)
+            self._prestart_pool = None
         with self._lock:
             self._stopping = True
             server, self._server = self._server, None
@@ -176,6 +203,13 @@ class AmdDevicePlugin:
             else:
                 self._start_grpcio_server()
             self._serving = True
+            if self.cfg is not None and self.cfg.health.canaryOnPreStart and self._prestart_thread is None:
+                self.table.resume_prestart()
+                self._prestart_pool = concurrent.futures.ThreadPoolExecutor(
+                    max_workers=4, thread_name_prefix="prestart-" + self.resource.get_resource_name())
+                self._prestart_thread = threading.Thread(target=self._prestart_loop, daemon=True,
+                                                         name="prestart-" + self.resource.get_resource_name())
+                self._prestart_thread.start()
         # blocking self-dial (plugin/plugin.go:130-134)
         try:
             if self.server_kind == "native":
@@ -244,8 +278,10 @@ class AmdDevicePlugin:
             raise FileNotFoundError("kubelet socket %s does not exist" % self.kubelet_socket)
         ch = dial(self.kubelet_socket, DIAL_TIMEOUT_S)
         try:
+            pre_start = bool(self.cfg.health.canaryOnPreStart) if self.cfg is not None else False
             req = v1beta1.RegisterRequest(version=v1beta1.VERSION, endpoint=os.path.basename(self.socket),
-                                          resource_name=str(self.resource), options=v1beta1.plugin_options())
+                                          resource_name=str(self.resource),
+                                          options=v1beta1.plugin_options(pre_start_required=pre_start))
             call = ch.unary_unary(v1beta1.METHOD_REGISTER, request_serializer=v1beta1.RegisterRequest.SerializeToString,
                                   response_deserializer=v1beta1.Empty.FromString)
             call(req, timeout=DIAL_TIMEOUT_S)
@@ -315,7 +351,24 @@ class AmdDevicePlugin:
             return out
 
         def pre_start(req: bytes, ctx) -> bytes:
-            table.observe(rpc_pre, 0.0, False)
+            t0 = perf()
+            if not (self.cfg is not None and self.cfg.health.canaryOnPreStart):
+                table.observe(rpc_pre, 0.0, False)
+                return b""
+            done = threading.Event()
+            result = []
+
+            def finished(ok: bool, err: str) -> None:
+                result.append((ok, err))
+                done.set()
+
+            queued, err = table.submit_prestart(req, finished)
+            if queued and not done.wait(30.0):  # kubelet's PreStartContainer deadline is 30 s
+                result.append((False, "PreStartContainer check timed out"))
+            ok, err = result[0] if result else (queued, err)
+            table.observe(rpc_pre, perf() - t0, not ok)
+            if not ok:
+                ctx.abort(grpc.StatusCode.UNKNOWN, err)
             return b""
 
         def list_and_watch(req: bytes, ctx):

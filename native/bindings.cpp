@@ -291,7 +291,8 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("permissions", &TableConfig::permissions)
       .def_readwrite("cdi", &TableConfig::cdi)
       .def_readwrite("cdi_prefix", &TableConfig::cdi_prefix)
-      .def_readwrite("reject_unhealthy", &TableConfig::reject_unhealthy);
+      .def_readwrite("reject_unhealthy", &TableConfig::reject_unhealthy)
+      .def_readwrite("pre_start_required", &TableConfig::pre_start_required);
 
   m.attr("RPC_OPTIONS") = static_cast<int>(kRpcOptions);
   m.attr("RPC_LIST_AND_WATCH") = static_cast<int>(kRpcListAndWatch);
@@ -323,6 +324,30 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("version", &DeviceTable::version)
       .def("list_and_watch", [](const DeviceTable& t) { return py::bytes(t.list_and_watch()); })
       .def("options", [](const DeviceTable& t) { return py::bytes(t.options_bytes()); })
+      // PreStartContainer job queue (verifier side + the grpcio server's submit)
+      .def("submit_prestart",
+           [](DeviceTable& t, const py::bytes& req, std::function<void(bool, std::string)> done) {
+             std::string err;
+             const bool ok = t.submit_prestart(std::string(req),
+                                               [done](bool pass, const std::string& e) { done(pass, e); }, &err);
+             return py::make_tuple(ok, err);
+           })
+      .def("pop_prestart",
+           [](DeviceTable& t, int timeout_ms) {
+             std::vector<PreStartJob> jobs;
+             {
+               py::gil_scoped_release rel;
+               jobs = t.pop_prestart(timeout_ms);
+             }
+             py::list out;
+             for (auto& j : jobs) out.append(py::make_tuple(j.id, j.ids));
+             return out;
+           },
+           py::arg("timeout_ms") = 200)
+      .def("complete_prestart", &DeviceTable::complete_prestart)
+      .def("cancel_prestart", &DeviceTable::cancel_prestart, py::call_guard<py::gil_scoped_release>())
+      .def("resume_prestart", &DeviceTable::resume_prestart)
+      .def_property_readonly("prestart_pending", &DeviceTable::prestart_pending)
       .def("allocate",
            [](const DeviceTable& t, const py::bytes& req) {
              std::string out;

@@ -205,8 +205,84 @@ std::string DeviceTable::list_and_watch() const {
 
 std::string DeviceTable::options_bytes() const {
   std::string s;
+  pb::put_bool_nz(&s, 1, cfg_.pre_start_required);
   pb::put_bool_nz(&s, 2, true);  // get_preferred_allocation_available
   return s;
+}
+
+bool DeviceTable::submit_prestart(std::string_view req, PreStartDone done, std::string* error) {
+  PreStartJob job;
+  try {
+    pb::Reader r(req);  // PreStartContainerRequest{ repeated string devices_ids = 1 }
+    uint32_t f, w;
+    while (r.next(&f, &w)) {
+      if (f == 1 && w == 2) job.ids.emplace_back(r.bytes());
+      else r.skip(w);
+    }
+  } catch (const pb::DecodeError& e) {
+    *error = std::string("malformed PreStartContainerRequest: ") + e.what();
+    return false;
+  }
+  for (const auto& id : job.ids)
+    if (index_of(id) < 0) {
+      *error = "PreStartContainer for '" + cfg_.resource_name + "': unknown device: " + id;
+      return false;
+    }
+  {
+    std::lock_guard<std::mutex> lk(pmu_);
+    if (pcancel_) {
+      *error = "plugin is stopping";
+      return false;
+    }
+    job.id = next_job_++;
+    pwait_.emplace(job.id, std::move(done));
+    pjobs_.push_back(std::move(job));
+  }
+  pcv_.notify_all();
+  return true;
+}
+
+std::vector<PreStartJob> DeviceTable::pop_prestart(int timeout_ms) {
+  std::unique_lock<std::mutex> lk(pmu_);
+  cv_wait_ms(pcv_, lk, timeout_ms, [&] { return !pjobs_.empty() || pcancel_; });
+  std::vector<PreStartJob> out(std::make_move_iterator(pjobs_.begin()), std::make_move_iterator(pjobs_.end()));
+  pjobs_.clear();
+  return out;
+}
+
+void DeviceTable::complete_prestart(uint64_t id, bool ok, const std::string& error) {
+  PreStartDone done;
+  {
+    std::lock_guard<std::mutex> lk(pmu_);
+    auto it = pwait_.find(id);
+    if (it == pwait_.end()) return;  // cancelled meanwhile
+    done = std::move(it->second);
+    pwait_.erase(it);
+  }
+  if (done) done(ok, error);
+}
+
+void DeviceTable::cancel_prestart(const std::string& why) {
+  std::unordered_map<uint64_t, PreStartDone> waiting;
+  {
+    std::lock_guard<std::mutex> lk(pmu_);
+    pcancel_ = true;
+    pjobs_.clear();
+    waiting.swap(pwait_);
+  }
+  pcv_.notify_all();
+  for (auto& kv : waiting)
+    if (kv.second) kv.second(false, why);
+}
+
+void DeviceTable::resume_prestart() {
+  std::lock_guard<std::mutex> lk(pmu_);
+  pcancel_ = false;
+}
+
+size_t DeviceTable::prestart_pending() const {
+  std::lock_guard<std::mutex> lk(pmu_);
+  return pwait_.size();
 }
 
 namespace {

@@ -17,6 +17,8 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -51,6 +53,13 @@ struct TableConfig {
   bool cdi = false;
   std::string cdi_prefix = "amd.com/gpu=";
   bool reject_unhealthy = true;
+  bool pre_start_required = false;  // DevicePluginOptions.pre_start_required
+};
+
+// A PreStartContainer check waiting for the plugin's verifier (the gfx950 canary).
+struct PreStartJob {
+  uint64_t id = 0;
+  std::vector<std::string> ids;
 };
 
 enum Rpc : int {
@@ -113,6 +122,22 @@ class DeviceTable {
   AllocResult preferred_core(const std::string_view* avail, size_t n_avail, const std::string_view* must,
                              size_t n_must, int size) const;
 
+  // PreStartContainer.  With pre_start_required the servers hand each request to the
+  // plugin's verifier through this queue and answer when it completes, so a check
+  // that runs for seconds (a canary on the allocated partitions) never occupies a
+  // server thread and no native thread ever calls into Python.
+  using PreStartDone = std::function<void(bool ok, const std::string& error)>;
+  // Decodes PreStartContainerRequest; unknown ids fail at once (done is not queued).
+  // Returns false with *error on a bad request.
+  bool submit_prestart(std::string_view req, PreStartDone done, std::string* error);
+  // Verifier side: blocks up to timeout_ms for jobs (GIL released by the binding).
+  std::vector<PreStartJob> pop_prestart(int timeout_ms);
+  void complete_prestart(uint64_t id, bool ok, const std::string& error);
+  // Fails every queued/running job (plugin stopping) and wakes pop_prestart.
+  void cancel_prestart(const std::string& why);
+  void resume_prestart();  // accept jobs again (plugin served again after a stop)
+  size_t prestart_pending() const;
+
   void observe(int rpc, double seconds, bool error) const;
   void render_metrics(std::string* out, bool with_headers) const;
   static void render_metric_headers(std::string* out);
@@ -158,6 +183,12 @@ class DeviceTable {
   std::unique_ptr<std::atomic<uint8_t>[]> health_;
   std::mutex wmu_;                                // serialises writers only
   std::mutex lmu_;                                // listeners_
+  mutable std::mutex pmu_;                        // PreStart queue
+  std::condition_variable pcv_;
+  uint64_t next_job_ = 1;
+  std::deque<PreStartJob> pjobs_;                // not yet popped by the verifier
+  std::unordered_map<uint64_t, PreStartDone> pwait_;  // queued or running -> completion
+  bool pcancel_ = false;
   mutable std::mutex vmu_;                        // version waiters
   mutable std::condition_variable vcv_;
   mutable uint64_t wakes_ = 0;

@@ -155,11 +155,43 @@ std::string request_headers(std::string_view path) {
 
 }  // namespace
 
+// Completions of asynchronous RPCs (PreStartContainer checks) for one worker.  Shared
+// with the pending jobs, so a verifier finishing after the worker is gone still has a
+// valid queue and eventfd to post to.
+struct AsyncDone {
+  struct Item {
+    int fd;
+    uint64_t serial;  // connection incarnation: the fd number may have been reused
+    uint32_t sid;
+    bool ok;
+    std::string error;
+    int64_t t0;
+  };
+  std::mutex mu;
+  std::vector<Item> items;
+  int efd = -1;
+  AsyncDone() : efd(eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC)) {}
+  ~AsyncDone() {
+    if (efd >= 0) ::close(efd);
+  }
+  void post(Item it) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      items.push_back(std::move(it));
+    }
+    const uint64_t one = 1;
+    (void)!write(efd, &one, sizeof(one));
+  }
+};
+
 struct GrpcServer::Worker {
   int ep = -1;
   int efd = -1;
+  std::shared_ptr<AsyncDone> done = std::make_shared<AsyncDone>();
+  uint64_t next_serial = 1;
   struct Conn {
     int fd = -1;
+    uint64_t serial = 0;
     std::string in;
     std::string out;
     size_t out_off = 0;
@@ -308,6 +340,10 @@ void GrpcServer::start() {
     ev2.events = EPOLLIN;
     ev2.data.fd = w->efd;
     epoll_ctl(w->ep, EPOLL_CTL_ADD, w->efd, &ev2);
+    struct epoll_event ev3 {};
+    ev3.events = EPOLLIN;
+    ev3.data.fd = w->done->efd;
+    epoll_ctl(w->ep, EPOLL_CTL_ADD, w->done->efd, &ev3);
     workers_.push_back(std::move(w));
   }
   for (auto& w : workers_) threads_.emplace_back([this, wp = w.get()] { run(wp); });
@@ -451,9 +487,25 @@ void GrpcServer::run(Worker* w) {
           rpc = kRpcOptions;
           out = table->options_bytes();
           break;
-        case kMPreStart:
+        case kMPreStart: {
           rpc = kRpcPreStart;
-          break;
+          if (!table->config().pre_start_required) break;  // reference behaviour: empty OK
+          // answered when the verifier completes the job (see the done-queue below)
+          auto q = w->done;
+          const int fd = c.fd;
+          const uint64_t serial = c.serial;
+          std::string err;
+          if (!table->submit_prestart(
+                  msg,
+                  [q, fd, serial, sid, t0](bool pass, const std::string& e) {
+                    q->post({fd, serial, sid, pass, e, t0});
+                  },
+                  &err)) {
+            send_error(c, sid, s, 2, err);
+            table->observe(rpc, (mono_ns() - t0) * 1e-9, true);
+          }
+          return;
+        }
         case kMLaw: {
           rpc = kRpcListAndWatch;
           s.law = true;
@@ -748,12 +800,39 @@ void GrpcServer::run(Worker* w) {
         law_tick = true;
         continue;
       }
+      if (fd == w->done->efd) {  // asynchronous RPCs completed: answer their streams
+        uint64_t x;
+        while (read(w->done->efd, &x, sizeof(x)) > 0) {
+        }
+        std::vector<AsyncDone::Item> items;
+        {
+          std::lock_guard<std::mutex> lk(w->done->mu);
+          items.swap(w->done->items);
+        }
+        for (auto& it : items) {
+          auto ci = w->conns.find(it.fd);
+          if (ci == w->conns.end() || ci->second->serial != it.serial) continue;  // client went away
+          Conn* c = ci->second.get();
+          auto si = c->streams.find(it.sid);
+          if (si == c->streams.end() || si->second.done) continue;
+          if (it.ok) {
+            send_headers(*c, it.sid);
+            send_message(*c, it.sid, si->second, std::string_view(), true);  // PreStartContainerResponse{}
+          } else {
+            send_error(*c, it.sid, si->second, 2, it.error);  // UNKNOWN, like a Go handler error
+          }
+          table->observe(kRpcPreStart, (mono_ns() - it.t0) * 1e-9, !it.ok);
+          flush(c);
+        }
+        continue;
+      }
       if (fd == listen_fd_) {
         for (;;) {
           const int cfd = accept4(listen_fd_, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
           if (cfd < 0) break;
           auto c = std::make_unique<Conn>();
           c->fd = cfd;
+          c->serial = w->next_serial++;
           // server preface: SETTINGS(MAX_CONCURRENT_STREAMS, INITIAL_WINDOW_SIZE) + conn window
           frame(&c->out, 12, kSettings, 0, 0);
           c->out.push_back(0);

@@ -300,3 +300,29 @@ def test_amdsmi_reinit_keeps_inventory_and_events():
     print("reinit", r)
     assert r["reinit"] and r["count"] == 1 and r["same"] and r["sample_ok"]
     assert r["armed_after"] == r["armed_before"]
+
+
+def test_prestart_canary_on_allocated_partition(make_cfg, plugin_dir):
+    """health.canaryOnPreStart on the real GPU: PreStartContainer runs the gfx950 canary
+    (child process) on the allocated partition and passes; the device stays Healthy."""
+    from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import KubeletStub
+    from k8s_gpu_device_plugin_amd.plugin.manager import PluginManager
+    cfg = make_cfg(backend="amdsmi", migStrategy="single", health={"canaryOnPreStart": True,
+                                                                   "canaryBytes": 256 << 20})
+    k = KubeletStub(plugin_dir).start()
+    mgr = PluginManager(cfg)
+    t = mgr.start_background()
+    try:
+        reg = k.wait_for_registrations(1, 20)[0]
+        assert reg.options.pre_start_required
+        ids = mgr.plugins[0].table.ids()
+        t0 = time.monotonic()
+        k.client(reg.endpoint).pre_start(ids[:1], timeout=60)
+        dt = time.monotonic() - t0
+        print("PreStartContainer with canary: %.2f s" % dt)
+        assert mgr.counters.get("canary_runs", 0) >= 1 and not mgr.counters.get("prestart_failures")
+        assert mgr.plugins[0].table.healthy(ids[0]) and dt < 30
+    finally:
+        mgr.stop()
+        t.join(10)
+        k.stop()
