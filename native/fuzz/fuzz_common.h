@@ -32,7 +32,7 @@ using namespace amdgpu_dp;
 // A CPX-style node: `ngpu` GPUs x `nparts` partitions, full xGMI mesh with one link
 // down, two NUMA nodes, plus every device advertised with `replicas` "::k" replicas
 // when replicas > 0 (exercises the distributed policy).
-inline std::shared_ptr<DeviceTable> make_table(int ngpu, int nparts, int replicas = 0) {
+inline std::shared_ptr<DeviceTable> make_table(int ngpu, int nparts, int replicas = 0, bool pre_start = false) {
   std::vector<TableDevice> devs;
   for (int g = 0; g < ngpu; ++g)
     for (int p = 0; p < nparts; ++p) {
@@ -63,6 +63,7 @@ inline std::shared_ptr<DeviceTable> make_table(int ngpu, int nparts, int replica
       }
   TableConfig cfg;
   cfg.reject_unhealthy = true;
+  cfg.pre_start_required = pre_start;
   return std::make_shared<DeviceTable>(cfg, devs, topo);
 }
 

@@ -6,6 +6,11 @@
 // server closes it.  Every 256 inputs a well-formed Allocate on a fresh connection
 // must still succeed, so a wedged worker, a leaked stream state or a server that stops
 // closing connections is a finding, not just a crash.
+//
+// The table has pre_start_required set and a verifier thread completes PreStartContainer
+// jobs (pass, fail, or after a short delay, in turn), so the asynchronous completion
+// path - answers arriving after the client reset the stream, closed the connection, or
+// after the fd number was reused - is fuzzed too.
 #include <poll.h>
 #include <sys/socket.h>
 #include <sys/un.h>
@@ -17,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 
 #include "fuzz_common.h"
 #include "grpc_h2.h"
@@ -47,6 +53,18 @@ void check_fds() {
 }
 
 std::unique_ptr<GrpcServer> g_srv;
+std::shared_ptr<DeviceTable> g_table;
+
+void verifier() {  // runs for the whole fuzzing session
+  uint64_t n = 0;
+  for (;;) {
+    for (auto& job : g_table->pop_prestart(50)) {
+      ++n;
+      if (n % 3 == 2) std::this_thread::sleep_for(std::chrono::milliseconds(2));
+      g_table->complete_prestart(job.id, n % 3 != 1, n % 3 == 1 ? "injected canary failure" : "");
+    }
+  }
+}
 std::string g_path;
 uint64_t g_iter = 0;
 
@@ -121,6 +139,13 @@ extern "C" int LLVMFuzzerInitialize(int*, char***) {
     fuzzutil::h2_frame(&cont, 0x0, 0x9, 5, std::string("\x02", 1) + fuzzutil::grpc_body("") + "pp");
     fuzzutil::h2_frame(&cont, 0x3, 0, 5, std::string(4, '\0'));
     fuzzutil::write_seed(dir, "continuation_padded", cont);
+    // PreStartContainer answered asynchronously, interleaved with an Allocate and a reset
+    std::string pre = h2_call(1, "/v1beta1.DevicePlugin/PreStartContainer",
+                              fuzzutil::alloc_req({{"gpu4-xcp1", "gpu4-xcp2"}}).substr(2)) +
+                      h2_call(3, "/v1beta1.DevicePlugin/Allocate", fuzzutil::alloc_req({{"gpu0-xcp0"}})) +
+                      h2_call(5, "/v1beta1.DevicePlugin/PreStartContainer", "");
+    fuzzutil::h2_frame(&pre, 0x3, 0, 5, std::string(4, '\0'));
+    fuzzutil::write_seed(dir, "prestart_async", pre);
     std::exit(0);
   }
   char tmpl[] = "/tmp/fuzz-grpc-XXXXXX";
@@ -128,8 +153,10 @@ extern "C" int LLVMFuzzerInitialize(int*, char***) {
   if (!dir) std::abort();
   g_path = std::string(dir) + "/plugin.sock";
   g_srv = std::make_unique<GrpcServer>(g_path, 2);
-  g_srv->set_table(fuzzutil::make_table(8, 8));
+  g_table = fuzzutil::make_table(8, 8, 0, true);
+  g_srv->set_table(g_table);
   g_srv->start();
+  std::thread(verifier).detach();
   liveness_check();
   return 0;
 }
