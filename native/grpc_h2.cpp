@@ -1124,6 +1124,12 @@ int H2Client::unary(std::string_view path, std::string_view req, std::string* re
   return status;
 }
 
+void H2Client::send_unary_nowait(std::string_view path, std::string_view req) {
+  const uint32_t sid = next_sid_;
+  next_sid_ += 2;
+  send_request(sid, path, req);
+}
+
 int H2Client::first_stream_message(std::string_view path, std::string_view req, std::string* resp) {
   const uint32_t sid = next_sid_;
   next_sid_ += 2;

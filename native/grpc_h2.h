@@ -72,6 +72,8 @@ class H2Client {
   ~H2Client();
   // Unary call. Returns the grpc-status (0 = OK), response message in *resp.
   int unary(std::string_view path, std::string_view req, std::string* resp, std::string* message);
+  // Sends a unary request without waiting for the answer (tests: calls in flight).
+  void send_unary_nowait(std::string_view path, std::string_view req);
   // Opens a server stream and returns its first message (ListAndWatch probe).
   int first_stream_message(std::string_view path, std::string_view req, std::string* resp);
   // A long-lived server stream (a kubelet-like ListAndWatch watcher): open it, then

@@ -192,6 +192,77 @@ static void test_grpc_server(std::shared_ptr<FixtureBackend> be, const std::stri
   srv.stop();
 }
 
+// PreStartContainer answered asynchronously: a verifier thread completes jobs while
+// clients call, some clients disconnect with checks in flight, and the server stops
+// with jobs still queued (their completions must land in a queue that outlives it).
+static void test_prestart_async(const std::string& dir) {
+  TableConfig tc;
+  tc.pre_start_required = true;
+  std::vector<TableDevice> devs;
+  for (int i = 0; i < 4; ++i) {
+    TableDevice d;
+    d.id = "dev" + std::to_string(i);
+    d.gpu = i;
+    devs.push_back(d);
+  }
+  Topology topo;
+  topo.resize(4);
+  auto table = std::make_shared<DeviceTable>(tc, devs, topo);
+  const std::string path = dir + "/prestart.sock";
+  auto srv = std::make_unique<GrpcServer>(path, 2);
+  srv->set_table(table);
+  srv->start();
+  std::atomic<bool> stop{false};
+  std::atomic<int> completed{0};
+  std::thread verifier([&] {
+    uint64_t n = 0;
+    while (!stop.load())
+      for (auto& j : table->pop_prestart(20)) {
+        if (++n % 4 == 0) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        table->complete_prestart(j.id, n % 5 != 0, n % 5 ? "" : "injected failure");
+        ++completed;
+      }
+  });
+  std::atomic<int> errors{0}, failed{0};
+  std::vector<std::thread> ts;
+  for (int i = 0; i < 4; ++i)
+    ts.emplace_back([&, i] {
+      try {
+        for (int round = 0; round < 5; ++round) {
+          H2Client c(path);
+          std::string resp, msg;
+          std::string req;
+          pb::put_bytes(&req, 1, devs[i].id);
+          for (int k = 0; k < 20; ++k) {
+            const int st = c.unary("/v1beta1.DevicePlugin/PreStartContainer", req, &resp, &msg);
+            if (st == 2) ++failed;
+            else if (st != 0) ++errors;
+          }
+          if (round % 2) c.close();  // next round reconnects (fd numbers get reused)
+        }
+      } catch (const std::exception& e) {
+        std::fprintf(stderr, "prestart client error: %s\n", e.what());
+        ++errors;
+      }
+    });
+  for (auto& t : ts) t.join();
+  CHECK(errors.load() == 0);
+  CHECK(failed.load() > 0 && failed.load() < 400);
+  // jobs left queued at stop: the server goes away, completions still find their queue
+  {
+    H2Client c(path);
+    std::string req;
+    pb::put_bytes(&req, 1, devs[0].id);
+    c.send_unary_nowait("/v1beta1.DevicePlugin/PreStartContainer", req);
+  }
+  srv->stop();
+  srv.reset();
+  stop.store(true);
+  verifier.join();
+  table->cancel_prestart("stopping");
+  CHECK(table->prestart_pending() == 0);
+}
+
 static void test_exporter_httpd_health(std::shared_ptr<FixtureBackend> be) {
   std::vector<GpuInfo> gpus;
   Topology topo;
@@ -380,6 +451,8 @@ int main() {
   test_allocator_and_table(be);
   std::fprintf(stderr, "[selftest] grpc server\n");
   test_grpc_server(make_node(4, 1), dir);
+  std::fprintf(stderr, "[selftest] prestart async\n");
+  test_prestart_async(dir);
   std::fprintf(stderr, "[selftest] exporter + httpd + health\n");
   test_exporter_httpd_health(make_node(2, 1));
   std::fprintf(stderr, "[selftest] reload races\n");
