@@ -340,22 +340,22 @@ int HttpServer::start() {
               const bool http10 = proto == "HTTP/1.0";
               const bool keep = !chunked && !method.empty() && (http10 ? conn_keep : !conn_close);
               const int64_t t0 = mono_ns();
-              std::string o;
               int status = 0;
               size_t body_bytes = 0;
+              // responses are appended straight to the connection's output buffer (its
+              // capacity is reused across requests): no per-request copy of the body
               if (method.empty() || chunked) {
                 status = method.empty() ? 400 : 501;
-                handle("", "", origin, false, http10, &o, &status, &body_bytes);
+                handle("", "", origin, false, http10, &c->out, &status, &body_bytes);
               } else {
                 const size_t qm = uri.find('?');
-                handle(method, qm == std::string::npos ? uri : uri.substr(0, qm), origin, keep, http10, &o, &status,
-                       &body_bytes, gzip_ok);
+                handle(method, qm == std::string::npos ? uri : uri.substr(0, qm), origin, keep, http10, &c->out,
+                       &status, &body_bytes, gzip_ok);
               }
               const double dt = (mono_ns() - t0) * 1e-9;
               requests_.fetch_add(1, std::memory_order_relaxed);
               if (cfg_.access_log && method != "OPTIONS" && !method.empty())
                 log_access(c->remote, hosth, method, uri, ua, status, dt, content_len, body_bytes);
-              c->out.append(o);
               pos = body_start + content_len;
               if (!keep) c->close_after = true;
             }
@@ -417,11 +417,16 @@ void HttpServer::handle(const std::string& method, const std::string& path, cons
                         bool gzip_ok) {
   const int64_t t0 = mono_ns();
   int status = 200;
-  std::string body;
+  static thread_local std::string body_buf;  // per worker thread, capacity reused
+  std::string& body = body_buf;
+  body.clear();
   const char* ctype = "application/json";
   int handler = -1;
   const bool cors = true;
   bool gz = false;
+  // plain /metrics: the exposition's segments are appended after the header, each once
+  Exposition expo;
+  bool have_expo = false;
   if (method.empty()) {
     status = *status_out ? *status_out : 400;
     body = std::string("{\"message\":\"") + reason(status) + "\"}\n";
@@ -461,9 +466,11 @@ void HttpServer::handle(const std::string& method, const std::string& path, cons
         if (exporter_) exporter_->render_gzip(&body, httpm);
         else gzip_member(httpm.data(), httpm.size(), &body);
         gz = true;
+      } else if (exporter_) {
+        exporter_->render(&expo);
+        have_expo = true;
+        render_http_metrics(&body);  // small; follows the exposition
       } else {
-        body.reserve(64 * 1024);
-        if (exporter_) exporter_->render(&body);
         render_http_metrics(&body);
       }
     }
@@ -474,6 +481,7 @@ void HttpServer::handle(const std::string& method, const std::string& path, cons
     body = "{\"message\":\"Internal Server Error\"}\n";
     ctype = "application/json";
     gz = false;
+    have_expo = false;
     std::fprintf(stderr, "httpd: handler for %s %s failed: %s\n", method.c_str(), path.c_str(), e.what());
     if (handler >= 0) record(method_index(method), handler, status, (mono_ns() - t0) * 1e-9);
   }
@@ -484,8 +492,9 @@ void HttpServer::handle(const std::string& method, const std::string& path, cons
     date = http_date();
     date_ns = now;
   }
+  const size_t body_len = body.size() + (have_expo ? expo.size() : 0);
   std::string& o = *out;
-  o.reserve(o.size() + body.size() + 512);
+  o.reserve(o.size() + body_len + 512);
   o.append(http10 ? "HTTP/1.0 " : "HTTP/1.1 ").append(std::to_string(status)).append(" ").append(reason(status)).append("\r\n");
   if (cors) {  // server/server.go:77-96
     o.append("Access-Control-Allow-Credentials: true\r\n");
@@ -496,14 +505,15 @@ void HttpServer::handle(const std::string& method, const std::string& path, cons
   if (!keep_alive) o.append("Connection: close\r\n");
   else if (http10) o.append("Connection: keep-alive\r\n");
   if (gz) o.append("Content-Encoding: gzip\r\n");
-  o.append("Content-Length: ").append(std::to_string(body.size())).append("\r\n");
+  o.append("Content-Length: ").append(std::to_string(body_len)).append("\r\n");
   o.append("Content-Type: ").append(ctype).append("\r\n");
   o.append("Date: ").append(date).append("\r\n");
   if (handler == 1) o.append("Vary: Accept-Encoding\r\n");
   o.append("\r\n");
+  if (have_expo) expo.append_to(&o);
   o.append(body);
   *status_out = status;
-  *body_bytes_out = body.size();
+  *body_bytes_out = body_len;
 }
 
 void HttpServer::render_http_metrics(std::string* out) const {

@@ -547,13 +547,12 @@ void Exporter::render_parts(std::shared_ptr<const std::string>* head, std::strin
 }
 
 void Exporter::render(std::string* out) const {
-  std::shared_ptr<const std::string> head, health;
-  std::string counters, tail;
-  render_parts(&head, &counters, &health, &tail);
-  out->append(*head).append(counters);
-  if (health) out->append(*health);
-  out->append(tail);
+  Exposition e;
+  render(&e);
+  e.append_to(out);
 }
+
+void Exporter::render(Exposition* e) const { render_parts(&e->head, &e->counters, &e->health, &e->tail); }
 
 void Exporter::render_gzip(std::string* out, std::string_view trailer) const {
   std::shared_ptr<const std::string> head, health;

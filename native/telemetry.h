@@ -27,6 +27,21 @@ namespace amdgpu_dp {
 // form a valid multi-member gzip stream (Go's gzip.Reader, Python's gzip, curl).
 void gzip_member(const char* data, size_t n, std::string* out, int level = 1);
 
+// One /metrics exposition as its segments: the per-tick inventory/GPU text and the
+// per-version device-health block are shared snapshots, the rest is rendered per
+// scrape.  Its size is known before any byte is copied, so a server can write the
+// response header and then append each segment once.
+struct Exposition {
+  std::shared_ptr<const std::string> head, health;
+  std::string counters, tail;
+  size_t size() const { return head->size() + counters.size() + (health ? health->size() : 0) + tail.size(); }
+  void append_to(std::string* out) const {
+    out->append(*head).append(counters);
+    if (health) out->append(*health);
+    out->append(tail);
+  }
+};
+
 struct PartitionLabel {
   int gpu = -1;
   int partition = -1;
@@ -56,6 +71,7 @@ class Exporter {
   GpuSample last_sample(int gpu) const;
   // Full exposition (everything except the HTTP server's own echo_http_* families).
   void render(std::string* out) const;
+  void render(Exposition* e) const;
   // Same exposition + `trailer` (the HTTP server's families) as a multi-member gzip
   // stream.  The inventory/GPU-text member is compressed once per sampling tick and
   // the device-health member once per table version; only the small per-scrape parts
