@@ -228,7 +228,9 @@ def config4():
                 "list_and_watch_first_message": {"p50_us": us(pct(law, 0.5)), "p99_us": us(pct(law, 0.99))},
                 "allocate": rpc_latency(node, v1beta1.METHOD_ALLOCATE, alloc_req(ids[9:10])),
                 "preferred_size8_whole_gpu_pack": rpc_latency(node, v1beta1.METHOD_GET_PREFERRED,
-                                                              pref_req(ids, [], 8), 2000, 0)}
+                                                              pref_req(ids, [], 8), 2000, 0),
+                "preferred_size16_two_gpus": rpc_latency(node, v1beta1.METHOD_GET_PREFERRED,
+                                                         pref_req(ids, [], 16), 1000, 0)}
     finally:
         node.close()
 

@@ -156,3 +156,28 @@ def test_table_switches_policy_on_annotations(n):
     assert t2.aligned_supported
     t2.set_link_up(0, 1, False)
     assert t2.preferred_ids(t2.ids()[:3], [], 2) != t2.ids()[:2]
+
+
+def test_large_cpx_requests_pack_whole_gpus_fast(n):
+    """Requests larger than one GPU's partitions on a CPX node take the greedy path:
+    whole GPUs first, the remainder on one more GPU of the same NUMA node, never spread
+    thin - and quickly (each step scores one device per (gpu, numa) class)."""
+    import time
+    from collections import Counter
+    topo = n.Topology(8)
+    for a in range(8):
+        for b in range(a + 1, 8):
+            topo.set_link(a, b, n.Link(type=n.LINK_XGMI, hops=1, up=True))
+    devs = [n.AllocDevice(g, p, g // 4, "g%dp%d" % (g, p)) for g in range(8) for p in range(8)]
+    cases = [(12, list(range(64)), {8, 4}), (16, list(range(64)), {8}), (12, list(range(4, 64)), {8, 4}),
+             (24, list(range(64)), {8})]
+    for size, avail, shape in cases:
+        t0 = time.perf_counter()
+        chosen = n.aligned_alloc(topo, devs, avail, [], size)
+        dt = time.perf_counter() - t0
+        per_gpu = Counter(c // 8 for c in chosen)
+        assert len(chosen) == size and set(chosen) <= set(avail)
+        assert set(per_gpu.values()) == shape, (size, per_gpu)
+        if size <= 16:
+            assert len({g // 4 for g in per_gpu}) == 1, per_gpu  # one NUMA node
+        assert dt < 0.02, dt
