@@ -292,7 +292,8 @@ def main() -> int:
             "metrics_bytes": gathered[0]["body"],
             "canary": ({"arch": can[0]["arch"], "hbm_read_gbps": round(min(c["read_gbps"] for c in can), 1),
                         "hbm_write_gbps": round(min(c["write_gbps"] for c in can), 1),
-                        "mfma_bf16_tflops": round(min(c["mfma_tflops"] for c in can), 1)} if can else None),
+                        "mfma_bf16_tflops": round(min(c["mfma_tflops"] for c in can), 1),
+                        "lds_gemm_bf16_tflops": round(min(c["gemm_tflops"] for c in can), 1)} if can else None),
         }
         print(json.dumps(out), flush=True)
     client.close()

@@ -152,6 +152,145 @@ __global__ void __launch_bounds__(64) mfma_gemm(const short* __restrict__ A, con
   }
 }
 
+// ---- LDS-staged MFMA GEMM: the matrix path a real workload takes --------------------
+// C[MxN] (fp32) = A[MxK] * B, A row-major bf16, B given transposed (Bt[NxK] row-major,
+// so both operands are K-contiguous).  A 128x128 block tile, BK = 64, 4 waves as 2x2,
+// each wave 64x64 = 2x2 v_mfma_f32_32x32x16_bf16 tiles (64 accumulator registers).
+// Operands stream HBM -> LDS with global_load_lds (16 B per lane, no VGPR round trip),
+// double-buffered so tile t+1 lands while tile t is multiplied; fragments come out of
+// LDS with one ds_read_b128 per operand per k-step.  Blocks are remapped XCD-aware so
+// the tiles that share A rows share an XCD's L2.  Integer-valued operands make every
+// result exact, so an ABFT row/column checksum (below) verifies the whole path - HBM,
+// L2, the LDS DMA, LDS reads and the matrix cores - not just the MFMA unit.
+constexpr int kTileM = 128, kTileN = 128, kTileK = 64;
+constexpr int kTileBytes = kTileM * kTileK * 2;  // one operand tile, 16 KiB
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {  // bijective for any nwg
+  const int xcd = orig % 8, q = nwg / 8, r = nwg % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+__global__ void __launch_bounds__(256) gemm_lds(const short* __restrict__ A, const short* __restrict__ Bt,
+                                               float* __restrict__ C, int M, int N, int K) {
+  // one __shared__ array for everything (a second object can de-pipeline glds waits)
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * kTileBytes];  // [buf][A|B][128][64] bf16
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nbn = N / kTileN;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (wg / nbn) * kTileM, n0 = (wg % nbn) * kTileN;
+  if (m0 + kTileM > M || n0 + kTileN > N) return;  // host checks shapes
+  const int wr = wave >> 1, wc = wave & 1;
+  const int r = lane & 31, h = lane >> 5;
+
+  // staging: wave w issues 4 x 1 KiB per operand = rows (4w+i)*8 .. +7; lane l lands at
+  // physical 16 B chunk l&7 of row l>>3.  LDS rows are 128 B, so the 32 lanes reading
+  // one fragment column would hit 2 bank groups (8-way conflict); the image is swizzled
+  // as physical chunk = logical chunk ^ (row & 7), done on the per-lane global source
+  // address (the glds destination must stay lane-linear): 2-way instead.
+  auto stage = [&](int t, int buf) {
+    const int k0 = t * kTileK;
+    char* base = smem + buf * 2 * kTileBytes;
+    for (int i = 0; i < 4; ++i) {
+      const int row = (wave * 4 + i) * 8 + (lane >> 3), kc = ((lane & 7) ^ ((lane >> 3) & 7)) * 8;
+      __builtin_amdgcn_global_load_lds(A + static_cast<size_t>(m0 + row) * K + k0 + kc,
+                                       (lds_void_ptr)(base + (wave * 4 + i) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(Bt + static_cast<size_t>(n0 + row) * K + k0 + kc,
+                                       (lds_void_ptr)(base + kTileBytes + (wave * 4 + i) * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x16 acc[2][2];
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j)
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int T = K / kTileK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < T; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < T) stage(t + 1, cur ^ 1);
+    const short* As = reinterpret_cast<const short*>(smem + cur * 2 * kTileBytes);
+    const short* Bs = As + kTileM * kTileK;
+#pragma unroll
+    for (int kk = 0; kk < kTileK / 16; ++kk) {
+      const int chunk = 2 * kk + h;  // logical 16 B chunk of this lane's 8 k values
+      bf16x8 a[2], b[2];
+      for (int i = 0; i < 2; ++i) {
+        const int row = wr * 64 + i * 32 + r;
+        a[i] = *reinterpret_cast<const bf16x8*>(As + row * kTileK + ((chunk ^ (row & 7)) << 3));
+      }
+      for (int j = 0; j < 2; ++j) {
+        const int row = wc * 64 + j * 32 + r;
+        b[j] = *reinterpret_cast<const bf16x8*>(Bs + row * kTileK + ((chunk ^ (row & 7)) << 3));
+      }
+      for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 has landed
+    __syncthreads();                                   // ... and nobody still reads tile t's buffer
+  }
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j)
+      for (int e = 0; e < 16; ++e) {
+        const int row = m0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        C[static_cast<size_t>(row) * N + n0 + wc * 64 + j * 32 + r] = acc[i][j][e];
+      }
+}
+
+// Integer operands in [-4, 4] (exact in bf16): element (i, k) of operand `which`.
+__global__ void __launch_bounds__(256) gemm_fill(short* __restrict__ X, int rows, int K, uint32_t which) {
+  const size_t n = static_cast<size_t>(rows) * K;
+  for (size_t e = blockIdx.x * 256ull + threadIdx.x; e < n; e += static_cast<size_t>(gridDim.x) * 256)
+    X[e] = bf16_of_int(small_int((static_cast<uint64_t>(which) << 56) ^ e));
+}
+
+__device__ __forceinline__ int bf16_to_int(short v) {
+  const uint32_t u = static_cast<uint32_t>(static_cast<uint16_t>(v)) << 16;
+  float f;
+  __builtin_memcpy(&f, &u, 4);
+  return static_cast<int>(f);
+}
+
+// colsum[k] = sum over rows of X[row][k] (threads over k: coalesced)
+__global__ void __launch_bounds__(256) gemm_colsum(const short* __restrict__ X, int rows, int K,
+                                                   long long* __restrict__ out) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= K) return;
+  long long s = 0;
+  for (int i = 0; i < rows; ++i) s += bf16_to_int(X[static_cast<size_t>(i) * K + k]);
+  out[k] = s;
+}
+
+// ABFT: for row i, sum_n C[i][n] must equal sum_k A[i][k] * (sum_n Bt[n][k]); for column
+// n, sum_m C[m][n] must equal sum_k (sum_m A[m][k]) * Bt[n][k].  One block per row /
+// column, int64 reductions (C holds exact integers).  mode 0 = rows, 1 = columns.
+__global__ void __launch_bounds__(256) gemm_abft(const short* __restrict__ X, const float* __restrict__ C,
+                                                 const long long* __restrict__ other_sum, int M, int N, int K,
+                                                 int mode, unsigned long long* __restrict__ errors) {
+  __shared__ long long red[2][256];
+  const int idx = blockIdx.x, tid = threadIdx.x;
+  long long expect = 0, got = 0;
+  for (int k = tid; k < K; k += 256) expect += static_cast<long long>(bf16_to_int(X[static_cast<size_t>(idx) * K + k])) * other_sum[k];
+  if (mode == 0)
+    for (int n = tid; n < N; n += 256) got += static_cast<long long>(C[static_cast<size_t>(idx) * N + n]);
+  else
+    for (int m = tid; m < M; m += 256) got += static_cast<long long>(C[static_cast<size_t>(m) * N + idx]);
+  red[0][tid] = expect;
+  red[1][tid] = got;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) {
+      red[0][tid] += red[0][tid + s];
+      red[1][tid] += red[1][tid + s];
+    }
+    __syncthreads();
+  }
+  if (tid == 0 && red[0][0] != red[1][0]) atomicAdd(errors, 1ull);
+}
+
 // ---- HBM access-shape sweep (used to pick the canary's streaming shape on gfx950) ----
 // UNROLL independent 16 B accesses in flight per lane; NT = non-temporal (streaming)
 // loads/stores; CHUNKED = each block streams one contiguous chunk instead of a
@@ -280,6 +419,8 @@ struct amdgpu_canary_result {
   int num_cus;
   char arch[64];
   char error[256];
+  double gemm_tflops;                   // LDS-staged MFMA GEMM (matrix path) rate
+  unsigned long long gemm_errors;       // ABFT row/column checksum mismatches
 };
 
 int amdgpu_canary_device_count() {
@@ -287,6 +428,9 @@ int amdgpu_canary_device_count() {
   if (hipGetDeviceCount(&n) != hipSuccess) return -1;
   return n;
 }
+
+int amdgpu_canary_gemm_rate(int device, int M, int N, int K, int iters, int inject, double* tflops,
+                            unsigned long long* errors, char* err, int err_len);
 
 #define CANARY_CHECK(expr)                                                                   \
   do {                                                                                       \
@@ -366,7 +510,15 @@ int amdgpu_canary_run(int device, unsigned long long hbm_bytes, int passes, int 
     out->mfma_tflops = flops / (t_mfma * 1e-3) / 1e12;
   }
   out->elapsed_ms = t_write + t_read + t_mfma;
-  out->ok = (out->hbm_errors == 0 && out->mfma_errors == 0) ? 1 : 0;
+  // matrix path: HBM -> L2 -> LDS DMA -> ds_read -> MFMA, exact and checksummed.  2048^3
+  // keeps it short; hbm_bytes < 256 MiB (fault-injection runs) uses 1024^3.
+  {
+    const int g = hbm_bytes >= (256ull << 20) ? 2048 : 1024;
+    if (amdgpu_canary_gemm_rate(device, g, g, g, 4, 0, &out->gemm_tflops, &out->gemm_errors, out->error,
+                                sizeof(out->error)) != 0)
+      goto done;
+  }
+  out->ok = (out->hbm_errors == 0 && out->mfma_errors == 0 && out->gemm_errors == 0) ? 1 : 0;
 done:
   if (e0) (void)hipEventDestroy(e0);
   if (e1) (void)hipEventDestroy(e1);
@@ -460,6 +612,103 @@ int amdgpu_canary_mfma_gemm(int device, const unsigned short* a_host, const unsi
   if (a) (void)hipFree(a);
   if (b) (void)hipFree(b);
   if (c) (void)hipFree(c);
+  return e == hipSuccess ? 0 : -1;
+}
+
+// LDS-staged GEMM on host data (numerics test): A [MxK], Bt [NxK] bf16 row-major.
+int amdgpu_canary_gemm(int device, const unsigned short* a_host, const unsigned short* bt_host, float* c_host, int M,
+                       int N, int K, char* err, int err_len) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % kTileM || N % kTileN || K % kTileK) {
+    std::snprintf(err, err_len, "shape (%d,%d,%d) must be M,N %% 128 == 0 and K %% 64 == 0", M, N, K);
+    return -1;
+  }
+  short *a = nullptr, *b = nullptr;
+  float* c = nullptr;
+  hipError_t e = hipSetDevice(device);
+  const size_t sa = static_cast<size_t>(M) * K * 2, sb = static_cast<size_t>(N) * K * 2,
+               sc = static_cast<size_t>(M) * N * 4;
+  if (e == hipSuccess) e = hipMalloc(&a, sa);
+  if (e == hipSuccess) e = hipMalloc(&b, sb);
+  if (e == hipSuccess) e = hipMalloc(&c, sc);
+  if (e == hipSuccess) e = hipMemcpy(a, a_host, sa, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(b, bt_host, sb, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(gemm_lds, dim3((M / kTileM) * (N / kTileN)), dim3(256), 0, 0, a, b, c, M, N, K);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(c_host, c, sc, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) std::snprintf(err, err_len, "%s", hipGetErrorString(e));
+  if (a) (void)hipFree(a);
+  if (b) (void)hipFree(b);
+  if (c) (void)hipFree(c);
+  return e == hipSuccess ? 0 : -1;
+}
+
+// Matrix-path canary: device-generated integer operands, `iters` timed GEMMs, then the
+// ABFT row + column checksums of the result.  *tflops = dense bf16 rate achieved,
+// *errors = rows + columns whose checksum is off (0 on a healthy partition).
+// inject != 0 corrupts one element of C before the check (verifier self-test).
+int amdgpu_canary_gemm_rate(int device, int M, int N, int K, int iters, int inject, double* tflops,
+                            unsigned long long* errors, char* err, int err_len) {
+  *tflops = 0;
+  *errors = 0;
+  if (M <= 0 || N <= 0 || K <= 0 || M % kTileM || N % kTileN || K % kTileK || K > 65536 || iters < 1) {
+    std::snprintf(err, err_len, "shape (%d,%d,%d) must be M,N %% 128 == 0, K %% 64 == 0, K <= 65536", M, N, K);
+    return -1;
+  }
+  short *a = nullptr, *b = nullptr;
+  float* c = nullptr;
+  long long *asum = nullptr, *bsum = nullptr;
+  unsigned long long* d_err = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  float ms = 0;
+  const dim3 grid((M / kTileM) * (N / kTileN));
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipMalloc(&a, static_cast<size_t>(M) * K * 2);
+  if (e == hipSuccess) e = hipMalloc(&b, static_cast<size_t>(N) * K * 2);
+  if (e == hipSuccess) e = hipMalloc(&c, static_cast<size_t>(M) * N * 4);
+  if (e == hipSuccess) e = hipMalloc(&asum, static_cast<size_t>(K) * 8);
+  if (e == hipSuccess) e = hipMalloc(&bsum, static_cast<size_t>(K) * 8);
+  if (e == hipSuccess) e = hipMalloc(&d_err, 8);
+  if (e == hipSuccess) e = hipMemset(d_err, 0, 8);
+  if (e == hipSuccess) e = hipEventCreate(&e0);
+  if (e == hipSuccess) e = hipEventCreate(&e1);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(gemm_fill, dim3(2048), dim3(256), 0, 0, a, M, K, 1u);
+    hipLaunchKernelGGL(gemm_fill, dim3(2048), dim3(256), 0, 0, b, N, K, 2u);
+    hipLaunchKernelGGL(gemm_lds, grid, dim3(256), 0, 0, a, b, c, M, N, K);  // warm-up
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipEventRecord(e0, 0);
+  for (int i = 0; e == hipSuccess && i < iters; ++i) hipLaunchKernelGGL(gemm_lds, grid, dim3(256), 0, 0, a, b, c, M, N, K);
+  if (e == hipSuccess) e = hipEventRecord(e1, 0);
+  if (e == hipSuccess) e = hipEventSynchronize(e1);
+  if (e == hipSuccess) e = hipGetLastError();
+  if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+  if (e == hipSuccess && inject) {
+    const float junk = 12345.0f;
+    e = hipMemcpy(c + static_cast<size_t>(M / 2) * N + N / 3, &junk, 4, hipMemcpyHostToDevice);
+  }
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(gemm_colsum, dim3((K + 255) / 256), dim3(256), 0, 0, a, M, K, asum);
+    hipLaunchKernelGGL(gemm_colsum, dim3((K + 255) / 256), dim3(256), 0, 0, b, N, K, bsum);
+    hipLaunchKernelGGL(gemm_abft, dim3(M), dim3(256), 0, 0, a, c, bsum, M, N, K, 0, d_err);
+    hipLaunchKernelGGL(gemm_abft, dim3(N), dim3(256), 0, 0, b, c, asum, M, N, K, 1, d_err);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(errors, d_err, 8, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && ms > 0) *tflops = 2.0 * M * N * K * iters / (ms * 1e-3) / 1e12;
+  if (e != hipSuccess) std::snprintf(err, err_len, "%s", hipGetErrorString(e));
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (d_err) (void)hipFree(d_err);
+  if (bsum) (void)hipFree(bsum);
+  if (asum) (void)hipFree(asum);
+  if (c) (void)hipFree(c);
+  if (b) (void)hipFree(b);
+  if (a) (void)hipFree(a);
   return e == hipSuccess ? 0 : -1;
 }
 

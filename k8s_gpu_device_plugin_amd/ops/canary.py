@@ -1,8 +1,9 @@
 """Python face of the gfx950 health canary (``ops/canary.hip``).
 
 ``run(device)`` loads ``libamdgpu_canary.so`` with ctypes (no torch needed) and runs
-the HBM pattern test + MFMA exactness/throughput probe on one HIP device (= one
-compute partition).  ``run_isolated(device)`` does the same in a child process so the
+the HBM pattern test, the MFMA exactness/throughput probe and the matrix-path check
+(an LDS-staged MFMA GEMM on exact integer data with ABFT row/column checksums) on one
+HIP device (= one compute partition).  ``run_isolated(device)`` does the same in a child process so the
 long-lived plugin daemon never creates a HIP context on GPUs it hands to pods.
 
 CLI: ``python -m k8s_gpu_device_plugin_amd.ops.canary --device 0 [--bytes N]`` prints
@@ -25,7 +26,8 @@ class CanaryResult(ctypes.Structure):
                 ("hbm_errors", ctypes.c_ulonglong), ("mfma_errors", ctypes.c_ulonglong),
                 ("write_gbps", ctypes.c_double), ("read_gbps", ctypes.c_double), ("mfma_tflops", ctypes.c_double),
                 ("elapsed_ms", ctypes.c_double), ("num_cus", ctypes.c_int), ("arch", ctypes.c_char * 64),
-                ("error", ctypes.c_char * 256)]
+                ("error", ctypes.c_char * 256), ("gemm_tflops", ctypes.c_double),
+                ("gemm_errors", ctypes.c_ulonglong)]
 
 
 _lib = None
@@ -54,6 +56,13 @@ def load():
                                                 ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                                 ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_ulonglong)]
         lib.amdgpu_canary_hbm_sweep.restype = ctypes.c_int
+        lib.amdgpu_canary_gemm.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        lib.amdgpu_canary_gemm.restype = ctypes.c_int
+        lib.amdgpu_canary_gemm_rate.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                                ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_char_p, ctypes.c_int]
+        lib.amdgpu_canary_gemm_rate.restype = ctypes.c_int
         _lib = lib
     return _lib
 
@@ -117,6 +126,38 @@ def mfma_gemm(a_bf16_bits, b_bf16_bits, device: int = 0):
     if rc != 0:
         raise RuntimeError("mfma_gemm failed: " + err.value.decode(errors="replace"))
     return c
+
+
+def gemm(a_bf16_bits, bt_bf16_bits, device: int = 0):
+    """C = A @ Bt.T through the LDS-staged MFMA GEMM (the canary's matrix path).
+    ``a``: uint16 [M, K] bf16 bit patterns, ``bt``: uint16 [N, K] (B transposed, K
+    contiguous); M, N % 128 == 0, K % 64 == 0.  Returns float32 [M, N]."""
+    import numpy as np
+
+    a = np.ascontiguousarray(a_bf16_bits, dtype=np.uint16)
+    bt = np.ascontiguousarray(bt_bf16_bits, dtype=np.uint16)
+    (m, k), (nn, k2) = a.shape, bt.shape
+    if k != k2:
+        raise ValueError("inner dimensions differ: %d vs %d" % (k, k2))
+    c = np.empty((m, nn), dtype=np.float32)
+    err = ctypes.create_string_buffer(256)
+    rc = load().amdgpu_canary_gemm(int(device), a.ctypes.data, bt.ctypes.data, c.ctypes.data, m, nn, k, err, 256)
+    if rc != 0:
+        raise RuntimeError("gemm failed: " + err.value.decode(errors="replace"))
+    return c
+
+
+def gemm_rate(device: int = 0, m: int = 4096, n: int = 4096, k: int = 4096, iters: int = 10,
+              inject: bool = False) -> dict:
+    """Matrix-path canary: timed LDS-staged MFMA GEMMs on exact integer data, then ABFT
+    row/column checksums.  ``errors`` counts rows + columns whose checksum is off."""
+    t, e = ctypes.c_double(), ctypes.c_ulonglong()
+    err = ctypes.create_string_buffer(256)
+    rc = load().amdgpu_canary_gemm_rate(int(device), m, n, k, iters, int(bool(inject)), ctypes.byref(t),
+                                        ctypes.byref(e), err, 256)
+    if rc != 0:
+        raise RuntimeError("gemm_rate failed: " + err.value.decode(errors="replace"))
+    return {"tflops": t.value, "errors": e.value, "shape": (m, n, k), "iters": iters}
 
 
 def run_isolated(device: int, hbm_bytes: int = 256 << 20, timeout: float = 120.0) -> dict:
