@@ -184,7 +184,13 @@ def main(argv=None) -> int:
     ap.add_argument("--bytes", type=int, default=1 << 30)
     ap.add_argument("--passes", type=int, default=3)
     ap.add_argument("--mfma-iters", type=int, default=8192)
+    ap.add_argument("--gemm", type=int, default=0, help="only the matrix-path GEMM, at this M=N=K")
+    ap.add_argument("--gemm-iters", type=int, default=20)
     a = ap.parse_args(argv)
+    if a.gemm:
+        res = gemm_rate(a.device, a.gemm, a.gemm, a.gemm, a.gemm_iters)
+        print(json.dumps(res))
+        return 0 if res["errors"] == 0 else 1
     res = run(a.device, a.bytes, a.passes, a.mfma_iters)
     print(json.dumps(res))
     return 0 if res["ok"] else 1
