@@ -184,15 +184,19 @@ __global__ void __launch_bounds__(256) gemm_lds(const short* __restrict__ A, con
   const int r = lane & 31, h = lane >> 5;
 
   // staging: wave w issues 4 x 1 KiB per operand = rows (4w+i)*8 .. +7; lane l lands at
-  // physical 16 B chunk l&7 of row l>>3.  LDS rows are 128 B, so the 32 lanes reading
-  // one fragment column would hit 2 bank groups (8-way conflict); the image is swizzled
-  // as physical chunk = logical chunk ^ (row & 7), done on the per-lane global source
-  // address (the glds destination must stay lane-linear): 2-way instead.
+  // physical 16 B chunk l&7 of row l>>3.  LDS rows are 128 B, so the 16 lanes of one
+  // ds_read_b128 cycle (rows r..r+15, same k chunk) would hit 2 of the 16 bank slots of
+  // a 256 B bank row (8-way conflict).  The image is swizzled as physical chunk =
+  // logical chunk ^ ((row >> 1) & 7): row parity picks the 128 B half of the bank row
+  // and (row >> 1) & 7 the slot in it, so 16 consecutive rows cover all 16 slots
+  // (conflict-free; `chunk ^ (row & 7)` measured 2-way, SQ_LDS_BANK_CONFLICT).  The
+  // swizzle is applied on the per-lane global source address, since the glds
+  // destination must stay lane-linear.
   auto stage = [&](int t, int buf) {
     const int k0 = t * kTileK;
     char* base = smem + buf * 2 * kTileBytes;
     for (int i = 0; i < 4; ++i) {
-      const int row = (wave * 4 + i) * 8 + (lane >> 3), kc = ((lane & 7) ^ ((lane >> 3) & 7)) * 8;
+      const int row = (wave * 4 + i) * 8 + (lane >> 3), kc = ((lane & 7) ^ ((row >> 1) & 7)) * 8;
       __builtin_amdgcn_global_load_lds(A + static_cast<size_t>(m0 + row) * K + k0 + kc,
                                        (lds_void_ptr)(base + (wave * 4 + i) * 1024), 16, 0, 0);
       __builtin_amdgcn_global_load_lds(Bt + static_cast<size_t>(n0 + row) * K + k0 + kc,
@@ -220,11 +224,11 @@ __global__ void __launch_bounds__(256) gemm_lds(const short* __restrict__ A, con
       bf16x8 a[2], b[2];
       for (int i = 0; i < 2; ++i) {
         const int row = wr * 64 + i * 32 + r;
-        a[i] = *reinterpret_cast<const bf16x8*>(As + row * kTileK + ((chunk ^ (row & 7)) << 3));
+        a[i] = *reinterpret_cast<const bf16x8*>(As + row * kTileK + ((chunk ^ ((row >> 1) & 7)) << 3));
       }
       for (int j = 0; j < 2; ++j) {
         const int row = wc * 64 + j * 32 + r;
-        b[j] = *reinterpret_cast<const bf16x8*>(Bs + row * kTileK + ((chunk ^ (row & 7)) << 3));
+        b[j] = *reinterpret_cast<const bf16x8*>(Bs + row * kTileK + ((chunk ^ ((row >> 1) & 7)) << 3));
       }
       for (int i = 0; i < 2; ++i)
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
@@ -254,14 +258,18 @@ __device__ __forceinline__ int bf16_to_int(short v) {
   return static_cast<int>(f);
 }
 
-// colsum[k] = sum over rows of X[row][k] (threads over k: coalesced)
+// colsum[k] += sum over a 64-row slab of X[row][k]: threads over k (coalesced), blocks
+// over (k range, row slab) so the whole chip takes part; out must be zeroed.  Two's-
+// complement wrap-around makes the unsigned atomic add a signed one.
+constexpr int kSlab = 64;
 __global__ void __launch_bounds__(256) gemm_colsum(const short* __restrict__ X, int rows, int K,
                                                    long long* __restrict__ out) {
   const int k = blockIdx.x * 256 + threadIdx.x;
   if (k >= K) return;
+  const int r0 = blockIdx.y * kSlab, r1 = r0 + kSlab < rows ? r0 + kSlab : rows;
   long long s = 0;
-  for (int i = 0; i < rows; ++i) s += bf16_to_int(X[static_cast<size_t>(i) * K + k]);
-  out[k] = s;
+  for (int i = r0; i < r1; ++i) s += bf16_to_int(X[static_cast<size_t>(i) * K + k]);
+  atomicAdd(reinterpret_cast<unsigned long long*>(out + k), static_cast<unsigned long long>(s));
 }
 
 // ABFT: for row i, sum_n C[i][n] must equal sum_k A[i][k] * (sum_n Bt[n][k]); for column
@@ -691,8 +699,10 @@ int amdgpu_canary_gemm_rate(int device, int M, int N, int K, int iters, int inje
     e = hipMemcpy(c + static_cast<size_t>(M / 2) * N + N / 3, &junk, 4, hipMemcpyHostToDevice);
   }
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(gemm_colsum, dim3((K + 255) / 256), dim3(256), 0, 0, a, M, K, asum);
-    hipLaunchKernelGGL(gemm_colsum, dim3((K + 255) / 256), dim3(256), 0, 0, b, N, K, bsum);
+    e = hipMemset(asum, 0, static_cast<size_t>(K) * 8);
+    if (e == hipSuccess) e = hipMemset(bsum, 0, static_cast<size_t>(K) * 8);
+    hipLaunchKernelGGL(gemm_colsum, dim3((K + 255) / 256, (M + kSlab - 1) / kSlab), dim3(256), 0, 0, a, M, K, asum);
+    hipLaunchKernelGGL(gemm_colsum, dim3((K + 255) / 256, (N + kSlab - 1) / kSlab), dim3(256), 0, 0, b, N, K, bsum);
     hipLaunchKernelGGL(gemm_abft, dim3(M), dim3(256), 0, 0, a, c, bsum, M, N, K, 0, d_err);
     hipLaunchKernelGGL(gemm_abft, dim3(N), dim3(256), 0, 0, b, c, asum, M, N, K, 1, d_err);
     e = hipGetLastError();
