@@ -59,6 +59,9 @@ FAMILIES = (
     Family("amdgpu_xgmi_link_up", "gauge", GPU + ("link", "peer"), "exporter", "xGMI link to peer is up"),
     Family("amdgpu_xgmi_read_bytes_total", "counter", GPU + ("link", "peer"), "exporter", "xGMI bytes received"),
     Family("amdgpu_xgmi_write_bytes_total", "counter", GPU + ("link", "peer"), "exporter", "xGMI bytes sent"),
+    Family("amdgpu_xgmi_link_speed_gbps", "gauge", GPU + ("link", "peer"), "exporter",
+           "Current link speed; below amdgpu_xgmi_link_max_speed_gbps = degraded training"),
+    Family("amdgpu_xgmi_link_max_speed_gbps", "gauge", GPU + ("link", "peer"), "exporter", "Maximum link speed"),
     # --- per-partition ---
     Family("amdgpu_partition_info", "gauge", PART, "exporter", "Partition -> device id / resource (value 1)"),
     Family("amdgpu_partition_gfx_busy_percent", "gauge", PART, "exporter", "Per-XCP compute busy"),
@@ -105,6 +108,7 @@ PROMQL_EXAMPLES = (
     ("Allocate p99 over 5 minutes",
      'histogram_quantile(0.99, sum by (le) (rate(amdgpu_device_plugin_rpc_duration_seconds_bucket{rpc="Allocate"}[5m])))'),
     ("Down xGMI links", "amdgpu_xgmi_link_up == 0"),
+    ("xGMI links trained below full speed", "amdgpu_xgmi_link_speed_gbps < amdgpu_xgmi_link_max_speed_gbps"),
     ("Partition busy per workload (podResources.enabled)",
      "amdgpu_partition_gfx_busy_percent * on(device_id) group_left(namespace, pod, container) "
      "amdgpu_device_plugin_allocation_info"),

@@ -539,6 +539,8 @@ class AmdSmiBackend : public Backend {
       s->link_peer[i] = gpu_of_bdf(lm.links[k].bdf);
       s->link_read_kb[i] = static_cast<double>(lm.links[k].read);
       s->link_write_kb[i] = static_cast<double>(lm.links[k].write);
+      s->link_bitrate_gbps[i] = lm.links[k].bit_rate != 0xFFFFFFFFu ? lm.links[k].bit_rate : 0;
+      s->link_max_gbps[i] = lm.links[k].max_bandwidth != 0xFFFFFFFFu ? lm.links[k].max_bandwidth : 0;
       if (have_status && k < ls.total_links)
         s->link_up[i] = ls.status[k] == AMDSMI_XGMI_LINK_UP ? 1 : (ls.status[k] == AMDSMI_XGMI_LINK_DOWN ? 0 : -1);
       else
