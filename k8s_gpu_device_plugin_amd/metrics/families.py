@@ -59,9 +59,10 @@ FAMILIES = (
     Family("amdgpu_xgmi_link_up", "gauge", GPU + ("link", "peer"), "exporter", "xGMI link to peer is up"),
     Family("amdgpu_xgmi_read_bytes_total", "counter", GPU + ("link", "peer"), "exporter", "xGMI bytes received"),
     Family("amdgpu_xgmi_write_bytes_total", "counter", GPU + ("link", "peer"), "exporter", "xGMI bytes sent"),
-    Family("amdgpu_xgmi_link_speed_gbps", "gauge", GPU + ("link", "peer"), "exporter",
-           "Current link speed; below amdgpu_xgmi_link_max_speed_gbps = degraded training"),
-    Family("amdgpu_xgmi_link_max_speed_gbps", "gauge", GPU + ("link", "peer"), "exporter", "Maximum link speed"),
+    Family("amdgpu_xgmi_link_bitrate_gbps", "gauge", GPU + ("link", "peer"), "exporter",
+           "Per-lane signalling rate (38 on MI355X); a link trained slower than its peers is degraded"),
+    Family("amdgpu_xgmi_link_bandwidth_gbps", "gauge", GPU + ("link", "peer"), "exporter",
+           "Link bandwidth over all lanes (608 Gb/s on MI355X)"),
     # --- per-partition ---
     Family("amdgpu_partition_info", "gauge", PART, "exporter", "Partition -> device id / resource (value 1)"),
     Family("amdgpu_partition_gfx_busy_percent", "gauge", PART, "exporter", "Per-XCP compute busy"),
@@ -108,7 +109,8 @@ PROMQL_EXAMPLES = (
     ("Allocate p99 over 5 minutes",
      'histogram_quantile(0.99, sum by (le) (rate(amdgpu_device_plugin_rpc_duration_seconds_bucket{rpc="Allocate"}[5m])))'),
     ("Down xGMI links", "amdgpu_xgmi_link_up == 0"),
-    ("xGMI links trained below full speed", "amdgpu_xgmi_link_speed_gbps < amdgpu_xgmi_link_max_speed_gbps"),
+    ("xGMI links trained slower than the node's fastest link",
+     "amdgpu_xgmi_link_bitrate_gbps < on() group_left max(amdgpu_xgmi_link_bitrate_gbps)"),
     ("Partition busy per workload (podResources.enabled)",
      "amdgpu_partition_gfx_busy_percent * on(device_id) group_left(namespace, pod, container) "
      "amdgpu_device_plugin_allocation_info"),

@@ -119,8 +119,8 @@ struct GpuSample {
   int link_up[kMaxXgmiLinks] = {};    // 1 up, 0 down, -1 unknown/disabled
   double link_read_kb[kMaxXgmiLinks] = {};
   double link_write_kb[kMaxXgmiLinks] = {};
-  double link_bitrate_gbps[kMaxXgmiLinks] = {};   // current link speed, Gb/s (0 = unknown)
-  double link_max_gbps[kMaxXgmiLinks] = {};       // max bandwidth of the link, Gb/s (0 = unknown)
+  double link_bitrate_gbps[kMaxXgmiLinks] = {};   // per-lane signalling rate, Gb/s (0 = unknown)
+  double link_max_gbps[kMaxXgmiLinks] = {};       // link bandwidth (all lanes), Gb/s (0 = unknown)
   int num_partitions = 0;
   double partition_gfx_busy_pct[kMaxPartitions] = {};
   double partition_vram_used_bytes[kMaxPartitions] = {};

@@ -155,8 +155,8 @@ bool FixtureBackend::sample(int gpu, GpuSample* s) {
     s->link_up[k] = topo_.at(gpu, peer).up ? 1 : 0;
     s->link_read_kb[k] = 1e6 * ts * load;
     s->link_write_kb[k] = 0.9e6 * ts * load;
-    s->link_bitrate_gbps[k] = topo_.at(gpu, peer).up ? 38.4 * 32 : 0;  // illustrative xGMI figures
-    s->link_max_gbps[k] = 38.4 * 32;
+    s->link_bitrate_gbps[k] = 38;  // what amdsmi reports on MI355X: 38 Gb/s per lane, 16 lanes
+    s->link_max_gbps[k] = 608;
   }
   s->num_partitions = std::min<int>(static_cast<int>(g.partitions.size()), kMaxPartitions);
   for (int p = 0; p < s->num_partitions; ++p) {

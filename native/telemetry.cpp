@@ -322,9 +322,9 @@ void Exporter::render_gpu_text(const std::vector<GpuSample>& samples, const std:
         if (s.link_up[k] >= 0) line(&up, "amdgpu_xgmi_link_up", l, s.link_up[k]);
         line(&rd, "amdgpu_xgmi_read_bytes_total", l, s.link_read_kb[k] * 1024.0);
         line(&wr, "amdgpu_xgmi_write_bytes_total", l, s.link_write_kb[k] * 1024.0);
-        if (s.link_max_gbps[k] > 0) {  // a link trained below its maximum is degraded
-          line(&rate, "amdgpu_xgmi_link_speed_gbps", l, s.link_bitrate_gbps[k]);
-          line(&maxr, "amdgpu_xgmi_link_max_speed_gbps", l, s.link_max_gbps[k]);
+        if (s.link_max_gbps[k] > 0) {  // a link trained slower than its peers shows here
+          line(&rate, "amdgpu_xgmi_link_bitrate_gbps", l, s.link_bitrate_gbps[k]);
+          line(&maxr, "amdgpu_xgmi_link_bandwidth_gbps", l, s.link_max_gbps[k]);
         }
       }
     }
@@ -339,9 +339,9 @@ void Exporter::render_gpu_text(const std::vector<GpuSample>& samples, const std:
       o.append(wr);
     }
     if (!rate.empty()) {
-      append_header(&o, "amdgpu_xgmi_link_speed_gbps", "Current xGMI link speed (Gb/s).", "gauge");
+      append_header(&o, "amdgpu_xgmi_link_bitrate_gbps", "xGMI per-lane signalling rate (Gb/s).", "gauge");
       o.append(rate);
-      append_header(&o, "amdgpu_xgmi_link_max_speed_gbps", "Maximum xGMI link speed (Gb/s).", "gauge");
+      append_header(&o, "amdgpu_xgmi_link_bandwidth_gbps", "xGMI link bandwidth over all lanes (Gb/s).", "gauge");
       o.append(maxr);
     }
   }
