@@ -244,6 +244,151 @@ __global__ void __launch_bounds__(256) gemm_lds(const short* __restrict__ A, con
       }
 }
 
+// ---- 256x256-tile GEMM, two wave groups in ping-pong: the fast matrix path ------------
+// Same contract as gemm_lds (A [MxK], Bt [NxK] bf16, fp32 C), M, N % 256 == 0, K % 64 == 0.
+// 8 waves = 2 groups (wr) x 4 (wc); a wave owns 128x64 of C as 2 halves x 4x4 tiles of
+// v_mfma_f32_16x16x32_bf16 (128 accumulator registers).  Per K-tile (BK = 64) a wave runs
+// four sections, each closed by a raw s_barrier:
+//   L0: ds_read A half 0 + all of B (16 x b128)   M0: 32 MFMA into half 0
+//   L1: ds_read A half 1 (8 x b128)               M1: 32 MFMA into half 1
+// Group 1 executes one extra barrier first, so it runs one barrier interval behind group
+// 0.  Waves w and w+4 share a SIMD, hence on every SIMD one wave is in an MFMA section
+// while its partner reads LDS: the MFMA pipe does not wait for fragment loads.
+// Operands stream in with global_load_lds into 2 LDS buffers (2 x 64 KiB, 1 block/CU).
+// Interval i (between barriers i and i+1) holds group 0's section i and group 1's
+// section i-1.  Tile t lives in buffer t&1 and is read in intervals 4t..4t+3; tile t+2
+// is issued by both groups in interval 4t+4 (right after the barrier that ends the last
+// read of tile t) and each wave retires its own copies with s_waitcnt vmcnt(0) before
+// barrier 4t+8, which precedes the first read of tile t+2.  The DMA therefore stays in
+// flight across three barriers (__syncthreads would drain it at each: vmcnt(0)).
+// Write-after-read is covered by every reading section ending in lgkmcnt(0) before its
+// barrier.  Row swizzle as in gemm_lds (chunk ^ ((row >> 1) & 7)): conflict-free for the
+// 16x16x32 lane groups too.  Tiles are rastered in groups of 4 tile rows, so one XCD's
+// consecutive workgroups share 4 A panels and a run of B panels in their L2.
+constexpr int kBT = 256, kBK = 64;
+constexpr int kBOp = kBT * kBK * 2;  // one operand tile, 32 KiB
+constexpr int kBStage = 2 * kBOp;    // A + B of one K-tile, 64 KiB
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+
+__device__ __forceinline__ void section_end() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this section's LDS reads are done
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);  // nothing crosses a section boundary
+}
+
+__global__ void __launch_bounds__(512) gemm256(const short* __restrict__ A, const short* __restrict__ Bt,
+                                              float* __restrict__ C, int M, int N, int K) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBStage];  // the only LDS object
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nbm = M / kBT, nbn = N / kBT;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  constexpr int kGroupM = 4;
+  const int per_group = kGroupM * nbn, first_m = (wg / per_group) * kGroupM;
+  const int gm = nbm - first_m < kGroupM ? nbm - first_m : kGroupM;
+  const int m0 = (first_m + (wg % per_group) % gm) * kBT, n0 = ((wg % per_group) / gm) * kBT;
+  if (m0 + kBT > M || n0 + kBT > N) return;  // host checks shapes (block-uniform exit)
+  const int wr = wave >> 2, wc = wave & 3;
+  const bool g1 = wr == 1;
+  const int r16 = lane & 15, q = lane >> 4;
+
+  auto stage = [&](int t) {  // 8 x 1 KiB pieces per wave: rows (4w+i)*8 .. +7 of A and of B
+    const int k0 = t * kBK;
+    char* base = smem + (t & 1) * kBStage;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (wave * 4 + i) * 8 + (lane >> 3), kc = ((lane & 7) ^ ((row >> 1) & 7)) * 8;
+      __builtin_amdgcn_global_load_lds(A + static_cast<size_t>(m0 + row) * K + k0 + kc,
+                                       (lds_void_ptr)(base + (wave * 4 + i) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(Bt + static_cast<size_t>(n0 + row) * K + k0 + kc,
+                                       (lds_void_ptr)(base + kBOp + (wave * 4 + i) * 1024), 16, 0, 0);
+    }
+  };
+  auto frag = [&](const short* S, int row, int chunk) {
+    return *reinterpret_cast<const bf16x8*>(S + row * kBK + ((chunk ^ ((row >> 1) & 7)) << 3));
+  };
+
+  f32x4 acc[2][4][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[h][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 a[4][2], b[4][2];
+
+  const int T = K / kBK;
+  stage(0);
+  if (T > 1) {
+    stage(1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile 0 landed; tile 1 may fly on
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  section_end();
+  if (g1) section_end();  // the one-interval stagger
+
+  for (int t = 0; t < T; ++t) {
+    const short* As = reinterpret_cast<const short*>(smem + (t & 1) * kBStage);
+    const short* Bs = As + kBT * kBK;
+    // L0
+    if (!g1 && t >= 1 && t + 1 < T) stage(t + 1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j][s] = frag(Bs, wc * 64 + j * 16 + r16, 4 * s + q);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i][s] = frag(As, wr * 128 + i * 16 + r16, 4 * s + q);
+    section_end();
+    // M0
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[0][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][s], b[j][s], acc[0][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    section_end();
+    // L1
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i][s] = frag(As, wr * 128 + 64 + i * 16 + r16, 4 * s + q);
+    if (g1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 (issued in interval 4t)
+    section_end();
+    // M1
+    if (g1 && t + 2 < T) stage(t + 2);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[1][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][s], b[j][s], acc[1][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    if (!g1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 (issued in interval 4t)
+    section_end();
+  }
+  if (!g1) section_end();  // both groups pass the same number of barriers
+
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = m0 + wr * 128 + h * 64 + i * 16 + q * 4 + e;
+          C[static_cast<size_t>(row) * N + n0 + wc * 64 + j * 16 + r16] = acc[h][i][j][e];
+        }
+}
+
 // Integer operands in [-4, 4] (exact in bf16): element (i, k) of operand `which`.
 __global__ void __launch_bounds__(256) gemm_fill(short* __restrict__ X, int rows, int K, uint32_t which) {
   const size_t n = static_cast<size_t>(rows) * K;
@@ -437,7 +582,7 @@ int amdgpu_canary_device_count() {
   return n;
 }
 
-int amdgpu_canary_gemm_rate(int device, int M, int N, int K, int iters, int inject, double* tflops,
+int amdgpu_canary_gemm_rate(int device, int M, int N, int K, int iters, int inject, int kernel, double* tflops,
                             unsigned long long* errors, char* err, int err_len);
 
 #define CANARY_CHECK(expr)                                                                   \
@@ -518,11 +663,12 @@ int amdgpu_canary_run(int device, unsigned long long hbm_bytes, int passes, int 
     out->mfma_tflops = flops / (t_mfma * 1e-3) / 1e12;
   }
   out->elapsed_ms = t_write + t_read + t_mfma;
-  // matrix path: HBM -> L2 -> LDS DMA -> ds_read -> MFMA, exact and checksummed.  2048^3
-  // keeps it short; hbm_bytes < 256 MiB (fault-injection runs) uses 1024^3.
+  // matrix path: HBM -> L2 -> LDS DMA -> ds_read -> MFMA, exact and checksummed.  4096^3
+  // (256 tiles of 256x256: one per CU) takes ~0.5 ms; hbm_bytes < 256 MiB (fault-injection
+  // runs) uses 1024^3 on the 128x128 kernel.
   {
-    const int g = hbm_bytes >= (256ull << 20) ? 2048 : 1024;
-    if (amdgpu_canary_gemm_rate(device, g, g, g, 4, 0, &out->gemm_tflops, &out->gemm_errors, out->error,
+    const int g = hbm_bytes >= (256ull << 20) ? 4096 : 1024;
+    if (amdgpu_canary_gemm_rate(device, g, g, g, 4, 0, 0, &out->gemm_tflops, &out->gemm_errors, out->error,
                                 sizeof(out->error)) != 0)
       goto done;
   }
@@ -623,11 +769,33 @@ int amdgpu_canary_mfma_gemm(int device, const unsigned short* a_host, const unsi
   return e == hipSuccess ? 0 : -1;
 }
 
+// GEMM kernel choice: 1 = gemm_lds (128x128 tiles), 2 = gemm256 (256x256 tiles, wave-group
+// ping-pong); 0 = gemm256 when the shape divides into 256x256 tiles and gives at least
+// 256 of them (one per CU), else gemm_lds.  Returns 0 for a shape the kernel cannot take.
+int pick_gemm(int M, int N, int K, int kernel) {
+  if (M <= 0 || N <= 0 || K <= 0 || K % kTileK) return 0;
+  const bool fits256 = M % kBT == 0 && N % kBT == 0, fits128 = M % kTileM == 0 && N % kTileN == 0;
+  if (kernel == 2) return fits256 ? 2 : 0;
+  if (kernel == 1) return fits128 ? 1 : 0;
+  if (kernel != 0) return 0;
+  if (fits256 && (M / kBT) * (N / kBT) >= 256) return 2;
+  return fits128 ? 1 : 0;
+}
+
+void launch_gemm(int kind, const short* a, const short* b, float* c, int M, int N, int K) {
+  if (kind == 2)
+    hipLaunchKernelGGL(gemm256, dim3((M / kBT) * (N / kBT)), dim3(512), 0, 0, a, b, c, M, N, K);
+  else
+    hipLaunchKernelGGL(gemm_lds, dim3((M / kTileM) * (N / kTileN)), dim3(256), 0, 0, a, b, c, M, N, K);
+}
+
 // LDS-staged GEMM on host data (numerics test): A [MxK], Bt [NxK] bf16 row-major.
 int amdgpu_canary_gemm(int device, const unsigned short* a_host, const unsigned short* bt_host, float* c_host, int M,
-                       int N, int K, char* err, int err_len) {
-  if (M <= 0 || N <= 0 || K <= 0 || M % kTileM || N % kTileN || K % kTileK) {
-    std::snprintf(err, err_len, "shape (%d,%d,%d) must be M,N %% 128 == 0 and K %% 64 == 0", M, N, K);
+                       int N, int K, int kernel, char* err, int err_len) {
+  const int kind = pick_gemm(M, N, K, kernel);
+  if (kind == 0) {
+    std::snprintf(err, err_len, "shape (%d,%d,%d) does not fit kernel %d (M,N %% 128 or 256, K %% 64)", M, N, K,
+                  kernel);
     return -1;
   }
   short *a = nullptr, *b = nullptr;
@@ -641,7 +809,7 @@ int amdgpu_canary_gemm(int device, const unsigned short* a_host, const unsigned 
   if (e == hipSuccess) e = hipMemcpy(a, a_host, sa, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(b, bt_host, sb, hipMemcpyHostToDevice);
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(gemm_lds, dim3((M / kTileM) * (N / kTileN)), dim3(256), 0, 0, a, b, c, M, N, K);
+    launch_gemm(kind, a, b, c, M, N, K);
     e = hipGetLastError();
   }
   if (e == hipSuccess) e = hipDeviceSynchronize();
@@ -657,12 +825,14 @@ int amdgpu_canary_gemm(int device, const unsigned short* a_host, const unsigned 
 // ABFT row + column checksums of the result.  *tflops = dense bf16 rate achieved,
 // *errors = rows + columns whose checksum is off (0 on a healthy partition).
 // inject != 0 corrupts one element of C before the check (verifier self-test).
-int amdgpu_canary_gemm_rate(int device, int M, int N, int K, int iters, int inject, double* tflops,
+int amdgpu_canary_gemm_rate(int device, int M, int N, int K, int iters, int inject, int kernel, double* tflops,
                             unsigned long long* errors, char* err, int err_len) {
   *tflops = 0;
   *errors = 0;
-  if (M <= 0 || N <= 0 || K <= 0 || M % kTileM || N % kTileN || K % kTileK || K > 65536 || iters < 1) {
-    std::snprintf(err, err_len, "shape (%d,%d,%d) must be M,N %% 128 == 0, K %% 64 == 0, K <= 65536", M, N, K);
+  const int kind = pick_gemm(M, N, K, kernel);
+  if (kind == 0 || K > 65536 || iters < 1) {
+    std::snprintf(err, err_len, "shape (%d,%d,%d) does not fit kernel %d (M,N %% 128 or 256, K %% 64, K <= 65536)",
+                  M, N, K, kernel);
     return -1;
   }
   short *a = nullptr, *b = nullptr;
@@ -671,7 +841,6 @@ int amdgpu_canary_gemm_rate(int device, int M, int N, int K, int iters, int inje
   unsigned long long* d_err = nullptr;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   float ms = 0;
-  const dim3 grid((M / kTileM) * (N / kTileN));
   hipError_t e = hipSetDevice(device);
   if (e == hipSuccess) e = hipMalloc(&a, static_cast<size_t>(M) * K * 2);
   if (e == hipSuccess) e = hipMalloc(&b, static_cast<size_t>(N) * K * 2);
@@ -685,11 +854,11 @@ int amdgpu_canary_gemm_rate(int device, int M, int N, int K, int iters, int inje
   if (e == hipSuccess) {
     hipLaunchKernelGGL(gemm_fill, dim3(2048), dim3(256), 0, 0, a, M, K, 1u);
     hipLaunchKernelGGL(gemm_fill, dim3(2048), dim3(256), 0, 0, b, N, K, 2u);
-    hipLaunchKernelGGL(gemm_lds, grid, dim3(256), 0, 0, a, b, c, M, N, K);  // warm-up
+    launch_gemm(kind, a, b, c, M, N, K);  // warm-up
     e = hipGetLastError();
   }
   if (e == hipSuccess) e = hipEventRecord(e0, 0);
-  for (int i = 0; e == hipSuccess && i < iters; ++i) hipLaunchKernelGGL(gemm_lds, grid, dim3(256), 0, 0, a, b, c, M, N, K);
+  for (int i = 0; e == hipSuccess && i < iters; ++i) launch_gemm(kind, a, b, c, M, N, K);
   if (e == hipSuccess) e = hipEventRecord(e1, 0);
   if (e == hipSuccess) e = hipEventSynchronize(e1);
   if (e == hipSuccess) e = hipGetLastError();

@@ -57,10 +57,11 @@ def load():
                                                 ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_ulonglong)]
         lib.amdgpu_canary_hbm_sweep.restype = ctypes.c_int
         lib.amdgpu_canary_gemm.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                           ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+                                           ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
+                                           ctypes.c_int]
         lib.amdgpu_canary_gemm.restype = ctypes.c_int
         lib.amdgpu_canary_gemm_rate.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                                ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                                ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                                 ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_char_p, ctypes.c_int]
         lib.amdgpu_canary_gemm_rate.restype = ctypes.c_int
         _lib = lib
@@ -128,10 +129,15 @@ def mfma_gemm(a_bf16_bits, b_bf16_bits, device: int = 0):
     return c
 
 
-def gemm(a_bf16_bits, bt_bf16_bits, device: int = 0):
+GEMM_KERNELS = {"auto": 0, "lds128": 1, "pingpong256": 2}
+
+
+def gemm(a_bf16_bits, bt_bf16_bits, device: int = 0, kernel: str = "auto"):
     """C = A @ Bt.T through the LDS-staged MFMA GEMM (the canary's matrix path).
     ``a``: uint16 [M, K] bf16 bit patterns, ``bt``: uint16 [N, K] (B transposed, K
-    contiguous); M, N % 128 == 0, K % 64 == 0.  Returns float32 [M, N]."""
+    contiguous); K % 64 == 0 and M, N % 128 == 0 (``lds128``) or % 256 == 0
+    (``pingpong256``; ``auto`` takes it when that gives >= 256 tiles).  Returns float32
+    [M, N]."""
     import numpy as np
 
     a = np.ascontiguousarray(a_bf16_bits, dtype=np.uint16)
@@ -141,23 +147,25 @@ def gemm(a_bf16_bits, bt_bf16_bits, device: int = 0):
         raise ValueError("inner dimensions differ: %d vs %d" % (k, k2))
     c = np.empty((m, nn), dtype=np.float32)
     err = ctypes.create_string_buffer(256)
-    rc = load().amdgpu_canary_gemm(int(device), a.ctypes.data, bt.ctypes.data, c.ctypes.data, m, nn, k, err, 256)
+    rc = load().amdgpu_canary_gemm(int(device), a.ctypes.data, bt.ctypes.data, c.ctypes.data, m, nn, k,
+                                   GEMM_KERNELS[kernel], err, 256)
     if rc != 0:
         raise RuntimeError("gemm failed: " + err.value.decode(errors="replace"))
     return c
 
 
 def gemm_rate(device: int = 0, m: int = 4096, n: int = 4096, k: int = 4096, iters: int = 10,
-              inject: bool = False) -> dict:
+              inject: bool = False, kernel: str = "auto") -> dict:
     """Matrix-path canary: timed LDS-staged MFMA GEMMs on exact integer data, then ABFT
     row/column checksums.  ``errors`` counts rows + columns whose checksum is off."""
     t, e = ctypes.c_double(), ctypes.c_ulonglong()
     err = ctypes.create_string_buffer(256)
-    rc = load().amdgpu_canary_gemm_rate(int(device), m, n, k, iters, int(bool(inject)), ctypes.byref(t),
+    rc = load().amdgpu_canary_gemm_rate(int(device), m, n, k, iters, int(bool(inject)), GEMM_KERNELS[kernel],
+                                        ctypes.byref(t),
                                         ctypes.byref(e), err, 256)
     if rc != 0:
         raise RuntimeError("gemm_rate failed: " + err.value.decode(errors="replace"))
-    return {"tflops": t.value, "errors": e.value, "shape": (m, n, k), "iters": iters}
+    return {"tflops": t.value, "errors": e.value, "shape": (m, n, k), "iters": iters, "kernel": kernel}
 
 
 def run_isolated(device: int, hbm_bytes: int = 256 << 20, timeout: float = 120.0) -> dict:
@@ -186,9 +194,10 @@ def main(argv=None) -> int:
     ap.add_argument("--mfma-iters", type=int, default=8192)
     ap.add_argument("--gemm", type=int, default=0, help="only the matrix-path GEMM, at this M=N=K")
     ap.add_argument("--gemm-iters", type=int, default=20)
+    ap.add_argument("--gemm-kernel", choices=sorted(GEMM_KERNELS), default="auto")
     a = ap.parse_args(argv)
     if a.gemm:
-        res = gemm_rate(a.device, a.gemm, a.gemm, a.gemm, a.gemm_iters)
+        res = gemm_rate(a.device, a.gemm, a.gemm, a.gemm, a.gemm_iters, kernel=a.gemm_kernel)
         print(json.dumps(res))
         return 0 if res["errors"] == 0 else 1
     res = run(a.device, a.bytes, a.passes, a.mfma_iters)

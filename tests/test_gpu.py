@@ -329,10 +329,15 @@ def test_prestart_canary_on_allocated_partition(make_cfg, plugin_dir):
         k.stop()
 
 
-@pytest.mark.parametrize("shape", [(128, 128, 64), (256, 384, 512), (512, 256, 1024)])
-def test_lds_gemm_matches_torch_fp32(shape):
-    """The LDS-staged MFMA GEMM (global_load_lds double buffer, XCD remap) against a
-    PyTorch fp32 reference on random bf16 operands."""
+@pytest.mark.parametrize("kernel,shape", [
+    ("lds128", (128, 128, 64)), ("lds128", (256, 384, 512)), ("lds128", (512, 256, 1024)),
+    ("pingpong256", (256, 256, 64)), ("pingpong256", (256, 512, 128)), ("pingpong256", (512, 768, 1024)),
+    ("pingpong256", (768, 256, 320))])
+def test_lds_gemm_matches_torch_fp32(kernel, shape):
+    """The LDS-staged MFMA GEMMs (global_load_lds, XCD remap; 128x128 double buffer and the
+    256x256 wave-group ping-pong) against a PyTorch fp32 reference on random bf16
+    operands.  K-tile counts 1, 2, 5 (odd) and 16 cover the ping-pong's prologue, its
+    peeled first iteration and both buffer parities."""
     import torch
 
     from k8s_gpu_device_plugin_amd.ops import canary
@@ -341,20 +346,30 @@ def test_lds_gemm_matches_torch_fp32(shape):
     a = torch.randn(m, k, generator=g).to(torch.bfloat16)
     b = torch.randn(k, nn, generator=g).to(torch.bfloat16)
     bits = lambda t: t.contiguous().view(torch.int16).numpy().view(np.uint16)  # noqa: E731
-    c = canary.gemm(bits(a), bits(b.t()), device=0)
+    c = canary.gemm(bits(a), bits(b.t()), device=0, kernel=kernel)
     ref = (a.float() @ b.float()).numpy()
     err = np.abs(c - ref).max() / max(1e-6, np.abs(ref).max())
     assert err < 1e-5, err
 
 
 def test_lds_gemm_rate_and_abft():
-    """Throughput of the matrix-path canary at 4096^3 and its exactness check: no
+    """Throughput of both matrix-path kernels at 4096^3 and their exactness check: no
     checksum errors on a healthy GPU, and a single corrupted output element is caught
-    (its row and its column).  torch.matmul (hipBLASLt) on the same shape for scale."""
+    (its row and its column).  The ping-pong kernel is also screened for staging races
+    over several shapes (exact integer data: any early LDS read shows as a checksum
+    error).  torch.matmul (hipBLASLt) on the same shape for scale."""
     from k8s_gpu_device_plugin_amd.ops import canary
-    r = canary.gemm_rate(0, 4096, 4096, 4096, iters=20)
-    assert r["errors"] == 0, r
+    rates = {}
+    for kernel in ("lds128", "pingpong256"):
+        r = canary.gemm_rate(0, 4096, 4096, 4096, iters=20, kernel=kernel)
+        assert r["errors"] == 0, r
+        rates[kernel] = r["tflops"]
+    for shape in [(256, 256, 64), (1024, 2048, 640), (2048, 1024, 4096), (8192, 8192, 1024)]:
+        r = canary.gemm_rate(0, *shape, iters=3, kernel="pingpong256")
+        assert r["errors"] == 0, r
     bad = canary.gemm_rate(0, 1024, 1024, 1024, iters=1, inject=True)
+    assert bad["errors"] == 2, bad
+    bad = canary.gemm_rate(0, 1024, 1024, 1024, iters=1, inject=True, kernel="pingpong256")
     assert bad["errors"] == 2, bad
     # torch's bundled HIP runtime and the system one the canary links cannot both own the
     # device in one process: time torch.matmul (hipBLASLt) in a child process
@@ -366,6 +381,6 @@ def test_lds_gemm_rate_and_abft():
             "print(2*4096**3*20/(time.perf_counter()-t)/1e12)")
     out = subprocess.run([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True, timeout=90)
     blas = float(out.stdout.strip().splitlines()[-1]) if out.returncode == 0 else float("nan")
-    print("LDS GEMM canary %.0f TFLOP/s (integer data), torch.matmul %.0f TFLOP/s (random data)"
-          % (r["tflops"], blas))
-    assert r["tflops"] > 200
+    print("GEMM canary lds128 %.0f / pingpong256 %.0f TFLOP/s (integer data), torch.matmul %.0f TFLOP/s "
+          "(random data)" % (rates["lds128"], rates["pingpong256"], blas))
+    assert min(rates.values()) > 200
