@@ -389,6 +389,145 @@ __global__ void __launch_bounds__(512) gemm256(const short* __restrict__ A, cons
         }
 }
 
+// ---- gemm256 with region-wise staging: the DMA issued from LDS-read sections ----------
+// gemm256 issues all eight 1 KiB pieces of a wave in one section, and a piece costs
+// ~60-185 issue cycles (MI355X_MICROARCH.md, LDS-DMA piece row), so that section runs
+// about twice as long as the others.  Here a tile's regions are refilled as soon as they
+// are free: B and the A rows every wave reads in L0 ("A-h0": rows 0-63 and 128-191) are
+// last read in interval 4t+1, so their refill for tile t+2 (6 pieces per wave) is issued
+// in L(t,1); the A-h1 rows are last read in interval 4t+3, so theirs (2 pieces) is issued
+// in L(t+1,0).  All DMA sits in L sections (which are shorter than the partner wave's
+// MFMA section), and a tile is retired with vmcnt(6) before barrier 4t+8: the next
+// tile's six younger pieces stay in flight.  Measured (4096^3 / 8192^3, integer data):
+// 1254-1264 / 1308-1314 TFLOP/s vs gemm256's 1069-1084 / 1078-1090.
+__global__ void __launch_bounds__(512) gemm256s(const short* __restrict__ A, const short* __restrict__ Bt,
+                                               float* __restrict__ C, int M, int N, int K) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBStage];  // the only LDS object
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nbm = M / kBT, nbn = N / kBT;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  constexpr int kGroupM = 4;
+  const int per_group = kGroupM * nbn, first_m = (wg / per_group) * kGroupM;
+  const int gm = nbm - first_m < kGroupM ? nbm - first_m : kGroupM;
+  const int m0 = (first_m + (wg % per_group) % gm) * kBT, n0 = ((wg % per_group) / gm) * kBT;
+  if (m0 + kBT > M || n0 + kBT > N) return;  // host checks shapes (block-uniform exit)
+  const int wr = wave >> 2, wc = wave & 3;
+  const bool g1 = wr == 1;
+  const int r16 = lane & 15, q = lane >> 4;
+
+  // piece p = rows 8p .. 8p+7 of one operand (1 KiB, 128 B rows, swizzled source)
+  auto piece = [&](const short* src, int r0, char* base, int p, int k0) {
+    const int row = p * 8 + (lane >> 3), kc = ((lane & 7) ^ ((row >> 1) & 7)) * 8;
+    __builtin_amdgcn_global_load_lds(src + static_cast<size_t>(r0 + row) * K + k0 + kc, (lds_void_ptr)(base + p * 1024),
+                                     16, 0, 0);
+  };
+  // A-h0 pieces are 0-7 and 16-23, A-h1 pieces 8-15 and 24-31; wave w owns list entries 2w, 2w+1
+  auto a_piece = [](int k, int half) { return (k < 8 ? k : k + 8) + 8 * half; };
+  auto stage_b_ah0 = [&](int t) {  // 4 B + 2 A-h0 pieces
+    char* base = smem + (t & 1) * kBStage;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) piece(Bt, n0, base + kBOp, wave * 4 + i, t * kBK);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) piece(A, m0, base, a_piece(wave * 2 + i, 0), t * kBK);
+  };
+  auto stage_ah1 = [&](int t) {  // 2 A-h1 pieces
+    char* base = smem + (t & 1) * kBStage;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) piece(A, m0, base, a_piece(wave * 2 + i, 1), t * kBK);
+  };
+  auto frag = [&](const short* S, int row, int chunk) {
+    return *reinterpret_cast<const bf16x8*>(S + row * kBK + ((chunk ^ ((row >> 1) & 7)) << 3));
+  };
+  auto retire = [&](int t) {  // tile t+1 landed; tile t+2's six B/A-h0 pieces may fly on
+    if (t + 2 < K / kBK)
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  f32x4 acc[2][4][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[h][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 a[4][2], b[4][2];
+
+  const int T = K / kBK;
+  stage_b_ah0(0);
+  stage_ah1(0);
+  if (T > 1) {
+    stage_b_ah0(1);
+    stage_ah1(1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile 0 landed; tile 1 may fly on
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  section_end();
+  if (g1) section_end();  // the one-interval stagger
+
+  for (int t = 0; t < T; ++t) {
+    const short* As = reinterpret_cast<const short*>(smem + (t & 1) * kBStage);
+    const short* Bs = As + kBT * kBK;
+    // L0
+    if (t >= 1 && t + 1 < T) stage_ah1(t + 1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j][s2] = frag(Bs, wc * 64 + j * 16 + r16, 4 * s2 + q);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i][s2] = frag(As, wr * 128 + i * 16 + r16, 4 * s2 + q);
+    section_end();
+    // M0
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[0][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][s2], b[j][s2], acc[0][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    section_end();
+    // L1
+    if (t + 2 < T) stage_b_ah0(t + 2);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i][s2] = frag(As, wr * 128 + 64 + i * 16 + r16, 4 * s2 + q);
+    if (g1) retire(t);
+    section_end();
+    // M1
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[1][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][s2], b[j][s2], acc[1][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    if (!g1) retire(t);
+    section_end();
+  }
+  if (!g1) section_end();  // both groups pass the same number of barriers
+
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = m0 + wr * 128 + h * 64 + i * 16 + q * 4 + e;
+          C[static_cast<size_t>(row) * N + n0 + wc * 64 + j * 16 + r16] = acc[h][i][j][e];
+        }
+}
+
 // Integer operands in [-4, 4] (exact in bf16): element (i, k) of operand `which`.
 __global__ void __launch_bounds__(256) gemm_fill(short* __restrict__ X, int rows, int K, uint32_t which) {
   const size_t n = static_cast<size_t>(rows) * K;
@@ -770,20 +909,23 @@ int amdgpu_canary_mfma_gemm(int device, const unsigned short* a_host, const unsi
 }
 
 // GEMM kernel choice: 1 = gemm_lds (128x128 tiles), 2 = gemm256 (256x256 tiles, wave-group
-// ping-pong); 0 = gemm256 when the shape divides into 256x256 tiles and gives at least
-// 256 of them (one per CU), else gemm_lds.  Returns 0 for a shape the kernel cannot take.
+// ping-pong), 3 = gemm256s (same, region-wise DMA from the LDS-read sections); 0 = gemm256s
+// when the shape divides into 256x256 tiles and gives at least 256 of them (one per CU),
+// else gemm_lds.  Returns 0 for a shape the kernel cannot take.
 int pick_gemm(int M, int N, int K, int kernel) {
   if (M <= 0 || N <= 0 || K <= 0 || K % kTileK) return 0;
   const bool fits256 = M % kBT == 0 && N % kBT == 0, fits128 = M % kTileM == 0 && N % kTileN == 0;
-  if (kernel == 2) return fits256 ? 2 : 0;
+  if (kernel == 2 || kernel == 3) return fits256 ? kernel : 0;
   if (kernel == 1) return fits128 ? 1 : 0;
   if (kernel != 0) return 0;
-  if (fits256 && (M / kBT) * (N / kBT) >= 256) return 2;
+  if (fits256 && (M / kBT) * (N / kBT) >= 256) return 3;
   return fits128 ? 1 : 0;
 }
 
 void launch_gemm(int kind, const short* a, const short* b, float* c, int M, int N, int K) {
-  if (kind == 2)
+  if (kind == 3)
+    hipLaunchKernelGGL(gemm256s, dim3((M / kBT) * (N / kBT)), dim3(512), 0, 0, a, b, c, M, N, K);
+  else if (kind == 2)
     hipLaunchKernelGGL(gemm256, dim3((M / kBT) * (N / kBT)), dim3(512), 0, 0, a, b, c, M, N, K);
   else
     hipLaunchKernelGGL(gemm_lds, dim3((M / kTileM) * (N / kTileN)), dim3(256), 0, 0, a, b, c, M, N, K);

@@ -332,7 +332,8 @@ def test_prestart_canary_on_allocated_partition(make_cfg, plugin_dir):
 @pytest.mark.parametrize("kernel,shape", [
     ("lds128", (128, 128, 64)), ("lds128", (256, 384, 512)), ("lds128", (512, 256, 1024)),
     ("pingpong256", (256, 256, 64)), ("pingpong256", (256, 512, 128)), ("pingpong256", (512, 768, 1024)),
-    ("pingpong256", (768, 256, 320))])
+    ("pingpong256", (768, 256, 320)), ("pingpong256s", (256, 256, 64)), ("pingpong256s", (256, 512, 128)),
+    ("pingpong256s", (512, 768, 1024)), ("pingpong256s", (768, 256, 320)), ("pingpong256s", (256, 256, 192))])
 def test_lds_gemm_matches_torch_fp32(kernel, shape):
     """The LDS-staged MFMA GEMMs (global_load_lds, XCD remap; 128x128 double buffer and the
     256x256 wave-group ping-pong) against a PyTorch fp32 reference on random bf16
@@ -360,13 +361,14 @@ def test_lds_gemm_rate_and_abft():
     error).  torch.matmul (hipBLASLt) on the same shape for scale."""
     from k8s_gpu_device_plugin_amd.ops import canary
     rates = {}
-    for kernel in ("lds128", "pingpong256"):
+    for kernel in ("lds128", "pingpong256", "pingpong256s"):
         r = canary.gemm_rate(0, 4096, 4096, 4096, iters=20, kernel=kernel)
         assert r["errors"] == 0, r
         rates[kernel] = r["tflops"]
-    for shape in [(256, 256, 64), (1024, 2048, 640), (2048, 1024, 4096), (8192, 8192, 1024)]:
-        r = canary.gemm_rate(0, *shape, iters=3, kernel="pingpong256")
-        assert r["errors"] == 0, r
+    for kernel in ("pingpong256", "pingpong256s"):
+        for shape in [(256, 256, 64), (1024, 2048, 640), (2048, 1024, 4096), (8192, 8192, 1024)]:
+            r = canary.gemm_rate(0, *shape, iters=3, kernel=kernel)
+            assert r["errors"] == 0, r
     bad = canary.gemm_rate(0, 1024, 1024, 1024, iters=1, inject=True)
     assert bad["errors"] == 2, bad
     bad = canary.gemm_rate(0, 1024, 1024, 1024, iters=1, inject=True, kernel="pingpong256")
@@ -381,6 +383,6 @@ def test_lds_gemm_rate_and_abft():
             "print(2*4096**3*20/(time.perf_counter()-t)/1e12)")
     out = subprocess.run([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True, timeout=90)
     blas = float(out.stdout.strip().splitlines()[-1]) if out.returncode == 0 else float("nan")
-    print("GEMM canary lds128 %.0f / pingpong256 %.0f TFLOP/s (integer data), torch.matmul %.0f TFLOP/s "
-          "(random data)" % (rates["lds128"], rates["pingpong256"], blas))
+    print("GEMM canary %s TFLOP/s (integer data), torch.matmul %.0f TFLOP/s (random data)"
+          % (" / ".join("%s %.0f" % kv for kv in rates.items()), blas))
     assert min(rates.values()) > 200
