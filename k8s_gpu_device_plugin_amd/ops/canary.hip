@@ -400,6 +400,10 @@ __global__ void __launch_bounds__(512) gemm256(const short* __restrict__ A, cons
 // MFMA section), and a tile is retired with vmcnt(6) before barrier 4t+8: the next
 // tile's six younger pieces stay in flight.  Measured (4096^3 / 8192^3, integer data):
 // 1254-1264 / 1308-1314 TFLOP/s vs gemm256's 1069-1084 / 1078-1090.
+// kBEarly of a wave's 4 B pieces of tile t+2 go with its A-h0 pieces in L(t,1), the rest
+// with the A-h1 pieces in L(t+1,0): the split balances DMA issue between the two L
+// sections (L0 also carries twice L1's ds_reads).
+template <int kBEarly>
 __global__ void __launch_bounds__(512) gemm256s(const short* __restrict__ A, const short* __restrict__ Bt,
                                                float* __restrict__ C, int M, int N, int K) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kBStage];  // the only LDS object
@@ -423,26 +427,36 @@ __global__ void __launch_bounds__(512) gemm256s(const short* __restrict__ A, con
   };
   // A-h0 pieces are 0-7 and 16-23, A-h1 pieces 8-15 and 24-31; wave w owns list entries 2w, 2w+1
   auto a_piece = [](int k, int half) { return (k < 8 ? k : k + 8) + 8 * half; };
-  auto stage_b_ah0 = [&](int t) {  // 4 B + 2 A-h0 pieces
+  auto stage_b_ah0 = [&](int t) {  // kBEarly B + 2 A-h0 pieces
     char* base = smem + (t & 1) * kBStage;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) piece(Bt, n0, base + kBOp, wave * 4 + i, t * kBK);
+    for (int i = 0; i < kBEarly; ++i) piece(Bt, n0, base + kBOp, wave * 4 + i, t * kBK);
 #pragma unroll
     for (int i = 0; i < 2; ++i) piece(A, m0, base, a_piece(wave * 2 + i, 0), t * kBK);
   };
-  auto stage_ah1 = [&](int t) {  // 2 A-h1 pieces
+  auto stage_ah1 = [&](int t) {  // 4 - kBEarly B + 2 A-h1 pieces
     char* base = smem + (t & 1) * kBStage;
+#pragma unroll
+    for (int i = kBEarly; i < 4; ++i) piece(Bt, n0, base + kBOp, wave * 4 + i, t * kBK);
 #pragma unroll
     for (int i = 0; i < 2; ++i) piece(A, m0, base, a_piece(wave * 2 + i, 1), t * kBK);
   };
   auto frag = [&](const short* S, int row, int chunk) {
     return *reinterpret_cast<const bf16x8*>(S + row * kBK + ((chunk ^ ((row >> 1) & 7)) << 3));
   };
-  auto retire = [&](int t) {  // tile t+1 landed; tile t+2's six B/A-h0 pieces may fly on
-    if (t + 2 < K / kBK)
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else
+  auto retire = [&](int t) {  // tile t+1 landed; tile t+2's 2 + kBEarly pieces may fly on
+    if (t + 2 >= K / kBK)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (kBEarly == 4)
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if constexpr (kBEarly == 3)
+      asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else if constexpr (kBEarly == 2)
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (kBEarly == 1)
+      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
   };
 
   f32x4 acc[2][4][4];
@@ -515,17 +529,30 @@ __global__ void __launch_bounds__(512) gemm256s(const short* __restrict__ A, con
   }
   if (!g1) section_end();  // both groups pass the same number of barriers
 
+  // Epilogue through LDS: after the last barrier no wave reads a staging buffer and no DMA
+  // is in flight, so each wave turns its 64x64 fp32 half-outputs into whole rows in a
+  // 16 KiB region of its own (8 x 16 KiB = the whole 128 KiB; 256 B rows: a ds_write_b32
+  // is 2-way, which costs nothing on that instruction, and the b128 read-back is
+  // conflict-free) and stores them with dwordx4: 16 row-contiguous stores of 4 rows x
+  // 256 B per half instead of 64 column-scattered dword stores.
+  static_assert(8 * 64 * 64 * 4 <= 2 * kBStage, "epilogue regions fit the staging LDS");
+  float* region = reinterpret_cast<float*>(smem + wave * (64 * 64 * 4));
+  constexpr int kLd = 64;  // floats per row
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < 2; ++h) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int row = m0 + wr * 128 + h * 64 + i * 16 + q * 4 + e;
-          C[static_cast<size_t>(row) * N + n0 + wc * 64 + j * 16 + r16] = acc[h][i][j][e];
-        }
+        for (int e = 0; e < 4; ++e) region[(i * 16 + q * 4 + e) * kLd + j * 16 + r16] = acc[h][i][j][e];
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+      const int row = p * 4 + (lane >> 4), c4 = (lane & 15) * 4;
+      const float4 v = *reinterpret_cast<const float4*>(region + row * kLd + c4);
+      *reinterpret_cast<float4*>(C + static_cast<size_t>(m0 + wr * 128 + h * 64 + row) * N + n0 + wc * 64 + c4) = v;
+    }
+  }
 }
 
 // Integer operands in [-4, 4] (exact in bf16): element (i, k) of operand `which`.
@@ -533,6 +560,18 @@ __global__ void __launch_bounds__(256) gemm_fill(short* __restrict__ X, int rows
   const size_t n = static_cast<size_t>(rows) * K;
   for (size_t e = blockIdx.x * 256ull + threadIdx.x; e < n; e += static_cast<size_t>(gridDim.x) * 256)
     X[e] = bf16_of_int(small_int((static_cast<uint64_t>(which) << 56) ^ e));
+}
+
+// Uniform random bf16 in [-1, 1) (rate measurement on data with full mantissas: the
+// clock the chip holds under MFMA load depends on operand bit activity).
+__global__ void __launch_bounds__(256) gemm_fill_random(short* __restrict__ X, int rows, int K, uint32_t which) {
+  const size_t n = static_cast<size_t>(rows) * K;
+  for (size_t e = blockIdx.x * 256ull + threadIdx.x; e < n; e += static_cast<size_t>(gridDim.x) * 256) {
+    const float f = static_cast<float>(mix32((static_cast<uint64_t>(which) << 56) ^ e) >> 8) * (2.0f / 16777216.0f) - 1.0f;
+    uint32_t u;
+    __builtin_memcpy(&u, &f, 4);
+    X[e] = static_cast<short>(u >> 16);
+  }
 }
 
 __device__ __forceinline__ int bf16_to_int(short v) {
@@ -915,7 +954,7 @@ int amdgpu_canary_mfma_gemm(int device, const unsigned short* a_host, const unsi
 int pick_gemm(int M, int N, int K, int kernel) {
   if (M <= 0 || N <= 0 || K <= 0 || K % kTileK) return 0;
   const bool fits256 = M % kBT == 0 && N % kBT == 0, fits128 = M % kTileM == 0 && N % kTileN == 0;
-  if (kernel == 2 || kernel == 3) return fits256 ? kernel : 0;
+  if (kernel >= 2 && kernel <= 6) return fits256 ? kernel : 0;
   if (kernel == 1) return fits128 ? 1 : 0;
   if (kernel != 0) return 0;
   if (fits256 && (M / kBT) * (N / kBT) >= 256) return 3;
@@ -923,8 +962,15 @@ int pick_gemm(int M, int N, int K, int kernel) {
 }
 
 void launch_gemm(int kind, const short* a, const short* b, float* c, int M, int N, int K) {
+  const dim3 g256((M / kBT) * (N / kBT)), b256(512);
   if (kind == 3)
-    hipLaunchKernelGGL(gemm256s, dim3((M / kBT) * (N / kBT)), dim3(512), 0, 0, a, b, c, M, N, K);
+    hipLaunchKernelGGL(gemm256s<4>, g256, b256, 0, 0, a, b, c, M, N, K);
+  else if (kind == 4)
+    hipLaunchKernelGGL(gemm256s<2>, g256, b256, 0, 0, a, b, c, M, N, K);
+  else if (kind == 5)
+    hipLaunchKernelGGL(gemm256s<0>, g256, b256, 0, 0, a, b, c, M, N, K);
+  else if (kind == 6)
+    hipLaunchKernelGGL(gemm256s<3>, g256, b256, 0, 0, a, b, c, M, N, K);
   else if (kind == 2)
     hipLaunchKernelGGL(gemm256, dim3((M / kBT) * (N / kBT)), dim3(512), 0, 0, a, b, c, M, N, K);
   else
@@ -966,9 +1012,12 @@ int amdgpu_canary_gemm(int device, const unsigned short* a_host, const unsigned 
 // Matrix-path canary: device-generated integer operands, `iters` timed GEMMs, then the
 // ABFT row + column checksums of the result.  *tflops = dense bf16 rate achieved,
 // *errors = rows + columns whose checksum is off (0 on a healthy partition).
-// inject != 0 corrupts one element of C before the check (verifier self-test).
-int amdgpu_canary_gemm_rate(int device, int M, int N, int K, int iters, int inject, int kernel, double* tflops,
+// flags bit 0 corrupts one element of C before the check (verifier self-test); bit 1
+// fills the operands with random bf16 in [-1, 1) instead and skips the (then inexact)
+// checksums: the rate on full-mantissa data, comparable with a BLAS benchmark.
+int amdgpu_canary_gemm_rate(int device, int M, int N, int K, int iters, int flags, int kernel, double* tflops,
                             unsigned long long* errors, char* err, int err_len) {
+  const bool inject = flags & 1, random_data = flags & 2;
   *tflops = 0;
   *errors = 0;
   const int kind = pick_gemm(M, N, K, kernel);
@@ -994,8 +1043,13 @@ int amdgpu_canary_gemm_rate(int device, int M, int N, int K, int iters, int inje
   if (e == hipSuccess) e = hipEventCreate(&e0);
   if (e == hipSuccess) e = hipEventCreate(&e1);
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(gemm_fill, dim3(2048), dim3(256), 0, 0, a, M, K, 1u);
-    hipLaunchKernelGGL(gemm_fill, dim3(2048), dim3(256), 0, 0, b, N, K, 2u);
+    if (random_data) {
+      hipLaunchKernelGGL(gemm_fill_random, dim3(2048), dim3(256), 0, 0, a, M, K, 1u);
+      hipLaunchKernelGGL(gemm_fill_random, dim3(2048), dim3(256), 0, 0, b, N, K, 2u);
+    } else {
+      hipLaunchKernelGGL(gemm_fill, dim3(2048), dim3(256), 0, 0, a, M, K, 1u);
+      hipLaunchKernelGGL(gemm_fill, dim3(2048), dim3(256), 0, 0, b, N, K, 2u);
+    }
     launch_gemm(kind, a, b, c, M, N, K);  // warm-up
     e = hipGetLastError();
   }
@@ -1009,7 +1063,7 @@ int amdgpu_canary_gemm_rate(int device, int M, int N, int K, int iters, int inje
     const float junk = 12345.0f;
     e = hipMemcpy(c + static_cast<size_t>(M / 2) * N + N / 3, &junk, 4, hipMemcpyHostToDevice);
   }
-  if (e == hipSuccess) {
+  if (e == hipSuccess && !random_data) {
     e = hipMemset(asum, 0, static_cast<size_t>(K) * 8);
     if (e == hipSuccess) e = hipMemset(bsum, 0, static_cast<size_t>(K) * 8);
     hipLaunchKernelGGL(gemm_colsum, dim3((K + 255) / 256, (M + kSlab - 1) / kSlab), dim3(256), 0, 0, a, M, K, asum);

@@ -129,7 +129,7 @@ def mfma_gemm(a_bf16_bits, b_bf16_bits, device: int = 0):
     return c
 
 
-GEMM_KERNELS = {"auto": 0, "lds128": 1, "pingpong256": 2, "pingpong256s": 3}
+GEMM_KERNELS = {"auto": 0, "lds128": 1, "pingpong256": 2, "pingpong256s": 3, "pingpong256s_b2": 4, "pingpong256s_b0": 5, "pingpong256s_b3": 6}
 
 
 def gemm(a_bf16_bits, bt_bf16_bits, device: int = 0, kernel: str = "auto"):
@@ -155,17 +155,21 @@ def gemm(a_bf16_bits, bt_bf16_bits, device: int = 0, kernel: str = "auto"):
 
 
 def gemm_rate(device: int = 0, m: int = 4096, n: int = 4096, k: int = 4096, iters: int = 10,
-              inject: bool = False, kernel: str = "auto") -> dict:
+              inject: bool = False, kernel: str = "auto", random_data: bool = False) -> dict:
     """Matrix-path canary: timed LDS-staged MFMA GEMMs on exact integer data, then ABFT
-    row/column checksums.  ``errors`` counts rows + columns whose checksum is off."""
+    row/column checksums.  ``errors`` counts rows + columns whose checksum is off.
+    ``random_data``: uniform bf16 operands in [-1, 1) instead (the rate a BLAS benchmark
+    quotes; no checksum, ``errors`` is None)."""
     t, e = ctypes.c_double(), ctypes.c_ulonglong()
     err = ctypes.create_string_buffer(256)
-    rc = load().amdgpu_canary_gemm_rate(int(device), m, n, k, iters, int(bool(inject)), GEMM_KERNELS[kernel],
+    rc = load().amdgpu_canary_gemm_rate(int(device), m, n, k, iters, int(bool(inject)) | (2 if random_data else 0),
+                                        GEMM_KERNELS[kernel],
                                         ctypes.byref(t),
                                         ctypes.byref(e), err, 256)
     if rc != 0:
         raise RuntimeError("gemm_rate failed: " + err.value.decode(errors="replace"))
-    return {"tflops": t.value, "errors": e.value, "shape": (m, n, k), "iters": iters, "kernel": kernel}
+    return {"tflops": t.value, "errors": None if random_data else e.value, "shape": (m, n, k), "iters": iters,
+            "kernel": kernel, "data": "random" if random_data else "integer"}
 
 
 def run_isolated(device: int, hbm_bytes: int = 256 << 20, timeout: float = 120.0) -> dict:
@@ -195,11 +199,13 @@ def main(argv=None) -> int:
     ap.add_argument("--gemm", type=int, default=0, help="only the matrix-path GEMM, at this M=N=K")
     ap.add_argument("--gemm-iters", type=int, default=20)
     ap.add_argument("--gemm-kernel", choices=sorted(GEMM_KERNELS), default="auto")
+    ap.add_argument("--gemm-random", action="store_true", help="random bf16 operands (rate only, no checksum)")
     a = ap.parse_args(argv)
     if a.gemm:
-        res = gemm_rate(a.device, a.gemm, a.gemm, a.gemm, a.gemm_iters, kernel=a.gemm_kernel)
+        res = gemm_rate(a.device, a.gemm, a.gemm, a.gemm, a.gemm_iters, kernel=a.gemm_kernel,
+                        random_data=a.gemm_random)
         print(json.dumps(res))
-        return 0 if res["errors"] == 0 else 1
+        return 0 if not res["errors"] else 1
     res = run(a.device, a.bytes, a.passes, a.mfma_iters)
     print(json.dumps(res))
     return 0 if res["ok"] else 1

@@ -31,11 +31,11 @@ for s in ${STEPS:-pytest smoke bench prof}; do
               (cd /tmp && export TMPDIR=/tmp && step "pmc_$tag" 90 rocprofv3 --pmc $ctr --kernel-trace --stats -d "$OUT/pmc_$tag" -o canary --output-format csv -- python3 -m k8s_gpu_device_plugin_amd.ops.canary --device 0 --bytes 1073741824 --passes 1) || exit $?
             done ;;
     gemmprof)  # matrix-path canary kernel: trace + one PMC group per pass
-            (cd /tmp && export TMPDIR=/tmp && step rocprof_gemm 120 rocprofv3 --kernel-trace --stats -d "$OUT/prof_gemm" -o gemm --output-format csv -- python3 -m k8s_gpu_device_plugin_amd.ops.canary --gemm 4096) || exit $?
-            IFS=';' read -r -a ctrs <<< "${GEMM_PMC:-SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_LDS_ADDR_CONFLICT;SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16;FETCH_SIZE;GRBM_GUI_ACTIVE}"
+            (cd /tmp && export TMPDIR=/tmp && step rocprof_gemm 120 rocprofv3 --kernel-trace --stats -d "$OUT/prof_gemm" -o gemm --output-format csv -- python3 -m k8s_gpu_device_plugin_amd.ops.canary ${GEMM_ARGS:---gemm 4096}) || exit $?
+            IFS=';' read -r -a ctrs <<< "${GEMM_PMC:-SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_LDS_ADDR_CONFLICT;SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16;FETCH_SIZE;GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY}"
             for ctr in "${ctrs[@]}"; do
               tag=$(echo "$ctr" | tr ' ' '_')
-              (cd /tmp && export TMPDIR=/tmp && step "gemm_pmc_$tag" 90 rocprofv3 --pmc $ctr --kernel-trace --stats -d "$OUT/gemm_pmc_$tag" -o gemm --output-format csv -- python3 -m k8s_gpu_device_plugin_amd.ops.canary --gemm 4096 --gemm-iters 5) || exit $?
+              (cd /tmp && export TMPDIR=/tmp && step "gemm_pmc_$tag" 90 rocprofv3 --pmc $ctr --kernel-trace --stats -d "$OUT/gemm_pmc_$tag" -o gemm --output-format csv -- python3 -m k8s_gpu_device_plugin_amd.ops.canary ${GEMM_ARGS:---gemm 4096} --gemm-iters 5) || exit $?
             done ;;
   esac
 done

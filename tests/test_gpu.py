@@ -383,6 +383,8 @@ def test_lds_gemm_rate_and_abft():
             "print(2*4096**3*20/(time.perf_counter()-t)/1e12)")
     out = subprocess.run([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True, timeout=90)
     blas = float(out.stdout.strip().splitlines()[-1]) if out.returncode == 0 else float("nan")
-    print("GEMM canary %s TFLOP/s (integer data), torch.matmul %.0f TFLOP/s (random data)"
-          % (" / ".join("%s %.0f" % kv for kv in rates.items()), blas))
+    rnd = canary.gemm_rate(0, 4096, 4096, 4096, iters=20, random_data=True)
+    assert rnd["errors"] is None and rnd["tflops"] > 200, rnd
+    print("GEMM canary %s TFLOP/s (integer data), %.0f (auto kernel, random data); torch.matmul %.0f TFLOP/s "
+          "(random data)" % (" / ".join("%s %.0f" % kv for kv in rates.items()), rnd["tflops"], blas))
     assert min(rates.values()) > 200
