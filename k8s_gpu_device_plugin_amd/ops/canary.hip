@@ -403,7 +403,9 @@ __global__ void __launch_bounds__(512) gemm256(const short* __restrict__ A, cons
 // kBEarly of a wave's 4 B pieces of tile t+2 go with its A-h0 pieces in L(t,1), the rest
 // with the A-h1 pieces in L(t+1,0): the split balances DMA issue between the two L
 // sections (L0 also carries twice L1's ds_reads).
-template <int kBEarly>
+// kG1Early: group 1 issues each refill from the MFMA section one interval earlier (the
+// first interval its region is free) instead of from its next LDS-read section.
+template <int kBEarly, bool kG1Early = false>
 __global__ void __launch_bounds__(512) gemm256s(const short* __restrict__ A, const short* __restrict__ Bt,
                                                float* __restrict__ C, int M, int N, int K) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kBStage];  // the only LDS object
@@ -485,7 +487,7 @@ __global__ void __launch_bounds__(512) gemm256s(const short* __restrict__ A, con
     const short* As = reinterpret_cast<const short*>(smem + (t & 1) * kBStage);
     const short* Bs = As + kBT * kBK;
     // L0
-    if (t >= 1 && t + 1 < T) stage_ah1(t + 1);
+    if ((!kG1Early || !g1) && t >= 1 && t + 1 < T) stage_ah1(t + 1);
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
@@ -496,6 +498,7 @@ __global__ void __launch_bounds__(512) gemm256s(const short* __restrict__ A, con
       for (int i = 0; i < 4; ++i) a[i][s2] = frag(As, wr * 128 + i * 16 + r16, 4 * s2 + q);
     section_end();
     // M0
+    if (kG1Early && g1 && t + 2 < T) stage_b_ah0(t + 2);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
@@ -507,7 +510,7 @@ __global__ void __launch_bounds__(512) gemm256s(const short* __restrict__ A, con
     __builtin_amdgcn_s_setprio(0);
     section_end();
     // L1
-    if (t + 2 < T) stage_b_ah0(t + 2);
+    if ((!kG1Early || !g1) && t + 2 < T) stage_b_ah0(t + 2);
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
@@ -515,6 +518,7 @@ __global__ void __launch_bounds__(512) gemm256s(const short* __restrict__ A, con
     if (g1) retire(t);
     section_end();
     // M1
+    if (kG1Early && g1 && t + 2 < T) stage_ah1(t + 2);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
@@ -954,7 +958,7 @@ int amdgpu_canary_mfma_gemm(int device, const unsigned short* a_host, const unsi
 int pick_gemm(int M, int N, int K, int kernel) {
   if (M <= 0 || N <= 0 || K <= 0 || K % kTileK) return 0;
   const bool fits256 = M % kBT == 0 && N % kBT == 0, fits128 = M % kTileM == 0 && N % kTileN == 0;
-  if (kernel >= 2 && kernel <= 6) return fits256 ? kernel : 0;
+  if (kernel >= 2 && kernel <= 7) return fits256 ? kernel : 0;
   if (kernel == 1) return fits128 ? 1 : 0;
   if (kernel != 0) return 0;
   if (fits256 && (M / kBT) * (N / kBT) >= 256) return 3;
@@ -971,6 +975,8 @@ void launch_gemm(int kind, const short* a, const short* b, float* c, int M, int 
     hipLaunchKernelGGL(gemm256s<0>, g256, b256, 0, 0, a, b, c, M, N, K);
   else if (kind == 6)
     hipLaunchKernelGGL(gemm256s<3>, g256, b256, 0, 0, a, b, c, M, N, K);
+  else if (kind == 7)
+    hipLaunchKernelGGL((gemm256s<4, true>), g256, b256, 0, 0, a, b, c, M, N, K);
   else if (kind == 2)
     hipLaunchKernelGGL(gemm256, dim3((M / kBT) * (N / kBT)), dim3(512), 0, 0, a, b, c, M, N, K);
   else

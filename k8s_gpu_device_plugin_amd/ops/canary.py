@@ -129,7 +129,7 @@ def mfma_gemm(a_bf16_bits, b_bf16_bits, device: int = 0):
     return c
 
 
-GEMM_KERNELS = {"auto": 0, "lds128": 1, "pingpong256": 2, "pingpong256s": 3, "pingpong256s_b2": 4, "pingpong256s_b0": 5, "pingpong256s_b3": 6}
+GEMM_KERNELS = {"auto": 0, "lds128": 1, "pingpong256": 2, "pingpong256s": 3, "pingpong256s_b2": 4, "pingpong256s_b0": 5, "pingpong256s_b3": 6, "pingpong256s_g1early": 7}
 
 
 def gemm(a_bf16_bits, bt_bf16_bits, device: int = 0, kernel: str = "auto"):
