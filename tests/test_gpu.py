@@ -51,14 +51,26 @@ def test_amdsmi_sample_cost_breakdown(amdsmi_backend):
     request path, but 8 GPUs x 8 partitions must fit a 1 s tick with room to spare)."""
     amdsmi_backend.discover()
     before = amdsmi_backend.sample_costs()
-    for _ in range(20):
-        assert amdsmi_backend.sample(0).ok
+    first = amdsmi_backend.sample(0)
+    assert first.ok
+    samples = [amdsmi_backend.sample(0) for _ in range(19)]
+    assert all(x.ok for x in samples)
     after = amdsmi_backend.sample_costs()
-    per = {k: (after[k][0] - before[k][0]) / 20 * 1e6 for k in after}
+    per = {k: (after[k][0] - before[k][0]) / 20 * 1e6 for k in after if not k.startswith("xgmi_links_")}
+    paths = {k: after[k][1] - before[k][1] for k in after if k.startswith("xgmi_links_")}
     print("amdsmi sample cost per GPU (us):", {k: round(v, 1) for k, v in per.items()},
-          "total %.1f us" % sum(per.values()))
+          "total %.1f us" % sum(per.values()), "link paths", paths)
     assert set(per) == {"gpu_metrics", "vram_usage", "ecc_count", "xgmi_links", "bad_pages"}
     assert sum(per.values()) < 50e3
+    # samples served from the gpu_metrics blob report the same links as the full path,
+    # with byte counters that never run backwards
+    for x in samples:
+        assert [lk[0] for lk in x.links] == [lk[0] for lk in first.links]
+        assert [lk[1] for lk in x.links] == [lk[1] for lk in first.links]
+        assert [lk[4:] for lk in x.links] == [lk[4:] for lk in first.links]
+    for prev, cur in zip([first] + samples, samples):
+        for a, b in zip(prev.links, cur.links):
+            assert b[2] >= a[2] and b[3] >= a[3], (a, b)
 
 
 def test_amdsmi_retired_pages(amdsmi_backend):
