@@ -405,11 +405,14 @@ __global__ void __launch_bounds__(512) gemm256(const short* __restrict__ A, cons
 // sections (L0 also carries twice L1's ds_reads).
 // kG1Early: group 1 issues each refill from the MFMA section one interval earlier (the
 // first interval its region is free) instead of from its next LDS-read section.
-template <int kBEarly, bool kG1Early = false>
+// kScalarWave: the wave index goes through readfirstlane, so everything derived from it
+// (LDS piece addresses -> M0, group branches) is scalar instead of per-lane.
+template <int kBEarly, bool kG1Early = false, bool kScalarWave = true>
 __global__ void __launch_bounds__(512) gemm256s(const short* __restrict__ A, const short* __restrict__ Bt,
                                                float* __restrict__ C, int M, int N, int K) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kBStage];  // the only LDS object
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = kScalarWave ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
   const int nbm = M / kBT, nbn = N / kBT;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   constexpr int kGroupM = 4;
@@ -958,7 +961,7 @@ int amdgpu_canary_mfma_gemm(int device, const unsigned short* a_host, const unsi
 int pick_gemm(int M, int N, int K, int kernel) {
   if (M <= 0 || N <= 0 || K <= 0 || K % kTileK) return 0;
   const bool fits256 = M % kBT == 0 && N % kBT == 0, fits128 = M % kTileM == 0 && N % kTileN == 0;
-  if (kernel >= 2 && kernel <= 7) return fits256 ? kernel : 0;
+  if (kernel >= 2 && kernel <= 8) return fits256 ? kernel : 0;
   if (kernel == 1) return fits128 ? 1 : 0;
   if (kernel != 0) return 0;
   if (fits256 && (M / kBT) * (N / kBT) >= 256) return 3;
@@ -977,6 +980,8 @@ void launch_gemm(int kind, const short* a, const short* b, float* c, int M, int 
     hipLaunchKernelGGL(gemm256s<3>, g256, b256, 0, 0, a, b, c, M, N, K);
   else if (kind == 7)
     hipLaunchKernelGGL((gemm256s<4, true>), g256, b256, 0, 0, a, b, c, M, N, K);
+  else if (kind == 8)
+    hipLaunchKernelGGL((gemm256s<4, false, false>), g256, b256, 0, 0, a, b, c, M, N, K);
   else if (kind == 2)
     hipLaunchKernelGGL(gemm256, dim3((M / kBT) * (N / kBT)), dim3(512), 0, 0, a, b, c, M, N, K);
   else
