@@ -407,7 +407,8 @@ __global__ void __launch_bounds__(512) gemm256(const short* __restrict__ A, cons
 // first interval its region is free) instead of from its next LDS-read section.
 // kScalarWave: the wave index goes through readfirstlane, so everything derived from it
 // (LDS piece addresses -> M0, group branches) is scalar instead of per-lane.
-template <int kBEarly, bool kG1Early = false, bool kScalarWave = true>
+// kGroupM: tile rows per raster group; kPrio: raise wave priority around MFMA sections.
+template <int kBEarly, bool kG1Early = false, bool kScalarWave = true, int kGroupM = 4, bool kPrio = true>
 __global__ void __launch_bounds__(512) gemm256s(const short* __restrict__ A, const short* __restrict__ Bt,
                                                float* __restrict__ C, int M, int N, int K) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kBStage];  // the only LDS object
@@ -415,7 +416,6 @@ __global__ void __launch_bounds__(512) gemm256s(const short* __restrict__ A, con
   const int wave = kScalarWave ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
   const int nbm = M / kBT, nbn = N / kBT;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  constexpr int kGroupM = 4;
   const int per_group = kGroupM * nbn, first_m = (wg / per_group) * kGroupM;
   const int gm = nbm - first_m < kGroupM ? nbm - first_m : kGroupM;
   const int m0 = (first_m + (wg % per_group) % gm) * kBT, n0 = ((wg % per_group) / gm) * kBT;
@@ -502,7 +502,7 @@ __global__ void __launch_bounds__(512) gemm256s(const short* __restrict__ A, con
     section_end();
     // M0
     if (kG1Early && g1 && t + 2 < T) stage_b_ah0(t + 2);
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (kPrio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
@@ -510,7 +510,7 @@ __global__ void __launch_bounds__(512) gemm256s(const short* __restrict__ A, con
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[0][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][s2], b[j][s2], acc[0][i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (kPrio) __builtin_amdgcn_s_setprio(0);
     section_end();
     // L1
     if ((!kG1Early || !g1) && t + 2 < T) stage_b_ah0(t + 2);
@@ -522,7 +522,7 @@ __global__ void __launch_bounds__(512) gemm256s(const short* __restrict__ A, con
     section_end();
     // M1
     if (kG1Early && g1 && t + 2 < T) stage_ah1(t + 2);
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (kPrio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
@@ -530,7 +530,7 @@ __global__ void __launch_bounds__(512) gemm256s(const short* __restrict__ A, con
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[1][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][s2], b[j][s2], acc[1][i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (kPrio) __builtin_amdgcn_s_setprio(0);
     if (!g1) retire(t);
     section_end();
   }
@@ -961,7 +961,7 @@ int amdgpu_canary_mfma_gemm(int device, const unsigned short* a_host, const unsi
 int pick_gemm(int M, int N, int K, int kernel) {
   if (M <= 0 || N <= 0 || K <= 0 || K % kTileK) return 0;
   const bool fits256 = M % kBT == 0 && N % kBT == 0, fits128 = M % kTileM == 0 && N % kTileN == 0;
-  if (kernel >= 2 && kernel <= 8) return fits256 ? kernel : 0;
+  if (kernel >= 2 && kernel <= 11) return fits256 ? kernel : 0;
   if (kernel == 1) return fits128 ? 1 : 0;
   if (kernel != 0) return 0;
   if (fits256 && (M / kBT) * (N / kBT) >= 256) return 3;
@@ -982,6 +982,12 @@ void launch_gemm(int kind, const short* a, const short* b, float* c, int M, int 
     hipLaunchKernelGGL((gemm256s<4, true>), g256, b256, 0, 0, a, b, c, M, N, K);
   else if (kind == 8)
     hipLaunchKernelGGL((gemm256s<4, false, false>), g256, b256, 0, 0, a, b, c, M, N, K);
+  else if (kind == 9)
+    hipLaunchKernelGGL((gemm256s<4, false, true, 2>), g256, b256, 0, 0, a, b, c, M, N, K);
+  else if (kind == 10)
+    hipLaunchKernelGGL((gemm256s<4, false, true, 8>), g256, b256, 0, 0, a, b, c, M, N, K);
+  else if (kind == 11)
+    hipLaunchKernelGGL((gemm256s<4, false, true, 4, false>), g256, b256, 0, 0, a, b, c, M, N, K);
   else if (kind == 2)
     hipLaunchKernelGGL(gemm256, dim3((M / kBT) * (N / kBT)), dim3(512), 0, 0, a, b, c, M, N, K);
   else

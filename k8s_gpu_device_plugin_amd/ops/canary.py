@@ -132,7 +132,8 @@ def mfma_gemm(a_bf16_bits, b_bf16_bits, device: int = 0):
 # kernel ids of amdgpu_canary_gemm*: "auto" picks pingpong256s for >= 256 tiles of 256x256, else lds128; the
 # pingpong256s_* entries are the ablations in profiles/gemm_r1/SUMMARY.md
 GEMM_KERNELS = {"auto": 0, "lds128": 1, "pingpong256": 2, "pingpong256s": 3, "pingpong256s_b2": 4,
-                "pingpong256s_b0": 5, "pingpong256s_b3": 6, "pingpong256s_g1early": 7, "pingpong256s_vwave": 8}
+                "pingpong256s_b0": 5, "pingpong256s_b3": 6, "pingpong256s_g1early": 7, "pingpong256s_vwave": 8,
+                "pingpong256s_group2": 9, "pingpong256s_group8": 10, "pingpong256s_noprio": 11}
 
 
 def gemm(a_bf16_bits, bt_bf16_bits, device: int = 0, kernel: str = "auto"):
