@@ -270,6 +270,17 @@ constexpr int kBOp = kBT * kBK * 2;  // one operand tile, 32 KiB
 constexpr int kBStage = 2 * kBOp;    // A + B of one K-tile, 64 KiB
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 
+// Output tile of this workgroup: XCD-aware bijective remap, then tiles rastered in groups
+// of `group` tile rows so one XCD's consecutive workgroups share A and B panels in L2.
+__device__ __forceinline__ void tile_origin256(int M, int N, int group, int* m0, int* n0) {
+  const int nbm = M / kBT, nbn = N / kBT;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_group = group * nbn, first_m = (wg / per_group) * group;
+  const int gm = nbm - first_m < group ? nbm - first_m : group;
+  *m0 = (first_m + (wg % per_group) % gm) * kBT;
+  *n0 = ((wg % per_group) / gm) * kBT;
+}
+
 __device__ __forceinline__ void section_end() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this section's LDS reads are done
   __builtin_amdgcn_s_barrier();
@@ -281,12 +292,8 @@ __global__ void __launch_bounds__(512) gemm256(const short* __restrict__ A, cons
                                               float* __restrict__ C, int M, int N, int K) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kBStage];  // the only LDS object
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nbm = M / kBT, nbn = N / kBT;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  constexpr int kGroupM = 4;
-  const int per_group = kGroupM * nbn, first_m = (wg / per_group) * kGroupM;
-  const int gm = nbm - first_m < kGroupM ? nbm - first_m : kGroupM;
-  const int m0 = (first_m + (wg % per_group) % gm) * kBT, n0 = ((wg % per_group) / gm) * kBT;
+  int m0, n0;
+  tile_origin256(M, N, 4, &m0, &n0);
   if (m0 + kBT > M || n0 + kBT > N) return;  // host checks shapes (block-uniform exit)
   const int wr = wave >> 2, wc = wave & 3;
   const bool g1 = wr == 1;
@@ -414,11 +421,8 @@ __global__ void __launch_bounds__(512) gemm256s(const short* __restrict__ A, con
   __shared__ __attribute__((aligned(16))) char smem[2 * kBStage];  // the only LDS object
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = kScalarWave ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
-  const int nbm = M / kBT, nbn = N / kBT;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int per_group = kGroupM * nbn, first_m = (wg / per_group) * kGroupM;
-  const int gm = nbm - first_m < kGroupM ? nbm - first_m : kGroupM;
-  const int m0 = (first_m + (wg % per_group) % gm) * kBT, n0 = ((wg % per_group) / gm) * kBT;
+  int m0, n0;
+  tile_origin256(M, N, kGroupM, &m0, &n0);
   if (m0 + kBT > M || n0 + kBT > N) return;  // host checks shapes (block-uniform exit)
   const int wr = wave >> 2, wc = wave & 3;
   const bool g1 = wr == 1;
