@@ -20,7 +20,9 @@ from __future__ import annotations
 
 import os
 
-from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
+# The protobuf runtime (~30 ms to import and build) is loaded on first use of a message
+# class: the native daemon path needs only the constants and method paths below, so
+# start-up does not pay for it (PEP 562 module __getattr__).
 
 VERSION = "v1beta1"
 DEVICE_PLUGIN_PATH = "/var/lib/kubelet/device-plugins/"
@@ -40,10 +42,10 @@ METHOD_GET_PREFERRED = "/%s/GetPreferredAllocation" % DEVICE_PLUGIN_SERVICE
 METHOD_ALLOCATE = "/%s/Allocate" % DEVICE_PLUGIN_SERVICE
 METHOD_PRE_START = "/%s/PreStartContainer" % DEVICE_PLUGIN_SERVICE
 
-_F = descriptor_pb2.FieldDescriptorProto
-_STR, _BOOL, _I32, _I64, _MSG = (_F.TYPE_STRING, _F.TYPE_BOOL, _F.TYPE_INT32,
-                                  _F.TYPE_INT64, _F.TYPE_MESSAGE)
-_OPT, _REP = _F.LABEL_OPTIONAL, _F.LABEL_REPEATED
+# FieldDescriptorProto enum values (descriptor.proto: TYPE_STRING = 9, TYPE_BOOL = 8,
+# TYPE_INT32 = 5, TYPE_INT64 = 3, TYPE_MESSAGE = 11; LABEL_OPTIONAL = 1, LABEL_REPEATED = 3)
+_STR, _BOOL, _I32, _I64, _MSG = 9, 8, 5, 3, 11
+_OPT, _REP = 1, 3
 
 # (message name, [(field name, number, type, label, type_name or None)])
 _MESSAGES = [
@@ -105,7 +107,8 @@ _SERVICES = [
 ]
 
 
-def _build_file() -> descriptor_pb2.FileDescriptorProto:
+def _build_file():
+    from google.protobuf import descriptor_pb2
     fdp = descriptor_pb2.FileDescriptorProto()
     fdp.name = "k8s_gpu_device_plugin_amd/deviceplugin/v1beta1/api.proto"
     fdp.package = PACKAGE
@@ -138,44 +141,62 @@ def _build_file() -> descriptor_pb2.FileDescriptorProto:
     return fdp
 
 
-FILE_DESCRIPTOR_PROTO = _build_file()
-_POOL = descriptor_pool.DescriptorPool()
-FILE_DESCRIPTOR = _POOL.Add(FILE_DESCRIPTOR_PROTO)
+_CLASS_NAMES = [name for name, _ in _MESSAGES]
+_LAZY = set(_CLASS_NAMES) | {"FILE_DESCRIPTOR_PROTO", "FILE_DESCRIPTOR", "METHODS"}
+_loaded = False
 
 
-def _cls(name: str):
-    return message_factory.GetMessageClass(_POOL.FindMessageTypeByName(PACKAGE + "." + name))
+def _load() -> None:
+    """Builds the descriptor pool and message classes into this module (idempotent)."""
+    global _loaded
+    if _loaded:
+        return
+    from google.protobuf import descriptor_pool, message_factory
+    g = globals()
+    fdp = _build_file()
+    pool = descriptor_pool.DescriptorPool()
+    fd = pool.Add(fdp)
+
+    def cls(name: str):
+        return message_factory.GetMessageClass(pool.FindMessageTypeByName(PACKAGE + "." + name))
+
+    for name in _CLASS_NAMES:
+        g[name] = cls(name)
+    # method path -> (request class, response class, server_streaming)
+    g["METHODS"] = {"/%s.%s/%s" % (PACKAGE, sname, mname): (g[inp], g[out], stream)
+                    for sname, methods in _SERVICES for mname, inp, out, stream in methods}
+    g["FILE_DESCRIPTOR_PROTO"], g["FILE_DESCRIPTOR"] = fdp, fd
+    _loaded = True
 
 
-DevicePluginOptions = _cls("DevicePluginOptions")
-RegisterRequest = _cls("RegisterRequest")
-Empty = _cls("Empty")
-ListAndWatchResponse = _cls("ListAndWatchResponse")
-TopologyInfo = _cls("TopologyInfo")
-NUMANode = _cls("NUMANode")
-Device = _cls("Device")
-PreStartContainerRequest = _cls("PreStartContainerRequest")
-PreStartContainerResponse = _cls("PreStartContainerResponse")
-PreferredAllocationRequest = _cls("PreferredAllocationRequest")
-ContainerPreferredAllocationRequest = _cls("ContainerPreferredAllocationRequest")
-PreferredAllocationResponse = _cls("PreferredAllocationResponse")
-ContainerPreferredAllocationResponse = _cls("ContainerPreferredAllocationResponse")
-AllocateRequest = _cls("AllocateRequest")
-ContainerAllocateRequest = _cls("ContainerAllocateRequest")
-CDIDevice = _cls("CDIDevice")
-AllocateResponse = _cls("AllocateResponse")
-ContainerAllocateResponse = _cls("ContainerAllocateResponse")
-Mount = _cls("Mount")
-DeviceSpec = _cls("DeviceSpec")
-
-# method path -> (request class, response class, server_streaming)
-METHODS = {}
-for _sname, _methods in _SERVICES:
-    for _mname, _inp, _out, _stream in _methods:
-        METHODS["/%s.%s/%s" % (PACKAGE, _sname, _mname)] = (_cls(_inp), _cls(_out), _stream)
+def __getattr__(name: str):
+    if name in _LAZY:
+        _load()
+        return globals()[name]
+    raise AttributeError("module %r has no attribute %r" % (__name__, name))
 
 
 def plugin_options(pre_start_required: bool = False) -> "DevicePluginOptions":
     """Options the plugin advertises (``plugin/plugin.go:165-170``)."""
-    return DevicePluginOptions(pre_start_required=pre_start_required,
-                               get_preferred_allocation_available=True)
+    _load()
+    return globals()["DevicePluginOptions"](pre_start_required=pre_start_required,
+                                            get_preferred_allocation_available=True)
+
+
+def _ld(field: int, payload: bytes) -> bytes:  # length-delimited field (len < 2**14 here)
+    n = len(payload)
+    ln = bytes([n]) if n < 0x80 else bytes([(n & 0x7F) | 0x80, n >> 7])
+    return bytes([(field << 3) | 2]) + ln + payload
+
+
+def encode_register_request(endpoint: str, resource_name: str, pre_start_required: bool = False,
+                            version: str = VERSION) -> bytes:
+    """``RegisterRequest`` wire bytes without the protobuf runtime, byte-identical to
+    ``RegisterRequest(...).SerializeToString()`` (proto3: fields in number order, empty
+    strings and false bools omitted; ``tests/test_v1beta1_wire.py`` checks it)."""
+    opts = (b"\x08\x01" if pre_start_required else b"") + b"\x10\x01"
+    out = b""
+    for num, val in ((1, version), (2, endpoint), (3, resource_name)):
+        if val:
+            out += _ld(num, val.encode())
+    return out + _ld(4, opts)

@@ -335,8 +335,10 @@ def startup(runs=5):
     rereg = []
     try:
         for i in range(runs):
-            t0 = time.perf_counter()
-            node.kubelet.restart()
+            node.kubelet.stop()  # kubelet gone (its socket removed) ...
+            time.sleep(0.05)
+            t0 = time.perf_counter()  # ... and back: the clock starts when kubelet.sock reappears
+            node.kubelet.start()
             node.kubelet.wait_for_registrations(i + 2, timeout=30)
             rereg.append(time.perf_counter() - t0)
             time.sleep(0.05)  # let the plugin's Register call return before the next restart

@@ -20,8 +20,6 @@ import re
 from dataclasses import dataclass, field
 from typing import Any
 
-import yaml
-
 from .api import v1beta1
 
 STRATEGIES = ("none", "single", "mixed")
@@ -287,6 +285,7 @@ def load(config_file: str | None = "config", search_dirs=(".",), environ=None, r
             raise ConfigError("config file not found: %s" % candidates)
     if path:
         with open(path, "r", encoding="utf-8") as f:
+            import yaml  # only when a config file is read
             raw = yaml.safe_load(f) or {}
     unknown = unknown_keys(raw)
     if unknown:

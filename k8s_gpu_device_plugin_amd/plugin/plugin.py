@@ -28,8 +28,6 @@ import os
 import threading
 import time
 
-import grpc
-
 from .. import native
 from ..api import v1beta1
 from ..device import Devices
@@ -51,8 +49,11 @@ def _unix_target(path: str) -> str:
     return "unix://" + os.path.abspath(path)
 
 
-def dial(path: str, timeout: float = DIAL_TIMEOUT_S) -> grpc.Channel:
-    """Blocking dial of a unix socket (reference ``dial`` ``plugin/plugin.go:231-246``)."""
+def dial(path: str, timeout: float = DIAL_TIMEOUT_S) -> "grpc.Channel":
+    """Blocking dial of a unix socket (reference ``dial`` ``plugin/plugin.go:231-246``).
+    grpcio is imported on demand: the native path (server, Register, self-check) never
+    loads it, which keeps ~70 ms of imports out of start-up."""
+    import grpc
     ch = grpc.insecure_channel(_unix_target(path), options=[("grpc.enable_http_proxy", 0)])
     try:
         grpc.channel_ready_future(ch).result(timeout=timeout)
@@ -62,7 +63,7 @@ def dial(path: str, timeout: float = DIAL_TIMEOUT_S) -> grpc.Channel:
     return ch
 
 
-def close_async(ch: grpc.Channel) -> None:
+def close_async(ch: "grpc.Channel") -> None:
     """grpcio's Channel.close() joins its polling thread, which wakes every 200 ms:
     closing inline would add up to 0.2 s to each start-up and registration."""
     threading.Thread(target=ch.close, name="grpc-channel-close", daemon=True).start()
@@ -228,6 +229,7 @@ class AmdDevicePlugin:
         self._native_server = srv
 
     def _start_grpcio_server(self) -> None:
+        import grpc
         server = grpc.server(concurrent.futures.ThreadPoolExecutor(
             max_workers=max(4, self.cfg.grpc.threads if self.cfg is not None else 4),
             thread_name_prefix="dp-" + self.resource.get_resource_name()))
@@ -274,11 +276,26 @@ class AmdDevicePlugin:
         self._serving = True
 
     def register(self) -> None:
+        """Registration.Register with kubelet (``plugin/plugin.go:139-162``).  Sent by the
+        compiled HTTP/2 client when the native module has one (no grpcio import, no
+        channel teardown), else over a grpcio channel."""
         if not os.path.exists(self.kubelet_socket):  # fail fast instead of a 5 s dial timeout
             raise FileNotFoundError("kubelet socket %s does not exist" % self.kubelet_socket)
+        pre_start = bool(self.cfg.health.canaryOnPreStart) if self.cfg is not None else False
+        n = native.load()
+        if hasattr(n, "H2Client"):
+            req = v1beta1.encode_register_request(os.path.basename(self.socket), str(self.resource), pre_start)
+            c = n.H2Client(self.kubelet_socket, DIAL_TIMEOUT_S)
+            try:
+                status, _, message = c.unary(v1beta1.METHOD_REGISTER, req)
+            finally:
+                c.close()
+            if status != 0:
+                raise RuntimeError("Register with kubelet failed: grpc-status %d %s" % (status, message))
+            self.registered = True
+            return
         ch = dial(self.kubelet_socket, DIAL_TIMEOUT_S)
         try:
-            pre_start = bool(self.cfg.health.canaryOnPreStart) if self.cfg is not None else False
             req = v1beta1.RegisterRequest(version=v1beta1.VERSION, endpoint=os.path.basename(self.socket),
                                           resource_name=str(self.resource),
                                           options=v1beta1.plugin_options(pre_start_required=pre_start))
@@ -322,6 +339,7 @@ class AmdDevicePlugin:
 
     # ------------------------------------------------------------------ RPCs (grpcio)
     def _handler(self):
+        import grpc
         n = native.load()
         table = self.table
         rpc_opt, rpc_law, rpc_pref, rpc_alloc, rpc_pre = (n.RPC_OPTIONS, n.RPC_LIST_AND_WATCH, n.RPC_PREFERRED,

@@ -145,3 +145,25 @@ def test_native_preferred_encoding(n):
 def test_options_bytes(n, size):
     t = _table(n, DEVS)
     assert v.DevicePluginOptions.FromString(t.options()).get_preferred_allocation_available
+
+
+@pytest.mark.parametrize("pre_start", [False, True])
+@pytest.mark.parametrize("endpoint,resource", [("amd-gpu.sock", "amd.com/gpu"), ("a" * 300, "amd.com/cpx_nps4"),
+                                               ("", "")])
+def test_protobuf_free_register_request_matches_runtime(pre_start, endpoint, resource):
+    """The native Register path encodes RegisterRequest by hand; it must be byte-identical
+    to the protobuf runtime's serialisation."""
+    want = v.RegisterRequest(version=v.VERSION, endpoint=endpoint, resource_name=resource,
+                             options=v.plugin_options(pre_start)).SerializeToString()
+    assert v.encode_register_request(endpoint, resource, pre_start) == want
+
+
+def test_daemon_imports_stay_light():
+    """Start-up path: the CLI and manager import neither grpcio, protobuf nor PyYAML (the
+    native servers, the compiled Register client and lazy v1beta1 classes need none)."""
+    import subprocess
+    import sys
+    code = ("import sys, k8s_gpu_device_plugin_amd.cli, k8s_gpu_device_plugin_amd.plugin.manager;"
+            "print(sorted(m for m in ('grpc', 'google.protobuf', 'yaml') if m in sys.modules))")
+    out = subprocess.run([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True, check=True)
+    assert out.stdout.strip() == "[]"
