@@ -27,6 +27,9 @@ namespace {
 
 std::mutex g_init_mu;
 int g_init_refs = 0;
+// A successful amdsmi_available() keeps its session open as one reference, which the next
+// backend adopts: amdsmi_init costs ~25 ms on MI355X, and start-up probes and then opens.
+bool g_probe_ref = false;
 
 std::string status_str(amdsmi_status_t st) {
   const char* s = nullptr;
@@ -100,14 +103,23 @@ bool amdsmi_available() {
   if (amdsmi_init(AMDSMI_INIT_AMD_GPUS) != AMDSMI_STATUS_SUCCESS) return false;
   uint32_t n = 0;
   const bool ok = amdsmi_get_socket_handles(&n, nullptr) == AMDSMI_STATUS_SUCCESS && n > 0;
-  amdsmi_shut_down();
-  return ok;
+  if (!ok) {
+    amdsmi_shut_down();
+    return false;
+  }
+  g_init_refs = 1;  // held for the backend that usually follows
+  g_probe_ref = true;
+  return true;
 }
 
 class AmdSmiBackend : public Backend {
  public:
   AmdSmiBackend() {
     std::lock_guard<std::mutex> lk(g_init_mu);
+    if (g_probe_ref) {
+      g_probe_ref = false;  // adopt the probe's session and its reference
+      return;
+    }
     if (g_init_refs == 0) check(amdsmi_init(AMDSMI_INIT_AMD_GPUS), "amdsmi_init");
     ++g_init_refs;
   }
