@@ -44,6 +44,7 @@ struct Ctx {
   // score() scratch, reused across the (up to thousands of) candidate evaluations
   mutable std::vector<int> taken;
   mutable std::vector<uint64_t> whole_free;
+  mutable std::vector<int> cnt;  // per-class counts of the set being scored
   // pair_score depends only on (gpu, numa) of the two devices: one matrix over those
   // classes replaces the per-pair topology lookups in score()
   std::vector<int> cls;                // device -> class
@@ -101,6 +102,7 @@ struct Ctx {
     }
     ncls = static_cast<int>(keys.size());
     cls_pair.assign(static_cast<size_t>(ncls) * ncls, kUnset);
+    cnt.assign(ncls, 0);
   }
 
   // Largest set of GPUs in `mask` that are pairwise connected by healthy links.
@@ -122,18 +124,28 @@ struct Ctx {
 
   // score of choosing set S (device indices) out of the available pool
   double score(const std::vector<int>& S) const {
+    std::fill(cnt.begin(), cnt.end(), 0);
+    for (int i : S) cnt[cls[i]]++;
+    return score_counts(cnt);
+  }
+
+  // Same score from per-class counts: devices of one (gpu, numa) class are
+  // interchangeable for every term, so a candidate costs O(classes^2 + gpus) instead of
+  // O(|S|^2) - the multi-GPU greedy/local search evaluates hundreds of candidates.
+  double score_counts(const std::vector<int>& cn) const {
     double s = 0;
-    for (size_t i = 0; i < S.size(); ++i)
-      for (size_t j = i + 1; j < S.size(); ++j) s += class_pair(cls[S[i]], cls[S[j]]);
-    // per-gpu usage after taking S
     std::fill(taken.begin(), taken.end(), 0);
-    for (int i : S)
-      if (devs[i].gpu >= 0) taken[devs[i].gpu]++;
-    bool multi_gpu = false;
     int first_gpu = -2;
-    for (int i : S) {
-      if (first_gpu == -2) first_gpu = devs[i].gpu;
-      else if (devs[i].gpu != first_gpu) multi_gpu = true;
+    bool multi_gpu = false;
+    for (int a = 0; a < ncls; ++a) {
+      if (!cn[a]) continue;
+      const int g = devs[cls_rep[a]].gpu;
+      if (first_gpu == -2) first_gpu = g;
+      else if (g != first_gpu) multi_gpu = true;
+      if (g >= 0) taken[g] += cn[a];
+      s += 0.5 * cn[a] * (cn[a] - 1) * class_pair(a, a);
+      for (int b = a + 1; b < ncls; ++b)
+        if (cn[b]) s += static_cast<double>(cn[a]) * cn[b] * class_pair(a, b);
     }
     for (int g = 0; g < ngpu; ++g) {
       if (!taken[g]) continue;
@@ -275,43 +287,59 @@ AllocResult aligned_alloc(const Topology& topo, const std::vector<AllocDevice>& 
         seen.push_back(key);
         return true;
       };
+      // class counts of S, updated in place around each candidate evaluation
+      std::vector<int> cn(ctx.ncls, 0);
+      for (int i : required) cn[ctx.cls[i]]++;
       while (static_cast<int>(S.size()) < size) {
         int pick = -1;
         double ps = -1e300;
-        S.push_back(-1);
         seen.clear();
         for (int c : cand) {
           if (used[c] || !first_of_class(c)) continue;
-          S.back() = c;
-          const double sc = ctx.score(S);
+          cn[ctx.cls[c]]++;
+          const double sc = ctx.score_counts(cn);
+          cn[ctx.cls[c]]--;
           if (sc > ps + 1e-9) {
             ps = sc;
             pick = c;
           }
         }
-        S.back() = pick;
+        S.push_back(pick);
+        cn[ctx.cls[pick]]++;
         used[pick] = 1;
       }
       // 1-swap local search (bounded)
-      double cur = ctx.score(S);
+      double cur = ctx.score_counts(cn);
+      // classes whose positions found no improving swap since the last change: another
+      // position of the same class would see exactly the same candidates and scores
+      std::vector<char> tried(ctx.ncls, 0);
       for (int pass = 0; pass < 4; ++pass) {
         bool improved = false;
         for (size_t k = required.size(); k < S.size(); ++k) {
+          const int k_cls = ctx.cls[S[k]];
+          if (tried[k_cls]) continue;
+          bool changed = false;
           seen.clear();
           for (int c : cand) {
             if (used[c] || !first_of_class(c)) continue;
             const int old = S[k];
-            S[k] = c;
-            const double sc = ctx.score(S);
+            if (ctx.cls[old] == ctx.cls[c]) continue;  // same class: same score
+            cn[ctx.cls[old]]--;
+            cn[ctx.cls[c]]++;
+            const double sc = ctx.score_counts(cn);
             if (sc > cur + 1e-9) {
               cur = sc;
+              S[k] = c;
               used[old] = 0;
               used[c] = 1;
-              improved = true;
+              improved = changed = true;
             } else {
-              S[k] = old;
+              cn[ctx.cls[c]]--;
+              cn[ctx.cls[old]]++;
             }
           }
+          if (changed) std::fill(tried.begin(), tried.end(), 0);
+          else tried[k_cls] = 1;
         }
         if (!improved) break;
       }
