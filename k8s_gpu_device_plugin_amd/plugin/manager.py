@@ -233,6 +233,8 @@ class PluginManager:
         self.exporter.set_partition_labels(labels)
         self.exporter.set_tables([p.table for p in plugins])
         self.monitor.set_fast_tables([p.table for p in plugins])  # Unhealthy applied natively, at once
+        # ... and Healthy too when no recovery canary may hold a GPU back
+        self.monitor.set_fast_recover(not self.cfg.health.canary)
         self.monitor.set_gpu_count(max([g.index for g in gpus], default=-1) + 1)
         log.info("loaded %d GPU(s), resources: %s", len(gpus),
                  ", ".join("%s=%d" % (k, len(v)) for k, v in self.device_map.items()) or "none")
@@ -287,7 +289,9 @@ class PluginManager:
                 return
             if healthy:
                 self._held_unhealthy.discard(u.gpu)
-            self._set_health(u.gpu, u.partition, healthy, u.reason)
+            # without the canary the monitor thread already applied both directions to
+            # the tables; re-applying a queued update here could briefly undo a newer one
+            self._set_health(u.gpu, u.partition, healthy, u.reason, apply=self.cfg.health.canary)
         elif u.link_up in (0, 1):
             for p in self.plugins:
                 p.set_link_up(u.gpu, u.peer, bool(u.link_up))
@@ -295,9 +299,12 @@ class PluginManager:
         else:
             log.info("GPU event on %d: %s", u.gpu, u.reason)
 
-    def _set_health(self, gpu: int, partition: int, healthy: bool, reason: str) -> None:
+    def _set_health(self, gpu: int, partition: int, healthy: bool, reason: str, apply: bool = True) -> None:
         for p in self.plugins:
-            p.set_gpu_health(gpu, partition, healthy)
+            if apply:
+                p.set_gpu_health(gpu, partition, healthy)
+            else:
+                p.sync_gpu_health(gpu, partition)
         self.health_log.append((time.monotonic(), gpu, int(healthy), reason))
         (log.info if healthy else log.warning)("GPU %d marked %s: %s", gpu, "Healthy" if healthy else "Unhealthy",
                                                reason)

@@ -316,14 +316,17 @@ class AmdDevicePlugin:
 
     def set_gpu_health(self, gpu: int, partition: int, healthy: bool) -> int:
         changed = self.table.set_gpu_health(gpu, partition, healthy)
-        # The table is the source of truth (the monitor thread may already have applied
-        # an Unhealthy transition natively): mirror it into the Python device view.
-        for d in self._devices:
-            if d.gpu == gpu and (partition < 0 or d.partition < 0 or d.partition == partition):
-                d.health = v1beta1.HEALTHY if self.table.healthy(d.id) else v1beta1.UNHEALTHY
+        self.sync_gpu_health(gpu, partition)
         if changed:
             self.notify()
         return changed
+
+    def sync_gpu_health(self, gpu: int, partition: int = -1) -> None:
+        """The table is the source of truth (the monitor thread may already have applied
+        a transition natively): mirror it into the Python device view."""
+        for d in self._devices:
+            if d.gpu == gpu and (partition < 0 or d.partition < 0 or d.partition == partition):
+                d.health = v1beta1.HEALTHY if self.table.healthy(d.id) else v1beta1.UNHEALTHY
 
     def set_device_health(self, device_id: str, healthy: bool) -> bool:
         changed = self.table.set_health(device_id, healthy)

@@ -401,6 +401,7 @@ PYBIND11_MODULE(_native, m) {
       .def("pop", &HealthMonitor::pop, py::call_guard<py::gil_scoped_release>(), py::arg("timeout_ms") = 200)
       .def("gpu_healthy", &HealthMonitor::gpu_healthy)
       .def("set_fast_tables", &HealthMonitor::set_fast_tables)
+      .def("set_fast_recover", &HealthMonitor::set_fast_recover)
       .def("set_bad_page_thresholds", &HealthMonitor::set_bad_page_thresholds)
       .def("on_sample", &HealthMonitor::on_sample, py::arg("gpu"), py::arg("ok"), py::arg("sample"),
            py::call_guard<py::gil_scoped_release>())

@@ -64,8 +64,8 @@ void HealthMonitor::reconcile_locked(int gpu, int kind, const std::string& reaso
   const bool healthy = !st.resetting && !st.ecc_bad && !st.lost && !st.pages_bad;
   if (healthy == st.reported_healthy) return;
   st.reported_healthy = healthy;
-  if (!healthy)
-    for (const auto& t : fast_tables_) t->set_gpu_health(gpu, -1, false);
+  if (!healthy || fast_recover_)
+    for (const auto& t : fast_tables_) t->set_gpu_health(gpu, -1, healthy);
   HealthUpdate u;
   u.kind = kind;
   u.gpu = gpu;
@@ -219,6 +219,11 @@ std::vector<HealthUpdate> HealthMonitor::pop(int timeout_ms) {
 void HealthMonitor::set_fast_tables(std::vector<std::shared_ptr<DeviceTable>> tables) {
   std::lock_guard<std::mutex> lk(mu_);
   fast_tables_ = std::move(tables);
+}
+
+void HealthMonitor::set_fast_recover(bool on) {
+  std::lock_guard<std::mutex> lk(mu_);
+  fast_recover_ = on;
 }
 
 void HealthMonitor::set_bad_page_thresholds(std::vector<int> thresholds) {

@@ -59,6 +59,9 @@ class HealthMonitor {
   // update reaches the Python manager.  Healthy transitions stay with the manager,
   // which may hold a GPU back for the recovery canary.
   void set_fast_tables(std::vector<std::shared_ptr<DeviceTable>> tables);
+  // With no recovery canary configured the manager holds nothing back, so Healthy
+  // transitions take the same native path (the manager then only records them).
+  void set_fast_recover(bool on);
   // Per-GPU retired-page limits (index = GPU; <= 0 disables the check for that GPU).
   void set_bad_page_thresholds(std::vector<int> thresholds);
   uint64_t events_seen() const { return events_seen_; }
@@ -85,6 +88,7 @@ class HealthMonitor {
   std::deque<HealthUpdate> queue_;
   std::vector<GpuState> state_;
   std::vector<std::shared_ptr<DeviceTable>> fast_tables_;
+  bool fast_recover_ = false;
   std::vector<int> page_thresholds_;
   std::thread thread_;
   std::atomic<bool> running_{false};

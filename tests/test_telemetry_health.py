@@ -77,6 +77,24 @@ def test_health_monitor_state_machine(n):
     m.process(n.HwEvent(n.EVT_PRE_RESET, 7))  # out of range gpu: ignored, no crash
 
 
+def test_health_monitor_fast_tables_both_directions(n):
+    """Unhealthy always reaches the tables from the monitor itself; Healthy only with
+    fast recovery on (no recovery canary), else it waits for the manager."""
+    t = n.DeviceTable(n.TableConfig(), [n.TableDevice("a", 0), n.TableDevice("b", 1)], n.Topology(2))
+    m = n.HealthMonitor(n.FixtureBackend(1), 2)
+    m.set_gpu_count(2)
+    m.set_fast_tables([t])
+    m.process(n.HwEvent(n.EVT_PRE_RESET, 1))
+    assert not t.healthy("b") and t.healthy("a")
+    m.process(n.HwEvent(n.EVT_POST_RESET, 1))
+    assert not t.healthy("b")  # held for the manager (canary policy)
+    m.set_fast_recover(True)
+    m.process(n.HwEvent(n.EVT_PRE_RESET, 1))
+    m.process(n.HwEvent(n.EVT_POST_RESET, 1))
+    assert t.healthy("b")
+    assert [(x.gpu, x.healthy) for x in m.pop(100)] == [(1, 0), (1, 1), (1, 0), (1, 1)]
+
+
 def test_health_monitor_from_samples(n):
     be = fixtures.build_backend("2gpu_spx")
     m = n.HealthMonitor(be, 2)
