@@ -126,13 +126,32 @@ struct Ctx {
   double score(const std::vector<int>& S) const {
     std::fill(cnt.begin(), cnt.end(), 0);
     for (int i : S) cnt[cls[i]]++;
-    return score_counts(cnt);
+    const size_t n = S.size();
+    if (n * (n - 1) >= static_cast<size_t>(ncls) * (ncls + 1)) return score_counts(cnt);
+    // small sets (the exhaustive path): summing the pairs directly is cheaper
+    double s = 0;
+    for (size_t i = 0; i < n; ++i)
+      for (size_t j = i + 1; j < n; ++j) s += class_pair(cls[S[i]], cls[S[j]]);
+    return s + set_terms(cnt);
   }
 
   // Same score from per-class counts: devices of one (gpu, numa) class are
   // interchangeable for every term, so a candidate costs O(classes^2 + gpus) instead of
   // O(|S|^2) - the multi-GPU greedy/local search evaluates hundreds of candidates.
+  // (Pair scores are integers, so both pair sums are exact and identical.)
   double score_counts(const std::vector<int>& cn) const {
+    double s = 0;
+    for (int a = 0; a < ncls; ++a) {
+      if (!cn[a]) continue;
+      s += 0.5 * cn[a] * (cn[a] - 1) * class_pair(a, a);
+      for (int b = a + 1; b < ncls; ++b)
+        if (cn[b]) s += static_cast<double>(cn[a]) * cn[b] * class_pair(a, b);
+    }
+    return s + set_terms(cn);
+  }
+
+  // every term but the pair scores: packing, link sharing, fragmentation
+  double set_terms(const std::vector<int>& cn) const {
     double s = 0;
     std::fill(taken.begin(), taken.end(), 0);
     int first_gpu = -2;
@@ -143,9 +162,6 @@ struct Ctx {
       if (first_gpu == -2) first_gpu = g;
       else if (g != first_gpu) multi_gpu = true;
       if (g >= 0) taken[g] += cn[a];
-      s += 0.5 * cn[a] * (cn[a] - 1) * class_pair(a, a);
-      for (int b = a + 1; b < ncls; ++b)
-        if (cn[b]) s += static_cast<double>(cn[a]) * cn[b] * class_pair(a, b);
     }
     for (int g = 0; g < ngpu; ++g) {
       if (!taken[g]) continue;
