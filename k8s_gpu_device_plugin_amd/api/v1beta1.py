@@ -19,6 +19,7 @@ Exports:
 from __future__ import annotations
 
 import os
+import threading
 
 # The protobuf runtime (~30 ms to import and build) is loaded on first use of a message
 # class: the native daemon path needs only the constants and method paths below, so
@@ -144,13 +145,24 @@ def _build_file():
 _CLASS_NAMES = [name for name, _ in _MESSAGES]
 _LAZY = set(_CLASS_NAMES) | {"FILE_DESCRIPTOR_PROTO", "FILE_DESCRIPTOR", "METHODS"}
 _loaded = False
+_load_lock = threading.Lock()
 
 
 def _load() -> None:
-    """Builds the descriptor pool and message classes into this module (idempotent)."""
+    """Builds the descriptor pool and message classes into this module (idempotent).
+    The first access may come from several threads at once (grpcio handler threads, the
+    kubelet stub): one builds, the others wait, so every caller sees classes from one
+    pool.  Globals are published before ``_loaded`` is set."""
     global _loaded
     if _loaded:
         return
+    with _load_lock:
+        if not _loaded:
+            _load_locked()
+
+
+def _load_locked() -> None:
+    global _loaded
     from google.protobuf import descriptor_pool, message_factory
     g = globals()
     fdp = _build_file()
@@ -183,10 +195,17 @@ def plugin_options(pre_start_required: bool = False) -> "DevicePluginOptions":
                                             get_preferred_allocation_available=True)
 
 
-def _ld(field: int, payload: bytes) -> bytes:  # length-delimited field (len < 2**14 here)
-    n = len(payload)
-    ln = bytes([n]) if n < 0x80 else bytes([(n & 0x7F) | 0x80, n >> 7])
-    return bytes([(field << 3) | 2]) + ln + payload
+def _varint(n: int) -> bytes:
+    out = bytearray()
+    while n >= 0x80:
+        out.append((n & 0x7F) | 0x80)
+        n >>= 7
+    out.append(n)
+    return bytes(out)
+
+
+def _ld(field: int, payload: bytes) -> bytes:  # length-delimited field, any length
+    return _varint((field << 3) | 2) + _varint(len(payload)) + payload
 
 
 def encode_register_request(endpoint: str, resource_name: str, pre_start_required: bool = False,

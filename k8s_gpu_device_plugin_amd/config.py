@@ -263,6 +263,13 @@ def validate(cfg: Config) -> Config:
         raise ConfigError("telemetry.intervalMs must be >= 10")
     if not cfg.resourcePrefix or "/" in cfg.resourcePrefix:
         raise ConfigError("resourcePrefix must be a DNS-like prefix without '/'")
+    # extended resource prefixes are DNS subdomains (RFC 1123, at most 253 characters);
+    # the name part is checked (1..63 characters) when resources are built
+    import re
+    label = r"[a-z0-9]([-a-z0-9]{0,61}[a-z0-9])?"
+    if len(cfg.resourcePrefix) > 253 or not re.fullmatch(r"%s(\.%s)*" % (label, label), cfg.resourcePrefix):
+        raise ConfigError("resourcePrefix %r is not a DNS subdomain (lower-case labels of at most 63 "
+                          "characters, 253 in total)" % cfg.resourcePrefix[:80])
     return cfg
 
 

@@ -21,7 +21,7 @@ def make_backend(cfg):
         return fixtures.build_backend(cfg.fixture)
     if kind == "amdsmi":
         return n.make_amdsmi_backend()
-    if n.amdsmi_available():
+    if n.amdsmi_available(keep=True):  # the backend adopts the probe's session
         return n.make_amdsmi_backend()
     log.warning("amdsmi found no AMD GPUs on this node; advertising nothing")
     return n.FixtureBackend(1)

@@ -194,13 +194,21 @@ class PluginManager:
         if self.cfg.health.canaryOnPreStart:
             for p in plugins:
                 p.prestart_check = self._prestart_check
-        # health state survives a reload: re-apply what the monitor currently reports
+        # start-up canary failures are per partition and known only here
         for p in plugins:
-            for g in gpus:
-                if (self.monitor.running and not self.monitor.gpu_healthy(g.index)) or g.index in self._held_unhealthy:
-                    p.set_gpu_health(g.index, -1, False)
             for gpu, part in failed:
                 p.set_gpu_health(gpu, part, False)
+        # Health state survives a reload.  The monitor installs the new tables and writes
+        # its current state into them under the lock that orders its transitions, so an
+        # event that lands during the reload reaches the new tables either way (reading
+        # gpu_healthy() here and calling set_fast_tables() later left a window in which
+        # it reached only the outgoing ones).
+        self.monitor.set_gpu_count(max([g.index for g in gpus], default=-1) + 1)
+        self.monitor.attach_tables([p.table for p in plugins], not self.cfg.health.canary,
+                                   sorted(self._held_unhealthy))
+        for p in plugins:
+            for g in gpus:
+                p.sync_gpu_health(g.index)
         self.plugins = plugins
         n = native.load()
         labels = []
@@ -232,10 +240,6 @@ class PluginManager:
         self.exporter.set_inventory(gpus)
         self.exporter.set_partition_labels(labels)
         self.exporter.set_tables([p.table for p in plugins])
-        self.monitor.set_fast_tables([p.table for p in plugins])  # Unhealthy applied natively, at once
-        # ... and Healthy too when no recovery canary may hold a GPU back
-        self.monitor.set_fast_recover(not self.cfg.health.canary)
-        self.monitor.set_gpu_count(max([g.index for g in gpus], default=-1) + 1)
         log.info("loaded %d GPU(s), resources: %s", len(gpus),
                  ", ".join("%s=%d" % (k, len(v)) for k, v in self.device_map.items()) or "none")
 

@@ -27,8 +27,10 @@ namespace {
 
 std::mutex g_init_mu;
 int g_init_refs = 0;
-// A successful amdsmi_available() keeps its session open as one reference, which the next
+// amdsmi_available(keep=true) keeps its session open as one reference, which the next
 // backend adopts: amdsmi_init costs ~25 ms on MI355X, and start-up probes and then opens.
+// Probe-only callers pass keep=false, or drop an unadopted session with
+// amdsmi_release_probe(), so no process holds a session that nothing owns.
 bool g_probe_ref = false;
 
 std::string status_str(amdsmi_status_t st) {
@@ -97,19 +99,31 @@ int partitions_of_mode(const std::string& mode) {
 
 }  // namespace
 
-bool amdsmi_available() {
+bool amdsmi_available(bool keep) {
   std::lock_guard<std::mutex> lk(g_init_mu);
   if (g_init_refs > 0) return true;
   if (amdsmi_init(AMDSMI_INIT_AMD_GPUS) != AMDSMI_STATUS_SUCCESS) return false;
   uint32_t n = 0;
   const bool ok = amdsmi_get_socket_handles(&n, nullptr) == AMDSMI_STATUS_SUCCESS && n > 0;
-  if (!ok) {
+  if (!ok || !keep) {
     amdsmi_shut_down();
-    return false;
+    return ok;
   }
-  g_init_refs = 1;  // held for the backend that usually follows
+  g_init_refs = 1;  // held for the backend that follows
   g_probe_ref = true;
   return true;
+}
+
+void amdsmi_release_probe() {
+  std::lock_guard<std::mutex> lk(g_init_mu);
+  if (!g_probe_ref) return;
+  g_probe_ref = false;
+  if (--g_init_refs == 0) amdsmi_shut_down();
+}
+
+bool amdsmi_probe_held() {
+  std::lock_guard<std::mutex> lk(g_init_mu);
+  return g_probe_ref;
 }
 
 class AmdSmiBackend : public Backend {

@@ -184,7 +184,11 @@ class Backend {
 };
 
 std::shared_ptr<Backend> make_amdsmi_backend();
-bool amdsmi_available();
+// Is an AMD GPU visible to amdsmi?  keep=true leaves the session open for the next
+// make_amdsmi_backend() to adopt; amdsmi_release_probe() drops it if none does.
+bool amdsmi_available(bool keep = false);
+void amdsmi_release_probe();
+bool amdsmi_probe_held();
 
 int64_t now_ns();
 int64_t mono_ns();

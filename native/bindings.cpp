@@ -225,7 +225,9 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("discover_calls", &FixtureBackend::discover_calls);
 
   m.def("make_amdsmi_backend", &make_amdsmi_backend, py::call_guard<py::gil_scoped_release>());
-  m.def("amdsmi_available", &amdsmi_available, py::call_guard<py::gil_scoped_release>());
+  m.def("amdsmi_available", &amdsmi_available, py::arg("keep") = false, py::call_guard<py::gil_scoped_release>());
+  m.def("amdsmi_release_probe", &amdsmi_release_probe, py::call_guard<py::gil_scoped_release>());
+  m.def("amdsmi_probe_held", &amdsmi_probe_held);
 
   // ---- allocator (raw, for tests / Python policies) ----
   py::class_<AllocDevice>(m, "AllocDevice")
@@ -402,6 +404,8 @@ PYBIND11_MODULE(_native, m) {
       .def("gpu_healthy", &HealthMonitor::gpu_healthy)
       .def("set_fast_tables", &HealthMonitor::set_fast_tables)
       .def("set_fast_recover", &HealthMonitor::set_fast_recover)
+      .def("attach_tables", &HealthMonitor::attach_tables, py::arg("tables"), py::arg("fast_recover"),
+           py::arg("held_unhealthy"), py::call_guard<py::gil_scoped_release>())
       .def("set_bad_page_thresholds", &HealthMonitor::set_bad_page_thresholds)
       .def("on_sample", &HealthMonitor::on_sample, py::arg("gpu"), py::arg("ok"), py::arg("sample"),
            py::call_guard<py::gil_scoped_release>())

@@ -226,6 +226,23 @@ void HealthMonitor::set_fast_recover(bool on) {
   fast_recover_ = on;
 }
 
+void HealthMonitor::attach_tables(std::vector<std::shared_ptr<DeviceTable>> tables, bool fast_recover,
+                                  const std::vector<int>& held_unhealthy) {
+  // One critical section: a transition processed before it is written into the new
+  // tables here, one processed after it goes to them through reconcile_locked.  No
+  // window exists in which an event reaches only the outgoing tables.
+  std::lock_guard<std::mutex> lk(mu_);
+  fast_tables_ = std::move(tables);
+  fast_recover_ = fast_recover;
+  std::vector<char> down(state_.size(), 0);
+  for (size_t g = 0; g < state_.size(); ++g) down[g] = running_ && !state_[g].reported_healthy;
+  for (int g : held_unhealthy)
+    if (g >= 0 && g < static_cast<int>(down.size())) down[g] = 1;
+  for (size_t g = 0; g < down.size(); ++g)
+    if (down[g])
+      for (const auto& t : fast_tables_) t->set_gpu_health(static_cast<int>(g), -1, false);
+}
+
 void HealthMonitor::set_bad_page_thresholds(std::vector<int> thresholds) {
   std::lock_guard<std::mutex> lk(mu_);
   page_thresholds_ = std::move(thresholds);

@@ -62,6 +62,12 @@ class HealthMonitor {
   // With no recovery canary configured the manager holds nothing back, so Healthy
   // transitions take the same native path (the manager then only records them).
   void set_fast_recover(bool on);
+  // Plugin reload: installs the new tables as the fast tables and, under the same lock
+  // that orders every transition, marks Unhealthy in them each GPU the monitor reports
+  // unhealthy or the caller holds back (`held_unhealthy`, e.g. a pending recovery
+  // canary).  Call after set_gpu_count.
+  void attach_tables(std::vector<std::shared_ptr<DeviceTable>> tables, bool fast_recover,
+                     const std::vector<int>& held_unhealthy);
   // Per-GPU retired-page limits (index = GPU; <= 0 disables the check for that GPU).
   void set_bad_page_thresholds(std::vector<int> thresholds);
   uint64_t events_seen() const { return events_seen_; }

@@ -192,6 +192,47 @@ static void test_grpc_server(std::shared_ptr<FixtureBackend> be, const std::stri
   srv.stop();
 }
 
+// Plugin reloads racing health transitions: an event thread flips GPUs while the main
+// thread keeps attaching fresh tables.  After every attach the newest table must agree
+// with the monitor once the event thread pauses (no transition lost in the hand-over).
+static void test_attach_tables_during_events(std::shared_ptr<FixtureBackend> be) {
+  std::vector<GpuInfo> gpus;
+  Topology topo;
+  be->discover(&gpus, &topo);
+  std::vector<TableDevice> devs;
+  for (const auto& g : gpus) {
+    TableDevice d;
+    d.id = "gpu" + std::to_string(g.index);
+    d.gpu = g.index;
+    devs.push_back(d);
+  }
+  TableConfig tc;
+  auto mon = std::make_shared<HealthMonitor>(be, 2);
+  mon->set_gpu_count(static_cast<int>(gpus.size()));
+  mon->start();
+  for (int round = 0; round < 20; ++round) {
+    std::atomic<bool> go{true};
+    std::thread ev([&, round] {
+      for (int k = 0; go.load() || k < 64; ++k) {
+        HwEvent e;
+        e.kind = (k + round) % 3 ? kEvtPreReset : kEvtPostReset;
+        e.gpu = (k * 7 + round) % static_cast<int>(gpus.size());
+        mon->process(e);
+      }
+    });
+    std::shared_ptr<DeviceTable> last;
+    for (int k = 0; k < 8; ++k) {
+      last = std::make_shared<DeviceTable>(tc, devs, topo);
+      mon->attach_tables({last}, true, {});
+    }
+    go.store(false);
+    ev.join();
+    for (const auto& g : gpus) CHECK(last->healthy("gpu" + std::to_string(g.index)) == mon->gpu_healthy(g.index));
+  }
+  mon->pop(0);
+  mon->stop();
+}
+
 // PreStartContainer answered asynchronously: a verifier thread completes jobs while
 // clients call, some clients disconnect with checks in flight, and the server stops
 // with jobs still queued (their completions must land in a queue that outlives it).
@@ -457,6 +498,8 @@ int main() {
   test_exporter_httpd_health(make_node(2, 1));
   std::fprintf(stderr, "[selftest] reload races\n");
   test_reload_races(dir);
+  std::fprintf(stderr, "[selftest] health hand-over on reload\n");
+  test_attach_tables_during_events(make_node(4, 1));
   rmdir(dir);
   if (g_failures) {
     std::fprintf(stderr, "native selftest: %d failure(s)\n", g_failures);

@@ -11,7 +11,7 @@ lap("import cli")
 from k8s_gpu_device_plugin_amd import native
 n = native.load()
 lap("native.load")
-be = n.make_amdsmi_backend() if n.amdsmi_available() else None
+be = n.make_amdsmi_backend() if n.amdsmi_available(keep=True) else None
 lap("amdsmi_available + make backend (%s)" % (be is not None))
 if be is not None:
     gpus, topo = be.discover()

@@ -57,10 +57,17 @@ def test_env_overrides(tmp_path):
 @pytest.mark.parametrize("raw", [{"migStrategy": "bogus"}, {"webListenAddress": "9002"},
                                  {"log": {"level": "verbose"}}, {"backend": "nvml"},
                                  {"sharing": {"replicas": 0}}, {"grpc": {"server": "java"}},
-                                 {"resourcePrefix": "a/b"}, {"resources": [{"pattern": "*"}]}])
+                                 {"resourcePrefix": "a/b"}, {"resources": [{"pattern": "*"}]},
+                                 {"resourcePrefix": "x" * 64 + ".com"}, {"resourcePrefix": ("a" * 60 + ".") * 5},
+                                 {"resourcePrefix": "AMD.com"}, {"resourcePrefix": "amd..com"}])
 def test_validation_errors(raw):
     with pytest.raises(C.ConfigError):
         C.validate(C.from_dict(raw))
+
+
+@pytest.mark.parametrize("prefix", ["amd.com", "gpu.example.org", "a-b.c0"])
+def test_valid_resource_prefixes(prefix):
+    assert C.validate(C.from_dict({"resourcePrefix": prefix})).resourcePrefix == prefix
 
 
 def test_util_helpers():

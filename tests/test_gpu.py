@@ -19,6 +19,25 @@ def amdsmi_backend(n):
     be.shutdown()
 
 
+def test_amdsmi_probe_session_ownership(n):
+    """A probe-only amdsmi_available() closes its session; keep=True hands it to the next
+    backend, and release_probe() drops it when no backend follows."""
+    assert n.amdsmi_available()
+    assert not n.amdsmi_probe_held()
+    assert n.amdsmi_available(keep=True)
+    n.amdsmi_release_probe()
+    assert not n.amdsmi_probe_held()
+    assert n.amdsmi_available(keep=True)
+    be = n.make_amdsmi_backend()  # adopts the probe's session
+    assert not n.amdsmi_probe_held()
+    gpus, _ = be.discover()
+    assert gpus
+    be.shutdown()
+    be2 = n.make_amdsmi_backend()  # the session was closed with be: a fresh init works
+    assert be2.discover()[0]
+    be2.shutdown()
+
+
 def test_amdsmi_discovers_mi355x(amdsmi_backend):
     gpus, topo = amdsmi_backend.discover()
     assert len(gpus) >= 1 and topo.n == len(gpus)

@@ -388,3 +388,71 @@ def test_pod_resources_allocation_metric(make_cfg, plugin_dir, run_manager, tmp_
             assert 'pod="trainer-1"' in m.exporter.render()  # last known map is kept
     finally:
         stub.stop()
+
+
+class _InjectOnCall:
+    """Delegating proxy that runs ``hook`` once, the first time ``method`` is called
+    while armed."""
+
+    def __init__(self, target, method, hook):
+        self._target, self._method, self._hook, self.armed = target, method, hook, False
+
+    def __getattr__(self, name):
+        attr = getattr(self._target, name)
+        if name != self._method:
+            return attr
+
+        def wrapped(*a, **kw):
+            if self.armed:
+                self.armed = False
+                self._hook()
+            return attr(*a, **kw)
+        return wrapped
+
+
+@pytest.mark.parametrize("canary", [False, True])
+@pytest.mark.parametrize("where", ["plugin_build", "exporter_inventory"])
+def test_health_event_during_reload_reaches_new_tables(make_cfg, plugin_dir, monkeypatch, where, canary):
+    """a PRE_RESET processed while load_plugins builds the new plugins
+    must reach the new tables whatever the point of the reload it lands on - before the
+    monitor adopts them (written in at adoption) or after (fast path).  The old code read
+    the monitor state, then installed the fast tables later: an event in between went
+    only to the outgoing tables, and the GPU stayed advertised Healthy."""
+    from k8s_gpu_device_plugin_amd.plugin import manager as manager_mod
+    be = fixtures.build_backend("2gpu_spx")
+    m = PluginManager(make_cfg(health={"canary": canary}), backend=be)
+    inject = lambda: m.monitor.process(be_event(m, "EVT_PRE_RESET", 1))  # noqa: E731
+    if where == "exporter_inventory":
+        proxy = _InjectOnCall(m.exporter, "set_inventory", inject)
+        m.exporter = proxy
+    else:
+        real = manager_mod.AmdDevicePlugin
+
+        class proxy:  # noqa: N801 - stands in for the class
+            armed = False
+
+        def build(*a, **kw):
+            p = real(*a, **kw)
+            if proxy.armed:
+                proxy.armed = False
+                inject()
+            return p
+        monkeypatch.setattr(manager_mod, "AmdDevicePlugin", build)
+    with KubeletStub(plugin_dir) as k:
+        t = m.start_background()
+        try:
+            k.wait_for_registrations(1)
+            assert m.plugins[0].table.healthy_count() == 2
+            proxy.armed = True
+            m.restart()
+            k.wait_for_registrations(2, timeout=10)
+            assert _wait(lambda: m.counters["restarts_api"] == 1)
+            assert not proxy.armed, "the hook did not run during the reload"
+            assert _wait(lambda: m.plugins[0].table.healthy_count() == 1), "GPU 1 advertised Healthy after reload"
+            assert not m.plugins[0].table.healthy(m.plugins[0].table.ids()[1])
+            w = k.watch("amd-gpu.sock")
+            _, devs = w.next()
+            assert [h for _, h, _ in devs] == ["Healthy", "Unhealthy"]
+        finally:
+            m.stop()
+            t.join(10)

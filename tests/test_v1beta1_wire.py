@@ -149,7 +149,8 @@ def test_options_bytes(n, size):
 
 @pytest.mark.parametrize("pre_start", [False, True])
 @pytest.mark.parametrize("endpoint,resource", [("amd-gpu.sock", "amd.com/gpu"), ("a" * 300, "amd.com/cpx_nps4"),
-                                               ("", "")])
+                                               ("", ""), ("e" * 16384, "amd.com/gpu"),
+                                               ("e" * 20000, "r" * 40000)])
 def test_protobuf_free_register_request_matches_runtime(pre_start, endpoint, resource):
     """The native Register path encodes RegisterRequest by hand; it must be byte-identical
     to the protobuf runtime's serialisation."""
@@ -167,3 +168,28 @@ def test_daemon_imports_stay_light():
             "print(sorted(m for m in ('grpc', 'google.protobuf', 'yaml') if m in sys.modules))")
     out = subprocess.run([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True, check=True)
     assert out.stdout.strip() == "[]"
+
+
+def test_lazy_classes_built_once_under_concurrent_first_use():
+    """the first message-class access from several threads at once must build
+    one descriptor pool; every thread gets the same class objects."""
+    import subprocess
+    import sys
+    code = """
+import threading
+from k8s_gpu_device_plugin_amd.api import v1beta1 as v
+start = threading.Barrier(16)
+seen = []
+def go():
+    start.wait()
+    seen.append((v.Device, v.ListAndWatchResponse, v.METHODS[v.METHOD_ALLOCATE][0]))
+ts = [threading.Thread(target=go) for _ in range(16)]
+[t.start() for t in ts]
+[t.join() for t in ts]
+assert len(set(seen)) == 1, len(set(seen))
+r = v.ListAndWatchResponse(devices=[v.Device(ID="x", health=v.HEALTHY)])
+assert v.ListAndWatchResponse.FromString(r.SerializeToString()).devices[0].ID == "x"
+print("ok")
+"""
+    out = subprocess.run([sys.executable, "-c", code], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    assert out.stdout.strip().endswith("ok"), out.stdout
