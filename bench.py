@@ -24,6 +24,11 @@ ranks scrape concurrently, so this is the daemon's aggregate throughput).  Befor
 each rank validates its allocation: the returned render node exists and the gfx950
 canary (HBM pattern + MFMA exactness/throughput) passes on that device.
 
+Speed-of-light references, measured untimed in the same run: ``uds_roundtrip_floor_p50_us``
+(the same unix-socket exchange between two threads, no protocol work, sleeping server
+thread) and ``uds_roundtrip_floor_spin_p50_us`` (server thread polling, which is what the
+daemon's ``grpc.busyPollUs`` window gives back-to-back kubelet RPCs).
+
 The reference publishes no numbers, so ``vs_baseline`` is null.
 """
 from __future__ import annotations
@@ -78,7 +83,7 @@ def _wait_http(port: int, timeout: float) -> None:
     raise TimeoutError("plugin web server did not come up on port %d" % port)
 
 
-def start_daemon(n_gpus: int, grpc_server: str, workdir: str, profile_dir: str = ""):
+def start_daemon(n_gpus: int, grpc_server: str, workdir: str, profile_dir: str = "", busy_poll_us=None):
     """Rank 0: kubelet stub + plugin daemon subprocess.  Must run before GPU init."""
     from k8s_gpu_device_plugin_amd import native
     from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import KubeletStub
@@ -91,12 +96,13 @@ def start_daemon(n_gpus: int, grpc_server: str, workdir: str, profile_dir: str =
     port = _free_port()
     cfg_path = os.path.join(workdir, "bench-config.yml")
     threads = max(4, n_gpus)  # one server worker per concurrent kubelet-client rank
+    bp = "" if busy_poll_us is None else "  busyPollUs: %d\n" % busy_poll_us
     with open(cfg_path, "w") as f:
         f.write("webListenAddress: \"127.0.0.1:%d\"\nmigStrategy: none\nbackend: %s\nfixture: %dgpu_spx\n"
                 "devices: \"0-%d\"\npluginDir: \"%s\"\nlog:\n  level: info\n  fileDir: \"\"\n"
-                "http:\n  accessLog: false\n  threads: %d\ngrpc:\n  server: %s\n  threads: %d\n"
-                "telemetry:\n  intervalMs: 1000\n"
-                % (port, backend, n_gpus, n_gpus - 1, plugin_dir, threads, grpc_server, threads))
+                "http:\n  accessLog: false\n  threads: %d\n%stelemetry:\n  intervalMs: 1000\n"
+                "grpc:\n  server: %s\n  threads: %d\n%s"
+                % (port, backend, n_gpus, n_gpus - 1, plugin_dir, threads, bp, grpc_server, threads, bp))
         if profile_dir:  # benchmark: true -> cpu/mem/threads/native profiles when the daemon exits
             f.write("benchmark: true\nbenchmarkDir: \"%s\"\n" % os.path.abspath(profile_dir))
     env = dict(os.environ)
@@ -116,6 +122,8 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--grpc-server", choices=["native", "python"], default="native")
     ap.add_argument("--no-canary", action="store_true")
+    ap.add_argument("--busy-poll-us", type=int, default=None,
+                    help="override grpc.busyPollUs of the daemon (default: the config default)")
     ap.add_argument("--profile-dir", default="", help="run the daemon with benchmark: true, profiles here")
     args = ap.parse_args()
 
@@ -138,7 +146,8 @@ def main() -> int:
     if rank == 0:  # daemon first: nothing has touched the GPU in this process yet
         shutil.rmtree(workdir, ignore_errors=True)
         os.makedirs(workdir)
-        proc, kubelet, port, reg, backend = start_daemon(n_gpus, args.grpc_server, workdir, args.profile_dir)
+        proc, kubelet, port, reg, backend = start_daemon(n_gpus, args.grpc_server, workdir, args.profile_dir,
+                                                         args.busy_poll_us)
         info = {"port": port, "endpoint": reg.endpoint, "resource": reg.resource_name, "backend": backend,
                 "plugin_dir": os.path.join(workdir, "device-plugins")}
 
@@ -246,8 +255,11 @@ def main() -> int:
     # Untimed speed-of-light reference: the same send/epoll_wait/recv/send/recv exchange
     # between two threads with no HTTP/2, HPACK or protobuf work (sizes ~ this Allocate's).
     alloc_resp_len = len(alloc_raw(alloc_req))
-    floor = n.uds_pingpong(10000, 500, 9 + 80 + 9 + 5 + len(alloc_req), 9 + 20 + 9 + 5 + alloc_resp_len + 9 + 16)
+    sizes = (9 + 80 + 9 + 5 + len(alloc_req), 9 + 20 + 9 + 5 + alloc_resp_len + 9 + 16)
+    floor = n.uds_pingpong(10000, 500, *sizes)
     mine["uds_floor_p50"] = _pct(floor, 0.5)
+    # ... and with a server thread that polls instead of sleeping (the busy-poll window)
+    mine["uds_floor_spin_p50"] = _pct(n.uds_pingpong(10000, 500, *sizes, server_spin=True), 0.5)
     if world > 1:
         gathered = [None] * world
         dist.all_gather_object(gathered, mine)
@@ -279,6 +291,7 @@ def main() -> int:
                        "backend": info["backend"], "grpc_server": args.grpc_server},
             "allocate_p50_us": round(p50, 2), "allocate_p99_us": round(_pct(allocs_native, 0.99) * 1e6, 2),
             "uds_roundtrip_floor_p50_us": round(gathered[0]["uds_floor_p50"] * 1e6, 2),
+            "uds_roundtrip_floor_spin_p50_us": round(gathered[0]["uds_floor_spin_p50"] * 1e6, 2),
             "allocate_p50_us_grpcio_client": round(p50_grpcio, 2),
             "allocate_p99_us_grpcio_client": round(_pct(allocs, 0.99) * 1e6, 2),
             "preferred_p50_us": round(_pct(prefs_native, 0.5) * 1e6, 2),

@@ -70,12 +70,14 @@ class HttpConfig:
     threads: int = 2
     accessLog: bool = True
     server: str = "native"       # native | python
+    busyPollUs: int = 50         # native server: keep polling this long after a request (0 = off)
 
 
 @dataclass
 class GrpcConfig:
     server: str = "native"       # native (C++ HTTP/2) | python (grpcio)
     threads: int = 4
+    busyPollUs: int = 50         # native server: keep polling this long after a request (0 = off)
 
 
 @dataclass
@@ -255,6 +257,9 @@ def validate(cfg: Config) -> Config:
         raise ConfigError("sharing.replicas must be >= 1")
     if cfg.grpc.server not in ("native", "python"):
         raise ConfigError("grpc.server must be native|python")
+    for sect in ("grpc", "http"):
+        if not 0 <= getattr(cfg, sect).busyPollUs <= 100000:
+            raise ConfigError("%s.busyPollUs must be within 0..100000" % sect)
     if cfg.http.server not in ("native", "python"):
         raise ConfigError("http.server must be native|python")
     if cfg.podResources.intervalS <= 0:

@@ -51,6 +51,7 @@ class WebServer:
             hc.threads = max(1, self.cfg.http.threads)
             hc.access_log = bool(self.cfg.http.accessLog)
             hc.read_timeout_s = 30  # server/server.go:45
+            hc.busy_poll_us = int(self.cfg.http.busyPollUs)
             hc.version = VERSION
             srv = n.HttpServer(hc, self.manager.exporter)
             srv.set_restart_hook(self.manager.restart)

@@ -454,6 +454,7 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("access_log", &HttpConfig::access_log)
       .def_readwrite("idle_timeout_s", &HttpConfig::idle_timeout_s)
       .def_readwrite("read_timeout_s", &HttpConfig::read_timeout_s)
+      .def_readwrite("busy_poll_us", &HttpConfig::busy_poll_us)
       .def_readwrite("version", &HttpConfig::version);
 
   py::class_<HttpServer, std::shared_ptr<HttpServer>>(m, "HttpServer")
@@ -508,7 +509,8 @@ PYBIND11_MODULE(_native, m) {
 
   // ---- native gRPC (HTTP/2) server + client ----
   py::class_<GrpcServer, std::shared_ptr<GrpcServer>>(m, "GrpcServer")
-      .def(py::init<std::string, int>(), py::arg("socket_path"), py::arg("threads") = 2)
+      .def(py::init<std::string, int, int>(), py::arg("socket_path"), py::arg("threads") = 2,
+           py::arg("busy_poll_us") = 0)
       .def("set_table", &GrpcServer::set_table)
       .def("add_table", &GrpcServer::set_table)
       .def("start", &GrpcServer::start, py::call_guard<py::gil_scoped_release>())
@@ -680,11 +682,12 @@ PYBIND11_MODULE(_native, m) {
     return out;
   });
   m.def("uds_pingpong",
-        [](int n, int warmup, int req_bytes, int resp_bytes) {
+        [](int n, int warmup, int req_bytes, int resp_bytes, bool server_spin) {
           py::gil_scoped_release rel;
-          return uds_pingpong(n, warmup, req_bytes, resp_bytes);
+          return uds_pingpong(n, warmup, req_bytes, resp_bytes, server_spin);
         },
-        py::arg("n") = 10000, py::arg("warmup") = 500, py::arg("req_bytes") = 128, py::arg("resp_bytes") = 256);
+        py::arg("n") = 10000, py::arg("warmup") = 500, py::arg("req_bytes") = 128, py::arg("resp_bytes") = 256,
+        py::arg("server_spin") = false);
   m.def("grpc_load",
         [load_dict](const std::string& sock, const std::string& method, const py::bytes& req, int conns,
                     double duration_s) {

@@ -298,7 +298,8 @@ void send_headers(Conn& c, uint32_t sid) {
 
 }  // namespace
 
-GrpcServer::GrpcServer(std::string socket_path, int threads) : path_(std::move(socket_path)), nthreads_(threads) {}
+GrpcServer::GrpcServer(std::string socket_path, int threads, int busy_poll_us)
+    : path_(std::move(socket_path)), nthreads_(threads), busy_poll_us_(std::max(0, std::min(busy_poll_us, 100000))) {}
 
 GrpcServer::~GrpcServer() { stop(); }
 
@@ -788,8 +789,20 @@ void GrpcServer::run(Worker* w) {
   };
 
   uint64_t seen_version = table->version();
+  const int64_t spin_ns = static_cast<int64_t>(busy_poll_us_) * 1000;
+  int64_t spin_until = 0;  // busy-poll window end (mono ns); 0 = closed
   while (!stop_.load(std::memory_order_relaxed)) {
-    const int n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), 100);
+    int n;
+    if (spin_until != 0) {
+      n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), 0);
+      if (n == 0) {
+        if (mono_ns() >= spin_until) spin_until = 0;
+        else __builtin_ia32_pause();
+        continue;
+      }
+    } else {
+      n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), 100);
+    }
     bool law_tick = false;
     for (int i = 0; i < n; ++i) {
       const int fd = evs[i].data.fd;
@@ -878,6 +891,7 @@ void GrpcServer::run(Worker* w) {
           }
         }
         if (!process(*c)) c->closing = true;
+        if (spin_ns > 0) spin_until = mono_ns() + spin_ns;
       }
       if (c->out.size() - c->out_off > kMaxPendingOut) {  // e.g. a PING flood that is never read
         close_conn(fd);

@@ -27,7 +27,13 @@ namespace amdgpu_dp {
 
 class GrpcServer {
  public:
-  GrpcServer(std::string socket_path, int threads);
+  // busy_poll_us: after a worker handles a request it keeps polling its epoll set
+  // without sleeping for this long (0 = always block).  A kubelet admits a pod as a
+  // burst of RPCs (GetPreferredAllocation, Allocate, PreStartContainer); a worker that
+  // is still polling when the next one lands skips the idle-CPU wake-up, which is most
+  // of a unix-socket round trip.  An idle plugin never spins: the window only opens on
+  // request activity and closes after busy_poll_us without any.
+  GrpcServer(std::string socket_path, int threads, int busy_poll_us = 0);
   ~GrpcServer();
   void set_table(std::shared_ptr<DeviceTable> t);
   void start();  // throws std::runtime_error on bind/listen failure
@@ -55,6 +61,7 @@ class GrpcServer {
   std::shared_ptr<Notifier> notifier_ = std::make_shared<Notifier>();
   std::string path_;
   int nthreads_;
+  int busy_poll_us_;
   std::shared_ptr<DeviceTable> table_;
   int listen_fd_ = -1;
   std::atomic<bool> running_{false};

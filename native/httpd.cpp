@@ -211,9 +211,20 @@ int HttpServer::start() {
         }
         return true;
       };
+      // busy-poll window (see GrpcServer): a scraper's next request on a keep-alive
+      // connection usually lands while the worker is still polling
+      const int64_t spin_ns = static_cast<int64_t>(std::max(0, std::min(cfg_.busy_poll_us, 100000))) * 1000;
+      int64_t spin_until = 0;
       while (!stop_.load(std::memory_order_relaxed)) {
-        const int n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), 200);
+        const int n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), spin_until ? 0 : 200);
         const int64_t now = mono_ns();
+        if (spin_until) {
+          if (n == 0 && now < spin_until) {
+            __builtin_ia32_pause();
+            continue;
+          }
+          if (n == 0) spin_until = 0;
+        }
         for (int i = 0; i < n; ++i) {
           const int fd = evs[i].data.fd;
           if (fd == listen_fd_) {
@@ -267,6 +278,7 @@ int HttpServer::start() {
                 break;
               }
             }
+            if (spin_ns > 0) spin_until = now + spin_ns;
             // parse and answer every complete request in the buffer (pipelining)
             size_t pos = 0;
             while (!c->close_after) {

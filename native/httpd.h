@@ -31,6 +31,7 @@ struct HttpConfig {
   bool access_log = true;
   int idle_timeout_s = 60;
   int read_timeout_s = 30;
+  int busy_poll_us = 0;  // keep polling this long after a request before sleeping (0 = off)
   std::string version = "0.1.0";
 };
 

@@ -173,7 +173,7 @@ LoadResult grpc_load(const std::string& socket_path, const std::string& method, 
   return total;
 }
 
-std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_bytes) {
+std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_bytes, bool server_spin) {
   if (n < 0 || warmup < 0 || req_bytes <= 0 || resp_bytes <= 0 || req_bytes > (1 << 20) || resp_bytes > (1 << 20))
     throw std::invalid_argument("uds_pingpong: bad sizes");
   int sv[2];
@@ -193,7 +193,9 @@ std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_byte
     size_t have = 0;
     epoll_event evs[4];
     for (;;) {
-      const int k = epoll_wait(ep, evs, 4, 1000);
+      // server_spin: the busy-poll worker (grpc.busyPollUs) never sleeps between requests
+      const int k = epoll_wait(ep, evs, 4, server_spin ? 0 : 1000);
+      if (k == 0 && server_spin) __builtin_ia32_pause();
       if (k < 0 && errno != EINTR) return;
       if (k <= 0) continue;
       bool closed = false;

@@ -32,7 +32,7 @@ LoadResult grpc_load(const std::string& socket_path, const std::string& method, 
 // send) and no protocol work at all.  Per-round-trip latency in seconds, n samples after
 // `warmup` untimed ones.  Allocate p50 minus this p50 is what HTTP/2 + HPACK + protobuf +
 // the device table cost.
-std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_bytes);
+std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_bytes, bool server_spin = false);
 
 class FixtureBackend;
 

@@ -285,3 +285,34 @@ def test_native_watch_client_follows_list_and_watch(n, server):
     srv.stop()
     assert c.next_stream_message(5.0) is None  # OK trailers end the stream
     c.close()
+
+
+def test_busy_poll_window_answers_and_idles_without_spinning(n, plugin_dir):
+    """grpc.busyPollUs: after a request the worker polls instead of sleeping, so calls in
+    a burst skip the wake-up; an idle server must not burn CPU (the window closes)."""
+    tc = n.TableConfig()
+    devs = [n.TableDevice("dev-%d" % i, i, 0, 0, -1, ["/dev/dri/renderD%d" % (128 + i)], True) for i in range(4)]
+    table = n.DeviceTable(tc, devs, n.Topology(4))
+    path = os.path.join(plugin_dir, "amd-gpu.sock")
+    srv = n.GrpcServer(path, 2, busy_poll_us=20000)
+    srv.set_table(table)
+    srv.start()
+    try:
+        c = n.H2Client(path)
+        req = v1beta1.AllocateRequest(container_requests=[v1beta1.ContainerAllocateRequest(
+            devices_ids=["dev-2"])]).SerializeToString()
+        for _ in range(200):
+            st, body, _ = c.unary(v1beta1.METHOD_ALLOCATE, req)
+            assert st == 0
+        assert v1beta1.AllocateResponse.FromString(body).container_responses[0].envs["AMD_VISIBLE_DEVICES"] == "dev-2"
+        time.sleep(0.1)  # the 20 ms window has closed
+        cpu0, wall0 = time.process_time(), time.perf_counter()
+        time.sleep(0.5)
+        cpu = time.process_time() - cpu0
+        assert cpu < 0.1 * (time.perf_counter() - wall0), "idle server used %.3f s of CPU" % cpu
+        # a request re-opens the window; the next call is still answered normally
+        st, _, _ = c.unary(v1beta1.METHOD_ALLOCATE, req)
+        assert st == 0
+        c.close()
+    finally:
+        srv.stop()
