@@ -13,9 +13,10 @@ test:             ## CPU suite (fixture backend, gloo)
 	$(PY) -m pytest tests -q -m "not gpu"
 test-gpu:         ## needs an MI355X (e.g. through gpurun)
 	$(PY) -m pytest tests -q -m gpu
-sanitize:         ## native self-test under ASan+UBSan and TSan
+sanitize:         ## native self-test, then the integration tests, under ASan+UBSan and TSan
 	$(PY) -m k8s_gpu_device_plugin_amd._build --sanitize address
 	$(PY) -m k8s_gpu_device_plugin_amd._build --sanitize thread
+	$(PY) -m pytest tests/test_sanitized_suite.py -q
 bench:
 	$(PY) bench.py --gpus 1 --steps 20 --warmup 3
 suite:            ## BASELINE.json configs 1-5 + scaling + health propagation

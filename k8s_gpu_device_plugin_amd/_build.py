@@ -139,6 +139,38 @@ def build_native(force: bool = False, jobs: int | None = None, verbose: bool = T
     return out
 
 
+def sanitized_ext_path(sanitize: str) -> str:
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return os.path.join(BUILD_DIR, "ext-" + sanitize, "_native" + suffix)
+
+
+def build_native_sanitized(sanitize: str, force: bool = False) -> str:
+    """The pybind11 extension itself instrumented (ASan+UBSan or TSan), loaded through
+    ``AMDGPU_DP_NATIVE_SO`` by a Python that preloads the sanitizer runtime, so the
+    integration tests (kubelet stub, manager, both servers) run against it."""
+    flags = _common_flags(sanitize)
+    jobs = min(8, os.cpu_count() or 4)
+    core, c1 = _compile_objects(CORE_SOURCES, os.path.join(BUILD_DIR, "obj-" + sanitize), flags, force, jobs)
+    import pybind11
+    py_flags = flags + ["-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"], "-fvisibility=hidden"]
+    bind, c2 = _compile_objects(BINDING_SOURCES, os.path.join(BUILD_DIR, "obj_py-" + sanitize), py_flags, force, jobs)
+    out = sanitized_ext_path(sanitize)
+    if force or c1 or c2 or not os.path.exists(out):
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        link = [_cxx(), "-shared", "-fsanitize=" + sanitize] + (["-fsanitize=undefined"] if sanitize == "address" else [])
+        _run(link + ["-o", out] + bind + core + _link_libs(), "link sanitized _native")
+    return out
+
+
+def sanitizer_runtime(sanitize: str) -> str:
+    """Path of the compiler's shared sanitizer runtime (to LD_PRELOAD into python)."""
+    lib = {"address": "libasan.so", "thread": "libtsan.so"}[sanitize]
+    out = subprocess.run([_cxx(), "-print-file-name=" + lib], stdout=subprocess.PIPE, text=True).stdout.strip()
+    if not out or not os.path.isabs(out) or not os.path.exists(out):
+        raise RuntimeError("%s not found by %s" % (lib, _cxx()))
+    return os.path.realpath(out)
+
+
 def build_selftest(sanitize: str | None = None, force: bool = False) -> str:
     """Standalone C++ self-test binary (optionally ASan+UBSan or TSan instrumented)."""
     tag = {"address": "-asan", "thread": "-tsan", None: ""}[sanitize]
@@ -241,6 +273,8 @@ def main(argv=None) -> int:
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--sanitize", choices=["address", "thread"], default=None,
                     help="build the native self-test with a sanitizer instead")
+    ap.add_argument("--sanitize-ext", choices=["address", "thread"], default=None,
+                    help="build the pybind11 extension with a sanitizer (under build/ext-<name>/)")
     ap.add_argument("--selftest", action="store_true", help="also build (and run) the native self-test")
     ap.add_argument("--no-canary", action="store_true")
     ap.add_argument("--fuzz", nargs="*", choices=FUZZ_TARGETS, default=None,
@@ -255,6 +289,10 @@ def main(argv=None) -> int:
             print("fuzz_%s: rc=%d\n  %s" % (t, p.returncode, "\n  ".join(tail)))
             rc = rc or p.returncode
         return rc
+    if args.sanitize_ext:
+        print("built", os.path.relpath(build_native_sanitized(args.sanitize_ext, force=args.force), ROOT))
+        print("run with: LD_PRELOAD=%s AMDGPU_DP_NATIVE_SO=<that path>" % sanitizer_runtime(args.sanitize_ext))
+        return 0
     if args.sanitize or args.selftest:
         exe = build_selftest(args.sanitize, force=args.force)
         print("built", os.path.relpath(exe, ROOT))

@@ -4,6 +4,10 @@ or older than ``native/*.cpp|h`` (g++ is part of the plugin's build image).
 There is deliberately no pure-Python fallback for the core: if the extension cannot
 be loaded the plugin fails loudly (a silently slower or partial plugin is worse than a
 crash-looping DaemonSet pod that shows the error).
+
+``AMDGPU_DP_NATIVE_SO=<path>`` loads another build of the same module instead, e.g. the
+ASan+UBSan one from ``python -m k8s_gpu_device_plugin_amd._build --sanitize-ext address``
+that ``tests/test_sanitized_suite.py`` runs the integration tests against.
 """
 from __future__ import annotations
 
@@ -38,6 +42,10 @@ def load():
     with _lock:
         if _mod is not None:
             return _mod
+        alt = os.environ.get("AMDGPU_DP_NATIVE_SO", "")
+        if alt:
+            _mod = _load_file(alt)
+            return _mod
         if os.environ.get("AMDGPU_DP_NO_AUTOBUILD", "") not in ("1", "true") and _stale():
             from . import _build
             _build.build_native(verbose=False)
@@ -47,3 +55,17 @@ def load():
             raise RuntimeError("native core k8s_gpu_device_plugin_amd._native is not built/loadable: %s "
                                "(run: python -m k8s_gpu_device_plugin_amd._build)" % e) from e
         return _mod
+
+
+def _load_file(path: str):
+    import importlib.util
+    import sys
+
+    name = __package__ + "._native"
+    spec = importlib.util.spec_from_file_location(name, path)
+    if spec is None or not os.path.exists(path):
+        raise RuntimeError("AMDGPU_DP_NATIVE_SO=%s: no such extension" % path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    sys.modules[name] = mod
+    return mod
