@@ -242,7 +242,7 @@ def main() -> int:
         step(junk)
     barrier()
     rec = ([], [], [], [], [])
-    scrape_time = 0.0
+    scrape_time, body_len = 0.0, len(body)
     t_start = perf()
     for _ in range(args.steps):
         st, body_len = step(rec)
@@ -260,6 +260,9 @@ def main() -> int:
     mine["uds_floor_p50"] = _pct(floor, 0.5)
     # ... and with a server thread that polls instead of sleeping (the busy-poll window)
     mine["uds_floor_spin_p50"] = _pct(n.uds_pingpong(10000, 500, *sizes, server_spin=True), 0.5)
+    # /metrics: one loopback TCP exchange of a scrape's size, polling server
+    mine["tcp_scrape_floor_p50"] = _pct(n.uds_pingpong(3000, 300, 90, body_len + 400, server_spin=True, tcp=True),
+                                        0.5)
     if world > 1:
         gathered = [None] * world
         dist.all_gather_object(gathered, mine)
@@ -292,6 +295,7 @@ def main() -> int:
             "allocate_p50_us": round(p50, 2), "allocate_p99_us": round(_pct(allocs_native, 0.99) * 1e6, 2),
             "uds_roundtrip_floor_p50_us": round(gathered[0]["uds_floor_p50"] * 1e6, 2),
             "uds_roundtrip_floor_spin_p50_us": round(gathered[0]["uds_floor_spin_p50"] * 1e6, 2),
+            "tcp_scrape_floor_p50_us": round(gathered[0]["tcp_scrape_floor_p50"] * 1e6, 2),
             "allocate_p50_us_grpcio_client": round(p50_grpcio, 2),
             "allocate_p99_us_grpcio_client": round(_pct(allocs, 0.99) * 1e6, 2),
             "preferred_p50_us": round(_pct(prefs_native, 0.5) * 1e6, 2),

@@ -464,6 +464,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("running", &HttpServer::running)
       .def_property_readonly("port", &HttpServer::port)
       .def_property_readonly("requests_total", &HttpServer::requests_total)
+      .def_property_readonly("worker_connections", &HttpServer::worker_connections)
       .def("render_http_metrics", [](const HttpServer& s) {
         std::string o;
         s.render_http_metrics(&o);
@@ -519,6 +520,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("running", &GrpcServer::running)
       .def_property_readonly("requests", &GrpcServer::requests)
       .def_property_readonly("connections", &GrpcServer::connections)
+      .def_property_readonly("worker_connections", &GrpcServer::worker_connections)
       .def_property_readonly("socket_path", &GrpcServer::socket_path);
 
   py::class_<H2Client>(m, "H2Client")
@@ -682,12 +684,12 @@ PYBIND11_MODULE(_native, m) {
     return out;
   });
   m.def("uds_pingpong",
-        [](int n, int warmup, int req_bytes, int resp_bytes, bool server_spin) {
+        [](int n, int warmup, int req_bytes, int resp_bytes, bool server_spin, bool tcp) {
           py::gil_scoped_release rel;
-          return uds_pingpong(n, warmup, req_bytes, resp_bytes, server_spin);
+          return uds_pingpong(n, warmup, req_bytes, resp_bytes, server_spin, tcp);
         },
         py::arg("n") = 10000, py::arg("warmup") = 500, py::arg("req_bytes") = 128, py::arg("resp_bytes") = 256,
-        py::arg("server_spin") = false);
+        py::arg("server_spin") = false, py::arg("tcp") = false);
   m.def("grpc_load",
         [load_dict](const std::string& sock, const std::string& method, const py::bytes& req, int conns,
                     double duration_s) {

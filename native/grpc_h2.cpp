@@ -211,6 +211,11 @@ struct GrpcServer::Worker {
     bool want_out = false;
   };
   std::unordered_map<int, std::unique_ptr<Conn>> conns;
+  // Connections are spread over the workers: the one that accepts hands a new
+  // connection to the least-loaded worker, which adopts it on its first event.
+  std::mutex in_mu;
+  std::vector<std::unique_ptr<Conn>> incoming;
+  std::atomic<int> load{0};  // owned + incoming connections
 };
 
 using Conn = GrpcServer::Worker::Conn;
@@ -352,6 +357,13 @@ void GrpcServer::start() {
   notifier_->srv = this;
 }
 
+std::vector<int> GrpcServer::worker_connections() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<int> out;
+  for (const auto& w : workers_) out.push_back(w->load.load(std::memory_order_relaxed));
+  return out;
+}
+
 void GrpcServer::notify() {
   for (auto& w : workers_) {
     const uint64_t one = 1;
@@ -372,6 +384,11 @@ void GrpcServer::stop() {
     if (t.joinable()) t.join();
   threads_.clear();
   for (auto& w : workers_) {
+    for (auto& c : w->incoming) {  // handed over after its owner had already left its loop
+      ::close(c->fd);
+      conns_.fetch_sub(1);
+    }
+    w->incoming.clear();
     if (w->ep >= 0) ::close(w->ep);
     if (w->efd >= 0) ::close(w->efd);
   }
@@ -394,6 +411,16 @@ void GrpcServer::run(Worker* w) {
     ::close(fd);
     w->conns.erase(fd);
     conns_.fetch_sub(1);
+    w->load.fetch_sub(1, std::memory_order_relaxed);
+  };
+  auto adopt = [&] {
+    std::lock_guard<std::mutex> lk(w->in_mu);
+    for (auto& c : w->incoming) {
+      c->serial = w->next_serial++;
+      const int fd = c->fd;
+      w->conns.emplace(fd, std::move(c));
+    }
+    w->incoming.clear();
   };
   // returns false if the connection was closed
   auto flush = [&](Conn* c) -> bool {
@@ -843,9 +870,12 @@ void GrpcServer::run(Worker* w) {
         for (;;) {
           const int cfd = accept4(listen_fd_, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
           if (cfd < 0) break;
+          Worker* t = w;  // least-loaded worker, this one on a tie
+          for (auto& o : workers_)
+            if (o->load.load(std::memory_order_relaxed) < t->load.load(std::memory_order_relaxed)) t = o.get();
+          t->load.fetch_add(1, std::memory_order_relaxed);
           auto c = std::make_unique<Conn>();
           c->fd = cfd;
-          c->serial = w->next_serial++;
           // server preface: SETTINGS(MAX_CONCURRENT_STREAMS, INITIAL_WINDOW_SIZE) + conn window
           frame(&c->out, 12, kSettings, 0, 0);
           c->out.push_back(0);
@@ -855,19 +885,34 @@ void GrpcServer::run(Worker* w) {
           c->out.push_back(4);
           put_u32(&c->out, static_cast<uint32_t>(kLocalWindow));
           window_update(&c->out, 0, static_cast<uint32_t>(kLocalWindow - 65535));
+          conns_.fetch_add(1);
           struct epoll_event ev {};
           ev.events = EPOLLIN | EPOLLRDHUP;
           ev.data.fd = cfd;
+          if (t != w) {  // EPOLLOUT: the owner wakes at once, adopts it and sends the preface
+            c->want_out = true;
+            {
+              std::lock_guard<std::mutex> lk(t->in_mu);
+              t->incoming.push_back(std::move(c));
+            }
+            ev.events |= EPOLLOUT;
+            epoll_ctl(t->ep, EPOLL_CTL_ADD, cfd, &ev);
+            continue;
+          }
+          c->serial = w->next_serial++;
           epoll_ctl(w->ep, EPOLL_CTL_ADD, cfd, &ev);
           Conn* cp = c.get();
           w->conns.emplace(cfd, std::move(c));
-          conns_.fetch_add(1);
           flush(cp);
         }
         continue;
       }
       auto it = w->conns.find(fd);
-      if (it == w->conns.end()) continue;
+      if (it == w->conns.end()) {
+        adopt();
+        it = w->conns.find(fd);
+        if (it == w->conns.end()) continue;
+      }
       Conn* c = it->second.get();
       if (evs[i].events & EPOLLERR) {
         close_conn(fd);
@@ -914,6 +959,7 @@ void GrpcServer::run(Worker* w) {
       }
     }
   }
+  adopt();
   // shutdown: finish open streams with OK trailers (like the reference's ListAndWatch
   // returning nil on stop), GOAWAY, best-effort flush, close.
   for (auto& kv : w->conns) {

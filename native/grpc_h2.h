@@ -42,6 +42,7 @@ class GrpcServer {
   bool running() const { return running_.load(); }
   uint64_t requests() const { return requests_.load(); }
   int connections() const { return conns_.load(); }
+  std::vector<int> worker_connections() const;  // connections owned per worker thread
   const std::string& socket_path() const { return path_; }
 
   struct Worker;
@@ -70,7 +71,7 @@ class GrpcServer {
   std::atomic<int> conns_{0};
   std::vector<std::unique_ptr<Worker>> workers_;
   std::vector<std::thread> threads_;
-  std::mutex mu_;
+  mutable std::mutex mu_;
 };
 
 class H2Client {

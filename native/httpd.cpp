@@ -109,6 +109,11 @@ struct Conn {
 struct HttpServer::Worker {
   int ep = -1;
   std::unordered_map<int, std::unique_ptr<Conn>> conns;
+  // the accepting worker hands each connection to the least-loaded worker (see
+  // GrpcServer::Worker): concurrent scrapers are served in parallel, not queued on one
+  std::mutex in_mu;
+  std::vector<std::unique_ptr<Conn>> incoming;
+  std::atomic<int> load{0};
 };
 
 HttpServer::HttpServer(HttpConfig cfg, std::shared_ptr<Exporter> exporter)
@@ -178,6 +183,15 @@ int HttpServer::start() {
         epoll_ctl(w->ep, EPOLL_CTL_DEL, cfd, nullptr);
         close(cfd);
         w->conns.erase(cfd);
+        w->load.fetch_sub(1, std::memory_order_relaxed);
+      };
+      auto adopt = [&] {
+        std::lock_guard<std::mutex> lk(w->in_mu);
+        for (auto& c : w->incoming) {
+          const int cfd = c->fd;
+          w->conns.emplace(cfd, std::move(c));
+        }
+        w->incoming.clear();
       };
       auto flush = [&](Conn* c) -> bool {  // false => connection closed
         while (c->out_off < c->out.size()) {
@@ -244,16 +258,34 @@ int HttpServer::start() {
               else if (peer.ss_family == AF_INET6)
                 inet_ntop(AF_INET6, &reinterpret_cast<sockaddr_in6*>(&peer)->sin6_addr, ip, sizeof(ip));
               c->remote = ip;
+              Worker* t = w;  // least-loaded worker, this one on a tie
+              for (auto& o : workers_)
+                if (o->load.load(std::memory_order_relaxed) < t->load.load(std::memory_order_relaxed)) t = o.get();
+              t->load.fetch_add(1, std::memory_order_relaxed);
               struct epoll_event ev {};
               ev.events = EPOLLIN | EPOLLRDHUP;
               ev.data.fd = cfd;
+              if (t != w) {  // EPOLLOUT: the owner wakes at once and adopts it (idle sweep included)
+                c->want_out = true;
+                ev.events |= EPOLLOUT;
+                {
+                  std::lock_guard<std::mutex> lk(t->in_mu);
+                  t->incoming.push_back(std::move(c));
+                }
+                epoll_ctl(t->ep, EPOLL_CTL_ADD, cfd, &ev);
+                continue;
+              }
               epoll_ctl(w->ep, EPOLL_CTL_ADD, cfd, &ev);
               w->conns.emplace(cfd, std::move(c));
             }
             continue;
           }
           auto it = w->conns.find(fd);
-          if (it == w->conns.end()) continue;
+          if (it == w->conns.end()) {
+            adopt();
+            it = w->conns.find(fd);
+            if (it == w->conns.end()) continue;
+          }
           Conn* c = it->second.get();
           c->last_ns = now;
           if (evs[i].events & EPOLLERR) {
@@ -389,6 +421,7 @@ int HttpServer::start() {
           for (int fd : dead) close_conn(fd);
         }
       }
+      adopt();
       for (auto& kv : w->conns) close(kv.first);
       w->conns.clear();
     });
@@ -405,6 +438,12 @@ int HttpServer::start() {
   return bound_port_;
 }
 
+std::vector<int> HttpServer::worker_connections() const {
+  std::vector<int> out;
+  for (const auto& w : workers_) out.push_back(w->load.load(std::memory_order_relaxed));
+  return out;
+}
+
 void HttpServer::stop() {
   if (!running_.exchange(false)) return;
   stop_ = true;
@@ -412,8 +451,11 @@ void HttpServer::stop() {
     if (t.joinable()) t.join();
   threads_.clear();
   if (log_thread_.joinable()) log_thread_.join();
-  for (auto& w : workers_)
+  for (auto& w : workers_) {
+    for (auto& c : w->incoming) close(c->fd);  // handed over after its owner had left its loop
+    w->incoming.clear();
     if (w->ep >= 0) close(w->ep);
+  }
   workers_.clear();
   if (listen_fd_ >= 0) close(listen_fd_);
   listen_fd_ = -1;

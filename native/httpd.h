@@ -46,6 +46,7 @@ class HttpServer {
   int port() const { return bound_port_; }
   void set_restart_hook(std::function<void()> hook);
   uint64_t requests_total() const { return requests_.load(); }
+  std::vector<int> worker_connections() const;  // connections owned per worker thread
   // Renders the echo_http_* families (exposed for tests).
   void render_http_metrics(std::string* out) const;
 

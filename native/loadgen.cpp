@@ -173,12 +173,41 @@ LoadResult grpc_load(const std::string& socket_path, const std::string& method, 
   return total;
 }
 
-std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_bytes, bool server_spin) {
-  if (n < 0 || warmup < 0 || req_bytes <= 0 || resp_bytes <= 0 || req_bytes > (1 << 20) || resp_bytes > (1 << 20))
+namespace {
+
+// A connected loopback TCP pair (client, server), both with TCP_NODELAY like the
+// loadgen's and the HTTP server's sockets.
+bool tcp_pair(int sv[2]) {
+  const int lfd = socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  if (lfd < 0) return false;
+  struct sockaddr_in a {};
+  a.sin_family = AF_INET;
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  socklen_t al = sizeof(a);
+  bool ok = bind(lfd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) == 0 && listen(lfd, 1) == 0 &&
+            getsockname(lfd, reinterpret_cast<sockaddr*>(&a), &al) == 0;
+  sv[0] = ok ? socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0) : -1;
+  ok = ok && sv[0] >= 0 && connect(sv[0], reinterpret_cast<sockaddr*>(&a), sizeof(a)) == 0;
+  sv[1] = ok ? accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC) : -1;
+  close(lfd);
+  if (!ok || sv[1] < 0) {
+    if (sv[0] >= 0) close(sv[0]);
+    return false;
+  }
+  int one = 1;
+  setsockopt(sv[0], IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  setsockopt(sv[1], IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  return true;
+}
+
+}  // namespace
+
+std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_bytes, bool server_spin, bool tcp) {
+  if (n < 0 || warmup < 0 || req_bytes <= 0 || resp_bytes <= 0 || req_bytes > (1 << 20) || resp_bytes > (4 << 20))
     throw std::invalid_argument("uds_pingpong: bad sizes");
   int sv[2];
-  if (socketpair(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0, sv) != 0)
-    throw std::runtime_error(std::string("socketpair: ") + strerror(errno));
+  if (tcp ? !tcp_pair(sv) : socketpair(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0, sv) != 0)
+    throw std::runtime_error(std::string(tcp ? "tcp loopback pair: " : "socketpair: ") + strerror(errno));
   const int cfd = sv[0], sfd = sv[1];
   fcntl(sfd, F_SETFL, fcntl(sfd, F_GETFL) | O_NONBLOCK);
   struct timeval tv {5, 0};  // a dead server thread ends the client's recv, not the process

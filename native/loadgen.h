@@ -31,8 +31,10 @@ LoadResult grpc_load(const std::string& socket_path, const std::string& method, 
 // plugin's Allocate path makes (client send + blocking recv; server epoll_wait + recv +
 // send) and no protocol work at all.  Per-round-trip latency in seconds, n samples after
 // `warmup` untimed ones.  Allocate p50 minus this p50 is what HTTP/2 + HPACK + protobuf +
-// the device table cost.
-std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_bytes, bool server_spin = false);
+// the device table cost.  tcp=true: the same over a loopback TCP connection, the floor
+// of one /metrics scrape of resp_bytes (what the kernel's copies and wake-ups cost).
+std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_bytes, bool server_spin = false,
+                                 bool tcp = false);
 
 class FixtureBackend;
 

@@ -12,6 +12,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <string_view>
 #include <vector>
@@ -82,6 +83,7 @@ class AtomicDouble {
       if (bits_.compare_exchange_weak(old, nb, std::memory_order_relaxed)) return;
     }
   }
+  uint64_t bits() const { return bits_.load(std::memory_order_relaxed); }
   double load() const {
     const uint64_t b = bits_.load(std::memory_order_relaxed);
     double d;
@@ -115,10 +117,39 @@ class Histogram {
     for (auto& x : counts_) c += x.load(std::memory_order_relaxed);
     return c;
   }
-  // labels: already-formatted `k="v",` prefix (may be empty)
+  // labels: already-formatted `k="v",` prefix (may be empty).  A scrape renders every
+  // histogram, but most of them (kubelet RPCs, sampling passes) have not moved since the
+  // previous scrape: their text is cached under (count, sum) and re-used.  The key is
+  // read before the buckets, and both only grow, so a cached text is never older than
+  // its key: an observation that lands mid-render changes the next key and forces a
+  // re-render.
   void render(std::string* out, const char* name, std::string_view labels) const {
+    const uint64_t key_count = count();
+    const uint64_t key_sum = sum_.bits();
+    {
+      std::lock_guard<std::mutex> lk(cache_mu_);
+      if (cache_valid_ && key_count == cache_count_ && key_sum == cache_sum_ && cache_name_ == name &&
+          cache_labels_ == labels) {
+        out->append(cache_);
+        return;
+      }
+    }
+    std::string text;
+    render_uncached(&text, name, labels);
+    out->append(text);
+    std::lock_guard<std::mutex> lk(cache_mu_);
+    cache_.swap(text);
+    cache_count_ = key_count;
+    cache_sum_ = key_sum;
+    cache_name_ = name;
+    cache_labels_.assign(labels.data(), labels.size());
+    cache_valid_ = true;
+  }
+
+  void render_uncached(std::string* out, const char* name, std::string_view labels) const {
     std::string prefix(name);
     prefix.append("_bucket{").append(labels.data(), labels.size()).append("le=\"");
+    out->reserve(out->size() + (prefix.size() + 24) * (bounds_.size() + 3));
     uint64_t cum = 0;
     for (size_t i = 0; i <= bounds_.size(); ++i) {
       cum += counts_[i].load(std::memory_order_relaxed);
@@ -145,6 +176,10 @@ class Histogram {
   std::vector<std::string> le_;
   std::vector<std::atomic<uint64_t>> counts_;
   AtomicDouble sum_;
+  mutable std::mutex cache_mu_;
+  mutable bool cache_valid_ = false;
+  mutable uint64_t cache_count_ = 0, cache_sum_ = 0;
+  mutable std::string cache_, cache_name_, cache_labels_;
 };
 
 // RPC latency buckets: 5 us .. 1 s (the echo buckets start at 500 us, too coarse

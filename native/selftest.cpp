@@ -481,12 +481,54 @@ static void test_reload_races(const std::string& dir) {
   }
 }
 
+// Histogram render cache: a cached text is reused only while nothing was observed,
+// never mixes name/label sets, and concurrent observe + render (scrapes on several
+// HTTP workers) always ends at the exact final counts.
+static void test_histogram_render_cache() {
+  Histogram h(rpc_buckets());
+  std::string a, b, c;
+  h.render(&a, "x_seconds", "rpc=\"a\",");
+  h.render(&b, "x_seconds", "rpc=\"a\",");
+  CHECK(a == b);
+  h.observe(3e-6);
+  h.render(&c, "x_seconds", "rpc=\"a\",");
+  CHECK(c != a && c.find("x_seconds_count{rpc=\"a\"} 1\n") != std::string::npos);
+  std::string d;
+  h.render(&d, "y_seconds", "");
+  CHECK(d.find("y_seconds_count 1\n") != std::string::npos && d.find("x_seconds") == std::string::npos);
+  std::string u;
+  h.render_uncached(&u, "y_seconds", "");
+  CHECK(u == d);
+  std::atomic<bool> go{true};
+  std::vector<std::thread> rs;
+  for (int t = 0; t < 3; ++t)
+    rs.emplace_back([&] {
+      std::string o;
+      while (go.load()) {
+        o.clear();
+        h.render(&o, "x_seconds", "rpc=\"a\",");
+      }
+    });
+  std::thread w([&] {
+    for (int i = 0; i < 20000; ++i) h.observe(1e-4);
+  });
+  w.join();
+  go = false;
+  for (auto& t : rs) t.join();
+  std::string fin, ref;
+  h.render(&fin, "x_seconds", "rpc=\"a\",");
+  h.render_uncached(&ref, "x_seconds", "rpc=\"a\",");
+  CHECK(fin == ref && fin.find("x_seconds_count{rpc=\"a\"} 20001\n") != std::string::npos);
+}
+
 int main() {
   char tmpl[] = "/tmp/amdgpu-selftest-XXXXXX";
   const char* dir = mkdtemp(tmpl);
   if (!dir) return 2;
   std::fprintf(stderr, "[selftest] hpack\n");
   test_hpack();
+  std::fprintf(stderr, "[selftest] histogram render cache\n");
+  test_histogram_render_cache();
   std::fprintf(stderr, "[selftest] allocator + table\n");
   auto be = make_node(8, 8);
   test_allocator_and_table(be);

@@ -316,3 +316,44 @@ def test_busy_poll_window_answers_and_idles_without_spinning(n, plugin_dir):
         c.close()
     finally:
         srv.stop()
+
+
+def test_connections_spread_over_workers(n, plugin_dir):
+    """Concurrent kubelet-side clients (bench ranks, kubelet + a debugging client) are
+    owned by different worker threads, not queued behind one that accepted them all."""
+    tc = n.TableConfig()
+    devs = [n.TableDevice("dev-%d" % i, i, 0, 0, -1, ["/dev/dri/renderD%d" % (128 + i)], True) for i in range(4)]
+    table = n.DeviceTable(tc, devs, n.Topology(4))
+    path = os.path.join(plugin_dir, "amd-gpu.sock")
+    srv = n.GrpcServer(path, 4, busy_poll_us=50)
+    srv.set_table(table)
+    srv.start()
+    try:
+        req = v1beta1.AllocateRequest(container_requests=[v1beta1.ContainerAllocateRequest(
+            devices_ids=["dev-1"])]).SerializeToString()
+        clients = [n.H2Client(path) for _ in range(4)]
+        for c in clients:  # every handed-over connection is adopted and answers
+            assert c.unary(v1beta1.METHOD_ALLOCATE, req)[0] == 0
+        assert sorted(srv.worker_connections) == [1, 1, 1, 1]
+        errors = []
+
+        def hammer(c):
+            try:
+                for _ in range(300):
+                    assert c.unary(v1beta1.METHOD_ALLOCATE, req)[0] == 0
+            except Exception as e:  # pragma: no cover - reported below
+                errors.append(e)
+        ts = [threading.Thread(target=hammer, args=(c,)) for c in clients]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(60)
+        assert not errors and srv.requests >= 1204
+        for c in clients:
+            c.close()
+        deadline = time.time() + 5
+        while sum(srv.worker_connections) and time.time() < deadline:
+            time.sleep(0.02)
+        assert srv.worker_connections == [0, 0, 0, 0] and srv.connections == 0
+    finally:
+        srv.stop()

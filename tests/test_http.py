@@ -197,3 +197,29 @@ def test_access_log_lines(make_cfg, capfd):
     rec = json.loads(line)
     assert rec["method"] == "GET" and rec["status"] == 200 and rec["user_agent"] == "probe/1"
     assert rec["remote_ip"] == "127.0.0.1" and rec["bytes_out"] > 0 and "latency" in rec
+
+
+def test_native_scrapers_spread_over_workers(make_cfg):
+    """Concurrent keep-alive scrapers are owned by different HTTP workers (the accepting
+    worker hands each connection to the least-loaded one) and all get answers."""
+    cfg = make_cfg(webListenAddress="127.0.0.1:0", http={"server": "native", "accessLog": False, "threads": 3})
+    mgr = PluginManager(cfg)
+    mgr.load_plugins()
+    w = WebServer(cfg, mgr)
+    port = w.start()
+    try:
+        conns = [http.client.HTTPConnection("127.0.0.1", port, timeout=5) for _ in range(3)]
+        for _ in range(5):
+            for c in conns:
+                c.request("GET", "/metrics")
+                r = c.getresponse()
+                assert r.status == 200 and b"process_start_time_seconds" in r.read()
+        assert sorted(w._impl.worker_connections) == [1, 1, 1]
+        for c in conns:
+            c.close()
+        deadline = time.time() + 5
+        while sum(w._impl.worker_connections) and time.time() < deadline:
+            time.sleep(0.02)
+        assert w._impl.worker_connections == [0, 0, 0]
+    finally:
+        w.stop()
