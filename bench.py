@@ -95,14 +95,17 @@ def start_daemon(n_gpus: int, grpc_server: str, workdir: str, profile_dir: str =
     kubelet = KubeletStub(plugin_dir).start()
     port = _free_port()
     cfg_path = os.path.join(workdir, "bench-config.yml")
-    threads = max(4, n_gpus)  # one server worker per concurrent kubelet-client rank
+    # one server worker per client connection: every rank holds two kubelet-side
+    # connections (compiled h2 + grpcio) and SCRAPE_CONNS scrapers
+    grpc_threads = max(4, 2 * n_gpus)
+    http_threads = max(4, SCRAPE_CONNS * n_gpus)
     bp = "" if busy_poll_us is None else "  busyPollUs: %d\n" % busy_poll_us
     with open(cfg_path, "w") as f:
         f.write("webListenAddress: \"127.0.0.1:%d\"\nmigStrategy: none\nbackend: %s\nfixture: %dgpu_spx\n"
                 "devices: \"0-%d\"\npluginDir: \"%s\"\nlog:\n  level: info\n  fileDir: \"\"\n"
                 "http:\n  accessLog: false\n  threads: %d\n%stelemetry:\n  intervalMs: 1000\n"
                 "grpc:\n  server: %s\n  threads: %d\n%s"
-                % (port, backend, n_gpus, n_gpus - 1, plugin_dir, threads, bp, grpc_server, threads, bp))
+                % (port, backend, n_gpus, n_gpus - 1, plugin_dir, http_threads, bp, grpc_server, grpc_threads, bp))
         if profile_dir:  # benchmark: true -> cpu/mem/threads/native profiles when the daemon exits
             f.write("benchmark: true\nbenchmarkDir: \"%s\"\n" % os.path.abspath(profile_dir))
     env = dict(os.environ)
