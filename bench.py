@@ -313,7 +313,10 @@ def main() -> int:
             "canary": ({"arch": can[0]["arch"], "hbm_read_gbps": round(min(c["read_gbps"] for c in can), 1),
                         "hbm_write_gbps": round(min(c["write_gbps"] for c in can), 1),
                         "mfma_bf16_tflops": round(min(c["mfma_tflops"] for c in can), 1),
-                        "lds_gemm_bf16_tflops": round(min(c["gemm_tflops"] for c in can), 1)} if can else None),
+                        "lds_gemm_bf16_tflops": round(min(c["gemm_tflops"] for c in can), 1),
+                        "mfma_mxfp8_tflops": round(min(c["fp8_tflops"] for c in can), 1),
+                        "mfma_mxfp4_tflops": round(min(c["fp4_tflops"] for c in can), 1),
+                        "lds_march_kb": min(c["lds_bytes"] for c in can) // 1024} if can else None),
         }
         print(json.dumps(out), flush=True)
     client.close()

@@ -50,7 +50,8 @@ CORE_SOURCES = [
 BINDING_SOURCES = ["bindings.cpp"]
 FUZZ_TARGETS = ("pbwire", "hpack", "grpc", "http")
 FUZZ_DIR = os.path.join(NATIVE_DIR, "fuzz")
-CANARY_SOURCE = os.path.join(PKG_DIR, "ops", "canary.hip")
+CANARY_SOURCES = [os.path.join(PKG_DIR, "ops", f) for f in ("canary.hip", "datapath.hip")]
+CANARY_HEADERS = [os.path.join(PKG_DIR, "ops", "canary_common.h")]
 CANARY_LIB = os.path.join(PKG_DIR, "ops", "libamdgpu_canary.so")
 
 
@@ -253,10 +254,10 @@ def build_canary(force: bool = False, verbose: bool = True) -> str:
     hipcc = hipcc_path()
     if hipcc is None:
         raise RuntimeError("hipcc not found under %s/bin" % ROCM)
-    if force or _stale(CANARY_LIB, [CANARY_SOURCE]):
+    if force or _stale(CANARY_LIB, CANARY_SOURCES + CANARY_HEADERS):
         tmp = CANARY_LIB + ".tmp"
         _run([hipcc, "--offload-arch=" + OFFLOAD_ARCH, "-O3", "-std=c++17", "-shared", "-fPIC",
-              "-Wall", "-o", tmp, CANARY_SOURCE], "hipcc canary")
+              "-Wall", "-o", tmp] + CANARY_SOURCES, "hipcc canary")
         os.replace(tmp, CANARY_LIB)
         if verbose:
             print("built", os.path.relpath(CANARY_LIB, ROOT))

@@ -17,6 +17,8 @@
 //      using the documented gfx950 fragment maps (cdna_hip_programming.md §3).
 //   3. MFMA throughput   - register-resident 32x32x16 bf16 MFMA chains, 4 waves
 //      per block (one per SIMD), 8 blocks per CU -> dense bf16 TFLOP/s.
+//   4. Matrix path       - LDS-staged MFMA GEMM on exact integer data, ABFT-checked.
+//   5. fp8 / bf8 / fp4 MFMA exactness and rate, LDS march (datapath.hip).
 //
 // C ABI for ctypes (k8s_gpu_device_plugin_amd/ops/canary.py).
 #include <hip/hip_runtime.h>
@@ -25,18 +27,11 @@
 #include <cstdio>
 #include <cstring>
 
+#include "canary_common.h"
+
 namespace {
 
-constexpr int kWave = 64;
-
-__device__ __forceinline__ uint32_t mix32(uint64_t x) {
-  x ^= x >> 33;
-  x *= 0xff51afd7ed558ccdull;
-  x ^= x >> 33;
-  x *= 0xc4ceb9fe1a85ec53ull;
-  x ^= x >> 33;
-  return static_cast<uint32_t>(x);
-}
+using namespace canary;
 
 // Address-derived 16-byte pattern, ~5 integer ops per word so the verify pass stays
 // HBM-bound: lo * odd constant is a bijection mod 2^32, so no two words of a <=64 GiB
@@ -53,24 +48,12 @@ __device__ __forceinline__ uint32_t diff(const uint4& a, const uint4& b) {
 }
 
 using bf16x8 = __attribute__((ext_vector_type(8))) short;
-using f32x16 = __attribute__((ext_vector_type(16))) float;
-
-// small integer in [-4, 4] from a hash: exactly representable in bf16
-__device__ __forceinline__ int small_int(uint64_t key) { return static_cast<int>(mix32(key) % 9u) - 4; }
 
 __device__ __forceinline__ short bf16_of_int(int v) {
   const float f = static_cast<float>(v);
   uint32_t u;
   __builtin_memcpy(&u, &f, 4);
   return static_cast<short>(u >> 16);  // exact for small integers
-}
-
-__device__ __forceinline__ int a_val(uint32_t blk, int row, int k) {
-  return small_int((static_cast<uint64_t>(blk) << 40) ^ (static_cast<uint64_t>(row) << 20) ^ static_cast<uint64_t>(k));
-}
-__device__ __forceinline__ int b_val(uint32_t blk, int k, int col) {
-  return small_int(0x5555ull ^ (static_cast<uint64_t>(blk) << 40) ^ (static_cast<uint64_t>(k) << 20) ^
-                   static_cast<uint64_t>(col) ^ (1ull << 62));
 }
 
 // One wave per block computes C[32x32] = A[32xK] * B[Kx32] with K = 16 * ksteps, then
@@ -763,7 +746,21 @@ struct amdgpu_canary_result {
   char error[256];
   double gemm_tflops;                   // LDS-staged MFMA GEMM (matrix path) rate
   unsigned long long gemm_errors;       // ABFT row/column checksum mismatches
+  double fp8_tflops;                    // block-scaled fp8 MFMA rate (datapath.hip)
+  double fp4_tflops;                    // block-scaled fp4 MFMA rate
+  unsigned long long lowp_errors;       // fp8 / bf8 / fp4 MFMA exactness mismatches
+  unsigned long long lds_errors;        // LDS march mismatches
+  unsigned long long lds_bytes;         // LDS bytes per workgroup the march covered
 };
+
+struct amdgpu_canary_datapath_result {  // datapath.hip
+  double fp8_tflops;
+  double fp4_tflops;
+  unsigned long long lowp_errors;
+  unsigned long long lds_errors;
+  unsigned long long lds_bytes;
+};
+int amdgpu_canary_datapaths(int device, int iters, amdgpu_canary_datapath_result* out, char* err, int err_len);
 
 int amdgpu_canary_device_count() {
   int n = 0;
@@ -861,7 +858,22 @@ int amdgpu_canary_run(int device, unsigned long long hbm_bytes, int passes, int 
                                 sizeof(out->error)) != 0)
       goto done;
   }
-  out->ok = (out->hbm_errors == 0 && out->mfma_errors == 0 && out->gemm_errors == 0) ? 1 : 0;
+  // low-precision datapaths (fp8 / bf8 / fp4 MFMA) and the LDS
+  {
+    amdgpu_canary_datapath_result dp;
+    if (amdgpu_canary_datapaths(device, mfma_iters / 4 > 0 ? mfma_iters / 4 : 1, &dp, out->error,
+                                sizeof(out->error)) != 0)
+      goto done;
+    out->fp8_tflops = dp.fp8_tflops;
+    out->fp4_tflops = dp.fp4_tflops;
+    out->lowp_errors = dp.lowp_errors;
+    out->lds_errors = dp.lds_errors;
+    out->lds_bytes = dp.lds_bytes;
+  }
+  out->ok = (out->hbm_errors == 0 && out->mfma_errors == 0 && out->gemm_errors == 0 && out->lowp_errors == 0 &&
+             out->lds_errors == 0)
+                ? 1
+                : 0;
 done:
   if (e0) (void)hipEventDestroy(e0);
   if (e1) (void)hipEventDestroy(e1);

@@ -1,9 +1,10 @@
 """Python face of the gfx950 health canary (``ops/canary.hip``).
 
 ``run(device)`` loads ``libamdgpu_canary.so`` with ctypes (no torch needed) and runs
-the HBM pattern test, the MFMA exactness/throughput probe and the matrix-path check
-(an LDS-staged MFMA GEMM on exact integer data with ABFT row/column checksums) on one
-HIP device (= one compute partition).  ``run_isolated(device)`` does the same in a child process so the
+the HBM pattern test, the MFMA exactness/throughput probe, the matrix-path check
+(an LDS-staged MFMA GEMM on exact integer data with ABFT row/column checksums), the
+fp8 / bf8 / fp4 MFMA exactness and rate checks and the LDS march (``datapath.hip``) on
+one HIP device (= one compute partition).  ``run_isolated(device)`` does the same in a child process so the
 long-lived plugin daemon never creates a HIP context on GPUs it hands to pods.
 
 CLI: ``python -m k8s_gpu_device_plugin_amd.ops.canary --device 0 [--bytes N]`` prints
@@ -27,7 +28,9 @@ class CanaryResult(ctypes.Structure):
                 ("write_gbps", ctypes.c_double), ("read_gbps", ctypes.c_double), ("mfma_tflops", ctypes.c_double),
                 ("elapsed_ms", ctypes.c_double), ("num_cus", ctypes.c_int), ("arch", ctypes.c_char * 64),
                 ("error", ctypes.c_char * 256), ("gemm_tflops", ctypes.c_double),
-                ("gemm_errors", ctypes.c_ulonglong)]
+                ("gemm_errors", ctypes.c_ulonglong), ("fp8_tflops", ctypes.c_double),
+                ("fp4_tflops", ctypes.c_double), ("lowp_errors", ctypes.c_ulonglong),
+                ("lds_errors", ctypes.c_ulonglong), ("lds_bytes", ctypes.c_ulonglong)]
 
 
 _lib = None
@@ -64,6 +67,16 @@ def load():
                                                 ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                                 ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_char_p, ctypes.c_int]
         lib.amdgpu_canary_gemm_rate.restype = ctypes.c_int
+        lib.amdgpu_canary_lowp_check.argtypes = [ctypes.c_int] * 5
+        lib.amdgpu_canary_lowp_check.restype = ctypes.c_longlong
+        lib.amdgpu_canary_lowp_rate.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                ctypes.POINTER(ctypes.c_double)]
+        lib.amdgpu_canary_lowp_rate.restype = ctypes.c_int
+        lib.amdgpu_canary_lds_check.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_ulonglong)]
+        lib.amdgpu_canary_lds_check.restype = ctypes.c_longlong
+        lib.amdgpu_canary_lowp_gemm.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 5 + \
+            [ctypes.c_int] * 3 + [ctypes.c_char_p, ctypes.c_int]
+        lib.amdgpu_canary_lowp_gemm.restype = ctypes.c_int
         _lib = lib
     return _lib
 
@@ -91,6 +104,63 @@ def mfma_detects_corruption(device: int = 0, inject_blocks: int = 3) -> int:
     """Fault-injection check of the MFMA exactness verifier; returns the wrong
     accumulator registers it found (0 expected with inject_blocks=0)."""
     return int(load().amdgpu_canary_mfma_detects(int(device), int(inject_blocks)))
+
+
+# cbsz/blgp format codes of v_mfma_scale_f32_32x32x64_f8f6f4 (OCP formats); "fp8_unscaled" is
+# v_mfma_f32_32x32x16_fp8_fp8
+LOWP_FORMATS = {"fp8": 0, "bf8": 1, "fp4": 4, "fp8_unscaled": 8}
+
+
+def lowp_check(device: int = 0, fmt: str = "fp8", ksteps: int = 4, vary_scale: bool = True,
+               inject_blocks: int = 0) -> int:
+    """Exactness of one low-precision MFMA form on small-integer operands with power-of-two
+    block scales (2 single-wave blocks per CU, K = 64 * ksteps); returns the wrong
+    accumulator registers (0 expected unless ``inject_blocks`` perturb an operand)."""
+    rc = load().amdgpu_canary_lowp_check(int(device), LOWP_FORMATS[fmt], int(ksteps), int(bool(vary_scale)),
+                                         int(inject_blocks))
+    if rc < 0:
+        raise RuntimeError("lowp_check(%s) failed on device %d" % (fmt, device))
+    return int(rc)
+
+
+def lowp_rate(device: int = 0, fmt: str = "fp8", iters: int = 2048) -> float:
+    """Dense TFLOP/s of the block-scaled MFMA on ``fmt`` (fp8, bf8 or fp4)."""
+    t = ctypes.c_double()
+    if load().amdgpu_canary_lowp_rate(int(device), LOWP_FORMATS[fmt], int(iters), ctypes.byref(t)) != 0:
+        raise RuntimeError("lowp_rate(%s) failed on device %d" % (fmt, device))
+    return t.value
+
+
+def lds_check(device: int = 0, inject_blocks: int = 0) -> tuple:
+    """LDS march over every CU's whole LDS; returns (mismatches, bytes per workgroup)."""
+    nbytes = ctypes.c_ulonglong()
+    rc = load().amdgpu_canary_lds_check(int(device), int(inject_blocks), ctypes.byref(nbytes))
+    if rc < 0:
+        raise RuntimeError("lds_check failed on device %d" % device)
+    return int(rc), int(nbytes.value)
+
+
+def lowp_gemm(a_codes, bt_codes, a_scales, b_scales, fmt: str = "fp8", device: int = 0):
+    """C = dequant(A) @ dequant(Bt).T through the block-scaled MFMA.  ``a_codes`` uint8 [M, K]
+    and ``bt_codes`` uint8 [N, K] hold one OCP code per element (fp4 in the low nibble);
+    ``a_scales`` [M, K/32], ``b_scales`` [N, K/32] are E8M0 exponents (127 = 1.0).
+    M, N % 32 == 0, K % 64 == 0.  Returns float32 [M, N]."""
+    import numpy as np
+
+    a = np.ascontiguousarray(a_codes, dtype=np.uint8)
+    bt = np.ascontiguousarray(bt_codes, dtype=np.uint8)
+    sa = np.ascontiguousarray(a_scales, dtype=np.uint8)
+    sb = np.ascontiguousarray(b_scales, dtype=np.uint8)
+    (m, k), (nn, k2) = a.shape, bt.shape
+    if k != k2 or sa.shape != (m, k // 32) or sb.shape != (nn, k // 32):
+        raise ValueError("shapes do not match: A %s, Bt %s, scales %s / %s" % (a.shape, bt.shape, sa.shape, sb.shape))
+    c = np.empty((m, nn), dtype=np.float32)
+    err = ctypes.create_string_buffer(256)
+    rc = load().amdgpu_canary_lowp_gemm(int(device), LOWP_FORMATS[fmt], a.ctypes.data, bt.ctypes.data,
+                                        sa.ctypes.data, sb.ctypes.data, c.ctypes.data, m, nn, k, err, 256)
+    if rc != 0:
+        raise RuntimeError("lowp_gemm failed: " + err.value.decode(errors="replace"))
+    return c
 
 
 SWEEP_VARIANTS = {0: "u4 grid-stride", 1: "u8 grid-stride", 2: "u4 nontemporal", 3: "u8 nontemporal",
