@@ -59,6 +59,11 @@ class HealthConfig:
     canaryOnPreStart: bool = False  # pre_start_required: canary the allocated partitions before each container
     canaryBytes: int = 256 << 20
     canaryTimeoutS: float = 120.0
+    # performance floors of a canary run (0 = off): a partition whose HBM write or
+    # read+verify bandwidth, or whose bf16 MFMA rate, comes out below them fails the
+    # canary like a wrong result does (thermal or power throttling, a degraded HBM stack)
+    canaryMinHbmGbps: float = 0.0
+    canaryMinTflops: float = 0.0
     rejectUnhealthyAllocate: bool = True
     # retired + pending HBM pages at which a GPU goes Unhealthy: 0 = the GPU's own RAS
     # threshold when readable (root), -1 = never, N > 0 = N

@@ -81,6 +81,17 @@ FAMILIES = (
            "Advertised devices per resource and health"),
     Family("amdgpu_device_plugin_registered", "gauge", ("resource",), "manager",
            "Resource registered with kubelet"),
+    # --- gfx950 canary (health.canary / canaryOnStart / canaryOnPreStart) ---
+    Family("amdgpu_canary_last_run_timestamp_seconds", "gauge", ("gpu", "partition"), "manager",
+           "Unix time of the partition's last canary run"),
+    Family("amdgpu_canary_last_ok", "gauge", ("gpu", "partition"), "manager",
+           "1 if the last canary run passed (exact results and the configured performance floors)"),
+    Family("amdgpu_canary_errors", "gauge", ("gpu", "partition", "check"), "manager",
+           "Mismatches found by the last run: hbm, mfma, gemm, lowp (fp8/bf8/fp4 MFMA), lds"),
+    Family("amdgpu_canary_hbm_gbps", "gauge", ("gpu", "partition", "direction"), "manager",
+           "HBM bandwidth of the last run: write, read (read + verify)"),
+    Family("amdgpu_canary_matrix_tflops", "gauge", ("gpu", "partition", "path"), "manager",
+           "Dense matrix-core rate of the last run: mfma_bf16, gemm_bf16 (LDS-staged GEMM), mxfp8, mxfp4"),
     # --- kubelet PodResources (podResources.enabled) ---
     Family("amdgpu_device_plugin_allocation_info", "gauge", ("resource", "device_id", "namespace", "pod", "container"),
            "manager", "Advertised device held by a container (value 1)"),
@@ -114,6 +125,8 @@ PROMQL_EXAMPLES = (
     ("Partition busy per workload (podResources.enabled)",
      "amdgpu_partition_gfx_busy_percent * on(device_id) group_left(namespace, pod, container) "
      "amdgpu_device_plugin_allocation_info"),
+    ("Partitions whose last canary ran below 90% of the node's best bf16 MFMA rate",
+     'amdgpu_canary_matrix_tflops{path="mfma_bf16"} < on() group_left 0.9 * max(amdgpu_canary_matrix_tflops{path="mfma_bf16"})'),
     ("xGMI traffic per link (bytes/s)", "rate(amdgpu_xgmi_read_bytes_total[1m]) + rate(amdgpu_xgmi_write_bytes_total[1m])"),
 )
 

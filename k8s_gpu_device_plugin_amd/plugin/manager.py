@@ -39,6 +39,7 @@ log = get_logger("manager")
 
 EV_STOP, EV_RESTART, EV_RETRY, EV_KUBELET, EV_HEALTH, EV_REDISCOVER, EV_VERIFIED, EV_PODRES, EV_PRESTART_FAIL = (
     "stop", "restart", "retry", "kubelet", "health", "rediscover", "verified", "podresources", "prestart_fail")
+EV_METRICS = "metrics"  # state read by /metrics changed off the manager thread (canary results)
 HEALTH_LOG_LEN = 4096
 
 
@@ -89,6 +90,10 @@ class PluginManager:
         self._held_unhealthy: set[int] = set()
         self._verify_pool: concurrent.futures.ThreadPoolExecutor | None = None
         self.podres = None  # PodResourcesWatcher when podResources.enabled
+        # last canary result per (gpu, hardware partition index): (unix time, result dict);
+        # written by canary pool threads, rendered by the manager thread
+        self.canary_results: dict[tuple[int, int], tuple[float, dict]] = {}
+        self._canary_lock = threading.Lock()
 
     # ------------------------------------------------------------ public API
     def restart(self) -> None:
@@ -165,8 +170,8 @@ class PluginManager:
                     self._apply_health(ev[1])
                 elif kind == EV_VERIFIED:
                     self._apply_verified(*ev[1:])
-                elif kind == EV_PODRES:
-                    pass  # allocation map changed: _publish_metrics below re-renders it
+                elif kind in (EV_PODRES, EV_METRICS):
+                    pass  # allocation map / canary results changed: _publish_metrics below re-renders
                 elif kind == EV_PRESTART_FAIL:
                     self.counters["prestart_failures"] = self.counters.get("prestart_failures", 0) + 1
                     self._set_health(ev[1], ev[2], False, ev[3])
@@ -335,20 +340,46 @@ class PluginManager:
         import concurrent.futures
 
         from ..ops import canary
-        jobs = [(g.index, p.index if len(g.partitions) > 1 else -1, p.hip_id) for g in gpus for p in g.partitions]
+        jobs = [(g.index, p.index if len(g.partitions) > 1 else -1, p.index, p.hip_id)
+                for g in gpus for p in g.partitions]
         failed = set()
         with concurrent.futures.ThreadPoolExecutor(max_workers=max(1, min(8, len(jobs)))) as ex:
-            futs = {ex.submit(canary.run_isolated, max(0, hip), self.cfg.health.canaryBytes,
-                              self.cfg.health.canaryTimeoutS): (gpu, part) for gpu, part, hip in jobs}
+            futs = {ex.submit(self._run_canary, gpu, hw_part, hip): (gpu, part) for gpu, part, hw_part, hip in jobs}
             for f in concurrent.futures.as_completed(futs):
                 gpu, part = futs[f]
                 res = f.result()
-                self.counters["canary_runs"] = self.counters.get("canary_runs", 0) + 1
                 if not res.get("ok"):
                     failed.add((gpu, part))
-                    self.counters["canary_failures"] = self.counters.get("canary_failures", 0) + 1
+                    self._count("canary_failures")
                     log.error("start-up canary failed on GPU %d partition %d: %s", gpu, part, res.get("error") or res)
         return failed
+
+    def _count(self, key: str, n: int = 1) -> None:
+        with self._canary_lock:  # counters touched from canary pool threads too
+            self.counters[key] = self.counters.get(key, 0) + n
+
+    def _run_canary(self, gpu: int, hw_part: int, hip: int) -> dict:
+        """One isolated canary run on HIP device ``hip`` (GPU ``gpu``, hardware partition
+        ``hw_part``): applies the configured performance floors and records the result for
+        /metrics.  Thread-safe; runs on canary pool threads."""
+        from ..ops import canary
+        res = dict(canary.run_isolated(max(0, hip), self.cfg.health.canaryBytes, self.cfg.health.canaryTimeoutS))
+        h = self.cfg.health
+        if res.get("ok"):
+            low = []
+            hbm = min(res.get("write_gbps", 0.0), res.get("read_gbps", 0.0))
+            if h.canaryMinHbmGbps > 0 and hbm < h.canaryMinHbmGbps:
+                low.append("HBM %.0f GB/s < %.0f" % (hbm, h.canaryMinHbmGbps))
+            if h.canaryMinTflops > 0 and res.get("mfma_tflops", 0.0) < h.canaryMinTflops:
+                low.append("bf16 MFMA %.0f TFLOP/s < %.0f" % (res.get("mfma_tflops", 0.0), h.canaryMinTflops))
+            if low:
+                res["ok"] = False
+                res["error"] = "below the canary performance floor: " + ", ".join(low)
+        with self._canary_lock:
+            self.counters["canary_runs"] = self.counters.get("canary_runs", 0) + 1
+            self.canary_results[(gpu, hw_part)] = (time.time(), res)
+        self.events.put((EV_METRICS,))
+        return res
 
     def _prestart_check(self, ids) -> str:
         """PreStartContainer verifier (health.canaryOnPreStart): the gfx950 canary on
@@ -359,24 +390,22 @@ class PluginManager:
         from ..ops import canary
         want = set(ids)
         gpus = {g.index: g for g in self.gpus}
-        targets = {}  # (gpu, partition) -> HIP device ids to check
+        targets = {}  # (gpu, partition) -> hardware partitions to check
         for p in self.plugins:
             for d in p.devices():
                 if d.id not in want or d.gpu not in gpus:
                     continue
                 parts = gpus[d.gpu].partitions
                 sel = parts if d.partition < 0 else [x for x in parts if x.index == d.partition]
-                targets[(d.gpu, d.partition)] = [max(0, x.hip_id) for x in sel]
-        jobs = [(key, hip) for key, hips in targets.items() for hip in hips]
+                targets[(d.gpu, d.partition)] = sel
+        jobs = [(key, x) for key, parts in targets.items() for x in parts]
         if not jobs:
             return ""
         failures = {}
         with concurrent.futures.ThreadPoolExecutor(max_workers=min(8, len(jobs))) as ex:
-            futs = {ex.submit(canary.run_isolated, hip, self.cfg.health.canaryBytes,
-                              self.cfg.health.canaryTimeoutS): key for key, hip in jobs}
+            futs = {ex.submit(self._run_canary, key[0], x.index, x.hip_id): key for key, x in jobs}
             for f in concurrent.futures.as_completed(futs):
                 res = f.result()
-                self.counters["canary_runs"] = self.counters.get("canary_runs", 0) + 1
                 if not res.get("ok"):
                     failures.setdefault(futs[f], res.get("error") or "canary reported errors")
         for (gpu, part), why in sorted(failures.items()):
@@ -399,13 +428,11 @@ class PluginManager:
             self.restart_plugins()
 
     def _canary_ok(self, gpu: int) -> bool:
-        from ..ops import canary
         for g in self.gpus:
             if g.index != gpu:
                 continue
             for part in g.partitions:
-                res = canary.run_isolated(max(0, part.hip_id), self.cfg.health.canaryBytes,
-                                          self.cfg.health.canaryTimeoutS)
+                res = self._run_canary(gpu, part.index, part.hip_id)
                 if not res.get("ok"):
                     log.error("canary failed on GPU %d partition %d: %s", gpu, part.index, res)
                     return False
@@ -494,7 +521,41 @@ class PluginManager:
             from .podresources import render
             allocs, up = self.podres.snapshot()
             lines += render(allocs, up)
+        lines += self._canary_lines()
         self.exporter.set_extra("\n".join(lines) + "\n")
+
+    def _canary_lines(self) -> list:
+        with self._canary_lock:
+            runs = sorted(self.canary_results.items())
+        if not runs:
+            return []
+        fams = (("amdgpu_canary_last_run_timestamp_seconds", "Unix time of the partition's last canary run."),
+                ("amdgpu_canary_last_ok", "1 if the last canary run passed."),
+                ("amdgpu_canary_errors", "Mismatches found by the last canary run, per check."),
+                ("amdgpu_canary_hbm_gbps", "HBM bandwidth measured by the last canary run."),
+                ("amdgpu_canary_matrix_tflops", "Dense matrix-core rate measured by the last canary run."))
+        rows = {name: [] for name, _ in fams}
+        for (gpu, part), (t, r) in runs:
+            lab = 'gpu="%d",partition="%d"' % (gpu, part)
+            rows["amdgpu_canary_last_run_timestamp_seconds"].append("{%s} %.3f" % (lab, t))
+            rows["amdgpu_canary_last_ok"].append("{%s} %d" % (lab, int(bool(r.get("ok")))))
+            for check, key in (("hbm", "hbm_errors"), ("mfma", "mfma_errors"), ("gemm", "gemm_errors"),
+                               ("lowp", "lowp_errors"), ("lds", "lds_errors")):
+                if key in r:
+                    rows["amdgpu_canary_errors"].append('{%s,check="%s"} %d' % (lab, check, int(r[key])))
+            for d, key in (("write", "write_gbps"), ("read", "read_gbps")):
+                if key in r:
+                    rows["amdgpu_canary_hbm_gbps"].append('{%s,direction="%s"} %.1f' % (lab, d, float(r[key])))
+            for path, key in (("mfma_bf16", "mfma_tflops"), ("gemm_bf16", "gemm_tflops"), ("mxfp8", "fp8_tflops"),
+                              ("mxfp4", "fp4_tflops")):
+                if key in r:
+                    rows["amdgpu_canary_matrix_tflops"].append('{%s,path="%s"} %.1f' % (lab, path, float(r[key])))
+        out = []
+        for name, help_ in fams:
+            if rows[name]:
+                out += ["# HELP %s %s" % (name, help_), "# TYPE %s gauge" % name]
+                out += [name + x for x in rows[name]]
+        return out
 
     def _shutdown(self) -> None:
         self._cancel_retry()

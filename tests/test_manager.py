@@ -457,3 +457,52 @@ def test_health_event_during_reload_reaches_new_tables(make_cfg, plugin_dir, mon
         finally:
             m.stop()
             t.join(10)
+
+
+def _full_canary_result(device, ok=True, read=5900.0, tflops=1800.0):
+    return {"ok": ok, "device": device, "error": "", "hbm_errors": 0, "mfma_errors": 0, "gemm_errors": 0,
+            "lowp_errors": 0, "lds_errors": 0, "write_gbps": 6100.0, "read_gbps": read, "mfma_tflops": tflops,
+            "gemm_tflops": 1400.0, "fp8_tflops": 3800.0, "fp4_tflops": 6500.0}
+
+
+def test_canary_results_are_exported_per_partition(make_cfg, plugin_dir, run_manager, monkeypatch):
+    """Every canary run (start-up here) leaves its verdict, HBM bandwidth and matrix-core
+    rates in /metrics, labelled with the GPU and hardware partition it ran on."""
+    from prometheus_client.parser import text_string_to_metric_families
+
+    from k8s_gpu_device_plugin_amd.ops import canary
+    monkeypatch.setattr(canary, "run_isolated",
+                        lambda device, nbytes, timeout=120.0: _full_canary_result(device, read=5000.0 + device))
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(fixture="2gpu_cpx_nps2", migStrategy="single", health={"canaryOnStart": True}))
+        k.wait_for_registrations(1)
+        assert _wait(lambda: 'partition="7",direction="read"' in m.exporter.render())
+        fams = {f.name: f for f in text_string_to_metric_families(m.exporter.render())}
+        ok = [s for s in fams["amdgpu_canary_last_ok"].samples]
+        assert len(ok) == 16 and all(s.value == 1 for s in ok)
+        reads = {(s.labels["gpu"], s.labels["partition"]): s.value for s in fams["amdgpu_canary_hbm_gbps"].samples
+                 if s.labels["direction"] == "read"}
+        assert reads[("1", "1")] == 5009.0  # GPU 1 partition 1 is HIP device 9 on this fixture
+        paths = {s.labels["path"] for s in fams["amdgpu_canary_matrix_tflops"].samples}
+        assert paths == {"mfma_bf16", "gemm_bf16", "mxfp8", "mxfp4"}
+        checks = {s.labels["check"] for s in fams["amdgpu_canary_errors"].samples}
+        assert checks == {"hbm", "mfma", "gemm", "lowp", "lds"}
+
+
+def test_canary_performance_floor_marks_slow_partition_unhealthy(make_cfg, plugin_dir, run_manager, monkeypatch):
+    """health.canaryMinHbmGbps / canaryMinTflops: exact but slow (throttled, degraded HBM)
+    partitions fail the canary like wrong ones do."""
+    from k8s_gpu_device_plugin_amd.ops import canary
+    monkeypatch.setattr(canary, "run_isolated", lambda device, nbytes, timeout=120.0: _full_canary_result(
+        device, read=2500.0 if device == 3 else 5900.0, tflops=900.0 if device == 12 else 1800.0))
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(fixture="2gpu_cpx_nps2", migStrategy="single",
+                                 health={"canaryOnStart": True, "canaryMinHbmGbps": 4000, "canaryMinTflops": 1500}))
+        _, devs = k.watch(k.wait_for_registrations(1)[0].endpoint).next()
+        bad = [i for i, (_, h, _) in enumerate(devs) if h == "Unhealthy"]
+        assert bad == [3, 12]
+        assert m.counters["canary_failures"] == 2
+        _, r = m.canary_results[(0, 3)]
+        assert not r["ok"] and "HBM 2500 GB/s < 4000" in r["error"]
+        _, r = m.canary_results[(1, 4)]
+        assert "bf16 MFMA 900 TFLOP/s < 1500" in r["error"]
