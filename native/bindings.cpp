@@ -690,6 +690,12 @@ PYBIND11_MODULE(_native, m) {
         },
         py::arg("n") = 10000, py::arg("warmup") = 500, py::arg("req_bytes") = 128, py::arg("resp_bytes") = 256,
         py::arg("server_spin") = false, py::arg("tcp") = false);
+  m.def("render_bench",
+        [](std::shared_ptr<Exporter> ex, std::shared_ptr<HttpServer> http, int threads, int iters) {
+          py::gil_scoped_release rel;
+          return render_bench(std::move(ex), std::move(http), threads, iters);
+        },
+        py::arg("exporter"), py::arg("http") = nullptr, py::arg("threads") = 1, py::arg("iters") = 10000);
   m.def("grpc_load",
         [load_dict](const std::string& sock, const std::string& method, const py::bytes& req, int conns,
                     double duration_s) {

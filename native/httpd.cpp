@@ -464,6 +464,8 @@ void HttpServer::stop() {
 void HttpServer::record(int mi, int hi, int status, double seconds) {
   hist_[mi][hi]->observe(seconds);
   counts_[status_class(status)][mi][hi].fetch_add(1, std::memory_order_relaxed);
+  const uint64_t bit = uint64_t{1} << (mi * kHandlers + hi);
+  if (!(used_mh_.load(std::memory_order_relaxed) & bit)) used_mh_.fetch_or(bit, std::memory_order_relaxed);
 }
 
 void HttpServer::handle(const std::string& method, const std::string& path, const std::string& origin,
@@ -479,7 +481,9 @@ void HttpServer::handle(const std::string& method, const std::string& path, cons
   const bool cors = true;
   bool gz = false;
   // plain /metrics: the exposition's segments are appended after the header, each once
-  Exposition expo;
+  // (per worker thread, its per-scrape strings keep their capacity across scrapes)
+  static thread_local Exposition expo;
+  expo.clear();
   bool have_expo = false;
   if (method.empty()) {
     status = *status_out ? *status_out : 400;
@@ -572,33 +576,38 @@ void HttpServer::handle(const std::string& method, const std::string& path, cons
 
 void HttpServer::render_http_metrics(std::string* out) const {
   // middleware/echo_metric.go:80-93 family names / help strings
+  static_assert(kMethods * kHandlers <= 64, "used_mh_ is one 64-bit mask");
+  const uint64_t used = used_mh_.load(std::memory_order_relaxed);
   bool any = false;
-  for (int s = 0; s < kStatus; ++s)
-    for (int m = 0; m < kMethods; ++m)
-      for (int h = 0; h < kHandlers; ++h) {
-        const uint64_t v = counts_[s][m][h].load(std::memory_order_relaxed);
-        if (!v) continue;
-        if (!any) {
-          append_header(out, "echo_http_requests_total", "Number of HTTP operations", "counter");
-          any = true;
-        }
-        out->append("echo_http_requests_total{handler=\"").append(kHandlerNames[h]).append("\",method=\"")
-            .append(kMethodNames[m]).append("\",status=\"").append(kStatusNames[s]).append("\"} ");
-        append_u64(out, v);
-        out->push_back('\n');
-      }
-  any = false;
-  std::string labels;
-  for (int m = 0; m < kMethods; ++m)
-    for (int h = 0; h < kHandlers; ++h) {
-      if (!hist_[m][h]->count()) continue;
+  for (int s = 0; s < kStatus; ++s) {
+    for (uint64_t bits = used; bits; bits &= bits - 1) {
+      const int mh = __builtin_ctzll(bits);
+      const int m = mh / kHandlers, h = mh % kHandlers;
+      const uint64_t v = counts_[s][m][h].load(std::memory_order_relaxed);
+      if (!v) continue;
       if (!any) {
-        append_header(out, "echo_http_request_duration_seconds", "Spend time by processing a route", "histogram");
+        append_header(out, "echo_http_requests_total", "Number of HTTP operations", "counter");
         any = true;
       }
-      labels.assign("handler=\"").append(kHandlerNames[h]).append("\",method=\"").append(kMethodNames[m]).append("\",");
-      hist_[m][h]->render(out, "echo_http_request_duration_seconds", labels);
+      out->append("echo_http_requests_total{handler=\"").append(kHandlerNames[h]).append("\",method=\"")
+          .append(kMethodNames[m]).append("\",status=\"").append(kStatusNames[s]).append("\"} ");
+      append_u64(out, v);
+      out->push_back('\n');
     }
+  }
+  any = false;
+  std::string labels;
+  for (uint64_t bits = used; bits; bits &= bits - 1) {
+    const int mh = __builtin_ctzll(bits);
+    const int m = mh / kHandlers, h = mh % kHandlers;
+    if (!hist_[m][h]->count()) continue;
+    if (!any) {
+      append_header(out, "echo_http_request_duration_seconds", "Spend time by processing a route", "histogram");
+      any = true;
+    }
+    labels.assign("handler=\"").append(kHandlerNames[h]).append("\",method=\"").append(kMethodNames[m]).append("\",");
+    hist_[m][h]->render(out, "echo_http_request_duration_seconds", labels);
+  }
 }
 
 void HttpServer::log_access(const std::string& remote, const std::string& host, const std::string& method,

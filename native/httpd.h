@@ -80,6 +80,9 @@ class HttpServer {
   static constexpr int kHandlers = 5;
   static constexpr int kStatus = 5;
   std::atomic<uint64_t> counts_[kStatus][kMethods][kHandlers];
+  // bit m * kHandlers + h: (method, handler) seen at least once; a scrape walks only these
+  // instead of every (status, method, handler) counter and every histogram
+  std::atomic<uint64_t> used_mh_{0};
   std::unique_ptr<Histogram> hist_[kMethods][kHandlers];
 
   std::mutex log_mu_;

@@ -19,6 +19,8 @@
 #include "backend.h"
 #include "fixture_backend.h"
 #include "grpc_h2.h"
+#include "httpd.h"
+#include "telemetry.h"
 
 namespace amdgpu_dp {
 
@@ -128,6 +130,34 @@ LoadResult http_load(const std::string& host, int port, const std::string& path,
   for (auto& t : ts) t.join();
   total.elapsed_s = duration_s;  // every connection issues requests over [t0, t_end)
   return total;
+}
+
+std::vector<double> render_bench(std::shared_ptr<Exporter> ex, std::shared_ptr<HttpServer> http, int threads,
+                                 int iters) {
+  if (!ex || threads < 1 || threads > 64 || iters < 1) throw std::invalid_argument("render_bench: bad arguments");
+  std::vector<double> out(static_cast<size_t>(threads), 0.0);
+  std::atomic<int> ready{0};
+  std::vector<std::thread> ts;
+  for (int t = 0; t < threads; ++t)
+    ts.emplace_back([&, t] {
+      std::string buf;
+      ready.fetch_add(1);
+      while (ready.load() < threads) {
+      }
+      const int64_t t0 = mono_ns();
+      Exposition e;  // reused like the HTTP worker's
+      for (int i = 0; i < iters; ++i) {
+        buf.clear();
+        e.clear();
+        ex->render(&e);
+        buf.append(256, ' ');  // the response header's share
+        e.append_to(&buf);
+        if (http) http->render_http_metrics(&buf);
+      }
+      out[static_cast<size_t>(t)] = static_cast<double>(mono_ns() - t0) / iters;
+    });
+  for (auto& t : ts) t.join();
+  return out;
 }
 
 LoadResult grpc_load(const std::string& socket_path, const std::string& method, const std::string& req, int conns,

@@ -8,6 +8,7 @@
 
 #include <cstdint>
 #include <string>
+#include <memory>
 #include <vector>
 
 namespace amdgpu_dp {
@@ -35,6 +36,16 @@ LoadResult grpc_load(const std::string& socket_path, const std::string& method, 
 // of one /metrics scrape of resp_bytes (what the kernel's copies and wake-ups cost).
 std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_bytes, bool server_spin = false,
                                  bool tcp = false);
+
+class Exporter;
+class HttpServer;
+
+// What one /metrics response costs in user space, without sockets: `threads` threads
+// each assemble `iters` expositions (Exporter::render + the HTTP server's echo_http_*
+// families, appended to a reused buffer) concurrently.  Mean ns per exposition, per
+// thread: if 4 threads take longer each than 1 does, the scrape path shares something.
+std::vector<double> render_bench(std::shared_ptr<Exporter> ex, std::shared_ptr<HttpServer> http, int threads,
+                                 int iters);
 
 class FixtureBackend;
 

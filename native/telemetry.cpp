@@ -55,11 +55,49 @@ void gzip_member(const char* data, size_t n, std::string* out, int level) {
   if (rc != Z_STREAM_END) throw std::runtime_error("deflate did not finish");
 }
 
+namespace {
+std::atomic<uint64_t> g_exporter_ids{0};
+}  // namespace
+
 Exporter::Exporter()
-    : sample_hist_({1e-4, 2.5e-4, 5e-4, 1e-3, 2.5e-3, 5e-3, 1e-2, 2.5e-2, 5e-2, 0.1, 0.25, 0.5, 1.0}) {
+    : id_(g_exporter_ids.fetch_add(1) + 1),
+      sample_hist_({1e-4, 2.5e-4, 5e-4, 1e-3, 2.5e-3, 5e-3, 1e-2, 2.5e-2, 5e-2, 0.1, 0.25, 0.5, 1.0}) {
   start_time_s_ = now_ns() / 1000000000LL;
   extra_ = std::make_shared<const std::string>();
   gpu_text_ = std::make_shared<const std::string>();
+  std::lock_guard<std::mutex> lk(mu_);
+  publish_view_locked();
+}
+
+void Exporter::publish_view_locked() {
+  auto v = std::make_shared<ScrapeView>();
+  auto h = std::make_shared<std::string>();
+  h->reserve(build_info_.size() + gpu_text_->size());
+  h->append(build_info_).append(*gpu_text_);
+  v->head = std::move(h);
+  v->extra = extra_;
+  v->tables = tables_;
+  std::shared_ptr<const ScrapeView> old;
+  {
+    std::lock_guard<SpinLock> lk(view_lock_);
+    old.swap(view_);
+    view_ = std::move(v);
+  }
+  view_gen_.fetch_add(1, std::memory_order_release);
+}
+
+Exporter::TlCache& Exporter::tl_cache() const {
+  static thread_local TlCache c;
+  if (c.exporter != id_) {  // another exporter rendered on this thread last (tests)
+    c = TlCache{};
+    c.exporter = id_;
+  }
+  return c;
+}
+
+std::shared_ptr<const Exporter::ScrapeView> Exporter::view() const {
+  std::lock_guard<SpinLock> lk(view_lock_);
+  return view_;
 }
 
 Exporter::~Exporter() { stop(); }
@@ -79,18 +117,20 @@ void Exporter::set_partition_labels(const std::vector<PartitionLabel>& labels) {
 void Exporter::set_build_info(const std::string& rendered) {
   std::lock_guard<std::mutex> lk(mu_);
   build_info_ = rendered;
-  ++build_info_version_;
+  publish_view_locked();
 }
 
 void Exporter::set_tables(const std::vector<std::shared_ptr<DeviceTable>>& tables) {
   std::lock_guard<std::mutex> lk(mu_);
   tables_ = tables;
+  publish_view_locked();
 }
 
 void Exporter::set_extra(const std::string& rendered) {
   auto p = std::make_shared<const std::string>(rendered);
   std::lock_guard<std::mutex> lk(mu_);
   extra_ = p;
+  publish_view_locked();
 }
 
 void Exporter::start(std::shared_ptr<Backend> backend, int interval_ms, std::shared_ptr<HealthMonitor> monitor) {
@@ -388,6 +428,7 @@ void Exporter::render_gpu_text(const std::vector<GpuSample>& samples, const std:
   auto p = std::make_shared<const std::string>(std::move(o));
   std::lock_guard<std::mutex> lk(mu_);
   gpu_text_ = p;
+  publish_view_locked();
 }
 
 std::shared_ptr<const std::string> Exporter::gpu_text() const {
@@ -402,14 +443,19 @@ GpuSample Exporter::last_sample(int gpu) const {
   return GpuSample{};
 }
 
-void Exporter::render_process(std::string* out) const {
-  std::lock_guard<std::mutex> lk(proc_mu_);
+void Exporter::render_process_cached(std::string* out) const {
+  TlCache& c = tl_cache();
   const int64_t now = mono_ns();
-  if (now - proc_cache_ns_ < 1000000000LL && !proc_cache_.empty()) {  // /proc reads cached 1 s
-    out->append(proc_cache_);
-    return;
+  if (c.proc.empty() || now - c.proc_ns >= 1000000000LL) {  // /proc reads cached 1 s
+    c.proc.clear();
+    render_process(&c.proc);
+    c.proc_ns = now;
   }
-  std::string o;
+  out->append(c.proc);
+}
+
+void Exporter::render_process(std::string* out) const {
+  std::string& o = *out;
   double utime = 0, stime = 0, vsize = 0, rss = 0;
   long long starttime = 0;
   {
@@ -469,33 +515,24 @@ void Exporter::render_process(std::string* out) const {
   o.append("process_start_time_seconds ");
   append_float(&o, static_cast<double>(start_time_s_));
   o.push_back('\n');
-  proc_cache_ = o;
-  proc_cache_ns_ = now;
-  out->append(o);
 }
 
 // The exposition is assembled from segments so the gzip path can cache the big,
 // slowly-changing ones: [inventory + per-tick GPU text] changes once per sampling
 // tick, [device health] once per table version; the rest is small and per-scrape.
-void Exporter::render_parts(std::shared_ptr<const std::string>* head, std::string* counters,
-                            std::shared_ptr<const std::string>* health, std::string* tail) const {
-  std::shared_ptr<const std::string> gt, extra;
-  std::vector<std::shared_ptr<DeviceTable>> tables;
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    gt = gpu_text_;
-    extra = extra_;
-    tables = tables_;
-    if (head_src_ != gt || head_build_ != build_info_version_) {
-      auto h = std::make_shared<std::string>();
-      h->reserve(build_info_.size() + gt->size());
-      h->append(build_info_).append(*gt);
-      head_ = std::move(h);
-      head_src_ = gt;
-      head_build_ = build_info_version_;
-    }
-    *head = head_;
+void Exporter::render_parts(std::string_view* head, std::string* counters, std::string_view* health,
+                            std::string* tail, std::shared_ptr<const std::string>* head_sp,
+                            std::shared_ptr<const std::string>* health_sp) const {
+  TlCache& c = tl_cache();
+  const uint64_t gen = view_gen_.load(std::memory_order_acquire);
+  if (!c.view || c.view_gen != gen) {
+    c.view = view();
+    c.view_gen = gen;
   }
+  const ScrapeView& v = *c.view;
+  const auto& tables = v.tables;
+  *head = *v.head;
+  if (head_sp) *head_sp = v.head;
   append_header(counters, "amdgpu_telemetry_samples_total", "Telemetry sampling passes completed.", "counter");
   counters->append("amdgpu_telemetry_samples_total ");
   append_u64(counters, samples_.load());
@@ -509,51 +546,54 @@ void Exporter::render_parts(std::shared_ptr<const std::string>* head, std::strin
                   "histogram");
     sample_hist_.render(counters, "amdgpu_telemetry_sample_duration_seconds", "");
   }
-  health->reset();
+  *health = std::string_view();
+  if (health_sp) health_sp->reset();
   if (!tables.empty()) {
-    std::vector<uint64_t> key;
-    key.reserve(tables.size() * 2);
-    for (const auto& t : tables) {
-      key.push_back(reinterpret_cast<uintptr_t>(t.get()));
-      key.push_back(t->version());
-    }
-    {
-      std::lock_guard<std::mutex> hk(health_mu_);
-      if (key != health_key_ || !health_cache_) {
-        auto hc = std::make_shared<std::string>();
-        append_header(hc.get(), "amdgpu_device_plugin_device_health",
-                      "1 if the advertised device is Healthy, 0 if Unhealthy.", "gauge");
-        std::string l;
-        for (const auto& t : tables) {
-          for (size_t i = 0; i < t->size(); ++i) {
-            const TableDevice& d = t->device(i);
-            l.assign("resource=\"");
-            append_label_value(&l, t->config().resource_name);
-            l.append("\",device_id=\"");
-            append_label_value(&l, d.id);
-            l.append("\"");
-            line(hc.get(), "amdgpu_device_plugin_device_health", l, t->healthy(d.id) ? 1 : 0);
-          }
-        }
-        health_cache_ = std::move(hc);
-        health_key_ = key;
+    // device-health block: re-rendered only when a table's version moves
+    bool same = c.health && c.health_key.size() == tables.size() * 2;
+    for (size_t i = 0; same && i < tables.size(); ++i)
+      same = c.health_key[2 * i] == reinterpret_cast<uintptr_t>(tables[i].get()) &&
+             c.health_key[2 * i + 1] == tables[i]->version();
+    if (!same) {
+      c.health_key.clear();
+      for (const auto& t : tables) {  // versions read before the text: never newer than it
+        c.health_key.push_back(reinterpret_cast<uintptr_t>(t.get()));
+        c.health_key.push_back(t->version());
       }
-      *health = health_cache_;
+      auto hc = std::make_shared<std::string>();
+      append_header(hc.get(), "amdgpu_device_plugin_device_health",
+                    "1 if the advertised device is Healthy, 0 if Unhealthy.", "gauge");
+      std::string l;
+      for (const auto& t : tables) {
+        for (size_t i = 0; i < t->size(); ++i) {
+          const TableDevice& d = t->device(i);
+          l.assign("resource=\"");
+          append_label_value(&l, t->config().resource_name);
+          l.append("\",device_id=\"");
+          append_label_value(&l, d.id);
+          l.append("\"");
+          line(hc.get(), "amdgpu_device_plugin_device_health", l, t->healthy(d.id) ? 1 : 0);
+        }
+      }
+      c.health = std::move(hc);
     }
+    *health = *c.health;
+    if (health_sp) *health_sp = c.health;
     bool any = false;
     for (const auto& t : tables) {
-      std::string tmp;
-      t->render_metrics(&tmp, false);
-      if (tmp.empty()) continue;
-      if (!any) {
-        DeviceTable::render_metric_headers(tail);
-        any = true;
+      const size_t before = tail->size();
+      if (!any) DeviceTable::render_metric_headers(tail);
+      const size_t body = tail->size();
+      t->render_metrics(tail, false);
+      if (tail->size() == body) {
+        tail->resize(before);  // nothing observed yet: no headers either
+        continue;
       }
-      tail->append(tmp);
+      any = true;
     }
   }
-  tail->append(*extra);
-  render_process(tail);
+  tail->append(*v.extra);
+  render_process_cached(tail);
 }
 
 void Exporter::render(std::string* out) const {
@@ -566,8 +606,9 @@ void Exporter::render(Exposition* e) const { render_parts(&e->head, &e->counters
 
 void Exporter::render_gzip(std::string* out, std::string_view trailer) const {
   std::shared_ptr<const std::string> head, health;
-  std::string dyn, tail;
-  render_parts(&head, &dyn, &health, &tail);
+  std::string_view hv, lv;
+  std::string dyn, tail, gz_health;
+  render_parts(&hv, &dyn, &lv, &tail, &head, &health);
   {
     std::lock_guard<std::mutex> lk(gz_mu_);
     if (gz_head_src_ != head) {
@@ -582,14 +623,12 @@ void Exporter::render_gzip(std::string* out, std::string_view trailer) const {
         gzip_member(health->data(), health->size(), &gz_health_);
         gz_health_src_ = health;
       }
+      gz_health = gz_health_;  // the member of this scrape's health text, not a later one's
     }
   }
   // members must follow the plain-text order: head, counters, health, tail + trailer
   gzip_member(dyn.data(), dyn.size(), out);
-  if (health) {
-    std::lock_guard<std::mutex> lk(gz_mu_);
-    out->append(gz_health_);
-  }
+  out->append(gz_health);
   tail.append(trailer.data(), trailer.size());
   gzip_member(tail.data(), tail.size(), out);
 }

@@ -28,17 +28,23 @@ namespace amdgpu_dp {
 void gzip_member(const char* data, size_t n, std::string* out, int level = 1);
 
 // One /metrics exposition as its segments: the per-tick inventory/GPU text and the
-// per-version device-health block are shared snapshots, the rest is rendered per
-// scrape.  Its size is known before any byte is copied, so a server can write the
-// response header and then append each segment once.
+// per-version device-health block are views of snapshots the rendering thread holds,
+// the rest is rendered per scrape.  Its size is known before any byte is copied, so a
+// server can write the response header and then append each segment once.  The views
+// stay valid until the same thread renders again (Exporter::render).
 struct Exposition {
-  std::shared_ptr<const std::string> head, health;
+  std::string_view head, health;
   std::string counters, tail;
-  size_t size() const { return head->size() + counters.size() + (health ? health->size() : 0) + tail.size(); }
+  size_t size() const { return head.size() + counters.size() + health.size() + tail.size(); }
   void append_to(std::string* out) const {
-    out->append(*head).append(counters);
-    if (health) out->append(*health);
+    out->append(head.data(), head.size()).append(counters);
+    out->append(health.data(), health.size());
     out->append(tail);
+  }
+  void clear() {
+    head = health = std::string_view();
+    counters.clear();
+    tail.clear();
   }
 };
 
@@ -82,21 +88,53 @@ class Exporter {
  private:
   void loop();
   void render_gpu_text(const std::vector<GpuSample>& samples, const std::vector<char>& ok, uint64_t inventory_gen);
-  void render_process(std::string* out) const;
-  void render_parts(std::shared_ptr<const std::string>* head, std::string* counters,
-                    std::shared_ptr<const std::string>* health, std::string* tail) const;
+  void render_process(std::string* out) const;  // reads /proc
+  void render_process_cached(std::string* out) const;  // per-thread copy, refreshed each second
+  // head_sp / health_sp (optional): owning references to the segments head / health view
+  void render_parts(std::string_view* head, std::string* counters, std::string_view* health, std::string* tail,
+                    std::shared_ptr<const std::string>* head_sp = nullptr,
+                    std::shared_ptr<const std::string>* health_sp = nullptr) const;
 
+  // What a scrape reads, as one immutable snapshot: rebuilt under mu_ by whatever changes
+  // an input (a sampling tick, set_build_info / set_tables / set_extra) and read by the
+  // HTTP workers through a pointer copy under a spin lock, so concurrent scrapers never
+  // queue on mu_ (or on the sampler holding it).
+  struct ScrapeView {
+    std::shared_ptr<const std::string> head;  // build info + per-tick GPU text
+    std::shared_ptr<const std::string> extra;
+    std::vector<std::shared_ptr<DeviceTable>> tables;
+  };
+  void publish_view_locked();  // mu_ held
+  std::shared_ptr<const ScrapeView> view() const;
+
+  // What each scraping thread keeps between scrapes, so that a scrape writes no cache
+  // line another scraper reads: the view (re-fetched only when view_gen_ moves), the
+  // device-health text (re-rendered only when a table version moves) and the process_*
+  // text (re-read from /proc at most once a second).  Shared copies behind a lock made 4
+  // concurrent scrapers each 3.5x slower than one (lock and reference-count lines
+  // bouncing between cores).
+  struct TlCache {
+    uint64_t exporter = 0;  // id_ of the exporter the entries belong to
+    uint64_t view_gen = 0;
+    std::shared_ptr<const ScrapeView> view;
+    std::vector<uint64_t> health_key;  // (table address, version) pairs
+    std::shared_ptr<const std::string> health;
+    int64_t proc_ns = 0;
+    std::string proc;
+  };
+  TlCache& tl_cache() const;
+
+  const uint64_t id_;
   mutable std::mutex mu_;
+  mutable SpinLock view_lock_;
+  std::shared_ptr<const ScrapeView> view_;
+  std::atomic<uint64_t> view_gen_{0};
   std::vector<GpuInfo> gpus_;
   uint64_t inventory_gen_ = 0;  // bumped by set_inventory; a sampling pass is tied to one
   std::vector<PartitionLabel> labels_;
   std::vector<GpuSample> last_;
   std::vector<std::shared_ptr<DeviceTable>> tables_;
   std::string build_info_;
-  uint64_t build_info_version_ = 0;
-  mutable std::shared_ptr<const std::string> head_;      // build_info_ + *gpu_text_
-  mutable std::shared_ptr<const std::string> head_src_;  // gpu_text_ that head_ was built from
-  mutable uint64_t head_build_ = 0;
   std::shared_ptr<const std::string> extra_;
   std::shared_ptr<const std::string> gpu_text_;
 
@@ -111,17 +149,12 @@ class Exporter {
   std::atomic<uint64_t> sample_errors_{0};
   Histogram sample_hist_;
   int64_t start_time_s_ = 0;
-  // device-health block, re-rendered only when a table's version changes
-  mutable std::mutex health_mu_;
-  mutable std::vector<uint64_t> health_key_;
-  mutable std::shared_ptr<const std::string> health_cache_;
+
   // gzip members cached against the exact segment objects they were compressed from
   mutable std::mutex gz_mu_;
   mutable std::string gz_head_, gz_health_;
   mutable std::shared_ptr<const std::string> gz_head_src_, gz_health_src_;
-  mutable std::mutex proc_mu_;
-  mutable std::string proc_cache_;
-  mutable int64_t proc_cache_ns_ = 0;
+
 };
 
 }  // namespace amdgpu_dp
