@@ -560,6 +560,17 @@ void Exporter::render_parts(std::string_view* head, std::string* counters, std::
         c.health_key.push_back(reinterpret_cast<uintptr_t>(t.get()));
         c.health_key.push_back(t->version());
       }
+      std::shared_ptr<const HealthShared> shared;
+      {
+        std::lock_guard<SpinLock> lk(health_lock_);
+        shared = health_shared_;
+      }
+      if (shared && shared->key == c.health_key) {
+        c.health = shared->text;  // another thread rendered this version already
+        same = true;
+      }
+    }
+    if (!same) {
       auto hc = std::make_shared<std::string>();
       append_header(hc.get(), "amdgpu_device_plugin_device_health",
                     "1 if the advertised device is Healthy, 0 if Unhealthy.", "gauge");
@@ -576,6 +587,13 @@ void Exporter::render_parts(std::string_view* head, std::string* counters, std::
         }
       }
       c.health = std::move(hc);
+      auto fresh = std::make_shared<HealthShared>();
+      fresh->key = c.health_key;
+      fresh->text = c.health;
+      std::shared_ptr<const HealthShared> old;
+      std::lock_guard<SpinLock> lk(health_lock_);
+      old.swap(health_shared_);
+      health_shared_ = std::move(fresh);
     }
     *health = *c.health;
     if (health_sp) *health_sp = c.health;

@@ -123,6 +123,15 @@ class Exporter {
     std::string proc;
   };
   TlCache& tl_cache() const;
+  // The last rendered device-health text, shared so that every thread serves the same
+  // object (the gzip path caches its compressed member by identity); a thread consults
+  // it only when its own key goes stale.
+  struct HealthShared {
+    std::vector<uint64_t> key;
+    std::shared_ptr<const std::string> text;
+  };
+  mutable SpinLock health_lock_;
+  mutable std::shared_ptr<const HealthShared> health_shared_;
 
   const uint64_t id_;
   mutable std::mutex mu_;
