@@ -477,7 +477,7 @@ void GrpcServer::run(Worker* w) {
     }
     s.dispatched = true;
     const int64_t t0 = mono_ns();
-    requests_.fetch_add(1, std::memory_order_relaxed);
+    requests_.add();
     const Method m = static_cast<Method>(s.method);
     if (m == kMUnknown) {
       send_error(c, sid, s, 12, "unknown method " + s.path);  // UNIMPLEMENTED

@@ -67,7 +67,7 @@ class GrpcServer {
   int listen_fd_ = -1;
   std::atomic<bool> running_{false};
   std::atomic<bool> stop_{false};
-  std::atomic<uint64_t> requests_{0};
+  ShardedCounter requests_;  // every worker counts its calls: no shared line per RPC
   std::atomic<int> conns_{0};
   std::vector<std::unique_ptr<Worker>> workers_;
   std::vector<std::thread> threads_;

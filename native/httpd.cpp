@@ -118,9 +118,11 @@ struct HttpServer::Worker {
 
 HttpServer::HttpServer(HttpConfig cfg, std::shared_ptr<Exporter> exporter)
     : cfg_(std::move(cfg)), exporter_(std::move(exporter)) {
-  for (auto& a : counts_)
-    for (auto& b : a)
-      for (auto& c : b) c.store(0);
+  counts_.reset(new CountShard[kMetricShards]);
+  for (int k = 0; k < kMetricShards; ++k)
+    for (auto& a : counts_[k].c)
+      for (auto& b : a)
+        for (auto& c : b) c.store(0, std::memory_order_relaxed);
   for (auto& row : hist_)
     for (auto& h : row) h = std::make_unique<Histogram>(echo_buckets());
 }
@@ -397,7 +399,7 @@ int HttpServer::start() {
                        &status, &body_bytes, gzip_ok);
               }
               const double dt = (mono_ns() - t0) * 1e-9;
-              requests_.fetch_add(1, std::memory_order_relaxed);
+              requests_.add();
               if (cfg_.access_log && method != "OPTIONS" && !method.empty())
                 log_access(c->remote, hosth, method, uri, ua, status, dt, content_len, body_bytes);
               pos = body_start + content_len;
@@ -463,7 +465,7 @@ void HttpServer::stop() {
 
 void HttpServer::record(int mi, int hi, int status, double seconds) {
   hist_[mi][hi]->observe(seconds);
-  counts_[status_class(status)][mi][hi].fetch_add(1, std::memory_order_relaxed);
+  counts_[thread_shard()].c[status_class(status)][mi][hi].fetch_add(1, std::memory_order_relaxed);
   const uint64_t bit = uint64_t{1} << (mi * kHandlers + hi);
   if (!(used_mh_.load(std::memory_order_relaxed) & bit)) used_mh_.fetch_or(bit, std::memory_order_relaxed);
 }
@@ -583,7 +585,8 @@ void HttpServer::render_http_metrics(std::string* out) const {
     for (uint64_t bits = used; bits; bits &= bits - 1) {
       const int mh = __builtin_ctzll(bits);
       const int m = mh / kHandlers, h = mh % kHandlers;
-      const uint64_t v = counts_[s][m][h].load(std::memory_order_relaxed);
+      uint64_t v = 0;
+      for (int k = 0; k < kMetricShards; ++k) v += counts_[k].c[s][m][h].load(std::memory_order_relaxed);
       if (!v) continue;
       if (!any) {
         append_header(out, "echo_http_requests_total", "Number of HTTP operations", "counter");

@@ -74,12 +74,17 @@ class HttpServer {
   std::vector<std::thread> threads_;
   std::vector<std::unique_ptr<Worker>> workers_;
   std::thread log_thread_;
-  std::atomic<uint64_t> requests_{0};
+  ShardedCounter requests_;
 
   static constexpr int kMethods = 8;
   static constexpr int kHandlers = 5;
   static constexpr int kStatus = 5;
-  std::atomic<uint64_t> counts_[kStatus][kMethods][kHandlers];
+  // echo_http_requests_total per (status class, method, handler), one copy per thread
+  // shard (metrics.h) so that concurrent workers never write the same line
+  struct alignas(64) CountShard {
+    std::atomic<uint64_t> c[kStatus][kMethods][kHandlers];
+  };
+  std::unique_ptr<CountShard[]> counts_;
   // bit m * kHandlers + h: (method, handler) seen at least once; a scrape walks only these
   // instead of every (status, method, handler) counter and every histogram
   std::atomic<uint64_t> used_mh_{0};

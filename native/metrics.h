@@ -88,75 +88,116 @@ class SpinLock {
   std::atomic<bool> f_{false};
 };
 
-class AtomicDouble {
+// Observation shard of the calling thread.  Threads are spread round-robin over
+// kMetricShards cache-line-separated copies of every counter, so concurrent kubelet RPC
+// and HTTP workers never write the same line: with one shared set, 4 concurrent clients
+// bounced the bucket, sum and count lines between cores on every call.
+constexpr int kMetricShards = 16;
+inline int thread_shard() {
+  static std::atomic<int> next{0};
+  static thread_local const int s = next.fetch_add(1, std::memory_order_relaxed) % kMetricShards;
+  return s;
+}
+
+// A counter incremented by many threads: one cache line per shard, summed on read.
+class ShardedCounter {
  public:
-  void add(double d) {
-    uint64_t old = bits_.load(std::memory_order_relaxed);
-    for (;;) {
-      double cur;
-      std::memcpy(&cur, &old, sizeof(cur));
-      const double nv = cur + d;
-      uint64_t nb;
-      std::memcpy(&nb, &nv, sizeof(nb));
-      if (bits_.compare_exchange_weak(old, nb, std::memory_order_relaxed)) return;
-    }
+  ShardedCounter() {
+    for (auto& s : shards_) s.v.store(0, std::memory_order_relaxed);
   }
-  uint64_t bits() const { return bits_.load(std::memory_order_relaxed); }
-  double load() const {
-    const uint64_t b = bits_.load(std::memory_order_relaxed);
-    double d;
-    std::memcpy(&d, &b, sizeof(d));
-    return d;
+  void add(uint64_t n = 1) { shards_[thread_shard()].v.fetch_add(n, std::memory_order_relaxed); }
+  uint64_t load() const {
+    uint64_t t = 0;
+    for (const auto& s : shards_) t += s.v.load(std::memory_order_relaxed);
+    return t;
   }
 
  private:
-  std::atomic<uint64_t> bits_{0};
+  struct alignas(64) Slot {
+    std::atomic<uint64_t> v;
+  };
+  Slot shards_[kMetricShards];
 };
+
+// Adds `d` to the double stored as bits in `a` (CAS loop; uncontended per shard).
+inline void atomic_add_double(std::atomic<uint64_t>* a, double d) {
+  uint64_t old = a->load(std::memory_order_relaxed);
+  for (;;) {
+    double cur;
+    std::memcpy(&cur, &old, sizeof(cur));
+    const double nv = cur + d;
+    uint64_t nb;
+    std::memcpy(&nb, &nv, sizeof(nb));
+    if (a->compare_exchange_weak(old, nb, std::memory_order_relaxed)) return;
+  }
+}
 
 class Histogram {
  public:
+  static constexpr size_t kMaxBuckets = 23;  // finite bounds (+Inf is one more slot)
+
   explicit Histogram(std::vector<double> bounds)
-      : bounds_(std::move(bounds)), counts_(bounds_.size() + 1), id_(next_id().fetch_add(1) + 1) {
+      : bounds_(std::move(bounds)), shards_(new Shard[kMetricShards]), id_(next_id().fetch_add(1) + 1) {
+    if (bounds_.size() > kMaxBuckets) bounds_.resize(kMaxBuckets);
     for (double b : bounds_) {  // the le="..." strings never change: format them once
       std::string s;
       append_float(&s, b);
       le_.push_back(std::move(s));
     }
     le_.push_back("+Inf");
+    for (int k = 0; k < kMetricShards; ++k) {
+      Shard& sh = shards_[k];
+      sh.n.store(0, std::memory_order_relaxed);
+      sh.sum.store(0, std::memory_order_relaxed);  // bits of 0.0
+      for (auto& c : sh.counts) c.store(0, std::memory_order_relaxed);
+    }
   }
   Histogram(const Histogram&) = delete;
   void observe(double v) {
     size_t i = 0;
     while (i < bounds_.size() && v > bounds_[i]) ++i;
-    counts_[i].fetch_add(1, std::memory_order_relaxed);
-    sum_.add(v);
-    n_.fetch_add(1, std::memory_order_release);  // last: a reader that sees n sees the bucket
+    Shard& sh = shards_[thread_shard()];
+    sh.counts[i].fetch_add(1, std::memory_order_relaxed);
+    atomic_add_double(&sh.sum, v);
+    sh.n.fetch_add(1, std::memory_order_release);  // last: a reader that sees n sees the bucket
   }
-  // Observations completed so far: one load (a scrape asks every histogram, most of
-  // which have not moved), never ahead of the buckets.
-  uint64_t count() const { return n_.load(std::memory_order_acquire); }
+  // Observations completed so far, never ahead of the buckets.
+  uint64_t count() const {
+    uint64_t c = 0;
+    for (int k = 0; k < kMetricShards; ++k) c += shards_[k].n.load(std::memory_order_acquire);
+    return c;
+  }
+  double sum() const {
+    double s = 0;
+    for (int k = 0; k < kMetricShards; ++k) {
+      const uint64_t b = shards_[k].sum.load(std::memory_order_relaxed);
+      double d;
+      std::memcpy(&d, &b, sizeof(d));
+      s += d;
+    }
+    return s;
+  }
   // labels: already-formatted `k="v",` prefix (may be empty).  A scrape renders every
   // histogram, but most of them (kubelet RPCs, sampling passes) have not moved since the
-  // previous scrape: their text is cached under (count, sum) and re-used.  The key is
-  // read before the buckets, and both only grow, so a cached text is never older than
-  // its key: an observation that lands mid-render changes the next key and forces a
-  // re-render.  The cache is per thread (each HTTP worker keeps its own copy): a shared
-  // one, even behind a spin lock, made concurrent scrapers bounce its lock and reference
-  // count between cores, and 4 scrapers each took 3.5x as long as one.
+  // previous scrape: their text is cached under the observation count and re-used.  The
+  // count only grows and is read before the buckets (each shard counts an observation
+  // after its bucket), so a cached text is never older than its key: an observation that
+  // lands mid-render changes the next key and forces a re-render.  The cache is per
+  // thread (each HTTP worker keeps its own copy): a shared one, even behind a spin lock,
+  // made concurrent scrapers bounce its lock and reference count between cores, and 4
+  // scrapers each took 3.5x as long as one.
   void render(std::string* out, const char* name, std::string_view labels) const {
     const uint64_t key_count = count();
-    const uint64_t key_sum = sum_.bits();
     auto& cache = tl_cache();
     auto it = cache.find(id_);
-    if (it != cache.end() && it->second.count == key_count && it->second.sum == key_sum &&
-        it->second.name == name && it->second.labels == labels) {
+    if (it != cache.end() && it->second.count == key_count && it->second.name == name &&
+        it->second.labels == labels) {
       out->append(it->second.text);
       return;
     }
     if (it == cache.end() && cache.size() >= 1024) cache.clear();  // histograms of old reloads
     Cached& c = cache[id_];
     c.count = key_count;
-    c.sum = key_sum;
     c.name = name;
     c.labels.assign(labels.data(), labels.size());
     c.text.clear();
@@ -170,7 +211,7 @@ class Histogram {
     out->reserve(out->size() + (prefix.size() + 24) * (bounds_.size() + 3));
     uint64_t cum = 0;
     for (size_t i = 0; i <= bounds_.size(); ++i) {
-      cum += counts_[i].load(std::memory_order_relaxed);
+      for (int k = 0; k < kMetricShards; ++k) cum += shards_[k].counts[i].load(std::memory_order_relaxed);
       out->append(prefix).append(le_[i]).append("\"} ");
       append_u64(out, cum);
       out->push_back('\n');
@@ -180,7 +221,7 @@ class Histogram {
     out->append(name).append("_sum");
     if (!lab.empty()) out->append("{").append(lab.data(), lab.size()).append("}");
     out->push_back(' ');
-    append_float(out, sum_.load());
+    append_float(out, sum());
     out->push_back('\n');
     out->append(name).append("_count");
     if (!lab.empty()) out->append("{").append(lab.data(), lab.size()).append("}");
@@ -190,13 +231,16 @@ class Histogram {
   }
 
  private:
+  struct alignas(64) Shard {
+    std::atomic<uint64_t> n;
+    std::atomic<uint64_t> sum;  // bits of a double
+    std::atomic<uint64_t> counts[kMaxBuckets + 1];
+  };
   std::vector<double> bounds_;
   std::vector<std::string> le_;
-  std::vector<std::atomic<uint64_t>> counts_;
-  AtomicDouble sum_;
-  std::atomic<uint64_t> n_{0};
+  std::unique_ptr<Shard[]> shards_;
   struct Cached {
-    uint64_t count = 0, sum = 0;
+    uint64_t count = 0;
     std::string name, labels, text;
   };
   // per-thread render cache, keyed by histogram id (ids are never reused, addresses are)
