@@ -27,7 +27,9 @@ canary (HBM pattern + MFMA exactness/throughput) passes on that device.
 Speed-of-light references, measured untimed in the same run: ``uds_roundtrip_floor_p50_us``
 (the same unix-socket exchange between two threads, no protocol work, sleeping server
 thread) and ``uds_roundtrip_floor_spin_p50_us`` (server thread polling, which is what the
-daemon's ``grpc.busyPollUs`` window gives back-to-back kubelet RPCs).
+daemon's ``grpc.busyPollUs`` window gives back-to-back kubelet RPCs).  Also untimed:
+``allocate_cold_p50_us``, Allocate calls 1 ms apart, each of which finds the server thread
+asleep (kubelet's pod admissions are sparse; compare with the sleeping-server floor).
 
 The reference publishes no numbers, so ``vs_baseline`` is null.
 """
@@ -263,6 +265,8 @@ def main() -> int:
     mine["uds_floor_p50"] = _pct(floor, 0.5)
     # ... and with a server thread that polls instead of sleeping (the busy-poll window)
     mine["uds_floor_spin_p50"] = _pct(n.uds_pingpong(10000, 500, *sizes, server_spin=True), 0.5)
+    # kubelet-like sparse calls: 1 ms apart, every one meets a sleeping server thread
+    mine["alloc_cold"] = h2.bench_unary(v1beta1.METHOD_ALLOCATE, alloc_req, 400, 1000)
     # /metrics: one loopback TCP exchange of a scrape's size, polling server
     mine["tcp_scrape_floor_p50"] = _pct(n.uds_pingpong(3000, 300, 90, body_len + 400, server_spin=True, tcp=True),
                                         0.5)
@@ -298,6 +302,7 @@ def main() -> int:
             "allocate_p50_us": round(p50, 2), "allocate_p99_us": round(_pct(allocs_native, 0.99) * 1e6, 2),
             "uds_roundtrip_floor_p50_us": round(gathered[0]["uds_floor_p50"] * 1e6, 2),
             "uds_roundtrip_floor_spin_p50_us": round(gathered[0]["uds_floor_spin_p50"] * 1e6, 2),
+            "allocate_cold_p50_us": round(_pct([x for g in gathered for x in g["alloc_cold"]], 0.5) * 1e6, 2),
             "tcp_scrape_floor_p50_us": round(gathered[0]["tcp_scrape_floor_p50"] * 1e6, 2),
             "allocate_p50_us_grpcio_client": round(p50_grpcio, 2),
             "allocate_p99_us_grpcio_client": round(_pct(allocs, 0.99) * 1e6, 2),

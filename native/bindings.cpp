@@ -1,5 +1,8 @@
 // pybind11 module `k8s_gpu_device_plugin_amd._native`.
 // Long-blocking calls (health pop, inotify read, server stop, scrapes) release the GIL.
+#include <chrono>
+#include <thread>
+
 #include <pybind11/functional.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -565,19 +568,23 @@ PYBIND11_MODULE(_native, m) {
           },
           py::arg("timeout_s") = 5.0)
       .def("bench_unary",
-           [](H2Client& c, const std::string& path, const py::bytes& req, int n) {
+           [](H2Client& c, const std::string& path, const py::bytes& req, int n, int gap_us) {
              std::string r(req), resp, msg;
              std::vector<double> out;
              out.reserve(static_cast<size_t>(n));
              py::gil_scoped_release rel;
              for (int i = 0; i < n; ++i) {
+               // gap_us > 0: idle between calls, so each one meets a sleeping server (the
+               // way kubelet's sparse pod-admission RPCs do), not its busy-poll window
+               if (gap_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(gap_us));
                const int64_t t0 = mono_ns();
                const int st = c.unary(path, r, &resp, &msg);
                out.push_back((mono_ns() - t0) * 1e-9);
                if (st != 0) throw std::runtime_error("grpc-status " + std::to_string(st) + ": " + msg);
              }
              return out;
-           })
+           },
+           py::arg("path"), py::arg("req"), py::arg("n"), py::arg("gap_us") = 0)
       .def("close", &H2Client::close);
 
   m.def("h2_bench_unary",
