@@ -12,6 +12,8 @@
 //                                             for CPU tests and the 8x8 CPX configs
 #pragma once
 
+#include <sys/socket.h>
+
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
@@ -192,6 +194,15 @@ bool amdsmi_probe_held();
 
 int64_t now_ns();
 int64_t mono_ns();
+
+// accept4 (non-blocking, close-on-exec) for a level-triggered listener that sheds load
+// instead of spinning when the process runs out of file descriptors: the pending
+// connection would stay in the backlog and keep the listener readable, and every
+// epoll_wait would return at once.  *spare is the caller's reserve descriptor (-1: opened
+// lazily); on EMFILE/ENFILE it is given up for one accept whose connection is closed at
+// once.  Returns the connection fd, or -1 with errno (EAGAIN: backlog empty;
+// ECONNABORTED: one connection was shed, *shed set; call again).
+int accept_or_shed(int lfd, struct sockaddr* addr, socklen_t* len, int* spare, bool* shed);
 
 // Timed condition-variable wait.  libstdc++ implements steady-clock waits with
 // pthread_cond_clockwait, which GCC 11's ThreadSanitizer does not intercept (it then

@@ -467,6 +467,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("running", &HttpServer::running)
       .def_property_readonly("port", &HttpServer::port)
       .def_property_readonly("requests_total", &HttpServer::requests_total)
+      .def_property_readonly("shed_connections", &HttpServer::shed_connections)
       .def_property_readonly("worker_connections", &HttpServer::worker_connections)
       .def("render_http_metrics", [](const HttpServer& s) {
         std::string o;
@@ -522,6 +523,7 @@ PYBIND11_MODULE(_native, m) {
       .def("notify", &GrpcServer::notify)
       .def_property_readonly("running", &GrpcServer::running)
       .def_property_readonly("requests", &GrpcServer::requests)
+      .def_property_readonly("shed_connections", &GrpcServer::shed_connections)
       .def_property_readonly("connections", &GrpcServer::connections)
       .def_property_readonly("worker_connections", &GrpcServer::worker_connections)
       .def_property_readonly("socket_path", &GrpcServer::socket_path);

@@ -1,4 +1,10 @@
+#include <fcntl.h>
+#include <sys/socket.h>
 #include <time.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <ctime>
 
 #include "backend.h"
 
@@ -8,6 +14,27 @@ int64_t now_ns() {
   struct timespec ts;
   clock_gettime(CLOCK_REALTIME, &ts);
   return static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
+}
+
+int accept_or_shed(int lfd, struct sockaddr* addr, socklen_t* len, int* spare, bool* shed) {
+  *shed = false;
+  if (*spare < 0) *spare = open("/dev/null", O_RDONLY | O_CLOEXEC);
+  const int fd = accept4(lfd, addr, len, SOCK_NONBLOCK | SOCK_CLOEXEC);
+  if (fd >= 0 || (errno != EMFILE && errno != ENFILE)) return fd;
+  if (*spare < 0) {  // no reserve to give up (ENFILE): back off instead of spinning
+    struct timespec ts {0, 1000000};
+    nanosleep(&ts, nullptr);
+    errno = EAGAIN;
+    return -1;
+  }
+  close(*spare);
+  *spare = -1;
+  const int victim = accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC);
+  if (victim >= 0) close(victim);
+  *spare = open("/dev/null", O_RDONLY | O_CLOEXEC);
+  *shed = victim >= 0;
+  errno = victim >= 0 ? ECONNABORTED : EAGAIN;
+  return -1;
 }
 
 int64_t mono_ns() {

@@ -401,6 +401,13 @@ void GrpcServer::stop() {
 void GrpcServer::run(Worker* w) {
   std::vector<epoll_event> evs(128);
   char rbuf[32768];
+  int spare = -1;  // reserve descriptor for accept_or_shed
+  struct SpareCloser {
+    int* fd;
+    ~SpareCloser() {
+      if (*fd >= 0) ::close(*fd);
+    }
+  } spare_closer{&spare};
   std::shared_ptr<DeviceTable> table;
   {
     std::lock_guard<std::mutex> lk(mu_);
@@ -868,8 +875,13 @@ void GrpcServer::run(Worker* w) {
       }
       if (fd == listen_fd_) {
         for (;;) {
-          const int cfd = accept4(listen_fd_, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
-          if (cfd < 0) break;
+          bool shed = false;
+          const int cfd = accept_or_shed(listen_fd_, nullptr, nullptr, &spare, &shed);
+          if (cfd < 0) {
+            if (!shed) break;
+            shed_.add();
+            continue;
+          }
           Worker* t = w;  // least-loaded worker, this one on a tie
           for (auto& o : workers_)
             if (o->load.load(std::memory_order_relaxed) < t->load.load(std::memory_order_relaxed)) t = o.get();

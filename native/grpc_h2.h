@@ -41,6 +41,7 @@ class GrpcServer {
   void notify(); // wake ListAndWatch streams now (health changed)
   bool running() const { return running_.load(); }
   uint64_t requests() const { return requests_.load(); }
+  uint64_t shed_connections() const { return shed_.load(); }  // closed at accept: out of fds
   int connections() const { return conns_.load(); }
   std::vector<int> worker_connections() const;  // connections owned per worker thread
   const std::string& socket_path() const { return path_; }
@@ -68,6 +69,7 @@ class GrpcServer {
   std::atomic<bool> running_{false};
   std::atomic<bool> stop_{false};
   ShardedCounter requests_;  // every worker counts its calls: no shared line per RPC
+  ShardedCounter shed_;
   std::atomic<int> conns_{0};
   std::vector<std::unique_ptr<Worker>> workers_;
   std::vector<std::thread> threads_;

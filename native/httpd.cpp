@@ -180,6 +180,7 @@ int HttpServer::start() {
     threads_.emplace_back([this, w] {
       std::vector<epoll_event> evs(128);
       char rbuf[16384];
+      int spare = -1;  // reserve descriptor for accept_or_shed
       int64_t last_sweep = mono_ns();
       auto close_conn = [&](int cfd) {
         epoll_ctl(w->ep, EPOLL_CTL_DEL, cfd, nullptr);
@@ -247,8 +248,13 @@ int HttpServer::start() {
             for (;;) {
               struct sockaddr_storage peer {};
               socklen_t pl = sizeof(peer);
-              const int cfd = accept4(listen_fd_, reinterpret_cast<sockaddr*>(&peer), &pl, SOCK_NONBLOCK | SOCK_CLOEXEC);
-              if (cfd < 0) break;
+              bool shed = false;
+              const int cfd = accept_or_shed(listen_fd_, reinterpret_cast<sockaddr*>(&peer), &pl, &spare, &shed);
+              if (cfd < 0) {
+                if (!shed) break;
+                shed_.add();
+                continue;
+              }
               int one = 1;
               setsockopt(cfd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
               auto c = std::make_unique<Conn>();
@@ -426,6 +432,7 @@ int HttpServer::start() {
       adopt();
       for (auto& kv : w->conns) close(kv.first);
       w->conns.clear();
+      if (spare >= 0) close(spare);
     });
   }
   if (cfg_.access_log) {

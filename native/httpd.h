@@ -46,6 +46,7 @@ class HttpServer {
   int port() const { return bound_port_; }
   void set_restart_hook(std::function<void()> hook);
   uint64_t requests_total() const { return requests_.load(); }
+  uint64_t shed_connections() const { return shed_.load(); }  // closed at accept: out of fds
   std::vector<int> worker_connections() const;  // connections owned per worker thread
   // Renders the echo_http_* families (exposed for tests).
   void render_http_metrics(std::string* out) const;
@@ -75,6 +76,7 @@ class HttpServer {
   std::vector<std::unique_ptr<Worker>> workers_;
   std::thread log_thread_;
   ShardedCounter requests_;
+  ShardedCounter shed_;
 
   static constexpr int kMethods = 8;
   static constexpr int kHandlers = 5;
