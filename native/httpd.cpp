@@ -102,7 +102,13 @@ struct Conn {
   std::string remote;
   bool close_after = false;
   bool want_out = false;
+  bool want_in = true;
 };
+
+// Unsent response bytes above which a connection's further requests wait (a /metrics
+// answer is up to ~100 KB; 4 MiB is dozens of pipelined scrapes).
+constexpr size_t kMaxPendingOut = 4u << 20;
+inline size_t backlog(const Conn* c) { return c->out.size() - c->out_off; }
 
 }  // namespace
 
@@ -219,14 +225,117 @@ int HttpServer::start() {
           }
         }
         const bool want = c->out_off < c->out.size() || !c->out.empty();
-        if (want != c->want_out) {
+        const bool want_in = backlog(c) <= kMaxPendingOut;
+        if (want != c->want_out || want_in != c->want_in) {
           struct epoll_event ev {};
-          ev.events = EPOLLIN | EPOLLRDHUP | (want ? EPOLLOUT : 0);
+          // throttled: no read interest, and no EPOLLRDHUP either (level-triggered, it
+          // would fire on every wait once the peer half-closes)
+          ev.events = (want_in ? EPOLLIN | EPOLLRDHUP : 0u) | (want ? EPOLLOUT : 0u);
           ev.data.fd = c->fd;
           epoll_ctl(w->ep, EPOLL_CTL_MOD, c->fd, &ev);
           c->want_out = want;
+          c->want_in = want_in;
         }
         return true;
+      };
+      // Parses and answers every complete request in the buffer (pipelining) while the
+      // connection's unsent output stays under kMaxPendingOut: a client that pipelines
+      // requests without reading the answers is throttled (its socket leaves the epoll
+      // read set, TCP flow control holds the rest) instead of growing our buffer.
+      auto serve = [&](Conn* c) {
+        // parse and answer every complete request in the buffer (pipelining)
+        size_t pos = 0;
+        while (!c->close_after && backlog(c) <= kMaxPendingOut) {
+          const size_t hdr_end = c->in.find("\r\n\r\n", pos);
+          if (hdr_end == std::string::npos) {
+            if (c->in.size() - pos > 65536) {  // header block too large
+              std::string o;
+              int st = 431;
+              size_t bytes = 0;
+              handle("", "", "", false, false, &o, &st, &bytes);
+              c->out.append(o);
+              c->close_after = true;
+            }
+            break;
+          }
+          const char* p = c->in.data() + pos;
+          const size_t hlen = hdr_end - pos;
+          const char* le = static_cast<const char*>(memchr(p, '\n', hlen + 2));
+          std::string reqline(p, le ? static_cast<size_t>(le - p) : hlen);
+          if (!reqline.empty() && reqline.back() == '\r') reqline.pop_back();
+          const size_t sp1 = reqline.find(' ');
+          const size_t sp2 = sp1 == std::string::npos ? std::string::npos : reqline.find(' ', sp1 + 1);
+          std::string method, uri, proto;
+          if (sp1 != std::string::npos && sp2 != std::string::npos) {
+            method = reqline.substr(0, sp1);
+            uri = reqline.substr(sp1 + 1, sp2 - sp1 - 1);
+            proto = reqline.substr(sp2 + 1);
+          }
+          std::string origin, hosth, ua;
+          size_t content_len = 0;
+          bool conn_close = false, conn_keep = false, chunked = false, gzip_ok = false;
+          const char* q = le ? le + 1 : p + hlen;
+          const char* hend = p + hlen;
+          while (q < hend) {
+            const char* e = static_cast<const char*>(memchr(q, '\n', static_cast<size_t>(hend - q)));
+            if (!e) e = hend;
+            const char* colon = static_cast<const char*>(memchr(q, ':', static_cast<size_t>(e - q)));
+            if (colon) {
+              const size_t nlen = static_cast<size_t>(colon - q);
+              const char* v = colon + 1;
+              while (v < e && (*v == ' ' || *v == '\t')) ++v;
+              const char* ve = e;
+              while (ve > v && (ve[-1] == '\r' || ve[-1] == ' ')) --ve;
+              std::string val(v, static_cast<size_t>(ve - v));
+              if (ieq(q, nlen, "origin")) origin = val;
+              else if (ieq(q, nlen, "host")) hosth = val;
+              else if (ieq(q, nlen, "user-agent")) ua = val;
+              else if (ieq(q, nlen, "content-length")) content_len = std::strtoull(val.c_str(), nullptr, 10);
+              else if (ieq(q, nlen, "transfer-encoding")) chunked = true;
+              else if (ieq(q, nlen, "accept-encoding")) gzip_ok = gzip_ok || accepts_gzip(val);
+              else if (ieq(q, nlen, "connection")) {
+                std::string lv = val;
+                std::transform(lv.begin(), lv.end(), lv.begin(), ::tolower);
+                if (lv.find("close") != std::string::npos) conn_close = true;
+                if (lv.find("keep-alive") != std::string::npos) conn_keep = true;
+              }
+            }
+            q = e + 1;
+          }
+          const size_t body_start = hdr_end + 4;
+          if (content_len > (1u << 20)) {
+            std::string o;
+            int st = 413;
+            size_t bytes = 0;
+            handle("", "", origin, false, false, &o, &st, &bytes);
+            c->out.append(o);
+            c->close_after = true;
+            break;
+          }
+          if (c->in.size() < body_start + content_len) break;  // wait for the body
+          const bool http10 = proto == "HTTP/1.0";
+          const bool keep = !chunked && !method.empty() && (http10 ? conn_keep : !conn_close);
+          const int64_t t0 = mono_ns();
+          int status = 0;
+          size_t body_bytes = 0;
+          // responses are appended straight to the connection's output buffer (its
+          // capacity is reused across requests): no per-request copy of the body
+          if (method.empty() || chunked) {
+            status = method.empty() ? 400 : 501;
+            handle("", "", origin, false, http10, &c->out, &status, &body_bytes);
+          } else {
+            const size_t qm = uri.find('?');
+            handle(method, qm == std::string::npos ? uri : uri.substr(0, qm), origin, keep, http10, &c->out,
+                   &status, &body_bytes, gzip_ok);
+          }
+          const double dt = (mono_ns() - t0) * 1e-9;
+          requests_.add();
+          if (cfg_.access_log && method != "OPTIONS" && !method.empty())
+            log_access(c->remote, hosth, method, uri, ua, status, dt, content_len, body_bytes);
+          pos = body_start + content_len;
+          if (!keep) c->close_after = true;
+        }
+        c->in.erase(0, pos);
       };
       // busy-poll window (see GrpcServer): a scraper's next request on a keep-alive
       // connection usually lands while the worker is still polling
@@ -301,7 +410,7 @@ int HttpServer::start() {
             continue;
           }
           bool peer_closed = false;
-          if (evs[i].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP)) {
+          if ((evs[i].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP)) && backlog(c) <= kMaxPendingOut) {
             for (;;) {
               const ssize_t r = recv(fd, rbuf, sizeof(rbuf), 0);
               if (r > 0) {
@@ -319,102 +428,35 @@ int HttpServer::start() {
               }
             }
             if (spin_ns > 0) spin_until = now + spin_ns;
-            // parse and answer every complete request in the buffer (pipelining)
-            size_t pos = 0;
-            while (!c->close_after) {
-              const size_t hdr_end = c->in.find("\r\n\r\n", pos);
-              if (hdr_end == std::string::npos) {
-                if (c->in.size() - pos > 65536) {  // header block too large
-                  std::string o;
-                  int st = 431;
-                  size_t bytes = 0;
-                  handle("", "", "", false, false, &o, &st, &bytes);
-                  c->out.append(o);
-                  c->close_after = true;
-                }
-                break;
-              }
-              const char* p = c->in.data() + pos;
-              const size_t hlen = hdr_end - pos;
-              const char* le = static_cast<const char*>(memchr(p, '\n', hlen + 2));
-              std::string reqline(p, le ? static_cast<size_t>(le - p) : hlen);
-              if (!reqline.empty() && reqline.back() == '\r') reqline.pop_back();
-              const size_t sp1 = reqline.find(' ');
-              const size_t sp2 = sp1 == std::string::npos ? std::string::npos : reqline.find(' ', sp1 + 1);
-              std::string method, uri, proto;
-              if (sp1 != std::string::npos && sp2 != std::string::npos) {
-                method = reqline.substr(0, sp1);
-                uri = reqline.substr(sp1 + 1, sp2 - sp1 - 1);
-                proto = reqline.substr(sp2 + 1);
-              }
-              std::string origin, hosth, ua;
-              size_t content_len = 0;
-              bool conn_close = false, conn_keep = false, chunked = false, gzip_ok = false;
-              const char* q = le ? le + 1 : p + hlen;
-              const char* hend = p + hlen;
-              while (q < hend) {
-                const char* e = static_cast<const char*>(memchr(q, '\n', static_cast<size_t>(hend - q)));
-                if (!e) e = hend;
-                const char* colon = static_cast<const char*>(memchr(q, ':', static_cast<size_t>(e - q)));
-                if (colon) {
-                  const size_t nlen = static_cast<size_t>(colon - q);
-                  const char* v = colon + 1;
-                  while (v < e && (*v == ' ' || *v == '\t')) ++v;
-                  const char* ve = e;
-                  while (ve > v && (ve[-1] == '\r' || ve[-1] == ' ')) --ve;
-                  std::string val(v, static_cast<size_t>(ve - v));
-                  if (ieq(q, nlen, "origin")) origin = val;
-                  else if (ieq(q, nlen, "host")) hosth = val;
-                  else if (ieq(q, nlen, "user-agent")) ua = val;
-                  else if (ieq(q, nlen, "content-length")) content_len = std::strtoull(val.c_str(), nullptr, 10);
-                  else if (ieq(q, nlen, "transfer-encoding")) chunked = true;
-                  else if (ieq(q, nlen, "accept-encoding")) gzip_ok = gzip_ok || accepts_gzip(val);
-                  else if (ieq(q, nlen, "connection")) {
-                    std::string lv = val;
-                    std::transform(lv.begin(), lv.end(), lv.begin(), ::tolower);
-                    if (lv.find("close") != std::string::npos) conn_close = true;
-                    if (lv.find("keep-alive") != std::string::npos) conn_keep = true;
-                  }
-                }
-                q = e + 1;
-              }
-              const size_t body_start = hdr_end + 4;
-              if (content_len > (1u << 20)) {
-                std::string o;
-                int st = 413;
-                size_t bytes = 0;
-                handle("", "", origin, false, false, &o, &st, &bytes);
-                c->out.append(o);
-                c->close_after = true;
-                break;
-              }
-              if (c->in.size() < body_start + content_len) break;  // wait for the body
-              const bool http10 = proto == "HTTP/1.0";
-              const bool keep = !chunked && !method.empty() && (http10 ? conn_keep : !conn_close);
-              const int64_t t0 = mono_ns();
-              int status = 0;
-              size_t body_bytes = 0;
-              // responses are appended straight to the connection's output buffer (its
-              // capacity is reused across requests): no per-request copy of the body
-              if (method.empty() || chunked) {
-                status = method.empty() ? 400 : 501;
-                handle("", "", origin, false, http10, &c->out, &status, &body_bytes);
-              } else {
-                const size_t qm = uri.find('?');
-                handle(method, qm == std::string::npos ? uri : uri.substr(0, qm), origin, keep, http10, &c->out,
-                       &status, &body_bytes, gzip_ok);
-              }
-              const double dt = (mono_ns() - t0) * 1e-9;
-              requests_.add();
-              if (cfg_.access_log && method != "OPTIONS" && !method.empty())
-                log_access(c->remote, hosth, method, uri, ua, status, dt, content_len, body_bytes);
-              pos = body_start + content_len;
-              if (!keep) c->close_after = true;
-            }
-            c->in.erase(0, pos);
           }
+          serve(c);
           if (!c->out.empty() || (evs[i].events & EPOLLOUT)) {
             if (!flush(c)) continue;
+            // Drained below the limit with requests still waiting (a throttled pipelining
+            // client): answer them now, no further EPOLLIN may come for them.  A few rounds
+            // per event, so one such client does not hold the worker; if requests remain
+            // and nothing is queued to send, EPOLLOUT (writable at once) brings us back.
+            bool closed = false;
+            for (int round = 0; round < 8 && !c->in.empty() && !c->close_after &&
+                                backlog(c) <= kMaxPendingOut;
+                 ++round) {
+              const size_t before = c->in.size();
+              serve(c);
+              if (!c->out.empty() && !flush(c)) {
+                closed = true;
+                break;
+              }
+              if (c->in.size() == before) break;  // only an incomplete request is left
+              if (round == 7 && !c->want_out) {
+                struct epoll_event ev {};
+                ev.events = EPOLLIN | EPOLLRDHUP | EPOLLOUT;
+                ev.data.fd = c->fd;
+                epoll_ctl(w->ep, EPOLL_CTL_MOD, c->fd, &ev);
+                c->want_out = true;
+                c->want_in = true;
+              }
+            }
+            if (closed) continue;
           }
           if (peer_closed && c->out.empty()) close_conn(fd);
         }

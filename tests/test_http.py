@@ -223,3 +223,60 @@ def test_native_scrapers_spread_over_workers(make_cfg):
         assert w._impl.worker_connections == [0, 0, 0]
     finally:
         w.stop()
+
+
+def _rss_bytes():
+    with open("/proc/self/status") as f:
+        for line in f:
+            if line.startswith("VmRSS:"):
+                return int(line.split()[1]) * 1024
+    return 0
+
+
+def test_pipelining_client_that_does_not_read_is_throttled(make_cfg):
+    """A client pipelines 2000 GET /metrics (77 KB answers, 150 MB in all) and reads
+    nothing for a second: the server stops reading its socket once 4 MiB of answers are
+    pending, so its memory stays flat; then every answer arrives, in order."""
+    import threading
+
+    cfg = make_cfg(webListenAddress="127.0.0.1:0", fixture="8gpu_cpx_nps4", migStrategy="single",
+                   http={"server": "native", "accessLog": False, "threads": 2})
+    mgr = PluginManager(cfg)
+    mgr.load_plugins()
+    mgr._start_telemetry()  # the full 64-partition exposition
+    w = WebServer(cfg, mgr)
+    port = w.start()
+    try:
+        s = socket.create_connection(("127.0.0.1", port), timeout=10)
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 16)
+        n = 2000
+        req = b"GET /metrics HTTP/1.1\r\nHost: x\r\n\r\n"
+        rss0 = _rss_bytes()
+        sender = threading.Thread(target=lambda: s.sendall(req * n), daemon=True)
+        sender.start()
+        time.sleep(1.0)
+        grown = _rss_bytes() - rss0
+        assert grown < 48 << 20, grown  # unthrottled: ~150 MB of queued answers
+        buf, got = b"", 0
+        while got < n:
+            chunk = s.recv(1 << 20)
+            assert chunk, "connection closed after %d answers" % got
+            buf += chunk
+            while True:
+                he = buf.find(b"\r\n\r\n")
+                if he < 0:
+                    break
+                head = buf[:he].decode()
+                assert head.startswith("HTTP/1.1 200 OK"), head[:80]
+                cl = int([h for h in head.split("\r\n") if h.lower().startswith("content-length:")][0].split(":")[1])
+                if len(buf) < he + 4 + cl:
+                    break
+                buf = buf[he + 4 + cl:]
+                got += 1
+        assert got == n and buf == b""
+        sender.join(5)
+        s.close()
+    finally:
+        w.stop()
+        mgr.exporter.stop()
+        mgr.monitor.stop()
