@@ -152,13 +152,14 @@ class PluginManager:
                 log.info("plugin server stopped")
                 return
             try:
-                if kind == EV_RESTART:
-                    self.counters["restarts_" + ev[1]] = self.counters.get("restarts_" + ev[1], 0) + 1
-                    log.info("restarting plugins (%s)", ev[1])
-                    self.restart_plugins()
-                elif kind == EV_KUBELET:
-                    self.counters["restarts_kubelet"] += 1
-                    log.info("kubelet.sock re-created: kubelet restarted; re-registering")
+                if kind in (EV_RESTART, EV_KUBELET):
+                    if kind == EV_RESTART:
+                        self.counters["restarts_" + ev[1]] = self.counters.get("restarts_" + ev[1], 0) + 1
+                        log.info("restarting plugins (%s)", ev[1])
+                    else:
+                        self.counters["restarts_kubelet"] += 1
+                        log.info("kubelet.sock re-created: kubelet restarted; re-registering")
+                    self._coalesce_restarts()
                     self.restart_plugins()
                 elif kind == EV_RETRY:
                     self.counters["restarts_retry"] += 1
@@ -182,6 +183,33 @@ class PluginManager:
                 log.error("event %s failed: %s; retrying in %.0fs", kind, e, self.cfg.retrySeconds)
                 self._arm_retry()
             self._publish_metrics()
+
+    def _coalesce_restarts(self) -> int:
+        """Takes the restart requests (``GET /restart``, kubelet re-creations) that are
+        already queued behind the one being handled: one reload serves them all, so a
+        burst of /restart calls cannot keep the manager reloading (the reference's
+        ``Restart()`` sets a flag, which coalesces too).  Every request is still counted;
+        other events keep their order."""
+        n = 0
+        with self.events.mutex:  # queue.Queue's own lock: nothing else runs meanwhile
+            q = self.events.queue
+            keep = collections.deque()
+            while q:
+                ev = q.popleft()
+                if ev[0] == EV_RESTART:
+                    key = "restarts_" + ev[1]
+                elif ev[0] == EV_KUBELET:
+                    key = "restarts_kubelet"
+                else:
+                    keep.append(ev)
+                    continue
+                self.counters[key] = self.counters.get(key, 0) + 1
+                n += 1
+            q.extend(keep)
+        if n:
+            self.counters["restarts_coalesced"] = self.counters.get("restarts_coalesced", 0) + n
+            log.info("%d more restart request(s) served by this reload", n)
+        return n
 
     # ------------------------------------------------------------ plugins
     def load_plugins(self) -> None:

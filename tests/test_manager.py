@@ -506,3 +506,27 @@ def test_canary_performance_floor_marks_slow_partition_unhealthy(make_cfg, plugi
         assert not r["ok"] and "HBM 2500 GB/s < 4000" in r["error"]
         _, r = m.canary_results[(1, 4)]
         assert "bf16 MFMA 900 TFLOP/s < 1500" in r["error"]
+
+
+def test_restart_burst_is_coalesced(make_cfg, plugin_dir, run_manager, monkeypatch):
+    """100 /restart calls that arrive while a reload runs are served by the next reload,
+    not by 100 reloads: every request is counted, a handful of reloads happen, and the
+    plugin ends registered and serving."""
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg())
+        k.wait_for_registrations(1)
+        orig = m.restart_plugins
+        reloads = []
+
+        def slow_restart():
+            reloads.append(time.monotonic())
+            time.sleep(0.05)  # the burst lands while this reload runs
+            orig()
+        monkeypatch.setattr(m, "restart_plugins", slow_restart)
+        for _ in range(100):
+            m.restart()
+        assert _wait(lambda: m.counters["restarts_api"] == 100, timeout=20)
+        assert _wait(lambda: m.events.empty(), timeout=10)
+        assert len(reloads) <= 5, len(reloads)
+        assert m.counters.get("restarts_coalesced", 0) == 100 - len(reloads)
+        assert k.client("amd-gpu.sock").get_options().get_preferred_allocation_available
