@@ -29,7 +29,9 @@ Speed-of-light references, measured untimed in the same run: ``uds_roundtrip_flo
 thread) and ``uds_roundtrip_floor_spin_p50_us`` (server thread polling, which is what the
 daemon's ``grpc.busyPollUs`` window gives back-to-back kubelet RPCs).  Also untimed:
 ``allocate_cold_p50_us``, Allocate calls 1 ms apart, each of which finds the server thread
-asleep (kubelet's pod admissions are sparse; compare with the sleeping-server floor).
+asleep (kubelet's pod admissions are sparse; compare with the sleeping-server floor), and
+``allocate_admission_p50_us``, the Allocate of a kubelet-like admission (GetPreferredAllocation,
+200 us of client-side work, Allocate) after 2 ms idle (``grpc.admissionPollUs``).
 
 The reference publishes no numbers, so ``vs_baseline`` is null.
 """
@@ -85,7 +87,8 @@ def _wait_http(port: int, timeout: float) -> None:
     raise TimeoutError("plugin web server did not come up on port %d" % port)
 
 
-def start_daemon(n_gpus: int, grpc_server: str, workdir: str, profile_dir: str = "", busy_poll_us=None):
+def start_daemon(n_gpus: int, grpc_server: str, workdir: str, profile_dir: str = "", busy_poll_us=None,
+                 admission_poll_us=None):
     """Rank 0: kubelet stub + plugin daemon subprocess.  Must run before GPU init."""
     from k8s_gpu_device_plugin_amd import native
     from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import KubeletStub
@@ -102,12 +105,13 @@ def start_daemon(n_gpus: int, grpc_server: str, workdir: str, profile_dir: str =
     grpc_threads = max(4, 2 * n_gpus)
     http_threads = max(4, SCRAPE_CONNS * n_gpus)
     bp = "" if busy_poll_us is None else "  busyPollUs: %d\n" % busy_poll_us
+    ap = "" if admission_poll_us is None else "  admissionPollUs: %d\n" % admission_poll_us
     with open(cfg_path, "w") as f:
         f.write("webListenAddress: \"127.0.0.1:%d\"\nmigStrategy: none\nbackend: %s\nfixture: %dgpu_spx\n"
                 "devices: \"0-%d\"\npluginDir: \"%s\"\nlog:\n  level: info\n  fileDir: \"\"\n"
                 "http:\n  accessLog: false\n  threads: %d\n%stelemetry:\n  intervalMs: 1000\n"
-                "grpc:\n  server: %s\n  threads: %d\n%s"
-                % (port, backend, n_gpus, n_gpus - 1, plugin_dir, http_threads, bp, grpc_server, grpc_threads, bp))
+                "grpc:\n  server: %s\n  threads: %d\n%s%s"
+                % (port, backend, n_gpus, n_gpus - 1, plugin_dir, http_threads, bp, grpc_server, grpc_threads, bp, ap))
         if profile_dir:  # benchmark: true -> cpu/mem/threads/native profiles when the daemon exits
             f.write("benchmark: true\nbenchmarkDir: \"%s\"\n" % os.path.abspath(profile_dir))
     env = dict(os.environ)
@@ -129,6 +133,8 @@ def main() -> int:
     ap.add_argument("--no-canary", action="store_true")
     ap.add_argument("--busy-poll-us", type=int, default=None,
                     help="override grpc.busyPollUs of the daemon (default: the config default)")
+    ap.add_argument("--admission-poll-us", type=int, default=None,
+                    help="override grpc.admissionPollUs of the daemon (default: the config default)")
     ap.add_argument("--profile-dir", default="", help="run the daemon with benchmark: true, profiles here")
     args = ap.parse_args()
 
@@ -152,7 +158,7 @@ def main() -> int:
         shutil.rmtree(workdir, ignore_errors=True)
         os.makedirs(workdir)
         proc, kubelet, port, reg, backend = start_daemon(n_gpus, args.grpc_server, workdir, args.profile_dir,
-                                                         args.busy_poll_us)
+                                                         args.busy_poll_us, args.admission_poll_us)
         info = {"port": port, "endpoint": reg.endpoint, "resource": reg.resource_name, "backend": backend,
                 "plugin_dir": os.path.join(workdir, "device-plugins")}
 
@@ -267,6 +273,17 @@ def main() -> int:
     mine["uds_floor_spin_p50"] = _pct(n.uds_pingpong(10000, 500, *sizes, server_spin=True), 0.5)
     # kubelet-like sparse calls: 1 ms apart, every one meets a sleeping server thread
     mine["alloc_cold"] = h2.bench_unary(v1beta1.METHOD_ALLOCATE, alloc_req, 400, 1000)
+    # a pod admission as kubelet runs it: GetPreferredAllocation, ~200 us of kubelet
+    # bookkeeping, then Allocate of the same container (2 ms idle before each admission)
+    adm = []
+    for _ in range(200):
+        time.sleep(0.002)
+        h2.bench_unary(v1beta1.METHOD_GET_PREFERRED, pref_req, 1)
+        t_go = perf() + 200e-6
+        while perf() < t_go:
+            pass
+        adm.extend(h2.bench_unary(v1beta1.METHOD_ALLOCATE, alloc_req, 1))
+    mine["alloc_admission"] = adm
     # /metrics: one loopback TCP exchange of a scrape's size, polling server
     mine["tcp_scrape_floor_p50"] = _pct(n.uds_pingpong(3000, 300, 90, body_len + 400, server_spin=True, tcp=True),
                                         0.5)
@@ -303,6 +320,7 @@ def main() -> int:
             "uds_roundtrip_floor_p50_us": round(gathered[0]["uds_floor_p50"] * 1e6, 2),
             "uds_roundtrip_floor_spin_p50_us": round(gathered[0]["uds_floor_spin_p50"] * 1e6, 2),
             "allocate_cold_p50_us": round(_pct([x for g in gathered for x in g["alloc_cold"]], 0.5) * 1e6, 2),
+            "allocate_admission_p50_us": round(_pct([x for g in gathered for x in g["alloc_admission"]], 0.5) * 1e6, 2),
             "tcp_scrape_floor_p50_us": round(gathered[0]["tcp_scrape_floor_p50"] * 1e6, 2),
             "allocate_p50_us_grpcio_client": round(p50_grpcio, 2),
             "allocate_p99_us_grpcio_client": round(_pct(allocs, 0.99) * 1e6, 2),

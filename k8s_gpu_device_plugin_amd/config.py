@@ -83,6 +83,7 @@ class GrpcConfig:
     server: str = "native"       # native (C++ HTTP/2) | python (grpcio)
     threads: int = 4
     busyPollUs: int = 50         # native server: keep polling this long after a request (0 = off)
+    admissionPollUs: int = 1000  # ... and this long after a GetPreferredAllocation (its Allocate follows)
 
 
 @dataclass
@@ -265,6 +266,8 @@ def validate(cfg: Config) -> Config:
     for sect in ("grpc", "http"):
         if not 0 <= getattr(cfg, sect).busyPollUs <= 100000:
             raise ConfigError("%s.busyPollUs must be within 0..100000" % sect)
+    if not 0 <= cfg.grpc.admissionPollUs <= 100000:
+        raise ConfigError("grpc.admissionPollUs must be within 0..100000")
     if cfg.http.server not in ("native", "python"):
         raise ConfigError("http.server must be native|python")
     if cfg.podResources.intervalS <= 0:

@@ -224,7 +224,8 @@ class AmdDevicePlugin:
     def _start_native_server(self) -> None:
         n = native.load()
         srv = n.GrpcServer(self.socket, max(1, self.cfg.grpc.threads if self.cfg is not None else 2),
-                           self.cfg.grpc.busyPollUs if self.cfg is not None else 0)
+                           self.cfg.grpc.busyPollUs if self.cfg is not None else 0,
+                           self.cfg.grpc.admissionPollUs if self.cfg is not None else 0)
         srv.set_table(self.table)
         srv.start()
         self._native_server = srv

@@ -514,8 +514,8 @@ PYBIND11_MODULE(_native, m) {
 
   // ---- native gRPC (HTTP/2) server + client ----
   py::class_<GrpcServer, std::shared_ptr<GrpcServer>>(m, "GrpcServer")
-      .def(py::init<std::string, int, int>(), py::arg("socket_path"), py::arg("threads") = 2,
-           py::arg("busy_poll_us") = 0)
+      .def(py::init<std::string, int, int, int>(), py::arg("socket_path"), py::arg("threads") = 2,
+           py::arg("busy_poll_us") = 0, py::arg("admission_poll_us") = 0)
       .def("set_table", &GrpcServer::set_table)
       .def("add_table", &GrpcServer::set_table)
       .def("start", &GrpcServer::start, py::call_guard<py::gil_scoped_release>())

@@ -303,8 +303,11 @@ void send_headers(Conn& c, uint32_t sid) {
 
 }  // namespace
 
-GrpcServer::GrpcServer(std::string socket_path, int threads, int busy_poll_us)
-    : path_(std::move(socket_path)), nthreads_(threads), busy_poll_us_(std::max(0, std::min(busy_poll_us, 100000))) {}
+GrpcServer::GrpcServer(std::string socket_path, int threads, int busy_poll_us, int admission_poll_us)
+    : path_(std::move(socket_path)),
+      nthreads_(threads),
+      busy_poll_us_(std::max(0, std::min(busy_poll_us, 100000))),
+      admission_poll_us_(std::max(0, std::min(admission_poll_us, 100000))) {}
 
 GrpcServer::~GrpcServer() { stop(); }
 
@@ -463,6 +466,7 @@ void GrpcServer::run(Worker* w) {
     return true;
   };
   std::string scratch;
+  bool admitting = false;  // a GetPreferredAllocation was answered in this batch
   auto push_law = [&](Conn* c) {
     const uint64_t v = table->version();
     std::string payload;
@@ -517,6 +521,7 @@ void GrpcServer::run(Worker* w) {
         case kMPreferred:
           rpc = kRpcPreferred;
           ok = table->preferred(msg, &out);
+          admitting = true;  // this container's Allocate is next
           break;
         case kMOptions:
           rpc = kRpcOptions;
@@ -824,6 +829,7 @@ void GrpcServer::run(Worker* w) {
 
   uint64_t seen_version = table->version();
   const int64_t spin_ns = static_cast<int64_t>(busy_poll_us_) * 1000;
+  const int64_t admission_ns = static_cast<int64_t>(admission_poll_us_) * 1000;
   int64_t spin_until = 0;  // busy-poll window end (mono ns); 0 = closed
   while (!stop_.load(std::memory_order_relaxed)) {
     int n;
@@ -948,7 +954,9 @@ void GrpcServer::run(Worker* w) {
           }
         }
         if (!process(*c)) c->closing = true;
-        if (spin_ns > 0) spin_until = mono_ns() + spin_ns;
+        const int64_t window = admitting ? std::max(spin_ns, admission_ns) : spin_ns;
+        admitting = false;
+        if (window > 0) spin_until = std::max(spin_until, mono_ns() + window);
       }
       if (c->out.size() - c->out_off > kMaxPendingOut) {  // e.g. a PING flood that is never read
         close_conn(fd);

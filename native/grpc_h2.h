@@ -33,7 +33,11 @@ class GrpcServer {
   // is still polling when the next one lands skips the idle-CPU wake-up, which is most
   // of a unix-socket round trip.  An idle plugin never spins: the window only opens on
   // request activity and closes after busy_poll_us without any.
-  GrpcServer(std::string socket_path, int threads, int busy_poll_us = 0);
+  // admission_poll_us: the window after a GetPreferredAllocation.  Kubelet asks for the
+  // preferred devices and then, after some bookkeeping of its own, Allocates them for
+  // the same container: a longer window there (once per pod admission) keeps that
+  // Allocate off the cold path.
+  GrpcServer(std::string socket_path, int threads, int busy_poll_us = 0, int admission_poll_us = 0);
   ~GrpcServer();
   void set_table(std::shared_ptr<DeviceTable> t);
   void start();  // throws std::runtime_error on bind/listen failure
@@ -64,6 +68,7 @@ class GrpcServer {
   std::string path_;
   int nthreads_;
   int busy_poll_us_;
+  int admission_poll_us_;
   std::shared_ptr<DeviceTable> table_;
   int listen_fd_ = -1;
   std::atomic<bool> running_{false};

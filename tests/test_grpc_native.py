@@ -357,3 +357,36 @@ def test_connections_spread_over_workers(n, plugin_dir):
         assert srv.worker_connections == [0, 0, 0, 0] and srv.connections == 0
     finally:
         srv.stop()
+
+
+def test_admission_window_polls_after_preferred_only(n, plugin_dir):
+    """grpc.admissionPollUs: a GetPreferredAllocation keeps its worker polling (the same
+    container's Allocate comes next); any other RPC leaves it asleep when busyPollUs is 0."""
+    tc = n.TableConfig()
+    devs = [n.TableDevice("dev-%d" % i, i, 0, 0, -1, ["/dev/dri/renderD%d" % (128 + i)], True) for i in range(4)]
+    table = n.DeviceTable(tc, devs, n.Topology(4))
+    path = os.path.join(plugin_dir, "amd-gpu.sock")
+    srv = n.GrpcServer(path, 1, busy_poll_us=0, admission_poll_us=100000)
+    srv.set_table(table)
+    srv.start()
+    try:
+        c = n.H2Client(path)
+        alloc = v1beta1.AllocateRequest(container_requests=[v1beta1.ContainerAllocateRequest(
+            devices_ids=["dev-2"])]).SerializeToString()
+        pref = v1beta1.PreferredAllocationRequest(container_requests=[v1beta1.ContainerPreferredAllocationRequest(
+            available_deviceIDs=["dev-0", "dev-1", "dev-2", "dev-3"], allocation_size=2)]).SerializeToString()
+
+        def cpu_after(method, req):
+            assert c.unary(method, req)[0] == 0
+            cpu0 = time.process_time()
+            time.sleep(0.06)
+            return time.process_time() - cpu0
+        assert cpu_after(v1beta1.METHOD_ALLOCATE, alloc) < 0.02  # asleep
+        assert cpu_after(v1beta1.METHOD_GET_PREFERRED, pref) > 0.03  # polling for the Allocate
+        time.sleep(0.1)  # the 100 ms window closes
+        cpu0 = time.process_time()
+        time.sleep(0.1)
+        assert time.process_time() - cpu0 < 0.02
+        c.close()
+    finally:
+        srv.stop()
