@@ -216,6 +216,10 @@ struct GrpcServer::Worker {
   std::mutex in_mu;
   std::vector<std::unique_ptr<Conn>> incoming;
   std::atomic<int> load{0};  // owned + incoming connections
+  // set once this worker has served a ListAndWatch stream: only such workers are woken
+  // for a table change (kubelet holds one stream per plugin, so usually one worker;
+  // waking all of them one eventfd write after another delayed the stream's push)
+  std::atomic<bool> law_seen{false};
 };
 
 using Conn = GrpcServer::Worker::Conn;
@@ -370,7 +374,9 @@ std::vector<int> GrpcServer::worker_connections() const {
 void GrpcServer::notify() {
   for (auto& w : workers_) {
     const uint64_t one = 1;
-    if (w->efd >= 0) (void)!write(w->efd, &one, sizeof(one));
+    // workers that never served a stream have nothing to push (their 100 ms version
+    // poll covers a stream that starts while this runs)
+    if (w->efd >= 0 && w->law_seen.load(std::memory_order_acquire)) (void)!write(w->efd, &one, sizeof(one));
   }
 }
 
@@ -382,7 +388,10 @@ void GrpcServer::stop() {
     notifier_->srv = nullptr;
   }
   stop_ = true;
-  notify();
+  for (auto& w : workers_) {  // every worker, streams or not: they all have to leave their loop
+    const uint64_t one = 1;
+    if (w->efd >= 0) (void)!write(w->efd, &one, sizeof(one));
+  }
   for (auto& t : threads_)
     if (t.joinable()) t.join();
   threads_.clear();
@@ -548,6 +557,7 @@ void GrpcServer::run(Worker* w) {
         }
         case kMLaw: {
           rpc = kRpcListAndWatch;
+          w->law_seen.store(true, std::memory_order_release);
           s.law = true;
           s.law_version = table->version();
           send_headers(c, sid);
