@@ -12,6 +12,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <iterator>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -188,15 +189,23 @@ class Histogram {
   // scrapers each took 3.5x as long as one.
   void render(std::string* out, const char* name, std::string_view labels) const {
     const uint64_t key_count = count();
-    auto& cache = tl_cache();
+    TlCache& tl = tl_cache();
+    // entries of histograms that are gone (a plugin reload replaces every table's) are
+    // never hit again: drop what was not rendered in the last kSweepEvery renders
+    if (++tl.renders % kSweepEvery == 0) {
+      for (auto e = tl.map.begin(); e != tl.map.end();)
+        e = tl.renders - e->second.last_render > kSweepEvery ? tl.map.erase(e) : std::next(e);
+    }
+    auto& cache = tl.map;
     auto it = cache.find(id_);
     if (it != cache.end() && it->second.count == key_count && it->second.name == name &&
         it->second.labels == labels) {
+      it->second.last_render = tl.renders;
       out->append(it->second.text);
       return;
     }
-    if (it == cache.end() && cache.size() >= 1024) cache.clear();  // histograms of old reloads
     Cached& c = cache[id_];
+    c.last_render = tl.renders;
     c.count = key_count;
     c.name = name;
     c.labels.assign(labels.data(), labels.size());
@@ -241,11 +250,18 @@ class Histogram {
   std::unique_ptr<Shard[]> shards_;
   struct Cached {
     uint64_t count = 0;
+    uint64_t last_render = 0;  // TlCache::renders when last used
     std::string name, labels, text;
   };
-  // per-thread render cache, keyed by histogram id (ids are never reused, addresses are)
-  static std::unordered_map<uint64_t, Cached>& tl_cache() {
-    static thread_local std::unordered_map<uint64_t, Cached> c;
+  // per-thread render cache, keyed by histogram id (ids are never reused, addresses are);
+  // a scrape renders every live histogram, so a live entry is touched every ~100 renders
+  struct TlCache {
+    std::unordered_map<uint64_t, Cached> map;
+    uint64_t renders = 0;
+  };
+  static constexpr uint64_t kSweepEvery = 4096;
+  static TlCache& tl_cache() {
+    static thread_local TlCache c;
     return c;
   }
   static std::atomic<uint64_t>& next_id() {
