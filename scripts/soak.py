@@ -4,6 +4,12 @@ fixed time.  Checks that the daemon stays up, keeps answering, re-registers afte
 reload and does not grow (RSS sampled every few seconds).  Prints one JSON line.
 
     python scripts/soak.py --seconds 90 [--restart-every 0.25] [--backend auto|fixture]
+                           [--fault-every 0.1]   # fixture: scripted GPU 1 resets
+
+With ``--fault-every`` (fixture backend) GPU 1 alternates PRE_RESET / POST_RESET on that
+period while a kubelet-like ListAndWatch watcher follows the stream (re-opened after each
+reload); the run checks that the watcher kept seeing updates and that GPU 1 ends in the
+state the last event left it in.
 """
 import argparse
 import http.client
@@ -47,6 +53,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=90.0)
     ap.add_argument("--restart-every", type=float, default=0.25)
     ap.add_argument("--backend", default="auto")
+    ap.add_argument("--fault-every", type=float, default=0.0)
     a = ap.parse_args()
     n = native.load()
     backend = a.backend if a.backend != "auto" else ("amdsmi" if n.amdsmi_available() else "fixture")
@@ -58,17 +65,29 @@ def main():
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
+    fixture = "2gpu_spx"
+    if a.fault_every > 0:
+        if backend != "fixture":
+            raise SystemExit("--fault-every needs the fixture backend")
+        from k8s_gpu_device_plugin_amd.models import fixtures
+        model = fixtures.load_model("2gpu_spx")
+        n_ev = int((a.seconds + 10) / a.fault_every)
+        model["events"] = [{"at": 3.0 + i * a.fault_every, "kind": "pre_reset" if i % 2 == 0 else "post_reset",
+                            "gpu": 1} for i in range(n_ev)]
+        fixture = os.path.join(work, "faults.json")
+        with open(fixture, "w") as f:
+            json.dump(model, f)
     cfg = os.path.join(work, "soak.yml")
     with open(cfg, "w") as f:
-        f.write("webListenAddress: \"127.0.0.1:%d\"\nmigStrategy: none\nbackend: %s\nfixture: 2gpu_spx\n"
+        f.write("webListenAddress: \"127.0.0.1:%d\"\nmigStrategy: none\nbackend: %s\nfixture: \"%s\"\n"
                 "pluginDir: \"%s\"\nlog:\n  level: warn\n  fileDir: \"\"\nhttp:\n  accessLog: false\n"
-                "telemetry:\n  intervalMs: 100\n" % (port, backend, plugin_dir))
+                "telemetry:\n  intervalMs: 100\n" % (port, backend, fixture, plugin_dir))
     env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
     log = open(os.path.join(work, "daemon.log"), "w")
     proc = subprocess.Popen([sys.executable, "-m", "k8s_gpu_device_plugin_amd", "--configFile", cfg], cwd=work,
                             env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
     stats = {"backend": backend, "allocs": 0, "alloc_errors": 0, "reconnects": 0, "scrapes": 0, "scrape_errors": 0,
-             "restarts": 0, "restart_errors": 0, "rss_kb": []}
+             "restarts": 0, "restart_errors": 0, "rss_kb": [], "law_updates": 0, "law_reopens": 0}
     stop = threading.Event()
     try:
         regs = kubelet.wait_for_registrations(1, timeout=60)
@@ -115,7 +134,28 @@ def main():
                 except OSError:
                     stats["restart_errors"] += 1
 
-        ts = [threading.Thread(target=f, daemon=True) for f in (allocator, scraper, restarter)]
+        last_law = {}
+
+        def watcher():  # kubelet's ListAndWatch: re-opened whenever a reload ends the stream
+            c = None
+            while not stop.is_set():
+                try:
+                    if c is None:
+                        c = n.H2Client(sock, 2.0)
+                        c.open_stream(v1beta1.METHOD_LIST_AND_WATCH, b"")
+                        stats["law_reopens"] += 1
+                    msg = c.next_stream_message(0.5)
+                    if msg is None:
+                        c = None
+                        continue
+                    stats["law_updates"] += 1
+                    last_law["devices"] = {d.ID: d.health for d in v1beta1.ListAndWatchResponse.FromString(msg).devices}
+                except Exception:
+                    c = None
+                    time.sleep(0.005)
+
+        workers = [allocator, scraper, restarter] + ([watcher] if a.fault_every > 0 else [])
+        ts = [threading.Thread(target=f, daemon=True) for f in workers]
         for t in ts:
             t.start()
         t0 = time.time()
@@ -139,6 +179,11 @@ def main():
         stats["ok"] = bool(stats["daemon_alive"] and stats["health_after"] == 200 and stats["allocs"] > 0
                            and stats["scrapes"] > 0 and stats["restarts"] > 0 and stats["alloc_errors"] == 0
                            and stats["scrape_errors"] <= stats["restarts"] * 4)
+        if a.fault_every > 0:
+            # both GPUs still advertised; the stream kept moving (faults + reloads)
+            stats["law_last"] = last_law.get("devices")
+            stats["ok"] = stats["ok"] and stats["law_updates"] > a.seconds / a.fault_every / 4 and \
+                len(last_law.get("devices", {})) == 2
     finally:
         stop.set()
         try:
