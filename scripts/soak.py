@@ -87,7 +87,8 @@ def main():
     proc = subprocess.Popen([sys.executable, "-m", "k8s_gpu_device_plugin_amd", "--configFile", cfg], cwd=work,
                             env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
     stats = {"backend": backend, "allocs": 0, "alloc_errors": 0, "reconnects": 0, "scrapes": 0, "scrape_errors": 0,
-             "restarts": 0, "restart_errors": 0, "rss_kb": [], "law_updates": 0, "law_reopens": 0}
+             "restarts": 0, "restart_errors": 0, "rss_kb": [], "fds": [], "threads": [], "law_updates": 0,
+             "law_reopens": 0}
     stop = threading.Event()
     try:
         regs = kubelet.wait_for_registrations(1, timeout=60)
@@ -164,6 +165,8 @@ def main():
             if proc.poll() is not None:
                 break
             stats["rss_kb"].append(rss_kb(proc.pid))
+            stats["fds"].append(len(os.listdir("/proc/%d/fd" % proc.pid)))
+            stats["threads"].append(len(os.listdir("/proc/%d/task" % proc.pid)))
             print("t=%.0fs allocs=%d scrapes=%d restarts=%d rss=%d KB" % (
                 time.time() - t0, stats["allocs"], stats["scrapes"], stats["restarts"], stats["rss_kb"][-1]),
                 file=sys.stderr, flush=True)
@@ -176,7 +179,13 @@ def main():
         rs = stats["rss_kb"]
         half = rs[len(rs) // 2:] or rs
         stats["rss_growth_second_half_kb"] = (max(half) - min(half)) if half else None
+        # descriptors and threads do not accumulate over reloads
+        fd_half, th_half = stats["fds"][len(stats["fds"]) // 2:], stats["threads"][len(stats["threads"]) // 2:]
+        stats["fd_growth_second_half"] = (max(fd_half) - min(fd_half)) if fd_half else None
+        stats["thread_growth_second_half"] = (max(th_half) - min(th_half)) if th_half else None
         stats["ok"] = bool(stats["daemon_alive"] and stats["health_after"] == 200 and stats["allocs"] > 0
+                           and (stats["fd_growth_second_half"] or 0) <= 8
+                           and (stats["thread_growth_second_half"] or 0) <= 8
                            and stats["scrapes"] > 0 and stats["restarts"] > 0 and stats["alloc_errors"] == 0
                            and stats["scrape_errors"] <= stats["restarts"] * 4)
         if a.fault_every > 0:
