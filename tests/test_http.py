@@ -280,3 +280,44 @@ def test_pipelining_client_that_does_not_read_is_throttled(make_cfg):
         w.stop()
         mgr.exporter.stop()
         mgr.monitor.stop()
+
+
+def test_connection_churn_across_workers_leaves_nothing_behind(make_cfg):
+    """2000 short connections from 8 threads, each answered by whichever worker the
+    accepting one hands it to: every answer arrives, and afterwards no worker still counts
+    a connection and the process holds no extra descriptors."""
+    import os
+    import threading
+
+    cfg = make_cfg(webListenAddress="127.0.0.1:0", http={"server": "native", "accessLog": False, "threads": 4})
+    mgr = PluginManager(cfg)
+    mgr.load_plugins()
+    w = WebServer(cfg, mgr)
+    port = w.start()
+    try:
+        fds0 = len(os.listdir("/proc/self/fd"))
+        errors = []
+
+        def churn():
+            for _ in range(250):
+                try:
+                    s = socket.create_connection(("127.0.0.1", port), timeout=5)
+                    s.sendall(b"GET /health HTTP/1.1\r\nHost: x\r\n\r\n")
+                    if not s.recv(4096).startswith(b"HTTP/1.1 200 OK"):
+                        errors.append("bad answer")
+                    s.close()
+                except OSError as e:
+                    errors.append(repr(e))
+        ts = [threading.Thread(target=churn) for _ in range(8)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(120)
+        assert not errors, errors[:3]
+        deadline = time.time() + 5
+        while sum(w._impl.worker_connections) and time.time() < deadline:
+            time.sleep(0.02)
+        assert w._impl.worker_connections == [0, 0, 0, 0]
+        assert len(os.listdir("/proc/self/fd")) <= fds0 + 4 + 2  # + one reserve descriptor per worker
+    finally:
+        w.stop()
