@@ -390,3 +390,42 @@ def test_admission_window_polls_after_preferred_only(n, plugin_dir):
         c.close()
     finally:
         srv.stop()
+
+
+def test_connection_churn_across_workers(n, plugin_dir):
+    """1600 short kubelet-side connections from 8 threads (connect, one Allocate, close):
+    every call answers, and afterwards no worker still counts a connection."""
+    tc = n.TableConfig()
+    devs = [n.TableDevice("dev-%d" % i, i, 0, 0, -1, ["/dev/dri/renderD%d" % (128 + i)], True) for i in range(4)]
+    table = n.DeviceTable(tc, devs, n.Topology(4))
+    path = os.path.join(plugin_dir, "amd-gpu.sock")
+    srv = n.GrpcServer(path, 4, busy_poll_us=50)
+    srv.set_table(table)
+    srv.start()
+    try:
+        req = v1beta1.AllocateRequest(container_requests=[v1beta1.ContainerAllocateRequest(
+            devices_ids=["dev-3"])]).SerializeToString()
+        errors = []
+
+        def churn():
+            for _ in range(200):
+                try:
+                    c = n.H2Client(path)
+                    if c.unary(v1beta1.METHOD_ALLOCATE, req)[0] != 0:
+                        errors.append("status")
+                    c.close()
+                except Exception as e:  # pragma: no cover - reported below
+                    errors.append(repr(e))
+        ts = [threading.Thread(target=churn) for _ in range(8)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(120)
+        assert not errors, errors[:3]
+        deadline = time.time() + 5
+        while (srv.connections or sum(srv.worker_connections)) and time.time() < deadline:
+            time.sleep(0.02)
+        assert srv.connections == 0 and srv.worker_connections == [0, 0, 0, 0]
+        assert srv.requests >= 1600
+    finally:
+        srv.stop()
