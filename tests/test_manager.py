@@ -532,6 +532,8 @@ def test_restart_burst_is_coalesced(make_cfg, plugin_dir, run_manager, monkeypat
         assert k.client("amd-gpu.sock").get_options().get_preferred_allocation_available
 
 
+@pytest.mark.skipif(bool(os.environ.get("AMDGPU_DP_NATIVE_SO")),
+                    reason="sanitizer runs: ASan's quarantine holds freed memory, TSan is too slow for a soak")
 def test_soak_reloads_under_traffic_do_not_grow_the_daemon():
     """scripts/soak.py on the fixture backend: Allocate + scrapes + a /restart every 50 ms
     for 10 s.  Every reload must re-register and the daemon must not grow (per-reload
