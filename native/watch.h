@@ -1,8 +1,10 @@
 // inotify directory watcher (reference: modules/watch/watch.go:11-26 via fsnotify;
 // consumed at plugin/manager.go:80-84 to detect kubelet restarts by the CREATE of
-// kubelet.sock).  Blocking reads with a timeout so the caller's thread can stop.
+// kubelet.sock).  Blocking reads with a timeout so the caller's thread can stop.  The
+// watch survives the directory being removed and created again (see watch.cpp).
 #pragma once
 
+#include <cstdint>
 #include <string>
 #include <utility>
 #include <vector>
@@ -25,9 +27,13 @@ class DirWatcher {
   const std::string& dir() const { return dir_; }
 
  private:
+  bool rewatch(std::vector<FsEvent>* out);  // re-adds a lost watch; reports existing entries
+  bool same_dir() const;                     // the path still names the watched inode
+
   std::string dir_;
   int fd_ = -1;
   int wd_ = -1;
+  uint64_t dev_ = 0, ino_ = 0;  // identity of the watched directory
 };
 
 }  // namespace amdgpu_dp

@@ -63,6 +63,63 @@ def test_kubelet_restart_triggers_reregistration(make_cfg, plugin_dir, run_manag
         k.stop()
 
 
+def _drain_until(w, pred, timeout=5.0):
+    deadline = time.monotonic() + timeout
+    seen = []
+    while time.monotonic() < deadline:
+        seen += w.read(100)
+        if any(pred(e) for e in seen):
+            return seen
+    raise AssertionError("no matching event in %r" % (seen,))
+
+
+@pytest.mark.parametrize("how", ["remove", "rename"])
+def test_dir_watcher_survives_directory_recreation(tmp_path, how):
+    """The watched directory goes away and comes back (a node agent wiping
+    /var/lib/kubelet/device-plugins): the watcher re-arms, and a kubelet.sock that was
+    created before it re-armed is still reported."""
+    import shutil
+    from k8s_gpu_device_plugin_amd import native
+    d = tmp_path / "device-plugins"
+    d.mkdir()
+    w = native.load().DirWatcher(str(d))
+    (d / "a").write_text("")
+    _drain_until(w, lambda e: e[0] == "a" and e[2])
+    if how == "remove":
+        shutil.rmtree(d)
+    else:
+        os.rename(d, tmp_path / "old")
+    for _ in range(3):
+        w.read(50)  # watch gone; reads just pause
+    d.mkdir()
+    (d / "kubelet.sock").write_text("")
+    _drain_until(w, lambda e: e[0] == "kubelet.sock" and e[2])
+    # and it keeps following the new directory
+    (d / "kubelet.sock").unlink()
+    (d / "kubelet.sock").write_text("")
+    _drain_until(w, lambda e: e[0] == "kubelet.sock" and e[3])
+    if how == "rename":
+        (tmp_path / "old" / "stale").write_text("")  # the old inode is no longer watched
+        assert not [e for e in w.read(100) if e[0] == "stale"]
+
+
+def test_plugin_dir_recreated_triggers_reregistration(make_cfg, plugin_dir, run_manager):
+    import shutil
+    k = KubeletStub(plugin_dir).start()
+    try:
+        m = run_manager(make_cfg())
+        k.wait_for_registrations(1)
+        k.stop()
+        shutil.rmtree(plugin_dir)
+        time.sleep(0.3)
+        k = KubeletStub(plugin_dir).start()  # recreates the directory and kubelet.sock
+        k.wait_for_registrations(1, timeout=10)
+        assert _wait(lambda: m.counters["restarts_kubelet"] >= 1)
+        assert k.client("amd-gpu.sock").get_options().get_preferred_allocation_available
+    finally:
+        k.stop()
+
+
 def test_restart_api_reloads(make_cfg, plugin_dir, run_manager):
     with KubeletStub(plugin_dir) as k:
         m = run_manager(make_cfg())
