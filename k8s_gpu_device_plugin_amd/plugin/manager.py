@@ -40,6 +40,7 @@ log = get_logger("manager")
 EV_STOP, EV_RESTART, EV_RETRY, EV_KUBELET, EV_HEALTH, EV_REDISCOVER, EV_VERIFIED, EV_PODRES, EV_PRESTART_FAIL = (
     "stop", "restart", "retry", "kubelet", "health", "rediscover", "verified", "podresources", "prestart_fail")
 EV_METRICS = "metrics"  # state read by /metrics changed off the manager thread (canary results)
+EV_SOCKET_GONE = "socket_gone"  # a *.sock other than kubelet.sock was removed from the plugin dir
 HEALTH_LOG_LEN = 4096
 
 
@@ -178,6 +179,8 @@ class PluginManager:
                     self._set_health(ev[1], ev[2], False, ev[3])
                 elif kind == EV_REDISCOVER:
                     self._check_inventory()
+                elif kind == EV_SOCKET_GONE:
+                    self._socket_gone(ev[1])
             except Exception as e:
                 self.counters["load_failures"] += 1
                 log.error("event %s failed: %s; retrying in %.0fs", kind, e, self.cfg.retrySeconds)
@@ -210,6 +213,21 @@ class PluginManager:
             self.counters["restarts_coalesced"] = self.counters.get("restarts_coalesced", 0) + n
             log.info("%d more restart request(s) served by this reload", n)
         return n
+
+    def _socket_gone(self, name: str) -> None:
+        """A plugin's own socket was deleted while it serves (an operator or a cleanup
+        job wiping the directory; the reference would keep serving on an unreachable
+        socket until the next kubelet restart): serve again on a fresh socket and
+        re-register.  The plugin's own stop removes its socket too; by the time this
+        event is handled the reload that did so has bound the new one, so the file
+        exists and nothing happens."""
+        for p in self.plugins:
+            if os.path.basename(p.socket) != name or not p.serving or os.path.exists(p.socket):
+                continue
+            self.counters["restarts_socket"] = self.counters.get("restarts_socket", 0) + 1
+            log.warning("plugin socket %s was removed; serving again and re-registering", p.socket)
+            p.stop()
+            self.start_plugins()
 
     # ------------------------------------------------------------ plugins
     def load_plugins(self) -> None:
@@ -480,6 +498,8 @@ class PluginManager:
                 for name, _mask, created, _removed in watcher.read(200):
                     if name == "kubelet.sock" and created:
                         self.events.put((EV_KUBELET,))
+                    elif _removed and name.endswith(".sock") and name != "kubelet.sock":
+                        self.events.put((EV_SOCKET_GONE, name))
             if watcher is not None:
                 watcher.close()
 

@@ -120,6 +120,25 @@ def test_plugin_dir_recreated_triggers_reregistration(make_cfg, plugin_dir, run_
         k.stop()
 
 
+@pytest.mark.parametrize("grpc_server", ["native", "python"])
+def test_removed_plugin_socket_is_served_again(make_cfg, plugin_dir, run_manager, grpc_server):
+    """Someone deletes amd-gpu.sock while the plugin serves: kubelet could no longer
+    reach it.  The plugin binds a fresh socket and registers again; its own reloads,
+    which remove and re-create the socket themselves, do not trigger this."""
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(grpc={"server": grpc_server}))
+        k.wait_for_registrations(1)
+        m.restart()  # own reload: removes + re-binds the socket
+        k.wait_for_registrations(2, timeout=10)
+        time.sleep(0.5)
+        assert m.counters.get("restarts_socket", 0) == 0
+        os.remove(os.path.join(plugin_dir, "amd-gpu.sock"))
+        k.wait_for_registrations(3, timeout=10)
+        assert _wait(lambda: m.counters.get("restarts_socket", 0) == 1)
+        assert k.client("amd-gpu.sock").get_options().get_preferred_allocation_available
+        assert 'amdgpu_device_plugin_events_total{event="restarts_socket"} 1' in m.exporter.render()
+
+
 def test_restart_api_reloads(make_cfg, plugin_dir, run_manager):
     with KubeletStub(plugin_dir) as k:
         m = run_manager(make_cfg())
