@@ -89,6 +89,10 @@ class PluginManager:
         # GPUs the manager holds Unhealthy although the monitor reports them healthy:
         # recovery canary pending or failed.  Survives plugin reloads.
         self._held_unhealthy: set[int] = set()
+        # (gpu, partition) whose PreStartContainer canary failed.  Re-applied by every
+        # reload (a /restart or kubelet restart must not re-advertise them Healthy) until
+        # the GPU reports healthy again or a start-up canary re-checks it.
+        self._canary_failed: set[tuple[int, int]] = set()
         self._verify_pool: concurrent.futures.ThreadPoolExecutor | None = None
         self.podres = None  # PodResourcesWatcher when podResources.enabled
         # last canary result per (gpu, hardware partition index): (unix time, result dict);
@@ -176,6 +180,7 @@ class PluginManager:
                     pass  # allocation map / canary results changed: _publish_metrics below re-renders
                 elif kind == EV_PRESTART_FAIL:
                     self.counters["prestart_failures"] = self.counters.get("prestart_failures", 0) + 1
+                    self._canary_failed.add((ev[1], ev[2]))
                     self._set_health(ev[1], ev[2], False, ev[3])
                 elif kind == EV_REDISCOVER:
                     self._check_inventory()
@@ -240,12 +245,16 @@ class PluginManager:
         resources = new_resources(gpus, self.cfg.strategy, self.cfg.resourcePrefix, self.cfg.resources)
         self.device_map = build_device_map(gpus, resources, self.cfg.strategy, self.cfg.mountCardNodes,
                                            self.cfg.sharing.replicas, self.cfg.sharing.renameByDefault)
-        failed = self._startup_canary(gpus) if self.cfg.health.canaryOnStart else set()
+        if self.cfg.health.canaryOnStart:
+            failed = self._startup_canary(gpus)
+            self._canary_failed = set(failed)  # fresh verdicts replace older ones
+        else:
+            failed = set(self._canary_failed)
         plugins = [AmdDevicePlugin(name, devs, topo, self.cfg) for name, devs in self.device_map.items()]
         if self.cfg.health.canaryOnPreStart:
             for p in plugins:
                 p.prestart_check = self._prestart_check
-        # start-up canary failures are per partition and known only here
+        # canary failures are per partition and known only here
         for p in plugins:
             for gpu, part in failed:
                 p.set_gpu_health(gpu, part, False)
@@ -355,6 +364,8 @@ class PluginManager:
             log.info("GPU event on %d: %s", u.gpu, u.reason)
 
     def _set_health(self, gpu: int, partition: int, healthy: bool, reason: str, apply: bool = True) -> None:
+        if healthy:  # a recovery supersedes earlier canary verdicts on this GPU
+            self._canary_failed = {k for k in self._canary_failed if k[0] != gpu}
         for p in self.plugins:
             if apply:
                 p.set_gpu_health(gpu, partition, healthy)

@@ -118,3 +118,29 @@ def test_prestart_disabled_is_the_reference_no_op(make_cfg, plugin_dir, fake_can
         finally:
             m.stop()
             t.join(10)
+
+
+def test_prestart_failure_survives_a_reload(make_cfg, plugin_dir, fake_canary):
+    """A partition whose PreStartContainer canary failed stays Unhealthy through a
+    /restart reload (the monitor's state of its GPU is healthy, so only the manager
+    remembers the verdict)."""
+    k, m, t, reg = _start(make_cfg, plugin_dir, "native")
+    try:
+        ids = m.plugins[0].table.ids()
+        parts = {p.id: p.hip_id for g in m.gpus for p in g.partitions}
+        fake_canary["fail_hip"].add(parts[ids[5]])
+        with pytest.raises(grpc.RpcError):
+            k.client(reg.endpoint).pre_start([ids[5]])
+        deadline = time.monotonic() + 5
+        while m.counters.get("prestart_failures") != 1 and time.monotonic() < deadline:
+            time.sleep(0.01)
+        m.restart()
+        reg2 = k.wait_for_registrations(2)[1]
+        _, devs = k.watch(reg2.endpoint).next(timeout=5)
+        health = dict((d, h) for d, h, _ in devs)
+        assert health[ids[5]] == "Unhealthy"
+        assert [h for d, h in health.items() if d != ids[5]] == ["Healthy"] * (len(ids) - 1)
+    finally:
+        m.stop()
+        t.join(10)
+        k.stop()
