@@ -29,7 +29,8 @@ Speed-of-light references, measured untimed in the same run: ``uds_roundtrip_flo
 thread) and ``uds_roundtrip_floor_spin_p50_us`` (server thread polling, which is what the
 daemon's ``grpc.busyPollUs`` window gives back-to-back kubelet RPCs).  Also untimed:
 ``allocate_cold_p50_us``, Allocate calls 1 ms apart, each of which finds the server thread
-asleep (kubelet's pod admissions are sparse; compare with the sleeping-server floor), and
+asleep (kubelet's pod admissions are sparse; its speed of light is
+``uds_roundtrip_floor_cold_p50_us``, the bare exchange with the same 1 ms idle gap), and
 ``allocate_admission_p50_us``, the Allocate of a kubelet-like admission (GetPreferredAllocation,
 200 us of client-side work, Allocate) after 2 ms idle (``grpc.admissionPollUs``).
 
@@ -273,6 +274,8 @@ def main() -> int:
     mine["uds_floor_spin_p50"] = _pct(n.uds_pingpong(10000, 500, *sizes, server_spin=True), 0.5)
     # kubelet-like sparse calls: 1 ms apart, every one meets a sleeping server thread
     mine["alloc_cold"] = h2.bench_unary(v1beta1.METHOD_ALLOCATE, alloc_req, 400, 1000)
+    # ... and the bare exchange with the same 1 ms idle gap (cold caches, idle CPU states)
+    mine["uds_floor_cold_p50"] = _pct(n.uds_pingpong(400, 20, *sizes, gap_us=1000), 0.5)
     # a pod admission as kubelet runs it: GetPreferredAllocation, ~200 us of kubelet
     # bookkeeping, then Allocate of the same container (2 ms idle before each admission)
     adm = []
@@ -319,6 +322,7 @@ def main() -> int:
             "allocate_p50_us": round(p50, 2), "allocate_p99_us": round(_pct(allocs_native, 0.99) * 1e6, 2),
             "uds_roundtrip_floor_p50_us": round(gathered[0]["uds_floor_p50"] * 1e6, 2),
             "uds_roundtrip_floor_spin_p50_us": round(gathered[0]["uds_floor_spin_p50"] * 1e6, 2),
+            "uds_roundtrip_floor_cold_p50_us": round(gathered[0]["uds_floor_cold_p50"] * 1e6, 2),
             "allocate_cold_p50_us": round(_pct([x for g in gathered for x in g["alloc_cold"]], 0.5) * 1e6, 2),
             "allocate_admission_p50_us": round(_pct([x for g in gathered for x in g["alloc_admission"]], 0.5) * 1e6, 2),
             "tcp_scrape_floor_p50_us": round(gathered[0]["tcp_scrape_floor_p50"] * 1e6, 2),

@@ -23,6 +23,24 @@ from typing import Any
 from .api import v1beta1
 
 STRATEGIES = ("none", "single", "mixed")
+# health.disabledChecks names -> the native HealthCheck bits (native/health.h)
+HEALTH_CHECKS = {"reset": 1, "ecc": 2, "lost": 4, "retiredpages": 8}
+
+
+def disabled_checks_mask(value: str) -> int:
+    mask = 0
+    for name in str(value or "").replace(";", ",").split(","):
+        name = name.strip().lower()
+        if not name:
+            continue
+        if name == "all":
+            mask |= sum(HEALTH_CHECKS.values())
+        elif name in HEALTH_CHECKS:
+            mask |= HEALTH_CHECKS[name]
+        else:
+            raise ConfigError("health.disabledChecks: unknown check %r (want %s or all)"
+                              % (name, ", ".join(["reset", "ecc", "lost", "retiredPages"])))
+    return mask
 
 
 @dataclass
@@ -68,6 +86,9 @@ class HealthConfig:
     # retired + pending HBM pages at which a GPU goes Unhealthy: 0 = the GPU's own RAS
     # threshold when readable (root), -1 = never, N > 0 = N
     badPageThreshold: int = 0
+    # health checks that no longer make a GPU Unhealthy (still logged): comma list or
+    # YAML list of reset, ecc, lost, retiredPages, or all (env AMDGPU_DP_DISABLE_HEALTHCHECKS)
+    disabledChecks: str = ""
 
 
 @dataclass
@@ -170,6 +191,8 @@ def _coerce(value: Any, default: Any):
     if isinstance(default, float):
         return float(value)
     if isinstance(default, str):
+        if isinstance(value, (list, tuple)):  # e.g. health.disabledChecks: [ecc, reset]
+            return ",".join(str(x) for x in value)
         return str(value)
     return value
 
@@ -242,6 +265,8 @@ def apply_env(cfg: Config, environ=None) -> Config:
                 cfg.log.fileDir = val
     if "AMDGPU_DP_GRPC_SERVER" in environ:
         cfg.grpc.server = environ["AMDGPU_DP_GRPC_SERVER"]
+    if "AMDGPU_DP_DISABLE_HEALTHCHECKS" in environ:
+        cfg.health.disabledChecks = environ["AMDGPU_DP_DISABLE_HEALTHCHECKS"]
     if "AMDGPU_DP_HTTP_SERVER" in environ:
         cfg.http.server = environ["AMDGPU_DP_HTTP_SERVER"]
     return cfg
@@ -259,6 +284,7 @@ def validate(cfg: Config) -> Config:
         raise ConfigError(str(e)) from None
     if cfg.backend not in ("auto", "amdsmi", "fixture"):
         raise ConfigError("backend must be auto|amdsmi|fixture, got %r" % cfg.backend)
+    disabled_checks_mask(cfg.health.disabledChecks)
     if cfg.sharing.replicas < 1:
         raise ConfigError("sharing.replicas must be >= 1")
     if cfg.grpc.server not in ("native", "python"):

@@ -27,6 +27,7 @@ import threading
 import time
 
 from .. import native
+from ..config import disabled_checks_mask
 from ..device import build_device_map
 from ..device.backend import make_backend
 from ..resource import new_resources
@@ -66,6 +67,7 @@ class PluginManager:
         self.exporter = n.Exporter()
         self.exporter.set_build_info(build_info_text())
         self.monitor = n.HealthMonitor(self.backend, cfg.health.lostAfterFailures)
+        self.monitor.set_disabled_checks(disabled_checks_mask(cfg.health.disabledChecks))
         self.events: "queue.Queue[tuple]" = queue.Queue()
         self.plugins: list[AmdDevicePlugin] = []
         self.gpus: list = []

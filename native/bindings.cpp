@@ -407,6 +407,7 @@ PYBIND11_MODULE(_native, m) {
       .def("gpu_healthy", &HealthMonitor::gpu_healthy)
       .def("set_fast_tables", &HealthMonitor::set_fast_tables)
       .def("set_fast_recover", &HealthMonitor::set_fast_recover)
+      .def("set_disabled_checks", &HealthMonitor::set_disabled_checks, py::call_guard<py::gil_scoped_release>())
       .def("attach_tables", &HealthMonitor::attach_tables, py::arg("tables"), py::arg("fast_recover"),
            py::arg("held_unhealthy"), py::call_guard<py::gil_scoped_release>())
       .def("set_bad_page_thresholds", &HealthMonitor::set_bad_page_thresholds)
@@ -693,12 +694,12 @@ PYBIND11_MODULE(_native, m) {
     return out;
   });
   m.def("uds_pingpong",
-        [](int n, int warmup, int req_bytes, int resp_bytes, bool server_spin, bool tcp) {
+        [](int n, int warmup, int req_bytes, int resp_bytes, bool server_spin, bool tcp, int gap_us) {
           py::gil_scoped_release rel;
-          return uds_pingpong(n, warmup, req_bytes, resp_bytes, server_spin, tcp);
+          return uds_pingpong(n, warmup, req_bytes, resp_bytes, server_spin, tcp, gap_us);
         },
         py::arg("n") = 10000, py::arg("warmup") = 500, py::arg("req_bytes") = 128, py::arg("resp_bytes") = 256,
-        py::arg("server_spin") = false, py::arg("tcp") = false);
+        py::arg("server_spin") = false, py::arg("tcp") = false, py::arg("gap_us") = 0);
   m.def("render_bench",
         [](std::shared_ptr<Exporter> ex, std::shared_ptr<HttpServer> http, int threads, int iters) {
           py::gil_scoped_release rel;

@@ -59,10 +59,39 @@ void HealthMonitor::emit_locked(HealthUpdate u) {
   cv_.notify_all();
 }
 
+namespace {
+int check_of(int kind) {
+  switch (kind) {
+    case kEvtPreReset:
+    case kEvtPostReset: return kCheckReset;
+    case kEvtEccUncorrectable: return kCheckEcc;
+    case kEvtDeviceLost:
+    case kEvtDeviceRecovered: return kCheckLost;
+    case kEvtRetiredPagesExceeded:
+    case kEvtRetiredPagesCleared: return kCheckRetiredPages;
+    default: return 0;
+  }
+}
+}  // namespace
+
+bool HealthMonitor::healthy_locked(const GpuState& st) const {
+  return !(st.resetting && !(disabled_ & kCheckReset)) && !(st.ecc_bad && !(disabled_ & kCheckEcc)) &&
+         !(st.lost && !(disabled_ & kCheckLost)) && !(st.pages_bad && !(disabled_ & kCheckRetiredPages));
+}
+
 void HealthMonitor::reconcile_locked(int gpu, int kind, const std::string& reason) {
   GpuState& st = state_[gpu];
-  const bool healthy = !st.resetting && !st.ecc_bad && !st.lost && !st.pages_bad;
-  if (healthy == st.reported_healthy) return;
+  const bool healthy = healthy_locked(st);
+  if (healthy == st.reported_healthy) {
+    if (disabled_ & check_of(kind)) {  // tracked, not acted on: still worth a log line
+      HealthUpdate u;
+      u.kind = kind;
+      u.gpu = gpu;
+      u.reason = reason + " (health check disabled)";
+      emit_locked(std::move(u));
+    }
+    return;
+  }
   st.reported_healthy = healthy;
   if (!healthy || fast_recover_)
     for (const auto& t : fast_tables_) t->set_gpu_health(gpu, -1, healthy);
@@ -246,6 +275,12 @@ void HealthMonitor::attach_tables(std::vector<std::shared_ptr<DeviceTable>> tabl
 void HealthMonitor::set_bad_page_thresholds(std::vector<int> thresholds) {
   std::lock_guard<std::mutex> lk(mu_);
   page_thresholds_ = std::move(thresholds);
+}
+
+void HealthMonitor::set_disabled_checks(int mask) {
+  std::lock_guard<std::mutex> lk(mu_);
+  disabled_ = mask & kCheckAll;
+  for (size_t g = 0; g < state_.size(); ++g) reconcile_locked(static_cast<int>(g), kEvtNone, "health checks changed");
 }
 
 bool HealthMonitor::gpu_healthy(int gpu) const {

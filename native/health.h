@@ -25,6 +25,17 @@
 
 namespace amdgpu_dp {
 
+// Health checks an operator can turn off (health.disabledChecks): the condition is still
+// tracked and reported as an informational update, but it no longer makes the GPU
+// Unhealthy (compare NVIDIA's DP_DISABLE_HEALTHCHECKS; the reference has no checks).
+enum HealthCheck : int {
+  kCheckReset = 1,         // PRE_RESET .. POST_RESET
+  kCheckEcc = 2,           // uncorrectable ECC count increased
+  kCheckLost = 4,          // telemetry failing / device gone
+  kCheckRetiredPages = 8,  // retired + pending HBM pages at the threshold
+  kCheckAll = 15,
+};
+
 struct HealthUpdate {
   int64_t ts_ns = 0;
   int kind = kEvtNone;
@@ -70,6 +81,9 @@ class HealthMonitor {
                      const std::vector<int>& held_unhealthy);
   // Per-GPU retired-page limits (index = GPU; <= 0 disables the check for that GPU).
   void set_bad_page_thresholds(std::vector<int> thresholds);
+  // Bitmask of HealthCheck values to ignore; re-evaluates every GPU (a GPU held only by a
+  // check that is now off becomes Healthy).
+  void set_disabled_checks(int mask);
   uint64_t events_seen() const { return events_seen_; }
 
  private:
@@ -86,6 +100,7 @@ class HealthMonitor {
   void loop();
   void emit_locked(HealthUpdate u);
   void reconcile_locked(int gpu, int kind, const std::string& reason);
+  bool healthy_locked(const GpuState& st) const;
 
   std::shared_ptr<Backend> backend_;
   int lost_after_;
@@ -96,6 +111,7 @@ class HealthMonitor {
   std::vector<std::shared_ptr<DeviceTable>> fast_tables_;
   bool fast_recover_ = false;
   std::vector<int> page_thresholds_;
+  int disabled_ = 0;  // HealthCheck bits
   std::thread thread_;
   std::atomic<bool> running_{false};
   bool stop_ = false;

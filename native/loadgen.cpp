@@ -232,8 +232,9 @@ bool tcp_pair(int sv[2]) {
 
 }  // namespace
 
-std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_bytes, bool server_spin, bool tcp) {
-  if (n < 0 || warmup < 0 || req_bytes <= 0 || resp_bytes <= 0 || req_bytes > (1 << 20) || resp_bytes > (4 << 20))
+std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_bytes, bool server_spin, bool tcp,
+                                 int gap_us) {
+  if (n < 0 || warmup < 0 || gap_us < 0 || req_bytes <= 0 || resp_bytes <= 0 || req_bytes > (1 << 20) || resp_bytes > (4 << 20))
     throw std::invalid_argument("uds_pingpong: bad sizes");
   int sv[2];
   if (tcp ? !tcp_pair(sv) : socketpair(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0, sv) != 0)
@@ -292,6 +293,8 @@ std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_byte
   std::vector<char> buf(static_cast<size_t>(resp_bytes));
   bool failed = false;
   for (int i = 0; i < n + warmup && !failed; ++i) {
+    // gap_us > 0: both threads idle between exchanges, as the cold Allocate's do
+    if (gap_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(gap_us));
     const int64_t t0 = mono_ns();
     if (send(cfd, req.data(), req.size(), MSG_NOSIGNAL) != static_cast<ssize_t>(req.size())) {
       failed = true;

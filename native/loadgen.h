@@ -35,7 +35,7 @@ LoadResult grpc_load(const std::string& socket_path, const std::string& method, 
 // the device table cost.  tcp=true: the same over a loopback TCP connection, the floor
 // of one /metrics scrape of resp_bytes (what the kernel's copies and wake-ups cost).
 std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_bytes, bool server_spin = false,
-                                 bool tcp = false);
+                                 bool tcp = false, int gap_us = 0);
 
 class Exporter;
 class HttpServer;

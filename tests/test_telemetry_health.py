@@ -1,6 +1,8 @@
 """Exporter (per-GPU / per-partition telemetry rendering) and the native health monitor."""
 import time
 
+import pytest
+
 from hypothesis import given, settings, strategies as st
 
 from prometheus_client.parser import text_string_to_metric_families
@@ -93,6 +95,43 @@ def test_health_monitor_fast_tables_both_directions(n):
     m.process(n.HwEvent(n.EVT_POST_RESET, 1))
     assert t.healthy("b")
     assert [(x.gpu, x.healthy) for x in m.pop(100)] == [(1, 0), (1, 1), (1, 0), (1, 1)]
+
+
+def test_disabled_health_checks(n):
+    """health.disabledChecks: an ignored condition is logged, not acted on; turning a
+    check off releases a GPU that only it held, turning it back on re-applies it."""
+    from k8s_gpu_device_plugin_amd.config import ConfigError, disabled_checks_mask
+    assert disabled_checks_mask("ecc, retiredPages") == 2 | 8 and disabled_checks_mask("all") == 15
+    assert disabled_checks_mask("") == 0
+    with pytest.raises(ConfigError):
+        disabled_checks_mask("xid")
+    t = n.DeviceTable(n.TableConfig(), [n.TableDevice("a", 0), n.TableDevice("b", 1)], n.Topology(2))
+    m = n.HealthMonitor(n.FixtureBackend(1), 2)
+    m.set_gpu_count(2)
+    m.set_fast_tables([t])
+    m.set_fast_recover(True)
+    m.set_disabled_checks(disabled_checks_mask("ecc"))
+    m.process(n.HwEvent(n.EVT_ECC_UNCORRECTABLE, 1))
+    u = m.pop(100)
+    assert [(x.gpu, x.healthy) for x in u] == [(1, -1)] and "disabled" in u[0].reason
+    assert t.healthy("b") and m.gpu_healthy(1)
+    m.process(n.HwEvent(n.EVT_PRE_RESET, 0))  # other checks still act
+    assert [(x.gpu, x.healthy) for x in m.pop(100)] == [(0, 0)] and not t.healthy("a")
+    m.set_disabled_checks(0)  # the ECC latch of GPU 1 counts again
+    assert [(x.gpu, x.healthy) for x in m.pop(100)] == [(1, 0)] and not t.healthy("b")
+    m.set_disabled_checks(disabled_checks_mask("all"))
+    assert sorted((x.gpu, x.healthy) for x in m.pop(100)) == [(0, 1), (1, 1)]
+    assert t.healthy("a") and t.healthy("b")
+
+
+def test_disabled_checks_config(make_cfg):
+    from k8s_gpu_device_plugin_amd import config
+    cfg = config.validate(config.from_dict({"health": {"disabledChecks": ["ecc", "lost"]}}))
+    assert config.disabled_checks_mask(cfg.health.disabledChecks) == 2 | 4
+    cfg = config.apply_env(config.Config(), {"AMDGPU_DP_DISABLE_HEALTHCHECKS": "all"})
+    assert config.disabled_checks_mask(cfg.health.disabledChecks) == 15
+    with pytest.raises(config.ConfigError):
+        config.validate(config.from_dict({"health": {"disabledChecks": "ecc,xids"}}))
 
 
 def test_health_monitor_from_samples(n):
