@@ -81,6 +81,9 @@ FAMILIES = (
            "Advertised devices per resource and health"),
     Family("amdgpu_device_plugin_registered", "gauge", ("resource",), "manager",
            "Resource registered with kubelet"),
+    Family("amdgpu_device_plugin_health_event_sources", "gauge", (), "manager",
+           "GPUs whose hardware event notification (reset, thermal, VM fault) is armed; 0 with GPUs "
+           "advertised means resets are only seen as failed telemetry (no /dev/kfd access)"),
     # --- gfx950 canary (health.canary / canaryOnStart / canaryOnPreStart) ---
     Family("amdgpu_canary_last_run_timestamp_seconds", "gauge", ("gpu", "partition"), "manager",
            "Unix time of the partition's last canary run"),

@@ -97,6 +97,9 @@ class PluginManager:
         self._canary_failed: set[tuple[int, int]] = set()
         self._verify_pool: concurrent.futures.ThreadPoolExecutor | None = None
         self.podres = None  # PodResourcesWatcher when podResources.enabled
+        # GPUs with hardware event notification armed (read when the monitor starts and
+        # after each re-discovery, which can re-initialise amdsmi); None = not monitoring
+        self._event_sources: int | None = None
         # last canary result per (gpu, hardware partition index): (unix time, result dict);
         # written by canary pool threads, rendered by the manager thread
         self.canary_results: dict[tuple[int, int], tuple[float, dict]] = {}
@@ -299,6 +302,8 @@ class PluginManager:
         for g in gpus:
             thresholds[g.index] = g.bad_page_threshold
         self.monitor.set_bad_page_thresholds(thresholds)
+        if self._event_sources is not None:
+            self._event_sources = getattr(self.backend, "armed_event_sources", None)
         self.exporter.set_inventory(gpus)
         self.exporter.set_partition_labels(labels)
         self.exporter.set_tables([p.table for p in plugins])
@@ -542,6 +547,12 @@ class PluginManager:
     def _start_telemetry(self) -> None:
         if self.cfg.health.enabled:
             self.monitor.start()
+            self._event_sources = getattr(self.backend, "armed_event_sources", None)
+            if self.gpus and self._event_sources == 0:
+                # amdsmi event notification needs /dev/kfd (device cgroup or privileged pod):
+                # without it resets are seen only as failed telemetry samples
+                log.warning("no GPU event source armed (GPU reset / thermal events will not be received; "
+                            "health falls back to telemetry polling): check access to /dev/kfd")
         if self.cfg.telemetry.enabled:
             self.exporter.start(self.backend, self.cfg.telemetry.intervalMs,
                                 self.monitor if self.cfg.health.enabled else None)
@@ -574,6 +585,11 @@ class PluginManager:
             lines.append('amdgpu_device_plugin_devices{resource="%s",health="Healthy"} %d' % (p.resource, healthy))
             lines.append('amdgpu_device_plugin_devices{resource="%s",health="Unhealthy"} %d'
                          % (p.resource, len(p) - healthy))
+        if self._event_sources is not None:
+            lines += ["# HELP amdgpu_device_plugin_health_event_sources GPUs whose hardware event notification "
+                      "(reset, thermal, VM fault) is armed.",
+                      "# TYPE amdgpu_device_plugin_health_event_sources gauge",
+                      "amdgpu_device_plugin_health_event_sources %d" % self._event_sources]
         lines += ["# HELP amdgpu_device_plugin_registered 1 if the resource is registered with kubelet.",
                   "# TYPE amdgpu_device_plugin_registered gauge"]
         for p in self.plugins:
