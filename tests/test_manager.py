@@ -626,3 +626,23 @@ def test_soak_reloads_under_traffic_do_not_grow_the_daemon():
     # every reload re-registers (bursts may coalesce, the last one may still be running)
     assert r["restarts"] >= 50 and r["registrations"] >= 0.9 * r["restarts"]
     assert r["rss_growth_second_half_kb"] < 600, r["rss_kb"]
+
+
+def test_kubelet_restart_that_wipes_plugin_sockets(make_cfg, plugin_dir, run_manager):
+    """What a kubelet restart does on disk: kubelet.sock goes, kubelet clears the
+    plugin sockets from the directory, then binds a new kubelet.sock.  The plugin is
+    registered again promptly (no retry-timer wait) and serves on a socket that exists."""
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(retrySeconds=30.0))
+        k.wait_for_registrations(1)
+        k.stop()
+        os.remove(os.path.join(plugin_dir, "amd-gpu.sock"))
+        time.sleep(0.05)
+        t0 = time.monotonic()
+        k.start()
+        k.wait_for_registrations(2, timeout=10)
+        assert time.monotonic() - t0 < 5.0
+        time.sleep(0.5)
+        assert os.path.exists(os.path.join(plugin_dir, "amd-gpu.sock"))
+        assert k.client("amd-gpu.sock").get_options().get_preferred_allocation_available
+        print("registrations", len(k.requests), m.counters)
