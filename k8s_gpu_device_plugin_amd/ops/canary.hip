@@ -691,9 +691,93 @@ __global__ void __launch_bounds__(256) sweep_verify(const uint4* __restrict__ bu
   }
 }
 
+// Tile-stride: block b streams tiles b, b + G, b + 2G, ... of 256 * UNROLL contiguous
+// 16 B elements, so every wave reads whole contiguous runs (like CHUNKED) while the grid
+// sweeps the buffer front to back together (like grid-stride): no per-block tail.
+template <int UNROLL, bool NT>
+__global__ void __launch_bounds__(256) tile_write(uint4* __restrict__ buf, uint64_t n, uint32_t seed) {
+  const uint64_t tile = 256ull * UNROLL;
+  for (uint64_t t0 = blockIdx.x * tile; t0 < n; t0 += static_cast<uint64_t>(gridDim.x) * tile) {
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const uint64_t i = t0 + u * 256ull + threadIdx.x;
+      if (i < n) {
+        const uint4 v = pattern(i, seed);
+        if (NT) nt_store(v, buf + i);
+        else buf[i] = v;
+      }
+    }
+  }
+}
+
+template <int UNROLL, bool NT>
+__global__ void __launch_bounds__(256) tile_verify(const uint4* __restrict__ buf, uint64_t n, uint32_t seed,
+                                                   unsigned long long* __restrict__ errors) {
+  const uint64_t tile = 256ull * UNROLL;
+  uint32_t bad = 0;
+  for (uint64_t t0 = blockIdx.x * tile; t0 < n; t0 += static_cast<uint64_t>(gridDim.x) * tile) {
+    if (t0 + tile <= n) {
+      uint4 v[UNROLL];
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        const uint64_t i = t0 + u * 256ull + threadIdx.x;
+        v[u] = NT ? nt_load(buf + i) : buf[i];
+      }
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) bad += diff(v[u], pattern(t0 + u * 256ull + threadIdx.x, seed));
+    } else {
+      for (uint64_t i = t0 + threadIdx.x; i < n; i += 256) bad += diff(buf[i], pattern(i, seed));
+    }
+  }
+  for (int off = kWave / 2; off > 0; off >>= 1) bad += __shfl_down(bad, off, kWave);
+  __shared__ uint32_t wave_bad[256 / kWave];
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+  if (lane == 0) wave_bad[wid] = bad;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < static_cast<int>(blockDim.x / kWave); ++w) t += wave_bad[w];
+    if (t) atomicAdd(errors, static_cast<unsigned long long>(t));
+  }
+}
+
+template <int U, bool NT>
+float time_tile(uint4* buf, uint64_t n, int blocks, unsigned long long* err, int reps, float* t_read) {
+  hipEvent_t a, b, c;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  (void)hipEventCreate(&c);
+  float tw = 0, tr = 0;
+  for (int r = 0; r < reps + 1; ++r) {  // first repetition is warm-up
+    (void)hipEventRecord(a, 0);
+    hipLaunchKernelGGL((tile_write<U, false>), dim3(blocks), dim3(256), 0, 0, buf, n, 9u + r);
+    (void)hipEventRecord(b, 0);
+    hipLaunchKernelGGL((tile_verify<U, NT>), dim3(blocks), dim3(256), 0, 0, buf, n, 9u + r, err);
+    (void)hipEventRecord(c, 0);
+    (void)hipEventSynchronize(c);
+    float x = 0, y = 0;
+    (void)hipEventElapsedTime(&x, a, b);
+    (void)hipEventElapsedTime(&y, b, c);
+    if (r) {
+      tw += x;
+      tr += y;
+    }
+  }
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  (void)hipEventDestroy(c);
+  *t_read = tr / reps;
+  return tw / reps;
+}
+
 // Shapes picked from the on-hardware sweep (profiles/hbm_sweep_gpu.json, 4 GiB buffer):
 // writes: block-contiguous chunks, plain stores (~6.0 TB/s); verify: block-contiguous
 // chunks, non-temporal loads (~6.8 TB/s), both at 16 blocks of 256 threads per CU.
+// Re-swept at the canary's 1 GiB (profiles/r2/hbm_sweep_session4.json): behind plain
+// stores the verify measures ~5.9 TB/s, since it also pays for the write-back of the lines
+// the write phase left dirty in the caches; behind non-temporal stores it reads at 6.7 TB/s
+// but the write drops to 5.6.  The write+verify pair takes the same time either way.
+// Tile-stride (no per-block tail) was no faster than block-contiguous chunks.
 constexpr int kBlocksPerCu = 16;
 #define hbm_write sweep_write<4, false, true>
 #define hbm_verify sweep_verify<4, true, true>
@@ -1121,7 +1205,8 @@ int amdgpu_canary_gemm_rate(int device, int M, int N, int K, int iters, int flag
 }
 
 // variant: 0 U4 grid-stride, 1 U8 grid-stride, 2 U4 NT, 3 U8 NT, 4 U4 chunked, 5 U8 chunked,
-// 6 U4 NT chunked, 7 U16 grid-stride.  blocks_per_cu scales the grid.
+// 6 U4 NT chunked, 7 U16 grid-stride, 8 U8 NT chunked, 9 U2 NT chunked, 10 U4 tile-stride
+// (NT verify), 11 U8 tile-stride (NT verify), 12 U8 tile-stride.  blocks_per_cu scales the grid.
 int amdgpu_canary_hbm_sweep(int device, unsigned long long bytes, int variant, int blocks_per_cu, int reps,
                             double* write_gbps, double* read_gbps, unsigned long long* errors) {
   hipDeviceProp_t prop;
@@ -1145,6 +1230,11 @@ int amdgpu_canary_hbm_sweep(int device, unsigned long long bytes, int variant, i
     case 5: tw = time_pair<8, false, true>(buf, n, blocks, err, reps, &tr); break;
     case 6: tw = time_pair<4, true, true>(buf, n, blocks, err, reps, &tr); break;
     case 7: tw = time_pair<16, false, false>(buf, n, blocks, err, reps, &tr); break;
+    case 8: tw = time_pair<8, true, true>(buf, n, blocks, err, reps, &tr); break;
+    case 9: tw = time_pair<2, true, true>(buf, n, blocks, err, reps, &tr); break;
+    case 10: tw = time_tile<4, true>(buf, n, blocks, err, reps, &tr); break;
+    case 11: tw = time_tile<8, true>(buf, n, blocks, err, reps, &tr); break;
+    case 12: tw = time_tile<8, false>(buf, n, blocks, err, reps, &tr); break;
     default: break;
   }
   const hipError_t e = hipDeviceSynchronize();

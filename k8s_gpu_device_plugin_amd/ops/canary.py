@@ -164,7 +164,9 @@ def lowp_gemm(a_codes, bt_codes, a_scales, b_scales, fmt: str = "fp8", device: i
 
 
 SWEEP_VARIANTS = {0: "u4 grid-stride", 1: "u8 grid-stride", 2: "u4 nontemporal", 3: "u8 nontemporal",
-                  4: "u4 chunked", 5: "u8 chunked", 6: "u4 nt chunked", 7: "u16 grid-stride"}
+                  4: "u4 chunked", 5: "u8 chunked", 6: "u4 nt chunked", 7: "u16 grid-stride",
+                  8: "u8 nt chunked", 9: "u2 nt chunked", 10: "u4 tile-stride (nt verify)",
+                  11: "u8 tile-stride (nt verify)", 12: "u8 tile-stride"}
 
 
 def hbm_sweep(device: int = 0, nbytes: int = 4 << 30, variants=tuple(SWEEP_VARIANTS), blocks_per_cu=(4, 8, 16),
