@@ -1,7 +1,7 @@
 # Convenience targets (everything is also reachable through python -m ...).
 PY ?= python3
 
-.PHONY: build native canary test test-gpu sanitize bench suite soak probes run-fixture image clean
+.PHONY: build native canary test test-gpu sanitize analyze bench suite soak probes run-fixture image clean
 
 build:            ## C++ core (pybind11 .so) + gfx950 HIP canary, in-tree
 	$(PY) -m k8s_gpu_device_plugin_amd._build
@@ -17,6 +17,8 @@ sanitize:         ## native self-test, then the integration tests, under ASan+UB
 	$(PY) -m k8s_gpu_device_plugin_amd._build --sanitize address
 	$(PY) -m k8s_gpu_device_plugin_amd._build --sanitize thread
 	$(PY) -m pytest tests/test_sanitized_suite.py -q
+analyze:          ## clang static analyzer over native/*.cpp (fails on any finding)
+	scripts/analyze.sh
 bench:
 	$(PY) bench.py --gpus 1 --steps 20 --warmup 3
 suite:            ## BASELINE.json configs 1-5 + scaling + health propagation

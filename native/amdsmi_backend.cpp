@@ -353,7 +353,7 @@ class AmdSmiBackend : public Backend {
     std::memset(&m, 0, sizeof(m));
     int64_t t = mono_ns();
     const amdsmi_status_t mst = amdsmi_get_gpu_metrics_info(h0, &m);
-    t = charge(kCallGpuMetrics, t);
+    charge(kCallGpuMetrics, t);  // the blob's parsing below is not charged to any call
     if (mst == AMDSMI_STATUS_SUCCESS) {
       s->ok = true;
       if (valid16(m.current_socket_power) && m.current_socket_power != 0) s->power_w = m.current_socket_power;

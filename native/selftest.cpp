@@ -329,6 +329,10 @@ static void test_exporter_httpd_health(std::shared_ptr<FixtureBackend> be) {
     ts.emplace_back([&, i] {
       for (int k = 0; k < 40; ++k) {
         const int fd = socket(AF_INET, SOCK_STREAM, 0);
+        if (fd < 0) {
+          ++bad;
+          continue;
+        }
         sockaddr_in a{};
         a.sin_family = AF_INET;
         a.sin_port = htons(static_cast<uint16_t>(port));
@@ -373,6 +377,7 @@ static void test_exporter_httpd_health(std::shared_ptr<FixtureBackend> be) {
 // sampler ticks; a server stop races open ListAndWatch streams.
 static std::string http_get(int port, const char* req) {
   const int fd = socket(AF_INET, SOCK_STREAM, 0);
+  if (fd < 0) return std::string();
   sockaddr_in a{};
   a.sin_family = AF_INET;
   a.sin_port = htons(static_cast<uint16_t>(port));
@@ -436,7 +441,9 @@ static void test_reload_races(const std::string& dir) {
       for (auto& p : g.partitions) labels.push_back({g.index, p.index, p.id, "amd.com/gpu"});
     ex->set_inventory(b ? gb : ga);
     ex->set_partition_labels(labels);
-    ex->set_tables({table_of(b ? gb : ga, b ? tb : ta)});
+    std::vector<std::shared_ptr<DeviceTable>> tables;
+    tables.push_back(table_of(b ? gb : ga, b ? tb : ta));
+    ex->set_tables(std::move(tables));
     ex->set_extra("# extra " + std::to_string(k) + "\n");
     std::this_thread::sleep_for(std::chrono::milliseconds(2));
   }
