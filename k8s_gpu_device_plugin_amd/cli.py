@@ -58,7 +58,11 @@ def main(argv=None) -> int:
         cfg.log.level = args.log_level
     if args.log_dir is not None:
         cfg.log.fileDir = args.log_dir
-    config_mod.validate(cfg)
+    try:  # the command-line overrides are checked like the file's values
+        config_mod.validate(cfg)
+    except config_mod.ConfigError as e:
+        print("fatal config error: %s" % e, file=sys.stderr)
+        return 2
     init_logger(cfg.log.level, cfg.log.fileDir or None, APP_NAME, console=cfg.log.console)
     log = get_logger()
     log.info("Starting %s %s", APP_NAME, VERSION)

@@ -38,6 +38,11 @@ def test_version_and_bad_config(tmp_path):
     out = subprocess.run([sys.executable, "-m", "k8s_gpu_device_plugin_amd", "--configFile", str(tmp_path / "bad.yml")],
                          env=_env(), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=60)
     assert out.returncode == 2 and "invalid partition" in out.stderr
+    # the same check on a command-line override: a clean exit 2, not a traceback
+    out = subprocess.run([sys.executable, "-m", "k8s_gpu_device_plugin_amd", "--configFile", "",
+                          "--web-listen-address", "9002"],  # the reference's default (D11)
+                         env=_env(), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=60)
+    assert out.returncode == 2 and "host:port" in out.stderr and "Traceback" not in out.stderr
 
 
 @pytest.mark.parametrize("sig", [signal.SIGTERM, signal.SIGINT, signal.SIGHUP, signal.SIGQUIT])
