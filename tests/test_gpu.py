@@ -191,7 +191,12 @@ def test_plugin_end_to_end_on_mi355x(make_cfg, plugin_dir):
         c.request("GET", "/metrics")
         body = c.getresponse().read().decode()
         assert "amdgpu_info{" in body and 'gfx_target="gfx950"' in body
-        assert "echo_http_request_duration_seconds" not in body or True
+        # GPU event notification (resets) is armed on every advertised GPU of the box
+        armed = [ln for ln in body.splitlines() if ln.startswith("amdgpu_device_plugin_health_event_sources ")]
+        assert armed and int(armed[0].split()[1]) == len(mgr.gpus) >= 1, armed
+        c.request("GET", "/metrics")  # the first scrape is counted once it has been answered
+        body = c.getresponse().read().decode()
+        assert 'echo_http_requests_total{handler="/metrics",method="GET",status="2xx"}' in body
     finally:
         web.stop()
         mgr.stop()
