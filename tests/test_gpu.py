@@ -205,8 +205,7 @@ def test_plugin_end_to_end_on_mi355x(make_cfg, plugin_dir):
 
 
 def test_native_grpc_server_on_gpu_box(make_cfg, plugin_dir, n):
-    if not hasattr(n, "GrpcServer"):
-        pytest.skip("native gRPC server not built")
+    assert hasattr(n, "GrpcServer"), "native gRPC server not built (fail loudly on the GPU box)"
     from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import KubeletStub
     from k8s_gpu_device_plugin_amd.plugin.manager import PluginManager
     cfg = make_cfg(backend="amdsmi", migStrategy="none", grpc={"server": "native"})
