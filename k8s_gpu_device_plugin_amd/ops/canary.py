@@ -260,9 +260,14 @@ def run_isolated(device: int, hbm_bytes: int = 256 << 20, timeout: float = 120.0
         return {"ok": False, "device": device, "error": "canary timed out after %.0fs" % timeout}
     for line in reversed(p.stdout.strip().splitlines()):
         try:
-            return json.loads(line)
+            res = json.loads(line)
         except ValueError:
             continue
+        if isinstance(res, dict):  # the result line, not stray output that happens to parse
+            if p.returncode != 0 and res.get("ok"):
+                res = dict(res, ok=False, error="canary reported ok but exited %d: %s"
+                           % (p.returncode, p.stderr[-300:]))
+            return res
     return {"ok": False, "device": device, "error": "canary exited %d: %s" % (p.returncode, p.stderr[-500:])}
 
 
