@@ -89,6 +89,9 @@ class HealthConfig:
     # health checks that no longer make a GPU Unhealthy (still logged): comma list or
     # YAML list of reset, ecc, lost, retiredPages, or all (env AMDGPU_DP_DISABLE_HEALTHCHECKS)
     disabledChecks: str = ""
+    # a telemetry (amdsmi) call of one GPU in flight for longer than this marks the GPU
+    # lost: a wedged driver never returns an error to count (0 = off)
+    sampleStallS: float = 10.0
 
 
 @dataclass
@@ -285,6 +288,8 @@ def validate(cfg: Config) -> Config:
     if cfg.backend not in ("auto", "amdsmi", "fixture"):
         raise ConfigError("backend must be auto|amdsmi|fixture, got %r" % cfg.backend)
     disabled_checks_mask(cfg.health.disabledChecks)
+    if cfg.health.sampleStallS < 0:
+        raise ConfigError("health.sampleStallS must be >= 0 (0 = off)")
     if cfg.sharing.replicas < 1:
         raise ConfigError("sharing.replicas must be >= 1")
     if cfg.grpc.server not in ("native", "python"):

@@ -71,6 +71,11 @@ FAMILIES = (
     Family("amdgpu_telemetry_samples_total", "counter", (), "exporter", "Sampling passes"),
     Family("amdgpu_telemetry_sample_errors_total", "counter", (), "exporter", "Per-GPU sample failures"),
     Family("amdgpu_telemetry_sample_duration_seconds", "histogram", (), "exporter", "One sampling pass"),
+    Family("amdgpu_telemetry_last_pass_age_seconds", "gauge", (), "exporter",
+           "Seconds since the sampler last completed a pass (grows while a driver call hangs)"),
+    Family("amdgpu_telemetry_sample_stalled", "gauge", ("gpu",), "exporter",
+           "1 while a telemetry call of the GPU has been in flight longer than health.sampleStallS "
+           "(the GPU is then marked lost)"),
     Family("amdgpu_device_plugin_device_health", "gauge", ("resource", "device_id"), "exporter",
            "1 Healthy / 0 Unhealthy per advertised device"),
     Family("amdgpu_device_plugin_rpc_duration_seconds", "histogram", ("resource", "rpc"), "device_table",

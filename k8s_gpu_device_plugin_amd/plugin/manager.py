@@ -554,6 +554,7 @@ class PluginManager:
                 log.warning("no GPU event source armed (GPU reset / thermal events will not be received; "
                             "health falls back to telemetry polling): check access to /dev/kfd")
         if self.cfg.telemetry.enabled:
+            self.exporter.set_stall_ms(int(self.cfg.health.sampleStallS * 1000) if self.cfg.health.enabled else 0)
             self.exporter.start(self.backend, self.cfg.telemetry.intervalMs,
                                 self.monitor if self.cfg.health.enabled else None)
         self._publish_metrics()

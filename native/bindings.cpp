@@ -224,6 +224,7 @@ PYBIND11_MODULE(_native, m) {
       .def("set_ecc_uncorrectable", &FixtureBackend::set_ecc_uncorrectable)
       .def("set_retired_pages", &FixtureBackend::set_retired_pages, py::arg("gpu"), py::arg("reserved"),
            py::arg("pending") = 0)
+      .def("set_sample_stall", &FixtureBackend::set_sample_stall, py::call_guard<py::gil_scoped_release>())
       .def("set_gpu_present", &FixtureBackend::set_gpu_present)
       .def_property_readonly("discover_calls", &FixtureBackend::discover_calls);
 
@@ -427,6 +428,8 @@ PYBIND11_MODULE(_native, m) {
       }));
 
   py::class_<Exporter, std::shared_ptr<Exporter>>(m, "Exporter")
+      .def("set_stall_ms", &Exporter::set_stall_ms)
+      .def_property_readonly("stalled_gpu", &Exporter::stalled_gpu)
       .def(py::init<>())
       .def("set_inventory", &Exporter::set_inventory)
       .def("set_partition_labels", &Exporter::set_partition_labels)

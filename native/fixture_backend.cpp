@@ -51,8 +51,10 @@ void FixtureBackend::clear() {
   ecc_ue_.clear();
   pages_.clear();
   present_.clear();
+  stalled_.clear();
   scheduled_.clear();
   pending_.clear();
+  cv_.notify_all();  // a sample() parked on a stall returns (its GPU is gone)
 }
 
 void FixtureBackend::set_link(int a, int b, const Link& l) {
@@ -91,6 +93,16 @@ void FixtureBackend::set_retired_pages(int gpu, int64_t reserved, int64_t pendin
   pages_[gpu] = {reserved, pending};
 }
 
+void FixtureBackend::set_sample_stall(int gpu, bool stall) {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (gpu < 0 || gpu >= static_cast<int>(gpus_.size())) throw std::out_of_range("bad gpu");
+    if (stalled_.size() < gpus_.size()) stalled_.resize(gpus_.size(), false);
+    stalled_[gpu] = stall;
+  }
+  cv_.notify_all();
+}
+
 void FixtureBackend::set_gpu_present(int gpu, bool present) {
   std::lock_guard<std::mutex> lk(mu_);
   if (gpu < 0 || gpu >= static_cast<int>(present_.size())) throw std::out_of_range("bad gpu");
@@ -119,8 +131,10 @@ void FixtureBackend::discover(std::vector<GpuInfo>* gpus, Topology* topo) {
 }
 
 bool FixtureBackend::sample(int gpu, GpuSample* s) {
-  std::lock_guard<std::mutex> lk(mu_);
+  std::unique_lock<std::mutex> lk(mu_);
   if (gpu < 0 || gpu >= static_cast<int>(gpus_.size()) || !present_[gpu]) return false;
+  cv_.wait(lk, [&] { return shutdown_ || gpu >= static_cast<int>(stalled_.size()) || !stalled_[gpu]; });
+  if (gpu >= static_cast<int>(gpus_.size()) || !present_[gpu]) return false;
   const GpuInfo& g = gpus_[gpu];
   const int64_t t = now_ns();
   const double ts = (mono_ns() - t0_ns_) * 1e-9;  // seconds since the fixture was created

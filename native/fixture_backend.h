@@ -38,6 +38,9 @@ class FixtureBackend : public Backend {
   void set_ecc_uncorrectable(int gpu, int64_t count);
   void set_retired_pages(int gpu, int64_t reserved, int64_t pending);
   void set_gpu_present(int gpu, bool present);
+  // A wedged driver: sample(gpu) blocks until the stall is lifted (or shutdown), the way
+  // an amdsmi call can hang on a GPU that stopped responding.
+  void set_sample_stall(int gpu, bool stall);
   int discover_calls() const { return discover_calls_; }
 
  private:
@@ -54,6 +57,7 @@ class FixtureBackend : public Backend {
   std::vector<int64_t> ecc_ue_;
   std::vector<std::pair<int64_t, int64_t>> pages_;  // (reserved, pending) per GPU
   std::vector<bool> present_;
+  std::vector<bool> stalled_;
   int64_t armed_at_ns_ = 0;
   uint64_t seed_;
   int64_t t0_ns_;

@@ -140,6 +140,7 @@ void Exporter::start(std::shared_ptr<Backend> backend, int interval_ms, std::sha
   interval_ms_ = interval_ms > 0 ? interval_ms : 1000;
   stop_ = false;
   running_ = true;
+  if (monitor_) watchdog_ = std::thread([this] { watchdog_loop(); });  // before the first call
   sample_once();  // first sample synchronously: /metrics is populated before start() returns
   thread_ = std::thread([this] { loop(); });
 }
@@ -147,8 +148,27 @@ void Exporter::start(std::shared_ptr<Backend> backend, int interval_ms, std::sha
 void Exporter::stop() {
   if (!running_.load()) return;
   stop_ = true;
+  if (watchdog_.joinable()) watchdog_.join();
   if (thread_.joinable()) thread_.join();
   running_ = false;
+}
+
+void Exporter::watchdog_loop() {
+  while (!stop_.load()) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    const int ms = stall_ms_.load();
+    const int g = inflight_gpu_.load();  // then its start time: never older than g's call
+    const int64_t since = inflight_since_.load();
+    if (ms <= 0 || g < 0 || stalled_gpu_.load() == g) continue;
+    const int64_t age = mono_ns() - since;
+    if (age <= static_cast<int64_t>(ms) * 1000000) continue;
+    stalled_gpu_.store(g);
+    HwEvent e;
+    e.kind = kEvtDeviceLost;
+    e.gpu = g;
+    e.message = "telemetry call in flight for " + std::to_string(age / 1000000) + " ms (health.sampleStallS)";
+    monitor_->process(e);  // the GPU recovers through on_sample once the call returns ok
+  }
 }
 
 void Exporter::loop() {
@@ -183,7 +203,14 @@ void Exporter::sample_once() {
   std::vector<char> ok(n, 0);
   const int64_t t0 = mono_ns();
   for (size_t g = 0; g < n; ++g) {
-    if (be) ok[g] = be->sample(index[g], &samples[g]) ? 1 : 0;
+    if (be) {
+      inflight_since_.store(mono_ns());
+      inflight_gpu_.store(index[g]);
+      ok[g] = be->sample(index[g], &samples[g]) ? 1 : 0;
+      inflight_gpu_.store(-1);
+      int stuck = index[g];
+      stalled_gpu_.compare_exchange_strong(stuck, -1);
+    }
     if (!ok[g]) sample_errors_.fetch_add(1, std::memory_order_relaxed);
     if (monitor_) monitor_->on_sample(index[g], ok[g], samples[g]);
   }
@@ -192,6 +219,7 @@ void Exporter::sample_once() {
     sample_hist_.observe(dt);
     samples_.fetch_add(1, std::memory_order_relaxed);
   }
+  last_pass_ns_.store(mono_ns());
   render_gpu_text(samples, ok, gen);
 }
 
@@ -541,6 +569,20 @@ void Exporter::render_parts(std::string_view* head, std::string* counters, std::
   counters->append("amdgpu_telemetry_sample_errors_total ");
   append_u64(counters, sample_errors_.load());
   counters->push_back('\n');
+  if (const int64_t last = last_pass_ns_.load()) {
+    append_header(counters, "amdgpu_telemetry_last_pass_age_seconds",
+                  "Seconds since the sampler last completed a pass over all GPUs.", "gauge");
+    counters->append("amdgpu_telemetry_last_pass_age_seconds ");
+    append_float(counters, (mono_ns() - last) * 1e-9);
+    counters->push_back('\n');
+  }
+  if (const int stuck = stalled_gpu_.load(); stuck >= 0) {
+    append_header(counters, "amdgpu_telemetry_sample_stalled",
+                  "1 while a telemetry call of the GPU has been in flight longer than health.sampleStallS.", "gauge");
+    counters->append("amdgpu_telemetry_sample_stalled{gpu=\"");
+    append_u64(counters, static_cast<uint64_t>(stuck));
+    counters->append("\"} 1\n");
+  }
   if (sample_hist_.count()) {
     append_header(counters, "amdgpu_telemetry_sample_duration_seconds", "Wall time of one sampling pass over all GPUs.",
                   "histogram");

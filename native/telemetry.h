@@ -70,6 +70,11 @@ class Exporter {
   void start(std::shared_ptr<Backend> backend, int interval_ms, std::shared_ptr<HealthMonitor> monitor);
   void stop();
   bool running() const { return running_.load(); }
+  // Watchdog (health.sampleStallS): a backend call that has been in flight for longer
+  // than this marks its GPU lost in the health monitor.  A wedged driver never returns
+  // an error to count, so without it such a GPU would stay advertised Healthy.  0 = off.
+  void set_stall_ms(int ms) { stall_ms_.store(ms > 0 ? ms : 0); }
+  int stalled_gpu() const { return stalled_gpu_.load(); }
   // One synchronous sampling pass (also used before the first scrape).
   void sample_once();
 
@@ -157,6 +162,13 @@ class Exporter {
   std::atomic<uint64_t> samples_{0};
   std::atomic<uint64_t> sample_errors_{0};
   Histogram sample_hist_;
+  void watchdog_loop();
+  std::thread watchdog_;
+  std::atomic<int> stall_ms_{0};
+  std::atomic<int> inflight_gpu_{-1};       // GPU whose backend call is in flight, -1 = none
+  std::atomic<int64_t> inflight_since_{0};  // stored before inflight_gpu_
+  std::atomic<int> stalled_gpu_{-1};        // GPU the watchdog has reported lost
+  std::atomic<int64_t> last_pass_ns_{0};    // end of the last complete pass (mono ns)
   int64_t start_time_s_ = 0;
 
   // gzip members cached against the exact segment objects they were compressed from

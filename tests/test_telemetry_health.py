@@ -134,6 +134,45 @@ def test_disabled_checks_config(make_cfg):
         config.validate(config.from_dict({"health": {"disabledChecks": "ecc,xids"}}))
 
 
+def test_sampler_watchdog_marks_a_wedged_gpu_lost(n):
+    """A telemetry call that never returns (wedged driver) produces no error to count:
+    the watchdog marks that GPU lost once the call has been in flight for
+    health.sampleStallS, and the GPU recovers when the call comes back."""
+    be = fixtures.build_backend("2gpu_spx")
+    m = n.HealthMonitor(be, 3)
+    m.set_gpu_count(2)
+    ex = n.Exporter()
+    gpus, _ = be.discover()
+    ex.set_inventory(gpus)
+    ex.set_stall_ms(300)
+    ex.start(be, 20, m)
+    try:
+        assert "amdgpu_telemetry_last_pass_age_seconds " in ex.render()
+        be.set_sample_stall(1, True)
+        t0 = time.monotonic()
+        got = []
+        while time.monotonic() - t0 < 5 and not got:
+            got = [u for u in m.pop(100) if u.healthy == 0]
+        assert got and got[0].gpu == 1 and "in flight" in got[0].reason, got
+        assert time.monotonic() - t0 >= 0.25  # not before the threshold
+        assert ex.stalled_gpu == 1 and not m.gpu_healthy(1) and m.gpu_healthy(0)
+        text = ex.render()
+        assert 'amdgpu_telemetry_sample_stalled{gpu="1"} 1' in text
+        age = float([ln for ln in text.splitlines()
+                     if ln.startswith("amdgpu_telemetry_last_pass_age_seconds ")][0].split()[1])
+        assert age >= 0.25  # the pass never completed
+        be.set_sample_stall(1, False)
+        deadline = time.monotonic() + 5
+        back = []
+        while time.monotonic() < deadline and not back:
+            back = [u for u in m.pop(100) if u.healthy == 1]
+        assert back and back[0].gpu == 1 and m.gpu_healthy(1)
+        assert ex.stalled_gpu == -1 and "amdgpu_telemetry_sample_stalled" not in ex.render()
+    finally:
+        be.set_sample_stall(1, False)
+        ex.stop()
+
+
 def test_health_monitor_from_samples(n):
     be = fixtures.build_backend("2gpu_spx")
     m = n.HealthMonitor(be, 2)

@@ -92,7 +92,8 @@ def test_metrics_contract_both_ways(n):
     # per-partition VRAM needs real usage and the RAS page threshold needs root (or
     # health.badPageThreshold); everything else must be present on the fixture node
     assert missing <= {"amdgpu_partition_vram_used_bytes", "amdgpu_device_plugin_allocation_info",
-                       "amdgpu_device_plugin_pod_resources_up", "amdgpu_retired_pages_threshold"}, missing
+                       "amdgpu_device_plugin_pod_resources_up", "amdgpu_retired_pages_threshold",
+                       "amdgpu_telemetry_sample_stalled"}, missing
 
 
 def test_metrics_doc_is_generated_from_the_registry():
