@@ -359,7 +359,7 @@ void GrpcServer::start() {
     epoll_ctl(w->ep, EPOLL_CTL_ADD, w->done->efd, &ev3);
     workers_.push_back(std::move(w));
   }
-  for (auto& w : workers_) threads_.emplace_back([this, wp = w.get()] { run(wp); });
+  for (auto& w : workers_) threads_.emplace_back([this, wp = w.get(), t = table_] { run(wp, t); });
   std::lock_guard<std::mutex> nk(notifier_->mu);
   notifier_->srv = this;
 }
@@ -410,7 +410,7 @@ void GrpcServer::stop() {
   ::unlink(path_.c_str());
 }
 
-void GrpcServer::run(Worker* w) {
+void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
   std::vector<epoll_event> evs(128);
   char rbuf[32768];
   int spare = -1;  // reserve descriptor for accept_or_shed
@@ -420,11 +420,6 @@ void GrpcServer::run(Worker* w) {
       if (*fd >= 0) ::close(*fd);
     }
   } spare_closer{&spare};
-  std::shared_ptr<DeviceTable> table;
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    table = table_;
-  }
   auto close_conn = [&](int fd) {
     epoll_ctl(w->ep, EPOLL_CTL_DEL, fd, nullptr);
     ::close(fd);

@@ -63,7 +63,9 @@ class GrpcServer {
       if (srv) srv->notify();
     }
   };
-  void run(Worker* w);
+  // `table` is handed over at thread creation: a worker never takes mu_, which stop()
+  // holds while it joins the workers (one not yet scheduled when stop() ran deadlocked)
+  void run(Worker* w, std::shared_ptr<DeviceTable> table);
   std::shared_ptr<Notifier> notifier_ = std::make_shared<Notifier>();
   std::string path_;
   int nthreads_;

@@ -180,6 +180,21 @@ def test_oversized_frame_is_rejected(server):
     s.close()
 
 
+def test_stop_right_after_start(n, plugin_dir):
+    """stop() held the server lock while joining the workers, and a worker that had not
+    run yet took that lock first thing: stop() right after start() deadlocked (seen as a
+    rare hang of a fixture teardown on a loaded machine)."""
+    tc = n.TableConfig()
+    table = n.DeviceTable(tc, [n.TableDevice("dev-000", 0)], n.Topology(1))
+    path = os.path.join(plugin_dir, "amd-gpu.sock")
+    for _ in range(100):
+        srv = n.GrpcServer(path, 8)
+        srv.set_table(table)
+        srv.start()
+        srv.stop()
+        assert not srv.running
+
+
 def test_many_connections_and_threads(n, server):
     srv, table, path = server
     req = v1beta1.AllocateRequest(container_requests=[v1beta1.ContainerAllocateRequest(
