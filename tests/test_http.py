@@ -96,17 +96,21 @@ def test_metrics_gzip_negotiation(web):
     import gzip
     port, _, kind = web
     get(port, "/health")  # so the echo_http families exist in every scrape below
-    st, h, plain = get(port, "/metrics")
-    assert "Content-Encoding" not in h
+    volatile = ("echo_http", "process_", "amdgpu_telemetry_last_pass_age")  # change between two scrapes
+    strip = lambda t: [ln for ln in t.splitlines() if not ln.startswith(volatile)]  # noqa: E731
+    ticks = lambda t: [ln for ln in t.splitlines() if ln.startswith("amdgpu_telemetry_samples_total ")]  # noqa: E731
     for ae in ("gzip", "deflate, gzip;q=1.0", "br,gzip"):
-        st, h, body = get(port, "/metrics", headers={"Accept-Encoding": ae})
-        assert st == 200 and h["Content-Encoding"] == "gzip", (ae, h)
-        text = gzip.decompress(body).decode()
+        for _ in range(20):  # a plain and a gzip scrape within one sampling tick
+            st, h, plain = get(port, "/metrics")
+            assert "Content-Encoding" not in h
+            st, h, body = get(port, "/metrics", headers={"Accept-Encoding": ae})
+            assert st == 200 and h["Content-Encoding"] == "gzip", (ae, h)
+            text = gzip.decompress(body).decode()
+            if ticks(text) == ticks(plain.decode()):
+                break
         fams = {f.name for f in text_string_to_metric_families(text)}
         assert fams == {f.name for f in text_string_to_metric_families(plain.decode())}
         # everything but the per-request counters is identical
-        volatile = ("echo_http", "process_", "amdgpu_telemetry_last_pass_age")  # change between two scrapes
-        strip = lambda t: [ln for ln in t.splitlines() if not ln.startswith(volatile)]  # noqa: E731
         assert strip(text) == strip(plain.decode())
         assert len(body) < len(plain) / 3
     st, h, body = get(port, "/metrics", headers={"Accept-Encoding": "identity, gzipx"})
