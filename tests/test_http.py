@@ -326,3 +326,16 @@ def test_connection_churn_across_workers_leaves_nothing_behind(make_cfg):
         assert len(os.listdir("/proc/self/fd")) <= fds0 + 4 + 2  # + one reserve descriptor per worker
     finally:
         w.stop()
+
+
+def test_native_http_stop_right_after_start(n):
+    """Counterpart of the gRPC server's stop-after-start case: workers that have not run
+    yet when stop() comes must still leave (no lock held across the join)."""
+    ex = n.Exporter()
+    for _ in range(50):
+        cfg = n.HttpConfig()
+        cfg.host, cfg.port, cfg.threads, cfg.access_log = "127.0.0.1", 0, 8, False
+        srv = n.HttpServer(cfg, ex)
+        srv.start()
+        srv.stop()
+        assert not srv.running

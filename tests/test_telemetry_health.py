@@ -311,3 +311,22 @@ def test_native_sampling_profiler_sees_native_threads(n):
     assert sum(c for _, _, c in rows) >= 20
     text = " ".join(fn for fn, _, _ in rows)
     assert any(k in text for k in ("send", "recv", "epoll_wait", "uds_pingpong")), rows[:10]
+
+
+def test_exporter_and_monitor_stop_right_after_start(n):
+    """Sampler, watchdog and monitor threads that have not run yet when stop() comes
+    still leave promptly."""
+    be = fixtures.build_backend("2gpu_spx")
+    gpus, _ = be.discover()
+    t0 = time.monotonic()
+    for _ in range(10):
+        m = n.HealthMonitor(be, 3)
+        m.set_gpu_count(2)
+        m.start()
+        ex = n.Exporter()
+        ex.set_inventory(gpus)
+        ex.set_stall_ms(1000)
+        ex.start(be, 20, m)
+        ex.stop()
+        m.stop()
+    assert time.monotonic() - t0 < 15
