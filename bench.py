@@ -21,8 +21,11 @@ is better; kubelet is a compiled grpc-go client, and a Python client's own ~80 u
 call would hide the plugin); the grpcio-client p50/p99 are reported alongside;
 ``scrape_rps`` = all ranks' completed scrapes / the slowest rank's scrape window (the
 ranks scrape concurrently, so this is the daemon's aggregate throughput).  Before timing,
-each rank validates its allocation: the returned render node exists and the gfx950
-canary (HBM pattern + MFMA exactness/throughput) passes on that device.
+each rank validates its GPU and its allocation: the gfx950 canary (HBM pattern + MFMA
+exactness/throughput) passes on the rank's device, in a child process that exits before
+the rank loads torch or joins the RCCL group, and the returned render node exists.  The
+run fails unless WORLD_SIZE == --gpus == the number of devices the daemon advertised
+(one kubelet-client rank per advertised GPU; rank r allocates device r).
 
 Speed-of-light references, measured untimed in the same run: ``uds_roundtrip_floor_p50_us``
 (the same unix-socket exchange between two threads, no protocol work, sleeping server
@@ -88,9 +91,59 @@ def _wait_http(port: int, timeout: float) -> None:
     raise TimeoutError("plugin web server did not come up on port %d" % port)
 
 
+def _tail_stats(batches) -> dict:
+    """Attribution of this rank's slow Allocates (> 2x the rank's p50): the first call of
+    a batch (it follows the previous step's scrape phase, so it meets a server worker
+    whose busy-poll window has closed), a call that ran on another CPU than the call
+    before it (the client thread migrated), or neither (an interrupt, timer tick or
+    another tenant's thread on the client's or the server's CPU)."""
+    lat = [x for _, l, _ in batches for x in l]
+    if not lat:
+        return {"calls": 0}
+    thr = 2 * _pct(lat, 0.5)
+    slow = first = migrated = 0
+    for starts, l, cpus in batches:
+        for i, x in enumerate(l):
+            if x <= thr:
+                continue
+            slow += 1
+            if i == 0:
+                first += 1
+            elif cpus[i] != cpus[i - 1]:
+                migrated += 1
+    return {"calls": len(lat), "slow": slow, "first_of_batch": first, "cpu_migrated": migrated,
+            "threshold_us": round(thr * 1e6, 2)}
+
+
+def _merge_tail(parts) -> dict:
+    out = {"calls": 0, "slow": 0, "first_of_batch": 0, "cpu_migrated": 0}
+    for p in parts:
+        for k in out:
+            out[k] += p.get(k, 0)
+    out["other"] = out["slow"] - out["first_of_batch"] - out["cpu_migrated"]
+    out["slow_fraction"] = round(out["slow"] / max(1, out["calls"]), 4)
+    return out
+
+
+def _allocator_probe(n) -> float:
+    """The xGMI allocator's own cost for a size-4 request over an 8-GPU mesh (two NUMA
+    nodes), timed natively.  On a 1-GPU box the kubelet GetPreferredAllocation above
+    can only return its one device, so this is what says what the policy costs."""
+    topo = n.Topology(8)
+    for a in range(8):
+        for b in range(a + 1, 8):
+            topo.set_link(a, b, n.Link(type=n.LINK_XGMI, hops=1, up=True))
+    devs = [n.AllocDevice(g, -1, g // 4, "gpu%d" % g) for g in range(8)]
+    lat = n.bench_aligned_alloc(topo, devs, list(range(8)), [1], 4, 2000)
+    return round(_pct(lat[200:], 0.5) * 1e6, 2)
+
+
 def start_daemon(n_gpus: int, grpc_server: str, workdir: str, profile_dir: str = "", busy_poll_us=None,
-                 admission_poll_us=None):
-    """Rank 0: kubelet stub + plugin daemon subprocess.  Must run before GPU init."""
+                 admission_poll_us=None, overrides=None):
+    """Rank 0: kubelet stub + plugin daemon subprocess.  Must run before GPU init.
+    ``overrides``: config sections merged over the bench's own (probes, A/B runs)."""
+    import yaml
+
     from k8s_gpu_device_plugin_amd import native
     from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import KubeletStub
 
@@ -103,18 +156,26 @@ def start_daemon(n_gpus: int, grpc_server: str, workdir: str, profile_dir: str =
     cfg_path = os.path.join(workdir, "bench-config.yml")
     # one server worker per client connection: every rank holds two kubelet-side
     # connections (compiled h2 + grpcio) and SCRAPE_CONNS scrapers
-    grpc_threads = max(4, 2 * n_gpus)
-    http_threads = max(4, SCRAPE_CONNS * n_gpus)
-    bp = "" if busy_poll_us is None else "  busyPollUs: %d\n" % busy_poll_us
-    ap = "" if admission_poll_us is None else "  admissionPollUs: %d\n" % admission_poll_us
+    cfg = {"webListenAddress": "127.0.0.1:%d" % port, "migStrategy": "none", "backend": backend,
+           "fixture": "%dgpu_spx" % n_gpus, "devices": "0-%d" % (n_gpus - 1), "pluginDir": plugin_dir,
+           "log": {"level": "info", "fileDir": ""},
+           "http": {"accessLog": False, "threads": max(4, SCRAPE_CONNS * n_gpus)},
+           "telemetry": {"intervalMs": 1000},
+           "grpc": {"server": grpc_server, "threads": max(4, 2 * n_gpus)}}
+    if busy_poll_us is not None:
+        cfg["http"]["busyPollUs"] = cfg["grpc"]["busyPollUs"] = busy_poll_us
+    if admission_poll_us is not None:
+        cfg["grpc"]["admissionPollUs"] = admission_poll_us
+    if profile_dir:  # benchmark: true -> cpu/mem/threads/native profiles when the daemon exits
+        cfg["benchmark"] = True
+        cfg["benchmarkDir"] = os.path.abspath(profile_dir)
+    for k, v in (overrides or {}).items():
+        if isinstance(v, dict) and isinstance(cfg.get(k), dict):
+            cfg[k] = {**cfg[k], **v}
+        else:
+            cfg[k] = v
     with open(cfg_path, "w") as f:
-        f.write("webListenAddress: \"127.0.0.1:%d\"\nmigStrategy: none\nbackend: %s\nfixture: %dgpu_spx\n"
-                "devices: \"0-%d\"\npluginDir: \"%s\"\nlog:\n  level: info\n  fileDir: \"\"\n"
-                "http:\n  accessLog: false\n  threads: %d\n%stelemetry:\n  intervalMs: 1000\n"
-                "grpc:\n  server: %s\n  threads: %d\n%s%s"
-                % (port, backend, n_gpus, n_gpus - 1, plugin_dir, http_threads, bp, grpc_server, grpc_threads, bp, ap))
-        if profile_dir:  # benchmark: true -> cpu/mem/threads/native profiles when the daemon exits
-            f.write("benchmark: true\nbenchmarkDir: \"%s\"\n" % os.path.abspath(profile_dir))
+        yaml.safe_dump(cfg, f)
     env = dict(os.environ)
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
     log = open(os.path.join(workdir, "daemon.log"), "w")
@@ -143,8 +204,11 @@ def main() -> int:
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     n_gpus = args.gpus
-    if world > 1 and world != n_gpus:
-        print("warning: WORLD_SIZE=%d != --gpus %d" % (world, n_gpus), file=sys.stderr)
+    if world != n_gpus:
+        # one kubelet-client rank per advertised GPU (weak scaling): anything else would
+        # report n_gpus for a run that did not have that many ranks or devices
+        raise SystemExit("bench.py: WORLD_SIZE=%d but --gpus %d; launch one rank per GPU "
+                         "(torch.distributed.run --nproc-per-node %d)" % (world, n_gpus, n_gpus))
 
     from k8s_gpu_device_plugin_amd import native
     n = native.load()
@@ -162,6 +226,16 @@ def main() -> int:
                                                          args.busy_poll_us, args.admission_poll_us)
         info = {"port": port, "endpoint": reg.endpoint, "resource": reg.resource_name, "backend": backend,
                 "plugin_dir": os.path.join(workdir, "device-plugins")}
+
+    # Validate this rank's GPU with the gfx950 canary (HBM pattern + MFMA exactness and
+    # rate) in a child process, before this process loads torch or initialises RCCL: each
+    # rank then holds exactly one HIP runtime (torch's) when the communicator comes up.
+    canary_res = None
+    if not args.no_canary and n.amdsmi_available():
+        from k8s_gpu_device_plugin_amd.ops import canary
+        canary_res = canary.run_isolated(local_rank, hbm_bytes=1 << 30, timeout=300.0, passes=3)
+        if not canary_res.get("ok"):
+            raise RuntimeError("canary failed on rank %d (GPU %d): %s" % (rank, local_rank, canary_res))
 
     import torch
     import torch.distributed as dist
@@ -192,7 +266,10 @@ def main() -> int:
     first = next(iter(law))
     law.cancel()
     ids = [d.ID for d in first.devices]
-    my_id = ids[rank % len(ids)]
+    if len(ids) != n_gpus:
+        raise RuntimeError("the plugin advertised %d device(s) of %s, --gpus is %d" % (len(ids), info["resource"],
+                                                                                     n_gpus))
+    my_id = ids[rank]
     alloc_req = v1beta1.AllocateRequest(container_requests=[
         v1beta1.ContainerAllocateRequest(devices_ids=[my_id])]).SerializeToString()
     pref_req = v1beta1.PreferredAllocationRequest(container_requests=[
@@ -204,16 +281,10 @@ def main() -> int:
     # ---- validate the allocation on the real device (untimed) ----
     resp = v1beta1.AllocateResponse.FromString(alloc_raw(alloc_req))
     specs = [s.host_path for s in resp.container_responses[0].devices]
-    canary_res = None
     if info["backend"] == "amdsmi":
         missing = [p for p in specs if not os.path.exists(p)]
         if missing:
             raise RuntimeError("allocated device nodes missing: %s" % missing)
-    if use_cuda and not args.no_canary:
-        from k8s_gpu_device_plugin_amd.ops import canary
-        canary_res = canary.run(torch.cuda.current_device(), hbm_bytes=1 << 30, passes=3, mfma_iters=8192)
-        if not canary_res["ok"]:
-            raise RuntimeError("canary failed on rank %d: %s" % (rank, canary_res))
 
     conn = http.client.HTTPConnection("127.0.0.1", info["port"], timeout=10)
     perf = time.perf_counter
@@ -226,9 +297,11 @@ def main() -> int:
             dist.barrier()
 
     def step(rec):
-        a, p, s, an, pn = rec
+        a, p, s, an, pn, tl = rec
         phase_sync()
-        an.extend(h2.bench_unary(v1beta1.METHOD_ALLOCATE, alloc_req, ALLOCS))
+        starts, lat, cpus = h2.bench_unary_ts(v1beta1.METHOD_ALLOCATE, alloc_req, ALLOCS)
+        an.extend(lat)
+        tl.append((starts, lat, cpus))
         pn.extend(h2.bench_unary(v1beta1.METHOD_GET_PREFERRED, pref_req, PREFS))
         for _ in range(ALLOCS):
             t0 = perf()
@@ -249,11 +322,11 @@ def main() -> int:
     body = conn.getresponse().read()
     if b"amdgpu_info{" not in body:
         raise RuntimeError("/metrics lacks the GPU inventory")
-    junk = ([], [], [], [], [])
+    junk = ([], [], [], [], [], [])
     for _ in range(args.warmup):
         step(junk)
     barrier()
-    rec = ([], [], [], [], [])
+    rec = ([], [], [], [], [], [])
     scrape_time, body_len = 0.0, len(body)
     t_start = perf()
     for _ in range(args.steps):
@@ -262,7 +335,7 @@ def main() -> int:
     barrier()
     elapsed = perf() - t_start
     mine = {"elapsed": elapsed, "scrape_time": scrape_time, "alloc": rec[0], "pref": rec[1], "scrape": rec[2],
-            "alloc_native": rec[3], "pref_native": rec[4],
+            "alloc_native": rec[3], "pref_native": rec[4], "alloc_tail": _tail_stats(rec[5]),
             "canary": canary_res, "body": body_len}
     # Untimed speed-of-light reference: the same send/epoll_wait/recv/send/recv exchange
     # between two threads with no HTTP/2, HPACK or protobuf work (sizes ~ this Allocate's).
@@ -270,8 +343,14 @@ def main() -> int:
     sizes = (9 + 80 + 9 + 5 + len(alloc_req), 9 + 20 + 9 + 5 + alloc_resp_len + 9 + 16)
     floor = n.uds_pingpong(10000, 500, *sizes)
     mine["uds_floor_p50"] = _pct(floor, 0.5)
-    # ... and with a server thread that polls instead of sleeping (the busy-poll window)
-    mine["uds_floor_spin_p50"] = _pct(n.uds_pingpong(10000, 500, *sizes, server_spin=True), 0.5)
+    # ... and with a server thread that polls instead of sleeping (the busy-poll window);
+    # its p99 is this machine's tail for a bare back-to-back exchange (timer ticks,
+    # interrupts and other tenants land on either thread's CPU), the floor Allocate's p99
+    # is compared against
+    spin = n.uds_pingpong(10000, 500, *sizes, server_spin=True)
+    mine["uds_floor_spin_p50"] = _pct(spin, 0.5)
+    mine["uds_floor_spin_p99"] = _pct(spin, 0.99)
+    mine["uds_floor_spin_p999"] = _pct(spin, 0.999)
     # kubelet-like sparse calls: 1 ms apart, every one meets a sleeping server thread
     mine["alloc_cold"] = h2.bench_unary(v1beta1.METHOD_ALLOCATE, alloc_req, 400, 1000)
     # ... and the bare exchange with the same 1 ms idle gap (cold caches, idle CPU states)
@@ -320,6 +399,14 @@ def main() -> int:
                        "parallelism": "%d kubelet-client rank(s), 1 plugin daemon" % world,
                        "backend": info["backend"], "grpc_server": args.grpc_server},
             "allocate_p50_us": round(p50, 2), "allocate_p99_us": round(_pct(allocs_native, 0.99) * 1e6, 2),
+            "allocate_p999_us": round(_pct(allocs_native, 0.999) * 1e6, 2),
+            "allocate_max_us": round(max(allocs_native) * 1e6, 2),
+            "allocate_tail": _merge_tail([g["alloc_tail"] for g in gathered]),
+            "uds_roundtrip_floor_spin_p99_us": round(gathered[0]["uds_floor_spin_p99"] * 1e6, 2),
+            "uds_roundtrip_floor_spin_p999_us": round(gathered[0]["uds_floor_spin_p999"] * 1e6, 2),
+            "preferred_allocator_8gpu_size4_p50_us": _allocator_probe(n),
+            "advertised_devices": len(ids), "world_size": world,
+            "dist_backend": (dist.get_backend() if world > 1 else None),
             "uds_roundtrip_floor_p50_us": round(gathered[0]["uds_floor_p50"] * 1e6, 2),
             "uds_roundtrip_floor_spin_p50_us": round(gathered[0]["uds_floor_spin_p50"] * 1e6, 2),
             "uds_roundtrip_floor_cold_p50_us": round(gathered[0]["uds_floor_cold_p50"] * 1e6, 2),

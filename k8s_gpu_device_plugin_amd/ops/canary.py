@@ -248,9 +248,10 @@ def gemm_rate(device: int = 0, m: int = 4096, n: int = 4096, k: int = 4096, iter
             "kernel": kernel, "data": "random" if random_data else "integer"}
 
 
-def run_isolated(device: int, hbm_bytes: int = 256 << 20, timeout: float = 120.0) -> dict:
+def run_isolated(device: int, hbm_bytes: int = 256 << 20, timeout: float = 120.0, passes: int = 1) -> dict:
+    """``run`` in a child process (its own HIP runtime, gone when it exits)."""
     cmd = [sys.executable, "-m", "k8s_gpu_device_plugin_amd.ops.canary", "--device", str(device),
-           "--bytes", str(hbm_bytes), "--passes", "1"]
+           "--bytes", str(hbm_bytes), "--passes", str(passes)]
     env = dict(os.environ)
     root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")

@@ -842,7 +842,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
       n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), 0);
       if (n == 0) {
         if (mono_ns() >= spin_until) spin_until = 0;
-        else __builtin_ia32_pause();
+        else cpu_relax();
         continue;
       }
     } else {

@@ -346,7 +346,7 @@ int HttpServer::start() {
         const int64_t now = mono_ns();
         if (spin_until) {
           if (n == 0 && now < spin_until) {
-            __builtin_ia32_pause();
+            cpu_relax();
             continue;
           }
           if (n == 0) spin_until = 0;

@@ -255,7 +255,7 @@ std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_byte
     for (;;) {
       // server_spin: the busy-poll worker (grpc.busyPollUs) never sleeps between requests
       const int k = epoll_wait(ep, evs, 4, server_spin ? 0 : 1000);
-      if (k == 0 && server_spin) __builtin_ia32_pause();
+      if (k == 0 && server_spin) cpu_relax();
       if (k < 0 && errno != EINTR) return;
       if (k <= 0) continue;
       bool closed = false;

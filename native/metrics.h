@@ -73,6 +73,18 @@ inline void append_header(std::string* out, const char* name, const char* help, 
       .append(type).append("\n");
 }
 
+// Spin-wait hint for busy-poll loops and spin locks (x86 PAUSE; a yield hint or a
+// compiler barrier elsewhere, so the native core still builds on non-x86 hosts).
+inline void cpu_relax() {
+#if defined(__x86_64__) || defined(__i386__)
+  __builtin_ia32_pause();
+#elif defined(__aarch64__) || defined(__arm__)
+  __asm__ __volatile__("yield" ::: "memory");
+#else
+  __asm__ __volatile__("" ::: "memory");
+#endif
+}
+
 // Guards pointer-sized critical sections on the scrape path (copying or swapping a
 // shared_ptr to a cached text).  A contended std::mutex parks the thread in futex_wait,
 // and the wake-up costs more than the whole critical section: with 4 concurrent
@@ -81,7 +93,7 @@ class SpinLock {
  public:
   void lock() {
     while (f_.exchange(true, std::memory_order_acquire))
-      while (f_.load(std::memory_order_relaxed)) __builtin_ia32_pause();
+      while (f_.load(std::memory_order_relaxed)) cpu_relax();
   }
   void unlock() { f_.store(false, std::memory_order_release); }
 

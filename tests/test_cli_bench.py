@@ -121,3 +121,26 @@ def test_bench_two_ranks_gloo():
     r = _run_bench(["--gpus", "2", "--steps", "2", "--warmup", "1"], nproc=2)
     _check_contract(r, 2, 2, 1)
     assert r["config"]["global_batch"] == 2 * 256
+
+
+def test_bench_refuses_rank_gpu_mismatch():
+    """--gpus must equal WORLD_SIZE (one kubelet-client rank per advertised GPU): a run
+    that would report n_gpus it did not have fails before it starts a daemon."""
+    env = _env()
+    env.pop("RANK", None)
+    env["WORLD_SIZE"] = "1"
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"], env=env,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=120)
+    assert p.returncode != 0
+    assert "WORLD_SIZE=1 but --gpus 2" in p.stderr
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bench_reports_advertised_devices_and_tail():
+    r = _run_bench(["--steps", "2", "--warmup", "1"])
+    assert r["advertised_devices"] == 1 and r["world_size"] == 1
+    t = r["allocate_tail"]
+    assert t["calls"] == 2 * 256 and t["slow"] == t["first_of_batch"] + t["cpu_migrated"] + t["other"]
+    assert r["allocate_p999_us"] >= r["allocate_p99_us"] >= r["allocate_p50_us"]
+    assert 0 < r["preferred_allocator_8gpu_size4_p50_us"] < 1000
+    assert r["uds_roundtrip_floor_spin_p99_us"] >= r["uds_roundtrip_floor_spin_p50_us"]
