@@ -192,6 +192,61 @@ def _churn(policy, n_gpu=8, steps=400, seed=7, degraded=()):
             "placements": stats["placed"]}
 
 
+def _churn_cpx(link_aware: bool, n_gpu=8, parts=8, steps=400, seed=11):
+    """CPX node (8 GPUs x 8 partitions): pods of 1..16 partitions arrive and leave.  For
+    each multi-GPU pod placed, counts the GPU pairs it spans that another live
+    multi-GPU pod already spans: both drive RCCL traffic over that one xGMI link.
+    ``link_aware``: the allocator sees the live pods' link load (what the plugin feeds it
+    from kubelet PodResources); otherwise the same allocator without it (round-2 policy)."""
+    nat = native.load()
+    devs = [nat.AllocDevice(g, p, g // 4, "g%dp%d" % (g, p)) for g in range(n_gpu) for p in range(parts)]
+    rng = random.Random(seed)
+    free = set(range(len(devs)))
+    pods = []  # (device indices, set of GPUs)
+    st = {"placed": 0, "multi": 0, "pairs": 0, "shared_pairs": 0, "pods_sharing": 0, "rejected": 0}
+
+    def topology():
+        load = {}
+        if link_aware:
+            for _, gs in pods:
+                for a, b in itertools.combinations(sorted(gs), 2):
+                    load[(a, b)] = load.get((a, b), 0) + 1
+        t = nat.Topology(n_gpu)
+        for a in range(n_gpu):
+            for b in range(a + 1, n_gpu):
+                t.set_link(a, b, nat.Link(type=nat.LINK_XGMI, hops=1, bw_gbps=608.0, pods=load.get((a, b), 0)))
+        return t
+
+    for _ in range(steps):
+        if pods and (rng.random() < 0.45 or not free):
+            chosen, _ = pods.pop(rng.randrange(len(pods)))
+            free |= set(chosen)
+            continue
+        size = rng.choice([1, 2, 4, 4, 8, 12, 16])
+        if size > len(free):
+            st["rejected"] += 1
+            continue
+        chosen = nat.aligned_alloc(topology(), devs, sorted(free), [], size)
+        gs = {devs[i].gpu for i in chosen}
+        st["placed"] += 1
+        if len(gs) > 1:
+            live = set()
+            for _, other in pods:
+                if len(other) > 1:
+                    live |= set(itertools.combinations(sorted(other), 2))
+            mine = set(itertools.combinations(sorted(gs), 2))
+            st["multi"] += 1
+            st["pairs"] += len(mine)
+            st["shared_pairs"] += len(mine & live)
+            st["pods_sharing"] += bool(mine & live)
+        free -= set(chosen)
+        pods.append((chosen, gs))
+    m = max(1, st["multi"])
+    return {"placements": st["placed"], "multi_gpu_pods": st["multi"], "gpu_pairs_spanned": st["pairs"],
+            "shared_link_pairs": st["shared_pairs"], "multi_gpu_pods_sharing_a_link": round(st["pods_sharing"] / m, 3),
+            "rejected": st["rejected"]}
+
+
 def config3():
     node = Node("fixture", "8gpu_spx_mesh")
     try:
@@ -205,6 +260,10 @@ def config3():
         deg = ((0, 5), (2, 3), (1, 2))
         out["placement_degraded_links"] = {"down": [list(d) for d in deg], "xgmi_policy": _churn("xgmi", degraded=deg),
                                            "first_fit": _churn("first", degraded=deg)}
+        out["placement_cpx_link_sharing"] = {
+            "protocol": "8x8 CPX partitions, 400 arrivals/departures, pods of 1-16 partitions, 3 seeds",
+            "pod_link_load_aware": [_churn_cpx(True, seed=s) for s in (11, 12, 13)],
+            "without_link_load": [_churn_cpx(False, seed=s) for s in (11, 12, 13)]}
         return out
     finally:
         node.close()

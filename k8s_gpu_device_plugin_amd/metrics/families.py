@@ -105,6 +105,8 @@ FAMILIES = (
            "manager", "Advertised device held by a container (value 1)"),
     Family("amdgpu_device_plugin_pod_resources_up", "gauge", (), "manager",
            "Last kubelet PodResources List succeeded"),
+    Family("amdgpu_xgmi_link_pods", "gauge", ("gpu", "peer"), "manager",
+           "Multi-GPU pods whose devices span the GPU pair, sharing its xGMI link (the allocator steers new pods off it)"),
 )
 
 BY_NAME = {f.name: f for f in FAMILIES}

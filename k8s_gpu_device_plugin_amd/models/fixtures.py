@@ -43,12 +43,14 @@ def fixture_uuid(seed: int, gpu: int) -> str:
 
 
 def mi355x_node(num_gpus: int = 8, compute: str = "SPX", memory: str = "NPS1", gpus_per_numa: int = 4,
-                nps_caps=("NPS1", "NPS2"), down_links=(), seed: int = 1, events=()) -> dict:
+                nps_caps=("NPS1", "NPS2"), down_links=(), seed: int = 1, events=(), slow_links=()) -> dict:
+    """slow_links: [(a, b, gbps)] links that trained below the nominal 608 Gb/s."""
     gpus = []
     for g in range(num_gpus):
         gpus.append({"compute_partition": compute, "memory_partition": memory,
                      "numa_node": g // max(1, gpus_per_numa), "nps_caps": list(nps_caps)})
-    return {"gpus": gpus, "links": {"type": "xgmi", "down": [list(p) for p in down_links]},
+    return {"gpus": gpus, "links": {"type": "xgmi", "down": [list(p) for p in down_links],
+                                    "slow": [list(p) for p in slow_links]},
             "events": list(events), "seed": seed}
 
 
@@ -62,7 +64,10 @@ BUILTIN = {
     "8gpu_cpx_nps2": lambda: mi355x_node(8, "CPX", "NPS2"),
     "8gpu_cpx_nps4": lambda: mi355x_node(8, "CPX", "NPS4", nps_caps=("NPS1", "NPS2", "NPS4")),
     "8gpu_spx_degraded": lambda: mi355x_node(8, down_links=[(0, 5), (2, 3)]),
+    # one xGMI link trained at half rate (x8 instead of x16): up, but half the bandwidth
+    "8gpu_spx_halfrate": lambda: mi355x_node(8, slow_links=[(0, 1, 304.0)]),
 }
+XGMI_LINK_GBPS = 608.0  # MI355X: 16 lanes x 38 Gb/s per xGMI link (what amdsmi reports)
 
 
 def load_model(spec) -> dict:
@@ -152,10 +157,12 @@ def build_backend(spec):
     links = model.get("links", {}) or {}
     ltype = {"xgmi": n.LINK_XGMI, "pcie": n.LINK_PCIE}.get(str(links.get("type", "xgmi")).lower(), n.LINK_XGMI)
     down = {tuple(sorted(p)) for p in links.get("down", [])}
+    slow = {tuple(sorted(p[:2])): float(p[2]) for p in links.get("slow", [])}
     for a in range(len(gpus)):
         for b in range(a + 1, len(gpus)):
-            be.set_link(a, b, n.Link(type=ltype, hops=1, weight=15 if ltype == n.LINK_XGMI else 40,
-                                     up=(a, b) not in down, p2p=True))
+            xgmi = ltype == n.LINK_XGMI
+            be.set_link(a, b, n.Link(type=ltype, hops=1, weight=15 if xgmi else 40, up=(a, b) not in down, p2p=True,
+                                     bw_gbps=slow.get((a, b), XGMI_LINK_GBPS) if xgmi else 0.0))
     for ev in model.get("events", []) or []:
         kind = getattr(n, EVENT_KINDS[str(ev["kind"]).lower()])
         be.schedule_event(float(ev.get("at", 0.0)),

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import collections
 import concurrent.futures
+import itertools
 import os
 import platform
 import queue
@@ -85,18 +86,25 @@ class PluginManager:
                          "load_failures": 0, "health_events": 0}
         # (t, gpu, healthy, reason); bounded so a flapping GPU cannot grow it forever
         self.health_log: "collections.deque[tuple[float, int, int, str]]" = collections.deque(maxlen=HEALTH_LOG_LEN)
+        # Health state the manager keeps is keyed by GPU identity (Backend.gpu_key: UUID,
+        # else BDF), never by index: when a GPU falls off the bus, re-discovery moves
+        # every later GPU down one index, and their health must not move with it.
+        self._key_of: dict[int, str] = {}   # advertised GPU index -> identity
+        self._index_of: dict[str, int] = {}  # identity -> advertised GPU index
         # Recovery canaries run off the manager thread; a per-GPU generation drops a
         # verdict that an Unhealthy event overtook while the canary was running.
-        self._health_gen: dict[int, int] = {}
+        self._health_gen: dict[str, int] = {}
         # GPUs the manager holds Unhealthy although the monitor reports them healthy:
         # recovery canary pending or failed.  Survives plugin reloads.
-        self._held_unhealthy: set[int] = set()
-        # (gpu, partition) whose PreStartContainer canary failed.  Re-applied by every
-        # reload (a /restart or kubelet restart must not re-advertise them Healthy) until
-        # the GPU reports healthy again or a start-up canary re-checks it.
-        self._canary_failed: set[tuple[int, int]] = set()
+        self._held_unhealthy: set[str] = set()
+        # (gpu identity, partition) whose PreStartContainer canary failed.  Re-applied by
+        # every reload (a /restart or kubelet restart must not re-advertise them Healthy)
+        # until the GPU reports healthy again or a start-up canary re-checks it.
+        self._canary_failed: set[tuple[str, int]] = set()
         self._verify_pool: concurrent.futures.ThreadPoolExecutor | None = None
         self.podres = None  # PodResourcesWatcher when podResources.enabled
+        self.link_pods: dict[tuple[int, int], int] = {}  # GPU pair -> multi-GPU pods spanning it
+        self.multi_gpu_pods = 0
         # GPUs with hardware event notification armed (read when the monitor starts and
         # after each re-discovery, which can re-initialise amdsmi); None = not monitoring
         self._event_sources: int | None = None
@@ -181,11 +189,13 @@ class PluginManager:
                     self._apply_health(ev[1])
                 elif kind == EV_VERIFIED:
                     self._apply_verified(*ev[1:])
-                elif kind in (EV_PODRES, EV_METRICS):
-                    pass  # allocation map / canary results changed: _publish_metrics below re-renders
+                elif kind == EV_PODRES:
+                    self._push_link_pods()  # and _publish_metrics below re-renders the allocation map
+                elif kind == EV_METRICS:
+                    pass  # canary results changed: _publish_metrics below re-renders
                 elif kind == EV_PRESTART_FAIL:
                     self.counters["prestart_failures"] = self.counters.get("prestart_failures", 0) + 1
-                    self._canary_failed.add((ev[1], ev[2]))
+                    self._canary_failed.add((ev[1], ev[2]))  # (identity, partition)
                     self._set_health(ev[1], ev[2], False, ev[3])
                 elif kind == EV_REDISCOVER:
                     self._check_inventory()
@@ -250,11 +260,13 @@ class PluginManager:
         resources = new_resources(gpus, self.cfg.strategy, self.cfg.resourcePrefix, self.cfg.resources)
         self.device_map = build_device_map(gpus, resources, self.cfg.strategy, self.cfg.mountCardNodes,
                                            self.cfg.sharing.replicas, self.cfg.sharing.renameByDefault)
+        self._key_of = {g.index: self._identity(g) for g in gpus}
+        self._index_of = {k: i for i, k in self._key_of.items()}
         if self.cfg.health.canaryOnStart:
             failed = self._startup_canary(gpus)
-            self._canary_failed = set(failed)  # fresh verdicts replace older ones
+            self._canary_failed = {(self._key_of[g], p) for g, p in failed}  # fresh verdicts replace older ones
         else:
-            failed = set(self._canary_failed)
+            failed = {(self._index_of[k], p) for k, p in self._canary_failed if k in self._index_of}
         plugins = [AmdDevicePlugin(name, devs, topo, self.cfg) for name, devs in self.device_map.items()]
         if self.cfg.health.canaryOnPreStart:
             for p in plugins:
@@ -268,9 +280,12 @@ class PluginManager:
         # event that lands during the reload reaches the new tables either way (reading
         # gpu_healthy() here and calling set_fast_tables() later left a window in which
         # it reached only the outgoing ones).
-        self.monitor.set_gpu_count(max([g.index for g in gpus], default=-1) + 1)
+        keys = [""] * (max([g.index for g in gpus], default=-1) + 1)
+        for i, k in self._key_of.items():
+            keys[i] = k
+        self.monitor.set_gpus(keys)
         self.monitor.attach_tables([p.table for p in plugins], not self.cfg.health.canary,
-                                   sorted(self._held_unhealthy))
+                                   sorted(self._index_of[k] for k in self._held_unhealthy if k in self._index_of))
         for p in plugins:
             for g in gpus:
                 p.sync_gpu_health(g.index)
@@ -304,6 +319,11 @@ class PluginManager:
         self.monitor.set_bad_page_thresholds(thresholds)
         if self._event_sources is not None:
             self._event_sources = getattr(self.backend, "armed_event_sources", None)
+        with self._canary_lock:  # results of partitions that no longer exist leave /metrics
+            live = {(g.index, p.index) for g in gpus for p in g.partitions}
+            for k in [k for k in self.canary_results if k not in live]:
+                del self.canary_results[k]
+        self._push_link_pods()  # the new tables start from the known allocation map
         self.exporter.set_inventory(gpus)
         self.exporter.set_partition_labels(labels)
         self.exporter.set_tables([p.table for p in plugins])
@@ -344,59 +364,121 @@ class PluginManager:
         self.start_plugins()
 
     # ------------------------------------------------------------ health
+    def _identity(self, g) -> str:
+        """The key health state is kept under: the backend's own (the monitor uses the
+        same), else the GPU's UUID or BDF."""
+        k = ""
+        try:
+            k = self.backend.gpu_key(g.index)
+        except Exception:  # pragma: no cover - every native backend implements it
+            pass
+        return k or g.uuid or g.bdf or "#%d" % g.index
+
+    def _key(self, u) -> str:
+        return getattr(u, "key", "") or self._key_of.get(u.gpu, "#%d" % u.gpu)
+
+    def _gpu_name(self, key: str) -> str:
+        i = self._index_of.get(key)
+        return "GPU %d (%s)" % (i, key) if i is not None else "GPU %s (not advertised)" % key
+
     def _apply_health(self, u) -> None:
         self.counters["health_events"] += 1
+        key = self._key(u)
         if u.healthy in (0, 1):
             healthy = bool(u.healthy)
-            gen = self._health_gen[u.gpu] = self._health_gen.get(u.gpu, 0) + 1
+            gen = self._health_gen[key] = self._health_gen.get(key, 0) + 1
             if healthy and self.cfg.health.canary:
                 # stay Unhealthy until the canary passes; do not block the event loop on it
                 if self._verify_pool is None:
                     self._verify_pool = concurrent.futures.ThreadPoolExecutor(max_workers=4,
                                                                               thread_name_prefix="canary")
-                log.info("GPU %d reports healthy (%s); verifying with the canary", u.gpu, u.reason)
-                self._held_unhealthy.add(u.gpu)
-                self._verify_pool.submit(self._verify_and_post, u, gen)
+                log.info("%s reports healthy (%s); verifying with the canary", self._gpu_name(key), u.reason)
+                self._held_unhealthy.add(key)
+                self._verify_pool.submit(self._verify_and_post, u, key, gen)
                 return
             if healthy:
-                self._held_unhealthy.discard(u.gpu)
+                self._held_unhealthy.discard(key)
             # without the canary the monitor thread already applied both directions to
             # the tables; re-applying a queued update here could briefly undo a newer one
-            self._set_health(u.gpu, u.partition, healthy, u.reason, apply=self.cfg.health.canary)
+            self._set_health(key, u.partition, healthy, u.reason, apply=self.cfg.health.canary)
         elif u.link_up in (0, 1):
-            for p in self.plugins:
-                p.set_link_up(u.gpu, u.peer, bool(u.link_up))
-            log.warning("xGMI link %d<->%d %s", u.gpu, u.peer, "up" if u.link_up else "down")
+            a = self._index_of.get(key, -1)
+            b = self._index_of.get(getattr(u, "peer_key", "") or self._key_of.get(u.peer, ""), -1)
+            if a >= 0 and b >= 0:
+                for p in self.plugins:
+                    p.set_link_up(a, b, bool(u.link_up))
+            log.warning("xGMI link %d<->%d %s", a, b, "up" if u.link_up else "down")
+        elif u.kind == native.load().EVT_LINK_QUALITY:
+            a = self._index_of.get(key, -1)
+            b = self._index_of.get(getattr(u, "peer_key", "") or self._key_of.get(u.peer, ""), -1)
+            if a >= 0 and b >= 0:
+                for p in self.plugins:
+                    p.set_link_bandwidth(a, b, u.link_gbps)
+            log.warning("xGMI link %d<->%d now trains at %.0f Gb/s: %s", a, b, u.link_gbps, u.reason)
         else:
-            log.info("GPU event on %d: %s", u.gpu, u.reason)
+            log.info("GPU event on %s: %s", self._gpu_name(key), u.reason)
 
-    def _set_health(self, gpu: int, partition: int, healthy: bool, reason: str, apply: bool = True) -> None:
-        if healthy:  # a recovery supersedes earlier canary verdicts on this GPU
-            self._canary_failed = {k for k in self._canary_failed if k[0] != gpu}
+    def _push_link_pods(self) -> None:
+        """Which GPU pairs' xGMI links already carry a multi-GPU pod (from the PodResources
+        allocation map): the allocator keeps a new pod's cross-GPU traffic off them when it
+        can (in CPX/QPX/DPX two pods that each span GPUs A and B
+        share the one A-B link)."""
+        if self.podres is None or not self.plugins:
+            return
+        allocs, _ = self.podres.snapshot()
+        gpu_of = {}
         for p in self.plugins:
-            if apply:
-                p.set_gpu_health(gpu, partition, healthy)
-            else:
-                p.sync_gpu_health(gpu, partition)
+            for d in p.devices():
+                gpu_of[(str(p.resource), d.id)] = d.gpu
+        spans = {}
+        for (res, dev), (ns, pod, _ctr) in allocs.items():
+            g = gpu_of.get((res, dev))
+            if g is not None and g >= 0:
+                spans.setdefault((ns, pod), set()).add(g)
+        n = max([g.index for g in self.gpus], default=-1) + 1
+        load = [0] * (n * n)
+        multi = 0
+        for gs in spans.values():
+            if len(gs) < 2:
+                continue
+            multi += 1
+            for a, b in itertools.combinations(sorted(gs), 2):
+                load[a * n + b] += 1
+                load[b * n + a] += 1
+        for p in self.plugins:
+            p.set_link_pods(load)
+        self.link_pods = {(a, b): load[a * n + b] for a in range(n) for b in range(a + 1, n) if load[a * n + b]}
+        self.multi_gpu_pods = multi
+
+    def _set_health(self, key: str, partition: int, healthy: bool, reason: str, apply: bool = True) -> None:
+        if healthy:  # a recovery supersedes earlier canary verdicts on this GPU
+            self._canary_failed = {k for k in self._canary_failed if k[0] != key}
+        gpu = self._index_of.get(key, -1)
+        if gpu >= 0:
+            for p in self.plugins:
+                if apply:
+                    p.set_gpu_health(gpu, partition, healthy)
+                else:
+                    p.sync_gpu_health(gpu, partition)
         self.health_log.append((time.monotonic(), gpu, int(healthy), reason))
-        (log.info if healthy else log.warning)("GPU %d marked %s: %s", gpu, "Healthy" if healthy else "Unhealthy",
-                                               reason)
+        (log.info if healthy else log.warning)("%s marked %s: %s", self._gpu_name(key),
+                                               "Healthy" if healthy else "Unhealthy", reason)
 
-    def _verify_and_post(self, u, gen: int) -> None:
+    def _verify_and_post(self, u, key: str, gen: int) -> None:
         try:
-            ok = self._canary_ok(u.gpu)
+            ok = self._canary_ok(key)
         except Exception as e:  # a canary that cannot run does not prove health
-            log.error("recovery canary on GPU %d could not run: %s", u.gpu, e)
+            log.error("recovery canary on %s could not run: %s", self._gpu_name(key), e)
             ok = False
-        self.events.put((EV_VERIFIED, u, gen, ok))
+        self.events.put((EV_VERIFIED, u, key, gen, ok))
 
-    def _apply_verified(self, u, gen: int, ok: bool) -> None:
-        if self._health_gen.get(u.gpu) != gen:
-            log.info("dropping stale canary verdict for GPU %d (newer health event)", u.gpu)
+    def _apply_verified(self, u, key: str, gen: int, ok: bool) -> None:
+        if self._health_gen.get(key) != gen:
+            log.info("dropping stale canary verdict for %s (newer health event)", self._gpu_name(key))
             return
         if ok:
-            self._held_unhealthy.discard(u.gpu)
-        self._set_health(u.gpu, u.partition, ok, u.reason + ("" if ok else "; canary failed"))
+            self._held_unhealthy.discard(key)
+        self._set_health(key, u.partition, ok, u.reason + ("" if ok else "; canary failed"))
 
     def _startup_canary(self, gpus) -> set:
         """Runs the gfx950 canary on every partition (one child process per partition, all
@@ -473,7 +555,8 @@ class PluginManager:
                 if not res.get("ok"):
                     failures.setdefault(futs[f], res.get("error") or "canary reported errors")
         for (gpu, part), why in sorted(failures.items()):
-            self.events.put((EV_PRESTART_FAIL, gpu, part, "PreStartContainer canary failed: %s" % why))
+            self.events.put((EV_PRESTART_FAIL, self._key_of.get(gpu, "#%d" % gpu), part,
+                             "PreStartContainer canary failed: %s" % why))
         if failures:
             return "PreStartContainer: gfx950 canary failed on %s" % ", ".join(
                 "GPU %d%s" % (g, "" if p < 0 else " partition %d" % p) for g, p in sorted(failures))
@@ -491,7 +574,10 @@ class PluginManager:
             log.warning("device inventory changed (partition mode or GPU set); re-advertising")
             self.restart_plugins()
 
-    def _canary_ok(self, gpu: int) -> bool:
+    def _canary_ok(self, key: str) -> bool:
+        gpu = self._index_of.get(key)
+        if gpu is None:
+            raise RuntimeError("GPU %s is not in the advertised inventory" % key)
         for g in self.gpus:
             if g.index != gpu:
                 continue
@@ -599,6 +685,12 @@ class PluginManager:
             from .podresources import render
             allocs, up = self.podres.snapshot()
             lines += render(allocs, up)
+            if self.link_pods:
+                lines += ["# HELP amdgpu_xgmi_link_pods Multi-GPU pods whose devices span this GPU pair (they share "
+                          "its xGMI link).",
+                          "# TYPE amdgpu_xgmi_link_pods gauge"]
+                lines += ['amdgpu_xgmi_link_pods{gpu="%d",peer="%d"} %d' % (a, b, c)
+                          for (a, b), c in sorted(self.link_pods.items())]
         lines += self._canary_lines()
         self.exporter.set_extra("\n".join(lines) + "\n")
 

@@ -342,6 +342,13 @@ class AmdDevicePlugin:
     def set_link_up(self, a: int, b: int, up: bool) -> None:
         self.table.set_link_up(a, b, up)
 
+    def set_link_bandwidth(self, a: int, b: int, gbps: float) -> None:
+        self.table.set_link_bandwidth(a, b, gbps)
+
+    def set_link_pods(self, load) -> None:
+        """n x n row-major counts of multi-GPU pods whose devices span each GPU pair."""
+        self.table.set_link_pods(list(load))
+
     # ------------------------------------------------------------------ RPCs (grpcio)
     def _handler(self):
         import grpc

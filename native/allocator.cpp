@@ -1,6 +1,7 @@
 #include "allocator.h"
 
 #include <algorithm>
+#include <cmath>
 #include <map>
 #include <numeric>
 #include <set>
@@ -8,7 +9,19 @@
 
 namespace amdgpu_dp {
 
-int pair_score(const Topology& topo, const AllocDevice& a, const AllocDevice& b) {
+LinkRefs link_refs(const Topology& topo) {
+  LinkRefs r;
+  for (int a = 0; a < topo.n; ++a)
+    for (int b = a + 1; b < topo.n; ++b) {
+      const Link& l = topo.at(a, b);
+      if (l.type != kLinkXgmi) continue;
+      if (l.bw_gbps > r.best_bw_gbps) r.best_bw_gbps = l.bw_gbps;
+      if (l.weight > 0 && (r.min_weight == 0 || l.weight < r.min_weight)) r.min_weight = l.weight;
+    }
+  return r;
+}
+
+int pair_score(const Topology& topo, const AllocDevice& a, const AllocDevice& b, const LinkRefs& refs) {
   const bool same_numa = a.numa >= 0 && a.numa == b.numa;
   if (a.gpu == b.gpu) return 100 + 5;  // partitions of one GPU: on-package fabric
   if (a.gpu < 0 || b.gpu < 0 || a.gpu >= topo.n || b.gpu >= topo.n) return 5;
@@ -16,7 +29,16 @@ int pair_score(const Topology& topo, const AllocDevice& a, const AllocDevice& b)
   int s;
   switch (l.type) {
     case kLinkXgmi:
-      s = l.up ? (l.hops <= 1 ? 60 : 40) : 10;
+      if (l.up) {
+        // A link that trained below the node's best scores in proportion, between a
+        // full-rate link and a down one: an RCCL ring runs at its slowest hop.
+        const double q = (l.bw_gbps > 0 && refs.best_bw_gbps > 0) ? std::min(1.0, l.bw_gbps / refs.best_bw_gbps) : 1.0;
+        s = 10 + static_cast<int>(std::floor((l.hops <= 1 ? 50 : 30) * q + 0.5));
+        if (l.weight > 0 && refs.min_weight > 0 && l.weight > refs.min_weight)
+          s -= std::min(10, static_cast<int>(std::floor(5 * std::log2(static_cast<double>(l.weight) / refs.min_weight) + 0.5)));
+      } else {
+        s = 10;
+      }
       break;
     case kLinkPcie:
       s = 20;
@@ -24,7 +46,12 @@ int pair_score(const Topology& topo, const AllocDevice& a, const AllocDevice& b)
     default:
       s = 5;
   }
+  s -= 8 * std::min(std::max(l.pods, 0), 4);  // other multi-GPU pods already drive traffic over it
   return s + (same_numa ? 5 : 0);
+}
+
+int pair_score(const Topology& topo, const AllocDevice& a, const AllocDevice& b) {
+  return pair_score(topo, a, b, link_refs(topo));
 }
 
 namespace {
@@ -55,11 +82,15 @@ struct Ctx {
 
   int class_pair(int a, int b) const {
     int& v = cls_pair[static_cast<size_t>(a) * ncls + b];
-    if (v == kUnset) v = cls_pair[static_cast<size_t>(b) * ncls + a] = pair_score(topo, devs[cls_rep[a]], devs[cls_rep[b]]);
+    if (v == kUnset)
+      v = cls_pair[static_cast<size_t>(b) * ncls + a] = pair_score(topo, devs[cls_rep[a]], devs[cls_rep[b]], refs);
     return v;
   }
 
-  Ctx(const Topology& t, const std::vector<AllocDevice>& d, const std::vector<int>& avail) : topo(t), devs(d) {
+  LinkRefs refs;
+
+  Ctx(const Topology& t, const std::vector<AllocDevice>& d, const std::vector<int>& avail)
+      : topo(t), devs(d), refs(link_refs(t)) {
     is_avail.assign(d.size(), 0);
     for (int i : avail) is_avail[i] = 1;
     for (auto& x : d) ngpu = std::max(ngpu, x.gpu + 1);

@@ -179,6 +179,13 @@ class AmdSmiBackend : public Backend {
     return !closed_ && reinit_locked();
   }
 
+  // Answered from a copy under its own lock: the sampler watchdog asks while an amdsmi
+  // call that hung may be holding mu_.
+  std::string gpu_key(int gpu) const override {
+    std::lock_guard<std::mutex> lk(keys_mu_);
+    return gpu >= 0 && gpu < static_cast<int>(keys_.size()) ? keys_[gpu] : "";
+  }
+
   int reinit_count() const override {
     std::lock_guard<std::mutex> lk(mu_);
     return reinits_;
@@ -322,10 +329,24 @@ class AmdSmiBackend : public Backend {
       GpuSample s;
       link_state_locked(a, &s, nullptr);
       (*gpus)[a].num_xgmi_links = s.num_links;
-      for (int k = 0; k < s.num_links; ++k)
-        if (s.link_peer[k] >= 0 && s.link_up[k] == 0) topo->at(a, s.link_peer[k]).up = topo->at(s.link_peer[k], a).up = false;
+      for (int k = 0; k < s.num_links; ++k) {
+        const int p = s.link_peer[k];
+        if (p < 0) continue;
+        if (s.link_up[k] == 0) topo->at(a, p).up = topo->at(p, a).up = false;
+        // trained bandwidth per link (the allocator scores a slow link below a full-rate one)
+        if (s.link_max_gbps[k] > 0) {
+          const double cur = topo->at(a, p).bw_gbps;
+          const double bw = cur > 0 ? std::min(cur, s.link_max_gbps[k]) : s.link_max_gbps[k];
+          topo->at(a, p).bw_gbps = topo->at(p, a).bw_gbps = bw;
+        }
+      }
     }
     gpus_ = *gpus;
+    {
+      std::lock_guard<std::mutex> kl(keys_mu_);
+      keys_.clear();
+      for (const auto& g : gpus_) keys_.push_back(key_of(g));
+    }
     if (want_rearm_) {
       want_rearm_ = false;
       arm_locked();
@@ -346,6 +367,7 @@ class AmdSmiBackend : public Backend {
 
   bool sample(int gpu, GpuSample* s) override {
     std::lock_guard<std::mutex> lk(mu_);
+    if (gpu >= 0 && gpu < static_cast<int>(gpus_.size())) s->key = key_of(gpus_[gpu]);
     if (closed_ || gpu < 0 || gpu >= static_cast<int>(procs_.size())) return false;
     amdsmi_processor_handle h0 = procs_[gpu][0];
     s->ts_ns = now_ns();
@@ -488,6 +510,7 @@ class AmdSmiBackend : public Backend {
         default: continue;
       }
       locate(data[i].processor_handle, &e.gpu, &e.partition);
+      if (e.gpu >= 0 && e.gpu < static_cast<int>(gpus_.size())) e.key = key_of(gpus_[e.gpu]);
       out->push_back(e);
       ++added;
     }
@@ -495,6 +518,8 @@ class AmdSmiBackend : public Backend {
   }
 
  private:
+  static std::string key_of(const GpuInfo& g) { return g.uuid.empty() ? g.bdf : g.uuid; }
+
   std::string uuid_of(amdsmi_processor_handle h) {
     char ubuf[AMDSMI_MAX_STRING_LENGTH] = {0};
     unsigned int ulen = sizeof(ubuf);
@@ -686,6 +711,8 @@ class AmdSmiBackend : public Backend {
   std::vector<std::vector<amdsmi_processor_handle>> procs_;
   std::vector<uint64_t> bdf_keys_;  // physical-device BDF key per GPU index (procs_ order)
   std::vector<GpuInfo> gpus_;
+  mutable std::mutex keys_mu_;       // keys_ only (never held across an amdsmi call)
+  std::vector<std::string> keys_;    // gpu_key per index of the latest discovery
   std::vector<amdsmi_processor_handle> armed_handles_;
   std::vector<amdsmi_processor_handle> armed_for_;  // processor set at arming time
   bool armed_ = false;

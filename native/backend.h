@@ -71,6 +71,8 @@ struct Link {
   uint64_t weight = 0;  // amdsmi link weight (lower = closer)
   bool up = true;       // all physical xGMI links between the pair are up
   bool p2p = false;
+  double bw_gbps = 0;   // trained bandwidth of the link (all lanes), Gb/s; 0 = unknown
+  int pods = 0;         // multi-GPU pods already placed across this GPU pair (share the link)
 };
 
 struct Topology {
@@ -94,6 +96,7 @@ constexpr int kMaxPartitions = 8;
 
 // One telemetry sample of a physical GPU.  NaN / negative = unavailable.
 struct GpuSample {
+  std::string key;  // Backend::gpu_key of the GPU this sample read (set even when it failed)
   int64_t ts_ns = 0;
   double power_w = -1;
   double energy_j = -1;            // accumulated
@@ -143,6 +146,7 @@ enum EventKind : int {
   kEvtDeviceRecovered = 9,
   kEvtRetiredPagesExceeded = 10,  // retired + pending pages >= threshold -> Unhealthy
   kEvtRetiredPagesCleared = 11,   // back below the threshold (threshold raised, GPU swapped)
+  kEvtLinkQuality = 12,   // an up xGMI link re-trained at another bandwidth (value = Gb/s)
 };
 
 const char* event_kind_name(int kind);
@@ -154,6 +158,10 @@ struct HwEvent {
   int partition = -1;  // -1 = whole GPU
   int peer = -1;       // for link events
   std::string message;
+  // Identity (gpu_key) of `gpu` / `peer` when the event was raised, if the source knew it:
+  // an index may be re-used by another GPU after re-enumeration, an identity never is.
+  std::string key, peer_key;
+  double value = 0;  // kEvtLinkQuality: the link's bandwidth now, Gb/s
 };
 
 class Backend {
@@ -164,6 +172,11 @@ class Backend {
   virtual void discover(std::vector<GpuInfo>* gpus, Topology* topo) = 0;
   // Telemetry for physical GPU `gpu`; returns false when unavailable.
   virtual bool sample(int gpu, GpuSample* out) = 0;
+  // Stable identity (UUID, else BDF) of the GPU at index `gpu` of the latest discover(),
+  // in the index space sample() and events use; "" when unknown.  Health state is keyed
+  // by it: when a GPU drops off the bus and the node re-enumerates, every later GPU moves
+  // down one index, and its health must not move with the index.
+  virtual std::string gpu_key(int gpu) const { return ""; }
   // Block up to timeout_ms for hardware events; append to *out.  Returns count.
   virtual int wait_events(int timeout_ms, std::vector<HwEvent>* out) = 0;
   // Arm event delivery for the discovered GPUs (idempotent).

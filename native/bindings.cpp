@@ -1,5 +1,7 @@
 // pybind11 module `k8s_gpu_device_plugin_amd._native`.
 // Long-blocking calls (health pop, inotify read, server stop, scrapes) release the GIL.
+#include <sched.h>
+
 #include <chrono>
 #include <thread>
 
@@ -70,17 +72,21 @@ PYBIND11_MODULE(_native, m) {
 
   py::class_<Link>(m, "Link")
       .def(py::init<>())
-      .def(py::init([](int type, int hops, uint64_t weight, bool up, bool p2p) {
+      .def(py::init([](int type, int hops, uint64_t weight, bool up, bool p2p, double bw_gbps, int pods) {
              Link l;
              l.type = type;
              l.hops = hops;
              l.weight = weight;
              l.up = up;
              l.p2p = p2p;
+             l.bw_gbps = bw_gbps;
+             l.pods = pods;
              return l;
            }),
            py::arg("type") = static_cast<int>(kLinkXgmi), py::arg("hops") = 1, py::arg("weight") = 15,
-           py::arg("up") = true, py::arg("p2p") = true)
+           py::arg("up") = true, py::arg("p2p") = true, py::arg("bw_gbps") = 0.0, py::arg("pods") = 0)
+      .def_readwrite("bw_gbps", &Link::bw_gbps)
+      .def_readwrite("pods", &Link::pods)
       .def_readwrite("type", &Link::type)
       .def_readwrite("hops", &Link::hops)
       .def_readwrite("weight", &Link::weight)
@@ -107,6 +113,7 @@ PYBIND11_MODULE(_native, m) {
 
   py::class_<GpuSample>(m, "GpuSample")
       .def(py::init<>())
+      .def_readonly("key", &GpuSample::key)
       .def_readonly("ts_ns", &GpuSample::ts_ns)
       .def_readonly("ok", &GpuSample::ok)
       .def_readonly("power_w", &GpuSample::power_w)
@@ -151,6 +158,7 @@ PYBIND11_MODULE(_native, m) {
   m.attr("EVT_DEVICE_RECOVERED") = static_cast<int>(kEvtDeviceRecovered);
   m.attr("EVT_RETIRED_PAGES_EXCEEDED") = static_cast<int>(kEvtRetiredPagesExceeded);
   m.attr("EVT_RETIRED_PAGES_CLEARED") = static_cast<int>(kEvtRetiredPagesCleared);
+  m.attr("EVT_LINK_QUALITY") = static_cast<int>(kEvtLinkQuality);
   m.attr("LINK_INTERNAL") = static_cast<int>(kLinkInternal);
   m.attr("LINK_PCIE") = static_cast<int>(kLinkPcie);
   m.attr("LINK_XGMI") = static_cast<int>(kLinkXgmi);
@@ -174,6 +182,9 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("partition", &HwEvent::partition)
       .def_readwrite("peer", &HwEvent::peer)
       .def_readwrite("message", &HwEvent::message)
+      .def_readwrite("key", &HwEvent::key)
+      .def_readwrite("value", &HwEvent::value)
+      .def_readwrite("peer_key", &HwEvent::peer_key)
       .def_readwrite("ts_ns", &HwEvent::ts_ns);
 
   py::class_<Backend, std::shared_ptr<Backend>>(m, "Backend")
@@ -205,6 +216,7 @@ PYBIND11_MODULE(_native, m) {
              if (!ok) return py::none();
              return py::cast(s);
            })
+      .def("gpu_key", &Backend::gpu_key, py::call_guard<py::gil_scoped_release>())
       .def("arm_events", &Backend::arm_events, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("armed_event_sources", &Backend::armed_event_sources)
       .def("reinit", &Backend::reinit, py::call_guard<py::gil_scoped_release>())
@@ -218,6 +230,7 @@ PYBIND11_MODULE(_native, m) {
       .def("clear", &FixtureBackend::clear)
       .def("set_link", &FixtureBackend::set_link)
       .def("set_link_up", &FixtureBackend::set_link_up)
+      .def("set_link_bandwidth", &FixtureBackend::set_link_bandwidth)
       .def("schedule_event", &FixtureBackend::schedule_event)
       .def("inject_event", &FixtureBackend::inject_event)
       .def("set_fail_discovery", &FixtureBackend::set_fail_discovery)
@@ -250,13 +263,27 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("partition", &AllocDevice::partition)
       .def_readwrite("numa", &AllocDevice::numa)
       .def_readwrite("base_id", &AllocDevice::base_id);
-  m.def("pair_score", &pair_score);
+  m.def("pair_score", [](const Topology& t, const AllocDevice& a, const AllocDevice& b) { return pair_score(t, a, b); });
   m.def("aligned_alloc", [](const Topology& t, const std::vector<AllocDevice>& d, const std::vector<int>& avail,
                             const std::vector<int>& req, int size) {
     AllocResult r = aligned_alloc(t, d, avail, req, size);
     if (!r.ok) throw std::runtime_error(r.error);
     return r.chosen;
   });
+  m.def("bench_aligned_alloc",  // per-call seconds of n aligned_alloc calls (allocator cost alone)
+        [](const Topology& t, const std::vector<AllocDevice>& d, const std::vector<int>& avail,
+           const std::vector<int>& req, int size, int n) {
+          std::vector<double> out;
+          out.reserve(static_cast<size_t>(std::max(0, n)));
+          py::gil_scoped_release rel;
+          for (int i = 0; i < n; ++i) {
+            const int64_t t0 = mono_ns();
+            AllocResult r = aligned_alloc(t, d, avail, req, size);
+            out.push_back((mono_ns() - t0) * 1e-9);
+            if (!r.ok) throw std::runtime_error(r.error);
+          }
+          return out;
+        });
   m.def("distributed_alloc", [](const std::vector<AllocDevice>& d, const std::vector<int>& avail,
                                 const std::vector<int>& req, int size) {
     AllocResult r = distributed_alloc(d, avail, req, size);
@@ -327,6 +354,8 @@ PYBIND11_MODULE(_native, m) {
       .def("healthy", [](const DeviceTable& t, const std::string& id) { return t.healthy(id); })
       .def("healthy_count", &DeviceTable::healthy_count)
       .def("set_link_up", &DeviceTable::set_link_up)
+      .def("set_link_bandwidth", &DeviceTable::set_link_bandwidth)
+      .def("set_link_pods", &DeviceTable::set_link_pods)
       .def("topology", &DeviceTable::topology)
       .def_property_readonly("version", &DeviceTable::version)
       .def("list_and_watch", [](const DeviceTable& t) { return py::bytes(t.list_and_watch()); })
@@ -392,6 +421,9 @@ PYBIND11_MODULE(_native, m) {
       .def_readonly("peer", &HealthUpdate::peer)
       .def_readonly("link_up", &HealthUpdate::link_up)
       .def_readonly("reason", &HealthUpdate::reason)
+      .def_readonly("key", &HealthUpdate::key)
+      .def_readonly("link_gbps", &HealthUpdate::link_gbps)
+      .def_readonly("peer_key", &HealthUpdate::peer_key)
       .def("__repr__", [](const HealthUpdate& u) {
         return "<HealthUpdate " + std::string(event_kind_name(u.kind)) + " gpu=" + std::to_string(u.gpu) +
                " healthy=" + std::to_string(u.healthy) + " " + u.reason + ">";
@@ -399,7 +431,9 @@ PYBIND11_MODULE(_native, m) {
 
   py::class_<HealthMonitor, std::shared_ptr<HealthMonitor>>(m, "HealthMonitor")
       .def(py::init<std::shared_ptr<Backend>, int>(), py::arg("backend"), py::arg("lost_after_failures") = 3)
-      .def("set_gpu_count", &HealthMonitor::set_gpu_count)
+      .def("set_gpu_count", &HealthMonitor::set_gpu_count, py::call_guard<py::gil_scoped_release>())
+      .def("set_gpus", &HealthMonitor::set_gpus, py::call_guard<py::gil_scoped_release>())
+      .def("unhealthy_keys", &HealthMonitor::unhealthy_keys)
       .def("start", &HealthMonitor::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &HealthMonitor::stop, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("running", &HealthMonitor::running)
@@ -440,7 +474,8 @@ PYBIND11_MODULE(_native, m) {
            py::call_guard<py::gil_scoped_release>())
       .def("stop", &Exporter::stop, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("running", &Exporter::running)
-      .def("sample_once", &Exporter::sample_once, py::call_guard<py::gil_scoped_release>())
+      .def("sample_once", [](Exporter& e) { e.sample_once(false); }, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("abandoned_samplers", &Exporter::abandoned_samplers)
       .def_property_readonly("samples_total", &Exporter::samples_total)
       .def("last_sample", &Exporter::last_sample)
       .def("render", [](const Exporter& e) {
@@ -589,6 +624,33 @@ PYBIND11_MODULE(_native, m) {
                if (st != 0) throw std::runtime_error("grpc-status " + std::to_string(st) + ": " + msg);
              }
              return out;
+           },
+           py::arg("path"), py::arg("req"), py::arg("n"), py::arg("gap_us") = 0)
+      .def("bench_unary_ts",
+           // Same as bench_unary, per call: (start, CLOCK_MONOTONIC ns; latency, s; the
+           // CPU the client ran on when the answer arrived) - for attributing the tail to
+           // idle gaps, CPU migrations or events of the server process at that time.
+           [](H2Client& c, const std::string& path, const py::bytes& req, int n, int gap_us) {
+             std::string r(req), resp, msg;
+             std::vector<int64_t> starts;
+             std::vector<double> lat;
+             std::vector<int> cpus;
+             starts.reserve(static_cast<size_t>(n));
+             lat.reserve(static_cast<size_t>(n));
+             cpus.reserve(static_cast<size_t>(n));
+             {
+               py::gil_scoped_release rel;
+               for (int i = 0; i < n; ++i) {
+                 if (gap_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(gap_us));
+                 const int64_t t0 = mono_ns();
+                 const int st = c.unary(path, r, &resp, &msg);
+                 lat.push_back((mono_ns() - t0) * 1e-9);
+                 starts.push_back(t0);
+                 cpus.push_back(sched_getcpu());
+                 if (st != 0) throw std::runtime_error("grpc-status " + std::to_string(st) + ": " + msg);
+               }
+             }
+             return py::make_tuple(starts, lat, cpus);
            },
            py::arg("path"), py::arg("req"), py::arg("n"), py::arg("gap_us") = 0)
       .def("close", &H2Client::close);

@@ -56,6 +56,7 @@ const char* event_kind_name(int kind) {
     case kEvtDeviceRecovered: return "device_recovered";
     case kEvtRetiredPagesExceeded: return "retired_pages_threshold";
     case kEvtRetiredPagesCleared: return "retired_pages_below_threshold";
+    case kEvtLinkQuality: return "xgmi_link_bandwidth_changed";
     default: return "none";
   }
 }

@@ -187,14 +187,42 @@ int DeviceTable::healthy_count() const {
   return n;
 }
 
-void DeviceTable::set_link_up(int a, int b, bool up) {
+template <class F>
+void DeviceTable::patch_topology(F&& f) {
   std::lock_guard<std::mutex> lk(wmu_);
   auto cur = std::atomic_load_explicit(&topo_, std::memory_order_acquire);
-  if (a < 0 || b < 0 || a >= cur->n || b >= cur->n) return;
-  auto next = std::make_shared<Topology>(*cur);  // copy-on-write
-  next->at(a, b).up = up;
-  next->at(b, a).up = up;
+  auto next = std::make_shared<Topology>(*cur);  // copy-on-write: readers keep their snapshot
+  if (!f(*next)) return;
   std::atomic_store_explicit(&topo_, std::shared_ptr<const Topology>(std::move(next)), std::memory_order_release);
+}
+
+void DeviceTable::set_link_up(int a, int b, bool up) {
+  patch_topology([&](Topology& t) {
+    if (a < 0 || b < 0 || a >= t.n || b >= t.n) return false;
+    t.at(a, b).up = t.at(b, a).up = up;
+    return true;
+  });
+}
+
+void DeviceTable::set_link_bandwidth(int a, int b, double gbps) {
+  patch_topology([&](Topology& t) {
+    if (a < 0 || b < 0 || a >= t.n || b >= t.n || a == b) return false;
+    t.at(a, b).bw_gbps = t.at(b, a).bw_gbps = std::max(0.0, gbps);
+    return true;
+  });
+}
+
+void DeviceTable::set_link_pods(const std::vector<int>& counts) {
+  patch_topology([&](Topology& t) {
+    const size_t nn = static_cast<size_t>(t.n) * t.n;
+    bool changed = false;
+    for (size_t i = 0; i < nn; ++i) {
+      const int v = i < counts.size() ? std::max(0, counts[i]) : 0;
+      changed |= t.links[i].pods != v;
+      t.links[i].pods = v;
+    }
+    return changed;
+  });
 }
 
 Topology DeviceTable::topology() const { return *std::atomic_load_explicit(&topo_, std::memory_order_acquire); }

@@ -99,6 +99,10 @@ class DeviceTable {
   bool healthy(std::string_view id) const;
   int healthy_count() const;
   void set_link_up(int a, int b, bool up);
+  void set_link_bandwidth(int a, int b, double gbps);
+  // n*n row-major (n = topology size): multi-GPU pods spanning each GPU pair.  Replaces
+  // every count; a shorter vector clears the rest.
+  void set_link_pods(const std::vector<int>& counts);
   Topology topology() const;
 
   uint64_t version() const { return version_.load(std::memory_order_acquire); }
@@ -144,6 +148,8 @@ class DeviceTable {
 
  private:
   void publish_law_locked();  // caller holds wmu_
+  template <class F>
+  void patch_topology(F&& f);  // copy-on-write edit of the topology snapshot (takes wmu_)
   void notify_listeners();    // caller must NOT hold wmu_
   void encode_container_alloc(const int* idx, size_t n, std::string* out) const;  // appends
   bool is_healthy(int i) const { return health_[i].load(std::memory_order_acquire) != 0; }

@@ -20,6 +20,39 @@ double unit(uint64_t x) { return (mix(x) >> 11) * (1.0 / 9007199254740992.0); }
 
 FixtureBackend::FixtureBackend(uint64_t seed) : seed_(seed), t0_ns_(mono_ns()) {}
 
+int FixtureBackend::slot_of_locked(int index) const {
+  if (view_.empty()) return index >= 0 && index < static_cast<int>(gpus_.size()) ? index : -1;
+  return index >= 0 && index < static_cast<int>(view_.size()) ? view_[index] : -1;
+}
+
+int FixtureBackend::index_of_locked(int slot) const {
+  if (view_.empty()) return slot;
+  for (size_t i = 0; i < view_.size(); ++i)
+    if (view_[i] == slot) return static_cast<int>(i);
+  return -1;
+}
+
+std::string FixtureBackend::key_of_slot_locked(int slot) const {
+  if (slot < 0 || slot >= static_cast<int>(gpus_.size())) return "";
+  return gpus_[slot].uuid.empty() ? "fixture-gpu-" + std::to_string(slot) : gpus_[slot].uuid;
+}
+
+void FixtureBackend::translate_locked(HwEvent* e) const {
+  if (e->gpu >= 0) {
+    e->key = key_of_slot_locked(e->gpu);
+    e->gpu = index_of_locked(e->gpu);
+  }
+  if (e->peer >= 0) {
+    e->peer_key = key_of_slot_locked(e->peer);
+    e->peer = index_of_locked(e->peer);
+  }
+}
+
+std::string FixtureBackend::gpu_key(int gpu) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return key_of_slot_locked(slot_of_locked(gpu));
+}
+
 void FixtureBackend::add_gpu(const GpuInfo& g) {
   std::lock_guard<std::mutex> lk(mu_);
   GpuInfo copy = g;
@@ -33,6 +66,7 @@ void FixtureBackend::add_gpu(const GpuInfo& g) {
   ecc_ue_.push_back(0);
   pages_.emplace_back(0, 0);
   present_.push_back(true);
+  if (!view_.empty()) view_.clear();  // a changed node: identity until it is discovered again
 }
 
 void FixtureBackend::replace_gpu(int index, const GpuInfo& g) {
@@ -52,6 +86,7 @@ void FixtureBackend::clear() {
   pages_.clear();
   present_.clear();
   stalled_.clear();
+  view_.clear();
   scheduled_.clear();
   pending_.clear();
   cv_.notify_all();  // a sample() parked on a stall returns (its GPU is gone)
@@ -79,6 +114,12 @@ void FixtureBackend::set_link_up(int a, int b, bool up) {
     pending_.push_back(e);
   }
   cv_.notify_all();
+}
+
+void FixtureBackend::set_link_bandwidth(int a, int b, double gbps) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (a < 0 || b < 0 || a >= topo_.n || b >= topo_.n) throw std::out_of_range("set_link_bandwidth: bad gpu index");
+  topo_.at(a, b).bw_gbps = topo_.at(b, a).bw_gbps = std::max(0.0, gbps);
 }
 
 void FixtureBackend::set_ecc_uncorrectable(int gpu, int64_t count) {
@@ -114,11 +155,14 @@ void FixtureBackend::discover(std::vector<GpuInfo>* gpus, Topology* topo) {
   ++discover_calls_;
   if (fail_discovery_) throw std::runtime_error("fixture: discovery failure injected");
   gpus->clear();
-  // A GPU that "fell off the bus" disappears from discovery, like a real one.
+  // A GPU that "fell off the bus" disappears from discovery, like a real one, and every
+  // later GPU moves down one index (amdsmi enumerates in BDF order).
   std::vector<int> remap(gpus_.size(), -1);
+  view_.clear();
   for (size_t i = 0; i < gpus_.size(); ++i) {
     if (!present_[i]) continue;
     remap[i] = static_cast<int>(gpus->size());
+    view_.push_back(static_cast<int>(i));
     GpuInfo g = gpus_[i];
     g.index = remap[i];
     for (auto& p : g.partitions) p.gpu = g.index;
@@ -130,8 +174,10 @@ void FixtureBackend::discover(std::vector<GpuInfo>* gpus, Topology* topo) {
       if (remap[a] >= 0 && remap[b] >= 0) topo->at(remap[a], remap[b]) = topo_.at(a, b);
 }
 
-bool FixtureBackend::sample(int gpu, GpuSample* s) {
+bool FixtureBackend::sample(int index, GpuSample* s) {
   std::unique_lock<std::mutex> lk(mu_);
+  const int gpu = slot_of_locked(index);
+  s->key = key_of_slot_locked(gpu);
   if (gpu < 0 || gpu >= static_cast<int>(gpus_.size()) || !present_[gpu]) return false;
   cv_.wait(lk, [&] { return shutdown_ || gpu >= static_cast<int>(stalled_.size()) || !stalled_[gpu]; });
   if (gpu >= static_cast<int>(gpus_.size()) || !present_[gpu]) return false;
@@ -165,12 +211,14 @@ bool FixtureBackend::sample(int gpu, GpuSample* s) {
   for (int peer = 0; peer < topo_.n && s->num_links < kMaxXgmiLinks; ++peer) {
     if (peer == gpu || topo_.at(gpu, peer).type != kLinkXgmi) continue;
     const int k = s->num_links++;
-    s->link_peer[k] = peer;
+    s->link_peer[k] = index_of_locked(peer);  // -1 while the peer is not discovered
     s->link_up[k] = topo_.at(gpu, peer).up ? 1 : 0;
     s->link_read_kb[k] = 1e6 * ts * load;
     s->link_write_kb[k] = 0.9e6 * ts * load;
-    s->link_bitrate_gbps[k] = 38;  // what amdsmi reports on MI355X: 38 Gb/s per lane, 16 lanes
-    s->link_max_gbps[k] = 608;
+    // what amdsmi reports on MI355X: 38 Gb/s per lane, 16 lanes -> 608 Gb/s per link
+    const double bw = topo_.at(gpu, peer).bw_gbps > 0 ? topo_.at(gpu, peer).bw_gbps : 608.0;
+    s->link_bitrate_gbps[k] = bw / 16.0;
+    s->link_max_gbps[k] = bw;
   }
   s->num_partitions = std::min<int>(static_cast<int>(g.partitions.size()), kMaxPartitions);
   for (int p = 0; p < s->num_partitions; ++p) {
@@ -238,8 +286,10 @@ int FixtureBackend::wait_events(int timeout_ms, std::vector<HwEvent>* out) {
     if (!pending_.empty()) {
       int n = 0;
       while (!pending_.empty()) {
-        out->push_back(pending_.front());
+        HwEvent e = pending_.front();
         pending_.pop_front();
+        translate_locked(&e);
+        out->push_back(std::move(e));
         ++n;
       }
       return n;

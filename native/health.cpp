@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 
 namespace amdgpu_dp {
 
@@ -10,12 +11,34 @@ HealthMonitor::HealthMonitor(std::shared_ptr<Backend> backend, int lost_after_fa
 
 HealthMonitor::~HealthMonitor() { stop(); }
 
-void HealthMonitor::set_gpu_count(int n) {
-  // Called on every plugin (re)load: keep the state of GPUs that are still there, or a
-  // GPU that is mid-reset when kubelet restarts would be forgotten as healthy and its
-  // POST_RESET would never produce the Healthy update.
+std::string HealthMonitor::key_of(int gpu, const std::string& given) const {
+  if (!given.empty()) return given;
+  if (gpu < 0) return "";
+  std::string k = backend_ ? backend_->gpu_key(gpu) : std::string();
+  return k.empty() ? "#" + std::to_string(gpu) : k;
+}
+
+int HealthMonitor::table_index_locked(const std::string& key) const {
+  if (key.empty()) return -1;
+  for (size_t i = 0; i < table_keys_.size(); ++i)
+    if (table_keys_[i] == key) return static_cast<int>(i);
+  return -1;
+}
+
+void HealthMonitor::set_gpus(std::vector<std::string> keys) {
+  // Called on every plugin (re)load.  State is never dropped here: a GPU that is
+  // mid-reset when kubelet restarts, or that fell off the bus and is coming back, keeps
+  // its latches; its POST_RESET (or recovery) still produces the Healthy update.
   std::lock_guard<std::mutex> lk(mu_);
-  state_.resize(static_cast<size_t>(std::max(0, n)));
+  table_keys_ = std::move(keys);
+  for (const auto& k : table_keys_)
+    if (!k.empty()) state_[k];
+}
+
+void HealthMonitor::set_gpu_count(int n) {
+  std::vector<std::string> keys;
+  for (int i = 0; i < n; ++i) keys.push_back(key_of(i, ""));
+  set_gpus(std::move(keys));
 }
 
 void HealthMonitor::start() {
@@ -79,84 +102,114 @@ bool HealthMonitor::healthy_locked(const GpuState& st) const {
          !(st.lost && !(disabled_ & kCheckLost)) && !(st.pages_bad && !(disabled_ & kCheckRetiredPages));
 }
 
-void HealthMonitor::reconcile_locked(int gpu, int kind, const std::string& reason) {
-  GpuState& st = state_[gpu];
+void HealthMonitor::reconcile_locked(const std::string& key, int kind, const std::string& reason) {
+  GpuState& st = state_[key];
+  const int idx = table_index_locked(key);
   const bool healthy = healthy_locked(st);
   if (healthy == st.reported_healthy) {
     if (disabled_ & check_of(kind)) {  // tracked, not acted on: still worth a log line
       HealthUpdate u;
       u.kind = kind;
-      u.gpu = gpu;
+      u.gpu = idx;
+      u.key = key;
       u.reason = reason + " (health check disabled)";
       emit_locked(std::move(u));
     }
     return;
   }
   st.reported_healthy = healthy;
-  if (!healthy || fast_recover_)
-    for (const auto& t : fast_tables_) t->set_gpu_health(gpu, -1, healthy);
+  if (idx >= 0 && (!healthy || fast_recover_))
+    for (const auto& t : fast_tables_) t->set_gpu_health(idx, -1, healthy);
   HealthUpdate u;
   u.kind = kind;
-  u.gpu = gpu;
+  u.gpu = idx;
+  u.key = key;
   u.healthy = healthy ? 1 : 0;
   u.reason = reason;
   emit_locked(std::move(u));
 }
 
 void HealthMonitor::process(const HwEvent& e) {
+  // identities first, outside mu_ (the backend answers them from its own small lock)
+  const std::string key = key_of(e.gpu, e.key);
+  const std::string peer_key = key_of(e.peer, e.peer_key);
   std::lock_guard<std::mutex> lk(mu_);
   ++events_seen_;
-  auto valid = [&](int g) { return g >= 0 && g < static_cast<int>(state_.size()); };
   const std::string why = std::string(event_kind_name(e.kind)) + (e.message.empty() ? "" : ": " + e.message);
+  const bool known = !key.empty();
   switch (e.kind) {
     case kEvtPreReset:
-      if (!valid(e.gpu)) return;
-      state_[e.gpu].resetting = true;
-      reconcile_locked(e.gpu, e.kind, why);
+      if (!known) return;
+      state_[key].resetting = true;
+      reconcile_locked(key, e.kind, why);
       return;
-    case kEvtPostReset:
-      if (!valid(e.gpu)) return;
-      state_[e.gpu].resetting = false;
-      state_[e.gpu].ecc_bad = false;  // a reset clears the uncorrectable-error latch
-      state_[e.gpu].last_ue = -1;     // re-baseline on next sample
-      reconcile_locked(e.gpu, e.kind, why);
+    case kEvtPostReset: {
+      if (!known) return;
+      GpuState& st = state_[key];
+      st.resetting = false;
+      st.ecc_bad = false;  // a reset clears the uncorrectable-error latch
+      st.last_ue = -1;     // re-baseline on next sample
+      reconcile_locked(key, e.kind, why);
       return;
+    }
     case kEvtEccUncorrectable:
-      if (!valid(e.gpu)) return;
-      state_[e.gpu].ecc_bad = true;
-      reconcile_locked(e.gpu, e.kind, why);
+      if (!known) return;
+      state_[key].ecc_bad = true;
+      reconcile_locked(key, e.kind, why);
       return;
     case kEvtDeviceLost:
-      if (!valid(e.gpu)) return;
-      state_[e.gpu].lost = true;
-      reconcile_locked(e.gpu, e.kind, why);
+      if (!known) return;
+      state_[key].lost = true;
+      reconcile_locked(key, e.kind, why);
       return;
-    case kEvtDeviceRecovered:
-      if (!valid(e.gpu)) return;
-      state_[e.gpu].lost = false;
-      state_[e.gpu].failures = 0;
-      reconcile_locked(e.gpu, e.kind, why);
+    case kEvtDeviceRecovered: {
+      if (!known) return;
+      GpuState& st = state_[key];
+      st.lost = false;
+      st.failures = 0;
+      reconcile_locked(key, e.kind, why);
       return;
+    }
     case kEvtRetiredPagesExceeded:
     case kEvtRetiredPagesCleared:
-      if (!valid(e.gpu)) return;
-      state_[e.gpu].pages_bad = e.kind == kEvtRetiredPagesExceeded;
-      reconcile_locked(e.gpu, e.kind, why);
+      if (!known) return;
+      state_[key].pages_bad = e.kind == kEvtRetiredPagesExceeded;
+      reconcile_locked(key, e.kind, why);
       return;
     case kEvtLinkDown:
     case kEvtLinkUp: {
-      if (!valid(e.gpu) || e.peer < 0) return;
+      if (!known || peer_key.empty()) return;
       const int up = e.kind == kEvtLinkUp ? 1 : 0;
-      auto& m = state_[e.gpu].link_up;
-      auto it = m.find(e.peer);
+      auto& m = state_[key].link_up;
+      auto it = m.find(peer_key);
       if (it != m.end() && it->second == up) return;  // already known (polling + event)
-      m[e.peer] = up;
-      if (valid(e.peer)) state_[e.peer].link_up[e.gpu] = up;
+      m[peer_key] = up;
+      state_[peer_key].link_up[key] = up;
       HealthUpdate u;
       u.kind = e.kind;
-      u.gpu = e.gpu;
-      u.peer = e.peer;
+      u.gpu = table_index_locked(key);
+      u.key = key;
+      u.peer = table_index_locked(peer_key);
+      u.peer_key = peer_key;
       u.link_up = up;
+      u.reason = why;
+      emit_locked(std::move(u));
+      return;
+    }
+    case kEvtLinkQuality: {
+      if (!known || peer_key.empty() || e.value <= 0) return;
+      auto& m = state_[key].link_bw;
+      auto it = m.find(peer_key);
+      if (it != m.end() && std::fabs(it->second - e.value) <= 0.05 * std::max(it->second, e.value)) return;
+      m[peer_key] = e.value;
+      state_[peer_key].link_bw[key] = e.value;  // the peer reports the same link: deduplicated
+      HealthUpdate u;
+      u.kind = e.kind;
+      u.gpu = table_index_locked(key);
+      u.key = key;
+      u.peer = table_index_locked(peer_key);
+      u.peer_key = peer_key;
+      u.link_gbps = e.value;
       u.reason = why;
       emit_locked(std::move(u));
       return;
@@ -164,7 +217,8 @@ void HealthMonitor::process(const HwEvent& e) {
     default: {
       HealthUpdate u;  // informational (thermal, vm fault)
       u.kind = e.kind;
-      u.gpu = e.gpu;
+      u.gpu = table_index_locked(key);
+      u.key = key;
       u.partition = e.partition;
       u.reason = why;
       emit_locked(std::move(u));
@@ -173,62 +227,72 @@ void HealthMonitor::process(const HwEvent& e) {
 }
 
 void HealthMonitor::on_sample(int gpu, bool ok, const GpuSample& s) {
+  if (gpu < 0) return;
+  // The sample names the GPU it read (backends fill s.key under the lock that also
+  // guards their enumeration), so a re-discovery between the read and this call cannot
+  // attribute one GPU's counters to another.
+  const std::string key = key_of(gpu, s.key);
+  std::vector<std::string> peer_keys(static_cast<size_t>(std::max(0, s.num_links)));
+  if (ok)
+    for (int k = 0; k < s.num_links; ++k)
+      if (s.link_peer[k] >= 0) peer_keys[k] = key_of(s.link_peer[k], "");
   std::vector<HwEvent> derived;
   {
     std::lock_guard<std::mutex> lk(mu_);
-    if (gpu < 0 || gpu >= static_cast<int>(state_.size())) return;
-    GpuState& st = state_[gpu];
+    GpuState& st = state_[key];
+    auto event = [&](int kind, std::string msg) {
+      HwEvent e;
+      e.kind = kind;
+      e.gpu = gpu;
+      e.key = key;
+      e.message = std::move(msg);
+      return e;
+    };
     if (!ok) {
-      if (++st.failures >= lost_after_ && !st.lost) {
-        HwEvent e;
-        e.kind = kEvtDeviceLost;
-        e.gpu = gpu;
-        e.message = "telemetry failed " + std::to_string(st.failures) + " times in a row";
-        derived.push_back(e);
-      }
+      if (++st.failures >= lost_after_ && !st.lost)
+        derived.push_back(event(kEvtDeviceLost, "telemetry failed " + std::to_string(st.failures) + " times in a row"));
     } else {
       st.failures = 0;
-      if (st.lost) {
-        HwEvent e;
-        e.kind = kEvtDeviceRecovered;
-        e.gpu = gpu;
-        e.message = "telemetry responding again";
-        derived.push_back(e);
-      }
+      if (st.lost) derived.push_back(event(kEvtDeviceRecovered, "telemetry responding again"));
       if (s.ecc_uncorrectable >= 0) {
-        if (st.last_ue >= 0 && s.ecc_uncorrectable > st.last_ue) {
-          HwEvent e;
-          e.kind = kEvtEccUncorrectable;
-          e.gpu = gpu;
-          e.message = "uncorrectable ECC count " + std::to_string(st.last_ue) + " -> " +
-                      std::to_string(s.ecc_uncorrectable);
-          derived.push_back(e);
-        }
+        if (st.last_ue >= 0 && s.ecc_uncorrectable > st.last_ue)
+          derived.push_back(event(kEvtEccUncorrectable, "uncorrectable ECC count " + std::to_string(st.last_ue) +
+                                                            " -> " + std::to_string(s.ecc_uncorrectable)));
         st.last_ue = s.ecc_uncorrectable;
       }
-      const int thr = gpu < static_cast<int>(page_thresholds_.size()) ? page_thresholds_[gpu] : 0;
+      const int thr = st.page_threshold;
       if (s.retired_pages >= 0) {
         const int64_t bad = s.retired_pages + std::max<int64_t>(0, s.pending_pages);
         const bool over = thr > 0 && bad >= thr;
-        if (over != st.pages_bad) {
-          HwEvent e;
-          e.kind = over ? kEvtRetiredPagesExceeded : kEvtRetiredPagesCleared;
-          e.gpu = gpu;
-          e.message = std::to_string(bad) + " retired/pending HBM pages, threshold " + std::to_string(thr);
-          derived.push_back(e);
-        }
+        if (over != st.pages_bad)
+          derived.push_back(event(over ? kEvtRetiredPagesExceeded : kEvtRetiredPagesCleared,
+                                  std::to_string(bad) + " retired/pending HBM pages, threshold " + std::to_string(thr)));
       }
       for (int k = 0; k < s.num_links; ++k) {
-        if (s.link_peer[k] < 0 || s.link_up[k] < 0) continue;
-        auto it = st.link_up.find(s.link_peer[k]);
+        if (s.link_peer[k] < 0 || s.link_up[k] < 0 || peer_keys[k].empty()) continue;
+        auto it = st.link_up.find(peer_keys[k]);
         const int prev = it == st.link_up.end() ? 1 : it->second;  // links assumed up at start
         if (prev != s.link_up[k]) {
-          HwEvent e;
-          e.kind = s.link_up[k] ? kEvtLinkUp : kEvtLinkDown;
-          e.gpu = gpu;
+          HwEvent e = event(s.link_up[k] ? kEvtLinkUp : kEvtLinkDown, "xgmi link status poll");
           e.peer = s.link_peer[k];
-          e.message = "xgmi link status poll";
+          e.peer_key = peer_keys[k];
           derived.push_back(e);
+        }
+        // Trained bandwidth: the first value seen is the baseline (discovery already put it
+        // in the topology); a re-train to another rate (> 5 % off) is reported.
+        const double bw = s.link_max_gbps[k];
+        if (s.link_up[k] == 1 && bw > 0) {
+          auto bt = st.link_bw.find(peer_keys[k]);
+          if (bt == st.link_bw.end()) {
+            st.link_bw[peer_keys[k]] = bw;
+          } else if (std::fabs(bt->second - bw) > 0.05 * std::max(bt->second, bw)) {
+            HwEvent e = event(kEvtLinkQuality, "xgmi link re-trained: " + std::to_string(static_cast<int>(bt->second)) +
+                                                   " -> " + std::to_string(static_cast<int>(bw)) + " Gb/s");
+            e.peer = s.link_peer[k];
+            e.peer_key = peer_keys[k];
+            e.value = bw;
+            derived.push_back(e);
+          }
         }
       }
     }
@@ -263,8 +327,12 @@ void HealthMonitor::attach_tables(std::vector<std::shared_ptr<DeviceTable>> tabl
   std::lock_guard<std::mutex> lk(mu_);
   fast_tables_ = std::move(tables);
   fast_recover_ = fast_recover;
-  std::vector<char> down(state_.size(), 0);
-  for (size_t g = 0; g < state_.size(); ++g) down[g] = running_ && !state_[g].reported_healthy;
+  std::vector<char> down(table_keys_.size(), 0);
+  for (size_t g = 0; g < table_keys_.size(); ++g) {
+    if (table_keys_[g].empty()) continue;
+    auto it = state_.find(table_keys_[g]);
+    down[g] = running_ && it != state_.end() && !it->second.reported_healthy;
+  }
   for (int g : held_unhealthy)
     if (g >= 0 && g < static_cast<int>(down.size())) down[g] = 1;
   for (size_t g = 0; g < down.size(); ++g)
@@ -274,19 +342,33 @@ void HealthMonitor::attach_tables(std::vector<std::shared_ptr<DeviceTable>> tabl
 
 void HealthMonitor::set_bad_page_thresholds(std::vector<int> thresholds) {
   std::lock_guard<std::mutex> lk(mu_);
-  page_thresholds_ = std::move(thresholds);
+  for (size_t g = 0; g < thresholds.size() && g < table_keys_.size(); ++g)
+    if (!table_keys_[g].empty()) state_[table_keys_[g]].page_threshold = thresholds[g];
 }
 
 void HealthMonitor::set_disabled_checks(int mask) {
   std::lock_guard<std::mutex> lk(mu_);
   disabled_ = mask & kCheckAll;
-  for (size_t g = 0; g < state_.size(); ++g) reconcile_locked(static_cast<int>(g), kEvtNone, "health checks changed");
+  std::vector<std::string> keys;
+  for (const auto& kv : state_) keys.push_back(kv.first);
+  std::sort(keys.begin(), keys.end());  // deterministic update order
+  for (const auto& k : keys) reconcile_locked(k, kEvtNone, "health checks changed");
 }
 
 bool HealthMonitor::gpu_healthy(int gpu) const {
   std::lock_guard<std::mutex> lk(mu_);
-  if (gpu < 0 || gpu >= static_cast<int>(state_.size())) return false;
-  return state_[gpu].reported_healthy;
+  if (gpu < 0 || gpu >= static_cast<int>(table_keys_.size()) || table_keys_[gpu].empty()) return false;
+  auto it = state_.find(table_keys_[gpu]);
+  return it == state_.end() || it->second.reported_healthy;
+}
+
+std::vector<std::string> HealthMonitor::unhealthy_keys() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<std::string> out;
+  for (const auto& kv : state_)
+    if (!kv.second.reported_healthy) out.push_back(kv.first);
+  std::sort(out.begin(), out.end());
+  return out;
 }
 
 }  // namespace amdgpu_dp

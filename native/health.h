@@ -17,7 +17,9 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "backend.h"
@@ -39,12 +41,15 @@ enum HealthCheck : int {
 struct HealthUpdate {
   int64_t ts_ns = 0;
   int kind = kEvtNone;
-  int gpu = -1;
+  int gpu = -1;        // index in the attached tables' inventory; -1 = not advertised now
   int partition = -1;
   int healthy = -1;  // 1 healthy, 0 unhealthy, -1 = not a health change (link/info)
   int peer = -1;     // link events
   int link_up = -1;
   std::string reason;
+  std::string key;       // identity of `gpu` (Backend::gpu_key): what the state belongs to
+  std::string peer_key;
+  double link_gbps = 0;  // kEvtLinkQuality: the link's trained bandwidth now
 };
 
 class HealthMonitor {
@@ -52,6 +57,12 @@ class HealthMonitor {
   explicit HealthMonitor(std::shared_ptr<Backend> backend, int lost_after_failures = 3);
   ~HealthMonitor();
 
+  // The advertised inventory, in the tables' index order: keys[i] is the identity
+  // (Backend::gpu_key) of GPU i.  Health state is kept per identity, so a re-enumeration
+  // that moves a GPU to another index moves its state with it, and a GPU that vanished
+  // keeps its state (e.g. mid-reset) until it returns.
+  void set_gpus(std::vector<std::string> keys);
+  // Legacy form for backends without identities: GPU i is "#i".
   void set_gpu_count(int n);
   void start();
   void stop();
@@ -75,12 +86,15 @@ class HealthMonitor {
   void set_fast_recover(bool on);
   // Plugin reload: installs the new tables as the fast tables and, under the same lock
   // that orders every transition, marks Unhealthy in them each GPU the monitor reports
-  // unhealthy or the caller holds back (`held_unhealthy`, e.g. a pending recovery
-  // canary).  Call after set_gpu_count.
+  // unhealthy or the caller holds back (`held_unhealthy`, table indices, e.g. a pending
+  // recovery canary).  Call after set_gpus.
   void attach_tables(std::vector<std::shared_ptr<DeviceTable>> tables, bool fast_recover,
                      const std::vector<int>& held_unhealthy);
-  // Per-GPU retired-page limits (index = GPU; <= 0 disables the check for that GPU).
+  // Per-GPU retired-page limits (index = table index of the GPU, as in set_gpus; <= 0
+  // disables the check for that GPU).
   void set_bad_page_thresholds(std::vector<int> thresholds);
+  // Identities the monitor holds state for that are unhealthy (advertised or not).
+  std::vector<std::string> unhealthy_keys() const;
   // Bitmask of HealthCheck values to ignore; re-evaluates every GPU (a GPU held only by a
   // check that is now off becomes Healthy).
   void set_disabled_checks(int mask);
@@ -95,22 +109,28 @@ class HealthMonitor {
     int failures = 0;
     int64_t last_ue = -1;
     bool reported_healthy = true;
-    std::map<int, int> link_up;  // peer -> 1/0
+    std::map<std::string, int> link_up;  // peer key -> 1/0
+    std::map<std::string, double> link_bw;  // peer key -> last trained bandwidth seen, Gb/s
+    int page_threshold = 0;
   };
   void loop();
   void emit_locked(HealthUpdate u);
-  void reconcile_locked(int gpu, int kind, const std::string& reason);
+  void reconcile_locked(const std::string& key, int kind, const std::string& reason);
   bool healthy_locked(const GpuState& st) const;
+  // Identity of backend index `gpu` (the index space of samples and events): the
+  // event's own key when it carries one, else the backend's, else "#<index>".
+  std::string key_of(int gpu, const std::string& given) const;
+  int table_index_locked(const std::string& key) const;  // -1 = not advertised
 
   std::shared_ptr<Backend> backend_;
   int lost_after_;
   mutable std::mutex mu_;
   std::condition_variable cv_;
   std::deque<HealthUpdate> queue_;
-  std::vector<GpuState> state_;
+  std::unordered_map<std::string, GpuState> state_;
+  std::vector<std::string> table_keys_;  // table index -> key
   std::vector<std::shared_ptr<DeviceTable>> fast_tables_;
   bool fast_recover_ = false;
-  std::vector<int> page_thresholds_;
   int disabled_ = 0;  // HealthCheck bits
   std::thread thread_;
   std::atomic<bool> running_{false};

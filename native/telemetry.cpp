@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <stdexcept>
 #include <cstdio>
 #include <cstring>
 #include <dirent.h>
@@ -135,32 +136,84 @@ void Exporter::set_extra(const std::string& rendered) {
 
 void Exporter::start(std::shared_ptr<Backend> backend, int interval_ms, std::shared_ptr<HealthMonitor> monitor) {
   stop();
+  std::weak_ptr<Exporter> weak = weak_from_this();
+  if (weak.expired()) throw std::logic_error("Exporter must be owned by a std::shared_ptr to start sampling");
   backend_ = std::move(backend);
   monitor_ = std::move(monitor);
   interval_ms_ = interval_ms > 0 ? interval_ms : 1000;
   stop_ = false;
   running_ = true;
+  {
+    std::lock_guard<std::mutex> lk(first_mu_);
+    first_done_ = false;
+  }
+  sampler_exit_ = std::make_shared<ThreadExit>();
   if (monitor_) watchdog_ = std::thread([this] { watchdog_loop(); });  // before the first call
-  sample_once();  // first sample synchronously: /metrics is populated before start() returns
-  thread_ = std::thread([this] { loop(); });
+  thread_ = std::thread(sampler_main, std::move(weak), sampler_exit_);
+  // /metrics is normally populated before start() returns, but a first amdsmi call that
+  // hangs (a wedged driver at start-up) must not keep the caller - the plugin manager,
+  // which still has kubelet restarts, /restart and health events to handle - from
+  // going on: wait for the first pass at most the stall threshold.
+  const int ms = stall_ms_.load();
+  std::unique_lock<std::mutex> lk(first_mu_);
+  cv_wait_ms(first_cv_, lk, ms > 0 ? ms : 10000, [&] { return first_done_; });
+}
+
+bool Exporter::ThreadExit::wait(int ms) {
+  std::unique_lock<std::mutex> lk(mu);
+  if (ms < 0) {
+    cv.wait(lk, [&] { return done; });
+    return true;
+  }
+  return cv_wait_ms(cv, lk, ms, [&] { return done; });
+}
+
+void Exporter::ThreadExit::mark() {
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    done = true;
+  }
+  cv.notify_all();
 }
 
 void Exporter::stop() {
-  if (!running_.load()) return;
+  if (!running_.exchange(false)) return;
   stop_ = true;
-  if (watchdog_.joinable()) watchdog_.join();
-  if (thread_.joinable()) thread_.join();
-  running_ = false;
+  const auto self_id = std::this_thread::get_id();
+  if (watchdog_.joinable()) {
+    if (watchdog_.get_id() == self_id) watchdog_.detach();
+    else watchdog_.join();
+  }
+  if (!thread_.joinable()) return;
+  if (thread_.get_id() == self_id) {  // the sampler dropped the last reference: it ends by itself
+    thread_.detach();
+    return;
+  }
+  // The sampler leaves its loop within one sleep slice, unless it is inside a backend
+  // call.  A call in flight past the stall threshold may never return (wedged driver):
+  // do not hang shutdown on it.  The sampler holds its own reference to this exporter
+  // for the whole pass, so leaving it behind is safe; it exits when the call returns.
+  const int ms = stall_ms_.load();
+  if (sampler_exit_->wait(ms > 0 ? ms + 200 : -1)) {
+    thread_.join();
+  } else {
+    abandoned_.fetch_add(1);
+    thread_.detach();
+  }
 }
 
 void Exporter::watchdog_loop() {
   while (!stop_.load()) {
     std::this_thread::sleep_for(std::chrono::milliseconds(50));
     const int ms = stall_ms_.load();
-    const int g = inflight_gpu_.load();  // then its start time: never older than g's call
-    const int64_t since = inflight_since_.load();
-    if (ms <= 0 || g < 0 || stalled_gpu_.load() == g) continue;
-    const int64_t age = mono_ns() - since;
+    if (ms <= 0) continue;
+    // Under inflight_mu_, which the sampler also takes to end a call: either the call
+    // is still in flight while the GPU is reported lost here (and the sampler's
+    // on_sample, which recovers it, comes after), or it has ended and nothing is reported.
+    std::lock_guard<std::mutex> lk(inflight_mu_);
+    const int g = inflight_gpu_.load();
+    if (g < 0 || stalled_gpu_.load() == g) continue;
+    const int64_t age = mono_ns() - inflight_since_.load();
     if (age <= static_cast<int64_t>(ms) * 1000000) continue;
     stalled_gpu_.store(g);
     HwEvent e;
@@ -171,22 +224,46 @@ void Exporter::watchdog_loop() {
   }
 }
 
-void Exporter::loop() {
-  int64_t next = mono_ns() + static_cast<int64_t>(interval_ms_) * 1000000;
-  while (!stop_.load()) {
-    const int64_t now = mono_ns();
-    if (now < next) {  // sleep in slices so stop() is prompt
-      const int64_t slice_ms = std::min<int64_t>(50, (next - now) / 1000000 + 1);
-      std::this_thread::sleep_for(std::chrono::milliseconds(slice_ms));
-      continue;
+void Exporter::sampler_main(std::weak_ptr<Exporter> weak, std::shared_ptr<ThreadExit> exit) {
+  // A strong reference only for the duration of each step: the exporter stays alive
+  // through a backend call (however long it blocks), and may be destroyed between
+  // steps, by whichever thread drops the last reference.  Nothing below touches it
+  // after the reference is released.
+  int64_t next = 0;  // mono ns of the next pass; 0 = now (first pass)
+  for (;;) {
+    int sleep_ms;
+    {
+      std::shared_ptr<Exporter> self = weak.lock();
+      if (!self) break;
+      sleep_ms = self->sampler_step(&next);
     }
-    sample_once();
-    next += static_cast<int64_t>(interval_ms_) * 1000000;  // fixed cadence, no drift
-    if (next < mono_ns()) next = mono_ns() + static_cast<int64_t>(interval_ms_) * 1000000;
+    if (sleep_ms < 0) break;
+    if (sleep_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(sleep_ms));
   }
+  exit->mark();
 }
 
-void Exporter::sample_once() {
+int Exporter::sampler_step(int64_t* next) {
+  if (stop_.load()) return -1;
+  const int64_t now = mono_ns();
+  if (*next != 0 && now < *next)  // sleep in slices so stop() is prompt
+    return static_cast<int>(std::min<int64_t>(50, (*next - now) / 1000000 + 1));
+  const bool first = *next == 0;
+  sample_once(true);
+  if (first) {
+    {
+      std::lock_guard<std::mutex> lk(first_mu_);
+      first_done_ = true;
+    }
+    first_cv_.notify_all();
+    *next = mono_ns();
+  }
+  *next += static_cast<int64_t>(interval_ms_) * 1000000;  // fixed cadence, no drift
+  if (*next < mono_ns()) *next = mono_ns() + static_cast<int64_t>(interval_ms_) * 1000000;
+  return 0;
+}
+
+void Exporter::sample_once(bool from_sampler) {
   std::lock_guard<std::mutex> slk(sample_mu_);
   std::shared_ptr<Backend> be = backend_;
   // The inventory may be a subset of the node (`devices: "4-7"`): sample, report health
@@ -203,13 +280,19 @@ void Exporter::sample_once() {
   std::vector<char> ok(n, 0);
   const int64_t t0 = mono_ns();
   for (size_t g = 0; g < n; ++g) {
+    if (from_sampler && stop_.load()) return;  // stop() is waiting: no more backend calls
     if (be) {
-      inflight_since_.store(mono_ns());
-      inflight_gpu_.store(index[g]);
+      {
+        std::lock_guard<std::mutex> lk(inflight_mu_);
+        inflight_since_.store(mono_ns());
+        inflight_gpu_.store(index[g]);
+      }
       ok[g] = be->sample(index[g], &samples[g]) ? 1 : 0;
-      inflight_gpu_.store(-1);
-      int stuck = index[g];
-      stalled_gpu_.compare_exchange_strong(stuck, -1);
+      {
+        std::lock_guard<std::mutex> lk(inflight_mu_);
+        inflight_gpu_.store(-1);
+        if (stalled_gpu_.load() == index[g]) stalled_gpu_.store(-1);
+      }
     }
     if (!ok[g]) sample_errors_.fetch_add(1, std::memory_order_relaxed);
     if (monitor_) monitor_->on_sample(index[g], ok[g], samples[g]);

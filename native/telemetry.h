@@ -9,6 +9,7 @@
 #pragma once
 
 #include <atomic>
+#include <condition_variable>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -55,7 +56,7 @@ struct PartitionLabel {
   std::string resource;
 };
 
-class Exporter {
+class Exporter : public std::enable_shared_from_this<Exporter> {
  public:
   Exporter();
   ~Exporter();
@@ -76,7 +77,11 @@ class Exporter {
   void set_stall_ms(int ms) { stall_ms_.store(ms > 0 ? ms : 0); }
   int stalled_gpu() const { return stalled_gpu_.load(); }
   // One synchronous sampling pass (also used before the first scrape).
-  void sample_once();
+  // from_sampler: the sampler thread's own pass (it ends early once stop() is waiting).
+  void sample_once(bool from_sampler = false);
+  // Samplers left running in a backend call that did not return within the stall
+  // threshold when stop() was called (each ends when its call returns).
+  int abandoned_samplers() const { return abandoned_.load(); }
 
   std::shared_ptr<const std::string> gpu_text() const;
   GpuSample last_sample(int gpu) const;
@@ -91,7 +96,15 @@ class Exporter {
   uint64_t samples_total() const { return samples_.load(); }
 
  private:
-  void loop();
+  struct ThreadExit {  // outlives the exporter: the sampler signals it after letting go
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false;
+    bool wait(int ms);  // ms < 0: no limit; true once the thread has exited
+    void mark();
+  };
+  static void sampler_main(std::weak_ptr<Exporter> weak, std::shared_ptr<ThreadExit> exit);
+  int sampler_step(int64_t* next);  // ms to sleep before the next step, -1 = stop
   void render_gpu_text(const std::vector<GpuSample>& samples, const std::vector<char>& ok, uint64_t inventory_gen);
   void render_process(std::string* out) const;  // reads /proc
   void render_process_cached(std::string* out) const;  // per-thread copy, refreshed each second
@@ -158,6 +171,12 @@ class Exporter {
   std::thread thread_;
   std::atomic<bool> running_{false};
   std::atomic<bool> stop_{false};
+  std::shared_ptr<ThreadExit> sampler_exit_;
+  std::mutex first_mu_;  // first pass of a start(): start() waits for it (bounded)
+  std::condition_variable first_cv_;
+  bool first_done_ = false;
+  std::atomic<int> abandoned_{0};
+  std::mutex inflight_mu_;  // orders a call's end against the watchdog's verdict on it
   std::mutex sample_mu_;  // serialises sampling passes
   std::atomic<uint64_t> samples_{0};
   std::atomic<uint64_t> sample_errors_{0};

@@ -181,3 +181,32 @@ def test_large_cpx_requests_pack_whole_gpus_fast(n):
         if size <= 16:
             assert len({g // 4 for g in per_gpu}) == 1, per_gpu  # one NUMA node
         assert dt < 0.02, dt
+
+
+def test_pod_link_load_steers_cross_gpu_pods_apart(n):
+    """CPX: GPUs 0, 1 and 2 each have 4 free partitions, a pod of 8 must span two GPUs.
+    With no other pod on any link the first pair wins (0+1); once a multi-GPU pod is
+    known to span GPUs 0 and 1 (kubelet PodResources), the new pod avoids sharing that
+    link."""
+    topo = n.Topology(4)
+    for a in range(4):
+        for b in range(a + 1, 4):
+            topo.set_link(a, b, n.Link(type=n.LINK_XGMI, hops=1, bw_gbps=608.0))
+    devs = [n.AllocDevice(g, p, 0, "g%dp%d" % (g, p)) for g in range(4) for p in range(8)]
+    avail = [g * 8 + p for g in range(3) for p in range(4, 8)]
+    gpus = lambda chosen: sorted({devs[i].gpu for i in chosen})  # noqa: E731
+    assert gpus(n.aligned_alloc(topo, devs, avail, [], 8)) == [0, 1]
+    topo.set_link(0, 1, n.Link(type=n.LINK_XGMI, hops=1, bw_gbps=608.0, pods=1))
+    assert gpus(n.aligned_alloc(topo, devs, avail, [], 8)) in ([0, 2], [1, 2])
+
+
+def test_table_link_setters_are_copy_on_write(n):
+    t = n.DeviceTable(n.TableConfig(), [n.TableDevice("a", 0), n.TableDevice("b", 1)], n.Topology(2))
+    before = t.topology()
+    t.set_link_bandwidth(0, 1, 304.0)
+    t.set_link_pods([0, 2, 2, 0])
+    after = t.topology()
+    assert after.link(0, 1).bw_gbps == after.link(1, 0).bw_gbps == 304.0
+    assert after.link(0, 1).pods == 2 and before.link(0, 1).pods == 0 and before.link(0, 1).bw_gbps == 0
+    t.set_link_pods([])
+    assert t.topology().link(0, 1).pods == 0

@@ -646,3 +646,87 @@ def test_kubelet_restart_that_wipes_plugin_sockets(make_cfg, plugin_dir, run_man
         assert os.path.exists(os.path.join(plugin_dir, "amd-gpu.sock"))
         assert k.client("amd-gpu.sock").get_options().get_preferred_allocation_available
         print("registrations", len(k.requests), m.counters)
+
+
+def test_health_follows_gpu_identity_through_rediscovery(make_cfg, plugin_dir, run_manager):
+    """GPU 0 enters a reset and falls off the bus; the periodic re-discovery re-advertises
+    the node with GPU 1 at index 0.  That GPU stays Healthy (state is keyed by identity,
+    not index); when GPU 0 returns it is advertised Unhealthy until its POST_RESET."""
+    from k8s_gpu_device_plugin_amd import native
+    n = native.load()
+    be = fixtures.build_backend("2gpu_spx")
+    gpus, _ = be.discover()
+    ids = [g.partitions[0].id for g in gpus]
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(telemetry={"intervalMs": 30}, rediscoverIntervalS=0.2,
+                                 health={"lostAfterFailures": 2}), backend=be)
+        k.wait_for_registrations(1)
+        table = lambda: m.plugins[0].table  # noqa: E731 - replaced by every reload
+        be.inject_event(n.HwEvent(n.EVT_PRE_RESET, 0, message="fixture reset"))
+        assert _wait(lambda: not table().healthy(ids[0]))
+        be.set_gpu_present(0, False)
+        assert _wait(lambda: table().ids() == [ids[1]], timeout=10)
+        time.sleep(0.4)  # several sampling passes and re-discoveries over the new indices
+        assert table().healthy(ids[1])
+        reg = k.wait_for_registrations(2, timeout=10)[-1]
+        _, devs = k.watch(reg.endpoint).next()
+        assert [(d, h) for d, h, _ in devs] == [(ids[1], "Healthy")]
+        be.set_gpu_present(0, True)
+        assert _wait(lambda: table().ids() == ids, timeout=10)
+        assert not table().healthy(ids[0]) and table().healthy(ids[1])
+        time.sleep(0.3)  # its telemetry answers again: still mid-reset, still Unhealthy
+        assert not table().healthy(ids[0])
+        be.inject_event(n.HwEvent(n.EVT_POST_RESET, 0))
+        assert _wait(lambda: table().healthy(ids[0]) and table().healthy(ids[1]))
+        assert _wait(lambda: m.monitor.unhealthy_keys() == [])
+
+
+def test_link_retrain_reaches_the_allocator(make_cfg, plugin_dir, run_manager):
+    """An up xGMI link re-trains at half its rate: the telemetry poll reports it, the
+    table's topology takes the new bandwidth, and a 2-GPU request that must include
+    GPU 0 moves off that link."""
+    be = fixtures.build_backend("4gpu_spx")
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(telemetry={"intervalMs": 30}), backend=be)
+        c = k.client(k.wait_for_registrations(1)[0].endpoint)
+        ids = m.plugins[0].table.ids()
+        assert m.plugins[0].table.topology().link(0, 1).bw_gbps == 608.0  # from discovery
+        assert list(c.preferred(ids, [ids[0]], 2).container_responses[0].deviceIDs) == ids[:2]
+        be.set_link_bandwidth(0, 1, 304.0)
+        assert _wait(lambda: m.plugins[0].table.topology().link(0, 1).bw_gbps == 304.0)
+        assert list(c.preferred(ids, [ids[0]], 2).container_responses[0].deviceIDs) == [ids[0], ids[2]]
+        be.set_link_bandwidth(0, 1, 608.0)
+        assert _wait(lambda: m.plugins[0].table.topology().link(0, 1).bw_gbps == 608.0)
+
+
+def test_halfrate_fixture_is_discovered_degraded(n):
+    gpus, topo = fixtures.build_backend("8gpu_spx_halfrate").discover()
+    from k8s_gpu_device_plugin_amd.parallel.topology import NodeTopology
+    assert NodeTopology(gpus, topo).degraded_links() == [(0, 1)]
+
+
+def test_pod_resources_feed_link_load_to_the_allocator(make_cfg, plugin_dir, run_manager, tmp_path):
+    """CPX: a running pod holds partitions on GPUs 0 and 1 (PodResources).  The tables'
+    topology counts it on link 0-1, /metrics shows it, and a new 2-GPU pod is placed off
+    that link."""
+    from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import PodResourcesStub
+    sock = str(tmp_path / "pod-resources" / "kubelet.sock")
+    stub = PodResourcesStub(sock).start()
+    try:
+        with KubeletStub(plugin_dir) as k:
+            m = run_manager(make_cfg(fixture="4gpu_cpx", migStrategy="single",
+                                     podResources={"enabled": True, "socket": sock, "intervalS": 0.05}))
+            c = k.client(k.wait_for_registrations(1)[0].endpoint)
+            ids = m.plugins[0].table.ids()  # 8 partitions per GPU, GPU-major
+            held = ids[0:4] + ids[8:12]
+            stub.set_pods([("ml", "ring-0", [("main", "amd.com/gpu", held)])])
+            assert _wait(lambda: m.plugins[0].table.topology().link(0, 1).pods == 1)
+            assert 'amdgpu_xgmi_link_pods{gpu="0",peer="1"} 1' in m.exporter.render()
+            avail = ids[4:8] + ids[12:16] + ids[20:24]  # 4 free on each of GPUs 0, 1, 2
+            got = list(c.preferred(avail, [], 8).container_responses[0].deviceIDs)
+            gpus = sorted({ids.index(x) // 8 for x in got})
+            assert gpus in ([0, 2], [1, 2]), gpus
+            stub.set_pods([])
+            assert _wait(lambda: m.plugins[0].table.topology().link(0, 1).pods == 0)
+    finally:
+        stub.stop()

@@ -330,3 +330,143 @@ def test_exporter_and_monitor_stop_right_after_start(n):
         ex.stop()
         m.stop()
     assert time.monotonic() - t0 < 15
+
+
+def test_health_follows_gpu_identity_across_reenumeration(n):
+    """GPU 0 starts a reset and drops off the bus; re-discovery moves GPU 1 to index 0.
+    Health is kept per identity, so the healthy GPU does not inherit the vanished one's
+    reset latch, and the vanished GPU is Unhealthy again when it returns, until its
+    POST_RESET (reference device/devices.go:41-85: device IDs are UUIDs)."""
+    be = fixtures.build_backend("2gpu_spx")
+    gpus, _ = be.discover()
+    keys = [be.gpu_key(g.index) for g in gpus]
+    assert keys == [g.uuid for g in gpus] and len(set(keys)) == 2
+    m = n.HealthMonitor(be, 3)
+    m.set_gpus(keys)
+    ids = [g.partitions[0].id for g in gpus]
+
+    def tables(gs):
+        return [n.DeviceTable(n.TableConfig(), [n.TableDevice(g.partitions[0].id, g.index) for g in gs],
+                              n.Topology(len(gs)))]
+
+    m.start()
+    try:
+        t = tables(gpus)
+        m.attach_tables(t, True, [])
+        be.inject_event(n.HwEvent(n.EVT_PRE_RESET, 0, message="fixture reset"))
+        deadline = time.monotonic() + 5
+        while time.monotonic() < deadline and t[0].healthy(ids[0]):
+            time.sleep(0.01)
+        assert not t[0].healthy(ids[0]) and t[0].healthy(ids[1])
+        u = [x for x in m.pop(100) if x.healthy == 0]
+        assert u and u[0].key == keys[0] and u[0].gpu == 0
+        # GPU 0 falls off the bus; the node is re-discovered and GPU 1 is now index 0
+        be.set_gpu_present(0, False)
+        gpus2, _ = be.discover()
+        assert [g.uuid for g in gpus2] == [keys[1]] and gpus2[0].index == 0
+        assert be.gpu_key(0) == keys[1]
+        s = be.sample(0)
+        assert s is not None and s.key == keys[1]  # index 0 now samples the old GPU 1
+        m.set_gpus([be.gpu_key(0)])
+        t2 = tables(gpus2)
+        m.attach_tables(t2, True, [])
+        assert t2[0].healthy(ids[1]) and m.gpu_healthy(0)
+        assert m.unhealthy_keys() == [keys[0]]
+        # a sampling pass over the new index space leaves it healthy
+        m.on_sample(0, True, be.sample(0))
+        assert m.gpu_healthy(0) and not [x for x in m.pop(50) if x.healthy == 0]
+        # the vanished GPU returns, still mid-reset: Unhealthy at once
+        be.set_gpu_present(0, True)
+        gpus3, _ = be.discover()
+        m.set_gpus([be.gpu_key(g.index) for g in gpus3])
+        t3 = tables(gpus3)
+        m.attach_tables(t3, True, [])
+        assert not t3[0].healthy(ids[0]) and t3[0].healthy(ids[1])
+        assert not m.gpu_healthy(0) and m.gpu_healthy(1)
+        be.inject_event(n.HwEvent(n.EVT_POST_RESET, 0))
+        deadline = time.monotonic() + 5
+        while time.monotonic() < deadline and not t3[0].healthy(ids[0]):
+            time.sleep(0.01)
+        assert t3[0].healthy(ids[0]) and m.gpu_healthy(0) and m.unhealthy_keys() == []
+    finally:
+        m.stop()
+
+
+def test_fixture_events_name_slots_and_arrive_in_discovery_indices(n):
+    """Scripted events name a fixture GPU by slot; delivered events carry the slot's
+    identity and its index in the latest discovery (-1 while it is not discovered)."""
+    be = fixtures.build_backend("4gpu_spx")
+    gpus, _ = be.discover()
+    uuid = [g.uuid for g in gpus]
+    be.set_gpu_present(1, False)
+    be.discover()
+    be.arm_events()
+    m = n.HealthMonitor(be, 3)
+    m.set_gpus([be.gpu_key(i) for i in range(3)])
+    assert [be.gpu_key(i) for i in range(3)] == [uuid[0], uuid[2], uuid[3]]
+    be.inject_event(n.HwEvent(n.EVT_LINK_DOWN, 3, peer=2))
+    be.inject_event(n.HwEvent(n.EVT_THERMAL, 1))
+    m.start()
+    try:
+        got = []
+        deadline = time.monotonic() + 5
+        while time.monotonic() < deadline and len(got) < 2:
+            got += m.pop(100)
+        link = [u for u in got if u.link_up == 0][0]
+        assert (link.gpu, link.peer, link.key, link.peer_key) == (2, 1, uuid[3], uuid[2])
+        info = [u for u in got if "thermal" in u.reason][0]
+        assert info.gpu == -1 and info.key == uuid[1]  # not advertised right now
+    finally:
+        m.stop()
+
+
+def test_exporter_start_and_stop_do_not_hang_on_a_wedged_first_call(n):
+    """The driver is already wedged when the plugin starts: start() must return after
+    the stall threshold (the manager still has an event loop to run), the watchdog marks
+    the GPU lost, and stop() returns too, leaving the stuck sampler behind (it holds its
+    own reference and ends when the call does)."""
+    be = fixtures.build_backend("2gpu_spx")
+    gpus, _ = be.discover()
+    m = n.HealthMonitor(be, 3)
+    m.set_gpus([be.gpu_key(g.index) for g in gpus])
+    ex = n.Exporter()
+    ex.set_inventory(gpus)
+    ex.set_stall_ms(300)
+    be.set_sample_stall(0, True)
+    try:
+        t0 = time.monotonic()
+        ex.start(be, 50, m)
+        assert 0.25 <= time.monotonic() - t0 < 3.0
+        deadline = time.monotonic() + 5
+        lost = []
+        while time.monotonic() < deadline and not lost:
+            lost = [u for u in m.pop(100) if u.healthy == 0]
+        assert lost and lost[0].gpu == 0 and "in flight" in lost[0].reason
+        t0 = time.monotonic()
+        ex.stop()
+        assert time.monotonic() - t0 < 3.0 and not ex.running
+        assert ex.abandoned_samplers == 1
+    finally:
+        be.set_sample_stall(0, False)  # the abandoned sampler's call returns; it exits
+    del ex
+    time.sleep(0.2)
+
+
+def test_watchdog_does_not_report_a_call_that_already_returned(n):
+    """Calls that return just under the threshold, over and over: the watchdog's check
+    and the sampler's end-of-call are ordered, so no GPU is ever reported lost."""
+    be = fixtures.build_backend("2gpu_spx")
+    gpus, _ = be.discover()
+    m = n.HealthMonitor(be, 3)
+    m.set_gpus([be.gpu_key(g.index) for g in gpus])
+    ex = n.Exporter()
+    ex.set_inventory(gpus)
+    ex.set_stall_ms(1000)
+    ex.start(be, 5, m)
+    try:
+        t_end = time.monotonic() + 1.0
+        while time.monotonic() < t_end:
+            assert not [u for u in m.pop(20) if u.healthy == 0]
+        assert m.gpu_healthy(0) and m.gpu_healthy(1)
+    finally:
+        ex.stop()
