@@ -63,7 +63,8 @@ def main(argv=None) -> int:
     except config_mod.ConfigError as e:
         print("fatal config error: %s" % e, file=sys.stderr)
         return 2
-    init_logger(cfg.log.level, cfg.log.fileDir or None, APP_NAME, console=cfg.log.console)
+    init_logger(cfg.log.level, cfg.log.fileDir or None, APP_NAME, console=cfg.log.console,
+                max_age_days=cfg.log.maxAgeDays)
     log = get_logger()
     log.info("Starting %s %s", APP_NAME, VERSION)
 

@@ -48,6 +48,7 @@ class LogConfig:
     level: str = "debug"
     fileDir: str = "./logs"
     console: bool = True
+    maxAgeDays: float = 30.0   # rotated files older than this are deleted (lumberjack MaxAge; 0 = keep)
 
 
 @dataclass
@@ -285,6 +286,8 @@ def validate(cfg: Config) -> Config:
         parse_level(cfg.log.level)
     except ValueError as e:
         raise ConfigError(str(e)) from None
+    if not cfg.log.maxAgeDays >= 0:
+        raise ConfigError("log.maxAgeDays must be >= 0 (0 keeps rotated files), got %r" % cfg.log.maxAgeDays)
     if cfg.backend not in ("auto", "amdsmi", "fixture"):
         raise ConfigError("backend must be auto|amdsmi|fixture, got %r" % cfg.backend)
     disabled_checks_mask(cfg.health.disabledChecks)

@@ -121,6 +121,8 @@ def set_gpu_mode(backend, gpu_index: int, compute: str, memory: str = "NPS1", fi
     g.compute_partition, g.memory_partition = compute.upper(), memory.upper()
     g.partitions = _partitions(n, gpu_index, g.uuid, PARTITIONS[g.compute_partition], g.numa_node,
                                g.vram_total_bytes, first_render)
+    g.partition_profile, g.profile_partitions = g.compute_partition, PARTITIONS[g.compute_partition]
+    g.profile_index = list(PARTITIONS).index(g.compute_partition)
     backend.replace_gpu(gpu_index, g)
 
 
@@ -150,6 +152,10 @@ def build_backend(spec):
         info.num_compute_units = int(g.get("num_cus", MI355X_CUS))
         info.bad_page_threshold = int(g.get("bad_page_threshold", -1))  # -1: RAS threshold not readable
         nparts = int(g.get("num_partitions", PARTITIONS.get(info.compute_partition, 1)))
+        # what amdsmi_get_gpu_accelerator_partition_profile reports for the mode
+        info.partition_profile = info.compute_partition
+        info.profile_partitions = int(g.get("profile_partitions", nparts))
+        info.profile_index = list(PARTITIONS).index(info.compute_partition) if info.compute_partition in PARTITIONS else -1
         info.num_xgmi_links = max(0, len(gpus) - 1)
         info.partitions = _partitions(n, gi, info.uuid, nparts, info.numa_node, info.vram_total_bytes, render)
         render += nparts

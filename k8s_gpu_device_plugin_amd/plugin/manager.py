@@ -44,6 +44,7 @@ EV_STOP, EV_RESTART, EV_RETRY, EV_KUBELET, EV_HEALTH, EV_REDISCOVER, EV_VERIFIED
 EV_METRICS = "metrics"  # state read by /metrics changed off the manager thread (canary results)
 EV_SOCKET_GONE = "socket_gone"  # a *.sock other than kubelet.sock was removed from the plugin dir
 HEALTH_LOG_LEN = 4096
+SERVER_CHECK_S = 1.0  # gRPC server supervision poll
 
 
 def inventory_signature(gpus) -> tuple:
@@ -154,16 +155,41 @@ class PluginManager:
         return t
 
     # ------------------------------------------------------------ loop
-    def _loop(self) -> None:
-        while True:
+    def _check_servers(self) -> bool:
+        """Supervises every plugin's gRPC server (polled about once a second, however
+        busy the queue is).  Returns False when a plugin reached its crash limit: the
+        manager then stops and the process exits non-zero."""
+        restarted = False
+        for p in self.plugins:
             try:
-                ev = self.events.get(timeout=1.0)
+                if p.check_server():
+                    restarted = True
+                    self.counters["restarts_server"] = self.counters.get("restarts_server", 0) + 1
+                    self.counters["registrations"] += 1
+            except Exception as e:
+                self.counters["load_failures"] += 1
+                log.error("restarting the gRPC server of %s failed: %s; retrying in %.0fs", p.resource, e,
+                          self.cfg.retrySeconds)
+                self._arm_retry()
+            if p.fatal_error:
+                self.fatal_error = p.fatal_error
+                log.critical("fatal: %s", p.fatal_error)
+                return False
+        if restarted:
+            self._publish_metrics()
+        return True
+
+    def _loop(self) -> None:
+        next_check = time.monotonic() + SERVER_CHECK_S
+        while True:
+            now = time.monotonic()
+            if now >= next_check:
+                if not self._check_servers():
+                    return
+                next_check = now + SERVER_CHECK_S
+            try:
+                ev = self.events.get(timeout=max(0.0, next_check - now))
             except queue.Empty:
-                for p in self.plugins:
-                    if p.fatal_error:
-                        self.fatal_error = p.fatal_error
-                        log.critical("fatal: %s", p.fatal_error)
-                        return
                 continue
             kind = ev[0]
             if kind == EV_STOP:

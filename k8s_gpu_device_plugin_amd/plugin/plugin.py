@@ -117,6 +117,10 @@ class AmdDevicePlugin:
         self._stopping = False
         self._supervisor: threading.Thread | None = None
         self.fatal_error: str | None = None
+        # Serve crash accounting (plugin/plugin.go:107-129), shared by both servers
+        self._crashes = 0
+        self._last_crash = time.monotonic()
+        self.server_restarts = 0
         self.registered = False
         # PreStartContainer verifier: fn(device ids) -> "" (pass) or an error message
         self.prestart_check = None
@@ -244,22 +248,51 @@ class AmdDevicePlugin:
                                             name="dp-supervise-" + self.resource.get_resource_name())
         self._supervisor.start()
 
+    def _note_crash(self, why: str) -> bool:
+        """Counts a server crash the way the reference's Serve loop does
+        (``plugin/plugin.go:107-129``): the count resets when the previous crash is more
+        than an hour old; more than 5 is fatal.  Returns True when fatal."""
+        now = time.monotonic()
+        self._crashes = 0 if now - self._last_crash > SERVE_CRASH_WINDOW_S else self._crashes + 1
+        self._last_crash = now
+        log.error("gRPC server for '%s' crashed with error: %s", self.resource, why)
+        if self._crashes > SERVE_CRASH_LIMIT:
+            self.fatal_error = "GRPC server for '%s' has repeatedly crashed recently. Quitting" % self.resource
+            log.critical(self.fatal_error)
+            return True
+        return False
+
+    def check_server(self) -> bool:
+        """Supervision of the native server, polled by the manager: a server whose worker
+        died or whose listener broke is restarted on a fresh socket and registered with
+        kubelet again.  Returns True if it was restarted.  Raises if the restart failed
+        (the manager's retry timer takes over); sets ``fatal_error`` after too many
+        crashes (the process then exits non-zero, as the reference's Fatal does)."""
+        srv = self._native_server
+        if srv is None or self._stopping or self.fatal_error:
+            return False
+        why = srv.failure()
+        if not why and srv.running:
+            return False
+        with self._lock:
+            if self._native_server is not srv or self._stopping:
+                return False
+        if self._note_crash(why or "server stopped unexpectedly"):
+            return False
+        self.server_restarts += 1
+        self.stop()
+        self.start()
+        return True
+
     def _supervise(self, server) -> None:
         """grpcio analogue of the Serve crash-restart loop (``plugin/plugin.go:107-129``):
         an unexpected termination restarts the server, >5 crashes within an hour is fatal."""
-        crashes, last = 0, time.monotonic()
         while True:
             server.wait_for_termination()
             with self._lock:
                 if self._stopping or self._server is not server:
                     return
-            now = time.monotonic()
-            crashes = 0 if now - last > SERVE_CRASH_WINDOW_S else crashes + 1
-            last = now
-            log.error("gRPC server for %s terminated unexpectedly", self.resource)
-            if crashes > SERVE_CRASH_LIMIT:
-                self.fatal_error = "gRPC server for '%s' has repeatedly crashed recently" % self.resource
-                log.critical(self.fatal_error)
+            if self._note_crash("terminated unexpectedly"):
                 return
             with self._lock:
                 self._serving = False

@@ -70,15 +70,28 @@ class _LevelBand(logging.Filter):
         return self.lo <= record.levelno <= self.hi
 
 
+MAX_AGE_DAYS = 30               # log.go:20 MaxAge
+
+
 def _gzip_rotator(source: str, dest: str) -> None:
     with open(source, "rb") as fi, gzip.open(dest, "wb") as fo:
         shutil.copyfileobj(fi, fo)
     os.remove(source)
 
 
+def _make_rotator(file_dir: str, app: str, max_age_days: float):
+    def rotate(source: str, dest: str) -> None:
+        _gzip_rotator(source, dest)
+        prune_old_logs(file_dir, max_age_days, app)  # lumberjack prunes on every rotation too
+    return rotate
+
+
 def init_logger(level: str = "debug", file_dir: str | None = "./logs", app: str = "k8s-gpu-device-plugin",
-                console: bool = True, max_bytes: int = MAX_BYTES, backups: int = BACKUP_COUNT) -> logging.Logger:
-    """Configures and returns the package logger (idempotent: replaces handlers)."""
+                console: bool = True, max_bytes: int = MAX_BYTES, backups: int = BACKUP_COUNT,
+                max_age_days: float = MAX_AGE_DAYS) -> logging.Logger:
+    """Configures and returns the package logger (idempotent: replaces handlers).
+    Rotated files older than ``max_age_days`` are deleted at start and after every
+    rotation (lumberjack MaxAge; 0 keeps them)."""
     logger = logging.getLogger(LOGGER_NAME)
     logger.setLevel(parse_level(level))
     for h in list(logger.handlers):
@@ -88,12 +101,13 @@ def init_logger(level: str = "debug", file_dir: str | None = "./logs", app: str 
     fmt = JsonFormatter()
     if file_dir:
         os.makedirs(file_dir, exist_ok=True)
+        prune_old_logs(file_dir, max_age_days, app)
         bands = [("debug", logging.DEBUG, logging.DEBUG), ("info", logging.INFO, logging.INFO),
                  ("warn", logging.WARNING, logging.WARNING), ("error", logging.ERROR, logging.CRITICAL)]
         for name, lo, hi in bands:
             h = logging.handlers.RotatingFileHandler(os.path.join(file_dir, "%s-%s.log" % (app, name)),
                                                      maxBytes=max_bytes, backupCount=backups, encoding="utf-8")
-            h.rotator = _gzip_rotator
+            h.rotator = _make_rotator(file_dir, app, max_age_days)
             h.namer = lambda n: n + ".gz"
             h.addFilter(_LevelBand(lo, hi))
             h.setFormatter(fmt)
@@ -110,15 +124,21 @@ def get_logger(name: str | None = None) -> logging.Logger:
     return base.getChild(name) if name else base
 
 
-def prune_old_logs(file_dir: str, max_age_days: int = 30) -> int:
-    """lumberjack ``MaxAge`` (30 days, ``log.go:20``): deletes rotated files older than that."""
-    if not os.path.isdir(file_dir):
+def prune_old_logs(file_dir: str, max_age_days: float = MAX_AGE_DAYS, app: str = "") -> int:
+    """lumberjack ``MaxAge`` (30 days, ``log.go:20``): deletes rotated (``.gz``) files of
+    ``app`` older than that; the live log files are never touched.  0 disables."""
+    if not max_age_days or max_age_days <= 0 or not os.path.isdir(file_dir):
         return 0
     cutoff = time.time() - max_age_days * 86400
     n = 0
     for f in os.listdir(file_dir):
+        if not f.endswith(".gz") or (app and not f.startswith(app + "-")):
+            continue
         p = os.path.join(file_dir, f)
-        if f.endswith(".gz") and os.path.getmtime(p) < cutoff:
-            os.remove(p)
-            n += 1
+        try:
+            if os.path.getmtime(p) < cutoff:
+                os.remove(p)
+                n += 1
+        except OSError:  # rotated away concurrently
+            pass
     return n

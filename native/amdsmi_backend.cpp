@@ -87,7 +87,19 @@ struct Proc {
   uint32_t partition_id;
 };
 
-// Processors a compute-partition mode implies on CDNA3/4 (8 XCDs on MI355X); 0 = unknown.
+const char* profile_type_name(amdsmi_accelerator_partition_type_t t) {
+  switch (t) {
+    case AMDSMI_ACCELERATOR_PARTITION_SPX: return "SPX";
+    case AMDSMI_ACCELERATOR_PARTITION_DPX: return "DPX";
+    case AMDSMI_ACCELERATOR_PARTITION_TPX: return "TPX";
+    case AMDSMI_ACCELERATOR_PARTITION_QPX: return "QPX";
+    case AMDSMI_ACCELERATOR_PARTITION_CPX: return "CPX";
+    default: return "";
+  }
+}
+
+// Fallback only: processors a compute-partition mode implies on CDNA3/4 (8 XCDs on
+// MI355X), used when the driver reports no accelerator partition profile; 0 = unknown.
 int partitions_of_mode(const std::string& mode) {
   if (mode == "SPX") return 1;
   if (mode == "DPX") return 2;
@@ -160,7 +172,7 @@ class AmdSmiBackend : public Backend {
     // list no longer matches the mode the GPU reports: re-initialise and enumerate again.
     bool stale = false;
     for (const auto& g : *gpus) {
-      const int want = partitions_of_mode(g.compute_partition);
+      const int want = g.profile_partitions > 0 ? g.profile_partitions : partitions_of_mode(g.compute_partition);
       if (want > 0 && want != static_cast<int>(g.partitions.size())) stale = true;
     }
     if (stale && reinit_locked()) discover_locked(gpus, topo);
@@ -266,6 +278,20 @@ class AmdSmiBackend : public Backend {
       amdsmi_memory_partition_config_t mcfg{};
       if (amdsmi_get_gpu_memory_partition_config(h0, &mcfg) == AMDSMI_STATUS_SUCCESS)
         g.nps_caps = mcfg.partition_caps.nps_cap_mask & 0xF;
+      // The driver's own profile of the current mode: partition count and NPS caps
+      // come from it rather than from a table keyed by the mode string.
+      amdsmi_accelerator_partition_profile_t prof;
+      std::memset(&prof, 0, sizeof(prof));
+      uint32_t part_ids[AMDSMI_MAX_ACCELERATOR_PARTITIONS] = {};
+      if (amdsmi_get_gpu_accelerator_partition_profile(h0, &prof, part_ids) == AMDSMI_STATUS_SUCCESS &&
+          prof.num_partitions > 0 && prof.num_partitions <= AMDSMI_MAX_ACCELERATOR_PARTITIONS &&
+          profile_type_name(prof.profile_type)[0] != '\0') {
+        g.partition_profile = profile_type_name(prof.profile_type);
+        g.profile_partitions = static_cast<int>(prof.num_partitions);
+        g.profile_index = static_cast<int>(prof.profile_index);
+        if (g.compute_partition.empty()) g.compute_partition = g.partition_profile;
+        if (g.nps_caps == 0) g.nps_caps = prof.memory_caps.nps_cap_mask & 0xF;
+      }
       if (g.compute_partition.empty()) g.compute_partition = plist.size() == 1 ? "SPX" : "UNKNOWN";
       if (g.memory_partition.empty()) g.memory_partition = "NPS1";
       uint32_t thr = 0;  // needs root; -1 when not readable

@@ -59,6 +59,12 @@ struct GpuInfo {
   std::string compute_partition;  // SPX/DPX/TPX/QPX/CPX
   std::string memory_partition;   // NPS1/NPS2/NPS4/NPS8
   uint32_t nps_caps = 0;          // bit0 NPS1, bit1 NPS2, bit2 NPS4, bit3 NPS8
+  // The accelerator partition profile the driver reports for the current mode
+  // (amdsmi_get_gpu_accelerator_partition_profile): its type and partition count.
+  // Empty / 0 when the driver does not report one; the mode string decides then.
+  std::string partition_profile;
+  int profile_partitions = 0;
+  int profile_index = -1;
   int num_compute_units = 0;
   int num_xgmi_links = 0;
   int bad_page_threshold = -1;    // RAS retired-page threshold (-1 = not readable)

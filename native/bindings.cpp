@@ -65,6 +65,9 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("compute_partition", &GpuInfo::compute_partition)
       .def_readwrite("memory_partition", &GpuInfo::memory_partition)
       .def_readwrite("nps_caps", &GpuInfo::nps_caps)
+      .def_readwrite("partition_profile", &GpuInfo::partition_profile)
+      .def_readwrite("profile_partitions", &GpuInfo::profile_partitions)
+      .def_readwrite("profile_index", &GpuInfo::profile_index)
       .def_readwrite("num_compute_units", &GpuInfo::num_compute_units)
       .def_readwrite("num_xgmi_links", &GpuInfo::num_xgmi_links)
       .def_readwrite("bad_page_threshold", &GpuInfo::bad_page_threshold)
@@ -565,7 +568,9 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("shed_connections", &GrpcServer::shed_connections)
       .def_property_readonly("connections", &GrpcServer::connections)
       .def_property_readonly("worker_connections", &GrpcServer::worker_connections)
-      .def_property_readonly("socket_path", &GrpcServer::socket_path);
+      .def_property_readonly("socket_path", &GrpcServer::socket_path)
+      .def("failure", &GrpcServer::failure)
+      .def("inject_fault", &GrpcServer::inject_fault);
 
   py::class_<H2Client>(m, "H2Client")
       .def(py::init<std::string, double>(), py::arg("socket_path"), py::arg("timeout_s") = 5.0,

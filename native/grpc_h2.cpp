@@ -359,7 +359,12 @@ void GrpcServer::start() {
     epoll_ctl(w->ep, EPOLL_CTL_ADD, w->done->efd, &ev3);
     workers_.push_back(std::move(w));
   }
-  for (auto& w : workers_) threads_.emplace_back([this, wp = w.get(), t = table_] { run(wp, t); });
+  failed_ = false;
+  {
+    std::lock_guard<std::mutex> fk(fail_mu_);
+    fail_reason_.clear();
+  }
+  for (auto& w : workers_) threads_.emplace_back([this, wp = w.get(), t = table_] { run_guarded(wp, t); });
   std::lock_guard<std::mutex> nk(notifier_->mu);
   notifier_->srv = this;
 }
@@ -408,6 +413,55 @@ void GrpcServer::stop() {
   if (listen_fd_ >= 0) ::close(listen_fd_);
   listen_fd_ = -1;
   ::unlink(path_.c_str());
+}
+
+void GrpcServer::fail(const std::string& why) {
+  std::lock_guard<std::mutex> lk(fail_mu_);
+  if (failed_.exchange(true)) return;  // the first fault is the one reported
+  fail_reason_ = why;
+}
+
+std::string GrpcServer::failure() const {
+  std::lock_guard<std::mutex> lk(fail_mu_);
+  return fail_reason_;
+}
+
+void GrpcServer::inject_fault(const std::string& kind) {
+  if (kind == "worker") {
+    std::lock_guard<std::mutex> lk(mu_);
+    inject_worker_fault_.store(1);
+    for (auto& w : workers_) {  // wake one at once rather than at its 100 ms poll
+      const uint64_t one = 1;
+      if (w->efd >= 0) (void)!write(w->efd, &one, sizeof(one));
+      break;
+    }
+  } else if (kind == "listener") {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (listen_fd_ >= 0) ::shutdown(listen_fd_, SHUT_RDWR);
+  } else {
+    throw std::invalid_argument("inject_fault: unknown kind " + kind);
+  }
+}
+
+void GrpcServer::run_guarded(Worker* w, std::shared_ptr<DeviceTable> table) {
+  try {
+    run(w, std::move(table));
+    return;
+  } catch (const std::exception& e) {
+    fail(std::string("gRPC worker died: ") + e.what());
+  } catch (...) {
+    fail("gRPC worker died: unknown exception");
+  }
+  // the dead worker's connections can no longer be served: close them, so their
+  // clients (kubelet) see the failure at once instead of a silent stall
+  for (auto& kv : w->conns) {
+    epoll_ctl(w->ep, EPOLL_CTL_DEL, kv.first, nullptr);
+    ::close(kv.first);
+    conns_.fetch_sub(1);
+  }
+  w->conns.clear();
+  w->load.store(1 << 20, std::memory_order_relaxed);  // never picked for a new connection
+  if (listen_fd_ >= 0) epoll_ctl(w->ep, EPOLL_CTL_DEL, listen_fd_, nullptr);
 }
 
 void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
@@ -837,6 +891,10 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
   const int64_t admission_ns = static_cast<int64_t>(admission_poll_us_) * 1000;
   int64_t spin_until = 0;  // busy-poll window end (mono ns); 0 = closed
   while (!stop_.load(std::memory_order_relaxed)) {
+    if (inject_worker_fault_.load(std::memory_order_relaxed)) {
+      int armed = 1;
+      if (inject_worker_fault_.compare_exchange_strong(armed, 0)) throw std::runtime_error("injected worker fault");
+    }
     int n;
     if (spin_until != 0) {
       n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), 0);
@@ -885,13 +943,25 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
         continue;
       }
       if (fd == listen_fd_) {
+        if (evs[i].events & (EPOLLERR | EPOLLHUP)) {  // the listening socket itself broke
+          epoll_ctl(w->ep, EPOLL_CTL_DEL, listen_fd_, nullptr);
+          fail("listening socket " + path_ + " reported an error");
+          continue;
+        }
         for (;;) {
           bool shed = false;
           const int cfd = accept_or_shed(listen_fd_, nullptr, nullptr, &spare, &shed);
           if (cfd < 0) {
-            if (!shed) break;
-            shed_.add();
-            continue;
+            if (shed) {
+              shed_.add();
+              continue;
+            }
+            if (errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) {
+              const int e = errno;
+              epoll_ctl(w->ep, EPOLL_CTL_DEL, listen_fd_, nullptr);
+              fail("accept on " + path_ + ": " + strerror(e));
+            }
+            break;
           }
           Worker* t = w;  // least-loaded worker, this one on a tie
           for (auto& o : workers_)

@@ -44,6 +44,15 @@ class GrpcServer {
   void stop();   // idempotent: trailers for open streams, GOAWAY, close, unlink socket
   void notify(); // wake ListAndWatch streams now (health changed)
   bool running() const { return running_.load(); }
+  // Supervision (reference: the Serve crash-restart loop, plugin/plugin.go:107-129): a
+  // worker thread that died on an exception, or a listener that broke (accept errors,
+  // EPOLLERR/HUP on the socket), leaves the server unable to serve.  failure() names
+  // the first such fault ("" while healthy); the plugin manager polls it and restarts
+  // the server on a fresh socket.
+  std::string failure() const;
+  // Test-only fault injection: "worker" (the next worker to wake throws) or "listener"
+  // (the listening socket is shut down underneath the workers).
+  void inject_fault(const std::string& kind);
   uint64_t requests() const { return requests_.load(); }
   uint64_t shed_connections() const { return shed_.load(); }  // closed at accept: out of fds
   int connections() const { return conns_.load(); }
@@ -66,6 +75,12 @@ class GrpcServer {
   // `table` is handed over at thread creation: a worker never takes mu_, which stop()
   // holds while it joins the workers (one not yet scheduled when stop() ran deadlocked)
   void run(Worker* w, std::shared_ptr<DeviceTable> table);
+  void run_guarded(Worker* w, std::shared_ptr<DeviceTable> table);  // run() + fault capture
+  void fail(const std::string& why);
+  std::atomic<bool> failed_{false};
+  std::atomic<int> inject_worker_fault_{0};
+  mutable std::mutex fail_mu_;
+  std::string fail_reason_;
   std::shared_ptr<Notifier> notifier_ = std::make_shared<Notifier>();
   std::string path_;
   int nthreads_;

@@ -156,3 +156,77 @@ def test_shipped_configs_are_valid():
     assert {"/var/lib/kubelet/device-plugins", "/dev/kfd", "/dev/dri"} <= mounts
     assert os.path.dirname(cfg.nodeFeatureFile) in mounts
     assert cfg.podResources.enabled and os.path.dirname(cfg.podResources.socket) in mounts
+    # /dev/kfd must be openable inside the pod for amdsmi event notification: a hostPath
+    # mount alone is not in the device cgroup; privileged grants it
+    c = ds["containers"][0]
+    sc = c.get("securityContext", {})
+    assert sc.get("privileged") is True, "no /dev/kfd access path: health events would never arm"
+    assert "allowPrivilegeEscalation" not in sc  # rejected by the API server together with privileged
+    vols = {v["name"]: v for v in ds["volumes"]}
+    kfd = [m for m in c["volumeMounts"] if m["mountPath"] == "/dev/kfd"][0]
+    assert vols[kfd["name"]]["hostPath"]["path"] == "/dev/kfd"
+    assert cfg.health.enabled and cfg.grpc.server == "native"
+    assert c["image"].startswith("amdgpu-device-plugin:")
+    assert c["args"] == ["--configFile", "/etc/amdgpu-dp/config.yml"]
+
+
+def test_container_image_builds_the_native_libraries():
+    """deploy/Dockerfile builds what the DaemonSet runs: the in-tree native core and the
+    gfx950 canary via _build, the config path the DaemonSet passes, no run-time builds."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "deploy", "Dockerfile")) as f:
+        text = f.read()
+    assert "python3 -m k8s_gpu_device_plugin_amd._build" in text
+    assert "AMDGPU_DP_NO_AUTOBUILD=1" in text
+    assert 'ENTRYPOINT ["python3", "-m", "k8s_gpu_device_plugin_amd"]' in text
+    assert "/etc/amdgpu-dp/config.yml" in text
+    for src in ("COPY k8s_gpu_device_plugin_amd", "COPY native"):
+        assert src in text
+
+
+def test_log_max_age_prunes_rotated_files(tmp_path):
+    """lumberjack MaxAge (30 days, modules/log/log.go:20,93,137): rotated files older
+    than log.maxAgeDays are deleted when the logger starts and after every rotation;
+    live files, young backups and other programs' files are kept."""
+    import gzip
+    import logging
+    import time
+    from k8s_gpu_device_plugin_amd.utils import log as L
+    d = tmp_path / "logs"
+    d.mkdir()
+    old = time.time() - 31 * 86400
+    for name in ("app-info.log.1.gz", "app-error.log.3.gz", "other-info.log.1.gz"):
+        with gzip.open(d / name, "wb") as f:
+            f.write(b"x")
+        os.utime(d / name, (old, old))
+    with gzip.open(d / "app-info.log.2.gz", "wb") as f:  # 1 day old: kept
+        f.write(b"y")
+    young = time.time() - 86400
+    os.utime(d / "app-info.log.2.gz", (young, young))
+    logger = L.init_logger("debug", str(d), "app", console=False, max_bytes=200, backups=10, max_age_days=30)
+    try:
+        left = sorted(os.listdir(d))
+        assert "app-info.log.1.gz" not in left and "app-error.log.3.gz" not in left
+        assert "app-info.log.2.gz" in left and "other-info.log.1.gz" in left
+        # an aged backup that appears later goes at the next rotation
+        with gzip.open(d / "app-warn.log.9.gz", "wb") as f:
+            f.write(b"z")
+        os.utime(d / "app-warn.log.9.gz", (old, old))
+        for i in range(20):
+            logger.info("line %d %s", i, "x" * 40)
+        left = sorted(os.listdir(d))
+        assert "app-warn.log.9.gz" not in left
+        assert any(f.startswith("app-info.log.") and f.endswith(".gz") for f in left)  # rotation happened
+        assert L.prune_old_logs(str(d), 0, "app") == 0  # 0 keeps everything
+    finally:
+        for h in list(logger.handlers):
+            logger.removeHandler(h)
+            h.close()
+        L.init_logger("info", None, console=False)
+
+
+def test_log_max_age_config_validation():
+    from k8s_gpu_device_plugin_amd import config
+    assert config.validate(config.from_dict({"log": {"maxAgeDays": 7}})).log.maxAgeDays == 7
+    with pytest.raises(config.ConfigError):
+        config.validate(config.from_dict({"log": {"maxAgeDays": -1}}))

@@ -56,6 +56,26 @@ def test_amdsmi_discovers_mi355x(amdsmi_backend):
                           len(x.partitions), x.numa_node, x.num_compute_units) for x in gpus])
 
 
+def test_partition_profile_comes_from_amdsmi(amdsmi_backend):
+    """The partition count is the driver's accelerator partition profile
+    (amdsmi_get_gpu_accelerator_partition_profile; reference resources.go:43-51 asks the
+    driver for MIG profiles too), and it agrees with the processors amdsmi enumerated
+    for the box's current mode."""
+    gpus, _ = amdsmi_backend.discover()
+    seen = []
+    for g in gpus:
+        seen.append((g.index, g.compute_partition, g.partition_profile, g.profile_partitions, g.profile_index,
+                     len(g.partitions), g.nps_caps))
+        if g.profile_partitions:
+            assert g.partition_profile == g.compute_partition, seen[-1]
+            assert g.profile_partitions == len(g.partitions), seen[-1]
+    print("partition profiles", seen)
+    assert any(x[3] for x in seen), "amdsmi reported no accelerator partition profile: %s" % seen
+    assert amdsmi_backend.gpu_key(0) == (gpus[0].uuid or gpus[0].bdf)
+    s = amdsmi_backend.sample(0)
+    assert s is not None and s.key == amdsmi_backend.gpu_key(0)
+
+
 def test_amdsmi_telemetry(amdsmi_backend):
     gpus, _ = amdsmi_backend.discover()
     s = amdsmi_backend.sample(0)

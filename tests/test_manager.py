@@ -730,3 +730,47 @@ def test_pod_resources_feed_link_load_to_the_allocator(make_cfg, plugin_dir, run
             assert _wait(lambda: m.plugins[0].table.topology().link(0, 1).pods == 0)
     finally:
         stub.stop()
+
+
+@pytest.mark.parametrize("fault", ["worker", "listener"])
+def test_native_server_fault_is_restarted_and_reregistered(make_cfg, plugin_dir, run_manager, fault):
+    """The native gRPC server loses a worker (exception) or its listening socket: the
+    manager's supervision poll restarts it on a fresh socket and registers again
+    (reference Serve crash-restart loop, plugin/plugin.go:107-129)."""
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(grpc={"server": "native"}))
+        k.wait_for_registrations(1)
+        srv = m.plugins[0]._native_server
+        srv.inject_fault(fault)
+        assert _wait(lambda: srv.failure() != "", timeout=3)
+        k.wait_for_registrations(2, timeout=10)
+        assert _wait(lambda: m.counters.get("restarts_server", 0) == 1)
+        assert m.plugins[0]._native_server is not srv and not m.plugins[0]._native_server.failure()
+        c = k.client("amd-gpu.sock")
+        ids = m.plugins[0].table.ids()
+        assert c.allocate(ids[:1]).container_responses[0].devices
+        assert m.fatal_error is None and m.running
+
+
+def test_native_server_crash_loop_is_fatal(make_cfg, plugin_dir):
+    """More than 5 crashes within an hour: the manager stops with fatal_error set (the
+    CLI exits non-zero), like the reference's Logger.Fatal."""
+    with KubeletStub(plugin_dir) as k:
+        m = PluginManager(make_cfg(grpc={"server": "native"}))
+        t = m.start_background()
+        try:
+            k.wait_for_registrations(1)
+            for i in range(6):
+                p = m.plugins[0]
+                srv = p._native_server
+                srv.inject_fault("worker")
+                if i < 5:  # restarted and registered again before the next fault
+                    k.wait_for_registrations(i + 2, timeout=10)
+                    assert _wait(lambda: p._native_server is not srv and p.registered)
+            t.join(10)
+            assert not t.is_alive()
+            assert m.fatal_error and "repeatedly crashed" in m.fatal_error
+            assert m.counters["restarts_server"] == 5
+        finally:
+            m.stop()
+            t.join(10)
