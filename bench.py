@@ -138,8 +138,16 @@ def _allocator_probe(n) -> float:
     return round(_pct(lat[200:], 0.5) * 1e6, 2)
 
 
+def resolve_backend(n, requested: str = "auto") -> str:
+    """amdsmi when asked for, or when auto and amdsmi sees a GPU; else the fixture node
+    model (CPU runs, and multi-rank rehearsals on a box with fewer GPUs than ranks)."""
+    if requested == "auto":
+        return "amdsmi" if n.amdsmi_available() else "fixture"
+    return requested
+
+
 def start_daemon(n_gpus: int, grpc_server: str, workdir: str, profile_dir: str = "", busy_poll_us=None,
-                 admission_poll_us=None, overrides=None):
+                 admission_poll_us=None, overrides=None, backend: str = "auto"):
     """Rank 0: kubelet stub + plugin daemon subprocess.  Must run before GPU init.
     ``overrides``: config sections merged over the bench's own (probes, A/B runs)."""
     import yaml
@@ -148,7 +156,7 @@ def start_daemon(n_gpus: int, grpc_server: str, workdir: str, profile_dir: str =
     from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import KubeletStub
 
     n = native.load()
-    backend = "amdsmi" if n.amdsmi_available() else "fixture"
+    backend = resolve_backend(n, backend)
     plugin_dir = os.path.join(workdir, "device-plugins")
     os.makedirs(plugin_dir, exist_ok=True)
     kubelet = KubeletStub(plugin_dir).start()
@@ -198,6 +206,8 @@ def main() -> int:
     ap.add_argument("--admission-poll-us", type=int, default=None,
                     help="override grpc.admissionPollUs of the daemon (default: the config default)")
     ap.add_argument("--profile-dir", default="", help="run the daemon with benchmark: true, profiles here")
+    ap.add_argument("--backend", choices=["auto", "amdsmi", "fixture"], default="auto",
+                    help="daemon backend (auto: amdsmi when it sees a GPU); the canary runs only on amdsmi")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -223,7 +233,8 @@ def main() -> int:
         shutil.rmtree(workdir, ignore_errors=True)
         os.makedirs(workdir)
         proc, kubelet, port, reg, backend = start_daemon(n_gpus, args.grpc_server, workdir, args.profile_dir,
-                                                         args.busy_poll_us, args.admission_poll_us)
+                                                         args.busy_poll_us, args.admission_poll_us,
+                                                         backend=args.backend)
         info = {"port": port, "endpoint": reg.endpoint, "resource": reg.resource_name, "backend": backend,
                 "plugin_dir": os.path.join(workdir, "device-plugins")}
 
@@ -231,7 +242,7 @@ def main() -> int:
     # rate) in a child process, before this process loads torch or initialises RCCL: each
     # rank then holds exactly one HIP runtime (torch's) when the communicator comes up.
     canary_res = None
-    if not args.no_canary and n.amdsmi_available():
+    if not args.no_canary and resolve_backend(n, args.backend) == "amdsmi":
         from k8s_gpu_device_plugin_amd.ops import canary
         canary_res = canary.run_isolated(local_rank, hbm_bytes=1 << 30, timeout=300.0, passes=3)
         if not canary_res.get("ok"):
