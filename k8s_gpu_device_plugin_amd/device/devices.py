@@ -64,9 +64,30 @@ class Device:
     compute_capability: str = ""    # gfx target, e.g. gfx950
     replicas: int = 0
     replica: int = -1
-    health: str = v1beta1.HEALTHY
     product: str = ""
     profile: str = ""               # e.g. "cpx_nps2" for partitions
+    # Health has one source of truth: the native DeviceTable of the plugin advertising the
+    # device (the health monitor writes it directly, ListAndWatch and Allocate read it).
+    # Once bound (bind_table) this view reads and writes through to the table; before,
+    # it holds the initial state the table is built from.
+    _health: str = field(default=v1beta1.HEALTHY, repr=False, compare=False)
+    _table: object = field(default=None, repr=False, compare=False)
+
+    @property
+    def health(self) -> str:
+        if self._table is not None:
+            return v1beta1.HEALTHY if self._table.healthy(self.id) else v1beta1.UNHEALTHY
+        return self._health
+
+    @health.setter
+    def health(self, value: str) -> None:
+        if self._table is not None:
+            self._table.set_health(self.id, value == v1beta1.HEALTHY)
+        else:
+            self._health = value
+
+    def bind_table(self, table) -> None:
+        self._table = table
 
     def is_partition(self) -> bool:
         """Reference ``IsMigDevice`` (index contains ':')."""

@@ -312,9 +312,6 @@ class PluginManager:
         self.monitor.set_gpus(keys)
         self.monitor.attach_tables([p.table for p in plugins], not self.cfg.health.canary,
                                    sorted(self._index_of[k] for k in self._held_unhealthy if k in self._index_of))
-        for p in plugins:
-            for g in gpus:
-                p.sync_gpu_health(g.index)
         self.plugins = plugins
         n = native.load()
         labels = []
@@ -480,12 +477,9 @@ class PluginManager:
         if healthy:  # a recovery supersedes earlier canary verdicts on this GPU
             self._canary_failed = {k for k in self._canary_failed if k[0] != key}
         gpu = self._index_of.get(key, -1)
-        if gpu >= 0:
+        if gpu >= 0 and apply:  # else the monitor thread has already written the tables
             for p in self.plugins:
-                if apply:
-                    p.set_gpu_health(gpu, partition, healthy)
-                else:
-                    p.sync_gpu_health(gpu, partition)
+                p.set_gpu_health(gpu, partition, healthy)
         self.health_log.append((time.monotonic(), gpu, int(healthy), reason))
         (log.info if healthy else log.warning)("%s marked %s: %s", self._gpu_name(key),
                                                "Healthy" if healthy else "Unhealthy", reason)

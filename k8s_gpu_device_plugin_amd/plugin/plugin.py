@@ -94,7 +94,10 @@ def make_table(resource: str, devices: Devices, topology, cfg) -> "object":
     tc.pre_start_required = bool(cfg.health.canaryOnPreStart) if cfg is not None else False
     tds = [n.TableDevice(d.id, d.gpu, d.partition, d.numa_node if d.numa_node is not None else -1, d.replica,
                          list(d.paths), d.health == v1beta1.HEALTHY) for d in devices]
-    return n.DeviceTable(tc, tds, topology)
+    table = n.DeviceTable(tc, tds, topology)
+    for d in devices:  # from here on the Python view reads health from the table
+        d.bind_table(table)
+    return table
 
 
 class AmdDevicePlugin:
@@ -350,25 +353,15 @@ class AmdDevicePlugin:
             srv.notify()
 
     def set_gpu_health(self, gpu: int, partition: int, healthy: bool) -> int:
+        """Health lives in the native table only (the Python devices read it from there)."""
         changed = self.table.set_gpu_health(gpu, partition, healthy)
-        self.sync_gpu_health(gpu, partition)
         if changed:
             self.notify()
         return changed
 
-    def sync_gpu_health(self, gpu: int, partition: int = -1) -> None:
-        """The table is the source of truth (the monitor thread may already have applied
-        a transition natively): mirror it into the Python device view."""
-        for d in self._devices:
-            if d.gpu == gpu and (partition < 0 or d.partition < 0 or d.partition == partition):
-                d.health = v1beta1.HEALTHY if self.table.healthy(d.id) else v1beta1.UNHEALTHY
-
     def set_device_health(self, device_id: str, healthy: bool) -> bool:
         changed = self.table.set_health(device_id, healthy)
         if changed:
-            d = self._devices.get_by_id(device_id)
-            if d is not None:
-                d.health = v1beta1.HEALTHY if healthy else v1beta1.UNHEALTHY
             self.notify()
         return changed
 

@@ -150,3 +150,19 @@ def test_fixture_models():
     assert fixtures.load_model("3gpu_qpx_nps2")["gpus"][0]["compute_partition"] == "QPX"
     with pytest.raises(ValueError):
         fixtures.load_model("nonsense")
+
+
+def test_device_health_is_read_from_the_native_table(n):
+    """One source of truth: once a plugin's table exists, a Device's health is the
+    table's (the health monitor writes the table directly, from its own thread), and
+    writing the view writes the table."""
+    from k8s_gpu_device_plugin_amd.device.devices import Device, Devices
+    from k8s_gpu_device_plugin_amd.plugin.plugin import make_table
+    devs = Devices([Device("a", "0", 0), Device("b", "1", 1)])
+    devs["b"].health = v1beta1.UNHEALTHY  # before the table: initial state
+    t = make_table("amd.com/gpu", devs, n.Topology(2), None)
+    assert not t.healthy("b") and devs["b"].health == v1beta1.UNHEALTHY
+    t.set_gpu_health(0, -1, False)  # e.g. the monitor's fail-fast path
+    assert devs["a"].health == v1beta1.UNHEALTHY
+    devs["a"].health = v1beta1.HEALTHY
+    assert t.healthy("a") and t.version >= 3
