@@ -152,18 +152,21 @@ def config2():
         node.close()
 
 
-def _churn(policy, n_gpu=8, steps=400, seed=7, degraded=()):
-    """Pods of 1/2/4 GPUs arrive/leave; returns placement-quality stats for `policy`."""
+def _churn(policy, n_gpu=8, steps=400, seed=7, degraded=(), slow=()):
+    """Pods of 1/2/4 GPUs arrive/leave; returns placement-quality stats for `policy`.
+    ``degraded``: links down; ``slow``: links up but trained at half rate."""
     nat = native.load()
     topo = nat.Topology(n_gpu)
     for a in range(n_gpu):
         for b in range(a + 1, n_gpu):
-            topo.set_link(a, b, nat.Link(type=nat.LINK_XGMI, hops=1, up=(a, b) not in degraded))
+            topo.set_link(a, b, nat.Link(type=nat.LINK_XGMI, hops=1, up=(a, b) not in degraded,
+                                         bw_gbps=304.0 if (a, b) in slow else 608.0))
     devs = [nat.AllocDevice(gi, -1, gi // 4, "g%d" % gi) for gi in range(n_gpu)]
     rng = random.Random(seed)
     free = set(range(n_gpu))
     pods = []
-    stats = {"placed": 0, "multi": 0, "numa_local": 0, "down_link": 0, "rejected": 0, "quad_ok": 0, "quad_probe": 0}
+    stats = {"placed": 0, "multi": 0, "numa_local": 0, "down_link": 0, "slow_link": 0, "rejected": 0, "quad_ok": 0,
+             "quad_probe": 0}
     for _ in range(steps):
         if pods and (rng.random() < 0.45 or not free):
             free |= set(pods.pop(rng.randrange(len(pods))))
@@ -179,6 +182,7 @@ def _churn(policy, n_gpu=8, steps=400, seed=7, degraded=()):
             stats["multi"] += 1
             stats["numa_local"] += len({c // 4 for c in chosen}) == 1
             stats["down_link"] += any(not topo.link(a, b).up for a in chosen for b in chosen if a < b)
+            stats["slow_link"] += any((a, b) in slow for a in chosen for b in chosen if a < b)
         free -= set(chosen)
         pods.append(chosen)
         if len(free) >= 4:  # could a 4-GPU NUMA-local, all-links-up job still land right now?
@@ -188,6 +192,7 @@ def _churn(policy, n_gpu=8, steps=400, seed=7, degraded=()):
     m = max(1, stats["multi"])
     return {"numa_local_multi_gpu": round(stats["numa_local"] / m, 3),
             "multi_gpu_on_down_link": round(stats["down_link"] / m, 3),
+            "multi_gpu_on_half_rate_link": round(stats["slow_link"] / m, 3),
             "quad_clique_available": round(stats["quad_ok"] / max(1, stats["quad_probe"]), 3),
             "placements": stats["placed"]}
 
@@ -260,6 +265,10 @@ def config3():
         deg = ((0, 5), (2, 3), (1, 2))
         out["placement_degraded_links"] = {"down": [list(d) for d in deg], "xgmi_policy": _churn("xgmi", degraded=deg),
                                            "first_fit": _churn("first", degraded=deg)}
+        slow = ((0, 1), (4, 6))
+        out["placement_half_rate_links"] = {"half_rate": [list(d) for d in slow],
+                                            "xgmi_policy": _churn("xgmi", slow=slow),
+                                            "first_fit": _churn("first", slow=slow)}
         out["placement_cpx_link_sharing"] = {
             "protocol": "8x8 CPX partitions, 400 arrivals/departures, pods of 1-16 partitions, 3 seeds",
             "pod_link_load_aware": [_churn_cpx(True, seed=s) for s in (11, 12, 13)],
