@@ -210,3 +210,14 @@ def test_table_link_setters_are_copy_on_write(n):
     assert after.link(0, 1).pods == 2 and before.link(0, 1).pods == 0 and before.link(0, 1).bw_gbps == 0
     t.set_link_pods([])
     assert t.topology().link(0, 1).pods == 0
+
+
+def test_cpx_churn_shares_fewer_links_with_pod_link_load():
+    """BASELINE round-3 protocol (8x8 CPX, 400 steps): feeding the live pods' link load
+    to the allocator lowers the number of GPU pairs a new multi-GPU pod shares with
+    another one, without rejecting more pods."""
+    from k8s_gpu_device_plugin_amd.benchmark.suite import _churn_cpx
+    aware = [_churn_cpx(True, seed=s) for s in (11, 12, 13)]
+    plain = [_churn_cpx(False, seed=s) for s in (11, 12, 13)]
+    assert sum(r["shared_link_pairs"] for r in aware) < sum(r["shared_link_pairs"] for r in plain)
+    assert [r["rejected"] for r in aware] == [r["rejected"] for r in plain]
