@@ -138,9 +138,17 @@ void Exporter::start(std::shared_ptr<Backend> backend, int interval_ms, std::sha
   stop();
   std::weak_ptr<Exporter> weak = weak_from_this();
   if (weak.expired()) throw std::logic_error("Exporter must be owned by a std::shared_ptr to start sampling");
-  backend_ = std::move(backend);
-  monitor_ = std::move(monitor);
-  interval_ms_ = interval_ms > 0 ? interval_ms : 1000;
+  // A sampler left behind by an earlier stop() (stuck in a backend call) sees another
+  // generation when its call returns and leaves without touching this exporter again;
+  // bump it before anything it could read changes.
+  const uint64_t gen = sampler_gen_.fetch_add(1) + 1;
+  const int interval = interval_ms > 0 ? interval_ms : 1000;
+  {
+    std::lock_guard<std::mutex> lk(run_mu_);
+    backend_ = std::move(backend);
+    monitor_ = std::move(monitor);
+    interval_ms_ = interval;
+  }
   stop_ = false;
   running_ = true;
   {
@@ -148,8 +156,11 @@ void Exporter::start(std::shared_ptr<Backend> backend, int interval_ms, std::sha
     first_done_ = false;
   }
   sampler_exit_ = std::make_shared<ThreadExit>();
-  if (monitor_) watchdog_ = std::thread([this] { watchdog_loop(); });  // before the first call
-  thread_ = std::thread(sampler_main, std::move(weak), sampler_exit_);
+  {
+    std::lock_guard<std::mutex> lk(run_mu_);
+    if (monitor_) watchdog_ = std::thread([this, m = monitor_] { watchdog_loop(m); });  // before the first call
+  }
+  thread_ = std::thread(sampler_main, std::move(weak), sampler_exit_, gen, interval);
   // /metrics is normally populated before start() returns, but a first amdsmi call that
   // hangs (a wedged driver at start-up) must not keep the caller - the plugin manager,
   // which still has kubelet restarts, /restart and health events to handle - from
@@ -202,7 +213,7 @@ void Exporter::stop() {
   }
 }
 
-void Exporter::watchdog_loop() {
+void Exporter::watchdog_loop(std::shared_ptr<HealthMonitor> monitor) {
   while (!stop_.load()) {
     std::this_thread::sleep_for(std::chrono::milliseconds(50));
     const int ms = stall_ms_.load();
@@ -220,11 +231,12 @@ void Exporter::watchdog_loop() {
     e.kind = kEvtDeviceLost;
     e.gpu = g;
     e.message = "telemetry call in flight for " + std::to_string(age / 1000000) + " ms (health.sampleStallS)";
-    monitor_->process(e);  // the GPU recovers through on_sample once the call returns ok
+    monitor->process(e);  // the GPU recovers through on_sample once the call returns ok
   }
 }
 
-void Exporter::sampler_main(std::weak_ptr<Exporter> weak, std::shared_ptr<ThreadExit> exit) {
+void Exporter::sampler_main(std::weak_ptr<Exporter> weak, std::shared_ptr<ThreadExit> exit, uint64_t gen,
+                            int interval_ms) {
   // A strong reference only for the duration of each step: the exporter stays alive
   // through a backend call (however long it blocks), and may be destroyed between
   // steps, by whichever thread drops the last reference.  Nothing below touches it
@@ -235,7 +247,7 @@ void Exporter::sampler_main(std::weak_ptr<Exporter> weak, std::shared_ptr<Thread
     {
       std::shared_ptr<Exporter> self = weak.lock();
       if (!self) break;
-      sleep_ms = self->sampler_step(&next);
+      sleep_ms = self->sampler_step(&next, gen, interval_ms);
     }
     if (sleep_ms < 0) break;
     if (sleep_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(sleep_ms));
@@ -243,13 +255,13 @@ void Exporter::sampler_main(std::weak_ptr<Exporter> weak, std::shared_ptr<Thread
   exit->mark();
 }
 
-int Exporter::sampler_step(int64_t* next) {
-  if (stop_.load()) return -1;
+int Exporter::sampler_step(int64_t* next, uint64_t gen, int interval_ms) {
+  if (stop_.load() || sampler_gen_.load() != gen) return -1;
   const int64_t now = mono_ns();
   if (*next != 0 && now < *next)  // sleep in slices so stop() is prompt
     return static_cast<int>(std::min<int64_t>(50, (*next - now) / 1000000 + 1));
   const bool first = *next == 0;
-  sample_once(true);
+  sample_once(gen);
   if (first) {
     {
       std::lock_guard<std::mutex> lk(first_mu_);
@@ -258,14 +270,21 @@ int Exporter::sampler_step(int64_t* next) {
     first_cv_.notify_all();
     *next = mono_ns();
   }
-  *next += static_cast<int64_t>(interval_ms_) * 1000000;  // fixed cadence, no drift
-  if (*next < mono_ns()) *next = mono_ns() + static_cast<int64_t>(interval_ms_) * 1000000;
+  *next += static_cast<int64_t>(interval_ms) * 1000000;  // fixed cadence, no drift
+  if (*next < mono_ns()) *next = mono_ns() + static_cast<int64_t>(interval_ms) * 1000000;
   return 0;
 }
 
-void Exporter::sample_once(bool from_sampler) {
+void Exporter::sample_once(uint64_t sampler_gen) {
   std::lock_guard<std::mutex> slk(sample_mu_);
-  std::shared_ptr<Backend> be = backend_;
+  if (sampler_gen != 0 && sampler_gen_.load() != sampler_gen) return;
+  std::shared_ptr<Backend> be;
+  std::shared_ptr<HealthMonitor> mon;
+  {
+    std::lock_guard<std::mutex> lk(run_mu_);
+    be = backend_;
+    mon = monitor_;
+  }
   // The inventory may be a subset of the node (`devices: "4-7"`): sample, report health
   // for and label each GPU by its backend index, never by its position in the subset.
   std::vector<int> index;
@@ -280,7 +299,9 @@ void Exporter::sample_once(bool from_sampler) {
   std::vector<char> ok(n, 0);
   const int64_t t0 = mono_ns();
   for (size_t g = 0; g < n; ++g) {
-    if (from_sampler && stop_.load()) return;  // stop() is waiting: no more backend calls
+    // the sampler thread's pass ends early once stop() is waiting (or another sampler
+    // generation has started): no more backend calls
+    if (sampler_gen != 0 && (stop_.load() || sampler_gen_.load() != sampler_gen)) return;
     if (be) {
       {
         std::lock_guard<std::mutex> lk(inflight_mu_);
@@ -293,9 +314,12 @@ void Exporter::sample_once(bool from_sampler) {
         inflight_gpu_.store(-1);
         if (stalled_gpu_.load() == index[g]) stalled_gpu_.store(-1);
       }
+      // left behind by stop() while this call hung, and the exporter was restarted
+      // meanwhile: this pass belongs to no one any more
+      if (sampler_gen != 0 && sampler_gen_.load() != sampler_gen) return;
     }
     if (!ok[g]) sample_errors_.fetch_add(1, std::memory_order_relaxed);
-    if (monitor_) monitor_->on_sample(index[g], ok[g], samples[g]);
+    if (mon) mon->on_sample(index[g], ok[g], samples[g]);
   }
   const double dt = (mono_ns() - t0) * 1e-9;
   if (be) {

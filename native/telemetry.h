@@ -77,8 +77,9 @@ class Exporter : public std::enable_shared_from_this<Exporter> {
   void set_stall_ms(int ms) { stall_ms_.store(ms > 0 ? ms : 0); }
   int stalled_gpu() const { return stalled_gpu_.load(); }
   // One synchronous sampling pass (also used before the first scrape).
-  // from_sampler: the sampler thread's own pass (it ends early once stop() is waiting).
-  void sample_once(bool from_sampler = false);
+  // sampler_gen: the sampler thread's own pass (0 = a caller's synchronous pass); it
+  // ends early once stop() is waiting or another sampler generation started.
+  void sample_once(uint64_t sampler_gen = 0);
   // Samplers left running in a backend call that did not return within the stall
   // threshold when stop() was called (each ends when its call returns).
   int abandoned_samplers() const { return abandoned_.load(); }
@@ -103,8 +104,9 @@ class Exporter : public std::enable_shared_from_this<Exporter> {
     bool wait(int ms);  // ms < 0: no limit; true once the thread has exited
     void mark();
   };
-  static void sampler_main(std::weak_ptr<Exporter> weak, std::shared_ptr<ThreadExit> exit);
-  int sampler_step(int64_t* next);  // ms to sleep before the next step, -1 = stop
+  static void sampler_main(std::weak_ptr<Exporter> weak, std::shared_ptr<ThreadExit> exit, uint64_t gen,
+                           int interval_ms);
+  int sampler_step(int64_t* next, uint64_t gen, int interval_ms);  // ms to sleep before the next step, -1 = stop
   void render_gpu_text(const std::vector<GpuSample>& samples, const std::vector<char>& ok, uint64_t inventory_gen);
   void render_process(std::string* out) const;  // reads /proc
   void render_process_cached(std::string* out) const;  // per-thread copy, refreshed each second
@@ -165,6 +167,7 @@ class Exporter : public std::enable_shared_from_this<Exporter> {
   std::shared_ptr<const std::string> extra_;
   std::shared_ptr<const std::string> gpu_text_;
 
+  std::mutex run_mu_;  // backend_, monitor_, interval_ms_: set by start(), copied by each pass
   std::shared_ptr<Backend> backend_;
   std::shared_ptr<HealthMonitor> monitor_;
   int interval_ms_ = 1000;
@@ -176,12 +179,13 @@ class Exporter : public std::enable_shared_from_this<Exporter> {
   std::condition_variable first_cv_;
   bool first_done_ = false;
   std::atomic<int> abandoned_{0};
+  std::atomic<uint64_t> sampler_gen_{0};  // bumped by every start()
   std::mutex inflight_mu_;  // orders a call's end against the watchdog's verdict on it
   std::mutex sample_mu_;  // serialises sampling passes
   std::atomic<uint64_t> samples_{0};
   std::atomic<uint64_t> sample_errors_{0};
   Histogram sample_hist_;
-  void watchdog_loop();
+  void watchdog_loop(std::shared_ptr<HealthMonitor> monitor);
   std::thread watchdog_;
   std::atomic<int> stall_ms_{0};
   std::atomic<int> inflight_gpu_{-1};       // GPU whose backend call is in flight, -1 = none

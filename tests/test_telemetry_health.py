@@ -470,3 +470,32 @@ def test_watchdog_does_not_report_a_call_that_already_returned(n):
         assert m.gpu_healthy(0) and m.gpu_healthy(1)
     finally:
         ex.stop()
+
+
+def test_exporter_restart_after_an_abandoned_sampler(n):
+    """stop() left a sampler stuck in a backend call; start() again: the new sampler
+    runs, and the old one, once its call returns, sees a newer generation and exits
+    instead of sampling alongside it."""
+    be = fixtures.build_backend("2gpu_spx")
+    gpus, _ = be.discover()
+    ex = n.Exporter()
+    ex.set_inventory(gpus)
+    ex.set_stall_ms(200)
+    be.set_sample_stall(1, True)
+    ex.start(be, 20, None)
+    time.sleep(0.1)
+    ex.stop()
+    assert ex.abandoned_samplers == 1
+    be.set_sample_stall(1, False)
+    ex.start(be, 20, None)
+    try:
+        n0 = ex.samples_total
+        deadline = time.monotonic() + 3
+        while time.monotonic() < deadline and ex.samples_total < n0 + 5:
+            time.sleep(0.02)
+        assert ex.samples_total >= n0 + 5
+        assert 'amdgpu_telemetry_up{gpu="1"} 1' in ex.render()
+    finally:
+        t0 = time.monotonic()
+        ex.stop()
+        assert time.monotonic() - t0 < 1.0
