@@ -52,6 +52,14 @@ void check_contract(const DeviceTable& t, std::string_view input) {
 extern "C" int LLVMFuzzerInitialize(int*, char***) {
   g_tables[0] = fuzzutil::make_table(8, 1);
   g_tables[1] = fuzzutil::make_table(8, 8);
+  // the CPX table carries the round-3 link terms: a half-rate link and links that other
+  // multi-GPU pods already span
+  g_tables[1]->set_link_bandwidth(0, 1, 304.0);
+  g_tables[1]->set_link_bandwidth(2, 5, 456.0);
+  std::vector<int> pods(64, 0);
+  pods[0 * 8 + 2] = pods[2 * 8 + 0] = 1;
+  pods[4 * 8 + 6] = pods[6 * 8 + 4] = 3;
+  g_tables[1]->set_link_pods(pods);
   g_tables[2] = fuzzutil::make_table(4, 1, 4);
   if (const char* dir = fuzzutil::seed_dir()) {
     using fuzzutil::alloc_req;
