@@ -197,34 +197,56 @@ def _churn(policy, n_gpu=8, steps=400, seed=7, degraded=(), slow=()):
             "placements": stats["placed"]}
 
 
-def _churn_cpx(link_aware: bool, n_gpu=8, parts=8, steps=400, seed=11):
+def _churn_cpx(visibility, n_gpu=8, parts=8, steps=400, seed=11, poll_every=10):
     """CPX node (8 GPUs x 8 partitions): pods of 1..16 partitions arrive and leave.  For
     each multi-GPU pod placed, counts the GPU pairs it spans that another live
     multi-GPU pod already spans: both drive RCCL traffic over that one xGMI link.
-    ``link_aware``: the allocator sees the live pods' link load (what the plugin feeds it
-    from kubelet PodResources); otherwise the same allocator without it (round-2 policy)."""
+
+    ``visibility`` is what link load the allocator is given:
+      * ``"none"``: nothing (the round-2 policy);
+      * ``"podresources"``: the kubelet PodResources map as of its last poll, one poll
+        per ``poll_every`` steps (pods placed since are invisible, pods gone since still
+        count);
+      * ``"podresources+allocate"``: that map plus the multi-GPU containers the plugin
+        allocated since the poll (what the plugin runs: ``RecentAllocations``);
+      * ``"oracle"``: exactly the live pods.
+    (``True`` / ``False`` are the oracle / none of the first version of this protocol.)"""
+    if visibility is True:
+        visibility = "oracle"
+    elif visibility is False:
+        visibility = "none"
     nat = native.load()
     devs = [nat.AllocDevice(g, p, g // 4, "g%dp%d" % (g, p)) for g in range(n_gpu) for p in range(parts)]
     rng = random.Random(seed)
     free = set(range(len(devs)))
-    pods = []  # (device indices, set of GPUs)
+    pods = []  # (device indices, set of GPUs, id)
+    polled, since_poll, next_id = [], [], 0
     st = {"placed": 0, "multi": 0, "pairs": 0, "shared_pairs": 0, "pods_sharing": 0, "rejected": 0}
 
     def topology():
+        if visibility == "oracle":
+            seen = [gs for _, gs, _ in pods]
+        elif visibility == "podresources":
+            seen = list(polled)
+        elif visibility == "podresources+allocate":
+            seen = list(polled) + list(since_poll)
+        else:
+            seen = []
         load = {}
-        if link_aware:
-            for _, gs in pods:
-                for a, b in itertools.combinations(sorted(gs), 2):
-                    load[(a, b)] = load.get((a, b), 0) + 1
+        for gs in seen:
+            for a, b in itertools.combinations(sorted(gs), 2):
+                load[(a, b)] = load.get((a, b), 0) + 1
         t = nat.Topology(n_gpu)
         for a in range(n_gpu):
             for b in range(a + 1, n_gpu):
                 t.set_link(a, b, nat.Link(type=nat.LINK_XGMI, hops=1, bw_gbps=608.0, pods=load.get((a, b), 0)))
         return t
 
-    for _ in range(steps):
+    for step in range(steps):
+        if step % poll_every == 0:
+            polled, since_poll = [gs for _, gs, _ in pods], []
         if pods and (rng.random() < 0.45 or not free):
-            chosen, _ = pods.pop(rng.randrange(len(pods)))
+            chosen, _, _ = pods.pop(rng.randrange(len(pods)))
             free |= set(chosen)
             continue
         size = rng.choice([1, 2, 4, 4, 8, 12, 16])
@@ -236,7 +258,7 @@ def _churn_cpx(link_aware: bool, n_gpu=8, parts=8, steps=400, seed=11):
         st["placed"] += 1
         if len(gs) > 1:
             live = set()
-            for _, other in pods:
+            for _, other, _ in pods:
                 if len(other) > 1:
                     live |= set(itertools.combinations(sorted(other), 2))
             mine = set(itertools.combinations(sorted(gs), 2))
@@ -244,8 +266,10 @@ def _churn_cpx(link_aware: bool, n_gpu=8, parts=8, steps=400, seed=11):
             st["pairs"] += len(mine)
             st["shared_pairs"] += len(mine & live)
             st["pods_sharing"] += bool(mine & live)
+            since_poll.append(gs)
         free -= set(chosen)
-        pods.append((chosen, gs))
+        pods.append((chosen, gs, next_id))
+        next_id += 1
     m = max(1, st["multi"])
     return {"placements": st["placed"], "multi_gpu_pods": st["multi"], "gpu_pairs_spanned": st["pairs"],
             "shared_link_pairs": st["shared_pairs"], "multi_gpu_pods_sharing_a_link": round(st["pods_sharing"] / m, 3),
@@ -269,10 +293,14 @@ def config3():
         out["placement_half_rate_links"] = {"half_rate": [list(d) for d in slow],
                                             "xgmi_policy": _churn("xgmi", slow=slow),
                                             "first_fit": _churn("first", slow=slow)}
+        runs = {vis: [_churn_cpx(vis, seed=s) for s in range(100, 130)]
+                for vis in ("none", "podresources", "podresources+allocate", "oracle")}
         out["placement_cpx_link_sharing"] = {
-            "protocol": "8x8 CPX partitions, 400 arrivals/departures, pods of 1-16 partitions, 3 seeds",
-            "pod_link_load_aware": [_churn_cpx(True, seed=s) for s in (11, 12, 13)],
-            "without_link_load": [_churn_cpx(False, seed=s) for s in (11, 12, 13)]}
+            "protocol": "8x8 CPX partitions, 400 arrivals/departures, pods of 1-16 partitions, 30 seeds; "
+                        "PodResources polled every 10 steps",
+            **{vis: {k: sum(r[k] for r in rs) for k in ("multi_gpu_pods", "gpu_pairs_spanned", "shared_link_pairs",
+                                                        "rejected")}
+               for vis, rs in runs.items()}}
         return out
     finally:
         node.close()

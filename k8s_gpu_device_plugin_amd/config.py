@@ -119,6 +119,14 @@ class PodResourcesConfig:
 
 
 @dataclass
+class AllocatorConfig:
+    # A multi-GPU container this plugin allocated counts as load on the xGMI links it
+    # spans until the kubelet PodResources map shows it (podResources.enabled), or for
+    # this long (0 = only the PodResources map).
+    recentAllocationTtlS: float = 30.0
+
+
+@dataclass
 class Config:
     webListenAddress: str = "0.0.0.0:9100"
     migStrategy: str = "none"            # alias partitionStrategy (none|single|mixed)
@@ -143,6 +151,7 @@ class Config:
     http: HttpConfig = field(default_factory=HttpConfig)
     grpc: GrpcConfig = field(default_factory=GrpcConfig)
     podResources: PodResourcesConfig = field(default_factory=PodResourcesConfig)
+    allocator: AllocatorConfig = field(default_factory=AllocatorConfig)
     retrySeconds: float = 30.0            # plugin start retry (plugin/manager.go:135-138)
 
     @property
@@ -286,6 +295,8 @@ def validate(cfg: Config) -> Config:
         parse_level(cfg.log.level)
     except ValueError as e:
         raise ConfigError(str(e)) from None
+    if not cfg.allocator.recentAllocationTtlS >= 0:
+        raise ConfigError("allocator.recentAllocationTtlS must be >= 0, got %r" % cfg.allocator.recentAllocationTtlS)
     if not cfg.log.maxAgeDays >= 0:
         raise ConfigError("log.maxAgeDays must be >= 0 (0 keeps rotated files), got %r" % cfg.log.maxAgeDays)
     if cfg.backend not in ("auto", "amdsmi", "fixture"):

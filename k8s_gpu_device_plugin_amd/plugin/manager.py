@@ -105,6 +105,10 @@ class PluginManager:
         self._verify_pool: concurrent.futures.ThreadPoolExecutor | None = None
         self.podres = None  # PodResourcesWatcher when podResources.enabled
         self.link_pods: dict[tuple[int, int], int] = {}  # GPU pair -> multi-GPU pods spanning it
+        # multi-GPU containers allocated since the last PodResources poll (shared by all
+        # tables, kept across reloads)
+        self.recent_allocations = n.RecentAllocations()
+        self.recent_allocations.set_ttl_ms(int(cfg.allocator.recentAllocationTtlS * 1000))
         self.multi_gpu_pods = 0
         # GPUs with hardware event notification armed (read when the monitor starts and
         # after each re-discovery, which can re-initialise amdsmi); None = not monitoring
@@ -294,6 +298,8 @@ class PluginManager:
         else:
             failed = {(self._index_of[k], p) for k, p in self._canary_failed if k in self._index_of}
         plugins = [AmdDevicePlugin(name, devs, topo, self.cfg) for name, devs in self.device_map.items()]
+        for p in plugins:
+            p.table.set_recent_allocations(self.recent_allocations)
         if self.cfg.health.canaryOnPreStart:
             for p in plugins:
                 p.prestart_check = self._prestart_check
@@ -449,6 +455,8 @@ class PluginManager:
         if self.podres is None or not self.plugins:
             return
         allocs, _ = self.podres.snapshot()
+        # allocations answered before that poll are in its map now
+        self.recent_allocations.set_covered_until(self.podres.covered_until())
         gpu_of = {}
         for p in self.plugins:
             for d in p.devices():

@@ -16,6 +16,7 @@ allocation.
 from __future__ import annotations
 
 import threading
+import time
 
 import grpc
 
@@ -81,6 +82,10 @@ class PodResourcesWatcher:
         self.allocations: Allocation = {}
         self.up: bool | None = None
         self.polls = 0
+        # CLOCK_MONOTONIC ns at which the List behind `allocations` was sent: every
+        # Allocate answered before it is in the map (kubelet records the devices at
+        # admission, before the containers start)
+        self.covered_until_ns = 0
         self._stop = threading.Event()
         self._thread: threading.Thread | None = None
         self._lock = threading.Lock()
@@ -89,8 +94,13 @@ class PodResourcesWatcher:
         with self._lock:
             return dict(self.allocations), self.up
 
+    def covered_until(self) -> int:
+        with self._lock:
+            return self.covered_until_ns
+
     def poll_once(self) -> bool:
         """Returns True when the allocation map or the up state changed."""
+        t0 = time.monotonic_ns()
         try:
             allocs, up = list_allocations(self.socket_path, self.resource_prefix), True
         except Exception as e:  # kubelet restarting, socket not mounted, API disabled
@@ -101,6 +111,9 @@ class PodResourcesWatcher:
             self.polls += 1
             changed = allocs != self.allocations or up != self.up
             self.allocations, self.up = allocs, up
+            if up:
+                changed = changed or self.covered_until_ns == 0
+                self.covered_until_ns = t0
         return changed
 
     def start(self) -> None:

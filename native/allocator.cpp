@@ -399,6 +399,60 @@ AllocResult aligned_alloc(const Topology& topo, const std::vector<AllocDevice>& 
   return res;
 }
 
+RecentAllocations::RecentAllocations() = default;
+
+void RecentAllocations::record(uint64_t gpu_mask, int64_t now_ns) {
+  if (__builtin_popcountll(gpu_mask) < 2 || ttl_ns_.load(std::memory_order_relaxed) == 0) return;
+  Slot& s = slots_[next_.fetch_add(1, std::memory_order_relaxed) % kSlots];
+  const uint64_t q = s.seq.load(std::memory_order_relaxed);
+  s.seq.store(q + 1, std::memory_order_relaxed);  // odd: being written
+  std::atomic_thread_fence(std::memory_order_release);
+  s.mask.store(gpu_mask, std::memory_order_relaxed);
+  s.ts.store(now_ns, std::memory_order_relaxed);
+  s.seq.store(q + 2, std::memory_order_release);
+  int64_t cur = newest_.load(std::memory_order_relaxed);
+  while (cur < now_ns && !newest_.compare_exchange_weak(cur, now_ns, std::memory_order_release)) {
+  }
+}
+
+bool RecentAllocations::fresh(int64_t ts, int64_t now_ns) const {
+  const int64_t ttl = ttl_ns_.load(std::memory_order_acquire);
+  return ts > 0 && ttl > 0 && ts > covered_.load(std::memory_order_acquire) && now_ns - ts < ttl;
+}
+
+int RecentAllocations::add_link_pods(int n, int64_t now_ns, std::vector<int>* pods) const {
+  if (!fresh(newest_.load(std::memory_order_acquire), now_ns)) return 0;  // the common case: nothing recent
+  int live = 0;
+  for (const Slot& s : slots_) {
+    uint64_t mask;
+    int64_t ts;
+    for (;;) {  // seqlock read: retry while a writer is in the slot
+      const uint64_t q0 = s.seq.load(std::memory_order_acquire);
+      if (q0 & 1) continue;
+      mask = s.mask.load(std::memory_order_relaxed);
+      ts = s.ts.load(std::memory_order_relaxed);
+      std::atomic_thread_fence(std::memory_order_acquire);
+      if (s.seq.load(std::memory_order_relaxed) == q0) break;
+    }
+    if (!fresh(ts, now_ns)) continue;
+    ++live;
+    if (!pods) continue;
+    for (uint64_t a = mask; a; a &= a - 1) {
+      const int ga = __builtin_ctzll(a);
+      for (uint64_t b = a & (a - 1); b; b &= b - 1) {
+        const int gb = __builtin_ctzll(b);
+        if (ga < n && gb < n) {
+          (*pods)[static_cast<size_t>(ga) * n + gb]++;
+          (*pods)[static_cast<size_t>(gb) * n + ga]++;
+        }
+      }
+    }
+  }
+  return live;
+}
+
+int RecentAllocations::live(int64_t now_ns) const { return add_link_pods(0, now_ns, nullptr); }
+
 AllocResult distributed_alloc(const std::vector<AllocDevice>& devs, const std::vector<int>& avail,
                               const std::vector<int>& required, int size) {
   AllocResult res;

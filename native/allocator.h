@@ -15,6 +15,7 @@
 // patched on link events), never per call.
 #pragma once
 
+#include <atomic>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -55,6 +56,41 @@ int pair_score(const Topology& topo, const AllocDevice& a, const AllocDevice& b)
 // satisfiable, deterministic for identical inputs.
 AllocResult aligned_alloc(const Topology& topo, const std::vector<AllocDevice>& devs,
                           const std::vector<int>& avail, const std::vector<int>& required, int size);
+
+// Multi-GPU allocations this plugin answered recently, as link load the allocator adds
+// on top of the kubelet PodResources map until that map covers them.  The PodResources
+// poll runs every podResources.intervalS (10 s), while a job's pods are admitted within
+// a second or two of each other: without this, every pod of a burst would see the links
+// as free and pile onto the same GPU pairs.  One tracker is shared by all of a node's
+// tables (pods of different resources share the links too).  Allocate records into a
+// fixed ring with one atomic increment; readers take a seqlock-style snapshot.
+class RecentAllocations {
+ public:
+  static constexpr int kSlots = 64;
+  RecentAllocations();
+  // Allocate answered a container request spanning these GPUs (bit g = GPU g < 64).
+  void record(uint64_t gpu_mask, int64_t now_ns);
+  // Entries allocated before this (mono ns) are in the PodResources map already.
+  void set_covered_until(int64_t mono_ns) { covered_.store(mono_ns, std::memory_order_release); }
+  void set_ttl_ms(int64_t ms) { ttl_ns_.store(ms > 0 ? ms * 1000000 : 0, std::memory_order_release); }
+  // Adds, for every live entry, one pod to each GPU pair it spans (n x n row-major).
+  // Returns the number of live entries (0: nothing added, the caller can skip a copy).
+  int add_link_pods(int n, int64_t now_ns, std::vector<int>* pods) const;
+  int live(int64_t now_ns) const;
+
+ private:
+  bool fresh(int64_t ts, int64_t now_ns) const;
+  struct alignas(64) Slot {
+    std::atomic<uint64_t> seq{0};  // odd while being written
+    std::atomic<int64_t> ts{0};
+    std::atomic<uint64_t> mask{0};
+  };
+  Slot slots_[kSlots];
+  std::atomic<uint64_t> next_{0};
+  std::atomic<int64_t> newest_{0};  // lets readers skip the scan when nothing can be live
+  std::atomic<int64_t> covered_{0};
+  std::atomic<int64_t> ttl_ns_{30'000'000'000LL};
+};
 
 // Replica-spreading policy (reference distributedAlloc, plugin/plugin.go:284-326) with a
 // stable, deterministic tie-break (fixes defect D14).

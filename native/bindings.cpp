@@ -287,6 +287,24 @@ PYBIND11_MODULE(_native, m) {
           }
           return out;
         });
+  py::class_<RecentAllocations, std::shared_ptr<RecentAllocations>>(m, "RecentAllocations")
+      .def(py::init<>())
+      .def("record_gpus",
+           [](RecentAllocations& r, const std::vector<int>& gpus) {
+             uint64_t mask = 0;
+             for (int g : gpus)
+               if (g >= 0 && g < 64) mask |= 1ull << g;
+             r.record(mask, mono_ns());
+           })
+      .def("set_covered_until", &RecentAllocations::set_covered_until, py::arg("mono_ns"))
+      .def("set_ttl_ms", &RecentAllocations::set_ttl_ms)
+      .def("live", [](const RecentAllocations& r) { return r.live(mono_ns()); })
+      .def("link_pods", [](const RecentAllocations& r, int n) {
+        std::vector<int> pods(static_cast<size_t>(std::max(0, n)) * std::max(0, n), 0);
+        r.add_link_pods(n, mono_ns(), &pods);
+        return pods;
+      });
+  m.def("mono_ns", &mono_ns);
   m.def("distributed_alloc", [](const std::vector<AllocDevice>& d, const std::vector<int>& avail,
                                 const std::vector<int>& req, int size) {
     AllocResult r = distributed_alloc(d, avail, req, size);
@@ -359,6 +377,7 @@ PYBIND11_MODULE(_native, m) {
       .def("set_link_up", &DeviceTable::set_link_up)
       .def("set_link_bandwidth", &DeviceTable::set_link_bandwidth)
       .def("set_link_pods", &DeviceTable::set_link_pods)
+      .def("set_recent_allocations", &DeviceTable::set_recent_allocations)
       .def("topology", &DeviceTable::topology)
       .def_property_readonly("version", &DeviceTable::version)
       .def("list_and_watch", [](const DeviceTable& t) { return py::bytes(t.list_and_watch()); })

@@ -225,6 +225,12 @@ void DeviceTable::set_link_pods(const std::vector<int>& counts) {
   });
 }
 
+void DeviceTable::set_recent_allocations(std::shared_ptr<RecentAllocations> r) {
+  std::lock_guard<std::mutex> lk(wmu_);
+  recent_.store(r.get(), std::memory_order_release);
+  if (r) recent_owned_.push_back(std::move(r));
+}
+
 Topology DeviceTable::topology() const { return *std::atomic_load_explicit(&topo_, std::memory_order_acquire); }
 
 std::string DeviceTable::list_and_watch() const {
@@ -371,9 +377,11 @@ bool DeviceTable::allocate(std::string_view req, std::string* out) const {
   thread_local std::vector<std::string_view> ids;
   thread_local std::vector<size_t> ends;  // ids[ends[k-1], ends[k]) belong to container k
   thread_local std::vector<int> idx;
+  thread_local std::vector<uint64_t> masks;  // GPUs each container spans
   thread_local std::string c;
   ids.clear();
   ends.clear();
+  masks.clear();
   try {
     pb::Reader r(req);
     uint32_t f, w;
@@ -411,11 +419,21 @@ bool DeviceTable::allocate(std::string_view req, std::string* out) const {
       }
       idx.push_back(i);
     }
+    uint64_t mask = 0;
+    for (const int i : idx)
+      if (alloc_devs_[i].gpu >= 0 && alloc_devs_[i].gpu < 64) mask |= 1ull << alloc_devs_[i].gpu;
+    masks.push_back(mask);
     begin = end;
     c.clear();
     encode_container_alloc(idx.data(), idx.size(), &c);
     pb::put_bytes(out, 1, c);
   }
+  // A container that spans GPUs will drive traffic over their links: count it as link
+  // load at once (the PodResources map catches up only at its next poll).  Recorded
+  // only once the whole request succeeded.
+  if (RecentAllocations* ra = recent_.load(std::memory_order_acquire))
+    for (const uint64_t mask : masks)
+      if (__builtin_popcountll(mask) >= 2) ra->record(mask, mono_ns());
   return true;
 }
 
@@ -453,6 +471,18 @@ AllocResult DeviceTable::preferred_core(const std::string_view* avail, size_t n_
   }
   if (aligned_ok_ && !any_annotated) {
     const auto topo = std::atomic_load_explicit(&topo_, std::memory_order_acquire);  // snapshot
+    if (RecentAllocations* ra = recent_.load(std::memory_order_acquire)) {
+      // multi-GPU containers allocated since the last PodResources poll: their links
+      // count as used too
+      thread_local std::vector<int> extra;
+      extra.assign(static_cast<size_t>(topo->n) * topo->n, 0);
+      if (ra->add_link_pods(topo->n, mono_ns(), &extra) > 0) {
+        thread_local Topology with_recent;
+        with_recent = *topo;
+        for (size_t i = 0; i < extra.size(); ++i) with_recent.links[i].pods += extra[i];
+        return aligned_alloc(with_recent, alloc_devs_, a, m, size);
+      }
+    }
     return aligned_alloc(*topo, alloc_devs_, a, m, size);
   }
   return distributed_alloc(alloc_devs_, a, m, size);

@@ -103,6 +103,9 @@ class DeviceTable {
   // n*n row-major (n = topology size): multi-GPU pods spanning each GPU pair.  Replaces
   // every count; a shorter vector clears the rest.
   void set_link_pods(const std::vector<int>& counts);
+  // The node's tracker of recent multi-GPU Allocates (shared by every table): Allocate
+  // records into it, GetPreferredAllocation adds its live entries to the link load.
+  void set_recent_allocations(std::shared_ptr<RecentAllocations> r);
   Topology topology() const;
 
   uint64_t version() const { return version_.load(std::memory_order_acquire); }
@@ -200,6 +203,10 @@ class DeviceTable {
   mutable uint64_t wakes_ = 0;
   std::vector<std::weak_ptr<TableListener>> listeners_;
   std::shared_ptr<const Topology> topo_;          // atomic_load / atomic_store
+  // Hot-path view of the tracker: a plain atomic pointer (no shared_ptr atomics on
+  // Allocate); every tracker ever set is kept alive with the table.
+  std::atomic<RecentAllocations*> recent_{nullptr};
+  std::vector<std::shared_ptr<RecentAllocations>> recent_owned_;  // guarded by wmu_
   std::shared_ptr<const std::string> law_;        // cached ListAndWatchResponse
   std::atomic<uint64_t> version_{1};
 

@@ -217,7 +217,58 @@ def test_cpx_churn_shares_fewer_links_with_pod_link_load():
     to the allocator lowers the number of GPU pairs a new multi-GPU pod shares with
     another one, without rejecting more pods."""
     from k8s_gpu_device_plugin_amd.benchmark.suite import _churn_cpx
-    aware = [_churn_cpx(True, seed=s) for s in (11, 12, 13)]
-    plain = [_churn_cpx(False, seed=s) for s in (11, 12, 13)]
-    assert sum(r["shared_link_pairs"] for r in aware) < sum(r["shared_link_pairs"] for r in plain)
-    assert [r["rejected"] for r in aware] == [r["rejected"] for r in plain]
+    seeds = range(100, 115)
+    runs = {vis: [_churn_cpx(vis, seed=s) for s in seeds] for vis in ("none", "podresources", "podresources+allocate")}
+    shared = {vis: sum(r["shared_link_pairs"] for r in rs) for vis, rs in runs.items()}
+    # the lagged PodResources map helps; adding the plugin's own recent Allocates helps more
+    assert shared["podresources+allocate"] < shared["podresources"] < shared["none"], shared
+    assert [r["rejected"] for r in runs["none"]] == [r["rejected"] for r in runs["podresources+allocate"]]
+
+
+def _cpx_table(n, ngpu=4, parts=8):
+    topo = n.Topology(ngpu)
+    for a in range(ngpu):
+        for b in range(a + 1, ngpu):
+            topo.set_link(a, b, n.Link(type=n.LINK_XGMI, hops=1, bw_gbps=608.0))
+    devs = [n.TableDevice("g%dp%d" % (g, p), g, p, 0, -1, ["/dev/dri/renderD%d" % (128 + g * parts + p)], True)
+            for g in range(ngpu) for p in range(parts)]
+    return n.DeviceTable(n.TableConfig(), devs, topo)
+
+
+def test_recent_multi_gpu_allocate_counts_as_link_load(n):
+    """A burst of pods is admitted faster than the PodResources poll: a container the
+    plugin just allocated across GPUs 0 and 1 already steers the next pod off link 0-1.
+    Once a poll covers it (the map has it now) or its TTL passes, it no longer counts."""
+    from k8s_gpu_device_plugin_amd.api import v1beta1
+    t = _cpx_table(n)
+    rec = n.RecentAllocations()
+    t.set_recent_allocations(rec)
+    ids = t.ids()
+    avail = ids[4:8] + ids[12:16] + ids[20:24]  # 4 free partitions on each of GPUs 0, 1, 2
+    gpus = lambda got: sorted({ids.index(x) // 8 for x in got})  # noqa: E731
+    first = t.preferred_ids(avail, [], 8)
+    assert gpus(first) == [0, 1]
+    req = v1beta1.AllocateRequest(container_requests=[
+        v1beta1.ContainerAllocateRequest(devices_ids=ids[0:4] + ids[8:12])]).SerializeToString()
+    ok, _ = t.allocate(req)
+    assert ok and rec.live() == 1 and rec.link_pods(4)[0 * 4 + 1] == 1
+    second = t.preferred_ids(avail, [], 8)
+    assert gpus(second) in ([0, 2], [1, 2])
+    rec.set_covered_until(n.mono_ns())  # a PodResources poll now reports that pod
+    assert rec.live() == 0
+    third = t.preferred_ids(avail, [], 8)
+    assert gpus(third) == [0, 1]
+    # single-GPU containers and failed requests record nothing; the TTL ends an entry
+    bad = v1beta1.AllocateRequest(container_requests=[
+        v1beta1.ContainerAllocateRequest(devices_ids=ids[0:2] + ids[8:10]),
+        v1beta1.ContainerAllocateRequest(devices_ids=["nope"])]).SerializeToString()
+    assert not t.allocate(bad)[0] and rec.live() == 0
+    assert t.allocate(v1beta1.AllocateRequest(container_requests=[
+        v1beta1.ContainerAllocateRequest(devices_ids=ids[0:8])]).SerializeToString())[0]
+    assert rec.live() == 0
+    rec.set_ttl_ms(50)
+    rec.record_gpus([2, 3])
+    assert rec.live() == 1
+    import time
+    time.sleep(0.08)
+    assert rec.live() == 0

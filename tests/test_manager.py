@@ -774,3 +774,31 @@ def test_native_server_crash_loop_is_fatal(make_cfg, plugin_dir):
         finally:
             m.stop()
             t.join(10)
+
+
+def test_allocate_counts_as_link_load_until_pod_resources_has_it(make_cfg, plugin_dir, run_manager, tmp_path):
+    """The plugin answers a multi-GPU Allocate: the link it spans counts as used at
+    once, before the PodResources poll; after the next poll the count comes from the
+    kubelet's map instead (not both)."""
+    from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import PodResourcesStub
+    sock = str(tmp_path / "pod-resources" / "kubelet.sock")
+    stub = PodResourcesStub(sock).start()
+    try:
+        with KubeletStub(plugin_dir) as k:
+            m = run_manager(make_cfg(fixture="4gpu_cpx", migStrategy="single",
+                                     podResources={"enabled": True, "socket": sock, "intervalS": 0.5}))
+            c = k.client(k.wait_for_registrations(1)[0].endpoint)
+            ids = m.plugins[0].table.ids()
+            held = ids[0:4] + ids[8:12]
+            assert _wait(lambda: m.podres.polls >= 1)
+            stub.set_pods([("ml", "ring-0", [("main", "amd.com/gpu", held)])])  # kubelet records it at admission
+            c.allocate(held)
+            assert m.recent_allocations.live() == 1
+            avail = ids[4:8] + ids[12:16] + ids[20:24]
+            got = list(c.preferred(avail, [], 8).container_responses[0].deviceIDs)
+            assert sorted({ids.index(x) // 8 for x in got}) in ([0, 2], [1, 2])
+            assert _wait(lambda: m.plugins[0].table.topology().link(0, 1).pods == 1, timeout=5)
+            assert _wait(lambda: m.recent_allocations.live() == 0, timeout=5)
+            assert m.recent_allocations.link_pods(4)[1] == 0  # not counted twice
+    finally:
+        stub.stop()
