@@ -963,10 +963,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
             }
             break;
           }
-          Worker* t = w;  // least-loaded worker, this one on a tie
-          for (auto& o : workers_)
-            if (o->load.load(std::memory_order_relaxed) < t->load.load(std::memory_order_relaxed)) t = o.get();
-          t->load.fetch_add(1, std::memory_order_relaxed);
+          Worker* t = pick_least_loaded(workers_, w);  // this one on a tie
           auto c = std::make_unique<Conn>();
           c->fd = cfd;
           // server preface: SETTINGS(MAX_CONCURRENT_STREAMS, INITIAL_WINDOW_SIZE) + conn window

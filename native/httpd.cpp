@@ -375,10 +375,7 @@ int HttpServer::start() {
               else if (peer.ss_family == AF_INET6)
                 inet_ntop(AF_INET6, &reinterpret_cast<sockaddr_in6*>(&peer)->sin6_addr, ip, sizeof(ip));
               c->remote = ip;
-              Worker* t = w;  // least-loaded worker, this one on a tie
-              for (auto& o : workers_)
-                if (o->load.load(std::memory_order_relaxed) < t->load.load(std::memory_order_relaxed)) t = o.get();
-              t->load.fetch_add(1, std::memory_order_relaxed);
+              Worker* t = pick_least_loaded(workers_, w);  // this one on a tie
               struct epoll_event ev {};
               ev.events = EPOLLIN | EPOLLRDHUP;
               ev.data.fd = cfd;

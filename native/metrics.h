@@ -85,6 +85,26 @@ inline void cpu_relax() {
 #endif
 }
 
+// The worker of `workers` (each with an atomic `load`) with the fewest connections,
+// `self` on a tie, with its load already incremented.  Claims the slot with a CAS, so
+// two workers that accept at the same moment never both hand their connection to the
+// same worker at the same load.
+template <class Workers, class W>
+W* pick_least_loaded(Workers& workers, W* self) {
+  for (;;) {
+    W* t = self;
+    int tl = t->load.load(std::memory_order_relaxed);
+    for (auto& o : workers) {
+      const int ol = o->load.load(std::memory_order_relaxed);
+      if (ol < tl) {
+        t = o.get();
+        tl = ol;
+      }
+    }
+    if (t->load.compare_exchange_weak(tl, tl + 1, std::memory_order_relaxed)) return t;
+  }
+}
+
 // Guards pointer-sized critical sections on the scrape path (copying or swapping a
 // shared_ptr to a cached text).  A contended std::mutex parks the thread in futex_wait,
 // and the wake-up costs more than the whole critical section: with 4 concurrent
