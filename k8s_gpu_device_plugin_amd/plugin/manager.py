@@ -440,10 +440,14 @@ class PluginManager:
         elif u.kind == native.load().EVT_LINK_QUALITY:
             a = self._index_of.get(key, -1)
             b = self._index_of.get(getattr(u, "peer_key", "") or self._key_of.get(u.peer, ""), -1)
-            if a >= 0 and b >= 0:
-                for p in self.plugins:
-                    p.set_link_bandwidth(a, b, u.link_gbps)
-            log.warning("xGMI link %d<->%d now trains at %.0f Gb/s: %s", a, b, u.link_gbps, u.reason)
+            if a < 0 or b < 0 or not self.plugins:
+                return
+            cur = self.plugins[0].table.topology().link(a, b).bw_gbps
+            if cur > 0 and abs(cur - u.link_gbps) <= 0.05 * max(cur, u.link_gbps):
+                return  # what discovery found (the first reading of every link lands here)
+            for p in self.plugins:
+                p.set_link_bandwidth(a, b, u.link_gbps)
+            log.warning("xGMI link %d<->%d trains at %.0f Gb/s (was %.0f): %s", a, b, u.link_gbps, cur, u.reason)
         else:
             log.info("GPU event on %s: %s", self._gpu_name(key), u.reason)
 

@@ -278,16 +278,19 @@ void HealthMonitor::on_sample(int gpu, bool ok, const GpuSample& s) {
           e.peer_key = peer_keys[k];
           derived.push_back(e);
         }
-        // Trained bandwidth: the first value seen is the baseline (discovery already put it
-        // in the topology); a re-train to another rate (> 5 % off) is reported.
+        // Trained bandwidth: the first reading of a link is reported too (the link may
+        // have re-trained between discovery and this sample; the manager applies it only
+        // where the tables disagree), and after that every re-train to another rate
+        // (> 5 % off).
         const double bw = s.link_max_gbps[k];
         if (s.link_up[k] == 1 && bw > 0) {
           auto bt = st.link_bw.find(peer_keys[k]);
-          if (bt == st.link_bw.end()) {
-            st.link_bw[peer_keys[k]] = bw;
-          } else if (std::fabs(bt->second - bw) > 0.05 * std::max(bt->second, bw)) {
-            HwEvent e = event(kEvtLinkQuality, "xgmi link re-trained: " + std::to_string(static_cast<int>(bt->second)) +
-                                                   " -> " + std::to_string(static_cast<int>(bw)) + " Gb/s");
+          const bool first = bt == st.link_bw.end();
+          if (first || std::fabs(bt->second - bw) > 0.05 * std::max(bt->second, bw)) {
+            HwEvent e = event(kEvtLinkQuality,
+                              first ? "xgmi link bandwidth: " + std::to_string(static_cast<int>(bw)) + " Gb/s"
+                                    : "xgmi link re-trained: " + std::to_string(static_cast<int>(bt->second)) + " -> " +
+                                          std::to_string(static_cast<int>(bw)) + " Gb/s");
             e.peer = s.link_peer[k];
             e.peer_key = peer_keys[k];
             e.value = bw;

@@ -244,7 +244,7 @@ def test_retired_pages_threshold_state_machine(n):
     be.set_retired_pages(1, 500, 0)  # threshold 0 on GPU 1: check disabled
     for g in (0, 1):
         m.on_sample(g, True, be.sample(g))
-    u = m.pop(100)
+    u = [x for x in m.pop(100) if x.kind != n.EVT_LINK_QUALITY]  # first link-bandwidth readings
     assert [(x.gpu, x.healthy) for x in u] == [(0, 0)] and "retired" in u[0].reason
     m.process(n.HwEvent(n.EVT_PRE_RESET, 0))
     m.process(n.HwEvent(n.EVT_POST_RESET, 0))
@@ -499,3 +499,25 @@ def test_exporter_restart_after_an_abandoned_sampler(n):
         t0 = time.monotonic()
         ex.stop()
         assert time.monotonic() - t0 < 1.0
+
+
+def test_link_bandwidth_first_reading_and_retrain(n):
+    """The first telemetry reading of each link is reported once per link (the peer's
+    sample of the same link is deduplicated), so a link that re-trained between
+    discovery and the first sample still reaches the tables; after that only a change
+    of more than 5 % is."""
+    be = fixtures.build_backend("2gpu_spx")
+    gpus, _ = be.discover()
+    m = n.HealthMonitor(be, 3)
+    m.set_gpus([be.gpu_key(g.index) for g in gpus])
+    for g in (0, 1):
+        m.on_sample(g, True, be.sample(g))
+    q = [u for u in m.pop(100) if u.kind == n.EVT_LINK_QUALITY]
+    assert len(q) == 1 and q[0].link_gbps == 608.0 and {q[0].gpu, q[0].peer} == {0, 1}
+    be.set_link_bandwidth(0, 1, 600.0)  # within 5 %: not a re-train
+    m.on_sample(0, True, be.sample(0))
+    assert not [u for u in m.pop(50) if u.kind == n.EVT_LINK_QUALITY]
+    be.set_link_bandwidth(0, 1, 304.0)
+    m.on_sample(1, True, be.sample(1))
+    q = [u for u in m.pop(100) if u.kind == n.EVT_LINK_QUALITY]
+    assert len(q) == 1 and q[0].link_gbps == 304.0 and "re-trained" in q[0].reason
