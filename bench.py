@@ -125,6 +125,20 @@ def _merge_tail(parts) -> dict:
     return out
 
 
+def _server_mean(text: str, rpc: str):
+    """Mean of the daemon's amdgpu_device_plugin_rpc_duration_seconds for one RPC: the
+    time from a request's dispatch to its encoded answer, without the transport."""
+    tot = cnt = 0.0
+    for line in text.splitlines():
+        if 'rpc="%s"' % rpc not in line:
+            continue
+        if line.startswith("amdgpu_device_plugin_rpc_duration_seconds_sum"):
+            tot += float(line.rsplit(" ", 1)[1])
+        elif line.startswith("amdgpu_device_plugin_rpc_duration_seconds_count"):
+            cnt += float(line.rsplit(" ", 1)[1])
+    return tot / cnt if cnt else None
+
+
 def _allocator_probe(n) -> float:
     """The xGMI allocator's own cost for a size-4 request over an 8-GPU mesh (two NUMA
     nodes), timed natively.  On a 1-GPU box the kubelet GetPreferredAllocation above
@@ -380,6 +394,9 @@ def main() -> int:
     # /metrics: one loopback TCP exchange of a scrape's size, polling server
     mine["tcp_scrape_floor_p50"] = _pct(n.uds_pingpong(3000, 300, 90, body_len + 400, server_spin=True, tcp=True),
                                         0.5)
+    if rank == 0:  # the daemon's own time per Allocate (decode, lookup, encode), from its histogram
+        conn.request("GET", "/metrics")
+        mine["server_allocate_mean_s"] = _server_mean(conn.getresponse().read().decode(), "Allocate")
     if world > 1:
         gathered = [None] * world
         dist.all_gather_object(gathered, mine)
@@ -416,6 +433,8 @@ def main() -> int:
             "uds_roundtrip_floor_spin_p99_us": round(gathered[0]["uds_floor_spin_p99"] * 1e6, 2),
             "uds_roundtrip_floor_spin_p999_us": round(gathered[0]["uds_floor_spin_p999"] * 1e6, 2),
             "preferred_allocator_8gpu_size4_p50_us": _allocator_probe(n),
+            "allocate_server_mean_us": (round(gathered[0]["server_allocate_mean_s"] * 1e6, 3)
+                                        if gathered[0].get("server_allocate_mean_s") else None),
             "advertised_devices": len(ids), "world_size": world,
             "dist_backend": (dist.get_backend() if world > 1 else None),
             "uds_roundtrip_floor_p50_us": round(gathered[0]["uds_floor_p50"] * 1e6, 2),
