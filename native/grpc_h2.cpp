@@ -956,7 +956,10 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
               shed_.add();
               continue;
             }
-            if (errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) {
+            // only a listener that is gone or no longer listening is a server fault;
+            // the rest (ECONNABORTED, EPROTO, ENOBUFS, pending network errors) concern
+            // one connection and the next accept may succeed
+            if (errno == EBADF || errno == EINVAL || errno == ENOTSOCK) {
               const int e = errno;
               epoll_ctl(w->ep, EPOLL_CTL_DEL, listen_fd_, nullptr);
               fail("accept on " + path_ + ": " + strerror(e));
