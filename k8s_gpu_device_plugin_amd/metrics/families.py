@@ -62,7 +62,7 @@ FAMILIES = (
     Family("amdgpu_xgmi_link_bitrate_gbps", "gauge", GPU + ("link", "peer"), "exporter",
            "Per-lane signalling rate (38 on MI355X); a link trained slower than its peers is degraded"),
     Family("amdgpu_xgmi_link_bandwidth_gbps", "gauge", GPU + ("link", "peer"), "exporter",
-           "Link bandwidth over all lanes (608 Gb/s on MI355X)"),
+           "Trained link bandwidth: current per-lane rate x current link width (608 Gb/s on a healthy MI355X link)"),
     # --- per-partition ---
     Family("amdgpu_partition_info", "gauge", PART, "exporter", "Partition -> device id / resource (value 1)"),
     Family("amdgpu_partition_gfx_busy_percent", "gauge", PART, "exporter", "Per-XCP compute busy"),

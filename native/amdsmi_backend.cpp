@@ -353,16 +353,22 @@ class AmdSmiBackend : public Backend {
     links_.assign(procs_.size(), LinkCache{});  // indexes may have moved: re-verify
     for (int a = 0; a < n; ++a) {
       GpuSample s;
+      amdsmi_gpu_metrics_t gm;
+      std::memset(&gm, 0, sizeof(gm));
+      if (amdsmi_get_gpu_metrics_info(procs_[a][0], &gm) == AMDSMI_STATUS_SUCCESS && valid16(gm.xgmi_link_width) &&
+          gm.xgmi_link_width != 0)
+        s.xgmi_link_width = gm.xgmi_link_width;
       link_state_locked(a, &s, nullptr);
       (*gpus)[a].num_xgmi_links = s.num_links;
       for (int k = 0; k < s.num_links; ++k) {
         const int p = s.link_peer[k];
         if (p < 0) continue;
         if (s.link_up[k] == 0) topo->at(a, p).up = topo->at(p, a).up = false;
-        // trained bandwidth per link (the allocator scores a slow link below a full-rate one)
-        if (s.link_max_gbps[k] > 0) {
+        // trained bandwidth per link (the allocator scores a slow link below a full-rate
+        // one); each end reports its view, the link runs at the slower of the two
+        if (s.link_trained_gbps[k] > 0) {
           const double cur = topo->at(a, p).bw_gbps;
-          const double bw = cur > 0 ? std::min(cur, s.link_max_gbps[k]) : s.link_max_gbps[k];
+          const double bw = cur > 0 ? std::min(cur, s.link_trained_gbps[k]) : s.link_trained_gbps[k];
           topo->at(a, p).bw_gbps = topo->at(p, a).bw_gbps = bw;
         }
       }
@@ -419,6 +425,8 @@ class AmdSmiBackend : public Backend {
       else if (valid16(m.average_gfxclk_frequency)) s->gfxclk_mhz = m.average_gfxclk_frequency;
       if (valid16(m.current_uclk)) s->uclk_mhz = m.current_uclk;
       if (m.throttle_status != 0xFFFFFFFFu) s->throttle_status = m.throttle_status;
+      if (valid16(m.xgmi_link_width)) s->xgmi_link_width = m.xgmi_link_width;
+      if (valid16(m.xgmi_link_speed)) s->xgmi_link_speed = m.xgmi_link_speed;
       const int nparts = static_cast<int>(procs_[gpu].size());
       s->num_partitions = std::min(nparts, kMaxPartitions);
       for (int p = 0; p < s->num_partitions && p < AMDSMI_MAX_NUM_XCP; ++p) {
@@ -656,6 +664,7 @@ class AmdSmiBackend : public Backend {
         else
           s->link_up[i] = -1;
       }
+      fill_trained(s);
       return;
     }
     ++link_full_;
@@ -702,6 +711,17 @@ class AmdSmiBackend : public Backend {
     lc.n = s->num_links;
     lc.counters_ok = counters_ok && lc.n > 0;
     lc.status_ok = lc.counters_ok && status_ok;
+    fill_trained(s);
+  }
+
+  // Trained bandwidth of each link: its current per-lane rate (link metrics bit_rate)
+  // times the GPU's current link width (gpu_metrics; set by the caller when known).
+  // max_bandwidth is the capability and stays 608 Gb/s on a link that trained narrower.
+  static void fill_trained(GpuSample* s) {
+    for (int i = 0; i < s->num_links; ++i)
+      s->link_trained_gbps[i] = (s->link_bitrate_gbps[i] > 0 && s->xgmi_link_width > 0)
+                                    ? s->link_bitrate_gbps[i] * s->xgmi_link_width
+                                    : s->link_max_gbps[i];
   }
 
   void disarm_locked() {

@@ -131,7 +131,13 @@ struct GpuSample {
   double link_read_kb[kMaxXgmiLinks] = {};
   double link_write_kb[kMaxXgmiLinks] = {};
   double link_bitrate_gbps[kMaxXgmiLinks] = {};   // per-lane signalling rate, Gb/s (0 = unknown)
-  double link_max_gbps[kMaxXgmiLinks] = {};       // link bandwidth (all lanes), Gb/s (0 = unknown)
+  double link_max_gbps[kMaxXgmiLinks] = {};       // link capability (all lanes, max rate), Gb/s (0 = unknown)
+  // What the link trained at: its current per-lane rate x the GPU's current link width
+  // (gpu_metrics); falls back to the capability when either is unknown.  0 = unknown.
+  double link_trained_gbps[kMaxXgmiLinks] = {};
+  // gpu_metrics: the GPU's current xGMI link width (lanes) and per-lane rate; -1 = unknown
+  double xgmi_link_width = -1;
+  double xgmi_link_speed = -1;
   int num_partitions = 0;
   double partition_gfx_busy_pct[kMaxPartitions] = {};
   double partition_vram_used_bytes[kMaxPartitions] = {};

@@ -139,11 +139,13 @@ PYBIND11_MODULE(_native, m) {
       .def_readonly("pending_pages", &GpuSample::pending_pages)
       .def_readonly("unreservable_pages", &GpuSample::unreservable_pages)
       .def_readonly("throttle_status", &GpuSample::throttle_status)
+      .def_readonly("xgmi_link_width", &GpuSample::xgmi_link_width)
+      .def_readonly("xgmi_link_speed", &GpuSample::xgmi_link_speed)
       .def_property_readonly("links", [](const GpuSample& s) {
         py::list l;
         for (int k = 0; k < s.num_links; ++k)
           l.append(py::make_tuple(s.link_peer[k], s.link_up[k], s.link_read_kb[k], s.link_write_kb[k],
-                                  s.link_bitrate_gbps[k], s.link_max_gbps[k]));
+                                  s.link_bitrate_gbps[k], s.link_max_gbps[k], s.link_trained_gbps[k]));
         return l;
       })
       .def_property_readonly("partition_gfx_busy_pct", [](const GpuSample& s) {

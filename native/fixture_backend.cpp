@@ -208,6 +208,8 @@ bool FixtureBackend::sample(int index, GpuSample* s) {
   s->unreservable_pages = 0;
   s->throttle_status = 0;
   s->num_links = 0;
+  s->xgmi_link_width = 16;
+  s->xgmi_link_speed = 38;
   for (int peer = 0; peer < topo_.n && s->num_links < kMaxXgmiLinks; ++peer) {
     if (peer == gpu || topo_.at(gpu, peer).type != kLinkXgmi) continue;
     const int k = s->num_links++;
@@ -217,8 +219,9 @@ bool FixtureBackend::sample(int index, GpuSample* s) {
     s->link_write_kb[k] = 0.9e6 * ts * load;
     // what amdsmi reports on MI355X: 38 Gb/s per lane, 16 lanes -> 608 Gb/s per link
     const double bw = topo_.at(gpu, peer).bw_gbps > 0 ? topo_.at(gpu, peer).bw_gbps : 608.0;
-    s->link_bitrate_gbps[k] = bw / 16.0;
-    s->link_max_gbps[k] = bw;
+    s->link_bitrate_gbps[k] = bw / 16.0;  // a slow fixture link trained at a lower rate, 16 lanes wide
+    s->link_max_gbps[k] = 608.0;          // capability
+    s->link_trained_gbps[k] = bw;
   }
   s->num_partitions = std::min<int>(static_cast<int>(g.partitions.size()), kMaxPartitions);
   for (int p = 0; p < s->num_partitions; ++p) {

@@ -197,12 +197,12 @@ void HealthMonitor::process(const HwEvent& e) {
       return;
     }
     case kEvtLinkQuality: {
+      // e.value: the link's bandwidth now (the slower end's view); one update per pair
       if (!known || peer_key.empty() || e.value <= 0) return;
-      auto& m = state_[key].link_bw;
-      auto it = m.find(peer_key);
-      if (it != m.end() && std::fabs(it->second - e.value) <= 0.05 * std::max(it->second, e.value)) return;
-      m[peer_key] = e.value;
-      state_[peer_key].link_bw[key] = e.value;  // the peer reports the same link: deduplicated
+      const auto pk = key < peer_key ? std::make_pair(key, peer_key) : std::make_pair(peer_key, key);
+      auto it = pair_bw_.find(pk);
+      if (it != pair_bw_.end() && std::fabs(it->second - e.value) <= 0.05 * std::max(it->second, e.value)) return;
+      pair_bw_[pk] = e.value;
       HealthUpdate u;
       u.kind = e.kind;
       u.gpu = table_index_locked(key);
@@ -278,22 +278,30 @@ void HealthMonitor::on_sample(int gpu, bool ok, const GpuSample& s) {
           e.peer_key = peer_keys[k];
           derived.push_back(e);
         }
-        // Trained bandwidth: the first reading of a link is reported too (the link may
+        // Trained bandwidth, as this end sees it.  A link runs at the slower of its two
+        // ends' views: the pair's value is reported when it is first known (the link may
         // have re-trained between discovery and this sample; the manager applies it only
-        // where the tables disagree), and after that every re-train to another rate
-        // (> 5 % off).
-        const double bw = s.link_max_gbps[k];
+        // where the tables disagree) and whenever it moves by more than 5 %.
+        const double bw = s.link_trained_gbps[k];
         if (s.link_up[k] == 1 && bw > 0) {
-          auto bt = st.link_bw.find(peer_keys[k]);
-          const bool first = bt == st.link_bw.end();
-          if (first || std::fabs(bt->second - bw) > 0.05 * std::max(bt->second, bw)) {
+          st.link_bw[peer_keys[k]] = bw;
+          const auto pt = state_.find(peer_keys[k]);
+          double eff = bw;
+          if (pt != state_.end()) {
+            const auto pv = pt->second.link_bw.find(key);
+            if (pv != pt->second.link_bw.end()) eff = std::min(eff, pv->second);
+          }
+          const auto pk = key < peer_keys[k] ? std::make_pair(key, peer_keys[k]) : std::make_pair(peer_keys[k], key);
+          const auto last = pair_bw_.find(pk);
+          if (last == pair_bw_.end() || std::fabs(last->second - eff) > 0.05 * std::max(last->second, eff)) {
             HwEvent e = event(kEvtLinkQuality,
-                              first ? "xgmi link bandwidth: " + std::to_string(static_cast<int>(bw)) + " Gb/s"
-                                    : "xgmi link re-trained: " + std::to_string(static_cast<int>(bt->second)) + " -> " +
-                                          std::to_string(static_cast<int>(bw)) + " Gb/s");
+                              last == pair_bw_.end()
+                                  ? "xgmi link bandwidth: " + std::to_string(static_cast<int>(eff)) + " Gb/s"
+                                  : "xgmi link re-trained: " + std::to_string(static_cast<int>(last->second)) + " -> " +
+                                        std::to_string(static_cast<int>(eff)) + " Gb/s");
             e.peer = s.link_peer[k];
             e.peer_key = peer_keys[k];
-            e.value = bw;
+            e.value = eff;
             derived.push_back(e);
           }
         }

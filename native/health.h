@@ -110,7 +110,7 @@ class HealthMonitor {
     int64_t last_ue = -1;
     bool reported_healthy = true;
     std::map<std::string, int> link_up;  // peer key -> 1/0
-    std::map<std::string, double> link_bw;  // peer key -> last trained bandwidth seen, Gb/s
+    std::map<std::string, double> link_bw;  // peer key -> trained bandwidth as this end last saw it
     int page_threshold = 0;
   };
   void loop();
@@ -128,6 +128,7 @@ class HealthMonitor {
   std::condition_variable cv_;
   std::deque<HealthUpdate> queue_;
   std::unordered_map<std::string, GpuState> state_;
+  std::map<std::pair<std::string, std::string>, double> pair_bw_;  // link -> last reported bandwidth
   std::vector<std::string> table_keys_;  // table index -> key
   std::vector<std::shared_ptr<DeviceTable>> fast_tables_;
   bool fast_recover_ = false;

@@ -497,9 +497,9 @@ void Exporter::render_gpu_text(const std::vector<GpuSample>& samples, const std:
         if (s.link_up[k] >= 0) line(&up, "amdgpu_xgmi_link_up", l, s.link_up[k]);
         line(&rd, "amdgpu_xgmi_read_bytes_total", l, s.link_read_kb[k] * 1024.0);
         line(&wr, "amdgpu_xgmi_write_bytes_total", l, s.link_write_kb[k] * 1024.0);
-        if (s.link_max_gbps[k] > 0) {  // a link trained slower than its peers shows here
+        if (s.link_trained_gbps[k] > 0) {  // a link trained slower than its peers shows here
           line(&rate, "amdgpu_xgmi_link_bitrate_gbps", l, s.link_bitrate_gbps[k]);
-          line(&maxr, "amdgpu_xgmi_link_bandwidth_gbps", l, s.link_max_gbps[k]);
+          line(&maxr, "amdgpu_xgmi_link_bandwidth_gbps", l, s.link_trained_gbps[k]);
         }
       }
     }
