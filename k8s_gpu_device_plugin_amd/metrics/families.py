@@ -48,6 +48,8 @@ FAMILIES = (
     Family("amdgpu_vram_used_bytes", "gauge", GPU, "exporter", "VRAM used"),
     Family("amdgpu_vram_total_bytes", "gauge", GPU, "exporter", "VRAM capacity"),
     Family("amdgpu_throttle_status", "gauge", GPU, "exporter", "Throttle status bitmask"),
+    Family("amdgpu_xgmi_link_width", "gauge", GPU, "exporter", "Current xGMI link width, lanes (16 when fully trained)"),
+    Family("amdgpu_xgmi_link_speed_gbps", "gauge", GPU, "exporter", "Current xGMI per-lane rate (38 Gb/s on MI355X)"),
     Family("amdgpu_temperature_celsius", "gauge", GPU + ("sensor",), "exporter",
            "Temperature by sensor: edge, hotspot, mem, hbm0..N"),
     Family("amdgpu_clock_mhz", "gauge", GPU + ("clock",), "exporter", "gfx / mem clocks"),

@@ -411,6 +411,10 @@ void Exporter::render_gpu_text(const std::vector<GpuSample>& samples, const std:
   per_gpu("amdgpu_vram_total_bytes", "VRAM capacity.", "gauge", [](const GpuSample& s) { return s.vram_total_bytes; });
   per_gpu("amdgpu_throttle_status", "Raw throttle status bitmask.", "gauge",
           [](const GpuSample& s) { return static_cast<double>(s.throttle_status); });
+  per_gpu("amdgpu_xgmi_link_width", "Current xGMI link width of the GPU, lanes (16 when fully trained).", "gauge",
+          [](const GpuSample& s) { return s.xgmi_link_width; });
+  per_gpu("amdgpu_xgmi_link_speed_gbps", "Current xGMI per-lane rate of the GPU, Gb/s.", "gauge",
+          [](const GpuSample& s) { return s.xgmi_link_speed; });
 
   {  // temperatures
     bool hdr = false;
