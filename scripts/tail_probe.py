@@ -10,6 +10,9 @@ several variants and attributes each slow call:
   no_gap         batches back to back, no scrape phase between them
   floor          the bare unix-socket exchange (no daemon, polling server thread)
 
+With --gap-kind: a plain 50 ms sleep between batches instead of the scrape phase, and
+the scrape phase with the HTTP workers' busy-poll off.
+
     python scripts/tail_probe.py [--batches 40] [--out gpurun_out/tail_probe.json]
 """
 from __future__ import annotations
@@ -62,7 +65,7 @@ def analyse(batches):
             "client_cpus": sorted({c for _, _, cs in batches for c in cs})}
 
 
-def run_variant(name, batches, overrides=None, pin=False, gap=True):
+def run_variant(name, batches, overrides=None, pin=False, gap=True, idle_gap_s=0.0):
     from k8s_gpu_device_plugin_amd import native
     from k8s_gpu_device_plugin_amd.api import v1beta1
     from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import DevicePluginClient
@@ -88,7 +91,9 @@ def run_variant(name, batches, overrides=None, pin=False, gap=True):
             recs = []
             for _ in range(batches):
                 recs.append(h2.bench_unary_ts(v1beta1.METHOD_ALLOCATE, req, ALLOCS))
-                if gap:
+                if idle_gap_s:
+                    time.sleep(idle_gap_s)
+                elif gap:
                     n.http_load("127.0.0.1", port, "/metrics", bench.SCRAPE_CONNS, bench.SCRAPE_S, 0.0)
         finally:
             h2.close()
@@ -114,6 +119,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--batches", type=int, default=40)
     ap.add_argument("--out", default="")
+    ap.add_argument("--gap-kind", action="store_true", help="A/B idle gaps against scrape-phase gaps instead")
     a = ap.parse_args()
     from k8s_gpu_device_plugin_amd import native
     n = native.load()
@@ -123,11 +129,17 @@ def main() -> int:
                     "p999_us": round(pct(floor, 0.999) * 1e6, 2), "max_us": round(max(floor) * 1e6, 2),
                     "slow_fraction": round(sum(1 for x in floor if x > 2 * pct(floor, 0.5)) / len(floor), 4)}
     print(json.dumps({"floor": res["floor"]}), flush=True)
-    for name, kw in (("default", {}),
-                     ("no_sampler", {"overrides": {"telemetry": {"enabled": False}, "health": {"enabled": False}}}),
-                     ("pinned_client", {"pin": True}),
-                     ("no_gap", {"gap": False}),
-                     ("default_again", {})):
+    variants = (("default", {}),
+                ("no_sampler", {"overrides": {"telemetry": {"enabled": False}, "health": {"enabled": False}}}),
+                ("pinned_client", {"pin": True}),
+                ("no_gap", {"gap": False}),
+                ("default_again", {}))
+    if a.gap_kind:  # what about the gap slows the next call: idleness or the scraping next door?
+        variants = (("scrape_gap", {}),
+                    ("idle_gap_50ms", {"idle_gap_s": 0.05}),
+                    ("scrape_gap_http_no_busy_poll", {"overrides": {"http": {"busyPollUs": 0}}}),
+                    ("scrape_gap_again", {}))
+    for name, kw in variants:
         t0 = time.time()
         r = run_variant(name, a.batches, **kw)
         r["wall_s"] = round(time.time() - t0, 1)
