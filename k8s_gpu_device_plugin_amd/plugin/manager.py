@@ -470,7 +470,8 @@ class PluginManager:
             g = gpu_of.get((res, dev))
             if g is not None and g >= 0:
                 spans.setdefault((ns, pod), set()).add(g)
-        n = max([g.index for g in self.gpus], default=-1) + 1
+        # the tables' topology spans every discovered GPU, also those `devices` leaves out
+        n = self.topology.n if self.topology is not None else max([g.index for g in self.gpus], default=-1) + 1
         load = [0] * (n * n)
         multi = 0
         for gs in spans.values():

@@ -1,5 +1,7 @@
 #include "allocator.h"
 
+#include "metrics.h"  // cpu_relax
+
 #include <algorithm>
 #include <cmath>
 #include <map>
@@ -403,13 +405,19 @@ RecentAllocations::RecentAllocations() = default;
 
 void RecentAllocations::record(uint64_t gpu_mask, int64_t now_ns) {
   if (__builtin_popcountll(gpu_mask) < 2 || ttl_ns_.load(std::memory_order_relaxed) == 0) return;
-  Slot& s = slots_[next_.fetch_add(1, std::memory_order_relaxed) % kSlots];
-  const uint64_t q = s.seq.load(std::memory_order_relaxed);
-  s.seq.store(q + 1, std::memory_order_relaxed);  // odd: being written
-  std::atomic_thread_fence(std::memory_order_release);
-  s.mask.store(gpu_mask, std::memory_order_relaxed);
-  s.ts.store(now_ns, std::memory_order_relaxed);
-  s.seq.store(q + 2, std::memory_order_release);
+  // Each writer owns its slot: it claims it by moving seq from even to odd with a CAS.  A
+  // slot another writer still holds (one preempted while the ring wrapped) is skipped;
+  // two writers in one slot could otherwise leave seq odd for good.
+  for (int tries = 0; tries < kSlots; ++tries) {
+    Slot& s = slots_[next_.fetch_add(1, std::memory_order_relaxed) % kSlots];
+    uint64_t q = s.seq.load(std::memory_order_relaxed);
+    if ((q & 1) || !s.seq.compare_exchange_strong(q, q + 1, std::memory_order_relaxed)) continue;
+    std::atomic_thread_fence(std::memory_order_release);
+    s.mask.store(gpu_mask, std::memory_order_relaxed);
+    s.ts.store(now_ns, std::memory_order_relaxed);
+    s.seq.store(q + 2, std::memory_order_release);
+    break;
+  }
   int64_t cur = newest_.load(std::memory_order_relaxed);
   while (cur < now_ns && !newest_.compare_exchange_weak(cur, now_ns, std::memory_order_release)) {
   }
@@ -426,15 +434,21 @@ int RecentAllocations::add_link_pods(int n, int64_t now_ns, std::vector<int>* po
   for (const Slot& s : slots_) {
     uint64_t mask;
     int64_t ts;
-    for (;;) {  // seqlock read: retry while a writer is in the slot
+    // seqlock read: retry while a writer is in the slot, but never wait on a writer that
+    // was preempted there (the entry is then left out of this one answer)
+    bool got = false;
+    for (int spin = 0; spin < 256 && !got; ++spin) {
       const uint64_t q0 = s.seq.load(std::memory_order_acquire);
-      if (q0 & 1) continue;
+      if (q0 & 1) {
+        cpu_relax();
+        continue;
+      }
       mask = s.mask.load(std::memory_order_relaxed);
       ts = s.ts.load(std::memory_order_relaxed);
       std::atomic_thread_fence(std::memory_order_acquire);
-      if (s.seq.load(std::memory_order_relaxed) == q0) break;
+      got = s.seq.load(std::memory_order_relaxed) == q0;
     }
-    if (!fresh(ts, now_ns)) continue;
+    if (!got || !fresh(ts, now_ns)) continue;
     ++live;
     if (!pods) continue;
     for (uint64_t a = mask; a; a &= a - 1) {
@@ -452,6 +466,8 @@ int RecentAllocations::add_link_pods(int n, int64_t now_ns, std::vector<int>* po
 }
 
 int RecentAllocations::live(int64_t now_ns) const { return add_link_pods(0, now_ns, nullptr); }
+
+bool RecentAllocations::maybe_live(int64_t now_ns) const { return fresh(newest_.load(std::memory_order_acquire), now_ns); }
 
 AllocResult distributed_alloc(const std::vector<AllocDevice>& devs, const std::vector<int>& avail,
                               const std::vector<int>& required, int size) {

@@ -77,6 +77,8 @@ class RecentAllocations {
   // Returns the number of live entries (0: nothing added, the caller can skip a copy).
   int add_link_pods(int n, int64_t now_ns, std::vector<int>* pods) const;
   int live(int64_t now_ns) const;
+  // False when no entry can be live (one load; the common case on the Allocate path).
+  bool maybe_live(int64_t now_ns) const;
 
  private:
   bool fresh(int64_t ts, int64_t now_ns) const;

@@ -471,12 +471,14 @@ AllocResult DeviceTable::preferred_core(const std::string_view* avail, size_t n_
   }
   if (aligned_ok_ && !any_annotated) {
     const auto topo = std::atomic_load_explicit(&topo_, std::memory_order_acquire);  // snapshot
-    if (RecentAllocations* ra = recent_.load(std::memory_order_acquire)) {
+    RecentAllocations* ra = recent_.load(std::memory_order_acquire);
+    const int64_t now = ra ? mono_ns() : 0;
+    if (ra && ra->maybe_live(now)) {
       // multi-GPU containers allocated since the last PodResources poll: their links
       // count as used too
       thread_local std::vector<int> extra;
       extra.assign(static_cast<size_t>(topo->n) * topo->n, 0);
-      if (ra->add_link_pods(topo->n, mono_ns(), &extra) > 0) {
+      if (ra->add_link_pods(topo->n, now, &extra) > 0) {
         thread_local Topology with_recent;
         with_recent = *topo;
         for (size_t i = 0; i < extra.size(); ++i) with_recent.links[i].pods += extra[i];

@@ -528,6 +528,44 @@ static void test_histogram_render_cache() {
   CHECK(fin == ref && fin.find("x_seconds_count{rpc=\"a\"} 20001\n") != std::string::npos);
 }
 
+// RecentAllocations: many writers wrap the 64-slot ring while readers snapshot it.
+// Readers must always finish (no slot left odd by two writers) and only ever see masks
+// that were written; once the writers stop, every slot is readable again.
+static void test_recent_allocations_ring() {
+  RecentAllocations ra;
+  const int64_t t0 = 1'000'000'000LL;
+  std::atomic<bool> go{true};
+  std::atomic<long> bad{0}, reads{0};
+  std::vector<std::thread> ws, rs;
+  for (int w = 0; w < 6; ++w)
+    ws.emplace_back([&, w] {
+      const uint64_t m = (1ull << w) | (1ull << (w + 1));  // GPU pair (w, w+1)
+      for (int i = 0; i < 40000; ++i) ra.record(m, t0 + i);
+    });
+  for (int r = 0; r < 3; ++r)
+    rs.emplace_back([&] {
+      std::vector<int> pods(64);
+      while (go.load(std::memory_order_relaxed)) {
+        std::fill(pods.begin(), pods.end(), 0);
+        const int live = ra.add_link_pods(8, t0 + 1000, &pods);
+        int pairs = 0;  // every live entry is exactly one adjacent pair
+        for (int a = 0; a < 8; ++a)
+          for (int b = a + 1; b < 8; ++b) {
+            if (pods[a * 8 + b] && b != a + 1) bad.fetch_add(1);
+            pairs += pods[a * 8 + b];
+          }
+        if (pairs != live) bad.fetch_add(1);
+        reads.fetch_add(1);
+      }
+    });
+  for (auto& t : ws) t.join();
+  go = false;
+  for (auto& t : rs) t.join();
+  CHECK(bad.load() == 0);
+  CHECK(reads.load() > 0);
+  CHECK(ra.live(t0 + 40000) == RecentAllocations::kSlots);  // no slot stuck mid-write
+}
+
 int main() {
   char tmpl[] = "/tmp/amdgpu-selftest-XXXXXX";
   const char* dir = mkdtemp(tmpl);
@@ -536,6 +574,8 @@ int main() {
   test_hpack();
   std::fprintf(stderr, "[selftest] histogram render cache\n");
   test_histogram_render_cache();
+  std::fprintf(stderr, "[selftest] recent allocations ring\n");
+  test_recent_allocations_ring();
   std::fprintf(stderr, "[selftest] allocator + table\n");
   auto be = make_node(8, 8);
   test_allocator_and_table(be);

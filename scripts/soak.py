@@ -179,10 +179,18 @@ def main():
         rs = stats["rss_kb"]
         half = rs[len(rs) // 2:] or rs
         stats["rss_growth_second_half_kb"] = (max(half) - min(half)) if half else None
-        # descriptors and threads do not accumulate over reloads
-        fd_half, th_half = stats["fds"][len(stats["fds"]) // 2:], stats["threads"][len(stats["threads"]) // 2:]
-        stats["fd_growth_second_half"] = (max(fd_half) - min(fd_half)) if fd_half else None
-        stats["thread_growth_second_half"] = (max(th_half) - min(th_half)) if th_half else None
+        # descriptors and threads do not accumulate over reloads.  A sample taken while a
+        # reload has the old servers down reads low (a dip, not growth): compare the
+        # medians of the second and last quarters instead of max - min.
+        def growth(xs):
+            q = len(xs) // 4
+            if q < 2:
+                return None
+            mid, last = sorted(xs[q:2 * q]), sorted(xs[-q:])
+            return last[len(last) // 2] - mid[len(mid) // 2]
+
+        stats["fd_growth_second_half"] = growth(stats["fds"])
+        stats["thread_growth_second_half"] = growth(stats["threads"])
         stats["ok"] = bool(stats["daemon_alive"] and stats["health_after"] == 200 and stats["allocs"] > 0
                            and (stats["fd_growth_second_half"] or 0) <= 8
                            and (stats["thread_growth_second_half"] or 0) <= 8

@@ -732,6 +732,31 @@ def test_pod_resources_feed_link_load_to_the_allocator(make_cfg, plugin_dir, run
         stub.stop()
 
 
+def test_pod_link_load_uses_the_whole_node_topology(make_cfg, plugin_dir, run_manager, tmp_path):
+    """`devices` advertises GPUs 0-2 of a 4-GPU node: the tables' topology still spans all
+    4 GPUs, so a pod on GPUs 1 and 2 must land on link 1-2 (a row stride of 3 put it on
+    1-1 and 1-3)."""
+    from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import PodResourcesStub
+    sock = str(tmp_path / "pod-resources" / "kubelet.sock")
+    stub = PodResourcesStub(sock).start()
+    try:
+        with KubeletStub(plugin_dir) as k:
+            m = run_manager(make_cfg(fixture="4gpu_cpx", migStrategy="single", devices="0-2",
+                                     podResources={"enabled": True, "socket": sock, "intervalS": 0.05}))
+            k.wait_for_registrations(1)
+            t = m.plugins[0].table
+            assert t.topology().n == 4 and len(t.ids()) == 24
+            ids = t.ids()
+            stub.set_pods([("ml", "ring-1", [("main", "amd.com/gpu", ids[8:12] + ids[16:20])])])
+            assert _wait(lambda: t.topology().link(1, 2).pods == 1)
+            topo = t.topology()
+            assert topo.link(2, 1).pods == 1
+            assert sum(topo.link(a, b).pods for a in range(4) for b in range(4)) == 2
+            assert 'amdgpu_xgmi_link_pods{gpu="1",peer="2"} 1' in m.exporter.render()
+    finally:
+        stub.stop()
+
+
 @pytest.mark.parametrize("fault", ["worker", "listener"])
 def test_native_server_fault_is_restarted_and_reregistered(make_cfg, plugin_dir, run_manager, fault):
     """The native gRPC server loses a worker (exception) or its listening socket: the
