@@ -230,3 +230,24 @@ def test_log_max_age_config_validation():
     assert config.validate(config.from_dict({"log": {"maxAgeDays": 7}})).log.maxAgeDays == 7
     with pytest.raises(config.ConfigError):
         config.validate(config.from_dict({"log": {"maxAgeDays": -1}}))
+
+
+def test_every_config_key_is_documented():
+    """docs/CONFIG.md names every key of the Config dataclasses (nested keys dotted), so a
+    new option cannot ship undocumented."""
+    import dataclasses
+
+    from k8s_gpu_device_plugin_amd import config as C
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    doc = open(os.path.join(root, "docs", "CONFIG.md")).read()
+
+    def keys(cls, prefix=""):
+        for f in dataclasses.fields(cls):
+            default = f.default_factory() if f.default_factory is not dataclasses.MISSING else f.default
+            if dataclasses.is_dataclass(default):
+                yield from keys(type(default), prefix + f.name + ".")
+            else:
+                yield prefix + f.name
+
+    missing = [k for k in keys(C.Config) if "`%s`" % k not in doc]
+    assert not missing, missing
