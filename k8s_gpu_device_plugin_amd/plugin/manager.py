@@ -433,9 +433,12 @@ class PluginManager:
         elif u.link_up in (0, 1):
             a = self._index_of.get(key, -1)
             b = self._index_of.get(getattr(u, "peer_key", "") or self._key_of.get(u.peer, ""), -1)
-            if a >= 0 and b >= 0:
-                for p in self.plugins:
-                    p.set_link_up(a, b, bool(u.link_up))
+            if a < 0 or b < 0:  # an end that is not advertised (gone, or left out by `devices`)
+                log.debug("xGMI link %s<->%s %s (not advertised)", key, getattr(u, "peer_key", "") or u.peer,
+                          "up" if u.link_up else "down")
+                return
+            for p in self.plugins:
+                p.set_link_up(a, b, bool(u.link_up))
             log.warning("xGMI link %d<->%d %s", a, b, "up" if u.link_up else "down")
         elif u.kind == native.load().EVT_LINK_QUALITY:
             a = self._index_of.get(key, -1)

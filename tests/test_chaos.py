@@ -1,0 +1,219 @@
+"""Chaos: a seeded random mix of every fault the manager handles, while a kubelet-like
+client keeps allocating, then a heal and a check that the node converges.
+
+Faults: GPU reset (PRE_RESET without its POST_RESET for a while), a GPU falling off the
+bus and coming back (the periodic re-discovery re-advertises around it), xGMI links going
+down and re-training at another rate, ``GET /restart`` reloads, kubelet restarts, and
+native gRPC server faults (supervised restart).  Each is covered alone elsewhere; here they
+overlap in arbitrary order.  After the heal every GPU must be advertised Healthy through
+the last registration's ListAndWatch, the allocator's topology must be whole again, the
+manager must still be running (not fatal), and a fresh reset must still reach kubelet -
+i.e. no latch, index or generation got stuck on the way.
+"""
+import os
+import random
+import threading
+import time
+
+import pytest
+
+from k8s_gpu_device_plugin_amd import native
+from k8s_gpu_device_plugin_amd.models import fixtures
+from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import DevicePluginClient, KubeletStub
+from k8s_gpu_device_plugin_amd.plugin.manager import PluginManager
+
+NGPU = 4
+FULL_GBPS = 608.0
+
+
+def _wait(pred, timeout=10.0, step=0.02):
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline:
+        if pred():
+            return True
+        time.sleep(step)
+    return False
+
+
+def _advertised(plugin_dir, k, timeout=5.0):
+    """(id, health) pairs of the first ListAndWatch message on the newest registration's
+    endpoint, over a fresh connection (what a restarted kubelet would see)."""
+    c = DevicePluginClient(os.path.join(plugin_dir, k.requests[-1].endpoint))
+    try:
+        stream = c.list_and_watch(timeout=timeout)
+        first = next(iter(stream))
+        stream.cancel()
+        return sorted((d.ID, d.health) for d in first.devices)
+    finally:
+        c.close()
+
+
+class _Allocator(threading.Thread):
+    """A kubelet-like client (the compiled HTTP/2 one: it redials at once, without grpc's
+    reconnect backoff) that keeps calling Allocate through every reload."""
+
+    def __init__(self, sock, m):
+        super().__init__(daemon=True)
+        self.sock, self.m = sock, m
+        self.stop_ev = threading.Event()
+        self.ok = 0
+        self.failed = 0
+        self.errors = {}
+
+    def run(self):
+        from k8s_gpu_device_plugin_amd.api import v1beta1
+        n = native.load()
+        c = None
+        i = 0
+        while not self.stop_ev.is_set():
+            try:
+                ids = self.m.plugins[0].table.ids() if self.m.plugins else []
+                if ids:
+                    if c is None:
+                        c = n.H2Client(self.sock)
+                    req = v1beta1.AllocateRequest(container_requests=[
+                        v1beta1.ContainerAllocateRequest(devices_ids=[ids[i % len(ids)]])]).SerializeToString()
+                    try:
+                        c.bench_unary(v1beta1.METHOD_ALLOCATE, req, 1)
+                        self.ok += 1
+                    except RuntimeError as e:
+                        if "grpc-status" not in str(e):
+                            raise
+                        self.failed += 1  # an answer (e.g. an Unhealthy device): the connection is fine
+                        key = str(e)[:60]
+                        self.errors[key] = self.errors.get(key, 0) + 1
+                i += 1
+            except Exception as e:  # noqa: BLE001 - sockets come and go during reloads
+                self.failed += 1
+                key = type(e).__name__ + ": " + str(e)[:60]
+                self.errors[key] = self.errors.get(key, 0) + 1
+                if c is not None:
+                    c.close()
+                c = None
+                time.sleep(0.005)
+            time.sleep(0.002)
+        if c is not None:
+            c.close()
+
+
+# CHAOS_SEEDS=N runs seeds 1..N (a longer hunt); the suite runs three
+@pytest.mark.parametrize("seed", range(1, 1 + int(os.environ.get("CHAOS_SEEDS", "3"))))
+@pytest.mark.parametrize("fixture,strategy,server", [("4gpu_spx", "none", "native"),
+                                                     ("4gpu_cpx", "single", "native"),
+                                                     ("4gpu_spx", "none", "python")])
+def test_random_fault_mix_converges(make_cfg, plugin_dir, seed, fixture, strategy, server):
+    n = native.load()
+    rng = random.Random(seed)
+    be = fixtures.build_backend(fixture)
+    gpus, _ = be.discover()
+    assert len(gpus) == NGPU
+    ids = sorted(p.id for g in gpus for p in g.partitions)  # one device per partition (SPX: per GPU)
+    id_of_slot = {g.index: g.partitions[0].id for g in gpus}
+    cfg = make_cfg(fixture=fixture, migStrategy=strategy, grpc={"server": server}, telemetry={"intervalMs": 30},
+                   rediscoverIntervalS=0.2, retrySeconds=0.2, health={"lostAfterFailures": 2})
+    resetting, present, server_faults = set(), set(range(NGPU)), 0
+    links = {}  # (a, b) -> (up, gbps) for the links chaos has touched
+    with KubeletStub(plugin_dir) as k:
+        m = PluginManager(cfg, backend=be)
+        t = m.start_background()
+        client = None
+        try:
+            k.wait_for_registrations(1)
+            client = _Allocator(os.path.join(plugin_dir, "amd-gpu.sock"), m)
+            client.start()
+            log = []
+            for _ in range(60):
+                op = rng.choice(["reset", "post_reset", "remove", "restore", "link_down", "link_up", "link_bw",
+                                 "api_restart", "kubelet_restart", "server_fault", "idle"])
+                g = rng.randrange(NGPU)
+                a, b = sorted(rng.sample(range(NGPU), 2))
+                if op == "reset" and g in present:
+                    be.inject_event(n.HwEvent(n.EVT_PRE_RESET, g, message="chaos reset"))
+                    resetting.add(g)
+                elif op == "post_reset" and g in present and g in resetting:
+                    be.inject_event(n.HwEvent(n.EVT_POST_RESET, g))
+                    resetting.discard(g)
+                elif op == "remove" and len(present) > 1 and g in present:
+                    be.set_gpu_present(g, False)
+                    present.discard(g)
+                elif op == "restore" and g not in present:
+                    be.set_gpu_present(g, True)
+                    present.add(g)
+                elif op == "link_down":
+                    be.set_link_up(a, b, False)
+                    links[(a, b)] = (False, links.get((a, b), (True, FULL_GBPS))[1])
+                elif op == "link_up":
+                    be.set_link_up(a, b, True)
+                    links[(a, b)] = (True, links.get((a, b), (True, FULL_GBPS))[1])
+                elif op == "link_bw":
+                    bw = rng.choice([FULL_GBPS / 2, FULL_GBPS / 4, FULL_GBPS])
+                    be.set_link_bandwidth(a, b, bw)
+                    links[(a, b)] = (links.get((a, b), (True, FULL_GBPS))[0], bw)
+                elif op == "api_restart":
+                    m.restart()
+                elif op == "kubelet_restart":
+                    k.restart()
+                elif op == "server_fault" and server_faults < 2 and m.plugins:
+                    srv = m.plugins[0]._native_server
+                    if srv is not None:
+                        srv.inject_fault("worker")
+                        server_faults += 1
+                else:
+                    op = "idle"
+                log.append((op, g, a, b))
+                time.sleep(rng.choice([0.0, 0.01, 0.03, 0.08]))
+                assert m.running and m.fatal_error is None, (m.fatal_error, log)
+
+            # ---- heal: everything back, every reset finished ----
+            for g in range(NGPU):
+                if g not in present:
+                    be.set_gpu_present(g, True)
+            for (a, b) in links:
+                be.set_link_up(a, b, True)
+                be.set_link_bandwidth(a, b, FULL_GBPS)
+            time.sleep(0.1)
+            for g in sorted(resetting):
+                be.inject_event(n.HwEvent(n.EVT_POST_RESET, g))
+
+            table = lambda: m.plugins[0].table  # noqa: E731 - replaced by every reload
+
+            def whole():
+                t_ = table()
+                if sorted(t_.ids()) != ids or not all(t_.healthy(i) for i in ids):
+                    return False
+                topo = t_.topology()
+                return all(topo.link(x, y).up and topo.link(x, y).bw_gbps == FULL_GBPS
+                           for x in range(NGPU) for y in range(NGPU) if x != y)
+
+            assert _wait(whole, timeout=15), (log, sorted(table().ids()),
+                                              [table().healthy(i) for i in table().ids()])
+            assert _wait(lambda: m.monitor.unhealthy_keys() == [], timeout=5), m.monitor.unhealthy_keys()
+            assert m.running and m.fatal_error is None
+            assert _wait(lambda: _advertised(plugin_dir, k) == [(i, "Healthy") for i in ids], timeout=10), \
+                _advertised(plugin_dir, k)
+
+            # still wired end to end: a new reset reaches kubelet, and so does its end
+            g = rng.randrange(NGPU)
+            be.inject_event(n.HwEvent(n.EVT_PRE_RESET, g, message="after chaos"))
+            assert _wait(lambda: not table().healthy(id_of_slot[g]))
+            be.inject_event(n.HwEvent(n.EVT_POST_RESET, g))
+            assert _wait(lambda: table().healthy(id_of_slot[g]))
+
+            client.stop_ev.set()
+            client.join(10)
+            assert client.ok > 0, client.errors
+            print("seed", seed, "ops", sorted({o for o, *_ in log}), "allocates ok/failed", client.ok, client.failed,
+                  "registrations", len(k.requests), "counters", dict(m.counters))
+            c = DevicePluginClient(os.path.join(plugin_dir, "amd-gpu.sock"))
+            try:
+                for i in ids:
+                    assert c.allocate([i]).container_responses[0].devices
+            finally:
+                c.close()
+        finally:
+            if client is not None:
+                client.stop_ev.set()
+                client.join(10)
+            m.stop()
+            t.join(10)
+            assert not t.is_alive()
