@@ -14,8 +14,11 @@ HealthMonitor::~HealthMonitor() { stop(); }
 std::string HealthMonitor::key_of(int gpu, const std::string& given) const {
   if (!given.empty()) return given;
   if (gpu < 0) return "";
-  std::string k = backend_ ? backend_->gpu_key(gpu) : std::string();
-  return k.empty() ? "#" + std::to_string(gpu) : k;
+  // The backend names the GPU at `gpu` in its current enumeration; "" means there is none
+  // (an index from before a re-discovery that dropped a GPU), and nothing is recorded for
+  // it.  Only a monitor without a backend numbers GPUs itself.
+  if (!backend_) return "#" + std::to_string(gpu);
+  return backend_->gpu_key(gpu);
 }
 
 int HealthMonitor::table_index_locked(const std::string& key) const {
@@ -232,6 +235,7 @@ void HealthMonitor::on_sample(int gpu, bool ok, const GpuSample& s) {
   // guards their enumeration), so a re-discovery between the read and this call cannot
   // attribute one GPU's counters to another.
   const std::string key = key_of(gpu, s.key);
+  if (key.empty()) return;  // no GPU at that index any more: its health is nobody's
   std::vector<std::string> peer_keys(static_cast<size_t>(std::max(0, s.num_links)));
   if (ok)
     for (int k = 0; k < s.num_links; ++k)

@@ -230,6 +230,7 @@ void Exporter::watchdog_loop(std::shared_ptr<HealthMonitor> monitor) {
     HwEvent e;
     e.kind = kEvtDeviceLost;
     e.gpu = g;
+    e.key = inflight_key_;  // the GPU the call went to, even if the node was re-enumerated since
     e.message = "telemetry call in flight for " + std::to_string(age / 1000000) + " ms (health.sampleStallS)";
     monitor->process(e);  // the GPU recovers through on_sample once the call returns ok
   }
@@ -303,8 +304,10 @@ void Exporter::sample_once(uint64_t sampler_gen) {
     // generation has started): no more backend calls
     if (sampler_gen != 0 && (stop_.load() || sampler_gen_.load() != sampler_gen)) return;
     if (be) {
+      std::string key = be->gpu_key(index[g]);  // outside inflight_mu_: the backend takes its own lock
       {
         std::lock_guard<std::mutex> lk(inflight_mu_);
+        inflight_key_ = std::move(key);
         inflight_since_.store(mono_ns());
         inflight_gpu_.store(index[g]);
       }

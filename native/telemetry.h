@@ -189,6 +189,7 @@ class Exporter : public std::enable_shared_from_this<Exporter> {
   std::thread watchdog_;
   std::atomic<int> stall_ms_{0};
   std::atomic<int> inflight_gpu_{-1};       // GPU whose backend call is in flight, -1 = none
+  std::string inflight_key_;                // its gpu_key when the call started (inflight_mu_)
   std::atomic<int64_t> inflight_since_{0};  // stored before inflight_gpu_
   std::atomic<int> stalled_gpu_{-1};        // GPU the watchdog has reported lost
   std::atomic<int64_t> last_pass_ns_{0};    // end of the last complete pass (mono ns)

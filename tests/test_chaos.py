@@ -110,9 +110,13 @@ def test_random_fault_mix_converges(make_cfg, plugin_dir, seed, fixture, strateg
     ids = sorted(p.id for g in gpus for p in g.partitions)  # one device per partition (SPX: per GPU)
     id_of_slot = {g.index: g.partitions[0].id for g in gpus}
     cfg = make_cfg(fixture=fixture, migStrategy=strategy, grpc={"server": server}, telemetry={"intervalMs": 30},
-                   rediscoverIntervalS=0.2, retrySeconds=0.2, health={"lostAfterFailures": 2})
+                   rediscoverIntervalS=0.2, retrySeconds=0.2,
+                   health={"lostAfterFailures": 2, "sampleStallS": 0.3, "badPageThreshold": 10})
+    orig, _ = be.discover()  # untouched descriptions, to undo partition-mode changes
     resetting, present, server_faults = set(), set(range(NGPU)), 0
     links = {}  # (a, b) -> (up, gbps) for the links chaos has touched
+    ecc = [0] * NGPU
+    stalled, pages_high, remoded = set(), set(), set()
     with KubeletStub(plugin_dir) as k:
         m = PluginManager(cfg, backend=be)
         t = m.start_background()
@@ -124,7 +128,9 @@ def test_random_fault_mix_converges(make_cfg, plugin_dir, seed, fixture, strateg
             log = []
             for _ in range(60):
                 op = rng.choice(["reset", "post_reset", "remove", "restore", "link_down", "link_up", "link_bw",
-                                 "api_restart", "kubelet_restart", "server_fault", "idle"])
+                                 "api_restart", "kubelet_restart", "server_fault", "ecc", "stall", "unstall",
+                                 "pages_high", "pages_low", "discovery_fails", "discovery_ok", "mode_change",
+                                 "mode_restore", "idle"])
                 g = rng.randrange(NGPU)
                 a, b = sorted(rng.sample(range(NGPU), 2))
                 if op == "reset" and g in present:
@@ -158,6 +164,36 @@ def test_random_fault_mix_converges(make_cfg, plugin_dir, seed, fixture, strateg
                     if srv is not None:
                         srv.inject_fault("worker")
                         server_faults += 1
+                elif op == "ecc":  # an uncorrectable error: latched until the GPU's next reset ends
+                    ecc[g] += 1
+                    be.set_ecc_uncorrectable(g, ecc[g])
+                    resetting.add(g)  # the heal's POST_RESET clears the latch
+                elif op == "stall" and not stalled:  # one wedged amdsmi call at a time
+                    be.set_sample_stall(g, True)
+                    stalled.add(g)
+                elif op == "unstall" and stalled:
+                    be.set_sample_stall(stalled.pop(), False)
+                elif op == "pages_high":
+                    be.set_retired_pages(g, 12, 0)
+                    pages_high.add(g)
+                elif op == "pages_low" and g in pages_high:
+                    be.set_retired_pages(g, 0, 0)
+                    pages_high.discard(g)
+                elif op == "discovery_fails":
+                    be.set_fail_discovery(True)
+                    log.append(("discovery_fails", g, a, b))
+                    time.sleep(0.05)
+                    be.set_fail_discovery(False)  # a failed reload waits for its retry
+                    continue
+                elif op == "mode_change" and len(present) == NGPU and g not in remoded:
+                    # an operator re-partitions GPU g (set_gpu_mode re-discovers, so only
+                    # while every GPU is present: slot and index agree)
+                    mode = "SPX" if orig[g].compute_partition != "SPX" else "CPX"
+                    fixtures.set_gpu_mode(be, g, mode, first_render=300 + 8 * g)
+                    remoded.add(g)
+                elif op == "mode_restore" and g in remoded and len(present) == NGPU:
+                    be.replace_gpu(g, orig[g])
+                    remoded.discard(g)
                 else:
                     op = "idle"
                 log.append((op, g, a, b))
@@ -165,9 +201,15 @@ def test_random_fault_mix_converges(make_cfg, plugin_dir, seed, fixture, strateg
                 assert m.running and m.fatal_error is None, (m.fatal_error, log)
 
             # ---- heal: everything back, every reset finished ----
+            for g in stalled:
+                be.set_sample_stall(g, False)
+            for g in pages_high:
+                be.set_retired_pages(g, 0, 0)
             for g in range(NGPU):
                 if g not in present:
                     be.set_gpu_present(g, True)
+            for g in remoded:
+                be.replace_gpu(g, orig[g])
             for (a, b) in links:
                 be.set_link_up(a, b, True)
                 be.set_link_bandwidth(a, b, FULL_GBPS)
@@ -175,18 +217,19 @@ def test_random_fault_mix_converges(make_cfg, plugin_dir, seed, fixture, strateg
             for g in sorted(resetting):
                 be.inject_event(n.HwEvent(n.EVT_POST_RESET, g))
 
-            table = lambda: m.plugins[0].table  # noqa: E731 - replaced by every reload
+            def table():  # replaced by every reload; none while a failed start waits for its retry
+                ps = m.plugins
+                return ps[0].table if ps else None
 
             def whole():
                 t_ = table()
-                if sorted(t_.ids()) != ids or not all(t_.healthy(i) for i in ids):
+                if t_ is None or sorted(t_.ids()) != ids or not all(t_.healthy(i) for i in ids):
                     return False
                 topo = t_.topology()
                 return all(topo.link(x, y).up and topo.link(x, y).bw_gbps == FULL_GBPS
                            for x in range(NGPU) for y in range(NGPU) if x != y)
 
-            assert _wait(whole, timeout=15), (log, sorted(table().ids()),
-                                              [table().healthy(i) for i in table().ids()])
+            assert _wait(whole, timeout=15), (log, table() and [(i, table().healthy(i)) for i in table().ids()])
             assert _wait(lambda: m.monitor.unhealthy_keys() == [], timeout=5), m.monitor.unhealthy_keys()
             assert m.running and m.fatal_error is None
             assert _wait(lambda: _advertised(plugin_dir, k) == [(i, "Healthy") for i in ids], timeout=10), \

@@ -55,8 +55,17 @@ def test_exporter_device_health_and_rpc_histogram(n):
     assert buckets[0].labels["rpc"] == "Allocate" and buckets[-1].value == 1
 
 
+def _discovered(spec="2gpu_spx"):
+    """A fixture node after its first discovery: the monitor names GPUs by the identities
+    the backend gives for its current enumeration (an index it does not know is ignored)."""
+    from k8s_gpu_device_plugin_amd.models import fixtures
+    be = fixtures.build_backend(spec)
+    be.discover()
+    return be
+
+
 def test_health_monitor_state_machine(n):
-    be = n.FixtureBackend(1)
+    be = _discovered()
     m = n.HealthMonitor(be, 2)
     m.set_gpu_count(2)
     m.process(n.HwEvent(n.EVT_PRE_RESET, 1, message="x"))
@@ -79,11 +88,26 @@ def test_health_monitor_state_machine(n):
     m.process(n.HwEvent(n.EVT_PRE_RESET, 7))  # out of range gpu: ignored, no crash
 
 
+def test_failed_sample_of_an_index_no_gpu_holds_is_ignored(n):
+    """A sampler pass that still uses the old inventory after a GPU vanished asks for an
+    index the backend no longer has.  That failure is nobody's: no phantom GPU state
+    (which used to be kept as "#<index>" and stay Unhealthy for ever)."""
+    be = _discovered()
+    m = n.HealthMonitor(be, 2)
+    m.set_gpu_count(2)
+    be.set_gpu_present(1, False)
+    be.discover()  # the node is re-enumerated: one GPU, index 0
+    assert be.gpu_key(1) == ""
+    for _ in range(4):
+        m.on_sample(1, False, n.GpuSample())  # what the backend answers for index 1: failed, no key
+    assert m.unhealthy_keys() == [] and m.pop(10) == []
+
+
 def test_health_monitor_fast_tables_both_directions(n):
     """Unhealthy always reaches the tables from the monitor itself; Healthy only with
     fast recovery on (no recovery canary), else it waits for the manager."""
     t = n.DeviceTable(n.TableConfig(), [n.TableDevice("a", 0), n.TableDevice("b", 1)], n.Topology(2))
-    m = n.HealthMonitor(n.FixtureBackend(1), 2)
+    m = n.HealthMonitor(_discovered(), 2)
     m.set_gpu_count(2)
     m.set_fast_tables([t])
     m.process(n.HwEvent(n.EVT_PRE_RESET, 1))
@@ -106,7 +130,7 @@ def test_disabled_health_checks(n):
     with pytest.raises(ConfigError):
         disabled_checks_mask("xid")
     t = n.DeviceTable(n.TableConfig(), [n.TableDevice("a", 0), n.TableDevice("b", 1)], n.Topology(2))
-    m = n.HealthMonitor(n.FixtureBackend(1), 2)
+    m = n.HealthMonitor(_discovered(), 2)
     m.set_gpu_count(2)
     m.set_fast_tables([t])
     m.set_fast_recover(True)
