@@ -444,3 +444,83 @@ def test_connection_churn_across_workers(n, plugin_dir):
         assert srv.requests >= 1600
     finally:
         srv.stop()
+
+
+def test_hostile_clients_do_not_disturb_allocate(n, server):
+    """While a kubelet-like client runs Allocates, other local clients misbehave on the
+    same socket: random bytes, a valid call cut off mid-frame, a preface and then silence,
+    a flood of PINGs that is never read, streams opened and reset, and connections closed
+    at every point.  Every Allocate must succeed, and the server must report no fault."""
+    import random
+    srv, table, path = server
+    req = v1beta1.AllocateRequest(container_requests=[v1beta1.ContainerAllocateRequest(
+        devices_ids=["dev-007"])]).SerializeToString()
+    stop = threading.Event()
+    errs = []
+    done = [0]
+    idle = []
+
+    def good():
+        c = n.H2Client(path)
+        try:
+            while not stop.is_set():
+                st, body, msg = c.unary(v1beta1.METHOD_ALLOCATE, req)
+                if st != 0:
+                    errs.append(msg)
+                done[0] += 1
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(repr(e))
+        finally:
+            c.close()
+
+    call = _grpc_call_frames(1, v1beta1.METHOD_ALLOCATE, req)
+
+    def hostile(seed):
+        rng = random.Random(seed)
+        while not stop.is_set():
+            s = socket.socket(socket.AF_UNIX)
+            try:
+                s.settimeout(0.5)
+                s.connect(path)
+                kind = rng.randrange(6)
+                if kind == 0:
+                    s.sendall(bytes(rng.randrange(256) for _ in range(rng.randrange(1, 200))))
+                elif kind == 1:
+                    blob = PREFACE + _frame(4, 0, 0) + call
+                    s.sendall(blob[:rng.randrange(1, len(blob))])
+                elif kind == 2:
+                    s.sendall(PREFACE)
+                    idle.append(s)  # holds the connection open, says nothing more
+                    s = None
+                    if len(idle) > 16:
+                        idle.pop(0).close()
+                elif kind == 3:
+                    s.sendall(PREFACE + _frame(4, 0, 0) + b"".join(_frame(6, 0, 0, b"%08d" % i) for i in range(400)))
+                elif kind == 4:
+                    sid = 1 + 2 * rng.randrange(100)
+                    s.sendall(PREFACE + _frame(4, 0, 0) + _grpc_call_frames(sid, v1beta1.METHOD_ALLOCATE, req, False)
+                              + _frame(3, 0, sid, struct.pack(">I", 8)))  # RST_STREAM(CANCEL)
+                else:
+                    s.sendall(PREFACE + _frame(4, 0, 0) + call)
+                    s.recv(rng.choice([1, 9, 4096]))
+            except OSError:
+                pass
+            finally:
+                if s is not None:
+                    s.close()
+
+    ts = [threading.Thread(target=good)] + [threading.Thread(target=hostile, args=(i,)) for i in range(4)]
+    for t in ts:
+        t.start()
+    time.sleep(3.0)
+    stop.set()
+    for t in ts:
+        t.join(10)
+    for s in idle:
+        s.close()
+    assert not errs, errs[:3]
+    assert done[0] > 100
+    assert srv.failure() == "" and srv.running
+    c = n.H2Client(path)
+    assert c.unary(v1beta1.METHOD_ALLOCATE, req)[0] == 0
+    c.close()
