@@ -339,3 +339,86 @@ def test_native_http_stop_right_after_start(n):
         srv.start()
         srv.stop()
         assert not srv.running
+
+
+def test_hostile_clients_do_not_disturb_scrapes(make_cfg):
+    """While a Prometheus-like client scrapes /metrics over keep-alive, other clients
+    misbehave on the same port: random bytes, requests cut off mid-header, connections
+    that send half a request line and go silent, oversized headers, a pipelined burst that
+    is closed unread, and resets (RST) at random points.  Every scrape must get its full
+    answer and the server must keep answering afterwards."""
+    import random
+    import struct
+    import threading
+    cfg = make_cfg(webListenAddress="127.0.0.1:0", http={"server": "native", "accessLog": False, "threads": 3})
+    mgr = PluginManager(cfg)
+    mgr.load_plugins()
+    w = WebServer(cfg, mgr)
+    port = w.start()
+    stop = threading.Event()
+    errs, done, idle = [], [0], []
+
+    def good():
+        c = http.client.HTTPConnection("127.0.0.1", port, timeout=5)
+        try:
+            while not stop.is_set():
+                c.request("GET", "/metrics")
+                r = c.getresponse()
+                body = r.read()
+                if r.status != 200 or b"process_start_time_seconds" not in body:
+                    errs.append((r.status, len(body)))
+                done[0] += 1
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(repr(e))
+        finally:
+            c.close()
+
+    def hostile(seed):
+        rng = random.Random(seed)
+        req = b"GET /metrics HTTP/1.1\r\nHost: x\r\nAccept-Encoding: gzip\r\n\r\n"
+        while not stop.is_set():
+            s = socket.socket()
+            try:
+                s.settimeout(0.5)
+                s.connect(("127.0.0.1", port))
+                kind = rng.randrange(6)
+                if kind == 0:
+                    s.sendall(bytes(rng.randrange(256) for _ in range(rng.randrange(1, 300))))
+                elif kind == 1:
+                    s.sendall(req[:rng.randrange(1, len(req))])
+                elif kind == 2:
+                    s.sendall(b"GET /metr")
+                    idle.append(s)  # slow client: half a request line, then nothing
+                    s = None
+                    if len(idle) > 16:
+                        idle.pop(0).close()
+                elif kind == 3:
+                    s.sendall(b"GET / HTTP/1.1\r\nX-Big: " + b"b" * 80000 + b"\r\n\r\n")
+                    s.recv(64)
+                elif kind == 4:
+                    s.sendall(req * 50)  # pipelined, closed unread
+                else:
+                    s.sendall(req)
+                    s.setsockopt(socket.SOL_SOCKET, socket.SO_LINGER, struct.pack("ii", 1, 0))  # RST on close
+            except OSError:
+                pass
+            finally:
+                if s is not None:
+                    s.close()
+
+    ts = [threading.Thread(target=good)] + [threading.Thread(target=hostile, args=(i,)) for i in range(4)]
+    try:
+        for t in ts:
+            t.start()
+        time.sleep(3.0)
+        stop.set()
+        for t in ts:
+            t.join(10)
+        assert not errs, errs[:3]
+        assert done[0] > 50
+        assert get(port, "/health")[0] == 200
+    finally:
+        stop.set()
+        for s in idle:
+            s.close()
+        w.stop()
