@@ -35,7 +35,7 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--strategy", dest="migStrategy", choices=["none", "single", "mixed"])
     ap.add_argument("--log-level")
     ap.add_argument("--log-dir")
-    ap.add_argument("--devices", help="physical GPU indices to advertise, e.g. 0-3")
+    ap.add_argument("--devices", help="GPUs to advertise: indices (e.g. 0-3), UUIDs or PCI BDFs")
     ap.add_argument("--version", action="store_true")
     return ap.parse_args(argv)
 

@@ -136,7 +136,7 @@ class Config:
     pluginDir: str = v1beta1.DEVICE_PLUGIN_PATH
     backend: str = "auto"                 # auto | amdsmi | fixture
     fixture: str = "2gpu_spx"             # builtin name or path, used by backend=fixture
-    devices: str = ""                     # physical GPU filter, e.g. "0-3" ("" = all)
+    devices: str = ""                     # physical GPU filter: "0-3", UUIDs or BDFs ("" = all)
     resourcePrefix: str = "amd.com"
     resources: list = field(default_factory=list)  # [ResourceSpec]
     visibleDevicesEnv: str = "AMD_VISIBLE_DEVICES"

@@ -33,7 +33,7 @@ from ..device import build_device_map
 from ..device.backend import make_backend
 from ..resource import new_resources
 from ..utils.log import get_logger
-from ..utils.util import CloseOnce, parse_index_list
+from ..utils.util import CloseOnce, parse_device_selector
 from ..utils.version import APP_NAME, VERSION
 from .plugin import AmdDevicePlugin
 
@@ -74,6 +74,7 @@ class PluginManager:
         self.plugins: list[AmdDevicePlugin] = []
         self.gpus: list = []
         self.topology = None
+        self._pinned_devices = None  # identities the `devices` indices named at first discovery
         self.device_map = None
         self._retry_timer: threading.Timer | None = None
         self._threads: list[threading.Thread] = []
@@ -92,6 +93,7 @@ class PluginManager:
         # every later GPU down one index, and their health must not move with it.
         self._key_of: dict[int, str] = {}   # advertised GPU index -> identity
         self._index_of: dict[str, int] = {}  # identity -> advertised GPU index
+        self._node_index_of: dict[str, int] = {}  # identity -> index, every GPU of the node
         # Recovery canaries run off the manager thread; a per-GPU generation drops a
         # verdict that an Unhealthy event overtook while the canary was running.
         self._health_gen: dict[str, int] = {}
@@ -282,11 +284,13 @@ class PluginManager:
     # ------------------------------------------------------------ plugins
     def load_plugins(self) -> None:
         gpus, topo = self.backend.discover()
-        wanted = parse_index_list(self.cfg.devices)
-        if wanted is not None:
-            gpus = [g for g in gpus if g.index in wanted]
+        # the tables' topology spans the whole node: link state and bandwidth are kept for
+        # every pair, also those with an end that `devices` leaves out
+        self._node_index_of = {self._identity(g): g.index for g in gpus}
+        node = gpus
+        gpus = self._selected(gpus)
         self.gpus, self.topology = gpus, topo
-        self.signature = inventory_signature(gpus)
+        self.signature = self._signature(node, gpus)
         resources = new_resources(gpus, self.cfg.strategy, self.cfg.resourcePrefix, self.cfg.resources)
         self.device_map = build_device_map(gpus, resources, self.cfg.strategy, self.cfg.mountCardNodes,
                                            self.cfg.sharing.replicas, self.cfg.sharing.renameByDefault)
@@ -392,6 +396,27 @@ class PluginManager:
         self.load_plugins()
         self.start_plugins()
 
+    def _signature(self, node, selected) -> tuple:
+        """The advertised set, plus which GPUs the node enumerates where: a GPU that
+        `devices` leaves out still has links in the tables' topology."""
+        return inventory_signature(selected), tuple((self._identity(g), g.index) for g in node)
+
+    def _selected(self, gpus) -> list:
+        """The GPUs `devices` selects.  Indices name the enumeration this process saw
+        first and are pinned to those GPUs' identities then: when a GPU later drops off
+        the bus and the others move down an index, the selection keeps the same physical
+        GPUs instead of taking in the next one.  UUIDs and BDFs are matched as given."""
+        sel = parse_device_selector(self.cfg.devices)
+        if sel is None:
+            return list(gpus)
+        indices, names = sel
+        if self._pinned_devices is None:
+            self._pinned_devices = {self._identity(g) for g in gpus if g.index in indices}
+            log.info("devices %r selects %s", self.cfg.devices,
+                     ", ".join(sorted(self._pinned_devices | names)) or "nothing yet")
+        return [g for g in gpus if self._identity(g) in self._pinned_devices
+                or (g.uuid or "").lower() in names or (g.bdf or "").lower() in names]
+
     # ------------------------------------------------------------ health
     def _identity(self, g) -> str:
         """The key health state is kept under: the backend's own (the monitor uses the
@@ -431,18 +456,18 @@ class PluginManager:
             # the tables; re-applying a queued update here could briefly undo a newer one
             self._set_health(key, u.partition, healthy, u.reason, apply=self.cfg.health.canary)
         elif u.link_up in (0, 1):
-            a = self._index_of.get(key, -1)
-            b = self._index_of.get(getattr(u, "peer_key", "") or self._key_of.get(u.peer, ""), -1)
-            if a < 0 or b < 0:  # an end that is not advertised (gone, or left out by `devices`)
-                log.debug("xGMI link %s<->%s %s (not advertised)", key, getattr(u, "peer_key", "") or u.peer,
+            a, b = self._link_ends(u, key)
+            if a < 0 or b < 0:  # an end the node no longer enumerates
+                log.debug("xGMI link %s<->%s %s (GPU gone)", key, getattr(u, "peer_key", "") or u.peer,
                           "up" if u.link_up else "down")
                 return
+            if not self.plugins or self.plugins[0].table.topology().link(a, b).up == bool(u.link_up):
+                return  # the tables agree (every link is reported once more after a reload)
             for p in self.plugins:
                 p.set_link_up(a, b, bool(u.link_up))
             log.warning("xGMI link %d<->%d %s", a, b, "up" if u.link_up else "down")
         elif u.kind == native.load().EVT_LINK_QUALITY:
-            a = self._index_of.get(key, -1)
-            b = self._index_of.get(getattr(u, "peer_key", "") or self._key_of.get(u.peer, ""), -1)
+            a, b = self._link_ends(u, key)
             if a < 0 or b < 0 or not self.plugins:
                 return
             cur = self.plugins[0].table.topology().link(a, b).bw_gbps
@@ -453,6 +478,11 @@ class PluginManager:
             log.warning("xGMI link %d<->%d trains at %.0f Gb/s (was %.0f): %s", a, b, u.link_gbps, cur, u.reason)
         else:
             log.info("GPU event on %s: %s", self._gpu_name(key), u.reason)
+
+    def _link_ends(self, u, key: str) -> tuple:
+        """Topology indices of a link event's two GPUs (-1: not in the node)."""
+        peer = getattr(u, "peer_key", "") or self._key_of.get(u.peer, "")
+        return self._node_index_of.get(key, -1), self._node_index_of.get(peer, -1)
 
     def _push_link_pods(self) -> None:
         """Which GPU pairs' xGMI links already carry a multi-GPU pod (from the PodResources
@@ -601,11 +631,8 @@ class PluginManager:
     def _check_inventory(self) -> None:
         """Periodic re-discovery: a compute/memory partition-mode change (SPX->CPX, ...) or a
         GPU appearing/disappearing changes the device set; re-advertise when it does."""
-        gpus, _ = self.backend.discover()
-        wanted = parse_index_list(self.cfg.devices)
-        if wanted is not None:
-            gpus = [g for g in gpus if g.index in wanted]
-        if inventory_signature(gpus) != getattr(self, "signature", None):
+        node = self.backend.discover()[0]
+        if self._signature(node, self._selected(node)) != getattr(self, "signature", None):
             self.counters["restarts_inventory"] = self.counters.get("restarts_inventory", 0) + 1
             log.warning("device inventory changed (partition mode or GPU set); re-advertising")
             self.restart_plugins()

@@ -53,6 +53,30 @@ def envelope_bytes(obj: dict) -> bytes:
     return (json.dumps(obj, separators=(",", ":"), ensure_ascii=False) + "\n").encode()
 
 
+def parse_device_selector(spec: str | None):
+    """``devices``: ``"0-3,6"`` style indices and/or GPU identities (UUID or PCI BDF),
+    comma-separated.  Returns ``None`` for "all", else ``(indices, names)``."""
+    if spec is None:
+        return None
+    spec = str(spec).strip()
+    if not spec or spec in ("all", "*"):
+        return None
+    indices: set[int] = set()
+    names: set[str] = set()
+    for part in spec.split(","):
+        part = part.strip()
+        if not part:
+            continue
+        a, sep, b = part.partition("-")
+        if part.isdigit():
+            indices.add(int(part))
+        elif sep and a.strip().isdigit() and b.strip().isdigit():
+            indices.update(range(int(a), int(b) + 1))
+        else:  # a UUID (has dashes) or a BDF such as 0000:75:00.0
+            names.add(part.lower())
+    return sorted(indices), names
+
+
 def parse_index_list(spec: str | None) -> list[int] | None:
     """Parses ``"0-3,6"`` into ``[0, 1, 2, 3, 6]``; empty/None means "all"."""
     if spec is None:

@@ -86,6 +86,10 @@ void HealthMonitor::emit_locked(HealthUpdate u) {
 }
 
 namespace {
+std::pair<std::string, std::string> link_of(const std::string& a, const std::string& b) {
+  return a < b ? std::make_pair(a, b) : std::make_pair(b, a);
+}
+
 int check_of(int kind) {
   switch (kind) {
     case kEvtPreReset:
@@ -185,7 +189,9 @@ void HealthMonitor::process(const HwEvent& e) {
       const int up = e.kind == kEvtLinkUp ? 1 : 0;
       auto& m = state_[key].link_up;
       auto it = m.find(peer_key);
-      if (it != m.end() && it->second == up) return;  // already known (polling + event)
+      uint64_t& ep = up_epoch_[link_of(key, peer_key)];
+      if (it != m.end() && it->second == up && ep == links_epoch_) return;  // already known (polling + event)
+      ep = links_epoch_;
       m[peer_key] = up;
       state_[peer_key].link_up[key] = up;
       HealthUpdate u;
@@ -202,9 +208,13 @@ void HealthMonitor::process(const HwEvent& e) {
     case kEvtLinkQuality: {
       // e.value: the link's bandwidth now (the slower end's view); one update per pair
       if (!known || peer_key.empty() || e.value <= 0) return;
-      const auto pk = key < peer_key ? std::make_pair(key, peer_key) : std::make_pair(peer_key, key);
+      const auto pk = link_of(key, peer_key);
       auto it = pair_bw_.find(pk);
-      if (it != pair_bw_.end() && std::fabs(it->second - e.value) <= 0.05 * std::max(it->second, e.value)) return;
+      uint64_t& ep = bw_epoch_[pk];
+      if (it != pair_bw_.end() && std::fabs(it->second - e.value) <= 0.05 * std::max(it->second, e.value) &&
+          ep == links_epoch_)
+        return;
+      ep = links_epoch_;
       pair_bw_[pk] = e.value;
       HealthUpdate u;
       u.kind = e.kind;
@@ -274,9 +284,11 @@ void HealthMonitor::on_sample(int gpu, bool ok, const GpuSample& s) {
       }
       for (int k = 0; k < s.num_links; ++k) {
         if (s.link_peer[k] < 0 || s.link_up[k] < 0 || peer_keys[k].empty()) continue;
+        const auto pk = link_of(key, peer_keys[k]);
         auto it = st.link_up.find(peer_keys[k]);
         const int prev = it == st.link_up.end() ? 1 : it->second;  // links assumed up at start
-        if (prev != s.link_up[k]) {
+        const auto ue = up_epoch_.find(pk);
+        if (prev != s.link_up[k] || ue == up_epoch_.end() || ue->second != links_epoch_) {
           HwEvent e = event(s.link_up[k] ? kEvtLinkUp : kEvtLinkDown, "xgmi link status poll");
           e.peer = s.link_peer[k];
           e.peer_key = peer_keys[k];
@@ -295,11 +307,14 @@ void HealthMonitor::on_sample(int gpu, bool ok, const GpuSample& s) {
             const auto pv = pt->second.link_bw.find(key);
             if (pv != pt->second.link_bw.end()) eff = std::min(eff, pv->second);
           }
-          const auto pk = key < peer_keys[k] ? std::make_pair(key, peer_keys[k]) : std::make_pair(peer_keys[k], key);
           const auto last = pair_bw_.find(pk);
-          if (last == pair_bw_.end() || std::fabs(last->second - eff) > 0.05 * std::max(last->second, eff)) {
+          const auto be = bw_epoch_.find(pk);
+          if (last == pair_bw_.end() || std::fabs(last->second - eff) > 0.05 * std::max(last->second, eff) ||
+              be == bw_epoch_.end() || be->second != links_epoch_) {
+            const bool moved =
+                last != pair_bw_.end() && std::fabs(last->second - eff) > 0.05 * std::max(last->second, eff);
             HwEvent e = event(kEvtLinkQuality,
-                              last == pair_bw_.end()
+                              !moved
                                   ? "xgmi link bandwidth: " + std::to_string(static_cast<int>(eff)) + " Gb/s"
                                   : "xgmi link re-trained: " + std::to_string(static_cast<int>(last->second)) + " -> " +
                                         std::to_string(static_cast<int>(eff)) + " Gb/s");
@@ -342,6 +357,7 @@ void HealthMonitor::attach_tables(std::vector<std::shared_ptr<DeviceTable>> tabl
   std::lock_guard<std::mutex> lk(mu_);
   fast_tables_ = std::move(tables);
   fast_recover_ = fast_recover;
+  ++links_epoch_;  // the new tables hold discovery's view of the links: report each link once more
   std::vector<char> down(table_keys_.size(), 0);
   for (size_t g = 0; g < table_keys_.size(); ++g) {
     if (table_keys_[g].empty()) continue;

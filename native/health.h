@@ -129,6 +129,13 @@ class HealthMonitor {
   std::deque<HealthUpdate> queue_;
   std::unordered_map<std::string, GpuState> state_;
   std::map<std::pair<std::string, std::string>, double> pair_bw_;  // link -> last reported bandwidth
+  // Tables built at a reload start from discovery's view of the links, which the monitor
+  // may never have reported (a link that re-trained while down, or flapped between the
+  // last sample and the discovery).  attach_tables() starts a new epoch; each link's
+  // state and bandwidth are reported once more in it, whether or not they changed (the
+  // manager applies them only where the new tables disagree).
+  uint64_t links_epoch_ = 1;
+  std::map<std::pair<std::string, std::string>, uint64_t> up_epoch_, bw_epoch_;  // link -> epoch last reported in
   std::vector<std::string> table_keys_;  // table index -> key
   std::vector<std::shared_ptr<DeviceTable>> fast_tables_;
   bool fast_recover_ = false;

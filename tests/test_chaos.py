@@ -98,19 +98,25 @@ class _Allocator(threading.Thread):
 
 # CHAOS_SEEDS=N runs seeds 1..N (a longer hunt); the suite runs three
 @pytest.mark.parametrize("seed", range(1, 1 + int(os.environ.get("CHAOS_SEEDS", "3"))))
-@pytest.mark.parametrize("fixture,strategy,server", [("4gpu_spx", "none", "native"),
-                                                     ("4gpu_cpx", "single", "native"),
-                                                     ("4gpu_spx", "none", "python")])
-def test_random_fault_mix_converges(make_cfg, plugin_dir, seed, fixture, strategy, server):
+@pytest.mark.parametrize("fixture,strategy,server,devices", [("4gpu_spx", "none", "native", ""),
+                                                             ("4gpu_cpx", "single", "native", ""),
+                                                             ("4gpu_spx", "none", "python", ""),
+                                                             ("4gpu_spx", "none", "native", "0-2")])
+def test_random_fault_mix_converges(make_cfg, plugin_dir, tmp_path, seed, fixture, strategy, server, devices):
+    from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import PodResourcesStub
     n = native.load()
     rng = random.Random(seed)
     be = fixtures.build_backend(fixture)
     gpus, _ = be.discover()
     assert len(gpus) == NGPU
-    ids = sorted(p.id for g in gpus for p in g.partitions)  # one device per partition (SPX: per GPU)
+    shown = range(NGPU - 1) if devices else range(NGPU)  # the GPUs `devices` advertises (all but the last)
+    ids = sorted(p.id for g in gpus if g.index in shown for p in g.partitions)  # one device per partition
     id_of_slot = {g.index: g.partitions[0].id for g in gpus}
+    podsock = str(tmp_path / "pod-resources" / "kubelet.sock")
+    pods = PodResourcesStub(podsock).start()
     cfg = make_cfg(fixture=fixture, migStrategy=strategy, grpc={"server": server}, telemetry={"intervalMs": 30},
-                   rediscoverIntervalS=0.2, retrySeconds=0.2,
+                   rediscoverIntervalS=0.2, retrySeconds=0.2, devices=devices,
+                   podResources={"enabled": True, "socket": podsock, "intervalS": 0.05},
                    health={"lostAfterFailures": 2, "sampleStallS": 0.3, "badPageThreshold": 10})
     orig, _ = be.discover()  # untouched descriptions, to undo partition-mode changes
     resetting, present, server_faults = set(), set(range(NGPU)), 0
@@ -130,7 +136,7 @@ def test_random_fault_mix_converges(make_cfg, plugin_dir, seed, fixture, strateg
                 op = rng.choice(["reset", "post_reset", "remove", "restore", "link_down", "link_up", "link_bw",
                                  "api_restart", "kubelet_restart", "server_fault", "ecc", "stall", "unstall",
                                  "pages_high", "pages_low", "discovery_fails", "discovery_ok", "mode_change",
-                                 "mode_restore", "idle"])
+                                 "mode_restore", "pods", "idle"])
                 g = rng.randrange(NGPU)
                 a, b = sorted(rng.sample(range(NGPU), 2))
                 if op == "reset" and g in present:
@@ -191,6 +197,11 @@ def test_random_fault_mix_converges(make_cfg, plugin_dir, seed, fixture, strateg
                     mode = "SPX" if orig[g].compute_partition != "SPX" else "CPX"
                     fixtures.set_gpu_mode(be, g, mode, first_render=300 + 8 * g)
                     remoded.add(g)
+                elif op == "pods":  # the kubelet's allocation map changes (PodResources)
+                    cur = list(m.plugins[0].table.ids()) if m.plugins else []
+                    if len(cur) >= 2:
+                        pods.set_pods([("ns", "p%d" % j, [("c", "amd.com/gpu", rng.sample(cur, 2))])
+                                       for j in range(rng.randrange(1, 4))])
                 elif op == "mode_restore" and g in remoded and len(present) == NGPU:
                     be.replace_gpu(g, orig[g])
                     remoded.discard(g)
@@ -216,6 +227,8 @@ def test_random_fault_mix_converges(make_cfg, plugin_dir, seed, fixture, strateg
             time.sleep(0.1)
             for g in sorted(resetting):
                 be.inject_event(n.HwEvent(n.EVT_POST_RESET, g))
+            # one pod spanning GPUs 1 and 2: only that pair's link carries a pod
+            pods.set_pods([("ns", "final", [("c", "amd.com/gpu", [id_of_slot[1], id_of_slot[2]])])])
 
             def table():  # replaced by every reload; none while a failed start waits for its retry
                 ps = m.plugins
@@ -226,17 +239,29 @@ def test_random_fault_mix_converges(make_cfg, plugin_dir, seed, fixture, strateg
                 if t_ is None or sorted(t_.ids()) != ids or not all(t_.healthy(i) for i in ids):
                     return False
                 topo = t_.topology()
-                return all(topo.link(x, y).up and topo.link(x, y).bw_gbps == FULL_GBPS
+                if topo.n != NGPU:
+                    return False
+                return all(topo.link(x, y).up and topo.link(x, y).bw_gbps == FULL_GBPS and
+                           topo.link(x, y).pods == (1 if {x, y} == {1, 2} else 0)
                            for x in range(NGPU) for y in range(NGPU) if x != y)
 
-            assert _wait(whole, timeout=15), (log, table() and [(i, table().healthy(i)) for i in table().ids()])
+            def links_now():
+                t_ = table()
+                topo = t_.topology() if t_ is not None else None
+                return topo and [(x, y, topo.link(x, y).up, topo.link(x, y).bw_gbps, topo.link(x, y).pods)
+                                 for x in range(topo.n) for y in range(x + 1, topo.n)]
+
+            assert _wait(whole, timeout=15), (table() and [(i, table().healthy(i)) for i in table().ids()],
+                                              links_now(), log,
+                                              [ln for ln in m.exporter.render().splitlines()
+                                               if ln.startswith("amdgpu_xgmi_link_bandwidth")])
             assert _wait(lambda: m.monitor.unhealthy_keys() == [], timeout=5), m.monitor.unhealthy_keys()
             assert m.running and m.fatal_error is None
             assert _wait(lambda: _advertised(plugin_dir, k) == [(i, "Healthy") for i in ids], timeout=10), \
                 _advertised(plugin_dir, k)
 
             # still wired end to end: a new reset reaches kubelet, and so does its end
-            g = rng.randrange(NGPU)
+            g = rng.choice(list(shown))
             be.inject_event(n.HwEvent(n.EVT_PRE_RESET, g, message="after chaos"))
             assert _wait(lambda: not table().healthy(id_of_slot[g]))
             be.inject_event(n.HwEvent(n.EVT_POST_RESET, g))
@@ -259,4 +284,5 @@ def test_random_fault_mix_converges(make_cfg, plugin_dir, seed, fixture, strateg
                 client.join(10)
             m.stop()
             t.join(10)
+            pods.stop()
             assert not t.is_alive()

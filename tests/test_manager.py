@@ -699,6 +699,33 @@ def test_link_retrain_reaches_the_allocator(make_cfg, plugin_dir, run_manager):
         assert _wait(lambda: m.plugins[0].table.topology().link(0, 1).bw_gbps == 608.0)
 
 
+def test_link_state_is_resynced_after_a_reload(make_cfg, plugin_dir, run_manager):
+    """Found by the chaos test: a link re-trains at a quarter rate while it is down, and
+    a reload's discovery puts that rate into the new tables.  The link then comes back up
+    at full rate - the value the monitor last reported, so it saw no change and the
+    tables kept the stale rate.  Every link is now reported once more after a reload."""
+    be = fixtures.build_backend("4gpu_spx")
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(fixture="4gpu_spx", telemetry={"intervalMs": 30}), backend=be)
+        k.wait_for_registrations(1)
+        topo = lambda: m.plugins[0].table.topology()  # noqa: E731 - replaced by every reload
+        be.set_link_up(0, 1, False)
+        assert _wait(lambda: not topo().link(0, 1).up)
+        be.set_link_bandwidth(0, 1, 152.0)
+        m.restart()
+        k.wait_for_registrations(2)
+        assert _wait(lambda: m.plugins and topo().link(0, 1).bw_gbps == 152.0 and not topo().link(0, 1).up)
+        be.set_link_bandwidth(0, 1, 608.0)
+        be.set_link_up(0, 1, True)
+        assert _wait(lambda: topo().link(0, 1).up and topo().link(0, 1).bw_gbps == 608.0), \
+            (topo().link(0, 1).up, topo().link(0, 1).bw_gbps)
+        # a link that flapped down between the last sample and the reload's discovery
+        be.set_link_up(2, 3, False)
+        m.restart()  # may or may not see it down; either way the tables converge
+        be.set_link_up(2, 3, True)
+        assert _wait(lambda: m.plugins and topo().link(2, 3).up)
+
+
 def test_halfrate_fixture_is_discovered_degraded(n):
     gpus, topo = fixtures.build_backend("8gpu_spx_halfrate").discover()
     from k8s_gpu_device_plugin_amd.parallel.topology import NodeTopology
@@ -755,6 +782,33 @@ def test_pod_link_load_uses_the_whole_node_topology(make_cfg, plugin_dir, run_ma
             assert 'amdgpu_xgmi_link_pods{gpu="1",peer="2"} 1' in m.exporter.render()
     finally:
         stub.stop()
+
+
+def test_devices_selection_stays_on_the_same_gpus(make_cfg, plugin_dir, run_manager):
+    """`devices: 0-2` on a 4-GPU node.  GPU 0 drops off the bus and the others move down
+    an index: the plugin must advertise GPUs 1 and 2, not take in GPU 3 (an operator may
+    have kept it for something else).  UUIDs and BDFs select the same way."""
+    be = fixtures.build_backend("4gpu_spx")
+    gpus, _ = be.discover()
+    uuid = {g.index: g.partitions[0].id for g in gpus}
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(fixture="4gpu_spx", devices="0-2", rediscoverIntervalS=0.1), backend=be)
+        k.wait_for_registrations(1)
+        assert sorted(m.plugins[0].table.ids()) == sorted(uuid[i] for i in (0, 1, 2))
+        be.set_gpu_present(0, False)
+        assert _wait(lambda: m.plugins and sorted(m.plugins[0].table.ids()) == sorted([uuid[1], uuid[2]]),
+                     timeout=10), m.plugins[0].table.ids()
+        time.sleep(0.3)
+        assert uuid[3] not in m.plugins[0].table.ids()
+        be.set_gpu_present(0, True)
+        assert _wait(lambda: m.plugins and sorted(m.plugins[0].table.ids()) == sorted(uuid[i] for i in (0, 1, 2)),
+                     timeout=10)
+    from k8s_gpu_device_plugin_amd.utils.util import parse_device_selector
+    assert parse_device_selector("0-1, 5,0000:75:00.0,ABC-def") == ([0, 1, 5], {"0000:75:00.0", "abc-def"})
+    assert parse_device_selector("") is None and parse_device_selector("all") is None
+    by_name = PluginManager(make_cfg(fixture="4gpu_spx", devices="%s,%s" % (gpus[3].bdf, gpus[1].uuid.upper())),
+                            backend=fixtures.build_backend("4gpu_spx"))
+    assert sorted(g.index for g in by_name._selected(gpus)) == [1, 3]
 
 
 @pytest.mark.parametrize("fault", ["worker", "listener"])

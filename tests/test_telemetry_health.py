@@ -268,7 +268,8 @@ def test_retired_pages_threshold_state_machine(n):
     be.set_retired_pages(1, 500, 0)  # threshold 0 on GPU 1: check disabled
     for g in (0, 1):
         m.on_sample(g, True, be.sample(g))
-    u = [x for x in m.pop(100) if x.kind != n.EVT_LINK_QUALITY]  # first link-bandwidth readings
+    # the first sample also reports every link's state and bandwidth once
+    u = [x for x in m.pop(100) if x.kind not in (n.EVT_LINK_QUALITY, n.EVT_LINK_UP, n.EVT_LINK_DOWN)]
     assert [(x.gpu, x.healthy) for x in u] == [(0, 0)] and "retired" in u[0].reason
     m.process(n.HwEvent(n.EVT_PRE_RESET, 0))
     m.process(n.HwEvent(n.EVT_POST_RESET, 0))
