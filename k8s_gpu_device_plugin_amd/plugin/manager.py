@@ -118,6 +118,7 @@ class PluginManager:
         # last canary result per (gpu, hardware partition index): (unix time, result dict);
         # written by canary pool threads, rendered by the manager thread
         self.canary_results: dict[tuple[int, int], tuple[float, dict]] = {}
+        self._canary_owner: dict[tuple[int, int], str] = {}  # same keys -> identity of the GPU it ran on
         self._canary_lock = threading.Lock()
 
     # ------------------------------------------------------------ public API
@@ -352,10 +353,13 @@ class PluginManager:
         self.monitor.set_bad_page_thresholds(thresholds)
         if self._event_sources is not None:
             self._event_sources = getattr(self.backend, "armed_event_sources", None)
-        with self._canary_lock:  # results of partitions that no longer exist leave /metrics
+        with self._canary_lock:  # results of partitions that no longer exist leave /metrics,
+            # and so do those of a GPU whose index another GPU holds after a re-enumeration
             live = {(g.index, p.index) for g in gpus for p in g.partitions}
-            for k in [k for k in self.canary_results if k not in live]:
+            for k in [k for k in self.canary_results
+                      if k not in live or self._canary_owner.get(k, self._key_of.get(k[0])) != self._key_of.get(k[0])]:
                 del self.canary_results[k]
+                self._canary_owner.pop(k, None)
         self._push_link_pods()  # the new tables start from the known allocation map
         self.exporter.set_inventory(gpus)
         self.exporter.set_partition_labels(labels)
@@ -590,6 +594,7 @@ class PluginManager:
         with self._canary_lock:
             self.counters["canary_runs"] = self.counters.get("canary_runs", 0) + 1
             self.canary_results[(gpu, hw_part)] = (time.time(), res)
+            self._canary_owner[(gpu, hw_part)] = self._key_of.get(gpu, "#%d" % gpu)
         self.events.put((EV_METRICS,))
         return res
 

@@ -681,6 +681,24 @@ def test_health_follows_gpu_identity_through_rediscovery(make_cfg, plugin_dir, r
         assert _wait(lambda: m.monitor.unhealthy_keys() == [])
 
 
+def test_canary_result_does_not_pass_to_the_gpu_that_takes_its_index(make_cfg, plugin_dir, run_manager):
+    """A canary result is the GPU's, not the index's: when GPU 0 falls off the bus and
+    GPU 1 moves to index 0, /metrics stops showing GPU 0's result under index 0."""
+    be = fixtures.build_backend("2gpu_spx")
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(rediscoverIntervalS=0.2), backend=be)
+        k.wait_for_registrations(1)
+        with m._canary_lock:  # as a canary run on GPU 0 and one on GPU 1 would leave them
+            for g in (0, 1):
+                m.canary_results[(g, 0)] = (time.time(), {"ok": g == 1})
+                m._canary_owner[(g, 0)] = m._key_of[g]
+        be.set_gpu_present(0, False)
+        assert _wait(lambda: len(m.plugins) == 1 and m.plugins[0].table.ids() != [], timeout=10)
+        assert _wait(lambda: len(m.gpus) == 1, timeout=10)
+        with m._canary_lock:
+            assert m.canary_results == {}  # (0, 0) was GPU 0's, (1, 0) no longer exists
+
+
 def test_link_retrain_reaches_the_allocator(make_cfg, plugin_dir, run_manager):
     """An up xGMI link re-trains at half its rate: the telemetry poll reports it, the
     table's topology takes the new bandwidth, and a 2-GPU request that must include
