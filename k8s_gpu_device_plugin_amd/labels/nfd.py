@@ -14,6 +14,8 @@ Labels (prefix ``amd.com/``)::
     gpu.vram-gb=288                    gpu.compute-units=256
     gpu.compute-partition=CPX          gpu.memory-partition=NPS2   (when uniform)
     gpu.partitions=64                  gpu.xgmi-links=7
+    gpu.device-id=75a3                 gpu.driver-version=6.14.14
+    gpu.vbios-version=<IFWI version>   (each when the driver reports it)
     gpu.mixed-partitions=true          (when GPUs differ)
 """
 from __future__ import annotations
@@ -48,6 +50,15 @@ def node_labels(gpus) -> dict:
         labels[PREFIX + "gpu.compute-units"] = str(g0.num_compute_units)
     if g0.num_xgmi_links:
         labels[PREFIX + "gpu.xgmi-links"] = str(g0.num_xgmi_links)
+    # what AMD's node labeller publishes too: pods pinned to a driver / firmware level
+    # (a validated stack) select nodes by these
+    # (one label value per node: left out while the GPUs disagree, e.g. mid firmware update)
+    for key, attr in (("gpu.device-id", "device_id"), ("gpu.driver-version", "driver_version"),
+                      ("gpu.vbios-version", "vbios_version")):
+        vals = {getattr(g, attr, "") for g in gpus}
+        if len(vals) == 1 and next(iter(vals)):
+            v = next(iter(vals))
+            labels[PREFIX + key] = "%04x" % v if isinstance(v, int) else _value(v)
     modes = {(g.compute_partition, g.memory_partition) for g in gpus}
     if len(modes) == 1:
         cp, mp = next(iter(modes))

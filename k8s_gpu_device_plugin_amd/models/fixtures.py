@@ -29,6 +29,9 @@ NPS_BITS = {"NPS1": 1, "NPS2": 2, "NPS4": 4, "NPS8": 8}
 MI355X_HBM_BYTES = 288 * 10**9
 MI355X_CUS = 256
 MI355X_NAME = "AMD Instinct MI355X"
+MI355X_DEVICE_ID = "0x75a3"  # PCI device id amdsmi reports on the MI355X box
+FIXTURE_DRIVER_VERSION = "6.14.14"
+FIXTURE_VBIOS_VERSION = "FIXTURE-VBIOS"
 
 EVENT_KINDS = {
     "pre_reset": "EVT_PRE_RESET", "post_reset": "EVT_POST_RESET",
@@ -150,6 +153,10 @@ def build_backend(spec):
             caps |= {1: 1, 2: 2, 4: 4, 8: 8}[NPS_BITS[str(c).upper()]]
         info.nps_caps = caps
         info.num_compute_units = int(g.get("num_cus", MI355X_CUS))
+        info.device_id = int(str(g.get("device_id", MI355X_DEVICE_ID)), 0)
+        info.oam_id = int(g.get("oam_id", gi))
+        info.driver_version = str(g.get("driver_version", FIXTURE_DRIVER_VERSION))
+        info.vbios_version = str(g.get("vbios_version", FIXTURE_VBIOS_VERSION))
         info.bad_page_threshold = int(g.get("bad_page_threshold", -1))  # -1: RAS threshold not readable
         nparts = int(g.get("num_partitions", PARTITIONS.get(info.compute_partition, 1)))
         # what amdsmi_get_gpu_accelerator_partition_profile reports for the mode

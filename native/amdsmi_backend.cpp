@@ -266,7 +266,13 @@ class AmdSmiBackend : public Backend {
         g.serial = asic.asic_serial;
         g.gfx_target = gfx_name(asic.target_graphics_version);
         if (asic.num_of_compute_units != 0xFFFFFFFFu) g.num_compute_units = static_cast<int>(asic.num_of_compute_units);
+        g.device_id = static_cast<uint32_t>(asic.device_id & 0xFFFF);
+        if (asic.oam_id != 0xFFFFFFFFu && asic.oam_id != 0xFFFFu) g.oam_id = static_cast<int>(asic.oam_id);
       }
+      amdsmi_driver_info_t drv{};
+      if (amdsmi_get_gpu_driver_info(h0, &drv) == AMDSMI_STATUS_SUCCESS) g.driver_version = normalize_driver_version(drv.driver_version);
+      amdsmi_vbios_info_t vb{};
+      if (amdsmi_get_gpu_vbios_info(h0, &vb) == AMDSMI_STATUS_SUCCESS) g.vbios_version = vb.version;
       if (g.market_name.empty()) g.market_name = "AMD Instinct";
       amdsmi_vram_info_t vram{};
       if (amdsmi_get_gpu_vram_info(h0, &vram) == AMDSMI_STATUS_SUCCESS)

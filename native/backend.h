@@ -19,6 +19,7 @@
 #include <cstdint>
 #include <memory>
 #include <mutex>
+#include <cctype>
 #include <string>
 #include <vector>
 
@@ -47,6 +48,26 @@ struct PartitionInfo {
   uint64_t vram_bytes = 0;
 };
 
+// amdsmi_get_gpu_driver_info's version: "6.14.14" for a packaged amdgpu module, but the
+// whole /proc/version banner (blanks removed, "Linuxversion6.18.54-...(gcc...)#1...") when
+// amdgpu is built into the kernel.  Keeps the first dotted version and its suffix.
+inline std::string normalize_driver_version(const std::string& s) {
+  auto digit = [](char c) { return c >= '0' && c <= '9'; };
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (!digit(s[i]) || (i > 0 && (digit(s[i - 1]) || s[i - 1] == '.'))) continue;
+    size_t j = i;
+    while (j < s.size() && digit(s[j])) ++j;
+    if (j + 1 >= s.size() || s[j] != '.' || !digit(s[j + 1])) continue;  // not "N.N"
+    while (j < s.size() && (digit(s[j]) || s[j] == '.')) ++j;
+    if (j < s.size() && (s[j] == '-' || s[j] == '+' || s[j] == '~'))
+      while (j < s.size() && (std::isalnum(static_cast<unsigned char>(s[j])) || s[j] == '.' || s[j] == '-' ||
+                              s[j] == '+' || s[j] == '_' || s[j] == '~'))
+        ++j;
+    return s.substr(i, j - i);
+  }
+  return s;
+}
+
 struct GpuInfo {
   int index = -1;
   std::string uuid;
@@ -66,6 +87,10 @@ struct GpuInfo {
   int profile_partitions = 0;
   int profile_index = -1;
   int num_compute_units = 0;
+  uint32_t device_id = 0;         // PCI device id (0 = unknown)
+  int oam_id = -1;                // OAM slot on the baseboard (-1 = not reported)
+  std::string driver_version;     // amdgpu kernel driver
+  std::string vbios_version;      // VBIOS / IFWI version string
   int num_xgmi_links = 0;
   int bad_page_threshold = -1;    // RAS retired-page threshold (-1 = not readable)
   std::vector<PartitionInfo> partitions;

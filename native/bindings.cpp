@@ -69,6 +69,10 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("profile_partitions", &GpuInfo::profile_partitions)
       .def_readwrite("profile_index", &GpuInfo::profile_index)
       .def_readwrite("num_compute_units", &GpuInfo::num_compute_units)
+      .def_readwrite("device_id", &GpuInfo::device_id)
+      .def_readwrite("oam_id", &GpuInfo::oam_id)
+      .def_readwrite("driver_version", &GpuInfo::driver_version)
+      .def_readwrite("vbios_version", &GpuInfo::vbios_version)
       .def_readwrite("num_xgmi_links", &GpuInfo::num_xgmi_links)
       .def_readwrite("bad_page_threshold", &GpuInfo::bad_page_threshold)
       .def_readwrite("partitions", &GpuInfo::partitions);
@@ -247,6 +251,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("discover_calls", &FixtureBackend::discover_calls);
 
   m.def("make_amdsmi_backend", &make_amdsmi_backend, py::call_guard<py::gil_scoped_release>());
+  m.def("normalize_driver_version", &normalize_driver_version, py::arg("reported"));
   m.def("amdsmi_available", &amdsmi_available, py::arg("keep") = false, py::call_guard<py::gil_scoped_release>());
   m.def("amdsmi_release_probe", &amdsmi_release_probe, py::call_guard<py::gil_scoped_release>());
   m.def("amdsmi_probe_held", &amdsmi_probe_held);

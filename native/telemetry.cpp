@@ -383,7 +383,12 @@ void Exporter::render_gpu_text(const std::vector<GpuSample>& samples, const std:
     append_label_value(&l, gi.compute_partition);
     l.append("\",memory_partition=\"");
     append_label_value(&l, gi.memory_partition);
-    l.append("\",numa_node=\"").append(std::to_string(gi.numa_node)).append("\"");
+    l.append("\",numa_node=\"").append(std::to_string(gi.numa_node));
+    l.append("\",driver_version=\"");
+    append_label_value(&l, gi.driver_version);
+    l.append("\",vbios_version=\"");
+    append_label_value(&l, gi.vbios_version);
+    l.append("\"");
     line(&o, "amdgpu_info", l, 1);
   }
   append_header(&o, "amdgpu_telemetry_up", "1 if the last telemetry sample of the GPU succeeded.", "gauge");

@@ -52,8 +52,13 @@ def test_amdsmi_discovers_mi355x(amdsmi_backend):
         assert p.render_minor >= 128
         assert os.path.exists("/dev/dri/renderD%d" % p.render_minor)
         assert p.id
+    # node-labeller inventory: PCI device id, OAM slot, driver and VBIOS versions
+    assert g.device_id != 0 and g.driver_version[:1].isdigit() and "." in g.driver_version, \
+        (hex(g.device_id), g.driver_version)
+    assert len(g.driver_version) <= 63  # fits a label value
     print("discovered", [(x.index, x.bdf, x.market_name, x.compute_partition, x.memory_partition,
-                          len(x.partitions), x.numa_node, x.num_compute_units) for x in gpus])
+                          len(x.partitions), x.numa_node, x.num_compute_units, hex(x.device_id), x.oam_id,
+                          x.driver_version, x.vbios_version) for x in gpus])
 
 
 def test_partition_profile_comes_from_amdsmi(amdsmi_backend):

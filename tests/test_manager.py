@@ -413,6 +413,9 @@ def test_node_feature_file_tracks_partition_mode(make_cfg, plugin_dir, run_manag
         assert labels["amd.com/gpu.count"] == "2" and labels["amd.com/gpu.compute-partition"] == "SPX"
         assert labels["amd.com/gpu.product"] == "AMD_Instinct_MI355X" and labels["amd.com/gpu.family"] == "gfx950"
         assert labels["amd.com/gpu.vram-gb"] == "288" and labels["amd.com/gpu.partitions"] == "2"
+        assert labels["amd.com/gpu.device-id"] == "75a3"
+        assert labels["amd.com/gpu.driver-version"] == fixtures.FIXTURE_DRIVER_VERSION
+        assert labels["amd.com/gpu.vbios-version"] == fixtures.FIXTURE_VBIOS_VERSION
         fixtures.set_gpu_mode(be, 0, "CPX", "NPS2")
         fixtures.set_gpu_mode(be, 1, "CPX", "NPS2")
         assert _wait(lambda: "gpu.compute-partition=CPX" in path.read_text(), timeout=10)
@@ -899,3 +902,31 @@ def test_allocate_counts_as_link_load_until_pod_resources_has_it(make_cfg, plugi
             assert m.recent_allocations.link_pods(4)[1] == 0  # not counted twice
     finally:
         stub.stop()
+
+
+def test_node_labels_leave_out_a_version_the_gpus_disagree_on():
+    """Driver / VBIOS labels name the node's one version; GPUs on different firmware (an
+    update rolling through the node) give no label rather than GPU 0's."""
+    from k8s_gpu_device_plugin_amd.labels import node_labels
+    be = fixtures.build_backend("2gpu_spx")
+    gpus, _ = be.discover()
+    gpus[1].vbios_version = "OTHER"
+    labels = node_labels(gpus)
+    assert "amd.com/gpu.vbios-version" not in labels
+    assert labels["amd.com/gpu.driver-version"] == fixtures.FIXTURE_DRIVER_VERSION
+    gpus[0].device_id = 0
+    assert "amd.com/gpu.device-id" not in node_labels(gpus)
+
+
+@pytest.mark.parametrize("reported,want", [
+    ("6.14.14", "6.14.14"),
+    # amdgpu built into the kernel: amdsmi hands back the /proc/version banner, blanks removed
+    # (what the MI355X box reports)
+    ("Linuxversion6.18.54-ant.1(nixbld@localhost)(gcc(GCC)15.3.0,GNUld(GNUBinutils)2.46)#1-ant-ociSMP", "6.18.54-ant.1"),
+    ("amdgpu 6.10.5-2109964.24.04", "6.10.5-2109964.24.04"),
+    ("", ""),
+    ("unknown", "unknown"),
+])
+def test_driver_version_is_normalised(reported, want):
+    from k8s_gpu_device_plugin_amd import native
+    assert native.load().normalize_driver_version(reported) == want

@@ -29,6 +29,8 @@ def test_exporter_cpx_64_partitions(n):
     fams = _families(ex.render())
     assert len(fams["amdgpu_info"].samples) == 8
     assert fams["amdgpu_info"].samples[0].labels["compute_partition"] == "CPX"
+    assert fams["amdgpu_info"].samples[0].labels["driver_version"] == fixtures.FIXTURE_DRIVER_VERSION
+    assert fams["amdgpu_info"].samples[0].labels["vbios_version"] == fixtures.FIXTURE_VBIOS_VERSION
     assert len(fams["amdgpu_partition_info"].samples) == 64
     assert len(fams["amdgpu_partition_gfx_busy_percent"].samples) == 64
     assert len(fams["amdgpu_xgmi_link_up"].samples) == 8 * 7
