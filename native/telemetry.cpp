@@ -388,7 +388,7 @@ void Exporter::render_gpu_text(const std::vector<GpuSample>& samples, const std:
     append_label_value(&l, gi.driver_version);
     l.append("\",vbios_version=\"");
     append_label_value(&l, gi.vbios_version);
-    l.append("\"");
+    l.append("\",oam_id=\"").append(std::to_string(gi.oam_id)).append("\"");
     line(&o, "amdgpu_info", l, 1);
   }
   append_header(&o, "amdgpu_telemetry_up", "1 if the last telemetry sample of the GPU succeeded.", "gauge");

@@ -31,6 +31,7 @@ def test_exporter_cpx_64_partitions(n):
     assert fams["amdgpu_info"].samples[0].labels["compute_partition"] == "CPX"
     assert fams["amdgpu_info"].samples[0].labels["driver_version"] == fixtures.FIXTURE_DRIVER_VERSION
     assert fams["amdgpu_info"].samples[0].labels["vbios_version"] == fixtures.FIXTURE_VBIOS_VERSION
+    assert [s.labels["oam_id"] for s in fams["amdgpu_info"].samples] == [str(i) for i in range(8)]
     assert len(fams["amdgpu_partition_info"].samples) == 64
     assert len(fams["amdgpu_partition_gfx_busy_percent"].samples) == 64
     assert len(fams["amdgpu_xgmi_link_up"].samples) == 8 * 7
