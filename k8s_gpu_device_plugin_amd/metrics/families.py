@@ -39,7 +39,9 @@ FAMILIES = (
     Family("process_start_time_seconds", "gauge", (), "exporter", "Process start time"),
     # --- per-GPU amdsmi telemetry ---
     Family("amdgpu_info", "gauge", GPU + ("uuid", "bdf", "name", "gfx_target", "compute_partition",
-                                          "memory_partition", "numa_node"), "exporter", "Static inventory (value 1)"),
+                                          "memory_partition", "numa_node", "driver_version", "vbios_version",
+                                          "oam_id"), "exporter",
+           "Static inventory (value 1); `oam_id` is the baseboard slot (-1 unknown)"),
     Family("amdgpu_telemetry_up", "gauge", GPU, "exporter", "Last sample succeeded"),
     Family("amdgpu_power_watts", "gauge", GPU, "exporter", "Socket power"),
     Family("amdgpu_energy_joules_total", "counter", GPU, "exporter", "Accumulated energy"),
@@ -50,6 +52,11 @@ FAMILIES = (
     Family("amdgpu_throttle_status", "gauge", GPU, "exporter", "Throttle status bitmask"),
     Family("amdgpu_xgmi_link_width", "gauge", GPU, "exporter", "Current xGMI link width, lanes (16 when fully trained)"),
     Family("amdgpu_xgmi_link_speed_gbps", "gauge", GPU, "exporter", "Current xGMI per-lane rate (38 Gb/s on MI355X)"),
+    Family("amdgpu_xgmi_error_status", "gauge", GPU, "exporter", "xGMI error state: 0 none, 1 an error, 2 multiple"),
+    Family("amdgpu_pcie_link_width", "gauge", GPU, "exporter", "Current PCIe link width to the host, lanes"),
+    Family("amdgpu_pcie_link_speed_gtps", "gauge", GPU, "exporter", "Current PCIe link rate to the host, GT/s"),
+    Family("amdgpu_pcie_replays_total", "counter", GPU, "exporter", "PCIe replays on the host link"),
+    Family("amdgpu_pcie_recoveries_total", "counter", GPU, "exporter", "PCIe L0 -> recovery transitions"),
     Family("amdgpu_temperature_celsius", "gauge", GPU + ("sensor",), "exporter",
            "Temperature by sensor: edge, hotspot, mem, hbm0..N"),
     Family("amdgpu_clock_mhz", "gauge", GPU + ("clock",), "exporter", "gfx / mem clocks"),
@@ -139,6 +146,8 @@ PROMQL_EXAMPLES = (
      "amdgpu_device_plugin_allocation_info"),
     ("Partitions whose last canary ran below 90% of the node's best bf16 MFMA rate",
      'amdgpu_canary_matrix_tflops{path="mfma_bf16"} < on() group_left 0.9 * max(amdgpu_canary_matrix_tflops{path="mfma_bf16"})'),
+    ("GPUs whose host PCIe link trained below the node's widest, or is replaying",
+     "amdgpu_pcie_link_width < on() group_left max(amdgpu_pcie_link_width) or rate(amdgpu_pcie_replays_total[5m]) > 0"),
     ("xGMI traffic per link (bytes/s)", "rate(amdgpu_xgmi_read_bytes_total[1m]) + rate(amdgpu_xgmi_write_bytes_total[1m])"),
 )
 

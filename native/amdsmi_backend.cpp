@@ -433,6 +433,10 @@ class AmdSmiBackend : public Backend {
       if (m.throttle_status != 0xFFFFFFFFu) s->throttle_status = m.throttle_status;
       if (valid16(m.xgmi_link_width)) s->xgmi_link_width = m.xgmi_link_width;
       if (valid16(m.xgmi_link_speed)) s->xgmi_link_speed = m.xgmi_link_speed;
+      if (valid16(m.pcie_link_width) && m.pcie_link_width != 0) s->pcie_link_width = m.pcie_link_width;
+      if (valid16(m.pcie_link_speed) && m.pcie_link_speed != 0) s->pcie_link_speed_gtps = m.pcie_link_speed * 0.1;
+      if (valid64(m.pcie_replay_count_acc)) s->pcie_replays = static_cast<double>(m.pcie_replay_count_acc);
+      if (valid64(m.pcie_l0_to_recov_count_acc)) s->pcie_recoveries = static_cast<double>(m.pcie_l0_to_recov_count_acc);
       const int nparts = static_cast<int>(procs_[gpu].size());
       s->num_partitions = std::min(nparts, kMaxPartitions);
       for (int p = 0; p < s->num_partitions && p < AMDSMI_MAX_NUM_XCP; ++p) {
@@ -473,6 +477,8 @@ class AmdSmiBackend : public Backend {
       s->ecc_correctable = static_cast<int64_t>(ec.correctable_count);
       s->ecc_uncorrectable = static_cast<int64_t>(ec.uncorrectable_count);
     }
+    amdsmi_xgmi_status_t xs = AMDSMI_XGMI_STATUS_NO_ERRORS;
+    if (amdsmi_gpu_xgmi_error_status(h0, &xs) == AMDSMI_STATUS_SUCCESS) s->xgmi_error_status = static_cast<int>(xs);
     t = charge(kCallEcc, t);
     link_state_locked(gpu, s, mst == AMDSMI_STATUS_SUCCESS ? &m : nullptr);
     t = charge(kCallLinks, t);

@@ -163,6 +163,15 @@ struct GpuSample {
   // gpu_metrics: the GPU's current xGMI link width (lanes) and per-lane rate; -1 = unknown
   double xgmi_link_width = -1;
   double xgmi_link_speed = -1;
+  // amdsmi_gpu_xgmi_error_status: 0 no errors, 1 an error, 2 multiple (latched until an
+  // operator clears them); -1 = unknown
+  int xgmi_error_status = -1;
+  // gpu_metrics: the host PCIe link (a link that re-trained narrower or slower, and
+  // replay / recovery counts, are the classic signs of a failing riser or retimer)
+  double pcie_link_width = -1;      // lanes
+  double pcie_link_speed_gtps = -1; // GT/s
+  double pcie_replays = -1;         // accumulated
+  double pcie_recoveries = -1;      // accumulated L0 -> recovery transitions
   int num_partitions = 0;
   double partition_gfx_busy_pct[kMaxPartitions] = {};
   double partition_vram_used_bytes[kMaxPartitions] = {};

@@ -145,6 +145,11 @@ PYBIND11_MODULE(_native, m) {
       .def_readonly("throttle_status", &GpuSample::throttle_status)
       .def_readonly("xgmi_link_width", &GpuSample::xgmi_link_width)
       .def_readonly("xgmi_link_speed", &GpuSample::xgmi_link_speed)
+      .def_readonly("xgmi_error_status", &GpuSample::xgmi_error_status)
+      .def_readonly("pcie_link_width", &GpuSample::pcie_link_width)
+      .def_readonly("pcie_link_speed_gtps", &GpuSample::pcie_link_speed_gtps)
+      .def_readonly("pcie_replays", &GpuSample::pcie_replays)
+      .def_readonly("pcie_recoveries", &GpuSample::pcie_recoveries)
       .def_property_readonly("links", [](const GpuSample& s) {
         py::list l;
         for (int k = 0; k < s.num_links; ++k)

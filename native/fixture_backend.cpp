@@ -210,6 +210,11 @@ bool FixtureBackend::sample(int index, GpuSample* s) {
   s->num_links = 0;
   s->xgmi_link_width = 16;
   s->xgmi_link_speed = 38;
+  s->xgmi_error_status = 0;
+  s->pcie_link_width = 16;
+  s->pcie_link_speed_gtps = 32;
+  s->pcie_replays = 0;
+  s->pcie_recoveries = 0;
   for (int peer = 0; peer < topo_.n && s->num_links < kMaxXgmiLinks; ++peer) {
     if (peer == gpu || topo_.at(gpu, peer).type != kLinkXgmi) continue;
     const int k = s->num_links++;

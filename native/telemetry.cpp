@@ -423,6 +423,16 @@ void Exporter::render_gpu_text(const std::vector<GpuSample>& samples, const std:
           [](const GpuSample& s) { return s.xgmi_link_width; });
   per_gpu("amdgpu_xgmi_link_speed_gbps", "Current xGMI per-lane rate of the GPU, Gb/s.", "gauge",
           [](const GpuSample& s) { return s.xgmi_link_speed; });
+  per_gpu("amdgpu_xgmi_error_status", "xGMI error state of the GPU: 0 none, 1 an error, 2 multiple errors.", "gauge",
+          [](const GpuSample& s) { return static_cast<double>(s.xgmi_error_status); });
+  per_gpu("amdgpu_pcie_link_width", "Current PCIe link width to the host, lanes.", "gauge",
+          [](const GpuSample& s) { return s.pcie_link_width; });
+  per_gpu("amdgpu_pcie_link_speed_gtps", "Current PCIe link rate to the host, GT/s per lane.", "gauge",
+          [](const GpuSample& s) { return s.pcie_link_speed_gtps; });
+  per_gpu("amdgpu_pcie_replays_total", "PCIe replays issued on the host link.", "counter",
+          [](const GpuSample& s) { return s.pcie_replays; });
+  per_gpu("amdgpu_pcie_recoveries_total", "PCIe host link transitions from L0 to recovery.", "counter",
+          [](const GpuSample& s) { return s.pcie_recoveries; });
 
   {  // temperatures
     bool hdr = false;

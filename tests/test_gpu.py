@@ -87,7 +87,12 @@ def test_amdsmi_telemetry(amdsmi_backend):
     assert s is not None and s.ok
     assert s.power_w > 0 or s.temp_hotspot_c > 0
     assert s.vram_total_bytes > 0
-    print("sample", s.power_w, s.temp_hotspot_c, s.temp_hbm_c, s.gfx_activity_pct, s.vram_used_bytes, s.links)
+    # the xGMI error state needs privileges the box's user lacks (-1 then: the family is left out)
+    assert s.xgmi_error_status in (-1, 0, 1, 2)
+    assert s.pcie_link_width == -1 or 1 <= s.pcie_link_width <= 32
+    print("sample", s.power_w, s.temp_hotspot_c, s.temp_hbm_c, s.gfx_activity_pct, s.vram_used_bytes, s.links,
+          "xgmi errors", s.xgmi_error_status, "pcie x%g %g GT/s replays %g recoveries %g"
+          % (s.pcie_link_width, s.pcie_link_speed_gtps, s.pcie_replays, s.pcie_recoveries))
 
 
 def test_amdsmi_sample_cost_breakdown(amdsmi_backend):
