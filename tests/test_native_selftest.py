@@ -7,6 +7,7 @@ import pytest
 from k8s_gpu_device_plugin_amd import _build
 
 
+@pytest.mark.timeout(900)  # a fresh instrumented build of the core takes minutes on a small host
 @pytest.mark.parametrize("sanitize", [None, "address", "thread"])
 def test_native_selftest(sanitize):
     exe = _build.build_selftest(sanitize)

@@ -56,6 +56,7 @@ def run_sanitized(sanitize: str, tests, log_dir: str, extra_args=()) -> subproce
 
 
 @pytest.mark.slow
+@pytest.mark.timeout(1800)  # an instrumented build plus the whole integration suite: past pytest.ini's 300 s
 @pytest.mark.parametrize("sanitize", ["address", "thread"])
 def test_integration_suite_under_sanitizer(sanitize, tmp_path):
     if os.environ.get("AMDGPU_DP_NATIVE_SO"):
