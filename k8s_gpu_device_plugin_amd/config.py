@@ -101,6 +101,7 @@ class HttpConfig:
     accessLog: bool = True
     server: str = "native"       # native | python
     busyPollUs: int = 50         # native server: keep polling this long after a request (0 = off)
+    restartLocalOnly: bool = False  # GET /restart only from loopback peers (others: 403)
 
 
 @dataclass

@@ -52,13 +52,14 @@ class WebServer:
             hc.access_log = bool(self.cfg.http.accessLog)
             hc.read_timeout_s = 30  # server/server.go:45
             hc.busy_poll_us = int(self.cfg.http.busyPollUs)
+            hc.restart_local_only = bool(self.cfg.http.restartLocalOnly)
             hc.version = VERSION
             srv = n.HttpServer(hc, self.manager.exporter)
             srv.set_restart_hook(self.manager.restart)
             self.port = srv.start()
             self._impl = srv
         else:
-            self._impl = PyWebServer(self.host, self.port, self.manager)
+            self._impl = PyWebServer(self.host, self.port, self.manager, bool(self.cfg.http.restartLocalOnly))
             self.port = self._impl.start()
         for r in ROUTES:  # server/server.go:48-54 prints the route table
             log.info("GET  %s", r)
@@ -70,6 +71,17 @@ class WebServer:
         if impl is not None:
             impl.stop()
             log.info("web server stopped")
+
+
+def _is_loopback(addr: str) -> bool:
+    import ipaddress
+    try:
+        ip = ipaddress.ip_address(addr)
+    except ValueError:
+        return False
+    if getattr(ip, "ipv4_mapped", None) is not None:
+        ip = ip.ipv4_mapped
+    return ip.is_loopback
 
 
 def accepts_gzip(header: str) -> bool:
@@ -120,8 +132,9 @@ class _Metrics:
 
 
 class PyWebServer:
-    def __init__(self, host: str, port: int, manager) -> None:
+    def __init__(self, host: str, port: int, manager, restart_local_only: bool = False) -> None:
         self.host, self.port, self.manager = host, port, manager
+        self.restart_local_only = restart_local_only
         self.metrics = _Metrics()
         self._httpd = None
         self._thread = None
@@ -138,7 +151,8 @@ class PyWebServer:
                 log.debug("%s %s", self.address_string(), fmt % args)
 
             def _send(self, status: int, body: bytes, ctype: str = "application/json", gz: bool = False) -> None:
-                self.send_response_only(status, {200: "OK", 404: "Not Found", 405: "Method Not Allowed"}.get(status))
+                self.send_response_only(status, {200: "OK", 403: "Forbidden", 404: "Not Found",
+                                                 405: "Method Not Allowed"}.get(status))
                 for k, v in CORS_HEADERS:
                     self.send_header(k, v)
                 self.send_header("Access-Control-Allow-Origin", self.headers.get("Origin") or "*")
@@ -168,6 +182,8 @@ class PyWebServer:
                     status, body, ctype = 200, envelope_bytes(success("version : " + VERSION)), "application/json"
                 elif path == "/health":
                     status, body, ctype = 200, envelope_bytes(success("ok")), "application/json"
+                elif path == "/restart" and outer.restart_local_only and not _is_loopback(self.client_address[0]):
+                    status, body, ctype = 403, b'{"message":"Forbidden"}\n', "application/json"
                 elif path == "/restart":
                     outer.manager.restart()
                     status, body, ctype = 200, envelope_bytes(success("ok")), "application/json"

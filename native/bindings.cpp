@@ -531,6 +531,7 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("idle_timeout_s", &HttpConfig::idle_timeout_s)
       .def_readwrite("read_timeout_s", &HttpConfig::read_timeout_s)
       .def_readwrite("busy_poll_us", &HttpConfig::busy_poll_us)
+      .def_readwrite("restart_local_only", &HttpConfig::restart_local_only)
       .def_readwrite("version", &HttpConfig::version);
 
   py::class_<HttpServer, std::shared_ptr<HttpServer>>(m, "HttpServer")

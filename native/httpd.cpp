@@ -100,6 +100,7 @@ struct Conn {
   size_t out_off = 0;
   int64_t last_ns = 0;
   std::string remote;
+  bool local = false;  // the peer is on a loopback address
   bool close_after = false;
   bool want_out = false;
   bool want_in = true;
@@ -326,7 +327,7 @@ int HttpServer::start() {
           } else {
             const size_t qm = uri.find('?');
             handle(method, qm == std::string::npos ? uri : uri.substr(0, qm), origin, keep, http10, &c->out,
-                   &status, &body_bytes, gzip_ok);
+                   &status, &body_bytes, gzip_ok, c->local);
           }
           const double dt = (mono_ns() - t0) * 1e-9;
           requests_.add();
@@ -375,6 +376,12 @@ int HttpServer::start() {
               else if (peer.ss_family == AF_INET6)
                 inet_ntop(AF_INET6, &reinterpret_cast<sockaddr_in6*>(&peer)->sin6_addr, ip, sizeof(ip));
               c->remote = ip;
+              if (peer.ss_family == AF_INET)
+                c->local = (ntohl(reinterpret_cast<sockaddr_in*>(&peer)->sin_addr.s_addr) >> 24) == 127;
+              else if (peer.ss_family == AF_INET6) {
+                const in6_addr& a6 = reinterpret_cast<sockaddr_in6*>(&peer)->sin6_addr;
+                c->local = IN6_IS_ADDR_LOOPBACK(&a6) || (IN6_IS_ADDR_V4MAPPED(&a6) && a6.s6_addr[12] == 127);
+              }
               Worker* t = pick_least_loaded(workers_, w);  // this one on a tie
               struct epoll_event ev {};
               ev.events = EPOLLIN | EPOLLRDHUP;
@@ -518,7 +525,7 @@ void HttpServer::record(int mi, int hi, int status, double seconds) {
 
 void HttpServer::handle(const std::string& method, const std::string& path, const std::string& origin,
                         bool keep_alive, bool http10, std::string* out, int* status_out, size_t* body_bytes_out,
-                        bool gzip_ok) {
+                        bool gzip_ok, bool peer_local) {
   const int64_t t0 = mono_ns();
   int status = 200;
   static thread_local std::string body_buf;  // per worker thread, capacity reused
@@ -556,6 +563,9 @@ void HttpServer::handle(const std::string& method, const std::string& path, cons
       body = "{\"code\":0,\"data\":\"version : " + cfg_.version + "\",\"msg\":\"success\"}\n";
     } else if (handler == 2) {  // router/api.go:45-47
       body = "{\"code\":0,\"data\":\"ok\",\"msg\":\"success\"}\n";
+    } else if (handler == 3 && cfg_.restart_local_only && !peer_local) {
+      status = 403;  // http.restartLocalOnly: a reload is not for remote callers
+      body = "{\"message\":\"Forbidden\"}\n";
     } else if (handler == 3) {  // router/api.go:50-54
       std::function<void()> hook;
       {

@@ -32,6 +32,9 @@ struct HttpConfig {
   int idle_timeout_s = 60;
   int read_timeout_s = 30;
   int busy_poll_us = 0;  // keep polling this long after a request before sleeping (0 = off)
+  // GET /restart only from a loopback peer (others get 403); off = the reference's
+  // behaviour, where anyone who reaches the port can reload the plugins
+  bool restart_local_only = false;
   std::string version = "0.1.0";
 };
 
@@ -57,7 +60,8 @@ class HttpServer {
  private:
   friend struct Worker;
   void handle(const std::string& method, const std::string& path, const std::string& origin, bool keep_alive,
-              bool http10, std::string* out, int* status_out, size_t* body_bytes_out, bool gzip_ok = false);
+              bool http10, std::string* out, int* status_out, size_t* body_bytes_out, bool gzip_ok = false,
+              bool peer_local = true);
   void record(int method_idx, int handler_idx, int status, double seconds);
   void log_access(const std::string& remote, const std::string& host, const std::string& method,
                   const std::string& uri, const std::string& ua, int status, double seconds, size_t bytes_in,

@@ -422,3 +422,70 @@ def test_hostile_clients_do_not_disturb_scrapes(make_cfg):
         for s in idle:
             s.close()
         w.stop()
+
+
+def _non_loopback_ipv4():
+    """An address of this host that is not loopback (None when the host has none)."""
+    s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    try:
+        s.connect(("198.51.100.1", 9))  # no packet is sent: this only picks a source address
+        ip = s.getsockname()[0]
+    except OSError:
+        return None
+    finally:
+        s.close()
+    return None if ip.startswith("127.") or ip == "0.0.0.0" else ip
+
+
+@pytest.mark.parametrize("server", ["native", "python"])
+def test_restart_local_only(make_cfg, server):
+    """http.restartLocalOnly: /restart from loopback reloads, from another address it is a
+    403 (counted as 4xx); /health and /metrics stay open to everyone."""
+    ip = _non_loopback_ipv4()
+    if ip is None:
+        pytest.skip("no non-loopback IPv4 address on this host")
+    cfg = make_cfg(webListenAddress="0.0.0.0:0", http={"server": server, "accessLog": False,
+                                                       "restartLocalOnly": True})
+    mgr = PluginManager(cfg)
+    restarts = []
+    mgr.restart = lambda: restarts.append(time.monotonic())
+    mgr.load_plugins()
+    w = WebServer(cfg, mgr)
+    port = w.start()
+    try:
+        def remote(path):
+            c = http.client.HTTPConnection(ip, port, timeout=5)
+            c.request("GET", path)
+            r = c.getresponse()
+            out = (r.status, r.read())
+            c.close()
+            return out
+        assert remote("/restart") == (403, b'{"message":"Forbidden"}\n') and restarts == []
+        assert remote("/health")[0] == 200
+        assert get(port, "/restart")[0] == 200 and len(restarts) == 1
+        body = remote("/metrics")[1].decode()
+        assert 'echo_http_requests_total{handler="/restart",method="GET",status="4xx"} 1' in body
+    finally:
+        w.stop()
+        mgr.exporter.stop()
+        mgr.monitor.stop()
+
+
+def test_restart_is_open_to_everyone_by_default(make_cfg):
+    """The reference's behaviour stays the default."""
+    ip = _non_loopback_ipv4()
+    if ip is None:
+        pytest.skip("no non-loopback IPv4 address on this host")
+    cfg = make_cfg(webListenAddress="0.0.0.0:0", http={"accessLog": False})
+    mgr = PluginManager(cfg)
+    restarts = []
+    mgr.restart = lambda: restarts.append(time.monotonic())
+    w = WebServer(cfg, mgr)
+    port = w.start()
+    try:
+        c = http.client.HTTPConnection(ip, port, timeout=5)
+        c.request("GET", "/restart")
+        assert c.getresponse().status == 200 and len(restarts) == 1
+        c.close()
+    finally:
+        w.stop()
