@@ -117,6 +117,9 @@ class PluginManager:
         self._event_sources: int | None = None
         # last canary result per (gpu, hardware partition index): (unix time, result dict);
         # written by canary pool threads, rendered by the manager thread
+        # GET /ready: (ready, reason) pushed to listeners (the web server) when it changes
+        self._readiness: tuple[bool, str] = (False, "plugins not loaded yet")
+        self._readiness_listeners: list = []
         self.canary_results: dict[tuple[int, int], tuple[float, dict]] = {}
         self._canary_owner: dict[tuple[int, int], str] = {}  # same keys -> identity of the GPU it ran on
         self._canary_lock = threading.Lock()
@@ -128,6 +131,47 @@ class PluginManager:
 
     def stop(self) -> None:
         self.events.put((EV_STOP,))
+
+    def add_readiness_listener(self, fn) -> None:
+        """fn(ready, reason) now and on every change of the readiness ``GET /ready`` reports."""
+        with self._lock:
+            self._readiness_listeners.append(fn)
+            state = self._readiness
+        fn(*state)
+
+    def remove_readiness_listener(self, fn) -> None:
+        with self._lock:
+            if fn in self._readiness_listeners:
+                self._readiness_listeners.remove(fn)
+
+    def readiness(self) -> tuple:
+        """Ready when every resource that has devices is registered with kubelet (the
+        reference has no such signal: its /health answers ok whatever the plugins do)."""
+        if self.fatal_error:
+            return False, "fatal: %s" % self.fatal_error
+        if not self._running.is_set():
+            return False, "plugin manager not running"
+        with_devices = [p for p in self.plugins if len(p)]
+        if not with_devices:
+            return False, "no devices found" if self.device_map is not None else "plugins not loaded yet"
+        missing = [str(p.resource) for p in with_devices if not p.registered]
+        if missing:
+            return False, "not registered with kubelet: %s" % ", ".join(missing)
+        return True, ""
+
+    def _push_readiness(self) -> None:
+        state = self.readiness()
+        with self._lock:
+            if state == self._readiness:
+                return
+            self._readiness = state
+            listeners = list(self._readiness_listeners)
+        (log.info if state[0] else log.warning)("readiness: %s", "ready" if state[0] else state[1])
+        for fn in listeners:
+            try:
+                fn(*state)
+            except Exception as e:  # pragma: no cover - a listener must not stop the manager
+                log.error("readiness listener failed: %s", e)
 
     @property
     def running(self) -> bool:
@@ -729,6 +773,7 @@ class PluginManager:
                 self._retry_timer = None
 
     def _publish_metrics(self) -> None:
+        self._push_readiness()  # runs after every event, like the metrics
         lines = ["# HELP amdgpu_device_plugin_events_total Plugin manager lifecycle events.",
                  "# TYPE amdgpu_device_plugin_events_total counter"]
         for k in sorted(self.counters):
@@ -809,5 +854,6 @@ class PluginManager:
         for t in self._threads:
             t.join(2.0)
         self._threads.clear()
+        self._push_readiness()
         self._stopped.set()
         self.ready.close()

@@ -20,12 +20,12 @@ import time
 
 from .. import native
 from ..utils.log import get_logger
-from ..utils.util import envelope_bytes, success
+from ..utils.util import envelope_bytes, failed, success
 from ..utils.version import VERSION
 
 log = get_logger("web")
 
-ROUTES = ("/", "/metrics", "/health", "/restart")
+ROUTES = ("/", "/metrics", "/health", "/restart", "/ready")
 CORS_HEADERS = (
     ("Access-Control-Allow-Credentials", "true"),
     ("Access-Control-Allow-Headers", "Content-Type, Content-Length, Accept-Encoding, Authorization, Origin"),
@@ -64,9 +64,20 @@ class WebServer:
         for r in ROUTES:  # server/server.go:48-54 prints the route table
             log.info("GET  %s", r)
         log.info("web server started on %s:%d (%s)", self.host, self.port, self.kind)
+        add = getattr(self.manager, "add_readiness_listener", None)
+        if add is not None:  # GET /ready follows the manager's registration state
+            add(self._set_ready)
         return self.port
 
+    def _set_ready(self, ready: bool, reason: str) -> None:
+        impl = self._impl
+        if impl is not None:
+            impl.set_ready(bool(ready), reason or "")
+
     def stop(self) -> None:
+        remove = getattr(self.manager, "remove_readiness_listener", None)
+        if remove is not None:
+            remove(self._set_ready)
         impl, self._impl = self._impl, None
         if impl is not None:
             impl.stop()
@@ -135,6 +146,7 @@ class PyWebServer:
     def __init__(self, host: str, port: int, manager, restart_local_only: bool = False) -> None:
         self.host, self.port, self.manager = host, port, manager
         self.restart_local_only = restart_local_only
+        self.ready, self.not_ready_reason = True, ""
         self.metrics = _Metrics()
         self._httpd = None
         self._thread = None
@@ -152,7 +164,7 @@ class PyWebServer:
 
             def _send(self, status: int, body: bytes, ctype: str = "application/json", gz: bool = False) -> None:
                 self.send_response_only(status, {200: "OK", 403: "Forbidden", 404: "Not Found",
-                                                 405: "Method Not Allowed"}.get(status))
+                                                 405: "Method Not Allowed", 503: "Service Unavailable"}.get(status))
                 for k, v in CORS_HEADERS:
                     self.send_header(k, v)
                 self.send_header("Access-Control-Allow-Origin", self.headers.get("Origin") or "*")
@@ -182,6 +194,11 @@ class PyWebServer:
                     status, body, ctype = 200, envelope_bytes(success("version : " + VERSION)), "application/json"
                 elif path == "/health":
                     status, body, ctype = 200, envelope_bytes(success("ok")), "application/json"
+                elif path == "/ready":
+                    if outer.ready:
+                        status, body, ctype = 200, envelope_bytes(success("ready")), "application/json"
+                    else:
+                        status, body, ctype = 503, envelope_bytes(failed(outer.not_ready_reason)), "application/json"
                 elif path == "/restart" and outer.restart_local_only and not _is_loopback(self.client_address[0]):
                     status, body, ctype = 403, b'{"message":"Forbidden"}\n', "application/json"
                 elif path == "/restart":
@@ -229,3 +246,6 @@ class PyWebServer:
             self._httpd.shutdown()
             self._httpd.server_close()
             self._httpd = None
+
+    def set_ready(self, ready: bool, reason: str = "") -> None:
+        self.ready, self.not_ready_reason = bool(ready), ("" if ready else reason)

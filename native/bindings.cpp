@@ -548,6 +548,7 @@ PYBIND11_MODULE(_native, m) {
         s.render_http_metrics(&o);
         return o;
       })
+      .def("set_ready", &HttpServer::set_ready, py::arg("ready"), py::arg("reason") = "")
       .def("set_restart_hook", [](HttpServer& s, py::object fn) {
         if (fn.is_none()) {
           s.set_restart_hook(nullptr);

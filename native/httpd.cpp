@@ -24,7 +24,7 @@ namespace amdgpu_dp {
 namespace {
 
 const char* kMethodNames[] = {"GET", "POST", "PUT", "DELETE", "PATCH", "HEAD", "OPTIONS", "OTHER"};
-const char* kHandlerNames[] = {"/", "/metrics", "/health", "/restart", "/not-found"};
+const char* kHandlerNames[] = {"/", "/metrics", "/health", "/restart", "/ready", "/not-found"};
 const char* kStatusNames[] = {"1xx", "2xx", "3xx", "4xx", "5xx"};
 
 int method_index(const std::string& m) {
@@ -41,16 +41,34 @@ int status_class(int status) {  // middleware/echo_metric.go:50-61
   return 4;
 }
 
+// a JSON string body (quotes, backslashes and control characters escaped)
+void append_json_string_body(std::string* out, const std::string& s) {
+  for (unsigned char c : s) {
+    if (c == '"' || c == '\\') {
+      out->push_back('\\');
+      out->push_back(static_cast<char>(c));
+    } else if (c < 0x20) {
+      char buf[8];
+      std::snprintf(buf, sizeof(buf), "\\u%04x", c);
+      out->append(buf);
+    } else {
+      out->push_back(static_cast<char>(c));
+    }
+  }
+}
+
 const char* reason(int status) {
   switch (status) {
     case 200: return "OK";
     case 400: return "Bad Request";
+    case 403: return "Forbidden";
     case 404: return "Not Found";
     case 405: return "Method Not Allowed";
     case 413: return "Request Entity Too Large";
     case 431: return "Request Header Fields Too Large";
     case 500: return "Internal Server Error";
     case 501: return "Not Implemented";
+    case 503: return "Service Unavailable";
     default: return "Unknown";
   }
 }
@@ -139,6 +157,12 @@ HttpServer::~HttpServer() { stop(); }
 void HttpServer::set_restart_hook(std::function<void()> hook) {
   std::lock_guard<std::mutex> lk(hook_mu_);
   restart_hook_ = std::move(hook);
+}
+
+void HttpServer::set_ready(bool ready, const std::string& reason) {
+  std::lock_guard<std::mutex> lk(hook_mu_);
+  ready_ = ready;
+  not_ready_reason_ = ready ? std::string() : reason;
 }
 
 int HttpServer::start() {
@@ -552,10 +576,11 @@ void HttpServer::handle(const std::string& method, const std::string& path, cons
     else if (path == "/metrics") handler = 1;
     else if (path == "/health") handler = 2;
     else if (path == "/restart") handler = 3;
+    else if (path == "/ready") handler = 4;
     if (handler < 0) {
       status = 404;
       body = "{\"message\":\"Not Found\"}\n";
-      handler = 4;
+      handler = 5;
     } else if (method != "GET") {
       status = 405;
       body = "{\"message\":\"Method Not Allowed\"}\n";
@@ -563,6 +588,16 @@ void HttpServer::handle(const std::string& method, const std::string& path, cons
       body = "{\"code\":0,\"data\":\"version : " + cfg_.version + "\",\"msg\":\"success\"}\n";
     } else if (handler == 2) {  // router/api.go:45-47
       body = "{\"code\":0,\"data\":\"ok\",\"msg\":\"success\"}\n";
+    } else if (handler == 4) {  // readiness: every resource registered with kubelet
+      std::lock_guard<std::mutex> lk(hook_mu_);
+      if (ready_) {
+        body = "{\"code\":0,\"data\":\"ready\",\"msg\":\"success\"}\n";
+      } else {
+        status = 503;  // util.Failed's envelope (modules/util/http.go:13-15)
+        body = "{\"code\":-1,\"data\":null,\"msg\":\"";
+        append_json_string_body(&body, not_ready_reason_);
+        body += "\"}\n";
+      }
     } else if (handler == 3 && cfg_.restart_local_only && !peer_local) {
       status = 403;  // http.restartLocalOnly: a reload is not for remote callers
       body = "{\"message\":\"Forbidden\"}\n";

@@ -48,6 +48,9 @@ class HttpServer {
   bool running() const { return running_.load(); }
   int port() const { return bound_port_; }
   void set_restart_hook(std::function<void()> hook);
+  // GET /ready answers 200 while ready, else 503 with the reason (the plugin manager
+  // pushes its registration state here)
+  void set_ready(bool ready, const std::string& reason);
   uint64_t requests_total() const { return requests_.load(); }
   uint64_t shed_connections() const { return shed_.load(); }  // closed at accept: out of fds
   std::vector<int> worker_connections() const;  // connections owned per worker thread
@@ -72,6 +75,8 @@ class HttpServer {
   std::shared_ptr<Exporter> exporter_;
   std::function<void()> restart_hook_;
   std::mutex hook_mu_;
+  bool ready_ = true;  // GET /ready (guarded by hook_mu_)
+  std::string not_ready_reason_;
   int listen_fd_ = -1;
   int bound_port_ = 0;
   std::atomic<bool> running_{false};
@@ -83,7 +88,7 @@ class HttpServer {
   ShardedCounter shed_;
 
   static constexpr int kMethods = 8;
-  static constexpr int kHandlers = 5;
+  static constexpr int kHandlers = 6;
   static constexpr int kStatus = 5;
   // echo_http_requests_total per (status class, method, handler), one copy per thread
   // shard (metrics.h) so that concurrent workers never write the same line

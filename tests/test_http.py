@@ -489,3 +489,42 @@ def test_restart_is_open_to_everyone_by_default(make_cfg):
         c.close()
     finally:
         w.stop()
+
+
+def _wait_for(pred, timeout=10.0):
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline:
+        if pred():
+            return True
+        time.sleep(0.05)
+    return False
+
+
+@pytest.mark.parametrize("server", ["native", "python"])
+def test_ready_follows_kubelet_registration(make_cfg, plugin_dir, server):
+    """GET /ready: 503 with the reason while a resource is not registered with kubelet
+    (no kubelet.sock yet), 200 once it is; /health answers ok throughout (reference)."""
+    from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import KubeletStub
+    cfg = make_cfg(webListenAddress="127.0.0.1:0", http={"server": server, "accessLog": False}, retrySeconds=0.2)
+    mgr = PluginManager(cfg)
+    w = WebServer(cfg, mgr)
+    port = w.start()  # the web server comes up before the plugins (D20)
+    t = mgr.start_background()
+    try:
+        st, hdrs, body = get(port, "/ready")
+        assert st == 503 and json.loads(body) == {"code": -1, "data": None,
+                                                 "msg": "not registered with kubelet: amd.com/gpu"}
+        assert get(port, "/health")[0] == 200
+        with KubeletStub(plugin_dir) as k:
+            k.wait_for_registrations(1, timeout=10)
+            assert _wait_for(lambda: get(port, "/ready")[0] == 200)
+            assert get(port, "/ready")[2] == b'{"code":0,"data":"ready","msg":"success"}\n'
+        reqs = {(s.labels["handler"], s.labels["status"]): s.value
+                 for f in text_string_to_metric_families(get(port, "/metrics")[2].decode())
+                 for s in f.samples if s.name == "echo_http_requests_total"}
+        assert reqs[("/ready", "5xx")] >= 1 and reqs[("/ready", "2xx")] >= 1
+    finally:
+        mgr.stop()
+        t.join(10)
+        assert get(port, "/ready")[0] == 503  # a stopped manager is not ready
+        w.stop()
