@@ -227,6 +227,17 @@ def test_plugin_end_to_end_on_mi355x(make_cfg, plugin_dir):
         c.request("GET", "/metrics")  # the first scrape is counted once it has been answered
         body = c.getresponse().read().decode()
         assert 'echo_http_requests_total{handler="/metrics",method="GET",status="2xx"}' in body
+        # registered with kubelet: the readiness route says so (the manager publishes its
+        # state after the registration event has been handled)
+        deadline = time.monotonic() + 5
+        while True:
+            c.request("GET", "/ready")
+            r = c.getresponse()
+            ready = (r.status, r.read())
+            if ready[0] == 200 or time.monotonic() > deadline:
+                break
+            time.sleep(0.05)
+        assert ready == (200, b'{"code":0,"data":"ready","msg":"success"}\n'), ready
     finally:
         web.stop()
         mgr.stop()
