@@ -120,6 +120,9 @@ class PluginManager:
         # GET /ready: (ready, reason) pushed to listeners (the web server) when it changes
         self._readiness: tuple[bool, str] = (False, "plugins not loaded yet")
         self._readiness_listeners: list = []
+        # held while listeners are called, so a listener added during a change cannot
+        # end up with the older state (listeners must not call back into the manager)
+        self._readiness_lock = threading.Lock()
         self.canary_results: dict[tuple[int, int], tuple[float, dict]] = {}
         self._canary_owner: dict[tuple[int, int], str] = {}  # same keys -> identity of the GPU it ran on
         self._canary_lock = threading.Lock()
@@ -134,13 +137,12 @@ class PluginManager:
 
     def add_readiness_listener(self, fn) -> None:
         """fn(ready, reason) now and on every change of the readiness ``GET /ready`` reports."""
-        with self._lock:
+        with self._readiness_lock:
             self._readiness_listeners.append(fn)
-            state = self._readiness
-        fn(*state)
+            fn(*self._readiness)
 
     def remove_readiness_listener(self, fn) -> None:
-        with self._lock:
+        with self._readiness_lock:
             if fn in self._readiness_listeners:
                 self._readiness_listeners.remove(fn)
 
@@ -161,17 +163,16 @@ class PluginManager:
 
     def _push_readiness(self) -> None:
         state = self.readiness()
-        with self._lock:
+        with self._readiness_lock:
             if state == self._readiness:
                 return
             self._readiness = state
-            listeners = list(self._readiness_listeners)
+            for fn in list(self._readiness_listeners):
+                try:
+                    fn(*state)
+                except Exception as e:  # pragma: no cover - a listener must not stop the manager
+                    log.error("readiness listener failed: %s", e)
         (log.info if state[0] else log.warning)("readiness: %s", "ready" if state[0] else state[1])
-        for fn in listeners:
-            try:
-                fn(*state)
-            except Exception as e:  # pragma: no cover - a listener must not stop the manager
-                log.error("readiness listener failed: %s", e)
 
     @property
     def running(self) -> bool:
