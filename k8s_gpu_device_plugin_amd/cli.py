@@ -37,6 +37,9 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--log-dir")
     ap.add_argument("--devices", help="GPUs to advertise: indices (e.g. 0-3), UUIDs or PCI BDFs")
     ap.add_argument("--version", action="store_true")
+    ap.add_argument("--inspect", nargs="?", const="", metavar="SIZES",
+                    help="print what would be advertised and where pods of SIZES devices (e.g. 2,4,8) would be "
+                         "placed, as JSON, and exit (nothing is served)")
     return ap.parse_args(argv)
 
 
@@ -63,6 +66,11 @@ def main(argv=None) -> int:
     except config_mod.ConfigError as e:
         print("fatal config error: %s" % e, file=sys.stderr)
         return 2
+    if args.inspect is not None:
+        from .inspect_node import main as inspect_main
+        init_logger("error", None, APP_NAME, console=True)  # stdout carries the JSON only
+        sizes = [int(x) for x in args.inspect.split(",") if x.strip()] if args.inspect else None
+        return inspect_main(cfg, sizes)
     init_logger(cfg.log.level, cfg.log.fileDir or None, APP_NAME, console=cfg.log.console,
                 max_age_days=cfg.log.maxAgeDays)
     log = get_logger()

@@ -144,3 +144,27 @@ def test_bench_reports_advertised_devices_and_tail():
     assert r["allocate_p999_us"] >= r["allocate_p99_us"] >= r["allocate_p50_us"]
     assert 0 < r["preferred_allocator_8gpu_size4_p50_us"] < 1000
     assert r["uds_roundtrip_floor_spin_p99_us"] >= r["uds_roundtrip_floor_spin_p50_us"]
+
+
+def test_inspect_prints_the_node_and_its_placements(tmp_path):
+    """--inspect: one JSON document with the GPUs, resources, xGMI links and where pods
+    of the asked sizes would go; nothing is served and nothing is written."""
+    import json as _json
+    import subprocess as _sp
+    import sys as _sys
+    feature = tmp_path / "features"
+    cfg = tmp_path / "c.yml"
+    cfg.write_text("nodeFeatureFile: %s\n" % feature)
+    out = _sp.run([_sys.executable, "-m", "k8s_gpu_device_plugin_amd", "--configFile", str(cfg),
+                   "--backend", "fixture", "--fixture", "8gpu_cpx_nps2", "--strategy", "single",
+                   "--plugin-dir", str(tmp_path / "dp"), "--inspect", "8,16"],
+                  cwd=ROOT, stdout=_sp.PIPE, stderr=_sp.PIPE, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    d = _json.loads(out.stdout)
+    assert len(d["gpus"]) == 8 and all(len(g["partitions"]) == 8 for g in d["gpus"])
+    assert len(d["resources"]["amd.com/gpu"]) == 64
+    assert len(d["xgmi"]) == 28 and all(x["type"] == "xgmi" and x["up"] for x in d["xgmi"])
+    eight = d["placement"]["amd.com/gpu"]["8"]
+    assert len(eight) == 8 and len({i.rsplit("-xcp", 1)[0] for i in eight}) == 1  # one whole GPU
+    assert len({i.rsplit("-xcp", 1)[0] for i in d["placement"]["amd.com/gpu"]["16"]}) == 2
+    assert not feature.exists() and not (tmp_path / "dp").exists()

@@ -1,6 +1,7 @@
 """Real-hardware tests (MI355X via gpurun): amdsmi discovery/telemetry, the gfx950
 canary kernels (incl. an MFMA GEMM numerics check against a PyTorch fp32 reference)
 and the full plugin path on the real backend."""
+import json
 import os
 import time
 
@@ -194,6 +195,16 @@ def test_canary_isolated_subprocess():
     from k8s_gpu_device_plugin_amd.ops import canary
     r = canary.run_isolated(0, 128 << 20)
     assert r["ok"], r
+
+
+def test_inspect_on_mi355x(make_cfg):
+    """--inspect's view of the real node: the amdsmi inventory and its placements."""
+    from k8s_gpu_device_plugin_amd.inspect_node import inspect
+    d = inspect(make_cfg(backend="amdsmi", migStrategy="single"), [1])
+    assert d["gpus"] and d["gpus"][0]["gfx"] == "gfx950" and d["gpus"][0]["partitions"]
+    ids = [x["id"] for x in d["resources"]["amd.com/gpu"]]
+    assert d["placement"]["amd.com/gpu"]["1"][0] in ids
+    print("inspect", json.dumps(d)[:600])
 
 
 def test_plugin_end_to_end_on_mi355x(make_cfg, plugin_dir):
