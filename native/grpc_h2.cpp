@@ -890,6 +890,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
   const int64_t spin_ns = static_cast<int64_t>(busy_poll_us_) * 1000;
   const int64_t admission_ns = static_cast<int64_t>(admission_poll_us_) * 1000;
   int64_t spin_until = 0;  // busy-poll window end (mono ns); 0 = closed
+  SpinGuard guard;
   while (!stop_.load(std::memory_order_relaxed)) {
     if (inject_worker_fault_.load(std::memory_order_relaxed)) {
       int armed = 1;
@@ -899,8 +900,14 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
     if (spin_until != 0) {
       n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), 0);
       if (n == 0) {
-        if (mono_ns() >= spin_until) spin_until = 0;
-        else cpu_relax();
+        if (mono_ns() >= spin_until) {
+          spin_until = 0;
+        } else if (!guard.keep_polling()) {  // preempted: the CPU is wanted (maybe by the client)
+          spin_until = 0;
+          poll_windows_yielded_.add();
+        } else {
+          guard.pause();
+        }
         continue;
       }
     } else {
@@ -1030,8 +1037,13 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
         }
         if (!process(*c)) c->closing = true;
         const int64_t window = admitting ? std::max(spin_ns, admission_ns) : spin_ns;
+        if (window > 0) {
+          spin_until = std::max(spin_until, mono_ns() + window);
+          guard.reset();
+          poll_windows_.add();
+          if (admitting && admission_ns > spin_ns) admission_windows_.add();
+        }
         admitting = false;
-        if (window > 0) spin_until = std::max(spin_until, mono_ns() + window);
       }
       if (c->out.size() - c->out_off > kMaxPendingOut) {  // e.g. a PING flood that is never read
         close_conn(fd);

@@ -6,6 +6,9 @@
 // happens only on scrape.
 #pragma once
 
+#include <sched.h>
+#include <sys/resource.h>
+
 #include <atomic>
 #include <charconv>
 #include <cmath>
@@ -84,6 +87,48 @@ inline void cpu_relax() {
   __asm__ __volatile__("" ::: "memory");
 #endif
 }
+
+// Busy-poll windows (gRPC and HTTP workers) must never keep a CPU from the thread the
+// worker is waiting for.  When the client runs on the same CPU (the scheduler places a
+// woken thread next to its waker), a polling worker and a client that is busy before
+// its next call share that CPU, and the call waits for the window's end or a scheduler
+// slice: on a shared host a 1 ms admission window turned a kubelet-like admission
+// (GetPreferredAllocation, client work, Allocate) into ~0.8 ms.  Once a window has
+// polled idle for kQuiet polls (~15-20 us: back-to-back calls arrive well before, so
+// they never pay for any of this), the poller offers the CPU every 16 polls
+// (sched_yield: a no-op when nothing else is runnable there) and ends the window as
+// soon as it has been preempted (an involuntary context switch, getrusage every 16
+// polls): someone else wants this CPU, so sleep.
+class SpinGuard {
+ public:
+  static constexpr unsigned kQuiet = 64;
+  // true while the window may keep polling
+  bool keep_polling() {
+    if (++polls_ < kQuiet || (polls_ & 15) != 0) return true;
+    const long now = nivcsw();
+    if (base_ < 0) {
+      base_ = now;
+      return true;
+    }
+    return now == base_;
+  }
+  void pause() {
+    if (polls_ >= kQuiet && (polls_ & 15) == 8) sched_yield();
+    else cpu_relax();
+  }
+  void reset() {  // a new window (after a request)
+    polls_ = 0;
+    base_ = -1;
+  }
+  static long nivcsw() {
+    struct rusage ru;
+    return getrusage(RUSAGE_THREAD, &ru) == 0 ? ru.ru_nivcsw : 0;
+  }
+
+ private:
+  unsigned polls_ = 0;
+  long base_ = -1;
+};
 
 // The worker of `workers` (each with an atomic `load`) with the fewest connections,
 // `self` on a tie, with its load already incremented.  Claims the slot with a CAS, so
