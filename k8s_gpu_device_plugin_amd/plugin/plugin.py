@@ -82,6 +82,26 @@ def native_probe(path: str, timeout: float = DIAL_TIMEOUT_S) -> None:
         c.close()
 
 
+def _socket_ident(path: str):
+    try:
+        st = os.stat(path)
+    except OSError:
+        return None
+    return st.st_dev, st.st_ino
+
+
+def _remove_if_ours(path: str, ident) -> None:
+    """Removes the plugin's socket file unless another instance has bound its own at
+    that path since (during a rolling update the next pod can start before this one has
+    stopped; deleting its socket would cut kubelet off from it)."""
+    if ident is None or _socket_ident(path) != ident:
+        return
+    try:
+        os.remove(path)
+    except FileNotFoundError:
+        pass
+
+
 def make_table(resource: str, devices: Devices, topology, cfg) -> "object":
     """Builds the native DeviceTable for a resource from the Python device view."""
     n = native.load()
@@ -125,6 +145,7 @@ class AmdDevicePlugin:
         self._last_crash = time.monotonic()
         self.server_restarts = 0
         self.registered = False
+        self._sock_ident = None  # (st_dev, st_ino) of the socket file this plugin bound
         # PreStartContainer verifier: fn(device ids) -> "" (pass) or an error message
         self.prestart_check = None
         self._prestart_thread: threading.Thread | None = None
@@ -186,10 +207,8 @@ class AmdDevicePlugin:
             nserver.stop()
         if was_serving:
             log.info("Stopped serving", extra={"resourceName": str(self.resource), "socket": self.socket})
-        try:
-            os.remove(self.socket)
-        except FileNotFoundError:
-            pass
+        _remove_if_ours(self.socket, self._sock_ident)
+        self._sock_ident = None
         self.registered = False
 
     @property
@@ -211,6 +230,7 @@ class AmdDevicePlugin:
             else:
                 self._start_grpcio_server()
             self._serving = True
+            self._sock_ident = _socket_ident(self.socket)
             if self.cfg is not None and self.cfg.health.canaryOnPreStart and self._prestart_thread is None:
                 self.table.resume_prestart()
                 self._prestart_pool = concurrent.futures.ThreadPoolExecutor(
@@ -312,6 +332,7 @@ class AmdDevicePlugin:
             pass
         self._start_grpcio_server()
         self._serving = True
+        self._sock_ident = _socket_ident(self.socket)
 
     def register(self) -> None:
         """Registration.Register with kubelet (``plugin/plugin.go:139-162``).  Sent by the

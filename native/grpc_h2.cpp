@@ -338,6 +338,11 @@ void GrpcServer::start() {
     throw std::runtime_error("GrpcServer: bind/listen " + path_ + ": " + strerror(e));
   }
   listen_fd_ = fd;
+  struct stat st {};
+  if (::stat(path_.c_str(), &st) == 0) {
+    sock_dev_ = st.st_dev;
+    sock_ino_ = st.st_ino;
+  }
   stop_ = false;
   running_ = true;
   const int n = std::max(1, nthreads_);
@@ -412,7 +417,8 @@ void GrpcServer::stop() {
   workers_.clear();
   if (listen_fd_ >= 0) ::close(listen_fd_);
   listen_fd_ = -1;
-  ::unlink(path_.c_str());
+  struct stat st {};
+  if (::stat(path_.c_str(), &st) == 0 && st.st_dev == sock_dev_ && st.st_ino == sock_ino_) ::unlink(path_.c_str());
 }
 
 void GrpcServer::fail(const std::string& why) {

@@ -15,6 +15,8 @@
 #include <atomic>
 #include <memory>
 #include <mutex>
+#include <sys/types.h>
+
 #include <string>
 #include <string_view>
 #include <thread>
@@ -93,6 +95,10 @@ class GrpcServer {
   int admission_poll_us_;
   std::shared_ptr<DeviceTable> table_;
   int listen_fd_ = -1;
+  // the socket file this server bound (device, inode): stop() removes only that file, not
+  // one a newer plugin instance (a rolling update's next pod) has bound at the same path
+  dev_t sock_dev_ = 0;
+  ino_t sock_ino_ = 0;
   std::atomic<bool> running_{false};
   std::atomic<bool> stop_{false};
   ShardedCounter requests_;  // every worker counts its calls: no shared line per RPC

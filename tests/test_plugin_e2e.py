@@ -171,3 +171,44 @@ def test_native_table_change_reaches_watchers_without_notify(plugin_dir, server_
             assert p.devices()[devs[1][0]].health == v1beta1.UNHEALTHY
         finally:
             p.stop()
+
+
+@pytest.mark.parametrize("server", ["native"])
+def test_stop_leaves_a_newer_instances_socket_alone(make_cfg, plugin_dir, server):
+    """Rolling update: the next plugin pod binds amd-gpu.sock while this one is still
+    stopping.  This one's stop must not delete the newer socket (kubelet would lose the
+    new plugin until its socket watcher re-served it).  The native server (the default);
+    grpcio's core unlinks its unix socket path on shutdown whatever is there, so with
+    grpc.server: python the newer instance's socket watcher re-serves instead."""
+    import socket as _socket
+    from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import KubeletStub
+    from k8s_gpu_device_plugin_amd.plugin.manager import PluginManager
+    with KubeletStub(plugin_dir):
+        m = PluginManager(make_cfg(grpc={"server": server}))
+        m.load_plugins()
+        m.start_plugins()
+        p = m.plugins[0]
+        assert p.serving and os.path.exists(p.socket)
+        os.remove(p.socket)  # the newer instance: remove the stale file, bind its own
+        newer = _socket.socket(_socket.AF_UNIX, _socket.SOCK_STREAM)
+        newer.bind(p.socket)
+        newer.listen(1)
+        try:
+            ident = os.stat(p.socket).st_ino
+            m.stop_plugins()
+            assert os.path.exists(p.socket) and os.stat(p.socket).st_ino == ident
+        finally:
+            newer.close()
+            os.remove(p.socket)
+        m.exporter.stop()
+        m.monitor.stop()
+    # and its own socket is removed as before
+    with KubeletStub(plugin_dir):
+        m = PluginManager(make_cfg(grpc={"server": server}))
+        m.load_plugins()
+        m.start_plugins()
+        sock = m.plugins[0].socket
+        m.stop_plugins()
+        assert not os.path.exists(sock)
+        m.exporter.stop()
+        m.monitor.stop()
