@@ -1,7 +1,7 @@
 # Convenience targets (everything is also reachable through python -m ...).
 PY ?= python3
 
-.PHONY: build native canary test test-gpu sanitize analyze bench suite soak probes run-fixture image clean
+.PHONY: build native canary test test-gpu sanitize analyze bench suite soak probes inspect run-fixture image clean
 
 build:            ## C++ core (pybind11 .so) + gfx950 HIP canary, in-tree
 	$(PY) -m k8s_gpu_device_plugin_amd._build
@@ -25,9 +25,12 @@ suite:            ## BASELINE.json configs 1-5 + scaling + health propagation
 	$(PY) -m k8s_gpu_device_plugin_amd.benchmark.suite --json suite.json
 soak:             ## daemon under Allocate + scrapes + /restart every 250 ms for 2 min (real backend if present)
 	$(PY) scripts/soak.py --seconds 120 --restart-every 0.25
-probes:           ## scrape-path and concurrency probes (JSON lines)
+probes:           ## scrape-path, concurrency and idle-gap probes (JSON lines)
 	$(PY) scripts/scrape_probe.py
 	$(PY) scripts/concurrency_probe.py
+	$(PY) scripts/idle_probe.py
+inspect:          ## what this node would advertise, and where 2/4/8-device pods would go
+	$(PY) -m k8s_gpu_device_plugin_amd --inspect
 run-fixture:      ## daemon on a fake 8x CPX node, no hardware needed
 	$(PY) -m k8s_gpu_device_plugin_amd --backend fixture --fixture 8gpu_cpx_nps2 --strategy single \
 	  --plugin-dir /tmp/amdgpu-dp --web-listen-address 127.0.0.1:9100
