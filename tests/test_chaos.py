@@ -259,6 +259,8 @@ def test_random_fault_mix_converges(make_cfg, plugin_dir, tmp_path, seed, fixtur
             assert m.running and m.fatal_error is None
             assert _wait(lambda: _advertised(plugin_dir, k) == [(i, "Healthy") for i in ids], timeout=10), \
                 _advertised(plugin_dir, k)
+            # and GET /ready says so: every resource is registered again
+            assert _wait(lambda: m._readiness == (True, ""), timeout=5), m._readiness
 
             # still wired end to end: a new reset reaches kubelet, and so does its end
             g = rng.choice(list(shown))
