@@ -95,6 +95,8 @@ FAMILIES = (
            "Advertised devices per resource and health"),
     Family("amdgpu_device_plugin_registered", "gauge", ("resource",), "manager",
            "Resource registered with kubelet"),
+    Family("amdgpu_device_plugin_ready", "gauge", (), "manager",
+           "1 if every resource with devices is registered with kubelet (GET /ready)"),
     Family("amdgpu_device_plugin_health_event_sources", "gauge", (), "manager",
            "GPUs whose hardware event notification (reset, thermal, VM fault) is armed; 0 with GPUs "
            "advertised means resets are only seen as failed telemetry (no /dev/kfd access)"),

@@ -795,6 +795,10 @@ class PluginManager:
                   "# TYPE amdgpu_device_plugin_registered gauge"]
         for p in self.plugins:
             lines.append('amdgpu_device_plugin_registered{resource="%s"} %d' % (p.resource, int(p.registered)))
+        lines += ["# HELP amdgpu_device_plugin_ready 1 if every resource with devices is registered with kubelet "
+                  "(GET /ready).",
+                  "# TYPE amdgpu_device_plugin_ready gauge",
+                  "amdgpu_device_plugin_ready %d" % int(self._readiness[0])]
         if self.podres is not None:
             from .podresources import render
             allocs, up = self.podres.snapshot()
