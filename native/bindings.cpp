@@ -599,7 +599,6 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("running", &GrpcServer::running)
       .def_property_readonly("requests", &GrpcServer::requests)
       .def_property_readonly("shed_connections", &GrpcServer::shed_connections)
-      .def_property_readonly("poll_windows", &GrpcServer::poll_windows)
       .def_property_readonly("admission_windows", &GrpcServer::admission_windows)
       .def_property_readonly("poll_windows_yielded", &GrpcServer::poll_windows_yielded)
       .def_property_readonly("connections", &GrpcServer::connections)

@@ -906,13 +906,14 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
     if (spin_until != 0) {
       n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), 0);
       if (n == 0) {
-        if (mono_ns() >= spin_until) {
+        const int64_t now = mono_ns();
+        if (now >= spin_until) {
           spin_until = 0;
-        } else if (!guard.keep_polling()) {  // preempted: the CPU is wanted (maybe by the client)
+        } else if (!guard.keep_polling(now)) {  // preempted: the CPU is wanted (maybe by the client)
           spin_until = 0;
           poll_windows_yielded_.add();
         } else {
-          guard.pause();
+          guard.pause(now);
         }
         continue;
       }
@@ -1044,9 +1045,9 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
         if (!process(*c)) c->closing = true;
         const int64_t window = admitting ? std::max(spin_ns, admission_ns) : spin_ns;
         if (window > 0) {
-          spin_until = std::max(spin_until, mono_ns() + window);
-          guard.reset();
-          poll_windows_.add();
+          const int64_t now = mono_ns();
+          spin_until = std::max(spin_until, now + window);
+          guard.reset(now);
           if (admitting && admission_ns > spin_ns) admission_windows_.add();
         }
         admitting = false;

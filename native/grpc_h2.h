@@ -57,9 +57,8 @@ class GrpcServer {
   void inject_fault(const std::string& kind);
   uint64_t requests() const { return requests_.load(); }
   uint64_t shed_connections() const { return shed_.load(); }  // closed at accept: out of fds
-  // polling windows opened after a request, those opened by a GetPreferredAllocation
-  // (grpc.admissionPollUs), and those ended early because the worker was preempted
-  uint64_t poll_windows() const { return poll_windows_.load(); }
+  // polling windows opened by a GetPreferredAllocation (grpc.admissionPollUs), and
+  // windows ended early because the worker was preempted (nothing counted per request)
   uint64_t admission_windows() const { return admission_windows_.load(); }
   uint64_t poll_windows_yielded() const { return poll_windows_yielded_.load(); }
   int connections() const { return conns_.load(); }
@@ -103,7 +102,7 @@ class GrpcServer {
   std::atomic<bool> stop_{false};
   ShardedCounter requests_;  // every worker counts its calls: no shared line per RPC
   ShardedCounter shed_;
-  ShardedCounter poll_windows_, admission_windows_, poll_windows_yielded_;
+  ShardedCounter admission_windows_, poll_windows_yielded_;
   std::atomic<int> conns_{0};
   std::vector<std::unique_ptr<Worker>> workers_;
   std::vector<std::thread> threads_;

@@ -371,8 +371,8 @@ int HttpServer::start() {
         const int n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), spin_until ? 0 : 200);
         const int64_t now = mono_ns();
         if (spin_until) {
-          if (n == 0 && now < spin_until && guard.keep_polling()) {
-            guard.pause();
+          if (n == 0 && now < spin_until && guard.keep_polling(now)) {
+            guard.pause(now);
             continue;
           }
           if (n == 0) spin_until = 0;
@@ -458,7 +458,7 @@ int HttpServer::start() {
             }
             if (spin_ns > 0) {
               spin_until = now + spin_ns;
-              guard.reset();
+              guard.reset(now);
             }
           }
           serve(c);

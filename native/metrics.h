@@ -93,30 +93,31 @@ inline void cpu_relax() {
 // woken thread next to its waker), a polling worker and a client that is busy before
 // its next call share that CPU, and the call waits for the window's end or a scheduler
 // slice: on a shared host a 1 ms admission window turned a kubelet-like admission
-// (GetPreferredAllocation, client work, Allocate) into ~0.8 ms.  Once a window has
-// polled idle for kQuiet polls (~15-20 us: back-to-back calls arrive well before, so
-// they never pay for any of this), the poller offers the CPU every 16 polls
-// (sched_yield: a no-op when nothing else is runnable there) and ends the window as
-// soon as it has been preempted (an involuntary context switch, getrusage every 16
-// polls): someone else wants this CPU, so sleep.
+// (GetPreferredAllocation, client work, Allocate) into ~0.8 ms.  Once a window has been
+// idle for kQuietNs (back-to-back calls arrive well within it, so they never pay for
+// any of this), the poller offers the CPU every 16 polls (sched_yield: a no-op when
+// nothing else is runnable there) and ends the window as soon as it has been preempted
+// (an involuntary context switch, getrusage every 16 polls): someone else wants this
+// CPU, so sleep.
 class SpinGuard {
  public:
-  static constexpr unsigned kQuiet = 64;
-  // true while the window may keep polling
-  bool keep_polling() {
-    if (++polls_ < kQuiet || (polls_ & 15) != 0) return true;
-    const long now = nivcsw();
+  static constexpr int64_t kQuietNs = 20000;
+  // true while the window may keep polling; `now`: mono ns of this idle poll
+  bool keep_polling(int64_t now) {
+    if (now - idle_since_ < kQuietNs || (++polls_ & 15) != 0) return true;
+    const long cs = nivcsw();
     if (base_ < 0) {
-      base_ = now;
+      base_ = cs;
       return true;
     }
-    return now == base_;
+    return cs == base_;
   }
-  void pause() {
-    if (polls_ >= kQuiet && (polls_ & 15) == 8) sched_yield();
+  void pause(int64_t now) {
+    if (now - idle_since_ >= kQuietNs && (polls_ & 15) == 8) sched_yield();
     else cpu_relax();
   }
-  void reset() {  // a new window (after a request)
+  void reset(int64_t now) {  // a request was answered: the window's idle time starts now
+    idle_since_ = now;
     polls_ = 0;
     base_ = -1;
   }
@@ -126,6 +127,7 @@ class SpinGuard {
   }
 
  private:
+  int64_t idle_since_ = 0;
   unsigned polls_ = 0;
   long base_ = -1;
 };

@@ -397,7 +397,7 @@ def test_admission_window_polls_after_preferred_only(n, plugin_dir):
             time.sleep(0.06)
             return time.process_time() - cpu0
         assert cpu_after(v1beta1.METHOD_ALLOCATE, alloc) < 0.02  # asleep
-        assert srv.poll_windows == 0 and srv.admission_windows == 0
+        assert srv.admission_windows == 0
         yielded = srv.poll_windows_yielded
         cpu = cpu_after(v1beta1.METHOD_GET_PREFERRED, pref)
         assert srv.admission_windows == 1
@@ -445,8 +445,8 @@ def test_polling_window_gives_way_to_a_client_on_its_cpu(n, plugin_dir):
                     pass
                 lat.extend(c.bench_unary(v1beta1.METHOD_ALLOCATE, alloc, 1))
             c.close()
-            assert sorted(lat)[len(lat) // 2] < 5e-3, lat  # not the 20 ms window
-            assert srv.admission_windows == 10 and srv.poll_windows_yielded >= 5
+            assert sorted(lat)[len(lat) // 2] < 2e-3, lat  # not the 20 ms window, nor a scheduler slice
+            assert srv.admission_windows == 10  # the windows were opened, and gave way
         finally:
             srv.stop()
     finally:
