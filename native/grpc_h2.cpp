@@ -897,6 +897,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
   const int64_t admission_ns = static_cast<int64_t>(admission_poll_us_) * 1000;
   int64_t spin_until = 0;  // busy-poll window end (mono ns); 0 = closed
   SpinGuard guard;
+  bool polite = false;  // the open window gives way to other threads (see SpinGuard)
   while (!stop_.load(std::memory_order_relaxed)) {
     if (inject_worker_fault_.load(std::memory_order_relaxed)) {
       int armed = 1;
@@ -909,6 +910,8 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
         const int64_t now = mono_ns();
         if (now >= spin_until) {
           spin_until = 0;
+        } else if (!polite) {
+          cpu_relax();
         } else if (!guard.keep_polling(now)) {  // preempted: the CPU is wanted (maybe by the client)
           spin_until = 0;
           poll_windows_yielded_.add();
@@ -1047,8 +1050,13 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
         if (window > 0) {
           const int64_t now = mono_ns();
           spin_until = std::max(spin_until, now + window);
-          guard.reset(now);
           if (admitting && admission_ns > spin_ns) admission_windows_.add();
+          // only a window that reaches past a busy-poll window (an admission window, or
+          // what is left of one) is long enough to keep a client on this CPU waiting for
+          // long; a busy-poll window (tens of us) polls throughout, so a call that comes
+          // after a short client hiccup still finds the worker awake
+          polite = spin_until - now > spin_ns;
+          if (polite) guard.reset(now);
         }
         admitting = false;
       }

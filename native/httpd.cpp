@@ -366,13 +366,12 @@ int HttpServer::start() {
       // connection usually lands while the worker is still polling
       const int64_t spin_ns = static_cast<int64_t>(std::max(0, std::min(cfg_.busy_poll_us, 100000))) * 1000;
       int64_t spin_until = 0;
-      SpinGuard guard;
       while (!stop_.load(std::memory_order_relaxed)) {
         const int n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), spin_until ? 0 : 200);
         const int64_t now = mono_ns();
         if (spin_until) {
-          if (n == 0 && now < spin_until && guard.keep_polling(now)) {
-            guard.pause(now);
+          if (n == 0 && now < spin_until) {
+            cpu_relax();
             continue;
           }
           if (n == 0) spin_until = 0;
@@ -458,7 +457,6 @@ int HttpServer::start() {
             }
             if (spin_ns > 0) {
               spin_until = now + spin_ns;
-              guard.reset(now);
             }
           }
           serve(c);

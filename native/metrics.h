@@ -88,8 +88,8 @@ inline void cpu_relax() {
 #endif
 }
 
-// Busy-poll windows (gRPC and HTTP workers) must never keep a CPU from the thread the
-// worker is waiting for.  When the client runs on the same CPU (the scheduler places a
+// A long polling window (the gRPC admission window after a GetPreferredAllocation) must
+// never keep a CPU from the thread the worker is waiting for.  When the client runs on the same CPU (the scheduler places a
 // woken thread next to its waker), a polling worker and a client that is busy before
 // its next call share that CPU, and the call waits for the window's end or a scheduler
 // slice: on a shared host a 1 ms admission window turned a kubelet-like admission
@@ -98,7 +98,9 @@ inline void cpu_relax() {
 // any of this), the poller offers the CPU every 16 polls (sched_yield: a no-op when
 // nothing else is runnable there) and ends the window as soon as it has been preempted
 // (an involuntary context switch, getrusage every 16 polls): someone else wants this
-// CPU, so sleep.
+// CPU, so sleep.  Short busy-poll windows (tens of us) do not use it: ending them early
+// turned a client's brief hiccup into a cold wake-up of the worker and raised the warm
+// Allocate tail on MI355X (profiles/r3/spin_guard_ab.txt).
 class SpinGuard {
  public:
   static constexpr int64_t kQuietNs = 20000;
