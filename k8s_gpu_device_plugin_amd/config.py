@@ -24,7 +24,7 @@ from .api import v1beta1
 
 STRATEGIES = ("none", "single", "mixed")
 # health.disabledChecks names -> the native HealthCheck bits (native/health.h)
-HEALTH_CHECKS = {"reset": 1, "ecc": 2, "lost": 4, "retiredpages": 8}
+HEALTH_CHECKS = {"reset": 1, "ecc": 2, "lost": 4, "retiredpages": 8, "pcie": 16}
 
 
 def disabled_checks_mask(value: str) -> int:
@@ -39,7 +39,7 @@ def disabled_checks_mask(value: str) -> int:
             mask |= HEALTH_CHECKS[name]
         else:
             raise ConfigError("health.disabledChecks: unknown check %r (want %s or all)"
-                              % (name, ", ".join(["reset", "ecc", "lost", "retiredPages"])))
+                              % (name, ", ".join(["reset", "ecc", "lost", "retiredPages", "pcie"])))
     return mask
 
 
@@ -87,6 +87,10 @@ class HealthConfig:
     # retired + pending HBM pages at which a GPU goes Unhealthy: 0 = the GPU's own RAS
     # threshold when readable (root), -1 = never, N > 0 = N
     badPageThreshold: int = 0
+    # host PCIe link floor: a GPU whose link trained narrower / slower is Unhealthy until it
+    # trains back (0 = no floor; e.g. 16 and 32 for an x16 Gen5 MI355X slot)
+    pcieMinWidth: int = 0
+    pcieMinSpeedGTs: float = 0.0
     # health checks that no longer make a GPU Unhealthy (still logged): comma list or
     # YAML list of reset, ecc, lost, retiredPages, or all (env AMDGPU_DP_DISABLE_HEALTHCHECKS)
     disabledChecks: str = ""
@@ -303,6 +307,8 @@ def validate(cfg: Config) -> Config:
     if cfg.backend not in ("auto", "amdsmi", "fixture"):
         raise ConfigError("backend must be auto|amdsmi|fixture, got %r" % cfg.backend)
     disabled_checks_mask(cfg.health.disabledChecks)
+    if cfg.health.pcieMinWidth < 0 or cfg.health.pcieMinSpeedGTs < 0:
+        raise ConfigError("health.pcieMinWidth / health.pcieMinSpeedGTs must be >= 0 (0 = no floor)")
     if cfg.health.sampleStallS < 0:
         raise ConfigError("health.sampleStallS must be >= 0 (0 = off)")
     if cfg.sharing.replicas < 1:

@@ -70,6 +70,7 @@ class PluginManager:
         self.exporter.set_build_info(build_info_text())
         self.monitor = n.HealthMonitor(self.backend, cfg.health.lostAfterFailures)
         self.monitor.set_disabled_checks(disabled_checks_mask(cfg.health.disabledChecks))
+        self.monitor.set_pcie_floor(int(cfg.health.pcieMinWidth), float(cfg.health.pcieMinSpeedGTs))
         self.events: "queue.Queue[tuple]" = queue.Queue()
         self.plugins: list[AmdDevicePlugin] = []
         self.gpus: list = []

@@ -193,6 +193,8 @@ enum EventKind : int {
   kEvtRetiredPagesExceeded = 10,  // retired + pending pages >= threshold -> Unhealthy
   kEvtRetiredPagesCleared = 11,   // back below the threshold (threshold raised, GPU swapped)
   kEvtLinkQuality = 12,   // an up xGMI link re-trained at another bandwidth (value = Gb/s)
+  kEvtPcieDegraded = 13,  // host PCIe link below the configured floor -> Unhealthy
+  kEvtPcieRestored = 14,  // back at or above it
 };
 
 const char* event_kind_name(int kind);

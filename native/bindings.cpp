@@ -172,6 +172,8 @@ PYBIND11_MODULE(_native, m) {
   m.attr("EVT_DEVICE_RECOVERED") = static_cast<int>(kEvtDeviceRecovered);
   m.attr("EVT_RETIRED_PAGES_EXCEEDED") = static_cast<int>(kEvtRetiredPagesExceeded);
   m.attr("EVT_RETIRED_PAGES_CLEARED") = static_cast<int>(kEvtRetiredPagesCleared);
+  m.attr("EVT_PCIE_DEGRADED") = static_cast<int>(kEvtPcieDegraded);
+  m.attr("EVT_PCIE_RESTORED") = static_cast<int>(kEvtPcieRestored);
   m.attr("EVT_LINK_QUALITY") = static_cast<int>(kEvtLinkQuality);
   m.attr("LINK_INTERNAL") = static_cast<int>(kLinkInternal);
   m.attr("LINK_PCIE") = static_cast<int>(kLinkPcie);
@@ -249,6 +251,7 @@ PYBIND11_MODULE(_native, m) {
       .def("inject_event", &FixtureBackend::inject_event)
       .def("set_fail_discovery", &FixtureBackend::set_fail_discovery)
       .def("set_ecc_uncorrectable", &FixtureBackend::set_ecc_uncorrectable)
+      .def("set_pcie_link", &FixtureBackend::set_pcie_link, py::arg("gpu"), py::arg("width"), py::arg("gts"))
       .def("set_retired_pages", &FixtureBackend::set_retired_pages, py::arg("gpu"), py::arg("reserved"),
            py::arg("pending") = 0)
       .def("set_sample_stall", &FixtureBackend::set_sample_stall, py::call_guard<py::gil_scoped_release>())
@@ -480,6 +483,8 @@ PYBIND11_MODULE(_native, m) {
       .def("attach_tables", &HealthMonitor::attach_tables, py::arg("tables"), py::arg("fast_recover"),
            py::arg("held_unhealthy"), py::call_guard<py::gil_scoped_release>())
       .def("set_bad_page_thresholds", &HealthMonitor::set_bad_page_thresholds)
+      .def("set_pcie_floor", &HealthMonitor::set_pcie_floor, py::arg("min_width"), py::arg("min_gts"),
+           py::call_guard<py::gil_scoped_release>())
       .def("on_sample", &HealthMonitor::on_sample, py::arg("gpu"), py::arg("ok"), py::arg("sample"),
            py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("events_seen", &HealthMonitor::events_seen);

@@ -57,6 +57,8 @@ const char* event_kind_name(int kind) {
     case kEvtRetiredPagesExceeded: return "retired_pages_threshold";
     case kEvtRetiredPagesCleared: return "retired_pages_below_threshold";
     case kEvtLinkQuality: return "xgmi_link_bandwidth_changed";
+    case kEvtPcieDegraded: return "pcie_link_degraded";
+    case kEvtPcieRestored: return "pcie_link_restored";
     default: return "none";
   }
 }

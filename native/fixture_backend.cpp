@@ -64,6 +64,7 @@ void FixtureBackend::add_gpu(const GpuInfo& g) {
   for (int a = 0; a < old.n; ++a)
     for (int b = 0; b < old.n; ++b) topo_.at(a, b) = old.at(a, b);
   ecc_ue_.push_back(0);
+  pcie_.emplace_back(16, 32.0);
   pages_.emplace_back(0, 0);
   present_.push_back(true);
   if (!view_.empty()) view_.clear();  // a changed node: identity until it is discovered again
@@ -83,6 +84,7 @@ void FixtureBackend::clear() {
   gpus_.clear();
   topo_.resize(0);
   ecc_ue_.clear();
+  pcie_.clear();
   pages_.clear();
   present_.clear();
   stalled_.clear();
@@ -126,6 +128,12 @@ void FixtureBackend::set_ecc_uncorrectable(int gpu, int64_t count) {
   std::lock_guard<std::mutex> lk(mu_);
   if (gpu < 0 || gpu >= static_cast<int>(ecc_ue_.size())) throw std::out_of_range("bad gpu");
   ecc_ue_[gpu] = count;
+}
+
+void FixtureBackend::set_pcie_link(int gpu, int width, double gts) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (gpu < 0 || gpu >= static_cast<int>(pcie_.size())) throw std::out_of_range("bad gpu");
+  pcie_[gpu] = {width, gts};
 }
 
 void FixtureBackend::set_retired_pages(int gpu, int64_t reserved, int64_t pending) {
@@ -211,8 +219,8 @@ bool FixtureBackend::sample(int index, GpuSample* s) {
   s->xgmi_link_width = 16;
   s->xgmi_link_speed = 38;
   s->xgmi_error_status = 0;
-  s->pcie_link_width = 16;
-  s->pcie_link_speed_gtps = 32;
+  s->pcie_link_width = pcie_[gpu].first;
+  s->pcie_link_speed_gtps = pcie_[gpu].second;
   s->pcie_replays = 0;
   s->pcie_recoveries = 0;
   for (int peer = 0; peer < topo_.n && s->num_links < kMaxXgmiLinks; ++peer) {

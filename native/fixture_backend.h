@@ -46,6 +46,7 @@ class FixtureBackend : public Backend {
   void set_fail_discovery(bool fail) { fail_discovery_ = fail; }
   void set_ecc_uncorrectable(int gpu, int64_t count);
   void set_retired_pages(int gpu, int64_t reserved, int64_t pending);
+  void set_pcie_link(int gpu, int width, double gts);  // the host link as gpu_metrics reports it
   void set_gpu_present(int gpu, bool present);
   // A wedged driver: sample(gpu) blocks until the stall is lifted (or shutdown), the way
   // an amdsmi call can hang on a GPU that stopped responding.
@@ -64,6 +65,7 @@ class FixtureBackend : public Backend {
   };
   std::vector<Scheduled> scheduled_;
   std::vector<int64_t> ecc_ue_;
+  std::vector<std::pair<int, double>> pcie_;  // (lanes, GT/s) per GPU
   std::vector<std::pair<int64_t, int64_t>> pages_;  // (reserved, pending) per GPU
   std::vector<bool> present_;
   std::vector<bool> stalled_;

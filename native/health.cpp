@@ -1,5 +1,7 @@
 #include "health.h"
 
+#include <cstdio>
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -99,6 +101,8 @@ int check_of(int kind) {
     case kEvtDeviceRecovered: return kCheckLost;
     case kEvtRetiredPagesExceeded:
     case kEvtRetiredPagesCleared: return kCheckRetiredPages;
+    case kEvtPcieDegraded:
+    case kEvtPcieRestored: return kCheckPcie;
     default: return 0;
   }
 }
@@ -106,7 +110,8 @@ int check_of(int kind) {
 
 bool HealthMonitor::healthy_locked(const GpuState& st) const {
   return !(st.resetting && !(disabled_ & kCheckReset)) && !(st.ecc_bad && !(disabled_ & kCheckEcc)) &&
-         !(st.lost && !(disabled_ & kCheckLost)) && !(st.pages_bad && !(disabled_ & kCheckRetiredPages));
+         !(st.lost && !(disabled_ & kCheckLost)) && !(st.pages_bad && !(disabled_ & kCheckRetiredPages)) &&
+         !(st.pcie_bad && !(disabled_ & kCheckPcie));
 }
 
 void HealthMonitor::reconcile_locked(const std::string& key, int kind, const std::string& reason) {
@@ -181,6 +186,12 @@ void HealthMonitor::process(const HwEvent& e) {
     case kEvtRetiredPagesCleared:
       if (!known) return;
       state_[key].pages_bad = e.kind == kEvtRetiredPagesExceeded;
+      reconcile_locked(key, e.kind, why);
+      return;
+    case kEvtPcieDegraded:
+    case kEvtPcieRestored:
+      if (!known) return;
+      state_[key].pcie_bad = e.kind == kEvtPcieDegraded;
       reconcile_locked(key, e.kind, why);
       return;
     case kEvtLinkDown:
@@ -273,6 +284,16 @@ void HealthMonitor::on_sample(int gpu, bool ok, const GpuSample& s) {
           derived.push_back(event(kEvtEccUncorrectable, "uncorrectable ECC count " + std::to_string(st.last_ue) +
                                                             " -> " + std::to_string(s.ecc_uncorrectable)));
         st.last_ue = s.ecc_uncorrectable;
+      }
+      if (pcie_min_width_ > 0 || pcie_min_gts_ > 0) {
+        const bool narrow = pcie_min_width_ > 0 && s.pcie_link_width > 0 && s.pcie_link_width < pcie_min_width_;
+        const bool slow = pcie_min_gts_ > 0 && s.pcie_link_speed_gtps > 0 && s.pcie_link_speed_gtps < pcie_min_gts_;
+        if ((narrow || slow) != st.pcie_bad) {
+          char msg[160];
+          std::snprintf(msg, sizeof(msg), "host PCIe link x%d at %.1f GT/s (floor x%d, %.1f GT/s)",
+                        static_cast<int>(s.pcie_link_width), s.pcie_link_speed_gtps, pcie_min_width_, pcie_min_gts_);
+          derived.push_back(event(narrow || slow ? kEvtPcieDegraded : kEvtPcieRestored, msg));
+        }
       }
       const int thr = st.page_threshold;
       if (s.retired_pages >= 0) {
@@ -375,6 +396,21 @@ void HealthMonitor::set_bad_page_thresholds(std::vector<int> thresholds) {
   std::lock_guard<std::mutex> lk(mu_);
   for (size_t g = 0; g < thresholds.size() && g < table_keys_.size(); ++g)
     if (!table_keys_[g].empty()) state_[table_keys_[g]].page_threshold = thresholds[g];
+}
+
+void HealthMonitor::set_pcie_floor(int min_width, double min_gts) {
+  std::lock_guard<std::mutex> lk(mu_);
+  pcie_min_width_ = std::max(0, min_width);
+  pcie_min_gts_ = std::max(0.0, min_gts);
+  if (pcie_min_width_ > 0 || pcie_min_gts_ > 0) return;  // the next samples re-judge every GPU
+  std::vector<std::string> keys;  // no floor any more: nothing is held for its link
+  for (auto& kv : state_)
+    if (kv.second.pcie_bad) {
+      kv.second.pcie_bad = false;
+      keys.push_back(kv.first);
+    }
+  std::sort(keys.begin(), keys.end());
+  for (const auto& k : keys) reconcile_locked(k, kEvtPcieRestored, "PCIe link floor removed");
 }
 
 void HealthMonitor::set_disabled_checks(int mask) {

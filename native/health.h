@@ -35,7 +35,8 @@ enum HealthCheck : int {
   kCheckEcc = 2,           // uncorrectable ECC count increased
   kCheckLost = 4,          // telemetry failing / device gone
   kCheckRetiredPages = 8,  // retired + pending HBM pages at the threshold
-  kCheckAll = 15,
+  kCheckPcie = 16,         // host PCIe link below health.pcieMinWidth / pcieMinSpeedGTs (opt-in)
+  kCheckAll = 31,
 };
 
 struct HealthUpdate {
@@ -93,6 +94,9 @@ class HealthMonitor {
   // Per-GPU retired-page limits (index = table index of the GPU, as in set_gpus; <= 0
   // disables the check for that GPU).
   void set_bad_page_thresholds(std::vector<int> thresholds);
+  // Host PCIe link floor (0 = no floor): a GPU whose link trained narrower or slower is
+  // Unhealthy until it trains back (a failing riser or retimer halves host bandwidth).
+  void set_pcie_floor(int min_width, double min_gts);
   // Identities the monitor holds state for that are unhealthy (advertised or not).
   std::vector<std::string> unhealthy_keys() const;
   // Bitmask of HealthCheck values to ignore; re-evaluates every GPU (a GPU held only by a
@@ -106,6 +110,7 @@ class HealthMonitor {
     bool ecc_bad = false;
     bool lost = false;
     bool pages_bad = false;  // retired + pending pages at/over the threshold (not cleared by a reset)
+    bool pcie_bad = false;   // host PCIe link trained below the configured floor
     int failures = 0;
     int64_t last_ue = -1;
     bool reported_healthy = true;
@@ -140,6 +145,8 @@ class HealthMonitor {
   std::vector<std::shared_ptr<DeviceTable>> fast_tables_;
   bool fast_recover_ = false;
   int disabled_ = 0;  // HealthCheck bits
+  int pcie_min_width_ = 0;
+  double pcie_min_gts_ = 0;
   std::thread thread_;
   std::atomic<bool> running_{false};
   bool stop_ = false;

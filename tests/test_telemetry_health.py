@@ -128,7 +128,7 @@ def test_disabled_health_checks(n):
     """health.disabledChecks: an ignored condition is logged, not acted on; turning a
     check off releases a GPU that only it held, turning it back on re-applies it."""
     from k8s_gpu_device_plugin_amd.config import ConfigError, disabled_checks_mask
-    assert disabled_checks_mask("ecc, retiredPages") == 2 | 8 and disabled_checks_mask("all") == 15
+    assert disabled_checks_mask("ecc, retiredPages") == 2 | 8 and disabled_checks_mask("all") == 31
     assert disabled_checks_mask("") == 0
     with pytest.raises(ConfigError):
         disabled_checks_mask("xid")
@@ -156,7 +156,7 @@ def test_disabled_checks_config(make_cfg):
     cfg = config.validate(config.from_dict({"health": {"disabledChecks": ["ecc", "lost"]}}))
     assert config.disabled_checks_mask(cfg.health.disabledChecks) == 2 | 4
     cfg = config.apply_env(config.Config(), {"AMDGPU_DP_DISABLE_HEALTHCHECKS": "all"})
-    assert config.disabled_checks_mask(cfg.health.disabledChecks) == 15
+    assert config.disabled_checks_mask(cfg.health.disabledChecks) == 31
     with pytest.raises(config.ConfigError):
         config.validate(config.from_dict({"health": {"disabledChecks": "ecc,xids"}}))
 
@@ -549,3 +549,66 @@ def test_link_bandwidth_first_reading_and_retrain(n):
     m.on_sample(1, True, be.sample(1))
     q = [u for u in m.pop(100) if u.kind == n.EVT_LINK_QUALITY]
     assert len(q) == 1 and q[0].link_gbps == 304.0 and "re-trained" in q[0].reason
+
+
+def test_pcie_floor_state_machine(n):
+    """health.pcieMinWidth / pcieMinSpeedGTs: a host link that trained narrower or slower
+    latches the GPU Unhealthy until it trains back; no floor, no check; the check can be
+    disabled (still logged) and removing the floor releases a held GPU."""
+    be = fixtures.build_backend("2gpu_spx")
+    m = n.HealthMonitor(be, 3)
+    m.set_gpu_count(2)
+
+    def health_updates():
+        return [(x.gpu, x.healthy, x.kind) for x in m.pop(100)
+                if x.kind not in (n.EVT_LINK_QUALITY, n.EVT_LINK_UP, n.EVT_LINK_DOWN)]
+    be.set_pcie_link(1, 8, 32.0)
+    for g in (0, 1):
+        m.on_sample(g, True, be.sample(g))
+    assert health_updates() == [] and m.gpu_healthy(1)  # no floor configured
+    m.set_pcie_floor(16, 32.0)
+    m.on_sample(1, True, be.sample(1))
+    u = m.pop(100)
+    assert [(x.gpu, x.healthy, x.kind) for x in u] == [(1, 0, n.EVT_PCIE_DEGRADED)] and "x8" in u[0].reason
+    m.on_sample(1, True, be.sample(1))
+    assert m.pop(50) == [] and not m.gpu_healthy(1)  # latched, reported once
+    be.set_pcie_link(1, 16, 16.0)  # full width, but Gen4
+    m.on_sample(1, True, be.sample(1))
+    assert m.pop(50) == [] and not m.gpu_healthy(1)
+    be.set_pcie_link(1, 16, 32.0)
+    m.on_sample(1, True, be.sample(1))
+    assert health_updates() == [(1, 1, n.EVT_PCIE_RESTORED)]
+    # disabled: tracked and logged, never Unhealthy
+    m.set_disabled_checks(16)
+    be.set_pcie_link(0, 4, 32.0)
+    m.on_sample(0, True, be.sample(0))
+    u = m.pop(50)
+    assert m.gpu_healthy(0) and u and "disabled" in u[0].reason
+    m.set_disabled_checks(0)
+    assert not m.gpu_healthy(0)
+    m.pop(50)
+    m.set_pcie_floor(0, 0.0)  # the floor removed: the held GPU is released at once
+    assert m.gpu_healthy(0) and [(x.gpu, x.healthy) for x in m.pop(50)] == [(0, 1)]
+
+
+def test_pcie_floor_from_config(make_cfg, plugin_dir):
+    """The manager applies health.pcieMinWidth: a GPU whose host link drops to x8 is
+    advertised Unhealthy, and Healthy again when it trains back to x16."""
+    from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import KubeletStub
+    from k8s_gpu_device_plugin_amd.plugin.manager import PluginManager
+    be = fixtures.build_backend("2gpu_spx")
+    with KubeletStub(plugin_dir) as k:
+        m = PluginManager(make_cfg(health={"pcieMinWidth": 16}, telemetry={"intervalMs": 30}), backend=be)
+        t = m.start_background()
+        try:
+            w = k.watch(k.wait_for_registrations(1)[0].endpoint)
+            w.next()
+            be.set_pcie_link(0, 8, 32.0)
+            _, devs = w.next(timeout=5)
+            assert [h for _, h, _ in devs] == ["Unhealthy", "Healthy"]
+            be.set_pcie_link(0, 16, 32.0)
+            _, devs = w.next(timeout=5)
+            assert [h for _, h, _ in devs] == ["Healthy", "Healthy"]
+        finally:
+            m.stop()
+            t.join(10)
