@@ -291,6 +291,27 @@ def test_amdsmi_health_monitor_runs_and_stops(n, amdsmi_backend):
     assert [u for u in mon.pop(10) if u.healthy == 0] == []
 
 
+def test_pcie_floor_on_the_real_link(n, amdsmi_backend):
+    """health.pcieMinWidth on real gpu_metrics: the box's x16 Gen5 link passes a 16 /
+    32 GT/s floor and fails a floor above it (then passes again once the floor is met)."""
+    gpus, _ = amdsmi_backend.discover()
+    s = amdsmi_backend.sample(0)
+    if s.pcie_link_width <= 0:
+        pytest.skip("gpu_metrics reports no PCIe link width on this box")
+    mon = n.HealthMonitor(amdsmi_backend, 3)
+    mon.set_gpu_count(len(gpus))
+    mon.set_pcie_floor(int(s.pcie_link_width), float(s.pcie_link_speed_gtps))
+    mon.on_sample(0, True, amdsmi_backend.sample(0))
+    assert mon.gpu_healthy(0)
+    mon.set_pcie_floor(int(s.pcie_link_width) * 2, 0.0)
+    mon.on_sample(0, True, amdsmi_backend.sample(0))
+    assert not mon.gpu_healthy(0)
+    assert any(u.kind == n.EVT_PCIE_DEGRADED for u in mon.pop(50))
+    mon.set_pcie_floor(int(s.pcie_link_width), 0.0)
+    mon.on_sample(0, True, amdsmi_backend.sample(0))
+    assert mon.gpu_healthy(0)
+
+
 def test_amdsmi_inventory_signature_is_stable(amdsmi_backend):
     from k8s_gpu_device_plugin_amd.plugin.manager import inventory_signature
     a = inventory_signature(amdsmi_backend.discover()[0])
