@@ -117,12 +117,12 @@ def test_random_fault_mix_converges(make_cfg, plugin_dir, tmp_path, seed, fixtur
     cfg = make_cfg(fixture=fixture, migStrategy=strategy, grpc={"server": server}, telemetry={"intervalMs": 30},
                    rediscoverIntervalS=0.2, retrySeconds=0.2, devices=devices,
                    podResources={"enabled": True, "socket": podsock, "intervalS": 0.05},
-                   health={"lostAfterFailures": 2, "sampleStallS": 0.3, "badPageThreshold": 10})
+                   health={"lostAfterFailures": 2, "sampleStallS": 0.3, "badPageThreshold": 10, "pcieMinWidth": 16})
     orig, _ = be.discover()  # untouched descriptions, to undo partition-mode changes
     resetting, present, server_faults = set(), set(range(NGPU)), 0
     links = {}  # (a, b) -> (up, gbps) for the links chaos has touched
     ecc = [0] * NGPU
-    stalled, pages_high, remoded = set(), set(), set()
+    stalled, pages_high, remoded, pcie_low = set(), set(), set(), set()
     with KubeletStub(plugin_dir) as k:
         m = PluginManager(cfg, backend=be)
         t = m.start_background()
@@ -136,7 +136,7 @@ def test_random_fault_mix_converges(make_cfg, plugin_dir, tmp_path, seed, fixtur
                 op = rng.choice(["reset", "post_reset", "remove", "restore", "link_down", "link_up", "link_bw",
                                  "api_restart", "kubelet_restart", "server_fault", "ecc", "stall", "unstall",
                                  "pages_high", "pages_low", "discovery_fails", "discovery_ok", "mode_change",
-                                 "mode_restore", "pods", "idle"])
+                                 "mode_restore", "pods", "pcie_low", "pcie_ok", "idle"])
                 g = rng.randrange(NGPU)
                 a, b = sorted(rng.sample(range(NGPU), 2))
                 if op == "reset" and g in present:
@@ -202,6 +202,12 @@ def test_random_fault_mix_converges(make_cfg, plugin_dir, tmp_path, seed, fixtur
                     if len(cur) >= 2:
                         pods.set_pods([("ns", "p%d" % j, [("c", "amd.com/gpu", rng.sample(cur, 2))])
                                        for j in range(rng.randrange(1, 4))])
+                elif op == "pcie_low":  # the host link trains at x8: below the x16 floor
+                    be.set_pcie_link(g, 8, 32.0)
+                    pcie_low.add(g)
+                elif op == "pcie_ok" and g in pcie_low:
+                    be.set_pcie_link(g, 16, 32.0)
+                    pcie_low.discard(g)
                 elif op == "mode_restore" and g in remoded and len(present) == NGPU:
                     be.replace_gpu(g, orig[g])
                     remoded.discard(g)
@@ -216,6 +222,8 @@ def test_random_fault_mix_converges(make_cfg, plugin_dir, tmp_path, seed, fixtur
                 be.set_sample_stall(g, False)
             for g in pages_high:
                 be.set_retired_pages(g, 0, 0)
+            for g in pcie_low:
+                be.set_pcie_link(g, 16, 32.0)
             for g in range(NGPU):
                 if g not in present:
                     be.set_gpu_present(g, True)
