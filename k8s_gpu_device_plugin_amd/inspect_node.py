@@ -7,7 +7,9 @@ strategy, device map and native allocator as the daemon (same config file and fl
 and prints one JSON document:
 
 * ``gpus``: each physical GPU (index, UUID, BDF, product, gfx target, partition modes,
-  NUMA node, partitions with their render nodes, driver / VBIOS versions);
+  NUMA node, partitions with their render nodes, driver / VBIOS versions) and one
+  telemetry reading of it (power, hotspot temperature, ECC, retired pages, PCIe and
+  xGMI link width / rate);
 * ``resources``: each advertised resource name with its device IDs and health;
 * ``xgmi``: every GPU pair's link (type, up, trained bandwidth, amdsmi weight, hops);
 * ``placement``: per resource and request size, the devices GetPreferredAllocation
@@ -21,6 +23,20 @@ from __future__ import annotations
 import json
 
 LINK_TYPES = {0: "internal", 1: "pcie", 2: "xgmi", 3: "n/a", 4: "unknown"}
+
+
+def _sample(backend, index: int) -> dict:
+    """One telemetry reading of the GPU (what the health checks look at), -1 = unknown."""
+    try:
+        s = backend.sample(index)
+    except Exception as e:  # a GPU that cannot be read is worth showing as such
+        return {"error": str(e)}
+    if s is None or not s.ok:
+        return {"ok": False}
+    return {"ok": True, "power_w": s.power_w, "temp_hotspot_c": s.temp_hotspot_c,
+            "ecc_uncorrectable": s.ecc_uncorrectable, "retired_pages": s.retired_pages,
+            "pcie_link_width": s.pcie_link_width, "pcie_link_speed_gtps": s.pcie_link_speed_gtps,
+            "xgmi_link_width": s.xgmi_link_width, "xgmi_link_speed_gbps": s.xgmi_link_speed}
 
 
 def inspect(cfg, sizes=None) -> dict:
@@ -44,7 +60,8 @@ def inspect(cfg, sizes=None) -> dict:
                 "xgmi_links": g.num_xgmi_links, "oam_id": g.oam_id, "device_id": "%04x" % g.device_id,
                 "driver_version": g.driver_version, "vbios_version": g.vbios_version,
                 "partitions": [{"index": p.index, "id": p.id, "render_minor": p.render_minor, "hip_id": p.hip_id}
-                               for p in g.partitions]})
+                               for p in g.partitions],
+                "now": _sample(m.backend, g.index)})
         resources, placement = {}, {}
         for p in m.plugins:
             ids = list(p.table.ids())

@@ -162,6 +162,7 @@ def test_inspect_prints_the_node_and_its_placements(tmp_path):
     assert out.returncode == 0, out.stderr
     d = _json.loads(out.stdout)
     assert len(d["gpus"]) == 8 and all(len(g["partitions"]) == 8 for g in d["gpus"])
+    assert all(g["now"]["ok"] and g["now"]["pcie_link_width"] == 16 for g in d["gpus"])
     assert len(d["resources"]["amd.com/gpu"]) == 64
     assert len(d["xgmi"]) == 28 and all(x["type"] == "xgmi" and x["up"] for x in d["xgmi"])
     eight = d["placement"]["amd.com/gpu"]["8"]

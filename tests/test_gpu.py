@@ -202,6 +202,7 @@ def test_inspect_on_mi355x(make_cfg):
     from k8s_gpu_device_plugin_amd.inspect_node import inspect
     d = inspect(make_cfg(backend="amdsmi", migStrategy="single"), [1])
     assert d["gpus"] and d["gpus"][0]["gfx"] == "gfx950" and d["gpus"][0]["partitions"]
+    assert d["gpus"][0]["now"]["ok"] and d["gpus"][0]["now"]["power_w"] > 0
     ids = [x["id"] for x in d["resources"]["amd.com/gpu"]]
     assert d["placement"]["amd.com/gpu"]["1"][0] in ids
     print("inspect", json.dumps(d)[:600])
