@@ -455,9 +455,7 @@ int HttpServer::start() {
                 break;
               }
             }
-            if (spin_ns > 0) {
-              spin_until = now + spin_ns;
-            }
+            if (spin_ns > 0) spin_until = now + spin_ns;
           }
           serve(c);
           if (!c->out.empty() || (evs[i].events & EPOLLOUT)) {
