@@ -173,7 +173,9 @@ class PluginManager:
                     fn(*state)
                 except Exception as e:  # pragma: no cover - a listener must not stop the manager
                     log.error("readiness listener failed: %s", e)
-        (log.info if state[0] else log.warning)("readiness: %s", "ready" if state[0] else state[1])
+        # an orderly stop is not a fault: only a running (or fatal) manager warns
+        quiet = state[0] or (not self._running.is_set() and not self.fatal_error)
+        (log.info if quiet else log.warning)("readiness: %s", "ready" if state[0] else state[1])
 
     @property
     def running(self) -> bool:
