@@ -212,3 +212,24 @@ def test_stop_leaves_a_newer_instances_socket_alone(make_cfg, plugin_dir, server
         assert not os.path.exists(sock)
         m.exporter.stop()
         m.monitor.stop()
+
+
+def test_crash_accounting_matches_the_reference_serve_loop(plugin_dir, monkeypatch):
+    """``plugin/plugin.go:107-129``: each crash within an hour of the previous one adds
+    one; the 6th such crash is fatal; a crash more than an hour after the previous one
+    starts the count again from 0."""
+    from k8s_gpu_device_plugin_amd.plugin import plugin as plugin_mod
+    now = [1000.0]
+    monkeypatch.setattr(plugin_mod.time, "monotonic", lambda: now[0])
+    p, _ = _plugin(plugin_dir, "native")
+    for i in range(5):
+        now[0] += 60
+        assert not p._note_crash("test"), i
+    now[0] += plugin_mod.SERVE_CRASH_WINDOW_S + 1  # quiet for over an hour: count resets
+    assert not p._note_crash("test") and p._crashes == 0
+    for i in range(5):
+        now[0] += 60
+        assert not p._note_crash("test"), i
+    now[0] += 60
+    assert p._note_crash("test")  # 6th crash within the hour
+    assert p.fatal_error and "repeatedly crashed" in p.fatal_error
