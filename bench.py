@@ -25,7 +25,10 @@ each rank validates its GPU and its allocation: the gfx950 canary (HBM pattern +
 exactness/throughput) passes on the rank's device, in a child process that exits before
 the rank loads torch or joins the RCCL group, and the returned render node exists.  The
 run fails unless WORLD_SIZE == --gpus == the number of devices the daemon advertised
-(one kubelet-client rank per advertised GPU; rank r allocates device r).
+(one kubelet-client rank per advertised GPU).  Rank r allocates the device whose host HIP
+ordinals (``hip_ids`` of ``amdgpu_partition_info``, from amdsmi's enumeration info) hold
+its LOCAL_RANK, so the canary, ``torch.cuda.set_device(local_rank)`` and the allocation
+name the same GPU even where the HIP runtime's numbering differs from BDF order.
 
 Speed-of-light references, measured untimed in the same run: ``uds_roundtrip_floor_p50_us``
 (the same unix-socket exchange between two threads, no protocol work, sleeping server
@@ -152,6 +155,27 @@ def _allocator_probe(n) -> float:
     return round(_pct(lat[200:], 0.5) * 1e6, 2)
 
 
+def device_for_rank(metrics_text: str, ids, resource: str, local_rank: int, rank: int):
+    """The advertised device whose host HIP ordinals include ``local_rank`` (from the
+    daemon's ``amdgpu_partition_info{device_id, resource, hip_ids}``); ``(device, hip_ids,
+    how)``.  Falls back to enumeration order (``ids[rank]``) only when the daemon reports
+    no HIP ordinals."""
+    from prometheus_client.parser import text_string_to_metric_families
+    hips = {}
+    for fam in text_string_to_metric_families(metrics_text):
+        if fam.name != "amdgpu_partition_info":
+            continue
+        for smp in fam.samples:
+            if smp.labels.get("resource") == resource and smp.labels.get("hip_ids"):
+                hips[smp.labels["device_id"]] = [int(x) for x in smp.labels["hip_ids"].split(",")]
+    mine = [d for d in ids if local_rank in hips.get(d, [])]
+    if len(mine) == 1:
+        return mine[0], hips[mine[0]], "hip_id"
+    if hips:
+        raise RuntimeError("no single advertised device holds HIP ordinal %d: %s" % (local_rank, hips))
+    return ids[rank], [], "enumeration order"
+
+
 def resolve_backend(n, requested: str = "auto") -> str:
     """amdsmi when asked for, or when auto and amdsmi sees a GPU; else the fixture node
     model (CPU runs, and multi-rank rehearsals on a box with fewer GPUs than ranks)."""
@@ -161,7 +185,7 @@ def resolve_backend(n, requested: str = "auto") -> str:
 
 
 def start_daemon(n_gpus: int, grpc_server: str, workdir: str, profile_dir: str = "", busy_poll_us=None,
-                 admission_poll_us=None, overrides=None, backend: str = "auto"):
+                 admission_poll_us=None, overrides=None, backend: str = "auto", fixture: str = ""):
     """Rank 0: kubelet stub + plugin daemon subprocess.  Must run before GPU init.
     ``overrides``: config sections merged over the bench's own (probes, A/B runs)."""
     import yaml
@@ -179,7 +203,7 @@ def start_daemon(n_gpus: int, grpc_server: str, workdir: str, profile_dir: str =
     # one server worker per client connection: every rank holds two kubelet-side
     # connections (compiled h2 + grpcio) and SCRAPE_CONNS scrapers
     cfg = {"webListenAddress": "127.0.0.1:%d" % port, "migStrategy": "none", "backend": backend,
-           "fixture": "%dgpu_spx" % n_gpus, "devices": "0-%d" % (n_gpus - 1), "pluginDir": plugin_dir,
+           "fixture": fixture or "%dgpu_spx" % n_gpus, "devices": "0-%d" % (n_gpus - 1), "pluginDir": plugin_dir,
            "log": {"level": "info", "fileDir": ""},
            "http": {"accessLog": False, "threads": max(4, SCRAPE_CONNS * n_gpus)},
            "telemetry": {"intervalMs": 1000},
@@ -222,6 +246,7 @@ def main() -> int:
     ap.add_argument("--profile-dir", default="", help="run the daemon with benchmark: true, profiles here")
     ap.add_argument("--backend", choices=["auto", "amdsmi", "fixture"], default="auto",
                     help="daemon backend (auto: amdsmi when it sees a GPU); the canary runs only on amdsmi")
+    ap.add_argument("--fixture", default="", help="fixture node model of a fixture daemon (default: <N>gpu_spx)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -248,7 +273,7 @@ def main() -> int:
         os.makedirs(workdir)
         proc, kubelet, port, reg, backend = start_daemon(n_gpus, args.grpc_server, workdir, args.profile_dir,
                                                          args.busy_poll_us, args.admission_poll_us,
-                                                         backend=args.backend)
+                                                         backend=args.backend, fixture=args.fixture)
         info = {"port": port, "endpoint": reg.endpoint, "resource": reg.resource_name, "backend": backend,
                 "plugin_dir": os.path.join(workdir, "device-plugins")}
 
@@ -294,7 +319,13 @@ def main() -> int:
     if len(ids) != n_gpus:
         raise RuntimeError("the plugin advertised %d device(s) of %s, --gpus is %d" % (len(ids), info["resource"],
                                                                                      n_gpus))
-    my_id = ids[rank]
+    conn = http.client.HTTPConnection("127.0.0.1", info["port"], timeout=10)
+    conn.request("GET", "/metrics")
+    body = conn.getresponse().read()
+    if b"amdgpu_info{" not in body:
+        raise RuntimeError("/metrics lacks the GPU inventory")
+    # the device of this rank's GPU (HIP ordinal local_rank), not the rank-th in BDF order
+    my_id, my_hips, mapped_by = device_for_rank(body.decode(), ids, info["resource"], local_rank, rank)
     alloc_req = v1beta1.AllocateRequest(container_requests=[
         v1beta1.ContainerAllocateRequest(devices_ids=[my_id])]).SerializeToString()
     pref_req = v1beta1.PreferredAllocationRequest(container_requests=[
@@ -311,7 +342,6 @@ def main() -> int:
         if missing:
             raise RuntimeError("allocated device nodes missing: %s" % missing)
 
-    conn = http.client.HTTPConnection("127.0.0.1", info["port"], timeout=10)
     perf = time.perf_counter
 
     def phase_sync():
@@ -343,10 +373,6 @@ def main() -> int:
         s.extend(r["latencies_s"])
         return r["elapsed_s"], r["bytes"] // max(1, r["ok"])
 
-    conn.request("GET", "/metrics")
-    body = conn.getresponse().read()
-    if b"amdgpu_info{" not in body:
-        raise RuntimeError("/metrics lacks the GPU inventory")
     junk = ([], [], [], [], [], [])
     for _ in range(args.warmup):
         step(junk)
@@ -361,7 +387,9 @@ def main() -> int:
     elapsed = perf() - t_start
     mine = {"elapsed": elapsed, "scrape_time": scrape_time, "alloc": rec[0], "pref": rec[1], "scrape": rec[2],
             "alloc_native": rec[3], "pref_native": rec[4], "alloc_tail": _tail_stats(rec[5]),
-            "canary": canary_res, "body": body_len}
+            "canary": canary_res, "body": body_len,
+            "device": {"rank": rank, "local_rank": local_rank, "device_id": my_id, "hip_ids": my_hips,
+                       "mapped_by": mapped_by}}
     # Untimed speed-of-light reference: the same send/epoll_wait/recv/send/recv exchange
     # between two threads with no HTTP/2, HPACK or protobuf work (sizes ~ this Allocate's).
     alloc_resp_len = len(alloc_raw(alloc_req))
@@ -418,7 +446,9 @@ def main() -> int:
             "metric": METRIC, "value": round(p50, 2), "unit": "us (Allocate p50, compiled h2 client; lower is better)",
             "n_gpus": n_gpus, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(t_max / args.steps * 1e3, 3), "higher_is_better": False, "scaling": "weak",
-            "vs_baseline": None, "dtype": "bf16",
+            # a control-plane workload: no tensor arithmetic on the timed path (the gfx950
+            # canary's bf16/MX-fp8/fp4 checks run untimed, see "canary")
+            "vs_baseline": None, "dtype": "n/a",
             "data": "synthetic kubelet allocation workload (%d Allocate + %d GetPreferredAllocation per client "
                     "per rank per step, %d ms of /metrics scraping on %d connections per rank per step) against "
                     "%s-discovered devices" % (ALLOCS, PREFS, SCRAPE_S * 1e3, SCRAPE_CONNS, info["backend"]),
@@ -436,6 +466,7 @@ def main() -> int:
             "allocate_server_mean_us": (round(gathered[0]["server_allocate_mean_s"] * 1e6, 3)
                                         if gathered[0].get("server_allocate_mean_s") else None),
             "advertised_devices": len(ids), "world_size": world,
+            "rank_devices": [g["device"] for g in gathered],
             "dist_backend": (dist.get_backend() if world > 1 else None),
             "uds_roundtrip_floor_p50_us": round(gathered[0]["uds_floor_p50"] * 1e6, 2),
             "uds_roundtrip_floor_spin_p50_us": round(gathered[0]["uds_floor_spin_p50"] * 1e6, 2),

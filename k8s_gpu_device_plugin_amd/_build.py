@@ -34,6 +34,8 @@ OFFLOAD_ARCH = "gfx950"
 
 CORE_SOURCES = [
     "common.cpp",
+    "lanes.cpp",
+    "backend.cpp",
     "fixture_backend.cpp",
     "amdsmi_backend.cpp",
     "allocator.cpp",

@@ -307,7 +307,9 @@ def config3():
 
 
 def config4():
-    node = Node("fixture", "8gpu_cpx_nps4", strategy="single")
+    # BASELINE.json names CPX+NPS4; MI355X exposes NPS1|NPS2 (profiles/r4/amdsmi_probe.json),
+    # so the measured mode is CPX+NPS2 (64 devices either way: CPX is 8 partitions per GPU)
+    node = Node("fixture", "8gpu_cpx_nps2", strategy="single")
     try:
         ids = node.ids()
         nat = native.load()
@@ -319,8 +321,9 @@ def config4():
             law.append(time.perf_counter() - t0)
             c.close()
         n_dev = len(v1beta1.ListAndWatchResponse.FromString(body).devices)
-        return {"config": "8xMI355X CPX+NPS4 -> 64 amd.com/gpu sub-devices via ListAndWatch",
-                "backend": "fixture:8gpu_cpx_nps4", "advertised": n_dev, "list_and_watch_bytes": len(body),
+        return {"config": "8xMI355X CPX+NPS2 (BASELINE's CPX+NPS4: NPS4 is not exposed by MI355X) -> 64 "
+                          "amd.com/gpu sub-devices via ListAndWatch",
+                "backend": "fixture:8gpu_cpx_nps2", "advertised": n_dev, "list_and_watch_bytes": len(body),
                 "list_and_watch_first_message": {"p50_us": us(pct(law, 0.5)), "p99_us": us(pct(law, 0.99))},
                 "allocate": rpc_latency(node, v1beta1.METHOD_ALLOCATE, alloc_req(ids[9:10])),
                 "preferred_size8_whole_gpu_pack": rpc_latency(node, v1beta1.METHOD_GET_PREFERRED,
@@ -332,10 +335,10 @@ def config4():
 
 
 def config5(seconds=10.0):
-    node = Node("fixture", "8gpu_cpx_nps4", strategy="single")
+    node = Node("fixture", "8gpu_cpx_nps2", strategy="single")
     try:
         return {"config": "Sustained /metrics at 1k RPS, 8 GPUs x 8 partitions, per-partition telemetry",
-                "backend": "fixture:8gpu_cpx_nps4",
+                "backend": "fixture:8gpu_cpx_nps2",
                 "sustained_1k": scrape(node, 4, seconds, 1000.0),
                 "sustained_1k_gzip": scrape(node, 4, seconds, 1000.0, gzip=True),
                 "max_rate_8conns": scrape(node, 8, 3.0),

@@ -97,6 +97,10 @@ class HealthConfig:
     # a telemetry (amdsmi) call of one GPU in flight for longer than this marks the GPU
     # lost: a wedged driver never returns an error to count (0 = off)
     sampleStallS: float = 10.0
+    # every hardware call of one GPU runs on that GPU's lane and is waited for at most this
+    # long; a discovery gives a GPU that does not answer in time its last known description
+    # (or leaves it out) and reports it on GET /ready
+    discoveryTimeoutS: float = 10.0
 
 
 @dataclass
@@ -311,6 +315,8 @@ def validate(cfg: Config) -> Config:
         raise ConfigError("health.pcieMinWidth / health.pcieMinSpeedGTs must be >= 0 (0 = no floor)")
     if cfg.health.sampleStallS < 0:
         raise ConfigError("health.sampleStallS must be >= 0 (0 = off)")
+    if cfg.health.discoveryTimeoutS <= 0:
+        raise ConfigError("health.discoveryTimeoutS must be > 0")
     if cfg.sharing.replicas < 1:
         raise ConfigError("sharing.replicas must be >= 1")
     if cfg.grpc.server not in ("native", "python"):

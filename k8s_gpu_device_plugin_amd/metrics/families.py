@@ -73,18 +73,32 @@ FAMILIES = (
     Family("amdgpu_xgmi_link_bandwidth_gbps", "gauge", GPU + ("link", "peer"), "exporter",
            "Trained link bandwidth: current per-lane rate x current link width (608 Gb/s on a healthy MI355X link)"),
     # --- per-partition ---
-    Family("amdgpu_partition_info", "gauge", PART, "exporter", "Partition -> device id / resource (value 1)"),
-    Family("amdgpu_partition_gfx_busy_percent", "gauge", PART, "exporter", "Per-XCP compute busy"),
+    Family("amdgpu_partition_info", "gauge", PART + ("hip_ids",), "exporter",
+           "Partition -> device id / resource / the host HIP ordinals it spans (value 1)"),
+    Family("amdgpu_partition_gfx_busy_percent", "gauge", PART + ("source",), "exporter",
+           "Per-partition compute busy; source=partition_metrics (the partition's own metrics table) or "
+           "xcp_stats (the socket blob, fallback)"),
+    Family("amdgpu_partition_profile_supported", "gauge",
+           ("gpu", "profile", "partitions", "memory_partition", "source"), "exporter",
+           "Compute partition profile x memory mode the GPU supports (1); source=driver (the driver's "
+           "profile list, needs root) or current (only the current profile was readable)"),
     Family("amdgpu_partition_vram_used_bytes", "gauge", PART, "exporter", "Per-partition VRAM used"),
     # --- sampler / plugin ---
     Family("amdgpu_telemetry_samples_total", "counter", (), "exporter", "Sampling passes"),
     Family("amdgpu_telemetry_sample_errors_total", "counter", (), "exporter", "Per-GPU sample failures"),
     Family("amdgpu_telemetry_sample_duration_seconds", "histogram", (), "exporter", "One sampling pass"),
     Family("amdgpu_telemetry_last_pass_age_seconds", "gauge", (), "exporter",
-           "Seconds since the sampler last completed a pass (grows while a driver call hangs)"),
+           "Seconds since the sampler last completed a pass (passes go on while one GPU's call hangs: "
+           "it holds that GPU's lane only)"),
+    Family("amdgpu_telemetry_sample_age_seconds", "gauge", ("gpu",), "exporter",
+           "Seconds since the GPU's last successful sample (grows for a GPU whose call hangs; the others "
+           "stay fresh)"),
     Family("amdgpu_telemetry_sample_stalled", "gauge", ("gpu",), "exporter",
-           "1 while a telemetry call of the GPU has been in flight longer than health.sampleStallS "
-           "(the GPU is then marked lost)"),
+           "1 while a hardware call of the GPU (sample, describe, arm) has been in flight longer than "
+           "health.sampleStallS (the GPU is then marked lost)"),
+    Family("amdgpu_telemetry_sample_blocked", "gauge", ("gpu",), "exporter",
+           "1 while the GPU's call is stuck behind another GPU's stalled call (no call has completed "
+           "since: the library serialises devices); the GPU is not marked lost for it"),
     Family("amdgpu_device_plugin_device_health", "gauge", ("resource", "device_id"), "exporter",
            "1 Healthy / 0 Unhealthy per advertised device"),
     Family("amdgpu_device_plugin_rpc_duration_seconds", "histogram", ("resource", "rpc"), "device_table",

@@ -3,9 +3,16 @@
 An MI355X node (OAM, 8 GPUs) is a full xGMI mesh: each GPU has 7 links, one direct
 link to every peer.  Each GPU has 8 XCDs x 32 CUs and 288 GB HBM3E
 (MI355X_MICROARCH.md); compute partitioning splits the XCDs: SPX 1, DPX 2, QPX 4,
-CPX 8 partitions.  Memory partitioning is NPS1 or NPS2 on MI355X; the BASELINE config
-names "CPX+NPS4", so ``8gpu_cpx_nps4`` is modelled too, with its caps declared so the
-plugin's capability checks can be exercised (SURVEY.md §7.5 hard part 3).
+CPX 8 partitions.
+
+Partition model, pinned to what the box reports (``profiles/r4/amdsmi_probe.json``):
+the current profile is SPX with memory caps NPS1|NPS2, and the memory-partition config
+reports the same caps.  The driver's full profile list needs root (NO_PERM for the box's
+user), so the fixture table lists the profiles 8 XCDs form (SPX/DPX/QPX/CPX) with those
+caps.  A GPU may not declare a compute/memory mode outside its profile table:
+``build_backend`` rejects it.  The BASELINE config names "CPX+NPS4", which this hardware
+does not expose; ``8gpu_cpx_nps4`` is kept only as a declared hypothetical (it brings its
+own profile table, marked ``hypothetical``), the measured config is ``8gpu_cpx_nps2``.
 
 A node model is a plain dict (also loadable from JSON/YAML)::
 
@@ -25,6 +32,11 @@ import yaml
 from .. import native
 
 PARTITIONS = {"SPX": 1, "DPX": 2, "TPX": 3, "QPX": 4, "CPX": 8}
+# recorded on the MI355X box (profiles/r4/amdsmi_probe.json): memory caps of the current
+# profile and of the memory-partition config
+MI355X_MEMORY_CAPS = ("NPS1", "NPS2")
+# compute profiles of a gfx950 with 8 XCDs (partitions per GPU)
+MI355X_PROFILES = (("SPX", 1), ("DPX", 2), ("QPX", 4), ("CPX", 8))
 NPS_BITS = {"NPS1": 1, "NPS2": 2, "NPS4": 4, "NPS8": 8}
 MI355X_HBM_BYTES = 288 * 10**9
 MI355X_CUS = 256
@@ -46,15 +58,21 @@ def fixture_uuid(seed: int, gpu: int) -> str:
 
 
 def mi355x_node(num_gpus: int = 8, compute: str = "SPX", memory: str = "NPS1", gpus_per_numa: int = 4,
-                nps_caps=("NPS1", "NPS2"), down_links=(), seed: int = 1, events=(), slow_links=()) -> dict:
-    """slow_links: [(a, b, gbps)] links that trained below the nominal 608 Gb/s."""
+                nps_caps=("NPS1", "NPS2"), down_links=(), seed: int = 1, events=(), slow_links=(),
+                hip_order=None) -> dict:
+    """slow_links: [(a, b, gbps)] links that trained below the nominal 608 Gb/s.
+    hip_order: GPUs (by BDF rank) in the order the HIP runtime numbers them (default: the
+    same order); the runtime's numbering need not follow BDF order on every platform."""
     gpus = []
     for g in range(num_gpus):
         gpus.append({"compute_partition": compute, "memory_partition": memory,
                      "numa_node": g // max(1, gpus_per_numa), "nps_caps": list(nps_caps)})
-    return {"gpus": gpus, "links": {"type": "xgmi", "down": [list(p) for p in down_links],
-                                    "slow": [list(p) for p in slow_links]},
-            "events": list(events), "seed": seed}
+    m = {"gpus": gpus, "links": {"type": "xgmi", "down": [list(p) for p in down_links],
+                                 "slow": [list(p) for p in slow_links]},
+         "events": list(events), "seed": seed}
+    if hip_order is not None:
+        m["hip_order"] = list(hip_order)
+    return m
 
 
 BUILTIN = {
@@ -65,10 +83,18 @@ BUILTIN = {
     "8gpu_dpx_nps2": lambda: mi355x_node(8, "DPX", "NPS2"),
     "8gpu_qpx_nps2": lambda: mi355x_node(8, "QPX", "NPS2"),
     "8gpu_cpx_nps2": lambda: mi355x_node(8, "CPX", "NPS2"),
-    "8gpu_cpx_nps4": lambda: mi355x_node(8, "CPX", "NPS4", nps_caps=("NPS1", "NPS2", "NPS4")),
+    # hypothetical: NPS4 is not exposed by MI355X (caps NPS1|NPS2 on the box); declared
+    # with its own profile table so the 64-device CPX path can also run under "NPS4"
+    "8gpu_cpx_nps4": lambda: dict(mi355x_node(8, "CPX", "NPS4", nps_caps=("NPS1", "NPS2", "NPS4")),
+                                  hypothetical=True,
+                                  profiles=[{"type": t, "partitions": k, "nps": ["NPS1", "NPS2", "NPS4"]}
+                                            for t, k in MI355X_PROFILES]),
     "8gpu_spx_degraded": lambda: mi355x_node(8, down_links=[(0, 5), (2, 3)]),
     # one xGMI link trained at half rate (x8 instead of x16): up, but half the bandwidth
     "8gpu_spx_halfrate": lambda: mi355x_node(8, slow_links=[(0, 1, 304.0)]),
+    # HIP ordinals permuted against BDF order (bench.py maps ranks by HIP ordinal)
+    "2gpu_spx_hip_swapped": lambda: mi355x_node(2, hip_order=[1, 0]),
+    "4gpu_spx_hip_permuted": lambda: mi355x_node(4, hip_order=[2, 0, 3, 1]),
 }
 XGMI_LINK_GBPS = 608.0  # MI355X: 16 lanes x 38 Gb/s per xGMI link (what amdsmi reports)
 
@@ -90,14 +116,15 @@ def load_model(spec) -> dict:
             mode = parts[1].upper()
             nps = parts[2].upper() if len(parts) > 2 else "NPS1"
             if mode in PARTITIONS and nps in NPS_BITS:
-                return mi355x_node(int(parts[0][:-3]), mode, nps,
-                                   nps_caps=tuple(sorted({"NPS1", "NPS2", nps}, key=lambda s: NPS_BITS[s])))
+                return mi355x_node(int(parts[0][:-3]), mode, nps)
         raise ValueError("unknown fixture %r (builtins: %s)" % (spec, ", ".join(sorted(BUILTIN))))
     return m
 
 
-def _partitions(n, gpu_index: int, uuid: str, nparts: int, numa: int, vram: int, first_render: int):
+def _partitions(n, gpu_index: int, uuid: str, nparts: int, numa: int, vram: int, first_render: int,
+                hip_base: int | None = None):
     parts = []
+    hip_base = gpu_index * nparts if hip_base is None else hip_base
     for p in range(nparts):
         pi = n.PartitionInfo()
         pi.gpu = gpu_index
@@ -106,8 +133,8 @@ def _partitions(n, gpu_index: int, uuid: str, nparts: int, numa: int, vram: int,
         pi.id = uuid if nparts == 1 else "%s-xcp%d" % (uuid, p)
         pi.render_minor = first_render + p
         pi.card_minor = first_render - 128 + p
-        pi.hip_id = gpu_index * nparts + p
-        pi.hsa_id = gpu_index * nparts + p
+        pi.hip_id = hip_base + p
+        pi.hsa_id = hip_base + p
         pi.kfd_node = 1 + gpu_index * nparts + p
         pi.numa_node = numa
         pi.vram_bytes = vram // nparts
@@ -122,11 +149,39 @@ def set_gpu_mode(backend, gpu_index: int, compute: str, memory: str = "NPS1", fi
     gpus, _ = backend.discover()
     g = gpus[gpu_index]
     g.compute_partition, g.memory_partition = compute.upper(), memory.upper()
+    if g.supported_profiles:  # the operator can only pick a mode the GPU supports
+        check_mode(gpu_index, g.compute_partition, g.memory_partition, g.supported_profiles)
     g.partitions = _partitions(n, gpu_index, g.uuid, PARTITIONS[g.compute_partition], g.numa_node,
                                g.vram_total_bytes, first_render)
     g.partition_profile, g.profile_partitions = g.compute_partition, PARTITIONS[g.compute_partition]
     g.profile_index = list(PARTITIONS).index(g.compute_partition)
     backend.replace_gpu(gpu_index, g)
+
+
+def profile_table(n, model: dict, g: dict, caps_mask: int):
+    """The partition profiles a fixture GPU supports: the model's own ``profiles`` (a
+    declared hypothetical part), else MI355X's with the GPU's memory caps."""
+    out = []
+    for i, p in enumerate(g.get("profiles") or model.get("profiles") or
+                          [{"type": t, "partitions": k} for t, k in MI355X_PROFILES]):
+        mask = caps_mask
+        if "nps" in p:
+            mask = 0
+            for c in p["nps"]:
+                mask |= NPS_BITS[str(c).upper()]
+        out.append(n.PartitionProfile(str(p["type"]).upper(), int(p["partitions"]), mask, i, "fixture"))
+    return out
+
+
+def check_mode(gi: int, compute: str, memory: str, profiles) -> None:
+    """A GPU cannot be in a compute/memory mode its profile table does not list."""
+    for p in profiles:
+        if p.type == compute and p.nps_caps & NPS_BITS.get(memory, 0):
+            return
+    raise ValueError("fixture GPU %d declares %s+%s, outside its supported profiles (%s); declare a profile "
+                     "table (\"profiles\") to model a hypothetical part" % (
+                         gi, compute, memory, ", ".join("%s[%s]" % (p.type, "|".join(
+                             k for k, b in NPS_BITS.items() if p.nps_caps & b)) for p in profiles)))
 
 
 def build_backend(spec):
@@ -136,6 +191,16 @@ def build_backend(spec):
     seed = int(model.get("seed", 1))
     be = n.FixtureBackend(seed)
     gpus = model.get("gpus", [])
+    nparts_of = [int(g.get("num_partitions", PARTITIONS.get(str(g.get("compute_partition", "SPX")).upper(), 1)))
+                 for g in gpus]
+    order = list(model.get("hip_order") or range(len(gpus)))
+    if sorted(order) != list(range(len(gpus))):
+        raise ValueError("hip_order must be a permutation of the GPU indices: %r" % (order,))
+    hip_base = {}
+    nxt = 0
+    for gi in order:  # the HIP runtime numbers partitions GPU after GPU in this order
+        hip_base[gi] = nxt
+        nxt += nparts_of[gi]
     render = 128
     for gi, g in enumerate(gpus):
         info = n.GpuInfo()
@@ -149,9 +214,12 @@ def build_backend(spec):
         info.compute_partition = str(g.get("compute_partition", "SPX")).upper()
         info.memory_partition = str(g.get("memory_partition", "NPS1")).upper()
         caps = 0
-        for c in g.get("nps_caps", ["NPS1", "NPS2"]):
-            caps |= {1: 1, 2: 2, 4: 4, 8: 8}[NPS_BITS[str(c).upper()]]
+        for c in g.get("nps_caps", list(MI355X_MEMORY_CAPS)):
+            caps |= NPS_BITS[str(c).upper()]
         info.nps_caps = caps
+        info.supported_profiles = profile_table(n, model, g, caps)
+        info.profiles_status = "ok"
+        check_mode(gi, info.compute_partition, info.memory_partition, info.supported_profiles)
         info.num_compute_units = int(g.get("num_cus", MI355X_CUS))
         info.device_id = int(str(g.get("device_id", MI355X_DEVICE_ID)), 0)
         info.oam_id = int(g.get("oam_id", gi))
@@ -164,7 +232,8 @@ def build_backend(spec):
         info.profile_partitions = int(g.get("profile_partitions", nparts))
         info.profile_index = list(PARTITIONS).index(info.compute_partition) if info.compute_partition in PARTITIONS else -1
         info.num_xgmi_links = max(0, len(gpus) - 1)
-        info.partitions = _partitions(n, gi, info.uuid, nparts, info.numa_node, info.vram_total_bytes, render)
+        info.partitions = _partitions(n, gi, info.uuid, nparts, info.numa_node, info.vram_total_bytes, render,
+                                      hip_base[gi])
         render += nparts
         be.add_gpu(info)
     links = model.get("links", {}) or {}
@@ -181,4 +250,5 @@ def build_backend(spec):
         be.schedule_event(float(ev.get("at", 0.0)),
                           n.HwEvent(kind, int(ev.get("gpu", -1)), int(ev.get("partition", -1)),
                                     int(ev.get("peer", -1)), str(ev.get("message", "scripted"))))
+    be.discover()  # usable at once, like an amdsmi session that enumerated at init
     return be

@@ -14,7 +14,17 @@ Defects fixed here:
   D9  a real health producer (native HealthMonitor) feeds ListAndWatch
   D20 a failed load does not end the process; it retries every ``retrySeconds``
 Event sources: native inotify thread (kubelet restarts), native health monitor,
-HTTP ``/restart``, retry timer, ``stop()``.
+HTTP ``/restart``, retry timer, ``stop()``, and the discovery worker.
+
+Discovery never runs on the manager thread (reference ``restartPlugins`` discovers inline,
+``plugin/manager.go:177-194``, so one hung NVML call stops its loop).  A worker thread
+runs ``backend.discover()`` - itself bounded per GPU by the backend's lanes - and posts
+the result back as an event; the manager keeps handling kubelet restarts, ``/restart``,
+health events and server supervision meanwhile.  Reloads are make-before-break: the new
+device tables are built from a finished discovery before the old plugins stop; a
+discovery that fails or stalls leaves the current plugins serving (the reference stops
+them first, defect class D6), and ``GET /ready`` says why.  A kubelet restart re-registers
+the plugins that serve at once and checks the inventory in the background.
 """
 from __future__ import annotations
 
@@ -43,6 +53,8 @@ EV_STOP, EV_RESTART, EV_RETRY, EV_KUBELET, EV_HEALTH, EV_REDISCOVER, EV_VERIFIED
     "stop", "restart", "retry", "kubelet", "health", "rediscover", "verified", "podresources", "prestart_fail")
 EV_METRICS = "metrics"  # state read by /metrics changed off the manager thread (canary results)
 EV_SOCKET_GONE = "socket_gone"  # a *.sock other than kubelet.sock was removed from the plugin dir
+EV_DISCOVERED = "discovered"  # the discovery worker finished: (purpose, gpus, topo, report, error)
+DISCOVERY_RELOAD, DISCOVERY_CHECK = "reload", "check"  # rebuild always / only if the inventory changed
 HEALTH_LOG_LEN = 4096
 SERVER_CHECK_S = 1.0  # gRPC server supervision poll
 
@@ -60,12 +72,86 @@ def build_info_text() -> str:
             % (APP_NAME, VERSION, platform.python_version(), "cxx17"))
 
 
+class DiscoveryStalled(RuntimeError):
+    pass
+
+
+class Discoverer:
+    """One thread that runs ``backend.discover()`` for the manager (GIL released), so the
+    manager thread never waits on the hardware.  Requests made while a discovery runs are
+    merged into one more run (a reload request outranks a check); each finished run is
+    handed to ``post(purpose, gpus, topo, report, error)``."""
+
+    def __init__(self, backend, post) -> None:
+        self._backend = backend
+        self._post = post
+        self._cv = threading.Condition()
+        self._want: str | None = None
+        self._since: float | None = None  # monotonic start of the run in flight
+        self._stop = False
+        self._runs = 0
+        self._thread = threading.Thread(target=self._run, name="discovery", daemon=True)
+        self._thread.start()
+
+    def request(self, purpose: str) -> None:
+        with self._cv:
+            if self._want != DISCOVERY_RELOAD:
+                self._want = purpose
+            self._cv.notify_all()
+
+    def inflight_s(self) -> float | None:
+        """Seconds the current discovery has been running (None: idle)."""
+        since = self._since
+        return None if since is None else time.monotonic() - since
+
+    @property
+    def runs(self) -> int:
+        return self._runs
+
+    def pending(self) -> bool:
+        with self._cv:
+            return self._want is not None or self._since is not None
+
+    def stop(self) -> None:
+        with self._cv:
+            self._stop = True
+            self._cv.notify_all()
+        self._thread.join(1.0)  # a discovery stuck in the driver stays behind (daemon)
+
+    def _run(self) -> None:
+        while True:
+            with self._cv:
+                while self._want is None and not self._stop:
+                    self._cv.wait()
+                if self._stop:
+                    return
+                purpose, self._want = self._want, None
+                self._since = time.monotonic()
+            gpus = topo = report = err = None
+            try:
+                gpus, topo = self._backend.discover()
+                report = self._backend.last_discovery() if hasattr(self._backend, "last_discovery") else None
+            except Exception as e:  # a failed enumeration: the caller keeps what it serves
+                err = e
+            with self._cv:
+                self._since = None
+                self._runs += 1
+                stopping = self._stop
+            if not stopping:
+                self._post(purpose, gpus, topo, report, err)
+
+
 class PluginManager:
     def __init__(self, cfg, ready: CloseOnce | None = None, backend=None) -> None:
         n = native.load()
         self.cfg = cfg
         self.ready = ready if ready is not None else CloseOnce()
         self.backend = backend if backend is not None else make_backend(cfg)
+        # every hardware call runs on its GPU's lane, waited for at most this long; a lane
+        # whose call is older than the stall threshold takes no more work
+        if hasattr(self.backend, "set_call_timeout_ms"):
+            self.backend.set_call_timeout_ms(int(cfg.health.discoveryTimeoutS * 1000))
+            self.backend.set_stall_ms(int(cfg.health.sampleStallS * 1000) if cfg.health.enabled else 0)
         self.exporter = n.Exporter()
         self.exporter.set_build_info(build_info_text())
         self.monitor = n.HealthMonitor(self.backend, cfg.health.lostAfterFailures)
@@ -75,8 +161,14 @@ class PluginManager:
         self.plugins: list[AmdDevicePlugin] = []
         self.gpus: list = []
         self.topology = None
-        self._pinned_devices = None  # identities the `devices` indices named at first discovery
+        # `devices` indices name GPUs by BDF rank among every GPU this process has seen,
+        # so a GPU that drops off the bus does not shift the others into the selection
+        self._seen_bdfs: dict[str, str] = {}  # bdf -> identity
+        self._selection: tuple | None = None
         self.device_map = None
+        self._discoverer: Discoverer | None = None
+        self._discovery_error: str | None = None
+        self._stale: list = []  # [(index, key, reason)] GPUs the last discovery could not reach
         self._retry_timer: threading.Timer | None = None
         self._threads: list[threading.Thread] = []
         self._running = threading.Event()
@@ -154,13 +246,37 @@ class PluginManager:
             return False, "fatal: %s" % self.fatal_error
         if not self._running.is_set():
             return False, "plugin manager not running"
+        bound = float(self.cfg.health.discoveryTimeoutS)
+        inflight = self._discoverer.inflight_s() if self._discoverer is not None else None
+        if inflight is not None and inflight > bound + 1.0:
+            return False, "discovery stalled: running for %.0f s%s" % (inflight, self._stuck_lanes_text())
+        if self._stale:
+            idx, key, why = self._stale[0]
+            more = " (and %d more GPU(s))" % (len(self._stale) - 1) if len(self._stale) > 1 else ""
+            where = "GPU %d" % idx if idx >= 0 else "a GPU"
+            return False, "discovery stalled on %s (%s): %s%s; %s" % (
+                where, key, why, more, "advertising its last known description" if idx >= 0 else "not advertised")
         with_devices = [p for p in self.plugins if len(p)]
+        if self._discovery_error:
+            return False, "discovery failed: %s%s" % (self._discovery_error, "; the current plugins keep serving"
+                                                       if with_devices else "")
         if not with_devices:
             return False, "no devices found" if self.device_map is not None else "plugins not loaded yet"
         missing = [str(p.resource) for p in with_devices if not p.registered]
         if missing:
             return False, "not registered with kubelet: %s" % ", ".join(missing)
         return True, ""
+
+    def _stuck_lanes_text(self) -> str:
+        try:
+            stuck = [(i, k, what, age) for i, k, what, age, _, _ in self.backend.lanes()
+                     if what and age > float(self.cfg.health.sampleStallS or self.cfg.health.discoveryTimeoutS)]
+        except Exception:  # pragma: no cover - every native backend has lanes
+            return ""
+        if not stuck:
+            return ""
+        i, k, what, age = max(stuck, key=lambda x: x[3])
+        return "; GPU %d (%s): %s call in flight for %.0f s" % (i, k, what, age)
 
     def _push_readiness(self) -> None:
         state = self.readiness()
@@ -190,13 +306,22 @@ class PluginManager:
         self._running.set()
         try:
             self._start_watch()
-            try:
-                self.load_plugins()
-                self.start_plugins()
-            except Exception as e:
-                self.counters["load_failures"] += 1
-                log.error("failed to load plugins: %s; retrying in %.0fs", e, self.cfg.retrySeconds)
-                self._arm_retry()
+            self._discoverer = Discoverer(self.backend, lambda *r: self.events.put((EV_DISCOVERED,) + r))
+            self._discoverer.request(DISCOVERY_RELOAD)
+            # the first discovery is normally done in milliseconds: wait for it (bounded) so
+            # plugins are registered when start() hands over to the loop; a stalled one is
+            # applied by the loop whenever it finishes
+            deadline = time.monotonic() + float(self.cfg.health.discoveryTimeoutS) + 1.0
+            while time.monotonic() < deadline:
+                try:
+                    ev = self.events.get(timeout=max(0.0, deadline - time.monotonic()))
+                except queue.Empty:
+                    break
+                if ev[0] == EV_DISCOVERED:
+                    self._handle(ev)
+                    break
+                self.events.put(ev)  # anything else waits for the loop (order kept enough:
+                time.sleep(0.001)    # nothing else is expected before the first discovery)
             self._start_telemetry()
             self.ready.close()
             self._loop()
@@ -241,60 +366,74 @@ class PluginManager:
             if now >= next_check:
                 if not self._check_servers():
                     return
+                # readiness follows plugin state and stalls that no event announces (a
+                # discovery running past its bound, a server that lost its registration)
+                self._push_readiness()
                 next_check = now + SERVER_CHECK_S
             try:
                 ev = self.events.get(timeout=max(0.0, next_check - now))
             except queue.Empty:
                 continue
-            kind = ev[0]
-            if kind == EV_STOP:
+            if ev[0] == EV_STOP:
                 log.info("plugin server stopped")
                 return
-            try:
-                if kind in (EV_RESTART, EV_KUBELET):
-                    if kind == EV_RESTART:
-                        self.counters["restarts_" + ev[1]] = self.counters.get("restarts_" + ev[1], 0) + 1
-                        log.info("restarting plugins (%s)", ev[1])
-                    else:
-                        self.counters["restarts_kubelet"] += 1
-                        log.info("kubelet.sock re-created: kubelet restarted; re-registering")
-                    self._coalesce_restarts()
-                    self.restart_plugins()
-                elif kind == EV_RETRY:
-                    self.counters["restarts_retry"] += 1
-                    self._retry_timer = None
-                    if not self.plugins:
-                        self.load_plugins()
-                    self.start_plugins()
-                elif kind == EV_HEALTH:
-                    self._apply_health(ev[1])
-                elif kind == EV_VERIFIED:
-                    self._apply_verified(*ev[1:])
-                elif kind == EV_PODRES:
-                    self._push_link_pods()  # and _publish_metrics below re-renders the allocation map
-                elif kind == EV_METRICS:
-                    pass  # canary results changed: _publish_metrics below re-renders
-                elif kind == EV_PRESTART_FAIL:
-                    self.counters["prestart_failures"] = self.counters.get("prestart_failures", 0) + 1
-                    self._canary_failed.add((ev[1], ev[2]))  # (identity, partition)
-                    self._set_health(ev[1], ev[2], False, ev[3])
-                elif kind == EV_REDISCOVER:
-                    self._check_inventory()
-                elif kind == EV_SOCKET_GONE:
-                    self._socket_gone(ev[1])
-            except Exception as e:
-                self.counters["load_failures"] += 1
-                log.error("event %s failed: %s; retrying in %.0fs", kind, e, self.cfg.retrySeconds)
-                self._arm_retry()
-            self._publish_metrics()
+            self._handle(ev)
 
-    def _coalesce_restarts(self) -> int:
+    def _handle(self, ev) -> None:
+        kind = ev[0]
+        try:
+            if kind == EV_RESTART:
+                self.counters["restarts_" + ev[1]] = self.counters.get("restarts_" + ev[1], 0) + 1
+                log.info("restarting plugins (%s)", ev[1])
+                kubelet = self._coalesce_restarts()
+                if kubelet:
+                    self._reregister()
+                self._request_discovery(DISCOVERY_RELOAD)
+            elif kind == EV_KUBELET:
+                self.counters["restarts_kubelet"] += 1
+                log.info("kubelet.sock re-created: kubelet restarted; re-registering")
+                self._coalesce_restarts()
+                self._reregister()
+                self._request_discovery(DISCOVERY_CHECK)
+            elif kind == EV_DISCOVERED:
+                self._apply_discovery(*ev[1:])
+            elif kind == EV_RETRY:
+                self.counters["restarts_retry"] += 1
+                self._retry_timer = None
+                if not self.plugins or self._discovery_error:
+                    self._request_discovery(DISCOVERY_RELOAD)
+                else:
+                    self.start_plugins()
+            elif kind == EV_HEALTH:
+                self._apply_health(ev[1])
+            elif kind == EV_VERIFIED:
+                self._apply_verified(*ev[1:])
+            elif kind == EV_PODRES:
+                self._push_link_pods()  # and _publish_metrics below re-renders the allocation map
+            elif kind == EV_METRICS:
+                pass  # canary results changed: _publish_metrics below re-renders
+            elif kind == EV_PRESTART_FAIL:
+                self.counters["prestart_failures"] = self.counters.get("prestart_failures", 0) + 1
+                self._canary_failed.add((ev[1], ev[2]))  # (identity, partition)
+                self._set_health(ev[1], ev[2], False, ev[3])
+            elif kind == EV_REDISCOVER:
+                self._request_discovery(DISCOVERY_CHECK)
+            elif kind == EV_SOCKET_GONE:
+                self._socket_gone(ev[1])
+        except Exception as e:
+            self.counters["load_failures"] += 1
+            log.error("event %s failed: %s; retrying in %.0fs", kind, e, self.cfg.retrySeconds)
+            self._arm_retry()
+        self._publish_metrics()
+
+    def _coalesce_restarts(self) -> bool:
         """Takes the restart requests (``GET /restart``, kubelet re-creations) that are
         already queued behind the one being handled: one reload serves them all, so a
         burst of /restart calls cannot keep the manager reloading (the reference's
         ``Restart()`` sets a flag, which coalesces too).  Every request is still counted;
-        other events keep their order."""
+        other events keep their order.  True when a kubelet restart was among them."""
         n = 0
+        kubelet = False
         with self.events.mutex:  # queue.Queue's own lock: nothing else runs meanwhile
             q = self.events.queue
             keep = collections.deque()
@@ -304,6 +443,7 @@ class PluginManager:
                     key = "restarts_" + ev[1]
                 elif ev[0] == EV_KUBELET:
                     key = "restarts_kubelet"
+                    kubelet = True
                 else:
                     keep.append(ev)
                     continue
@@ -313,7 +453,7 @@ class PluginManager:
         if n:
             self.counters["restarts_coalesced"] = self.counters.get("restarts_coalesced", 0) + n
             log.info("%d more restart request(s) served by this reload", n)
-        return n
+        return kubelet
 
     def _socket_gone(self, name: str) -> None:
         """A plugin's own socket was deleted while it serves (an operator or a cleanup
@@ -331,26 +471,45 @@ class PluginManager:
             self.start_plugins()
 
     # ------------------------------------------------------------ plugins
-    def load_plugins(self) -> None:
-        gpus, topo = self.backend.discover()
-        # the tables' topology spans the whole node: link state and bandwidth are kept for
-        # every pair, also those with an end that `devices` leaves out
-        self._node_index_of = {self._identity(g): g.index for g in gpus}
+    def load_plugins(self, gpus=None, topo=None) -> None:
+        """Builds the plugins for a discovery (``gpus``/``topo``; a synchronous discovery
+        when not given), then replaces the current ones with them.  Everything that can
+        fail - discovery, resources, device map, tables, canaries - happens before the
+        old plugins stop: a failure leaves them serving (make-before-break)."""
+        if gpus is None:
+            gpus, topo = self.backend.discover()
+            self._note_report(self.backend.last_discovery() if hasattr(self.backend, "last_discovery") else None)
+        self._note_seen(gpus)
         node = gpus
-        gpus = self._selected(gpus)
-        self.gpus, self.topology = gpus, topo
-        self.signature = self._signature(node, gpus)
-        resources = new_resources(gpus, self.cfg.strategy, self.cfg.resourcePrefix, self.cfg.resources)
-        self.device_map = build_device_map(gpus, resources, self.cfg.strategy, self.cfg.mountCardNodes,
-                                           self.cfg.sharing.replicas, self.cfg.sharing.renameByDefault)
-        self._key_of = {g.index: self._identity(g) for g in gpus}
-        self._index_of = {k: i for i, k in self._key_of.items()}
+        sel = self._selected(gpus)
+        resources = new_resources(sel, self.cfg.strategy, self.cfg.resourcePrefix, self.cfg.resources)
+        device_map = build_device_map(sel, resources, self.cfg.strategy, self.cfg.mountCardNodes,
+                                      self.cfg.sharing.replicas, self.cfg.sharing.renameByDefault)
+        key_of = {g.index: self._identity(g) for g in sel}
+        index_of = {k: i for i, k in key_of.items()}
         if self.cfg.health.canaryOnStart:
-            failed = self._startup_canary(gpus)
-            self._canary_failed = {(self._key_of[g], p) for g, p in failed}  # fresh verdicts replace older ones
+            failed = self._startup_canary(sel, key_of)
+            canary_failed = {(key_of[g], p) for g, p in failed}  # fresh verdicts replace older ones
         else:
-            failed = {(self._index_of[k], p) for k, p in self._canary_failed if k in self._index_of}
-        plugins = [AmdDevicePlugin(name, devs, topo, self.cfg) for name, devs in self.device_map.items()]
+            canary_failed = self._canary_failed
+            failed = {(index_of[k], p) for k, p in canary_failed if k in index_of}
+        plugins = [AmdDevicePlugin(name, devs, topo, self.cfg) for name, devs in device_map.items()]
+        # built: from here on the new inventory replaces the old one (readers of
+        # self.plugins see the old list, then the new one, never an empty one)
+        for p in self.plugins:
+            try:
+                p.stop()
+            except Exception as e:  # pragma: no cover
+                log.error("failed to stop plugin %s: %s", p.resource, e)
+        self.plugins = plugins
+        self._node_index_of = {self._identity(g): g.index for g in node}
+        self.gpus, self.topology = sel, topo
+        self.signature = self._signature(node, sel)
+        self.device_map = device_map
+        self._key_of, self._index_of = key_of, index_of
+        self._canary_failed = canary_failed
+        gpus = sel
+        self.counters["reloads"] = self.counters.get("reloads", 0) + 1
         for p in plugins:
             p.table.set_recent_allocations(self.recent_allocations)
         if self.cfg.health.canaryOnPreStart:
@@ -371,13 +530,16 @@ class PluginManager:
         self.monitor.set_gpus(keys)
         self.monitor.attach_tables([p.table for p in plugins], not self.cfg.health.canary,
                                    sorted(self._index_of[k] for k in self._held_unhealthy if k in self._index_of))
-        self.plugins = plugins
         n = native.load()
         labels = []
+        hips = {(g.index, p.index): p.hip_id for g in gpus for p in g.partitions}
         for name, devs in self.device_map.items():
             for d in devs:
                 if d.replica <= 0:
-                    labels.append(n.PartitionLabel(d.gpu, d.partition, d.get_uuid(), name))
+                    spans = sorted(h for (gi, pi), h in hips.items()
+                                   if gi == d.gpu and (d.partition < 0 or pi == d.partition) and h >= 0)
+                    labels.append(n.PartitionLabel(d.gpu, d.partition, d.get_uuid(), name,
+                                                   ",".join(str(h) for h in spans)))
         if self.cfg.cdi:
             from ..cdi import build_spec, write_spec
             for name, devs in self.device_map.items():
@@ -441,11 +603,68 @@ class PluginManager:
             except Exception as e:  # pragma: no cover
                 log.error("failed to stop plugin %s: %s", p.resource, e)
 
-    def restart_plugins(self) -> None:
+    def restart_plugins(self, gpus=None, topo=None) -> None:
+        """Reload (make-before-break, see load_plugins) and register the new plugins."""
         self._cancel_retry()
-        self.stop_plugins()
-        self.plugins = []
-        self.load_plugins()
+        self.load_plugins(gpus, topo)
+        self.start_plugins()
+
+    def _request_discovery(self, purpose: str) -> None:
+        if self._discoverer is None:  # not started (direct callers): synchronous
+            gpus, topo = self.backend.discover()
+            self._apply_discovery(purpose, gpus, topo, self.backend.last_discovery()
+                                  if hasattr(self.backend, "last_discovery") else None, None)
+            return
+        self._discoverer.request(purpose)
+
+    def _note_report(self, report) -> None:
+        stale = list(report["stale"]) if report else []
+        # the GPU whose own call is stuck first (behind a library-wide lock the others only
+        # wait for it)
+        stalled = set(self.exporter.stalled_gpus)
+        stale.sort(key=lambda x: (x[0] not in stalled, x[0] < 0, x[0]))
+        for idx, key, why in stale:
+            if (idx, key, why) not in self._stale:
+                log.warning("discovery could not reach GPU %s (%s): %s; %s", idx if idx >= 0 else "?", key, why,
+                            "serving its last known description" if idx >= 0 else "left out")
+        if stale:
+            self.counters["discovery_stale"] = self.counters.get("discovery_stale", 0) + 1
+        elif self._stale:
+            log.info("discovery reaches every GPU again")
+        self._stale = stale
+
+    def _apply_discovery(self, purpose, gpus, topo, report, err) -> None:
+        """A finished discovery (worker thread, via the queue).  Failure: what serves keeps
+        serving.  Success: reload if asked to, or if the inventory changed."""
+        if err is not None:
+            self.counters["load_failures"] += 1
+            self._discovery_error = str(err)
+            log.error("discovery failed: %s; %s, retrying in %.0fs", err,
+                      "the current plugins keep serving" if self.plugins else "nothing advertised yet",
+                      self.cfg.retrySeconds)
+            self._arm_retry()
+            return
+        self._discovery_error = None
+        self._note_report(report)
+        self._note_seen(gpus)
+        changed = self._signature(gpus, self._selected(gpus)) != self.signature
+        if purpose == DISCOVERY_CHECK and self.plugins and not changed:
+            if any(not p.registered for p in self.plugins if len(p)):
+                self.start_plugins()
+            return
+        if purpose == DISCOVERY_CHECK and self.plugins:
+            self.counters["restarts_inventory"] = self.counters.get("restarts_inventory", 0) + 1
+            log.warning("device inventory changed (partition mode or GPU set); re-advertising")
+        self.restart_plugins(gpus, topo)
+
+    def _reregister(self) -> None:
+        """A kubelet restart drops every registration (and kubelet clears the plugin
+        sockets): serve the current plugins on fresh sockets and register them again at
+        once - no discovery on this path, so a wedged GPU cannot delay it."""
+        self._cancel_retry()
+        for p in self.plugins:
+            if len(p):
+                p.stop()
         self.start_plugins()
 
     def _signature(self, node, selected) -> tuple:
@@ -453,21 +672,30 @@ class PluginManager:
         `devices` leaves out still has links in the tables' topology."""
         return inventory_signature(selected), tuple((self._identity(g), g.index) for g in node)
 
+    def _note_seen(self, gpus) -> None:
+        for g in gpus:
+            if g.bdf:
+                self._seen_bdfs[g.bdf.lower()] = self._identity(g)
+
     def _selected(self, gpus) -> list:
-        """The GPUs `devices` selects.  Indices name the enumeration this process saw
-        first and are pinned to those GPUs' identities then: when a GPU later drops off
-        the bus and the others move down an index, the selection keeps the same physical
-        GPUs instead of taking in the next one.  UUIDs and BDFs are matched as given."""
+        """The GPUs `devices` selects.  An index names a GPU by its BDF rank among every
+        GPU this process has seen, not by its position in one enumeration: when a GPU
+        drops off the bus the others keep their index (the selection does not take in
+        the next GPU), and a GPU missing from the first discovery takes its own index when
+        it appears instead of leaving its index to a neighbour for good.  UUIDs and BDFs
+        are matched as given."""
         sel = parse_device_selector(self.cfg.devices)
         if sel is None:
             return list(gpus)
         indices, names = sel
-        if self._pinned_devices is None:
-            self._pinned_devices = {self._identity(g) for g in gpus if g.index in indices}
-            log.info("devices %r selects %s", self.cfg.devices,
-                     ", ".join(sorted(self._pinned_devices | names)) or "nothing yet")
-        return [g for g in gpus if self._identity(g) in self._pinned_devices
-                or (g.uuid or "").lower() in names or (g.bdf or "").lower() in names]
+        rank = {bdf: i for i, bdf in enumerate(sorted(self._seen_bdfs))}
+        out = [g for g in gpus if rank.get((g.bdf or "").lower(), -1) in indices
+               or (g.uuid or "").lower() in names or (g.bdf or "").lower() in names]
+        chosen = tuple(self._identity(g) for g in out)
+        if chosen != self._selection:
+            log.info("devices %r selects %s", self.cfg.devices, ", ".join(chosen) or "nothing (yet)")
+            self._selection = chosen
+        return out
 
     # ------------------------------------------------------------ health
     def _identity(self, g) -> str:
@@ -598,7 +826,7 @@ class PluginManager:
             self._held_unhealthy.discard(key)
         self._set_health(key, u.partition, ok, u.reason + ("" if ok else "; canary failed"))
 
-    def _startup_canary(self, gpus) -> set:
+    def _startup_canary(self, gpus, key_of=None) -> set:
         """Runs the gfx950 canary on every partition (one child process per partition, all
         GPUs in parallel) before the first advertisement; returns failing (gpu, partition)."""
         import concurrent.futures
@@ -608,7 +836,8 @@ class PluginManager:
                 for g in gpus for p in g.partitions]
         failed = set()
         with concurrent.futures.ThreadPoolExecutor(max_workers=max(1, min(8, len(jobs)))) as ex:
-            futs = {ex.submit(self._run_canary, gpu, hw_part, hip): (gpu, part) for gpu, part, hw_part, hip in jobs}
+            futs = {ex.submit(self._run_canary, gpu, hw_part, hip, (key_of or {}).get(gpu)): (gpu, part)
+                    for gpu, part, hw_part, hip in jobs}
             for f in concurrent.futures.as_completed(futs):
                 gpu, part = futs[f]
                 res = f.result()
@@ -622,7 +851,7 @@ class PluginManager:
         with self._canary_lock:  # counters touched from canary pool threads too
             self.counters[key] = self.counters.get(key, 0) + n
 
-    def _run_canary(self, gpu: int, hw_part: int, hip: int) -> dict:
+    def _run_canary(self, gpu: int, hw_part: int, hip: int, owner: str | None = None) -> dict:
         """One isolated canary run on HIP device ``hip`` (GPU ``gpu``, hardware partition
         ``hw_part``): applies the configured performance floors and records the result for
         /metrics.  Thread-safe; runs on canary pool threads."""
@@ -642,7 +871,7 @@ class PluginManager:
         with self._canary_lock:
             self.counters["canary_runs"] = self.counters.get("canary_runs", 0) + 1
             self.canary_results[(gpu, hw_part)] = (time.time(), res)
-            self._canary_owner[(gpu, hw_part)] = self._key_of.get(gpu, "#%d" % gpu)
+            self._canary_owner[(gpu, hw_part)] = owner or self._key_of.get(gpu, "#%d" % gpu)
         self.events.put((EV_METRICS,))
         return res
 
@@ -684,11 +913,9 @@ class PluginManager:
     def _check_inventory(self) -> None:
         """Periodic re-discovery: a compute/memory partition-mode change (SPX->CPX, ...) or a
         GPU appearing/disappearing changes the device set; re-advertise when it does."""
-        node = self.backend.discover()[0]
-        if self._signature(node, self._selected(node)) != getattr(self, "signature", None):
-            self.counters["restarts_inventory"] = self.counters.get("restarts_inventory", 0) + 1
-            log.warning("device inventory changed (partition mode or GPU set); re-advertising")
-            self.restart_plugins()
+        gpus, topo = self.backend.discover()
+        self._apply_discovery(DISCOVERY_CHECK, gpus, topo, self.backend.last_discovery()
+                              if hasattr(self.backend, "last_discovery") else None, None)
 
     def _canary_ok(self, key: str) -> bool:
         gpu = self._index_of.get(key)
@@ -850,6 +1077,8 @@ class PluginManager:
 
     def _shutdown(self) -> None:
         self._cancel_retry()
+        if self._discoverer is not None:
+            self._discoverer.stop()
         if self._verify_pool is not None:
             self._verify_pool.shutdown(wait=False, cancel_futures=True)
         self._stop_flag.set()

@@ -3,13 +3,16 @@
 // Replaces: NVML device queries (reference device/device.go:37-181), NVML MIG
 // enumeration (device/device_map.go:78-98, resource/resources.go:22-51), the
 // sysfs NUMA lookup (device/device.go:69-93) and go-gpuallocator's NVLink graph
-// (plugin/plugin.go:259-264).  Every amdsmi call is serialised behind one mutex
-// (SURVEY.md §7.5 hard part 6) except the blocking event wait.
+// (plugin/plugin.go:259-264).  Every call that talks to one GPU runs on that GPU's lane
+// (lanes.h, backend.cpp: one owner thread per physical GPU, waited for with a bound), so
+// a call wedged in the driver stalls that GPU only; the library session is guarded by a
+// gate that a re-initialisation closes (SURVEY.md §7.5 hard part 6).
 #include <amd_smi/amdsmi.h>
 
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <ctime>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -138,6 +141,17 @@ bool amdsmi_probe_held() {
   return g_probe_ref;
 }
 
+// Enters the library session for a call made off the lanes (enumeration, event wait,
+// disarm); leaves it on scope exit.
+class GateGuard {
+ public:
+  explicit GateGuard(SessionGate& g) : g_(g) { g_.enter(0); }
+  ~GateGuard() { g_.leave(); }
+
+ private:
+  SessionGate& g_;
+};
+
 class AmdSmiBackend : public Backend {
  public:
   AmdSmiBackend() {
@@ -154,73 +168,110 @@ class AmdSmiBackend : public Backend {
   std::string name() const override { return "amdsmi"; }
 
   void shutdown() override {
-    std::lock_guard<std::mutex> lk(mu_);
-    disarm_locked();
-    if (!closed_) {
-      closed_ = true;
+    {
+      std::lock_guard<std::mutex> lk(life_mu_);
+      if (closed_.exchange(true)) return;
+    }
+    evt_live_.store(false);
+    // amdsmi_shut_down only with no call inside the library: a call stuck in a wedged
+    // driver keeps the session (and its reference) for the rest of the process.
+    if (!gate().close(1000)) return;
+    {
+      std::lock_guard<std::mutex> ek(evt_mu_);
+      disarm_locked();
+    }
+    {
       std::lock_guard<std::mutex> ilk(g_init_mu);
       if (--g_init_refs == 0) amdsmi_shut_down();
     }
-  }
-
-  void discover(std::vector<GpuInfo>* gpus, Topology* topo) override {
-    std::lock_guard<std::mutex> lk(mu_);
-    if (closed_) throw std::runtime_error("amdsmi backend is shut down");
-    discover_locked(gpus, topo);
-    // amdsmi enumerates processors once, at amdsmi_init.  After an operator switches a
-    // GPU's compute partition mode (amd-smi set --compute-partition), the cached handle
-    // list no longer matches the mode the GPU reports: re-initialise and enumerate again.
-    bool stale = false;
-    for (const auto& g : *gpus) {
-      const int want = g.profile_partitions > 0 ? g.profile_partitions : partitions_of_mode(g.compute_partition);
-      if (want > 0 && want != static_cast<int>(g.partitions.size())) stale = true;
-    }
-    if (stale && reinit_locked()) discover_locked(gpus, topo);
-    // keep event delivery armed across periodic re-discovery; re-arm only when the
-    // processor set changed (handles from a re-init are new objects)
-    std::vector<amdsmi_processor_handle> flat;
-    for (const auto& hs : procs_) flat.insert(flat.end(), hs.begin(), hs.end());
-    if (armed_ && flat != armed_for_) {
-      disarm_locked();
-      arm_locked();
-    }
+    gate().reopen();  // later calls see another session and leave at once
   }
 
   bool reinit() override {
-    std::lock_guard<std::mutex> lk(mu_);
-    return !closed_ && reinit_locked();
+    if (closed_.load() || !gate().close(call_timeout_ms())) return false;
+    bool ok = false;
+    try {
+      ok = reopen_session();
+    } catch (...) {
+      gate().reopen();
+      throw;
+    }
+    gate().reopen();
+    return ok;
   }
 
-  // Answered from a copy under its own lock: the sampler watchdog asks while an amdsmi
-  // call that hung may be holding mu_.
-  std::string gpu_key(int gpu) const override {
-    std::lock_guard<std::mutex> lk(keys_mu_);
-    return gpu >= 0 && gpu < static_cast<int>(keys_.size()) ? keys_[gpu] : "";
+  int reinit_count() const override { return reinits_.load(); }
+
+  std::vector<CallCost> sample_costs() const override {
+    std::vector<CallCost> out;
+    for (int c = 0; c < kCallCount; ++c) out.push_back({kCallNames[c], cost_ns_[c].load() * 1e-9, cost_n_[c].load()});
+    // how many link samples took the full amdsmi path vs the gpu_metrics blob (counts only)
+    out.push_back({"xgmi_links_full_path", 0.0, link_full_.load()});
+    out.push_back({"xgmi_links_blob_path", 0.0, link_fast_.load()});
+    // partitions whose busy figure came from the partition API vs the socket blob
+    out.push_back({"partition_busy_from_partition_api", 0.0, part_from_api_.load()});
+    out.push_back({"partition_busy_from_socket_blob", 0.0, part_from_blob_.load()});
+    return out;
   }
 
-  int reinit_count() const override {
-    std::lock_guard<std::mutex> lk(mu_);
-    return reinits_;
+  void arm_events() override {
+    arm_wanted_.store(true);
+    arm_on_lanes(inventory());
   }
 
- private:
-  // amdsmi is process-global: only the sole owner may shut it down and start it again.
-  bool reinit_locked() {
-    std::lock_guard<std::mutex> ilk(g_init_mu);
-    if (g_init_refs != 1) return false;
-    const bool was_armed = armed_;
-    disarm_locked();
-    procs_.clear();
-    std::lock_guard<std::mutex> ek(evt_mu_);  // no event wait may run across shut-down/init
-    amdsmi_shut_down();
-    check(amdsmi_init(AMDSMI_INIT_AMD_GPUS), "amdsmi_init (re-init)");
-    ++reinits_;
-    armed_ = false;
-    if (was_armed) want_rearm_ = true;
-    return true;
+  int armed_event_sources() const override { return armed_count_.load(); }
+
+  // The blocking wait enters the session first, then takes evt_mu_: disarming (which
+  // takes the same lock) waits for an in-flight wait to return instead of stopping
+  // notification underneath it, and a re-initialisation (gate closed) never waits on it.
+  int wait_events(int timeout_ms, std::vector<HwEvent>* out) override {
+    amdsmi_evt_notification_data_t data[16];
+    uint32_t num = 16;
+    amdsmi_status_t st = AMDSMI_STATUS_NOT_INIT;
+    bool waited = false;
+    if (evt_live_.load() && !closed_.load()) {
+      GateGuard g(gate());
+      std::lock_guard<std::mutex> ek(evt_mu_);
+      if (evt_live_.load()) {
+        st = amdsmi_get_gpu_event_notification(timeout_ms, &num, data);
+        waited = true;
+      }
+    }
+    if (!waited) {
+      // nothing armed (e.g. unprivileged container): the health monitor polls instead
+      struct timespec ts{timeout_ms / 1000, (timeout_ms % 1000) * 1000000L};
+      nanosleep(&ts, nullptr);
+      return 0;
+    }
+    if (st != AMDSMI_STATUS_SUCCESS) return 0;
+    auto inv = inventory();
+    int added = 0;
+    for (uint32_t i = 0; i < num; ++i) {
+      HwEvent e;
+      e.ts_ns = now_ns();
+      e.message = data[i].message;
+      switch (data[i].event) {
+        case AMDSMI_EVT_NOTIF_GPU_PRE_RESET: e.kind = kEvtPreReset; break;
+        case AMDSMI_EVT_NOTIF_GPU_POST_RESET: e.kind = kEvtPostReset; break;
+        case AMDSMI_EVT_NOTIF_THERMAL_THROTTLE: e.kind = kEvtThermal; break;
+        case AMDSMI_EVT_NOTIF_VMFAULT: e.kind = kEvtVmFault; break;
+        default: continue;
+      }
+      locate(*inv, data[i].processor_handle, &e.gpu, &e.partition);
+      e.key = inv->key_of(e.gpu);
+      out->push_back(e);
+      ++added;
+    }
+    return added;
   }
 
-  void discover_locked(std::vector<GpuInfo>* gpus, Topology* topo) {
+ protected:
+  // Sockets -> processors -> physical GPUs (BDF order).  Nothing here waits on a device:
+  // the processor list, BDFs and KFD partition ids come from amdsmi's enumeration at
+  // init and from KFD topology; the UUID is read once per BDF and remembered.
+  void enumerate(std::vector<DeviceRef>* refs) override {
+    if (closed_.load()) throw std::runtime_error("amdsmi backend is shut down");
+    GateGuard g(gate());
     uint32_t nsock = 0;
     check(amdsmi_get_socket_handles(&nsock, nullptr), "amdsmi_get_socket_handles(count)");
     std::vector<amdsmi_socket_handle> socks(nsock);
@@ -245,175 +296,178 @@ class AmdSmiBackend : public Backend {
         groups[bdf_key(p.bdf)].push_back(p);
       }
     }
-    gpus->clear();
-    procs_.clear();
-    bdf_keys_.clear();
+    std::lock_guard<std::mutex> lk(uuid_mu_);
     for (auto& kv : groups) {
-      bdf_keys_.push_back(kv.first);
       auto& plist = kv.second;
       std::stable_sort(plist.begin(), plist.end(),
                        [](const Proc& a, const Proc& b) { return a.partition_id < b.partition_id; });
-      GpuInfo g;
-      g.index = static_cast<int>(gpus->size());
-      amdsmi_processor_handle h0 = plist.front().h;
+      DeviceRef r;
       amdsmi_bdf_t b0 = plist.front().bdf;
       b0.function_number = 0;
-      g.bdf = bdf_str(b0);
-      g.uuid = uuid_of(h0);
-      amdsmi_asic_info_t asic{};
-      if (amdsmi_get_gpu_asic_info(h0, &asic) == AMDSMI_STATUS_SUCCESS) {
-        g.market_name = asic.market_name;
-        g.serial = asic.asic_serial;
-        g.gfx_target = gfx_name(asic.target_graphics_version);
-        if (asic.num_of_compute_units != 0xFFFFFFFFu) g.num_compute_units = static_cast<int>(asic.num_of_compute_units);
-        g.device_id = static_cast<uint32_t>(asic.device_id & 0xFFFF);
-        if (asic.oam_id != 0xFFFFFFFFu && asic.oam_id != 0xFFFFu) g.oam_id = static_cast<int>(asic.oam_id);
-      }
-      amdsmi_driver_info_t drv{};
-      if (amdsmi_get_gpu_driver_info(h0, &drv) == AMDSMI_STATUS_SUCCESS) g.driver_version = normalize_driver_version(drv.driver_version);
-      amdsmi_vbios_info_t vb{};
-      if (amdsmi_get_gpu_vbios_info(h0, &vb) == AMDSMI_STATUS_SUCCESS) g.vbios_version = vb.version;
-      if (g.market_name.empty()) g.market_name = "AMD Instinct";
-      amdsmi_vram_info_t vram{};
-      if (amdsmi_get_gpu_vram_info(h0, &vram) == AMDSMI_STATUS_SUCCESS)
-        g.vram_total_bytes = static_cast<uint64_t>(vram.vram_size) << 20;
-      char buf[64] = {0};
-      if (amdsmi_get_gpu_compute_partition(h0, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS) g.compute_partition = buf;
-      std::memset(buf, 0, sizeof(buf));
-      if (amdsmi_get_gpu_memory_partition(h0, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS) g.memory_partition = buf;
-      amdsmi_memory_partition_config_t mcfg{};
-      if (amdsmi_get_gpu_memory_partition_config(h0, &mcfg) == AMDSMI_STATUS_SUCCESS)
-        g.nps_caps = mcfg.partition_caps.nps_cap_mask & 0xF;
-      // The driver's own profile of the current mode: partition count and NPS caps
-      // come from it rather than from a table keyed by the mode string.
-      amdsmi_accelerator_partition_profile_t prof;
-      std::memset(&prof, 0, sizeof(prof));
-      uint32_t part_ids[AMDSMI_MAX_ACCELERATOR_PARTITIONS] = {};
-      if (amdsmi_get_gpu_accelerator_partition_profile(h0, &prof, part_ids) == AMDSMI_STATUS_SUCCESS &&
-          prof.num_partitions > 0 && prof.num_partitions <= AMDSMI_MAX_ACCELERATOR_PARTITIONS &&
-          profile_type_name(prof.profile_type)[0] != '\0') {
-        g.partition_profile = profile_type_name(prof.profile_type);
-        g.profile_partitions = static_cast<int>(prof.num_partitions);
-        g.profile_index = static_cast<int>(prof.profile_index);
-        if (g.compute_partition.empty()) g.compute_partition = g.partition_profile;
-        if (g.nps_caps == 0) g.nps_caps = prof.memory_caps.nps_cap_mask & 0xF;
-      }
-      if (g.compute_partition.empty()) g.compute_partition = plist.size() == 1 ? "SPX" : "UNKNOWN";
-      if (g.memory_partition.empty()) g.memory_partition = "NPS1";
-      uint32_t thr = 0;  // needs root; -1 when not readable
-      if (amdsmi_get_gpu_bad_page_threshold(h0, &thr) == AMDSMI_STATUS_SUCCESS) g.bad_page_threshold = static_cast<int>(thr);
-      int32_t numa = -1;
-      if (amdsmi_get_gpu_topo_numa_affinity(h0, &numa) != AMDSMI_STATUS_SUCCESS || numa < 0) numa = sysfs_numa(g.bdf);
-      g.numa_node = numa;
-      std::vector<amdsmi_processor_handle> handles;
-      for (size_t k = 0; k < plist.size(); ++k) {
-        const Proc& p = plist[k];
-        PartitionInfo part;
-        part.gpu = g.index;
-        part.index = static_cast<int>(k);
-        part.uuid = uuid_of(p.h);
-        part.id = plist.size() == 1 ? g.uuid : g.uuid + "-xcp" + std::to_string(k);
-        amdsmi_enumeration_info_t en{};
-        if (amdsmi_get_gpu_enumeration_info(p.h, &en) == AMDSMI_STATUS_SUCCESS) {
-          part.render_minor = static_cast<int>(en.drm_render);
-          part.card_minor = static_cast<int>(en.drm_card);
-          part.hip_id = static_cast<int>(en.hip_id);
-          part.hsa_id = static_cast<int>(en.hsa_id);
-        }
-        amdsmi_kfd_info_t kfd{};
-        if (amdsmi_get_gpu_kfd_info(p.h, &kfd) == AMDSMI_STATUS_SUCCESS && kfd.node_id != 0xFFFFFFFFu)
-          part.kfd_node = kfd.node_id;
-        part.numa_node = g.numa_node;
-        amdsmi_vram_usage_t vu{};
-        if (amdsmi_get_gpu_vram_usage(p.h, &vu) == AMDSMI_STATUS_SUCCESS)
-          part.vram_bytes = static_cast<uint64_t>(vu.vram_total) << 20;
-        if (part.vram_bytes == 0 && !plist.empty()) part.vram_bytes = g.vram_total_bytes / plist.size();
-        g.partitions.push_back(part);
-        handles.push_back(p.h);
-      }
-      procs_.push_back(handles);
-      gpus->push_back(std::move(g));
-    }
-    const int n = static_cast<int>(gpus->size());
-    topo->resize(n);
-    for (int a = 0; a < n; ++a) {
-      for (int b = 0; b < n; ++b) {
-        if (a == b) continue;
-        Link l;
-        uint64_t hops = 0;
-        amdsmi_link_type_t t = AMDSMI_LINK_TYPE_UNKNOWN;
-        if (amdsmi_topo_get_link_type(procs_[a][0], procs_[b][0], &hops, &t) == AMDSMI_STATUS_SUCCESS) {
-          l.type = static_cast<int>(t);
-          l.hops = static_cast<int>(hops);
-        }
-        uint64_t w = 0;
-        if (amdsmi_topo_get_link_weight(procs_[a][0], procs_[b][0], &w) == AMDSMI_STATUS_SUCCESS) l.weight = w;
-        amdsmi_link_type_t pt;
-        amdsmi_p2p_capability_t cap{};
-        if (amdsmi_topo_get_p2p_status(procs_[a][0], procs_[b][0], &pt, &cap) == AMDSMI_STATUS_SUCCESS)
-          l.p2p = true;
-        topo->at(a, b) = l;
-      }
-    }
-    // xGMI per-link health: link metrics name the peer BDF of each physical link.
-    links_.assign(procs_.size(), LinkCache{});  // indexes may have moved: re-verify
-    for (int a = 0; a < n; ++a) {
-      GpuSample s;
-      amdsmi_gpu_metrics_t gm;
-      std::memset(&gm, 0, sizeof(gm));
-      if (amdsmi_get_gpu_metrics_info(procs_[a][0], &gm) == AMDSMI_STATUS_SUCCESS && valid16(gm.xgmi_link_width) &&
-          gm.xgmi_link_width != 0)
-        s.xgmi_link_width = gm.xgmi_link_width;
-      link_state_locked(a, &s, nullptr);
-      (*gpus)[a].num_xgmi_links = s.num_links;
-      for (int k = 0; k < s.num_links; ++k) {
-        const int p = s.link_peer[k];
-        if (p < 0) continue;
-        if (s.link_up[k] == 0) topo->at(a, p).up = topo->at(p, a).up = false;
-        // trained bandwidth per link (the allocator scores a slow link below a full-rate
-        // one); each end reports its view, the link runs at the slower of the two
-        if (s.link_trained_gbps[k] > 0) {
-          const double cur = topo->at(a, p).bw_gbps;
-          const double bw = cur > 0 ? std::min(cur, s.link_trained_gbps[k]) : s.link_trained_gbps[k];
-          topo->at(a, p).bw_gbps = topo->at(p, a).bw_gbps = bw;
-        }
-      }
-    }
-    gpus_ = *gpus;
-    {
-      std::lock_guard<std::mutex> kl(keys_mu_);
-      keys_.clear();
-      for (const auto& g : gpus_) keys_.push_back(key_of(g));
-    }
-    if (want_rearm_) {
-      want_rearm_ = false;
-      arm_locked();
+      r.bdf = bdf_str(b0);
+      r.order = kv.first;
+      for (const auto& p : plist) r.handles.push_back(p.h);
+      auto it = uuid_of_bdf_.find(kv.first);
+      if (it == uuid_of_bdf_.end()) it = uuid_of_bdf_.emplace(kv.first, uuid_of(plist.front().h)).first;
+      r.key = it->second.empty() ? r.bdf : it->second;
+      refs->push_back(std::move(r));
     }
   }
 
- public:
-  std::vector<CallCost> sample_costs() const override {
-    std::lock_guard<std::mutex> lk(mu_);
-    std::vector<CallCost> out;
-    for (int c = 0; c < kCallCount; ++c)
-      out.push_back({kCallNames[c], cost_ns_[c] * 1e-9, cost_n_[c]});
-    // how many link samples took the full amdsmi path vs the gpu_metrics blob (counts only)
-    out.push_back({"xgmi_links_full_path", 0.0, link_full_});
-    out.push_back({"xgmi_links_blob_path", 0.0, link_fast_});
-    return out;
+  // Everything discovery reads from one GPU, on its lane: identity, partition model,
+  // per-partition render/KFD nodes, and this GPU's view of its links.
+  void describe(const DeviceRef& ref, const std::vector<DeviceRef>& all, GpuInfo* out,
+                std::vector<Link>* row) override {
+    GpuInfo& g = *out;
+    amdsmi_processor_handle h0 = ref.handles.front();
+    g.bdf = ref.bdf;
+    g.uuid = ref.key == ref.bdf ? uuid_of(h0) : ref.key;
+    amdsmi_asic_info_t asic{};
+    if (amdsmi_get_gpu_asic_info(h0, &asic) == AMDSMI_STATUS_SUCCESS) {
+      g.market_name = asic.market_name;
+      g.serial = asic.asic_serial;
+      g.gfx_target = gfx_name(asic.target_graphics_version);
+      if (asic.num_of_compute_units != 0xFFFFFFFFu) g.num_compute_units = static_cast<int>(asic.num_of_compute_units);
+      g.device_id = static_cast<uint32_t>(asic.device_id & 0xFFFF);
+      if (asic.oam_id != 0xFFFFFFFFu && asic.oam_id != 0xFFFFu) g.oam_id = static_cast<int>(asic.oam_id);
+    }
+    amdsmi_driver_info_t drv{};
+    if (amdsmi_get_gpu_driver_info(h0, &drv) == AMDSMI_STATUS_SUCCESS) g.driver_version = normalize_driver_version(drv.driver_version);
+    amdsmi_vbios_info_t vb{};
+    if (amdsmi_get_gpu_vbios_info(h0, &vb) == AMDSMI_STATUS_SUCCESS) g.vbios_version = vb.version;
+    if (g.market_name.empty()) g.market_name = "AMD Instinct";
+    amdsmi_vram_info_t vram{};
+    if (amdsmi_get_gpu_vram_info(h0, &vram) == AMDSMI_STATUS_SUCCESS)
+      g.vram_total_bytes = static_cast<uint64_t>(vram.vram_size) << 20;
+    char buf[64] = {0};
+    if (amdsmi_get_gpu_compute_partition(h0, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS) g.compute_partition = buf;
+    std::memset(buf, 0, sizeof(buf));
+    if (amdsmi_get_gpu_memory_partition(h0, buf, sizeof(buf)) == AMDSMI_STATUS_SUCCESS) g.memory_partition = buf;
+    amdsmi_memory_partition_config_t mcfg{};
+    if (amdsmi_get_gpu_memory_partition_config(h0, &mcfg) == AMDSMI_STATUS_SUCCESS)
+      g.nps_caps = mcfg.partition_caps.nps_cap_mask & 0xF;
+    // The driver's own profile of the current mode: partition count and NPS caps come
+    // from it rather than from a table keyed by the mode string.
+    amdsmi_accelerator_partition_profile_t prof;
+    std::memset(&prof, 0, sizeof(prof));
+    uint32_t part_ids[AMDSMI_MAX_ACCELERATOR_PARTITIONS] = {};
+    if (amdsmi_get_gpu_accelerator_partition_profile(h0, &prof, part_ids) == AMDSMI_STATUS_SUCCESS &&
+        prof.num_partitions > 0 && prof.num_partitions <= AMDSMI_MAX_ACCELERATOR_PARTITIONS &&
+        profile_type_name(prof.profile_type)[0] != '\0') {
+      g.partition_profile = profile_type_name(prof.profile_type);
+      g.profile_partitions = static_cast<int>(prof.num_partitions);
+      g.profile_index = static_cast<int>(prof.profile_index);
+      if (g.compute_partition.empty()) g.compute_partition = g.partition_profile;
+      if (g.nps_caps == 0) g.nps_caps = prof.memory_caps.nps_cap_mask & 0xF;
+    }
+    // Every profile the GPU supports (the reference's mixed strategy asks NVML for every
+    // MIG profile, resource/resources.go:43-51 VisitMigProfiles).
+    // The list needs root (AMDSMI_STATUS_NO_PERM as an ordinary user on the MI355X box,
+    // profiles/r4/amdsmi_probe.json); then only the current profile is known supported.
+    auto cfg = std::make_unique<amdsmi_accelerator_partition_profile_config_t>();
+    std::memset(cfg.get(), 0, sizeof(*cfg));
+    const amdsmi_status_t cst = amdsmi_get_gpu_accelerator_partition_profile_config(h0, cfg.get());
+    g.profiles_status = cst == AMDSMI_STATUS_SUCCESS ? "ok" : status_str(cst);
+    if (cst == AMDSMI_STATUS_SUCCESS) {
+      for (uint32_t i = 0; i < cfg->num_profiles && i < AMDSMI_MAX_ACCELERATOR_PROFILE; ++i) {
+        const auto& p = cfg->profiles[i];
+        if (profile_type_name(p.profile_type)[0] == '\0' || p.num_partitions == 0) continue;
+        PartitionProfile pp;
+        pp.type = profile_type_name(p.profile_type);
+        pp.partitions = static_cast<int>(p.num_partitions);
+        pp.nps_caps = p.memory_caps.nps_cap_mask & 0xF;
+        pp.index = static_cast<int>(p.profile_index);
+        g.supported_profiles.push_back(pp);
+      }
+    }
+    if (g.supported_profiles.empty() && !g.partition_profile.empty()) {
+      PartitionProfile pp;
+      pp.type = g.partition_profile;
+      pp.partitions = g.profile_partitions;
+      pp.nps_caps = g.nps_caps;
+      pp.index = g.profile_index;
+      pp.source = "current";
+      g.supported_profiles.push_back(pp);
+    }
+    if (g.compute_partition.empty()) g.compute_partition = ref.handles.size() == 1 ? "SPX" : "UNKNOWN";
+    if (g.memory_partition.empty()) g.memory_partition = "NPS1";
+    uint32_t thr = 0;  // needs root; -1 when not readable
+    if (amdsmi_get_gpu_bad_page_threshold(h0, &thr) == AMDSMI_STATUS_SUCCESS) g.bad_page_threshold = static_cast<int>(thr);
+    int32_t numa = -1;
+    if (amdsmi_get_gpu_topo_numa_affinity(h0, &numa) != AMDSMI_STATUS_SUCCESS || numa < 0) numa = sysfs_numa(g.bdf);
+    g.numa_node = numa;
+    for (size_t k = 0; k < ref.handles.size(); ++k) {
+      amdsmi_processor_handle h = ref.handles[k];
+      PartitionInfo part;
+      part.index = static_cast<int>(k);
+      part.uuid = uuid_of(h);
+      part.id = ref.handles.size() == 1 ? g.uuid : g.uuid + "-xcp" + std::to_string(k);
+      amdsmi_enumeration_info_t en{};
+      if (amdsmi_get_gpu_enumeration_info(h, &en) == AMDSMI_STATUS_SUCCESS) {
+        part.render_minor = static_cast<int>(en.drm_render);
+        part.card_minor = static_cast<int>(en.drm_card);
+        part.hip_id = static_cast<int>(en.hip_id);
+        part.hsa_id = static_cast<int>(en.hsa_id);
+      }
+      amdsmi_kfd_info_t kfd{};
+      if (amdsmi_get_gpu_kfd_info(h, &kfd) == AMDSMI_STATUS_SUCCESS && kfd.node_id != 0xFFFFFFFFu)
+        part.kfd_node = kfd.node_id;
+      part.numa_node = g.numa_node;
+      amdsmi_vram_usage_t vu{};
+      if (amdsmi_get_gpu_vram_usage(h, &vu) == AMDSMI_STATUS_SUCCESS)
+        part.vram_bytes = static_cast<uint64_t>(vu.vram_total) << 20;
+      if (part.vram_bytes == 0) part.vram_bytes = g.vram_total_bytes / ref.handles.size();
+      g.partitions.push_back(part);
+    }
+    // This GPU's view of its links: class, hops and weight per peer, then xGMI health and
+    // trained bandwidth from the link metrics (which name each link's peer by BDF).
+    row->assign(all.size(), Link{});
+    for (size_t p = 0; p < all.size(); ++p) {
+      if (all[p].order == ref.order || all[p].handles.empty()) continue;
+      Link& l = (*row)[p];
+      amdsmi_processor_handle hp = all[p].handles.front();
+      uint64_t hops = 0;
+      amdsmi_link_type_t t = AMDSMI_LINK_TYPE_UNKNOWN;
+      if (amdsmi_topo_get_link_type(h0, hp, &hops, &t) == AMDSMI_STATUS_SUCCESS) {
+        l.type = static_cast<int>(t);
+        l.hops = static_cast<int>(hops);
+      }
+      uint64_t w = 0;
+      if (amdsmi_topo_get_link_weight(h0, hp, &w) == AMDSMI_STATUS_SUCCESS) l.weight = w;
+      amdsmi_link_type_t pt;
+      amdsmi_p2p_capability_t cap{};
+      if (amdsmi_topo_get_p2p_status(h0, hp, &pt, &cap) == AMDSMI_STATUS_SUCCESS) l.p2p = true;
+    }
+    auto ds = dev(ref.key);
+    ds->links = LinkCache{};  // indexes may have moved: take the full path and re-verify
+    GpuSample s;
+    amdsmi_gpu_metrics_t gm;
+    std::memset(&gm, 0, sizeof(gm));
+    if (amdsmi_get_gpu_metrics_info(h0, &gm) == AMDSMI_STATUS_SUCCESS && valid16(gm.xgmi_link_width) &&
+        gm.xgmi_link_width != 0)
+      s.xgmi_link_width = gm.xgmi_link_width;
+    link_state(*ds, h0, all, &s, nullptr);
+    g.num_xgmi_links = s.num_links;
+    for (int k = 0; k < s.num_links; ++k) {
+      const int p = s.link_peer[k];  // position in `all` here
+      if (p < 0) continue;
+      if (s.link_up[k] == 0) (*row)[p].up = false;
+      if (s.link_trained_gbps[k] > 0) (*row)[p].bw_gbps = s.link_trained_gbps[k];
+    }
   }
 
-  bool sample(int gpu, GpuSample* s) override {
-    std::lock_guard<std::mutex> lk(mu_);
-    if (gpu >= 0 && gpu < static_cast<int>(gpus_.size())) s->key = key_of(gpus_[gpu]);
-    if (closed_ || gpu < 0 || gpu >= static_cast<int>(procs_.size())) return false;
-    amdsmi_processor_handle h0 = procs_[gpu][0];
+  bool sample_device(const Inventory& inv, int gpu, GpuSample* s) override {
+    if (closed_.load()) return false;
+    const DeviceRef& ref = inv.refs[gpu];
+    amdsmi_processor_handle h0 = ref.handles.front();
+    auto ds = dev(ref.key);
     s->ts_ns = now_ns();
     amdsmi_gpu_metrics_t m;
     std::memset(&m, 0, sizeof(m));
     int64_t t = mono_ns();
     const amdsmi_status_t mst = amdsmi_get_gpu_metrics_info(h0, &m);
-    charge(kCallGpuMetrics, t);  // the blob's parsing below is not charged to any call
+    t = charge(kCallGpuMetrics, t);  // the blob's parsing below is not charged to any call
+    const int nparts = static_cast<int>(ref.handles.size());
     if (mst == AMDSMI_STATUS_SUCCESS) {
       s->ok = true;
       if (valid16(m.current_socket_power) && m.current_socket_power != 0) s->power_w = m.current_socket_power;
@@ -437,33 +491,21 @@ class AmdSmiBackend : public Backend {
       if (valid16(m.pcie_link_speed) && m.pcie_link_speed != 0) s->pcie_link_speed_gtps = m.pcie_link_speed * 0.1;
       if (valid64(m.pcie_replay_count_acc)) s->pcie_replays = static_cast<double>(m.pcie_replay_count_acc);
       if (valid64(m.pcie_l0_to_recov_count_acc)) s->pcie_recoveries = static_cast<double>(m.pcie_l0_to_recov_count_acc);
-      const int nparts = static_cast<int>(procs_[gpu].size());
-      s->num_partitions = std::min(nparts, kMaxPartitions);
-      for (int p = 0; p < s->num_partitions && p < AMDSMI_MAX_NUM_XCP; ++p) {
-        double sum = 0;
-        int cnt = 0;
-        for (int x = 0; x < AMDSMI_MAX_NUM_XCC; ++x) {
-          const uint16_t v = m.xcp_stats[p].gfx_busy_inst[x];
-          if (valid16(v)) {
-            sum += v;
-            ++cnt;
-          }
-        }
-        s->partition_gfx_busy_pct[p] = cnt ? sum / cnt : (nparts == 1 ? s->gfx_activity_pct : -1);
-      }
     }
-    t = mono_ns();
+    s->num_partitions = std::min(nparts, kMaxPartitions);
+    partition_busy(*ds, ref, mst == AMDSMI_STATUS_SUCCESS ? &m : nullptr, s);
+    t = charge(kCallPartitionMetrics, t);
     double used = 0, total = 0;
     bool have_vram = false;
-    for (size_t p = 0; p < procs_[gpu].size(); ++p) {
+    const bool shared_pool = inv.gpus[gpu].memory_partition == "NPS1";
+    for (size_t p = 0; p < ref.handles.size(); ++p) {
       amdsmi_vram_usage_t vu{};
-      if (amdsmi_get_gpu_vram_usage(procs_[gpu][p], &vu) == AMDSMI_STATUS_SUCCESS) {
+      if (amdsmi_get_gpu_vram_usage(ref.handles[p], &vu) == AMDSMI_STATUS_SUCCESS) {
         have_vram = true;
         used += static_cast<double>(vu.vram_used) * 1048576.0;
         total += static_cast<double>(vu.vram_total) * 1048576.0;
         if (static_cast<int>(p) < kMaxPartitions) s->partition_vram_used_bytes[p] = static_cast<double>(vu.vram_used) * 1048576.0;
-        // partitions share one VRAM pool in NPS1; do not double count
-        if (gpus_.size() > static_cast<size_t>(gpu) && gpus_[gpu].memory_partition == "NPS1") break;
+        if (shared_pool) break;  // partitions share one VRAM pool in NPS1; do not double count
       }
     }
     if (have_vram) {
@@ -480,87 +522,59 @@ class AmdSmiBackend : public Backend {
     amdsmi_xgmi_status_t xs = AMDSMI_XGMI_STATUS_NO_ERRORS;
     if (amdsmi_gpu_xgmi_error_status(h0, &xs) == AMDSMI_STATUS_SUCCESS) s->xgmi_error_status = static_cast<int>(xs);
     t = charge(kCallEcc, t);
-    link_state_locked(gpu, s, mst == AMDSMI_STATUS_SUCCESS ? &m : nullptr);
+    link_state(*ds, h0, inv.refs, s, mst == AMDSMI_STATUS_SUCCESS ? &m : nullptr);
     t = charge(kCallLinks, t);
-    bad_pages_locked(gpu, h0, s);
+    bad_pages(*ds, h0, s);
     charge(kCallBadPages, t);
     return s->ok;
   }
 
-  void arm_events() override {
-    std::lock_guard<std::mutex> lk(mu_);
-    arm_locked();
-  }
-
-  void arm_locked() {
-    if (armed_ || closed_) return;
-    const uint64_t mask = AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_GPU_PRE_RESET) |
-                          AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_GPU_POST_RESET) |
-                          AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_THERMAL_THROTTLE) |
-                          AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_VMFAULT);
-    armed_handles_.clear();
-    armed_for_.clear();
-    for (auto& handles : procs_) {
-      armed_for_.insert(armed_for_.end(), handles.begin(), handles.end());
-      for (auto h : handles) {
-        if (amdsmi_init_gpu_event_notification(h) != AMDSMI_STATUS_SUCCESS) continue;
-        if (amdsmi_set_gpu_event_notification_mask(h, mask) != AMDSMI_STATUS_SUCCESS) {
-          amdsmi_stop_gpu_event_notification(h);
-          continue;
-        }
-        armed_handles_.push_back(h);
-      }
+  bool handles_stale(const std::vector<GpuInfo>& described) override {
+    // amdsmi enumerates processors once, at amdsmi_init.  After an operator switches a
+    // GPU's compute partition mode (amd-smi set --compute-partition), the cached handle
+    // list no longer matches the mode the GPU reports: re-initialise and enumerate again.
+    for (const auto& g : described) {
+      const int want = g.profile_partitions > 0 ? g.profile_partitions : partitions_of_mode(g.compute_partition);
+      if (want > 0 && want != static_cast<int>(g.partitions.size())) return true;
     }
-    armed_ = true;
-    evt_live_.store(!armed_handles_.empty());
+    return false;
   }
 
-  int armed_event_sources() const override {
-    std::lock_guard<std::mutex> lk(mu_);
-    return static_cast<int>(armed_handles_.size());
-  }
-
-  // Lock order: mu_ -> evt_mu_ (disarm/re-init); the blocking wait holds only evt_mu_
-  // and takes mu_ after releasing it, so disarming waits for an in-flight wait to
-  // return instead of stopping notification underneath it.
-  int wait_events(int timeout_ms, std::vector<HwEvent>* out) override {
-    amdsmi_evt_notification_data_t data[16];
-    uint32_t num = 16;
-    amdsmi_status_t st = AMDSMI_STATUS_NOT_INIT;
-    bool waited = false;
+  // amdsmi is process-global: only the sole owner may shut it down and start it again.
+  // Runs with the session gate closed (no call inside the library).
+  bool reopen_session() override {
+    std::lock_guard<std::mutex> ilk(g_init_mu);
+    if (g_init_refs != 1 || closed_.load()) return false;
     {
       std::lock_guard<std::mutex> ek(evt_mu_);
-      if (evt_live_.load()) {
-        st = amdsmi_get_gpu_event_notification(timeout_ms, &num, data);
-        waited = true;
-      }
+      disarm_locked();
     }
-    if (!waited) {
-      // nothing armed (e.g. unprivileged container): the health monitor polls instead
-      struct timespec ts{timeout_ms / 1000, (timeout_ms % 1000) * 1000000L};
-      nanosleep(&ts, nullptr);
-      return 0;
+    amdsmi_shut_down();
+    check(amdsmi_init(AMDSMI_INIT_AMD_GPUS), "amdsmi_init (re-init)");
+    reinits_.fetch_add(1);
+    {
+      std::lock_guard<std::mutex> lk(devs_mu_);
+      devs_.clear();  // caches of the old handles
     }
-    if (st != AMDSMI_STATUS_SUCCESS) return 0;
-    int added = 0;
-    std::lock_guard<std::mutex> lk(mu_);
-    for (uint32_t i = 0; i < num; ++i) {
-      HwEvent e;
-      e.ts_ns = now_ns();
-      e.message = data[i].message;
-      switch (data[i].event) {
-        case AMDSMI_EVT_NOTIF_GPU_PRE_RESET: e.kind = kEvtPreReset; break;
-        case AMDSMI_EVT_NOTIF_GPU_POST_RESET: e.kind = kEvtPostReset; break;
-        case AMDSMI_EVT_NOTIF_THERMAL_THROTTLE: e.kind = kEvtThermal; break;
-        case AMDSMI_EVT_NOTIF_VMFAULT: e.kind = kEvtVmFault; break;
-        default: continue;
-      }
-      locate(data[i].processor_handle, &e.gpu, &e.partition);
-      if (e.gpu >= 0 && e.gpu < static_cast<int>(gpus_.size())) e.key = key_of(gpus_[e.gpu]);
-      out->push_back(e);
-      ++added;
+    return true;
+  }
+
+  // Keeps event delivery armed across re-discovery; re-arms only when the processor set
+  // changed (handles from a re-init are new objects).
+  void installed(const std::shared_ptr<const Inventory>& inv) override {
+    if (!arm_wanted_.load()) return;
+    std::vector<void*> flat;
+    for (const auto& r : inv->refs) flat.insert(flat.end(), r.handles.begin(), r.handles.end());
+    {
+      std::lock_guard<std::mutex> ek(arm_mu_);
+      if (flat == armed_for_) return;
     }
-    return added;
+    {
+      GateGuard g(gate());
+      std::lock_guard<std::mutex> ek(evt_mu_);
+      disarm_locked();
+    }
+    arm_on_lanes(inv);
   }
 
  private:
@@ -575,24 +589,115 @@ class AmdSmiBackend : public Backend {
     return "amdgpu-" + bdf_str(b);
   }
 
-  void locate(amdsmi_processor_handle h, int* gpu, int* part) {
-    for (size_t g = 0; g < procs_.size(); ++g)
-      for (size_t p = 0; p < procs_[g].size(); ++p)
-        if (procs_[g][p] == h) {
+  static void locate(const Inventory& inv, amdsmi_processor_handle h, int* gpu, int* part) {
+    for (size_t g = 0; g < inv.refs.size(); ++g)
+      for (size_t p = 0; p < inv.refs[g].handles.size(); ++p)
+        if (inv.refs[g].handles[p] == h) {
           *gpu = static_cast<int>(g);
-          *part = procs_[g].size() == 1 ? -1 : static_cast<int>(p);
+          *part = inv.refs[g].handles.size() == 1 ? -1 : static_cast<int>(p);
           return;
         }
   }
 
-  // Peer lookup for every xGMI link of every sample: BDF keys are cached at discovery
-  // (7 links x 8 GPUs per tick would otherwise re-query amdsmi 8 times per link).
+  // Arms event notification on every processor, each on its GPU's lane (a wedged GPU's
+  // lane refuses; it is armed at the next discovery).
+  void arm_on_lanes(const std::shared_ptr<const Inventory>& inv) {
+    if (closed_.load()) return;
+    const uint64_t mask = AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_GPU_PRE_RESET) |
+                          AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_GPU_POST_RESET) |
+                          AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_THERMAL_THROTTLE) |
+                          AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_VMFAULT);
+    std::vector<void*> flat;
+    std::vector<std::shared_ptr<std::vector<void*>>> armed;
+    std::vector<std::shared_ptr<LaneJob>> jobs;
+    for (const auto& r : inv->refs) {
+      flat.insert(flat.end(), r.handles.begin(), r.handles.end());
+      auto out = std::make_shared<std::vector<void*>>();
+      armed.push_back(out);
+      const std::vector<void*> hs = r.handles;
+      jobs.push_back(post_job(r.key, "arm", inv->session, [hs, mask, out] {
+        for (auto h : hs) {
+          if (amdsmi_init_gpu_event_notification(h) != AMDSMI_STATUS_SUCCESS) continue;
+          if (amdsmi_set_gpu_event_notification_mask(h, mask) != AMDSMI_STATUS_SUCCESS) {
+            amdsmi_stop_gpu_event_notification(h);
+            continue;
+          }
+          out->push_back(h);
+        }
+      }));
+    }
+    const int64_t deadline = mono_ns() + static_cast<int64_t>(call_timeout_ms()) * 1000000;
+    std::vector<void*> live;
+    for (size_t g = 0; g < jobs.size(); ++g) {
+      if (!jobs[g] || !jobs[g]->wait(std::max<int64_t>(0, (deadline - mono_ns()) / 1000000)) || jobs[g]->dropped())
+        continue;
+      live.insert(live.end(), armed[g]->begin(), armed[g]->end());
+    }
+    std::lock_guard<std::mutex> ek(arm_mu_);
+    armed_handles_ = live;
+    armed_for_ = flat;
+    armed_count_.store(static_cast<int>(live.size()));
+    evt_live_.store(!live.empty());
+  }
+
+  // evt_mu_ held, inside the session (or with the gate closed)
+  void disarm_locked() {
+    std::lock_guard<std::mutex> ak(arm_mu_);
+    evt_live_.store(false);
+    for (auto h : armed_handles_) amdsmi_stop_gpu_event_notification(h);
+    armed_handles_.clear();
+    armed_for_.clear();
+    armed_count_.store(0);
+  }
+
+  // ---- per-GPU state, touched only on the GPU's lane ----
+  // Peer lookup for every xGMI link of every sample: peers are cached by BDF order key at
+  // discovery (7 links x 8 GPUs per tick would otherwise re-query amdsmi 8 times per link).
+  // amdsmi_get_link_metrics resolves every link's peer BDF and costs ~0.9-1.3 ms per GPU
+  // on MI355X (test_amdsmi_sample_cost_breakdown), while the per-link byte counters and
+  // up/down status it reports are also in the gpu_metrics blob sample() has just read.  So
+  // the full call (plus amdsmi_get_gpu_xgmi_link_status) runs at discovery and every
+  // kLinkRefreshNs, and cross-checks the blob index for index: counters within a small
+  // skew of the blob's and, separately, blob status equal to the link-status call.
+  // Between refreshes a verified GPU takes counters (and, if verified, status) from the
+  // blob and peers / rates from the cache; an unverified one takes the full path.
+  static constexpr int64_t kLinkRefreshNs = 10'000'000'000;
+  struct LinkCache {
+    int64_t read_ns = 0;
+    bool counters_ok = false;  // blob counters line up with link_metrics
+    bool status_ok = false;    // blob status lines up with the link-status call
+    int n = 0;
+    int k[kMaxXgmiLinks] = {};            // metrics index of reported link i
+    uint64_t peer[kMaxXgmiLinks] = {};    // peer's BDF order key (0 = unknown)
+    double bitrate[kMaxXgmiLinks] = {}, maxbw[kMaxXgmiLinks] = {};
+  };
   // RAS retired-page records change only when the driver retires a page: re-read them
   // every kBadPageRefreshNs and report the cached counts in between.
   static constexpr int64_t kBadPageRefreshNs = 10'000'000'000LL;
-  void bad_pages_locked(int gpu, amdsmi_processor_handle h, GpuSample* s) {
-    if (bad_pages_.size() != procs_.size()) bad_pages_.assign(procs_.size(), BadPages{});
-    BadPages& bp = bad_pages_[gpu];
+  struct BadPages {
+    int64_t read_ns = 0;
+    int64_t reserved = -1, pending = -1, unreservable = -1;
+  };
+  struct DevState {
+    LinkCache links;
+    BadPages pages;
+    int partition_api = 0;  // amdsmi_get_gpu_partition_metrics_info: 0 untried, 1 answers, -1 not supported
+  };
+  std::shared_ptr<DevState> dev(const std::string& key) {
+    std::lock_guard<std::mutex> lk(devs_mu_);
+    auto& d = devs_[key];
+    if (!d) d = std::make_shared<DevState>();
+    return d;
+  }
+
+  static int position_of(const std::vector<DeviceRef>& refs, uint64_t order) {
+    for (size_t i = 0; i < refs.size(); ++i)
+      if (refs[i].order == order) return static_cast<int>(i);
+    return -1;
+  }
+
+  void bad_pages(DevState& ds, amdsmi_processor_handle h, GpuSample* s) {
+    BadPages& bp = ds.pages;
     const int64_t now = mono_ns();
     if (bp.read_ns == 0 || now - bp.read_ns >= kBadPageRefreshNs) {
       bp.read_ns = now;
@@ -619,52 +724,76 @@ class AmdSmiBackend : public Backend {
     s->unreservable_pages = bp.unreservable;
   }
 
-  int gpu_of_bdf(const amdsmi_bdf_t& b) const {
-    const auto it = std::find(bdf_keys_.begin(), bdf_keys_.end(), bdf_key(b));
-    return it == bdf_keys_.end() ? -1 : static_cast<int>(it - bdf_keys_.begin());
+  // Per-partition compute busy.  Preferred source: the partition's own metrics
+  // (amdsmi_get_gpu_partition_metrics_info on the partition's processor);
+  // fallback: the socket blob's xcp_stats[p] (assumes partition order == XCP order).
+  void partition_busy(DevState& ds, const DeviceRef& ref, const amdsmi_gpu_metrics_t* blob, GpuSample* s) {
+    auto mean = [](const amdsmi_gpu_xcp_metrics_t& x) {
+      double sum = 0;
+      int cnt = 0;
+      for (int i = 0; i < AMDSMI_MAX_NUM_XCC; ++i)  // uint32 fields: all-ones = not reported
+        if (x.gfx_busy_inst[i] != 0xFFFFFFFFu && x.gfx_busy_inst[i] <= 100) {
+          sum += x.gfx_busy_inst[i];
+          ++cnt;
+        }
+      return cnt ? sum / cnt : -1.0;
+    };
+    for (int p = 0; p < s->num_partitions; ++p) {
+      double v = -1;
+      if (ds.partition_api >= 0) {
+        auto pm = std::make_unique<amdsmi_gpu_metrics_t>();
+        std::memset(pm.get(), 0, sizeof(*pm));
+        const amdsmi_status_t st = amdsmi_get_gpu_partition_metrics_info(ref.handles[p], pm.get());
+        if (st == AMDSMI_STATUS_SUCCESS) {
+          // a partition's table carries its own XCP's stats; take the slot with data
+          // (slot p when it carries the whole socket's)
+          int with_data = 0, first = -1;
+          for (int x = 0; x < AMDSMI_MAX_NUM_XCP; ++x)
+            if (mean(pm->xcp_stats[x]) >= 0) {
+              ++with_data;
+              if (first < 0) first = x;
+            }
+          if (first >= 0) v = mean(pm->xcp_stats[with_data > 1 && p < AMDSMI_MAX_NUM_XCP ? p : first]);
+          if (v >= 0) ds.partition_api = 1;
+        } else if (st == AMDSMI_STATUS_NOT_SUPPORTED || st == AMDSMI_STATUS_NOT_YET_IMPLEMENTED) {
+          ds.partition_api = -1;
+        }
+      }
+      if (v >= 0) {
+        s->partition_busy_source[p] = 1;
+        part_from_api_.fetch_add(1, std::memory_order_relaxed);
+      } else if (blob && p < AMDSMI_MAX_NUM_XCP) {
+        v = mean(blob->xcp_stats[p]);
+        if (v < 0 && s->num_partitions == 1) v = s->gfx_activity_pct;
+        if (v >= 0) {
+          s->partition_busy_source[p] = 2;
+          part_from_blob_.fetch_add(1, std::memory_order_relaxed);
+        }
+      }
+      s->partition_gfx_busy_pct[p] = v;
+    }
   }
-
-  // Fills per-link peer/up/read/write/rate.  amdsmi_get_link_metrics resolves every
-  // link's peer BDF and costs ~0.9-1.3 ms per GPU on MI355X (test_amdsmi_sample_cost_
-  // breakdown), while the per-link byte counters and up/down status it reports are also
-  // in the gpu_metrics blob sample() has just read.  So the full call (plus
-  // amdsmi_get_gpu_xgmi_link_status) runs at discovery and every kLinkRefreshNs, and
-  // cross-checks the blob index for index: counters within a small skew of the blob's
-  // and, separately, blob status equal to the link-status call.  Between refreshes a
-  // verified GPU takes counters (and, if verified, status) from the blob and peers /
-  // rates from the cache; an unverified one takes the full path every sample.
-  static constexpr int64_t kLinkRefreshNs = 10'000'000'000;
-  struct LinkCache {
-    int64_t read_ns = 0;
-    bool counters_ok = false;  // blob counters line up with link_metrics
-    bool status_ok = false;    // blob status lines up with the link-status call
-    int n = 0;
-    int k[kMaxXgmiLinks] = {};  // metrics index of reported link i
-    int peer[kMaxXgmiLinks] = {};
-    double bitrate[kMaxXgmiLinks] = {}, maxbw[kMaxXgmiLinks] = {};
-  };
-  std::vector<LinkCache> links_;  // per GPU, guarded by mu_
-  uint64_t link_fast_ = 0, link_full_ = 0;
 
   static int blob_up(uint16_t v) { return v == 1 ? 1 : (v == 0 ? 0 : -1); }
 
-  void link_state_locked(int gpu, GpuSample* s, const amdsmi_gpu_metrics_t* m) {
-    if (links_.size() != procs_.size()) links_.assign(procs_.size(), LinkCache{});
-    LinkCache& lc = links_[gpu];
+  // Fills per-link peer/up/read/write/rate; peers are positions in `refs`.
+  void link_state(DevState& ds, amdsmi_processor_handle h0, const std::vector<DeviceRef>& refs, GpuSample* s,
+                  const amdsmi_gpu_metrics_t* m) {
+    LinkCache& lc = ds.links;
     const int64_t now = mono_ns();
     s->num_links = 0;
     if (m && lc.counters_ok && lc.read_ns != 0 && now - lc.read_ns < kLinkRefreshNs) {
-      ++link_fast_;
+      link_fast_.fetch_add(1, std::memory_order_relaxed);
       amdsmi_xgmi_link_status_t ls;
       bool have_status = false;
       if (!lc.status_ok) {
         std::memset(&ls, 0, sizeof(ls));
-        have_status = amdsmi_get_gpu_xgmi_link_status(procs_[gpu][0], &ls) == AMDSMI_STATUS_SUCCESS;
+        have_status = amdsmi_get_gpu_xgmi_link_status(h0, &ls) == AMDSMI_STATUS_SUCCESS;
       }
       s->num_links = lc.n;
       for (int i = 0; i < lc.n; ++i) {
         const int k = lc.k[i];
-        s->link_peer[i] = lc.peer[i];
+        s->link_peer[i] = lc.peer[i] ? position_of(refs, lc.peer[i]) : -1;
         s->link_read_kb[i] = static_cast<double>(m->xgmi_read_data_acc[k]);
         s->link_write_kb[i] = static_cast<double>(m->xgmi_write_data_acc[k]);
         s->link_bitrate_gbps[i] = lc.bitrate[i];
@@ -679,22 +808,23 @@ class AmdSmiBackend : public Backend {
       fill_trained(s);
       return;
     }
-    ++link_full_;
+    link_full_.fetch_add(1, std::memory_order_relaxed);
     lc.read_ns = now;
     lc.counters_ok = lc.status_ok = false;
     lc.n = 0;
     amdsmi_link_metrics_t lm;
     std::memset(&lm, 0, sizeof(lm));
-    if (amdsmi_get_link_metrics(procs_[gpu][0], &lm) != AMDSMI_STATUS_SUCCESS) return;
+    if (amdsmi_get_link_metrics(h0, &lm) != AMDSMI_STATUS_SUCCESS) return;
     amdsmi_xgmi_link_status_t ls;
     std::memset(&ls, 0, sizeof(ls));
-    const bool have_status = amdsmi_get_gpu_xgmi_link_status(procs_[gpu][0], &ls) == AMDSMI_STATUS_SUCCESS;
+    const bool have_status = amdsmi_get_gpu_xgmi_link_status(h0, &ls) == AMDSMI_STATUS_SUCCESS;
     const uint32_t nl = std::min<uint32_t>(lm.num_links, std::min<uint32_t>(kMaxXgmiLinks, AMDSMI_MAX_NUM_XGMI_LINKS));
     bool counters_ok = m != nullptr, status_ok = m != nullptr && have_status;
     for (uint32_t k = 0; k < nl; ++k) {
       if (lm.links[k].link_type != AMDSMI_LINK_TYPE_XGMI) continue;
       const int i = s->num_links++;
-      s->link_peer[i] = gpu_of_bdf(lm.links[k].bdf);
+      const uint64_t peer = bdf_key(lm.links[k].bdf);
+      s->link_peer[i] = position_of(refs, peer);
       s->link_read_kb[i] = static_cast<double>(lm.links[k].read);
       s->link_write_kb[i] = static_cast<double>(lm.links[k].write);
       s->link_bitrate_gbps[i] = lm.links[k].bit_rate != 0xFFFFFFFFu ? lm.links[k].bit_rate : 0;
@@ -704,7 +834,7 @@ class AmdSmiBackend : public Backend {
       else
         s->link_up[i] = -1;
       lc.k[i] = static_cast<int>(k);
-      lc.peer[i] = s->link_peer[i];
+      lc.peer[i] = s->link_peer[i] >= 0 ? peer : 0;
       lc.bitrate[i] = s->link_bitrate_gbps[i];
       lc.maxbw[i] = s->link_max_gbps[i];
       if (m) {
@@ -736,47 +866,34 @@ class AmdSmiBackend : public Backend {
                                     : s->link_max_gbps[i];
   }
 
-  void disarm_locked() {
-    if (!armed_) return;
-    evt_live_.store(false);
-    std::lock_guard<std::mutex> ek(evt_mu_);
-    for (auto h : armed_handles_) amdsmi_stop_gpu_event_notification(h);
-    armed_handles_.clear();
-    armed_ = false;
-  }
-
-  // per-call cost accounting for sample() (guarded by mu_)
-  enum SampleCall { kCallGpuMetrics, kCallVram, kCallEcc, kCallLinks, kCallBadPages, kCallCount };
-  static constexpr const char* kCallNames[kCallCount] = {"gpu_metrics", "vram_usage", "ecc_count", "xgmi_links",
-                                                         "bad_pages"};
-  struct BadPages {
-    int64_t read_ns = 0;
-    int64_t reserved = -1, pending = -1, unreservable = -1;
-  };
-  std::vector<BadPages> bad_pages_;  // per GPU, guarded by mu_
+  // per-call cost accounting for sample_device()
+  enum SampleCall { kCallGpuMetrics, kCallPartitionMetrics, kCallVram, kCallEcc, kCallLinks, kCallBadPages, kCallCount };
+  static constexpr const char* kCallNames[kCallCount] = {"gpu_metrics", "partition_metrics", "vram_usage",
+                                                         "ecc_count", "xgmi_links", "bad_pages"};
   int64_t charge(int call, int64_t since) {
     const int64_t now = mono_ns();
-    cost_ns_[call] += now - since;
-    ++cost_n_[call];
+    cost_ns_[call].fetch_add(now - since, std::memory_order_relaxed);
+    cost_n_[call].fetch_add(1, std::memory_order_relaxed);
     return now;
   }
-  int64_t cost_ns_[kCallCount] = {};
-  uint64_t cost_n_[kCallCount] = {};
+  std::atomic<int64_t> cost_ns_[kCallCount] = {};
+  std::atomic<uint64_t> cost_n_[kCallCount] = {};
+  std::atomic<uint64_t> link_fast_{0}, link_full_{0}, part_from_api_{0}, part_from_blob_{0};
 
-  mutable std::mutex mu_;
+  std::mutex life_mu_;
+  std::atomic<bool> closed_{false};
+  std::mutex devs_mu_;  // the map only; a DevState's contents belong to its GPU's lane
+  std::map<std::string, std::shared_ptr<DevState>> devs_;
+  std::mutex uuid_mu_;
+  std::map<uint64_t, std::string> uuid_of_bdf_;  // BDF order key -> UUID (read once)
   std::mutex evt_mu_;                   // held across the blocking event wait
+  std::mutex arm_mu_;                   // armed_handles_ / armed_for_
   std::atomic<bool> evt_live_{false};   // armed with at least one source
-  std::vector<std::vector<amdsmi_processor_handle>> procs_;
-  std::vector<uint64_t> bdf_keys_;  // physical-device BDF key per GPU index (procs_ order)
-  std::vector<GpuInfo> gpus_;
-  mutable std::mutex keys_mu_;       // keys_ only (never held across an amdsmi call)
-  std::vector<std::string> keys_;    // gpu_key per index of the latest discovery
+  std::atomic<bool> arm_wanted_{false};
+  std::atomic<int> armed_count_{0};
   std::vector<amdsmi_processor_handle> armed_handles_;
-  std::vector<amdsmi_processor_handle> armed_for_;  // processor set at arming time
-  bool armed_ = false;
-  bool want_rearm_ = false;
-  int reinits_ = 0;
-  bool closed_ = false;
+  std::vector<void*> armed_for_;        // processor set at arming time
+  std::atomic<int> reinits_{0};
 };
 
 std::shared_ptr<Backend> make_amdsmi_backend() { return std::make_shared<AmdSmiBackend>(); }

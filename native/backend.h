@@ -14,14 +14,19 @@
 
 #include <sys/socket.h>
 
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
+#include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <cctype>
 #include <string>
 #include <vector>
+
+#include "lanes.h"
 
 namespace amdgpu_dp {
 
@@ -68,6 +73,18 @@ inline std::string normalize_driver_version(const std::string& s) {
   return s;
 }
 
+// One accelerator partition profile the GPU supports
+// (amdsmi_get_gpu_accelerator_partition_profile_config).
+struct PartitionProfile {
+  std::string type;   // SPX/DPX/TPX/QPX/CPX
+  int partitions = 0;
+  uint32_t nps_caps = 0;  // memory modes allowed with it (bit0 NPS1 .. bit3 NPS8)
+  int index = -1;
+  // "driver": the driver's profile list (amdsmi_get_gpu_accelerator_partition_profile_config,
+  // needs root); "current": only the current profile is known (the list was not readable)
+  std::string source = "driver";
+};
+
 struct GpuInfo {
   int index = -1;
   std::string uuid;
@@ -86,6 +103,9 @@ struct GpuInfo {
   std::string partition_profile;
   int profile_partitions = 0;
   int profile_index = -1;
+  // Every profile the driver reports for the GPU (empty: not reported).
+  std::vector<PartitionProfile> supported_profiles;
+  std::string profiles_status;    // "ok", or why the driver's profile list was not read
   int num_compute_units = 0;
   uint32_t device_id = 0;         // PCI device id (0 = unknown)
   int oam_id = -1;                // OAM slot on the baseboard (-1 = not reported)
@@ -174,6 +194,9 @@ struct GpuSample {
   double pcie_recoveries = -1;      // accumulated L0 -> recovery transitions
   int num_partitions = 0;
   double partition_gfx_busy_pct[kMaxPartitions] = {};
+  // where partition_gfx_busy_pct[p] came from: 0 unavailable, 1 the partition's own
+  // metrics (amdsmi_get_gpu_partition_metrics_info), 2 the socket blob's xcp_stats[p]
+  int partition_busy_source[kMaxPartitions] = {};
   double partition_vram_used_bytes[kMaxPartitions] = {};
   bool ok = false;
 };
@@ -212,24 +235,95 @@ struct HwEvent {
   double value = 0;  // kEvtLinkQuality: the link's bandwidth now, Gb/s
 };
 
-class Backend {
+// A GPU as enumeration finds it, before any call that talks to the device: its identity
+// (which names its lane and its health state) and what the backend needs to reach it.
+struct DeviceRef {
+  std::string key;                 // stable identity (UUID, else BDF)
+  std::string bdf;
+  uint64_t order = 0;              // enumeration order (BDF)
+  std::vector<void*> handles;      // backend handles, partition order (amdsmi processors)
+  int slot = -1;                   // fixture slot
+};
+
+// The node as one discover() installed it.  Immutable once published: readers take a
+// reference and never lock anything a hardware call holds.
+struct Inventory {
+  uint64_t gen = 0;                // bumped by every discover()
+  uint64_t session = 0;            // hardware-library session the handles belong to
+  std::vector<DeviceRef> refs;     // index order
+  std::vector<GpuInfo> gpus;
+  int index_of(const std::string& key) const {
+    for (size_t i = 0; i < refs.size(); ++i)
+      if (refs[i].key == key) return static_cast<int>(i);
+    return -1;
+  }
+  std::string key_of(int gpu) const {
+    return gpu >= 0 && gpu < static_cast<int>(refs.size()) ? refs[gpu].key : std::string();
+  }
+};
+
+// What the last discover() could not read fresh.  A GPU whose lane is wedged (or whose
+// description did not arrive within the call bound) keeps the description of the last
+// discovery that reached it; one that no discovery ever reached is left out.
+struct DiscoveryReport {
+  struct Stale {
+    int index = -1;      // in the installed inventory (-1: left out)
+    std::string key;
+    std::string reason;
+  };
+  std::vector<Stale> stale;
+  double seconds = 0;
+  uint64_t gen = 0;
+  bool reinit_deferred = false;  // handles looked stale but a call was still inside the library
+};
+
+// One GPU's lane as seen from the inventory's index space.
+struct LaneReport {
+  int index = -1;
+  LaneState lane;
+};
+
+class Backend : public std::enable_shared_from_this<Backend> {
  public:
+  Backend();
   virtual ~Backend() = default;
   virtual std::string name() const = 0;
-  // (Re)discover GPUs/partitions/topology.  Throws std::runtime_error on failure.
-  virtual void discover(std::vector<GpuInfo>* gpus, Topology* topo) = 0;
-  // Telemetry for physical GPU `gpu`; returns false when unavailable.
-  virtual bool sample(int gpu, GpuSample* out) = 0;
+
+  // ---- what the plugin calls ----
+  // (Re)discover GPUs/partitions/topology.  Throws std::runtime_error when enumeration
+  // fails.  Every per-GPU query runs on that GPU's lane and is waited for at most the call
+  // bound (set_call_timeout_ms): a wedged GPU costs one bound once, then nothing (its lane
+  // refuses work), and is described from the previous discovery (last_discovery()).
+  void discover(std::vector<GpuInfo>* gpus, Topology* topo);
+  // Telemetry for GPU `gpu` (index of the latest discover()), waited for at most the call
+  // bound; false when unavailable or still in flight.
+  bool sample(int gpu, GpuSample* out);
+  // The same call without waiting: null when there is no such GPU or its lane refused the
+  // job (wedged).  The job fills *out; read it only once job->done() && !job->dropped().
+  std::shared_ptr<LaneJob> sample_async(int gpu, std::shared_ptr<GpuSample> out);
   // Stable identity (UUID, else BDF) of the GPU at index `gpu` of the latest discover(),
   // in the index space sample() and events use; "" when unknown.  Health state is keyed
   // by it: when a GPU drops off the bus and the node re-enumerates, every later GPU moves
-  // down one index, and its health must not move with the index.
-  virtual std::string gpu_key(int gpu) const { return ""; }
+  // down one index, and its health must not move with the index.  Never blocks.
+  virtual std::string gpu_key(int gpu) const;
+  std::shared_ptr<const Inventory> inventory() const;
+  DiscoveryReport last_discovery() const;
+  // Lanes of the inventory's GPUs (index order) and, after them, lanes of GPUs that left it
+  // with a call still in flight (index -1).
+  std::vector<LaneReport> lanes() const;
+  // mono ns at which the latest hardware call on any lane ended (0: none yet)
+  int64_t last_completion_ns() const;
+  void set_call_timeout_ms(int ms) { call_timeout_ms_.store(ms > 0 ? ms : 10000); }
+  int call_timeout_ms() const { return call_timeout_ms_.load(); }
+  // A lane whose call has been in flight longer than this takes no more work (0: never).
+  void set_stall_ms(int ms) { stall_ms_.store(ms > 0 ? ms : 0); }
+  int stall_ms() const { return stall_ms_.load(); }
+
   // Block up to timeout_ms for hardware events; append to *out.  Returns count.
   virtual int wait_events(int timeout_ms, std::vector<HwEvent>* out) = 0;
   // Arm event delivery for the discovered GPUs (idempotent).
   virtual void arm_events() {}
-  // Number of processors with hardware event delivery armed (0 = polling only).
+  // Number of processors with hardware event delivery armed (0 = polling only).  Never blocks.
   virtual int armed_event_sources() const { return 0; }
   // Drop cached device handles so the next discover() enumerates afresh (a compute
   // partition change creates new processors).  Returns false when not possible.
@@ -244,6 +338,59 @@ class Backend {
   };
   virtual std::vector<CallCost> sample_costs() const { return {}; }
   virtual void shutdown() {}
+
+ protected:
+  // ---- what a backend implements ----
+  // The GPUs present, in a stable order, without talking to any one device (amdsmi keeps
+  // its processor list from amdsmi_init).  Throws on failure.
+  virtual void enumerate(std::vector<DeviceRef>* refs) = 0;
+  // Everything discovery reads from one GPU, on that GPU's lane: its description (index
+  // fields are set by the caller) and its view of the link to each GPU of `all` (row[i]:
+  // the link to all[i]).  Throws (or leaves out->partitions empty) on failure.
+  virtual void describe(const DeviceRef& ref, const std::vector<DeviceRef>& all, GpuInfo* out,
+                        std::vector<Link>* row) = 0;
+  // One telemetry sample of inv.refs[index], on that GPU's lane.
+  virtual bool sample_device(const Inventory& inv, int index, GpuSample* out) = 0;
+  // Handles are out of date (e.g. amdsmi enumerates processors once, at init, and a
+  // compute-partition change created new ones): called with discovery's fresh
+  // descriptions; return true to have the library re-initialised (reopen_session) and
+  // the node enumerated again.
+  virtual bool handles_stale(const std::vector<GpuInfo>& described) { return false; }
+  // Re-initialises the hardware library with no call inside it (the gate is closed).
+  virtual bool reopen_session() { return false; }
+  // After an inventory was installed (the handles to arm event delivery on, say).
+  virtual void installed(const std::shared_ptr<const Inventory>& inv) {}
+
+  // Runs fn on the lane of `key` inside the library session (see SessionGate); waits at
+  // most ms.  false: refused (wedged lane, stale session) or not done in time.
+  bool run_on_lane(const std::string& key, const char* what, uint64_t session, std::function<void()> fn,
+                   int64_t ms);
+  // Same, without waiting: null when the lane refused it.
+  std::shared_ptr<LaneJob> post_job(const std::string& key, const char* what, uint64_t session,
+                                    std::function<void()> fn);
+  SessionGate& gate() { return gate_; }
+  LaneSet& lanes_set() { return lanes_; }
+
+ private:
+  struct Described {
+    GpuInfo info;
+    std::map<std::string, Link> links;  // peer key -> this GPU's view of the link
+  };
+  LaneSet lanes_;
+  SessionGate gate_;
+  std::atomic<int> call_timeout_ms_{10000};
+  std::atomic<int> stall_ms_{0};
+  std::atomic<int64_t> last_completion_ns_{0};
+  // one discovery at a time (a flag + condition: libstdc++'s timed mutex waits are not
+  // visible to GCC 11's ThreadSanitizer)
+  std::mutex discover_mu_;
+  std::condition_variable discover_cv_;
+  bool discovering_ = false;               // guarded by discover_mu_
+  std::map<std::string, Described> last_described_;  // by key; owned by the running discovery
+  mutable std::mutex inv_mu_;              // inv_ and report_ only, never held across a call
+  std::shared_ptr<const Inventory> inv_;
+  DiscoveryReport report_;
+  uint64_t gen_ = 0;                       // owned by the running discovery
 };
 
 std::shared_ptr<Backend> make_amdsmi_backend();

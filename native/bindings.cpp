@@ -52,6 +52,29 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("numa_node", &PartitionInfo::numa_node)
       .def_readwrite("vram_bytes", &PartitionInfo::vram_bytes);
 
+  py::class_<PartitionProfile>(m, "PartitionProfile")
+      .def(py::init([](const std::string& type, int partitions, uint32_t nps_caps, int index,
+                       const std::string& source) {
+             PartitionProfile p;
+             p.type = type;
+             p.partitions = partitions;
+             p.nps_caps = nps_caps;
+             p.index = index;
+             p.source = source;
+             return p;
+           }),
+           py::arg("type") = "", py::arg("partitions") = 0, py::arg("nps_caps") = 0, py::arg("index") = -1,
+           py::arg("source") = "driver")
+      .def_readwrite("source", &PartitionProfile::source)
+      .def_readwrite("type", &PartitionProfile::type)
+      .def_readwrite("partitions", &PartitionProfile::partitions)
+      .def_readwrite("nps_caps", &PartitionProfile::nps_caps)
+      .def_readwrite("index", &PartitionProfile::index)
+      .def("__repr__", [](const PartitionProfile& p) {
+        return "<PartitionProfile " + p.type + " x" + std::to_string(p.partitions) + " nps_caps=" +
+               std::to_string(p.nps_caps) + ">";
+      });
+
   py::class_<GpuInfo>(m, "GpuInfo")
       .def(py::init<>())
       .def_readwrite("index", &GpuInfo::index)
@@ -75,6 +98,8 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("vbios_version", &GpuInfo::vbios_version)
       .def_readwrite("num_xgmi_links", &GpuInfo::num_xgmi_links)
       .def_readwrite("bad_page_threshold", &GpuInfo::bad_page_threshold)
+      .def_readwrite("supported_profiles", &GpuInfo::supported_profiles)
+      .def_readwrite("profiles_status", &GpuInfo::profiles_status)
       .def_readwrite("partitions", &GpuInfo::partitions);
 
   py::class_<Link>(m, "Link")
@@ -159,6 +184,12 @@ PYBIND11_MODULE(_native, m) {
       })
       .def_property_readonly("partition_gfx_busy_pct", [](const GpuSample& s) {
         return std::vector<double>(s.partition_gfx_busy_pct, s.partition_gfx_busy_pct + s.num_partitions);
+      })
+      .def_property_readonly("partition_busy_source", [](const GpuSample& s) {
+        return std::vector<int>(s.partition_busy_source, s.partition_busy_source + s.num_partitions);
+      })
+      .def_property_readonly("partition_vram_used_bytes", [](const GpuSample& s) {
+        return std::vector<double>(s.partition_vram_used_bytes, s.partition_vram_used_bytes + s.num_partitions);
       });
 
   m.attr("EVT_PRE_RESET") = static_cast<int>(kEvtPreReset);
@@ -233,6 +264,32 @@ PYBIND11_MODULE(_native, m) {
              return py::cast(s);
            })
       .def("gpu_key", &Backend::gpu_key, py::call_guard<py::gil_scoped_release>())
+      .def("set_call_timeout_ms", &Backend::set_call_timeout_ms)
+      .def_property_readonly("call_timeout_ms", &Backend::call_timeout_ms)
+      .def("set_stall_ms", &Backend::set_stall_ms)
+      .def_property_readonly("stall_ms", &Backend::stall_ms)
+      .def("last_discovery",
+           [](const Backend& b) {
+             DiscoveryReport r = b.last_discovery();
+             py::dict d;
+             py::list stale;
+             for (const auto& s : r.stale) stale.append(py::make_tuple(s.index, s.key, s.reason));
+             d["stale"] = stale;
+             d["seconds"] = r.seconds;
+             d["generation"] = r.gen;
+             d["reinit_deferred"] = r.reinit_deferred;
+             return d;
+           })
+      .def("lanes",  // [(index, key, in-flight call or "", in flight s, completed, queued)]
+           [](const Backend& b) {
+             py::list out;
+             const int64_t now = mono_ns();
+             for (const auto& r : b.lanes())
+               out.append(py::make_tuple(r.index, r.lane.key, r.lane.inflight_what,
+                                         r.lane.inflight_since_ns ? (now - r.lane.inflight_since_ns) * 1e-9 : 0.0,
+                                         r.lane.completed, r.lane.queued));
+             return out;
+           })
       .def("arm_events", &Backend::arm_events, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("armed_event_sources", &Backend::armed_event_sources)
       .def("reinit", &Backend::reinit, py::call_guard<py::gil_scoped_release>())
@@ -255,6 +312,8 @@ PYBIND11_MODULE(_native, m) {
       .def("set_retired_pages", &FixtureBackend::set_retired_pages, py::arg("gpu"), py::arg("reserved"),
            py::arg("pending") = 0)
       .def("set_sample_stall", &FixtureBackend::set_sample_stall, py::call_guard<py::gil_scoped_release>())
+      .def("set_serialised", &FixtureBackend::set_serialised, py::arg("on"))
+      .def_property_readonly("serialised", &FixtureBackend::serialised)
       .def("set_gpu_present", &FixtureBackend::set_gpu_present)
       .def_property_readonly("discover_calls", &FixtureBackend::discover_calls);
 
@@ -491,18 +550,24 @@ PYBIND11_MODULE(_native, m) {
 
   // ---- exporter ----
   py::class_<PartitionLabel>(m, "PartitionLabel")
-      .def(py::init([](int gpu, int partition, const std::string& device_id, const std::string& resource) {
-        PartitionLabel l;
-        l.gpu = gpu;
-        l.partition = partition;
-        l.device_id = device_id;
-        l.resource = resource;
-        return l;
-      }));
+      .def(py::init([](int gpu, int partition, const std::string& device_id, const std::string& resource,
+                       const std::string& hip_ids) {
+             PartitionLabel l;
+             l.gpu = gpu;
+             l.partition = partition;
+             l.device_id = device_id;
+             l.resource = resource;
+             l.hip_ids = hip_ids;
+             return l;
+           }),
+           py::arg("gpu"), py::arg("partition"), py::arg("device_id"), py::arg("resource"), py::arg("hip_ids") = "");
 
   py::class_<Exporter, std::shared_ptr<Exporter>>(m, "Exporter")
       .def("set_stall_ms", &Exporter::set_stall_ms)
       .def_property_readonly("stalled_gpu", &Exporter::stalled_gpu)
+      .def_property_readonly("stalled_gpus", &Exporter::stalled_gpus)
+      .def_property_readonly("blocked_gpus", &Exporter::blocked_gpus)
+      .def("sample_age_s", &Exporter::sample_age_s)
       .def(py::init<>())
       .def("set_inventory", &Exporter::set_inventory)
       .def("set_partition_labels", &Exporter::set_partition_labels)

@@ -20,41 +20,46 @@ double unit(uint64_t x) { return (mix(x) >> 11) * (1.0 / 9007199254740992.0); }
 
 FixtureBackend::FixtureBackend(uint64_t seed) : seed_(seed), t0_ns_(mono_ns()) {}
 
-int FixtureBackend::slot_of_locked(int index) const {
-  if (view_.empty()) return index >= 0 && index < static_cast<int>(gpus_.size()) ? index : -1;
-  return index >= 0 && index < static_cast<int>(view_.size()) ? view_[index] : -1;
-}
-
-int FixtureBackend::index_of_locked(int slot) const {
-  if (view_.empty()) return slot;
-  for (size_t i = 0; i < view_.size(); ++i)
-    if (view_[i] == slot) return static_cast<int>(i);
-  return -1;
-}
-
 std::string FixtureBackend::key_of_slot_locked(int slot) const {
   if (slot < 0 || slot >= static_cast<int>(gpus_.size())) return "";
   return gpus_[slot].uuid.empty() ? "fixture-gpu-" + std::to_string(slot) : gpus_[slot].uuid;
 }
 
-void FixtureBackend::translate_locked(HwEvent* e) const {
+void FixtureBackend::translate(HwEvent* e) const {  // mu_ held
+  auto inv = inventory();
+  auto index_of_slot = [&](int slot) {
+    // identity until the first discovery, like an amdsmi session's enumeration order
+    if (inv->refs.empty()) return slot;
+    for (size_t i = 0; i < inv->refs.size(); ++i)
+      if (inv->refs[i].slot == slot) return static_cast<int>(i);
+    return -1;
+  };
   if (e->gpu >= 0) {
     e->key = key_of_slot_locked(e->gpu);
-    e->gpu = index_of_locked(e->gpu);
+    e->gpu = index_of_slot(e->gpu);
   }
   if (e->peer >= 0) {
     e->peer_key = key_of_slot_locked(e->peer);
-    e->peer = index_of_locked(e->peer);
+    e->peer = index_of_slot(e->peer);
   }
 }
 
 std::string FixtureBackend::gpu_key(int gpu) const {
+  if (!inventory()->refs.empty()) return Backend::gpu_key(gpu);
   std::lock_guard<std::mutex> lk(mu_);
-  return key_of_slot_locked(slot_of_locked(gpu));
+  return gpu >= 0 && gpu < static_cast<int>(gpus_.size()) && present_[gpu] ? key_of_slot_locked(gpu) : "";
+}
+
+std::unique_lock<std::mutex> FixtureBackend::device_call(int slot) {
+  std::unique_lock<std::mutex> lk(serialised_.load() ? driver_mu_ : dev_mu_[slot >= 0 ? slot % kMaxGpus : 0]);
+  std::unique_lock<std::mutex> w(wedge_mu_);
+  wedge_cv_.wait(w, [&] { return unwedge_all_ || slot >= static_cast<int>(wedged_.size()) || !wedged_[slot]; });
+  return lk;
 }
 
 void FixtureBackend::add_gpu(const GpuInfo& g) {
   std::lock_guard<std::mutex> lk(mu_);
+  if (gpus_.size() >= static_cast<size_t>(kMaxGpus)) throw std::length_error("fixture: too many GPUs");
   GpuInfo copy = g;
   copy.index = static_cast<int>(gpus_.size());
   for (auto& p : copy.partitions) p.gpu = copy.index;
@@ -67,7 +72,6 @@ void FixtureBackend::add_gpu(const GpuInfo& g) {
   pcie_.emplace_back(16, 32.0);
   pages_.emplace_back(0, 0);
   present_.push_back(true);
-  if (!view_.empty()) view_.clear();  // a changed node: identity until it is discovered again
 }
 
 void FixtureBackend::replace_gpu(int index, const GpuInfo& g) {
@@ -87,11 +91,13 @@ void FixtureBackend::clear() {
   pcie_.clear();
   pages_.clear();
   present_.clear();
-  stalled_.clear();
-  view_.clear();
   scheduled_.clear();
   pending_.clear();
-  cv_.notify_all();  // a sample() parked on a stall returns (its GPU is gone)
+  {
+    std::lock_guard<std::mutex> w(wedge_mu_);
+    wedged_.clear();  // a call parked on a wedge returns (its GPU is gone)
+  }
+  wedge_cv_.notify_all();
 }
 
 void FixtureBackend::set_link(int a, int b, const Link& l) {
@@ -146,10 +152,13 @@ void FixtureBackend::set_sample_stall(int gpu, bool stall) {
   {
     std::lock_guard<std::mutex> lk(mu_);
     if (gpu < 0 || gpu >= static_cast<int>(gpus_.size())) throw std::out_of_range("bad gpu");
-    if (stalled_.size() < gpus_.size()) stalled_.resize(gpus_.size(), false);
-    stalled_[gpu] = stall;
   }
-  cv_.notify_all();
+  {
+    std::lock_guard<std::mutex> w(wedge_mu_);
+    if (wedged_.size() <= static_cast<size_t>(gpu)) wedged_.resize(gpu + 1, false);
+    wedged_[gpu] = stall;
+  }
+  wedge_cv_.notify_all();
 }
 
 void FixtureBackend::set_gpu_present(int gpu, bool present) {
@@ -158,37 +167,45 @@ void FixtureBackend::set_gpu_present(int gpu, bool present) {
   present_[gpu] = present;
 }
 
-void FixtureBackend::discover(std::vector<GpuInfo>* gpus, Topology* topo) {
+void FixtureBackend::enumerate(std::vector<DeviceRef>* refs) {
+  discover_calls_.fetch_add(1);
+  if (fail_discovery_.load()) throw std::runtime_error("fixture: discovery failure injected");
   std::lock_guard<std::mutex> lk(mu_);
-  ++discover_calls_;
-  if (fail_discovery_) throw std::runtime_error("fixture: discovery failure injected");
-  gpus->clear();
-  // A GPU that "fell off the bus" disappears from discovery, like a real one, and every
-  // later GPU moves down one index (amdsmi enumerates in BDF order).
-  std::vector<int> remap(gpus_.size(), -1);
-  view_.clear();
+  // A GPU that "fell off the bus" is not enumerated, like a real one, and every later GPU
+  // moves down one index (amdsmi enumerates in BDF order).
   for (size_t i = 0; i < gpus_.size(); ++i) {
     if (!present_[i]) continue;
-    remap[i] = static_cast<int>(gpus->size());
-    view_.push_back(static_cast<int>(i));
-    GpuInfo g = gpus_[i];
-    g.index = remap[i];
-    for (auto& p : g.partitions) p.gpu = g.index;
-    gpus->push_back(std::move(g));
+    DeviceRef r;
+    r.key = key_of_slot_locked(static_cast<int>(i));
+    r.bdf = gpus_[i].bdf;
+    r.order = i;
+    r.slot = static_cast<int>(i);
+    refs->push_back(std::move(r));
   }
-  topo->resize(static_cast<int>(gpus->size()));
-  for (size_t a = 0; a < gpus_.size(); ++a)
-    for (size_t b = 0; b < gpus_.size(); ++b)
-      if (remap[a] >= 0 && remap[b] >= 0) topo->at(remap[a], remap[b]) = topo_.at(a, b);
 }
 
-bool FixtureBackend::sample(int index, GpuSample* s) {
-  std::unique_lock<std::mutex> lk(mu_);
-  const int gpu = slot_of_locked(index);
-  s->key = key_of_slot_locked(gpu);
+void FixtureBackend::describe(const DeviceRef& ref, const std::vector<DeviceRef>& all, GpuInfo* out,
+                              std::vector<Link>* row) {
+  auto call = device_call(ref.slot);
+  std::lock_guard<std::mutex> lk(mu_);
+  if (ref.slot < 0 || ref.slot >= static_cast<int>(gpus_.size()) || !present_[ref.slot])
+    throw std::runtime_error("fixture: GPU " + std::to_string(ref.slot) + " is gone");
+  *out = gpus_[ref.slot];
+  row->assign(all.size(), Link{});
+  for (size_t p = 0; p < all.size(); ++p)
+    if (all[p].slot >= 0 && all[p].slot < topo_.n && all[p].slot != ref.slot) (*row)[p] = topo_.at(ref.slot, all[p].slot);
+}
+
+bool FixtureBackend::sample_device(const Inventory& inv, int index, GpuSample* s) {
+  const int gpu = inv.refs[index].slot;
+  auto call = device_call(gpu);
+  std::lock_guard<std::mutex> lk(mu_);
   if (gpu < 0 || gpu >= static_cast<int>(gpus_.size()) || !present_[gpu]) return false;
-  cv_.wait(lk, [&] { return shutdown_ || gpu >= static_cast<int>(stalled_.size()) || !stalled_[gpu]; });
-  if (gpu >= static_cast<int>(gpus_.size()) || !present_[gpu]) return false;
+  auto index_of_slot = [&](int slot) {
+    for (size_t i = 0; i < inv.refs.size(); ++i)
+      if (inv.refs[i].slot == slot) return static_cast<int>(i);
+    return -1;
+  };
   const GpuInfo& g = gpus_[gpu];
   const int64_t t = now_ns();
   const double ts = (mono_ns() - t0_ns_) * 1e-9;  // seconds since the fixture was created
@@ -226,7 +243,7 @@ bool FixtureBackend::sample(int index, GpuSample* s) {
   for (int peer = 0; peer < topo_.n && s->num_links < kMaxXgmiLinks; ++peer) {
     if (peer == gpu || topo_.at(gpu, peer).type != kLinkXgmi) continue;
     const int k = s->num_links++;
-    s->link_peer[k] = index_of_locked(peer);  // -1 while the peer is not discovered
+    s->link_peer[k] = index_of_slot(peer);  // -1 while the peer is not discovered
     s->link_up[k] = topo_.at(gpu, peer).up ? 1 : 0;
     s->link_read_kb[k] = 1e6 * ts * load;
     s->link_write_kb[k] = 0.9e6 * ts * load;
@@ -239,6 +256,7 @@ bool FixtureBackend::sample(int index, GpuSample* s) {
   s->num_partitions = std::min<int>(static_cast<int>(g.partitions.size()), kMaxPartitions);
   for (int p = 0; p < s->num_partitions; ++p) {
     s->partition_gfx_busy_pct[p] = 100.0 * (0.5 + 0.45 * std::sin(ts * 0.7 + gpu + 0.3 * p));
+    s->partition_busy_source[p] = 1;  // as the partition metrics API reports it
     s->partition_vram_used_bytes[p] = s->vram_used_bytes / std::max(1, s->num_partitions);
   }
   s->ok = true;
@@ -247,7 +265,7 @@ bool FixtureBackend::sample(int index, GpuSample* s) {
 
 void FixtureBackend::arm_events() {
   std::lock_guard<std::mutex> lk(mu_);
-  armed_at_ns_ = mono_ns();
+  armed_at_ns_.store(mono_ns());
   shutdown_ = false;
 }
 
@@ -277,6 +295,11 @@ void FixtureBackend::shutdown() {
     shutdown_ = true;
   }
   cv_.notify_all();
+  {
+    std::lock_guard<std::mutex> w(wedge_mu_);
+    unwedge_all_ = true;
+  }
+  wedge_cv_.notify_all();
 }
 
 int FixtureBackend::wait_events(int timeout_ms, std::vector<HwEvent>* out) {
@@ -284,8 +307,9 @@ int FixtureBackend::wait_events(int timeout_ms, std::vector<HwEvent>* out) {
   const int64_t deadline = mono_ns() + static_cast<int64_t>(timeout_ms) * 1000000;
   for (;;) {
     // promote due scheduled events
-    if (armed_at_ns_ != 0) {
-      const double elapsed = (mono_ns() - armed_at_ns_) * 1e-9;
+    const int64_t armed_at = armed_at_ns_.load();
+    if (armed_at != 0) {
+      const double elapsed = (mono_ns() - armed_at) * 1e-9;
       while (!scheduled_.empty() && scheduled_.front().delay_s <= elapsed) {
         HwEvent e = scheduled_.front().ev;
         e.ts_ns = now_ns();
@@ -304,7 +328,7 @@ int FixtureBackend::wait_events(int timeout_ms, std::vector<HwEvent>* out) {
       while (!pending_.empty()) {
         HwEvent e = pending_.front();
         pending_.pop_front();
-        translate_locked(&e);
+        translate(&e);
         out->push_back(std::move(e));
         ++n;
       }
@@ -314,8 +338,8 @@ int FixtureBackend::wait_events(int timeout_ms, std::vector<HwEvent>* out) {
     const int64_t now = mono_ns();
     if (now >= deadline) return 0;
     int64_t wait_ns = deadline - now;
-    if (armed_at_ns_ != 0 && !scheduled_.empty()) {
-      const int64_t due = armed_at_ns_ + static_cast<int64_t>(scheduled_.front().delay_s * 1e9);
+    if (armed_at != 0 && !scheduled_.empty()) {
+      const int64_t due = armed_at + static_cast<int64_t>(scheduled_.front().delay_s * 1e9);
       wait_ns = std::min<int64_t>(wait_ns, std::max<int64_t>(0, due - now));
     }
     cv_wait_ms(cv_, lk, wait_ns / 1000000 + 1, [&] { return !pending_.empty() || shutdown_; });

@@ -2,6 +2,13 @@
 // an xGMI link matrix with per-link health, deterministic telemetry generators and
 // timed fault scripts.  The reference has no fake NVML at all; this is
 // the seam every CPU test and the BASELINE "Mock-device backend" config run on.
+//
+// A wedged driver is modelled by the lock it holds.  Every call that talks to one GPU
+// (describe at discovery, a telemetry sample) holds a "driver lock" for its duration:
+// per device by default (rocm_smi's per-device mutex), or one lock for the whole library
+// (set_serialised(true)).  A wedged GPU's call blocks while holding that lock, so in the
+// serialised model every later call to any GPU waits behind it, exactly as it would in a
+// library that serialises all devices.
 #pragma once
 
 #include <condition_variable>
@@ -14,16 +21,14 @@ namespace amdgpu_dp {
 
 class FixtureBackend : public Backend {
  public:
+  static constexpr int kMaxGpus = 64;
   explicit FixtureBackend(uint64_t seed = 1);
   std::string name() const override { return "fixture"; }
-  void discover(std::vector<GpuInfo>* gpus, Topology* topo) override;
-  // `gpu` is an index of the latest discover(), like amdsmi's: after a GPU vanished and
-  // the node was re-discovered, index k samples the GPU that moved to k.
-  bool sample(int gpu, GpuSample* out) override;
+  // before the first discovery, index = slot (like an amdsmi session's enumeration order)
   std::string gpu_key(int gpu) const override;
   int wait_events(int timeout_ms, std::vector<HwEvent>* out) override;
   void arm_events() override;
-  int armed_event_sources() const override { return armed_at_ns_ != 0 ? 1 : 0; }
+  int armed_event_sources() const override { return armed_at_ns_.load() != 0 ? 1 : 0; }
   void shutdown() override;
 
   // --- configuration (called before / between discoveries) ---
@@ -48,13 +53,26 @@ class FixtureBackend : public Backend {
   void set_retired_pages(int gpu, int64_t reserved, int64_t pending);
   void set_pcie_link(int gpu, int width, double gts);  // the host link as gpu_metrics reports it
   void set_gpu_present(int gpu, bool present);
-  // A wedged driver: sample(gpu) blocks until the stall is lifted (or shutdown), the way
-  // an amdsmi call can hang on a GPU that stopped responding.
+  // A wedged driver: every call to `gpu` (sample, describe) blocks, holding its driver
+  // lock, until the wedge is lifted (or shutdown) - the way an amdsmi call can hang on a
+  // GPU that stopped responding.
   void set_sample_stall(int gpu, bool stall);
-  int discover_calls() const { return discover_calls_; }
+  // One driver lock for all GPUs (a library that serialises every device) instead of one
+  // per GPU.  Set it while no call is in flight.
+  void set_serialised(bool on) { serialised_.store(on); }
+  bool serialised() const { return serialised_.load(); }
+  int discover_calls() const { return discover_calls_.load(); }
+
+ protected:
+  void enumerate(std::vector<DeviceRef>* refs) override;
+  void describe(const DeviceRef& ref, const std::vector<DeviceRef>& all, GpuInfo* out,
+                std::vector<Link>* row) override;
+  bool sample_device(const Inventory& inv, int index, GpuSample* out) override;
 
  private:
-  mutable std::mutex mu_;
+  // Held for the duration of one device call; blocks while the GPU is wedged.
+  std::unique_lock<std::mutex> device_call(int slot);
+  mutable std::mutex mu_;  // fixture state; never held while a device call waits
   std::condition_variable cv_;
   std::vector<GpuInfo> gpus_;
   Topology topo_;
@@ -68,18 +86,22 @@ class FixtureBackend : public Backend {
   std::vector<std::pair<int, double>> pcie_;  // (lanes, GT/s) per GPU
   std::vector<std::pair<int64_t, int64_t>> pages_;  // (reserved, pending) per GPU
   std::vector<bool> present_;
-  std::vector<bool> stalled_;
-  std::vector<int> view_;  // latest discover(): index -> slot (identity until the first)
-  int slot_of_locked(int index) const;
-  int index_of_locked(int slot) const;
   std::string key_of_slot_locked(int slot) const;
-  void translate_locked(HwEvent* e) const;  // slot -> discovered index, plus keys
-  int64_t armed_at_ns_ = 0;
+  void translate(HwEvent* e) const;  // slot -> discovered index, plus keys
+  std::atomic<int64_t> armed_at_ns_{0};
   uint64_t seed_;
   int64_t t0_ns_;
-  bool fail_discovery_ = false;
-  bool shutdown_ = false;
-  int discover_calls_ = 0;
+  std::atomic<bool> fail_discovery_{false};
+  bool shutdown_ = false;  // guarded by mu_
+  std::atomic<int> discover_calls_{0};
+  // driver locks and wedges
+  std::atomic<bool> serialised_{false};
+  std::mutex driver_mu_;              // the one lock of the serialised model
+  std::mutex dev_mu_[kMaxGpus];       // per-GPU locks of the default model
+  std::mutex wedge_mu_;
+  std::condition_variable wedge_cv_;
+  std::vector<bool> wedged_;          // guarded by wedge_mu_
+  bool unwedge_all_ = false;          // shutdown: guarded by wedge_mu_
 };
 
 }  // namespace amdgpu_dp

@@ -47,12 +47,22 @@ void HealthMonitor::set_gpu_count(int n) {
 }
 
 void HealthMonitor::start() {
-  std::lock_guard<std::mutex> lk(mu_);
-  if (running_) return;
-  stop_ = false;
-  running_ = true;
-  backend_->arm_events();
-  thread_ = std::thread([this] { loop(); });
+  auto armed = std::make_shared<ThreadExitFlag>();
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (running_) return;
+    stop_ = false;
+    running_ = true;
+    // arming talks to every GPU (on their lanes, bounded): the event thread does it, so
+    // nothing that needs mu_ waits on a wedged GPU
+    thread_ = std::thread([this, armed] {
+      backend_->arm_events();
+      armed->set();
+      loop();
+    });
+  }
+  // the caller reads armed_event_sources() next: give arming a short, bounded wait
+  armed->wait(std::min(2000, backend_->call_timeout_ms()));
 }
 
 void HealthMonitor::stop() {

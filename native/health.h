@@ -53,6 +53,24 @@ struct HealthUpdate {
   double link_gbps = 0;  // kEvtLinkQuality: the link's trained bandwidth now
 };
 
+// A one-shot flag another thread can wait on with a bound.
+struct ThreadExitFlag {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool done = false;
+  void set() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      done = true;
+    }
+    cv.notify_all();
+  }
+  bool wait(int ms) {
+    std::unique_lock<std::mutex> lk(mu);
+    return cv_wait_ms(cv, lk, ms, [&] { return done; });
+  }
+};
+
 class HealthMonitor {
  public:
   explicit HealthMonitor(std::shared_ptr<Backend> backend, int lost_after_failures = 3);

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <map>
 #include <stdexcept>
 #include <cstdio>
 #include <cstring>
@@ -66,6 +67,8 @@ Exporter::Exporter()
   start_time_s_ = now_ns() / 1000000000LL;
   extra_ = std::make_shared<const std::string>();
   gpu_text_ = std::make_shared<const std::string>();
+  fresh_ = std::make_shared<const Freshness>();
+  stalls_ = std::make_shared<const Stalls>();
   std::lock_guard<std::mutex> lk(mu_);
   publish_view_locked();
 }
@@ -158,13 +161,14 @@ void Exporter::start(std::shared_ptr<Backend> backend, int interval_ms, std::sha
   sampler_exit_ = std::make_shared<ThreadExit>();
   {
     std::lock_guard<std::mutex> lk(run_mu_);
-    if (monitor_) watchdog_ = std::thread([this, m = monitor_] { watchdog_loop(m); });  // before the first call
+    watchdog_ = std::thread([this, m = monitor_] { watchdog_loop(m); });  // before the first call
   }
   thread_ = std::thread(sampler_main, std::move(weak), sampler_exit_, gen, interval);
-  // /metrics is normally populated before start() returns, but a first amdsmi call that
-  // hangs (a wedged driver at start-up) must not keep the caller - the plugin manager,
-  // which still has kubelet restarts, /restart and health events to handle - from
-  // going on: wait for the first pass at most the stall threshold.
+  // /metrics is normally populated before start() returns.  The first pass waits on the
+  // lanes at most its budget (a wedged driver at start-up stalls one lane, not the pass),
+  // and start() waits for the first pass at most the stall threshold: the caller - the
+  // plugin manager, which has kubelet restarts, /restart and health events to handle -
+  // goes on either way.
   const int ms = stall_ms_.load();
   std::unique_lock<std::mutex> lk(first_mu_);
   cv_wait_ms(first_cv_, lk, ms > 0 ? ms : 10000, [&] { return first_done_; });
@@ -200,39 +204,93 @@ void Exporter::stop() {
     thread_.detach();
     return;
   }
-  // The sampler leaves its loop within one sleep slice, unless it is inside a backend
-  // call.  A call in flight past the stall threshold may never return (wedged driver):
-  // do not hang shutdown on it.  The sampler holds its own reference to this exporter
-  // for the whole pass, so leaving it behind is safe; it exits when the call returns.
-  const int ms = stall_ms_.load();
-  if (sampler_exit_->wait(ms > 0 ? ms + 200 : -1)) {
-    thread_.join();
-  } else {
-    abandoned_.fetch_add(1);
-    thread_.detach();
-  }
+  // The sampler never blocks in a hardware call (it waits on lane jobs in short slices),
+  // so it leaves within one slice; a call wedged on a lane stays with the lane.
+  sampler_exit_->wait(-1);
+  thread_.join();
 }
 
+int Exporter::stalled_gpu() const {
+  std::shared_ptr<const Stalls> st;
+  {
+    std::lock_guard<SpinLock> lk(fresh_lock_);
+    st = stalls_;
+  }
+  return st->stalled.empty() ? -1 : *std::min_element(st->stalled.begin(), st->stalled.end());
+}
+
+std::vector<int> Exporter::stalled_gpus() const {
+  std::lock_guard<SpinLock> lk(fresh_lock_);
+  return stalls_->stalled;
+}
+
+std::vector<int> Exporter::blocked_gpus() const {
+  std::lock_guard<SpinLock> lk(fresh_lock_);
+  return stalls_->blocked;
+}
+
+double Exporter::sample_age_s(int gpu) const {
+  std::shared_ptr<const Freshness> f;
+  {
+    std::lock_guard<SpinLock> lk(fresh_lock_);
+    f = fresh_;
+  }
+  for (const auto& kv : f->last_ok)
+    if (kv.first == gpu) return kv.second ? (mono_ns() - kv.second) * 1e-9 : -1.0;
+  return -1.0;
+}
+
+// Lanes whose call has been in flight past the threshold.  The one stuck longest is the
+// culprit.  Another is reported as well only if some call completed after its own call
+// had been in flight for a grace period - proof that the library is not serialised behind
+// the first wedge, so this GPU is stuck on its own; otherwise it is only waiting behind
+// the first (a library that serialises every device) and is reported "blocked".  Each
+// stuck call is reported once; the GPU recovers through on_sample once a sample returns.
 void Exporter::watchdog_loop(std::shared_ptr<HealthMonitor> monitor) {
+  std::map<std::string, int64_t> reported;  // key -> since of the call reported lost
   while (!stop_.load()) {
-    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    std::this_thread::sleep_for(std::chrono::milliseconds(25));
     const int ms = stall_ms_.load();
-    if (ms <= 0) continue;
-    // Under inflight_mu_, which the sampler also takes to end a call: either the call
-    // is still in flight while the GPU is reported lost here (and the sampler's
-    // on_sample, which recovers it, comes after), or it has ended and nothing is reported.
-    std::lock_guard<std::mutex> lk(inflight_mu_);
-    const int g = inflight_gpu_.load();
-    if (g < 0 || stalled_gpu_.load() == g) continue;
-    const int64_t age = mono_ns() - inflight_since_.load();
-    if (age <= static_cast<int64_t>(ms) * 1000000) continue;
-    stalled_gpu_.store(g);
-    HwEvent e;
-    e.kind = kEvtDeviceLost;
-    e.gpu = g;
-    e.key = inflight_key_;  // the GPU the call went to, even if the node was re-enumerated since
-    e.message = "telemetry call in flight for " + std::to_string(age / 1000000) + " ms (health.sampleStallS)";
-    monitor->process(e);  // the GPU recovers through on_sample once the call returns ok
+    std::shared_ptr<Backend> be;
+    {
+      std::lock_guard<std::mutex> lk(run_mu_);
+      be = backend_;
+    }
+    if (ms <= 0 || !be) continue;
+    const int64_t now = mono_ns();
+    const int64_t threshold = static_cast<int64_t>(ms) * 1000000;
+    const int64_t grace = std::min<int64_t>(threshold / 2, 200000000);
+    const int64_t last_done = be->last_completion_ns();
+    std::vector<LaneReport> stuck;
+    for (auto& r : be->lanes())
+      if (r.index >= 0 && r.lane.inflight_since_ns && now - r.lane.inflight_since_ns > threshold) stuck.push_back(r);
+    int64_t root = 0;
+    for (const auto& r : stuck) root = root ? std::min(root, r.lane.inflight_since_ns) : r.lane.inflight_since_ns;
+    auto st = std::make_shared<Stalls>();
+    std::map<std::string, int64_t> still;
+    for (const auto& r : stuck) {
+      const int64_t since = r.lane.inflight_since_ns;
+      if (since != root && last_done <= since + grace) {
+        st->blocked.push_back(r.index);
+        continue;
+      }
+      st->stalled.push_back(r.index);
+      still[r.lane.key] = since;
+      auto it = reported.find(r.lane.key);
+      if (it != reported.end() && it->second == since) continue;
+      HwEvent e;
+      e.kind = kEvtDeviceLost;
+      e.gpu = r.index;
+      e.key = r.lane.key;  // the GPU the call went to, even if the node was re-enumerated since
+      e.message = r.lane.inflight_what + " call in flight for " + std::to_string((now - since) / 1000000) +
+                  " ms (health.sampleStallS)";
+      if (monitor) monitor->process(e);
+    }
+    reported.swap(still);
+    std::sort(st->stalled.begin(), st->stalled.end());
+    std::sort(st->blocked.begin(), st->blocked.end());
+    std::lock_guard<SpinLock> lk(fresh_lock_);
+    stalls_ = std::move(st);
   }
 }
 
@@ -281,53 +339,103 @@ void Exporter::sample_once(uint64_t sampler_gen) {
   if (sampler_gen != 0 && sampler_gen_.load() != sampler_gen) return;
   std::shared_ptr<Backend> be;
   std::shared_ptr<HealthMonitor> mon;
+  int interval;
   {
     std::lock_guard<std::mutex> lk(run_mu_);
     be = backend_;
     mon = monitor_;
+    interval = interval_ms_;
   }
   // The inventory may be a subset of the node (`devices: "4-7"`): sample, report health
   // for and label each GPU by its backend index, never by its position in the subset.
-  std::vector<int> index;
   uint64_t gen;
+  std::vector<int> index;
   {
     std::lock_guard<std::mutex> lk(mu_);
     for (const auto& g : gpus_) index.push_back(g.index);
     gen = inventory_gen_;
   }
-  const size_t n = index.size();
-  std::vector<GpuSample> samples(n);
-  std::vector<char> ok(n, 0);
+  if (gen != slots_gen_) {  // a reload: samples in flight belong to the old indices
+    slots_.assign(index.size(), Slot{});
+    for (size_t g = 0; g < index.size(); ++g) slots_[g].index = index[g];
+    slots_gen_ = gen;
+  }
+  const size_t n = slots_.size();
   const int64_t t0 = mono_ns();
-  for (size_t g = 0; g < n; ++g) {
-    // the sampler thread's pass ends early once stop() is waiting (or another sampler
-    // generation has started): no more backend calls
-    if (sampler_gen != 0 && (stop_.load() || sampler_gen_.load() != sampler_gen)) return;
-    if (be) {
-      std::string key = be->gpu_key(index[g]);  // outside inflight_mu_: the backend takes its own lock
-      {
-        std::lock_guard<std::mutex> lk(inflight_mu_);
-        inflight_key_ = std::move(key);
-        inflight_since_.store(mono_ns());
-        inflight_gpu_.store(index[g]);
-      }
-      ok[g] = be->sample(index[g], &samples[g]) ? 1 : 0;
-      {
-        std::lock_guard<std::mutex> lk(inflight_mu_);
-        inflight_gpu_.store(-1);
-        if (stalled_gpu_.load() == index[g]) stalled_gpu_.store(-1);
-      }
-      // left behind by stop() while this call hung, and the exporter was restarted
-      // meanwhile: this pass belongs to no one any more
-      if (sampler_gen != 0 && sampler_gen_.load() != sampler_gen) return;
+  // One call in flight at a time, GPU after GPU: each sample is waited for a slice of the
+  // pass budget, then left pending on its lane (collected by a later pass) while the walk
+  // goes on.  A GPU whose sample is still out from an earlier pass is skipped, not waited
+  // for again.  Walking instead of posting all at once keeps the stall attribution exact:
+  // in a library that serialises devices, a call posted in parallel can start before the
+  // one that wedges and then wait behind it, and "stuck longest" would name the wrong GPU.
+  // 8 GPUs x ~1-5 ms per amdsmi sample fits a 1 s tick many times over.
+  const int stall = stall_ms_.load();
+  const int64_t budget_ms = sampler_gen != 0 ? std::max(1, std::min(interval, stall > 0 ? stall : interval))
+                                             : (stall > 0 ? stall : (be ? be->call_timeout_ms() : 1000));
+  const int64_t slice_ms = std::max<int64_t>(2, budget_ms / std::max<size_t>(1, n));
+  for (size_t g = 0; g < n && be; ++g) {
+    Slot& sl = slots_[g];
+    if (sl.job && !sl.job->done()) continue;
+    sl.out = std::make_shared<GpuSample>();
+    sl.job = be->sample_async(sl.index, sl.out);
+    sl.posted_ns = mono_ns();
+    const int64_t until = mono_ns() + slice_ms * 1000000;
+    while (sl.job && !sl.job->done()) {  // in short waits, so stop() stays prompt
+      const int64_t left = (until - mono_ns()) / 1000000;
+      if (left <= 0) break;
+      if (sampler_gen != 0 && (stop_.load() || sampler_gen_.load() != sampler_gen)) return;
+      sl.job->wait(std::min<int64_t>(left, 50));
     }
-    if (!ok[g]) sample_errors_.fetch_add(1, std::memory_order_relaxed);
-    if (mon) mon->on_sample(index[g], ok[g], samples[g]);
+  }
+  std::vector<GpuSample> samples(n);
+  std::vector<char> ok(n, 0), fresh(n, 0);
+  const int64_t now = mono_ns();
+  for (size_t g = 0; g < n; ++g) {
+    Slot& sl = slots_[g];
+    if (sl.job && sl.job->done()) {
+      const bool good = !sl.job->dropped() && sl.out->ok;
+      sl.last = *sl.out;
+      sl.last_ok = good;
+      if (good) sl.last_ok_ns = now;
+      fresh[g] = 1;
+      sl.job.reset();
+    }
+    // a sample is shown while its GPU's newer call is still within the budget; not once
+    // that call is stuck (the values would pass for current)
+    const bool stuck = sl.job && stall > 0 && now - sl.posted_ns > static_cast<int64_t>(stall) * 1000000;
+    ok[g] = sl.last_ok && !stuck && sl.last_ok_ns != 0;
+    samples[g] = sl.last;
+  }
+  for (size_t g = 0; g < n; ++g) {
+    if (!fresh[g]) continue;
+    const bool good = slots_[g].last_ok;
+    if (!good) sample_errors_.fetch_add(1, std::memory_order_relaxed);
+    if (mon) mon->on_sample(slots_[g].index, good, slots_[g].last);
   }
   const double dt = (mono_ns() - t0) * 1e-9;
   if (be) {
     sample_hist_.observe(dt);
     samples_.fetch_add(1, std::memory_order_relaxed);
+  }
+  auto f = std::make_shared<Freshness>();
+  for (const auto& sl : slots_) f->last_ok.emplace_back(sl.index, sl.last_ok_ns);
+  {
+    std::lock_guard<SpinLock> lk(fresh_lock_);
+    fresh_ = std::move(f);
+    // a GPU whose call came back is no longer stalled or blocked (the watchdog would say
+    // so at its next look; a reader must not see the stale verdict meanwhile)
+    auto returned = [&](int gpu) {
+      for (size_t g = 0; g < n; ++g)
+        if (fresh[g] && slots_[g].index == gpu) return true;
+      return false;
+    };
+    if (std::any_of(stalls_->stalled.begin(), stalls_->stalled.end(), returned) ||
+        std::any_of(stalls_->blocked.begin(), stalls_->blocked.end(), returned)) {
+      auto st = std::make_shared<Stalls>(*stalls_);
+      st->stalled.erase(std::remove_if(st->stalled.begin(), st->stalled.end(), returned), st->stalled.end());
+      st->blocked.erase(std::remove_if(st->blocked.begin(), st->blocked.end(), returned), st->blocked.end());
+      stalls_ = std::move(st);
+    }
   }
   last_pass_ns_.store(mono_ns());
   render_gpu_text(samples, ok, gen);
@@ -390,6 +498,33 @@ void Exporter::render_gpu_text(const std::vector<GpuSample>& samples, const std:
     append_label_value(&l, gi.vbios_version);
     l.append("\",oam_id=\"").append(std::to_string(gi.oam_id)).append("\"");
     line(&o, "amdgpu_info", l, 1);
+  }
+  {  // partition profiles the GPU supports, one series per (profile, memory mode)
+    static const char* kNps[] = {"NPS1", "NPS2", "NPS4", "NPS8"};
+    bool hdr = false;
+    for (size_t g = 0; g < gpus.size(); ++g) {
+      for (const auto& pp : gpus[g].supported_profiles) {
+        for (int b = 0; b < 4; ++b) {
+          if (!(pp.nps_caps & (1u << b))) continue;
+          if (!hdr) {
+            append_header(&o, "amdgpu_partition_profile_supported",
+                          "Compute partition profile x memory partition mode the GPU supports (value 1); "
+                          "source=current when only the current profile could be read.",
+                          "gauge");
+            hdr = true;
+          }
+          std::string l = gl[g];
+          l.append(",profile=\"");
+          append_label_value(&l, pp.type);
+          l.append("\",partitions=\"").append(std::to_string(pp.partitions));
+          l.append("\",memory_partition=\"").append(kNps[b]);
+          l.append("\",source=\"");
+          append_label_value(&l, pp.source);
+          l.append("\"");
+          line(&o, "amdgpu_partition_profile_supported", l, 1);
+        }
+      }
+    }
   }
   append_header(&o, "amdgpu_telemetry_up", "1 if the last telemetry sample of the GPU succeeded.", "gauge");
   for (size_t g = 0; g < gpus.size(); ++g) line(&o, "amdgpu_telemetry_up", gl[g], ok[g] ? 1 : 0);
@@ -559,12 +694,18 @@ void Exporter::render_gpu_text(const std::vector<GpuSample>& samples, const std:
       l.append("\",resource=\"");
       append_label_value(&l, pl.resource);
       l.append("\"");
-      line(&info, "amdgpu_partition_info", l, 1);
+      std::string il = l;
+      il.append(",hip_ids=\"");
+      append_label_value(&il, pl.hip_ids);
+      il.append("\"");
+      line(&info, "amdgpu_partition_info", il, 1);
       if (!ok[g]) continue;
       const GpuSample& s = samples[g];
       const int p = pl.partition < 0 ? 0 : pl.partition;
       if (p < s.num_partitions && s.partition_gfx_busy_pct[p] >= 0)
-        line(&busy, "amdgpu_partition_gfx_busy_percent", l, s.partition_gfx_busy_pct[p]);
+        line(&busy, "amdgpu_partition_gfx_busy_percent",
+             l + (s.partition_busy_source[p] == 1 ? ",source=\"partition_metrics\"" : ",source=\"xcp_stats\""),
+             s.partition_gfx_busy_pct[p]);
       if (p < s.num_partitions && s.partition_vram_used_bytes[p] > 0)
         line(&vram, "amdgpu_partition_vram_used_bytes", l, s.partition_vram_used_bytes[p]);
     }
@@ -574,7 +715,10 @@ void Exporter::render_gpu_text(const std::vector<GpuSample>& samples, const std:
       o.append(info);
     }
     if (!busy.empty()) {
-      append_header(&o, "amdgpu_partition_gfx_busy_percent", "Per-partition (XCP) compute busy.", "gauge");
+      append_header(&o, "amdgpu_partition_gfx_busy_percent",
+                    "Per-partition (XCP) compute busy: from the partition's own metrics "
+                    "(amdsmi_get_gpu_partition_metrics_info) or the socket blob's xcp_stats.",
+                    "gauge");
       o.append(busy);
     }
     if (!vram.empty()) {
@@ -705,12 +849,45 @@ void Exporter::render_parts(std::string_view* head, std::string* counters, std::
     append_float(counters, (mono_ns() - last) * 1e-9);
     counters->push_back('\n');
   }
-  if (const int stuck = stalled_gpu_.load(); stuck >= 0) {
-    append_header(counters, "amdgpu_telemetry_sample_stalled",
-                  "1 while a telemetry call of the GPU has been in flight longer than health.sampleStallS.", "gauge");
-    counters->append("amdgpu_telemetry_sample_stalled{gpu=\"");
-    append_u64(counters, static_cast<uint64_t>(stuck));
-    counters->append("\"} 1\n");
+  {
+    std::shared_ptr<const Freshness> f;
+    std::shared_ptr<const Stalls> st;
+    {
+      std::lock_guard<SpinLock> lk(fresh_lock_);
+      f = fresh_;
+      st = stalls_;
+    }
+    if (!f->last_ok.empty()) {
+      append_header(counters, "amdgpu_telemetry_sample_age_seconds",
+                    "Seconds since the GPU's last successful telemetry sample.", "gauge");
+      const int64_t now = mono_ns();
+      for (const auto& kv : f->last_ok) {
+        if (!kv.second) continue;
+        counters->append("amdgpu_telemetry_sample_age_seconds{gpu=\"");
+        append_u64(counters, static_cast<uint64_t>(kv.first));
+        counters->append("\"} ");
+        append_float(counters, (now - kv.second) * 1e-9);
+        counters->push_back('\n');
+      }
+    }
+    if (!st->stalled.empty()) {
+      append_header(counters, "amdgpu_telemetry_sample_stalled",
+                    "1 while a hardware call of the GPU has been in flight longer than health.sampleStallS.", "gauge");
+      for (int g : st->stalled) {
+        counters->append("amdgpu_telemetry_sample_stalled{gpu=\"");
+        append_u64(counters, static_cast<uint64_t>(g));
+        counters->append("\"} 1\n");
+      }
+    }
+    if (!st->blocked.empty()) {
+      append_header(counters, "amdgpu_telemetry_sample_blocked",
+                    "1 while the GPU's hardware call waits behind another GPU's stalled call.", "gauge");
+      for (int g : st->blocked) {
+        counters->append("amdgpu_telemetry_sample_blocked{gpu=\"");
+        append_u64(counters, static_cast<uint64_t>(g));
+        counters->append("\"} 1\n");
+      }
+    }
   }
   if (sample_hist_.count()) {
     append_header(counters, "amdgpu_telemetry_sample_duration_seconds", "Wall time of one sampling pass over all GPUs.",

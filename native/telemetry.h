@@ -4,8 +4,11 @@
 // carries Go runtime, build info and echo HTTP metrics.  This adds per-GPU and
 // per-partition amdsmi telemetry (power, energy, temperatures incl. HBM stacks,
 // activity, clocks, VRAM, ECC, xGMI link state and traffic) with the sampling
-// decoupled from scraping: one sampler thread reads one gpu_metrics blob per physical
-// GPU per tick and renders the text once; a scrape copies bytes.
+// decoupled from scraping: one sampler thread posts one sample per physical GPU per tick
+// to the GPUs' lanes (backend.h), collects what came back within the tick and renders the
+// text once; a scrape copies bytes.  A GPU whose call wedged keeps
+// its lane busy and nothing else: the other GPUs' samples, health checks and series stay
+// fresh, and each GPU's sample age is exported.
 #pragma once
 
 #include <atomic>
@@ -54,6 +57,7 @@ struct PartitionLabel {
   int partition = -1;
   std::string device_id;
   std::string resource;
+  std::string hip_ids;  // host HIP ordinals the device spans, comma-joined ("" = unknown)
 };
 
 class Exporter : public std::enable_shared_from_this<Exporter> {
@@ -71,18 +75,26 @@ class Exporter : public std::enable_shared_from_this<Exporter> {
   void start(std::shared_ptr<Backend> backend, int interval_ms, std::shared_ptr<HealthMonitor> monitor);
   void stop();
   bool running() const { return running_.load(); }
-  // Watchdog (health.sampleStallS): a backend call that has been in flight for longer
-  // than this marks its GPU lost in the health monitor.  A wedged driver never returns
-  // an error to count, so without it such a GPU would stay advertised Healthy.  0 = off.
+  // Watchdog (health.sampleStallS): a hardware call (sample, describe, ...) that has been
+  // in flight on a GPU's lane for longer than this marks that GPU lost in the health
+  // monitor.  A wedged driver never returns an error to count, so without it such a GPU
+  // would stay advertised Healthy.  0 = off.  Attribution: the GPU whose call has been
+  // stuck longest is the culprit; another stuck GPU is reported too only when some call
+  // completed after its own began (the library is not serialised behind the first
+  // wedge), otherwise it is "blocked" behind it and stays Healthy.
   void set_stall_ms(int ms) { stall_ms_.store(ms > 0 ? ms : 0); }
-  int stalled_gpu() const { return stalled_gpu_.load(); }
+  int stalled_gpu() const;                 // lowest stalled GPU index, -1 = none
+  std::vector<int> stalled_gpus() const;   // reported lost by the watchdog
+  std::vector<int> blocked_gpus() const;   // stuck behind another GPU's call
   // One synchronous sampling pass (also used before the first scrape).
   // sampler_gen: the sampler thread's own pass (0 = a caller's synchronous pass); it
   // ends early once stop() is waiting or another sampler generation started.
   void sample_once(uint64_t sampler_gen = 0);
-  // Samplers left running in a backend call that did not return within the stall
-  // threshold when stop() was called (each ends when its call returns).
-  int abandoned_samplers() const { return abandoned_.load(); }
+  // The sampler never waits on a hardware call past its pass budget, so stop() always
+  // joins it; kept for compatibility (always 0).
+  int abandoned_samplers() const { return 0; }
+  // Seconds since GPU `gpu`'s last successful sample (-1: none yet).
+  double sample_age_s(int gpu) const;
 
   std::shared_ptr<const std::string> gpu_text() const;
   GpuSample last_sample(int gpu) const;
@@ -108,6 +120,28 @@ class Exporter : public std::enable_shared_from_this<Exporter> {
                            int interval_ms);
   int sampler_step(int64_t* next, uint64_t gen, int interval_ms);  // ms to sleep before the next step, -1 = stop
   void render_gpu_text(const std::vector<GpuSample>& samples, const std::vector<char>& ok, uint64_t inventory_gen);
+  // One GPU's sampling state across passes (guarded by sample_mu_).
+  struct Slot {
+    int index = -1;                        // backend index
+    std::shared_ptr<LaneJob> job;          // in flight (null: none)
+    std::shared_ptr<GpuSample> out;
+    int64_t posted_ns = 0;
+    GpuSample last;                        // last completed sample
+    bool last_ok = false;
+    int64_t last_ok_ns = 0;
+  };
+  std::vector<Slot> slots_;
+  uint64_t slots_gen_ = ~0ull;             // inventory generation slots_ belongs to
+  // What the per-scrape counters need, published by the sampler and the watchdog.
+  struct Freshness {
+    std::vector<std::pair<int, int64_t>> last_ok;  // (gpu, mono ns of its last good sample)
+  };
+  struct Stalls {
+    std::vector<int> stalled, blocked;
+  };
+  mutable SpinLock fresh_lock_;
+  std::shared_ptr<const Freshness> fresh_;
+  std::shared_ptr<const Stalls> stalls_;
   void render_process(std::string* out) const;  // reads /proc
   void render_process_cached(std::string* out) const;  // per-thread copy, refreshed each second
   // head_sp / health_sp (optional): owning references to the segments head / health view
@@ -178,9 +212,7 @@ class Exporter : public std::enable_shared_from_this<Exporter> {
   std::mutex first_mu_;  // first pass of a start(): start() waits for it (bounded)
   std::condition_variable first_cv_;
   bool first_done_ = false;
-  std::atomic<int> abandoned_{0};
   std::atomic<uint64_t> sampler_gen_{0};  // bumped by every start()
-  std::mutex inflight_mu_;  // orders a call's end against the watchdog's verdict on it
   std::mutex sample_mu_;  // serialises sampling passes
   std::atomic<uint64_t> samples_{0};
   std::atomic<uint64_t> sample_errors_{0};
@@ -188,10 +220,6 @@ class Exporter : public std::enable_shared_from_this<Exporter> {
   void watchdog_loop(std::shared_ptr<HealthMonitor> monitor);
   std::thread watchdog_;
   std::atomic<int> stall_ms_{0};
-  std::atomic<int> inflight_gpu_{-1};       // GPU whose backend call is in flight, -1 = none
-  std::string inflight_key_;                // its gpu_key when the call started (inflight_mu_)
-  std::atomic<int64_t> inflight_since_{0};  // stored before inflight_gpu_
-  std::atomic<int> stalled_gpu_{-1};        // GPU the watchdog has reported lost
   std::atomic<int64_t> last_pass_ns_{0};    // end of the last complete pass (mono ns)
   int64_t start_time_s_ = 0;
 

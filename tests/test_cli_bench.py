@@ -123,6 +123,26 @@ def test_bench_two_ranks_gloo():
     assert r["config"]["global_batch"] == 2 * 256
 
 
+@pytest.mark.slow
+def test_bench_ranks_allocate_the_gpu_of_their_hip_ordinal():
+    """on a node whose HIP numbering is not BDF order, rank r allocates
+    the device whose HIP ordinal is its LOCAL_RANK (the GPU its canary and
+    torch.cuda.set_device use), not the r-th device in BDF order."""
+    from k8s_gpu_device_plugin_amd.models import fixtures
+    gpus, _ = fixtures.build_backend("2gpu_spx_hip_swapped").discover()
+    hip_of = {g.uuid: g.partitions[0].hip_id for g in gpus}
+    assert [hip_of[g.uuid] for g in gpus] == [1, 0]  # BDF order != HIP order
+    r = _run_bench(["--gpus", "2", "--steps", "1", "--warmup", "1", "--backend", "fixture",
+                    "--fixture", "2gpu_spx_hip_swapped"], nproc=2)
+    _check_contract(r, 2, 1, 1)
+    devs = sorted(r["rank_devices"], key=lambda d: d["rank"])
+    assert [d["mapped_by"] for d in devs] == ["hip_id", "hip_id"]
+    for d in devs:
+        assert d["hip_ids"] == [d["local_rank"]] and hip_of[d["device_id"]] == d["local_rank"], d
+    assert devs[0]["device_id"] == gpus[1].uuid  # rank 0 = HIP 0 = the second GPU in BDF order
+    assert r["dtype"] == "n/a"
+
+
 def test_bench_refuses_rank_gpu_mismatch():
     """--gpus must equal WORLD_SIZE (one kubelet-client rank per advertised GPU): a run
     that would report n_gpus it did not have fails before it starts a daemon."""

@@ -166,3 +166,50 @@ def test_device_health_is_read_from_the_native_table(n):
     assert devs["a"].health == v1beta1.UNHEALTHY
     devs["a"].health = v1beta1.HEALTHY
     assert t.healthy("a") and t.version >= 3
+
+
+def test_fixture_cannot_declare_a_mode_outside_its_caps():
+    """the fixture's partition model is pinned to what the MI355X box
+    reports (memory caps NPS1|NPS2, profiles/r4/amdsmi_probe.json).  A node model - or an
+    operator's simulated re-partitioning - that puts a GPU in a mode outside its profile
+    table is rejected; CPX+NPS4 exists only as the declared hypothetical 8gpu_cpx_nps4."""
+    from k8s_gpu_device_plugin_amd.models import fixtures
+    with pytest.raises(ValueError, match="CPX\\+NPS4, outside its supported profiles"):
+        fixtures.build_backend("2gpu_cpx_nps4")
+    with pytest.raises(ValueError, match="outside its supported profiles"):
+        fixtures.build_backend(fixtures.mi355x_node(2, "QPX", "NPS8"))
+    be = fixtures.build_backend("2gpu_cpx_nps2")
+    gpus, _ = be.discover()
+    assert [(p.type, p.partitions, p.nps_caps) for p in gpus[0].supported_profiles] == [
+        ("SPX", 1, 3), ("DPX", 2, 3), ("QPX", 4, 3), ("CPX", 8, 3)]
+    with pytest.raises(ValueError, match="outside its supported profiles"):
+        fixtures.set_gpu_mode(be, 0, "CPX", "NPS4")
+    fixtures.set_gpu_mode(be, 0, "DPX", "NPS1")  # a supported mode is accepted
+    assert fixtures.load_model("8gpu_cpx_nps4").get("hypothetical") is True
+    hyp, _ = fixtures.build_backend("8gpu_cpx_nps4").discover()
+    assert hyp[0].memory_partition == "NPS4" and all(p.nps_caps & 4 for p in hyp[0].supported_profiles)
+    assert sum(len(g.partitions) for g in hyp) == 64
+
+
+def test_supported_profiles_are_exported(n):
+    from prometheus_client.parser import text_string_to_metric_families
+
+    from k8s_gpu_device_plugin_amd.models import fixtures
+    be = fixtures.build_backend("2gpu_qpx_nps2")
+    gpus, _ = be.discover()
+    ex = n.Exporter()
+    ex.set_inventory(gpus)
+    ex.set_partition_labels([n.PartitionLabel(g.index, p.index, p.id, "amd.com/gpu", str(p.hip_id))
+                             for g in gpus for p in g.partitions])
+    ex.start(be, 50, None)
+    try:
+        fams = {f.name: f for f in text_string_to_metric_families(ex.render())}
+    finally:
+        ex.stop()
+    rows = {(s.labels["gpu"], s.labels["profile"], s.labels["partitions"], s.labels["memory_partition"])
+            for s in fams["amdgpu_partition_profile_supported"].samples}
+    assert len(rows) == 2 * 4 * 2 and ("1", "CPX", "8", "NPS2") in rows and ("0", "QPX", "4", "NPS1") in rows
+    busy = fams["amdgpu_partition_gfx_busy_percent"].samples
+    assert len(busy) == 8 and {s.labels["source"] for s in busy} == {"partition_metrics"}
+    info = fams["amdgpu_partition_info"].samples
+    assert sorted(int(s.labels["hip_ids"]) for s in info) == list(range(8))

@@ -106,11 +106,12 @@ def test_amdsmi_sample_cost_breakdown(amdsmi_backend):
     samples = [amdsmi_backend.sample(0) for _ in range(19)]
     assert all(x.ok for x in samples)
     after = amdsmi_backend.sample_costs()
-    per = {k: (after[k][0] - before[k][0]) / 20 * 1e6 for k in after if not k.startswith("xgmi_links_")}
-    paths = {k: after[k][1] - before[k][1] for k in after if k.startswith("xgmi_links_")}
+    per = {k: (after[k][0] - before[k][0]) / 20 * 1e6 for k in after
+           if not k.startswith(("xgmi_links_", "partition_busy_"))}
+    paths = {k: after[k][1] - before[k][1] for k in after if k.startswith(("xgmi_links_", "partition_busy_"))}
     print("amdsmi sample cost per GPU (us):", {k: round(v, 1) for k, v in per.items()},
           "total %.1f us" % sum(per.values()), "link paths", paths)
-    assert set(per) == {"gpu_metrics", "vram_usage", "ecc_count", "xgmi_links", "bad_pages"}
+    assert set(per) == {"gpu_metrics", "partition_metrics", "vram_usage", "ecc_count", "xgmi_links", "bad_pages"}
     assert sum(per.values()) < 50e3
     # samples served from the gpu_metrics blob report the same links as the full path,
     # with byte counters that never run backwards

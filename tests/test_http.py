@@ -96,7 +96,7 @@ def test_metrics_gzip_negotiation(web):
     import gzip
     port, _, kind = web
     get(port, "/health")  # so the echo_http families exist in every scrape below
-    volatile = ("echo_http", "process_", "amdgpu_telemetry_last_pass_age")  # change between two scrapes
+    volatile = ("echo_http", "process_", "amdgpu_telemetry_last_pass_age", "amdgpu_telemetry_sample_age")  # change between two scrapes
     strip = lambda t: [ln for ln in t.splitlines() if not ln.startswith(volatile)]  # noqa: E731
     ticks = lambda t: [ln for ln in t.splitlines() if ln.startswith("amdgpu_telemetry_samples_total ")]  # noqa: E731
     for ae in ("gzip", "deflate, gzip;q=1.0", "br,gzip"):

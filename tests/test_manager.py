@@ -588,29 +588,31 @@ def test_canary_performance_floor_marks_slow_partition_unhealthy(make_cfg, plugi
 
 
 def test_restart_burst_is_coalesced(make_cfg, plugin_dir, run_manager, monkeypatch):
-    """100 /restart calls that arrive while a reload runs are served by the next reload,
+    """100 /restart calls that arrive while a discovery runs are served by the next one,
     not by 100 reloads: every request is counted, a handful of reloads happen, and the
     plugin ends registered and serving."""
     with KubeletStub(plugin_dir) as k:
         m = run_manager(make_cfg())
         k.wait_for_registrations(1)
-        orig = m.restart_plugins
-        reloads = []
-        done = []
+        orig = m.backend.discover
+        reloads0 = m.counters["reloads"]
 
-        def slow_restart():
-            reloads.append(time.monotonic())
-            time.sleep(0.05)  # the burst lands while this reload runs
-            orig()
-            done.append(time.monotonic())
-        monkeypatch.setattr(m, "restart_plugins", slow_restart)
+        class SlowBackend:  # the burst lands while each discovery runs
+            def __getattr__(self, name):
+                return getattr(m.backend_real, name)
+
+            def discover(self):
+                time.sleep(0.05)
+                return orig()
+        m.backend_real = m.backend
+        m._discoverer._backend = SlowBackend()
         for _ in range(100):
             m.restart()
         assert _wait(lambda: m.counters["restarts_api"] == 100, timeout=20)
-        # an empty queue only means the last reload was dequeued: wait for it to finish
-        assert _wait(lambda: m.events.empty() and len(done) == len(reloads), timeout=10)
-        assert len(reloads) <= 5, len(reloads)
-        assert m.counters.get("restarts_coalesced", 0) == 100 - len(reloads)
+        assert _wait(lambda: m.events.empty() and not m._discoverer.pending(), timeout=10)
+        time.sleep(0.1)
+        reloads = m.counters["reloads"] - reloads0
+        assert 1 <= reloads <= 5, reloads
         assert k.client("amd-gpu.sock").get_options().get_preferred_allocation_available
 
 

@@ -99,7 +99,8 @@ def test_metrics_contract_both_ways(n):
     # health.badPageThreshold); everything else must be present on the fixture node
     assert missing <= {"amdgpu_partition_vram_used_bytes", "amdgpu_device_plugin_allocation_info",
                        "amdgpu_device_plugin_pod_resources_up", "amdgpu_retired_pages_threshold",
-                       "amdgpu_telemetry_sample_stalled", "amdgpu_xgmi_link_pods"}, missing
+                       "amdgpu_telemetry_sample_stalled", "amdgpu_telemetry_sample_blocked",
+                       "amdgpu_xgmi_link_pods"}, missing
 
 
 def test_metrics_doc_is_generated_from_the_registry():
