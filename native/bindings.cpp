@@ -875,6 +875,9 @@ PYBIND11_MODULE(_native, m) {
         },
         py::arg("n") = 10000, py::arg("warmup") = 500, py::arg("req_bytes") = 128, py::arg("resp_bytes") = 256,
         py::arg("server_spin") = false, py::arg("tcp") = false, py::arg("gap_us") = 0);
+  py::class_<UdsPinger>(m, "UdsPinger")
+      .def(py::init<int, int, int>(), py::arg("req_bytes"), py::arg("resp_bytes"), py::arg("server_timeout_ms") = 100)
+      .def("once", &UdsPinger::once, py::call_guard<py::gil_scoped_release>());
   m.def("render_bench",
         [](std::shared_ptr<Exporter> ex, std::shared_ptr<HttpServer> http, int threads, int iters) {
           py::gil_scoped_release rel;

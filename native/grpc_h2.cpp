@@ -3,6 +3,7 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <poll.h>
+#include <pthread.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
@@ -369,7 +370,12 @@ void GrpcServer::start() {
     std::lock_guard<std::mutex> fk(fail_mu_);
     fail_reason_.clear();
   }
-  for (auto& w : workers_) threads_.emplace_back([this, wp = w.get(), t = table_] { run_guarded(wp, t); });
+  for (size_t i = 0; i < workers_.size(); ++i)
+    threads_.emplace_back([this, wp = workers_[i].get(), t = table_, i] {
+      // named, so /proc/<pid>/task/*/comm tells the workers apart (scripts/idle_probe.py)
+      pthread_setname_np(pthread_self(), ("dpgrpc-" + std::to_string(i)).c_str());
+      run_guarded(wp, t);
+    });
   std::lock_guard<std::mutex> nk(notifier_->mu);
   notifier_->srv = this;
 }

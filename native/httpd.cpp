@@ -1,5 +1,7 @@
 #include "httpd.h"
 
+#include <pthread.h>
+
 #include <arpa/inet.h>
 #include <errno.h>
 #include <fcntl.h>
@@ -208,7 +210,8 @@ int HttpServer::start() {
   }
   for (int t = 0; t < nthreads; ++t) {
     Worker* w = workers_[t].get();
-    threads_.emplace_back([this, w] {
+    threads_.emplace_back([this, w, t] {
+      pthread_setname_np(pthread_self(), ("dphttp-" + std::to_string(t)).c_str());
       std::vector<epoll_event> evs(128);
       char rbuf[16384];
       int spare = -1;  // reserve descriptor for accept_or_shed

@@ -323,6 +323,84 @@ std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_byte
   return lat;
 }
 
+UdsPinger::UdsPinger(int req_bytes, int resp_bytes, int server_timeout_ms)
+    : req_(static_cast<size_t>(req_bytes), 'q'), buf_(static_cast<size_t>(resp_bytes)) {
+  if (req_bytes <= 0 || resp_bytes <= 0 || req_bytes > (1 << 20) || resp_bytes > (4 << 20) || server_timeout_ms < 0)
+    throw std::invalid_argument("UdsPinger: bad sizes");
+  int sv[2];
+  if (socketpair(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0, sv) != 0)
+    throw std::runtime_error(std::string("socketpair: ") + strerror(errno));
+  cfd_ = sv[0];
+  sfd_ = sv[1];
+  fcntl(sfd_, F_SETFL, fcntl(sfd_, F_GETFL) | O_NONBLOCK);
+  struct timeval tv {5, 0};
+  setsockopt(cfd_, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+  ep_ = epoll_create1(EPOLL_CLOEXEC);
+  struct epoll_event ev {};
+  ev.events = EPOLLIN | EPOLLRDHUP;
+  ev.data.fd = sfd_;
+  epoll_ctl(ep_, EPOLL_CTL_ADD, sfd_, &ev);
+  server_ = std::thread([this, req_bytes, resp_bytes, server_timeout_ms] {
+    std::vector<char> in(static_cast<size_t>(req_bytes) + 65536), out(static_cast<size_t>(resp_bytes), 'r');
+    size_t have = 0;
+    epoll_event evs[4];
+    for (;;) {
+      const int k = epoll_wait(ep_, evs, 4, server_timeout_ms);
+      if (k < 0 && errno != EINTR) return;
+      if (k <= 0) continue;
+      bool closed = false;
+      for (;;) {
+        const ssize_t r = recv(sfd_, in.data() + have, in.size() - have, 0);
+        if (r > 0) {
+          have += static_cast<size_t>(r);
+          if (have >= in.size()) break;
+        } else if (r < 0 && errno == EINTR) {
+          continue;
+        } else {
+          if (r == 0 || errno != EAGAIN) closed = true;
+          break;
+        }
+      }
+      while (have >= static_cast<size_t>(req_bytes)) {
+        have -= static_cast<size_t>(req_bytes);
+        size_t off = 0;
+        while (off < out.size()) {
+          const ssize_t w = send(sfd_, out.data() + off, out.size() - off, MSG_NOSIGNAL);
+          if (w > 0)
+            off += static_cast<size_t>(w);
+          else if (w < 0 && (errno == EAGAIN || errno == EINTR))
+            continue;
+          else
+            return;
+        }
+      }
+      if (closed) return;
+    }
+  });
+}
+
+UdsPinger::~UdsPinger() {
+  shutdown(cfd_, SHUT_RDWR);
+  if (server_.joinable()) server_.join();
+  close(cfd_);
+  close(sfd_);
+  close(ep_);
+}
+
+double UdsPinger::once() {
+  const int64_t t0 = mono_ns();
+  if (send(cfd_, req_.data(), req_.size(), MSG_NOSIGNAL) != static_cast<ssize_t>(req_.size()))
+    throw std::runtime_error("UdsPinger: send failed");
+  size_t got = 0;
+  while (got < buf_.size()) {
+    const ssize_t r = recv(cfd_, buf_.data() + got, buf_.size() - got, 0);
+    if (r > 0) got += static_cast<size_t>(r);
+    else if (r < 0 && errno == EINTR) continue;
+    else throw std::runtime_error("UdsPinger: recv failed");
+  }
+  return (mono_ns() - t0) * 1e-9;
+}
+
 namespace {
 
 int count_unhealthy(const std::string& law) {

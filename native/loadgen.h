@@ -6,6 +6,10 @@
 //   grpc_load : N native HTTP/2 clients issuing unary calls, closed-loop.
 #pragma once
 
+#include <string>
+#include <thread>
+#include <vector>
+
 #include <cstdint>
 #include <string>
 #include <memory>
@@ -36,6 +40,24 @@ LoadResult grpc_load(const std::string& socket_path, const std::string& method, 
 // of one /metrics scrape of resp_bytes (what the kernel's copies and wake-ups cost).
 std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_bytes, bool server_spin = false,
                                  bool tcp = false, int gap_us = 0);
+
+// The same bare exchange, one at a time on demand: a persistent socket pair whose server
+// thread sleeps in epoll_wait(timeout_ms) between exchanges the way the plugin's worker
+// does (its loop wakes every 100 ms).  once() is one round trip, in seconds; interleaved
+// with real RPCs after the same idle gap it gives each a paired floor
+// (scripts/idle_probe.py).
+class UdsPinger {
+ public:
+  UdsPinger(int req_bytes, int resp_bytes, int server_timeout_ms);
+  ~UdsPinger();
+  double once();
+
+ private:
+  int cfd_ = -1, sfd_ = -1, ep_ = -1;
+  std::string req_;
+  std::vector<char> buf_;
+  std::thread server_;
+};
 
 class Exporter;
 class HttpServer;

@@ -1,24 +1,37 @@
-"""Allocate latency as a function of how long the plugin sat idle before the call.
+"""Allocate latency as a function of how long the plugin sat idle before the call
+(VERDICT r3 item 6).
 
-Kubelet calls the plugin a few times per pod admission, seconds or minutes apart, so
-the call it makes almost never finds a warm server.  For idle gaps of 1 ms to 1 s this
-measures, on one daemon (bench config, amdsmi backend when present):
+Kubelet calls the plugin a few times per pod admission, seconds or minutes apart, so the
+call it makes almost never finds a warm server.  For each idle gap this measures, on one
+daemon (bench config, amdsmi backend when present), three kinds of call, each after the
+same gap, interleaved call by call (the kind order rotates every iteration) so slow drift
+of the machine hits all three alike:
 
-  * ``allocate``: one Allocate after the gap (compiled HTTP/2 client, kubelet-like);
-  * ``admission``: GetPreferredAllocation after the gap, ~200 us of client work, then
-    Allocate (the Allocate is timed: kubelet's admission sequence);
-  * ``floor``: the bare unix-socket exchange of the same sizes after the same gap
-    between two threads of this process (no HTTP/2, protobuf or table work).
+  * ``allocate``  - Allocate after the gap (compiled HTTP/2 client, kubelet-like);
+  * ``preferred`` - GetPreferredAllocation after the gap: the first call of a kubelet pod
+    admission, the one that pays for the idle gap;
+  * ``floor``     - the bare unix-socket exchange of Allocate's sizes after the gap, to a
+    server thread that sleeps in epoll_wait(100 ms) like the plugin's workers do
+    (``native.UdsPinger``; no HTTP/2, protobuf or table work).
 
-    python scripts/idle_probe.py [--gaps 0.001,0.01,0.1,1] [--calls 40] [--out FILE]
+Reported per gap: p50/p90 of each kind, and the median of the paired differences
+allocate - floor and preferred - floor (iteration i's calls are a pair) with a bootstrap
+95 % confidence interval.  Evidence for where an excess comes from, per call: minor and
+major page faults and scheduler counters (run time, run-queue wait, time slices) of the
+daemon's gRPC worker threads (``dpgrpc-*`` in /proc/<pid>/task) and of the calling
+thread, read before and after the call.
 
-Prints one JSON line per gap, then the whole result.
+    python scripts/idle_probe.py [--gaps 0.001,0.01,0.1,1] [--calls 300] [--out FILE]
+
+Prints a progress line every 30 s, one JSON line per gap, then the whole result.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import random
+import resource
 import shutil
 import signal
 import subprocess
@@ -31,16 +44,66 @@ sys.path.insert(0, ROOT)
 
 import bench  # noqa: E402
 
+KINDS = ("allocate", "preferred", "floor")
+
 
 def pct(xs, q):
     xs = sorted(xs)
-    return round(xs[min(len(xs) - 1, int(q * len(xs)))] * 1e6, 2) if xs else None
+    return xs[min(len(xs) - 1, int(q * len(xs)))] if xs else None
+
+
+def median(xs):
+    return pct(xs, 0.5)
+
+
+def bootstrap_ci(diffs, n=2000, seed=7):
+    """95 % percentile-bootstrap interval of the median of paired differences."""
+    rng = random.Random(seed)
+    k = len(diffs)
+    meds = sorted(median([diffs[rng.randrange(k)] for _ in range(k)]) for _ in range(n))
+    return meds[int(0.025 * n)], meds[int(0.975 * n)]
+
+
+def worker_tids(pid: int, prefix: str = "dpgrpc-"):
+    out = []
+    for tid in os.listdir("/proc/%d/task" % pid):
+        try:
+            with open("/proc/%d/task/%s/comm" % (pid, tid)) as f:
+                if f.read().strip().startswith(prefix):
+                    out.append(int(tid))
+        except OSError:
+            pass
+    return out
+
+
+def thread_counters(pid: int, tids):
+    """Sum over `tids` of (minflt, majflt, run_ns, wait_ns, slices)."""
+    tot = [0, 0, 0, 0, 0]
+    for tid in tids:
+        try:
+            with open("/proc/%d/task/%d/stat" % (pid, tid)) as f:
+                fields = f.read().rsplit(")", 1)[1].split()
+            with open("/proc/%d/task/%d/schedstat" % (pid, tid)) as f:
+                run, wait, slices = (int(x) for x in f.read().split())
+        except OSError:
+            continue
+        tot[0] += int(fields[7])   # minflt (field 10)
+        tot[1] += int(fields[9])   # majflt (field 12)
+        tot[2] += run
+        tot[3] += wait
+        tot[4] += slices
+    return tot
+
+
+def self_faults():
+    r = resource.getrusage(resource.RUSAGE_THREAD)
+    return r.ru_minflt, r.ru_majflt
 
 
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gaps", default="0.001,0.01,0.1,1")
-    ap.add_argument("--calls", type=int, default=40, help="calls per gap (the 1 s gap takes this many seconds)")
+    ap.add_argument("--calls", type=int, default=300, help="calls per kind per gap")
     ap.add_argument("--backend", default="auto")
     ap.add_argument("--admission-poll-us", type=int, default=None, help="override grpc.admissionPollUs")
     ap.add_argument("--busy-poll-us", type=int, default=None, help="override grpc.busyPollUs / http.busyPollUs")
@@ -55,7 +118,9 @@ def main() -> int:
     workdir = tempfile.mkdtemp(prefix="idleprobe-", dir="/tmp")
     proc, kubelet, port, reg, backend = bench.start_daemon(1, "native", workdir, busy_poll_us=a.busy_poll_us,
                                                          admission_poll_us=a.admission_poll_us, backend=a.backend)
-    res = {"backend": backend, "calls_per_gap": a.calls, "rows": []}
+    res = {"backend": backend, "calls_per_kind_per_gap": a.calls, "kinds": list(KINDS),
+           "floor_server_epoll_timeout_ms": 100, "rows": []}
+    t_progress = time.monotonic()
     try:
         sock = os.path.join(workdir, "device-plugins", reg.endpoint)
         c = DevicePluginClient(sock)
@@ -70,28 +135,57 @@ def main() -> int:
         resp_len = len(c.allocate_raw(alloc))
         c.close()
         sizes = (9 + 80 + 9 + 5 + len(alloc), 9 + 20 + 9 + 5 + resp_len + 9 + 16)
+        pinger = n.UdsPinger(*sizes, server_timeout_ms=100)
         h2 = n.H2Client(sock)
         h2.bench_unary(v1beta1.METHOD_ALLOCATE, alloc, 2000)  # warm the connection and the code
-        perf = time.perf_counter
+        for _ in range(200):
+            pinger.once()
+        tids = worker_tids(proc.pid)
+        res["daemon_grpc_workers"] = len(tids)
+        call = {"allocate": lambda: h2.bench_unary(v1beta1.METHOD_ALLOCATE, alloc, 1)[0],
+                "preferred": lambda: h2.bench_unary(v1beta1.METHOD_GET_PREFERRED, pref, 1)[0],
+                "floor": pinger.once}
         for gap in [float(x) for x in a.gaps.split(",")]:
-            al, adm = [], []
-            for _ in range(a.calls):
-                time.sleep(gap)
-                al.extend(h2.bench_unary(v1beta1.METHOD_ALLOCATE, alloc, 1))
-            for _ in range(a.calls):
-                time.sleep(gap)
-                h2.bench_unary(v1beta1.METHOD_GET_PREFERRED, pref, 1)
-                t_go = perf() + 200e-6
-                while perf() < t_go:
-                    pass
-                adm.extend(h2.bench_unary(v1beta1.METHOD_ALLOCATE, alloc, 1))
-            floor = n.uds_pingpong(a.calls, 2, *sizes, gap_us=int(gap * 1e6))
-            row = {"gap_s": gap, "allocate_p50_us": pct(al, 0.5), "allocate_p90_us": pct(al, 0.9),
-                   "admission_allocate_p50_us": pct(adm, 0.5), "admission_allocate_p90_us": pct(adm, 0.9),
-                   "floor_p50_us": pct(floor, 0.5), "floor_p90_us": pct(floor, 0.9)}
+            lat = {k: [] for k in KINDS}
+            ev = {k: {"daemon_minflt": 0, "daemon_majflt": 0, "daemon_run_us": 0.0, "daemon_wait_us": 0.0,
+                      "daemon_slices": 0, "client_minflt": 0} for k in KINDS}
+            for i in range(a.calls):
+                order = KINDS[i % 3:] + KINDS[:i % 3]
+                for kind in order:
+                    time.sleep(gap)
+                    # the counters are read around every kind, the floor's too, so each
+                    # call follows the same client-side work
+                    d0 = thread_counters(proc.pid, tids)
+                    s0 = self_faults()
+                    lat[kind].append(call[kind]())
+                    s1 = self_faults()
+                    d1 = thread_counters(proc.pid, tids)
+                    if kind != "floor":
+                        e = ev[kind]
+                        e["daemon_minflt"] += d1[0] - d0[0]
+                        e["daemon_majflt"] += d1[1] - d0[1]
+                        e["daemon_run_us"] += (d1[2] - d0[2]) / 1e3
+                        e["daemon_wait_us"] += (d1[3] - d0[3]) / 1e3
+                        e["daemon_slices"] += d1[4] - d0[4]
+                    ev[kind]["client_minflt"] += s1[0] - s0[0]
+                if time.monotonic() - t_progress > 30:
+                    t_progress = time.monotonic()
+                    print(json.dumps({"progress": {"gap_s": gap, "iteration": i + 1, "of": a.calls}}), flush=True)
+            us = lambda v: round(v * 1e6, 2)  # noqa: E731
+            row = {"gap_s": gap, "calls": a.calls}
+            for k in KINDS:
+                row[k] = {"p50_us": us(median(lat[k])), "p90_us": us(pct(lat[k], 0.9))}
+            for k in ("allocate", "preferred"):
+                diffs = [x - y for x, y in zip(lat[k], lat["floor"])]
+                lo, hi = bootstrap_ci(diffs)
+                row[k]["minus_floor_median_us"] = us(median(diffs))
+                row[k]["minus_floor_ci95_us"] = [us(lo), us(hi)]
+                row[k]["per_call"] = {kk: round(v / a.calls, 3) for kk, v in ev[k].items()}
+            row["floor"]["per_call"] = {"client_minflt": round(ev["floor"]["client_minflt"] / a.calls, 3)}
             res["rows"].append(row)
             print(json.dumps(row), flush=True)
         h2.close()
+        del pinger
     finally:
         try:
             os.killpg(proc.pid, signal.SIGTERM)
