@@ -91,6 +91,9 @@ class HealthConfig:
     # trains back (0 = no floor; e.g. 16 and 32 for an x16 Gen5 MI355X slot)
     pcieMinWidth: int = 0
     pcieMinSpeedGTs: float = 0.0
+    # consecutive telemetry samples below (at or above) the PCIe floor that degrade
+    # (restore) a GPU: one reading of a link in a power-saving state flaps nothing
+    pcieDebounceSamples: int = 3
     # health checks that no longer make a GPU Unhealthy (still logged): comma list or
     # YAML list of reset, ecc, lost, retiredPages, or all (env AMDGPU_DP_DISABLE_HEALTHCHECKS)
     disabledChecks: str = ""
@@ -315,6 +318,8 @@ def validate(cfg: Config) -> Config:
         raise ConfigError("health.pcieMinWidth / health.pcieMinSpeedGTs must be >= 0 (0 = no floor)")
     if cfg.health.sampleStallS < 0:
         raise ConfigError("health.sampleStallS must be >= 0 (0 = off)")
+    if cfg.health.pcieDebounceSamples < 1:
+        raise ConfigError("health.pcieDebounceSamples must be >= 1")
     if cfg.health.discoveryTimeoutS <= 0:
         raise ConfigError("health.discoveryTimeoutS must be > 0")
     if cfg.sharing.replicas < 1:

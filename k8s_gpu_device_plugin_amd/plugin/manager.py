@@ -156,7 +156,8 @@ class PluginManager:
         self.exporter.set_build_info(build_info_text())
         self.monitor = n.HealthMonitor(self.backend, cfg.health.lostAfterFailures)
         self.monitor.set_disabled_checks(disabled_checks_mask(cfg.health.disabledChecks))
-        self.monitor.set_pcie_floor(int(cfg.health.pcieMinWidth), float(cfg.health.pcieMinSpeedGTs))
+        self.monitor.set_pcie_floor(int(cfg.health.pcieMinWidth), float(cfg.health.pcieMinSpeedGTs),
+                                    int(cfg.health.pcieDebounceSamples))
         self.events: "queue.Queue[tuple]" = queue.Queue()
         self.plugins: list[AmdDevicePlugin] = []
         self.gpus: list = []
@@ -369,6 +370,9 @@ class PluginManager:
                 # readiness follows plugin state and stalls that no event announces (a
                 # discovery running past its bound, a server that lost its registration)
                 self._push_readiness()
+                if self.podres is not None:  # PodResources' coverage moves on with every poll,
+                    # changed map or not (its grace keeps a just-answered Allocate counted)
+                    self.recent_allocations.set_covered_until(self.podres.covered_until())
                 next_check = now + SERVER_CHECK_S
             try:
                 ev = self.events.get(timeout=max(0.0, next_check - now))

@@ -94,9 +94,17 @@ class PodResourcesWatcher:
         with self._lock:
             return dict(self.allocations), self.up
 
+    # kubelet adds a container's devices to the map PodResources List reads only after
+    # the plugin's Allocate answer came back (and its own bookkeeping ran): a List sent
+    # within this window of an Allocate may not show it yet, so allocations that recent
+    # are not counted as covered by that List
+    COVER_GRACE_NS = 2_000_000_000
+
     def covered_until(self) -> int:
+        """mono ns before which every allocation is in the last map: the last List's send
+        time less the grace above (0 while no List has succeeded)."""
         with self._lock:
-            return self.covered_until_ns
+            return max(0, self.covered_until_ns - self.COVER_GRACE_NS) if self.covered_until_ns else 0
 
     def poll_once(self) -> bool:
         """Returns True when the allocation map or the up state changed."""

@@ -543,7 +543,7 @@ PYBIND11_MODULE(_native, m) {
            py::arg("held_unhealthy"), py::call_guard<py::gil_scoped_release>())
       .def("set_bad_page_thresholds", &HealthMonitor::set_bad_page_thresholds)
       .def("set_pcie_floor", &HealthMonitor::set_pcie_floor, py::arg("min_width"), py::arg("min_gts"),
-           py::call_guard<py::gil_scoped_release>())
+           py::arg("debounce") = 1, py::call_guard<py::gil_scoped_release>())
       .def("on_sample", &HealthMonitor::on_sample, py::arg("gpu"), py::arg("ok"), py::arg("sample"),
            py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("events_seen", &HealthMonitor::events_seen);

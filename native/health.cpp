@@ -298,7 +298,15 @@ void HealthMonitor::on_sample(int gpu, bool ok, const GpuSample& s) {
       if (pcie_min_width_ > 0 || pcie_min_gts_ > 0) {
         const bool narrow = pcie_min_width_ > 0 && s.pcie_link_width > 0 && s.pcie_link_width < pcie_min_width_;
         const bool slow = pcie_min_gts_ > 0 && s.pcie_link_speed_gtps > 0 && s.pcie_link_speed_gtps < pcie_min_gts_;
-        if ((narrow || slow) != st.pcie_bad) {
+        if (narrow || slow) {
+          st.pcie_ok = 0;
+          ++st.pcie_low;
+        } else {
+          st.pcie_low = 0;
+          ++st.pcie_ok;
+        }
+        const bool settled = (narrow || slow) ? st.pcie_low >= pcie_debounce_ : st.pcie_ok >= pcie_debounce_;
+        if (settled && (narrow || slow) != st.pcie_bad) {
           char msg[160];
           std::snprintf(msg, sizeof(msg), "host PCIe link x%d at %.1f GT/s (floor x%d, %.1f GT/s)",
                         static_cast<int>(s.pcie_link_width), s.pcie_link_speed_gtps, pcie_min_width_, pcie_min_gts_);
@@ -408,10 +416,11 @@ void HealthMonitor::set_bad_page_thresholds(std::vector<int> thresholds) {
     if (!table_keys_[g].empty()) state_[table_keys_[g]].page_threshold = thresholds[g];
 }
 
-void HealthMonitor::set_pcie_floor(int min_width, double min_gts) {
+void HealthMonitor::set_pcie_floor(int min_width, double min_gts, int debounce) {
   std::lock_guard<std::mutex> lk(mu_);
   pcie_min_width_ = std::max(0, min_width);
   pcie_min_gts_ = std::max(0.0, min_gts);
+  pcie_debounce_ = std::max(1, debounce);
   if (pcie_min_width_ > 0 || pcie_min_gts_ > 0) return;  // the next samples re-judge every GPU
   std::vector<std::string> keys;  // no floor any more: nothing is held for its link
   for (auto& kv : state_)

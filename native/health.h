@@ -114,7 +114,10 @@ class HealthMonitor {
   void set_bad_page_thresholds(std::vector<int> thresholds);
   // Host PCIe link floor (0 = no floor): a GPU whose link trained narrower or slower is
   // Unhealthy until it trains back (a failing riser or retimer halves host bandwidth).
-  void set_pcie_floor(int min_width, double min_gts);
+  // `debounce` consecutive samples below the floor degrade the GPU, as many at or above
+  // it restore it: one low reading (a link in a power-saving state for a moment) flaps
+  // nothing.
+  void set_pcie_floor(int min_width, double min_gts, int debounce = 1);
   // Identities the monitor holds state for that are unhealthy (advertised or not).
   std::vector<std::string> unhealthy_keys() const;
   // Bitmask of HealthCheck values to ignore; re-evaluates every GPU (a GPU held only by a
@@ -129,6 +132,8 @@ class HealthMonitor {
     bool lost = false;
     bool pages_bad = false;  // retired + pending pages at/over the threshold (not cleared by a reset)
     bool pcie_bad = false;   // host PCIe link trained below the configured floor
+    int pcie_low = 0;        // consecutive samples below the floor
+    int pcie_ok = 0;         // consecutive samples at or above it
     int failures = 0;
     int64_t last_ue = -1;
     bool reported_healthy = true;
@@ -165,6 +170,7 @@ class HealthMonitor {
   int disabled_ = 0;  // HealthCheck bits
   int pcie_min_width_ = 0;
   double pcie_min_gts_ = 0;
+  int pcie_debounce_ = 1;
   std::thread thread_;
   std::atomic<bool> running_{false};
   bool stop_ = false;

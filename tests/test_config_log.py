@@ -156,12 +156,20 @@ def test_shipped_configs_are_valid():
     assert {"/var/lib/kubelet/device-plugins", "/dev/kfd", "/dev/dri"} <= mounts
     assert os.path.dirname(cfg.nodeFeatureFile) in mounts
     assert cfg.podResources.enabled and os.path.dirname(cfg.podResources.socket) in mounts
-    # /dev/kfd must be openable inside the pod for amdsmi event notification: a hostPath
-    # mount alone is not in the device cgroup; privileged grants it
+    # unprivileged by default; deploy/privileged-patch.yaml opts in to /dev/kfd
+    # access (amdsmi event notification, canaries): a hostPath mount alone is not in the
+    # device cgroup, privileged grants it
     c = ds["containers"][0]
     sc = c.get("securityContext", {})
-    assert sc.get("privileged") is True, "no /dev/kfd access path: health events would never arm"
-    assert "allowPrivilegeEscalation" not in sc  # rejected by the API server together with privileged
+    assert "privileged" not in sc and sc["allowPrivilegeEscalation"] is False
+    assert sc["capabilities"] == {"drop": ["ALL"]} and sc["readOnlyRootFilesystem"] is True
+    with open(os.path.join(root, "deploy", "privileged-patch.yaml")) as f:
+        patch = yaml.safe_load(f)
+    psc = patch["spec"]["template"]["spec"]["containers"][0]
+    assert psc["name"] == c["name"]
+    merged = {k: v for k, v in {**sc, **psc["securityContext"]}.items() if v is not None}
+    assert merged["privileged"] is True, "no /dev/kfd access path in the opt-in patch"
+    assert "allowPrivilegeEscalation" not in merged  # rejected by the API server together with privileged
     vols = {v["name"]: v for v in ds["volumes"]}
     kfd = [m for m in c["volumeMounts"] if m["mountPath"] == "/dev/kfd"][0]
     assert vols[kfd["name"]]["hostPath"]["path"] == "/dev/kfd"

@@ -608,6 +608,34 @@ def test_pcie_floor_state_machine(n):
     assert m.gpu_healthy(0) and [(x.gpu, x.healthy) for x in m.pop(50)] == [(0, 1)]
 
 
+def test_pcie_floor_is_debounced(n):
+    """one low PCIe reading (a link caught in a power-saving state) must not flap
+    ListAndWatch: `debounce` consecutive samples below the floor degrade the GPU, as many
+    at or above it restore it; an alternating link never degrades."""
+    be = fixtures.build_backend("2gpu_spx")
+    m = n.HealthMonitor(be, 3)
+    m.set_gpu_count(2)
+    m.set_pcie_floor(16, 32.0, 3)
+
+    def health():
+        return [(x.gpu, x.healthy) for x in m.pop(20)
+                if x.kind not in (n.EVT_LINK_QUALITY, n.EVT_LINK_UP, n.EVT_LINK_DOWN)]
+    for width in (8, 16, 8, 16, 8, 16):  # flapping: never three low readings in a row
+        be.set_pcie_link(1, width, 32.0)
+        m.on_sample(1, True, be.sample(1))
+    assert health() == [] and m.gpu_healthy(1)
+    be.set_pcie_link(1, 8, 32.0)
+    for i in range(3):
+        m.on_sample(1, True, be.sample(1))
+        assert m.gpu_healthy(1) == (i < 2)
+    assert health() == [(1, 0)]
+    be.set_pcie_link(1, 16, 32.0)
+    for i in range(3):
+        m.on_sample(1, True, be.sample(1))
+        assert m.gpu_healthy(1) == (i == 2)
+    assert health() == [(1, 1)]
+
+
 def test_pcie_floor_from_config(make_cfg, plugin_dir):
     """The manager applies health.pcieMinWidth: a GPU whose host link drops to x8 is
     advertised Unhealthy, and Healthy again when it trains back to x16."""
