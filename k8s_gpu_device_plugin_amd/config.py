@@ -121,6 +121,7 @@ class GrpcConfig:
     threads: int = 4
     busyPollUs: int = 50         # native server: keep polling this long after a request (0 = off)
     admissionPollUs: int = 1000  # ... and this long after a GetPreferredAllocation (its Allocate follows)
+    keepWarmMs: int = 10         # native server: idle workers with a connection replay canned requests (0 = off)
 
 
 @dataclass

@@ -254,6 +254,8 @@ class AmdDevicePlugin:
                            self.cfg.grpc.busyPollUs if self.cfg is not None else 0,
                            self.cfg.grpc.admissionPollUs if self.cfg is not None else 0)
         srv.set_table(self.table)
+        if self.cfg is not None:
+            srv.set_keep_warm_ms(int(self.cfg.grpc.keepWarmMs))
         srv.start()
         self._native_server = srv
 

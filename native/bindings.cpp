@@ -675,7 +675,9 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("worker_connections", &GrpcServer::worker_connections)
       .def_property_readonly("socket_path", &GrpcServer::socket_path)
       .def("failure", &GrpcServer::failure)
-      .def("inject_fault", &GrpcServer::inject_fault);
+      .def("inject_fault", &GrpcServer::inject_fault)
+      .def("set_keep_warm_ms", &GrpcServer::set_keep_warm_ms)
+      .def_property_readonly("warm_ticks", &GrpcServer::warm_ticks);
 
   py::class_<H2Client>(m, "H2Client")
       .def(py::init<std::string, double>(), py::arg("socket_path"), py::arg("timeout_s") = 5.0,

@@ -564,6 +564,12 @@ void DeviceTable::render_metric_headers(std::string* out) {
                 "Latency of kubelet DevicePlugin RPCs served by this plugin.", "histogram");
 }
 
+uint64_t DeviceTable::metrics_version() const {
+  uint64_t v = 0;
+  for (int r = 0; r < kRpcCount; ++r) v += hist_[r]->count();
+  return v;
+}
+
 void DeviceTable::render_metrics(std::string* out, bool with_headers) const {
   if (with_headers) render_metric_headers(out);
   std::string labels;

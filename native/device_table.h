@@ -118,6 +118,9 @@ class DeviceTable {
   std::string list_and_watch() const;  // ListAndWatchResponse bytes (cached)
 
   // RPC bodies.  Return true and response bytes in *out, or false and an error message.
+  // Observations recorded in this table's RPC histograms so far: render_metrics' output
+  // changes only when this does (a scrape caches the text under it).
+  uint64_t metrics_version() const;
   bool allocate(std::string_view req, std::string* out) const;
   bool preferred(std::string_view req, std::string* out) const;
   std::string options_bytes() const;  // DevicePluginOptions

@@ -1,5 +1,8 @@
 #include "grpc_h2.h"
 
+#include "hpack.h"
+#include "pbwire.h"
+
 #include <errno.h>
 #include <fcntl.h>
 #include <poll.h>
@@ -899,6 +902,29 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
   };
 
   uint64_t seen_version = table->version();
+  // canned requests for the keep-warm tick: a typical request header block and an
+  // Allocate / GetPreferredAllocation of the table's first device
+  std::string warm_hdrs, warm_alloc, warm_pref, warm_out;
+  {
+    hpack::encode_indexed(&warm_hdrs, 3);  // :method POST
+    hpack::encode_indexed(&warm_hdrs, 6);  // :scheme http
+    hpack::encode_literal_name_index(&warm_hdrs, 4, "/v1beta1.DevicePlugin/Allocate");  // :path
+    hpack::encode_literal_name_index(&warm_hdrs, 1, "localhost");                      // :authority
+    hpack::encode_literal(&warm_hdrs, "content-type", "application/grpc");
+    hpack::encode_literal(&warm_hdrs, "te", "trailers");
+    const std::vector<std::string> ids = table->ids();
+    if (!ids.empty()) {
+      std::string ctr;
+      pb::put_bytes(&ctr, 1, ids[0]);
+      pb::put_bytes(&warm_alloc, 1, ctr);
+      std::string pctr;
+      pb::put_bytes(&pctr, 1, ids[0]);
+      pb::put_bytes(&pctr, 2, ids[0]);
+      pb::put_int_nz(&pctr, 3, 1);
+      pb::put_bytes(&warm_pref, 1, pctr);
+    }
+  }
+  int64_t last_activity = mono_ns();
   const int64_t spin_ns = static_cast<int64_t>(busy_poll_us_) * 1000;
   const int64_t admission_ns = static_cast<int64_t>(admission_poll_us_) * 1000;
   int64_t spin_until = 0;  // busy-poll window end (mono ns); 0 = closed
@@ -927,8 +953,24 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
         continue;
       }
     } else {
-      n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), 100);
+      const int warm = keep_warm_ms_.load(std::memory_order_relaxed);
+      n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), warm > 0 ? std::min(warm, 100) : 100);
+      if (n == 0 && warm > 0 && !w->conns.empty() && !warm_alloc.empty()) {
+        const int64_t now = mono_ns();
+        if (now - last_activity >= static_cast<int64_t>(warm) * 1000000) {
+          hpack::Decoder d(4096);
+          d.decode(reinterpret_cast<const uint8_t*>(warm_hdrs.data()), warm_hdrs.size(),
+                   [](void*, std::string_view, std::string_view) {}, nullptr);
+          warm_out.clear();
+          table->allocate(warm_alloc, &warm_out);
+          warm_out.clear();
+          table->preferred(warm_pref, &warm_out);
+          warm_ticks_.fetch_add(1, std::memory_order_relaxed);
+          last_activity = now;
+        }
+      }
     }
+    if (n > 0) last_activity = mono_ns();
     bool law_tick = false;
     for (int i = 0; i < n; ++i) {
       const int fd = evs[i].data.fd;

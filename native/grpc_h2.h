@@ -62,6 +62,13 @@ class GrpcServer {
   uint64_t admission_windows() const { return admission_windows_.load(); }
   uint64_t poll_windows_yielded() const { return poll_windows_yielded_.load(); }
   int connections() const { return conns_.load(); }
+  // Keep-warm (grpc.keepWarmMs, 0 = off): a worker that holds a connection and has been
+  // idle this long runs the request path on canned requests (HPACK decode of a typical
+  // request header block, Allocate and GetPreferredAllocation through the table), so
+  // kubelet's sparse calls do not find that code and data evicted.  Experimental: see
+  // scripts/idle_probe.py --keep-warm-ms and BASELINE.md.
+  void set_keep_warm_ms(int ms) { keep_warm_ms_.store(ms > 0 ? ms : 0); }
+  uint64_t warm_ticks() const { return warm_ticks_.load(); }
   std::vector<int> worker_connections() const;  // connections owned per worker thread
   const std::string& socket_path() const { return path_; }
 
@@ -92,6 +99,8 @@ class GrpcServer {
   int nthreads_;
   int busy_poll_us_;
   int admission_poll_us_;
+  std::atomic<int> keep_warm_ms_{0};
+  std::atomic<uint64_t> warm_ticks_{0};
   std::shared_ptr<DeviceTable> table_;
   int listen_fd_ = -1;
   // the socket file this server bound (device, inode): stop() removes only that file, not

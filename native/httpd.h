@@ -62,9 +62,12 @@ class HttpServer {
 
  private:
   friend struct Worker;
+  // direct_fd >= 0: nothing is queued on that connection, so a /metrics answer may go
+  // to the socket straight from the exposition's cached segments (one sendmsg, no copy
+  // into *out); what the socket does not take is appended to *out as usual.
   void handle(const std::string& method, const std::string& path, const std::string& origin, bool keep_alive,
               bool http10, std::string* out, int* status_out, size_t* body_bytes_out, bool gzip_ok = false,
-              bool peer_local = true);
+              bool peer_local = true, int direct_fd = -1);
   void record(int method_idx, int handler_idx, int status, double seconds);
   void log_access(const std::string& remote, const std::string& host, const std::string& method,
                   const std::string& uri, const std::string& ua, int status, double seconds, size_t bytes_in,

@@ -945,18 +945,34 @@ void Exporter::render_parts(std::string_view* head, std::string* counters, std::
     }
     *health = *c.health;
     if (health_sp) *health_sp = c.health;
-    bool any = false;
-    for (const auto& t : tables) {
-      const size_t before = tail->size();
-      if (!any) DeviceTable::render_metric_headers(tail);
-      const size_t body = tail->size();
-      t->render_metrics(tail, false);
-      if (tail->size() == body) {
-        tail->resize(before);  // nothing observed yet: no headers either
-        continue;
+    // RPC histograms: between kubelet RPCs (scrapes come far more often) their text does
+    // not change; it is rendered again only when a table's observation count moves
+    // (versions read before the text, so a cached text is never older than its key)
+    bool same_tables = c.tables_key.size() == tables.size() * 2;
+    for (size_t i = 0; same_tables && i < tables.size(); ++i)
+      same_tables = c.tables_key[2 * i] == reinterpret_cast<uintptr_t>(tables[i].get()) &&
+                    c.tables_key[2 * i + 1] == tables[i]->metrics_version();
+    if (!same_tables) {
+      c.tables_key.clear();
+      for (const auto& t : tables) {
+        c.tables_key.push_back(reinterpret_cast<uintptr_t>(t.get()));
+        c.tables_key.push_back(t->metrics_version());
       }
-      any = true;
+      c.tables_text.clear();
+      bool any = false;
+      for (const auto& t : tables) {
+        const size_t before = c.tables_text.size();
+        if (!any) DeviceTable::render_metric_headers(&c.tables_text);
+        const size_t body = c.tables_text.size();
+        t->render_metrics(&c.tables_text, false);
+        if (c.tables_text.size() == body) {
+          c.tables_text.resize(before);  // nothing observed yet: no headers either
+          continue;
+        }
+        any = true;
+      }
     }
+    tail->append(c.tables_text);
   }
   tail->append(*v.extra);
   render_process_cached(tail);

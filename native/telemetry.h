@@ -175,6 +175,9 @@ class Exporter : public std::enable_shared_from_this<Exporter> {
     std::shared_ptr<const std::string> health;
     int64_t proc_ns = 0;
     std::string proc;
+    // the device tables' RPC histograms, rendered once per change of their counts
+    std::vector<uint64_t> tables_key;  // (table address, metrics_version) pairs
+    std::string tables_text;
   };
   TlCache& tl_cache() const;
   // The last rendered device-health text, shared so that every thread serves the same

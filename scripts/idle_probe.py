@@ -95,6 +95,18 @@ def thread_counters(pid: int, tids):
     return tot
 
 
+def server_seconds(conn, rpc: str) -> float:
+    """Sum of the daemon's own time for `rpc` so far (amdgpu_device_plugin_rpc_duration_
+    seconds: request dispatched -> answer encoded, no transport)."""
+    conn.request("GET", "/metrics")
+    body = conn.getresponse().read().decode()
+    tot = 0.0
+    for line in body.splitlines():
+        if line.startswith("amdgpu_device_plugin_rpc_duration_seconds_sum") and 'rpc="%s"' % rpc in line:
+            tot += float(line.rsplit(" ", 1)[1])
+    return tot
+
+
 def self_faults():
     r = resource.getrusage(resource.RUSAGE_THREAD)
     return r.ru_minflt, r.ru_majflt
@@ -107,6 +119,10 @@ def main() -> int:
     ap.add_argument("--backend", default="auto")
     ap.add_argument("--admission-poll-us", type=int, default=None, help="override grpc.admissionPollUs")
     ap.add_argument("--busy-poll-us", type=int, default=None, help="override grpc.busyPollUs / http.busyPollUs")
+    ap.add_argument("--keep-warm-ms", type=int, default=None, help="override grpc.keepWarmMs")
+    ap.add_argument("--server-time", action="store_true",
+                    help="also read the daemon's own time per call from its RPC histogram (a /metrics "
+                         "scrape after each timed call)")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
 
@@ -116,9 +132,11 @@ def main() -> int:
 
     n = native.load()
     workdir = tempfile.mkdtemp(prefix="idleprobe-", dir="/tmp")
+    over = {"grpc": {"keepWarmMs": a.keep_warm_ms}} if a.keep_warm_ms is not None else None
     proc, kubelet, port, reg, backend = bench.start_daemon(1, "native", workdir, busy_poll_us=a.busy_poll_us,
-                                                         admission_poll_us=a.admission_poll_us, backend=a.backend)
-    res = {"backend": backend, "calls_per_kind_per_gap": a.calls, "kinds": list(KINDS),
+                                                         admission_poll_us=a.admission_poll_us, backend=a.backend,
+                                                         overrides=over)
+    res = {"backend": backend, "keep_warm_ms": a.keep_warm_ms, "calls_per_kind_per_gap": a.calls, "kinds": list(KINDS),
            "floor_server_epoll_timeout_ms": 100, "rows": []}
     t_progress = time.monotonic()
     try:
@@ -141,12 +159,17 @@ def main() -> int:
         for _ in range(200):
             pinger.once()
         tids = worker_tids(proc.pid)
+        import http.client
+        mconn = http.client.HTTPConnection("127.0.0.1", port, timeout=10)
+        rpc_name = {"allocate": "Allocate", "preferred": "GetPreferredAllocation"}
         res["daemon_grpc_workers"] = len(tids)
         call = {"allocate": lambda: h2.bench_unary(v1beta1.METHOD_ALLOCATE, alloc, 1)[0],
                 "preferred": lambda: h2.bench_unary(v1beta1.METHOD_GET_PREFERRED, pref, 1)[0],
                 "floor": pinger.once}
         for gap in [float(x) for x in a.gaps.split(",")]:
             lat = {k: [] for k in KINDS}
+            srv = {k: [] for k in ("allocate", "preferred")}  # the daemon's own time per call
+            mconn._base = {}
             ev = {k: {"daemon_minflt": 0, "daemon_majflt": 0, "daemon_run_us": 0.0, "daemon_wait_us": 0.0,
                       "daemon_slices": 0, "client_minflt": 0} for k in KINDS}
             for i in range(a.calls):
@@ -168,6 +191,12 @@ def main() -> int:
                         e["daemon_wait_us"] += (d1[3] - d0[3]) / 1e3
                         e["daemon_slices"] += d1[4] - d0[4]
                     ev[kind]["client_minflt"] += s1[0] - s0[0]
+                    if kind != "floor" and a.server_time:  # read after the timed call
+                        base = mconn._base.get(kind)
+                        cur = server_seconds(mconn, rpc_name[kind])
+                        if base is not None:
+                            srv[kind].append(cur - base)
+                        mconn._base[kind] = cur
                 if time.monotonic() - t_progress > 30:
                     t_progress = time.monotonic()
                     print(json.dumps({"progress": {"gap_s": gap, "iteration": i + 1, "of": a.calls}}), flush=True)
@@ -181,6 +210,9 @@ def main() -> int:
                 row[k]["minus_floor_median_us"] = us(median(diffs))
                 row[k]["minus_floor_ci95_us"] = [us(lo), us(hi)]
                 row[k]["per_call"] = {kk: round(v / a.calls, 3) for kk, v in ev[k].items()}
+                if srv[k]:  # the daemon's own part of the call (dispatch -> encoded answer)
+                    row[k]["server_p50_us"] = us(median(srv[k]))
+                    row[k]["server_p90_us"] = us(pct(srv[k], 0.9))
             row["floor"]["per_call"] = {"client_minflt": round(ev["floor"]["client_minflt"] / a.calls, 3)}
             res["rows"].append(row)
             print(json.dumps(row), flush=True)

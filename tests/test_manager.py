@@ -288,6 +288,9 @@ def test_concurrent_restart_requests_are_serialized(make_cfg, plugin_dir, run_ma
         for t in ts:
             t.join()
         assert _wait(lambda: m.counters["restarts_api"] == 10, timeout=20)
+        # reloads run behind the requests (discovery on its worker, then the swap)
+        assert _wait(lambda: m.events.empty() and not m._discoverer.pending(), timeout=20)
+        assert _wait(lambda: m.plugins and m.plugins[0].registered, timeout=20)
         assert k.client("amd-gpu.sock").get_options().get_preferred_allocation_available
 
 
@@ -754,7 +757,7 @@ def test_link_state_is_resynced_after_a_reload(make_cfg, plugin_dir, run_manager
 
 def test_halfrate_fixture_is_discovered_degraded(n):
     gpus, topo = fixtures.build_backend("8gpu_spx_halfrate").discover()
-    from k8s_gpu_device_plugin_amd.parallel.topology import NodeTopology
+    from topology_model import NodeTopology
     assert NodeTopology(gpus, topo).degraded_links() == [(0, 1)]
 
 

@@ -1,11 +1,11 @@
 """Differential tests: native allocator vs the pure-Python reference model
-(parallel/topology.py), and the /metrics contract vs metrics/families.py."""
+(tests/topology_model.py), and the /metrics contract vs metrics/families.py."""
 from hypothesis import given, settings, strategies as st
 from prometheus_client.parser import text_string_to_metric_families
 
 from k8s_gpu_device_plugin_amd.metrics import families
 from k8s_gpu_device_plugin_amd.models import fixtures
-from k8s_gpu_device_plugin_amd.parallel import topology as T
+import topology_model as T
 
 
 def _native_topo(n, ngpu, links):
