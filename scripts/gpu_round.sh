@@ -21,6 +21,7 @@ for s in ${STEPS:-pytest smoke bench prof}; do
     smoke)  step smoke 240 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  step bench 300 python bench.py ${BENCH_ARGS:-} ;;
     idle)   step idle_probe ${IDLE_TIMEOUT:-400} python -u scripts/idle_probe.py --gaps ${IDLE_GAPS:-0.001,0.01,0.1} --calls ${IDLE_CALLS:-300} --out "$OUT/idle_probe${IDLE_TAG:-}.json" ;;
+    soak)   step soak $(( ${SOAK_SECONDS:-120} + 120 )) python -u scripts/soak.py --seconds ${SOAK_SECONDS:-120} --backend amdsmi ;;
     suite)  step suite 600 python -m k8s_gpu_device_plugin_amd.benchmark.suite --json "$OUT/baseline_suite_gpu.json" ;;
     sweep)  step hbm_sweep 300 python -c "import json; from k8s_gpu_device_plugin_amd.ops import canary; rows = canary.hbm_sweep(0); print(json.dumps(rows, indent=1)); json.dump(rows, open('$OUT/hbm_sweep.json', 'w'), indent=1)" ;;
     prof)   (cd /tmp && export TMPDIR=/tmp && step rocprof_canary 240 rocprofv3 --kernel-trace --stats -d "$OUT/prof_canary" -o canary --output-format csv -- python3 -m k8s_gpu_device_plugin_amd.ops.canary --device 0 --bytes 2147483648 --passes 3) ;;

@@ -272,3 +272,23 @@ def test_recent_multi_gpu_allocate_counts_as_link_load(n):
     import time
     time.sleep(0.08)
     assert rec.live() == 0
+
+
+def test_podresources_coverage_keeps_a_grace_before_the_list(n, monkeypatch):
+    """kubelet writes a container's devices into the PodResources map only after the
+    plugin's Allocate answer came back, so a List sent just after an Allocate may miss
+    it: coverage stops COVER_GRACE_NS before the List's send time, and an
+    Allocate answered inside that window keeps counting as link load."""
+    from k8s_gpu_device_plugin_amd.plugin import podresources as pr
+    w = pr.PodResourcesWatcher("/nonexistent.sock", 1.0, "amd.com/", lambda: None)
+    assert w.covered_until() == 0  # no List yet: nothing covered
+    rec = n.RecentAllocations()
+    rec.record_gpus([0, 1])  # answered just before the List went out
+    monkeypatch.setattr(pr, "list_allocations", lambda *a, **k: {})
+    assert w.poll_once()
+    assert 0 < w.covered_until_ns <= n.mono_ns()
+    assert w.covered_until() == w.covered_until_ns - w.COVER_GRACE_NS
+    rec.set_covered_until(w.covered_until())
+    assert rec.live() == 1, "an Allocate inside the grace window was treated as covered"
+    rec.set_covered_until(n.mono_ns() + 1)  # a List sent COVER_GRACE_NS later covers it
+    assert rec.live() == 0

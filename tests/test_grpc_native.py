@@ -333,6 +333,51 @@ def test_busy_poll_window_answers_and_idles_without_spinning(n, plugin_dir):
         srv.stop()
 
 
+def test_keep_warm_ticks_are_invisible_to_kubelet_and_metrics(n, plugin_dir):
+    """grpc.keepWarmMs: a worker that owns a connection and has been idle that long
+    replays a canned header decode + Allocate/GetPreferredAllocation against its table,
+    so the first call after a long gap finds warm caches (profiles/r4/idle_probe_*).  The
+    tick is not an RPC: no request, histogram observation or answer leaves the server,
+    and a worker without connections does not tick."""
+    tc = n.TableConfig()
+    devs = [n.TableDevice("dev-%d" % i, i, 0, 0, -1, ["/dev/dri/renderD%d" % (128 + i)], True) for i in range(4)]
+    table = n.DeviceTable(tc, devs, n.Topology(4))
+    path = os.path.join(plugin_dir, "amd-gpu.sock")
+    srv = n.GrpcServer(path, 2)
+    srv.set_keep_warm_ms(10)
+    srv.set_table(table)
+    srv.start()
+    try:
+        time.sleep(0.2)
+        assert srv.warm_ticks == 0, "ticked with no connection"
+        c = n.H2Client(path)
+        req = v1beta1.AllocateRequest(container_requests=[v1beta1.ContainerAllocateRequest(
+            devices_ids=["dev-1"])]).SerializeToString()
+        st, _, _ = c.unary(v1beta1.METHOD_ALLOCATE, req)
+        assert st == 0
+        requests = srv.requests
+        time.sleep(0.3)
+        assert srv.warm_ticks >= 5
+        assert srv.requests == requests
+        text = table.render_metrics()
+        assert 'rpc="Allocate"' in text and 'rpc="GetPreferredAllocation"' not in text
+        count = [ln for ln in text.splitlines()
+                 if ln.startswith("amdgpu_device_plugin_rpc_duration_seconds_count") and 'rpc="Allocate"' in ln]
+        assert count and count[0].endswith(" 1"), count
+        st, body, _ = c.unary(v1beta1.METHOD_ALLOCATE, req)  # the next real call is answered as usual
+        assert st == 0 and v1beta1.AllocateResponse.FromString(body).container_responses[0].envs[
+            "AMD_VISIBLE_DEVICES"] == "dev-1"
+        c.close()
+        srv.set_keep_warm_ms(0)
+        ticks = srv.warm_ticks
+        c = n.H2Client(path)
+        time.sleep(0.2)
+        assert srv.warm_ticks == ticks, "ticked with keep-warm off"
+        c.close()
+    finally:
+        srv.stop()
+
+
 def test_connections_spread_over_workers(n, plugin_dir):
     """Concurrent kubelet-side clients (bench ranks, kubelet + a debugging client) are
     owned by different worker threads, not queued behind one that accepted them all."""
