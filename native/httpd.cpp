@@ -705,9 +705,34 @@ void HttpServer::handle(const std::string& method, const std::string& path, cons
   o.append(body);
 }
 
+namespace {
+// the fixed text of every echo_http_* line, built once: a scrape re-renders these
+// families each time (its own request moves them), so only the numbers are formatted
+struct EchoText {
+  std::string requests[HttpServer::kStatus][HttpServer::kMethods][HttpServer::kHandlers];
+  std::string labels[HttpServer::kMethods][HttpServer::kHandlers];
+  EchoText() {
+    for (int m = 0; m < HttpServer::kMethods; ++m)
+      for (int h = 0; h < HttpServer::kHandlers; ++h) {
+        labels[m][h].append("handler=\"").append(kHandlerNames[h]).append("\",method=\"").append(kMethodNames[m])
+            .append("\",");
+        for (int s = 0; s < HttpServer::kStatus; ++s)
+          requests[s][m][h].append("echo_http_requests_total{handler=\"").append(kHandlerNames[h])
+              .append("\",method=\"").append(kMethodNames[m]).append("\",status=\"").append(kStatusNames[s])
+              .append("\"} ");
+      }
+  }
+};
+const EchoText& echo_text() {
+  static const EchoText t;
+  return t;
+}
+}  // namespace
+
 void HttpServer::render_http_metrics(std::string* out) const {
   // middleware/echo_metric.go:80-93 family names / help strings
   static_assert(kMethods * kHandlers <= 64, "used_mh_ is one 64-bit mask");
+  const EchoText& et = echo_text();
   const uint64_t used = used_mh_.load(std::memory_order_relaxed);
   bool any = false;
   for (int s = 0; s < kStatus; ++s) {
@@ -721,14 +746,12 @@ void HttpServer::render_http_metrics(std::string* out) const {
         append_header(out, "echo_http_requests_total", "Number of HTTP operations", "counter");
         any = true;
       }
-      out->append("echo_http_requests_total{handler=\"").append(kHandlerNames[h]).append("\",method=\"")
-          .append(kMethodNames[m]).append("\",status=\"").append(kStatusNames[s]).append("\"} ");
+      out->append(et.requests[s][m][h]);
       append_u64(out, v);
       out->push_back('\n');
     }
   }
   any = false;
-  std::string labels;
   for (uint64_t bits = used; bits; bits &= bits - 1) {
     const int mh = __builtin_ctzll(bits);
     const int m = mh / kHandlers, h = mh % kHandlers;
@@ -737,8 +760,7 @@ void HttpServer::render_http_metrics(std::string* out) const {
       append_header(out, "echo_http_request_duration_seconds", "Spend time by processing a route", "histogram");
       any = true;
     }
-    labels.assign("handler=\"").append(kHandlerNames[h]).append("\",method=\"").append(kMethodNames[m]).append("\",");
-    hist_[m][h]->render(out, "echo_http_request_duration_seconds", labels);
+    hist_[m][h]->render(out, "echo_http_request_duration_seconds", et.labels[m][h]);
   }
 }
 

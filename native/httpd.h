@@ -40,6 +40,10 @@ struct HttpConfig {
 
 class HttpServer {
  public:
+  // echo_http_* label dimensions: methods, handlers (routes), status classes
+  static constexpr int kMethods = 8;
+  static constexpr int kHandlers = 6;
+  static constexpr int kStatus = 5;
   HttpServer(HttpConfig cfg, std::shared_ptr<Exporter> exporter);
   ~HttpServer();
   // Returns the bound port (cfg.port may be 0 = ephemeral).  Throws on bind failure.
@@ -90,9 +94,6 @@ class HttpServer {
   ShardedCounter requests_;
   ShardedCounter shed_;
 
-  static constexpr int kMethods = 8;
-  static constexpr int kHandlers = 6;
-  static constexpr int kStatus = 5;
   // echo_http_requests_total per (status class, method, handler), one copy per thread
   // shard (metrics.h) so that concurrent workers never write the same line
   struct alignas(64) CountShard {

@@ -288,10 +288,30 @@ class Histogram {
     Cached& c = cache[id_];
     c.last_render = tl.renders;
     c.count = key_count;
-    c.name = name;
-    c.labels.assign(labels.data(), labels.size());
+    if (c.pre.empty() || c.name != name || c.labels != labels) {
+      c.name = name;
+      c.labels.assign(labels.data(), labels.size());
+      build_prefixes(&c);
+    }
+    // only the numbers move: the line texts were built once for this (name, labels)
     c.text.clear();
-    render_uncached(&c.text, name, labels);
+    c.text.reserve(c.pre.size() + 24 * c.ends.size());
+    uint64_t cum = 0;
+    size_t at = 0;
+    for (size_t i = 0; i <= bounds_.size(); ++i) {
+      for (int k = 0; k < kMetricShards; ++k) cum += shards_[k].counts[i].load(std::memory_order_relaxed);
+      c.text.append(c.pre, at, c.ends[i] - at);
+      at = c.ends[i];
+      append_u64(&c.text, cum);
+      c.text.push_back('\n');
+    }
+    c.text.append(c.pre, at, c.ends[bounds_.size() + 1] - at);
+    at = c.ends[bounds_.size() + 1];
+    append_float(&c.text, sum());
+    c.text.push_back('\n');
+    c.text.append(c.pre, at, c.ends[bounds_.size() + 2] - at);
+    append_u64(&c.text, cum);
+    c.text.push_back('\n');
     out->append(c.text);
   }
 
@@ -333,7 +353,27 @@ class Histogram {
     uint64_t count = 0;
     uint64_t last_render = 0;  // TlCache::renders when last used
     std::string name, labels, text;
+    // the text before each number, concatenated: bucket lines `name_bucket{labels le="x"} `,
+    // then `name_sum{labels} ` and `name_count{labels} `; ends[i] = end of prefix i
+    std::string pre;
+    std::vector<size_t> ends;
   };
+  void build_prefixes(Cached* c) const {
+    c->pre.clear();
+    c->ends.clear();
+    for (size_t i = 0; i <= bounds_.size(); ++i) {
+      c->pre.append(c->name).append("_bucket{").append(c->labels).append("le=\"").append(le_[i]).append("\"} ");
+      c->ends.push_back(c->pre.size());
+    }
+    std::string_view lab = c->labels;
+    if (!lab.empty() && lab.back() == ',') lab.remove_suffix(1);
+    for (const char* suffix : {"_sum", "_count"}) {
+      c->pre.append(c->name).append(suffix);
+      if (!lab.empty()) c->pre.append("{").append(lab.data(), lab.size()).append("}");
+      c->pre.push_back(' ');
+      c->ends.push_back(c->pre.size());
+    }
+  }
   // per-thread render cache, keyed by histogram id (ids are never reused, addresses are);
   // a scrape renders every live histogram, so a live entry is touched every ~100 renders
   struct TlCache {
