@@ -37,8 +37,11 @@ std::shared_ptr<LaneJob> Backend::post_job(const std::string& key, const char* w
   // the completion clock it touches outlive a caller that stopped waiting.
   auto job = std::make_shared<LaneJob>(what, [this, session, fn = std::move(fn)] {
     if (!gate_.enter(session)) return;  // handles of an older session: never use them
+    struct Leave {  // also when fn throws (LaneJob::run catches it): a call left inside
+      SessionGate& g;  // the gate for good would defer every re-initialisation
+      ~Leave() { g.leave(); }
+    } leave{gate_};
     fn();
-    gate_.leave();
     last_completion_ns_.store(mono_ns());
   });
   const int stall = stall_ms_.load();

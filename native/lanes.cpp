@@ -11,7 +11,14 @@ namespace amdgpu_dp {
 
 void LaneJob::run() {
   started_ns_.store(mono_ns());
-  fn_();
+  // a throwing call must not take the lane thread (and with it the process) down
+  try {
+    fn_();
+  } catch (const std::exception& e) {
+    error_ = e.what()[0] ? e.what() : "exception";
+  } catch (...) {
+    error_ = "unknown exception";
+  }
   fn_ = nullptr;  // captures (and what they keep alive) go with the call, not with the job
   finish();
 }

@@ -44,6 +44,9 @@ class LaneJob {
   const std::string& what() const { return what_; }
   int64_t started_ns() const { return started_ns_.load(); }
   int64_t finished_ns() const { return finished_ns_.load(); }
+  // the call threw (the lane caught it and carried on); valid once done()
+  bool failed() const { return !error_.empty(); }
+  const std::string& error() const { return error_; }
 
  private:
   friend class Lane;
@@ -52,6 +55,7 @@ class LaneJob {
   void finish();
   std::string what_;
   std::function<void()> fn_;
+  std::string error_;  // written before done_ is released
   std::mutex mu_;
   std::condition_variable cv_;
   std::atomic<bool> done_{false};

@@ -15,6 +15,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <stdexcept>
 #include <string>
 #include <thread>
 #include <vector>
@@ -528,6 +530,61 @@ static void test_histogram_render_cache() {
   CHECK(fin == ref && fin.find("x_seconds_count{rpc=\"a\"} 20001\n") != std::string::npos);
 }
 
+// Lanes: a throwing call is caught on the lane (which keeps serving), a wedged lane
+// refuses new work past the stall bound, a lane destroyed mid-call is detached and its
+// call still completes; the session gate refuses an old session's calls and a close
+// that a call inside outlasts fails and reopens the gate.
+static void test_lanes_and_gate() {
+  {
+    Lane lane("gpu-a");
+    auto bad = std::make_shared<LaneJob>("throws", [] { throw std::runtime_error("driver said no"); });
+    int ran = 0;
+    auto good = std::make_shared<LaneJob>("ok", [&ran] { ++ran; });
+    CHECK(lane.post(bad, 0) && lane.post(good, 0));
+    CHECK(bad->wait(2000) && good->wait(2000));
+    CHECK(bad->failed() && bad->error() == "driver said no" && !bad->dropped());
+    CHECK(!good->failed() && ran == 1 && lane.state().completed == 2);
+  }
+  std::atomic<bool> release{false};
+  std::atomic<int> finished{0};
+  {
+    auto lane = std::make_unique<Lane>("gpu-b");
+    auto stuck = std::make_shared<LaneJob>("stuck", [&] {
+      while (!release.load()) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      finished.fetch_add(1);
+    });
+    CHECK(lane->post(stuck, 0));
+    std::this_thread::sleep_for(std::chrono::milliseconds(30));
+    auto refused = std::make_shared<LaneJob>("later", [&] { finished.fetch_add(100); });
+    CHECK(!lane->post(refused, 10 * 1000000LL) && refused->dropped());  // in flight > 10 ms
+    auto queued = std::make_shared<LaneJob>("queued", [&] { finished.fetch_add(100); });
+    CHECK(lane->post(queued, 0));  // no stall bound: queued behind the stuck call
+    CHECK(lane->state().inflight_what == "stuck" && lane->state().queued == 1);
+    lane.reset();  // must not wait for the stuck call
+    CHECK(queued->dropped() && !stuck->done());
+    release = true;
+    CHECK(stuck->wait(2000) && finished.load() == 1);
+  }
+  SessionGate g;
+  const uint64_t s1 = g.session();
+  CHECK(g.enter(s1));
+  CHECK(!g.close(20));  // a call is inside: the close gives up, the gate stays open
+  CHECK(g.enter(s1));
+  g.leave();
+  g.leave();
+  CHECK(g.active() == 0 && g.close(20));
+  std::atomic<bool> entered{false};
+  std::thread t([&] { entered = g.enter(0); });  // waits while the gate is closed
+  std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  CHECK(!entered.load());
+  const uint64_t s2 = g.reopen();
+  t.join();
+  CHECK(entered.load() && s2 == s1 + 1);
+  g.leave();
+  CHECK(!g.enter(s1));  // handles of the previous session are never used again
+  CHECK(g.active() == 0);
+}
+
 // RecentAllocations: many writers wrap the 64-slot ring while readers snapshot it.
 // Readers must always finish (no slot left odd by two writers) and only ever see masks
 // that were written; once the writers stop, every slot is readable again.
@@ -574,6 +631,8 @@ int main() {
   test_hpack();
   std::fprintf(stderr, "[selftest] histogram render cache\n");
   test_histogram_render_cache();
+  std::fprintf(stderr, "[selftest] lanes + session gate\n");
+  test_lanes_and_gate();
   std::fprintf(stderr, "[selftest] recent allocations ring\n");
   test_recent_allocations_ring();
   std::fprintf(stderr, "[selftest] allocator + table\n");

@@ -378,6 +378,7 @@ void Exporter::sample_once(uint64_t sampler_gen) {
     if (sl.job && !sl.job->done()) continue;
     sl.out = std::make_shared<GpuSample>();
     sl.job = be->sample_async(sl.index, sl.out);
+    sl.refused = !sl.job;
     sl.posted_ns = mono_ns();
     const int64_t until = mono_ns() + slice_ms * 1000000;
     while (sl.job && !sl.job->done()) {  // in short waits, so stop() stays prompt
@@ -402,7 +403,10 @@ void Exporter::sample_once(uint64_t sampler_gen) {
     }
     // a sample is shown while its GPU's newer call is still within the budget; not once
     // that call is stuck (the values would pass for current)
-    const bool stuck = sl.job && stall > 0 && now - sl.posted_ns > static_cast<int64_t>(stall) * 1000000;
+    // nor when its lane refused the call (another call to that GPU, e.g. a discovery's,
+    // is stuck there)
+    const bool stuck = sl.refused ||
+                       (sl.job && stall > 0 && now - sl.posted_ns > static_cast<int64_t>(stall) * 1000000);
     ok[g] = sl.last_ok && !stuck && sl.last_ok_ns != 0;
     samples[g] = sl.last;
   }

@@ -129,6 +129,7 @@ class Exporter : public std::enable_shared_from_this<Exporter> {
     GpuSample last;                        // last completed sample
     bool last_ok = false;
     int64_t last_ok_ns = 0;
+    bool refused = false;                  // the lane took no job this pass (busy with a stuck call)
   };
   std::vector<Slot> slots_;
   uint64_t slots_gen_ = ~0ull;             // inventory generation slots_ belongs to

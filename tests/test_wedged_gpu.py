@@ -272,3 +272,37 @@ def test_devices_indices_wait_for_gpus_missing_at_first_discovery(make_cfg, plug
         # and a GPU that drops off the bus does not shift GPU 2 into the selection
         be.set_gpu_present(0, False)
         assert _wait(lambda: [g.uuid for g in m.gpus] == [uuids[1]], 5), [g.uuid for g in m.gpus]
+
+
+def test_sampler_refused_by_a_lane_stuck_in_discovery_shows_the_gpu_down(n):
+    """The call that wedges a GPU need not be a sample: a discovery's describe can hang on
+    its lane while the sampler is between passes.  Past the stall threshold the lane takes
+    no new job, and the sampler must then show that GPU as not sampled
+    (`amdgpu_telemetry_up` 0, growing sample age), not keep rendering its last values as
+    current."""
+    import threading
+    be = fixtures.build_backend("2gpu_spx")
+    gpus, _ = be.discover()
+    be.set_stall_ms(150)
+    be.set_call_timeout_ms(100)
+    ex = n.Exporter()
+    ex.set_inventory(gpus)
+    ex.set_stall_ms(150)
+    ex.start(be, 400, None)  # long interval: the wedge starts between passes
+    try:
+        assert _wait(lambda: 'amdgpu_telemetry_up{gpu="1"} 1' in ex.render(), 3)
+        time.sleep(0.05)  # just after a pass
+        be.set_sample_stall(1, True)
+        t = threading.Thread(target=be.discover, daemon=True)  # describe(1) hangs on lane 1
+        t.start()
+        t.join(5)
+        assert not t.is_alive(), "discovery waited on the wedged GPU past its bound"
+        assert _wait(lambda: 'amdgpu_telemetry_up{gpu="1"} 0' in ex.render(), 3)
+        text = ex.render()
+        assert 'amdgpu_telemetry_up{gpu="0"} 1' in text
+        assert ex.sample_age_s(1) > 0.15 and 0 <= ex.sample_age_s(0) < 1.0
+        lanes = {r[0]: r for r in be.lanes()}
+        assert lanes[1][2] == "describe", lanes  # the stuck call is the discovery's
+    finally:
+        be.set_sample_stall(1, False)
+        ex.stop()
