@@ -2,8 +2,8 @@
 
 Metric and configs come from BASELINE.json.  One rank per GPU (``torch.distributed.run
 --nproc-per-node N``); rank 0 launches the plugin daemon as a child process *before*
-anything touches the GPU, advertising the node's first N physical GPUs (amdsmi backend
-on MI355X, an N-GPU fixture node model elsewhere) and an in-process kubelet stub for it
+anything touches the GPU, advertising the N GPUs that HIP numbers 0..N-1 (``devices:
+hip:0-<N-1>``; amdsmi backend on MI355X, an N-GPU fixture node model elsewhere) and an in-process kubelet stub for it
 to register with.  Every rank then acts as one kubelet-side client for "its" GPU:
 
   step = ALLOCS Allocate RPCs through a compiled HTTP/2 gRPC client (kubelet-like)
@@ -203,7 +203,7 @@ def start_daemon(n_gpus: int, grpc_server: str, workdir: str, profile_dir: str =
     # one server worker per client connection: every rank holds two kubelet-side
     # connections (compiled h2 + grpcio) and SCRAPE_CONNS scrapers
     cfg = {"webListenAddress": "127.0.0.1:%d" % port, "migStrategy": "none", "backend": backend,
-           "fixture": fixture or "%dgpu_spx" % n_gpus, "devices": "0-%d" % (n_gpus - 1), "pluginDir": plugin_dir,
+           "fixture": fixture or "%dgpu_spx" % n_gpus, "devices": "hip:0-%d" % (n_gpus - 1), "pluginDir": plugin_dir,
            "log": {"level": "info", "fileDir": ""},
            "http": {"accessLog": False, "threads": max(4, SCRAPE_CONNS * n_gpus)},
            "telemetry": {"intervalMs": 1000},

@@ -166,6 +166,7 @@ class PluginManager:
         # so a GPU that drops off the bus does not shift the others into the selection
         self._seen_bdfs: dict[str, str] = {}  # bdf -> identity
         self._selection: tuple | None = None
+        self._hip_fallback_logged = False
         self.device_map = None
         self._discoverer: Discoverer | None = None
         self._discovery_error: str | None = None
@@ -687,14 +688,23 @@ class PluginManager:
         drops off the bus the others keep their index (the selection does not take in
         the next GPU), and a GPU missing from the first discovery takes its own index when
         it appears instead of leaving its index to a neighbour for good.  UUIDs and BDFs
-        are matched as given."""
+        are matched as given, and ``hip:<n>`` selects the GPU a HIP ordinal opens."""
         sel = parse_device_selector(self.cfg.devices)
         if sel is None:
             return list(gpus)
         indices, names = sel
+        hips = {int(x[4:]) for x in names if x.startswith("hip:")}
+        if hips and not any(p.hip_id >= 0 for g in gpus for p in g.partitions):
+            # the driver reports no HIP ordinals: the HIP runtime numbers GPUs in PCI order
+            # unless told otherwise, so hip:<n> falls back to BDF rank n
+            if not self._hip_fallback_logged:
+                log.warning("devices %r: no HIP ordinals reported; hip:<n> selects by BDF rank", self.cfg.devices)
+                self._hip_fallback_logged = True
+            indices = sorted(set(indices) | hips)
         rank = {bdf: i for i, bdf in enumerate(sorted(self._seen_bdfs))}
         out = [g for g in gpus if rank.get((g.bdf or "").lower(), -1) in indices
-               or (g.uuid or "").lower() in names or (g.bdf or "").lower() in names]
+               or (g.uuid or "").lower() in names or (g.bdf or "").lower() in names
+               or any(p.hip_id >= 0 and "hip:%d" % p.hip_id in names for p in g.partitions)]
         chosen = tuple(self._identity(g) for g in out)
         if chosen != self._selection:
             log.info("devices %r selects %s", self.cfg.devices, ", ".join(chosen) or "nothing (yet)")

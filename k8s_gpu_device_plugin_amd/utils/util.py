@@ -54,8 +54,10 @@ def envelope_bytes(obj: dict) -> bytes:
 
 
 def parse_device_selector(spec: str | None):
-    """``devices``: ``"0-3,6"`` style indices and/or GPU identities (UUID or PCI BDF),
-    comma-separated.  Returns ``None`` for "all", else ``(indices, names)``."""
+    """``devices``: ``"0-3,6"`` style indices, GPU identities (UUID or PCI BDF) and/or
+    host HIP ordinals (``"hip:0-3"``: the GPUs whose partitions the HIP runtime numbers
+    0-3, i.e. what ``cuda:0``..``cuda:3`` open), comma-separated.  Returns ``None`` for
+    "all", else ``(indices, names)``; HIP ordinals are in ``names`` as ``"hip:<n>"``."""
     if spec is None:
         return None
     spec = str(spec).strip()
@@ -66,6 +68,12 @@ def parse_device_selector(spec: str | None):
     for part in spec.split(","):
         part = part.strip()
         if not part:
+            continue
+        if part.lower().startswith("hip:"):
+            hip = parse_index_list(part[4:])
+            if not hip:
+                raise ValueError("devices: %r names no HIP ordinal" % part)
+            names.update("hip:%d" % i for i in hip)
             continue
         a, sep, b = part.partition("-")
         if part.isdigit():

@@ -838,6 +838,25 @@ def test_devices_selection_stays_on_the_same_gpus(make_cfg, plugin_dir, run_mana
     by_name = PluginManager(make_cfg(fixture="4gpu_spx", devices="%s,%s" % (gpus[3].bdf, gpus[1].uuid.upper())),
                             backend=fixtures.build_backend("4gpu_spx"))
     assert sorted(g.index for g in by_name._selected(gpus)) == [1, 3]
+    # hip:<n> selects the GPU a HIP ordinal opens (bench.py advertises hip:0-<N-1>), also
+    # where HIP numbers GPUs in another order than PCI
+    assert parse_device_selector("hip:0-1,2") == ([2], {"hip:0", "hip:1"})
+    pbe = fixtures.build_backend("4gpu_spx_hip_permuted")
+    pgpus, _ = pbe.discover()
+    by_hip = PluginManager(make_cfg(fixture="4gpu_spx_hip_permuted", devices="hip:0-1"), backend=pbe)
+    chosen = by_hip._selected(pgpus)
+    assert sorted(p.hip_id for g in chosen for p in g.partitions) == [0, 1]
+    assert sorted(g.index for g in chosen) != [0, 1], "fixture no longer permutes HIP against BDF order"
+    # a driver that reports no HIP ordinals: hip:<n> is BDF rank n
+    for g in pgpus:
+        for p in g.partitions:
+            p.hip_id = -1
+    no_hip = PluginManager(make_cfg(fixture="4gpu_spx_hip_permuted", devices="hip:0-1"),
+                           backend=fixtures.build_backend("4gpu_spx_hip_permuted"))
+    no_hip._note_seen(pgpus)
+    by_bdf = sorted(pgpus, key=lambda g: g.bdf.lower())[:2]
+    assert sorted(g.index for g in no_hip._selected(pgpus)) == sorted(g.index for g in by_bdf)
+    assert sorted(g.index for g in by_bdf) != sorted(g.index for g in chosen)
 
 
 @pytest.mark.parametrize("fault", ["worker", "listener"])
