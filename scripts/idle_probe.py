@@ -22,6 +22,7 @@ daemon's gRPC worker threads (``dpgrpc-*`` in /proc/<pid>/task) and of the calli
 thread, read before and after the call.
 
     python scripts/idle_probe.py [--gaps 0.001,0.01,0.1,1] [--calls 300] [--out FILE]
+    python scripts/idle_probe.py --gaps 1 --calls 100 --ab-keep-warm 0,10   # A/B, interleaved
 
 Prints a progress line every 30 s, one JSON line per gap, then the whole result.
 """
@@ -112,6 +113,56 @@ def self_faults():
     return r.ru_minflt, r.ru_majflt
 
 
+class Daemon:
+    """One plugin daemon (bench config) with a kubelet-like compiled HTTP/2 client."""
+
+    def __init__(self, n, a, keep_warm_ms):
+        from k8s_gpu_device_plugin_amd.api import v1beta1
+        from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import DevicePluginClient
+        self.keep_warm_ms = keep_warm_ms
+        self.workdir = tempfile.mkdtemp(prefix="idleprobe-", dir="/tmp")
+        over = {"grpc": {"keepWarmMs": keep_warm_ms}} if keep_warm_ms is not None else None
+        self.proc, self.kubelet, self.port, reg, self.backend = bench.start_daemon(
+            1, "native", self.workdir, busy_poll_us=a.busy_poll_us, admission_poll_us=a.admission_poll_us,
+            backend=a.backend, overrides=over)
+        sock = os.path.join(self.workdir, "device-plugins", reg.endpoint)
+        c = DevicePluginClient(sock)
+        law = c.list_and_watch()
+        ids = [d.ID for d in next(iter(law)).devices]
+        law.cancel()
+        self.alloc = v1beta1.AllocateRequest(container_requests=[
+            v1beta1.ContainerAllocateRequest(devices_ids=ids[:1])]).SerializeToString()
+        self.pref = v1beta1.PreferredAllocationRequest(container_requests=[
+            v1beta1.ContainerPreferredAllocationRequest(available_deviceIDs=ids, must_include_deviceIDs=ids[:1],
+                                                        allocation_size=1)]).SerializeToString()
+        self.resp_len = len(c.allocate_raw(self.alloc))
+        c.close()
+        self.h2 = n.H2Client(sock)
+        self.h2.bench_unary(v1beta1.METHOD_ALLOCATE, self.alloc, 2000)  # warm the connection and the code
+        self.tids = worker_tids(self.proc.pid)
+        import http.client
+        self.mconn = http.client.HTTPConnection("127.0.0.1", self.port, timeout=10)
+        self.base = {}
+        self.allocate = lambda: self.h2.bench_unary(v1beta1.METHOD_ALLOCATE, self.alloc, 1)[0]
+        self.preferred = lambda: self.h2.bench_unary(v1beta1.METHOD_GET_PREFERRED, self.pref, 1)[0]
+
+    def close(self):
+        try:
+            self.h2.close()
+        except Exception:
+            pass
+        try:
+            os.killpg(self.proc.pid, signal.SIGTERM)
+        except ProcessLookupError:
+            pass
+        try:
+            self.proc.wait(15)
+        except subprocess.TimeoutExpired:
+            os.killpg(self.proc.pid, signal.SIGKILL)
+        self.kubelet.stop()
+        shutil.rmtree(self.workdir, ignore_errors=True)
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gaps", default="0.001,0.01,0.1,1")
@@ -120,6 +171,10 @@ def main() -> int:
     ap.add_argument("--admission-poll-us", type=int, default=None, help="override grpc.admissionPollUs")
     ap.add_argument("--busy-poll-us", type=int, default=None, help="override grpc.busyPollUs / http.busyPollUs")
     ap.add_argument("--keep-warm-ms", type=int, default=None, help="override grpc.keepWarmMs")
+    ap.add_argument("--ab-keep-warm", default="",
+                    help="A,B[,C..]: one daemon per grpc.keepWarmMs value, their Allocate and "
+                         "GetPreferredAllocation calls interleaved with the floor's (kinds allocate@A, ...); "
+                         "paired differences of A to each other value")
     ap.add_argument("--server-time", action="store_true",
                     help="also read the daemon's own time per call from its RPC histogram (a /metrics "
                          "scrape after each timed call)")
@@ -127,62 +182,55 @@ def main() -> int:
     a = ap.parse_args()
 
     from k8s_gpu_device_plugin_amd import native
-    from k8s_gpu_device_plugin_amd.api import v1beta1
-    from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import DevicePluginClient
 
     n = native.load()
-    workdir = tempfile.mkdtemp(prefix="idleprobe-", dir="/tmp")
-    over = {"grpc": {"keepWarmMs": a.keep_warm_ms}} if a.keep_warm_ms is not None else None
-    proc, kubelet, port, reg, backend = bench.start_daemon(1, "native", workdir, busy_poll_us=a.busy_poll_us,
-                                                         admission_poll_us=a.admission_poll_us, backend=a.backend,
-                                                         overrides=over)
-    res = {"backend": backend, "keep_warm_ms": a.keep_warm_ms, "calls_per_kind_per_gap": a.calls, "kinds": list(KINDS),
-           "floor_server_epoll_timeout_ms": 100, "rows": []}
+    ab = [int(x) for x in a.ab_keep_warm.split(",")] if a.ab_keep_warm else None
+    daemons = {}
     t_progress = time.monotonic()
+    res = {"calls_per_kind_per_gap": a.calls, "floor_server_epoll_timeout_ms": 100, "rows": []}
     try:
-        sock = os.path.join(workdir, "device-plugins", reg.endpoint)
-        c = DevicePluginClient(sock)
-        law = c.list_and_watch()
-        ids = [d.ID for d in next(iter(law)).devices]
-        law.cancel()
-        alloc = v1beta1.AllocateRequest(container_requests=[
-            v1beta1.ContainerAllocateRequest(devices_ids=ids[:1])]).SerializeToString()
-        pref = v1beta1.PreferredAllocationRequest(container_requests=[
-            v1beta1.ContainerPreferredAllocationRequest(available_deviceIDs=ids, must_include_deviceIDs=ids[:1],
-                                                        allocation_size=1)]).SerializeToString()
-        resp_len = len(c.allocate_raw(alloc))
-        c.close()
-        sizes = (9 + 80 + 9 + 5 + len(alloc), 9 + 20 + 9 + 5 + resp_len + 9 + 16)
+        if ab:
+            for kw in ab:
+                daemons["@%d" % kw] = Daemon(n, a, kw)
+        else:
+            daemons[""] = Daemon(n, a, a.keep_warm_ms)
+        first = next(iter(daemons.values()))
+        res["backend"] = first.backend
+        res["keep_warm_ms"] = ab if ab else a.keep_warm_ms
+        sizes = (9 + 80 + 9 + 5 + len(first.alloc), 9 + 20 + 9 + 5 + first.resp_len + 9 + 16)
         pinger = n.UdsPinger(*sizes, server_timeout_ms=100)
-        h2 = n.H2Client(sock)
-        h2.bench_unary(v1beta1.METHOD_ALLOCATE, alloc, 2000)  # warm the connection and the code
         for _ in range(200):
             pinger.once()
-        tids = worker_tids(proc.pid)
-        import http.client
-        mconn = http.client.HTTPConnection("127.0.0.1", port, timeout=10)
+        # kinds: <rpc><daemon tag>, and the floor
+        call, owner = {"floor": pinger.once}, {}
+        for tag, d in daemons.items():
+            call["allocate" + tag], owner["allocate" + tag] = d.allocate, d
+            call["preferred" + tag], owner["preferred" + tag] = d.preferred, d
+        kinds = tuple(k for k in call if k != "floor") + ("floor",)
+        rpcs = [k for k in kinds if k != "floor"]
+        res["kinds"] = list(kinds)
+        res["daemon_grpc_workers"] = len(first.tids)
         rpc_name = {"allocate": "Allocate", "preferred": "GetPreferredAllocation"}
-        res["daemon_grpc_workers"] = len(tids)
-        call = {"allocate": lambda: h2.bench_unary(v1beta1.METHOD_ALLOCATE, alloc, 1)[0],
-                "preferred": lambda: h2.bench_unary(v1beta1.METHOD_GET_PREFERRED, pref, 1)[0],
-                "floor": pinger.once}
         for gap in [float(x) for x in a.gaps.split(",")]:
-            lat = {k: [] for k in KINDS}
-            srv = {k: [] for k in ("allocate", "preferred")}  # the daemon's own time per call
-            mconn._base = {}
+            lat = {k: [] for k in kinds}
+            srv = {k: [] for k in rpcs}  # the daemon's own time per call
+            for d in daemons.values():
+                d.base = {}
             ev = {k: {"daemon_minflt": 0, "daemon_majflt": 0, "daemon_run_us": 0.0, "daemon_wait_us": 0.0,
-                      "daemon_slices": 0, "client_minflt": 0} for k in KINDS}
+                      "daemon_slices": 0, "client_minflt": 0} for k in kinds}
             for i in range(a.calls):
-                order = KINDS[i % 3:] + KINDS[:i % 3]
+                r = i % len(kinds)
+                order = kinds[r:] + kinds[:r]
                 for kind in order:
                     time.sleep(gap)
                     # the counters are read around every kind, the floor's too, so each
                     # call follows the same client-side work
-                    d0 = thread_counters(proc.pid, tids)
+                    d = owner.get(kind, first)
+                    d0 = thread_counters(d.proc.pid, d.tids)
                     s0 = self_faults()
                     lat[kind].append(call[kind]())
                     s1 = self_faults()
-                    d1 = thread_counters(proc.pid, tids)
+                    d1 = thread_counters(d.proc.pid, d.tids)
                     if kind != "floor":
                         e = ev[kind]
                         e["daemon_minflt"] += d1[0] - d0[0]
@@ -192,19 +240,19 @@ def main() -> int:
                         e["daemon_slices"] += d1[4] - d0[4]
                     ev[kind]["client_minflt"] += s1[0] - s0[0]
                     if kind != "floor" and a.server_time:  # read after the timed call
-                        base = mconn._base.get(kind)
-                        cur = server_seconds(mconn, rpc_name[kind])
+                        base = d.base.get(kind)
+                        cur = server_seconds(d.mconn, rpc_name[kind.split("@")[0]])
                         if base is not None:
                             srv[kind].append(cur - base)
-                        mconn._base[kind] = cur
+                        d.base[kind] = cur
                 if time.monotonic() - t_progress > 30:
                     t_progress = time.monotonic()
                     print(json.dumps({"progress": {"gap_s": gap, "iteration": i + 1, "of": a.calls}}), flush=True)
             us = lambda v: round(v * 1e6, 2)  # noqa: E731
             row = {"gap_s": gap, "calls": a.calls}
-            for k in KINDS:
+            for k in kinds:
                 row[k] = {"p50_us": us(median(lat[k])), "p90_us": us(pct(lat[k], 0.9))}
-            for k in ("allocate", "preferred"):
+            for k in rpcs:
                 diffs = [x - y for x, y in zip(lat[k], lat["floor"])]
                 lo, hi = bootstrap_ci(diffs)
                 row[k]["minus_floor_median_us"] = us(median(diffs))
@@ -213,22 +261,21 @@ def main() -> int:
                 if srv[k]:  # the daemon's own part of the call (dispatch -> encoded answer)
                     row[k]["server_p50_us"] = us(median(srv[k]))
                     row[k]["server_p90_us"] = us(pct(srv[k], 0.9))
+            if ab:  # paired difference of the first daemon to each other one, call by call
+                for other in ab[1:]:
+                    for rpc in ("allocate", "preferred"):
+                        x, y = lat["%s@%d" % (rpc, ab[0])], lat["%s@%d" % (rpc, other)]
+                        diffs = [p - q for p, q in zip(x, y)]
+                        lo, hi = bootstrap_ci(diffs)
+                        row["%s_@%d_minus_@%d" % (rpc, ab[0], other)] = {
+                            "median_us": us(median(diffs)), "ci95_us": [us(lo), us(hi)]}
             row["floor"]["per_call"] = {"client_minflt": round(ev["floor"]["client_minflt"] / a.calls, 3)}
             res["rows"].append(row)
             print(json.dumps(row), flush=True)
-        h2.close()
         del pinger
     finally:
-        try:
-            os.killpg(proc.pid, signal.SIGTERM)
-        except ProcessLookupError:
-            pass
-        try:
-            proc.wait(15)
-        except subprocess.TimeoutExpired:
-            os.killpg(proc.pid, signal.SIGKILL)
-        kubelet.stop()
-        shutil.rmtree(workdir, ignore_errors=True)
+        for d in daemons.values():
+            d.close()
     if a.out:
         os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
         with open(a.out, "w") as f:
