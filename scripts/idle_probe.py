@@ -175,6 +175,11 @@ def main() -> int:
                     help="A,B[,C..]: one daemon per grpc.keepWarmMs value, their Allocate and "
                          "GetPreferredAllocation calls interleaved with the floor's (kinds allocate@A, ...); "
                          "paired differences of A to each other value")
+    ap.add_argument("--replicas", type=int, default=1,
+                    help="with --ab-keep-warm: daemons per value (their placement on the host's CPUs "
+                         "differs; several per value keep one daemon's placement from passing for the "
+                         "setting's effect)")
+    ap.add_argument("--rpcs", default="allocate,preferred", help="RPC kinds to time (allocate, preferred)")
     ap.add_argument("--server-time", action="store_true",
                     help="also read the daemon's own time per call from its RPC histogram (a /metrics "
                          "scrape after each timed call)")
@@ -190,8 +195,9 @@ def main() -> int:
     res = {"calls_per_kind_per_gap": a.calls, "floor_server_epoll_timeout_ms": 100, "rows": []}
     try:
         if ab:
-            for kw in ab:
-                daemons["@%d" % kw] = Daemon(n, a, kw)
+            for r in range(a.replicas):
+                for kw in ab:
+                    daemons["@%d" % kw + ("#%d" % r if a.replicas > 1 else "")] = Daemon(n, a, kw)
         else:
             daemons[""] = Daemon(n, a, a.keep_warm_ms)
         first = next(iter(daemons.values()))
@@ -203,9 +209,12 @@ def main() -> int:
             pinger.once()
         # kinds: <rpc><daemon tag>, and the floor
         call, owner = {"floor": pinger.once}, {}
+        want = a.rpcs.split(",")
         for tag, d in daemons.items():
-            call["allocate" + tag], owner["allocate" + tag] = d.allocate, d
-            call["preferred" + tag], owner["preferred" + tag] = d.preferred, d
+            if "allocate" in want:
+                call["allocate" + tag], owner["allocate" + tag] = d.allocate, d
+            if "preferred" in want:
+                call["preferred" + tag], owner["preferred" + tag] = d.preferred, d
         kinds = tuple(k for k in call if k != "floor") + ("floor",)
         rpcs = [k for k in kinds if k != "floor"]
         res["kinds"] = list(kinds)
@@ -241,7 +250,7 @@ def main() -> int:
                     ev[kind]["client_minflt"] += s1[0] - s0[0]
                     if kind != "floor" and a.server_time:  # read after the timed call
                         base = d.base.get(kind)
-                        cur = server_seconds(d.mconn, rpc_name[kind.split("@")[0]])
+                        cur = server_seconds(d.mconn, rpc_name[kind.split("@")[0].split("#")[0]])
                         if base is not None:
                             srv[kind].append(cur - base)
                         d.base[kind] = cur
@@ -261,10 +270,14 @@ def main() -> int:
                 if srv[k]:  # the daemon's own part of the call (dispatch -> encoded answer)
                     row[k]["server_p50_us"] = us(median(srv[k]))
                     row[k]["server_p90_us"] = us(pct(srv[k], 0.9))
-            if ab:  # paired difference of the first daemon to each other one, call by call
+            if ab:  # paired difference of the first value to each other one, iteration by
+                # iteration (each arm's latency averaged over its replicas)
+                def arm(rpc, kw):
+                    ks = [k for k in kinds if k.split("#")[0] == "%s@%d" % (rpc, kw)]
+                    return [sum(v) / len(v) for v in zip(*(lat[k] for k in ks))]
                 for other in ab[1:]:
-                    for rpc in ("allocate", "preferred"):
-                        x, y = lat["%s@%d" % (rpc, ab[0])], lat["%s@%d" % (rpc, other)]
+                    for rpc in [r for r in ("allocate", "preferred") if r in want]:
+                        x, y = arm(rpc, ab[0]), arm(rpc, other)
                         diffs = [p - q for p, q in zip(x, y)]
                         lo, hi = bootstrap_ci(diffs)
                         row["%s_@%d_minus_@%d" % (rpc, ab[0], other)] = {
