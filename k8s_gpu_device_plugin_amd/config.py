@@ -149,7 +149,7 @@ class Config:
     pluginDir: str = v1beta1.DEVICE_PLUGIN_PATH
     backend: str = "auto"                 # auto | amdsmi | fixture
     fixture: str = "2gpu_spx"             # builtin name or path, used by backend=fixture
-    devices: str = ""                     # physical GPU filter: "0-3", UUIDs or BDFs ("" = all)
+    devices: str = ""                     # physical GPU filter: "0-3", UUIDs, BDFs, "hip:0-3" ("" = all)
     resourcePrefix: str = "amd.com"
     resources: list = field(default_factory=list)  # [ResourceSpec]
     visibleDevicesEnv: str = "AMD_VISIBLE_DEVICES"
@@ -325,6 +325,11 @@ def validate(cfg: Config) -> Config:
         raise ConfigError("health.discoveryTimeoutS must be > 0")
     if cfg.sharing.replicas < 1:
         raise ConfigError("sharing.replicas must be >= 1")
+    from .utils.util import parse_device_selector
+    try:
+        parse_device_selector(cfg.devices)
+    except ValueError as e:
+        raise ConfigError("devices: %s" % e) from None
     if cfg.grpc.server not in ("native", "python"):
         raise ConfigError("grpc.server must be native|python")
     for sect in ("grpc", "http"):

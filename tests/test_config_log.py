@@ -61,7 +61,8 @@ def test_env_overrides(tmp_path):
                                  {"resourcePrefix": "x" * 64 + ".com"}, {"resourcePrefix": ("a" * 60 + ".") * 5},
                                  {"resourcePrefix": "AMD.com"}, {"resourcePrefix": "amd..com"},
                                  {"grpc": {"busyPollUs": -1}}, {"http": {"busyPollUs": 200000}},
-                                 {"grpc": {"admissionPollUs": 100001}}])
+                                 {"grpc": {"admissionPollUs": 100001}}, {"devices": "hip:"},
+                                 {"devices": "hip:x-2"}])
 def test_validation_errors(raw):
     with pytest.raises(C.ConfigError):
         C.validate(C.from_dict(raw))
