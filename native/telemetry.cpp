@@ -261,6 +261,18 @@ void Exporter::watchdog_loop(std::shared_ptr<HealthMonitor> monitor) {
     const int64_t threshold = static_cast<int64_t>(ms) * 1000000;
     const int64_t grace = std::min<int64_t>(threshold / 2, 200000000);
     const int64_t last_done = be->last_completion_ns();
+    // only GPUs this exporter serves (the `devices` selection) are reported: a GPU left out
+    // is never sampled, so nothing would clear a "lost" verdict on it.  Every stuck lane
+    // still counts for attribution (a left-out GPU can be the root of a library-wide block).
+    std::vector<char> served;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (const auto& g : gpus_) {
+        if (g.index >= static_cast<int>(served.size())) served.resize(g.index + 1, 0);
+        if (g.index >= 0) served[g.index] = 1;
+      }
+    }
+    auto is_served = [&](int i) { return i >= 0 && i < static_cast<int>(served.size()) && served[i]; };
     std::vector<LaneReport> stuck;
     for (auto& r : be->lanes())
       if (r.index >= 0 && r.lane.inflight_since_ns && now - r.lane.inflight_since_ns > threshold) stuck.push_back(r);
@@ -269,6 +281,7 @@ void Exporter::watchdog_loop(std::shared_ptr<HealthMonitor> monitor) {
     auto st = std::make_shared<Stalls>();
     std::map<std::string, int64_t> still;
     for (const auto& r : stuck) {
+      if (!is_served(r.index)) continue;
       const int64_t since = r.lane.inflight_since_ns;
       if (since != root && last_done <= since + grace) {
         st->blocked.push_back(r.index);

@@ -98,15 +98,21 @@ class _Allocator(threading.Thread):
 
 # CHAOS_SEEDS=N runs seeds 1..N (a longer hunt); the suite runs three
 @pytest.mark.parametrize("seed", range(1, 1 + int(os.environ.get("CHAOS_SEEDS", "3"))))
-@pytest.mark.parametrize("fixture,strategy,server,devices", [("4gpu_spx", "none", "native", ""),
-                                                             ("4gpu_cpx", "single", "native", ""),
-                                                             ("4gpu_spx", "none", "python", ""),
-                                                             ("4gpu_spx", "none", "native", "0-2")])
-def test_random_fault_mix_converges(make_cfg, plugin_dir, tmp_path, seed, fixture, strategy, server, devices):
+# serialised: the fixture driver takes one library-wide lock for every device call (as a
+# driver that serialises devices would), so a wedged call also blocks every other GPU's
+# calls and every discovery until it returns
+@pytest.mark.parametrize("fixture,strategy,server,devices,serialised", [("4gpu_spx", "none", "native", "", False),
+                                                                        ("4gpu_cpx", "single", "native", "", False),
+                                                                        ("4gpu_spx", "none", "python", "", False),
+                                                                        ("4gpu_spx", "none", "native", "0-2", False),
+                                                                        ("4gpu_spx", "none", "native", "", True)])
+def test_random_fault_mix_converges(make_cfg, plugin_dir, tmp_path, seed, fixture, strategy, server, devices,
+                                    serialised):
     from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import PodResourcesStub
     n = native.load()
     rng = random.Random(seed)
     be = fixtures.build_backend(fixture)
+    be.set_serialised(serialised)
     gpus, _ = be.discover()
     assert len(gpus) == NGPU
     shown = range(NGPU - 1) if devices else range(NGPU)  # the GPUs `devices` advertises (all but the last)

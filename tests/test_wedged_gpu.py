@@ -306,3 +306,39 @@ def test_sampler_refused_by_a_lane_stuck_in_discovery_shows_the_gpu_down(n):
     finally:
         be.set_sample_stall(1, False)
         ex.stop()
+
+
+def test_watchdog_ignores_a_gpu_the_devices_selection_leaves_out(n):
+    """A GPU outside `devices` is never sampled, so nothing would ever clear a "lost"
+    verdict on it: a call stuck on its lane (a discovery's describe) must not be reported.
+    It still roots a library-wide block: the served GPUs are then "blocked", not lost."""
+    import threading
+    for serialised in (False, True):
+        be = fixtures.build_backend("4gpu_spx")
+        be.set_serialised(serialised)
+        gpus, _ = be.discover()
+        be.set_stall_ms(150)
+        be.set_call_timeout_ms(100)
+        mon = n.HealthMonitor(be, 3)
+        served = [g for g in gpus if g.index in (0, 1)]
+        mon.set_gpus([be.gpu_key(g.index) for g in served])
+        ex = n.Exporter()
+        ex.set_inventory(served)
+        ex.set_stall_ms(150)
+        ex.start(be, 50, mon)
+        try:
+            be.set_sample_stall(3, True)
+            t = threading.Thread(target=be.discover, daemon=True)  # describe(3) hangs on lane 3
+            t.start()
+            t.join(5)
+            time.sleep(0.5)
+            assert ex.stalled_gpus == [] and mon.unhealthy_keys() == [], (serialised, ex.stalled_gpus,
+                                                                          mon.unhealthy_keys())
+            if serialised:  # behind the library-wide lock, the served GPUs wait on GPU 3's call
+                assert _wait(lambda: ex.blocked_gpus == [0, 1], 3), ex.blocked_gpus
+            else:
+                assert _wait(lambda: all(0 <= ex.sample_age_s(g) < 0.5 for g in (0, 1)), 3)
+        finally:
+            be.set_sample_stall(3, False)
+            ex.stop()
+        assert _wait(lambda: ex.blocked_gpus == [] or not ex.running, 3)
