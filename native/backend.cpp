@@ -55,13 +55,15 @@ bool Backend::run_on_lane(const std::string& key, const char* what, uint64_t ses
   return job && job->wait(ms) && !job->dropped();
 }
 
-std::shared_ptr<LaneJob> Backend::sample_async(int gpu, std::shared_ptr<GpuSample> out) {
+std::shared_ptr<LaneJob> Backend::sample_async(int gpu, std::shared_ptr<GpuSample> out, const std::string& key) {
   auto inv = inventory();
+  if (!key.empty()) gpu = inv->index_of(key);
   if (gpu < 0 || gpu >= static_cast<int>(inv->refs.size())) return nullptr;
   out->key = inv->refs[gpu].key;
   auto self = shared_from_this();
   return post_job(inv->refs[gpu].key, "sample", inv->session, [self, inv, gpu, out] {
     out->ok = self->sample_device(*inv, gpu, out.get());
+    for (int k = 0; k < out->num_links && k < kMaxXgmiLinks; ++k) out->link_peer_key[k] = inv->key_of(out->link_peer[k]);
   });
 }
 
@@ -232,6 +234,7 @@ void Backend::discover(std::vector<GpuInfo>* gpus, Topology* topo) {
     inv->refs.push_back(refs[kept[k]]);
     GpuInfo g = desc[k]->info;
     g.index = k;
+    g.key = refs[kept[k]].key;
     for (auto& p : g.partitions) p.gpu = k;
     inv->gpus.push_back(std::move(g));
   }

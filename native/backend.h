@@ -87,6 +87,7 @@ struct PartitionProfile {
 
 struct GpuInfo {
   int index = -1;
+  std::string key;            // Backend::gpu_key: the identity lanes and health are keyed by
   std::string uuid;
   std::string bdf;            // dddd:bb:dd.f
   std::string market_name;    // e.g. "AMD Instinct MI355X"
@@ -148,6 +149,9 @@ constexpr int kMaxPartitions = 8;
 // One telemetry sample of a physical GPU.  NaN / negative = unavailable.
 struct GpuSample {
   std::string key;  // Backend::gpu_key of the GPU this sample read (set even when it failed)
+  // link_peer[k] as identities, resolved against the inventory the sample was read with
+  // (an index means another GPU once a re-discovery has moved the indices)
+  std::string link_peer_key[kMaxXgmiLinks];
   int64_t ts_ns = 0;
   double power_w = -1;
   double energy_j = -1;            // accumulated
@@ -300,7 +304,10 @@ class Backend : public std::enable_shared_from_this<Backend> {
   bool sample(int gpu, GpuSample* out);
   // The same call without waiting: null when there is no such GPU or its lane refused the
   // job (wedged).  The job fills *out; read it only once job->done() && !job->dropped().
-  std::shared_ptr<LaneJob> sample_async(int gpu, std::shared_ptr<GpuSample> out);
+  // `key` (optional): the GPU's identity; it is looked up in the current inventory, so a
+  // caller holding indices of an older discovery never samples the GPU that moved into
+  // that index (null when the GPU is gone).
+  std::shared_ptr<LaneJob> sample_async(int gpu, std::shared_ptr<GpuSample> out, const std::string& key = "");
   // Stable identity (UUID, else BDF) of the GPU at index `gpu` of the latest discover(),
   // in the index space sample() and events use; "" when unknown.  Health state is keyed
   // by it: when a GPU drops off the bus and the node re-enumerates, every later GPU moves

@@ -78,6 +78,7 @@ PYBIND11_MODULE(_native, m) {
   py::class_<GpuInfo>(m, "GpuInfo")
       .def(py::init<>())
       .def_readwrite("index", &GpuInfo::index)
+      .def_readwrite("key", &GpuInfo::key)
       .def_readwrite("uuid", &GpuInfo::uuid)
       .def_readwrite("bdf", &GpuInfo::bdf)
       .def_readwrite("market_name", &GpuInfo::market_name)
@@ -146,6 +147,9 @@ PYBIND11_MODULE(_native, m) {
   py::class_<GpuSample>(m, "GpuSample")
       .def(py::init<>())
       .def_readonly("key", &GpuSample::key)
+      .def_property_readonly("link_peer_keys", [](const GpuSample& s) {
+        return std::vector<std::string>(s.link_peer_key, s.link_peer_key + std::max(0, std::min(s.num_links, kMaxXgmiLinks)));
+      })
       .def_readonly("ts_ns", &GpuSample::ts_ns)
       .def_readonly("ok", &GpuSample::ok)
       .def_readonly("power_w", &GpuSample::power_w)

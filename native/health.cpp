@@ -270,7 +270,8 @@ void HealthMonitor::on_sample(int gpu, bool ok, const GpuSample& s) {
   std::vector<std::string> peer_keys(static_cast<size_t>(std::max(0, s.num_links)));
   if (ok)
     for (int k = 0; k < s.num_links; ++k)
-      if (s.link_peer[k] >= 0) peer_keys[k] = key_of(s.link_peer[k], "");
+      if (s.link_peer[k] >= 0)
+        peer_keys[k] = !s.link_peer_key[k].empty() ? s.link_peer_key[k] : key_of(s.link_peer[k], "");
   std::vector<HwEvent> derived;
   {
     std::lock_guard<std::mutex> lk(mu_);

@@ -264,15 +264,20 @@ void Exporter::watchdog_loop(std::shared_ptr<HealthMonitor> monitor) {
     // only GPUs this exporter serves (the `devices` selection) are reported: a GPU left out
     // is never sampled, so nothing would clear a "lost" verdict on it.  Every stuck lane
     // still counts for attribution (a left-out GPU can be the root of a library-wide block).
-    std::vector<char> served;
+    std::vector<std::string> served;  // keys (an index may have moved since set_inventory)
+    std::vector<int> served_index;
     {
       std::lock_guard<std::mutex> lk(mu_);
       for (const auto& g : gpus_) {
-        if (g.index >= static_cast<int>(served.size())) served.resize(g.index + 1, 0);
-        if (g.index >= 0) served[g.index] = 1;
+        served.push_back(g.key);
+        served_index.push_back(g.index);
       }
     }
-    auto is_served = [&](int i) { return i >= 0 && i < static_cast<int>(served.size()) && served[i]; };
+    auto is_served = [&](const LaneReport& r) {
+      for (size_t i = 0; i < served.size(); ++i)
+        if (served[i].empty() ? served_index[i] == r.index : served[i] == r.lane.key) return true;
+      return false;
+    };
     std::vector<LaneReport> stuck;
     for (auto& r : be->lanes())
       if (r.index >= 0 && r.lane.inflight_since_ns && now - r.lane.inflight_since_ns > threshold) stuck.push_back(r);
@@ -281,7 +286,7 @@ void Exporter::watchdog_loop(std::shared_ptr<HealthMonitor> monitor) {
     auto st = std::make_shared<Stalls>();
     std::map<std::string, int64_t> still;
     for (const auto& r : stuck) {
-      if (!is_served(r.index)) continue;
+      if (!is_served(r)) continue;
       const int64_t since = r.lane.inflight_since_ns;
       if (since != root && last_done <= since + grace) {
         st->blocked.push_back(r.index);
@@ -363,14 +368,21 @@ void Exporter::sample_once(uint64_t sampler_gen) {
   // for and label each GPU by its backend index, never by its position in the subset.
   uint64_t gen;
   std::vector<int> index;
+  std::vector<std::string> keys;
   {
     std::lock_guard<std::mutex> lk(mu_);
-    for (const auto& g : gpus_) index.push_back(g.index);
+    for (const auto& g : gpus_) {
+      index.push_back(g.index);
+      keys.push_back(g.key);
+    }
     gen = inventory_gen_;
   }
   if (gen != slots_gen_) {  // a reload: samples in flight belong to the old indices
     slots_.assign(index.size(), Slot{});
-    for (size_t g = 0; g < index.size(); ++g) slots_[g].index = index[g];
+    for (size_t g = 0; g < index.size(); ++g) {
+      slots_[g].index = index[g];
+      slots_[g].key = keys[g];
+    }
     slots_gen_ = gen;
   }
   const size_t n = slots_.size();
@@ -390,7 +402,7 @@ void Exporter::sample_once(uint64_t sampler_gen) {
     Slot& sl = slots_[g];
     if (sl.job && !sl.job->done()) continue;
     sl.out = std::make_shared<GpuSample>();
-    sl.job = be->sample_async(sl.index, sl.out);
+    sl.job = be->sample_async(sl.index, sl.out, sl.key);
     sl.refused = !sl.job;
     sl.posted_ns = mono_ns();
     const int64_t until = mono_ns() + slice_ms * 1000000;

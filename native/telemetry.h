@@ -123,6 +123,7 @@ class Exporter : public std::enable_shared_from_this<Exporter> {
   // One GPU's sampling state across passes (guarded by sample_mu_).
   struct Slot {
     int index = -1;                        // backend index
+    std::string key;                       // the GPU's identity (sampled by it, see sample_async)
     std::shared_ptr<LaneJob> job;          // in flight (null: none)
     std::shared_ptr<GpuSample> out;
     int64_t posted_ns = 0;

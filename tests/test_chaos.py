@@ -265,10 +265,14 @@ def test_random_fault_mix_converges(make_cfg, plugin_dir, tmp_path, seed, fixtur
                 return topo and [(x, y, topo.link(x, y).up, topo.link(x, y).bw_gbps, topo.link(x, y).pods)
                                  for x in range(topo.n) for y in range(x + 1, topo.n)]
 
-            assert _wait(whole, timeout=15), (table() and [(i, table().healthy(i)) for i in table().ids()],
-                                              links_now(), log,
-                                              [ln for ln in m.exporter.render().splitlines()
-                                               if ln.startswith("amdgpu_xgmi_link_bandwidth")])
+            if not _wait(whole, timeout=15):
+                detail = (table() and [(i, table().healthy(i)) for i in table().ids()], links_now(), log,
+                          [ln for ln in m.exporter.render().splitlines()
+                           if ln.startswith("amdgpu_xgmi_link_bandwidth")])
+                if os.environ.get("CHAOS_DUMP"):  # the full picture; pytest truncates the message
+                    with open(os.path.join(os.environ["CHAOS_DUMP"], "chaos_%s_%d.txt" % (fixture, seed)), "w") as f:
+                        f.write(repr(detail))
+                raise AssertionError(detail)
             assert _wait(lambda: m.monitor.unhealthy_keys() == [], timeout=5), m.monitor.unhealthy_keys()
             assert m.running and m.fatal_error is None
             assert _wait(lambda: _advertised(plugin_dir, k) == [(i, "Healthy") for i in ids], timeout=10), \

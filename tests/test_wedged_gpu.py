@@ -342,3 +342,35 @@ def test_watchdog_ignores_a_gpu_the_devices_selection_leaves_out(n):
             be.set_sample_stall(3, False)
             ex.stop()
         assert _wait(lambda: ex.blocked_gpus == [] or not ex.running, 3)
+
+
+def test_samples_follow_identity_when_a_rediscovery_moves_the_indices(n):
+    """Between a re-discovery and the manager's reload the exporter still holds the old
+    indices.  GPU 1 leaves the bus: the backend's index 2 is now slot 3.  The exporter
+    must keep sampling the GPU it serves as "2" (by identity), never the one that moved
+    into that index, and link peers must name the GPUs the sample saw (found by the chaos
+    test: a left-out GPU's stale link view pinned a healed link at half rate)."""
+    be = fixtures.build_backend("4gpu_spx")
+    gpus, _ = be.discover()
+    keys = [g.key for g in gpus]
+    assert all(keys) and len(set(keys)) == 4
+    served = [g for g in gpus if g.index in (0, 1, 2)]
+    mon = n.HealthMonitor(be, 3)
+    mon.set_gpus([g.key for g in served])
+    ex = n.Exporter()
+    ex.set_inventory(served)
+    ex.start(be, 30, mon)
+    try:
+        assert _wait(lambda: ex.last_sample(2).key == keys[2], 3)
+        peers = ex.last_sample(0).link_peer_keys
+        assert sorted(peers) == sorted(keys[1:]), peers
+        be.set_gpu_present(1, False)
+        moved, _ = be.discover()
+        assert [g.key for g in moved] == [keys[0], keys[2], keys[3]]
+        time.sleep(0.3)  # several passes with the old indices
+        assert ex.last_sample(2).key == keys[2]  # sampled by identity, not index 2 (slot 3)
+        peers = [k for k in ex.last_sample(0).link_peer_keys if k]  # "" = a peer no longer enumerated
+        assert set(peers) <= set(keys) and keys[3] in peers and keys[1] not in peers, peers
+        assert 'amdgpu_telemetry_up{gpu="1"} 0' in ex.render()  # gone from the bus: not sampled
+    finally:
+        ex.stop()
