@@ -18,8 +18,11 @@ namespace prof {
 namespace {
 
 constexpr size_t kCapacity = 1u << 20;  // ~17 min at 1 kHz of one busy core
-uintptr_t g_buf[kCapacity];
-uint32_t g_weight[kCapacity];  // 1 + expirations merged into this signal (overrun)
+// Slots are atomics: the handler may still be writing one (a signal in flight while stop()
+// runs, or histogram() read while sampling) - relaxed atomics are lock-free and
+// async-signal-safe, and a reader sees either a whole slot or an empty one (pc 0).
+std::atomic<uintptr_t> g_buf[kCapacity];
+std::atomic<uint32_t> g_weight[kCapacity];  // 1 + expirations merged into this signal (overrun)
 std::atomic<size_t> g_next{0};
 timer_t g_timer{};
 std::atomic<bool> g_on{false};
@@ -40,8 +43,8 @@ void on_sigprof(int, siginfo_t*, void* uc) {
   const int over = timer_getoverrun(g_timer);
   const size_t i = g_next.fetch_add(1, std::memory_order_relaxed);
   if (i < kCapacity) {
-    g_buf[i] = pc;
-    g_weight[i] = 1u + static_cast<uint32_t>(over > 0 ? over : 0);
+    g_weight[i].store(1u + static_cast<uint32_t>(over > 0 ? over : 0), std::memory_order_relaxed);
+    g_buf[i].store(pc, std::memory_order_release);  // publishes the weight with it
   }
 }
 
@@ -50,6 +53,8 @@ void on_sigprof(int, siginfo_t*, void* uc) {
 bool start(int hz) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (g_on.load() || hz <= 0) return false;
+  const size_t used = std::min(g_next.load(), kCapacity);
+  for (size_t i = 0; i < used; ++i) g_buf[i].store(0, std::memory_order_relaxed);
   g_next.store(0);
   struct sigaction sa {};
   sa.sa_sigaction = on_sigprof;
@@ -94,7 +99,10 @@ std::vector<std::pair<uintptr_t, uint64_t>> histogram() {
   std::lock_guard<std::mutex> lk(g_mu);
   const size_t n = std::min(g_next.load(), kCapacity);
   std::unordered_map<uintptr_t, uint64_t> counts;
-  for (size_t i = 0; i < n; ++i) counts[g_buf[i]] += g_weight[i];
+  for (size_t i = 0; i < n; ++i) {
+    const uintptr_t pc = g_buf[i].load(std::memory_order_acquire);
+    if (pc != 0) counts[pc] += g_weight[i].load(std::memory_order_relaxed);  // 0: not written yet
+  }
   std::vector<std::pair<uintptr_t, uint64_t>> out(counts.begin(), counts.end());
   std::sort(out.begin(), out.end(), [](const auto& a, const auto& b) {
     return a.second != b.second ? a.second > b.second : a.first < b.first;

@@ -706,8 +706,11 @@ def test_canary_result_does_not_pass_to_the_gpu_that_takes_its_index(make_cfg, p
         be.set_gpu_present(0, False)
         assert _wait(lambda: len(m.plugins) == 1 and m.plugins[0].table.ids() != [], timeout=10)
         assert _wait(lambda: len(m.gpus) == 1, timeout=10)
-        with m._canary_lock:
-            assert m.canary_results == {}  # (0, 0) was GPU 0's, (1, 0) no longer exists
+
+        def pruned():  # the reload prunes them just after it installs the new inventory
+            with m._canary_lock:
+                return m.canary_results == {}  # (0, 0) was GPU 0's, (1, 0) no longer exists
+        assert _wait(pruned, timeout=5), m.canary_results
 
 
 def test_link_retrain_reaches_the_allocator(make_cfg, plugin_dir, run_manager):
