@@ -610,6 +610,7 @@ class AmdSmiBackend : public Backend {
     std::vector<void*> flat;
     std::vector<std::shared_ptr<std::vector<void*>>> armed;
     std::vector<std::shared_ptr<LaneJob>> jobs;
+    const uint64_t batch = next_batch();  // posted to every lane at once
     for (const auto& r : inv->refs) {
       flat.insert(flat.end(), r.handles.begin(), r.handles.end());
       auto out = std::make_shared<std::vector<void*>>();
@@ -624,7 +625,7 @@ class AmdSmiBackend : public Backend {
           }
           out->push_back(h);
         }
-      }));
+      }, batch));
     }
     const int64_t deadline = mono_ns() + static_cast<int64_t>(call_timeout_ms()) * 1000000;
     std::vector<void*> live;

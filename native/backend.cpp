@@ -32,7 +32,7 @@ std::string Backend::gpu_key(int gpu) const { return inventory()->key_of(gpu); }
 int64_t Backend::last_completion_ns() const { return last_completion_ns_.load(); }
 
 std::shared_ptr<LaneJob> Backend::post_job(const std::string& key, const char* what, uint64_t session,
-                                       std::function<void()> fn) {
+                                       std::function<void()> fn, uint64_t batch) {
   // The closure keeps the backend alive (fn captures shared_from_this()), so the gate and
   // the completion clock it touches outlive a caller that stopped waiting.
   auto job = std::make_shared<LaneJob>(what, [this, session, fn = std::move(fn)] {
@@ -43,7 +43,7 @@ std::shared_ptr<LaneJob> Backend::post_job(const std::string& key, const char* w
     } leave{gate_};
     fn();
     last_completion_ns_.store(mono_ns());
-  });
+  }, batch);
   const int stall = stall_ms_.load();
   if (!lanes_.get(key)->post(job, static_cast<int64_t>(stall) * 1000000)) return nullptr;
   return job;
@@ -142,6 +142,7 @@ void Backend::discover(std::vector<GpuInfo>* gpus, Topology* topo) {
     session = gate_.session();
     enumerate(&refs);  // throws: nothing installed, the previous inventory stays
     auto all = std::make_shared<const std::vector<DeviceRef>>(refs);
+    const uint64_t batch = next_batch();  // posted to every lane at once
     for (size_t i = 0; i < refs.size(); ++i) {
       auto out = std::make_shared<Out>();
       outs.push_back(out);
@@ -153,7 +154,7 @@ void Backend::discover(std::vector<GpuInfo>* gpus, Topology* topo) {
         } catch (const std::exception& e) {
           out->error = e.what();
         }
-      }));
+      }, batch));
     }
     const int64_t deadline = mono_ns() + static_cast<int64_t>(call_timeout_ms_.load()) * 1000000;
     for (auto& j : jobs)

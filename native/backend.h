@@ -374,7 +374,9 @@ class Backend : public std::enable_shared_from_this<Backend> {
                    int64_t ms);
   // Same, without waiting: null when the lane refused it.
   std::shared_ptr<LaneJob> post_job(const std::string& key, const char* what, uint64_t session,
-                                    std::function<void()> fn);
+                                    std::function<void()> fn, uint64_t batch = 0);
+  // a fresh batch number for jobs posted to several lanes at once (see LaneJob)
+  uint64_t next_batch() { return batch_seq_.fetch_add(1) + 1; }
   SessionGate& gate() { return gate_; }
   LaneSet& lanes_set() { return lanes_; }
 
@@ -384,6 +386,7 @@ class Backend : public std::enable_shared_from_this<Backend> {
     std::map<std::string, Link> links;  // peer key -> this GPU's view of the link
   };
   LaneSet lanes_;
+  std::atomic<uint64_t> batch_seq_{0};
   SessionGate gate_;
   std::atomic<int> call_timeout_ms_{10000};
   std::atomic<int> stall_ms_{0};

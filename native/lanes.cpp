@@ -113,7 +113,10 @@ LaneState Lane::state() const {
   st.key = key_;
   std::lock_guard<std::mutex> lk(s_->mu);
   st.inflight_since_ns = s_->inflight ? s_->inflight_since : 0;
-  if (s_->inflight) st.inflight_what = s_->inflight->what();
+  if (s_->inflight) {
+    st.inflight_what = s_->inflight->what();
+    st.inflight_batch = s_->inflight->batch();
+  }
   st.completed = s_->completed;
   st.last_done_ns = s_->last_done;
   st.queued = s_->queue.size();

@@ -35,13 +35,17 @@ int64_t mono_ns();
 // owned by the closure (shared_ptr captures), never by the submitter's stack.
 class LaneJob {
  public:
-  LaneJob(std::string what, std::function<void()> fn) : what_(std::move(what)), fn_(std::move(fn)) {}
+  // batch: jobs posted to several lanes at once by one caller (a discovery's describes)
+  // share a nonzero batch; 0 = a job posted on its own
+  LaneJob(std::string what, std::function<void()> fn, uint64_t batch = 0)
+      : what_(std::move(what)), fn_(std::move(fn)), batch_(batch) {}
   // true once the call has run (or was dropped, see dropped()); waits at most ms (< 0: forever)
   bool wait(int64_t ms);
   bool done() const { return done_.load(std::memory_order_acquire); }
   // the lane shut down (or refused it) before the call ran: its outputs were never written
   bool dropped() const { return dropped_.load(std::memory_order_acquire); }
   const std::string& what() const { return what_; }
+  uint64_t batch() const { return batch_; }
   int64_t started_ns() const { return started_ns_.load(); }
   int64_t finished_ns() const { return finished_ns_.load(); }
   // the call threw (the lane caught it and carried on); valid once done()
@@ -55,6 +59,7 @@ class LaneJob {
   void finish();
   std::string what_;
   std::function<void()> fn_;
+  const uint64_t batch_;
   std::string error_;  // written before done_ is released
   std::mutex mu_;
   std::condition_variable cv_;
@@ -67,6 +72,7 @@ struct LaneState {
   std::string key;
   int64_t inflight_since_ns = 0;  // 0 = idle
   std::string inflight_what;
+  uint64_t inflight_batch = 0;    // LaneJob::batch of the call in flight
   uint64_t completed = 0;         // calls run to completion
   int64_t last_done_ns = 0;       // mono ns the last call ended
   size_t queued = 0;

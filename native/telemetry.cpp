@@ -282,13 +282,25 @@ void Exporter::watchdog_loop(std::shared_ptr<HealthMonitor> monitor) {
     for (auto& r : be->lanes())
       if (r.index >= 0 && r.lane.inflight_since_ns && now - r.lane.inflight_since_ns > threshold) stuck.push_back(r);
     int64_t root = 0;
-    for (const auto& r : stuck) root = root ? std::min(root, r.lane.inflight_since_ns) : r.lane.inflight_since_ns;
+    uint64_t root_batch = 0;
+    for (const auto& r : stuck)
+      if (!root || r.lane.inflight_since_ns < root) {
+        root = r.lane.inflight_since_ns;
+        root_batch = r.lane.inflight_batch;
+      }
+    // The root is known only if its call went out on its own (the sampler's walk posts one
+    // call at a time).  When the earliest stuck call belongs to a batch posted to several
+    // lanes at once (a discovery's describes) and other calls of that batch are stuck too,
+    // any of them may hold a library-wide lock the others wait on: blame none of them.
+    const bool ambiguous = root_batch != 0 && std::count_if(stuck.begin(), stuck.end(), [&](const LaneReport& r) {
+                                                 return r.lane.inflight_batch == root_batch;
+                                               }) > 1;
     auto st = std::make_shared<Stalls>();
     std::map<std::string, int64_t> still;
     for (const auto& r : stuck) {
       if (!is_served(r)) continue;
       const int64_t since = r.lane.inflight_since_ns;
-      if (since != root && last_done <= since + grace) {
+      if ((since != root || ambiguous) && last_done <= since + grace) {
         st->blocked.push_back(r.index);
         continue;
       }
