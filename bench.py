@@ -27,7 +27,8 @@ the rank loads torch or joins the RCCL group, and the returned render node exist
 run fails unless WORLD_SIZE == --gpus == the number of devices the daemon advertised
 (one kubelet-client rank per advertised GPU).  Rank r allocates the device whose host HIP
 ordinals (``hip_ids`` of ``amdgpu_partition_info``, from amdsmi's enumeration info) hold
-its LOCAL_RANK, so the canary, ``torch.cuda.set_device(local_rank)`` and the allocation
+its LOCAL_RANK (mapped through ROCR_/HIP_VISIBLE_DEVICES to the host's numbering when
+they are set), so the canary, ``torch.cuda.set_device(local_rank)`` and the allocation
 name the same GPU even where the HIP runtime's numbering differs from BDF order.
 
 Speed-of-light references, measured untimed in the same run: ``uds_roundtrip_floor_p50_us``
@@ -176,6 +177,28 @@ def device_for_rank(metrics_text: str, ids, resource: str, local_rank: int, rank
     return ids[rank], [], "enumeration order"
 
 
+def host_ordinals(count: int, env=None):
+    """The host's HIP ordinal of each of this process's GPU ordinals 0..count-1.  amdsmi
+    reports a partition's ``hip_id`` in the host's numbering, while ROCR_VISIBLE_DEVICES
+    and then HIP_VISIBLE_DEVICES (or CUDA_VISIBLE_DEVICES) renumber what a process - torch,
+    the canary - sees.  ``None`` when a list is not plain ordinals (UUIDs): then the two
+    numberings are taken to agree."""
+    env = os.environ if env is None else env
+    phys = list(range(4096))
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES" if "HIP_VISIBLE_DEVICES" in env else "CUDA_VISIBLE_DEVICES"):
+        spec = env.get(var)
+        if spec is None or spec.strip() == "":
+            continue
+        try:
+            sel = [int(x) for x in spec.split(",") if x.strip()]
+        except ValueError:
+            return None
+        if any(i < 0 or i >= len(phys) for i in sel):
+            return None
+        phys = [phys[i] for i in sel]
+    return phys[:count] if len(phys) >= count else None
+
+
 def resolve_backend(n, requested: str = "auto") -> str:
     """amdsmi when asked for, or when auto and amdsmi sees a GPU; else the fixture node
     model (CPU runs, and multi-rank rehearsals on a box with fewer GPUs than ranks)."""
@@ -185,7 +208,7 @@ def resolve_backend(n, requested: str = "auto") -> str:
 
 
 def start_daemon(n_gpus: int, grpc_server: str, workdir: str, profile_dir: str = "", busy_poll_us=None,
-                 admission_poll_us=None, overrides=None, backend: str = "auto", fixture: str = ""):
+                 admission_poll_us=None, overrides=None, backend: str = "auto", fixture: str = "", hips=None):
     """Rank 0: kubelet stub + plugin daemon subprocess.  Must run before GPU init.
     ``overrides``: config sections merged over the bench's own (probes, A/B runs)."""
     import yaml
@@ -203,7 +226,7 @@ def start_daemon(n_gpus: int, grpc_server: str, workdir: str, profile_dir: str =
     # one server worker per client connection: every rank holds two kubelet-side
     # connections (compiled h2 + grpcio) and SCRAPE_CONNS scrapers
     cfg = {"webListenAddress": "127.0.0.1:%d" % port, "migStrategy": "none", "backend": backend,
-           "fixture": fixture or "%dgpu_spx" % n_gpus, "devices": "hip:0-%d" % (n_gpus - 1), "pluginDir": plugin_dir,
+           "fixture": fixture or "%dgpu_spx" % n_gpus, "devices": ",".join("hip:%d" % h for h in (hips or range(n_gpus))), "pluginDir": plugin_dir,
            "log": {"level": "info", "fileDir": ""},
            "http": {"accessLog": False, "threads": max(4, SCRAPE_CONNS * n_gpus)},
            "telemetry": {"intervalMs": 1000},
@@ -268,12 +291,16 @@ def main() -> int:
     workdir = os.path.join(tempfile.gettempdir(), "amdgpu-dp-bench-%s-%d" % (master_port, os.getuid()))
     proc = kubelet = None
     info = None
+    # the host HIP ordinals of the ranks' GPUs (local rank r opens its ordinal r, which the
+    # *_VISIBLE_DEVICES variables may have renumbered); a fixture node numbers its own
+    real = resolve_backend(n, args.backend) == "amdsmi"
+    hips = (host_ordinals(n_gpus) if real else None) or list(range(n_gpus))
     if rank == 0:  # daemon first: nothing has touched the GPU in this process yet
         shutil.rmtree(workdir, ignore_errors=True)
         os.makedirs(workdir)
         proc, kubelet, port, reg, backend = start_daemon(n_gpus, args.grpc_server, workdir, args.profile_dir,
                                                          args.busy_poll_us, args.admission_poll_us,
-                                                         backend=args.backend, fixture=args.fixture)
+                                                         backend=args.backend, fixture=args.fixture, hips=hips)
         info = {"port": port, "endpoint": reg.endpoint, "resource": reg.resource_name, "backend": backend,
                 "plugin_dir": os.path.join(workdir, "device-plugins")}
 
@@ -324,8 +351,10 @@ def main() -> int:
     body = conn.getresponse().read()
     if b"amdgpu_info{" not in body:
         raise RuntimeError("/metrics lacks the GPU inventory")
-    # the device of this rank's GPU (HIP ordinal local_rank), not the rank-th in BDF order
-    my_id, my_hips, mapped_by = device_for_rank(body.decode(), ids, info["resource"], local_rank, rank)
+    # the device of this rank's GPU (HIP ordinal local_rank, in the host's numbering), not
+    # the rank-th in BDF order
+    my_id, my_hips, mapped_by = device_for_rank(body.decode(), ids, info["resource"],
+                                                hips[local_rank] if local_rank < len(hips) else local_rank, rank)
     alloc_req = v1beta1.AllocateRequest(container_requests=[
         v1beta1.ContainerAllocateRequest(devices_ids=[my_id])]).SerializeToString()
     pref_req = v1beta1.PreferredAllocationRequest(container_requests=[

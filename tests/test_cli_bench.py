@@ -143,6 +143,22 @@ def test_bench_ranks_allocate_the_gpu_of_their_hip_ordinal():
     assert r["dtype"] == "n/a"
 
 
+def test_host_ordinals_follow_the_visible_devices_variables():
+    """amdsmi's hip_id is the host's numbering; a launcher that sets HIP_VISIBLE_DEVICES
+    (or CUDA_/ROCR_VISIBLE_DEVICES) renumbers what the ranks open.  bench.py advertises and
+    allocates by the host ordinals of the ranks' GPUs."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.host_ordinals(2, {}) == [0, 1]
+    assert bench.host_ordinals(2, {"HIP_VISIBLE_DEVICES": "4,5,6"}) == [4, 5]
+    assert bench.host_ordinals(2, {"CUDA_VISIBLE_DEVICES": "7,3"}) == [7, 3]
+    assert bench.host_ordinals(1, {"HIP_VISIBLE_DEVICES": "2", "CUDA_VISIBLE_DEVICES": "5"}) == [2]
+    # ROCR renumbers first, HIP indexes into what ROCR left
+    assert bench.host_ordinals(2, {"ROCR_VISIBLE_DEVICES": "2,4,6", "HIP_VISIBLE_DEVICES": "2,0"}) == [6, 2]
+    assert bench.host_ordinals(1, {"HIP_VISIBLE_DEVICES": "GPU-abc"}) is None  # UUIDs: not mappable
+    assert bench.host_ordinals(3, {"HIP_VISIBLE_DEVICES": "0,1"}) is None  # fewer GPUs than ranks
+
+
 def test_bench_refuses_rank_gpu_mismatch():
     """--gpus must equal WORLD_SIZE (one kubelet-client rank per advertised GPU): a run
     that would report n_gpus it did not have fails before it starts a daemon."""
