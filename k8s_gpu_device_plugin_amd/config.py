@@ -122,6 +122,7 @@ class GrpcConfig:
     busyPollUs: int = 50         # native server: keep polling this long after a request (0 = off)
     admissionPollUs: int = 1000  # ... and this long after a GetPreferredAllocation (its Allocate follows)
     keepWarmMs: int = 10         # native server: idle workers with a connection replay canned requests (0 = off)
+    keepWarmFull: bool = True    # ... through the whole request path of an in-memory connection (else HPACK + table)
 
 
 @dataclass

@@ -256,6 +256,7 @@ class AmdDevicePlugin:
         srv.set_table(self.table)
         if self.cfg is not None:
             srv.set_keep_warm_ms(int(self.cfg.grpc.keepWarmMs))
+            srv.set_keep_warm_full(bool(self.cfg.grpc.keepWarmFull))
         srv.start()
         self._native_server = srv
 

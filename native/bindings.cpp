@@ -681,6 +681,7 @@ PYBIND11_MODULE(_native, m) {
       .def("failure", &GrpcServer::failure)
       .def("inject_fault", &GrpcServer::inject_fault)
       .def("set_keep_warm_ms", &GrpcServer::set_keep_warm_ms)
+      .def("set_keep_warm_full", &GrpcServer::set_keep_warm_full)
       .def_property_readonly("warm_ticks", &GrpcServer::warm_ticks);
 
   py::class_<H2Client>(m, "H2Client")

@@ -213,6 +213,7 @@ struct GrpcServer::Worker {
     size_t buffered = 0;  // request bytes held across all streams
     bool closing = false;
     bool want_out = false;
+    bool internal = false;  // the keep-warm tick's private connection: no fd, no accounting
   };
   std::unordered_map<int, std::unique_ptr<Conn>> conns;
   // Connections are spread over the workers: the one that accepts hands a new
@@ -553,6 +554,10 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
       table->observe(kRpcListAndWatch, (mono_ns() - t0) * 1e-9, false);
     }
   };
+  // the keep-warm connection's requests are not kubelet's: no counter or histogram sees them
+  auto observe = [&](const Conn& c, int rpc, double dt, bool err) {
+    if (!c.internal) table->observe(rpc, dt, err);
+  };
   auto dispatch = [&](Conn& c, uint32_t sid, Stream& s, std::string_view body) {
     if (s.dispatched) {  // END_STREAM seen twice (trailers or DATA after the request)
       rst_stream(c, sid, kStreamClosed);
@@ -561,7 +566,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
     }
     s.dispatched = true;
     const int64_t t0 = mono_ns();
-    requests_.add();
+    if (!c.internal) requests_.add();
     const Method m = static_cast<Method>(s.method);
     if (m == kMUnknown) {
       send_error(c, sid, s, 12, "unknown method " + s.path);  // UNIMPLEMENTED
@@ -594,7 +599,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
         case kMPreferred:
           rpc = kRpcPreferred;
           ok = table->preferred(msg, &out);
-          admitting = true;  // this container's Allocate is next
+          if (!c.internal) admitting = true;  // this container's Allocate is next
           break;
         case kMOptions:
           rpc = kRpcOptions;
@@ -615,7 +620,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
                   },
                   &err)) {
             send_error(c, sid, s, 2, err);
-            table->observe(rpc, (mono_ns() - t0) * 1e-9, true);
+            observe(c, rpc, (mono_ns() - t0) * 1e-9, true);
           }
           return;
         }
@@ -626,7 +631,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
           s.law_version = table->version();
           send_headers(c, sid);
           send_message(c, sid, s, table->list_and_watch(), false);
-          table->observe(rpc, (mono_ns() - t0) * 1e-9, false);
+          observe(c, rpc, (mono_ns() - t0) * 1e-9, false);
           return;
         }
         default:
@@ -634,7 +639,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
       }
     } catch (const std::exception& e) {  // e.g. bad_alloc on a hostile request: INTERNAL, keep serving
       send_error(c, sid, s, 13, std::string("internal error: ") + e.what());
-      table->observe(rpc, (mono_ns() - t0) * 1e-9, true);
+      observe(c, rpc, (mono_ns() - t0) * 1e-9, true);
       return;
     }
     if (ok) {
@@ -643,7 +648,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
     } else {
       send_error(c, sid, s, 2, out);  // UNKNOWN, like a plain Go error from a handler
     }
-    table->observe(rpc, (mono_ns() - t0) * 1e-9, !ok);
+    observe(c, rpc, (mono_ns() - t0) * 1e-9, !ok);
   };
   struct PathSink {
     bool seen = false;
@@ -902,16 +907,20 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
   };
 
   uint64_t seen_version = table->version();
-  // canned requests for the keep-warm tick: a typical request header block and an
+  // canned requests for the keep-warm tick: typical request header blocks and an
   // Allocate / GetPreferredAllocation of the table's first device
-  std::string warm_hdrs, warm_alloc, warm_pref, warm_out;
+  std::string warm_hdrs, warm_hdrs_pref, warm_alloc, warm_pref, warm_out;
   {
-    hpack::encode_indexed(&warm_hdrs, 3);  // :method POST
-    hpack::encode_indexed(&warm_hdrs, 6);  // :scheme http
-    hpack::encode_literal_name_index(&warm_hdrs, 4, "/v1beta1.DevicePlugin/Allocate");  // :path
-    hpack::encode_literal_name_index(&warm_hdrs, 1, "localhost");                      // :authority
-    hpack::encode_literal(&warm_hdrs, "content-type", "application/grpc");
-    hpack::encode_literal(&warm_hdrs, "te", "trailers");
+    auto headers = [](std::string* h, std::string_view path) {
+      hpack::encode_indexed(h, 3);                                    // :method POST
+      hpack::encode_indexed(h, 6);                                    // :scheme http
+      hpack::encode_literal_name_index(h, 4, path);                   // :path
+      hpack::encode_literal_name_index(h, 1, "localhost");            // :authority
+      hpack::encode_literal(h, "content-type", "application/grpc");
+      hpack::encode_literal(h, "te", "trailers");
+    };
+    headers(&warm_hdrs, "/v1beta1.DevicePlugin/Allocate");
+    headers(&warm_hdrs_pref, "/v1beta1.DevicePlugin/GetPreferredAllocation");
     const std::vector<std::string> ids = table->ids();
     if (!ids.empty()) {
       std::string ctr;
@@ -924,6 +933,39 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
       pb::put_bytes(&warm_pref, 1, pctr);
     }
   }
+  // The full tick: a private in-memory connection (no socket) gets an Allocate and a
+  // GetPreferredAllocation as kubelet's client would frame them, and the worker runs them
+  // through the same path as a real request - frame parsing, HPACK, dispatch, the table,
+  // response framing - then drops the answer.  Marked internal: nothing is counted.
+  std::unique_ptr<Conn> warm_conn;
+  uint32_t warm_sid = 1;
+  auto warm_full = [&] {
+    if (warm_alloc.empty()) return;
+    if (!warm_conn || warm_sid > (1u << 30)) {  // (re)start: preface + empty SETTINGS
+      warm_conn = std::make_unique<Conn>();
+      warm_conn->internal = true;
+      warm_sid = 1;
+      warm_conn->in.assign(kPreface, kPrefaceLen);
+      frame(&warm_conn->in, 0, kSettings, 0, 0);
+    }
+    Conn& c = *warm_conn;
+    for (int k = 0; k < 2; ++k) {
+      const std::string& h = k == 0 ? warm_hdrs : warm_hdrs_pref;
+      const std::string& m = k == 0 ? warm_alloc : warm_pref;
+      frame(&c.in, static_cast<uint32_t>(h.size()), kHeaders, kEndHeaders, warm_sid);
+      c.in.append(h);
+      frame(&c.in, static_cast<uint32_t>(5 + m.size()), kData, kEndStream, warm_sid);
+      grpc_prefix(&c.in, m.size());
+      c.in.append(m);
+      warm_sid += 2;
+    }
+    if (!process(c)) warm_conn.reset();  // cannot happen with these frames; start over if it does
+    if (warm_conn) {
+      c.out.clear();
+      c.out_off = 0;
+      c.send_window = 65535;  // no peer sends WINDOW_UPDATEs here
+    }
+  };
   int64_t last_activity = mono_ns();
   const int64_t spin_ns = static_cast<int64_t>(busy_poll_us_) * 1000;
   const int64_t admission_ns = static_cast<int64_t>(admission_poll_us_) * 1000;
@@ -958,13 +1000,17 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
       if (n == 0 && warm > 0 && !w->conns.empty() && !warm_alloc.empty()) {
         const int64_t now = mono_ns();
         if (now - last_activity >= static_cast<int64_t>(warm) * 1000000) {
-          hpack::Decoder d(4096);
-          d.decode(reinterpret_cast<const uint8_t*>(warm_hdrs.data()), warm_hdrs.size(),
-                   [](void*, std::string_view, std::string_view) {}, nullptr);
-          warm_out.clear();
-          table->allocate(warm_alloc, &warm_out);
-          warm_out.clear();
-          table->preferred(warm_pref, &warm_out);
+          if (keep_warm_full_.load(std::memory_order_relaxed)) {
+            warm_full();
+          } else {
+            hpack::Decoder d(4096);
+            d.decode(reinterpret_cast<const uint8_t*>(warm_hdrs.data()), warm_hdrs.size(),
+                     [](void*, std::string_view, std::string_view) {}, nullptr);
+            warm_out.clear();
+            table->allocate(warm_alloc, &warm_out);
+            warm_out.clear();
+            table->preferred(warm_pref, &warm_out);
+          }
           warm_ticks_.fetch_add(1, std::memory_order_relaxed);
           last_activity = now;
         }

@@ -68,6 +68,10 @@ class GrpcServer {
   // kubelet's sparse calls do not find that code and data evicted.  Experimental: see
   // scripts/idle_probe.py --keep-warm-ms and BASELINE.md.
   void set_keep_warm_ms(int ms) { keep_warm_ms_.store(ms > 0 ? ms : 0); }
+  // full: the tick runs canned requests through the whole request path of a private
+  // in-memory connection (frame parsing, HPACK, dispatch, table, response framing);
+  // otherwise only the HPACK decode and the table calls
+  void set_keep_warm_full(bool on) { keep_warm_full_.store(on); }
   uint64_t warm_ticks() const { return warm_ticks_.load(); }
   std::vector<int> worker_connections() const;  // connections owned per worker thread
   const std::string& socket_path() const { return path_; }
@@ -100,6 +104,7 @@ class GrpcServer {
   int busy_poll_us_;
   int admission_poll_us_;
   std::atomic<int> keep_warm_ms_{0};
+  std::atomic<bool> keep_warm_full_{true};
   std::atomic<uint64_t> warm_ticks_{0};
   std::shared_ptr<DeviceTable> table_;
   int listen_fd_ = -1;

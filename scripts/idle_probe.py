@@ -116,12 +116,14 @@ def self_faults():
 class Daemon:
     """One plugin daemon (bench config) with a kubelet-like compiled HTTP/2 client."""
 
-    def __init__(self, n, a, keep_warm_ms):
+    def __init__(self, n, a, keep_warm_ms, overrides=None):
         from k8s_gpu_device_plugin_amd.api import v1beta1
         from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import DevicePluginClient
         self.keep_warm_ms = keep_warm_ms
         self.workdir = tempfile.mkdtemp(prefix="idleprobe-", dir="/tmp")
         over = {"grpc": {"keepWarmMs": keep_warm_ms}} if keep_warm_ms is not None else None
+        if overrides:
+            over = overrides
         self.proc, self.kubelet, self.port, reg, self.backend = bench.start_daemon(
             1, "native", self.workdir, busy_poll_us=a.busy_poll_us, admission_poll_us=a.admission_poll_us,
             backend=a.backend, overrides=over)
@@ -175,6 +177,9 @@ def main() -> int:
                     help="A,B[,C..]: one daemon per grpc.keepWarmMs value, their Allocate and "
                          "GetPreferredAllocation calls interleaved with the floor's (kinds allocate@A, ...); "
                          "paired differences of A to each other value")
+    ap.add_argument("--ab-overrides", default="",
+                    help='JSON {"name": {config overrides}, ...}: one daemon per entry (arms in that '
+                         'order, the first compared with each other), like --ab-keep-warm')
     ap.add_argument("--replicas", type=int, default=1,
                     help="with --ab-keep-warm: daemons per value (their placement on the host's CPUs "
                          "differs; several per value keep one daemon's placement from passing for the "
@@ -190,19 +195,25 @@ def main() -> int:
 
     n = native.load()
     ab = [int(x) for x in a.ab_keep_warm.split(",")] if a.ab_keep_warm else None
+    arms = None  # (name, overrides) per arm
+    if a.ab_overrides:
+        arms = list(json.loads(a.ab_overrides).items())
+    elif ab:
+        arms = [(str(kw), {"grpc": {"keepWarmMs": kw}}) for kw in ab]
     daemons = {}
     t_progress = time.monotonic()
     res = {"calls_per_kind_per_gap": a.calls, "floor_server_epoll_timeout_ms": 100, "rows": []}
     try:
-        if ab:
+        if arms:
             for r in range(a.replicas):
-                for kw in ab:
-                    daemons["@%d" % kw + ("#%d" % r if a.replicas > 1 else "")] = Daemon(n, a, kw)
+                for name, over in arms:
+                    daemons["@%s" % name + ("#%d" % r if a.replicas > 1 else "")] = Daemon(n, a, None, over)
         else:
             daemons[""] = Daemon(n, a, a.keep_warm_ms)
         first = next(iter(daemons.values()))
         res["backend"] = first.backend
         res["keep_warm_ms"] = ab if ab else a.keep_warm_ms
+        res["arms"] = dict(arms) if arms else None
         sizes = (9 + 80 + 9 + 5 + len(first.alloc), 9 + 20 + 9 + 5 + first.resp_len + 9 + 16)
         pinger = n.UdsPinger(*sizes, server_timeout_ms=100)
         for _ in range(200):
@@ -270,17 +281,18 @@ def main() -> int:
                 if srv[k]:  # the daemon's own part of the call (dispatch -> encoded answer)
                     row[k]["server_p50_us"] = us(median(srv[k]))
                     row[k]["server_p90_us"] = us(pct(srv[k], 0.9))
-            if ab:  # paired difference of the first value to each other one, iteration by
+            if arms:  # paired difference of the first arm to each other one, iteration by
                 # iteration (each arm's latency averaged over its replicas)
-                def arm(rpc, kw):
-                    ks = [k for k in kinds if k.split("#")[0] == "%s@%d" % (rpc, kw)]
+                def arm(rpc, name):
+                    ks = [k for k in kinds if k.split("#")[0] == "%s@%s" % (rpc, name)]
                     return [sum(v) / len(v) for v in zip(*(lat[k] for k in ks))]
-                for other in ab[1:]:
+                first_arm = arms[0][0]
+                for other, _ in arms[1:]:
                     for rpc in [r for r in ("allocate", "preferred") if r in want]:
-                        x, y = arm(rpc, ab[0]), arm(rpc, other)
+                        x, y = arm(rpc, first_arm), arm(rpc, other)
                         diffs = [p - q for p, q in zip(x, y)]
                         lo, hi = bootstrap_ci(diffs)
-                        row["%s_@%d_minus_@%d" % (rpc, ab[0], other)] = {
+                        row["%s_@%s_minus_@%s" % (rpc, first_arm, other)] = {
                             "median_us": us(median(diffs)), "ci95_us": [us(lo), us(hi)]}
             row["floor"]["per_call"] = {"client_minflt": round(ev["floor"]["client_minflt"] / a.calls, 3)}
             res["rows"].append(row)

@@ -333,7 +333,8 @@ def test_busy_poll_window_answers_and_idles_without_spinning(n, plugin_dir):
         srv.stop()
 
 
-def test_keep_warm_ticks_are_invisible_to_kubelet_and_metrics(n, plugin_dir):
+@pytest.mark.parametrize("full", [True, False])
+def test_keep_warm_ticks_are_invisible_to_kubelet_and_metrics(n, plugin_dir, full):
     """grpc.keepWarmMs: a worker that owns a connection and has been idle that long
     replays a canned header decode + Allocate/GetPreferredAllocation against its table,
     so the first call after a long gap finds warm caches (profiles/r4/idle_probe_*).  The
@@ -345,6 +346,7 @@ def test_keep_warm_ticks_are_invisible_to_kubelet_and_metrics(n, plugin_dir):
     path = os.path.join(plugin_dir, "amd-gpu.sock")
     srv = n.GrpcServer(path, 2)
     srv.set_keep_warm_ms(10)
+    srv.set_keep_warm_full(full)  # full: canned requests through an in-memory connection
     srv.set_table(table)
     srv.start()
     try:
@@ -367,6 +369,20 @@ def test_keep_warm_ticks_are_invisible_to_kubelet_and_metrics(n, plugin_dir):
         st, body, _ = c.unary(v1beta1.METHOD_ALLOCATE, req)  # the next real call is answered as usual
         assert st == 0 and v1beta1.AllocateResponse.FromString(body).container_responses[0].envs[
             "AMD_VISIBLE_DEVICES"] == "dev-1"
+        # thousands of ticks: the private connection's stream ids, flow-control window and
+        # HPACK table keep working, and an idle server with a 1 ms tick stays cheap
+        srv.set_keep_warm_ms(1)
+        ticks = srv.warm_ticks
+        cpu0, wall0 = time.process_time(), time.perf_counter()
+        time.sleep(1.5)
+        cpu = time.process_time() - cpu0
+        assert srv.warm_ticks - ticks > 300, srv.warm_ticks - ticks
+        assert cpu < 0.25 * (time.perf_counter() - wall0), "1 ms ticks used %.3f s of CPU" % cpu
+        assert srv.requests == requests + 1
+        assert 'rpc="GetPreferredAllocation"' not in table.render_metrics()
+        st, body, _ = c.unary(v1beta1.METHOD_ALLOCATE, req)
+        assert st == 0
+        srv.set_keep_warm_ms(10)
         c.close()
         srv.set_keep_warm_ms(0)
         ticks = srv.warm_ticks
