@@ -344,7 +344,9 @@ def test_keep_warm_ticks_are_invisible_to_kubelet_and_metrics(n, plugin_dir, ful
     devs = [n.TableDevice("dev-%d" % i, i, 0, 0, -1, ["/dev/dri/renderD%d" % (128 + i)], True) for i in range(4)]
     table = n.DeviceTable(tc, devs, n.Topology(4))
     path = os.path.join(plugin_dir, "amd-gpu.sock")
-    srv = n.GrpcServer(path, 2)
+    # the production polling windows: a tick must open neither (a GetPreferredAllocation
+    # on the internal connection is not an admission)
+    srv = n.GrpcServer(path, 2, busy_poll_us=50, admission_poll_us=1000)
     srv.set_keep_warm_ms(10)
     srv.set_keep_warm_full(full)  # full: canned requests through an in-memory connection
     srv.set_table(table)
@@ -377,6 +379,7 @@ def test_keep_warm_ticks_are_invisible_to_kubelet_and_metrics(n, plugin_dir, ful
         time.sleep(1.5)
         cpu = time.process_time() - cpu0
         assert srv.warm_ticks - ticks > 300, srv.warm_ticks - ticks
+        assert srv.admission_windows == 0
         assert cpu < 0.25 * (time.perf_counter() - wall0), "1 ms ticks used %.3f s of CPU" % cpu
         assert srv.requests == requests + 1
         assert 'rpc="GetPreferredAllocation"' not in table.render_metrics()
