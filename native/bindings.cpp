@@ -583,7 +583,6 @@ PYBIND11_MODULE(_native, m) {
       .def("stop", &Exporter::stop, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("running", &Exporter::running)
       .def("sample_once", [](Exporter& e) { e.sample_once(0); }, py::call_guard<py::gil_scoped_release>())
-      .def_property_readonly("abandoned_samplers", &Exporter::abandoned_samplers)
       .def_property_readonly("samples_total", &Exporter::samples_total)
       .def("last_sample", &Exporter::last_sample)
       .def("render", [](const Exporter& e) {

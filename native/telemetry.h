@@ -90,9 +90,6 @@ class Exporter : public std::enable_shared_from_this<Exporter> {
   // sampler_gen: the sampler thread's own pass (0 = a caller's synchronous pass); it
   // ends early once stop() is waiting or another sampler generation started.
   void sample_once(uint64_t sampler_gen = 0);
-  // The sampler never waits on a hardware call past its pass budget, so stop() always
-  // joins it; kept for compatibility (always 0).
-  int abandoned_samplers() const { return 0; }
   // Seconds since GPU `gpu`'s last successful sample (-1: none yet).
   double sample_age_s(int gpu) const;
 

@@ -479,7 +479,6 @@ def test_exporter_start_and_stop_do_not_hang_on_a_wedged_first_call(n):
         t0 = time.monotonic()
         ex.stop()
         assert time.monotonic() - t0 < 0.5 and not ex.running
-        assert ex.abandoned_samplers == 0
         lane0 = [x for x in be.lanes() if x[0] == 0][0]
         assert lane0[2] == "sample" and lane0[3] >= 0.25, lane0  # still stuck, on its lane
     finally:
