@@ -90,6 +90,7 @@ class Discoverer:
         self._since: float | None = None  # monotonic start of the run in flight
         self._stop = False
         self._runs = 0
+        self.first_done = threading.Event()  # set once the first run has been posted
         self._thread = threading.Thread(target=self._run, name="discovery", daemon=True)
         self._thread.start()
 
@@ -139,6 +140,7 @@ class Discoverer:
                 stopping = self._stop
             if not stopping:
                 self._post(purpose, gpus, topo, report, err)
+            self.first_done.set()
 
 
 class PluginManager:
@@ -310,20 +312,19 @@ class PluginManager:
             self._start_watch()
             self._discoverer = Discoverer(self.backend, lambda *r: self.events.put((EV_DISCOVERED,) + r))
             self._discoverer.request(DISCOVERY_RELOAD)
-            # the first discovery is normally done in milliseconds: wait for it (bounded) so
-            # plugins are registered when start() hands over to the loop; a stalled one is
-            # applied by the loop whenever it finishes
-            deadline = time.monotonic() + float(self.cfg.health.discoveryTimeoutS) + 1.0
-            while time.monotonic() < deadline:
-                try:
-                    ev = self.events.get(timeout=max(0.0, deadline - time.monotonic()))
-                except queue.Empty:
-                    break
-                if ev[0] == EV_DISCOVERED:
+            # the first discovery is normally done in milliseconds: wait for it (bounded) and
+            # handle what is queued by then, in order, so plugins are registered when start()
+            # hands over to the loop; a stalled one is applied by the loop whenever it finishes
+            if self._discoverer.first_done.wait(float(self.cfg.health.discoveryTimeoutS) + 1.0):
+                while True:
+                    try:
+                        ev = self.events.get_nowait()
+                    except queue.Empty:
+                        break
+                    if ev[0] == EV_STOP:
+                        self.events.put(ev)  # the loop ends on it
+                        break
                     self._handle(ev)
-                    break
-                self.events.put(ev)  # anything else waits for the loop (order kept enough:
-                time.sleep(0.001)    # nothing else is expected before the first discovery)
             self._start_telemetry()
             self.ready.close()
             self._loop()

@@ -160,8 +160,10 @@ def test_wedged_gpu_does_not_freeze_the_other_gpus_telemetry(n, serialised):
             for g in others:
                 assert 0 <= ex.sample_age_s(g) < 2 * interval * SLOW, (g, ex.sample_age_s(g))
             assert ex.sample_age_s(3) > 0.3
-            text = ex.render()
-            assert 'amdgpu_telemetry_up{gpu="5"} 1' in text and 'amdgpu_telemetry_up{gpu="3"} 0' in text
+            # the exposition is rendered at the end of each pass: wait for one past the bound
+            assert _wait(lambda: 'amdgpu_telemetry_up{gpu="5"} 1' in ex.render()
+                         and 'amdgpu_telemetry_up{gpu="3"} 0' in ex.render(), 2), \
+                [ln for ln in ex.render().splitlines() if ln.startswith("amdgpu_telemetry_up")]
         else:
             assert _wait(lambda: ex.blocked_gpus == others, 5), ex.blocked_gpus
             assert all(mon.gpu_healthy(g) for g in others)
