@@ -270,6 +270,8 @@ def main() -> int:
     ap.add_argument("--backend", choices=["auto", "amdsmi", "fixture"], default="auto",
                     help="daemon backend (auto: amdsmi when it sees a GPU); the canary runs only on amdsmi")
     ap.add_argument("--fixture", default="", help="fixture node model of a fixture daemon (default: <N>gpu_spx)")
+    ap.add_argument("--daemon-config", default="",
+                    help='JSON config sections merged over the daemon\'s (A/B runs), e.g. {"grpc": {"keepWarmMs": 0}}')
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -300,7 +302,9 @@ def main() -> int:
         os.makedirs(workdir)
         proc, kubelet, port, reg, backend = start_daemon(n_gpus, args.grpc_server, workdir, args.profile_dir,
                                                          args.busy_poll_us, args.admission_poll_us,
-                                                         backend=args.backend, fixture=args.fixture, hips=hips)
+                                                         backend=args.backend, fixture=args.fixture, hips=hips,
+                                                         overrides=json.loads(args.daemon_config) if args.daemon_config
+                                                         else None)
         info = {"port": port, "endpoint": reg.endpoint, "resource": reg.resource_name, "backend": backend,
                 "plugin_dir": os.path.join(workdir, "device-plugins")}
 
