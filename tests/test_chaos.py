@@ -105,7 +105,8 @@ class _Allocator(threading.Thread):
                                                                         ("4gpu_cpx", "single", "native", "", False),
                                                                         ("4gpu_spx", "none", "python", "", False),
                                                                         ("4gpu_spx", "none", "native", "0-2", False),
-                                                                        ("4gpu_spx", "none", "native", "", True)])
+                                                                        ("4gpu_spx", "none", "native", "", True),
+                                                                        ("4gpu_cpx", "single", "native", "0-2", True)])
 def test_random_fault_mix_converges(make_cfg, plugin_dir, tmp_path, seed, fixture, strategy, server, devices,
                                     serialised):
     from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import PodResourcesStub
