@@ -144,10 +144,11 @@ def _partitions(n, gpu_index: int, uuid: str, nparts: int, numa: int, vram: int,
 
 def set_gpu_mode(backend, gpu_index: int, compute: str, memory: str = "NPS1", first_render: int = 200) -> None:
     """Simulates an operator re-partitioning one GPU (amd-smi set --compute-partition):
-    the GPU's partitions (and their render nodes) are replaced."""
+    the GPU's partitions (and their render nodes) are replaced.  ``gpu_index`` is the
+    model's slot; the description is the model's own, not a discovery's (whose indices
+    shift while a GPU is missing or left out)."""
     n = native.load()
-    gpus, _ = backend.discover()
-    g = gpus[gpu_index]
+    g = backend.slot_info(gpu_index)
     g.compute_partition, g.memory_partition = compute.upper(), memory.upper()
     if g.supported_profiles:  # the operator can only pick a mode the GPU supports
         check_mode(gpu_index, g.compute_partition, g.memory_partition, g.supported_profiles)

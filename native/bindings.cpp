@@ -304,6 +304,7 @@ PYBIND11_MODULE(_native, m) {
       .def(py::init<uint64_t>(), py::arg("seed") = 1)
       .def("add_gpu", &FixtureBackend::add_gpu)
       .def("replace_gpu", &FixtureBackend::replace_gpu)
+      .def("slot_info", &FixtureBackend::slot_info)
       .def("clear", &FixtureBackend::clear)
       .def("set_link", &FixtureBackend::set_link)
       .def("set_link_up", &FixtureBackend::set_link_up)

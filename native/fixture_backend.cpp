@@ -83,6 +83,12 @@ void FixtureBackend::replace_gpu(int index, const GpuInfo& g) {
   gpus_[index] = copy;
 }
 
+GpuInfo FixtureBackend::slot_info(int slot) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (slot < 0 || slot >= static_cast<int>(gpus_.size())) throw std::out_of_range("slot_info: bad gpu index");
+  return gpus_[slot];
+}
+
 void FixtureBackend::clear() {
   std::lock_guard<std::mutex> lk(mu_);
   gpus_.clear();

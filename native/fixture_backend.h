@@ -38,6 +38,8 @@ class FixtureBackend : public Backend {
   void add_gpu(const GpuInfo& g);
   // Swap a GPU's description (e.g. a compute/memory partition-mode change).
   void replace_gpu(int index, const GpuInfo& g);
+  // The model's own description of slot `slot` (no discovery, no device call).
+  GpuInfo slot_info(int slot) const;
   void clear();
   void set_link(int a, int b, const Link& l);  // symmetric
   void set_link_up(int a, int b, bool up);      // also emits LinkDown/LinkUp events

@@ -199,7 +199,7 @@ def test_random_fault_mix_converges(make_cfg, plugin_dir, tmp_path, seed, fixtur
                     be.set_fail_discovery(False)  # a failed reload waits for its retry
                     continue
                 elif op == "mode_change" and len(present) == NGPU and g not in remoded:
-                    # an operator re-partitions GPU g (set_gpu_mode re-discovers, so only
+                    # an operator re-partitions GPU g (by fixture slot; only
                     # while every GPU is present: slot and index agree)
                     mode = "SPX" if orig[g].compute_partition != "SPX" else "CPX"
                     fixtures.set_gpu_mode(be, g, mode, first_render=300 + 8 * g)
