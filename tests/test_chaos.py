@@ -15,6 +15,7 @@ import random
 import threading
 import time
 
+import grpc
 import pytest
 
 from k8s_gpu_device_plugin_amd import native
@@ -38,7 +39,10 @@ def _wait(pred, timeout=10.0, step=0.02):
 def _advertised(plugin_dir, k, timeout=5.0):
     """(id, health) pairs of the first ListAndWatch message on the newest registration's
     endpoint, over a fresh connection (what a restarted kubelet would see)."""
-    c = DevicePluginClient(os.path.join(plugin_dir, k.requests[-1].endpoint))
+    try:  # a connect that times out under load is retried by the caller's wait, as kubelet would
+        c = DevicePluginClient(os.path.join(plugin_dir, k.requests[-1].endpoint))
+    except grpc.FutureTimeoutError:
+        return None
     try:
         stream = c.list_and_watch(timeout=timeout)
         first = next(iter(stream))
@@ -269,7 +273,10 @@ def test_random_fault_mix_converges(make_cfg, plugin_dir, tmp_path, seed, fixtur
             if not _wait(whole, timeout=15):
                 detail = (table() and [(i, table().healthy(i)) for i in table().ids()], links_now(), log,
                           [ln for ln in m.exporter.render().splitlines()
-                           if ln.startswith("amdgpu_xgmi_link_bandwidth")])
+                           if ln.startswith("amdgpu_xgmi_link_bandwidth")],
+                          {"monitor_unhealthy": m.monitor.unhealthy_keys(), "held": sorted(m._held_unhealthy),
+                           "canary_failed": sorted(m._canary_failed), "resetting": sorted(resetting),
+                           "health_log": list(getattr(m, "_health_log", []))[-20:]})
                 if os.environ.get("CHAOS_DUMP"):  # the full picture; pytest truncates the message
                     with open(os.path.join(os.environ["CHAOS_DUMP"], "chaos_%s_%d.txt" % (fixture, seed)), "w") as f:
                         f.write(repr(detail))
