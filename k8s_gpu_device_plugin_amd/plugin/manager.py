@@ -500,14 +500,14 @@ class PluginManager:
             canary_failed = self._canary_failed
             failed = {(index_of[k], p) for k, p in canary_failed if k in index_of}
         plugins = [AmdDevicePlugin(name, devs, topo, self.cfg) for name, devs in device_map.items()]
-        # built: from here on the new inventory replaces the old one (readers of
-        # self.plugins see the old list, then the new one, never an empty one)
+        # built: from here on the new inventory replaces the old one.  Readers of
+        # self.plugins see the old list until the new tables carry every health verdict
+        # (below), then the new one - never an empty one, nor one that is briefly all Healthy
         for p in self.plugins:
             try:
                 p.stop()
             except Exception as e:  # pragma: no cover
                 log.error("failed to stop plugin %s: %s", p.resource, e)
-        self.plugins = plugins
         self._node_index_of = {self._identity(g): g.index for g in node}
         self.gpus, self.topology = sel, topo
         self.signature = self._signature(node, sel)
@@ -536,6 +536,7 @@ class PluginManager:
         self.monitor.set_gpus(keys)
         self.monitor.attach_tables([p.table for p in plugins], not self.cfg.health.canary,
                                    sorted(self._index_of[k] for k in self._held_unhealthy if k in self._index_of))
+        self.plugins = plugins
         n = native.load()
         labels = []
         hips = {(g.index, p.index): p.hip_id for g in gpus for p in g.partitions}
