@@ -191,7 +191,9 @@ def test_sampler_watchdog_marks_a_wedged_gpu_lost(n):
         ages = {ln.split('"')[1]: float(ln.split()[1]) for ln in text.splitlines()
                 if ln.startswith("amdgpu_telemetry_sample_age_seconds{")}
         assert ages["1"] >= 0.25 and ages["0"] < 0.25, ages  # GPU 0 stays fresh
-        assert 'amdgpu_telemetry_up{gpu="1"} 0' in text and 'amdgpu_telemetry_up{gpu="0"} 1' in text
+        # telemetry_up comes with the GPU text of a pass: wait for one past the bound
+        assert _wait_for(lambda: 'amdgpu_telemetry_up{gpu="1"} 0' in ex.render()
+                         and 'amdgpu_telemetry_up{gpu="0"} 1' in ex.render())
         be.set_sample_stall(1, False)
         deadline = time.monotonic() + 5
         back = []
