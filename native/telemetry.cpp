@@ -447,12 +447,6 @@ void Exporter::sample_once(uint64_t sampler_gen) {
     ok[g] = sl.last_ok && !stuck && sl.last_ok_ns != 0;
     samples[g] = sl.last;
   }
-  for (size_t g = 0; g < n; ++g) {
-    if (!fresh[g]) continue;
-    const bool good = slots_[g].last_ok;
-    if (!good) sample_errors_.fetch_add(1, std::memory_order_relaxed);
-    if (mon) mon->on_sample(slots_[g].index, good, slots_[g].last);
-  }
   const double dt = (mono_ns() - t0) * 1e-9;
   if (be) {
     sample_hist_.observe(dt);
@@ -477,6 +471,14 @@ void Exporter::sample_once(uint64_t sampler_gen) {
       st->blocked.erase(std::remove_if(st->blocked.begin(), st->blocked.end(), returned), st->blocked.end());
       stalls_ = std::move(st);
     }
+  }
+  // after the verdicts above are published: a reader woken by this pass's health
+  // update must not still see the GPU's stale stall
+  for (size_t g = 0; g < n; ++g) {
+    if (!fresh[g]) continue;
+    const bool good = slots_[g].last_ok;
+    if (!good) sample_errors_.fetch_add(1, std::memory_order_relaxed);
+    if (mon) mon->on_sample(slots_[g].index, good, slots_[g].last);
   }
   last_pass_ns_.store(mono_ns());
   render_gpu_text(samples, ok, gen);

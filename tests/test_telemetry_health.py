@@ -200,7 +200,8 @@ def test_sampler_watchdog_marks_a_wedged_gpu_lost(n):
         while time.monotonic() < deadline and not back:
             back = [u for u in m.pop(100) if u.healthy == 1]
         assert back and back[0].gpu == 1 and m.gpu_healthy(1)
-        assert ex.stalled_gpu == -1 and "amdgpu_telemetry_sample_stalled" not in ex.render()
+        # cleared with the pass that brought the call back (and the watchdog's next look)
+        assert _wait_for(lambda: ex.stalled_gpu == -1 and "amdgpu_telemetry_sample_stalled" not in ex.render())
     finally:
         be.set_sample_stall(1, False)
         ex.stop()
