@@ -72,11 +72,12 @@ def run_manager():
         assert not t.is_alive()
 
 
-@pytest.mark.parametrize("serialised", [False, True], ids=["per_device_lock", "library_lock"])
-def test_wedged_gpu_keeps_the_node_advertised(make_cfg, plugin_dir, run_manager, serialised):
+@pytest.mark.parametrize("serialised,server", [(False, "native"), (True, "native"), (False, "python")],
+                         ids=["per_device_lock", "library_lock", "per_device_lock_grpcio_server"])
+def test_wedged_gpu_keeps_the_node_advertised(make_cfg, plugin_dir, run_manager, serialised, server):
     be = fixtures.build_backend("8gpu_spx_mesh")
     be.set_serialised(serialised)
-    cfg = make_cfg(fixture="8gpu_spx_mesh", grpc={"server": "native"}, telemetry={"intervalMs": 50},
+    cfg = make_cfg(fixture="8gpu_spx_mesh", grpc={"server": server}, telemetry={"intervalMs": 50},
                    rediscoverIntervalS=0.3, retrySeconds=0.2,
                    health={"sampleStallS": 0.3, "discoveryTimeoutS": 0.5, "lostAfterFailures": 3})
     with KubeletStub(plugin_dir) as k:
