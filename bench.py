@@ -11,7 +11,7 @@ to register with.  Every rank then acts as one kubelet-side client for "its" GPU
        + PREFS GetPreferredAllocation RPCs over the whole advertised set, compiled
          client and grpcio client (each timed)
        + SCRAPE_S seconds of closed-loop GET /metrics on SCRAPE_CONNS keep-alive
-         connections from the compiled load generator (native/loadgen.cpp)
+         connections from the compiled load generator (tests/native/loadgen.cpp)
 
 W warm-up steps, then K timed steps bracketed by barrier + torch.cuda.synchronize().
 With N > 1 the ranks also barrier between a step's RPC phase and its scrape phase.
@@ -286,10 +286,13 @@ def main() -> int:
 
     from k8s_gpu_device_plugin_amd import native
     n = native.load()
+    nb = native.load_bench()  # load generators and latency probes (not part of the plugin)
     if args.grpc_server == "native" and not hasattr(n, "GrpcServer"):
         args.grpc_server = "python"
 
-    master_port = os.environ.get("MASTER_PORT", "0")
+    # one directory per job: ranks of one torchrun job share it (same MASTER_PORT), two
+    # single-process runs on one host (concurrent test workers) must not
+    master_port = os.environ.get("MASTER_PORT") or "pid%d" % os.getpid()
     workdir = os.path.join(tempfile.gettempdir(), "amdgpu-dp-bench-%s-%d" % (master_port, os.getuid()))
     proc = kubelet = None
     info = None
@@ -400,7 +403,7 @@ def main() -> int:
             pref_raw(pref_req)
             p.append(perf() - t0)
         phase_sync()
-        r = n.http_load("127.0.0.1", info["port"], "/metrics", SCRAPE_CONNS, SCRAPE_S, 0.0)
+        r = nb.http_load("127.0.0.1", info["port"], "/metrics", SCRAPE_CONNS, SCRAPE_S, 0.0)
         if r["errors"]:
             raise RuntimeError("%d /metrics scrape errors" % r["errors"])
         s.extend(r["latencies_s"])
@@ -427,20 +430,20 @@ def main() -> int:
     # between two threads with no HTTP/2, HPACK or protobuf work (sizes ~ this Allocate's).
     alloc_resp_len = len(alloc_raw(alloc_req))
     sizes = (9 + 80 + 9 + 5 + len(alloc_req), 9 + 20 + 9 + 5 + alloc_resp_len + 9 + 16)
-    floor = n.uds_pingpong(10000, 500, *sizes)
+    floor = nb.uds_pingpong(10000, 500, *sizes)
     mine["uds_floor_p50"] = _pct(floor, 0.5)
     # ... and with a server thread that polls instead of sleeping (the busy-poll window);
     # its p99 is this machine's tail for a bare back-to-back exchange (timer ticks,
     # interrupts and other tenants land on either thread's CPU), the floor Allocate's p99
     # is compared against
-    spin = n.uds_pingpong(10000, 500, *sizes, server_spin=True)
+    spin = nb.uds_pingpong(10000, 500, *sizes, server_spin=True)
     mine["uds_floor_spin_p50"] = _pct(spin, 0.5)
     mine["uds_floor_spin_p99"] = _pct(spin, 0.99)
     mine["uds_floor_spin_p999"] = _pct(spin, 0.999)
     # kubelet-like sparse calls: 1 ms apart, every one meets a sleeping server thread
     mine["alloc_cold"] = h2.bench_unary(v1beta1.METHOD_ALLOCATE, alloc_req, 400, 1000)
     # ... and the bare exchange with the same 1 ms idle gap (cold caches, idle CPU states)
-    mine["uds_floor_cold_p50"] = _pct(n.uds_pingpong(400, 20, *sizes, gap_us=1000), 0.5)
+    mine["uds_floor_cold_p50"] = _pct(nb.uds_pingpong(400, 20, *sizes, gap_us=1000), 0.5)
     # a pod admission as kubelet runs it: GetPreferredAllocation, ~200 us of kubelet
     # bookkeeping, then Allocate of the same container (2 ms idle before each admission)
     adm = []
@@ -453,7 +456,7 @@ def main() -> int:
         adm.extend(h2.bench_unary(v1beta1.METHOD_ALLOCATE, alloc_req, 1))
     mine["alloc_admission"] = adm
     # /metrics: one loopback TCP exchange of a scrape's size, polling server
-    mine["tcp_scrape_floor_p50"] = _pct(n.uds_pingpong(3000, 300, 90, body_len + 400, server_spin=True, tcp=True),
+    mine["tcp_scrape_floor_p50"] = _pct(nb.uds_pingpong(3000, 300, 90, body_len + 400, server_spin=True, tcp=True),
                                         0.5)
     if rank == 0:  # the daemon's own time per Allocate (decode, lookup, encode), from its histogram
         conn.request("GET", "/metrics")

@@ -6,11 +6,16 @@ the repo snapshot to the GPU box):
   native HTTP/2 gRPC server) + pybind11 bindings, linked against ``libamd_smi``.
 * ``k8s_gpu_device_plugin_amd/ops/libamdgpu_canary.so``  HIP/CDNA4 health canary,
   ``hipcc --offload-arch=gfx950``.
-* ``build/native_selftest[-asan|-tsan]``  standalone C++ self-test (no Python) for
-  sanitizer runs.
-* ``build/fuzz/fuzz_<target>``  libFuzzer + ASan + UBSan binaries (amdclang++) for
-  every parser that faces a peer: ``pbwire`` (kubelet protobuf + allocator contract),
-  ``hpack``, ``grpc`` (HTTP/2 server on its socket), ``http`` (HTTP/1.1 ops server).
+* ``k8s_gpu_device_plugin_amd/_native_bench*.so``  the load generators and latency
+  probes of ``bench.py``, ``scripts/`` and the tests (``tests/native/loadgen.cpp``,
+  ``tests/native/bench_bindings.cpp``) over the same core objects.  Harness only: the
+  plugin never imports it, so no DaemonSet pod carries it.
+* ``build/native_selftest[-asan|-tsan]``  standalone C++ self-test (``tests/native/
+  selftest.cpp``, no Python) for sanitizer runs.
+* ``build/fuzz/fuzz_<target>``  libFuzzer + ASan + UBSan binaries (amdclang++, sources in
+  ``tests/native/fuzz/``) for every parser that faces a peer: ``pbwire`` (kubelet protobuf
+  + allocator contract), ``hpack``, ``grpc`` (HTTP/2 server on its socket), ``http``
+  (HTTP/1.1 ops server).
 
 Usage: ``python -m k8s_gpu_device_plugin_amd._build [--force] [--sanitize address|thread]
 [--fuzz TARGET... --fuzz-seconds N]``
@@ -28,6 +33,7 @@ import sysconfig
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG_DIR)
 NATIVE_DIR = os.path.join(ROOT, "native")
+HARNESS_DIR = os.path.join(ROOT, "tests", "native")  # C++ test / bench harness
 BUILD_DIR = os.path.join(ROOT, "build")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 OFFLOAD_ARCH = "gfx950"
@@ -46,12 +52,12 @@ CORE_SOURCES = [
     "watch.cpp",
     "hpack.cpp",
     "grpc_h2.cpp",
-    "loadgen.cpp",
     "profiler.cpp",
 ]
 BINDING_SOURCES = ["bindings.cpp"]
+BENCH_SOURCES = ["loadgen.cpp", "bench_bindings.cpp"]  # in HARNESS_DIR
 FUZZ_TARGETS = ("pbwire", "hpack", "grpc", "http")
-FUZZ_DIR = os.path.join(NATIVE_DIR, "fuzz")
+FUZZ_DIR = os.path.join(HARNESS_DIR, "fuzz")
 CANARY_SOURCES = [os.path.join(PKG_DIR, "ops", f) for f in ("canary.hip", "datapath.hip")]
 CANARY_HEADERS = [os.path.join(PKG_DIR, "ops", "canary_common.h")]
 CANARY_LIB = os.path.join(PKG_DIR, "ops", "libamdgpu_canary.so")
@@ -62,8 +68,14 @@ def native_ext_path() -> str:
     return os.path.join(PKG_DIR, "_native" + suffix)
 
 
+def bench_ext_path() -> str:
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return os.path.join(PKG_DIR, "_native_bench" + suffix)
+
+
 def _headers():
-    return [os.path.join(NATIVE_DIR, f) for f in os.listdir(NATIVE_DIR) if f.endswith(".h")]
+    return [os.path.join(d, f) for d in (NATIVE_DIR, HARNESS_DIR) if os.path.isdir(d)
+            for f in os.listdir(d) if f.endswith(".h")]
 
 
 def _stale(target: str, deps) -> bool:
@@ -142,6 +154,28 @@ def build_native(force: bool = False, jobs: int | None = None, verbose: bool = T
     return out
 
 
+def build_bench(force: bool = False, jobs: int | None = None, verbose: bool = True) -> str:
+    """The harness extension (``_native_bench``): load generators and latency probes,
+    linked with the same core objects as ``_native``."""
+    import pybind11
+
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    out = bench_ext_path()
+    flags = _common_flags(None) + ["-I" + HARNESS_DIR]
+    core_objs, core_changed = _compile_objects(CORE_SOURCES, os.path.join(BUILD_DIR, "obj"), _common_flags(None),
+                                               force, jobs)
+    py_flags = flags + ["-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"], "-fvisibility=hidden"]
+    objs, changed = _compile_objects(BENCH_SOURCES, os.path.join(BUILD_DIR, "obj_bench"), py_flags, force, jobs,
+                                     src_dir=HARNESS_DIR)
+    if force or core_changed or changed or not os.path.exists(out):
+        tmp = out + ".tmp"
+        _run([_cxx(), "-shared", "-o", tmp] + objs + core_objs + _link_libs(), "link _native_bench")
+        os.replace(tmp, out)
+        if verbose:
+            print("built", os.path.relpath(out, ROOT))
+    return out
+
+
 def sanitized_ext_path(sanitize: str) -> str:
     suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
     return os.path.join(BUILD_DIR, "ext-" + sanitize, "_native" + suffix)
@@ -179,8 +213,9 @@ def build_selftest(sanitize: str | None = None, force: bool = False) -> str:
     tag = {"address": "-asan", "thread": "-tsan", None: ""}[sanitize]
     obj_dir = os.path.join(BUILD_DIR, "obj_selftest" + tag)
     flags = _common_flags(sanitize)
-    objs, changed = _compile_objects(CORE_SOURCES + ["selftest.cpp"], obj_dir, flags, force,
-                                     min(8, os.cpu_count() or 4))
+    objs, changed = _compile_objects(CORE_SOURCES, obj_dir, flags, force, min(8, os.cpu_count() or 4))
+    st, st_changed = _compile_objects(["selftest.cpp"], obj_dir, flags, force, 1, src_dir=HARNESS_DIR)
+    objs, changed = objs + st, changed or st_changed
     exe = os.path.join(BUILD_DIR, "native_selftest" + tag)
     if force or changed or not os.path.exists(exe):
         link = [_cxx()] + (["-fsanitize=" + sanitize] if sanitize else [])
@@ -268,6 +303,7 @@ def build_canary(force: bool = False, verbose: bool = True) -> str:
 
 def build_all(force: bool = False) -> None:
     build_native(force=force)
+    build_bench(force=force)
     build_canary(force=force)
 
 
@@ -302,6 +338,7 @@ def main(argv=None) -> int:
         r = subprocess.run([exe])
         return r.returncode
     build_native(force=args.force)
+    build_bench(force=args.force)
     if not args.no_canary:
         build_canary(force=args.force)
     return 0

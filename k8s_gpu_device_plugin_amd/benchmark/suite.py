@@ -83,6 +83,7 @@ def pref_req(avail, must, size):
 
 def rpc_latency(node, method, req, n_native=10000, n_grpcio=2000):
     nat = native.load()
+    native.load_bench()  # H2Client.bench_unary
     c = nat.H2Client(node.socket)
     c.bench_unary(method, req, 500)  # warm-up
     lat = c.bench_unary(method, req, n_native)
@@ -104,7 +105,7 @@ def rpc_latency(node, method, req, n_native=10000, n_grpcio=2000):
 
 
 def scrape(node, conns=4, seconds=2.0, rate=0.0, gzip=False, path="/metrics"):
-    r = native.load().http_load("127.0.0.1", node.port, path, conns, seconds, rate, gzip)
+    r = native.load_bench().http_load("127.0.0.1", node.port, path, conns, seconds, rate, gzip)
     lat = r["latencies_s"]
     return {"rps": round(r["ok"] / r["elapsed_s"], 1), "errors": r["errors"], "p50_us": us(pct(lat, 0.5)),
             "p99_us": us(pct(lat, 0.99)), "bytes": r["bytes"] // max(1, r["ok"]), "conns": conns,
@@ -370,8 +371,8 @@ def health_propagation(events=60):
     nat = native.load()
     node = Node("fixture", "8gpu_spx_mesh")
     try:
-        nat.health_propagation(node.mgr.backend, node.socket, 3, 2)  # warm-up pair
-        res = nat.health_propagation(node.mgr.backend, node.socket, 3, events)
+        native.load_bench().health_propagation(node.mgr.backend, node.socket, 3, 2)  # warm-up pair
+        res = native.load_bench().health_propagation(node.mgr.backend, node.socket, 3, events)
         down = [t for d, t in res if d == 1]
         up = [t for d, t in res if d == 0]
         both = down + up
@@ -388,7 +389,7 @@ def uds_floor():
     """Speed-of-light reference for one kubelet RPC: two threads exchange Allocate-sized
     messages over a unix socket with the server's exact syscalls (epoll_wait, recv, send)
     and no protocol work.  Allocate p50 minus this is the plugin's own cost."""
-    lat = native.load().uds_pingpong(20000, 1000, 140, 250)
+    lat = native.load_bench().uds_pingpong(20000, 1000, 140, 250)
     return {"config": "unix-socket round trip floor (no HTTP/2, HPACK, protobuf or table work)",
             "p50_us": us(pct(lat, 0.5)), "p99_us": us(pct(lat, 0.99)), "round_trips": len(lat)}
 

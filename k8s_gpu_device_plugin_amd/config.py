@@ -104,6 +104,21 @@ class HealthConfig:
     # long; a discovery gives a GPU that does not answer in time its last known description
     # (or leaves it out) and reports it on GET /ready
     discoveryTimeoutS: float = 10.0
+    # Health latches that must survive a plugin restart (uncorrectable ECC, failed canaries),
+    # keyed by GPU identity and the host's boot id: "auto" = <pluginDir>/.amdgpu-device-plugin/
+    # health-state.json (kubelet removes only sockets from that directory), a path, or "" /
+    # "none" = in memory only
+    stateFile: str = "auto"
+
+
+def state_file_path(cfg) -> str:
+    """Where the health latches are persisted ("" = nowhere)."""
+    v = str(cfg.health.stateFile or "").strip()
+    if v.lower() in ("", "none", "off"):
+        return ""
+    if v.lower() == "auto":
+        return os.path.join(cfg.pluginDir, ".amdgpu-device-plugin", "health-state.json")
+    return v
 
 
 @dataclass
@@ -326,6 +341,11 @@ def validate(cfg: Config) -> Config:
         raise ConfigError("health.discoveryTimeoutS must be > 0")
     if cfg.sharing.replicas < 1:
         raise ConfigError("sharing.replicas must be >= 1")
+    if cfg.health.canaryOnPreStart and cfg.sharing.replicas > 1:
+        # a time-sliced partition already runs another container: its canary would
+        # contend with it (or fail to allocate HBM) and mark a shared, healthy GPU Unhealthy
+        raise ConfigError("health.canaryOnPreStart cannot be combined with sharing.replicas > 1: the canary would "
+                          "run on a partition another container is using")
     from .utils.util import parse_device_selector
     try:
         parse_device_selector(cfg.devices)

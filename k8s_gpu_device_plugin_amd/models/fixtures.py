@@ -20,7 +20,11 @@ A node model is a plain dict (also loadable from JSON/YAML)::
                "numa_node": 0, ...}, ...],
      "links": {"type": "xgmi", "down": [[0, 5]]},
      "events": [{"at": 2.0, "kind": "pre_reset", "gpu": 3}, ...],
+     "hardware_events": true,   # false: no event notification (an unprivileged pod)
      "seed": 1}
+
+Per GPU, ``ecc_uncorrectable`` sets the UE count the hardware reports from the start and
+``fw_clock: false`` stops samples reporting the firmware clock.
 """
 from __future__ import annotations
 
@@ -50,6 +54,8 @@ EVENT_KINDS = {
     "ecc_uncorrectable": "EVT_ECC_UNCORRECTABLE", "link_down": "EVT_LINK_DOWN",
     "link_up": "EVT_LINK_UP", "thermal": "EVT_THERMAL", "vm_fault": "EVT_VM_FAULT",
     "device_lost": "EVT_DEVICE_LOST", "device_recovered": "EVT_DEVICE_RECOVERED",
+    # not an event: the GPU's firmware restarts (a reset as an unprivileged poller sees it)
+    "firmware_reset": "EVT_FIXTURE_FIRMWARE_RESET",
 }
 
 
@@ -237,6 +243,10 @@ def build_backend(spec):
                                       hip_base[gi])
         render += nparts
         be.add_gpu(info)
+        if int(g.get("ecc_uncorrectable", 0)):
+            be.set_ecc_uncorrectable(gi, int(g["ecc_uncorrectable"]))
+        if not g.get("fw_clock", True):
+            be.set_fw_clock_reported(gi, False)
     links = model.get("links", {}) or {}
     ltype = {"xgmi": n.LINK_XGMI, "pcie": n.LINK_PCIE}.get(str(links.get("type", "xgmi")).lower(), n.LINK_XGMI)
     down = {tuple(sorted(p)) for p in links.get("down", [])}
@@ -246,6 +256,7 @@ def build_backend(spec):
             xgmi = ltype == n.LINK_XGMI
             be.set_link(a, b, n.Link(type=ltype, hops=1, weight=15 if xgmi else 40, up=(a, b) not in down, p2p=True,
                                      bw_gbps=slow.get((a, b), XGMI_LINK_GBPS) if xgmi else 0.0))
+    be.set_events_enabled(bool(model.get("hardware_events", True)))
     for ev in model.get("events", []) or []:
         kind = getattr(n, EVENT_KINDS[str(ev["kind"]).lower()])
         be.schedule_event(float(ev.get("at", 0.0)),

@@ -17,19 +17,20 @@ import threading
 
 _lock = threading.Lock()
 _mod = None
+_bench = None
 
 
-def _stale() -> bool:
+def _stale(so: str | None = None, dirs=None) -> bool:
     from . import _build
-    so = _build.native_ext_path()
+    so = so or _build.native_ext_path()
     if not os.path.exists(so):
         return True
     if not os.path.isdir(_build.NATIVE_DIR):
         return False  # installed without sources: use what ships
     t = os.path.getmtime(so)
-    for f in os.listdir(_build.NATIVE_DIR):
-        if f.endswith((".cpp", ".h")) and f != "selftest.cpp":
-            if os.path.getmtime(os.path.join(_build.NATIVE_DIR, f)) > t:
+    for d in dirs or (_build.NATIVE_DIR,):
+        for f in os.listdir(d):
+            if f.endswith((".cpp", ".h")) and os.path.getmtime(os.path.join(d, f)) > t:
                 return True
     return False
 
@@ -55,6 +56,28 @@ def load():
             raise RuntimeError("native core k8s_gpu_device_plugin_amd._native is not built/loadable: %s "
                                "(run: python -m k8s_gpu_device_plugin_amd._build)" % e) from e
         return _mod
+
+
+def load_bench():
+    """The harness extension ``_native_bench`` (load generators, latency probes): for
+    bench.py, scripts/ and tests only - the plugin never imports it."""
+    global _bench
+    if _bench is not None:
+        return _bench
+    load()  # its types are _native's
+    with _lock:
+        if _bench is not None:
+            return _bench
+        from . import _build
+        if os.environ.get("AMDGPU_DP_NO_AUTOBUILD", "") not in ("1", "true") and \
+                _stale(_build.bench_ext_path(), (_build.NATIVE_DIR, _build.HARNESS_DIR)):
+            _build.build_bench(verbose=False)
+        try:
+            _bench = importlib.import_module("k8s_gpu_device_plugin_amd._native_bench")
+        except ImportError as e:  # pragma: no cover
+            raise RuntimeError("bench extension k8s_gpu_device_plugin_amd._native_bench is not built/loadable: %s "
+                               "(run: python -m k8s_gpu_device_plugin_amd._build)" % e) from e
+        return _bench
 
 
 def _load_file(path: str):

@@ -88,6 +88,16 @@ class _Watch:
     def next(self, timeout: float = 5.0):
         return self.updates.get(timeout=timeout)
 
+    def last(self, timeout: float = 5.0, settle: float = 0.2) -> list:
+        """The newest device list once the stream has been quiet for ``settle`` seconds
+        (waits up to ``timeout`` for the first message)."""
+        _, devs = self.updates.get(timeout=timeout)
+        while True:
+            try:
+                _, devs = self.updates.get(timeout=settle)
+            except queue.Empty:
+                return devs
+
     def cancel(self) -> None:
         self.stream.cancel()
 

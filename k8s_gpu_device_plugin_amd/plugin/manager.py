@@ -38,7 +38,7 @@ import threading
 import time
 
 from .. import native
-from ..config import disabled_checks_mask
+from ..config import disabled_checks_mask, state_file_path
 from ..device import build_device_map
 from ..device.backend import make_backend
 from ..resource import new_resources
@@ -46,6 +46,7 @@ from ..utils.log import get_logger
 from ..utils.util import CloseOnce, parse_device_selector
 from ..utils.version import APP_NAME, VERSION
 from .plugin import AmdDevicePlugin
+from .state import HealthState
 
 log = get_logger("manager")
 
@@ -54,6 +55,7 @@ EV_STOP, EV_RESTART, EV_RETRY, EV_KUBELET, EV_HEALTH, EV_REDISCOVER, EV_VERIFIED
 EV_METRICS = "metrics"  # state read by /metrics changed off the manager thread (canary results)
 EV_SOCKET_GONE = "socket_gone"  # a *.sock other than kubelet.sock was removed from the plugin dir
 EV_DISCOVERED = "discovered"  # the discovery worker finished: (purpose, gpus, topo, report, error)
+EV_START_CANARY = "start_canary"  # a start-up canary verdict: (identity, partition, ok, why)
 DISCOVERY_RELOAD, DISCOVERY_CHECK = "reload", "check"  # rebuild always / only if the inventory changed
 HEALTH_LOG_LEN = 4096
 SERVER_CHECK_S = 1.0  # gRPC server supervision poll
@@ -202,6 +204,11 @@ class PluginManager:
         # until the GPU reports healthy again or a start-up canary re-checks it.
         self._canary_failed: set[tuple[str, int]] = set()
         self._verify_pool: concurrent.futures.ThreadPoolExecutor | None = None
+        # health.canaryOnStart: identities canaried by this process, and (identity,
+        # partition) whose verdict is pending (advertised Unhealthy until it arrives)
+        self._start_canaried: set[str] = set()
+        self._start_pending: set[tuple[str, int]] = set()
+        self._canary_pool: concurrent.futures.ThreadPoolExecutor | None = None
         self.podres = None  # PodResourcesWatcher when podResources.enabled
         self.link_pods: dict[tuple[int, int], int] = {}  # GPU pair -> multi-GPU pods spanning it
         # multi-GPU containers allocated since the last PodResources poll (shared by all
@@ -223,6 +230,10 @@ class PluginManager:
         self.canary_results: dict[tuple[int, int], tuple[float, dict]] = {}
         self._canary_owner: dict[tuple[int, int], str] = {}  # same keys -> identity of the GPU it ran on
         self._canary_lock = threading.Lock()
+        # health latches persisted across plugin restarts (plugin/state.py)
+        path = state_file_path(cfg)
+        self._state = HealthState(path) if path else None
+        self._reverify: set[str] = set()  # restored recovery-canary holds to verify once loaded
 
     # ------------------------------------------------------------ public API
     def restart(self) -> None:
@@ -309,6 +320,7 @@ class PluginManager:
         os.makedirs(self.cfg.pluginDir, exist_ok=True)
         self._running.set()
         try:
+            self._restore_state()
             self._start_watch()
             self._discoverer = Discoverer(self.backend, lambda *r: self.events.put((EV_DISCOVERED,) + r))
             self._discoverer.request(DISCOVERY_RELOAD)
@@ -385,6 +397,53 @@ class PluginManager:
                 return
             self._handle(ev)
 
+    # ------------------------------------------------------------ persisted latches
+    def _restore_state(self) -> None:
+        """Re-applies the latches the previous process of this boot persisted, before the
+        first discovery: a GPU it held Unhealthy is never advertised Healthy in between."""
+        if self._state is None:
+            return
+        snap = self._state.load()
+        if not snap:
+            return
+        n = native.load()
+        latches = [n.HealthLatch(k, e["last_ue"], e["fw_boot_s"], e["reason"], e["since_ns"])
+                   for k, e in sorted(snap["ecc"].items())]
+        if latches:
+            self.monitor.restore_latches(latches)
+        self._canary_failed = {(k, p) for k, parts in snap["canary_failed"].items() for p in parts}
+        if self.cfg.health.canary:
+            self._held_unhealthy |= set(snap["held"])
+            self._reverify |= set(snap["held"])
+        restored = len(latches) + len(self._canary_failed) + len(snap["held"])
+        self.counters["latches_restored"] = restored
+        if restored:
+            log.warning("restored health latches from %s: uncorrectable ECC on %s; failed canaries on %s; "
+                        "recovery canary held on %s", self._state.path,
+                        ", ".join(e.key for e in latches) or "none",
+                        ", ".join("%s/%d" % kp for kp in sorted(self._canary_failed)) or "none",
+                        ", ".join(sorted(snap["held"])) or "none")
+
+    def _state_snapshot(self) -> dict:
+        ecc = {}
+        for l in self.monitor.latches():
+            ecc[l.key] = {"last_ue": int(l.last_ue), "fw_boot_s": round(float(l.fw_boot_s)),
+                          "reason": l.reason, "since_ns": int(l.since_ns)}
+        failed: dict = {}
+        for k, part in self._canary_failed:
+            failed.setdefault(k, set()).add(part)
+        return {"ecc": ecc, "canary_failed": {k: sorted(v) for k, v in failed.items()},
+                "held": sorted(self._held_unhealthy)}
+
+    def _save_state(self) -> None:
+        if self._state is None:
+            return
+        try:
+            if self._state.save(self._state_snapshot()):
+                self.counters["state_writes"] = self._state.writes
+        except Exception as e:  # pragma: no cover - persistence never stops the manager
+            log.error("persisting health latches failed: %s", e)
+
     def _handle(self, ev) -> None:
         kind = ev[0]
         try:
@@ -426,10 +485,14 @@ class PluginManager:
                 self._request_discovery(DISCOVERY_CHECK)
             elif kind == EV_SOCKET_GONE:
                 self._socket_gone(ev[1])
+            elif kind == EV_START_CANARY:
+                self._apply_start_canary(*ev[1:])
         except Exception as e:
             self.counters["load_failures"] += 1
             log.error("event %s failed: %s; retrying in %.0fs", kind, e, self.cfg.retrySeconds)
             self._arm_retry()
+        if kind in (EV_HEALTH, EV_VERIFIED, EV_PRESTART_FAIL, EV_DISCOVERED, EV_START_CANARY):
+            self._save_state()
         self._publish_metrics()
 
     def _coalesce_restarts(self) -> bool:
@@ -479,9 +542,16 @@ class PluginManager:
     # ------------------------------------------------------------ plugins
     def load_plugins(self, gpus=None, topo=None) -> None:
         """Builds the plugins for a discovery (``gpus``/``topo``; a synchronous discovery
-        when not given), then replaces the current ones with them.  Everything that can
-        fail - discovery, resources, device map, tables, canaries - happens before the
-        old plugins stop: a failure leaves them serving (make-before-break)."""
+        when not given), then puts them in service.  Everything that can fail - discovery,
+        resources, device map, tables - happens before anything that serves changes: a
+        failure leaves the current plugins serving (make-before-break).
+
+        A resource that keeps its name keeps its socket, server and kubelet registration:
+        its new table is swapped into the running server, whose ListAndWatch streams push
+        the new device list at once (reference ``restartPlugins`` stops every server and
+        starts new ones, ``plugin/manager.go:177-194``, so kubelet's endpoint is gone for a
+        moment on every reload and an admission landing then fails).  Only resources that
+        disappeared stop; only new ones start (``start_plugins``)."""
         if gpus is None:
             gpus, topo = self.backend.discover()
             self._note_report(self.backend.last_discovery() if hasattr(self.backend, "last_discovery") else None)
@@ -493,35 +563,19 @@ class PluginManager:
                                       self.cfg.sharing.replicas, self.cfg.sharing.renameByDefault)
         key_of = {g.index: self._identity(g) for g in sel}
         index_of = {k: i for i, k in key_of.items()}
-        if self.cfg.health.canaryOnStart:
-            failed = self._startup_canary(sel, key_of)
-            canary_failed = {(key_of[g], p) for g, p in failed}  # fresh verdicts replace older ones
-        else:
-            canary_failed = self._canary_failed
-            failed = {(index_of[k], p) for k, p in canary_failed if k in index_of}
+        node_keys = {self._identity(g) for g in node}
+        canary_jobs = self._plan_startup_canary(sel, key_of, node_keys, device_map) \
+            if self.cfg.health.canaryOnStart else []
+        # partitions held Unhealthy by a canary: failed before, or a start-up verdict pending
+        held = self._canary_failed | self._start_pending
+        failed = {(index_of[k], p) for k, p in held if k in index_of}
         plugins = [AmdDevicePlugin(name, devs, topo, self.cfg) for name, devs in device_map.items()]
-        # built: from here on the new inventory replaces the old one.  Readers of
-        # self.plugins see the old list until the new tables carry every health verdict
-        # (below), then the new one - never an empty one, nor one that is briefly all Healthy
-        for p in self.plugins:
-            try:
-                p.stop()
-            except Exception as e:  # pragma: no cover
-                log.error("failed to stop plugin %s: %s", p.resource, e)
-        self._node_index_of = {self._identity(g): g.index for g in node}
-        self.gpus, self.topology = sel, topo
-        self.signature = self._signature(node, sel)
-        self.device_map = device_map
-        self._key_of, self._index_of = key_of, index_of
-        self._canary_failed = canary_failed
-        gpus = sel
-        self.counters["reloads"] = self.counters.get("reloads", 0) + 1
         for p in plugins:
             p.table.set_recent_allocations(self.recent_allocations)
         if self.cfg.health.canaryOnPreStart:
             for p in plugins:
                 p.prestart_check = self._prestart_check
-        # canary failures are per partition and known only here
+        # canary verdicts are per partition and known only here
         for p in plugins:
             for gpu, part in failed:
                 p.set_gpu_health(gpu, part, False)
@@ -530,13 +584,45 @@ class PluginManager:
         # event that lands during the reload reaches the new tables either way (reading
         # gpu_healthy() here and calling set_fast_tables() later left a window in which
         # it reached only the outgoing ones).
-        keys = [""] * (max([g.index for g in gpus], default=-1) + 1)
-        for i, k in self._key_of.items():
+        keys = [""] * (max([g.index for g in sel], default=-1) + 1)
+        for i, k in key_of.items():
             keys[i] = k
         self.monitor.set_gpus(keys)
         self.monitor.attach_tables([p.table for p in plugins], not self.cfg.health.canary,
-                                   sorted(self._index_of[k] for k in self._held_unhealthy if k in self._index_of))
+                                   sorted(index_of[k] for k in self._held_unhealthy if k in index_of))
+        # the new tables carry every health verdict: put them in service.  A resource that
+        # stays takes over the running server of its predecessor (table swap, no socket
+        # change); readers of self.plugins see the old list until then, never an empty one
+        old = {str(p.resource): p for p in self.plugins}
+        swapped = 0
+        for p in plugins:
+            prev = old.pop(str(p.resource), None)
+            if prev is not None and prev.serving and not prev.fatal_error:
+                try:
+                    p.adopt(prev)
+                    swapped += 1
+                    continue
+                except Exception as e:  # the fresh plugin starts in start_plugins instead
+                    log.error("swapping the device table of %s into its server failed: %s", p.resource, e)
+            if prev is not None:
+                self._stop_plugin(prev)
+        for prev in old.values():  # resources that are gone
+            self._stop_plugin(prev)
+        if swapped:
+            self.counters["table_swaps"] = self.counters.get("table_swaps", 0) + swapped
+        self._node_index_of = {self._identity(g): g.index for g in node}
+        self.gpus, self.topology = sel, topo
+        self.signature = self._signature(node, sel)
+        self.device_map = device_map
+        self._key_of, self._index_of = key_of, index_of
+        gpus = sel
+        self.counters["reloads"] = self.counters.get("reloads", 0) + 1
         self.plugins = plugins
+        for job in canary_jobs:
+            self._start_canary_pool().submit(self._startup_canary_job, *job)
+        for key in [k for k in self._reverify if k in index_of]:
+            self._reverify.discard(key)
+            self._verify_later(key, -1, "recovery canary held when the previous plugin process stopped")
         n = native.load()
         labels = []
         hips = {(g.index, p.index): p.hip_id for g in gpus for p in g.partitions}
@@ -739,11 +825,11 @@ class PluginManager:
             gen = self._health_gen[key] = self._health_gen.get(key, 0) + 1
             if healthy and self.cfg.health.canary:
                 # stay Unhealthy until the canary passes; do not block the event loop on it
+                log.info("%s reports healthy (%s); verifying with the canary", self._gpu_name(key), u.reason)
+                self._held_unhealthy.add(key)
                 if self._verify_pool is None:
                     self._verify_pool = concurrent.futures.ThreadPoolExecutor(max_workers=4,
                                                                               thread_name_prefix="canary")
-                log.info("%s reports healthy (%s); verifying with the canary", self._gpu_name(key), u.reason)
-                self._held_unhealthy.add(key)
                 self._verify_pool.submit(self._verify_and_post, u, key, gen)
                 return
             if healthy:
@@ -842,26 +928,98 @@ class PluginManager:
             self._held_unhealthy.discard(key)
         self._set_health(key, u.partition, ok, u.reason + ("" if ok else "; canary failed"))
 
-    def _startup_canary(self, gpus, key_of=None) -> set:
-        """Runs the gfx950 canary on every partition (one child process per partition, all
-        GPUs in parallel) before the first advertisement; returns failing (gpu, partition)."""
-        import concurrent.futures
+    def _stop_plugin(self, p) -> None:
+        try:
+            p.stop()
+        except Exception as e:  # pragma: no cover
+            log.error("failed to stop plugin %s: %s", p.resource, e)
 
-        from ..ops import canary
-        jobs = [(g.index, p.index if len(g.partitions) > 1 else -1, p.index, p.hip_id)
-                for g in gpus for p in g.partitions]
-        failed = set()
-        with concurrent.futures.ThreadPoolExecutor(max_workers=max(1, min(8, len(jobs)))) as ex:
-            futs = {ex.submit(self._run_canary, gpu, hw_part, hip, (key_of or {}).get(gpu)): (gpu, part)
-                    for gpu, part, hw_part, hip in jobs}
-            for f in concurrent.futures.as_completed(futs):
-                gpu, part = futs[f]
-                res = f.result()
-                if not res.get("ok"):
-                    failed.add((gpu, part))
-                    self._count("canary_failures")
-                    log.error("start-up canary failed on GPU %d partition %d: %s", gpu, part, res.get("error") or res)
-        return failed
+    def _start_canary_pool(self) -> concurrent.futures.ThreadPoolExecutor:
+        if self._canary_pool is None:
+            self._canary_pool = concurrent.futures.ThreadPoolExecutor(max_workers=8, thread_name_prefix="canary-start")
+        return self._canary_pool
+
+    def _in_use_partitions(self, device_map) -> set:
+        """(gpu, partition) pairs a container holds, as far as this process can tell: the
+        kubelet PodResources map when it is polled, else kubelet's device checkpoint in the
+        plugin directory (it lists every device kubelet has handed to a pod)."""
+        ids = set()
+        if self.podres is not None:
+            allocs, up = self.podres.snapshot()
+            if up:
+                ids |= {(res, dev.split("::")[0]) for res, dev in allocs}
+        if not ids:
+            from .podresources import checkpoint_allocations
+            ids = {(res, dev.split("::")[0]) for res, dev in
+                   checkpoint_allocations(os.path.join(self.cfg.pluginDir, "kubelet_internal_checkpoint"),
+                                          self.cfg.resourcePrefix)}
+        out = set()
+        for name, devs in device_map.items():
+            for d in devs:
+                if (name, d.id.split("::")[0]) in ids:
+                    out.add((d.gpu, d.partition))
+        return out
+
+    def _plan_startup_canary(self, sel, key_of, node_keys, device_map) -> list:
+        """health.canaryOnStart: the partitions to canary before they are advertised
+        Healthy - those of each GPU identity this process advertises for the first time
+        (a plain /restart or reload runs none; a GPU that left the node and came back runs
+        it again), except partitions a container holds already (a plugin restart on a busy
+        node must not run the canary next to a job, nor fail it on the memory the job
+        holds).  Marked pending: they are advertised Unhealthy until their verdict."""
+        self._start_canaried &= node_keys
+        in_use = self._in_use_partitions(device_map) if any(key_of[g.index] not in self._start_canaried
+                                                               for g in sel) else set()
+        jobs = []
+        for g in sel:
+            key = key_of[g.index]
+            if key in self._start_canaried:
+                continue
+            self._start_canaried.add(key)
+            for p in g.partitions:
+                part = p.index if len(g.partitions) > 1 else -1
+                if (g.index, part) in in_use or (g.index, -1) in in_use:
+                    self.counters["canary_skipped_in_use"] = self.counters.get("canary_skipped_in_use", 0) + 1
+                    log.info("start-up canary skips GPU %d partition %d: a container holds it", g.index, part)
+                    continue
+                self._start_pending.add((key, part))
+                jobs.append((key, g.index, part, p.index, p.hip_id))
+        return jobs
+
+    def _startup_canary_job(self, key: str, gpu: int, part: int, hw_part: int, hip: int) -> None:
+        """Pool thread: one partition's start-up canary; the verdict goes back as an event."""
+        try:
+            res = self._run_canary(gpu, hw_part, hip, key)
+            ok, why = bool(res.get("ok")), res.get("error") or ("" if res.get("ok") else str(res))
+        except Exception as e:  # a canary that cannot run does not pass the partition
+            ok, why = False, "canary could not run: %s" % e
+        self.events.put((EV_START_CANARY, key, part, ok, why))
+
+    def _apply_start_canary(self, key: str, part: int, ok: bool, why: str) -> None:
+        if (key, part) not in self._start_pending:
+            return  # the GPU left the node meanwhile
+        self._start_pending.discard((key, part))
+        gpu = self._index_of.get(key, -1)
+        if not ok:
+            self._canary_failed.add((key, part))
+            self._count("canary_failures")
+            log.error("start-up canary failed on %s partition %d: %s", self._gpu_name(key), part, why)
+            return
+        self._canary_failed.discard((key, part))  # a fresh verdict replaces an older one
+        if gpu >= 0 and self.monitor.gpu_healthy(gpu) and key not in self._held_unhealthy:
+            for p in self.plugins:
+                p.set_gpu_health(gpu, part, True)
+        log.info("start-up canary passed on %s partition %d", self._gpu_name(key), part)
+
+    def _verify_later(self, key: str, partition: int, reason: str) -> None:
+        """Holds a GPU Unhealthy and runs the recovery canary on it off the manager thread."""
+        import types
+        gen = self._health_gen[key] = self._health_gen.get(key, 0) + 1
+        if self._verify_pool is None:
+            self._verify_pool = concurrent.futures.ThreadPoolExecutor(max_workers=4, thread_name_prefix="canary")
+        self._held_unhealthy.add(key)
+        self._verify_pool.submit(self._verify_and_post, types.SimpleNamespace(partition=partition, reason=reason),
+                                 key, gen)
 
     def _count(self, key: str, n: int = 1) -> None:
         with self._canary_lock:  # counters touched from canary pool threads too
@@ -925,13 +1083,6 @@ class PluginManager:
             return "PreStartContainer: gfx950 canary failed on %s" % ", ".join(
                 "GPU %d%s" % (g, "" if p < 0 else " partition %d" % p) for g, p in sorted(failures))
         return ""
-
-    def _check_inventory(self) -> None:
-        """Periodic re-discovery: a compute/memory partition-mode change (SPX->CPX, ...) or a
-        GPU appearing/disappearing changes the device set; re-advertise when it does."""
-        gpus, topo = self.backend.discover()
-        self._apply_discovery(DISCOVERY_CHECK, gpus, topo, self.backend.last_discovery()
-                              if hasattr(self.backend, "last_discovery") else None, None)
 
     def _canary_ok(self, key: str) -> bool:
         gpu = self._index_of.get(key)
@@ -1097,6 +1248,8 @@ class PluginManager:
             self._discoverer.stop()
         if self._verify_pool is not None:
             self._verify_pool.shutdown(wait=False, cancel_futures=True)
+        if self._canary_pool is not None:
+            self._canary_pool.shutdown(wait=False, cancel_futures=True)
         self._stop_flag.set()
         self._running.clear()
         if self.podres is not None:

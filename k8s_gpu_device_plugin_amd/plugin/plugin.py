@@ -150,6 +150,10 @@ class AmdDevicePlugin:
         self.prestart_check = None
         self._prestart_thread: threading.Thread | None = None
         self._prestart_pool: concurrent.futures.ThreadPoolExecutor | None = None
+        self._retiring = False  # a successor took the server over (adopt)
+        # the plugin a grpcio server's handlers serve from: shared with (and redirected
+        # by) a successor that adopts the server, so requests follow the current table
+        self._front = [self]
 
     # ------------------------------------------------------------------ views
     def devices(self) -> Devices:
@@ -178,6 +182,10 @@ class AmdDevicePlugin:
         while not self._stopping:
             for job_id, ids in self.table.pop_prestart(200):
                 self._prestart_pool.submit(self._run_prestart, job_id, ids)
+            if self._retiring and self.table.prestart_pending == 0:
+                # a successor serves now and every check queued here has been answered
+                self._prestart_pool.shutdown(wait=False)
+                return
 
     def _run_prestart(self, job_id: int, ids) -> None:
         try:
@@ -186,7 +194,53 @@ class AmdDevicePlugin:
             err = "PreStartContainer check failed to run: %s" % e
         self.table.complete_prestart(job_id, not err, err or "")
 
+    def adopt(self, prev: "AmdDevicePlugin") -> None:
+        """Takes over ``prev``'s running server, socket and kubelet registration and
+        swaps this plugin's table into it: kubelet's connection stays up, its ListAndWatch
+        stream gets the new device list, and no admission finds the endpoint gone.
+        ``prev`` is left inert (its stop() does nothing to the server)."""
+        self.table.inherit_stats(prev.table)  # RPC histograms continue across the swap
+        with prev._lock:
+            if not prev._serving or prev._stopping:
+                raise RuntimeError("%s is not serving" % prev.resource)
+            server, nserver = prev._server, prev._native_server
+            prev._server = prev._native_server = None
+            prev._serving = False
+            prev._retiring = True
+            sock_ident, prev._sock_ident = prev._sock_ident, None
+            registered, prev.registered = prev.registered, False
+        with self._lock:
+            self._server, self._native_server = server, nserver
+            self._serving, self._stopping = True, False
+            self._sock_ident, self.registered = sock_ident, registered
+            self._crashes, self._last_crash = prev._crashes, prev._last_crash
+            self.server_restarts = prev.server_restarts
+            self._front = prev._front
+            if self.cfg is not None and self.cfg.health.canaryOnPreStart and self._prestart_thread is None:
+                self._start_prestart_locked()
+        if nserver is not None:
+            nserver.set_table(self.table)  # workers switch tables and push ListAndWatch
+        self._front[0] = self  # grpcio handlers serve from this plugin's table from now on
+        prev.table.wake()      # grpcio ListAndWatch generators waiting on the old table
+        if server is not None:
+            self._supervisor = threading.Thread(target=self._supervise, args=(server,), daemon=True,
+                                                name="dp-supervise-" + self.resource.get_resource_name())
+            self._supervisor.start()
+        # the predecessor's PreStartContainer loop answers what is queued on its table, then ends
+        log.info("device table swapped into the running server", extra={"resourceName": str(self.resource),
+                                                                        "devices": len(self)})
+
+    def _start_prestart_locked(self) -> None:
+        self.table.resume_prestart()
+        self._prestart_pool = concurrent.futures.ThreadPoolExecutor(
+            max_workers=4, thread_name_prefix="prestart-" + self.resource.get_resource_name())
+        self._prestart_thread = threading.Thread(target=self._prestart_loop, daemon=True,
+                                                 name="prestart-" + self.resource.get_resource_name())
+        self._prestart_thread.start()
+
     def stop(self) -> None:
+        if self._retiring:  # the server belongs to a successor now
+            return
         self.table.cancel_prestart("device plugin for %s is stopping" % self.resource)
         if self._prestart_thread is not None:
             self._stopping = True
@@ -232,12 +286,7 @@ class AmdDevicePlugin:
             self._serving = True
             self._sock_ident = _socket_ident(self.socket)
             if self.cfg is not None and self.cfg.health.canaryOnPreStart and self._prestart_thread is None:
-                self.table.resume_prestart()
-                self._prestart_pool = concurrent.futures.ThreadPoolExecutor(
-                    max_workers=4, thread_name_prefix="prestart-" + self.resource.get_resource_name())
-                self._prestart_thread = threading.Thread(target=self._prestart_loop, daemon=True,
-                                                         name="prestart-" + self.resource.get_resource_name())
-                self._prestart_thread.start()
+                self._start_prestart_locked()
         # blocking self-dial (plugin/plugin.go:130-134)
         try:
             if self.server_kind == "native":
@@ -401,21 +450,25 @@ class AmdDevicePlugin:
 
     # ------------------------------------------------------------------ RPCs (grpcio)
     def _handler(self):
+        """grpcio handlers.  They read the table through ``front``, the plugin currently
+        serving this server: a reload that swaps in a successor's table redirects them."""
         import grpc
         n = native.load()
-        table = self.table
+        front = self._front
         rpc_opt, rpc_law, rpc_pref, rpc_alloc, rpc_pre = (n.RPC_OPTIONS, n.RPC_LIST_AND_WATCH, n.RPC_PREFERRED,
                                                           n.RPC_ALLOCATE, n.RPC_PRE_START)
         perf = time.perf_counter
-        opts = table.options()
 
         def get_options(req: bytes, ctx) -> bytes:
             t0 = perf()
+            table = front[0].table
+            out = table.options()
             table.observe(rpc_opt, perf() - t0, False)
-            return opts
+            return out
 
         def allocate(req: bytes, ctx) -> bytes:
             t0 = perf()
+            table = front[0].table
             ok, out = table.allocate(req)
             table.observe(rpc_alloc, perf() - t0, not ok)
             if not ok:
@@ -424,6 +477,7 @@ class AmdDevicePlugin:
 
         def preferred(req: bytes, ctx) -> bytes:
             t0 = perf()
+            table = front[0].table
             ok, out = table.preferred(req)
             table.observe(rpc_pref, perf() - t0, not ok)
             if not ok:
@@ -432,7 +486,9 @@ class AmdDevicePlugin:
 
         def pre_start(req: bytes, ctx) -> bytes:
             t0 = perf()
-            if not (self.cfg is not None and self.cfg.health.canaryOnPreStart):
+            plugin = front[0]
+            table = plugin.table
+            if not (plugin.cfg is not None and plugin.cfg.health.canaryOnPreStart):
                 table.observe(rpc_pre, 0.0, False)
                 return b""
             done = threading.Event()
@@ -452,6 +508,8 @@ class AmdDevicePlugin:
             return b""
 
         def list_and_watch(req: bytes, ctx):
+            plugin = front[0]
+            table = plugin.table
             version = table.version
             t0 = perf()
             payload = table.list_and_watch()
@@ -459,13 +517,18 @@ class AmdDevicePlugin:
             yield payload
             while True:
                 # native wait (GIL released): woken by any table change, including the
-                # monitor thread's fail-fast Unhealthy path, or by stop() -> table.wake()
-                while table.version == version and not self._stopping and ctx.is_active():
+                # monitor thread's fail-fast Unhealthy path, by stop() -> table.wake(), or
+                # by a successor's adopt() swapping its table in (it wakes the old one)
+                while (front[0] is plugin and table.version == version and not plugin._stopping
+                       and ctx.is_active()):
                     table.wait_change(version, 500)
-                if self._stopping or not ctx.is_active():
+                if front[0] is not plugin:  # table swapped: follow the successor
+                    plugin = front[0]
+                    table = plugin.table
+                elif plugin._stopping or not ctx.is_active():
                     return
                 version = table.version
-                log.info("'%s' device health changed; sending update", self.resource)
+                log.info("'%s' device list changed; sending update", plugin.resource)
                 yield table.list_and_watch()
 
         u = grpc.unary_unary_rpc_method_handler

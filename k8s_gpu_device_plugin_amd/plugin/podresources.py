@@ -50,6 +50,34 @@ def list_allocations(socket_path: str, resource_prefix: str, timeout: float = 5.
     return out
 
 
+def checkpoint_allocations(path: str, resource_prefix: str) -> set:
+    """``{(resource, device_id)}`` from kubelet's device-manager checkpoint
+    (``<device-plugins dir>/kubelet_internal_checkpoint``): every device kubelet has
+    handed to a pod it still tracks.  Read when PodResources is not polled (a plugin
+    restarting on a busy node).  Understands both layouts kubelet has written
+    (``DeviceIDs`` as a list, and as a NUMA-node -> list map); an unreadable file is
+    an empty set."""
+    import json
+    try:
+        with open(path, "r", encoding="utf-8") as f:
+            raw = json.load(f)
+    except (OSError, ValueError):
+        return set()
+    data = raw.get("Data") if isinstance(raw, dict) else None
+    entries = data.get("PodDeviceEntries") if isinstance(data, dict) else None
+    prefix = resource_prefix.rstrip("/") + "/"
+    out = set()
+    for e in entries if isinstance(entries, list) else []:
+        if not isinstance(e, dict) or not str(e.get("ResourceName", "")).startswith(prefix):
+            continue
+        ids = e.get("DeviceIDs")
+        if isinstance(ids, dict):
+            ids = [d for v in ids.values() if isinstance(v, list) for d in v]
+        for d in ids if isinstance(ids, list) else []:
+            out.add((str(e["ResourceName"]), str(d)))
+    return out
+
+
 def _esc(v: str) -> str:
     return str(v).replace("\\", "\\\\").replace('"', '\\"').replace("\n", "\\n")
 

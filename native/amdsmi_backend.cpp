@@ -491,6 +491,7 @@ class AmdSmiBackend : public Backend {
       if (valid16(m.pcie_link_speed) && m.pcie_link_speed != 0) s->pcie_link_speed_gtps = m.pcie_link_speed * 0.1;
       if (valid64(m.pcie_replay_count_acc)) s->pcie_replays = static_cast<double>(m.pcie_replay_count_acc);
       if (valid64(m.pcie_l0_to_recov_count_acc)) s->pcie_recoveries = static_cast<double>(m.pcie_l0_to_recov_count_acc);
+      if (valid64(m.firmware_timestamp) && m.firmware_timestamp != 0) s->fw_clock_s = m.firmware_timestamp * 1e-8;
     }
     s->num_partitions = std::min(nparts, kMaxPartitions);
     partition_busy(*ds, ref, mst == AMDSMI_STATUS_SUCCESS ? &m : nullptr, s);

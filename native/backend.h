@@ -202,6 +202,11 @@ struct GpuSample {
   // metrics (amdsmi_get_gpu_partition_metrics_info), 2 the socket blob's xcp_stats[p]
   int partition_busy_source[kMaxPartitions] = {};
   double partition_vram_used_bytes[kMaxPartitions] = {};
+  // The power-management firmware's own clock, seconds since the firmware started
+  // (gpu_metrics firmware_timestamp, 10 ns ticks).  A GPU reset reloads the firmware, so
+  // the clock restarting is a reset an unprivileged reader can see without amdsmi event
+  // notification (which needs /dev/kfd).  -1 = not reported.
+  double fw_clock_s = -1;
   bool ok = false;
 };
 
@@ -222,6 +227,10 @@ enum EventKind : int {
   kEvtLinkQuality = 12,   // an up xGMI link re-trained at another bandwidth (value = Gb/s)
   kEvtPcieDegraded = 13,  // host PCIe link below the configured floor -> Unhealthy
   kEvtPcieRestored = 14,  // back at or above it
+  // A reset seen by polling (no event delivery): the firmware clock restarted, or the GPU
+  // came back from a telemetry outage on a GPU that reports no firmware clock.  Acts
+  // like POST_RESET: clears the reset and uncorrectable-ECC latches.
+  kEvtResetObserved = 15,
 };
 
 const char* event_kind_name(int kind);

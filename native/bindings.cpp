@@ -17,7 +17,6 @@
 #include "hpack.h"
 #include "health.h"
 #include "httpd.h"
-#include "loadgen.h"
 #include "metrics.h"
 #include "profiler.h"
 #include "telemetry.h"
@@ -179,6 +178,7 @@ PYBIND11_MODULE(_native, m) {
       .def_readonly("pcie_link_speed_gtps", &GpuSample::pcie_link_speed_gtps)
       .def_readonly("pcie_replays", &GpuSample::pcie_replays)
       .def_readonly("pcie_recoveries", &GpuSample::pcie_recoveries)
+      .def_readonly("fw_clock_s", &GpuSample::fw_clock_s)
       .def_property_readonly("links", [](const GpuSample& s) {
         py::list l;
         for (int k = 0; k < s.num_links; ++k)
@@ -210,6 +210,8 @@ PYBIND11_MODULE(_native, m) {
   m.attr("EVT_PCIE_DEGRADED") = static_cast<int>(kEvtPcieDegraded);
   m.attr("EVT_PCIE_RESTORED") = static_cast<int>(kEvtPcieRestored);
   m.attr("EVT_LINK_QUALITY") = static_cast<int>(kEvtLinkQuality);
+  m.attr("EVT_RESET_OBSERVED") = static_cast<int>(kEvtResetObserved);
+  m.attr("EVT_FIXTURE_FIRMWARE_RESET") = FixtureBackend::kScriptFirmwareReset;
   m.attr("LINK_INTERNAL") = static_cast<int>(kLinkInternal);
   m.attr("LINK_PCIE") = static_cast<int>(kLinkPcie);
   m.attr("LINK_XGMI") = static_cast<int>(kLinkXgmi);
@@ -320,6 +322,10 @@ PYBIND11_MODULE(_native, m) {
       .def("set_serialised", &FixtureBackend::set_serialised, py::arg("on"))
       .def_property_readonly("serialised", &FixtureBackend::serialised)
       .def("set_gpu_present", &FixtureBackend::set_gpu_present)
+      .def("reset_firmware", &FixtureBackend::reset_firmware)
+      .def("set_fw_clock_reported", &FixtureBackend::set_fw_clock_reported, py::arg("gpu"), py::arg("reported"))
+      .def("set_sample_fail", &FixtureBackend::set_sample_fail, py::arg("gpu"), py::arg("fail"))
+      .def("set_events_enabled", &FixtureBackend::set_events_enabled, py::arg("on"))
       .def_property_readonly("discover_calls", &FixtureBackend::discover_calls);
 
   m.def("make_amdsmi_backend", &make_amdsmi_backend, py::call_guard<py::gil_scoped_release>());
@@ -435,6 +441,7 @@ PYBIND11_MODULE(_native, m) {
   m.attr("RPC_PRE_START") = static_cast<int>(kRpcPreStart);
 
   py::class_<DeviceTable, std::shared_ptr<DeviceTable>>(m, "DeviceTable")
+      .def("inherit_stats", &DeviceTable::inherit_stats, py::arg("prev"))
       .def("wait_change", &DeviceTable::wait_change, py::call_guard<py::gil_scoped_release>(), py::arg("seen"),
            py::arg("timeout_ms") = 500)
       .def("wake", &DeviceTable::wake)
@@ -530,6 +537,28 @@ PYBIND11_MODULE(_native, m) {
                " healthy=" + std::to_string(u.healthy) + " " + u.reason + ">";
       });
 
+  py::class_<HealthLatch>(m, "HealthLatch")
+      .def(py::init<>())
+      .def(py::init([](std::string key, int64_t last_ue, double fw_boot_s, std::string reason, int64_t since_ns) {
+             HealthLatch l;
+             l.key = std::move(key);
+             l.ecc_bad = true;
+             l.last_ue = last_ue;
+             l.fw_boot_s = fw_boot_s;
+             l.reason = std::move(reason);
+             l.since_ns = since_ns;
+             return l;
+           }),
+           py::arg("key"), py::arg("last_ue") = -1, py::arg("fw_boot_s") = -1.0, py::arg("reason") = "",
+           py::arg("since_ns") = 0)
+      .def_readwrite("key", &HealthLatch::key)
+      .def_readwrite("ecc_bad", &HealthLatch::ecc_bad)
+      .def_readwrite("last_ue", &HealthLatch::last_ue)
+      .def_readwrite("fw_boot_s", &HealthLatch::fw_boot_s)
+      .def_readwrite("reason", &HealthLatch::reason)
+      .def_readwrite("since_ns", &HealthLatch::since_ns);
+  m.def("boottime_s", &boottime_s);
+
   py::class_<HealthMonitor, std::shared_ptr<HealthMonitor>>(m, "HealthMonitor")
       .def(py::init<std::shared_ptr<Backend>, int>(), py::arg("backend"), py::arg("lost_after_failures") = 3)
       .def("set_gpu_count", &HealthMonitor::set_gpu_count, py::call_guard<py::gil_scoped_release>())
@@ -551,7 +580,10 @@ PYBIND11_MODULE(_native, m) {
            py::arg("debounce") = 1, py::call_guard<py::gil_scoped_release>())
       .def("on_sample", &HealthMonitor::on_sample, py::arg("gpu"), py::arg("ok"), py::arg("sample"),
            py::call_guard<py::gil_scoped_release>())
-      .def_property_readonly("events_seen", &HealthMonitor::events_seen);
+      .def_property_readonly("events_seen", &HealthMonitor::events_seen)
+      .def("latches", &HealthMonitor::latches)
+      .def("restore_latches", &HealthMonitor::restore_latches, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("resets_observed", &HealthMonitor::resets_observed);
 
   // ---- exporter ----
   py::class_<PartitionLabel>(m, "PartitionLabel")
@@ -665,7 +697,8 @@ PYBIND11_MODULE(_native, m) {
   py::class_<GrpcServer, std::shared_ptr<GrpcServer>>(m, "GrpcServer")
       .def(py::init<std::string, int, int, int>(), py::arg("socket_path"), py::arg("threads") = 2,
            py::arg("busy_poll_us") = 0, py::arg("admission_poll_us") = 0)
-      .def("set_table", &GrpcServer::set_table)
+      .def("set_table", &GrpcServer::set_table, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("table_swaps", &GrpcServer::table_swaps)
       .def("add_table", &GrpcServer::set_table)
       .def("start", &GrpcServer::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &GrpcServer::stop, py::call_guard<py::gil_scoped_release>())
@@ -725,59 +758,7 @@ PYBIND11_MODULE(_native, m) {
             return py::bytes(resp);
           },
           py::arg("timeout_s") = 5.0)
-      .def("bench_unary",
-           [](H2Client& c, const std::string& path, const py::bytes& req, int n, int gap_us) {
-             std::string r(req), resp, msg;
-             std::vector<double> out;
-             out.reserve(static_cast<size_t>(n));
-             py::gil_scoped_release rel;
-             for (int i = 0; i < n; ++i) {
-               // gap_us > 0: idle between calls, so each one meets a sleeping server (the
-               // way kubelet's sparse pod-admission RPCs do), not its busy-poll window
-               if (gap_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(gap_us));
-               const int64_t t0 = mono_ns();
-               const int st = c.unary(path, r, &resp, &msg);
-               out.push_back((mono_ns() - t0) * 1e-9);
-               if (st != 0) throw std::runtime_error("grpc-status " + std::to_string(st) + ": " + msg);
-             }
-             return out;
-           },
-           py::arg("path"), py::arg("req"), py::arg("n"), py::arg("gap_us") = 0)
-      .def("bench_unary_ts",
-           // Same as bench_unary, per call: (start, CLOCK_MONOTONIC ns; latency, s; the
-           // CPU the client ran on when the answer arrived) - for attributing the tail to
-           // idle gaps, CPU migrations or events of the server process at that time.
-           [](H2Client& c, const std::string& path, const py::bytes& req, int n, int gap_us) {
-             std::string r(req), resp, msg;
-             std::vector<int64_t> starts;
-             std::vector<double> lat;
-             std::vector<int> cpus;
-             starts.reserve(static_cast<size_t>(n));
-             lat.reserve(static_cast<size_t>(n));
-             cpus.reserve(static_cast<size_t>(n));
-             {
-               py::gil_scoped_release rel;
-               for (int i = 0; i < n; ++i) {
-                 if (gap_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(gap_us));
-                 const int64_t t0 = mono_ns();
-                 const int st = c.unary(path, r, &resp, &msg);
-                 lat.push_back((mono_ns() - t0) * 1e-9);
-                 starts.push_back(t0);
-                 cpus.push_back(sched_getcpu());
-                 if (st != 0) throw std::runtime_error("grpc-status " + std::to_string(st) + ": " + msg);
-               }
-             }
-             return py::make_tuple(starts, lat, cpus);
-           },
-           py::arg("path"), py::arg("req"), py::arg("n"), py::arg("gap_us") = 0)
       .def("close", &H2Client::close);
-
-  m.def("h2_bench_unary",
-        [](const std::string& sock, const std::string& path, const py::bytes& req, int n) {
-          std::string r(req);
-          py::gil_scoped_release rel;
-          return h2_bench_unary(sock, path, r, n);
-        });
 
   m.def("format_float", [](double v) {  // Prometheus number formatting (exposed for tests)
     std::string s;
@@ -827,37 +808,6 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("table_size", &hpack::Decoder::table_size)
       .def_property_readonly("table_entries", &hpack::Decoder::table_entries);
 
-  // ---- load generators (bench / BASELINE protocol) ----
-  auto load_dict = [](const LoadResult& r) {
-    py::dict d;
-    d["ok"] = r.ok;
-    d["errors"] = r.errors;
-    d["bytes"] = r.bytes;
-    d["elapsed_s"] = r.elapsed_s;
-    d["latencies_s"] = r.latencies_s;
-    return d;
-  };
-  m.def("http_load",
-        [load_dict](const std::string& host, int port, const std::string& path, int conns, double duration_s,
-                    double target_rps, bool accept_gzip) {
-          LoadResult r;
-          {
-            py::gil_scoped_release rel;
-            r = http_load(host, port, path, conns, duration_s, target_rps, accept_gzip);
-          }
-          return load_dict(r);
-        },
-        py::arg("host"), py::arg("port"), py::arg("path") = "/metrics", py::arg("conns") = 4,
-        py::arg("duration_s") = 2.0, py::arg("target_rps") = 0.0, py::arg("accept_gzip") = false);
-  m.def(
-      "health_propagation",
-      [](std::shared_ptr<Backend> be, const std::string& sock, int gpu, int events) {
-        auto* fx = dynamic_cast<FixtureBackend*>(be.get());
-        if (!fx) throw std::invalid_argument("health_propagation needs a fixture backend");
-        py::gil_scoped_release rel;
-        return health_propagation(*fx, sock, gpu, events);
-      },
-      py::arg("backend"), py::arg("socket_path"), py::arg("gpu"), py::arg("events") = 60);
   // ---- whole-process CPU sampling profiler (benchmark: true) ----
   m.def("prof_start", &prof::start, py::arg("hz") = 997);
   m.def("prof_stop", &prof::stop);
@@ -875,32 +825,4 @@ PYBIND11_MODULE(_native, m) {
     }
     return out;
   });
-  m.def("uds_pingpong",
-        [](int n, int warmup, int req_bytes, int resp_bytes, bool server_spin, bool tcp, int gap_us) {
-          py::gil_scoped_release rel;
-          return uds_pingpong(n, warmup, req_bytes, resp_bytes, server_spin, tcp, gap_us);
-        },
-        py::arg("n") = 10000, py::arg("warmup") = 500, py::arg("req_bytes") = 128, py::arg("resp_bytes") = 256,
-        py::arg("server_spin") = false, py::arg("tcp") = false, py::arg("gap_us") = 0);
-  py::class_<UdsPinger>(m, "UdsPinger")
-      .def(py::init<int, int, int>(), py::arg("req_bytes"), py::arg("resp_bytes"), py::arg("server_timeout_ms") = 100)
-      .def("once", &UdsPinger::once, py::call_guard<py::gil_scoped_release>());
-  m.def("render_bench",
-        [](std::shared_ptr<Exporter> ex, std::shared_ptr<HttpServer> http, int threads, int iters) {
-          py::gil_scoped_release rel;
-          return render_bench(std::move(ex), std::move(http), threads, iters);
-        },
-        py::arg("exporter"), py::arg("http") = nullptr, py::arg("threads") = 1, py::arg("iters") = 10000);
-  m.def("grpc_load",
-        [load_dict](const std::string& sock, const std::string& method, const py::bytes& req, int conns,
-                    double duration_s) {
-          std::string rq(req);
-          LoadResult r;
-          {
-            py::gil_scoped_release rel;
-            r = grpc_load(sock, method, rq, conns, duration_s);
-          }
-          return load_dict(r);
-        },
-        py::arg("socket_path"), py::arg("method"), py::arg("req"), py::arg("conns") = 4, py::arg("duration_s") = 2.0);
 }

@@ -59,6 +59,7 @@ const char* event_kind_name(int kind) {
     case kEvtLinkQuality: return "xgmi_link_bandwidth_changed";
     case kEvtPcieDegraded: return "pcie_link_degraded";
     case kEvtPcieRestored: return "pcie_link_restored";
+    case kEvtResetObserved: return "gpu_reset_observed";
     default: return "none";
   }
 }

@@ -38,14 +38,18 @@ std::string base_of(const std::string& id) {
 }
 }  // namespace
 
+DeviceTable::RpcStats::RpcStats() {
+  for (int r = 0; r < kRpcCount; ++r) {
+    hist[r] = std::make_unique<Histogram>(rpc_buckets());
+    errors[r].store(0);
+  }
+}
+
 DeviceTable::DeviceTable(TableConfig cfg, std::vector<TableDevice> devices, Topology topo)
     : cfg_(std::move(cfg)), devs_(std::move(devices)), topo_(std::make_shared<const Topology>(std::move(topo))) {
   health_.reset(new std::atomic<uint8_t>[devs_.size() ? devs_.size() : 1]);
   for (size_t i = 0; i < devs_.size(); ++i) health_[i].store(devs_[i].healthy ? 1 : 0);
-  for (int r = 0; r < kRpcCount; ++r) {
-    hist_[r] = std::make_unique<Histogram>(rpc_buckets());
-    errors_[r].store(0);
-  }
+  stats_ = std::make_shared<RpcStats>();
   for (size_t i = 0; i < devs_.size(); ++i) {
     const auto& d = devs_[i];
     index_.emplace(std::string_view(devs_[i].id), static_cast<int>(i));
@@ -555,8 +559,8 @@ bool DeviceTable::preferred(std::string_view req, std::string* out) const {
 
 void DeviceTable::observe(int rpc, double seconds, bool error) const {
   if (rpc < 0 || rpc >= kRpcCount) return;
-  hist_[rpc]->observe(seconds);
-  if (error) errors_[rpc].fetch_add(1, std::memory_order_relaxed);
+  stats_->hist[rpc]->observe(seconds);
+  if (error) stats_->errors[rpc].fetch_add(1, std::memory_order_relaxed);
 }
 
 void DeviceTable::render_metric_headers(std::string* out) {
@@ -566,7 +570,7 @@ void DeviceTable::render_metric_headers(std::string* out) {
 
 uint64_t DeviceTable::metrics_version() const {
   uint64_t v = 0;
-  for (int r = 0; r < kRpcCount; ++r) v += hist_[r]->count();
+  for (int r = 0; r < kRpcCount; ++r) v += stats_->hist[r]->count();
   return v;
 }
 
@@ -574,11 +578,11 @@ void DeviceTable::render_metrics(std::string* out, bool with_headers) const {
   if (with_headers) render_metric_headers(out);
   std::string labels;
   for (int r = 0; r < kRpcCount; ++r) {
-    if (hist_[r]->count() == 0) continue;
+    if (stats_->hist[r]->count() == 0) continue;
     labels.assign("resource=\"");
     append_label_value(&labels, cfg_.resource_name);
     labels.append("\",rpc=\"").append(rpc_name(r)).append("\",");
-    hist_[r]->render(out, "amdgpu_device_plugin_rpc_duration_seconds", labels);
+    stats_->hist[r]->render(out, "amdgpu_device_plugin_rpc_duration_seconds", labels);
   }
 }
 

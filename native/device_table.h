@@ -149,6 +149,8 @@ class DeviceTable {
   size_t prestart_pending() const;
 
   void observe(int rpc, double seconds, bool error) const;
+  // Continue `prev`'s RPC histograms (call before this table serves anything).
+  void inherit_stats(const DeviceTable& prev) { stats_ = prev.stats_; }
   void render_metrics(std::string* out, bool with_headers) const;
   static void render_metric_headers(std::string* out);
 
@@ -213,8 +215,15 @@ class DeviceTable {
   std::shared_ptr<const std::string> law_;        // cached ListAndWatchResponse
   std::atomic<uint64_t> version_{1};
 
-  mutable std::unique_ptr<Histogram> hist_[kRpcCount];
-  mutable std::atomic<uint64_t> errors_[kRpcCount];
+  // RPC latency histograms and error counts.  Shared: a table swapped into a running
+  // server in place of another (a reload that keeps the resource) carries on its
+  // predecessor's series instead of resetting them (inherit_stats).
+  struct RpcStats {
+    std::unique_ptr<Histogram> hist[kRpcCount];
+    std::atomic<uint64_t> errors[kRpcCount];
+    RpcStats();
+  };
+  std::shared_ptr<RpcStats> stats_;
 };
 
 }  // namespace amdgpu_dp

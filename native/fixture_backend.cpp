@@ -72,6 +72,9 @@ void FixtureBackend::add_gpu(const GpuInfo& g) {
   pcie_.emplace_back(16, 32.0);
   pages_.emplace_back(0, 0);
   present_.push_back(true);
+  fw_start_ns_.push_back(1000000000LL);  // firmware up since one second after the host booted
+  fw_reported_.push_back(true);
+  sample_fail_.push_back(false);
 }
 
 void FixtureBackend::replace_gpu(int index, const GpuInfo& g) {
@@ -97,6 +100,9 @@ void FixtureBackend::clear() {
   pcie_.clear();
   pages_.clear();
   present_.clear();
+  fw_start_ns_.clear();
+  fw_reported_.clear();
+  sample_fail_.clear();
   scheduled_.clear();
   pending_.clear();
   {
@@ -173,6 +179,24 @@ void FixtureBackend::set_gpu_present(int gpu, bool present) {
   present_[gpu] = present;
 }
 
+void FixtureBackend::reset_firmware(int gpu) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (gpu < 0 || gpu >= static_cast<int>(fw_start_ns_.size())) throw std::out_of_range("bad gpu");
+  fw_start_ns_[gpu] = mono_ns();
+}
+
+void FixtureBackend::set_fw_clock_reported(int gpu, bool reported) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (gpu < 0 || gpu >= static_cast<int>(fw_reported_.size())) throw std::out_of_range("bad gpu");
+  fw_reported_[gpu] = reported;
+}
+
+void FixtureBackend::set_sample_fail(int gpu, bool fail) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (gpu < 0 || gpu >= static_cast<int>(sample_fail_.size())) throw std::out_of_range("bad gpu");
+  sample_fail_[gpu] = fail;
+}
+
 void FixtureBackend::enumerate(std::vector<DeviceRef>* refs) {
   discover_calls_.fetch_add(1);
   if (fail_discovery_.load()) throw std::runtime_error("fixture: discovery failure injected");
@@ -206,7 +230,7 @@ bool FixtureBackend::sample_device(const Inventory& inv, int index, GpuSample* s
   const int gpu = inv.refs[index].slot;
   auto call = device_call(gpu);
   std::lock_guard<std::mutex> lk(mu_);
-  if (gpu < 0 || gpu >= static_cast<int>(gpus_.size()) || !present_[gpu]) return false;
+  if (gpu < 0 || gpu >= static_cast<int>(gpus_.size()) || !present_[gpu] || sample_fail_[gpu]) return false;
   auto index_of_slot = [&](int slot) {
     for (size_t i = 0; i < inv.refs.size(); ++i)
       if (inv.refs[i].slot == slot) return static_cast<int>(i);
@@ -246,6 +270,7 @@ bool FixtureBackend::sample_device(const Inventory& inv, int index, GpuSample* s
   s->pcie_link_speed_gtps = pcie_[gpu].second;
   s->pcie_replays = 0;
   s->pcie_recoveries = 0;
+  s->fw_clock_s = fw_reported_[gpu] ? std::max<int64_t>(0, mono_ns() - fw_start_ns_[gpu]) * 1e-9 : -1;
   for (int peer = 0; peer < topo_.n && s->num_links < kMaxXgmiLinks; ++peer) {
     if (peer == gpu || topo_.at(gpu, peer).type != kLinkXgmi) continue;
     const int k = s->num_links++;
@@ -271,6 +296,7 @@ bool FixtureBackend::sample_device(const Inventory& inv, int index, GpuSample* s
 
 void FixtureBackend::arm_events() {
   std::lock_guard<std::mutex> lk(mu_);
+  // scheduled scripts run either way (their ECC / link effects are what polling sees)
   armed_at_ns_.store(mono_ns());
   shutdown_ = false;
 }
@@ -321,6 +347,11 @@ int FixtureBackend::wait_events(int timeout_ms, std::vector<HwEvent>* out) {
         e.ts_ns = now_ns();
         if (e.kind == kEvtEccUncorrectable && e.gpu >= 0 && e.gpu < static_cast<int>(ecc_ue_.size()))
           ecc_ue_[e.gpu] += 1;
+        if (e.kind == kScriptFirmwareReset) {
+          if (e.gpu >= 0 && e.gpu < static_cast<int>(fw_start_ns_.size())) fw_start_ns_[e.gpu] = mono_ns();
+          scheduled_.erase(scheduled_.begin());
+          continue;  // seen only through the firmware clock
+        }
         if ((e.kind == kEvtLinkDown || e.kind == kEvtLinkUp) && e.gpu >= 0 && e.peer >= 0 &&
             e.gpu < topo_.n && e.peer < topo_.n) {
           topo_.at(e.gpu, e.peer).up = topo_.at(e.peer, e.gpu).up = (e.kind == kEvtLinkUp);
@@ -331,9 +362,15 @@ int FixtureBackend::wait_events(int timeout_ms, std::vector<HwEvent>* out) {
     }
     if (!pending_.empty()) {
       int n = 0;
+      const bool delivered = events_enabled_.load();
       while (!pending_.empty()) {
         HwEvent e = pending_.front();
         pending_.pop_front();
+        // what only amdsmi event notification reports is lost without it; an uncorrectable
+        // ECC error is then seen by polling the count (incremented when it fired)
+        if (!delivered && (e.kind == kEvtPreReset || e.kind == kEvtPostReset || e.kind == kEvtThermal ||
+                           e.kind == kEvtVmFault || e.kind == kEvtEccUncorrectable))
+          continue;
         translate(&e);
         out->push_back(std::move(e));
         ++n;

@@ -22,13 +22,16 @@ namespace amdgpu_dp {
 class FixtureBackend : public Backend {
  public:
   static constexpr int kMaxGpus = 64;
+  // A scripted event kind that is not delivered: the GPU's firmware restarts (a reset as
+  // polling sees it, with no event notification) when it fires.
+  static constexpr int kScriptFirmwareReset = 100;
   explicit FixtureBackend(uint64_t seed = 1);
   std::string name() const override { return "fixture"; }
   // before the first discovery, index = slot (like an amdsmi session's enumeration order)
   std::string gpu_key(int gpu) const override;
   int wait_events(int timeout_ms, std::vector<HwEvent>* out) override;
   void arm_events() override;
-  int armed_event_sources() const override { return armed_at_ns_.load() != 0 ? 1 : 0; }
+  int armed_event_sources() const override { return armed_at_ns_.load() != 0 && events_enabled_.load() ? 1 : 0; }
   void shutdown() override;
 
   // --- configuration (called before / between discoveries) ---
@@ -55,6 +58,16 @@ class FixtureBackend : public Backend {
   void set_retired_pages(int gpu, int64_t reserved, int64_t pending);
   void set_pcie_link(int gpu, int width, double gts);  // the host link as gpu_metrics reports it
   void set_gpu_present(int gpu, bool present);
+  // The GPU's firmware restarts now (what a reset does): its clock starts again at zero.
+  void reset_firmware(int gpu);
+  // Whether samples report the firmware clock (some firmware does not).
+  void set_fw_clock_reported(int gpu, bool reported);
+  // Telemetry of `gpu` fails (returns at once, unlike a wedge) while the GPU stays enumerated:
+  // a GPU in the middle of a reset.
+  void set_sample_fail(int gpu, bool fail);
+  // false: the node delivers no hardware events (an unprivileged pod cannot open /dev/kfd):
+  // arm_events arms nothing and reset / thermal / VM-fault events are dropped.
+  void set_events_enabled(bool on) { events_enabled_.store(on); }
   // A wedged driver: every call to `gpu` (sample, describe) blocks, holding its driver
   // lock, until the wedge is lifted (or shutdown) - the way an amdsmi call can hang on a
   // GPU that stopped responding.
@@ -88,6 +101,10 @@ class FixtureBackend : public Backend {
   std::vector<std::pair<int, double>> pcie_;  // (lanes, GT/s) per GPU
   std::vector<std::pair<int64_t, int64_t>> pages_;  // (reserved, pending) per GPU
   std::vector<bool> present_;
+  std::vector<int64_t> fw_start_ns_;   // CLOCK_MONOTONIC ns the GPU's firmware started at
+  std::vector<bool> fw_reported_;
+  std::vector<bool> sample_fail_;
+  std::atomic<bool> events_enabled_{true};
   std::string key_of_slot_locked(int slot) const;
   void translate(HwEvent* e) const;  // slot -> discovered index, plus keys
   std::atomic<int64_t> armed_at_ns_{0};

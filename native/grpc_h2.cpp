@@ -321,15 +321,33 @@ GrpcServer::GrpcServer(std::string socket_path, int threads, int busy_poll_us, i
 GrpcServer::~GrpcServer() { stop(); }
 
 void GrpcServer::set_table(std::shared_ptr<DeviceTable> t) {
+  if (!t) throw std::invalid_argument("GrpcServer: null device table");
   std::lock_guard<std::mutex> lk(mu_);
-  table_ = std::move(t);
-  table_->add_listener(notifier_);
+  t->add_listener(notifier_);
+  {
+    std::lock_guard<std::mutex> sk(swap_mu_);
+    table_ = std::move(t);
+    table_gen_.fetch_add(1, std::memory_order_release);
+  }
+  // running: wake every worker (not only those with a stream) so none serves a request
+  // from the old table after an idle wait
+  for (auto& w : workers_) {
+    const uint64_t one = 1;
+    if (w->efd >= 0) (void)!write(w->efd, &one, sizeof(one));
+  }
 }
 
 void GrpcServer::start() {
   std::lock_guard<std::mutex> lk(mu_);
   if (running_) return;
-  if (!table_) throw std::runtime_error("GrpcServer: no device table");
+  std::shared_ptr<DeviceTable> table;
+  uint64_t gen;
+  {
+    std::lock_guard<std::mutex> sk(swap_mu_);
+    table = table_;
+    gen = table_gen_.load();
+  }
+  if (!table) throw std::runtime_error("GrpcServer: no device table");
   struct sockaddr_un addr {};
   addr.sun_family = AF_UNIX;
   if (path_.size() >= sizeof(addr.sun_path)) throw std::runtime_error("GrpcServer: socket path too long: " + path_);
@@ -375,10 +393,10 @@ void GrpcServer::start() {
     fail_reason_.clear();
   }
   for (size_t i = 0; i < workers_.size(); ++i)
-    threads_.emplace_back([this, wp = workers_[i].get(), t = table_, i] {
+    threads_.emplace_back([this, wp = workers_[i].get(), t = table, gen, i] {
       // named, so /proc/<pid>/task/*/comm tells the workers apart (scripts/idle_probe.py)
       pthread_setname_np(pthread_self(), ("dpgrpc-" + std::to_string(i)).c_str());
-      run_guarded(wp, t);
+      run_guarded(wp, t, gen);
     });
   std::lock_guard<std::mutex> nk(notifier_->mu);
   notifier_->srv = this;
@@ -459,9 +477,9 @@ void GrpcServer::inject_fault(const std::string& kind) {
   }
 }
 
-void GrpcServer::run_guarded(Worker* w, std::shared_ptr<DeviceTable> table) {
+void GrpcServer::run_guarded(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t gen) {
   try {
-    run(w, std::move(table));
+    run(w, std::move(table), gen);
     return;
   } catch (const std::exception& e) {
     fail(std::string("gRPC worker died: ") + e.what());
@@ -480,7 +498,7 @@ void GrpcServer::run_guarded(Worker* w, std::shared_ptr<DeviceTable> table) {
   if (listen_fd_ >= 0) epoll_ctl(w->ep, EPOLL_CTL_DEL, listen_fd_, nullptr);
 }
 
-void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
+void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t table_gen) {
   std::vector<epoll_event> evs(128);
   char rbuf[32768];
   int spare = -1;  // reserve descriptor for accept_or_shed
@@ -921,6 +939,10 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
     };
     headers(&warm_hdrs, "/v1beta1.DevicePlugin/Allocate");
     headers(&warm_hdrs_pref, "/v1beta1.DevicePlugin/GetPreferredAllocation");
+  }
+  auto warm_requests = [&] {  // for the table's first device (again after a table swap)
+    warm_alloc.clear();
+    warm_pref.clear();
     const std::vector<std::string> ids = table->ids();
     if (!ids.empty()) {
       std::string ctr;
@@ -932,7 +954,8 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
       pb::put_int_nz(&pctr, 3, 1);
       pb::put_bytes(&warm_pref, 1, pctr);
     }
-  }
+  };
+  warm_requests();
   // The full tick: a private in-memory connection (no socket) gets an Allocate and a
   // GetPreferredAllocation as kubelet's client would frame them, and the worker runs them
   // through the same path as a real request - frame parsing, HPACK, dispatch, the table,
@@ -973,6 +996,20 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table) {
   SpinGuard guard;
   bool polite = false;  // the open window gives way to other threads (see SpinGuard)
   while (!stop_.load(std::memory_order_relaxed)) {
+    if (table_gen_.load(std::memory_order_acquire) != table_gen) {
+      // hot table swap (set_table): serve from the new table from here on and send every
+      // ListAndWatch stream its device list (versions of two tables do not compare)
+      {
+        std::lock_guard<std::mutex> sk(swap_mu_);
+        table = table_;
+        table_gen = table_gen_.load(std::memory_order_relaxed);
+      }
+      for (auto& kv : w->conns)
+        for (auto& st : kv.second->streams)
+          if (st.second.law) st.second.law_version = 0;
+      warm_requests();
+      seen_version = 0;  // table versions start at 1: the push below runs
+    }
     if (inject_worker_fault_.load(std::memory_order_relaxed)) {
       int armed = 1;
       if (inject_worker_fault_.compare_exchange_strong(armed, 0)) throw std::runtime_error("injected worker fault");
@@ -1482,21 +1519,6 @@ int H2Client::next_stream_message(std::string* resp, int timeout_ms) {
       return -1;  // the server ended the stream (plugin stopped)
     }
   }
-}
-
-std::vector<double> h2_bench_unary(const std::string& socket_path, const std::string& path, const std::string& req,
-                                   int n) {
-  H2Client c(socket_path);
-  std::vector<double> out;
-  out.reserve(static_cast<size_t>(n));
-  std::string resp, msg;
-  for (int i = 0; i < n; ++i) {
-    const int64_t t0 = mono_ns();
-    const int st = c.unary(path, req, &resp, &msg);
-    out.push_back((mono_ns() - t0) * 1e-9);
-    if (st != 0) throw std::runtime_error("h2_bench_unary: grpc-status " + std::to_string(st) + ": " + msg);
-  }
-  return out;
 }
 
 }  // namespace amdgpu_dp

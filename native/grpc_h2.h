@@ -8,8 +8,10 @@
 // (HEADERS + DATA + trailers) per call.  ListAndWatch streams stay open and are
 // re-sent whenever the table's health version changes (eventfd wake-up).
 //
-// Also: H2Client, a minimal blocking client used as the load generator in bench.py
-// and by tests (it speaks full HPACK, so it can talk to grpcio / grpc-go servers too).
+// Also: H2Client, a minimal blocking client: the plugin registers with kubelet and
+// probes its own socket through it (it speaks full HPACK, so it can talk to grpcio /
+// grpc-go servers too).  The load generators built on it live in tests/native/loadgen.cpp
+// (the bench extension), not in the plugin.
 #pragma once
 
 #include <atomic>
@@ -41,7 +43,12 @@ class GrpcServer {
   // Allocate off the cold path.
   GrpcServer(std::string socket_path, int threads, int busy_poll_us = 0, int admission_poll_us = 0);
   ~GrpcServer();
+  // Before start(): the table to serve.  While running: a hot swap (a plugin reload that
+  // keeps the resource): every worker switches to the new table before its next request,
+  // and every ListAndWatch stream is sent the new device list - kubelet's connection, its
+  // registration and the socket stay as they are.
   void set_table(std::shared_ptr<DeviceTable> t);
+  uint64_t table_swaps() const { return table_gen_.load(); }
   void start();  // throws std::runtime_error on bind/listen failure
   void stop();   // idempotent: trailers for open streams, GOAWAY, close, unlink socket
   void notify(); // wake ListAndWatch streams now (health changed)
@@ -91,8 +98,8 @@ class GrpcServer {
   };
   // `table` is handed over at thread creation: a worker never takes mu_, which stop()
   // holds while it joins the workers (one not yet scheduled when stop() ran deadlocked)
-  void run(Worker* w, std::shared_ptr<DeviceTable> table);
-  void run_guarded(Worker* w, std::shared_ptr<DeviceTable> table);  // run() + fault capture
+  void run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t gen);
+  void run_guarded(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t gen);  // run() + fault capture
   void fail(const std::string& why);
   std::atomic<bool> failed_{false};
   std::atomic<int> inject_worker_fault_{0};
@@ -106,7 +113,11 @@ class GrpcServer {
   std::atomic<int> keep_warm_ms_{0};
   std::atomic<bool> keep_warm_full_{true};
   std::atomic<uint64_t> warm_ticks_{0};
+  // table_ and table_gen_ change together under swap_mu_ (never held across anything else);
+  // workers poll table_gen_ (one relaxed load per loop) and take table_ when it moved
+  std::mutex swap_mu_;
   std::shared_ptr<DeviceTable> table_;
+  std::atomic<uint64_t> table_gen_{0};
   int listen_fd_ = -1;
   // the socket file this server bound (device, inode): stop() removes only that file, not
   // one a newer plugin instance (a rolling update's next pod) has bound at the same path
@@ -166,8 +177,5 @@ class H2Client {
   std::string out_buf_, body_buf_, data_buf_, frame_buf_;  // per-call scratch, capacity reused
 };
 
-// n sequential unary calls on one connection; per-call latency in seconds.
-std::vector<double> h2_bench_unary(const std::string& socket_path, const std::string& path, const std::string& req,
-                                   int n);
 
 }  // namespace amdgpu_dp

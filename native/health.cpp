@@ -1,5 +1,7 @@
 #include "health.h"
 
+#include <time.h>
+
 #include <cstdio>
 
 #include <algorithm>
@@ -105,7 +107,8 @@ std::pair<std::string, std::string> link_of(const std::string& a, const std::str
 int check_of(int kind) {
   switch (kind) {
     case kEvtPreReset:
-    case kEvtPostReset: return kCheckReset;
+    case kEvtPostReset:
+    case kEvtResetObserved: return kCheckReset;
     case kEvtEccUncorrectable: return kCheckEcc;
     case kEvtDeviceLost:
     case kEvtDeviceRecovered: return kCheckLost;
@@ -165,20 +168,32 @@ void HealthMonitor::process(const HwEvent& e) {
       state_[key].resetting = true;
       reconcile_locked(key, e.kind, why);
       return;
-    case kEvtPostReset: {
+    case kEvtPostReset:
+    case kEvtResetObserved: {
       if (!known) return;
       GpuState& st = state_[key];
       st.resetting = false;
       st.ecc_bad = false;  // a reset clears the uncorrectable-error latch
-      st.last_ue = -1;     // re-baseline on next sample
+      st.restored = false;
+      st.ecc_reason.clear();
+      // POST_RESET arrives on its own: re-baseline on the next sample.  A reset observed
+      // by polling comes from the sample that already took the new baseline.
+      if (e.kind == kEvtPostReset) st.last_ue = -1;
+      if (e.kind == kEvtResetObserved) ++resets_observed_;
       reconcile_locked(key, e.kind, why);
       return;
     }
-    case kEvtEccUncorrectable:
+    case kEvtEccUncorrectable: {
       if (!known) return;
-      state_[key].ecc_bad = true;
+      GpuState& st = state_[key];
+      if (!st.ecc_bad) {
+        st.ecc_reason = why;
+        st.ecc_since_ns = now_ns();
+      }
+      st.ecc_bad = true;
       reconcile_locked(key, e.kind, why);
       return;
+    }
     case kEvtDeviceLost:
       if (!known) return;
       state_[key].lost = true;
@@ -290,6 +305,45 @@ void HealthMonitor::on_sample(int gpu, bool ok, const GpuSample& s) {
     } else {
       st.failures = 0;
       if (st.lost) derived.push_back(event(kEvtDeviceRecovered, "telemetry responding again"));
+      // Resets seen without event delivery (an unprivileged pod cannot arm amdsmi events):
+      // a reset reloads the power-management firmware, whose clock then starts again.
+      std::string reset_why;
+      const double now_b = boottime_s();
+      if (s.fw_clock_s >= 0) {
+        const double fw_boot = now_b - s.fw_clock_s;
+        char msg[200];
+        if (st.restored_fw_boot >= 0) {
+          // a latch from a previous process: did the firmware start after it was recorded?
+          const double tol = std::max(30.0, 1e-4 * std::max(0.0, now_b - st.restored_fw_boot));
+          if (fw_boot > st.restored_fw_boot + tol) {
+            std::snprintf(msg, sizeof(msg), "firmware restarted while the plugin was not running (%.0f s after the "
+                          "start recorded with the latch)", fw_boot - st.restored_fw_boot);
+            reset_why = msg;
+          }
+          st.restored_fw_boot = -1;
+        }
+        if (st.fw_clock >= 0 && s.fw_clock_s + 1.0 < st.fw_clock) {
+          std::snprintf(msg, sizeof(msg), "firmware clock restarted (%.1f s -> %.1f s)", st.fw_clock, s.fw_clock_s);
+          reset_why = msg;
+          st.fw_advancing = false;
+        } else if (st.fw_clock >= 0) {
+          const double dt = now_b - st.fw_read_at, dc = s.fw_clock_s - st.fw_clock;
+          // a clock that ticks at about one second per second (a frozen or garbage
+          // timestamp never qualifies, so it can never be mistaken for a restart later)
+          if (dt >= 0.05 && dc > 0 && dc / dt > 0.5 && dc / dt < 2.0) st.fw_advancing = true;
+        }
+        st.fw_clock = s.fw_clock_s;
+        st.fw_read_at = now_b;
+        if (st.fw_advancing) st.fw_boot = fw_boot;
+      } else {
+        st.restored_fw_boot = -1;  // nothing to compare it with
+        // a GPU that reports no firmware clock: coming back from an outage is the reset
+        if (st.lost) reset_why = "telemetry back after an outage (the GPU reports no firmware clock)";
+      }
+      if (!reset_why.empty()) {
+        derived.push_back(event(kEvtResetObserved, reset_why));
+        st.last_ue = -1;  // counters after a reset start a new baseline (taken just below)
+      }
       if (s.ecc_uncorrectable >= 0) {
         if (st.last_ue >= 0 && s.ecc_uncorrectable > st.last_ue)
           derived.push_back(event(kEvtEccUncorrectable, "uncorrectable ECC count " + std::to_string(st.last_ue) +
@@ -402,7 +456,8 @@ void HealthMonitor::attach_tables(std::vector<std::shared_ptr<DeviceTable>> tabl
   for (size_t g = 0; g < table_keys_.size(); ++g) {
     if (table_keys_[g].empty()) continue;
     auto it = state_.find(table_keys_[g]);
-    down[g] = running_ && it != state_.end() && !it->second.reported_healthy;
+    // (a restored latch holds before the monitor runs: it came from a previous process)
+    down[g] = it != state_.end() && !it->second.reported_healthy && (running_ || it->second.restored);
   }
   for (int g : held_unhealthy)
     if (g >= 0 && g < static_cast<int>(down.size())) down[g] = 1;
@@ -456,6 +511,55 @@ std::vector<std::string> HealthMonitor::unhealthy_keys() const {
     if (!kv.second.reported_healthy) out.push_back(kv.first);
   std::sort(out.begin(), out.end());
   return out;
+}
+
+std::vector<HealthLatch> HealthMonitor::latches() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<HealthLatch> out;
+  for (const auto& kv : state_) {
+    const GpuState& st = kv.second;
+    if (!st.ecc_bad) continue;
+    HealthLatch l;
+    l.key = kv.first;
+    l.ecc_bad = true;
+    l.last_ue = st.last_ue;
+    l.fw_boot_s = st.fw_boot >= 0 ? st.fw_boot : st.restored_fw_boot;
+    l.reason = st.ecc_reason;
+    l.since_ns = st.ecc_since_ns;
+    out.push_back(std::move(l));
+  }
+  std::sort(out.begin(), out.end(), [](const HealthLatch& a, const HealthLatch& b) { return a.key < b.key; });
+  return out;
+}
+
+void HealthMonitor::restore_latches(const std::vector<HealthLatch>& latches) {
+  std::lock_guard<std::mutex> lk(mu_);
+  for (const auto& l : latches) {
+    if (l.key.empty() || !l.ecc_bad) continue;
+    GpuState& st = state_[l.key];
+    if (st.ecc_bad) continue;  // this process has its own verdict already
+    st.ecc_bad = true;
+    st.restored = true;
+    st.last_ue = l.last_ue;
+    st.ecc_reason = l.reason;
+    st.ecc_since_ns = l.since_ns;
+    st.restored_fw_boot = l.fw_boot_s;
+    st.fw_boot = l.fw_boot_s;
+    reconcile_locked(l.key, kEvtEccUncorrectable,
+                     "uncorrectable ECC latch restored from the previous plugin process" +
+                         (l.reason.empty() ? std::string() : " (" + l.reason + ")"));
+  }
+}
+
+uint64_t HealthMonitor::resets_observed() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return resets_observed_;
+}
+
+double boottime_s() {
+  struct timespec ts;
+  clock_gettime(CLOCK_BOOTTIME, &ts);
+  return static_cast<double>(ts.tv_sec) + ts.tv_nsec * 1e-9;
 }
 
 }  // namespace amdgpu_dp

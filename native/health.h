@@ -53,6 +53,21 @@ struct HealthUpdate {
   double link_gbps = 0;  // kEvtLinkQuality: the link's trained bandwidth now
 };
 
+// A latch that must outlive the plugin process (a DaemonSet rolling update, an OOM kill):
+// the manager writes these to its state file, keyed by the host's boot id, and hands them
+// back to the next process (HealthMonitor::restore_latches).
+struct HealthLatch {
+  std::string key;          // GPU identity
+  bool ecc_bad = false;     // uncorrectable-ECC latch (cleared only by a reset)
+  int64_t last_ue = -1;     // the UE count the latch was taken at (the next baseline)
+  // CLOCK_BOOTTIME second at which the GPU's firmware started (boot time - firmware
+  // clock), from a clock seen advancing; -1 = unknown.  A later process that finds the
+  // firmware started later than this knows the GPU was reset while nobody watched.
+  double fw_boot_s = -1;
+  std::string reason;
+  int64_t since_ns = 0;     // wall clock of the latch
+};
+
 // A one-shot flag another thread can wait on with a bound.
 struct ThreadExitFlag {
   std::mutex mu;
@@ -124,6 +139,15 @@ class HealthMonitor {
   // check that is now off becomes Healthy).
   void set_disabled_checks(int mask);
   uint64_t events_seen() const { return events_seen_; }
+  // Latches to persist: every GPU whose uncorrectable-ECC latch is set (identity order).
+  std::vector<HealthLatch> latches() const;
+  // Re-applies latches a previous process persisted (same host boot): each GPU is held
+  // Unhealthy as before, with the UE baseline it had, until a reset is seen.  A GPU whose
+  // firmware is found to have started after the recorded time was reset meanwhile: its
+  // first sample clears the latch.  Call before the first attach_tables.
+  void restore_latches(const std::vector<HealthLatch>& latches);
+  // Resets observed by polling (firmware clock restarts, outages on clockless GPUs).
+  uint64_t resets_observed() const;
 
  private:
   struct GpuState {
@@ -137,6 +161,17 @@ class HealthMonitor {
     int failures = 0;
     int64_t last_ue = -1;
     bool reported_healthy = true;
+    bool restored = false;        // a latch restored from a previous process is set
+    std::string ecc_reason;       // what set the ECC latch (persisted with it)
+    int64_t ecc_since_ns = 0;
+    // firmware clock tracking (GpuSample::fw_clock_s): last reading, the boot-time second
+    // it was read at, whether the clock was seen advancing at about one second per
+    // second, and the boot-time second the firmware started at (-1 unknown)
+    double fw_clock = -1;
+    double fw_read_at = -1;
+    bool fw_advancing = false;
+    double fw_boot = -1;
+    double restored_fw_boot = -1;  // from a previous process; checked by the first sample
     std::map<std::string, int> link_up;  // peer key -> 1/0
     std::map<std::string, double> link_bw;  // peer key -> trained bandwidth as this end last saw it
     int page_threshold = 0;
@@ -175,6 +210,10 @@ class HealthMonitor {
   std::atomic<bool> running_{false};
   bool stop_ = false;
   uint64_t events_seen_ = 0;
+  uint64_t resets_observed_ = 0;
 };
+
+// CLOCK_BOOTTIME in seconds (monotonic across the host's uptime, suspend included).
+double boottime_s();
 
 }  // namespace amdgpu_dp

@@ -84,6 +84,7 @@ def main() -> int:
     from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import DevicePluginClient
 
     n = native.load()
+    native.load_bench()  # the harness extension: load generators, H2Client.bench_unary
     workdir = tempfile.mkdtemp(prefix="concprobe-", dir="/tmp")
     over = {"grpc": {"threads": max(4, kmax)}, "http": {"threads": max(4, 2 * kmax)}}
     proc, kubelet, port, reg, backend = bench.start_daemon(1, "native", workdir, overrides=over, backend=a.backend)
@@ -100,7 +101,7 @@ def main() -> int:
             v1beta1.ContainerAllocateRequest(devices_ids=ids[:1])]).SerializeToString()
         for k in ks:
             al = allocate_round(n, sock, req, v1beta1.METHOD_ALLOCATE, k, a.batches, a.per_batch)
-            sc = n.http_load("127.0.0.1", port, "/metrics", 2 * k, a.scrape_s, 0.0)
+            sc = native.load_bench().http_load("127.0.0.1", port, "/metrics", 2 * k, a.scrape_s, 0.0)
             if sc["errors"]:
                 raise RuntimeError("%d scrape errors at k=%d" % (sc["errors"], k))
             sl = sc["latencies_s"]

@@ -194,6 +194,7 @@ def main() -> int:
     from k8s_gpu_device_plugin_amd import native
 
     n = native.load()
+    native.load_bench()  # the harness extension: load generators, H2Client.bench_unary
     ab = [int(x) for x in a.ab_keep_warm.split(",")] if a.ab_keep_warm else None
     arms = None  # (name, overrides) per arm
     if a.ab_overrides:
@@ -215,7 +216,7 @@ def main() -> int:
         res["keep_warm_ms"] = ab if ab else a.keep_warm_ms
         res["arms"] = dict(arms) if arms else None
         sizes = (9 + 80 + 9 + 5 + len(first.alloc), 9 + 20 + 9 + 5 + first.resp_len + 9 + 16)
-        pinger = n.UdsPinger(*sizes, server_timeout_ms=100)
+        pinger = native.load_bench().UdsPinger(*sizes, server_timeout_ms=100)
         for _ in range(200):
             pinger.once()
         # kinds: <rpc><daemon tag>, and the floor

@@ -23,7 +23,7 @@ def floor_parallel(n, pairs, body):
     res = [None] * pairs
 
     def run(i):
-        res[i] = n.uds_pingpong(3000, 300, 90, body, server_spin=True, tcp=True)
+        res[i] = native.load_bench().uds_pingpong(3000, 300, 90, body, server_spin=True, tcp=True)
     ts = [threading.Thread(target=run, args=(i,)) for i in range(pairs)]
     for t in ts:
         t.start()
@@ -34,6 +34,7 @@ def floor_parallel(n, pairs, body):
 
 def main():
     n = native.load()
+    native.load_bench()  # the harness extension: load generators, H2Client.bench_unary
     out = {}
     for threads in (2, 4):
         d = tempfile.mkdtemp()
@@ -49,13 +50,13 @@ def main():
         time.sleep(0.3)
         try:
             if threads == 4:  # user-space cost of one exposition, 1/2/4 threads at once, no sockets
-                n.http_load("127.0.0.1", port, "/metrics", 1, 0.2, 0.0)  # populate the echo_http_* families
+                native.load_bench().http_load("127.0.0.1", port, "/metrics", 1, 0.2, 0.0)  # populate the echo_http_* families
                 for nt in (1, 2, 4):
-                    out["render_ns_threads%d" % nt] = [round(x) for x in n.render_bench(m.exporter, w._impl, nt, 20000)]
+                    out["render_ns_threads%d" % nt] = [round(x) for x in native.load_bench().render_bench(m.exporter, w._impl, nt, 20000)]
             for conns in (1, 2, 4):
                 rows = []
                 for _ in range(3):
-                    r = n.http_load("127.0.0.1", port, "/metrics", conns, 1.0, 0.0)
+                    r = native.load_bench().http_load("127.0.0.1", port, "/metrics", conns, 1.0, 0.0)
                     rows.append((r["ok"] / r["elapsed_s"], pct(r["latencies_s"], 0.5) * 1e6, r["bytes"] // max(1, r["ok"])))
                 out["threads%d_conns%d" % (threads, conns)] = {"rps": [round(x[0]) for x in rows],
                                                               "p50_us": [round(x[1], 2) for x in rows],

@@ -26,6 +26,7 @@ def main() -> int:
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     n = native.load()
+    native.load_bench()  # the harness extension: load generators, H2Client.bench_unary
     d = tempfile.mkdtemp(prefix="scrapeprof-")
     cfg = config_mod.validate(config_mod.from_dict({
         "backend": "fixture", "fixture": "1gpu_spx", "pluginDir": d, "log": {"fileDir": ""},
@@ -38,9 +39,9 @@ def main() -> int:
     port = w.start()
     try:
         time.sleep(0.3)
-        n.http_load("127.0.0.1", port, "/metrics", a.conns, 0.5, 0.0)  # warm up
+        native.load_bench().http_load("127.0.0.1", port, "/metrics", a.conns, 0.5, 0.0)  # warm up
         n.prof_start(4999)
-        r = n.http_load("127.0.0.1", port, "/metrics", a.conns, a.seconds, 0.0)
+        r = native.load_bench().http_load("127.0.0.1", port, "/metrics", a.conns, a.seconds, 0.0)
         n.prof_stop()
         agg = collections.Counter()
         for mod, off, sym, cnt in n.prof_histogram():

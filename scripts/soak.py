@@ -1,15 +1,17 @@
 """Soak test of the daemon on the real backend: kubelet-like Allocate traffic, /metrics
 scrapes and frequent GET /restart reloads at once, with fast telemetry sampling, for a
-fixed time.  Checks that the daemon stays up, keeps answering, re-registers after every
-reload and does not grow (RSS sampled every few seconds).  Prints one JSON line.
+fixed time.  Checks that the daemon stays up, keeps answering and does not grow (RSS
+sampled every few seconds), and that reloads are hitless for kubelet: the Allocate
+connection never drops (``reconnects`` 0), the kubelet-like ListAndWatch stream opened at
+the start stays open through every reload (``law_reopens`` 1) and is sent each new device
+table (``law_updates``), and the plugin registers once.  Prints one JSON line.
 
     python scripts/soak.py --seconds 90 [--restart-every 0.25] [--backend auto|fixture]
                            [--fault-every 0.1]   # fixture: scripted GPU 1 resets
 
 With ``--fault-every`` (fixture backend) GPU 1 alternates PRE_RESET / POST_RESET on that
-period while a kubelet-like ListAndWatch watcher follows the stream (re-opened after each
-reload); the run checks that the watcher kept seeing updates and that GPU 1 ends in the
-state the last event left it in.
+period; the run checks that the watcher kept seeing updates and that both GPUs are still
+advertised at the end.
 """
 import argparse
 import http.client
@@ -56,6 +58,7 @@ def main():
     ap.add_argument("--fault-every", type=float, default=0.0)
     a = ap.parse_args()
     n = native.load()
+    native.load_bench()  # the harness extension: load generators, H2Client.bench_unary
     backend = a.backend if a.backend != "auto" else ("amdsmi" if n.amdsmi_available() else "fixture")
     work = tempfile.mkdtemp(prefix="dp-soak-")
     plugin_dir = os.path.join(work, "device-plugins")
@@ -116,14 +119,14 @@ def main():
                         stats["allocs"] += 1
                     else:
                         stats["alloc_errors"] += 1
-                except Exception:  # the plugin socket goes away during each reload
+                except Exception:  # the connection dropped (a reload must not do this)
                     stats["reconnects"] += 1
                     c = None
                     time.sleep(0.005)
 
         def scraper():
             while not stop.is_set():
-                r = n.http_load("127.0.0.1", port, "/metrics", 2, 0.2, 0.0)
+                r = native.load_bench().http_load("127.0.0.1", port, "/metrics", 2, 0.2, 0.0)
                 stats["scrapes"] += r["ok"]
                 stats["scrape_errors"] += r["errors"]
 
@@ -137,7 +140,7 @@ def main():
 
         last_law = {}
 
-        def watcher():  # kubelet's ListAndWatch: re-opened whenever a reload ends the stream
+        def watcher():  # kubelet's ListAndWatch: re-opened only if the stream ends
             c = None
             while not stop.is_set():
                 try:
@@ -155,7 +158,7 @@ def main():
                     c = None
                     time.sleep(0.005)
 
-        workers = [allocator, scraper, restarter] + ([watcher] if a.fault_every > 0 else [])
+        workers = [allocator, scraper, restarter, watcher]
         ts = [threading.Thread(target=f, daemon=True) for f in workers]
         for t in ts:
             t.start()
@@ -176,6 +179,12 @@ def main():
         stats["daemon_alive"] = proc.poll() is None
         stats["health_after"] = http_get(port, "/health")[0] if stats["daemon_alive"] else None
         stats["registrations"] = len(kubelet.requests)
+        if stats["daemon_alive"]:
+            import re
+            body = http_get(port, "/metrics")[1].decode()
+            for ev in ("reloads", "table_swaps", "restarts_coalesced"):
+                m = re.search(r'amdgpu_device_plugin_events_total\{event="%s"\} (\d+)' % ev, body)
+                stats[ev] = int(m.group(1)) if m else 0
         rs = stats["rss_kb"]
         half = rs[len(rs) // 2:] or rs
         stats["rss_growth_second_half_kb"] = (max(half) - min(half)) if half else None
@@ -195,10 +204,13 @@ def main():
                            and (stats["fd_growth_second_half"] or 0) <= 8
                            and (stats["thread_growth_second_half"] or 0) <= 8
                            and stats["scrapes"] > 0 and stats["restarts"] > 0 and stats["alloc_errors"] == 0
-                           and stats["scrape_errors"] <= stats["restarts"] * 4)
+                           and stats["scrape_errors"] <= stats["restarts"] * 4
+                           # hitless reloads: one connection, one stream, one registration
+                           and stats["reconnects"] == 0 and stats["law_reopens"] == 1
+                           and stats["registrations"] == 1 and stats["law_updates"] > 1)
+        stats["law_last"] = last_law.get("devices")
         if a.fault_every > 0:
             # both GPUs still advertised; the stream kept moving (faults + reloads)
-            stats["law_last"] = last_law.get("devices")
             stats["ok"] = stats["ok"] and stats["law_updates"] > a.seconds / a.fault_every / 4 and \
                 len(last_law.get("devices", {})) == 2
     finally:

@@ -71,6 +71,7 @@ def run_variant(name, batches, overrides=None, pin=False, gap=True, idle_gap_s=0
     from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import DevicePluginClient
 
     n = native.load()
+    native.load_bench()  # the harness extension: load generators, H2Client.bench_unary
     workdir = tempfile.mkdtemp(prefix="tailprobe-", dir="/tmp")
     proc, kubelet, port, reg, backend = bench.start_daemon(1, "native", workdir, overrides=overrides)
     try:
@@ -94,7 +95,7 @@ def run_variant(name, batches, overrides=None, pin=False, gap=True, idle_gap_s=0
                 if idle_gap_s:
                     time.sleep(idle_gap_s)
                 elif gap:
-                    n.http_load("127.0.0.1", port, "/metrics", bench.SCRAPE_CONNS, bench.SCRAPE_S, 0.0)
+                    native.load_bench().http_load("127.0.0.1", port, "/metrics", bench.SCRAPE_CONNS, bench.SCRAPE_S, 0.0)
         finally:
             h2.close()
             if pin:
@@ -124,7 +125,7 @@ def main() -> int:
     from k8s_gpu_device_plugin_amd import native
     n = native.load()
     res = {"host_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)), "variants": []}
-    floor = n.uds_pingpong(a.batches * ALLOCS, 500, 140, 190, server_spin=True)
+    floor = native.load_bench().uds_pingpong(a.batches * ALLOCS, 500, 140, 190, server_spin=True)
     res["floor"] = {"p50_us": round(pct(floor, 0.5) * 1e6, 2), "p99_us": round(pct(floor, 0.99) * 1e6, 2),
                     "p999_us": round(pct(floor, 0.999) * 1e6, 2), "max_us": round(max(floor) * 1e6, 2),
                     "slow_fraction": round(sum(1 for x in floor if x > 2 * pct(floor, 0.5)) / len(floor), 4)}

@@ -436,4 +436,19 @@ std::vector<std::pair<int, double>> health_propagation(FixtureBackend& be, const
   return out;
 }
 
+std::vector<double> h2_bench_unary(const std::string& socket_path, const std::string& path, const std::string& req,
+                                   int n) {
+  H2Client c(socket_path);
+  std::vector<double> out;
+  out.reserve(static_cast<size_t>(n));
+  std::string resp, msg;
+  for (int i = 0; i < n; ++i) {
+    const int64_t t0 = mono_ns();
+    const int st = c.unary(path, req, &resp, &msg);
+    out.push_back((mono_ns() - t0) * 1e-9);
+    if (st != 0) throw std::runtime_error("h2_bench_unary: grpc-status " + std::to_string(st) + ": " + msg);
+  }
+  return out;
+}
+
 }  // namespace amdgpu_dp

@@ -79,4 +79,8 @@ class FixtureBackend;
 std::vector<std::pair<int, double>> health_propagation(FixtureBackend& be, const std::string& socket_path, int gpu,
                                                        int events);
 
+// n sequential unary calls on one connection; per-call latency in seconds.
+std::vector<double> h2_bench_unary(const std::string& socket_path, const std::string& path, const std::string& req,
+                                   int n);
+
 }  // namespace amdgpu_dp

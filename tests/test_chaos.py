@@ -67,6 +67,7 @@ class _Allocator(threading.Thread):
     def run(self):
         from k8s_gpu_device_plugin_amd.api import v1beta1
         n = native.load()
+        native.load_bench()  # H2Client.bench_unary
         c = None
         i = 0
         while not self.stop_ev.is_set():

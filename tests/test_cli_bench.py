@@ -62,8 +62,17 @@ def test_daemon_serves_and_exits_gracefully(plugin_dir, tmp_path, sig):
             c.request("GET", "/health")
             assert c.getresponse().read() == b'{"code":0,"data":"ok","msg":"success"}\n'
             c.request("GET", "/restart")
-            assert c.getresponse().status == 200
-            k.wait_for_registrations(2, timeout=30)
+            r = c.getresponse()
+            assert r.status == 200 and r.read()
+            deadline = time.monotonic() + 30  # the reload swaps the table in (no new registration)
+            while time.monotonic() < deadline:
+                c.request("GET", "/metrics")
+                if 'amdgpu_device_plugin_events_total{event="table_swaps"} 1' in c.getresponse().read().decode():
+                    break
+                time.sleep(0.1)
+            else:
+                raise AssertionError("/restart did not reload")
+            assert len(k.requests) == 1
             time.sleep(0.2)
             p.send_signal(sig)
             rc = p.wait(30)

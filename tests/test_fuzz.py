@@ -1,5 +1,5 @@
 """libFuzzer + ASan + UBSan smoke runs of every peer-facing native parser
-(native/fuzz/*.cpp): kubelet protobuf decoding with the allocator contract, HPACK,
+(tests/native/fuzz/*.cpp): kubelet protobuf decoding with the allocator contract, HPACK,
 the HTTP/2 gRPC server and the HTTP/1.1 ops server.  The reference never fuzzed its
 (Go) parsers; ours are hand-written C++, so each target runs a few seconds per test
 run and longer on demand: ``python -m k8s_gpu_device_plugin_amd._build --fuzz``."""

@@ -134,9 +134,13 @@ def test_prestart_failure_survives_a_reload(make_cfg, plugin_dir, fake_canary):
         deadline = time.monotonic() + 5
         while m.counters.get("prestart_failures") != 1 and time.monotonic() < deadline:
             time.sleep(0.01)
+        reloads = m.counters["reloads"]
         m.restart()
-        reg2 = k.wait_for_registrations(2)[1]
-        _, devs = k.watch(reg2.endpoint).next(timeout=5)
+        deadline = time.monotonic() + 10
+        while m.counters["reloads"] == reloads and time.monotonic() < deadline:
+            time.sleep(0.01)
+        assert m.counters["reloads"] > reloads and len(k.requests) == 1  # the table was swapped in
+        _, devs = k.watch(reg.endpoint).next(timeout=5)
         health = dict((d, h) for d, h, _ in devs)
         assert health[ids[5]] == "Unhealthy"
         assert [h for d, h in health.items() if d != ids[5]] == ["Healthy"] * (len(ids) - 1)

@@ -23,10 +23,12 @@ SUITES = {
     "address": ["tests/test_grpc_native.py", "tests/test_plugin_e2e.py", "tests/test_manager.py",
                 "tests/test_http.py", "tests/test_telemetry_health.py", "tests/test_prestart.py",
                 "tests/test_allocator.py", "tests/test_v1beta1_wire.py", "tests/test_device_subset.py",
-                "tests/test_checkpoint_resume.py", "tests/test_chaos.py", "tests/test_wedged_gpu.py"],
+                "tests/test_checkpoint_resume.py", "tests/test_chaos.py", "tests/test_wedged_gpu.py",
+                "tests/test_health_latches.py", "tests/test_canary_scope.py"],
     "thread": ["tests/test_grpc_native.py", "tests/test_plugin_e2e.py", "tests/test_manager.py",
                "tests/test_http.py", "tests/test_telemetry_health.py", "tests/test_prestart.py",
-               "tests/test_chaos.py", "tests/test_wedged_gpu.py"],
+               "tests/test_chaos.py", "tests/test_wedged_gpu.py", "tests/test_health_latches.py",
+               "tests/test_canary_scope.py"],
 }
 
 

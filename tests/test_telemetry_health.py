@@ -7,6 +7,7 @@ from hypothesis import given, settings, strategies as st
 
 from prometheus_client.parser import text_string_to_metric_families
 
+from k8s_gpu_device_plugin_amd import native
 from k8s_gpu_device_plugin_amd.models import fixtures
 
 
@@ -338,7 +339,7 @@ def test_native_sampling_profiler_sees_native_threads(n):
     assert not n.prof_start(2000)  # one profile at a time
     t0 = time.monotonic()
     while time.monotonic() - t0 < 0.6:
-        n.uds_pingpong(2000, 0, 128, 256)  # client + epoll server threads, no GIL
+        native.load_bench().uds_pingpong(2000, 0, 128, 256)  # client + epoll server threads, no GIL
     n.prof_stop()
     n.prof_stop()
     assert not n.prof_running()
