@@ -95,37 +95,124 @@ def _wait_http(port: int, timeout: float) -> None:
     raise TimeoutError("plugin web server did not come up on port %d" % port)
 
 
-def _tail_stats(batches) -> dict:
-    """Attribution of this rank's slow Allocates (> 2x the rank's p50): the first call of
-    a batch (it follows the previous step's scrape phase, so it meets a server worker
-    whose busy-poll window has closed), a call that ran on another CPU than the call
-    before it (the client thread migrated), or neither (an interrupt, timer tick or
-    another tenant's thread on the client's or the server's CPU)."""
-    lat = [x for _, l, _ in batches for x in l]
+TRACE_DTYPE = [("t_ready", "<i8"), ("t_dispatch", "<i8"), ("t_sent", "<i8"), ("conn", "<u8"), ("seq", "<u4"),
+               ("method", "u1"), ("spinning", "u1"), ("cpu", "<u2")]  # native/grpc_h2.h CallTraceEntry
+
+
+def read_call_trace(path: str):
+    """The daemon's per-call trace ring (grpc.callTraceFile), as a numpy record array of
+    the records written so far (None when absent or malformed)."""
+    import numpy as np
+    try:
+        raw = open(path, "rb").read()
+    except OSError:
+        return None
+    if len(raw) < 64 or int.from_bytes(raw[:8], "little") != 0x5452434c4c414344:
+        return None
+    cap = int.from_bytes(raw[12:16], "little")
+    recs = np.frombuffer(raw, dtype=np.dtype(TRACE_DTYPE), count=cap, offset=64)
+    return recs[recs["seq"] > 0]
+
+
+def _tail_stats(batches, trace=None, rpc_allocate: int = 3) -> dict:
+    """Attribution of this rank's slow Allocates (> 2x the rank's p50), call by call.
+
+    Client-side evidence for every call: the first call of a batch (it follows the
+    previous step's scrape phase, so it meets a server worker whose busy-poll window has
+    closed), a call that ran on another CPU than the call before it (the client thread
+    migrated), and the client thread's involuntary context switches during the call
+    (preempted).  With the daemon's call trace (grpc.callTraceFile) each call is matched
+    to the server's record of it and split into inbound (client send -> the worker's
+    epoll_wait returning with it), server (-> response sent) and outbound (-> the client
+    has the answer); a slow call is put on the segment with the largest excess over that
+    segment's median, inbound split by whether the worker was polling or asleep.  What
+    has no evidence at all is "other"."""
+    import collections
+
+    import numpy as np
+    lat = [x for b in batches for x in b[1]]
     if not lat:
         return {"calls": 0}
     thr = 2 * _pct(lat, 0.5)
-    slow = first = migrated = 0
-    for starts, l, cpus in batches:
-        for i, x in enumerate(l):
-            if x <= thr:
-                continue
-            slow += 1
-            if i == 0:
-                first += 1
-            elif cpus[i] != cpus[i - 1]:
-                migrated += 1
-    return {"calls": len(lat), "slow": slow, "first_of_batch": first, "cpu_migrated": migrated,
-            "threshold_us": round(thr * 1e6, 2)}
+    calls = []  # (start ns, latency s, client cpu, preempted, first, migrated)
+    for b in batches:
+        starts, lats, cpus = b[0], b[1], b[2]
+        pre = b[3] if len(b) > 3 else [0] * len(lats)
+        for i, x in enumerate(lats):
+            calls.append((int(starts[i]), x, cpus[i], pre[i], i == 0, i > 0 and cpus[i] != cpus[i - 1]))
+    out = {"calls": len(calls), "slow": 0, "first_of_batch": 0, "cpu_migrated": 0, "client_preempted": 0,
+           "threshold_us": round(thr * 1e6, 2)}
+    matched = [None] * len(calls)
+    seg_med = None
+    if trace is not None and len(trace):
+        a = trace[(trace["method"] == rpc_allocate) & (trace["t_sent"] > 0)]
+        a = a[np.argsort(a["t_dispatch"], kind="stable")]
+        td = a["t_dispatch"]
+        ranges = []
+        for s, x, *_ in calls:
+            ranges.append((int(np.searchsorted(td, s, "left")), int(np.searchsorted(td, s + int(x * 1e9), "right"))))
+        votes = collections.Counter(int(a["conn"][i0]) for i0, i1 in ranges if i1 - i0 == 1)
+        if votes:
+            mine = votes.most_common(1)[0][0]  # this client's connection
+            for k, (i0, i1) in enumerate(ranges):
+                for j in range(i0, i1):
+                    if int(a["conn"][j]) == mine:
+                        matched[k] = a[j]
+                        break
+        segs = [(int(e["t_ready"]) - c[0], int(e["t_sent"]) - int(e["t_ready"]), c[0] + int(c[1] * 1e9) - int(e["t_sent"]))
+                for c, e in zip(calls, matched) if e is not None]
+        if segs:
+            seg_med = [float(np.median([sg[i] for sg in segs])) for i in range(3)]
+            out["matched"] = len(segs)
+            out["segment_p50_us"] = {"inbound": round(seg_med[0] / 1e3, 2), "server": round(seg_med[1] / 1e3, 2),
+                                     "outbound": round(seg_med[2] / 1e3, 2)}
+    causes = collections.Counter()
+    excess = collections.defaultdict(list)
+    same_cpu = 0
+    for c, e in zip(calls, matched):
+        s, x, cpu, pre, first, migrated = c
+        if x <= thr:
+            continue
+        out["slow"] += 1
+        out["first_of_batch"] += int(first)
+        out["cpu_migrated"] += int(migrated)
+        out["client_preempted"] += int(pre > 0)
+        if e is None or seg_med is None:
+            cause = "client_preempted" if pre > 0 else ("first_of_batch" if first else
+                                                        "cpu_migrated" if migrated else "other")
+        else:
+            if int(e["cpu"]) == cpu:
+                same_cpu += 1
+            seg = (int(e["t_ready"]) - s, int(e["t_sent"]) - int(e["t_ready"]), s + int(x * 1e9) - int(e["t_sent"]))
+            ex = [seg[i] - seg_med[i] for i in range(3)]
+            k = int(np.argmax(ex))
+            cause = (("inbound_worker_polling" if e["spinning"] else "inbound_worker_asleep"), "server_handling",
+                     "outbound_client_wakeup")[k]
+            if pre > 0 and k != 1:
+                cause = "client_preempted"
+            excess[cause].append(ex[k])
+        causes[cause] += 1
+    out["by_cause"] = dict(sorted(causes.items()))
+    out["cause_mean_excess_us"] = {k: round(sum(v) / len(v) / 1e3, 2) for k, v in sorted(excess.items())}
+    out["same_cpu_as_worker"] = same_cpu
+    return out
 
 
 def _merge_tail(parts) -> dict:
-    out = {"calls": 0, "slow": 0, "first_of_batch": 0, "cpu_migrated": 0}
+    import collections
+    out = {"calls": 0, "slow": 0, "first_of_batch": 0, "cpu_migrated": 0, "client_preempted": 0, "matched": 0,
+           "same_cpu_as_worker": 0}
+    causes = collections.Counter()
     for p in parts:
         for k in out:
             out[k] += p.get(k, 0)
-    out["other"] = out["slow"] - out["first_of_batch"] - out["cpu_migrated"]
+        causes.update(p.get("by_cause", {}))
+    out["by_cause"] = dict(sorted(causes.items()))
+    out["other"] = causes.get("other", 0)  # slow calls with no evidence at all
     out["slow_fraction"] = round(out["slow"] / max(1, out["calls"]), 4)
+    if parts and parts[0].get("segment_p50_us"):
+        out["segment_p50_us"] = parts[0]["segment_p50_us"]
+        out["cause_mean_excess_us"] = parts[0].get("cause_mean_excess_us")
     return out
 
 
@@ -230,7 +317,9 @@ def start_daemon(n_gpus: int, grpc_server: str, workdir: str, profile_dir: str =
            "log": {"level": "info", "fileDir": ""},
            "http": {"accessLog": False, "threads": max(4, SCRAPE_CONNS * n_gpus)},
            "telemetry": {"intervalMs": 1000},
-           "grpc": {"server": grpc_server, "threads": max(4, 2 * n_gpus)}}
+           "grpc": {"server": grpc_server, "threads": max(4, 2 * n_gpus),
+                    # per-call server records: the tail attribution reads them (allocate_tail)
+                    "callTraceFile": os.path.join(workdir, "calltrace-{resource}.bin"), "callTraceEntries": 1 << 18}}
     if busy_poll_us is not None:
         cfg["http"]["busyPollUs"] = cfg["grpc"]["busyPollUs"] = busy_poll_us
     if admission_poll_us is not None:
@@ -390,9 +479,9 @@ def main() -> int:
     def step(rec):
         a, p, s, an, pn, tl = rec
         phase_sync()
-        starts, lat, cpus = h2.bench_unary_ts(v1beta1.METHOD_ALLOCATE, alloc_req, ALLOCS)
+        starts, lat, cpus, pre = h2.bench_unary_ts(v1beta1.METHOD_ALLOCATE, alloc_req, ALLOCS)
         an.extend(lat)
-        tl.append((starts, lat, cpus))
+        tl.append((starts, lat, cpus, pre))
         pn.extend(h2.bench_unary(v1beta1.METHOD_GET_PREFERRED, pref_req, PREFS))
         for _ in range(ALLOCS):
             t0 = perf()
@@ -421,8 +510,10 @@ def main() -> int:
         scrape_time += st
     barrier()
     elapsed = perf() - t_start
+    # the daemon's record of every call so far (untimed): the tail attribution matches them
+    trace = read_call_trace(os.path.join(workdir, "calltrace-%s.bin" % info["resource"].split("/")[-1]))
     mine = {"elapsed": elapsed, "scrape_time": scrape_time, "alloc": rec[0], "pref": rec[1], "scrape": rec[2],
-            "alloc_native": rec[3], "pref_native": rec[4], "alloc_tail": _tail_stats(rec[5]),
+            "alloc_native": rec[3], "pref_native": rec[4], "alloc_tail": _tail_stats(rec[5], trace, n.RPC_ALLOCATE),
             "canary": canary_res, "body": body_len,
             "device": {"rank": rank, "local_rank": local_rank, "device_id": my_id, "hip_ids": my_hips,
                        "mapped_by": mapped_by}}

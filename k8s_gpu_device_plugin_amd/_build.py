@@ -167,7 +167,8 @@ def build_bench(force: bool = False, jobs: int | None = None, verbose: bool = Tr
     py_flags = flags + ["-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"], "-fvisibility=hidden"]
     objs, changed = _compile_objects(BENCH_SOURCES, os.path.join(BUILD_DIR, "obj_bench"), py_flags, force, jobs,
                                      src_dir=HARNESS_DIR)
-    if force or core_changed or changed or not os.path.exists(out):
+    # the core objects are shared with _native: build_native may have refreshed them first
+    if force or core_changed or changed or _stale(out, core_objs + objs):
         tmp = out + ".tmp"
         _run([_cxx(), "-shared", "-o", tmp] + objs + core_objs + _link_libs(), "link _native_bench")
         os.replace(tmp, out)

@@ -44,6 +44,18 @@ def build_spec(kind: str, devices, kfd_path: str = "/dev/kfd") -> dict:
             "devices": uniq}
 
 
+# The device plugin's own access to /dev/kfd (deploy/kfd-cdi-patch.yaml): the pod names
+# PLUGIN_KFD_DEVICE in a cdi.k8s.io/ annotation and the runtime adds the node and its
+# device-cgroup rule, no privileged container needed.
+PLUGIN_KIND = "amd.com/device-plugin"
+PLUGIN_KFD_DEVICE = PLUGIN_KIND + "=kfd"
+
+
+def plugin_kfd_spec(kfd_path: str = "/dev/kfd") -> dict:
+    return {"cdiVersion": CDI_VERSION, "kind": PLUGIN_KIND,
+            "devices": [{"name": "kfd", "containerEdits": {"deviceNodes": [_node(kfd_path)]}}]}
+
+
 def spec_path(spec_dir: str, kind: str) -> str:
     return os.path.join(spec_dir, kind.replace("/", "-") + ".json")
 

@@ -138,6 +138,10 @@ class GrpcConfig:
     admissionPollUs: int = 1000  # ... and this long after a GetPreferredAllocation (its Allocate follows)
     keepWarmMs: int = 10         # native server: idle workers with a connection replay canned requests (0 = off)
     keepWarmFull: bool = True    # ... through the whole request path of an in-memory connection (else HPACK + table)
+    # native server: per-call trace of unary RPCs in a file-backed ring ("" = off), read by
+    # bench.py to attribute slow calls; one record per call, callTraceEntries records
+    callTraceFile: str = ""
+    callTraceEntries: int = 65536
 
 
 @dataclass

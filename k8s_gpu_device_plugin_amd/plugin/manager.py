@@ -170,6 +170,8 @@ class PluginManager:
         # so a GPU that drops off the bus does not shift the others into the selection
         self._seen_bdfs: dict[str, str] = {}  # bdf -> identity
         self._selection: tuple | None = None
+        self._pinned_index: dict[int, str] = {}  # `devices` index -> identity it was first resolved to
+        self._index_conflicts: set[tuple[int, str]] = set()
         self._hip_fallback_logged = False
         self.device_map = None
         self._discoverer: Discoverer | None = None
@@ -265,9 +267,12 @@ class PluginManager:
         inflight = self._discoverer.inflight_s() if self._discoverer is not None else None
         if inflight is not None and inflight > bound + 1.0:
             return False, "discovery stalled: running for %.0f s%s" % (inflight, self._stuck_lanes_text())
-        if self._stale:
-            idx, key, why = self._stale[0]
-            more = " (and %d more GPU(s))" % (len(self._stale) - 1) if len(self._stale) > 1 else ""
+        # a wedged GPU that `devices` leaves out is not this plugin's to wait for (ADVICE
+        # r4): it is logged, but readiness (and so rolling updates) does not hang on it
+        stale = [s for s in self._stale if self._serves(s[1])]
+        if stale:
+            idx, key, why = stale[0]
+            more = " (and %d more GPU(s))" % (len(stale) - 1) if len(stale) > 1 else ""
             where = "GPU %d" % idx if idx >= 0 else "a GPU"
             return False, "discovery stalled on %s (%s): %s%s; %s" % (
                 where, key, why, more, "advertising its last known description" if idx >= 0 else "not advertised")
@@ -281,6 +286,11 @@ class PluginManager:
         if missing:
             return False, "not registered with kubelet: %s" % ", ".join(missing)
         return True, ""
+
+    def _serves(self, key: str) -> bool:
+        """Whether the GPU with this identity is (or, before the first load, may be) in
+        what this plugin advertises."""
+        return parse_device_selector(self.cfg.devices) is None or not self._key_of or key in self._key_of.values()
 
     def _stuck_lanes_text(self) -> str:
         try:
@@ -407,7 +417,8 @@ class PluginManager:
         if not snap:
             return
         n = native.load()
-        latches = [n.HealthLatch(k, e["last_ue"], e["fw_boot_s"], e["reason"], e["since_ns"])
+        latches = [n.HealthLatch(k, e["last_ue"], float("nan") if e["fw_boot_s"] is None else e["fw_boot_s"],
+                                 e["reason"], e["since_ns"])
                    for k, e in sorted(snap["ecc"].items())]
         if latches:
             self.monitor.restore_latches(latches)
@@ -427,7 +438,8 @@ class PluginManager:
     def _state_snapshot(self) -> dict:
         ecc = {}
         for l in self.monitor.latches():
-            ecc[l.key] = {"last_ue": int(l.last_ue), "fw_boot_s": round(float(l.fw_boot_s)),
+            fw = float(l.fw_boot_s)  # NaN: the firmware clock was never seen advancing
+            ecc[l.key] = {"last_ue": int(l.last_ue), "fw_boot_s": None if fw != fw else round(fw),
                           "reason": l.reason, "since_ns": int(l.since_ns)}
         failed: dict = {}
         for k, part in self._canary_failed:
@@ -772,11 +784,14 @@ class PluginManager:
 
     def _selected(self, gpus) -> list:
         """The GPUs `devices` selects.  An index names a GPU by its BDF rank among every
-        GPU this process has seen, not by its position in one enumeration: when a GPU
-        drops off the bus the others keep their index (the selection does not take in
-        the next GPU), and a GPU missing from the first discovery takes its own index when
-        it appears instead of leaving its index to a neighbour for good.  UUIDs and BDFs
-        are matched as given, and ``hip:<n>`` selects the GPU a HIP ordinal opens."""
+        GPU this process has seen, not by its position in one enumeration, and once an
+        index has been advertised it stays pinned to that GPU's identity: a
+        GPU that drops off the bus leaves its index empty (the selection does not take in
+        the next GPU), and one that appears later with a lower BDF does not push a served
+        GPU - which pods may hold - out of the selection; it is logged and counted
+        (``devices_index_conflicts``) instead.  Indices never resolved are filled as GPUs
+        appear.  UUIDs and BDFs are matched as given, and ``hip:<n>`` selects the GPU a
+        HIP ordinal opens."""
         sel = parse_device_selector(self.cfg.devices)
         if sel is None:
             return list(gpus)
@@ -790,7 +805,29 @@ class PluginManager:
                 self._hip_fallback_logged = True
             indices = sorted(set(indices) | hips)
         rank = {bdf: i for i, bdf in enumerate(sorted(self._seen_bdfs))}
-        out = [g for g in gpus if rank.get((g.bdf or "").lower(), -1) in indices
+        by_key = {self._identity(g): g for g in gpus}
+        picked = set()
+        for i in sorted(indices):
+            at_rank = [g for g in gpus if rank.get((g.bdf or "").lower(), -1) == i]
+            pinned = self._pinned_index.get(i)
+            if pinned is not None:
+                if pinned in by_key:
+                    picked.add(pinned)
+                if at_rank and self._identity(at_rank[0]) != pinned:
+                    moved = (i, self._identity(at_rank[0]))
+                    if moved not in self._index_conflicts:
+                        self._index_conflicts.add(moved)
+                        self.counters["devices_index_conflicts"] = self.counters.get("devices_index_conflicts", 0) + 1
+                        log.warning("devices %r: index %d is pinned to %s, which this process advertised; %s now "
+                                    "ranks %d by BDF and is not selected (restart the plugin to re-resolve indices)",
+                                    self.cfg.devices, i, pinned, moved[1], i)
+                continue
+            if at_rank:
+                k = self._identity(at_rank[0])
+                if k not in self._pinned_index.values():
+                    self._pinned_index[i] = k
+                    picked.add(k)
+        out = [g for g in gpus if self._identity(g) in picked
                or (g.uuid or "").lower() in names or (g.bdf or "").lower() in names
                or any(p.hip_id >= 0 and "hip:%d" % p.hip_id in names for p in g.partitions)]
         chosen = tuple(self._identity(g) for g in out)

@@ -45,7 +45,7 @@ def read_boot_id(path: str | None = None) -> str:
 class HealthState:
     """Reader/writer of the state file.  ``snapshot`` dicts look like::
 
-        {"ecc": {key: {"last_ue": int, "fw_boot_s": float, "reason": str, "since_ns": int}},
+        {"ecc": {key: {"last_ue": int, "fw_boot_s": float | None, "reason": str, "since_ns": int}},
          "canary_failed": {key: [partition, ...]},   # -1 = the whole GPU
          "held": [key, ...]}                          # recovery canary pending or failed
     """
@@ -80,8 +80,9 @@ class HealthState:
                 continue
             ecc = g.get("ecc")
             if isinstance(ecc, dict):
+                fw = ecc.get("fw_boot_s")
                 snap["ecc"][str(key)] = {"last_ue": int(ecc.get("last_ue", -1)),
-                                         "fw_boot_s": float(ecc.get("fw_boot_s", -1.0)),
+                                         "fw_boot_s": None if fw is None else float(fw),
                                          "reason": str(ecc.get("reason", "")),
                                          "since_ns": int(ecc.get("since_ns", 0))}
             parts = g.get("canary_failed_partitions")

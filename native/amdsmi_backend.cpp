@@ -600,51 +600,55 @@ class AmdSmiBackend : public Backend {
         }
   }
 
-  // Arms event notification on every processor, each on its GPU's lane (a wedged GPU's
-  // lane refuses; it is armed at the next discovery).
+  // Arms event notification on every processor, each on its GPU's lane.  Every handle a
+  // job arms is recorded in armed_handles_ by the job itself, under arm_mu_:
+  // one that finishes after the wait below still gets disarmed.  armed_for_ lists only
+  // the processors whose job ran (armed, or refused by the driver - an unprivileged pod):
+  // a GPU whose lane was wedged, or whose job missed the deadline, is armed again at the
+  // next discovery instead of never.
   void arm_on_lanes(const std::shared_ptr<const Inventory>& inv) {
     if (closed_.load()) return;
     const uint64_t mask = AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_GPU_PRE_RESET) |
                           AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_GPU_POST_RESET) |
                           AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_THERMAL_THROTTLE) |
                           AMDSMI_EVENT_MASK_FROM_INDEX(AMDSMI_EVT_NOTIF_VMFAULT);
-    std::vector<void*> flat;
-    std::vector<std::shared_ptr<std::vector<void*>>> armed;
     std::vector<std::shared_ptr<LaneJob>> jobs;
+    std::vector<std::vector<void*>> handles;
     const uint64_t batch = next_batch();  // posted to every lane at once
+    const uint64_t epoch = arm_epoch_.fetch_add(1) + 1;
     for (const auto& r : inv->refs) {
-      flat.insert(flat.end(), r.handles.begin(), r.handles.end());
-      auto out = std::make_shared<std::vector<void*>>();
-      armed.push_back(out);
       const std::vector<void*> hs = r.handles;
-      jobs.push_back(post_job(r.key, "arm", inv->session, [hs, mask, out] {
+      handles.push_back(hs);
+      jobs.push_back(post_job(r.key, "arm", inv->session, [this, hs, mask, epoch] {
         for (auto h : hs) {
           if (amdsmi_init_gpu_event_notification(h) != AMDSMI_STATUS_SUCCESS) continue;
           if (amdsmi_set_gpu_event_notification_mask(h, mask) != AMDSMI_STATUS_SUCCESS) {
             amdsmi_stop_gpu_event_notification(h);
             continue;
           }
-          out->push_back(h);
+          std::lock_guard<std::mutex> ak(arm_mu_);
+          armed_handles_.push_back(h);
+          armed_count_.store(static_cast<int>(armed_handles_.size()));
+          evt_live_.store(true);
+          if (arm_epoch_.load() != epoch) break;  // disarmed / re-armed meanwhile: stop here
         }
       }, batch));
     }
     const int64_t deadline = mono_ns() + static_cast<int64_t>(call_timeout_ms()) * 1000000;
-    std::vector<void*> live;
+    std::vector<void*> ran;
     for (size_t g = 0; g < jobs.size(); ++g) {
       if (!jobs[g] || !jobs[g]->wait(std::max<int64_t>(0, (deadline - mono_ns()) / 1000000)) || jobs[g]->dropped())
         continue;
-      live.insert(live.end(), armed[g]->begin(), armed[g]->end());
+      ran.insert(ran.end(), handles[g].begin(), handles[g].end());
     }
     std::lock_guard<std::mutex> ek(arm_mu_);
-    armed_handles_ = live;
-    armed_for_ = flat;
-    armed_count_.store(static_cast<int>(live.size()));
-    evt_live_.store(!live.empty());
+    armed_for_ = ran;
   }
 
   // evt_mu_ held, inside the session (or with the gate closed)
   void disarm_locked() {
     std::lock_guard<std::mutex> ak(arm_mu_);
+    arm_epoch_.fetch_add(1);  // an arm job still running stops after its current handle
     evt_live_.store(false);
     for (auto h : armed_handles_) amdsmi_stop_gpu_event_notification(h);
     armed_handles_.clear();
@@ -894,7 +898,8 @@ class AmdSmiBackend : public Backend {
   std::atomic<bool> arm_wanted_{false};
   std::atomic<int> armed_count_{0};
   std::vector<amdsmi_processor_handle> armed_handles_;
-  std::vector<void*> armed_for_;        // processor set at arming time
+  std::vector<void*> armed_for_;        // processors whose arm job ran (see arm_on_lanes)
+  std::atomic<uint64_t> arm_epoch_{0};  // bumped by every arming and disarming
   std::atomic<int> reinits_{0};
 };
 

@@ -33,9 +33,11 @@ int64_t Backend::last_completion_ns() const { return last_completion_ns_.load();
 
 std::shared_ptr<LaneJob> Backend::post_job(const std::string& key, const char* what, uint64_t session,
                                        std::function<void()> fn, uint64_t batch) {
-  // The closure keeps the backend alive (fn captures shared_from_this()), so the gate and
-  // the completion clock it touches outlive a caller that stopped waiting.
-  auto job = std::make_shared<LaneJob>(what, [this, session, fn = std::move(fn)] {
+  // The closure keeps the backend alive, so the gate and the completion clock it touches
+  // outlive a caller that stopped waiting - and a backend destroyed while a wedged call
+  // (a lane thread the destructor detached) is still inside the library.  A
+  // backend not owned by a shared_ptr (a stack object in a test) has no keep-alive.
+  auto job = std::make_shared<LaneJob>(what, [this, self = weak_from_this().lock(), session, fn = std::move(fn)] {
     if (!gate_.enter(session)) return;  // handles of an older session: never use them
     struct Leave {  // also when fn throws (LaneJob::run catches it): a call left inside
       SessionGate& g;  // the gate for good would defer every re-initialisation

@@ -549,7 +549,8 @@ PYBIND11_MODULE(_native, m) {
              l.since_ns = since_ns;
              return l;
            }),
-           py::arg("key"), py::arg("last_ue") = -1, py::arg("fw_boot_s") = -1.0, py::arg("reason") = "",
+           py::arg("key"), py::arg("last_ue") = -1,
+           py::arg("fw_boot_s") = std::numeric_limits<double>::quiet_NaN(), py::arg("reason") = "",
            py::arg("since_ns") = 0)
       .def_readwrite("key", &HealthLatch::key)
       .def_readwrite("ecc_bad", &HealthLatch::ecc_bad)
@@ -699,6 +700,7 @@ PYBIND11_MODULE(_native, m) {
            py::arg("busy_poll_us") = 0, py::arg("admission_poll_us") = 0)
       .def("set_table", &GrpcServer::set_table, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("table_swaps", &GrpcServer::table_swaps)
+      .def("set_call_trace", &GrpcServer::set_call_trace, py::arg("path"), py::arg("capacity") = 65536)
       .def("add_table", &GrpcServer::set_table)
       .def("start", &GrpcServer::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &GrpcServer::stop, py::call_guard<py::gil_scoped_release>())

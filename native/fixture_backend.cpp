@@ -72,7 +72,9 @@ void FixtureBackend::add_gpu(const GpuInfo& g) {
   pcie_.emplace_back(16, 32.0);
   pages_.emplace_back(0, 0);
   present_.push_back(true);
-  fw_start_ns_.push_back(1000000000LL);  // firmware up since one second after the host booted
+  // as on the MI355X box (profiles/r5/reset_signal_probe.json): the firmware started before
+  // the kernel did, ~180 s ahead of CLOCK_MONOTONIC zero
+  fw_start_ns_.push_back(-180000000000LL);
   fw_reported_.push_back(true);
   sample_fail_.push_back(false);
 }

@@ -7,6 +7,8 @@
 #include <fcntl.h>
 #include <poll.h>
 #include <pthread.h>
+#include <sched.h>
+#include <sys/mman.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
@@ -17,6 +19,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <new>
 #include <stdexcept>
 #include <unordered_map>
 
@@ -189,6 +192,7 @@ struct AsyncDone {
 };
 
 struct GrpcServer::Worker {
+  int index = 0;
   int ep = -1;
   int efd = -1;
   std::shared_ptr<AsyncDone> done = std::make_shared<AsyncDone>();
@@ -318,7 +322,33 @@ GrpcServer::GrpcServer(std::string socket_path, int threads, int busy_poll_us, i
       busy_poll_us_(std::max(0, std::min(busy_poll_us, 100000))),
       admission_poll_us_(std::max(0, std::min(admission_poll_us, 100000))) {}
 
-GrpcServer::~GrpcServer() { stop(); }
+GrpcServer::~GrpcServer() {
+  stop();
+  if (trace_hdr_) munmap(trace_hdr_, trace_bytes_);
+}
+
+void GrpcServer::set_call_trace(const std::string& path, int capacity) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (running_) throw std::runtime_error("set_call_trace: server already running");
+  if (capacity <= 0) throw std::invalid_argument("set_call_trace: capacity must be > 0");
+  const size_t bytes = sizeof(CallTraceHeader) + static_cast<size_t>(capacity) * sizeof(CallTraceEntry);
+  const int fd = ::open(path.c_str(), O_RDWR | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  if (fd < 0) throw std::runtime_error("set_call_trace: open " + path + ": " + strerror(errno));
+  if (ftruncate(fd, static_cast<off_t>(bytes)) != 0) {
+    const int e = errno;
+    ::close(fd);
+    throw std::runtime_error("set_call_trace: ftruncate: " + std::string(strerror(e)));
+  }
+  void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  ::close(fd);
+  if (p == MAP_FAILED) throw std::runtime_error("set_call_trace: mmap: " + std::string(strerror(errno)));
+  if (trace_hdr_) munmap(trace_hdr_, trace_bytes_);
+  trace_hdr_ = new (p) CallTraceHeader();
+  trace_hdr_->capacity = static_cast<uint32_t>(capacity);
+  trace_ = reinterpret_cast<CallTraceEntry*>(static_cast<char*>(p) + sizeof(CallTraceHeader));
+  trace_bytes_ = bytes;
+  trace_hdr_->magic = kCallTraceMagic;
+}
 
 void GrpcServer::set_table(std::shared_ptr<DeviceTable> t) {
   if (!t) throw std::invalid_argument("GrpcServer: null device table");
@@ -371,6 +401,7 @@ void GrpcServer::start() {
   const int n = std::max(1, nthreads_);
   for (int i = 0; i < n; ++i) {
     auto w = std::make_unique<Worker>();
+    w->index = i;
     w->ep = epoll_create1(EPOLL_CLOEXEC);
     w->efd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
     struct epoll_event ev {};
@@ -559,6 +590,19 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
   };
   std::string scratch;
   bool admitting = false;  // a GetPreferredAllocation was answered in this batch
+  // call trace (set_call_trace): when the events being handled were delivered, whether the
+  // worker was polling then, and the records of this batch still waiting for their send
+  int64_t wake_ts = 0;
+  bool wake_spin = false;
+  std::vector<uint64_t> trace_pending;
+  auto stamp_sent = [&] {
+    const int64_t t = mono_ns();
+    for (uint64_t idx : trace_pending) {
+      CallTraceEntry& e = trace_[idx % trace_hdr_->capacity];
+      if (e.seq == static_cast<uint32_t>(idx + 1)) e.t_sent = t;
+    }
+    trace_pending.clear();
+  };
   auto push_law = [&](Conn* c) {
     const uint64_t v = table->version();
     std::string payload;
@@ -586,6 +630,21 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
     const int64_t t0 = mono_ns();
     if (!c.internal) requests_.add();
     const Method m = static_cast<Method>(s.method);
+    if (trace_ && !c.internal && m != kMLaw && m != kMPreStart) {
+      const uint64_t idx = trace_hdr_->next.fetch_add(1, std::memory_order_relaxed);
+      CallTraceEntry& e = trace_[idx % trace_hdr_->capacity];
+      e.t_ready = wake_ts;
+      e.t_dispatch = t0;
+      e.t_sent = 0;
+      e.conn = (static_cast<uint64_t>(w->index) << 48) | (c.serial & 0xFFFFFFFFFFFFull);
+      e.method = static_cast<uint8_t>(m == kMAllocate ? kRpcAllocate : m == kMPreferred ? kRpcPreferred
+                                      : m == kMOptions ? kRpcOptions : 255);
+      e.spinning = wake_spin ? 1 : 0;
+      const int cpu = sched_getcpu();
+      e.cpu = static_cast<uint16_t>(cpu < 0 ? 0xFFFF : cpu);
+      e.seq = static_cast<uint32_t>(idx + 1);
+      trace_pending.push_back(idx);
+    }
     if (m == kMUnknown) {
       send_error(c, sid, s, 12, "unknown method " + s.path);  // UNIMPLEMENTED
       return;
@@ -1015,7 +1074,8 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
       if (inject_worker_fault_.compare_exchange_strong(armed, 0)) throw std::runtime_error("injected worker fault");
     }
     int n;
-    if (spin_until != 0) {
+    const bool polling = spin_until != 0;
+    if (polling) {
       n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), 0);
       if (n == 0) {
         const int64_t now = mono_ns();
@@ -1053,7 +1113,11 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
         }
       }
     }
-    if (n > 0) last_activity = mono_ns();
+    if (n > 0) {
+      last_activity = mono_ns();
+      wake_ts = last_activity;
+      wake_spin = polling;
+    }
     bool law_tick = false;
     for (int i = 0; i < n; ++i) {
       const int fd = evs[i].data.fd;
@@ -1195,7 +1259,9 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
         close_conn(fd);
         continue;
       }
-      if (!flush(c)) continue;
+      const bool alive = flush(c);
+      if (!trace_pending.empty()) stamp_sent();
+      if (!alive) continue;
       if (peer_closed) close_conn(fd);
     }
     // ListAndWatch: push on notify() and on any version change seen by the poll tick

@@ -29,6 +29,30 @@
 
 namespace amdgpu_dp {
 
+// Per-call trace of unary RPCs (grpc.callTraceFile): a ring of fixed-size records in a
+// shared file mapping, so a benchmark in another process can attribute each slow call
+// it measured to a segment of the server's handling.  All times CLOCK_MONOTONIC ns.
+struct CallTraceEntry {
+  int64_t t_ready = 0;     // the epoll_wait return that delivered the request
+  int64_t t_dispatch = 0;  // request decoded, handler entered
+  int64_t t_sent = 0;      // response handed to send() (the worker's flush of the batch)
+  uint64_t conn = 0;       // worker index << 48 | connection serial
+  uint32_t seq = 0;        // write order + 1 (0: slot never written)
+  uint8_t method = 0;      // Rpc
+  uint8_t spinning = 0;    // 1: the worker was polling (busy-poll window), 0: it slept in epoll_wait
+  uint16_t cpu = 0;        // CPU the worker ran on at dispatch
+};
+static_assert(sizeof(CallTraceEntry) == 40, "trace record layout is read by bench.py");
+struct CallTraceHeader {
+  uint64_t magic = 0;      // kCallTraceMagic
+  uint32_t version = 1;
+  uint32_t capacity = 0;   // records after the header
+  std::atomic<uint64_t> next{0};
+  uint64_t pad[5] = {};
+};
+static_assert(sizeof(CallTraceHeader) == 64, "trace header layout is read by bench.py");
+constexpr uint64_t kCallTraceMagic = 0x5452434c4c414344ull;  // "DCALLCRT"
+
 class GrpcServer {
  public:
   // busy_poll_us: after a worker handles a request it keeps polling its epoll set
@@ -49,6 +73,9 @@ class GrpcServer {
   // registration and the socket stay as they are.
   void set_table(std::shared_ptr<DeviceTable> t);
   uint64_t table_swaps() const { return table_gen_.load(); }
+  // Before start(): record every unary call in a ring of `capacity` CallTraceEntry records
+  // mapped from `path` (created / truncated).  Costs one clock read per response batch.
+  void set_call_trace(const std::string& path, int capacity);
   void start();  // throws std::runtime_error on bind/listen failure
   void stop();   // idempotent: trailers for open streams, GOAWAY, close, unlink socket
   void notify(); // wake ListAndWatch streams now (health changed)
@@ -129,6 +156,9 @@ class GrpcServer {
   ShardedCounter shed_;
   ShardedCounter admission_windows_, poll_windows_yielded_;
   std::atomic<int> conns_{0};
+  CallTraceHeader* trace_hdr_ = nullptr;  // mapped by set_call_trace (nullptr: off)
+  CallTraceEntry* trace_ = nullptr;
+  size_t trace_bytes_ = 0;
   std::vector<std::unique_ptr<Worker>> workers_;
   std::vector<std::thread> threads_;
   mutable std::mutex mu_;

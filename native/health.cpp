@@ -312,7 +312,7 @@ void HealthMonitor::on_sample(int gpu, bool ok, const GpuSample& s) {
       if (s.fw_clock_s >= 0) {
         const double fw_boot = now_b - s.fw_clock_s;
         char msg[200];
-        if (st.restored_fw_boot >= 0) {
+        if (!std::isnan(st.restored_fw_boot)) {
           // a latch from a previous process: did the firmware start after it was recorded?
           const double tol = std::max(30.0, 1e-4 * std::max(0.0, now_b - st.restored_fw_boot));
           if (fw_boot > st.restored_fw_boot + tol) {
@@ -320,7 +320,7 @@ void HealthMonitor::on_sample(int gpu, bool ok, const GpuSample& s) {
                           "start recorded with the latch)", fw_boot - st.restored_fw_boot);
             reset_why = msg;
           }
-          st.restored_fw_boot = -1;
+          st.restored_fw_boot = std::numeric_limits<double>::quiet_NaN();
         }
         if (st.fw_clock >= 0 && s.fw_clock_s + 1.0 < st.fw_clock) {
           std::snprintf(msg, sizeof(msg), "firmware clock restarted (%.1f s -> %.1f s)", st.fw_clock, s.fw_clock_s);
@@ -336,7 +336,7 @@ void HealthMonitor::on_sample(int gpu, bool ok, const GpuSample& s) {
         st.fw_read_at = now_b;
         if (st.fw_advancing) st.fw_boot = fw_boot;
       } else {
-        st.restored_fw_boot = -1;  // nothing to compare it with
+        st.restored_fw_boot = std::numeric_limits<double>::quiet_NaN();  // nothing to compare it with
         // a GPU that reports no firmware clock: coming back from an outage is the reset
         if (st.lost) reset_why = "telemetry back after an outage (the GPU reports no firmware clock)";
       }
@@ -523,7 +523,7 @@ std::vector<HealthLatch> HealthMonitor::latches() const {
     l.key = kv.first;
     l.ecc_bad = true;
     l.last_ue = st.last_ue;
-    l.fw_boot_s = st.fw_boot >= 0 ? st.fw_boot : st.restored_fw_boot;
+    l.fw_boot_s = !std::isnan(st.fw_boot) ? st.fw_boot : st.restored_fw_boot;
     l.reason = st.ecc_reason;
     l.since_ns = st.ecc_since_ns;
     out.push_back(std::move(l));

@@ -14,6 +14,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <deque>
+#include <limits>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -61,9 +62,10 @@ struct HealthLatch {
   bool ecc_bad = false;     // uncorrectable-ECC latch (cleared only by a reset)
   int64_t last_ue = -1;     // the UE count the latch was taken at (the next baseline)
   // CLOCK_BOOTTIME second at which the GPU's firmware started (boot time - firmware
-  // clock), from a clock seen advancing; -1 = unknown.  A later process that finds the
-  // firmware started later than this knows the GPU was reset while nobody watched.
-  double fw_boot_s = -1;
+  // clock), from a clock seen advancing; NaN = unknown.  Negative when the firmware
+  // started before the kernel's clock (it does on every boot).  A later process that
+  // finds the firmware started later than this knows the GPU was reset meanwhile.
+  double fw_boot_s = std::numeric_limits<double>::quiet_NaN();
   std::string reason;
   int64_t since_ns = 0;     // wall clock of the latch
 };
@@ -170,8 +172,8 @@ class HealthMonitor {
     double fw_clock = -1;
     double fw_read_at = -1;
     bool fw_advancing = false;
-    double fw_boot = -1;
-    double restored_fw_boot = -1;  // from a previous process; checked by the first sample
+    double fw_boot = std::numeric_limits<double>::quiet_NaN();
+    double restored_fw_boot = std::numeric_limits<double>::quiet_NaN();  // previous process; first sample checks it
     std::map<std::string, int> link_up;  // peer key -> 1/0
     std::map<std::string, double> link_bw;  // peer key -> trained bandwidth as this end last saw it
     int page_threshold = 0;

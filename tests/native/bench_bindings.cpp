@@ -7,6 +7,7 @@
 // between the two modules, and both are built from the same sources by _build.py.
 // `_native` must be imported first (the module does it).
 #include <sched.h>
+#include <sys/resource.h>
 
 #include <chrono>
 #include <thread>
@@ -49,32 +50,41 @@ PYBIND11_MODULE(_native_bench, m) {
            },
            py::arg("path"), py::arg("req"), py::arg("n"), py::arg("gap_us") = 0);
   h2.def("bench_unary_ts",
-           // Same as bench_unary, per call: (start, CLOCK_MONOTONIC ns; latency, s; the
-           // CPU the client ran on when the answer arrived) - for attributing the tail to
-           // idle gaps, CPU migrations or events of the server process at that time.
-           [](H2Client& c, const std::string& path, const py::bytes& req, int n, int gap_us) {
-             std::string r(req), resp, msg;
-             std::vector<int64_t> starts;
-             std::vector<double> lat;
-             std::vector<int> cpus;
-             starts.reserve(static_cast<size_t>(n));
-             lat.reserve(static_cast<size_t>(n));
-             cpus.reserve(static_cast<size_t>(n));
-             {
-               py::gil_scoped_release rel;
-               for (int i = 0; i < n; ++i) {
-                 if (gap_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(gap_us));
-                 const int64_t t0 = mono_ns();
-                 const int st = c.unary(path, r, &resp, &msg);
-                 lat.push_back((mono_ns() - t0) * 1e-9);
-                 starts.push_back(t0);
-                 cpus.push_back(sched_getcpu());
-                 if (st != 0) throw std::runtime_error("grpc-status " + std::to_string(st) + ": " + msg);
-               }
+         // Same as bench_unary, per call: (start, CLOCK_MONOTONIC ns; latency, s; the CPU the
+         // client ran on when the answer arrived; involuntary context switches of the client
+         // thread during the call, read outside the timed interval) - for attributing the
+         // tail to idle gaps, CPU migrations, preemption or the server's handling (the
+         // server's own per-call record: grpc.callTraceFile).
+         [](H2Client& c, const std::string& path, const py::bytes& req, int n, int gap_us) {
+           std::string r(req), resp, msg;
+           std::vector<int64_t> starts;
+           std::vector<double> lat;
+           std::vector<int> cpus, preempted;
+           starts.reserve(static_cast<size_t>(n));
+           lat.reserve(static_cast<size_t>(n));
+           cpus.reserve(static_cast<size_t>(n));
+           preempted.reserve(static_cast<size_t>(n));
+           {
+             py::gil_scoped_release rel;
+             struct rusage ru {};
+             getrusage(RUSAGE_THREAD, &ru);
+             long ivcsw = ru.ru_nivcsw;
+             for (int i = 0; i < n; ++i) {
+               if (gap_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(gap_us));
+               const int64_t t0 = mono_ns();
+               const int st = c.unary(path, r, &resp, &msg);
+               lat.push_back((mono_ns() - t0) * 1e-9);
+               starts.push_back(t0);
+               cpus.push_back(sched_getcpu());
+               getrusage(RUSAGE_THREAD, &ru);
+               preempted.push_back(static_cast<int>(ru.ru_nivcsw - ivcsw));
+               ivcsw = ru.ru_nivcsw;
+               if (st != 0) throw std::runtime_error("grpc-status " + std::to_string(st) + ": " + msg);
              }
-             return py::make_tuple(starts, lat, cpus);
-           },
-           py::arg("path"), py::arg("req"), py::arg("n"), py::arg("gap_us") = 0);
+           }
+           return py::make_tuple(starts, lat, cpus, preempted);
+         },
+         py::arg("path"), py::arg("req"), py::arg("n"), py::arg("gap_us") = 0);
 
   m.def("h2_bench_unary",
         [](const std::string& sock, const std::string& path, const py::bytes& req, int n) {

@@ -185,7 +185,13 @@ def test_bench_reports_advertised_devices_and_tail():
     r = _run_bench(["--steps", "2", "--warmup", "1"])
     assert r["advertised_devices"] == 1 and r["world_size"] == 1
     t = r["allocate_tail"]
-    assert t["calls"] == 2 * 256 and t["slow"] == t["first_of_batch"] + t["cpu_migrated"] + t["other"]
+    # every slow call has exactly one cause; with the daemon's call trace each call is
+    # matched to the server's record of it, so nothing is left unattributed
+    assert t["calls"] == 2 * 256 and t["slow"] == sum(t["by_cause"].values())
+    assert t["matched"] == t["calls"] and t["other"] == 0
+    assert set(t["segment_p50_us"]) == {"inbound", "server", "outbound"}
+    assert set(t["by_cause"]) <= {"inbound_worker_polling", "inbound_worker_asleep", "server_handling",
+                                  "outbound_client_wakeup", "client_preempted"}
     assert r["allocate_p999_us"] >= r["allocate_p99_us"] >= r["allocate_p50_us"]
     assert 0 < r["preferred_allocator_8gpu_size4_p50_us"] < 1000
     assert r["uds_roundtrip_floor_spin_p99_us"] >= r["uds_roundtrip_floor_spin_p50_us"]

@@ -314,6 +314,32 @@ def test_pcie_floor_on_the_real_link(n, amdsmi_backend):
     assert mon.gpu_healthy(0)
 
 
+def test_firmware_clock_reset_signal_on_real_gpu(n, amdsmi_backend, tmp_path):
+    """The reset signal an unprivileged pod has (native/health.cpp): the GPU firmware's
+    clock, read from gpu_metrics, ticks at one second per second (profiles/r5/
+    reset_signal_probe.json: 100.004 MHz); a latch restored with the firmware start it
+    recorded holds, and one restored with an earlier start (the firmware restarted since,
+    i.e. the GPU was reset) is cleared by the first sample."""
+    gpus, _ = amdsmi_backend.discover()
+    a = amdsmi_backend.sample(0)
+    time.sleep(0.5)
+    b = amdsmi_backend.sample(0)
+    assert a.fw_clock_s > 0 and b.fw_clock_s > a.fw_clock_s, (a.fw_clock_s, b.fw_clock_s)
+    rate = (b.fw_clock_s - a.fw_clock_s) / ((b.ts_ns - a.ts_ns) * 1e-9)
+    assert 0.9 < rate < 1.1, rate
+    fw_boot = n.boottime_s() - b.fw_clock_s
+    key = amdsmi_backend.gpu_key(0)
+    for recorded, stays in ((fw_boot, True), (fw_boot - 3600.0, False)):
+        mon = n.HealthMonitor(amdsmi_backend, 3)
+        mon.set_gpus([key])
+        mon.restore_latches([n.HealthLatch(key, max(0, b.ecc_uncorrectable), recorded, "test latch", 0)])
+        assert not mon.gpu_healthy(0)
+        mon.on_sample(0, True, amdsmi_backend.sample(0))
+        assert mon.gpu_healthy(0) != stays, (recorded, fw_boot)
+        assert mon.resets_observed == (0 if stays else 1)
+    print("firmware clock %.1f s, rate %.6f s/s, firmware started at boot+%.1f s" % (b.fw_clock_s, rate, fw_boot))
+
+
 def test_amdsmi_inventory_signature_is_stable(amdsmi_backend):
     from k8s_gpu_device_plugin_amd.plugin.manager import inventory_signature
     a = inventory_signature(amdsmi_backend.discover()[0])

@@ -89,7 +89,7 @@ def _latch(make_cfg, plugin_dir, k, **cfg):
     key1 = r.m._key_of[1]
     assert _wait(lambda: _latched_gpus(plugin_dir) == [key1])
     ecc = _state(plugin_dir)["gpus"][key1]["ecc"]
-    assert ecc["last_ue"] == 1 and ecc["fw_boot_s"] >= 0 and "uncorrectable ECC count 0 -> 1" in ecc["reason"]
+    assert ecc["last_ue"] == 1 and ecc["fw_boot_s"] is not None and "uncorrectable ECC count 0 -> 1" in ecc["reason"]
     return r, key1
 
 

@@ -256,8 +256,9 @@ def test_failed_reload_keeps_serving_and_kubelet_restart_reregisters(make_cfg, p
 
 def test_devices_indices_wait_for_gpus_missing_at_first_discovery(make_cfg, plugin_dir, run_manager):
     """`devices: "0-1"` with no GPU at the first discovery selects
-    nothing *yet* and picks the GPUs up when they appear; a GPU missing from the first
-    discovery takes its own index when it appears instead of leaving it to a neighbour."""
+    nothing *yet* and picks the GPUs up when they appear.  ADVICE r4 (low): once an index
+    has been advertised it stays pinned to that GPU - a GPU that appears later with a lower
+    BDF does not push it out (it may be allocated to pods); the conflict is counted."""
     be = fixtures.build_backend("4gpu_spx")
     uuids = [g.uuid for g in be.discover()[0]]
     for g in range(4):
@@ -270,12 +271,15 @@ def test_devices_indices_wait_for_gpus_missing_at_first_discovery(make_cfg, plug
         be.set_gpu_present(2, True)
         be.set_gpu_present(3, True)  # GPU 1 still missing
         assert _wait(lambda: [g.uuid for g in m.gpus] == [uuids[0], uuids[2]], 5), [g.uuid for g in m.gpus]
-        be.set_gpu_present(1, True)  # now it shows up: index 1 is its own
-        assert _wait(lambda: [g.uuid for g in m.gpus] == [uuids[0], uuids[1]], 5), [g.uuid for g in m.gpus]
         k.wait_for_registrations(1, timeout=5)
-        # and a GPU that drops off the bus does not shift GPU 2 into the selection
+        be.set_gpu_present(1, True)  # now it shows up, ranking 1 by BDF: GPU 2 keeps index 1
+        assert _wait(lambda: m.counters.get("devices_index_conflicts", 0) == 1, 5)
+        assert [g.uuid for g in m.gpus] == [uuids[0], uuids[2]]
+        # and a GPU that drops off the bus leaves its index empty (no neighbour moves in)
         be.set_gpu_present(0, False)
-        assert _wait(lambda: [g.uuid for g in m.gpus] == [uuids[1]], 5), [g.uuid for g in m.gpus]
+        assert _wait(lambda: [g.uuid for g in m.gpus] == [uuids[2]], 5), [g.uuid for g in m.gpus]
+        time.sleep(0.3)
+        assert [g.uuid for g in m.gpus] == [uuids[2]]
 
 
 def test_sampler_refused_by_a_lane_stuck_in_discovery_shows_the_gpu_down(n):
@@ -378,3 +382,23 @@ def test_samples_follow_identity_when_a_rediscovery_moves_the_indices(n):
         assert 'amdgpu_telemetry_up{gpu="1"} 0' in ex.render()  # gone from the bus: not sampled
     finally:
         ex.stop()
+
+
+def test_wedged_gpu_outside_the_selection_does_not_fail_readiness(make_cfg, plugin_dir, run_manager):
+    """a GPU that `devices` leaves out wedges; discovery reports it stale,
+    but GET /ready - and so a DaemonSet rolling update - does not wait on a GPU this plugin
+    does not serve.  The same wedge on a served GPU fails readiness."""
+    be = fixtures.build_backend("4gpu_spx")
+    cfg = make_cfg(fixture="4gpu_spx", devices="0-1", telemetry={"intervalMs": 50}, rediscoverIntervalS=0.2,
+                   health={"sampleStallS": 0.3, "discoveryTimeoutS": 0.3, "lostAfterFailures": 3})
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(cfg, be)
+        k.wait_for_registrations(1)
+        assert _wait(lambda: m.readiness() == (True, ""), 5)
+        be.set_sample_stall(3, True)
+        assert _wait(lambda: m._stale and m._stale[0][1] == fixtures.fixture_uuid(1, 3), 5), m._stale
+        time.sleep(0.5)
+        assert m.readiness() == (True, ""), m.readiness()
+        be.set_sample_stall(3, False)
+        be.set_sample_stall(1, True)
+        assert _wait(lambda: "discovery stalled on GPU 1" in m.readiness()[1], 5), m.readiness()
