@@ -114,6 +114,40 @@ def read_call_trace(path: str):
     return recs[recs["seq"] > 0]
 
 
+def match_calls(starts, lats, trace, rpc: int) -> list:
+    """The server's record (grpc.callTraceFile) of each client call (start mono ns,
+    latency s), or None: a record of that RPC dispatched within the call, on the client's
+    connection - the one most calls with a single candidate record were answered on."""
+    import collections
+
+    import numpy as np
+    out = [None] * len(starts)
+    if trace is None or not len(trace):
+        return out
+    a = trace[(trace["method"] == rpc) & (trace["t_sent"] > 0)]
+    a = a[np.argsort(a["t_dispatch"], kind="stable")]
+    td = a["t_dispatch"]
+    ranges = [(int(np.searchsorted(td, s, "left")), int(np.searchsorted(td, s + int(x * 1e9), "right")))
+              for s, x in zip(starts, lats)]
+    votes = collections.Counter(int(a["conn"][i0]) for i0, i1 in ranges if i1 - i0 == 1)
+    if not votes:
+        return out
+    mine = votes.most_common(1)[0][0]
+    for k, (i0, i1) in enumerate(ranges):
+        for j in range(i0, i1):
+            if int(a["conn"][j]) == mine:
+                out[k] = a[j]
+                break
+    return out
+
+
+def segments(start: int, lat: float, e) -> tuple:
+    """(inbound, server, outbound) ns of one call matched to its server record: client
+    start -> the worker's epoll_wait returning with the request -> response sent -> the
+    client has the answer."""
+    return (int(e["t_ready"]) - start, int(e["t_sent"]) - int(e["t_ready"]), start + int(lat * 1e9) - int(e["t_sent"]))
+
+
 def _tail_stats(batches, trace=None, rpc_allocate: int = 3) -> dict:
     """Attribution of this rank's slow Allocates (> 2x the rank's p50), call by call.
 
@@ -142,25 +176,10 @@ def _tail_stats(batches, trace=None, rpc_allocate: int = 3) -> dict:
             calls.append((int(starts[i]), x, cpus[i], pre[i], i == 0, i > 0 and cpus[i] != cpus[i - 1]))
     out = {"calls": len(calls), "slow": 0, "first_of_batch": 0, "cpu_migrated": 0, "client_preempted": 0,
            "threshold_us": round(thr * 1e6, 2)}
-    matched = [None] * len(calls)
+    matched = match_calls([c[0] for c in calls], [c[1] for c in calls], trace, rpc_allocate)
     seg_med = None
     if trace is not None and len(trace):
-        a = trace[(trace["method"] == rpc_allocate) & (trace["t_sent"] > 0)]
-        a = a[np.argsort(a["t_dispatch"], kind="stable")]
-        td = a["t_dispatch"]
-        ranges = []
-        for s, x, *_ in calls:
-            ranges.append((int(np.searchsorted(td, s, "left")), int(np.searchsorted(td, s + int(x * 1e9), "right"))))
-        votes = collections.Counter(int(a["conn"][i0]) for i0, i1 in ranges if i1 - i0 == 1)
-        if votes:
-            mine = votes.most_common(1)[0][0]  # this client's connection
-            for k, (i0, i1) in enumerate(ranges):
-                for j in range(i0, i1):
-                    if int(a["conn"][j]) == mine:
-                        matched[k] = a[j]
-                        break
-        segs = [(int(e["t_ready"]) - c[0], int(e["t_sent"]) - int(e["t_ready"]), c[0] + int(c[1] * 1e9) - int(e["t_sent"]))
-                for c, e in zip(calls, matched) if e is not None]
+        segs = [segments(c[0], c[1], e) for c, e in zip(calls, matched) if e is not None]
         if segs:
             seg_med = [float(np.median([sg[i] for sg in segs])) for i in range(3)]
             out["matched"] = len(segs)
@@ -183,7 +202,7 @@ def _tail_stats(batches, trace=None, rpc_allocate: int = 3) -> dict:
         else:
             if int(e["cpu"]) == cpu:
                 same_cpu += 1
-            seg = (int(e["t_ready"]) - s, int(e["t_sent"]) - int(e["t_ready"]), s + int(x * 1e9) - int(e["t_sent"]))
+            seg = segments(s, x, e)
             ex = [seg[i] - seg_med[i] for i in range(3)]
             k = int(np.argmax(ex))
             cause = (("inbound_worker_polling" if e["spinning"] else "inbound_worker_asleep"), "server_handling",

@@ -19,7 +19,12 @@ allocate - floor and preferred - floor (iteration i's calls are a pair) with a b
 95 % confidence interval.  Evidence for where an excess comes from, per call: minor and
 major page faults and scheduler counters (run time, run-queue wait, time slices) of the
 daemon's gRPC worker threads (``dpgrpc-*`` in /proc/<pid>/task) and of the calling
-thread, read before and after the call.
+thread, read before and after the call; and the daemon's own record of the call
+(grpc.callTraceFile, see bench.match_calls), which splits it into inbound (client send ->
+the worker's epoll_wait returning with it; the worker's wake-up), server (-> response
+sent) and outbound (-> the client has it; the client's wake-up), with whether the worker
+was asleep.  ``attribution`` compares each segment's median at the longest gap with the
+shortest (bootstrap 95 % intervals): the parts of the idle excess, summing to it.
 
     python scripts/idle_probe.py [--gaps 0.001,0.01,0.1,1] [--calls 300] [--out FILE]
     python scripts/idle_probe.py --gaps 1 --calls 100 --ab-keep-warm 0,10   # A/B, interleaved
@@ -46,6 +51,7 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 KINDS = ("allocate", "preferred", "floor")
+SEGMENTS = ("inbound", "server", "outbound")
 
 
 def pct(xs, q):
@@ -63,6 +69,15 @@ def bootstrap_ci(diffs, n=2000, seed=7):
     k = len(diffs)
     meds = sorted(median([diffs[rng.randrange(k)] for _ in range(k)]) for _ in range(n))
     return meds[int(0.025 * n)], meds[int(0.975 * n)]
+
+
+def median_shift(a, b, n=2000, seed=11):
+    """median(a) - median(b) and its 95 % percentile-bootstrap interval (a and b are
+    independent samples, resampled separately)."""
+    rng = random.Random(seed)
+    ds = sorted(median([a[rng.randrange(len(a))] for _ in a]) - median([b[rng.randrange(len(b))] for _ in b])
+                for _ in range(n))
+    return median(a) - median(b), (ds[int(0.025 * n)], ds[int(0.975 * n)])
 
 
 def worker_tids(pid: int, prefix: str = "dpgrpc-"):
@@ -145,8 +160,15 @@ class Daemon:
         import http.client
         self.mconn = http.client.HTTPConnection("127.0.0.1", self.port, timeout=10)
         self.base = {}
-        self.allocate = lambda: self.h2.bench_unary(v1beta1.METHOD_ALLOCATE, self.alloc, 1)[0]
-        self.preferred = lambda: self.h2.bench_unary(v1beta1.METHOD_GET_PREFERRED, self.pref, 1)[0]
+        self.trace_path = os.path.join(self.workdir, "calltrace-%s.bin" % reg.resource_name.split("/")[-1])
+        self.starts = {"allocate": [], "preferred": []}  # client start (mono ns) of every timed call
+
+        def timed(kind, method, req):
+            starts, lat, _, _ = self.h2.bench_unary_ts(method, req, 1)
+            self.starts[kind].append(starts[0])
+            return lat[0]
+        self.allocate = lambda: timed("allocate", v1beta1.METHOD_ALLOCATE, self.alloc)
+        self.preferred = lambda: timed("preferred", v1beta1.METHOD_GET_PREFERRED, self.pref)
 
     def close(self):
         try:
@@ -232,11 +254,13 @@ def main() -> int:
         res["kinds"] = list(kinds)
         res["daemon_grpc_workers"] = len(first.tids)
         rpc_name = {"allocate": "Allocate", "preferred": "GetPreferredAllocation"}
+        segs_by_gap, lat_by_gap = {}, {}  # rpc kind -> gap -> per-call segments / latencies
         for gap in [float(x) for x in a.gaps.split(",")]:
             lat = {k: [] for k in kinds}
             srv = {k: [] for k in rpcs}  # the daemon's own time per call
             for d in daemons.values():
                 d.base = {}
+                d.starts = {"allocate": [], "preferred": []}
             ev = {k: {"daemon_minflt": 0, "daemon_majflt": 0, "daemon_run_us": 0.0, "daemon_wait_us": 0.0,
                       "daemon_slices": 0, "client_minflt": 0} for k in kinds}
             for i in range(a.calls):
@@ -296,9 +320,41 @@ def main() -> int:
                         row["%s_@%s_minus_@%s" % (rpc, first_arm, other)] = {
                             "median_us": us(median(diffs)), "ci95_us": [us(lo), us(hi)]}
             row["floor"]["per_call"] = {"client_minflt": round(ev["floor"]["client_minflt"] / a.calls, 3)}
+            # the daemon's record of each timed call: segments and whether the worker slept
+            for k in rpcs:
+                d = owner[k]
+                base = k.split("@")[0].split("#")[0]
+                rpc = n.RPC_ALLOCATE if base == "allocate" else n.RPC_PREFERRED
+                recs = bench.match_calls(d.starts[base], lat[k], bench.read_call_trace(d.trace_path), rpc)
+                seg = [bench.segments(st, x, e) for st, x, e in zip(d.starts[base], lat[k], recs) if e is not None]
+                if seg:
+                    row[k]["matched"] = len(seg)
+                    row[k]["segments_p50_us"] = {name: round(median([s_[i] for s_ in seg]) / 1e3, 2)
+                                                 for i, name in enumerate(SEGMENTS)}
+                    row[k]["worker_asleep_fraction"] = round(
+                        sum(1 for e in recs if e is not None and not e["spinning"]) / len(seg), 3)
+                    segs_by_gap.setdefault(k, {})[gap] = seg
+                    lat_by_gap.setdefault(k, {})[gap] = [x for x, e in zip(lat[k], recs) if e is not None]
             res["rows"].append(row)
             print(json.dumps(row), flush=True)
         del pinger
+        # where the idle excess goes: each segment's median at the longest gap minus at the
+        # shortest, with a bootstrap 95 % interval (independent samples resampled apart)
+        res["attribution"] = {}
+        for k, by_gap in segs_by_gap.items():
+            if len(by_gap) < 2:
+                continue
+            lo_gap, hi_gap = min(by_gap), max(by_gap)
+            cold, warm = by_gap[hi_gap], by_gap[lo_gap]
+            att = {"from_gap_s": lo_gap, "to_gap_s": hi_gap}
+            for i, name in enumerate(SEGMENTS):
+                d, ci = median_shift([x[i] for x in cold], [x[i] for x in warm])
+                att[name + "_us"] = {"median": round(d / 1e3, 2), "ci95": [round(ci[0] / 1e3, 2), round(ci[1] / 1e3, 2)]}
+            d, ci = median_shift(lat_by_gap[k][hi_gap], lat_by_gap[k][lo_gap])
+            att["total_us"] = {"median": round(d * 1e6, 2), "ci95": [round(ci[0] * 1e6, 2), round(ci[1] * 1e6, 2)]}
+            att["sum_of_segments_us"] = round(sum(att[n_ + "_us"]["median"] for n_ in SEGMENTS), 2)
+            res["attribution"][k] = att
+        print(json.dumps({"attribution": res["attribution"]}), flush=True)
     finally:
         for d in daemons.values():
             d.close()
