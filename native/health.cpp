@@ -127,17 +127,21 @@ bool HealthMonitor::healthy_locked(const GpuState& st) const {
          !(st.pcie_bad && !(disabled_ & kCheckPcie));
 }
 
-void HealthMonitor::reconcile_locked(const std::string& key, int kind, const std::string& reason) {
+void HealthMonitor::reconcile_locked(const std::string& key, int kind, const std::string& reason,
+                                     bool latch_changed) {
   GpuState& st = state_[key];
   const int idx = table_index_locked(key);
   const bool healthy = healthy_locked(st);
   if (healthy == st.reported_healthy) {
-    if (disabled_ & check_of(kind)) {  // tracked, not acted on: still worth a log line
+    // tracked, not acted on (check disabled), or a persisted latch that moved without a
+    // health transition (a UE on a GPU already Unhealthy for another reason): the manager
+    // still hears of it, logs it and persists the latch
+    if ((disabled_ & check_of(kind)) || latch_changed) {
       HealthUpdate u;
       u.kind = kind;
       u.gpu = idx;
       u.key = key;
-      u.reason = reason + " (health check disabled)";
+      u.reason = reason + ((disabled_ & check_of(kind)) ? " (health check disabled)" : " (latched)");
       emit_locked(std::move(u));
     }
     return;
@@ -172,6 +176,7 @@ void HealthMonitor::process(const HwEvent& e) {
     case kEvtResetObserved: {
       if (!known) return;
       GpuState& st = state_[key];
+      const bool had_latch = st.ecc_bad;
       st.resetting = false;
       st.ecc_bad = false;  // a reset clears the uncorrectable-error latch
       st.restored = false;
@@ -180,18 +185,19 @@ void HealthMonitor::process(const HwEvent& e) {
       // by polling comes from the sample that already took the new baseline.
       if (e.kind == kEvtPostReset) st.last_ue = -1;
       if (e.kind == kEvtResetObserved) ++resets_observed_;
-      reconcile_locked(key, e.kind, why);
+      reconcile_locked(key, e.kind, why, had_latch);
       return;
     }
     case kEvtEccUncorrectable: {
       if (!known) return;
       GpuState& st = state_[key];
-      if (!st.ecc_bad) {
+      const bool fresh = !st.ecc_bad;
+      if (fresh) {
         st.ecc_reason = why;
         st.ecc_since_ns = now_ns();
       }
       st.ecc_bad = true;
-      reconcile_locked(key, e.kind, why);
+      reconcile_locked(key, e.kind, why, fresh);
       return;
     }
     case kEvtDeviceLost:

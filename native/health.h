@@ -180,7 +180,7 @@ class HealthMonitor {
   };
   void loop();
   void emit_locked(HealthUpdate u);
-  void reconcile_locked(const std::string& key, int kind, const std::string& reason);
+  void reconcile_locked(const std::string& key, int kind, const std::string& reason, bool latch_changed = false);
   bool healthy_locked(const GpuState& st) const;
   // Identity of backend index `gpu` (the index space of samples and events): the
   // event's own key when it carries one, else the backend's, else "#<index>".

@@ -266,3 +266,23 @@ def test_canary_on_prestart_with_replicas_is_a_config_error(make_cfg):
     from k8s_gpu_device_plugin_amd.config import ConfigError
     with pytest.raises(ConfigError, match="sharing.replicas"):
         make_cfg(health={"canaryOnPreStart": True}, sharing={"replicas": 2})
+
+
+def test_ue_on_a_gpu_already_unhealthy_is_still_persisted(make_cfg, plugin_dir):
+    """A UE latch set while the GPU is Unhealthy for another reason (here a degraded PCIe
+    link) is no health transition, but it must still reach the state file: when the link
+    recovers the GPU stays Unhealthy, and so does a restarted plugin."""
+    with KubeletStub(plugin_dir) as k:
+        r = Run(make_cfg, _model(), health={"pcieMinWidth": 16, "pcieDebounceSamples": 1})
+        try:
+            k.wait_for_registrations(1)
+            r.be.set_pcie_link(1, 8, 32.0)
+            assert _wait(lambda: not r.healthy(1))
+            r.be.set_ecc_uncorrectable(1, 1)
+            key1 = r.m._key_of[1]
+            assert _wait(lambda: _latched_gpus(plugin_dir) == [key1]), "latch not persisted"
+            r.be.set_pcie_link(1, 16, 32.0)
+            time.sleep(0.4)
+            assert not r.healthy(1)  # the UE latch holds it
+        finally:
+            r.stop()

@@ -981,3 +981,65 @@ def test_node_labels_leave_out_a_version_the_gpus_disagree_on():
 def test_driver_version_is_normalised(reported, want):
     from k8s_gpu_device_plugin_amd import native
     assert native.load().normalize_driver_version(reported) == want
+
+
+@pytest.mark.parametrize("grpc_server", ["native", "python"])
+def test_allocate_never_fails_through_restarts_and_inventory_changes(make_cfg, plugin_dir, run_manager,
+                                                                     grpc_server):
+    """Allocate in a tight loop on one connection through 50 /restart
+    reloads and partition-mode flips of another GPU (inventory changes): zero failed calls,
+    one connection, one registration, and the open ListAndWatch stream follows the new
+    device lists."""
+    from k8s_gpu_device_plugin_amd import native
+    from k8s_gpu_device_plugin_amd.api import v1beta1
+    be = fixtures.build_backend("2gpu_spx")
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(migStrategy="single", grpc={"server": grpc_server}, rediscoverIntervalS=0.05),
+                        backend=be)
+        reg = k.wait_for_registrations(1)[0]
+        w = k.watch(reg.endpoint)
+        w.next()
+        dev0 = m.plugins[0].table.ids()[0]  # GPU 0 keeps its device through every change
+        req = v1beta1.AllocateRequest(container_requests=[v1beta1.ContainerAllocateRequest(
+            devices_ids=[dev0])]).SerializeToString()
+        stop = threading.Event()
+        stats = {"ok": 0, "failed": [], "connections": 0}
+
+        def loop():
+            n = native.load()
+            c = n.H2Client(os.path.join(plugin_dir, reg.endpoint))
+            stats["connections"] += 1
+            while not stop.is_set():
+                try:
+                    st, _, msg = c.unary(v1beta1.METHOD_ALLOCATE, req)
+                except Exception as e:  # the connection dropped
+                    stats["failed"].append(repr(e))
+                    c = n.H2Client(os.path.join(plugin_dir, reg.endpoint))
+                    stats["connections"] += 1
+                    continue
+                if st == 0:
+                    stats["ok"] += 1
+                else:
+                    stats["failed"].append(msg)
+            c.close()
+
+        t = threading.Thread(target=loop, daemon=True)
+        t.start()
+        try:
+            for i in range(50):
+                reloads = m.counters["reloads"]
+                m.restart()
+                assert _wait(lambda: m.counters["reloads"] > reloads, 10)
+                if i % 10 == 5:  # an operator re-partitions GPU 1: the inventory re-check reloads
+                    fixtures.set_gpu_mode(be, 1, "CPX" if i % 20 == 5 else "SPX", "NPS1")
+                    inv = m.counters.get("restarts_inventory", 0)
+                    assert _wait(lambda: m.counters.get("restarts_inventory", 0) > inv, 10)
+        finally:
+            stop.set()
+            t.join(10)
+        assert not stats["failed"], stats["failed"][:5]
+        assert stats["ok"] > 100 and stats["connections"] == 1
+        assert len(k.requests) == 1 and m.counters.get("table_swaps", 0) >= 50
+        assert m.counters.get("restarts_inventory", 0) >= 5
+        devs = w.last(timeout=5)
+        assert len(devs) == len(m.plugins[0].table.ids())
