@@ -187,6 +187,7 @@ def _tail_stats(batches, trace=None, rpc_allocate: int = 3) -> dict:
                                      "outbound": round(seg_med[2] / 1e3, 2)}
     causes = collections.Counter()
     excess = collections.defaultdict(list)
+    slowest = []  # (latency s, cause, [inbound, server, outbound] us, worker was polling)
     same_cpu = 0
     for c, e in zip(calls, matched):
         s, x, cpu, pre, first, migrated = c
@@ -210,10 +211,16 @@ def _tail_stats(batches, trace=None, rpc_allocate: int = 3) -> dict:
             if pre > 0 and k != 1:
                 cause = "client_preempted"
             excess[cause].append(ex[k])
+            slowest.append((x, cause, [round(v / 1e3, 2) for v in seg], int(e["spinning"])))
+        if e is None or seg_med is None:
+            slowest.append((x, cause, None, None))
         causes[cause] += 1
     out["by_cause"] = dict(sorted(causes.items()))
     out["cause_mean_excess_us"] = {k: round(sum(v) / len(v) / 1e3, 2) for k, v in sorted(excess.items())}
     out["same_cpu_as_worker"] = same_cpu
+    # the calls p99.9 is made of, each with its cause and segments
+    out["slowest"] = [{"us": round(x * 1e6, 2), "cause": c, "segments_us": sg, "worker_polling": sp}
+                      for x, c, sg, sp in sorted(slowest, key=lambda r: -r[0])[:8]]
     return out
 
 
@@ -232,6 +239,7 @@ def _merge_tail(parts) -> dict:
     if parts and parts[0].get("segment_p50_us"):
         out["segment_p50_us"] = parts[0]["segment_p50_us"]
         out["cause_mean_excess_us"] = parts[0].get("cause_mean_excess_us")
+    out["slowest"] = sorted((x for p in parts for x in p.get("slowest", [])), key=lambda r: -r["us"])[:8]
     return out
 
 
@@ -550,6 +558,12 @@ def main() -> int:
     mine["uds_floor_spin_p50"] = _pct(spin, 0.5)
     mine["uds_floor_spin_p99"] = _pct(spin, 0.99)
     mine["uds_floor_spin_p999"] = _pct(spin, 0.999)
+    # ... and in the timed loop's own rhythm (batches of ALLOCS back-to-back exchanges, a
+    # scrape phase apart) against a server with the plugin worker's polling policy: this
+    # host's tail for that pattern, which Allocate's p99 / p99.9 are compared against
+    bf = nb.uds_pingpong_batched(args.steps, ALLOCS, int(SCRAPE_S * 1e6), *sizes,
+                                 server_poll_us=args.busy_poll_us if args.busy_poll_us is not None else 50)
+    mine["uds_floor_batched"] = (_pct(bf, 0.5), _pct(bf, 0.99), _pct(bf, 0.999), max(bf))
     # kubelet-like sparse calls: 1 ms apart, every one meets a sleeping server thread
     mine["alloc_cold"] = h2.bench_unary(v1beta1.METHOD_ALLOCATE, alloc_req, 400, 1000)
     # ... and the bare exchange with the same 1 ms idle gap (cold caches, idle CPU states)
@@ -608,6 +622,8 @@ def main() -> int:
             "allocate_tail": _merge_tail([g["alloc_tail"] for g in gathered]),
             "uds_roundtrip_floor_spin_p99_us": round(gathered[0]["uds_floor_spin_p99"] * 1e6, 2),
             "uds_roundtrip_floor_spin_p999_us": round(gathered[0]["uds_floor_spin_p999"] * 1e6, 2),
+            # the bare exchange timed in the same batches as Allocate (p50, p99, p99.9, max)
+            "uds_roundtrip_floor_batched_us": [round(x * 1e6, 2) for x in gathered[0]["uds_floor_batched"]],
             "preferred_allocator_8gpu_size4_p50_us": _allocator_probe(n),
             "allocate_server_mean_us": (round(gathered[0]["server_allocate_mean_s"] * 1e6, 3)
                                         if gathered[0].get("server_allocate_mean_s") else None),

@@ -131,6 +131,13 @@ PYBIND11_MODULE(_native_bench, m) {
         },
         py::arg("n") = 10000, py::arg("warmup") = 500, py::arg("req_bytes") = 128, py::arg("resp_bytes") = 256,
         py::arg("server_spin") = false, py::arg("tcp") = false, py::arg("gap_us") = 0);
+  m.def("uds_pingpong_batched",
+        [](int batches, int batch, int batch_gap_us, int req_bytes, int resp_bytes, int server_poll_us) {
+          py::gil_scoped_release rel;
+          return uds_pingpong_batched(batches, batch, batch_gap_us, req_bytes, resp_bytes, server_poll_us);
+        },
+        py::arg("batches"), py::arg("batch"), py::arg("batch_gap_us"), py::arg("req_bytes"), py::arg("resp_bytes"),
+        py::arg("server_poll_us") = 50);
   py::class_<UdsPinger>(m, "UdsPinger")
       .def(py::init<int, int, int>(), py::arg("req_bytes"), py::arg("resp_bytes"), py::arg("server_timeout_ms") = 100)
       .def("once", &UdsPinger::once, py::call_guard<py::gil_scoped_release>());

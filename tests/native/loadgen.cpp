@@ -323,6 +323,107 @@ std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_byte
   return lat;
 }
 
+std::vector<double> uds_pingpong_batched(int batches, int batch, int batch_gap_us, int req_bytes, int resp_bytes,
+                                         int server_poll_us) {
+  if (batches <= 0 || batch <= 0 || batch_gap_us < 0 || server_poll_us < 0 || req_bytes <= 0 || resp_bytes <= 0 ||
+      req_bytes > (1 << 20) || resp_bytes > (4 << 20))
+    throw std::invalid_argument("uds_pingpong_batched: bad arguments");
+  int sv[2];
+  if (socketpair(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0, sv) != 0)
+    throw std::runtime_error(std::string("socketpair: ") + strerror(errno));
+  const int cfd = sv[0], sfd = sv[1];
+  fcntl(sfd, F_SETFL, fcntl(sfd, F_GETFL) | O_NONBLOCK);
+  struct timeval tv {5, 0};
+  setsockopt(cfd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+  const int ep = epoll_create1(EPOLL_CLOEXEC);
+  struct epoll_event ev {};
+  ev.events = EPOLLIN | EPOLLRDHUP;
+  ev.data.fd = sfd;
+  epoll_ctl(ep, EPOLL_CTL_ADD, sfd, &ev);
+  // the plugin worker's policy: after a request, poll for server_poll_us, then sleep in
+  // epoll_wait (100 ms timeouts) until the next one
+  std::thread server([&] {
+    std::vector<char> in(static_cast<size_t>(req_bytes) + 65536), out(static_cast<size_t>(resp_bytes), 'r');
+    size_t have = 0;
+    epoll_event evs[4];
+    int64_t poll_until = 0;
+    for (;;) {
+      const bool polling = poll_until != 0;
+      const int k = epoll_wait(ep, evs, 4, polling ? 0 : 100);
+      if (k == 0 && polling) {
+        if (mono_ns() >= poll_until) poll_until = 0;
+        else cpu_relax();
+        continue;
+      }
+      if (k < 0 && errno != EINTR) return;
+      if (k <= 0) continue;
+      bool closed = false;
+      for (;;) {
+        const ssize_t r = recv(sfd, in.data() + have, in.size() - have, 0);
+        if (r > 0) {
+          have += static_cast<size_t>(r);
+          if (have >= in.size()) break;
+        } else if (r < 0 && errno == EINTR) {
+          continue;
+        } else {
+          if (r == 0 || errno != EAGAIN) closed = true;
+          break;
+        }
+      }
+      while (have >= static_cast<size_t>(req_bytes)) {
+        have -= static_cast<size_t>(req_bytes);
+        size_t off = 0;
+        while (off < out.size()) {
+          const ssize_t w = send(sfd, out.data() + off, out.size() - off, MSG_NOSIGNAL);
+          if (w > 0)
+            off += static_cast<size_t>(w);
+          else if (w < 0 && (errno == EAGAIN || errno == EINTR))
+            continue;
+          else
+            return;
+        }
+      }
+      if (server_poll_us > 0) poll_until = mono_ns() + static_cast<int64_t>(server_poll_us) * 1000;
+      if (closed) return;
+    }
+  });
+  std::vector<double> lat;
+  lat.reserve(static_cast<size_t>(batches) * batch);
+  const std::string req(static_cast<size_t>(req_bytes), 'q');
+  std::vector<char> buf(static_cast<size_t>(resp_bytes));
+  bool failed = false;
+  for (int b = 0; b < batches && !failed; ++b) {
+    std::this_thread::sleep_for(std::chrono::microseconds(batch_gap_us));
+    for (int i = 0; i < batch && !failed; ++i) {
+      const int64_t t0 = mono_ns();
+      if (send(cfd, req.data(), req.size(), MSG_NOSIGNAL) != static_cast<ssize_t>(req.size())) {
+        failed = true;
+        break;
+      }
+      size_t got = 0;
+      while (got < buf.size()) {
+        const ssize_t r = recv(cfd, buf.data() + got, buf.size() - got, 0);
+        if (r > 0) {
+          got += static_cast<size_t>(r);
+        } else if (r < 0 && errno == EINTR) {
+          continue;
+        } else {
+          failed = true;
+          break;
+        }
+      }
+      if (!failed) lat.push_back((mono_ns() - t0) * 1e-9);
+    }
+  }
+  shutdown(cfd, SHUT_RDWR);
+  server.join();
+  close(cfd);
+  close(sfd);
+  close(ep);
+  if (failed) throw std::runtime_error("uds_pingpong_batched: socket error");
+  return lat;
+}
+
 UdsPinger::UdsPinger(int req_bytes, int resp_bytes, int server_timeout_ms)
     : req_(static_cast<size_t>(req_bytes), 'q'), buf_(static_cast<size_t>(resp_bytes)) {
   if (req_bytes <= 0 || resp_bytes <= 0 || req_bytes > (1 << 20) || resp_bytes > (4 << 20) || server_timeout_ms < 0)

@@ -79,6 +79,13 @@ class FixtureBackend;
 std::vector<std::pair<int, double>> health_propagation(FixtureBackend& be, const std::string& socket_path, int gpu,
                                                        int events);
 
+// The bare exchange in the benchmark's rhythm: `batches` batches of `batch` back-to-back
+// exchanges, `batch_gap_us` apart, to a server thread that polls for `server_poll_us`
+// after each request and sleeps in epoll_wait otherwise (the plugin worker's policy):
+// the host's own tail for the pattern bench.py times Allocate in.
+std::vector<double> uds_pingpong_batched(int batches, int batch, int batch_gap_us, int req_bytes, int resp_bytes,
+                                         int server_poll_us);
+
 // n sequential unary calls on one connection; per-call latency in seconds.
 std::vector<double> h2_bench_unary(const std::string& socket_path, const std::string& path, const std::string& req,
                                    int n);
