@@ -78,7 +78,10 @@ def test_health_monitor_state_machine(n):
     assert [(x.gpu, x.healthy) for x in u] == [(1, 0)]
     assert not m.gpu_healthy(1) and m.gpu_healthy(0)
     m.process(n.HwEvent(n.EVT_ECC_UNCORRECTABLE, 1))
-    assert m.pop(10) == []  # still unhealthy, no transition
+    # still unhealthy, no transition; the new latch is reported (the manager persists it)
+    assert [(x.gpu, x.healthy, "(latched)" in x.reason) for x in m.pop(10)] == [(1, -1, True)]
+    m.process(n.HwEvent(n.EVT_ECC_UNCORRECTABLE, 1))
+    assert m.pop(10) == []  # the latch was already set: nothing new
     m.process(n.HwEvent(n.EVT_POST_RESET, 1))  # reset clears the ECC latch too
     assert [(x.gpu, x.healthy) for x in m.pop(100)] == [(1, 1)]
     m.process(n.HwEvent(n.EVT_LINK_DOWN, 0, peer=1))
