@@ -95,8 +95,9 @@ def _wait_http(port: int, timeout: float) -> None:
     raise TimeoutError("plugin web server did not come up on port %d" % port)
 
 
-TRACE_DTYPE = [("t_ready", "<i8"), ("t_dispatch", "<i8"), ("t_sent", "<i8"), ("conn", "<u8"), ("seq", "<u4"),
-               ("method", "u1"), ("spinning", "u1"), ("cpu", "<u2")]  # native/grpc_h2.h CallTraceEntry
+TRACE_DTYPE = [("t_ready", "<i8"), ("t_dispatch", "<i8"), ("t_sent", "<i8"), ("conn", "<u8"), ("idle_ns", "<i8"),
+               ("seq", "<u4"), ("method", "u1"), ("spinning", "u1"), ("cpu", "<u2"), ("prev_cpu", "<u2"),
+               ("pad0", "<u2"), ("pad1", "<u4")]  # native/grpc_h2.h CallTraceEntry (56 bytes)
 
 
 def read_call_trace(path: str):
@@ -185,6 +186,12 @@ def _tail_stats(batches, trace=None, rpc_allocate: int = 3) -> dict:
             out["matched"] = len(segs)
             out["segment_p50_us"] = {"inbound": round(seg_med[0] / 1e3, 2), "server": round(seg_med[1] / 1e3, 2),
                                      "outbound": round(seg_med[2] / 1e3, 2)}
+            # the server segment split at dispatch: recv + HTTP/2 + HPACK before it, the
+            # table, the response framing and send() (which wakes the client) after it
+            rp = [int(e["t_dispatch"]) - int(e["t_ready"]) for e in matched if e is not None]
+            hs = [int(e["t_sent"]) - int(e["t_dispatch"]) for e in matched if e is not None]
+            out["server_split_p50_us"] = {"recv_parse": round(float(np.median(rp)) / 1e3, 2),
+                                          "handle_send": round(float(np.median(hs)) / 1e3, 2)}
     causes = collections.Counter()
     excess = collections.defaultdict(list)
     slowest = []  # (latency s, cause, [inbound, server, outbound] us, worker was polling)
@@ -239,6 +246,7 @@ def _merge_tail(parts) -> dict:
     if parts and parts[0].get("segment_p50_us"):
         out["segment_p50_us"] = parts[0]["segment_p50_us"]
         out["cause_mean_excess_us"] = parts[0].get("cause_mean_excess_us")
+        out["server_split_p50_us"] = parts[0].get("server_split_p50_us")
     out["slowest"] = sorted((x for p in parts for x in p.get("slowest", [])), key=lambda r: -r["us"])[:8]
     return out
 

@@ -594,6 +594,8 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
   // worker was polling then, and the records of this batch still waiting for their send
   int64_t wake_ts = 0;
   bool wake_spin = false;
+  int64_t wake_idle = 0;      // the worker's time without work before this wake-up
+  uint16_t last_cpu = 0xFFFF;  // CPU of the worker's previous work
   std::vector<uint64_t> trace_pending;
   auto stamp_sent = [&] {
     const int64_t t = mono_ns();
@@ -640,8 +642,11 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
       e.method = static_cast<uint8_t>(m == kMAllocate ? kRpcAllocate : m == kMPreferred ? kRpcPreferred
                                       : m == kMOptions ? kRpcOptions : 255);
       e.spinning = wake_spin ? 1 : 0;
+      e.idle_ns = wake_idle;
       const int cpu = sched_getcpu();
       e.cpu = static_cast<uint16_t>(cpu < 0 ? 0xFFFF : cpu);
+      e.prev_cpu = last_cpu;
+      last_cpu = e.cpu;
       e.seq = static_cast<uint32_t>(idx + 1);
       trace_pending.push_back(idx);
     }
@@ -1110,12 +1115,18 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
           }
           warm_ticks_.fetch_add(1, std::memory_order_relaxed);
           last_activity = now;
+          if (trace_) {
+            const int cpu = sched_getcpu();
+            last_cpu = static_cast<uint16_t>(cpu < 0 ? 0xFFFF : cpu);
+          }
         }
       }
     }
     if (n > 0) {
-      last_activity = mono_ns();
-      wake_ts = last_activity;
+      const int64_t now = mono_ns();
+      wake_idle = now - last_activity;
+      last_activity = now;
+      wake_ts = now;
       wake_spin = polling;
     }
     bool law_tick = false;

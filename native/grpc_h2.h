@@ -37,12 +37,16 @@ struct CallTraceEntry {
   int64_t t_dispatch = 0;  // request decoded, handler entered
   int64_t t_sent = 0;      // response handed to send() (the worker's flush of the batch)
   uint64_t conn = 0;       // worker index << 48 | connection serial
+  int64_t idle_ns = 0;     // how long the worker had been without work (requests or keep-warm ticks)
   uint32_t seq = 0;        // write order + 1 (0: slot never written)
   uint8_t method = 0;      // Rpc
   uint8_t spinning = 0;    // 1: the worker was polling (busy-poll window), 0: it slept in epoll_wait
   uint16_t cpu = 0;        // CPU the worker ran on at dispatch
+  uint16_t prev_cpu = 0;   // CPU of the worker's previous work (0xFFFF: none yet)
+  uint16_t pad0 = 0;
+  uint32_t pad1 = 0;
 };
-static_assert(sizeof(CallTraceEntry) == 40, "trace record layout is read by bench.py");
+static_assert(sizeof(CallTraceEntry) == 56, "trace record layout is read by bench.py");
 struct CallTraceHeader {
   uint64_t magic = 0;      // kCallTraceMagic
   uint32_t version = 1;

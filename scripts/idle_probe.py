@@ -51,7 +51,13 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 KINDS = ("allocate", "preferred", "floor")
-SEGMENTS = ("inbound", "server", "outbound")
+SEGMENTS = ("inbound", "server_recv_parse", "server_handle_send", "outbound")
+
+
+def segments4(start, lat, e):
+    """bench.segments with the server part split at dispatch."""
+    inbound, _, outbound = bench.segments(start, lat, e)
+    return (inbound, int(e["t_dispatch"]) - int(e["t_ready"]), int(e["t_sent"]) - int(e["t_dispatch"]), outbound)
 
 
 def pct(xs, q):
@@ -69,6 +75,13 @@ def bootstrap_ci(diffs, n=2000, seed=7):
     k = len(diffs)
     meds = sorted(median([diffs[rng.randrange(k)] for _ in range(k)]) for _ in range(n))
     return meds[int(0.025 * n)], meds[int(0.975 * n)]
+
+
+def process_cpu_s(pid: int) -> float:
+    """utime + stime of the whole process, seconds."""
+    with open("/proc/%d/stat" % pid) as f:
+        fields = f.read().rsplit(")", 1)[1].split()
+    return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
 
 
 def median_shift(a, b, n=2000, seed=11):
@@ -157,6 +170,7 @@ class Daemon:
         self.h2 = n.H2Client(sock)
         self.h2.bench_unary(v1beta1.METHOD_ALLOCATE, self.alloc, 2000)  # warm the connection and the code
         self.tids = worker_tids(self.proc.pid)
+        self.cpu0 = (process_cpu_s(self.proc.pid), time.monotonic())
         import http.client
         self.mconn = http.client.HTTPConnection("127.0.0.1", self.port, timeout=10)
         self.base = {}
@@ -326,18 +340,28 @@ def main() -> int:
                 base = k.split("@")[0].split("#")[0]
                 rpc = n.RPC_ALLOCATE if base == "allocate" else n.RPC_PREFERRED
                 recs = bench.match_calls(d.starts[base], lat[k], bench.read_call_trace(d.trace_path), rpc)
-                seg = [bench.segments(st, x, e) for st, x, e in zip(d.starts[base], lat[k], recs) if e is not None]
+                seg = [segments4(st, x, e) for st, x, e in zip(d.starts[base], lat[k], recs) if e is not None]
                 if seg:
+                    got = [e for e in recs if e is not None]
                     row[k]["matched"] = len(seg)
                     row[k]["segments_p50_us"] = {name: round(median([s_[i] for s_ in seg]) / 1e3, 2)
                                                  for i, name in enumerate(SEGMENTS)}
-                    row[k]["worker_asleep_fraction"] = round(
-                        sum(1 for e in recs if e is not None and not e["spinning"]) / len(seg), 3)
+                    row[k]["worker_asleep_fraction"] = round(sum(1 for e in got if not e["spinning"]) / len(got), 3)
+                    # the worker woke on another CPU than its previous work (request or tick) ran on
+                    row[k]["worker_cpu_changed_fraction"] = round(
+                        sum(1 for e in got if e["prev_cpu"] != 0xFFFF and e["prev_cpu"] != e["cpu"]) / len(got), 3)
+                    row[k]["worker_idle_p50_ms"] = round(median([int(e["idle_ns"]) for e in got]) / 1e6, 3)
                     segs_by_gap.setdefault(k, {})[gap] = seg
                     lat_by_gap.setdefault(k, {})[gap] = [x for x, e in zip(lat[k], recs) if e is not None]
             res["rows"].append(row)
             print(json.dumps(row), flush=True)
         del pinger
+        # what each daemon cost while the probe ran (mostly idle: keep-warm ticks, telemetry)
+        res["daemon_cpu_percent"] = {}
+        for tag, d in daemons.items():
+            c0, t0 = d.cpu0
+            res["daemon_cpu_percent"][tag or "daemon"] = round(
+                100.0 * (process_cpu_s(d.proc.pid) - c0) / max(1e-9, time.monotonic() - t0), 3)
         # where the idle excess goes: each segment's median at the longest gap minus at the
         # shortest, with a bootstrap 95 % interval (independent samples resampled apart)
         res["attribution"] = {}
