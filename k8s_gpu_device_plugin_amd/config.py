@@ -136,7 +136,10 @@ class GrpcConfig:
     threads: int = 4
     busyPollUs: int = 50         # native server: keep polling this long after a request (0 = off)
     admissionPollUs: int = 1000  # ... and this long after a GetPreferredAllocation (its Allocate follows)
-    keepWarmMs: int = 10         # native server: idle workers with a connection replay canned requests (0 = off)
+    # native server: idle workers with a connection replay canned requests every keepWarmMs
+    # (0 = off); 1 ms also keeps the worker's core out of deep idle states, which is most
+    # of what a call after a long idle pays (profiles/r5/idle_ab_kw_10_1_0.json)
+    keepWarmMs: int = 1
     keepWarmFull: bool = True    # ... through the whole request path of an in-memory connection (else HPACK + table)
     # native server: per-call trace of unary RPCs in a file-backed ring ("" = off), read by
     # bench.py to attribute slow calls; one record per call, callTraceEntries records
