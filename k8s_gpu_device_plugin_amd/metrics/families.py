@@ -3,7 +3,8 @@
 The reference's ``metrics`` package is empty (``metrics/metrics.go:1``); its /metrics
 carries only the Go runtime/process collectors, ``go_build_info`` (``main.go:26-28``)
 and the echo HTTP families (``middleware/echo_metric.go:80-93``).  This registry is the
-single place that documents the MI355X plugin's families; ``tests/test_metrics_contract``
+single place that documents the MI355X plugin's families;
+``tests/test_topology_model.py::test_metrics_contract_both_ways``
 checks the native exporter against it in both directions.
 """
 from __future__ import annotations

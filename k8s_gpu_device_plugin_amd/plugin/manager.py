@@ -856,6 +856,8 @@ class PluginManager:
 
     def _apply_health(self, u) -> None:
         self.counters["health_events"] += 1
+        if u.kind == native.load().EVT_RESET_OBSERVED:  # a reset seen by polling, not by an event
+            self.counters["resets_observed"] = self.counters.get("resets_observed", 0) + 1
         key = self._key(u)
         if u.healthy in (0, 1):
             healthy = bool(u.healthy)

@@ -104,6 +104,7 @@ def test_polled_ue_latches_and_polled_reset_clears(make_cfg, plugin_dir):
             assert r.m.monitor.resets_observed == 1
             assert any(h == 1 and "gpu_reset_observed" in why or "firmware clock restarted" in why
                        for _, g, h, why in r.m.health_log if g == 1)
+            assert _wait(lambda: 'amdgpu_device_plugin_events_total{event="resets_observed"} 1' in r.m.exporter.render())
             assert _wait(lambda: _latched_gpus(plugin_dir) == [])
         finally:
             r.stop()
