@@ -222,10 +222,8 @@ class AmdDevicePlugin:
             nserver.set_table(self.table)  # workers switch tables and push ListAndWatch
         self._front[0] = self  # grpcio handlers serve from this plugin's table from now on
         prev.table.wake()      # grpcio ListAndWatch generators waiting on the old table
-        if server is not None:
-            self._supervisor = threading.Thread(target=self._supervise, args=(server,), daemon=True,
-                                                name="dp-supervise-" + self.resource.get_resource_name())
-            self._supervisor.start()
+        # (a grpcio server's supervisor thread follows _front: it now acts for this plugin)
+        self._supervisor, prev._supervisor = prev._supervisor, None
         # the predecessor's PreStartContainer loop answers what is queued on its table, then ends
         log.info("device table swapped into the running server", extra={"resourceName": str(self.resource),
                                                                         "devices": len(self)})
@@ -365,18 +363,22 @@ class AmdDevicePlugin:
 
     def _supervise(self, server) -> None:
         """grpcio analogue of the Serve crash-restart loop (``plugin/plugin.go:107-129``):
-        an unexpected termination restarts the server, >5 crashes within an hour is fatal."""
+        an unexpected termination restarts the server, >5 crashes within an hour is fatal.
+        One thread per server: it acts for whichever plugin serves from it now (a
+        successor that adopted the server is ``_front[0]``)."""
+        front = self._front
         while True:
             server.wait_for_termination()
-            with self._lock:
-                if self._stopping or self._server is not server:
+            owner = front[0]
+            with owner._lock:
+                if owner._stopping or owner._server is not server:
                     return
-            if self._note_crash("terminated unexpectedly"):
+            if owner._note_crash("terminated unexpectedly"):
                 return
-            with self._lock:
-                self._serving = False
+            with owner._lock:
+                owner._serving = False
                 try:
-                    self._start_grpcio_server_locked_restart()
+                    owner._start_grpcio_server_locked_restart()
                 except Exception as e:  # pragma: no cover
                     log.error("restart failed: %s", e)
                 return

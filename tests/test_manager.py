@@ -1043,3 +1043,20 @@ def test_allocate_never_fails_through_restarts_and_inventory_changes(make_cfg, p
         assert m.counters.get("restarts_inventory", 0) >= 5
         devs = w.last(timeout=5)
         assert len(devs) == len(m.plugins[0].table.ids())
+
+
+def test_grpcio_reloads_do_not_accumulate_threads(make_cfg, plugin_dir, run_manager):
+    """Each hitless reload of the grpcio server hands its supervisor thread over instead
+    of starting another one (one thread per server, whatever the number of reloads)."""
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(grpc={"server": "python"}))
+        k.wait_for_registrations(1)
+        names = lambda: [t.name for t in threading.enumerate() if t.name.startswith("dp-supervise-")]  # noqa: E731
+        assert len(names()) == 1
+        for _ in range(20):
+            reloads = m.counters["reloads"]
+            m.restart()
+            assert _wait(lambda: m.counters["reloads"] > reloads)
+        time.sleep(0.2)
+        assert len(names()) == 1, names()
+        assert k.client("amd-gpu.sock").get_options().get_preferred_allocation_available
