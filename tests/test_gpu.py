@@ -258,6 +258,50 @@ def test_plugin_end_to_end_on_mi355x(make_cfg, plugin_dir):
         k.stop()
 
 
+def test_restored_latch_on_real_gpu(make_cfg, plugin_dir, n, amdsmi_backend):
+    """The persisted uncorrectable-ECC latch end to end on the MI355X: a state file that
+    records the GPU's firmware start as it is now (no reset since) keeps the GPU Unhealthy
+    through a plugin start; one that records an hour-earlier start (the firmware restarted
+    since: a reset) is cleared by the first telemetry sample."""
+    import json
+
+    from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import KubeletStub
+    from k8s_gpu_device_plugin_amd.plugin.manager import PluginManager
+    from k8s_gpu_device_plugin_amd.plugin.state import read_boot_id
+    gpus, _ = amdsmi_backend.discover()
+    key = amdsmi_backend.gpu_key(0)
+    s = amdsmi_backend.sample(0)
+    assert s.fw_clock_s > 0
+    fw_boot = n.boottime_s() - s.fw_clock_s
+    path = os.path.join(plugin_dir, ".amdgpu-device-plugin", "health-state.json")
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+
+    def run(recorded):
+        with open(path, "w") as f:
+            json.dump({"version": 1, "boot_id": read_boot_id(), "gpus": {key: {"ecc": {
+                "last_ue": max(0, s.ecc_uncorrectable), "fw_boot_s": recorded, "reason": "gpu test latch",
+                "since_ns": 0}}}}, f)
+        cfg = make_cfg(backend="amdsmi", migStrategy="none", telemetry={"intervalMs": 100})
+        k = KubeletStub(plugin_dir).start()
+        mgr = PluginManager(cfg)
+        t = mgr.start_background()
+        try:
+            w = k.watch(k.wait_for_registrations(1, 20)[0].endpoint)
+            _, first = w.next(10)
+            assert mgr.counters.get("latches_restored") == 1
+            time.sleep(1.0)  # ten samples
+            return first, mgr.plugins[0].table.healthy_count(), mgr.counters.get("resets_observed", 0)
+        finally:
+            mgr.stop()
+            t.join(10)
+            k.stop()
+
+    first, healthy, resets = run(round(fw_boot))
+    assert first[0][1] == "Unhealthy" and healthy == 0 and resets == 0, (first, healthy, resets)
+    first, healthy, resets = run(round(fw_boot) - 3600)
+    assert first[0][1] == "Unhealthy" and healthy == 1 and resets == 1, (first, healthy, resets)
+
+
 def test_native_grpc_server_on_gpu_box(make_cfg, plugin_dir, n):
     assert hasattr(n, "GrpcServer"), "native gRPC server not built (fail loudly on the GPU box)"
     from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import KubeletStub
