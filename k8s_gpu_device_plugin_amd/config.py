@@ -143,9 +143,6 @@ class GrpcConfig:
     keepWarmFull: bool = True    # ... through the whole request path of an in-memory connection (else HPACK + table)
     # native server: per-call trace of unary RPCs in a file-backed ring ("" = off), read by
     # bench.py to attribute slow calls; one record per call, callTraceEntries records
-    # native server, busy-poll window: poll the connection that carried the last request
-    # with a direct recv on most spins instead of epoll_wait (one syscall less per request)
-    hotRecvPoll: bool = True
     callTraceFile: str = ""
     callTraceEntries: int = 65536
 

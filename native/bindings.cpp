@@ -701,7 +701,6 @@ PYBIND11_MODULE(_native, m) {
       .def("set_table", &GrpcServer::set_table, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("table_swaps", &GrpcServer::table_swaps)
       .def("set_call_trace", &GrpcServer::set_call_trace, py::arg("path"), py::arg("capacity") = 65536)
-      .def("set_hot_recv", &GrpcServer::set_hot_recv, py::arg("on"))
       .def("add_table", &GrpcServer::set_table)
       .def("start", &GrpcServer::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &GrpcServer::stop, py::call_guard<py::gil_scoped_release>())

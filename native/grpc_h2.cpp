@@ -233,10 +233,6 @@ struct GrpcServer::Worker {
 
 using Conn = GrpcServer::Worker::Conn;
 
-// Marks an event the worker made up after reading the data itself (never passed to the
-// kernel; the bit is an epoll *input* flag, EPOLLONESHOT, which epoll_wait never returns).
-constexpr uint32_t kPreRead = 1u << 30;
-
 namespace {
 
 void goaway(Conn& c, uint32_t code) {
@@ -543,16 +539,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
       if (*fd >= 0) ::close(*fd);
     }
   } spare_closer{&spare};
-  // The connection that carried the last request (busy-poll window only): polled with a
-  // direct non-blocking recv instead of epoll_wait on most spins, so a request that lands
-  // in the window is read by the call that sees it (one syscall on the critical path
-  // instead of epoll_wait + recv).  Every 8th spin still asks epoll, for the other
-  // connections, the eventfds and the listener.
-  int hot_fd = -1;
-  uint32_t spin_iter = 0;
-  const bool hot_poll = hot_recv_.load();
   auto close_conn = [&](int fd) {
-    if (fd == hot_fd) hot_fd = -1;
     epoll_ctl(w->ep, EPOLL_CTL_DEL, fd, nullptr);
     ::close(fd);
     w->conns.erase(fd);
@@ -1094,24 +1081,9 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
     int n;
     const bool polling = spin_until != 0;
     if (polling) {
-      n = 0;
-      if (hot_poll && hot_fd >= 0 && (++spin_iter & 7u) != 0) {
-        const ssize_t r = recv(hot_fd, rbuf, sizeof(rbuf), MSG_DONTWAIT);
-        if (r > 0) {
-          auto it = w->conns.find(hot_fd);
-          if (it != w->conns.end()) {
-            it->second->in.append(rbuf, static_cast<size_t>(r));
-            evs[0].data.fd = hot_fd;
-            // all of it read: the handler skips its own recv (a full buffer: it reads on)
-            evs[0].events = EPOLLIN | (static_cast<size_t>(r) < sizeof(rbuf) ? kPreRead : 0u);
-            n = 1;
-          }
-        } else if (r == 0 || (errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR)) {
-          hot_fd = -1;  // closed or failed: epoll reports it on the next spin
-        }
-      } else {
-        n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), 0);
-      }
+      // (polling the last request's connection with a direct recv instead, one syscall less
+      // on the request's path, measured slower: 2.87 vs 2.67 us p50, profiles/r5/ab_hot_recv.jsonl)
+      n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), 0);
       if (n == 0) {
         const int64_t now = mono_ns();
         if (now >= spin_until) {
@@ -1266,9 +1238,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
       }
       bool peer_closed = false;
       if (evs[i].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP)) {
-        if (!c->internal) hot_fd = fd;
         for (;;) {
-          if (evs[i].events & kPreRead) break;  // the hot-connection poll read it already
           const ssize_t r = recv(fd, rbuf, sizeof(rbuf), 0);
           if (r > 0) {
             c->in.append(rbuf, static_cast<size_t>(r));

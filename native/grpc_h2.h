@@ -110,10 +110,6 @@ class GrpcServer {
   // in-memory connection (frame parsing, HPACK, dispatch, table, response framing);
   // otherwise only the HPACK decode and the table calls
   void set_keep_warm_full(bool on) { keep_warm_full_.store(on); }
-  // Busy-poll window: read the connection that carried the last request with a direct
-  // non-blocking recv on most spins instead of epoll_wait (grpc.hotRecvPoll).  Read by a
-  // worker when it starts.
-  void set_hot_recv(bool on) { hot_recv_.store(on); }
   uint64_t warm_ticks() const { return warm_ticks_.load(); }
   std::vector<int> worker_connections() const;  // connections owned per worker thread
   const std::string& socket_path() const { return path_; }
@@ -147,7 +143,6 @@ class GrpcServer {
   int admission_poll_us_;
   std::atomic<int> keep_warm_ms_{0};
   std::atomic<bool> keep_warm_full_{true};
-  std::atomic<bool> hot_recv_{true};
   std::atomic<uint64_t> warm_ticks_{0};
   // table_ and table_gen_ change together under swap_mu_ (never held across anything else);
   // workers poll table_gen_ (one relaxed load per loop) and take table_ when it moved
