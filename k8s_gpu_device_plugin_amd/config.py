@@ -140,6 +140,9 @@ class GrpcConfig:
     # (0 = off); 1 ms also keeps the worker's core out of deep idle states, which is most
     # of what a call after a long idle pays (profiles/r5/idle_ab_kw_10_1_0.json)
     keepWarmMs: int = 1
+    # native server: a worker holding a connection wakes at least this often, doing nothing
+    # (0 = off): keeps its core out of deep idle states without running the request path
+    idleWakeMs: int = 0
     keepWarmFull: bool = True    # ... through the whole request path of an in-memory connection (else HPACK + table)
     # native server: per-call trace of unary RPCs in a file-backed ring ("" = off), read by
     # bench.py to attribute slow calls; one record per call, callTraceEntries records

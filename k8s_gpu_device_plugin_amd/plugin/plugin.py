@@ -304,6 +304,7 @@ class AmdDevicePlugin:
         if self.cfg is not None:
             srv.set_keep_warm_ms(int(self.cfg.grpc.keepWarmMs))
             srv.set_keep_warm_full(bool(self.cfg.grpc.keepWarmFull))
+            srv.set_idle_wake_ms(int(self.cfg.grpc.idleWakeMs))
             if self.cfg.grpc.callTraceFile:
                 srv.set_call_trace(self.cfg.grpc.callTraceFile.replace("{resource}", self.resource.get_resource_name()),
                                    int(self.cfg.grpc.callTraceEntries))

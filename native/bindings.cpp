@@ -701,6 +701,7 @@ PYBIND11_MODULE(_native, m) {
       .def("set_table", &GrpcServer::set_table, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("table_swaps", &GrpcServer::table_swaps)
       .def("set_call_trace", &GrpcServer::set_call_trace, py::arg("path"), py::arg("capacity") = 65536)
+      .def("set_idle_wake_ms", &GrpcServer::set_idle_wake_ms, py::arg("ms"))
       .def("add_table", &GrpcServer::set_table)
       .def("start", &GrpcServer::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &GrpcServer::stop, py::call_guard<py::gil_scoped_release>())

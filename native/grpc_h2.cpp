@@ -1100,7 +1100,12 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
       }
     } else {
       const int warm = keep_warm_ms_.load(std::memory_order_relaxed);
-      n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), warm > 0 ? std::min(warm, 100) : 100);
+      // a worker that holds a connection wakes at least every idle_wake_ms (keeps its core
+      // out of deep idle states: what the first request after a long idle pays most of)
+      const int wake = w->conns.empty() ? 0 : idle_wake_ms_.load(std::memory_order_relaxed);
+      int timeout = warm > 0 ? std::min(warm, 100) : 100;
+      if (wake > 0) timeout = std::min(timeout, wake);
+      n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), timeout);
       if (n == 0 && warm > 0 && !w->conns.empty() && !warm_alloc.empty()) {
         const int64_t now = mono_ns();
         if (now - last_activity >= static_cast<int64_t>(warm) * 1000000) {

@@ -111,6 +111,10 @@ class GrpcServer {
   // otherwise only the HPACK decode and the table calls
   void set_keep_warm_full(bool on) { keep_warm_full_.store(on); }
   uint64_t warm_ticks() const { return warm_ticks_.load(); }
+  // A worker that holds a connection sleeps at most this long at a time (0 = only the
+  // keep-warm period / 100 ms): the wake-ups alone, no work, keep its core from settling
+  // into a deep idle state whose exit the next request would pay (grpc.idleWakeMs).
+  void set_idle_wake_ms(int ms) { idle_wake_ms_.store(ms > 0 ? ms : 0); }
   std::vector<int> worker_connections() const;  // connections owned per worker thread
   const std::string& socket_path() const { return path_; }
 
@@ -143,6 +147,7 @@ class GrpcServer {
   int admission_poll_us_;
   std::atomic<int> keep_warm_ms_{0};
   std::atomic<bool> keep_warm_full_{true};
+  std::atomic<int> idle_wake_ms_{0};
   std::atomic<uint64_t> warm_ticks_{0};
   // table_ and table_gen_ change together under swap_mu_ (never held across anything else);
   // workers poll table_gen_ (one relaxed load per loop) and take table_ when it moved
