@@ -137,12 +137,13 @@ class GrpcConfig:
     busyPollUs: int = 50         # native server: keep polling this long after a request (0 = off)
     admissionPollUs: int = 1000  # ... and this long after a GetPreferredAllocation (its Allocate follows)
     # native server: idle workers with a connection replay canned requests every keepWarmMs
-    # (0 = off); 1 ms also keeps the worker's core out of deep idle states, which is most
-    # of what a call after a long idle pays (profiles/r5/idle_ab_kw_10_1_0.json)
-    keepWarmMs: int = 1
+    # (0 = off), so kubelet's sparse calls find that code and data cached
+    keepWarmMs: int = 10
     # native server: a worker holding a connection wakes at least this often, doing nothing
-    # (0 = off): keeps its core out of deep idle states without running the request path
-    idleWakeMs: int = 0
+    # (0 = off): keeps its core out of deep idle states, which is most of what a call after
+    # a long idle pays, at half the CPU of a 1 ms keepWarmMs and without its collisions
+    # with calls 1 ms apart (profiles/r5/idle_ab_wake.json, ab_wake_bench.jsonl)
+    idleWakeMs: int = 1
     keepWarmFull: bool = True    # ... through the whole request path of an in-memory connection (else HPACK + table)
     # native server: per-call trace of unary RPCs in a file-backed ring ("" = off), read by
     # bench.py to attribute slow calls; one record per call, callTraceEntries records
@@ -192,6 +193,11 @@ class Config:
     podResources: PodResourcesConfig = field(default_factory=PodResourcesConfig)
     allocator: AllocatorConfig = field(default_factory=AllocatorConfig)
     retrySeconds: float = 30.0            # plugin start retry (plugin/manager.go:135-138)
+    # scheduling policy of the background threads (sampler, watchdog, driver lanes, event
+    # wait, manager helpers): "batch" = SCHED_BATCH, which never preempts a gRPC worker on
+    # wake-up; "normal" = SCHED_OTHER.  On an idle MI355X box the Allocate tail was the same
+    # either way (profiles/r5/ab_sched.jsonl), so the default stays normal
+    backgroundSched: str = "normal"
 
     @property
     def strategy(self) -> str:
@@ -372,6 +378,8 @@ def validate(cfg: Config) -> Config:
         raise ConfigError("http.server must be native|python")
     if cfg.podResources.intervalS <= 0:
         raise ConfigError("podResources.intervalS must be > 0")
+    if cfg.backgroundSched not in ("batch", "normal"):
+        raise ConfigError("backgroundSched must be batch|normal, got %r" % cfg.backgroundSched)
     if cfg.telemetry.intervalMs < 10:
         raise ConfigError("telemetry.intervalMs must be >= 10")
     if not cfg.resourcePrefix or "/" in cfg.resourcePrefix:

@@ -122,6 +122,7 @@ class Discoverer:
         self._thread.join(1.0)  # a discovery stuck in the driver stays behind (daemon)
 
     def _run(self) -> None:
+        background_thread()
         while True:
             with self._cv:
                 while self._want is None and not self._stop:
@@ -145,9 +146,28 @@ class Discoverer:
             self.first_done.set()
 
 
+def background_thread() -> None:
+    """The calling helper thread runs SCHED_BATCH (config ``backgroundSched``): it never
+    preempts a gRPC worker when it wakes.  Native servers started from it switch their
+    workers back to SCHED_OTHER (``foreground_thread`` in native/common.cpp)."""
+    if native.load().background_batch():
+        try:
+            os.sched_setscheduler(0, os.SCHED_BATCH, os.sched_param(0))  # 0: this thread
+        except (OSError, AttributeError):
+            pass
+
+
+def _as_background(fn):
+    def run():
+        background_thread()
+        fn()
+    return run
+
+
 class PluginManager:
     def __init__(self, cfg, ready: CloseOnce | None = None, backend=None) -> None:
         n = native.load()
+        n.set_background_batch(getattr(cfg, "backgroundSched", "normal") == "batch")
         self.cfg = cfg
         self.ready = ready if ready is not None else CloseOnce()
         self.backend = backend if backend is not None else make_backend(cfg)
@@ -868,7 +888,8 @@ class PluginManager:
                 self._held_unhealthy.add(key)
                 if self._verify_pool is None:
                     self._verify_pool = concurrent.futures.ThreadPoolExecutor(max_workers=4,
-                                                                              thread_name_prefix="canary")
+                                                                              thread_name_prefix="canary",
+                                                                              initializer=background_thread)
                 self._verify_pool.submit(self._verify_and_post, u, key, gen)
                 return
             if healthy:
@@ -975,7 +996,8 @@ class PluginManager:
 
     def _start_canary_pool(self) -> concurrent.futures.ThreadPoolExecutor:
         if self._canary_pool is None:
-            self._canary_pool = concurrent.futures.ThreadPoolExecutor(max_workers=8, thread_name_prefix="canary-start")
+            self._canary_pool = concurrent.futures.ThreadPoolExecutor(max_workers=8, thread_name_prefix="canary-start",
+                                                                      initializer=background_thread)
         return self._canary_pool
 
     def _in_use_partitions(self, device_map) -> set:
@@ -1055,7 +1077,8 @@ class PluginManager:
         import types
         gen = self._health_gen[key] = self._health_gen.get(key, 0) + 1
         if self._verify_pool is None:
-            self._verify_pool = concurrent.futures.ThreadPoolExecutor(max_workers=4, thread_name_prefix="canary")
+            self._verify_pool = concurrent.futures.ThreadPoolExecutor(max_workers=4, thread_name_prefix="canary",
+                                                                     initializer=background_thread)
         self._held_unhealthy.add(key)
         self._verify_pool.submit(self._verify_and_post, types.SimpleNamespace(partition=partition, reason=reason),
                                  key, gen)
@@ -1170,7 +1193,7 @@ class PluginManager:
                 self.events.put((EV_REDISCOVER,))
 
         for fn, name in ((watch_loop, "fs-watch"), (health_loop, "health-pump"), (rediscover_loop, "rediscover")):
-            t = threading.Thread(target=fn, name=name, daemon=True)
+            t = threading.Thread(target=_as_background(fn), name=name, daemon=True)
             t.start()
             self._threads.append(t)
         if self.cfg.podResources.enabled:

@@ -154,6 +154,8 @@ class PodResourcesWatcher:
 
     def start(self) -> None:
         def loop():
+            from .manager import background_thread
+            background_thread()
             while not self._stop.is_set():
                 if self.poll_once():
                     self.on_change()

@@ -422,6 +422,17 @@ bool amdsmi_probe_held();
 int64_t now_ns();
 int64_t mono_ns();
 
+// Background threads (sampler, watchdog, lanes, event wait, access log) name themselves
+// and, with set_background_batch(true), switch to SCHED_BATCH: still a fair share of the
+// CPU, but a batch thread that wakes never preempts the thread running on its CPU.  Off by
+// default (config backgroundSched): on an idle box it did not change the Allocate tail.
+// Threads started before the switch keep their policy.
+void set_background_batch(bool on);
+bool background_batch();
+int64_t background_batched_threads();  // threads switched so far
+void background_thread(const char* name);
+void foreground_thread();  // back to SCHED_OTHER if the creator was a batch thread
+
 // accept4 (non-blocking, close-on-exec) for a level-triggered listener that sheds load
 // instead of spinning when the process runs out of file descriptors: the pending
 // connection would stay in the backlog and keep the listener readable, and every

@@ -390,6 +390,9 @@ PYBIND11_MODULE(_native, m) {
         return pods;
       });
   m.def("mono_ns", &mono_ns);
+  m.def("set_background_batch", &set_background_batch, py::arg("on"));
+  m.def("background_batch", &background_batch);
+  m.def("background_batched_threads", &background_batched_threads);
   m.def("distributed_alloc", [](const std::vector<AllocDevice>& d, const std::vector<int>& avail,
                                 const std::vector<int>& req, int size) {
     AllocResult r = distributed_alloc(d, avail, req, size);

@@ -1,8 +1,11 @@
 #include <fcntl.h>
+#include <pthread.h>
+#include <sched.h>
 #include <sys/socket.h>
 #include <time.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <cerrno>
 #include <ctime>
 
@@ -41,6 +44,33 @@ int64_t mono_ns() {
   struct timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
   return static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
+}
+
+namespace {
+std::atomic<bool> g_background_batch{false};
+std::atomic<int64_t> g_background_batched{0};
+}  // namespace
+
+void set_background_batch(bool on) { g_background_batch.store(on, std::memory_order_relaxed); }
+bool background_batch() { return g_background_batch.load(std::memory_order_relaxed); }
+int64_t background_batched_threads() { return g_background_batched.load(std::memory_order_relaxed); }
+
+void background_thread(const char* name) {
+  if (name && *name) pthread_setname_np(pthread_self(), name);
+  if (!g_background_batch.load(std::memory_order_relaxed)) return;
+  struct sched_param sp {};
+  sp.sched_priority = 0;
+  // a non-real-time policy change needs no privilege; failure leaves SCHED_OTHER
+  if (pthread_setschedparam(pthread_self(), SCHED_BATCH, &sp) == 0)
+    g_background_batched.fetch_add(1, std::memory_order_relaxed);
+}
+
+void foreground_thread() {
+  // threads inherit the creator's policy: a server started from a batch thread must not
+  // serve as one
+  if (sched_getscheduler(0) != SCHED_BATCH) return;
+  struct sched_param sp {};
+  pthread_setschedparam(pthread_self(), SCHED_OTHER, &sp);
 }
 
 const char* event_kind_name(int kind) {

@@ -427,6 +427,7 @@ void GrpcServer::start() {
     threads_.emplace_back([this, wp = workers_[i].get(), t = table, gen, i] {
       // named, so /proc/<pid>/task/*/comm tells the workers apart (scripts/idle_probe.py)
       pthread_setname_np(pthread_self(), ("dpgrpc-" + std::to_string(i)).c_str());
+      foreground_thread();
       run_guarded(wp, t, gen);
     });
   std::lock_guard<std::mutex> nk(notifier_->mu);

@@ -58,6 +58,7 @@ void HealthMonitor::start() {
     // arming talks to every GPU (on their lanes, bounded): the event thread does it, so
     // nothing that needs mu_ waits on a wedged GPU
     thread_ = std::thread([this, armed] {
+      background_thread("dpevents");
       backend_->arm_events();
       armed->set();
       loop();

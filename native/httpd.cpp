@@ -212,6 +212,7 @@ int HttpServer::start() {
     Worker* w = workers_[t].get();
     threads_.emplace_back([this, w, t] {
       pthread_setname_np(pthread_self(), ("dphttp-" + std::to_string(t)).c_str());
+      foreground_thread();
       std::vector<epoll_event> evs(128);
       char rbuf[16384];
       int spare = -1;  // reserve descriptor for accept_or_shed
@@ -510,6 +511,7 @@ int HttpServer::start() {
   }
   if (cfg_.access_log) {
     log_thread_ = std::thread([this] {
+      background_thread("dpaccesslog");
       while (!stop_.load()) {
         std::this_thread::sleep_for(std::chrono::milliseconds(100));
         flush_log();

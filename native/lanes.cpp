@@ -74,6 +74,7 @@ Lane::~Lane() {
 }
 
 void Lane::loop(std::shared_ptr<Shared> s) {
+  background_thread("dplane");
   for (;;) {
     std::shared_ptr<LaneJob> job;
     {

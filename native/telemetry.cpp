@@ -247,6 +247,7 @@ double Exporter::sample_age_s(int gpu) const {
 // the first (a library that serialises every device) and is reported "blocked".  Each
 // stuck call is reported once; the GPU recovers through on_sample once a sample returns.
 void Exporter::watchdog_loop(std::shared_ptr<HealthMonitor> monitor) {
+  background_thread("dpwatchdog");
   std::map<std::string, int64_t> reported;  // key -> since of the call reported lost
   while (!stop_.load()) {
     std::this_thread::sleep_for(std::chrono::milliseconds(25));
@@ -326,6 +327,7 @@ void Exporter::watchdog_loop(std::shared_ptr<HealthMonitor> monitor) {
 
 void Exporter::sampler_main(std::weak_ptr<Exporter> weak, std::shared_ptr<ThreadExit> exit, uint64_t gen,
                             int interval_ms) {
+  background_thread("dpsampler");
   // A strong reference only for the duration of each step: the exporter stays alive
   // through a backend call (however long it blocks), and may be destroyed between
   // steps, by whichever thread drops the last reference.  Nothing below touches it

@@ -1060,3 +1060,41 @@ def test_grpcio_reloads_do_not_accumulate_threads(make_cfg, plugin_dir, run_mana
         time.sleep(0.2)
         assert len(names()) == 1, names()
         assert k.client("amd-gpu.sock").get_options().get_preferred_allocation_available
+
+
+def _thread_policies(exclude=frozenset()):
+    """{comm: {policy, ...}} of this process's threads not in `exclude` (stat field 41:
+    0 OTHER, 3 BATCH)."""
+    out: dict = {}
+    for tid in set(os.listdir("/proc/self/task")) - exclude:
+        try:
+            with open("/proc/self/task/%s/stat" % tid) as f:
+                stat = f.read()
+        except OSError:
+            continue
+        comm = stat[stat.index("(") + 1:stat.rindex(")")]
+        policy = int(stat[stat.rindex(")") + 2:].split()[38])
+        out.setdefault(comm.rstrip("0123456789-"), set()).add(policy)
+    return out
+
+
+@pytest.mark.parametrize("sched", ["batch", "normal"])
+def test_background_threads_never_preempt_grpc_workers(make_cfg, plugin_dir, run_manager, sched):
+    """Sampler, watchdog, lanes and the event thread run SCHED_BATCH (a waking batch
+    thread does not preempt a worker mid-request); the gRPC and HTTP workers stay
+    SCHED_OTHER even when started from a batch thread."""
+    from k8s_gpu_device_plugin_amd import native
+    before = frozenset(os.listdir("/proc/self/task"))  # earlier tests' lanes may linger
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(backgroundSched=sched, grpc={"server": "native"}, http={"server": "native"}))
+        k.wait_for_registrations(1)
+        assert m.running
+        want = 3 if sched == "batch" else 0
+        assert _wait(lambda: {"dpsampler", "dpwatchdog", "dplane", "dpevents", "dpgrpc"} <= set(_thread_policies(before)))
+        pol = _thread_policies(before)
+        for name in ("dpsampler", "dpwatchdog", "dplane", "dpevents"):
+            assert pol[name] == {want}, (name, pol)
+        assert pol["dpgrpc"] == {0}, pol
+        if "dphttp" in pol:
+            assert pol["dphttp"] == {0}, pol
+        assert native.load().background_batch() == (sched == "batch")
