@@ -42,6 +42,14 @@ def read_boot_id(path: str | None = None) -> str:
         return ""
 
 
+def _i64(v) -> int:
+    """int(v) that fits the native latch's int64 fields (ValueError otherwise)."""
+    i = int(v)
+    if not -(1 << 63) <= i < (1 << 63):
+        raise ValueError("%r out of range" % v)
+    return i
+
+
 class HealthState:
     """Reader/writer of the state file.  ``snapshot`` dicts look like::
 
@@ -75,19 +83,27 @@ class HealthState:
                      "starting without its latches", self.path)
             return None
         snap = {"ecc": {}, "canary_failed": {}, "held": []}
-        for key, g in (raw.get("gpus") or {}).items():
+        gpus = raw.get("gpus")
+        for key, g in (gpus.items() if isinstance(gpus, dict) else ()):
             if not isinstance(g, dict):
                 continue
-            ecc = g.get("ecc")
+            try:  # a damaged entry costs that GPU its latches, never the start-up
+                ecc = g.get("ecc")
+                if isinstance(ecc, dict):
+                    fw = ecc.get("fw_boot_s")
+                    e = {"last_ue": _i64(ecc.get("last_ue", -1)),
+                         "fw_boot_s": None if fw is None else float(fw),
+                         "reason": str(ecc.get("reason", "")),
+                         "since_ns": _i64(ecc.get("since_ns", 0))}
+                parts = g.get("canary_failed_partitions")
+                parts = sorted({int(p) for p in parts}) if isinstance(parts, list) and parts else None
+            except (TypeError, ValueError, OverflowError) as err:
+                log.warning("ignoring the damaged health state of %s in %s: %s", key, self.path, err)
+                continue
             if isinstance(ecc, dict):
-                fw = ecc.get("fw_boot_s")
-                snap["ecc"][str(key)] = {"last_ue": int(ecc.get("last_ue", -1)),
-                                         "fw_boot_s": None if fw is None else float(fw),
-                                         "reason": str(ecc.get("reason", "")),
-                                         "since_ns": int(ecc.get("since_ns", 0))}
-            parts = g.get("canary_failed_partitions")
-            if isinstance(parts, list) and parts:
-                snap["canary_failed"][str(key)] = sorted({int(p) for p in parts})
+                snap["ecc"][str(key)] = e
+            if parts:
+                snap["canary_failed"][str(key)] = parts
             if g.get("recovery_canary_held"):
                 snap["held"].append(str(key))
         self._written = snap

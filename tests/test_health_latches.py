@@ -102,8 +102,9 @@ def test_polled_ue_latches_and_polled_reset_clears(make_cfg, plugin_dir):
             r.be.reset_firmware(1)  # the GPU is reset: its firmware clock starts again
             assert _wait(lambda: r.healthy(1)), "firmware clock restart not taken as a reset"
             assert r.m.monitor.resets_observed == 1
-            assert any(h == 1 and "gpu_reset_observed" in why or "firmware clock restarted" in why
-                       for _, g, h, why in r.m.health_log if g == 1)
+            # the table turns Healthy on the monitor's fast path; the manager logs it after
+            assert _wait(lambda: any(h == 1 and ("gpu_reset_observed" in why or "firmware clock restarted" in why)
+                                     for _, g, h, why in list(r.m.health_log) if g == 1))
             assert _wait(lambda: 'amdgpu_device_plugin_events_total{event="resets_observed"} 1' in r.m.exporter.render())
             assert _wait(lambda: _latched_gpus(plugin_dir) == [])
         finally:
@@ -291,3 +292,44 @@ def test_ue_on_a_gpu_already_unhealthy_is_still_persisted(make_cfg, plugin_dir):
             assert not r.healthy(1)  # the UE latch holds it
         finally:
             r.stop()
+
+
+def test_damaged_state_file_never_breaks_startup(tmp_path):
+    """Any JSON in the state file loads (damaged entries dropped, good ones kept), and a
+    file that is not JSON at all is ignored."""
+    from hypothesis import given, settings, strategies as st
+    from k8s_gpu_device_plugin_amd import native
+    from k8s_gpu_device_plugin_amd.plugin.state import VERSION, HealthState
+
+    n = native.load()
+    path = str(tmp_path / "health-state.json")
+    scalars = st.one_of(st.none(), st.booleans(), st.integers(), st.floats(allow_nan=True), st.text(max_size=8))
+    values = st.recursive(scalars, lambda c: st.one_of(st.lists(c, max_size=3),
+                                                       st.dictionaries(st.text(max_size=6), c, max_size=3)),
+                          max_leaves=8)
+    entry = st.fixed_dictionaries({}, optional={"ecc": st.one_of(values, st.dictionaries(
+        st.sampled_from(["last_ue", "fw_boot_s", "reason", "since_ns"]), scalars)),
+        "canary_failed_partitions": values, "recovery_canary_held": values})
+
+    @settings(max_examples=200, deadline=None)
+    @given(gpus=st.one_of(values, st.dictionaries(st.text(max_size=6), st.one_of(entry, values), max_size=4)))
+    def check(gpus):
+        with open(path, "w") as f:
+            json.dump({"version": VERSION, "boot_id": "b", "gpus": gpus}, f)
+        snap = HealthState(path, boot_id="b").load()
+        assert snap is not None and set(snap) == {"ecc", "canary_failed", "held"}
+        for k, e in snap["ecc"].items():  # what the manager hands the native latch
+            n.HealthLatch(k, e["last_ue"], float("nan") if e["fw_boot_s"] is None else e["fw_boot_s"],
+                          e["reason"], e["since_ns"])
+
+    check()
+    good = {"GPU-1": {"ecc": {"last_ue": 3, "fw_boot_s": -175.0, "reason": "ue", "since_ns": 7}},
+            "GPU-2": {"ecc": {"last_ue": "three"}}, "GPU-4": {"ecc": {"since_ns": 1 << 70}}, "GPU-3": {"canary_failed_partitions": [1, "x"]}}
+    with open(path, "w") as f:
+        json.dump({"version": VERSION, "boot_id": "b", "gpus": good}, f)
+    snap = HealthState(path, boot_id="b").load()
+    assert snap["ecc"] == {"GPU-1": {"last_ue": 3, "fw_boot_s": -175.0, "reason": "ue", "since_ns": 7}}
+    assert snap["canary_failed"] == {}
+    with open(path, "w") as f:
+        f.write("{not json")
+    assert HealthState(path, boot_id="b").load() is None
