@@ -398,6 +398,80 @@ def test_keep_warm_ticks_are_invisible_to_kubelet_and_metrics(n, plugin_dir, ful
         srv.stop()
 
 
+def _switches(tids):
+    """voluntary context switches of each thread in `tids` (a sleeping worker's wake-ups)."""
+    out = {}
+    for tid in tids:
+        try:
+            with open("/proc/self/task/%s/status" % tid) as f:
+                for ln in f:
+                    if ln.startswith("voluntary_ctxt_switches:"):
+                        out[tid] = int(ln.split()[1])
+        except OSError:
+            pass
+    return out
+
+
+def _grpc_workers(exclude):
+    tids = []
+    for tid in set(os.listdir("/proc/self/task")) - exclude:
+        try:
+            with open("/proc/self/task/%s/comm" % tid) as f:
+                if f.read().startswith("dpgrpc"):
+                    tids.append(tid)
+        except OSError:
+            pass
+    return tids
+
+
+def test_idle_wake_wakes_only_the_worker_holding_a_connection(n, plugin_dir):
+    """grpc.idleWakeMs: the worker that holds kubelet's connection wakes every idle
+    millisecond (its core stays out of deep idle states) without running the request path
+    (no keep-warm tick, no request); workers without a connection keep their 100 ms sleep."""
+    tc = n.TableConfig()
+    devs = [n.TableDevice("dev-%d" % i, i, 0, 0, -1, ["/dev/dri/renderD%d" % (128 + i)], True) for i in range(2)]
+    table = n.DeviceTable(tc, devs, n.Topology(2))
+    path = os.path.join(plugin_dir, "amd-gpu.sock")
+    before = set(os.listdir("/proc/self/task"))
+    srv = n.GrpcServer(path, 2, busy_poll_us=0, admission_poll_us=0)
+    srv.set_keep_warm_ms(0)
+    srv.set_idle_wake_ms(1)
+    srv.set_table(table)
+    srv.start()
+    try:
+        deadline = time.monotonic() + 5
+        while len(_grpc_workers(before)) < 2 and time.monotonic() < deadline:
+            time.sleep(0.01)
+        workers = _grpc_workers(before)
+        assert len(workers) == 2
+        s0 = _switches(workers)
+        time.sleep(0.3)
+        s1 = _switches(workers)
+        assert max(s1[t] - s0[t] for t in workers) <= 12, "woke without a connection: %s %s" % (s0, s1)
+        c = n.H2Client(path)
+        req = v1beta1.AllocateRequest(container_requests=[v1beta1.ContainerAllocateRequest(
+            devices_ids=["dev-1"])]).SerializeToString()
+        assert c.unary(v1beta1.METHOD_ALLOCATE, req)[0] == 0
+        requests = srv.requests
+        time.sleep(0.05)
+        s0 = _switches(workers)
+        time.sleep(0.4)
+        s1 = _switches(workers)
+        d = sorted(s1[t] - s0[t] for t in workers)
+        assert d[-1] >= 100 and d[0] <= 12, d  # the holder ~400 wake-ups, the other ~4
+        assert srv.warm_ticks == 0 and srv.requests == requests
+        srv.set_idle_wake_ms(0)
+        time.sleep(0.15)
+        s0 = _switches(workers)
+        time.sleep(0.3)
+        s1 = _switches(workers)
+        assert max(s1[t] - s0[t] for t in workers) <= 12
+        assert c.unary(v1beta1.METHOD_ALLOCATE, req)[0] == 0
+        c.close()
+    finally:
+        srv.stop()
+
+
 def test_connections_spread_over_workers(n, plugin_dir):
     """Concurrent kubelet-side clients (bench ranks, kubelet + a debugging client) are
     owned by different worker threads, not queued behind one that accepted them all."""
