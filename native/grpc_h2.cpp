@@ -342,6 +342,10 @@ void GrpcServer::set_call_trace(const std::string& path, int capacity) {
   void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
   ::close(fd);
   if (p == MAP_FAILED) throw std::runtime_error("set_call_trace: mmap: " + std::string(strerror(errno)));
+  // write every page now: a page's first write faults (page-cache allocation, the file
+  // system's page_mkwrite), and in the ring that happened inside every 73rd request
+  // (0.017 minor faults per call in the idle probe's daemon counters)
+  std::memset(p, 0, bytes);
   if (trace_hdr_) munmap(trace_hdr_, trace_bytes_);
   trace_hdr_ = new (p) CallTraceHeader();
   trace_hdr_->capacity = static_cast<uint32_t>(capacity);
