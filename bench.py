@@ -265,6 +265,20 @@ def _server_mean(text: str, rpc: str):
     return tot / cnt if cnt else None
 
 
+def _scrape_server_mean(text: str):
+    """Mean of the daemon's echo_http_request_duration_seconds for GET /metrics: from a
+    parsed request to its answer handed to the kernel (render + sendmsg)."""
+    tot = cnt = 0.0
+    for line in text.splitlines():
+        if 'handler="/metrics"' not in line or 'method="GET"' not in line:
+            continue
+        if line.startswith("echo_http_request_duration_seconds_sum"):
+            tot += float(line.rsplit(" ", 1)[1])
+        elif line.startswith("echo_http_request_duration_seconds_count"):
+            cnt += float(line.rsplit(" ", 1)[1])
+    return tot / cnt if cnt else None
+
+
 def _allocator_probe(n) -> float:
     """The xGMI allocator's own cost for a size-4 request over an 8-GPU mesh (two NUMA
     nodes), timed natively.  On a 1-GPU box the kubelet GetPreferredAllocation above
@@ -592,7 +606,9 @@ def main() -> int:
                                         0.5)
     if rank == 0:  # the daemon's own time per Allocate (decode, lookup, encode), from its histogram
         conn.request("GET", "/metrics")
-        mine["server_allocate_mean_s"] = _server_mean(conn.getresponse().read().decode(), "Allocate")
+        text = conn.getresponse().read().decode()
+        mine["server_allocate_mean_s"] = _server_mean(text, "Allocate")
+        mine["server_scrape_mean_s"] = _scrape_server_mean(text)
     if world > 1:
         gathered = [None] * world
         dist.all_gather_object(gathered, mine)
@@ -652,6 +668,9 @@ def main() -> int:
             "scrape_p50_us": round(_pct(scrapes, 0.5) * 1e6, 2),
             "scrape_rps": round(len(scrapes) / scrape_t, 1) if scrape_t > 0 else None,
             "scrape_p99_us": round(_pct(scrapes, 0.99) * 1e6, 2),
+            # the daemon's own time per /metrics answer (render + the sendmsg that hands it over)
+            "scrape_server_mean_us": (round(gathered[0]["server_scrape_mean_s"] * 1e6, 3)
+                                      if gathered[0].get("server_scrape_mean_s") else None),
             "scrapes": len(scrapes),
             "allocate_calls": len(allocs) + len(allocs_native),
             "metrics_bytes": gathered[0]["body"],
