@@ -1,5 +1,8 @@
 #include "httpd.h"
 
+#include <charconv>
+#include <limits>
+
 #include <pthread.h>
 
 #include <arpa/inet.h>
@@ -80,25 +83,39 @@ std::vector<double> echo_buckets() {
   return {0.0005, 0.001, 0.002, 0.005, 0.01, 0.02, 0.05, 0.1, 0.2, 0.5, 1.0, 2.0, 5.0, 10.0, 15.0, 20.0, 30.0};
 }
 
-bool ieq(const char* a, size_t n, const char* b) {
-  if (std::strlen(b) != n) return false;
+inline char lower_ascii(char c) { return c >= 'A' && c <= 'Z' ? static_cast<char>(c + ('a' - 'A')) : c; }
+
+// header-name match against a lower-case literal (field names are ASCII, RFC 9110 5.1)
+template <size_t N>
+bool ieq(const char* a, size_t n, const char (&lower)[N]) {
+  if (n != N - 1) return false;
   for (size_t i = 0; i < n; ++i)
-    if (std::tolower(static_cast<unsigned char>(a[i])) != std::tolower(static_cast<unsigned char>(b[i]))) return false;
+    if (lower_ascii(a[i]) != lower[i]) return false;
   return true;
+}
+
+bool icontains(std::string_view h, std::string_view lower) {
+  if (lower.size() > h.size()) return false;
+  for (size_t i = 0; i + lower.size() <= h.size(); ++i) {
+    size_t k = 0;
+    while (k < lower.size() && lower_ascii(h[i + k]) == lower[k]) ++k;
+    if (k == lower.size()) return true;
+  }
+  return false;
 }
 
 // promhttp's gzipAccepted: any comma-separated part equal to "gzip" or starting with
 // "gzip;" (q-values are not weighed, as in the reference's client_golang v1.19).
-bool accepts_gzip(const std::string& v) {
+bool accepts_gzip(std::string_view v) {
   size_t i = 0;
   while (i <= v.size()) {
     size_t j = v.find(',', i);
-    if (j == std::string::npos) j = v.size();
+    if (j == std::string_view::npos) j = v.size();
     size_t a = i, b = j;
     while (a < b && (v[a] == ' ' || v[a] == '\t')) ++a;
     while (b > a && (v[b - 1] == ' ' || v[b - 1] == '\t')) --b;
-    const std::string part = v.substr(a, b - a);
-    if (part == "gzip" || part.compare(0, 5, "gzip;") == 0) return true;
+    const std::string_view part = v.substr(a, b - a);
+    if (part == "gzip" || part.substr(0, 5) == "gzip;") return true;
     i = j + 1;
   }
   return false;
@@ -315,18 +332,25 @@ int HttpServer::start() {
               while (v < e && (*v == ' ' || *v == '\t')) ++v;
               const char* ve = e;
               while (ve > v && (ve[-1] == '\r' || ve[-1] == ' ')) --ve;
-              std::string val(v, static_cast<size_t>(ve - v));
-              if (ieq(q, nlen, "origin")) origin = val;
-              else if (ieq(q, nlen, "host")) hosth = val;
-              else if (ieq(q, nlen, "user-agent")) ua = val;
-              else if (ieq(q, nlen, "content-length")) content_len = std::strtoull(val.c_str(), nullptr, 10);
-              else if (ieq(q, nlen, "transfer-encoding")) chunked = true;
+              const std::string_view val(v, static_cast<size_t>(ve - v));
+              if (ieq(q, nlen, "origin")) origin.assign(val);
+              else if (ieq(q, nlen, "host")) hosth.assign(val);
+              else if (ieq(q, nlen, "user-agent")) ua.assign(val);
+              else if (ieq(q, nlen, "content-length")) {
+                // leading digits, as strtoull reads them: a malformed value is 0; a
+                // negative or overflowing one is huge, and refused below as too large
+                std::string_view d = val;
+                if (!d.empty() && d[0] == '+') d.remove_prefix(1);
+                unsigned long long cl = 0;
+                const auto r = std::from_chars(d.data(), d.data() + d.size(), cl);
+                content_len = (!d.empty() && d[0] == '-') || r.ec == std::errc::result_out_of_range
+                                  ? std::numeric_limits<size_t>::max()
+                                  : static_cast<size_t>(cl);
+              } else if (ieq(q, nlen, "transfer-encoding")) chunked = true;
               else if (ieq(q, nlen, "accept-encoding")) gzip_ok = gzip_ok || accepts_gzip(val);
               else if (ieq(q, nlen, "connection")) {
-                std::string lv = val;
-                std::transform(lv.begin(), lv.end(), lv.begin(), ::tolower);
-                if (lv.find("close") != std::string::npos) conn_close = true;
-                if (lv.find("keep-alive") != std::string::npos) conn_keep = true;
+                if (icontains(val, "close")) conn_close = true;
+                if (icontains(val, "keep-alive")) conn_keep = true;
               }
             }
             q = e + 1;

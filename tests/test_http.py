@@ -170,6 +170,28 @@ def test_native_http_rejects_garbage(make_cfg):
         s.sendall(b"GET / HTTP/1.1\r\n" + b"X-Long: " + b"a" * 70000 + b"\r\n")
         assert s.recv(4096).startswith(b"HTTP/1.1 431")
         s.close()
+        # a negative or overflowing Content-Length is refused, never read as 0 (the body
+        # would otherwise be parsed as the next request)
+        for cl in (b"-1", b"99999999999999999999999", b"+2000000"):
+            s = socket.create_connection(("127.0.0.1", port))
+            s.settimeout(5)
+            s.sendall(b"POST /health HTTP/1.1\r\nContent-Length: " + cl + b"\r\n\r\nGET / HTTP/1.1\r\n\r\n")
+            assert s.recv(4096).startswith(b"HTTP/1.1 413"), cl
+            s.close()
+        # header names in any case; a body of the announced length is skipped, the next
+        # pipelined request answered; "Connection: CLOSE" closes after the answer
+        s = socket.create_connection(("127.0.0.1", port))
+        s.settimeout(5)
+        s.sendall(b"POST /health HTTP/1.1\r\nCONTENT-LENGTH: 2\r\n\r\nxxGET /health HTTP/1.1\r\n"
+                  b"CoNNection: CLOSE\r\n\r\n")
+        data = b""
+        while True:
+            chunk = s.recv(65536)
+            if not chunk:
+                break
+            data += chunk
+        assert data.count(b"HTTP/1.1 ") == 2 and b"Connection: close" in data.split(b"HTTP/1.1 ")[2], data
+        s.close()
         assert get(port, "/health")[0] == 200  # server still fine
     finally:
         w.stop()
