@@ -307,14 +307,15 @@ int HttpServer::start() {
           const char* p = c->in.data() + pos;
           const size_t hlen = hdr_end - pos;
           const char* le = static_cast<const char*>(memchr(p, '\n', hlen + 2));
-          std::string reqline(p, le ? static_cast<size_t>(le - p) : hlen);
-          if (!reqline.empty() && reqline.back() == '\r') reqline.pop_back();
+          std::string_view reqline(p, le ? static_cast<size_t>(le - p) : hlen);
+          if (!reqline.empty() && reqline.back() == '\r') reqline.remove_suffix(1);
           const size_t sp1 = reqline.find(' ');
-          const size_t sp2 = sp1 == std::string::npos ? std::string::npos : reqline.find(' ', sp1 + 1);
-          std::string method, uri, proto;
-          if (sp1 != std::string::npos && sp2 != std::string::npos) {
-            method = reqline.substr(0, sp1);
-            uri = reqline.substr(sp1 + 1, sp2 - sp1 - 1);
+          const size_t sp2 = sp1 == std::string_view::npos ? std::string_view::npos : reqline.find(' ', sp1 + 1);
+          std::string method, uri;
+          std::string_view proto;
+          if (sp1 != std::string_view::npos && sp2 != std::string_view::npos) {
+            method.assign(reqline.substr(0, sp1));
+            uri.assign(reqline.substr(sp1 + 1, sp2 - sp1 - 1));
             proto = reqline.substr(sp2 + 1);
           }
           std::string origin, hosth, ua;
