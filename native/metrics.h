@@ -238,27 +238,39 @@ class Histogram {
   void observe(double v) {
     size_t i = 0;
     while (i < bounds_.size() && v > bounds_[i]) ++i;
-    Shard& sh = shards_[thread_shard()];
+    const int k = thread_shard();
+    // readers sum only the shards some thread has observed into (one or two for most
+    // histograms); the bit is written once per shard, the check is a shared read
+    const uint32_t bit = 1u << k;
+    if (!(used_.load(std::memory_order_relaxed) & bit)) used_.fetch_or(bit, std::memory_order_release);
+    Shard& sh = shards_[k];
     sh.counts[i].fetch_add(1, std::memory_order_relaxed);
     atomic_add_double(&sh.sum, v);
     sh.n.fetch_add(1, std::memory_order_release);  // last: a reader that sees n sees the bucket
   }
   // Observations completed so far, never ahead of the buckets.
-  uint64_t count() const {
+  uint64_t count() const { return count(used()); }
+  double sum() const { return sum(used()); }
+
+ private:
+  uint32_t used() const { return used_.load(std::memory_order_acquire); }
+  uint64_t count(uint32_t used) const {
     uint64_t c = 0;
-    for (int k = 0; k < kMetricShards; ++k) c += shards_[k].n.load(std::memory_order_acquire);
+    for (uint32_t b = used; b; b &= b - 1) c += shards_[__builtin_ctz(b)].n.load(std::memory_order_acquire);
     return c;
   }
-  double sum() const {
+  double sum(uint32_t used) const {
     double s = 0;
-    for (int k = 0; k < kMetricShards; ++k) {
-      const uint64_t b = shards_[k].sum.load(std::memory_order_relaxed);
+    for (uint32_t b = used; b; b &= b - 1) {
+      const uint64_t bits = shards_[__builtin_ctz(b)].sum.load(std::memory_order_relaxed);
       double d;
-      std::memcpy(&d, &b, sizeof(d));
+      std::memcpy(&d, &bits, sizeof(d));
       s += d;
     }
     return s;
   }
+
+ public:
   // labels: already-formatted `k="v",` prefix (may be empty).  A scrape renders every
   // histogram, but most of them (kubelet RPCs, sampling passes) have not moved since the
   // previous scrape: their text is cached under the observation count and re-used.  The
@@ -269,7 +281,8 @@ class Histogram {
   // made concurrent scrapers bounce its lock and reference count between cores, and 4
   // scrapers each took 3.5x as long as one.
   void render(std::string* out, const char* name, std::string_view labels) const {
-    const uint64_t key_count = count();
+    const uint32_t shards = used();  // one snapshot for the key and the numbers
+    const uint64_t key_count = count(shards);
     TlCache& tl = tl_cache();
     // entries of histograms that are gone (a plugin reload replaces every table's) are
     // never hit again: drop what was not rendered in the last kSweepEvery renders
@@ -299,7 +312,7 @@ class Histogram {
     uint64_t cum = 0;
     size_t at = 0;
     for (size_t i = 0; i <= bounds_.size(); ++i) {
-      for (int k = 0; k < kMetricShards; ++k) cum += shards_[k].counts[i].load(std::memory_order_relaxed);
+      for (uint32_t b = shards; b; b &= b - 1) cum += shards_[__builtin_ctz(b)].counts[i].load(std::memory_order_relaxed);
       c.text.append(c.pre, at, c.ends[i] - at);
       at = c.ends[i];
       append_u64(&c.text, cum);
@@ -307,7 +320,7 @@ class Histogram {
     }
     c.text.append(c.pre, at, c.ends[bounds_.size() + 1] - at);
     at = c.ends[bounds_.size() + 1];
-    append_float(&c.text, sum());
+    append_float(&c.text, sum(shards));
     c.text.push_back('\n');
     c.text.append(c.pre, at, c.ends[bounds_.size() + 2] - at);
     append_u64(&c.text, cum);
@@ -319,9 +332,10 @@ class Histogram {
     std::string prefix(name);
     prefix.append("_bucket{").append(labels.data(), labels.size()).append("le=\"");
     out->reserve(out->size() + (prefix.size() + 24) * (bounds_.size() + 3));
+    const uint32_t shards = used();
     uint64_t cum = 0;
     for (size_t i = 0; i <= bounds_.size(); ++i) {
-      for (int k = 0; k < kMetricShards; ++k) cum += shards_[k].counts[i].load(std::memory_order_relaxed);
+      for (uint32_t b = shards; b; b &= b - 1) cum += shards_[__builtin_ctz(b)].counts[i].load(std::memory_order_relaxed);
       out->append(prefix).append(le_[i]).append("\"} ");
       append_u64(out, cum);
       out->push_back('\n');
@@ -331,7 +345,7 @@ class Histogram {
     out->append(name).append("_sum");
     if (!lab.empty()) out->append("{").append(lab.data(), lab.size()).append("}");
     out->push_back(' ');
-    append_float(out, sum());
+    append_float(out, sum(shards));
     out->push_back('\n');
     out->append(name).append("_count");
     if (!lab.empty()) out->append("{").append(lab.data(), lab.size()).append("}");
@@ -349,6 +363,8 @@ class Histogram {
   std::vector<double> bounds_;
   std::vector<std::string> le_;
   std::unique_ptr<Shard[]> shards_;
+  std::atomic<uint32_t> used_{0};  // bit k: shard k has seen an observation
+  static_assert(kMetricShards <= 32, "used_ is a 32-bit mask");
   struct Cached {
     uint64_t count = 0;
     uint64_t last_render = 0;  // TlCache::renders when last used

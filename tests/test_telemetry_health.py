@@ -59,6 +59,41 @@ def test_exporter_device_health_and_rpc_histogram(n):
     assert buckets[0].labels["rpc"] == "Allocate" and buckets[-1].value == 1
 
 
+def test_rpc_histogram_sums_every_observing_thread(n):
+    """Observations land in per-thread shards; a render sums exactly the shards that were
+    written (the used-shard mask), re-rendering whenever a new thread's shard appears."""
+    import threading
+    tc = n.TableConfig()
+    t = n.DeviceTable(tc, [n.TableDevice("a", 0)], n.Topology(1))
+    ex = n.Exporter()
+    ex.set_tables([t])
+
+    def counts():
+        fams = _families(ex.render())
+        samples = fams["amdgpu_device_plugin_rpc_duration_seconds"].samples
+        b = [s.value for s in samples if s.name.endswith("_bucket") and s.labels["rpc"] == "Allocate"]
+        c = [s.value for s in samples if s.name.endswith("_count") and s.labels["rpc"] == "Allocate"]
+        return b, c[0]
+
+    t.observe(n.RPC_ALLOCATE, 3e-6, False)
+    assert counts()[1] == 1
+    done = []
+
+    def worker(i):
+        for k in range(500):
+            t.observe(n.RPC_ALLOCATE, (1 + (k % 7)) * 1e-6 * (10 ** (i % 4)), False)
+        done.append(i)
+
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(12)]
+    for th in ts:
+        th.start()
+    for th in ts:
+        th.join()
+    buckets, count = counts()
+    assert count == 1 + 12 * 500
+    assert buckets[-1] == count and buckets == sorted(buckets)  # cumulative, +Inf holds all
+
+
 def _discovered(spec="2gpu_spx"):
     """A fixture node after its first discovery: the monitor names GPUs by the identities
     the backend gives for its current enumeration (an index it does not know is ignored)."""
