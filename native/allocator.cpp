@@ -140,8 +140,10 @@ struct Ctx {
 
   // Largest set of GPUs in `mask` that are pairwise connected by healthy links.
   int max_clique(uint64_t mask) const {
+    const int all = __builtin_popcountll(mask);
     int best = 0;
-    // enumerate subsets of mask (callers pass <= 8-16 GPUs of one NUMA node)
+    // enumerate subsets of mask (callers pass <= 8-16 GPUs of one NUMA node); the first
+    // is the whole mask, which on a healthy mesh is a clique: then nothing can beat it
     for (uint64_t sub = mask; sub; sub = (sub - 1) & mask) {
       const int pc = __builtin_popcountll(sub);
       if (pc <= best) continue;
@@ -151,6 +153,7 @@ struct Ctx {
         ok = (sub & ~(adj[v] | (1ull << v))) == 0;
       }
       if (ok) best = pc;
+      if (best == all) break;
     }
     return best;
   }
