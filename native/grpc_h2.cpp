@@ -601,12 +601,17 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
   bool wake_spin = false;
   int64_t wake_idle = 0;      // the worker's time without work before this wake-up
   uint16_t last_cpu = 0xFFFF;  // CPU of the worker's previous work
-  std::vector<uint64_t> trace_pending;
+  // Each worker writes its own slice of the ring with its own counter: one shared counter
+  // was a cache line every traced call of every worker wrote (N ranks -> N cores)
+  std::vector<std::pair<uint64_t, uint32_t>> trace_pending;  // (slot, seq) awaiting the send
+  const uint64_t trace_slice = trace_ ? std::max<uint64_t>(1, trace_hdr_->capacity / std::max(1, nthreads_)) : 1;
+  const uint64_t trace_base = trace_ ? (static_cast<uint64_t>(w->index) * trace_slice) % trace_hdr_->capacity : 0;
+  uint64_t trace_next = 0;
   auto stamp_sent = [&] {
     const int64_t t = mono_ns();
-    for (uint64_t idx : trace_pending) {
-      CallTraceEntry& e = trace_[idx % trace_hdr_->capacity];
-      if (e.seq == static_cast<uint32_t>(idx + 1)) e.t_sent = t;
+    for (const auto& ps : trace_pending) {
+      CallTraceEntry& e = trace_[ps.first];
+      if (e.seq == ps.second) e.t_sent = t;
     }
     trace_pending.clear();
   };
@@ -638,8 +643,9 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
     if (!c.internal) requests_.add();
     const Method m = static_cast<Method>(s.method);
     if (trace_ && !c.internal && m != kMLaw && m != kMPreStart) {
-      const uint64_t idx = trace_hdr_->next.fetch_add(1, std::memory_order_relaxed);
-      CallTraceEntry& e = trace_[idx % trace_hdr_->capacity];
+      const uint64_t idx = trace_next++;
+      const uint64_t slot = trace_base + idx % trace_slice;
+      CallTraceEntry& e = trace_[slot];
       e.t_ready = wake_ts;
       e.t_dispatch = t0;
       e.t_sent = 0;
@@ -653,7 +659,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
       e.prev_cpu = last_cpu;
       last_cpu = e.cpu;
       e.seq = static_cast<uint32_t>(idx + 1);
-      trace_pending.push_back(idx);
+      trace_pending.emplace_back(slot, e.seq);
     }
     if (m == kMUnknown) {
       send_error(c, sid, s, 12, "unknown method " + s.path);  // UNIMPLEMENTED

@@ -49,9 +49,9 @@ struct CallTraceEntry {
 static_assert(sizeof(CallTraceEntry) == 56, "trace record layout is read by bench.py");
 struct CallTraceHeader {
   uint64_t magic = 0;      // kCallTraceMagic
-  uint32_t version = 1;
+  uint32_t version = 2;    // 2: worker i writes records [i * slice, (i + 1) * slice)
   uint32_t capacity = 0;   // records after the header
-  std::atomic<uint64_t> next{0};
+  std::atomic<uint64_t> next{0};  // unused since version 2 (kept for the layout)
   uint64_t pad[5] = {};
 };
 static_assert(sizeof(CallTraceHeader) == 64, "trace header layout is read by bench.py");

@@ -398,6 +398,46 @@ def test_keep_warm_ticks_are_invisible_to_kubelet_and_metrics(n, plugin_dir, ful
         srv.stop()
 
 
+def test_call_trace_records_every_call_in_per_worker_slices(n, plugin_dir, tmp_path):
+    """grpc.callTraceFile: one record per unary call (ListAndWatch and keep-warm ticks are
+    not traced), each worker in its own slice of the ring (no shared counter), the ring
+    pre-written, and t_ready <= t_dispatch <= t_sent."""
+    import numpy as np
+    import bench
+    tc = n.TableConfig()
+    devs = [n.TableDevice("dev-%d" % i, i, 0, 0, -1, ["/dev/dri/renderD%d" % (128 + i)], True) for i in range(2)]
+    table = n.DeviceTable(tc, devs, n.Topology(2))
+    path = os.path.join(plugin_dir, "amd-gpu.sock")
+    trace = str(tmp_path / "trace.bin")
+    srv = n.GrpcServer(path, 2, busy_poll_us=0, admission_poll_us=0)
+    srv.set_call_trace(trace, 64)
+    srv.set_keep_warm_ms(1)
+    srv.set_table(table)
+    srv.start()
+    try:
+        req = v1beta1.AllocateRequest(container_requests=[v1beta1.ContainerAllocateRequest(
+            devices_ids=["dev-1"])]).SerializeToString()
+        clients = [n.H2Client(path) for _ in range(2)]  # one connection per worker
+        for c in clients:
+            for _ in range(10):
+                assert c.unary(v1beta1.METHOD_ALLOCATE, req)[0] == 0
+        time.sleep(0.05)  # keep-warm ticks: never traced
+        recs = bench.read_call_trace(trace)
+        assert len(recs) == 20
+        assert (recs["method"] == n.RPC_ALLOCATE).all()
+        assert ((recs["t_ready"] <= recs["t_dispatch"]) & (recs["t_dispatch"] <= recs["t_sent"])).all()
+        workers = recs["conn"] >> np.uint64(48)
+        assert sorted(set(workers.tolist())) == [0, 1]
+        raw = np.fromfile(trace, dtype=np.dtype(bench.TRACE_DTYPE), count=64, offset=64)
+        for wi in (0, 1):  # worker i writes records [32 i, 32 i + 10)
+            mine = raw[32 * wi:32 * (wi + 1)]
+            assert list(mine["seq"][:10]) == list(range(1, 11)) and (mine["seq"][10:] == 0).all()
+        for c in clients:
+            c.close()
+    finally:
+        srv.stop()
+
+
 def _switches(tids):
     """voluntary context switches of each thread in `tids` (a sleeping worker's wake-ups)."""
     out = {}
