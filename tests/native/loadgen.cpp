@@ -97,7 +97,12 @@ LoadResult http_load(const std::string& host, int port, const std::string& path,
       for (;;) {
         int64_t sched = mono_ns();
         if (interval_ns > 0) {
-          while (mono_ns() < next) std::this_thread::sleep_for(std::chrono::microseconds(20));
+          // sleep until ~150 us before the slot, then spin: a sleep alone wakes up to one
+          // timer slack (50 us) late, and the latency is counted from the slot (open loop)
+          for (int64_t now = mono_ns(); now < next; now = mono_ns()) {
+            if (next - now > 200000) std::this_thread::sleep_for(std::chrono::nanoseconds(next - now - 150000));
+            else cpu_relax();
+          }
           sched = next;
           next += static_cast<int64_t>(interval_ns);
         }
