@@ -473,6 +473,8 @@ class PluginManager:
         try:
             if self._state.save(self._state_snapshot()):
                 self.counters["state_writes"] = self._state.writes
+            elif self._state.write_errors:
+                self.counters["state_write_errors"] = self._state.write_errors
         except Exception as e:  # pragma: no cover - persistence never stops the manager
             log.error("persisting health latches failed: %s", e)
 

@@ -206,6 +206,27 @@ def test_state_file_can_be_turned_off(make_cfg, plugin_dir):
             r.stop()
 
 
+def test_unwritable_state_file_keeps_serving_with_latches_in_memory(make_cfg, plugin_dir, tmp_path):
+    """A state file that cannot be written (read-only mount, a file where its directory
+    should be) costs the persistence only: the latch holds in memory, the error is
+    counted in /metrics, and the plugin keeps serving."""
+    blocker = tmp_path / "not-a-dir"
+    blocker.write_text("x")
+    with KubeletStub(plugin_dir) as k:
+        r = Run(make_cfg, _model(), health={"stateFile": str(blocker / "health-state.json")})
+        try:
+            k.wait_for_registrations(1)
+            r.be.set_ecc_uncorrectable(1, 1)
+            assert _wait(lambda: not r.healthy(1))
+            assert _wait(lambda: r.m.counters.get("state_write_errors", 0) >= 1)
+            assert _wait(lambda: 'amdgpu_device_plugin_events_total{event="state_write_errors"}'
+                         in r.m.exporter.render())
+            time.sleep(0.2)
+            assert not r.healthy(1) and r.healthy(0) and r.m.running
+        finally:
+            r.stop()
+
+
 def test_failed_canary_verdict_survives_a_restart(make_cfg, plugin_dir):
     with KubeletStub(plugin_dir) as k:
         r = Run(make_cfg, _model())
