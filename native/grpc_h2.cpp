@@ -432,6 +432,7 @@ void GrpcServer::start() {
       // named, so /proc/<pid>/task/*/comm tells the workers apart (scripts/idle_probe.py)
       pthread_setname_np(pthread_self(), ("dpgrpc-" + std::to_string(i)).c_str());
       foreground_thread();
+      set_thread_shard(static_cast<int>(i));
       run_guarded(wp, t, gen);
     });
   std::lock_guard<std::mutex> nk(notifier_->mu);

@@ -230,6 +230,7 @@ int HttpServer::start() {
     threads_.emplace_back([this, w, t] {
       pthread_setname_np(pthread_self(), ("dphttp-" + std::to_string(t)).c_str());
       foreground_thread();
+      set_thread_shard(kMetricShards - 1 - static_cast<int>(t));
       std::vector<epoll_event> evs(128);
       char rbuf[16384];
       int spare = -1;  // reserve descriptor for accept_or_shed

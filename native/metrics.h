@@ -175,11 +175,20 @@ class SpinLock {
 // and HTTP workers never write the same line: with one shared set, 4 concurrent clients
 // bounced the bucket, sum and count lines between cores on every call.
 constexpr int kMetricShards = 16;
-inline int thread_shard() {
-  static std::atomic<int> next{0};
-  static thread_local const int s = next.fetch_add(1, std::memory_order_relaxed) % kMetricShards;
+inline int& thread_shard_slot() {
+  static thread_local int s = -1;
   return s;
 }
+inline int thread_shard() {
+  static std::atomic<int> next{0};
+  int& s = thread_shard_slot();
+  if (s < 0) s = next.fetch_add(1, std::memory_order_relaxed) % kMetricShards;
+  return s;
+}
+// Server workers claim their shard by index (gRPC worker i: shard i, HTTP worker j: shard
+// 15 - j), so the workers of one server never share a line, whatever order they first
+// count in (round-robin at first use let 8 busy workers collide with high probability).
+inline void set_thread_shard(int s) { thread_shard_slot() = ((s % kMetricShards) + kMetricShards) % kMetricShards; }
 
 // A counter incremented by many threads: one cache line per shard, summed on read.
 class ShardedCounter {
