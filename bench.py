@@ -385,6 +385,7 @@ def start_daemon(n_gpus: int, grpc_server: str, workdir: str, profile_dir: str =
         yaml.safe_dump(cfg, f)
     env = dict(os.environ)
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    env["AMDGPU_DP_PARENT_PID"] = str(os.getpid())  # the daemon exits with this process
     log = open(os.path.join(workdir, "daemon.log"), "w")
     proc = subprocess.Popen([sys.executable, "-m", "k8s_gpu_device_plugin_amd", "--configFile", cfg_path],
                             cwd=workdir, env=env, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)

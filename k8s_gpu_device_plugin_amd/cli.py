@@ -43,8 +43,26 @@ def parse_args(argv=None) -> argparse.Namespace:
     return ap.parse_args(argv)
 
 
+def _exit_with_parent() -> bool:
+    """AMDGPU_DP_PARENT_PID (benchmarks and probes that spawn a daemon): SIGTERM this
+    process when that parent exits, so a harness killed mid-run leaves no daemon behind.
+    False if the parent is already gone."""
+    import os
+    want = os.environ.get("AMDGPU_DP_PARENT_PID")
+    if not want:
+        return True
+    try:
+        import ctypes
+        ctypes.CDLL(None, use_errno=True).prctl(1, int(signal.SIGTERM), 0, 0, 0)  # PR_SET_PDEATHSIG
+    except (OSError, AttributeError):
+        pass
+    return os.getppid() == int(want)
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
+    if not _exit_with_parent():
+        return 1
     if args.version:
         print("%s %s" % (APP_NAME, VERSION))
         return 0

@@ -220,3 +220,27 @@ def test_inspect_prints_the_node_and_its_placements(tmp_path):
     assert len(eight) == 8 and len({i.rsplit("-xcp", 1)[0] for i in eight}) == 1  # one whole GPU
     assert len({i.rsplit("-xcp", 1)[0] for i in d["placement"]["amd.com/gpu"]["16"]}) == 2
     assert not feature.exists() and not (tmp_path / "dp").exists()
+
+
+def test_bench_daemon_exits_with_a_harness_that_dies(tmp_path):
+    """A benchmark or probe killed mid-run (timeout, OOM, an exception before its
+    cleanup) must not leave its plugin daemon running: the daemon is told its parent's
+    pid (AMDGPU_DP_PARENT_PID) and gets SIGTERM when that parent exits."""
+    script = (
+        "import os, sys\n"
+        "sys.path.insert(0, %r)\n"
+        "import bench\n"
+        "proc, kubelet, port, reg, backend = bench.start_daemon(1, 'native', %r, backend='fixture')\n"
+        "print(proc.pid, flush=True)\n"
+        "os._exit(0)\n" % (ROOT, str(tmp_path)))
+    out = subprocess.run([sys.executable, "-c", script], capture_output=True, text=True, timeout=90, cwd=ROOT)
+    pid = int(out.stdout.strip().splitlines()[-1])
+    deadline = time.monotonic() + 15
+    while time.monotonic() < deadline:
+        try:
+            os.kill(pid, 0)
+        except ProcessLookupError:
+            return
+        time.sleep(0.1)
+    os.kill(pid, signal.SIGKILL)
+    raise AssertionError("daemon %d outlived its harness" % pid)
