@@ -105,7 +105,10 @@ FAMILIES = (
     Family("amdgpu_device_plugin_rpc_duration_seconds", "histogram", ("resource", "rpc"), "device_table",
            "kubelet RPC latency (5 us .. 1 s buckets)"),
     Family("amdgpu_device_plugin_events_total", "counter", ("event",), "manager",
-           "Lifecycle events: restarts (api/kubelet/retry), registrations, load failures, health events"),
+           "Lifecycle events: restarts (api/kubelet/retry), registrations, load failures, health events; "
+           "reloads and `table_swaps` (hitless reloads), `resets_observed` (GPU resets seen by polling the "
+           "firmware clock), `latches_restored`, `state_writes` / `state_write_errors` (`health.stateFile`), "
+           "start-up canary runs and skips"),
     Family("amdgpu_device_plugin_devices", "gauge", ("resource", "health"), "manager",
            "Advertised devices per resource and health"),
     Family("amdgpu_device_plugin_registered", "gauge", ("resource",), "manager",
