@@ -128,11 +128,15 @@ def main(argv=None) -> int:
 
     mt = threading.Thread(target=run_manager, name="plugin-manager", daemon=True)
     rc = 0
+    import os
+    parent = int(os.environ.get("AMDGPU_DP_PARENT_PID") or 0)
     try:
         web.start()
         mt.start()
         while not done.wait(0.5):
-            pass
+            if parent and os.getppid() != parent:  # the harness is gone (PDEATHSIG backstop)
+                reason["why"] = "parent process %d exited, exiting gracefully..." % parent
+                break
     except Exception as e:
         log.error("error starting web server: %s", e)
         rc = 1

@@ -715,6 +715,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("admission_windows", &GrpcServer::admission_windows)
       .def_property_readonly("poll_windows_yielded", &GrpcServer::poll_windows_yielded)
       .def_property_readonly("connections", &GrpcServer::connections)
+      .def("list_and_watch_streams", &GrpcServer::list_and_watch_streams, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("worker_connections", &GrpcServer::worker_connections)
       .def_property_readonly("socket_path", &GrpcServer::socket_path)
       .def("failure", &GrpcServer::failure)

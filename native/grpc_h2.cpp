@@ -229,6 +229,7 @@ struct GrpcServer::Worker {
   // for a table change (kubelet holds one stream per plugin, so usually one worker;
   // waking all of them one eventfd write after another delayed the stream's push)
   std::atomic<bool> law_seen{false};
+  std::atomic<int> law_open{0};  // ListAndWatch streams open on this worker's connections
 };
 
 using Conn = GrpcServer::Worker::Conn;
@@ -352,6 +353,13 @@ void GrpcServer::set_call_trace(const std::string& path, int capacity) {
   trace_ = reinterpret_cast<CallTraceEntry*>(static_cast<char*>(p) + sizeof(CallTraceHeader));
   trace_bytes_ = bytes;
   trace_hdr_->magic = kCallTraceMagic;
+}
+
+int GrpcServer::list_and_watch_streams() const {
+  std::lock_guard<std::mutex> lk(mu_);  // workers_ changes only under it (start / stop)
+  int n = 0;
+  for (const auto& w : workers_) n += w->law_open.load(std::memory_order_relaxed);
+  return n;
 }
 
 void GrpcServer::set_table(std::shared_ptr<DeviceTable> t) {
@@ -531,6 +539,7 @@ void GrpcServer::run_guarded(Worker* w, std::shared_ptr<DeviceTable> table, uint
     conns_.fetch_sub(1);
   }
   w->conns.clear();
+  w->law_open.store(0, std::memory_order_relaxed);
   w->load.store(1 << 20, std::memory_order_relaxed);  // never picked for a new connection
   if (listen_fd_ >= 0) epoll_ctl(w->ep, EPOLL_CTL_DEL, listen_fd_, nullptr);
 }
@@ -548,6 +557,10 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
   auto close_conn = [&](int fd) {
     epoll_ctl(w->ep, EPOLL_CTL_DEL, fd, nullptr);
     ::close(fd);
+    auto ci = w->conns.find(fd);
+    if (ci != w->conns.end())
+      for (const auto& st : ci->second->streams)
+        if (st.second.law) w->law_open.fetch_sub(1, std::memory_order_relaxed);
     w->conns.erase(fd);
     conns_.fetch_sub(1);
     w->load.fetch_sub(1, std::memory_order_relaxed);
@@ -721,6 +734,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
         case kMLaw: {
           rpc = kRpcListAndWatch;
           w->law_seen.store(true, std::memory_order_release);
+          if (!s.law) w->law_open.fetch_add(1, std::memory_order_relaxed);
           s.law = true;
           s.law_version = table->version();
           send_headers(c, sid);
@@ -978,6 +992,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
           auto it = c.streams.find(sid);
           if (it != c.streams.end()) {
             drop_data(c, it->second);
+            if (it->second.law) w->law_open.fetch_sub(1, std::memory_order_relaxed);
             c.streams.erase(it);
           }
           break;
@@ -993,6 +1008,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
     for (auto it = c.streams.begin(); it != c.streams.end();)
       if (it->second.done && it->second.pend.empty()) {
         drop_data(c, it->second);
+        if (it->second.law) w->law_open.fetch_sub(1, std::memory_order_relaxed);
         it = c.streams.erase(it);
       } else {
         ++it;
@@ -1324,6 +1340,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
     conns_.fetch_sub(1);
   }
   w->conns.clear();
+  w->law_open.store(0, std::memory_order_relaxed);
 }
 
 // ------------------------------------------------------------------- client

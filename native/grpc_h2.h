@@ -100,6 +100,9 @@ class GrpcServer {
   uint64_t admission_windows() const { return admission_windows_.load(); }
   uint64_t poll_windows_yielded() const { return poll_windows_yielded_.load(); }
   int connections() const { return conns_.load(); }
+  // ListAndWatch streams open now (kubelet holds one per registered plugin; none while
+  // registered means kubelet dropped the endpoint and waits for a new Register)
+  int list_and_watch_streams() const;
   // Keep-warm (grpc.keepWarmMs, 0 = off): a worker that holds a connection and has been
   // idle this long runs the request path on canned requests (HPACK decode of a typical
   // request header block, Allocate and GetPreferredAllocation through the table), so

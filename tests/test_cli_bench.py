@@ -238,9 +238,15 @@ def test_bench_daemon_exits_with_a_harness_that_dies(tmp_path):
     deadline = time.monotonic() + 15
     while time.monotonic() < deadline:
         try:
-            os.kill(pid, 0)
-        except ProcessLookupError:
+            with open("/proc/%d/stat" % pid) as f:
+                if f.read().rsplit(")", 1)[1].split()[0] in ("Z", "X"):
+                    return  # exited; its new parent just has not reaped it yet
+        except (FileNotFoundError, ProcessLookupError):
             return
         time.sleep(0.1)
+    with open("/proc/%d/status" % pid) as f:
+        status = f.read()
     os.kill(pid, signal.SIGKILL)
-    raise AssertionError("daemon %d outlived its harness" % pid)
+    with open(tmp_path / "daemon.log") as f:
+        tail = f.read()[-3000:]
+    raise AssertionError("daemon %d outlived its harness\n%s\n%s" % (pid, status[:600], tail))
