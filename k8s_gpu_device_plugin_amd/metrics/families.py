@@ -108,7 +108,7 @@ FAMILIES = (
            "Lifecycle events: restarts (api/kubelet/retry), registrations, load failures, health events; "
            "reloads and `table_swaps` (hitless reloads), `resets_observed` (GPU resets seen by polling the "
            "firmware clock), `latches_restored`, `state_writes` / `state_write_errors` (`health.stateFile`), "
-           "start-up canary runs and skips"),
+           "start-up canary runs and skips, `reregistrations_stream_lost` (kubelet ended a ListAndWatch stream)"),
     Family("amdgpu_device_plugin_devices", "gauge", ("resource", "health"), "manager",
            "Advertised devices per resource and health"),
     Family("amdgpu_device_plugin_registered", "gauge", ("resource",), "manager",

@@ -172,8 +172,10 @@ class KubeletStub:
             self._clients[endpoint] = DevicePluginClient(os.path.join(self.plugin_dir, endpoint))
         return self._clients[endpoint]
 
-    def watch(self, endpoint: str) -> _Watch:
-        if endpoint not in self._watches:
+    def watch(self, endpoint: str, new: bool = False) -> _Watch:
+        """The stream kubelet keeps on ``endpoint`` (``new``: open another, as kubelet
+        does after a Register)."""
+        if new or endpoint not in self._watches:
             self._watches[endpoint] = _Watch(self.client(endpoint))
         return self._watches[endpoint]
 

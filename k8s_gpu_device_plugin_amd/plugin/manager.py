@@ -59,6 +59,10 @@ EV_START_CANARY = "start_canary"  # a start-up canary verdict: (identity, partit
 DISCOVERY_RELOAD, DISCOVERY_CHECK = "reload", "check"  # rebuild always / only if the inventory changed
 HEALTH_LOG_LEN = 4096
 SERVER_CHECK_S = 1.0  # gRPC server supervision poll
+# kubelet holds one ListAndWatch stream per registered plugin for the plugin's life; when
+# it ends the stream (its side failed) it drops the endpoint and waits for a new Register.
+# A plugin whose stream has been gone this long, kubelet.sock still in place, registers again
+LAW_LOST_GRACE_S = 5.0
 
 
 def inventory_signature(gpus) -> tuple:
@@ -400,8 +404,43 @@ class PluginManager:
                 self.fatal_error = p.fatal_error
                 log.critical("fatal: %s", p.fatal_error)
                 return False
+            restarted = self._check_stream(p) or restarted
         if restarted:
             self._publish_metrics()
+        return True
+
+    def _check_stream(self, p) -> bool:
+        """Re-registers a plugin whose kubelet ListAndWatch stream ended and was not
+        reopened within LAW_LOST_GRACE_S (kubelet dropped the endpoint without restarting:
+        the reference recovered from this only on a /restart, which re-registered every
+        plugin).  True if it registered again."""
+        if not p.registered or not p.serving:
+            return False
+        try:
+            open_streams = p.list_and_watch_streams()
+        except Exception:  # pragma: no cover - a stopping server
+            return False
+        now = time.monotonic()
+        if open_streams > 0:
+            p.law_had, p.law_lost_since = True, None
+            return False
+        if not p.law_had:
+            return False  # kubelet has not opened its stream since the last Register yet
+        if p.law_lost_since is None:
+            p.law_lost_since = now
+            return False
+        if now - p.law_lost_since < LAW_LOST_GRACE_S or not os.path.exists(self.cfg.kubelet_socket):
+            return False
+        log.warning("kubelet ended the ListAndWatch stream of %s %.0f s ago and did not open another: "
+                    "registering again", p.resource, now - p.law_lost_since)
+        try:
+            p.register()
+        except Exception as e:
+            p.law_lost_since = now  # try again after another grace period
+            log.error("registering %s again failed: %s", p.resource, e)
+            return False
+        self.counters["reregistrations_stream_lost"] = self.counters.get("reregistrations_stream_lost", 0) + 1
+        self.counters["registrations"] += 1
         return True
 
     def _loop(self) -> None:

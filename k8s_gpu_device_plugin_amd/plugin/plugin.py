@@ -154,6 +154,13 @@ class AmdDevicePlugin:
         # the plugin a grpcio server's handlers serve from: shared with (and redirected
         # by) a successor that adopts the server, so requests follow the current table
         self._front = [self]
+        # ListAndWatch streams open on the grpcio server (the native server counts its own);
+        # shared with a successor that adopts the server, like _front
+        self._law = [0]
+        # stream watchdog (PluginManager._check_stream): kubelet opened a stream since the
+        # last Register, and since when none is open
+        self.law_had = False
+        self.law_lost_since: float | None = None
 
     # ------------------------------------------------------------------ views
     def devices(self) -> Devices:
@@ -216,6 +223,8 @@ class AmdDevicePlugin:
             self._crashes, self._last_crash = prev._crashes, prev._last_crash
             self.server_restarts = prev.server_restarts
             self._front = prev._front
+            self._law = prev._law
+            self.law_had, self.law_lost_since = prev.law_had, prev.law_lost_since
             if self.cfg is not None and self.cfg.health.canaryOnPreStart and self._prestart_thread is None:
                 self._start_prestart_locked()
         if nserver is not None:
@@ -392,10 +401,18 @@ class AmdDevicePlugin:
         self._serving = True
         self._sock_ident = _socket_ident(self.socket)
 
+    def list_and_watch_streams(self) -> int:
+        """ListAndWatch streams open on this plugin's server now."""
+        srv = self._native_server
+        if srv is not None:
+            return srv.list_and_watch_streams()
+        return self._law[0] if self._serving else 0
+
     def register(self) -> None:
         """Registration.Register with kubelet (``plugin/plugin.go:139-162``).  Sent by the
         compiled HTTP/2 client when the native module has one (no grpcio import, no
         channel teardown), else over a grpcio channel."""
+        self.law_had, self.law_lost_since = False, None
         if not os.path.exists(self.kubelet_socket):  # fail fast instead of a 5 s dial timeout
             raise FileNotFoundError("kubelet socket %s does not exist" % self.kubelet_socket)
         pre_start = bool(self.cfg.health.canaryOnPreStart) if self.cfg is not None else False
@@ -513,7 +530,19 @@ class AmdDevicePlugin:
                 ctx.abort(grpc.StatusCode.UNKNOWN, err)
             return b""
 
+        law = self._law
+        law_lock = threading.Lock()
+
         def list_and_watch(req: bytes, ctx):
+            with law_lock:
+                law[0] += 1
+            try:
+                yield from _list_and_watch(ctx)
+            finally:
+                with law_lock:
+                    law[0] -= 1
+
+        def _list_and_watch(ctx):
             plugin = front[0]
             table = plugin.table
             version = table.version

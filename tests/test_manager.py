@@ -1098,3 +1098,33 @@ def test_background_threads_never_preempt_grpc_workers(make_cfg, plugin_dir, run
         if "dphttp" in pol:
             assert pol["dphttp"] == {0}, pol
         assert native.load().background_batch() == (sched == "batch")
+
+
+@pytest.mark.parametrize("grpc_server", ["native", "python"])
+def test_plugin_registers_again_when_kubelet_ends_its_stream(make_cfg, plugin_dir, run_manager, grpc_server,
+                                                            monkeypatch):
+    """kubelet ends its ListAndWatch stream (its side failed) without restarting: it drops
+    the endpoint and waits for a Register.  The plugin sees no stream for the grace
+    period and registers again; a plugin kubelet never opened a stream to is left alone."""
+    from k8s_gpu_device_plugin_amd.plugin import manager as manager_mod
+    monkeypatch.setattr(manager_mod, "LAW_LOST_GRACE_S", 0.5)
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(grpc={"server": grpc_server}))
+        regs = k.wait_for_registrations(1)
+        time.sleep(2.5)  # no stream opened yet: nothing to recover
+        assert len(k.requests) == 1 and m.counters.get("reregistrations_stream_lost", 0) == 0
+        w = k.watch(regs[0].endpoint)
+        assert len(w.next()[1]) == 2
+        p = m.plugins[0]
+        assert _wait(lambda: p.list_and_watch_streams() == 1)
+        assert _wait(lambda: p.law_had, timeout=3)
+        w.cancel()
+        assert _wait(lambda: p.list_and_watch_streams() == 0, timeout=5)
+        regs = k.wait_for_registrations(2, timeout=10)
+        assert _wait(lambda: m.counters.get("reregistrations_stream_lost") == 1)
+        w2 = k.watch(regs[1].endpoint, new=True)  # the same socket serves the new stream
+        assert len(w2.next()[1]) == 2
+        assert _wait(lambda: p.list_and_watch_streams() == 1)
+        time.sleep(1.5)
+        assert len(k.requests) == 2  # an open stream: no further Register
+        w2.cancel()
