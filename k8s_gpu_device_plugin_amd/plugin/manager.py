@@ -431,14 +431,19 @@ class PluginManager:
             return False
         if now - p.law_lost_since < LAW_LOST_GRACE_S or not os.path.exists(self.cfg.kubelet_socket):
             return False
-        log.warning("kubelet ended the ListAndWatch stream of %s %.0f s ago and did not open another: "
-                    "registering again", p.resource, now - p.law_lost_since)
+        failures = getattr(p, "_reregister_failures", 0)
+        if not failures:
+            log.warning("kubelet ended the ListAndWatch stream of %s %.0f s ago and did not open another: "
+                        "registering again", p.resource, now - p.law_lost_since)
         try:
             p.register()
         except Exception as e:
             p.law_lost_since = now  # try again after another grace period
-            log.error("registering %s again failed: %s", p.resource, e)
+            p._reregister_failures = failures + 1
+            # a kubelet that is down but left its socket: one error, then quiet retries
+            (log.error if not failures else log.debug)("registering %s again failed: %s", p.resource, e)
             return False
+        p._reregister_failures = 0
         self.counters["reregistrations_stream_lost"] = self.counters.get("reregistrations_stream_lost", 0) + 1
         self.counters["registrations"] += 1
         return True
