@@ -298,6 +298,7 @@ void Exporter::watchdog_loop(std::shared_ptr<HealthMonitor> monitor) {
                                                }) > 1;
     auto st = std::make_shared<Stalls>();
     std::map<std::string, int64_t> still;
+    std::vector<HwEvent> lost;  // fed to the monitor once the stall list below is published
     for (const auto& r : stuck) {
       if (!is_served(r)) continue;
       const int64_t since = r.lane.inflight_since_ns;
@@ -315,13 +316,18 @@ void Exporter::watchdog_loop(std::shared_ptr<HealthMonitor> monitor) {
       e.key = r.lane.key;  // the GPU the call went to, even if the node was re-enumerated since
       e.message = r.lane.inflight_what + " call in flight for " + std::to_string((now - since) / 1000000) +
                   " ms (health.sampleStallS)";
-      if (monitor) monitor->process(e);
+      lost.push_back(std::move(e));
     }
     reported.swap(still);
     std::sort(st->stalled.begin(), st->stalled.end());
     std::sort(st->blocked.begin(), st->blocked.end());
-    std::lock_guard<SpinLock> lk(fresh_lock_);
-    stalls_ = std::move(st);
+    {
+      std::lock_guard<SpinLock> lk(fresh_lock_);
+      stalls_ = std::move(st);
+    }
+    // whoever sees the lost verdict (the manager, /ready) also sees the stall behind it
+    if (monitor)
+      for (const auto& e : lost) monitor->process(e);
   }
 }
 
