@@ -210,6 +210,7 @@ void HealthMonitor::process(const HwEvent& e) {
       if (!known) return;
       GpuState& st = state_[key];
       st.lost = false;
+      st.lost_failing = false;
       st.failures = 0;
       reconcile_locked(key, e.kind, why);
       return;
@@ -307,8 +308,10 @@ void HealthMonitor::on_sample(int gpu, bool ok, const GpuSample& s) {
       return e;
     };
     if (!ok) {
-      if (++st.failures >= lost_after_ && !st.lost)
+      if (++st.failures >= lost_after_ && !st.lost) {
+        st.lost_failing = true;
         derived.push_back(event(kEvtDeviceLost, "telemetry failed " + std::to_string(st.failures) + " times in a row"));
+      }
     } else {
       st.failures = 0;
       if (st.lost) derived.push_back(event(kEvtDeviceRecovered, "telemetry responding again"));
@@ -344,8 +347,10 @@ void HealthMonitor::on_sample(int gpu, bool ok, const GpuSample& s) {
         if (st.fw_advancing) st.fw_boot = fw_boot;
       } else {
         st.restored_fw_boot = std::numeric_limits<double>::quiet_NaN();  // nothing to compare it with
-        // a GPU that reports no firmware clock: coming back from an outage is the reset
-        if (st.lost) reset_why = "telemetry back after an outage (the GPU reports no firmware clock)";
+        // a GPU that reports no firmware clock: coming back from an outage of failed
+        // samples is the reset (a driver refuses calls while it resets the GPU); a call
+        // that merely hung for a while is not taken as one
+        if (st.lost && st.lost_failing) reset_why = "telemetry back after an outage (the GPU reports no firmware clock)";
       }
       if (!reset_why.empty()) {
         derived.push_back(event(kEvtResetObserved, reset_why));

@@ -156,6 +156,7 @@ class HealthMonitor {
     bool resetting = false;
     bool ecc_bad = false;
     bool lost = false;
+    bool lost_failing = false;  // lost because its samples failed (not a call that hung)
     bool pages_bad = false;  // retired + pending pages at/over the threshold (not cleared by a reset)
     bool pcie_bad = false;   // host PCIe link trained below the configured floor
     int pcie_low = 0;        // consecutive samples below the floor

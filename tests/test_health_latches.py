@@ -132,6 +132,26 @@ def test_clockless_gpu_outage_clears_the_latch(make_cfg, plugin_dir):
             r.stop()
 
 
+def test_clockless_gpu_call_that_hung_is_not_a_reset(make_cfg, plugin_dir):
+    """On a clockless GPU only an outage of failed samples counts as a reset: a telemetry
+    call that hung (the watchdog marks the GPU lost) and then returned leaves the
+    uncorrectable-ECC latch in place."""
+    with KubeletStub(plugin_dir) as k:
+        r = Run(make_cfg, _model(fw_clock=False), health={"sampleStallS": 0.3})
+        try:
+            k.wait_for_registrations(1)
+            r.be.set_ecc_uncorrectable(1, 1)
+            assert _wait(lambda: not r.healthy(1))
+            r.be.set_sample_stall(1, True)  # the call hangs: lost by the watchdog
+            assert _wait(lambda: r.m.exporter.stalled_gpu == 1)
+            r.be.set_sample_stall(1, False)
+            assert _wait(lambda: r.m.exporter.stalled_gpu == -1)
+            time.sleep(0.5)  # samples flow again
+            assert not r.healthy(1) and r.m.monitor.resets_observed == 0
+        finally:
+            r.stop()
+
+
 def test_latch_survives_plugin_restart_until_reset(make_cfg, plugin_dir):
     with KubeletStub(plugin_dir) as k:
         r, key1 = _latch(make_cfg, plugin_dir, k)
