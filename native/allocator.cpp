@@ -58,27 +58,42 @@ int pair_score(const Topology& topo, const AllocDevice& a, const AllocDevice& b)
 
 namespace {
 
+// The vectors of one allocation's context live in the calling thread and keep their
+// capacity between calls: a context is built per GetPreferredAllocation, and its ~15
+// vectors were as many heap allocations per request.
+struct CtxScratch {
+  std::vector<char> is_avail;
+  std::vector<int> gpu_total, gpu_avail, gpu_numa, numa_ids, gpu_numa_slot, taken, cnt, cls, cls_rep, cls_pair;
+  std::vector<uint64_t> adj, whole_free;
+  std::vector<std::pair<int, int>> keys;
+};
+CtxScratch& ctx_scratch() {
+  static thread_local CtxScratch s;
+  return s;
+}
+
 struct Ctx {
   const Topology& topo;
   const std::vector<AllocDevice>& devs;
-  std::vector<char> is_avail;   // device index -> available
-  std::vector<int> gpu_total;   // devices per gpu (all)
-  std::vector<int> gpu_avail;   // available devices per gpu
-  std::vector<int> gpu_numa;
-  std::vector<uint64_t> adj;       // healthy direct-link adjacency bitmask per GPU
-  std::vector<int> numa_ids;       // distinct NUMA nodes
-  std::vector<int> gpu_numa_slot;  // gpu -> index into numa_ids
+  CtxScratch& sc = ctx_scratch();
+  std::vector<char>& is_avail = sc.is_avail;    // device index -> available
+  std::vector<int>& gpu_total = sc.gpu_total;   // devices per gpu (all)
+  std::vector<int>& gpu_avail = sc.gpu_avail;   // available devices per gpu
+  std::vector<int>& gpu_numa = sc.gpu_numa;
+  std::vector<uint64_t>& adj = sc.adj;                 // healthy direct-link adjacency bitmask per GPU
+  std::vector<int>& numa_ids = sc.numa_ids;            // distinct NUMA nodes
+  std::vector<int>& gpu_numa_slot = sc.gpu_numa_slot;  // gpu -> index into numa_ids
   int ngpu = 0;
   int parts_per_gpu = 1;
   // score() scratch, reused across the (up to thousands of) candidate evaluations
-  mutable std::vector<int> taken;
-  mutable std::vector<uint64_t> whole_free;
-  mutable std::vector<int> cnt;  // per-class counts of the set being scored
+  std::vector<int>& taken = sc.taken;
+  std::vector<uint64_t>& whole_free = sc.whole_free;
+  std::vector<int>& cnt = sc.cnt;  // per-class counts of the set being scored
   // pair_score depends only on (gpu, numa) of the two devices: one matrix over those
   // classes replaces the per-pair topology lookups in score()
-  std::vector<int> cls;                // device -> class
-  std::vector<int> cls_rep;            // class -> a device of it
-  mutable std::vector<int> cls_pair;   // nclass x nclass pair scores, filled on first use
+  std::vector<int>& cls = sc.cls;            // device -> class
+  std::vector<int>& cls_rep = sc.cls_rep;    // class -> a device of it
+  std::vector<int>& cls_pair = sc.cls_pair;  // nclass x nclass pair scores, filled on first use
   int ncls = 0;
   static constexpr int kUnset = -1;
 
@@ -113,6 +128,7 @@ struct Ctx {
             (t.at(a, b).type == kLinkXgmi || t.at(a, b).type == kLinkPcie))
           adj[a] |= 1ull << b;
     gpu_numa_slot.assign(ngpu, 0);
+    numa_ids.clear();
     for (int g = 0; g < ngpu; ++g) {
       auto it = std::find(numa_ids.begin(), numa_ids.end(), gpu_numa[g]);
       if (it == numa_ids.end()) it = numa_ids.insert(numa_ids.end(), gpu_numa[g]);
@@ -120,8 +136,10 @@ struct Ctx {
     }
     taken.assign(ngpu, 0);
     whole_free.assign(numa_ids.size(), 0);
-    std::vector<std::pair<int, int>> keys;
+    std::vector<std::pair<int, int>>& keys = sc.keys;
+    keys.clear();
     std::vector<int>& rep = cls_rep;
+    rep.clear();
     cls.assign(d.size(), 0);
     for (size_t i = 0; i < d.size(); ++i) {
       const std::pair<int, int> key(d[i].gpu, d[i].numa);
