@@ -609,6 +609,7 @@ def main() -> int:
         conn.request("GET", "/metrics")
         text = conn.getresponse().read().decode()
         mine["server_allocate_mean_s"] = _server_mean(text, "Allocate")
+        mine["server_preferred_mean_s"] = _server_mean(text, "GetPreferredAllocation")
         mine["server_scrape_mean_s"] = _scrape_server_mean(text)
     if world > 1:
         gathered = [None] * world
@@ -665,6 +666,8 @@ def main() -> int:
             "allocate_p99_us_grpcio_client": round(_pct(allocs, 0.99) * 1e6, 2),
             "preferred_p50_us": round(_pct(prefs_native, 0.5) * 1e6, 2),
             "preferred_p99_us": round(_pct(prefs_native, 0.99) * 1e6, 2),
+            "preferred_server_mean_us": (round(gathered[0]["server_preferred_mean_s"] * 1e6, 3)
+                                         if gathered[0].get("server_preferred_mean_s") else None),
             "preferred_p50_us_grpcio_client": round(_pct(prefs, 0.5) * 1e6, 2),
             "scrape_p50_us": round(_pct(scrapes, 0.5) * 1e6, 2),
             "scrape_rps": round(len(scrapes) / scrape_t, 1) if scrape_t > 0 else None,
