@@ -64,7 +64,8 @@ namespace {
 struct CtxScratch {
   std::vector<char> is_avail;
   std::vector<int> gpu_total, gpu_avail, gpu_numa, numa_ids, gpu_numa_slot, taken, cnt, cls, cls_rep, cls_pair;
-  std::vector<uint64_t> adj, whole_free;
+  std::vector<uint64_t> adj, whole_free, base_free;
+  std::vector<int> touched;
   std::vector<std::pair<int, int>> keys;
 };
 CtxScratch& ctx_scratch() {
@@ -95,6 +96,10 @@ struct Ctx {
   std::vector<int>& cls_rep = sc.cls_rep;    // class -> a device of it
   std::vector<int>& cls_pair = sc.cls_pair;  // nclass x nclass pair scores, filled on first use
   int ncls = 0;
+  // set_terms() starts from the pool as it is and adjusts only the GPUs a candidate
+  // touches: the fragmentation sum with nothing taken, and the whole-free GPUs per NUMA node
+  double base_frag = 0;
+  std::vector<uint64_t>& base_free = sc.base_free;
   static constexpr int kUnset = -1;
 
   int class_pair(int a, int b) const {
@@ -136,6 +141,11 @@ struct Ctx {
     }
     taken.assign(ngpu, 0);
     whole_free.assign(numa_ids.size(), 0);
+    base_free.assign(numa_ids.size(), 0);
+    for (int g = 0; g < ngpu; ++g) {
+      base_frag += static_cast<double>(gpu_avail[g]) * gpu_avail[g] / parts_per_gpu;
+      if (gpu_total[g] > 0 && gpu_avail[g] == gpu_total[g] && g < 64) base_free[gpu_numa_slot[g]] |= 1ull << g;
+    }
     std::vector<std::pair<int, int>>& keys = sc.keys;
     keys.clear();
     std::vector<int>& rep = cls_rep;
@@ -207,7 +217,9 @@ struct Ctx {
   // every term but the pair scores: packing, link sharing, fragmentation
   double set_terms(const std::vector<int>& cn) const {
     double s = 0;
-    std::fill(taken.begin(), taken.end(), 0);
+    // the GPUs this candidate takes devices from (taken[] is all zero between calls)
+    std::vector<int>& touched = sc.touched;
+    touched.clear();
     int first_gpu = -2;
     bool multi_gpu = false;
     for (int a = 0; a < ncls; ++a) {
@@ -215,23 +227,26 @@ struct Ctx {
       const int g = devs[cls_rep[a]].gpu;
       if (first_gpu == -2) first_gpu = g;
       else if (g != first_gpu) multi_gpu = true;
-      if (g >= 0) taken[g] += cn[a];
-    }
-    for (int g = 0; g < ngpu; ++g) {
-      if (!taken[g]) continue;
-      const bool busy = gpu_avail[g] < gpu_total[g];  // other pods already on this GPU
-      if (busy && gpu_total[g] > 1) s += 6.0 * taken[g];  // pack into partially used GPUs
-      if (busy && multi_gpu) s -= 4.0;  // cross-GPU traffic would share this GPU's links
+      if (g < 0) continue;
+      if (!taken[g]) touched.push_back(g);
+      taken[g] += cn[a];
     }
     // fragmentation of the remainder: concentrate leftovers, and keep the largest
     // healthy-link clique of whole free GPUs per NUMA node (what a future multi-GPU
-    // RCCL job needs) - on a healthy mesh this is just the whole-free count.
-    double frag = 0;
-    std::fill(whole_free.begin(), whole_free.end(), 0);
-    for (int g = 0; g < ngpu; ++g) {
+    // RCCL job needs) - on a healthy mesh this is just the whole-free count.  Only the
+    // touched GPUs differ from the pool as it is (every term is a multiple of
+    // 1/parts_per_gpu: exact in any order for the power-of-two partition counts, and off
+    // by far less than the 1e-9 tie tolerance otherwise).
+    double frag = base_frag;
+    std::copy(base_free.begin(), base_free.end(), whole_free.begin());
+    for (const int g : touched) {
+      const bool busy = gpu_avail[g] < gpu_total[g];  // other pods already on this GPU
+      if (busy && gpu_total[g] > 1) s += 6.0 * taken[g];  // pack into partially used GPUs
+      if (busy && multi_gpu) s -= 4.0;  // cross-GPU traffic would share this GPU's links
       const int f = gpu_avail[g] - taken[g];
-      frag += static_cast<double>(f) * f / parts_per_gpu;
-      if (gpu_total[g] > 0 && f == gpu_total[g] && g < 64) whole_free[gpu_numa_slot[g]] |= 1ull << g;
+      frag += (static_cast<double>(f) * f - static_cast<double>(gpu_avail[g]) * gpu_avail[g]) / parts_per_gpu;
+      if (g < 64) whole_free[gpu_numa_slot[g]] &= ~(1ull << g);  // no longer whole and free
+      taken[g] = 0;
     }
     for (uint64_t m : whole_free) {
       const int c = __builtin_popcountll(m) <= 16 ? max_clique(m) : __builtin_popcountll(m);
