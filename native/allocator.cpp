@@ -203,7 +203,10 @@ struct Ctx {
   // interchangeable for every term, so a candidate costs O(classes^2 + gpus) instead of
   // O(|S|^2) - the multi-GPU greedy/local search evaluates hundreds of candidates.
   // (Pair scores are integers, so both pair sums are exact and identical.)
-  double score_counts(const std::vector<int>& cn) const {
+  double score_counts(const std::vector<int>& cn) const { return pair_sum(cn) + set_terms(cn); }
+
+  // the pair-score part of score_counts (an integer: every sum below is exact)
+  double pair_sum(const std::vector<int>& cn) const {
     double s = 0;
     for (int a = 0; a < ncls; ++a) {
       if (!cn[a]) continue;
@@ -211,7 +214,14 @@ struct Ctx {
       for (int b = a + 1; b < ncls; ++b)
         if (cn[b]) s += static_cast<double>(cn[a]) * cn[b] * class_pair(a, b);
     }
-    return s + set_terms(cn);
+    return s;
+  }
+  // how pair_sum(cn) grows when one device of class a joins: sum over b of cn[b] * P(a, b)
+  double pair_gain(const std::vector<int>& cn, int a) const {
+    double s = 0;
+    for (int b = 0; b < ncls; ++b)
+      if (cn[b]) s += static_cast<double>(cn[b]) * class_pair(a, b);
+    return s;
   }
 
   // every term but the pair scores: packing, link sharing, fragmentation
@@ -365,36 +375,44 @@ AllocResult aligned_alloc(const Topology& topo, const std::vector<AllocDevice>& 
       // scores and every per-GPU term depend on nothing else), so each step evaluates
       // only the first unused one of each class - the one the full scan would have
       // kept on a tie anyway.  A 64-partition CPX node: 8 evaluations per step, not 64.
-      std::vector<std::pair<int, int>> seen;
+      // (a class is exactly a (gpu, numa) pair)
+      std::vector<char> seen(ctx.ncls, 0);
       auto first_of_class = [&](int c) {
-        const std::pair<int, int> key(devs[c].gpu, devs[c].numa);
-        if (std::find(seen.begin(), seen.end(), key) != seen.end()) return false;
-        seen.push_back(key);
+        char& s = seen[ctx.cls[c]];
+        if (s) return false;
+        s = 1;
         return true;
       };
-      // class counts of S, updated in place around each candidate evaluation
+      // class counts of S, updated in place around each candidate evaluation; the pair
+      // part of a candidate's score is the current sum plus what the device adds (all
+      // integers, so exactly score_counts' value)
       std::vector<int> cn(ctx.ncls, 0);
       for (int i : required) cn[ctx.cls[i]]++;
+      double pairs = ctx.pair_sum(cn);
       while (static_cast<int>(S.size()) < size) {
         int pick = -1;
-        double ps = -1e300;
-        seen.clear();
+        double ps = -1e300, pick_gain = 0;
+        std::fill(seen.begin(), seen.end(), 0);
         for (int c : cand) {
           if (used[c] || !first_of_class(c)) continue;
-          cn[ctx.cls[c]]++;
-          const double sc = ctx.score_counts(cn);
-          cn[ctx.cls[c]]--;
+          const int a = ctx.cls[c];
+          const double gain = ctx.pair_gain(cn, a);
+          cn[a]++;
+          const double sc = pairs + gain + ctx.set_terms(cn);
+          cn[a]--;
           if (sc > ps + 1e-9) {
             ps = sc;
             pick = c;
+            pick_gain = gain;
           }
         }
         S.push_back(pick);
         cn[ctx.cls[pick]]++;
+        pairs += pick_gain;
         used[pick] = 1;
       }
       // 1-swap local search (bounded)
-      double cur = ctx.score_counts(cn);
+      double cur = pairs + ctx.set_terms(cn);
       // classes whose positions found no improving swap since the last change: another
       // position of the same class would see exactly the same candidates and scores
       std::vector<char> tried(ctx.ncls, 0);
@@ -404,16 +422,20 @@ AllocResult aligned_alloc(const Topology& topo, const std::vector<AllocDevice>& 
           const int k_cls = ctx.cls[S[k]];
           if (tried[k_cls]) continue;
           bool changed = false;
-          seen.clear();
+          std::fill(seen.begin(), seen.end(), 0);
           for (int c : cand) {
             if (used[c] || !first_of_class(c)) continue;
             const int old = S[k];
             if (ctx.cls[old] == ctx.cls[c]) continue;  // same class: same score
+            // pairs without `old`, then with `c` in its place
             cn[ctx.cls[old]]--;
+            const double without = pairs - ctx.pair_gain(cn, ctx.cls[old]);
+            const double with_c = without + ctx.pair_gain(cn, ctx.cls[c]);
             cn[ctx.cls[c]]++;
-            const double sc = ctx.score_counts(cn);
+            const double sc = with_c + ctx.set_terms(cn);
             if (sc > cur + 1e-9) {
               cur = sc;
+              pairs = with_c;
               S[k] = c;
               used[old] = 0;
               used[c] = 1;
