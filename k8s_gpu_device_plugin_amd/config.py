@@ -374,6 +374,14 @@ def validate(cfg: Config) -> Config:
             raise ConfigError("%s.busyPollUs must be within 0..100000" % sect)
     if not 0 <= cfg.grpc.admissionPollUs <= 100000:
         raise ConfigError("grpc.admissionPollUs must be within 0..100000")
+    for key in ("keepWarmMs", "idleWakeMs"):
+        if not 0 <= getattr(cfg.grpc, key) <= 100000:
+            raise ConfigError("grpc.%s must be within 0..100000 (0 = off)" % key)
+    if cfg.grpc.callTraceFile and not 1 <= cfg.grpc.callTraceEntries <= (1 << 26):
+        raise ConfigError("grpc.callTraceEntries must be within 1..%d" % (1 << 26))
+    for sect in ("grpc", "http"):
+        if not 1 <= getattr(cfg, sect).threads <= 256:
+            raise ConfigError("%s.threads must be within 1..256" % sect)
     if cfg.http.server not in ("native", "python"):
         raise ConfigError("http.server must be native|python")
     if cfg.podResources.intervalS <= 0:

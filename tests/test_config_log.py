@@ -62,7 +62,11 @@ def test_env_overrides(tmp_path):
                                  {"resourcePrefix": "AMD.com"}, {"resourcePrefix": "amd..com"},
                                  {"grpc": {"busyPollUs": -1}}, {"http": {"busyPollUs": 200000}},
                                  {"grpc": {"admissionPollUs": 100001}}, {"devices": "hip:"},
-                                 {"devices": "hip:x-2"}])
+                                 {"devices": "hip:x-2"}, {"grpc": {"keepWarmMs": -1}},
+                                 {"grpc": {"idleWakeMs": 100001}}, {"grpc": {"threads": 0}},
+                                 {"http": {"threads": 1000}},
+                                 {"grpc": {"callTraceFile": "/tmp/t.bin", "callTraceEntries": 0}},
+                                 {"backgroundSched": "idle"}])
 def test_validation_errors(raw):
     with pytest.raises(C.ConfigError):
         C.validate(C.from_dict(raw))
