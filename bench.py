@@ -46,6 +46,7 @@ The reference publishes no numbers, so ``vs_baseline`` is null.
 from __future__ import annotations
 
 import argparse
+import collections
 import http.client
 import json
 import os
@@ -249,6 +250,154 @@ def _merge_tail(parts) -> dict:
         out["server_split_p50_us"] = parts[0].get("server_split_p50_us")
     out["slowest"] = sorted((x for p in parts for x in p.get("slowest", [])), key=lambda r: -r["us"])[:8]
     return out
+
+
+def _read(path: str, default=None):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return default
+
+
+def _cpu_list(spec):
+    """'0-3,8,10-11' -> [0, 1, 2, 3, 8, 10, 11] (None for an unreadable list)."""
+    if spec is None:
+        return None
+    out = []
+    for part in spec.split(","):
+        part = part.strip()
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out.extend(range(int(a), int(b or a) + 1))
+    return out
+
+
+def cpu_topology(cpus) -> dict:
+    """For each CPU: (package, core id, SMT siblings, L3 siblings, NUMA node), from sysfs."""
+    out = {}
+    base = "/sys/devices/system/cpu/cpu%d"
+    for c in cpus:
+        d = base % c
+        l3 = None
+        for idx in range(8):
+            if _read("%s/cache/index%d/level" % (d, idx)) == "3":
+                l3 = _cpu_list(_read("%s/cache/index%d/shared_cpu_list" % (d, idx)))
+                break
+        node = None
+        try:
+            node = next(int(x[4:]) for x in os.listdir(d) if x.startswith("node") and x[4:].isdigit())
+        except (OSError, StopIteration):
+            pass
+        out[c] = {"package": _read(d + "/topology/physical_package_id"), "core": _read(d + "/topology/core_id"),
+                  "smt": _cpu_list(_read(d + "/topology/thread_siblings_list")), "l3": l3, "numa": node}
+    return out
+
+
+def cpu_relation(a: int, b: int, topo: dict) -> str:
+    """Where two CPUs sit relative to each other: same_cpu, smt_sibling, same_l3,
+    same_package (another L3 of the socket), other_package, or unknown."""
+    if a == b:
+        return "same_cpu"
+    ta, tb = topo.get(a), topo.get(b)
+    if not ta or not tb:
+        return "unknown"
+    if ta["smt"] and b in ta["smt"]:
+        return "smt_sibling"
+    if ta["l3"] and b in ta["l3"]:
+        return "same_l3"
+    if ta["package"] is not None and ta["package"] == tb["package"]:
+        return "same_package"
+    return "other_package"
+
+
+def host_fingerprint(cpus=()) -> dict:
+    """What a latency number depends on besides the code: CPU model and measured clock,
+    frequency driver and governor, SMT, idle states, CPU quota and set, speculative-execution
+    mitigations (every syscall pays them) and the load, for the CPUs named in `cpus`
+    (the client's and the daemon workers')."""
+    cpuinfo = _read("/proc/cpuinfo", "") or ""
+    model = next((ln.split(":", 1)[1].strip() for ln in cpuinfo.splitlines() if ln.startswith("model name")), None)
+    sysc = "/sys/devices/system/cpu"
+    fp = {"cpu_model": model, "logical_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+          "kernel": os.uname().release, "smt_active": _read(sysc + "/smt/active"),
+          "cpufreq_driver": _read(sysc + "/cpu0/cpufreq/scaling_driver"),
+          "cpufreq_governor": _read(sysc + "/cpu0/cpufreq/scaling_governor"),
+          "amd_pstate": _read(sysc + "/amd_pstate/status"), "boost": _read(sysc + "/cpufreq/boost"),
+          "cpuidle_driver": _read(sysc + "/cpuidle/current_driver"),
+          "cpuidle_governor": _read(sysc + "/cpuidle/current_governor_ro") or _read(sysc + "/cpuidle/current_governor"),
+          "cgroup_cpu_max": _read("/sys/fs/cgroup/cpu.max"),
+          "cgroup_cpuset": _read("/sys/fs/cgroup/cpuset.cpus.effective"),
+          "loadavg": _read("/proc/loadavg")}
+    vul = {}
+    try:
+        for name in sorted(os.listdir(sysc + "/vulnerabilities")):
+            v = _read(sysc + "/vulnerabilities/" + name)
+            if v and not v.startswith("Not affected"):
+                vul[name] = v
+    except OSError:
+        pass
+    fp["mitigations"] = vul
+    per = {}
+    topo = cpu_topology(sorted(set(c for c in cpus if c is not None and c >= 0)))
+    for c, t in topo.items():
+        d = "%s/cpu%d" % (sysc, c)
+        states = []
+        for k in range(16):
+            name = _read("%s/cpuidle/state%d/name" % (d, k))
+            if name is None:
+                break
+            states.append({"name": name, "latency_us": _read("%s/cpuidle/state%d/latency" % (d, k)),
+                           "disabled": _read("%s/cpuidle/state%d/disable" % (d, k)),
+                           "usage": _read("%s/cpuidle/state%d/usage" % (d, k))})
+        per[str(c)] = {**{k: v for k, v in t.items() if k not in ("smt", "l3")},
+                       "smt": t["smt"], "l3_size": len(t["l3"]) if t["l3"] else None,
+                       "cur_khz": _read(d + "/cpufreq/scaling_cur_freq"), "max_khz": _read(d + "/cpufreq/cpuinfo_max_freq"),
+                       "idle_states": states}
+    fp["cpus"] = per
+    return fp
+
+
+def placement_floor(nb, client_cpu: int, sizes, n: int = 3000) -> dict:
+    """The bare spin exchange (uds_roundtrip_floor_spin) between the client's CPU and one
+    CPU of each relation to it that this process may use: p50 us per relation.  Says what
+    a worker on another core, L3 or socket costs on this host, independent of the plugin."""
+    allowed = sorted(os.sched_getaffinity(0))
+    topo = cpu_topology(allowed)
+    picks = {}
+    for c in allowed:
+        rel = cpu_relation(client_cpu, c, topo)
+        if rel not in ("same_cpu", "unknown") and rel not in picks:
+            picks[rel] = c
+    out = {}
+    for rel, c in sorted(picks.items()):
+        try:
+            lat = nb.uds_pingpong(n, 300, *sizes, server_spin=True, client_cpu=client_cpu, server_cpu=c)
+        except RuntimeError as e:
+            out[rel] = {"server_cpu": c, "error": str(e)}
+            continue
+        out[rel] = {"server_cpu": c, "p50_us": round(_pct(lat, 0.5) * 1e6, 2)}
+    return out
+
+
+def _placement_stats(batches, trace, topo_cpus: dict, rpc_allocate: int) -> dict:
+    """Allocate latency by where the daemon's worker ran relative to the client (the
+    worker's CPU is in its call-trace record, the client's in bench_unary_ts)."""
+    import collections
+    if trace is None or not len(trace):
+        return {}
+    starts = [int(s) for b in batches for s in b[0]]
+    lats = [x for b in batches for x in b[1]]
+    cpus = [c for b in batches for c in b[2]]
+    matched = match_calls(starts, lats, trace, rpc_allocate)
+    topo = cpu_topology(sorted(set(cpus) | {int(e["cpu"]) for e in matched if e is not None}))
+    topo_cpus.update(topo)
+    by = collections.defaultdict(list)
+    for x, c, e in zip(lats, cpus, matched):
+        if e is not None:
+            by[cpu_relation(c, int(e["cpu"]), topo)].append(x)
+    return {rel: {"calls": len(v), "p50_us": round(_pct(v, 0.5) * 1e6, 2)} for rel, v in sorted(by.items())}
 
 
 def _server_mean(text: str, rpc: str):
@@ -567,6 +716,14 @@ def main() -> int:
             "canary": canary_res, "body": body_len,
             "device": {"rank": rank, "local_rank": local_rank, "device_id": my_id, "hip_ids": my_hips,
                        "mapped_by": mapped_by}}
+    # where the client and the daemon's worker ran, per call, and what the host is (untimed)
+    topo_cpus = {}
+    mine["placement"] = _placement_stats(rec[5], trace, topo_cpus, n.RPC_ALLOCATE)
+    client_cpus = collections.Counter(c for b in rec[5] for c in b[2])
+    client_cpu = client_cpus.most_common(1)[0][0] if client_cpus else os.sched_getcpu()
+    worker_cpus = collections.Counter(int(c) for c in trace["cpu"]) if trace is not None and len(trace) else {}
+    mine["client_cpus"] = dict(client_cpus.most_common(4))
+    mine["worker_cpus"] = dict(collections.Counter(worker_cpus).most_common(4))
     # Untimed speed-of-light reference: the same send/epoll_wait/recv/send/recv exchange
     # between two threads with no HTTP/2, HPACK or protobuf work (sizes ~ this Allocate's).
     alloc_resp_len = len(alloc_raw(alloc_req))
@@ -605,6 +762,10 @@ def main() -> int:
     # /metrics: one loopback TCP exchange of a scrape's size, polling server
     mine["tcp_scrape_floor_p50"] = _pct(nb.uds_pingpong(3000, 300, 90, body_len + 400, server_spin=True, tcp=True),
                                         0.5)
+    mine["placement_floor"] = placement_floor(nb, client_cpu, sizes)
+    if rank == 0:
+        mine["host"] = host_fingerprint(list(mine["client_cpus"]) + list(mine["worker_cpus"]))
+        mine["host"]["core_ghz"] = round(nb.core_ghz(), 3)
     if rank == 0:  # the daemon's own time per Allocate (decode, lookup, encode), from its histogram
         conn.request("GET", "/metrics")
         text = conn.getresponse().read().decode()
@@ -676,6 +837,12 @@ def main() -> int:
             "scrape_server_mean_us": (round(gathered[0]["server_scrape_mean_s"] * 1e6, 3)
                                       if gathered[0].get("server_scrape_mean_s") else None),
             "scrapes": len(scrapes),
+            # where each Allocate's client and daemon worker ran relative to each other, the
+            # bare exchange between the client's CPU and one CPU of each relation, and the host
+            "placement": {"allocate_by_relation": gathered[0].get("placement"),
+                          "client_cpus": gathered[0].get("client_cpus"), "worker_cpus": gathered[0].get("worker_cpus"),
+                          "floor_spin_by_relation": gathered[0].get("placement_floor")},
+            "host": gathered[0].get("host"),
             "allocate_calls": len(allocs) + len(allocs_native),
             "metrics_bytes": gathered[0]["body"],
             "canary": ({"arch": can[0]["arch"], "hbm_read_gbps": round(min(c["read_gbps"] for c in can), 1),

@@ -45,6 +45,7 @@ CORE_SOURCES = [
     "backend.cpp",
     "fixture_backend.cpp",
     "amdsmi_backend.cpp",
+    "drm_reset.cpp",
     "allocator.cpp",
     "device_table.cpp",
     "health.cpp",

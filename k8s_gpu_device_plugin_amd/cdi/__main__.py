@@ -4,14 +4,16 @@ Writes the CDI spec that gives the device plugin's own container ``/dev/kfd`` wi
 ``privileged: true`` (``deploy/kfd-cdi-patch.yaml`` runs it as an init container and
 names the device in a ``cdi.k8s.io/`` pod annotation).  A hostPath mount of /dev/kfd is
 not in the container's device cgroup; a CDI device node edit is, so amdsmi event
-notification (GPU reset, thermal, VM fault) can be armed by an unprivileged pod.
+notification (GPU reset, thermal, VM fault) can be armed by an unprivileged pod.  The
+AMD GPUs' render nodes go into the same device, for the kernel reset count
+(``health.resetQuery``), unless ``--no-render-nodes``.
 """
 from __future__ import annotations
 
 import argparse
 import sys
 
-from .spec import plugin_kfd_spec, write_spec
+from .spec import amdgpu_render_nodes, plugin_kfd_spec, write_spec
 
 
 def main(argv=None) -> int:
@@ -20,8 +22,12 @@ def main(argv=None) -> int:
     p = sub.add_parser("plugin-kfd", help="CDI spec giving the device plugin's container /dev/kfd")
     p.add_argument("--spec-dir", default="/var/run/cdi")
     p.add_argument("--kfd", default="/dev/kfd")
+    p.add_argument("--no-render-nodes", action="store_true",
+                   help="leave out the GPUs' render nodes (then health.resetQuery has nothing to open)")
+    p.add_argument("--dri-dir", default="/dev/dri")
     args = ap.parse_args(argv)
-    path = write_spec(args.spec_dir, plugin_kfd_spec(args.kfd))
+    renders = [] if args.no_render_nodes else amdgpu_render_nodes(args.dri_dir)
+    path = write_spec(args.spec_dir, plugin_kfd_spec(args.kfd, renders))
     print("wrote", path)
     return 0
 

@@ -51,9 +51,33 @@ PLUGIN_KIND = "amd.com/device-plugin"
 PLUGIN_KFD_DEVICE = PLUGIN_KIND + "=kfd"
 
 
-def plugin_kfd_spec(kfd_path: str = "/dev/kfd") -> dict:
+def plugin_kfd_spec(kfd_path: str = "/dev/kfd", render_nodes=()) -> dict:
+    """``render_nodes``: the GPUs' render nodes, added to the same device so the plugin can
+    also read each GPU's kernel reset count (health.resetQuery; an amdgpu context on the
+    node needs only the node in the container's device cgroup)."""
+    nodes = [_node(kfd_path)] + [_node(p) for p in render_nodes]
     return {"cdiVersion": CDI_VERSION, "kind": PLUGIN_KIND,
-            "devices": [{"name": "kfd", "containerEdits": {"deviceNodes": [_node(kfd_path)]}}]}
+            "devices": [{"name": "kfd", "containerEdits": {"deviceNodes": nodes}}]}
+
+
+def amdgpu_render_nodes(dri_dir: str = "/dev/dri", sys_class: str = "/sys/class/drm") -> list:
+    """The render nodes of AMD GPUs on this host (PCI vendor 0x1002), sorted."""
+    out = []
+    try:
+        names = os.listdir(dri_dir)
+    except OSError:
+        return out
+    for name in sorted(names, key=lambda x: (len(x), x)):
+        if not name.startswith("renderD"):
+            continue
+        try:
+            with open(os.path.join(sys_class, name, "device", "vendor")) as f:
+                if f.read().strip().lower() != "0x1002":
+                    continue
+        except OSError:
+            continue
+        out.append(os.path.join(dri_dir, name))
+    return out
 
 
 def spec_path(spec_dir: str, kind: str) -> str:

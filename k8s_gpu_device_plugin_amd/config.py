@@ -109,6 +109,11 @@ class HealthConfig:
     # health-state.json (kubelet removes only sockets from that directory), a path, or "" /
     # "none" = in memory only
     stateFile: str = "auto"
+    # read each GPU's kernel reset count through an amdgpu context on its render node (no
+    # privileges; needs the node in the container's device cgroup, e.g. deploy/kfd-cdi-patch
+    # .yaml): a reset the driver performs - also one that keeps the GPU firmware running -
+    # clears the uncorrectable-ECC latch without amdsmi event notification
+    resetQuery: bool = True
 
 
 def state_file_path(cfg) -> str:
@@ -128,6 +133,9 @@ class HttpConfig:
     server: str = "native"       # native | python
     busyPollUs: int = 50         # native server: keep polling this long after a request (0 = off)
     restartLocalOnly: bool = False  # GET /restart only from loopback peers (others: 403)
+    # GET /health/clear?gpu=<uuid|bdf|index|device id> (an operator drops a GPU's health
+    # latches) only from loopback peers (kubectl exec / port-forward); false = any peer
+    healthClearLocalOnly: bool = True
 
 
 @dataclass
@@ -144,6 +152,10 @@ class GrpcConfig:
     # a long idle pays, at half the CPU of a 1 ms keepWarmMs and without its collisions
     # with calls 1 ms apart (profiles/r5/idle_ab_wake.json, ab_wake_bench.jsonl)
     idleWakeMs: int = 1
+    # native server: idleWakeMs and keepWarmMs run only this long after a worker's last
+    # kubelet RPC (0 = always).  Outside this admission window the workers sleep: an idle
+    # node pays ~1 wake-up per worker per second for the plugin's gRPC server
+    activeWindowMs: int = 10000
     keepWarmFull: bool = True    # ... through the whole request path of an in-memory connection (else HPACK + table)
     # native server: per-call trace of unary RPCs in a file-backed ring ("" = off), read by
     # bench.py to attribute slow calls; one record per call, callTraceEntries records
@@ -377,6 +389,8 @@ def validate(cfg: Config) -> Config:
     for key in ("keepWarmMs", "idleWakeMs"):
         if not 0 <= getattr(cfg.grpc, key) <= 100000:
             raise ConfigError("grpc.%s must be within 0..100000 (0 = off)" % key)
+    if not 0 <= cfg.grpc.activeWindowMs <= 86400000:
+        raise ConfigError("grpc.activeWindowMs must be within 0..86400000 (0 = always)")
     if cfg.grpc.callTraceFile and not 1 <= cfg.grpc.callTraceEntries <= (1 << 26):
         raise ConfigError("grpc.callTraceEntries must be within 1..%d" % (1 << 26))
     for sect in ("grpc", "http"):

@@ -24,7 +24,8 @@ A node model is a plain dict (also loadable from JSON/YAML)::
      "seed": 1}
 
 Per GPU, ``ecc_uncorrectable`` sets the UE count the hardware reports from the start and
-``fw_clock: false`` stops samples reporting the firmware clock.
+``fw_clock: false`` stops samples reporting the firmware clock; ``reset_query: true`` makes
+them report the kernel's reset count (a plugin that can open the render node).
 """
 from __future__ import annotations
 
@@ -247,6 +248,8 @@ def build_backend(spec):
             be.set_ecc_uncorrectable(gi, int(g["ecc_uncorrectable"]))
         if not g.get("fw_clock", True):
             be.set_fw_clock_reported(gi, False)
+        if g.get("reset_query", False):  # the render node can be opened: kernel reset counts
+            be.set_gpu_reset_query(gi, True)
     links = model.get("links", {}) or {}
     ltype = {"xgmi": n.LINK_XGMI, "pcie": n.LINK_PCIE}.get(str(links.get("type", "xgmi")).lower(), n.LINK_XGMI)
     down = {tuple(sorted(p)) for p in links.get("down", [])}

@@ -103,8 +103,14 @@ class _Watch:
 
 
 class KubeletStub:
-    def __init__(self, plugin_dir: str) -> None:
+    """``redial``: behave like kubelet's device manager on a Register for an endpoint it
+    already watches - drop that connection and its ListAndWatch stream, dial the
+    endpoint again and open a new stream (``reopened`` counts them)."""
+
+    def __init__(self, plugin_dir: str, redial: bool = False) -> None:
         self.plugin_dir = plugin_dir
+        self.redial = redial
+        self.reopened = 0
         self.socket = os.path.join(plugin_dir, v1beta1.KUBELET_SOCKET_NAME)
         self.requests: list = []
         self.registered = threading.Condition()
@@ -117,12 +123,26 @@ class KubeletStub:
             with self.registered:
                 self.requests.append(req)
                 self.registered.notify_all()
+            if self.redial and req.endpoint in self._watches:
+                threading.Thread(target=self._redial, args=(req.endpoint,), daemon=True).start()
             return v1beta1.Empty()
 
         return grpc.method_handlers_generic_handler(v1beta1.REGISTRATION_SERVICE, {
             "Register": grpc.unary_unary_rpc_method_handler(
                 register, request_deserializer=v1beta1.RegisterRequest.FromString,
                 response_serializer=v1beta1.Empty.SerializeToString)})
+
+    def _redial(self, endpoint: str) -> None:
+        old_w, old_c = self._watches.pop(endpoint, None), self._clients.pop(endpoint, None)
+        if old_w is not None:
+            old_w.cancel()
+        if old_c is not None:
+            old_c.close()
+        try:
+            self._watches[endpoint] = _Watch(self.client(endpoint))
+            self.reopened += 1
+        except Exception:  # pragma: no cover - the plugin went away meanwhile
+            pass
 
     def start(self) -> "KubeletStub":
         os.makedirs(self.plugin_dir, exist_ok=True)

@@ -45,7 +45,7 @@ from ..resource import new_resources
 from ..utils.log import get_logger
 from ..utils.util import CloseOnce, parse_device_selector
 from ..utils.version import APP_NAME, VERSION
-from .plugin import AmdDevicePlugin
+from .plugin import AmdDevicePlugin, _socket_ident
 from .state import HealthState
 
 log = get_logger("manager")
@@ -56,6 +56,8 @@ EV_METRICS = "metrics"  # state read by /metrics changed off the manager thread 
 EV_SOCKET_GONE = "socket_gone"  # a *.sock other than kubelet.sock was removed from the plugin dir
 EV_DISCOVERED = "discovered"  # the discovery worker finished: (purpose, gpus, topo, report, error)
 EV_START_CANARY = "start_canary"  # a start-up canary verdict: (identity, partition, ok, why)
+EV_CLEAR = "clear"  # GET /health/clear: (gpu selector, concurrent.futures.Future)
+EV_CANDIDATE_VERIFIED = "candidate_verified"  # recovery canary after a reset candidate: (identity, gen, ok)
 DISCOVERY_RELOAD, DISCOVERY_CHECK = "reload", "check"  # rebuild always / only if the inventory changed
 HEALTH_LOG_LEN = 4096
 SERVER_CHECK_S = 1.0  # gRPC server supervision poll
@@ -186,6 +188,8 @@ class PluginManager:
         self.monitor.set_disabled_checks(disabled_checks_mask(cfg.health.disabledChecks))
         self.monitor.set_pcie_floor(int(cfg.health.pcieMinWidth), float(cfg.health.pcieMinSpeedGTs),
                                     int(cfg.health.pcieDebounceSamples))
+        if hasattr(self.backend, "set_reset_query"):
+            self.backend.set_reset_query(bool(cfg.health.resetQuery))
         self.events: "queue.Queue[tuple]" = queue.Queue()
         self.plugins: list[AmdDevicePlugin] = []
         self.gpus: list = []
@@ -260,6 +264,13 @@ class PluginManager:
         path = state_file_path(cfg)
         self._state = HealthState(path) if path else None
         self._reverify: set[str] = set()  # restored recovery-canary holds to verify once loaded
+        # a /restart (or SIGHUP) is being served: once its reload is done every plugin that
+        # kept its server registers again on the same socket (reference contract, see
+        # _register_again): the monotonic time it was asked for, else None
+        self._register_pending: float | None = None
+        # identities whose next Healthy transition was verified already (the recovery canary
+        # passed after a reset candidate): no second canary for it
+        self._verified_clear: set[str] = set()
 
     # ------------------------------------------------------------ public API
     def restart(self) -> None:
@@ -268,6 +279,18 @@ class PluginManager:
 
     def stop(self) -> None:
         self.events.put((EV_STOP,))
+
+    def clear_health(self, gpu: str, timeout: float = 10.0) -> tuple:
+        """Thread-safe operator clear (``GET /health/clear?gpu=...``): drops the health
+        latches of the GPU ``gpu`` names (identity/UUID, BDF, index or an advertised device
+        ID) on the manager thread.  (HTTP status, data or message).  Raises TimeoutError
+        when the manager does not answer within ``timeout``."""
+        fut = concurrent.futures.Future()
+        self.events.put((EV_CLEAR, str(gpu), fut))
+        try:
+            return fut.result(timeout)
+        except concurrent.futures.TimeoutError:
+            raise TimeoutError("manager busy") from None
 
     def add_readiness_listener(self, fn) -> None:
         """fn(ready, reason) now and on every change of the readiness ``GET /ready`` reports."""
@@ -431,6 +454,17 @@ class PluginManager:
             return False
         if now - p.law_lost_since < LAW_LOST_GRACE_S or not os.path.exists(self.cfg.kubelet_socket):
             return False
+        if _socket_ident(p.socket) != p._sock_ident:
+            # another instance bound this path since (an overlapping old/new pod): kubelet's
+            # stream went to it.  Registering would make kubelet re-dial the path and tear
+            # down the new instance's stream every grace period; leave the path to it (a
+            # deleted socket is EV_SOCKET_GONE's business)
+            if p.law_lost_since is not None and not getattr(p, "_socket_taken_logged", False):
+                p._socket_taken_logged = True
+                self.counters["stream_watch_socket_taken"] = self.counters.get("stream_watch_socket_taken", 0) + 1
+                log.warning("the socket %s of %s is no longer the one this process bound (another instance "
+                            "serves it): not registering again", p.socket, p.resource)
+            return False
         failures = getattr(p, "_reregister_failures", 0)
         if not failures:
             log.warning("kubelet ended the ListAndWatch stream of %s %.0f s ago and did not open another: "
@@ -531,6 +565,8 @@ class PluginManager:
                 kubelet = self._coalesce_restarts()
                 if kubelet:
                     self._reregister()
+                elif self._register_pending is None:
+                    self._register_pending = time.monotonic()
                 self._request_discovery(DISCOVERY_RELOAD)
             elif kind == EV_KUBELET:
                 self.counters["restarts_kubelet"] += 1
@@ -565,11 +601,19 @@ class PluginManager:
                 self._socket_gone(ev[1])
             elif kind == EV_START_CANARY:
                 self._apply_start_canary(*ev[1:])
+            elif kind == EV_CLEAR:
+                self._clear_health(*ev[1:])
+            elif kind == EV_CANDIDATE_VERIFIED:
+                self._apply_candidate_verified(*ev[1:])
         except Exception as e:
             self.counters["load_failures"] += 1
             log.error("event %s failed: %s; retrying in %.0fs", kind, e, self.cfg.retrySeconds)
             self._arm_retry()
-        if kind in (EV_HEALTH, EV_VERIFIED, EV_PRESTART_FAIL, EV_DISCOVERED, EV_START_CANARY):
+            if kind == EV_CLEAR and not ev[2].done():
+                ev[2].set_result((500, "clearing failed: %s" % e))
+        if kind in (EV_HEALTH, EV_VERIFIED, EV_PRESTART_FAIL, EV_DISCOVERED, EV_START_CANARY, EV_CLEAR,
+                    EV_CANDIDATE_VERIFIED):
+            self._sync_held()
             self._save_state()
         self._publish_metrics()
 
@@ -666,6 +710,7 @@ class PluginManager:
         for i, k in key_of.items():
             keys[i] = k
         self.monitor.set_gpus(keys)
+        self._sync_held()
         self.monitor.attach_tables([p.table for p in plugins], not self.cfg.health.canary,
                                    sorted(index_of[k] for k in self._held_unhealthy if k in index_of))
         # the new tables carry every health verdict: put them in service.  A resource that
@@ -814,6 +859,7 @@ class PluginManager:
                       "the current plugins keep serving" if self.plugins else "nothing advertised yet",
                       self.cfg.retrySeconds)
             self._arm_retry()
+            self._register_again()  # what serves still answers: kubelet is pointed at it again
             return
         self._discovery_error = None
         self._note_report(report)
@@ -827,6 +873,37 @@ class PluginManager:
             self.counters["restarts_inventory"] = self.counters.get("restarts_inventory", 0) + 1
             log.warning("device inventory changed (partition mode or GPU set); re-advertising")
         self.restart_plugins(gpus, topo)
+        self._register_again()
+
+    def _register_again(self) -> None:
+        """The end of a ``GET /restart`` (or SIGHUP): every plugin that kept its server
+        through the reload sends ``Register`` again for its still-served socket.  The
+        reference's restart always ends in a fresh Register (``router/api.go:50-54`` ->
+        ``plugin/manager.go:177-194`` -> ``plugin/plugin.go:140-162``), which is the
+        operator's way out when kubelet's view of a plugin went wrong (allocatable 0, a
+        stale endpoint) while its stream may still be open.  The socket is not dropped:
+        kubelet dials the same endpoint again and reopens ListAndWatch, so admissions keep
+        finding it.  A plugin that registered after the restart was asked for (started by this
+        reload, or re-registered by a kubelet restart) is skipped."""
+        since = self._register_pending
+        if since is None:
+            return
+        self._register_pending = None
+        for p in self.plugins:
+            # (one that registered after the restart was asked for has met it already)
+            if not len(p) or not p.serving or not p.registered or p.registered_at >= since:
+                continue
+            try:
+                p.register()
+            except Exception as e:
+                p.registered = False  # start_plugins (the retry timer) registers it later
+                log.error("registering %s again after the restart failed: %s; retrying in %.0fs", p.resource, e,
+                          self.cfg.retrySeconds)
+                self._arm_retry()
+                continue
+            self.counters["registrations"] += 1
+            self.counters["reregistrations_restart"] = self.counters.get("reregistrations_restart", 0) + 1
+            log.info("registered %s again on its running socket (restart)", p.resource)
 
     def _reregister(self) -> None:
         """A kubelet restart drops every registration (and kubelet clears the plugin
@@ -921,13 +998,23 @@ class PluginManager:
         return "GPU %d (%s)" % (i, key) if i is not None else "GPU %s (not advertised)" % key
 
     def _apply_health(self, u) -> None:
+        n = native.load()
         self.counters["health_events"] += 1
-        if u.kind == native.load().EVT_RESET_OBSERVED:  # a reset seen by polling, not by an event
+        if u.kind == n.EVT_RESET_OBSERVED:  # a reset seen by polling, not by an event
             self.counters["resets_observed"] = self.counters.get("resets_observed", 0) + 1
         key = self._key(u)
+        if u.kind == n.EVT_RESET_CANDIDATE:
+            self._reset_candidate(key, u.reason)
+            return
         if u.healthy in (0, 1):
             healthy = bool(u.healthy)
             gen = self._health_gen[key] = self._health_gen.get(key, 0) + 1
+            if healthy and key in self._verified_clear:
+                # the recovery canary that cleared these latches has just passed: no second run
+                self._verified_clear.discard(key)
+                self._held_unhealthy.discard(key)
+                self._set_health(key, u.partition, True, u.reason, apply=self.cfg.health.canary)
+                return
             if healthy and self.cfg.health.canary:
                 # stay Unhealthy until the canary passes; do not block the event loop on it
                 log.info("%s reports healthy (%s); verifying with the canary", self._gpu_name(key), u.reason)
@@ -1010,10 +1097,14 @@ class PluginManager:
     def _set_health(self, key: str, partition: int, healthy: bool, reason: str, apply: bool = True) -> None:
         if healthy:  # a recovery supersedes earlier canary verdicts on this GPU
             self._canary_failed = {k for k in self._canary_failed if k[0] != key}
+            self._sync_held()
         gpu = self._index_of.get(key, -1)
         if gpu >= 0 and apply:  # else the monitor thread has already written the tables
+            held = {part for k, part in self._start_pending if k == key} if healthy else ()
+            if -1 in held:
+                return  # the whole GPU waits for its start-up canary
             for p in self.plugins:
-                p.set_gpu_health(gpu, partition, healthy)
+                p.set_gpu_health(gpu, partition, healthy, held)
         self.health_log.append((time.monotonic(), gpu, int(healthy), reason))
         (log.info if healthy else log.warning)("%s marked %s: %s", self._gpu_name(key),
                                                "Healthy" if healthy else "Unhealthy", reason)
@@ -1109,6 +1200,12 @@ class PluginManager:
         gpu = self._index_of.get(key, -1)
         if not ok:
             self._canary_failed.add((key, part))
+            self._sync_held()
+            # it was advertised Unhealthy while pending, but a recovery in between may have
+            # written the GPU Healthy: the verdict is applied to the tables, not assumed
+            if gpu >= 0:
+                for p in self.plugins:
+                    p.set_gpu_health(gpu, part, False)
             self._count("canary_failures")
             log.error("start-up canary failed on %s partition %d: %s", self._gpu_name(key), part, why)
             return
@@ -1117,6 +1214,119 @@ class PluginManager:
             for p in self.plugins:
                 p.set_gpu_health(gpu, part, True)
         log.info("start-up canary passed on %s partition %d", self._gpu_name(key), part)
+
+    def _sync_held(self) -> None:
+        """Tells the monitor which partitions a recovery must leave Unhealthy: failed
+        canary verdicts and start-up verdicts still pending (its fast path writes Healthy
+        transitions to the tables itself)."""
+        held: dict = {}
+        for k, part in self._canary_failed | self._start_pending:
+            held.setdefault(k, set()).add(part)
+        snap = {k: sorted(v) for k, v in held.items()}
+        if snap != getattr(self, "_held_pushed", None):
+            self.monitor.set_held_partitions(snap)
+            self._held_pushed = snap
+
+    def _reset_candidate(self, key: str, reason: str) -> None:
+        """A latched GPU came back from a telemetry outage and nothing confirmed a reset
+        (no kernel reset count, no firmware clock restart): re-verify it with the recovery
+        canary when one is configured, else leave it latched for an operator."""
+        self.counters["reset_candidates"] = self.counters.get("reset_candidates", 0) + 1
+        if self.cfg.health.canary:
+            log.warning("%s is back from a telemetry outage (%s); verifying it with the canary before its health "
+                        "latches are dropped", self._gpu_name(key), reason)
+            gen = self._health_gen[key] = self._health_gen.get(key, 0) + 1
+            if self._verify_pool is None:
+                self._verify_pool = concurrent.futures.ThreadPoolExecutor(max_workers=4, thread_name_prefix="canary",
+                                                                         initializer=background_thread)
+            self._verify_pool.submit(self._verify_candidate, key, gen)
+            return
+        log.warning("%s is back from a telemetry outage (%s), but nothing confirms a reset: its health latches hold. "
+                    "Once the GPU is known good: GET /health/clear?gpu=%s (or enable health.canary to verify such "
+                    "GPUs automatically)", self._gpu_name(key), reason, key)
+
+    def _verify_candidate(self, key: str, gen: int) -> None:
+        try:
+            ok = self._canary_ok(key)
+        except Exception as e:  # a canary that cannot run does not prove health
+            log.error("recovery canary on %s could not run: %s", self._gpu_name(key), e)
+            ok = False
+        self.events.put((EV_CANDIDATE_VERIFIED, key, gen, ok))
+
+    def _apply_candidate_verified(self, key: str, gen: int, ok: bool) -> None:
+        if self._health_gen.get(key) != gen:
+            log.info("dropping stale canary verdict for %s (newer health event)", self._gpu_name(key))
+            return
+        if not ok:
+            self._count("canary_failures")
+            log.error("%s failed the recovery canary after a telemetry outage: its health latches hold",
+                      self._gpu_name(key))
+            return
+        self._verified_clear.add(key)
+        cleared = self.monitor.clear_latches(key, "recovery canary passed after a telemetry outage")
+        if not cleared:
+            self._verified_clear.discard(key)
+        self.counters["latches_cleared_verified"] = self.counters.get("latches_cleared_verified", 0) + 1
+        log.warning("%s passed the recovery canary after a telemetry outage: cleared %s", self._gpu_name(key),
+                    ", ".join(cleared) or "nothing (no latch was set any more)")
+
+    def _resolve_gpu(self, sel: str):
+        """The identity ``sel`` names: an identity/UUID, a BDF, a GPU index or an advertised
+        device ID (a partition's, or a replica's ``<id>::<n>``).  None when nothing matches."""
+        sel = sel.strip()
+        known = set(self._node_index_of) | set(self._index_of) | set(self.monitor.unhealthy_keys())
+        if sel in known:
+            return sel
+        low = sel.lower()
+        for k in known:
+            if k.lower() == low:
+                return k
+        for bdf in (low, "0000:" + low):  # a BDF, with or without its PCI domain
+            if bdf in self._seen_bdfs:
+                return self._seen_bdfs[bdf]
+        if sel.isdigit() and int(sel) in self._key_of:
+            return self._key_of[int(sel)]
+        base = sel.split("::")[0]
+        for p in self.plugins:
+            for d in p.devices():
+                if d.id == base or d.id.split("::")[0] == base:
+                    return self._key_of.get(d.gpu)
+        return None
+
+    def _clear_health(self, sel: str, fut) -> None:
+        """GET /health/clear: drops GPU ``sel``'s latches (uncorrectable ECC, a reset that
+        never finished, failed canary verdicts, a held recovery canary).  Levels the next
+        samples judge again (telemetry lost, retired pages, PCIe) stay, and are reported;
+        with health.canary the GPU is verified before it is advertised Healthy again."""
+        key = self._resolve_gpu(sel)
+        if key is None:
+            fut.set_result((404, "no GPU matches %r" % sel))
+            return
+        reason = "operator: GET /health/clear"
+        cleared = list(self.monitor.clear_latches(key, reason))
+        failed = sorted(part for k, part in self._canary_failed if k == key)
+        if failed:
+            self._canary_failed = {kp for kp in self._canary_failed if kp[0] != key}
+            cleared.append("canary_failed")
+        if key in self._held_unhealthy:
+            self._held_unhealthy.discard(key)
+            self._reverify.discard(key)
+            cleared.append("recovery_canary_held")
+        self._health_gen[key] = self._health_gen.get(key, 0) + 1  # a canary verdict in flight is stale now
+        self._sync_held()
+        holds = list(self.monitor.holds(key))
+        gpu = self._index_of.get(key, -1)
+        if gpu >= 0 and not holds and (failed or "recovery_canary_held" in cleared) and not self.cfg.health.canary:
+            held = {part for k, part in self._start_pending if k == key}
+            for p in self.plugins:  # what only the manager held: written here
+                p.set_gpu_health(gpu, -1, True, held)
+        self.counters["health_clears"] = self.counters.get("health_clears", 0) + 1
+        self.health_log.append((time.monotonic(), gpu, -1, "%s (cleared: %s)" % (reason, ", ".join(cleared) or "nothing")))
+        log.warning("%s: health latches cleared by an operator: %s%s", self._gpu_name(key),
+                    ", ".join(cleared) or "nothing was latched",
+                    ("; still Unhealthy: " + ", ".join(holds)) if holds else "")
+        fut.set_result((200, {"gpu": key, "index": gpu, "cleared": cleared, "still_unhealthy": holds,
+                              "verify_with_canary": bool(self.cfg.health.canary and not holds and cleared)}))
 
     def _verify_later(self, key: str, partition: int, reason: str) -> None:
         """Holds a GPU Unhealthy and runs the recovery canary on it off the manager thread."""
@@ -1215,9 +1425,13 @@ class PluginManager:
             log.error("failed to create FS watcher on %s: %s", self.cfg.pluginDir, e)
             watcher = None
 
+        self._watcher = watcher  # _shutdown wakes its read
+
         def watch_loop():
+            # a second per read: an idle node pays one wake-up a second for it, and
+            # _shutdown cuts the read short (DirWatcher.wake)
             while self._running.is_set() and watcher is not None:
-                for name, _mask, created, _removed in watcher.read(200):
+                for name, _mask, created, _removed in watcher.read(1000):
                     if name == "kubelet.sock" and created:
                         self.events.put((EV_KUBELET,))
                     elif _removed and name.endswith(".sock") and name != "kubelet.sock":
@@ -1230,7 +1444,7 @@ class PluginManager:
                 if not self.monitor.running:
                     time.sleep(0.1)
                     continue
-                for u in self.monitor.pop(200):
+                for u in self.monitor.pop(1000):  # (returns at once on an update or stop)
                     self.events.put((EV_HEALTH, u))
 
         def rediscover_loop():
@@ -1280,6 +1494,9 @@ class PluginManager:
 
     def _publish_metrics(self) -> None:
         self._push_readiness()  # runs after every event, like the metrics
+        glitches = self.monitor.fw_clock_glitches
+        if glitches:
+            self.counters["fw_clock_glitches"] = glitches
         lines = ["# HELP amdgpu_device_plugin_events_total Plugin manager lifecycle events.",
                  "# TYPE amdgpu_device_plugin_events_total counter"]
         for k in sorted(self.counters):
@@ -1360,6 +1577,8 @@ class PluginManager:
             self._canary_pool.shutdown(wait=False, cancel_futures=True)
         self._stop_flag.set()
         self._running.clear()
+        if getattr(self, "_watcher", None) is not None:
+            self._watcher.wake()
         if self.podres is not None:
             self.podres.stop()
         self.stop_plugins()

@@ -145,6 +145,7 @@ class AmdDevicePlugin:
         self._last_crash = time.monotonic()
         self.server_restarts = 0
         self.registered = False
+        self.registered_at = -1.0  # time.monotonic() of the last successful Register
         self._sock_ident = None  # (st_dev, st_ino) of the socket file this plugin bound
         # PreStartContainer verifier: fn(device ids) -> "" (pass) or an error message
         self.prestart_check = None
@@ -220,6 +221,7 @@ class AmdDevicePlugin:
             self._server, self._native_server = server, nserver
             self._serving, self._stopping = True, False
             self._sock_ident, self.registered = sock_ident, registered
+            self.registered_at = prev.registered_at
             self._crashes, self._last_crash = prev._crashes, prev._last_crash
             self.server_restarts = prev.server_restarts
             self._front = prev._front
@@ -314,6 +316,7 @@ class AmdDevicePlugin:
             srv.set_keep_warm_ms(int(self.cfg.grpc.keepWarmMs))
             srv.set_keep_warm_full(bool(self.cfg.grpc.keepWarmFull))
             srv.set_idle_wake_ms(int(self.cfg.grpc.idleWakeMs))
+            srv.set_active_window_ms(int(self.cfg.grpc.activeWindowMs))
             if self.cfg.grpc.callTraceFile:
                 srv.set_call_trace(self.cfg.grpc.callTraceFile.replace("{resource}", self.resource.get_resource_name()),
                                    int(self.cfg.grpc.callTraceEntries))
@@ -426,7 +429,7 @@ class AmdDevicePlugin:
                 c.close()
             if status != 0:
                 raise RuntimeError("Register with kubelet failed: grpc-status %d %s" % (status, message))
-            self.registered = True
+            self.registered, self.registered_at = True, time.monotonic()
             return
         ch = dial(self.kubelet_socket, DIAL_TIMEOUT_S)
         try:
@@ -436,7 +439,7 @@ class AmdDevicePlugin:
             call = ch.unary_unary(v1beta1.METHOD_REGISTER, request_serializer=v1beta1.RegisterRequest.SerializeToString,
                                   response_deserializer=v1beta1.Empty.FromString)
             call(req, timeout=DIAL_TIMEOUT_S)
-            self.registered = True
+            self.registered, self.registered_at = True, time.monotonic()
         finally:
             close_async(ch)
 
@@ -448,9 +451,14 @@ class AmdDevicePlugin:
         if srv is not None:
             srv.notify()
 
-    def set_gpu_health(self, gpu: int, partition: int, healthy: bool) -> int:
-        """Health lives in the native table only (the Python devices read it from there)."""
-        changed = self.table.set_gpu_health(gpu, partition, healthy)
+    def set_gpu_health(self, gpu: int, partition: int, healthy: bool, held=()) -> int:
+        """Health lives in the native table only (the Python devices read it from there).
+        ``held``: partitions a Healthy whole-GPU update leaves as they are (canary verdicts),
+        in the same table update."""
+        if healthy and partition < 0 and held:
+            changed = self.table.set_gpu_health_except(gpu, sorted(held))
+        else:
+            changed = self.table.set_gpu_health(gpu, partition, healthy)
         if changed:
             self.notify()
         return changed

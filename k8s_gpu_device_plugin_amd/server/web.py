@@ -1,4 +1,5 @@
-"""HTTP ops surface: ``GET /``, ``/metrics``, ``/health``, ``/restart``.
+"""HTTP ops surface: ``GET /``, ``/metrics``, ``/health``, ``/restart``, ``/ready``,
+``/health/clear``.
 
 Reference: ``server/server.go`` (echo, middleware Recover->Cros->Logger->Metrics,
 30 s read timeout), ``router/api.go:27-54`` (routes), ``router/router.go`` (global
@@ -25,7 +26,7 @@ from ..utils.version import VERSION
 
 log = get_logger("web")
 
-ROUTES = ("/", "/metrics", "/health", "/restart", "/ready")
+ROUTES = ("/", "/metrics", "/health", "/restart", "/ready", "/health/clear")
 CORS_HEADERS = (
     ("Access-Control-Allow-Credentials", "true"),
     ("Access-Control-Allow-Headers", "Content-Type, Content-Length, Accept-Encoding, Authorization, Origin"),
@@ -33,6 +34,27 @@ CORS_HEADERS = (
 )
 METRICS_CTYPE = "text/plain; version=0.0.4; charset=utf-8"
 ECHO_BUCKETS = (0.0005, 0.001, 0.002, 0.005, 0.01, 0.02, 0.05, 0.1, 0.2, 0.5, 1.0, 2.0, 5.0, 10.0, 15.0, 20.0, 30.0)
+
+
+def health_clear(manager, query: str) -> tuple:
+    """``GET /health/clear?gpu=<uuid|bdf|index|device id>``: the operator's way to drop a
+    GPU's health latches (uncorrectable ECC, a reset that never finished, failed canary
+    verdicts) once they know it is fine - e.g. after a reset no signal this deployment can
+    see.  Logged, counted (``health_clears``) and persisted like any latch change.
+    Returns (status, JSON body) in the envelope of the other routes."""
+    import urllib.parse
+    gpu = (urllib.parse.parse_qs(query or "").get("gpu") or [""])[0].strip()
+    if not gpu:
+        return 400, envelope_bytes(failed("missing ?gpu=<uuid|bdf|index|device id>")).decode()
+    clear = getattr(manager, "clear_health", None)
+    if clear is None:
+        return 503, envelope_bytes(failed("no health monitor")).decode()
+    try:
+        status, data = clear(gpu)
+    except TimeoutError:
+        return 503, envelope_bytes(failed("the plugin manager did not answer in time")).decode()
+    body = success(data) if status == 200 else failed(data)
+    return status, envelope_bytes(body).decode()
 
 
 class WebServer:
@@ -53,13 +75,16 @@ class WebServer:
             hc.read_timeout_s = 30  # server/server.go:45
             hc.busy_poll_us = int(self.cfg.http.busyPollUs)
             hc.restart_local_only = bool(self.cfg.http.restartLocalOnly)
+            hc.clear_local_only = bool(self.cfg.http.healthClearLocalOnly)
             hc.version = VERSION
             srv = n.HttpServer(hc, self.manager.exporter)
             srv.set_restart_hook(self.manager.restart)
+            srv.set_clear_hook(lambda q: health_clear(self.manager, q))
             self.port = srv.start()
             self._impl = srv
         else:
-            self._impl = PyWebServer(self.host, self.port, self.manager, bool(self.cfg.http.restartLocalOnly))
+            self._impl = PyWebServer(self.host, self.port, self.manager, bool(self.cfg.http.restartLocalOnly),
+                                     bool(self.cfg.http.healthClearLocalOnly))
             self.port = self._impl.start()
         for r in ROUTES:  # server/server.go:48-54 prints the route table
             log.info("GET  %s", r)
@@ -143,9 +168,11 @@ class _Metrics:
 
 
 class PyWebServer:
-    def __init__(self, host: str, port: int, manager, restart_local_only: bool = False) -> None:
+    def __init__(self, host: str, port: int, manager, restart_local_only: bool = False,
+                 clear_local_only: bool = True) -> None:
         self.host, self.port, self.manager = host, port, manager
         self.restart_local_only = restart_local_only
+        self.clear_local_only = clear_local_only
         self.ready, self.not_ready_reason = True, ""
         self.metrics = _Metrics()
         self._httpd = None
@@ -163,7 +190,7 @@ class PyWebServer:
                 log.debug("%s %s", self.address_string(), fmt % args)
 
             def _send(self, status: int, body: bytes, ctype: str = "application/json", gz: bool = False) -> None:
-                self.send_response_only(status, {200: "OK", 403: "Forbidden", 404: "Not Found",
+                self.send_response_only(status, {200: "OK", 400: "Bad Request", 403: "Forbidden", 404: "Not Found",
                                                  405: "Method Not Allowed", 503: "Service Unavailable"}.get(status))
                 for k, v in CORS_HEADERS:
                     self.send_header(k, v)
@@ -199,6 +226,11 @@ class PyWebServer:
                         status, body, ctype = 200, envelope_bytes(success("ready")), "application/json"
                     else:
                         status, body, ctype = 503, envelope_bytes(failed(outer.not_ready_reason)), "application/json"
+                elif path == "/health/clear" and outer.clear_local_only and not _is_loopback(self.client_address[0]):
+                    status, body, ctype = 403, b'{"message":"Forbidden"}\n', "application/json"
+                elif path == "/health/clear":
+                    st, text = health_clear(outer.manager, self.path.split("?", 1)[1] if "?" in self.path else "")
+                    status, body, ctype = st, text.encode(), "application/json"
                 elif path == "/restart" and outer.restart_local_only and not _is_loopback(self.client_address[0]):
                     status, body, ctype = 403, b'{"message":"Forbidden"}\n', "application/json"
                 elif path == "/restart":

@@ -17,12 +17,14 @@
 #include <cstring>
 #include <fstream>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
 #include "backend.h"
+#include "drm_reset.h"
 
 namespace amdgpu_dp {
 
@@ -224,6 +226,8 @@ class AmdSmiBackend : public Backend {
   // The blocking wait enters the session first, then takes evt_mu_: disarming (which
   // takes the same lock) waits for an in-flight wait to return instead of stopping
   // notification underneath it, and a re-initialisation (gate closed) never waits on it.
+  bool delivers_events() const override { return evt_live_.load() && !closed_.load(); }
+
   int wait_events(int timeout_ms, std::vector<HwEvent>* out) override {
     amdsmi_evt_notification_data_t data[16];
     uint32_t num = 16;
@@ -493,6 +497,17 @@ class AmdSmiBackend : public Backend {
       if (valid64(m.pcie_l0_to_recov_count_acc)) s->pcie_recoveries = static_cast<double>(m.pcie_l0_to_recov_count_acc);
       if (valid64(m.firmware_timestamp) && m.firmware_timestamp != 0) s->fw_clock_s = m.firmware_timestamp * 1e-8;
     }
+    if (reset_query()) {  // the kernel's reset count, through the GPU's first render node
+      const auto& parts = inv.gpus[gpu].partitions;
+      const int minor = parts.empty() ? -1 : parts.front().render_minor;
+      if (minor > 0) {
+        const std::string path = "/dev/dri/renderD" + std::to_string(minor);
+        if (!ds->reset_watch || ds->reset_watch->path() != path) ds->reset_watch = std::make_unique<DrmResetWatch>(path);
+        s->reset_count = ds->reset_watch->poll();
+      }
+    } else if (ds->reset_watch) {
+      ds->reset_watch.reset();
+    }
     s->num_partitions = std::min(nparts, kMaxPartitions);
     partition_busy(*ds, ref, mst == AMDSMI_STATUS_SUCCESS ? &m : nullptr, s);
     t = charge(kCallPartitionMetrics, t);
@@ -687,6 +702,7 @@ class AmdSmiBackend : public Backend {
   struct DevState {
     LinkCache links;
     BadPages pages;
+    std::unique_ptr<DrmResetWatch> reset_watch;  // the render node's amdgpu context (health.resetQuery)
     int partition_api = 0;  // amdsmi_get_gpu_partition_metrics_info: 0 untried, 1 answers, -1 not supported
   };
   std::shared_ptr<DevState> dev(const std::string& key) {

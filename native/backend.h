@@ -207,6 +207,11 @@ struct GpuSample {
   // the clock restarting is a reset an unprivileged reader can see without amdsmi event
   // notification (which needs /dev/kfd).  -1 = not reported.
   double fw_clock_s = -1;
+  // GPU resets the kernel reports for this device since the backend started watching it
+  // (amdgpu context query on the GPU's render node: the driver's own reset counter moved).
+  // Attested by the kernel, so it covers resets that leave the firmware running (mode-2,
+  // engine resets).  -1 = not available (the render node cannot be opened here).
+  int64_t reset_count = -1;
   bool ok = false;
 };
 
@@ -231,6 +236,14 @@ enum EventKind : int {
   // came back from a telemetry outage on a GPU that reports no firmware clock.  Acts
   // like POST_RESET: clears the reset and uncorrectable-ECC latches.
   kEvtResetObserved = 15,
+  // The GPU came back from a telemetry outage of failed samples (what a reset looks like
+  // to a poller) but nothing confirms a reset: no kernel reset count, no firmware clock
+  // restart, no reset uncorrectable-ECC counter.  Informational: the latches hold; the
+  // manager re-verifies the GPU with the recovery canary when it is configured.
+  kEvtResetCandidate = 16,
+  // Latches (uncorrectable ECC, reset in progress) dropped by a re-verification or an
+  // operator (HealthMonitor::clear_latches): acts like a reset for the health state.
+  kEvtLatchCleared = 17,
 };
 
 const char* event_kind_name(int kind);
@@ -334,6 +347,10 @@ class Backend : public std::enable_shared_from_this<Backend> {
   // A lane whose call has been in flight longer than this takes no more work (0: never).
   void set_stall_ms(int ms) { stall_ms_.store(ms > 0 ? ms : 0); }
   int stall_ms() const { return stall_ms_.load(); }
+  // health.resetQuery: samples read the kernel's reset count through an amdgpu context on
+  // each GPU's render node (GpuSample::reset_count) where the node can be opened.
+  void set_reset_query(bool on) { reset_query_.store(on); }
+  bool reset_query() const { return reset_query_.load(); }
 
   // Block up to timeout_ms for hardware events; append to *out.  Returns count.
   virtual int wait_events(int timeout_ms, std::vector<HwEvent>* out) = 0;
@@ -341,6 +358,9 @@ class Backend : public std::enable_shared_from_this<Backend> {
   virtual void arm_events() {}
   // Number of processors with hardware event delivery armed (0 = polling only).  Never blocks.
   virtual int armed_event_sources() const { return 0; }
+  // Whether wait_events has anything to wait on (armed sources, a fixture's scripts).  When
+  // not, the health monitor's event thread sleeps a second at a time instead of calling it.
+  virtual bool delivers_events() const { return true; }
   // Drop cached device handles so the next discover() enumerates afresh (a compute
   // partition change creates new processors).  Returns false when not possible.
   virtual bool reinit() { return true; }
@@ -398,6 +418,7 @@ class Backend : public std::enable_shared_from_this<Backend> {
   std::atomic<uint64_t> batch_seq_{0};
   SessionGate gate_;
   std::atomic<int> call_timeout_ms_{10000};
+  std::atomic<bool> reset_query_{true};
   std::atomic<int> stall_ms_{0};
   std::atomic<int64_t> last_completion_ns_{0};
   // one discovery at a time (a flag + condition: libstdc++'s timed mutex waits are not

@@ -179,6 +179,7 @@ PYBIND11_MODULE(_native, m) {
       .def_readonly("pcie_replays", &GpuSample::pcie_replays)
       .def_readonly("pcie_recoveries", &GpuSample::pcie_recoveries)
       .def_readonly("fw_clock_s", &GpuSample::fw_clock_s)
+      .def_readonly("reset_count", &GpuSample::reset_count)
       .def_property_readonly("links", [](const GpuSample& s) {
         py::list l;
         for (int k = 0; k < s.num_links; ++k)
@@ -211,6 +212,8 @@ PYBIND11_MODULE(_native, m) {
   m.attr("EVT_PCIE_RESTORED") = static_cast<int>(kEvtPcieRestored);
   m.attr("EVT_LINK_QUALITY") = static_cast<int>(kEvtLinkQuality);
   m.attr("EVT_RESET_OBSERVED") = static_cast<int>(kEvtResetObserved);
+  m.attr("EVT_RESET_CANDIDATE") = static_cast<int>(kEvtResetCandidate);
+  m.attr("EVT_LATCH_CLEARED") = static_cast<int>(kEvtLatchCleared);
   m.attr("EVT_FIXTURE_FIRMWARE_RESET") = FixtureBackend::kScriptFirmwareReset;
   m.attr("LINK_INTERNAL") = static_cast<int>(kLinkInternal);
   m.attr("LINK_PCIE") = static_cast<int>(kLinkPcie);
@@ -273,6 +276,7 @@ PYBIND11_MODULE(_native, m) {
       .def("set_call_timeout_ms", &Backend::set_call_timeout_ms)
       .def_property_readonly("call_timeout_ms", &Backend::call_timeout_ms)
       .def("set_stall_ms", &Backend::set_stall_ms)
+      .def("set_reset_query", &Backend::set_reset_query, py::arg("on"))
       .def_property_readonly("stall_ms", &Backend::stall_ms)
       .def("last_discovery",
            [](const Backend& b) {
@@ -324,6 +328,11 @@ PYBIND11_MODULE(_native, m) {
       .def("set_gpu_present", &FixtureBackend::set_gpu_present)
       .def("reset_firmware", &FixtureBackend::reset_firmware)
       .def("set_fw_clock_reported", &FixtureBackend::set_fw_clock_reported, py::arg("gpu"), py::arg("reported"))
+      .def("set_fw_clock_frozen", &FixtureBackend::set_fw_clock_frozen, py::arg("gpu"), py::arg("frozen"),
+           py::arg("at_s") = -1.0)
+      .def("glitch_fw_clock", &FixtureBackend::glitch_fw_clock, py::arg("gpu"), py::arg("value_s"))
+      .def("set_gpu_reset_query", &FixtureBackend::set_gpu_reset_query, py::arg("gpu"), py::arg("available"))
+      .def("reset_gpu", &FixtureBackend::reset_gpu, py::arg("gpu"), py::arg("reload_firmware"))
       .def("set_sample_fail", &FixtureBackend::set_sample_fail, py::arg("gpu"), py::arg("fail"))
       .def("set_events_enabled", &FixtureBackend::set_events_enabled, py::arg("on"))
       .def_property_readonly("discover_calls", &FixtureBackend::discover_calls);
@@ -461,6 +470,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("aligned_supported", &DeviceTable::aligned_supported)
       .def("set_health", [](DeviceTable& t, const std::string& id, bool h) { return t.set_health(id, h); })
       .def("set_gpu_health", &DeviceTable::set_gpu_health)
+      .def("set_gpu_health_except", &DeviceTable::set_gpu_health_except, py::arg("gpu"), py::arg("held"))
       .def("healthy", [](const DeviceTable& t, const std::string& id) { return t.healthy(id); })
       .def("healthy_count", &DeviceTable::healthy_count)
       .def("set_link_up", &DeviceTable::set_link_up)
@@ -587,7 +597,14 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("events_seen", &HealthMonitor::events_seen)
       .def("latches", &HealthMonitor::latches)
       .def("restore_latches", &HealthMonitor::restore_latches, py::call_guard<py::gil_scoped_release>())
-      .def_property_readonly("resets_observed", &HealthMonitor::resets_observed);
+      .def_property_readonly("resets_observed", &HealthMonitor::resets_observed)
+      .def_property_readonly("reset_candidates", &HealthMonitor::reset_candidates)
+      .def_property_readonly("fw_clock_glitches", &HealthMonitor::fw_clock_glitches)
+      .def("clear_latches", &HealthMonitor::clear_latches, py::arg("key"), py::arg("reason"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("holds", &HealthMonitor::holds, py::arg("key"))
+      .def("set_held_partitions", &HealthMonitor::set_held_partitions, py::arg("held"),
+           py::call_guard<py::gil_scoped_release>());
 
   // ---- exporter ----
   py::class_<PartitionLabel>(m, "PartitionLabel")
@@ -642,6 +659,7 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("read_timeout_s", &HttpConfig::read_timeout_s)
       .def_readwrite("busy_poll_us", &HttpConfig::busy_poll_us)
       .def_readwrite("restart_local_only", &HttpConfig::restart_local_only)
+      .def_readwrite("clear_local_only", &HttpConfig::clear_local_only)
       .def_readwrite("version", &HttpConfig::version);
 
   py::class_<HttpServer, std::shared_ptr<HttpServer>>(m, "HttpServer")
@@ -677,6 +695,28 @@ PYBIND11_MODULE(_native, m) {
             e.discard_as_unraisable("restart hook");
           }
         });
+      })
+      .def("set_clear_hook", [](HttpServer& s, py::object fn) {
+        // fn(query: str) -> (status: int, body: str); GET /health/clear
+        if (fn.is_none()) {
+          s.set_clear_hook(nullptr);
+          return;
+        }
+        auto holder = std::shared_ptr<py::object>(new py::object(fn), [](py::object* o) {
+          py::gil_scoped_acquire g;
+          delete o;
+        });
+        s.set_clear_hook([holder](const std::string& query) -> std::pair<int, std::string> {
+          py::gil_scoped_acquire g;
+          try {
+            auto r = (*holder)(query).cast<std::pair<int, std::string>>();
+            return r;
+          } catch (py::error_already_set& e) {
+            e.discard_as_unraisable("health clear hook");
+          } catch (const std::exception&) {
+          }
+          return {500, "{\"message\":\"Internal Server Error\"}\n"};
+        });
       });
 
   // ---- fs watch ----
@@ -695,6 +735,7 @@ PYBIND11_MODULE(_native, m) {
            },
            py::arg("timeout_ms") = 200)
       .def("close", &DirWatcher::close)
+      .def("wake", &DirWatcher::wake)
       .def_property_readonly("dir", &DirWatcher::dir);
 
   // ---- native gRPC (HTTP/2) server + client ----
@@ -705,6 +746,8 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("table_swaps", &GrpcServer::table_swaps)
       .def("set_call_trace", &GrpcServer::set_call_trace, py::arg("path"), py::arg("capacity") = 65536)
       .def("set_idle_wake_ms", &GrpcServer::set_idle_wake_ms, py::arg("ms"))
+      .def("set_active_window_ms", &GrpcServer::set_active_window_ms, py::arg("ms"))
+      .def_property_readonly("idle_wakeups", &GrpcServer::idle_wakeups)
       .def("add_table", &GrpcServer::set_table)
       .def("start", &GrpcServer::start, py::call_guard<py::gil_scoped_release>())
       .def("stop", &GrpcServer::stop, py::call_guard<py::gil_scoped_release>())

@@ -90,6 +90,8 @@ const char* event_kind_name(int kind) {
     case kEvtPcieDegraded: return "pcie_link_degraded";
     case kEvtPcieRestored: return "pcie_link_restored";
     case kEvtResetObserved: return "gpu_reset_observed";
+    case kEvtResetCandidate: return "gpu_reset_candidate";
+    case kEvtLatchCleared: return "health_latch_cleared";
     default: return "none";
   }
 }

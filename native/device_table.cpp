@@ -180,6 +180,28 @@ int DeviceTable::set_gpu_health(int gpu, int partition, bool healthy) {
   return changed;
 }
 
+int DeviceTable::set_gpu_health_except(int gpu, const std::vector<int>& held) {
+  std::unique_lock<std::mutex> lk(wmu_);
+  int changed = 0;
+  for (size_t i = 0; i < devs_.size(); ++i) {
+    const auto& d = devs_[i];
+    if (d.gpu != gpu) continue;
+    // a held partition stays as it is, and so does a whole-GPU device that contains one
+    if (d.partition < 0 ? !held.empty() : std::find(held.begin(), held.end(), d.partition) != held.end()) continue;
+    if (!is_healthy(static_cast<int>(i))) {
+      health_[i].store(1, std::memory_order_release);
+      ++changed;
+    }
+  }
+  if (changed) {
+    publish_law_locked();
+    version_.fetch_add(1, std::memory_order_acq_rel);
+    lk.unlock();
+    notify_listeners();
+  }
+  return changed;
+}
+
 bool DeviceTable::healthy(std::string_view id) const {
   const int i = index_of(id);
   return i >= 0 && is_healthy(i);

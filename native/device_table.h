@@ -96,6 +96,10 @@ class DeviceTable {
   // Health: return true if anything changed (ListAndWatch version bumps).
   bool set_health(std::string_view id, bool healthy);
   int set_gpu_health(int gpu, int partition, bool healthy);
+  // Every device of `gpu` Healthy except the partitions in `held` (and a whole-GPU device
+  // containing one), in one update: a recovery that must not re-advertise partitions a
+  // canary failed on.
+  int set_gpu_health_except(int gpu, const std::vector<int>& held);
   bool healthy(std::string_view id) const;
   int healthy_count() const;
   void set_link_up(int a, int b, bool up);

@@ -76,6 +76,10 @@ void FixtureBackend::add_gpu(const GpuInfo& g) {
   // the kernel did, ~180 s ahead of CLOCK_MONOTONIC zero
   fw_start_ns_.push_back(-180000000000LL);
   fw_reported_.push_back(true);
+  fw_frozen_at_.push_back(-1);
+  fw_glitch_.push_back(-1);
+  gpu_reset_query_.push_back(false);
+  reset_count_.push_back(0);
   sample_fail_.push_back(false);
 }
 
@@ -104,6 +108,10 @@ void FixtureBackend::clear() {
   present_.clear();
   fw_start_ns_.clear();
   fw_reported_.clear();
+  fw_frozen_at_.clear();
+  fw_glitch_.clear();
+  gpu_reset_query_.clear();
+  reset_count_.clear();
   sample_fail_.clear();
   scheduled_.clear();
   pending_.clear();
@@ -193,6 +201,44 @@ void FixtureBackend::set_fw_clock_reported(int gpu, bool reported) {
   fw_reported_[gpu] = reported;
 }
 
+void FixtureBackend::set_fw_clock_frozen(int gpu, bool frozen, double at_s) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (gpu < 0 || gpu >= static_cast<int>(fw_frozen_at_.size())) throw std::out_of_range("bad gpu");
+  if (frozen && at_s >= 0) {
+    fw_frozen_at_[gpu] = at_s;
+    return;
+  }
+  if (frozen == (fw_frozen_at_[gpu] >= 0)) return;
+  if (frozen) {
+    fw_frozen_at_[gpu] = std::max<int64_t>(0, mono_ns() - fw_start_ns_[gpu]) * 1e-9;
+  } else {  // runs on from the frozen value
+    fw_start_ns_[gpu] = mono_ns() - static_cast<int64_t>(fw_frozen_at_[gpu] * 1e9);
+    fw_frozen_at_[gpu] = -1;
+  }
+}
+
+void FixtureBackend::glitch_fw_clock(int gpu, double value_s) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (gpu < 0 || gpu >= static_cast<int>(fw_glitch_.size())) throw std::out_of_range("bad gpu");
+  fw_glitch_[gpu] = std::max(0.0, value_s);
+}
+
+void FixtureBackend::set_gpu_reset_query(int gpu, bool available) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (gpu < 0 || gpu >= static_cast<int>(gpu_reset_query_.size())) throw std::out_of_range("bad gpu");
+  gpu_reset_query_[gpu] = available;
+}
+
+void FixtureBackend::reset_gpu(int gpu, bool reload_firmware) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (gpu < 0 || gpu >= static_cast<int>(reset_count_.size())) throw std::out_of_range("bad gpu");
+  ++reset_count_[gpu];
+  if (reload_firmware) {
+    fw_start_ns_[gpu] = mono_ns();
+    if (fw_frozen_at_[gpu] >= 0) fw_frozen_at_[gpu] = -1;  // the reloaded firmware runs
+  }
+}
+
 void FixtureBackend::set_sample_fail(int gpu, bool fail) {
   std::lock_guard<std::mutex> lk(mu_);
   if (gpu < 0 || gpu >= static_cast<int>(sample_fail_.size())) throw std::out_of_range("bad gpu");
@@ -272,7 +318,12 @@ bool FixtureBackend::sample_device(const Inventory& inv, int index, GpuSample* s
   s->pcie_link_speed_gtps = pcie_[gpu].second;
   s->pcie_replays = 0;
   s->pcie_recoveries = 0;
-  s->fw_clock_s = fw_reported_[gpu] ? std::max<int64_t>(0, mono_ns() - fw_start_ns_[gpu]) * 1e-9 : -1;
+  s->fw_clock_s = !fw_reported_[gpu]         ? -1
+                  : fw_glitch_[gpu] >= 0     ? fw_glitch_[gpu]
+                  : fw_frozen_at_[gpu] >= 0  ? fw_frozen_at_[gpu]
+                                             : std::max<int64_t>(0, mono_ns() - fw_start_ns_[gpu]) * 1e-9;
+  fw_glitch_[gpu] = -1;
+  s->reset_count = gpu_reset_query_[gpu] && reset_query() ? reset_count_[gpu] : -1;
   for (int peer = 0; peer < topo_.n && s->num_links < kMaxXgmiLinks; ++peer) {
     if (peer == gpu || topo_.at(gpu, peer).type != kLinkXgmi) continue;
     const int k = s->num_links++;

@@ -62,6 +62,19 @@ class FixtureBackend : public Backend {
   void reset_firmware(int gpu);
   // Whether samples report the firmware clock (some firmware does not).
   void set_fw_clock_reported(int gpu, bool reported);
+  // The firmware clock stops (a hung SMU) - where it is, or at `at_s` seconds when >= 0 -
+  // or runs again from there.
+  void set_fw_clock_frozen(int gpu, bool frozen, double at_s = -1);
+  // The next sample alone reports this clock value (one stale or garbage reading).
+  void glitch_fw_clock(int gpu, double value_s);
+  // Whether samples report the kernel's reset count (GpuSample::reset_count): the render
+  // node can be opened (CDI-injected or privileged), or not (the default DaemonSet).
+  void set_gpu_reset_query(int gpu, bool available);
+  // The driver resets the GPU: the kernel's reset count moves; reload_firmware = a reset
+  // that reloads the power-management firmware (mode-1: its clock starts again), else one
+  // that keeps it running (mode-2, engine resets).  Telemetry failing meanwhile is the
+  // caller's to model (set_sample_fail).
+  void reset_gpu(int gpu, bool reload_firmware);
   // Telemetry of `gpu` fails (returns at once, unlike a wedge) while the GPU stays enumerated:
   // a GPU in the middle of a reset.
   void set_sample_fail(int gpu, bool fail);
@@ -103,6 +116,10 @@ class FixtureBackend : public Backend {
   std::vector<bool> present_;
   std::vector<int64_t> fw_start_ns_;   // CLOCK_MONOTONIC ns the GPU's firmware started at
   std::vector<bool> fw_reported_;
+  std::vector<double> fw_frozen_at_;   // >= 0: the clock reads this, frozen
+  std::vector<double> fw_glitch_;      // >= 0: the next sample reads this once
+  std::vector<bool> gpu_reset_query_;
+  std::vector<int64_t> reset_count_;
   std::vector<bool> sample_fail_;
   std::atomic<bool> events_enabled_{true};
   std::string key_of_slot_locked(int slot) const;

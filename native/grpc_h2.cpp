@@ -609,6 +609,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
   };
   std::string scratch;
   bool admitting = false;  // a GetPreferredAllocation was answered in this batch
+  int64_t last_rpc = 0;    // mono ns of this worker's last kubelet RPC (admission window)
   // call trace (set_call_trace): when the events being handled were delivered, whether the
   // worker was polling then, and the records of this batch still waiting for their send
   int64_t wake_ts = 0;
@@ -654,7 +655,10 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
     }
     s.dispatched = true;
     const int64_t t0 = mono_ns();
-    if (!c.internal) requests_.add();
+    if (!c.internal) {
+      requests_.add();
+      last_rpc = t0;  // opens (extends) this worker's admission window
+    }
     const Method m = static_cast<Method>(s.method);
     if (trace_ && !c.internal && m != kMLaw && m != kMPreStart) {
       const uint64_t idx = trace_next++;
@@ -1127,13 +1131,19 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
         continue;
       }
     } else {
-      const int warm = keep_warm_ms_.load(std::memory_order_relaxed);
-      // a worker that holds a connection wakes at least every idle_wake_ms (keeps its core
-      // out of deep idle states: what the first request after a long idle pays most of)
-      const int wake = w->conns.empty() ? 0 : idle_wake_ms_.load(std::memory_order_relaxed);
-      int timeout = warm > 0 ? std::min(warm, 100) : 100;
+      // Within the admission window (a kubelet RPC less than active_window_ms ago): keep-warm
+      // ticks, and a worker that holds a connection wakes at least every idle_wake_ms (keeps
+      // its core out of deep idle states: what the first request after a long idle pays most
+      // of).  Outside it: nothing runs; the worker sleeps until a request, a notify, a table
+      // swap or stop (all of which write its eventfd), with a 1 s safety tick.
+      const int window = active_window_ms_.load(std::memory_order_relaxed);
+      const bool active = window == 0 || (last_rpc != 0 && mono_ns() - last_rpc < static_cast<int64_t>(window) * 1000000);
+      const int warm = active ? keep_warm_ms_.load(std::memory_order_relaxed) : 0;
+      const int wake = (!active || w->conns.empty()) ? 0 : idle_wake_ms_.load(std::memory_order_relaxed);
+      int timeout = warm > 0 ? std::min(warm, 100) : (active ? 100 : 1000);
       if (wake > 0) timeout = std::min(timeout, wake);
       n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), timeout);
+      if (n == 0) idle_wakeups_.fetch_add(1, std::memory_order_relaxed);
       if (n == 0 && warm > 0 && !w->conns.empty() && !warm_alloc.empty()) {
         const int64_t now = mono_ns();
         if (now - last_activity >= static_cast<int64_t>(warm) * 1000000) {

@@ -118,6 +118,14 @@ class GrpcServer {
   // keep-warm period / 100 ms): the wake-ups alone, no work, keep its core from settling
   // into a deep idle state whose exit the next request would pay (grpc.idleWakeMs).
   void set_idle_wake_ms(int ms) { idle_wake_ms_.store(ms > 0 ? ms : 0); }
+  // Admission window (grpc.activeWindowMs, 0 = always): idle wake-ups and keep-warm ticks
+  // run only for this long after a worker's last kubelet RPC.  Outside it the worker sleeps
+  // in epoll_wait for up to a second at a time: an idle node pays nothing for the plugin,
+  // and a pod admission's first call (GetPreferredAllocation) opens the window for the
+  // Allocate that follows it.
+  void set_active_window_ms(int ms) { active_window_ms_.store(ms > 0 ? ms : 0); }
+  // Epoll wake-ups of the workers that found nothing to do (timeouts), all workers.
+  uint64_t idle_wakeups() const { return idle_wakeups_.load(); }
   std::vector<int> worker_connections() const;  // connections owned per worker thread
   const std::string& socket_path() const { return path_; }
 
@@ -151,6 +159,8 @@ class GrpcServer {
   std::atomic<int> keep_warm_ms_{0};
   std::atomic<bool> keep_warm_full_{true};
   std::atomic<int> idle_wake_ms_{0};
+  std::atomic<int> active_window_ms_{0};
+  std::atomic<uint64_t> idle_wakeups_{0};
   std::atomic<uint64_t> warm_ticks_{0};
   // table_ and table_gen_ change together under swap_mu_ (never held across anything else);
   // workers poll table_gen_ (one relaxed load per loop) and take table_ when it moved

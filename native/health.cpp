@@ -88,6 +88,13 @@ void HealthMonitor::loop() {
       if (stop_) return;
     }
     evs.clear();
+    if (!backend_->delivers_events()) {
+      // nothing armed (an unprivileged pod): health runs on polling; sleep until stop() or
+      // a second has passed (arming may happen later, after a re-initialisation)
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_wait_ms(cv_, lk, 1000, [&] { return stop_; });
+      continue;
+    }
     // bounded wait so stop() is honoured within ~200 ms
     backend_->wait_events(200, &evs);
     for (const auto& e : evs) process(e);
@@ -148,8 +155,10 @@ void HealthMonitor::reconcile_locked(const std::string& key, int kind, const std
     return;
   }
   st.reported_healthy = healthy;
-  if (idx >= 0 && (!healthy || fast_recover_))
-    for (const auto& t : fast_tables_) t->set_gpu_health(idx, -1, healthy);
+  if (idx >= 0 && !healthy)
+    for (const auto& t : fast_tables_) t->set_gpu_health(idx, -1, false);
+  else if (idx >= 0 && fast_recover_)
+    write_healthy_locked(idx, key);
   HealthUpdate u;
   u.kind = kind;
   u.gpu = idx;
@@ -157,6 +166,16 @@ void HealthMonitor::reconcile_locked(const std::string& key, int kind, const std
   u.healthy = healthy ? 1 : 0;
   u.reason = reason;
   emit_locked(std::move(u));
+}
+
+void HealthMonitor::write_healthy_locked(int idx, const std::string& key) {
+  const auto it = held_parts_.find(key);
+  if (it == held_parts_.end() || it->second.empty()) {
+    for (const auto& t : fast_tables_) t->set_gpu_health(idx, -1, true);
+    return;
+  }
+  if (std::find(it->second.begin(), it->second.end(), -1) != it->second.end()) return;  // the whole GPU is held
+  for (const auto& t : fast_tables_) t->set_gpu_health_except(idx, it->second);
 }
 
 void HealthMonitor::process(const HwEvent& e) {
@@ -181,6 +200,7 @@ void HealthMonitor::process(const HwEvent& e) {
       st.resetting = false;
       st.ecc_bad = false;  // a reset clears the uncorrectable-error latch
       st.restored = false;
+      st.candidate = false;
       st.ecc_reason.clear();
       // POST_RESET arrives on its own: re-baseline on the next sample.  A reset observed
       // by polling comes from the sample that already took the new baseline.
@@ -314,43 +334,111 @@ void HealthMonitor::on_sample(int gpu, bool ok, const GpuSample& s) {
       }
     } else {
       st.failures = 0;
+      // back from an outage of failed samples (a driver refuses calls while it resets the
+      // GPU); a call that merely hung and returned is not one
+      const bool outage = st.lost && st.lost_failing;
       if (st.lost) derived.push_back(event(kEvtDeviceRecovered, "telemetry responding again"));
-      // Resets seen without event delivery (an unprivileged pod cannot arm amdsmi events):
-      // a reset reloads the power-management firmware, whose clock then starts again.
+      // Resets seen without event delivery (an unprivileged pod cannot arm amdsmi events),
+      // strongest evidence first.
       std::string reset_why;
       const double now_b = boottime_s();
+      char msg[240];
+      // 1. The kernel's own reset counter (amdgpu context query on the render node): every
+      //    reset the driver performs moves it, also those that keep the firmware running.
+      if (s.reset_count >= 0) {
+        if (st.reset_count >= 0 && s.reset_count > st.reset_count) {
+          std::snprintf(msg, sizeof(msg), "the kernel reports %lld GPU reset(s) (amdgpu context query)",
+                        static_cast<long long>(s.reset_count - st.reset_count));
+          reset_why = msg;
+        }
+        st.reset_count = s.reset_count;
+      }
+      // 2. The power-management firmware's clock starting again (a reset that reloads the
+      //    firmware).  A step back counts only if the new reading is no larger than the
+      //    time since the previous one (the firmware started after it), and only once the
+      //    new clock is seen ticking at about 1 s/s - for one interval after a clock this
+      //    process saw ticking for two, for two intervals otherwise: a frozen, garbage or
+      //    one-off reading never clears a latch.
+      bool jump_dropped = false;
       if (s.fw_clock_s >= 0) {
         const double fw_boot = now_b - s.fw_clock_s;
-        char msg[200];
-        if (!std::isnan(st.restored_fw_boot)) {
-          // a latch from a previous process: did the firmware start after it was recorded?
+        if (st.fw_clock >= 0 && s.fw_clock_s + 1.0 < st.fw_clock) {
+          const double since = now_b - st.fw_read_at;
+          if (s.fw_clock_s <= since + 5.0) {
+            std::snprintf(msg, sizeof(msg), "firmware clock restarted (%.1f s -> %.1f s)", st.fw_clock, s.fw_clock_s);
+            st.fw_jump_pending = true;
+            st.fw_jump_confirms = st.fw_adv_n >= 2 ? 1 : 2;
+            st.fw_jump_why = msg;
+          } else {
+            ++fw_glitches_;
+            jump_dropped = st.fw_jump_pending;
+            st.fw_jump_pending = false;
+          }
+          st.fw_adv_n = 0;
+          st.fw_advancing = false;
+        } else if (st.fw_clock >= 0) {
+          const double dt = now_b - st.fw_read_at, dc = s.fw_clock_s - st.fw_clock;
+          if (dt >= 0.05) {  // (two readings closer than that say nothing about the rate)
+            if (dc > 0 && dc / dt > 0.5 && dc / dt < 2.0) {
+              ++st.fw_adv_n;
+              st.fw_advancing = true;
+              if (st.fw_jump_pending && --st.fw_jump_confirms <= 0) {
+                if (reset_why.empty()) reset_why = st.fw_jump_why;
+                st.fw_jump_pending = false;
+              }
+            } else {
+              st.fw_adv_n = 0;
+              st.fw_advancing = false;
+              if (st.fw_jump_pending) {
+                ++fw_glitches_;
+                jump_dropped = true;
+                st.fw_jump_pending = false;
+              }
+            }
+          }
+        }
+        st.fw_clock = s.fw_clock_s;
+        st.fw_read_at = now_b;
+        if (st.fw_advancing) st.fw_boot = fw_boot;
+        // a latch from a previous process: did the firmware start after it was recorded?
+        // Judged once this process has seen the clock tick (a frozen clock never is).
+        if (!std::isnan(st.restored_fw_boot) && st.fw_adv_n >= 2) {
           const double tol = std::max(30.0, 1e-4 * std::max(0.0, now_b - st.restored_fw_boot));
-          if (fw_boot > st.restored_fw_boot + tol) {
+          if (fw_boot > st.restored_fw_boot + tol && reset_why.empty()) {
             std::snprintf(msg, sizeof(msg), "firmware restarted while the plugin was not running (%.0f s after the "
                           "start recorded with the latch)", fw_boot - st.restored_fw_boot);
             reset_why = msg;
           }
           st.restored_fw_boot = std::numeric_limits<double>::quiet_NaN();
         }
-        if (st.fw_clock >= 0 && s.fw_clock_s + 1.0 < st.fw_clock) {
-          std::snprintf(msg, sizeof(msg), "firmware clock restarted (%.1f s -> %.1f s)", st.fw_clock, s.fw_clock_s);
-          reset_why = msg;
-          st.fw_advancing = false;
-        } else if (st.fw_clock >= 0) {
-          const double dt = now_b - st.fw_read_at, dc = s.fw_clock_s - st.fw_clock;
-          // a clock that ticks at about one second per second (a frozen or garbage
-          // timestamp never qualifies, so it can never be mistaken for a restart later)
-          if (dt >= 0.05 && dc > 0 && dc / dt > 0.5 && dc / dt < 2.0) st.fw_advancing = true;
-        }
-        st.fw_clock = s.fw_clock_s;
-        st.fw_read_at = now_b;
-        if (st.fw_advancing) st.fw_boot = fw_boot;
       } else {
         st.restored_fw_boot = std::numeric_limits<double>::quiet_NaN();  // nothing to compare it with
-        // a GPU that reports no firmware clock: coming back from an outage of failed
-        // samples is the reset (a driver refuses calls while it resets the GPU); a call
-        // that merely hung for a while is not taken as one
-        if (st.lost && st.lost_failing) reset_why = "telemetry back after an outage (the GPU reports no firmware clock)";
+        st.fw_jump_pending = false;
+      }
+      // 3. Back from an outage with nothing above confirming a reset: a reset only if the
+      //    uncorrectable-ECC counter restarted below the latched baseline; otherwise a
+      //    candidate - the latches hold and the manager re-verifies the GPU (recovery
+      //    canary) or an operator clears it (GET /health/clear).  An outage alone is also
+      //    what an amdsmi re-init, a busy driver or a library error look like.
+      const bool undecided = outage || (jump_dropped && st.outage_unresolved);
+      if (!reset_why.empty() || !undecided) {
+        if (!reset_why.empty()) st.outage_unresolved = false;
+      } else if (st.fw_jump_pending) {
+        st.outage_unresolved = true;  // the next reading decides (a confirmed restart, or a candidate)
+      } else {
+        st.outage_unresolved = false;
+        if (s.ecc_uncorrectable >= 0 && st.last_ue > 0 && s.ecc_uncorrectable < st.last_ue) {
+          std::snprintf(msg, sizeof(msg), "telemetry back after an outage with the uncorrectable ECC count reset "
+                        "(%lld -> %lld)", static_cast<long long>(st.last_ue),
+                        static_cast<long long>(s.ecc_uncorrectable));
+          reset_why = msg;
+        } else if ((st.ecc_bad || st.resetting) && !st.candidate) {
+          st.candidate = true;
+          ++reset_candidates_;
+          derived.push_back(event(kEvtResetCandidate,
+                                  "telemetry back after an outage of failed samples, no reset confirmed (no kernel "
+                                  "reset count, no firmware clock restart)"));
+        }
       }
       if (!reset_why.empty()) {
         derived.push_back(event(kEvtResetObserved, reset_why));
@@ -476,6 +564,13 @@ void HealthMonitor::attach_tables(std::vector<std::shared_ptr<DeviceTable>> tabl
   for (size_t g = 0; g < down.size(); ++g)
     if (down[g])
       for (const auto& t : fast_tables_) t->set_gpu_health(static_cast<int>(g), -1, false);
+  // partitions the manager holds (canary verdicts) start Unhealthy in the new tables too
+  for (size_t g = 0; g < table_keys_.size(); ++g) {
+    const auto it = held_parts_.find(table_keys_[g]);
+    if (table_keys_[g].empty() || it == held_parts_.end()) continue;
+    for (int part : it->second)
+      for (const auto& t : fast_tables_) t->set_gpu_health(static_cast<int>(g), part, false);
+  }
 }
 
 void HealthMonitor::set_bad_page_thresholds(std::vector<int> thresholds) {
@@ -566,6 +661,58 @@ void HealthMonitor::restore_latches(const std::vector<HealthLatch>& latches) {
 uint64_t HealthMonitor::resets_observed() const {
   std::lock_guard<std::mutex> lk(mu_);
   return resets_observed_;
+}
+
+uint64_t HealthMonitor::reset_candidates() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return reset_candidates_;
+}
+
+uint64_t HealthMonitor::fw_clock_glitches() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  return fw_glitches_;
+}
+
+std::vector<std::string> HealthMonitor::clear_latches(const std::string& key, const std::string& reason) {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<std::string> out;
+  auto it = state_.find(key);
+  if (key.empty() || it == state_.end()) return out;
+  GpuState& st = it->second;
+  if (st.ecc_bad) out.push_back("uncorrectable_ecc");
+  if (st.resetting) out.push_back("reset_in_progress");
+  st.ecc_bad = false;
+  st.resetting = false;
+  st.restored = false;
+  st.candidate = false;
+  st.ecc_reason.clear();
+  st.restored_fw_boot = std::numeric_limits<double>::quiet_NaN();
+  st.last_ue = -1;  // the next sample takes a new baseline
+  if (!out.empty()) {
+    std::string what;
+    for (const auto& w : out) what += (what.empty() ? "" : ", ") + w;
+    reconcile_locked(key, kEvtLatchCleared, reason + " (cleared: " + what + ")", true);
+  }
+  return out;
+}
+
+std::vector<std::string> HealthMonitor::holds(const std::string& key) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  std::vector<std::string> out;
+  auto it = state_.find(key);
+  if (it == state_.end()) return out;
+  const GpuState& st = it->second;
+  if (st.resetting) out.push_back("reset_in_progress");
+  if (st.ecc_bad) out.push_back("uncorrectable_ecc");
+  if (st.lost) out.push_back("telemetry_lost");
+  if (st.pages_bad) out.push_back("retired_pages");
+  if (st.pcie_bad) out.push_back("pcie_link");
+  return out;
+}
+
+void HealthMonitor::set_held_partitions(std::map<std::string, std::vector<int>> held) {
+  std::lock_guard<std::mutex> lk(mu_);
+  held_parts_ = std::move(held);
 }
 
 double boottime_s() {

@@ -148,8 +148,30 @@ class HealthMonitor {
   // firmware is found to have started after the recorded time was reset meanwhile: its
   // first sample clears the latch.  Call before the first attach_tables.
   void restore_latches(const std::vector<HealthLatch>& latches);
-  // Resets observed by polling (firmware clock restarts, outages on clockless GPUs).
+  // Resets observed by polling (a kernel reset count that moved, a confirmed firmware
+  // clock restart, an outage after which the uncorrectable-ECC counter had been reset).
   uint64_t resets_observed() const;
+  // GPUs that came back from a telemetry outage with a latch set and nothing confirming
+  // a reset (kEvtResetCandidate): re-verified by the recovery canary, or by an operator.
+  uint64_t reset_candidates() const;
+  // Firmware clock readings that went backwards without looking like a restart (the clock
+  // had not been seen advancing, or the new reading exceeds the time since the last one),
+  // or a restart the next reading did not confirm: ignored, counted here.
+  uint64_t fw_clock_glitches() const;
+  // Drops the latches of GPU `key` that only a reset clears: uncorrectable ECC (its count
+  // is re-baselined on the next sample) and a reset in progress (PRE_RESET without
+  // POST_RESET).  For a GPU re-verified by the recovery canary after a reset candidate,
+  // and for an operator's GET /health/clear.  Levels the next samples re-judge (telemetry
+  // lost, retired pages, PCIe) are not touched.  Returns the names of what was cleared
+  // ("uncorrectable_ecc", "reset_in_progress"); emits kEvtLatchCleared when any was.
+  std::vector<std::string> clear_latches(const std::string& key, const std::string& reason);
+  // What holds GPU `key` Unhealthy now ("reset_in_progress", "uncorrectable_ecc",
+  // "telemetry_lost", "retired_pages", "pcie_link"), checks turned off included.
+  std::vector<std::string> holds(const std::string& key) const;
+  // Partitions a recovery must leave Unhealthy (identity -> partition indices; -1 = the
+  // whole GPU): failed or pending canary verdicts the manager keeps.  The fast path of a
+  // Healthy transition writes the other devices of the GPU only, in one table update.
+  void set_held_partitions(std::map<std::string, std::vector<int>> held);
 
  private:
   struct GpuState {
@@ -173,6 +195,13 @@ class HealthMonitor {
     double fw_clock = -1;
     double fw_read_at = -1;
     bool fw_advancing = false;
+    int fw_adv_n = 0;             // consecutive readings that advanced at about 1 s/s
+    bool fw_jump_pending = false;  // a restart-like step back, confirmed by readings that tick
+    int fw_jump_confirms = 0;      // ticking intervals still needed to confirm it
+    std::string fw_jump_why;
+    int64_t reset_count = -1;      // last kernel reset count seen (GpuSample::reset_count)
+    bool candidate = false;        // reset candidate reported, not resolved yet
+    bool outage_unresolved = false;  // back from an outage with a clock restart still to confirm
     double fw_boot = std::numeric_limits<double>::quiet_NaN();
     double restored_fw_boot = std::numeric_limits<double>::quiet_NaN();  // previous process; first sample checks it
     std::map<std::string, int> link_up;  // peer key -> 1/0
@@ -214,6 +243,12 @@ class HealthMonitor {
   bool stop_ = false;
   uint64_t events_seen_ = 0;
   uint64_t resets_observed_ = 0;
+  uint64_t reset_candidates_ = 0;
+  uint64_t fw_glitches_ = 0;
+  std::map<std::string, std::vector<int>> held_parts_;
+  // Healthy fast path for table index `idx` of GPU `key`: every device, except the held
+  // partitions, in one update per table.
+  void write_healthy_locked(int idx, const std::string& key);
 };
 
 // CLOCK_BOOTTIME in seconds (monotonic across the host's uptime, suspend included).

@@ -12,6 +12,7 @@
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <sys/epoll.h>
+#include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <sys/uio.h>
 #include <unistd.h>
@@ -29,7 +30,7 @@ namespace amdgpu_dp {
 namespace {
 
 const char* kMethodNames[] = {"GET", "POST", "PUT", "DELETE", "PATCH", "HEAD", "OPTIONS", "OTHER"};
-const char* kHandlerNames[] = {"/", "/metrics", "/health", "/restart", "/ready", "/not-found"};
+const char* kHandlerNames[] = {"/", "/metrics", "/health", "/restart", "/ready", "/not-found", "/health/clear"};
 const char* kStatusNames[] = {"1xx", "2xx", "3xx", "4xx", "5xx"};
 
 int method_index(const std::string& m) {
@@ -173,6 +174,11 @@ HttpServer::HttpServer(HttpConfig cfg, std::shared_ptr<Exporter> exporter)
 
 HttpServer::~HttpServer() { stop(); }
 
+void HttpServer::set_clear_hook(ClearHook hook) {
+  std::lock_guard<std::mutex> lk(hook_mu_);
+  clear_hook_ = std::move(hook);
+}
+
 void HttpServer::set_restart_hook(std::function<void()> hook) {
   std::lock_guard<std::mutex> lk(hook_mu_);
   restart_hook_ = std::move(hook);
@@ -216,6 +222,9 @@ int HttpServer::start() {
   stop_ = false;
   running_ = true;
   const int nthreads = std::max(1, cfg_.threads);
+  // stop() writes this (never read: level-triggered, it wakes every worker at once), so the
+  // workers can sleep a second at a time when no scraper is around
+  stop_efd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
   for (int t = 0; t < nthreads; ++t) {
     auto w = std::make_unique<Worker>();
     w->ep = epoll_create1(EPOLL_CLOEXEC);
@@ -223,6 +232,12 @@ int HttpServer::start() {
     ev.events = EPOLLIN | EPOLLEXCLUSIVE;
     ev.data.fd = listen_fd_;
     epoll_ctl(w->ep, EPOLL_CTL_ADD, listen_fd_, &ev);
+    if (stop_efd_ >= 0) {
+      struct epoll_event sev {};
+      sev.events = EPOLLIN;
+      sev.data.fd = stop_efd_;
+      epoll_ctl(w->ep, EPOLL_CTL_ADD, stop_efd_, &sev);
+    }
     workers_.push_back(std::move(w));
   }
   for (int t = 0; t < nthreads; ++t) {
@@ -381,7 +396,8 @@ int HttpServer::start() {
           } else {
             const size_t qm = uri.find('?');
             handle(method, qm == std::string::npos ? uri : uri.substr(0, qm), origin, keep, http10, &c->out,
-                   &status, &body_bytes, gzip_ok, c->local, c->out.empty() ? c->fd : -1);
+                   &status, &body_bytes, gzip_ok, c->local, c->out.empty() ? c->fd : -1,
+                   qm == std::string::npos ? std::string() : uri.substr(qm + 1));
           }
           const double dt = (mono_ns() - t0) * 1e-9;
           requests_.add();
@@ -397,7 +413,7 @@ int HttpServer::start() {
       const int64_t spin_ns = static_cast<int64_t>(std::max(0, std::min(cfg_.busy_poll_us, 100000))) * 1000;
       int64_t spin_until = 0;
       while (!stop_.load(std::memory_order_relaxed)) {
-        const int n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), spin_until ? 0 : 200);
+        const int n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), spin_until ? 0 : 1000);
         const int64_t now = mono_ns();
         if (spin_until) {
           if (n == 0 && now < spin_until) {
@@ -408,6 +424,7 @@ int HttpServer::start() {
         }
         for (int i = 0; i < n; ++i) {
           const int fd = evs[i].data.fd;
+          if (fd == stop_efd_) continue;  // stop(): the loop condition ends it
           if (fd == listen_fd_) {
             for (;;) {
               struct sockaddr_storage peer {};
@@ -538,8 +555,16 @@ int HttpServer::start() {
   if (cfg_.access_log) {
     log_thread_ = std::thread([this] {
       background_thread("dpaccesslog");
-      while (!stop_.load()) {
-        std::this_thread::sleep_for(std::chrono::milliseconds(100));
+      for (;;) {
+        {  // asleep until there is something to write (no periodic wake-ups on an idle node)
+          std::unique_lock<std::mutex> lk(log_mu_);
+          log_cv_.wait(lk, [&] { return stop_.load() || !log_buf_.empty(); });
+        }
+        if (stop_.load()) break;
+        // batch what the next 100 ms bring into one write
+        std::unique_lock<std::mutex> lk(log_mu_);
+        log_cv_.wait_for(lk, std::chrono::milliseconds(100), [&] { return stop_.load(); });
+        lk.unlock();
         flush_log();
       }
       flush_log();
@@ -557,10 +582,20 @@ std::vector<int> HttpServer::worker_connections() const {
 void HttpServer::stop() {
   if (!running_.exchange(false)) return;
   stop_ = true;
+  if (stop_efd_ >= 0) {
+    const uint64_t one = 1;
+    (void)!write(stop_efd_, &one, sizeof(one));
+  }
+  {
+    std::lock_guard<std::mutex> lk(log_mu_);
+  }
+  log_cv_.notify_all();
   for (auto& t : threads_)
     if (t.joinable()) t.join();
   threads_.clear();
   if (log_thread_.joinable()) log_thread_.join();
+  if (stop_efd_ >= 0) close(stop_efd_);
+  stop_efd_ = -1;
   for (auto& w : workers_) {
     for (auto& c : w->incoming) close(c->fd);  // handed over after its owner had left its loop
     w->incoming.clear();
@@ -580,7 +615,7 @@ void HttpServer::record(int mi, int hi, int status, double seconds) {
 
 void HttpServer::handle(const std::string& method, const std::string& path, const std::string& origin,
                         bool keep_alive, bool http10, std::string* out, int* status_out, size_t* body_bytes_out,
-                        bool gzip_ok, bool peer_local, int direct_fd) {
+                        bool gzip_ok, bool peer_local, int direct_fd, const std::string& query) {
   const int64_t t0 = mono_ns();
   int status = 200;
   static thread_local std::string body_buf;  // per worker thread, capacity reused
@@ -608,6 +643,7 @@ void HttpServer::handle(const std::string& method, const std::string& path, cons
     else if (path == "/health") handler = 2;
     else if (path == "/restart") handler = 3;
     else if (path == "/ready") handler = 4;
+    else if (path == "/health/clear") handler = 6;
     if (handler < 0) {
       status = 404;
       body = "{\"message\":\"Not Found\"}\n";
@@ -628,6 +664,23 @@ void HttpServer::handle(const std::string& method, const std::string& path, cons
         body = "{\"code\":-1,\"data\":null,\"msg\":\"";
         append_json_string_body(&body, not_ready_reason_);
         body += "\"}\n";
+      }
+    } else if (handler == 6 && cfg_.clear_local_only && !peer_local) {
+      status = 403;  // http.healthClearLocalOnly: dropping a health latch is an operator's act
+      body = "{\"message\":\"Forbidden\"}\n";
+    } else if (handler == 6) {
+      ClearHook hook;
+      {
+        std::lock_guard<std::mutex> lk(hook_mu_);
+        hook = clear_hook_;
+      }
+      if (hook) {
+        auto r = hook(query);
+        status = r.first;
+        body = std::move(r.second);
+      } else {
+        status = 503;
+        body = "{\"code\":-1,\"data\":null,\"msg\":\"no health monitor\"}\n";
       }
     } else if (handler == 3 && cfg_.restart_local_only && !peer_local) {
       status = 403;  // http.restartLocalOnly: a reload is not for remote callers
@@ -819,13 +872,18 @@ void HttpServer::log_access(const std::string& remote, const std::string& host, 
   std::snprintf(human, sizeof(human), "%.3fµs", seconds * 1e6);
   line.append(",\"latency_human\":\"").append(human).append("\",\"bytes_in\":").append(std::to_string(bytes_in));
   line.append(",\"bytes_out\":").append(std::to_string(bytes_out)).append("}\n");
-  std::lock_guard<std::mutex> lk(log_mu_);
-  log_buf_.append(line);
-  if (log_buf_.size() > (256u << 10)) {
-    fwrite(log_buf_.data(), 1, log_buf_.size(), stdout);
-    fflush(stdout);
-    log_buf_.clear();
+  bool was_empty;
+  {
+    std::lock_guard<std::mutex> lk(log_mu_);
+    was_empty = log_buf_.empty();
+    log_buf_.append(line);
+    if (log_buf_.size() > (256u << 10)) {
+      fwrite(log_buf_.data(), 1, log_buf_.size(), stdout);
+      fflush(stdout);
+      log_buf_.clear();
+    }
   }
+  if (was_empty) log_cv_.notify_one();  // the writer thread sleeps until there is a first line
 }
 
 void HttpServer::flush_log() {

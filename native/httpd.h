@@ -1,4 +1,4 @@
-// Native HTTP/1.1 ops server: GET / /metrics /health /restart.
+// Native HTTP/1.1 ops server: GET / /metrics /health /restart /ready /health/clear.
 //
 // Reference: echo v4 server (server/server.go:35-69) with middleware chain
 // Recover -> Cros -> Logger -> MetricsMiddleware (server/server.go:39-43,
@@ -12,6 +12,7 @@
 #pragma once
 
 #include <atomic>
+#include <condition_variable>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -35,6 +36,8 @@ struct HttpConfig {
   // GET /restart only from a loopback peer (others get 403); off = the reference's
   // behaviour, where anyone who reaches the port can reload the plugins
   bool restart_local_only = false;
+  // GET /health/clear only from a loopback peer (others get 403)
+  bool clear_local_only = true;
   std::string version = "0.1.0";
 };
 
@@ -42,7 +45,7 @@ class HttpServer {
  public:
   // echo_http_* label dimensions: methods, handlers (routes), status classes
   static constexpr int kMethods = 8;
-  static constexpr int kHandlers = 6;
+  static constexpr int kHandlers = 7;
   static constexpr int kStatus = 5;
   HttpServer(HttpConfig cfg, std::shared_ptr<Exporter> exporter);
   ~HttpServer();
@@ -52,6 +55,10 @@ class HttpServer {
   bool running() const { return running_.load(); }
   int port() const { return bound_port_; }
   void set_restart_hook(std::function<void()> hook);
+  // GET /health/clear?<query>: an operator drops a GPU's health latches.  The hook gets
+  // the raw query string and returns (HTTP status, JSON body).
+  using ClearHook = std::function<std::pair<int, std::string>(const std::string& query)>;
+  void set_clear_hook(ClearHook hook);
   // GET /ready answers 200 while ready, else 503 with the reason (the plugin manager
   // pushes its registration state here)
   void set_ready(bool ready, const std::string& reason);
@@ -71,7 +78,7 @@ class HttpServer {
   // into *out); what the socket does not take is appended to *out as usual.
   void handle(const std::string& method, const std::string& path, const std::string& origin, bool keep_alive,
               bool http10, std::string* out, int* status_out, size_t* body_bytes_out, bool gzip_ok = false,
-              bool peer_local = true, int direct_fd = -1);
+              bool peer_local = true, int direct_fd = -1, const std::string& query = std::string());
   void record(int method_idx, int handler_idx, int status, double seconds);
   void log_access(const std::string& remote, const std::string& host, const std::string& method,
                   const std::string& uri, const std::string& ua, int status, double seconds, size_t bytes_in,
@@ -81,6 +88,7 @@ class HttpServer {
   HttpConfig cfg_;
   std::shared_ptr<Exporter> exporter_;
   std::function<void()> restart_hook_;
+  ClearHook clear_hook_;
   std::mutex hook_mu_;
   bool ready_ = true;  // GET /ready (guarded by hook_mu_)
   std::string not_ready_reason_;
@@ -106,7 +114,9 @@ class HttpServer {
   std::unique_ptr<Histogram> hist_[kMethods][kHandlers];
 
   std::mutex log_mu_;
+  std::condition_variable log_cv_;  // log_buf_ became non-empty, or stop
   std::string log_buf_;
+  int stop_efd_ = -1;
 };
 
 }  // namespace amdgpu_dp

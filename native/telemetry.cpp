@@ -159,11 +159,12 @@ void Exporter::start(std::shared_ptr<Backend> backend, int interval_ms, std::sha
     first_done_ = false;
   }
   sampler_exit_ = std::make_shared<ThreadExit>();
+  waker_ = std::make_shared<Waker>();
   {
     std::lock_guard<std::mutex> lk(run_mu_);
-    watchdog_ = std::thread([this, m = monitor_] { watchdog_loop(m); });  // before the first call
+    watchdog_ = std::thread([this, m = monitor_, wk = waker_] { watchdog_loop(m, wk); });  // before the first call
   }
-  thread_ = std::thread(sampler_main, std::move(weak), sampler_exit_, gen, interval);
+  thread_ = std::thread(sampler_main, std::move(weak), sampler_exit_, waker_, gen, interval);
   // /metrics is normally populated before start() returns.  The first pass waits on the
   // lanes at most its budget (a wedged driver at start-up stalls one lane, not the pass),
   // and start() waits for the first pass at most the stall threshold: the caller - the
@@ -172,6 +173,19 @@ void Exporter::start(std::shared_ptr<Backend> backend, int interval_ms, std::sha
   const int ms = stall_ms_.load();
   std::unique_lock<std::mutex> lk(first_mu_);
   cv_wait_ms(first_cv_, lk, ms > 0 ? ms : 10000, [&] { return first_done_; });
+}
+
+void Exporter::Waker::sleep_ms(int64_t ms) {
+  std::unique_lock<std::mutex> lk(mu);
+  cv_wait_ms(cv, lk, static_cast<int>(std::min<int64_t>(ms, 3600000)), [&] { return stopping; });
+}
+
+void Exporter::Waker::wake() {
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    stopping = true;
+  }
+  cv.notify_all();
 }
 
 bool Exporter::ThreadExit::wait(int ms) {
@@ -194,6 +208,7 @@ void Exporter::ThreadExit::mark() {
 void Exporter::stop() {
   if (!running_.exchange(false)) return;
   stop_ = true;
+  if (waker_) waker_->wake();
   const auto self_id = std::this_thread::get_id();
   if (watchdog_.joinable()) {
     if (watchdog_.get_id() == self_id) watchdog_.detach();
@@ -246,12 +261,19 @@ double Exporter::sample_age_s(int gpu) const {
 // the first wedge, so this GPU is stuck on its own; otherwise it is only waiting behind
 // the first (a library that serialises every device) and is reported "blocked".  Each
 // stuck call is reported once; the GPU recovers through on_sample once a sample returns.
-void Exporter::watchdog_loop(std::shared_ptr<HealthMonitor> monitor) {
+void Exporter::watchdog_loop(std::shared_ptr<HealthMonitor> monitor, std::shared_ptr<Waker> waker) {
   background_thread("dpwatchdog");
   std::map<std::string, int64_t> reported;  // key -> since of the call reported lost
+  int64_t sleep_ms = 25;
   while (!stop_.load()) {
-    std::this_thread::sleep_for(std::chrono::milliseconds(25));
+    waker->sleep_ms(sleep_ms);
+    if (stop_.load()) break;
     const int ms = stall_ms_.load();
+    // Checks an eighth of the stall threshold apart (25 ms .. 1 s; 1 s with no threshold),
+    // sooner when a call in flight is about to cross it: a 10 s threshold costs one
+    // wake-up a second on an idle node instead of forty.
+    const int64_t period = ms > 0 ? std::max<int64_t>(25, std::min<int64_t>(1000, ms / 8)) : 1000;
+    sleep_ms = period;
     std::shared_ptr<Backend> be;
     {
       std::lock_guard<std::mutex> lk(run_mu_);
@@ -280,8 +302,12 @@ void Exporter::watchdog_loop(std::shared_ptr<HealthMonitor> monitor) {
       return false;
     };
     std::vector<LaneReport> stuck;
-    for (auto& r : be->lanes())
-      if (r.index >= 0 && r.lane.inflight_since_ns && now - r.lane.inflight_since_ns > threshold) stuck.push_back(r);
+    for (auto& r : be->lanes()) {
+      if (r.index < 0 || !r.lane.inflight_since_ns) continue;
+      const int64_t left = r.lane.inflight_since_ns + threshold - now;
+      if (left < 0) stuck.push_back(r);
+      else sleep_ms = std::max<int64_t>(25, std::min(sleep_ms, left / 1000000 + 1));  // wake as it crosses
+    }
     int64_t root = 0;
     uint64_t root_batch = 0;
     for (const auto& r : stuck)
@@ -331,8 +357,8 @@ void Exporter::watchdog_loop(std::shared_ptr<HealthMonitor> monitor) {
   }
 }
 
-void Exporter::sampler_main(std::weak_ptr<Exporter> weak, std::shared_ptr<ThreadExit> exit, uint64_t gen,
-                            int interval_ms) {
+void Exporter::sampler_main(std::weak_ptr<Exporter> weak, std::shared_ptr<ThreadExit> exit,
+                            std::shared_ptr<Waker> waker, uint64_t gen, int interval_ms) {
   background_thread("dpsampler");
   // A strong reference only for the duration of each step: the exporter stays alive
   // through a backend call (however long it blocks), and may be destroyed between
@@ -347,7 +373,7 @@ void Exporter::sampler_main(std::weak_ptr<Exporter> weak, std::shared_ptr<Thread
       sleep_ms = self->sampler_step(&next, gen, interval_ms);
     }
     if (sleep_ms < 0) break;
-    if (sleep_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(sleep_ms));
+    if (sleep_ms > 0) waker->sleep_ms(sleep_ms);  // until the next pass, or stop()
   }
   exit->mark();
 }
@@ -355,8 +381,8 @@ void Exporter::sampler_main(std::weak_ptr<Exporter> weak, std::shared_ptr<Thread
 int Exporter::sampler_step(int64_t* next, uint64_t gen, int interval_ms) {
   if (stop_.load() || sampler_gen_.load() != gen) return -1;
   const int64_t now = mono_ns();
-  if (*next != 0 && now < *next)  // sleep in slices so stop() is prompt
-    return static_cast<int>(std::min<int64_t>(50, (*next - now) / 1000000 + 1));
+  if (*next != 0 && now < *next)  // (stop() cuts the sleep short)
+    return static_cast<int>((*next - now) / 1000000 + 1);
   const bool first = *next == 0;
   sample_once(gen);
   if (first) {

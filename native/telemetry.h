@@ -113,8 +113,15 @@ class Exporter : public std::enable_shared_from_this<Exporter> {
     bool wait(int ms);  // ms < 0: no limit; true once the thread has exited
     void mark();
   };
-  static void sampler_main(std::weak_ptr<Exporter> weak, std::shared_ptr<ThreadExit> exit, uint64_t gen,
-                           int interval_ms);
+  struct Waker {  // the sampler's and the watchdog's sleeps, cut short by stop()
+    std::mutex mu;
+    std::condition_variable cv;
+    bool stopping = false;
+    void sleep_ms(int64_t ms);
+    void wake();
+  };
+  static void sampler_main(std::weak_ptr<Exporter> weak, std::shared_ptr<ThreadExit> exit,
+                           std::shared_ptr<Waker> waker, uint64_t gen, int interval_ms);
   int sampler_step(int64_t* next, uint64_t gen, int interval_ms);  // ms to sleep before the next step, -1 = stop
   void render_gpu_text(const std::vector<GpuSample>& samples, const std::vector<char>& ok, uint64_t inventory_gen);
   // One GPU's sampling state across passes (guarded by sample_mu_).
@@ -211,6 +218,7 @@ class Exporter : public std::enable_shared_from_this<Exporter> {
   std::atomic<bool> running_{false};
   std::atomic<bool> stop_{false};
   std::shared_ptr<ThreadExit> sampler_exit_;
+  std::shared_ptr<Waker> waker_;
   std::mutex first_mu_;  // first pass of a start(): start() waits for it (bounded)
   std::condition_variable first_cv_;
   bool first_done_ = false;
@@ -219,7 +227,7 @@ class Exporter : public std::enable_shared_from_this<Exporter> {
   std::atomic<uint64_t> samples_{0};
   std::atomic<uint64_t> sample_errors_{0};
   Histogram sample_hist_;
-  void watchdog_loop(std::shared_ptr<HealthMonitor> monitor);
+  void watchdog_loop(std::shared_ptr<HealthMonitor> monitor, std::shared_ptr<Waker> waker);
   std::thread watchdog_;
   std::atomic<int> stall_ms_{0};
   std::atomic<int64_t> last_pass_ns_{0};    // end of the last complete pass (mono ns)

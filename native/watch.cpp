@@ -3,6 +3,7 @@
 #include <dirent.h>
 #include <errno.h>
 #include <poll.h>
+#include <sys/eventfd.h>
 #include <sys/inotify.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -22,6 +23,7 @@ constexpr uint32_t kWatchMask = IN_CREATE | IN_DELETE | IN_MOVED_TO | IN_MOVED_F
 DirWatcher::DirWatcher(const std::string& dir) : dir_(dir) {
   fd_ = inotify_init1(IN_NONBLOCK | IN_CLOEXEC);
   if (fd_ < 0) throw std::runtime_error(std::string("inotify_init1: ") + strerror(errno));
+  efd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
   wd_ = inotify_add_watch(fd_, dir.c_str(), kWatchMask);
   struct stat st;
   if (wd_ >= 0 && ::stat(dir.c_str(), &st) == 0) {
@@ -32,6 +34,8 @@ DirWatcher::DirWatcher(const std::string& dir) : dir_(dir) {
     const int e = errno;
     ::close(fd_);
     fd_ = -1;
+    if (efd_ >= 0) ::close(efd_);
+    efd_ = -1;
     throw std::runtime_error("inotify_add_watch(" + dir + "): " + strerror(e));
   }
 }
@@ -41,6 +45,16 @@ DirWatcher::~DirWatcher() { close(); }
 void DirWatcher::close() {
   if (fd_ >= 0) ::close(fd_);
   fd_ = -1;
+  std::lock_guard<std::mutex> lk(efd_mu_);
+  if (efd_ >= 0) ::close(efd_);
+  efd_ = -1;
+}
+
+void DirWatcher::wake() {
+  std::lock_guard<std::mutex> lk(efd_mu_);
+  if (efd_ < 0) return;
+  const uint64_t one = 1;
+  (void)!::write(efd_, &one, sizeof(one));
 }
 
 // The watched directory itself can go away (a node agent that wipes
@@ -83,8 +97,15 @@ std::vector<FsEvent> DirWatcher::read(int timeout_ms) {
   std::vector<FsEvent> out;
   if (fd_ < 0) return out;
   if (wd_ < 0 && rewatch(&out)) return out;
-  struct pollfd p {fd_, POLLIN, 0};
-  if (poll(&p, 1, timeout_ms) <= 0) {  // (watch gone: this is the retry pause)
+  struct pollfd p[2] = {{fd_, POLLIN, 0}, {efd_, POLLIN, 0}};
+  const int np = poll(p, efd_ >= 0 ? 2 : 1, timeout_ms);
+  if (np > 0 && efd_ >= 0 && (p[1].revents & POLLIN)) {  // wake()
+    uint64_t x;
+    while (::read(efd_, &x, sizeof(x)) > 0) {
+    }
+    return out;
+  }
+  if (np <= 0) {  // (watch gone: this is the retry pause)
     if (wd_ >= 0 && !same_dir()) {
       inotify_rm_watch(fd_, wd_);  // its IN_IGNORED is skipped below
       wd_ = -1;

@@ -1,10 +1,11 @@
 // inotify directory watcher (reference: modules/watch/watch.go:11-26 via fsnotify;
 // consumed at plugin/manager.go:80-84 to detect kubelet restarts by the CREATE of
-// kubelet.sock).  Blocking reads with a timeout so the caller's thread can stop.  The
+// kubelet.sock).  Blocking reads with a timeout, cut short by wake().  The
 // watch survives the directory being removed and created again (see watch.cpp).
 #pragma once
 
 #include <cstdint>
+#include <mutex>
 #include <string>
 #include <utility>
 #include <vector>
@@ -23,6 +24,10 @@ class DirWatcher {
   explicit DirWatcher(const std::string& dir);  // throws on failure
   ~DirWatcher();
   std::vector<FsEvent> read(int timeout_ms);
+  // Ends a read() in progress (or the next one) at once, with no events: lets the reading
+  // thread sleep long between events and still stop promptly.  Safe from any thread, also
+  // after close().
+  void wake();
   void close();
   const std::string& dir() const { return dir_; }
 
@@ -33,6 +38,8 @@ class DirWatcher {
   std::string dir_;
   int fd_ = -1;
   int wd_ = -1;
+  int efd_ = -1;     // wake(): an eventfd read() polls next to the inotify descriptor
+  std::mutex efd_mu_;  // wake() against close()
   uint64_t dev_ = 0, ino_ = 0;  // identity of the watched directory
 };
 

@@ -182,7 +182,7 @@ def main():
         if stats["daemon_alive"]:
             import re
             body = http_get(port, "/metrics")[1].decode()
-            for ev in ("reloads", "table_swaps", "restarts_coalesced"):
+            for ev in ("reloads", "table_swaps", "restarts_coalesced", "reregistrations_restart"):
                 m = re.search(r'amdgpu_device_plugin_events_total\{event="%s"\} (\d+)' % ev, body)
                 stats[ev] = int(m.group(1)) if m else 0
         rs = stats["rss_kb"]
@@ -205,9 +205,11 @@ def main():
                            and (stats["thread_growth_second_half"] or 0) <= 8
                            and stats["scrapes"] > 0 and stats["restarts"] > 0 and stats["alloc_errors"] == 0
                            and stats["scrape_errors"] <= stats["restarts"] * 4
-                           # hitless reloads: one connection, one stream, one registration
+                           # hitless reloads: one connection, one stream; every /restart's
+                           # reload registers again on the same socket (reference contract)
                            and stats["reconnects"] == 0 and stats["law_reopens"] == 1
-                           and stats["registrations"] == 1 and stats["law_updates"] > 1)
+                           and stats["registrations"] == 1 + stats.get("reregistrations_restart", 0)
+                           and stats.get("reregistrations_restart", 0) >= 1 and stats["law_updates"] > 1)
         stats["law_last"] = last_law.get("devices")
         if a.fault_every > 0:
             # both GPUs still advertised; the stream kept moving (faults + reloads)

@@ -5,11 +5,13 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <fcntl.h>
+#include <sched.h>
 #include <netinet/tcp.h>
 #include <sys/epoll.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstring>
 #include <mutex>
@@ -237,10 +239,38 @@ bool tcp_pair(int sv[2]) {
 
 }  // namespace
 
+namespace {
+
+// Pins the calling thread to `cpu` (no-op for cpu < 0); the mask it had goes to *saved.
+bool pin_self(int cpu, cpu_set_t* saved) {
+  if (cpu < 0) return true;
+  if (saved && sched_getaffinity(0, sizeof(*saved), saved) != 0) return false;
+  cpu_set_t one;
+  CPU_ZERO(&one);
+  CPU_SET(cpu, &one);
+  return sched_setaffinity(0, sizeof(one), &one) == 0;
+}
+
+}  // namespace
+
+double core_ghz(int64_t iters, int reps) {
+  if (iters < 1000 || reps < 1) throw std::invalid_argument("core_ghz: bad arguments");
+  double best = 0;
+  for (int r = 0; r < reps; ++r) {
+    uint64_t x = static_cast<uint64_t>(r) + 1;
+    const int64_t t0 = mono_ns();
+    for (int64_t i = 0; i < iters; ++i) asm volatile("add $1, %0" : "+r"(x));  // 1 cycle, dependent
+    const int64_t dt = mono_ns() - t0;
+    if (dt > 0) best = std::max(best, static_cast<double>(iters) / static_cast<double>(dt));
+  }
+  return best;
+}
+
 std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_bytes, bool server_spin, bool tcp,
-                                 int gap_us) {
+                                 int gap_us, int client_cpu, int server_cpu) {
   if (n < 0 || warmup < 0 || gap_us < 0 || req_bytes <= 0 || resp_bytes <= 0 || req_bytes > (1 << 20) || resp_bytes > (4 << 20))
     throw std::invalid_argument("uds_pingpong: bad sizes");
+  if (client_cpu >= CPU_SETSIZE || server_cpu >= CPU_SETSIZE) throw std::invalid_argument("uds_pingpong: bad cpu");
   int sv[2];
   if (tcp ? !tcp_pair(sv) : socketpair(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0, sv) != 0)
     throw std::runtime_error(std::string(tcp ? "tcp loopback pair: " : "socketpair: ") + strerror(errno));
@@ -253,7 +283,9 @@ std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_byte
   ev.events = EPOLLIN | EPOLLRDHUP;
   ev.data.fd = sfd;
   epoll_ctl(ep, EPOLL_CTL_ADD, sfd, &ev);
+  std::atomic<int> server_pinned{-1};
   std::thread server([&] {  // the plugin server's syscall pattern: epoll_wait, recv, send
+    server_pinned.store(pin_self(server_cpu, nullptr) ? 1 : 0);
     std::vector<char> in(static_cast<size_t>(req_bytes) + 65536), out(static_cast<size_t>(resp_bytes), 'r');
     size_t have = 0;
     epoll_event evs[4];
@@ -292,11 +324,15 @@ std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_byte
       if (closed) return;
     }
   });
+  cpu_set_t saved;
+  CPU_ZERO(&saved);
+  const bool client_pinned = pin_self(client_cpu, &saved);
+  while (server_pinned.load() < 0) std::this_thread::yield();
   std::vector<double> lat;
   lat.reserve(static_cast<size_t>(n));
   const std::string req(static_cast<size_t>(req_bytes), 'q');
   std::vector<char> buf(static_cast<size_t>(resp_bytes));
-  bool failed = false;
+  bool failed = !client_pinned || server_pinned.load() == 0;
   for (int i = 0; i < n + warmup && !failed; ++i) {
     // gap_us > 0: both threads idle between exchanges, as the cold Allocate's do
     if (gap_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(gap_us));
@@ -321,10 +357,12 @@ std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_byte
   }
   shutdown(cfd, SHUT_RDWR);  // the server sees EOF and leaves its loop
   server.join();
+  if (client_cpu >= 0 && client_pinned) sched_setaffinity(0, sizeof(saved), &saved);
   close(cfd);
   close(sfd);
   close(ep);
-  if (failed) throw std::runtime_error("uds_pingpong: socket error");
+  if (failed) throw std::runtime_error(!client_pinned || server_pinned.load() == 0 ? "uds_pingpong: cannot pin to the CPU"
+                                                                                    : "uds_pingpong: socket error");
   return lat;
 }
 

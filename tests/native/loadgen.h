@@ -38,8 +38,16 @@ LoadResult grpc_load(const std::string& socket_path, const std::string& method, 
 // `warmup` untimed ones.  Allocate p50 minus this p50 is what HTTP/2 + HPACK + protobuf +
 // the device table cost.  tcp=true: the same over a loopback TCP connection, the floor
 // of one /metrics scrape of resp_bytes (what the kernel's copies and wake-ups cost).
+// client_cpu / server_cpu >= 0 pin the two threads (the calling thread's own affinity is
+// restored afterwards): the same exchange between two chosen CPUs - SMT siblings, two
+// cores of one L3, two L3 domains - is what says what a placement costs on this host.
 std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_bytes, bool server_spin = false,
-                                 bool tcp = false, int gap_us = 0);
+                                 bool tcp = false, int gap_us = 0, int client_cpu = -1, int server_cpu = -1);
+
+// Effective core clock of the calling thread, GHz: a chain of `iters` dependent integer
+// adds (one per cycle on x86-64) timed with CLOCK_MONOTONIC; the best of `reps`.  Tells a
+// box whose cores run at 2 GHz from one whose cores boost to 4+.
+double core_ghz(int64_t iters = 20000000, int reps = 5);
 
 // The same bare exchange, one at a time on demand: a persistent socket pair whose server
 // thread sleeps in epoll_wait(timeout_ms) between exchanges the way the plugin's worker

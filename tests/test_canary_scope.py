@@ -150,3 +150,34 @@ def test_gpu_that_comes_back_is_canaried_again(make_cfg, plugin_dir, monkeypatch
         finally:
             m.stop()
             t.join(10)
+
+
+def test_recovery_while_a_start_up_verdict_is_pending_keeps_it_unhealthy(make_cfg, plugin_dir, monkeypatch):
+    """with health.canary off the monitor writes Healthy transitions into the
+    tables itself.  A reset that ends while a partition's start-up verdict is pending must
+    not advertise it Healthy, and a failed verdict is applied to the tables, not assumed."""
+    from k8s_gpu_device_plugin_amd import native
+    n = native.load()
+    calls, release = _fake_canary(monkeypatch, delay=5.0, fail=(0,))
+    be = fixtures.build_backend("2gpu_spx")
+    with KubeletStub(plugin_dir) as k:
+        m = PluginManager(make_cfg(health={"canaryOnStart": True}), backend=be)
+        t = m.start_background()
+        try:
+            k.wait_for_registrations(1)
+            assert _wait(lambda: len(calls) == 2)
+            ids = m.plugins[0].table.ids()
+            be.inject_event(n.HwEvent(n.EVT_PRE_RESET, 0, message="test reset"))
+            assert _wait(lambda: m.counters["health_events"] >= 1)
+            be.inject_event(n.HwEvent(n.EVT_POST_RESET, 0, message="test reset"))
+            assert _wait(lambda: m.counters["health_events"] >= 2)
+            time.sleep(0.3)
+            assert not m.plugins[0].table.healthy(ids[0])  # its verdict is still pending
+            release.set()  # GPU 0 fails, GPU 1 passes
+            assert _wait(lambda: not m._start_pending)
+            time.sleep(0.2)
+            assert not m.plugins[0].table.healthy(ids[0]) and m.plugins[0].table.healthy(ids[1])
+            assert m.counters.get("canary_failures") == 1
+        finally:
+            m.stop()
+            t.join(10)

@@ -64,7 +64,7 @@ def test_daemon_serves_and_exits_gracefully(plugin_dir, tmp_path, sig):
             c.request("GET", "/restart")
             r = c.getresponse()
             assert r.status == 200 and r.read()
-            deadline = time.monotonic() + 30  # the reload swaps the table in (no new registration)
+            deadline = time.monotonic() + 30  # the reload swaps the table in, then registers again
             while time.monotonic() < deadline:
                 c.request("GET", "/metrics")
                 if 'amdgpu_device_plugin_events_total{event="table_swaps"} 1' in c.getresponse().read().decode():
@@ -72,7 +72,8 @@ def test_daemon_serves_and_exits_gracefully(plugin_dir, tmp_path, sig):
                 time.sleep(0.1)
             else:
                 raise AssertionError("/restart did not reload")
-            assert len(k.requests) == 1
+            k.wait_for_registrations(2, timeout=10)  # the same socket, registered again
+            assert len({r.endpoint for r in k.requests}) == 1
             time.sleep(0.2)
             p.send_signal(sig)
             rc = p.wait(30)

@@ -66,7 +66,7 @@ def test_env_overrides(tmp_path):
                                  {"grpc": {"idleWakeMs": 100001}}, {"grpc": {"threads": 0}},
                                  {"http": {"threads": 1000}},
                                  {"grpc": {"callTraceFile": "/tmp/t.bin", "callTraceEntries": 0}},
-                                 {"backgroundSched": "idle"}])
+                                 {"backgroundSched": "idle"}, {"grpc": {"activeWindowMs": -1}}])
 def test_validation_errors(raw):
     with pytest.raises(C.ConfigError):
         C.validate(C.from_dict(raw))
@@ -221,7 +221,25 @@ def test_kfd_cdi_patch_arms_events_without_privileges(tmp_path):
     kind, dev = PLUGIN_KFD_DEVICE.split("=")
     assert spec["kind"] == kind and spec["cdiVersion"] == "0.6.0"
     [d] = [d for d in spec["devices"] if d["name"] == dev]
-    assert d["containerEdits"]["deviceNodes"] == [{"path": "/dev/kfd", "permissions": "rw"}]
+    assert d["containerEdits"]["deviceNodes"][0] == {"path": "/dev/kfd", "permissions": "rw"}
+    assert all(x["path"].startswith("/dev/dri/renderD") for x in d["containerEdits"]["deviceNodes"][1:])
+
+
+def test_plugin_cdi_spec_carries_the_amd_render_nodes(tmp_path):
+    """health.resetQuery needs each GPU's render node in the plugin container's device
+    cgroup: the plugin's CDI device lists the AMD render nodes next to /dev/kfd."""
+    from k8s_gpu_device_plugin_amd.cdi.spec import amdgpu_render_nodes, plugin_kfd_spec
+    dri, cls = tmp_path / "dri", tmp_path / "class"
+    dri.mkdir()
+    for name, vendor in (("renderD128", "0x1002"), ("renderD129", "0x10de"), ("renderD130", "0x1002"),
+                         ("card0", "0x1002")):
+        (dri / name).write_text("")
+        (cls / name / "device").mkdir(parents=True)
+        (cls / name / "device" / "vendor").write_text(vendor + "\n")
+    nodes = amdgpu_render_nodes(str(dri), str(cls))
+    assert nodes == [str(dri / "renderD128"), str(dri / "renderD130")]
+    spec = plugin_kfd_spec("/dev/kfd", nodes)
+    assert [x["path"] for x in spec["devices"][0]["containerEdits"]["deviceNodes"]] == ["/dev/kfd"] + nodes
 
 
 def test_container_image_builds_the_native_libraries():

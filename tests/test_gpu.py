@@ -364,7 +364,8 @@ def test_firmware_clock_reset_signal_on_real_gpu(n, amdsmi_backend, tmp_path):
     clock, read from gpu_metrics, ticks at one second per second (profiles/r5/
     reset_signal_probe.json: 100.004 MHz); a latch restored with the firmware start it
     recorded holds, and one restored with an earlier start (the firmware restarted since,
-    i.e. the GPU was reset) is cleared by the first sample."""
+    i.e. the GPU was reset) is cleared once this process has seen the clock tick (three
+    samples: ADVICE r5, a frozen clock never clears a latch)."""
     gpus, _ = amdsmi_backend.discover()
     a = amdsmi_backend.sample(0)
     time.sleep(0.5)
@@ -380,9 +381,38 @@ def test_firmware_clock_reset_signal_on_real_gpu(n, amdsmi_backend, tmp_path):
         mon.restore_latches([n.HealthLatch(key, max(0, b.ecc_uncorrectable), recorded, "test latch", 0)])
         assert not mon.gpu_healthy(0)
         mon.on_sample(0, True, amdsmi_backend.sample(0))
+        assert not mon.gpu_healthy(0)  # one reading says nothing about the clock ticking
+        for _ in range(3):
+            time.sleep(0.2)
+            mon.on_sample(0, True, amdsmi_backend.sample(0))
         assert mon.gpu_healthy(0) != stays, (recorded, fw_boot)
         assert mon.resets_observed == (0 if stays else 1)
     print("firmware clock %.1f s, rate %.6f s/s, firmware started at boot+%.1f s" % (b.fw_clock_s, rate, fw_boot))
+
+
+def test_kernel_reset_count_through_the_render_node(n, amdsmi_backend):
+    """health.resetQuery on the real GPU: the sample reads the amdgpu driver's reset count
+    through a context on the GPU's render node (unprivileged: the box's user can open it).
+    No reset happens here, so it reads 0 and stays 0; turned off, no count is read."""
+    amdsmi_backend.discover()
+    samples = []
+    for _ in range(3):
+        samples.append(amdsmi_backend.sample(0))
+        time.sleep(0.1)
+    counts = [s.reset_count for s in samples]
+    assert counts == [0, 0, 0], counts
+    amdsmi_backend.set_reset_query(False)
+    try:
+        assert amdsmi_backend.sample(0).reset_count == -1
+    finally:
+        amdsmi_backend.set_reset_query(True)
+    key = amdsmi_backend.gpu_key(0)
+    mon = n.HealthMonitor(amdsmi_backend, 3)
+    mon.set_gpus([key])
+    for _ in range(3):
+        mon.on_sample(0, True, amdsmi_backend.sample(0))
+    assert mon.gpu_healthy(0) and mon.resets_observed == 0
+    print("kernel reset count through the render node: %s" % counts)
 
 
 def test_amdsmi_inventory_signature_is_stable(amdsmi_backend):

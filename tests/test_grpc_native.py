@@ -750,3 +750,95 @@ def test_hostile_clients_do_not_disturb_allocate(n, server):
     c = n.H2Client(path)
     assert c.unary(v1beta1.METHOD_ALLOCATE, req)[0] == 0
     c.close()
+
+
+def test_idle_wake_and_keep_warm_run_only_in_the_admission_window(n, plugin_dir):
+    """grpc.activeWindowMs.  Right after a kubelet RPC the worker that
+    holds the connection wakes every idle millisecond and runs keep-warm ticks; once the
+    window has passed without an RPC every worker sleeps (about one wake-up a second, no
+    tick), and the next RPC opens the window again."""
+    tc = n.TableConfig()
+    devs = [n.TableDevice("dev-%d" % i, i, 0, 0, -1, ["/dev/dri/renderD%d" % (128 + i)], True) for i in range(2)]
+    table = n.DeviceTable(tc, devs, n.Topology(2))
+    path = os.path.join(plugin_dir, "amd-gpu.sock")
+    before = set(os.listdir("/proc/self/task"))
+    srv = n.GrpcServer(path, 2, busy_poll_us=0, admission_poll_us=0)
+    srv.set_keep_warm_ms(10)
+    srv.set_idle_wake_ms(1)
+    srv.set_active_window_ms(400)
+    srv.set_table(table)
+    srv.start()
+    try:
+        deadline = time.monotonic() + 5
+        while len(_grpc_workers(before)) < 2 and time.monotonic() < deadline:
+            time.sleep(0.01)
+        workers = _grpc_workers(before)
+        c = n.H2Client(path)
+        req = v1beta1.AllocateRequest(container_requests=[v1beta1.ContainerAllocateRequest(
+            devices_ids=["dev-1"])]).SerializeToString()
+        assert c.unary(v1beta1.METHOD_ALLOCATE, req)[0] == 0
+        s0, t0 = _switches(workers), srv.warm_ticks
+        time.sleep(0.25)  # inside the window
+        s1, t1 = _switches(workers), srv.warm_ticks
+        assert max(s1[t] - s0[t] for t in workers) >= 60 and t1 > t0, (s0, s1)
+        time.sleep(0.4)  # the window closes
+        s0, t0, i0 = _switches(workers), srv.warm_ticks, srv.idle_wakeups
+        time.sleep(1.0)
+        s1, t1, i1 = _switches(workers), srv.warm_ticks, srv.idle_wakeups
+        assert max(s1[t] - s0[t] for t in workers) <= 4, (s0, s1)  # ~1 per worker per second
+        assert t1 == t0 and i1 - i0 <= 6
+        assert c.unary(v1beta1.METHOD_ALLOCATE, req)[0] == 0  # a sleeping worker answers
+        s0 = _switches(workers)
+        time.sleep(0.2)
+        s1 = _switches(workers)
+        assert max(s1[t] - s0[t] for t in workers) >= 50  # the window is open again
+        c.close()
+    finally:
+        srv.stop()
+
+
+def test_idle_daemon_threads_sleep(n, plugin_dir, make_cfg):
+    """An idle daemon's own threads (HTTP workers, sampler, watchdog, event thread,
+    directory watch, health pump) wake about once a second at most, and still stop at once."""
+    from k8s_gpu_device_plugin_amd.models import fixtures
+    from k8s_gpu_device_plugin_amd.plugin.manager import PluginManager
+    from k8s_gpu_device_plugin_amd.server.web import WebServer
+    model = fixtures.mi355x_node(2)
+    model["hardware_events"] = False
+    before = set(os.listdir("/proc/self/task"))
+    cfg = make_cfg(webListenAddress="127.0.0.1:0", http={"accessLog": True}, telemetry={"intervalMs": 1000})
+    m = PluginManager(cfg, backend=fixtures.build_backend(model))
+    t = m.start_background()
+    w = WebServer(cfg, m)
+    w.start()
+    try:
+        time.sleep(1.5)
+        mine = [x for x in os.listdir("/proc/self/task") if x not in before]
+
+        def switches():
+            out = {}
+            for tid in mine:
+                try:
+                    with open("/proc/self/task/%s/comm" % tid) as f:
+                        name = f.read().strip()
+                    with open("/proc/self/task/%s/status" % tid) as f:
+                        st = f.read()
+                except OSError:
+                    continue
+                out[tid] = (name, sum(int(ln.split()[1]) for ln in st.splitlines()
+                                      if ln.startswith(("voluntary_ctxt", "nonvoluntary_ctxt"))))
+            return out
+        a = switches()
+        time.sleep(2.0)
+        b = switches()
+        rates = {a[k][0] + "/" + k: (b[k][1] - a[k][1]) / 2.0 for k in a if k in b}
+        native_threads = {k: v for k, v in rates.items() if k.startswith(("dphttp", "dpsampler", "dpwatchdog",
+                                                                          "dpaccesslog", "dpgrpc"))}
+        # (round 5: the watchdog woke 40 times a second, the sampler 20, the HTTP workers 5)
+        assert native_threads and max(native_threads.values()) <= 8.0, rates
+        t0 = time.monotonic()
+    finally:
+        w.stop()
+        m.stop()
+        t.join(10)
+    assert time.monotonic() - t0 < 3.0

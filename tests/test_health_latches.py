@@ -5,8 +5,13 @@ and no GPU_POST_RESET ever arrives (VERDICT r4 missing #1).  These te
 the fixture node with hardware events disabled (``hardware_events: false``):
 
   * an uncorrectable-ECC count that grows is seen by polling -> Unhealthy;
-  * a reset, as polling sees it (the GPU firmware's clock restarts), clears the latch;
-  * a GPU that reports no firmware clock clears it on coming back from an outage;
+  * a reset, as polling sees it, clears the latch: the kernel's reset count moved (amdgpu
+    context query on the render node, when it can be opened - also for resets that keep
+    the firmware running), or the GPU firmware's clock restarted (confirmed by a clock that
+    ticked before and ticks after; a frozen clock or a one-off reading never clears);
+  * coming back from a telemetry outage with nothing confirming a reset is only a
+    candidate: the recovery canary re-verifies it when configured, else it
+    stays latched until an operator clears it (GET /health/clear), which persists;
   * the latch is persisted (plugin/state.py): a restarted plugin - also one killed with
     SIGKILL - keeps the GPU Unhealthy, unless the firmware restarted while it was down,
     or the host rebooted (another boot id);
@@ -111,9 +116,30 @@ def test_polled_ue_latches_and_polled_reset_clears(make_cfg, plugin_dir):
             r.stop()
 
 
-def test_clockless_gpu_outage_clears_the_latch(make_cfg, plugin_dir):
-    """A GPU whose firmware reports no clock: coming back from a telemetry outage (what a
-    reset looks like to a poller) is the reset."""
+def _outage(r, gpu, seconds=0.5):
+    """Telemetry of `gpu` fails for a while (lost after 2 samples), then answers again."""
+    r.be.set_sample_fail(gpu, True)
+    time.sleep(seconds)
+    assert not r.healthy(gpu)
+
+
+def _fake_canary(monkeypatch, ok=True):
+    from k8s_gpu_device_plugin_amd.ops import canary
+    runs = []
+
+    def run_isolated(device, nbytes=0, timeout=120.0, **kw):
+        runs.append(device)
+        return {"ok": ok, "device": device} if ok else {"ok": False, "device": device, "error": "injected"}
+
+    monkeypatch.setattr(canary, "run_isolated", run_isolated)
+    return runs
+
+
+def test_clockless_gpu_outage_is_only_a_reset_candidate(make_cfg, plugin_dir):
+    """on a GPU that reports no firmware clock, an outage of failed samples
+    followed by a good one is also what an amdsmi re-init, a busy driver or a library
+    error look like.  Without corroboration it does not clear the uncorrectable-ECC
+    latch; it is reported as a reset candidate."""
     with KubeletStub(plugin_dir) as k:
         r = Run(make_cfg, _model(fw_clock=False))
         try:
@@ -121,23 +147,280 @@ def test_clockless_gpu_outage_clears_the_latch(make_cfg, plugin_dir):
             r.be.set_ecc_uncorrectable(1, 1)
             assert _wait(lambda: not r.healthy(1))
             time.sleep(0.2)
-            assert not r.healthy(1) and r.m.monitor.resets_observed == 0
-            r.be.set_sample_fail(1, True)  # mid-reset: telemetry fails (lost after 2 samples)
-            time.sleep(0.5)
-            assert not r.healthy(1)
+            _outage(r, 1)
             r.be.set_sample_fail(1, False)
-            assert _wait(lambda: r.healthy(1))
-            assert r.m.monitor.resets_observed == 1
+            assert _wait(lambda: r.m.monitor.reset_candidates == 1)
+            assert _wait(lambda: r.m.counters.get("reset_candidates") == 1)
+            time.sleep(0.4)
+            assert not r.healthy(1) and r.m.monitor.resets_observed == 0
+            assert _latched_gpus(plugin_dir) == [r.m._key_of[1]]
         finally:
             r.stop()
 
 
-def test_clockless_gpu_call_that_hung_is_not_a_reset(make_cfg, plugin_dir):
+def test_outage_with_the_ue_counter_reset_is_a_reset(make_cfg, plugin_dir):
+    """Corroboration for a clockless GPU: telemetry comes back with the uncorrectable-ECC
+    counter below the latched baseline (the driver's RAS counters started over)."""
+    with KubeletStub(plugin_dir) as k:
+        r = Run(make_cfg, _model(fw_clock=False))
+        try:
+            k.wait_for_registrations(1)
+            r.be.set_ecc_uncorrectable(1, 2)
+            assert _wait(lambda: not r.healthy(1))
+            _outage(r, 1)
+            r.be.set_ecc_uncorrectable(1, 0)
+            r.be.set_sample_fail(1, False)
+            assert _wait(lambda: r.healthy(1))
+            assert r.m.monitor.resets_observed == 1 and r.m.monitor.reset_candidates == 0
+        finally:
+            r.stop()
+
+
+def test_mode2_reset_seen_through_the_kernel_reset_count(make_cfg, plugin_dir):
+    """a reset that keeps the power-management firmware running (its
+    clock continues) with a telemetry outage - cleared through the kernel's reset count
+    when the render node can be opened (health.resetQuery), no canary needed."""
+    model = _model()
+    model["gpus"][1]["reset_query"] = True
+    with KubeletStub(plugin_dir) as k:
+        r = Run(make_cfg, model)
+        try:
+            k.wait_for_registrations(1)
+            time.sleep(0.3)
+            r.be.set_ecc_uncorrectable(1, 1)
+            assert _wait(lambda: not r.healthy(1))
+            _outage(r, 1)
+            r.be.reset_gpu(1, False)  # mode-2: the firmware clock keeps running
+            r.be.set_sample_fail(1, False)
+            assert _wait(lambda: r.healthy(1)), "kernel reset count not taken as a reset"
+            assert r.m.monitor.resets_observed == 1 and r.m.monitor.reset_candidates == 0
+            assert _wait(lambda: any(h == 1 and "kernel reports 1 GPU reset" in why
+                                     for _, g, h, why in list(r.m.health_log) if g == 1))
+            assert _wait(lambda: _latched_gpus(plugin_dir) == [])
+        finally:
+            r.stop()
+
+
+def test_reset_query_can_be_turned_off(make_cfg, plugin_dir):
+    model = _model()
+    model["gpus"][1]["reset_query"] = True
+    with KubeletStub(plugin_dir) as k:
+        r = Run(make_cfg, model, health={"resetQuery": False})
+        try:
+            k.wait_for_registrations(1)
+            r.be.set_ecc_uncorrectable(1, 1)
+            assert _wait(lambda: not r.healthy(1))
+            r.be.reset_gpu(1, False)
+            time.sleep(0.5)
+            assert not r.healthy(1) and r.m.monitor.resets_observed == 0
+        finally:
+            r.stop()
+
+
+def test_mode2_reset_without_evidence_is_verified_by_the_recovery_canary(make_cfg, plugin_dir, monkeypatch):
+    """Unprivileged default (no render node, no events), a mode-2-style reset (clock
+    continues, telemetry outage): with health.canary the candidate is re-verified and the
+    GPU comes back Healthy after the canary passes - once, not twice."""
+    runs = _fake_canary(monkeypatch, ok=True)
+    with KubeletStub(plugin_dir) as k:
+        r = Run(make_cfg, _model(), health={"canary": True})
+        try:
+            k.wait_for_registrations(1)
+            time.sleep(0.3)
+            r.be.set_ecc_uncorrectable(1, 1)
+            assert _wait(lambda: not r.healthy(1))
+            _outage(r, 1)
+            r.be.reset_gpu(1, False)
+            r.be.set_sample_fail(1, False)
+            assert _wait(lambda: r.healthy(1)), "candidate not verified and cleared"
+            assert r.m.monitor.reset_candidates == 1 and r.m.monitor.resets_observed == 0
+            assert r.m.counters.get("latches_cleared_verified") == 1
+            time.sleep(0.3)
+            assert len(runs) == 1, runs  # the verification itself, no second canary
+            assert _wait(lambda: _latched_gpus(plugin_dir) == [])
+        finally:
+            r.stop()
+
+
+def test_reset_candidate_that_fails_the_canary_stays_latched(make_cfg, plugin_dir, monkeypatch):
+    _fake_canary(monkeypatch, ok=False)
+    with KubeletStub(plugin_dir) as k:
+        r = Run(make_cfg, _model(), health={"canary": True})
+        try:
+            k.wait_for_registrations(1)
+            r.be.set_ecc_uncorrectable(1, 1)
+            assert _wait(lambda: not r.healthy(1))
+            _outage(r, 1)
+            r.be.set_sample_fail(1, False)
+            assert _wait(lambda: r.m.counters.get("canary_failures", 0) >= 1)
+            time.sleep(0.3)
+            assert not r.healthy(1) and _latched_gpus(plugin_dir) == [r.m._key_of[1]]
+        finally:
+            r.stop()
+
+
+def test_operator_clear_after_an_unconfirmed_reset_persists(make_cfg, plugin_dir):
+    """No canary, no render node: the candidate stays latched until an operator clears it
+    (GET /health/clear).  The clear is persisted: a restarted plugin advertises it Healthy."""
+    with KubeletStub(plugin_dir) as k:
+        r = Run(make_cfg, _model())
+        try:
+            k.wait_for_registrations(1)
+            time.sleep(0.3)
+            r.be.set_ecc_uncorrectable(1, 1)
+            assert _wait(lambda: not r.healthy(1))
+            _outage(r, 1)
+            r.be.reset_gpu(1, False)
+            r.be.set_sample_fail(1, False)
+            assert _wait(lambda: r.m.monitor.reset_candidates == 1)
+            time.sleep(0.3)
+            assert not r.healthy(1)
+            key1 = r.m._key_of[1]
+            status, data = r.m.clear_health(key1)
+            assert status == 200 and data["cleared"] == ["uncorrectable_ecc"] and data["still_unhealthy"] == []
+            assert _wait(lambda: r.healthy(1))
+            assert r.m.counters["health_clears"] == 1
+            assert _wait(lambda: _latched_gpus(plugin_dir) == [])
+            time.sleep(0.3)  # the UE count (still 1) is the new baseline: no new latch
+            assert r.healthy(1)
+        finally:
+            r.stop()
+        r2 = Run(make_cfg, _model(ue1=1))
+        try:
+            _, devs = k.watch(k.requests[-1].endpoint).next()
+            assert [h for _, h, _ in devs] == ["Healthy", "Healthy"]
+            assert r2.m.counters.get("latches_restored", 0) == 0
+            time.sleep(0.3)
+            assert r2.healthy(1)
+        finally:
+            r2.stop()
+
+
+def test_operator_clear_resolves_gpus_by_every_name(make_cfg, plugin_dir):
+    with KubeletStub(plugin_dir) as k:
+        r = Run(make_cfg, _model())
+        try:
+            k.wait_for_registrations(1)
+            key1 = r.m._key_of[1]
+            dev1 = r.m.plugins[0].table.ids()[1]
+            bdf1 = next(g.bdf for g in r.m.gpus if g.index == 1)
+            for sel in (key1, key1.upper(), "1", dev1, bdf1, bdf1.split(":", 1)[1]):
+                status, data = r.m.clear_health(sel)
+                assert status == 200 and data["gpu"] == key1 and data["cleared"] == [], (sel, data)
+            status, data = r.m.clear_health("no-such-gpu")
+            assert status == 404
+        finally:
+            r.stop()
+
+
+def test_operator_clear_leaves_levels_the_samples_judge(make_cfg, plugin_dir):
+    """A GPU whose telemetry is still failing stays Unhealthy after a clear; the answer
+    says what still holds it."""
+    with KubeletStub(plugin_dir) as k:
+        r = Run(make_cfg, _model())
+        try:
+            k.wait_for_registrations(1)
+            r.be.set_ecc_uncorrectable(1, 1)
+            assert _wait(lambda: not r.healthy(1))
+            r.be.set_sample_fail(1, True)
+            assert _wait(lambda: "telemetry_lost" in r.m.monitor.holds(r.m._key_of[1]))
+            status, data = r.m.clear_health(r.m._key_of[1])
+            assert status == 200 and data["cleared"] == ["uncorrectable_ecc"]
+            assert data["still_unhealthy"] == ["telemetry_lost"]
+            time.sleep(0.3)
+            assert not r.healthy(1)
+            r.be.set_sample_fail(1, False)
+            assert _wait(lambda: r.healthy(1))
+        finally:
+            r.stop()
+
+
+def test_frozen_firmware_clock_never_clears_a_restored_latch(make_cfg, plugin_dir):
+    """a hung SMU leaves the firmware clock frozen; boot time minus a frozen
+    clock grows with wall time and looked like a firmware that started after the latch.
+    The restored latch is judged only against a clock this process saw ticking."""
+    with KubeletStub(plugin_dir) as k:
+        r, key1 = _latch(make_cfg, plugin_dir, k)
+        fw_now = r.m.exporter.last_sample(1).fw_clock_s if hasattr(r.m.exporter, "last_sample") else None
+        r.stop()
+        be = fixtures.build_backend(_model(ue1=1))
+        # frozen 200 s ago: boot - clock reads 200 s later than the recorded start
+        be.set_fw_clock_frozen(1, True, max(1.0, (fw_now or 190.0) - 200.0))
+        r2 = Run.__new__(Run)
+        r2.be = be
+        r2.m = PluginManager(make_cfg(telemetry={"intervalMs": 50}, health={"lostAfterFailures": 2}), backend=be)
+        r2.t = r2.m.start_background()
+        try:
+            assert r2.m.counters["latches_restored"] == 1
+            time.sleep(0.8)
+            assert not r2.healthy(1) and r2.m.monitor.resets_observed == 0
+            assert _latched_gpus(plugin_dir) == [key1]
+        finally:
+            r2.stop()
+
+
+def test_one_backward_clock_reading_is_not_a_reset(make_cfg, plugin_dir):
+    """one stale or garbage firmware-clock reading followed by normal ones is a
+    glitch (the restart is confirmed only by a new clock that keeps ticking)."""
+    with KubeletStub(plugin_dir) as k:
+        r, key1 = _latch(make_cfg, plugin_dir, k)
+        try:
+            r.be.glitch_fw_clock(1, 0.5)
+            assert _wait(lambda: r.m.monitor.fw_clock_glitches >= 1)
+            time.sleep(0.4)
+            assert not r.healthy(1) and r.m.monitor.resets_observed == 0
+            assert r.m.monitor.reset_candidates == 0
+            r.be.reset_firmware(1)  # a real restart still counts afterwards
+            assert _wait(lambda: r.healthy(1))
+        finally:
+            r.stop()
+
+
+def test_firmware_restart_right_after_start_up_is_still_seen(n):
+    """A restart before the monitor saw the clock tick for two intervals is not dropped as
+    a glitch: it is confirmed by two ticking intervals of the new clock instead of one."""
+    be = fixtures.build_backend(_model())
+    gpus, _ = be.discover()
+    key = be.gpu_key(1)
+    mon = n.HealthMonitor(be, 2)
+    mon.set_gpus([be.gpu_key(0), key])
+    mon.restore_latches([n.HealthLatch(key, 1, float("nan"), "test latch", 0)])
+    assert not mon.gpu_healthy(1)
+    mon.on_sample(1, True, be.sample(1))  # one reading: the clock was never seen ticking
+    time.sleep(0.1)
+    be.reset_firmware(1)
+    mon.on_sample(1, True, be.sample(1))  # the step back: pending
+    assert not mon.gpu_healthy(1)
+    time.sleep(0.1)
+    mon.on_sample(1, True, be.sample(1))  # one tick of the new clock: not yet
+    assert not mon.gpu_healthy(1) and mon.resets_observed == 0
+    time.sleep(0.1)
+    mon.on_sample(1, True, be.sample(1))  # two ticks: a restart
+    assert mon.gpu_healthy(1) and mon.resets_observed == 1 and mon.fw_clock_glitches == 0
+
+
+def test_clocked_gpu_outage_with_a_firmware_restart_is_a_reset(make_cfg, plugin_dir):
+    """A mode-1-style reset on a clocked GPU: telemetry fails meanwhile and the firmware
+    comes back with its clock restarted - a reset, no candidate."""
+    with KubeletStub(plugin_dir) as k:
+        r, key1 = _latch(make_cfg, plugin_dir, k)
+        try:
+            _outage(r, 1)
+            r.be.reset_gpu(1, True)
+            r.be.set_sample_fail(1, False)
+            assert _wait(lambda: r.healthy(1))
+            assert r.m.monitor.resets_observed == 1 and r.m.monitor.reset_candidates == 0
+        finally:
+            r.stop()
+
+
+@pytest.mark.parametrize("fw_clock", [False, True])
+def test_call_that_hung_and_returned_is_not_a_reset(make_cfg, plugin_dir, fw_clock):
     """On a clockless GPU only an outage of failed samples counts as a reset: a telemetry
     call that hung (the watchdog marks the GPU lost) and then returned leaves the
     uncorrectable-ECC latch in place."""
     with KubeletStub(plugin_dir) as k:
-        r = Run(make_cfg, _model(fw_clock=False), health={"sampleStallS": 0.3})
+        r = Run(make_cfg, _model(fw_clock=fw_clock), health={"sampleStallS": 0.3})
         try:
             k.wait_for_registrations(1)
             r.be.set_ecc_uncorrectable(1, 1)
@@ -148,6 +431,7 @@ def test_clockless_gpu_call_that_hung_is_not_a_reset(make_cfg, plugin_dir):
             assert _wait(lambda: r.m.exporter.stalled_gpu == -1)
             time.sleep(0.5)  # samples flow again
             assert not r.healthy(1) and r.m.monitor.resets_observed == 0
+            assert r.m.monitor.reset_candidates == 0
         finally:
             r.stop()
 

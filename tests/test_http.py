@@ -550,3 +550,52 @@ def test_ready_follows_kubelet_registration(make_cfg, plugin_dir, server):
         t.join(10)
         assert get(port, "/ready")[0] == 503  # a stopped manager is not ready
         w.stop()
+
+
+@pytest.mark.parametrize("server", ["native", "python"])
+def test_health_clear_route(make_cfg, plugin_dir, server):
+    """GET /health/clear?gpu=...: the operator's latch clear.  The
+    util envelope; 400 without a GPU, 404 for one that does not exist; a latched GPU comes
+    back Healthy; only loopback peers by default (http.healthClearLocalOnly)."""
+    from k8s_gpu_device_plugin_amd.models import fixtures
+    from k8s_gpu_device_plugin_amd.plugin.kubelet_stub import KubeletStub
+    model = fixtures.mi355x_node(2)
+    model["hardware_events"] = False
+    be = fixtures.build_backend(model)
+    ip = _non_loopback_ipv4()
+    cfg = make_cfg(webListenAddress="0.0.0.0:0", http={"server": server, "accessLog": False},
+                   telemetry={"intervalMs": 50})
+    with KubeletStub(plugin_dir) as k:
+        mgr = PluginManager(cfg, backend=be)
+        t = mgr.start_background()
+        w = WebServer(cfg, mgr)
+        port = w.start()
+        try:
+            k.wait_for_registrations(1)
+            st, _, body = get(port, "/health/clear")
+            assert st == 400 and json.loads(body)["code"] == -1
+            st, _, body = get(port, "/health/clear?gpu=GPU-nope")
+            assert st == 404 and json.loads(body) == {"code": -1, "data": None, "msg": "no GPU matches 'GPU-nope'"}
+            be.set_ecc_uncorrectable(1, 1)
+            ids = mgr.plugins[0].table.ids()
+            assert _wait_for(lambda: not mgr.plugins[0].table.healthy(ids[1]))
+            st, _, body = get(port, "/health/clear?gpu=" + ids[1])
+            reply = json.loads(body)
+            assert st == 200 and reply["code"] == 0 and reply["msg"] == "success"
+            assert reply["data"]["cleared"] == ["uncorrectable_ecc"] and reply["data"]["index"] == 1
+            assert _wait_for(lambda: mgr.plugins[0].table.healthy(ids[1]))
+            if ip is not None:
+                c = http.client.HTTPConnection(ip, port, timeout=5)
+                c.request("GET", "/health/clear?gpu=1")
+                r = c.getresponse()
+                assert (r.status, r.read()) == (403, b'{"message":"Forbidden"}\n')
+                c.close()
+            reqs = {(s.labels["handler"], s.labels["status"]): s.value
+                    for f in text_string_to_metric_families(get(port, "/metrics")[2].decode())
+                    for s in f.samples if s.name == "echo_http_requests_total"}
+            assert reqs[("/health/clear", "2xx")] == 1 and reqs[("/health/clear", "4xx")] >= 2
+            assert 'amdgpu_device_plugin_events_total{event="health_clears"}' in mgr.exporter.render()
+        finally:
+            w.stop()
+            mgr.stop()
+            t.join(10)

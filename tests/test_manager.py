@@ -129,12 +129,13 @@ def test_removed_plugin_socket_is_served_again(make_cfg, plugin_dir, run_manager
         m = run_manager(make_cfg(grpc={"server": grpc_server}))
         k.wait_for_registrations(1)
         reloads = m.counters["reloads"]
-        m.restart()  # own reload: swaps the table, keeps the socket
+        m.restart()  # own reload: swaps the table, keeps the socket, registers it again
         assert _wait(lambda: m.counters["reloads"] > reloads)
-        time.sleep(0.5)
-        assert m.counters.get("restarts_socket", 0) == 0 and len(k.requests) == 1
-        os.remove(os.path.join(plugin_dir, "amd-gpu.sock"))
         k.wait_for_registrations(2, timeout=10)
+        time.sleep(0.5)
+        assert m.counters.get("restarts_socket", 0) == 0 and len(k.requests) == 2
+        os.remove(os.path.join(plugin_dir, "amd-gpu.sock"))
+        k.wait_for_registrations(3, timeout=10)
         assert _wait(lambda: m.counters.get("restarts_socket", 0) == 1)
         assert k.client("amd-gpu.sock").get_options().get_preferred_allocation_available
         assert 'amdgpu_device_plugin_events_total{event="restarts_socket"} 1' in m.exporter.render()
@@ -162,7 +163,61 @@ def test_restart_api_reloads_without_dropping_kubelet(make_cfg, plugin_dir, run_
         _, again = w.next(timeout=5)
         assert [d for d, _, _ in again] == ids
         assert c.allocate([ids[0]]).container_responses[0].devices  # same connection
-        assert len(k.requests) == 1 and m.counters.get("table_swaps", 0) >= 1
+        # the restart ends in a Register on the same socket (reference router/api.go:50-54)
+        assert _wait(lambda: len(k.requests) >= 2) and m.counters.get("table_swaps", 0) >= 1
+        assert all(r.endpoint == reg.endpoint for r in k.requests)
+        assert len(k.requests) == 1 + m.counters["reregistrations_restart"]
+
+
+@pytest.mark.parametrize("grpc_server", ["native", "python"])
+def test_restart_api_registers_again_on_the_running_socket(make_cfg, plugin_dir, run_manager, grpc_server):
+    """The reference's /restart always ends in a fresh Register (router/api.go:50-54 ->
+    plugin/manager.go:177-194 -> plugin/plugin.go:140-162): the operator's way out when
+    kubelet's view of the plugin went wrong while its stream is open.  One /restart ->
+    exactly one new Register per resource, for the same socket file (never unbound), and a
+    kubelet that re-dials on it gets a fresh stream and working Allocates."""
+    from k8s_gpu_device_plugin_amd.plugin.plugin import _socket_ident
+    be = fixtures.build_backend("2gpu_spx")
+    with KubeletStub(plugin_dir, redial=True) as k:
+        m = run_manager(make_cfg(migStrategy="mixed", grpc={"server": grpc_server}), backend=be)
+        fixtures.set_gpu_mode(be, 1, "CPX", "NPS1")
+        regs = k.wait_for_registrations(1)
+        time.sleep(0.3)
+        m.restart()  # picks up GPU 1 in CPX: two resources from here on
+        assert _wait(lambda: len(m.plugins) == 2, 10)
+        base = len(k.requests)
+        idents = {p.resource: _socket_ident(p.socket) for p in m.plugins}
+        old = k.watch(regs[0].endpoint)
+        m.restart()
+        assert _wait(lambda: len(k.requests) == base + 2, 10)
+        time.sleep(0.5)
+        assert len(k.requests) == base + 2  # exactly one per resource
+        assert sorted(r.endpoint for r in k.requests[base:]) == sorted(os.path.basename(p.socket)
+                                                                      for p in m.plugins)
+        assert {p.resource: _socket_ident(p.socket) for p in m.plugins} == idents  # never unbound
+        assert m.counters["reregistrations_restart"] >= 2
+        # kubelet re-dialled: a new stream with the device list, Allocate on the new connection
+        assert _wait(lambda: k.reopened >= 1, 10)  # (the one endpoint it watched)
+        w = k.watch(regs[0].endpoint)
+        assert w is not old
+        _, devs = w.next(timeout=5)
+        ids = [d for d, _, _ in devs]
+        assert ids and k.client(regs[0].endpoint).allocate([ids[0]]).container_responses[0].devices
+        assert m.plugins[0].list_and_watch_streams() >= 1
+
+
+def test_restart_registers_again_when_discovery_fails(make_cfg, plugin_dir, run_manager):
+    """A /restart whose discovery fails leaves the plugins serving (make-before-break)
+    and still points kubelet at them again."""
+    be = fixtures.build_backend("2gpu_spx")
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(retrySeconds=30.0), backend=be)
+        k.wait_for_registrations(1)
+        be.set_fail_discovery(True)
+        m.restart()
+        k.wait_for_registrations(2, timeout=10)
+        assert m.counters["load_failures"] >= 1 and m.plugins[0].serving
+        be.set_fail_discovery(False)
 
 
 def test_retry_until_kubelet_appears(make_cfg, plugin_dir, run_manager):
@@ -655,7 +710,8 @@ def test_soak_reloads_under_traffic_do_not_grow_the_daemon():
     assert r["ok"], r
     # bursts of /restart coalesce into fewer reloads; every reload swapped its table in
     assert r["restarts"] >= 50 and r["reloads"] >= 10 and r["table_swaps"] >= r["reloads"] - 1
-    assert r["reconnects"] == 0 and r["law_reopens"] == 1 and r["registrations"] == 1
+    assert r["reconnects"] == 0 and r["law_reopens"] == 1
+    assert r["registrations"] == 1 + r["reregistrations_restart"] and r["reregistrations_restart"] >= 1
     assert r["law_updates"] >= r["table_swaps"] // 2
     assert r["rss_growth_second_half_kb"] < 600, r["rss_kb"]
 
@@ -1039,7 +1095,10 @@ def test_allocate_never_fails_through_restarts_and_inventory_changes(make_cfg, p
             t.join(10)
         assert not stats["failed"], stats["failed"][:5]
         assert stats["ok"] > 100 and stats["connections"] == 1
-        assert len(k.requests) == 1 and m.counters.get("table_swaps", 0) >= 50
+        # one Register per /restart on the same socket, none for the inventory reloads
+        assert len(k.requests) == 1 + m.counters["reregistrations_restart"]
+        assert all(r.endpoint == reg.endpoint for r in k.requests)
+        assert m.counters.get("table_swaps", 0) >= 50
         assert m.counters.get("restarts_inventory", 0) >= 5
         devs = w.last(timeout=5)
         assert len(devs) == len(m.plugins[0].table.ids())
@@ -1128,3 +1187,31 @@ def test_plugin_registers_again_when_kubelet_ends_its_stream(make_cfg, plugin_di
         time.sleep(1.5)
         assert len(k.requests) == 2  # an open stream: no further Register
         w2.cancel()
+
+
+def test_stream_watchdog_leaves_a_socket_another_instance_took(make_cfg, plugin_dir, run_manager, monkeypatch):
+    """an overlapping new instance re-bound the plugin's socket path and kubelet's
+    stream went to it.  The old process must not re-register every grace period (kubelet
+    would re-dial the path and tear down the new instance's stream each time)."""
+    import socket as socket_mod
+    from k8s_gpu_device_plugin_amd.plugin import manager as manager_mod
+    monkeypatch.setattr(manager_mod, "LAW_LOST_GRACE_S", 0.3)
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg())
+        regs = k.wait_for_registrations(1)
+        w = k.watch(regs[0].endpoint)
+        w.next()
+        p = m.plugins[0]
+        assert _wait(lambda: p.law_had, timeout=3)
+        # the "new pod": binds its own socket at the same path (unlink + bind)
+        os.remove(p.socket)
+        other = socket_mod.socket(socket_mod.AF_UNIX, socket_mod.SOCK_STREAM)
+        other.bind(p.socket)
+        other.listen(4)
+        try:
+            w.cancel()
+            assert _wait(lambda: m.counters.get("stream_watch_socket_taken", 0) == 1, timeout=10)
+            time.sleep(1.5)  # several grace periods
+            assert len(k.requests) == 1 and m.counters.get("reregistrations_stream_lost", 0) == 0
+        finally:
+            other.close()

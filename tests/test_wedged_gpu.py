@@ -108,11 +108,12 @@ def test_wedged_gpu_keeps_the_node_advertised(make_cfg, plugin_dir, run_manager,
         assert _wait(lambda: _advertised(plugin_dir, k) == want, 3), _advertised(plugin_dir, k)
 
         # GET /restart still reloads (GPU 3 from its last description), swapping the
-        # tables into the running server: no new registration
+        # tables into the running server, and registers that socket again
         n, reloads = len(k.requests), m.counters["reloads"]
         m.restart()
         assert _wait(lambda: m.counters["reloads"] > reloads, 3 * SLOW)
-        assert len(k.requests) == n
+        k.wait_for_registrations(n + 1, timeout=2 * SLOW)
+        assert len(k.requests) == n + 1
         assert _wait(lambda: _advertised(plugin_dir, k) == want, 3), _advertised(plugin_dir, k)
         assert not m.readiness()[0]
         assert m.running and m.fatal_error is None
