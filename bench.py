@@ -98,7 +98,7 @@ def _wait_http(port: int, timeout: float) -> None:
 
 TRACE_DTYPE = [("t_ready", "<i8"), ("t_dispatch", "<i8"), ("t_sent", "<i8"), ("conn", "<u8"), ("idle_ns", "<i8"),
                ("seq", "<u4"), ("method", "u1"), ("spinning", "u1"), ("cpu", "<u2"), ("prev_cpu", "<u2"),
-               ("pad0", "<u2"), ("pad1", "<u4")]  # native/grpc_h2.h CallTraceEntry (56 bytes)
+               ("pad0", "<u2"), ("recv_ns", "<u4")]  # native/grpc_h2.h CallTraceEntry (56 bytes)
 
 
 def read_call_trace(path: str):
@@ -191,7 +191,13 @@ def _tail_stats(batches, trace=None, rpc_allocate: int = 3) -> dict:
             # table, the response framing and send() (which wakes the client) after it
             rp = [int(e["t_dispatch"]) - int(e["t_ready"]) for e in matched if e is not None]
             hs = [int(e["t_sent"]) - int(e["t_dispatch"]) for e in matched if e is not None]
+            rv = [int(e["recv_ns"]) for e in matched if e is not None]
+            tails = [int(t) for b in batches if len(b) > 4 for t in b[4]]
+            if tails:  # outbound = the client's wake-up and recv (kernel) + its own parsing after it
+                out["outbound_split_p50_us"] = {"client_parse": round(float(np.median(tails)) / 1e3, 2)}
             out["server_split_p50_us"] = {"recv_parse": round(float(np.median(rp)) / 1e3, 2),
+                                          "recv": round(float(np.median(rv)) / 1e3, 2),
+                                          "parse": round(float(np.median([a - b for a, b in zip(rp, rv)])) / 1e3, 2),
                                           "handle_send": round(float(np.median(hs)) / 1e3, 2)}
     causes = collections.Counter()
     excess = collections.defaultdict(list)
@@ -248,6 +254,7 @@ def _merge_tail(parts) -> dict:
         out["segment_p50_us"] = parts[0]["segment_p50_us"]
         out["cause_mean_excess_us"] = parts[0].get("cause_mean_excess_us")
         out["server_split_p50_us"] = parts[0].get("server_split_p50_us")
+        out["outbound_split_p50_us"] = parts[0].get("outbound_split_p50_us")
     out["slowest"] = sorted((x for p in parts for x in p.get("slowest", [])), key=lambda r: -r["us"])[:8]
     return out
 
@@ -379,6 +386,33 @@ def placement_floor(nb, client_cpu: int, sizes, n: int = 3000) -> dict:
             continue
         out[rel] = {"server_cpu": c, "p50_us": round(_pct(lat, 0.5) * 1e6, 2)}
     return out
+
+
+def paired_floor(h2, nb, method: str, req: bytes, sizes, rounds: int = 16, batch: int = 256) -> dict:
+    """Allocate and the bare spin exchange (uds_roundtrip_floor_spin) in alternating
+    batches, untimed: per round the ratio of the two p50s.  On a shared host the floor
+    measured once, after the timed loop, meets other moments of the host than the
+    Allocates did; paired rounds compare like with like."""
+    import statistics
+    ratios, alloc_p50, floor_p50 = [], [], []
+    for r in range(rounds):
+        order = (0, 1) if r % 2 == 0 else (1, 0)
+        got = {}
+        for k in order:
+            if k == 0:
+                got[0] = _pct(h2.bench_unary(method, req, batch), 0.5)
+            else:
+                got[1] = _pct(nb.uds_pingpong(batch, 32, *sizes, server_spin=True), 0.5)
+        alloc_p50.append(got[0])
+        floor_p50.append(got[1])
+        ratios.append(got[0] / got[1])
+    ratios.sort()
+    # distribution-free ~95 % interval of the median: order statistics n/2 -+ 0.98 sqrt(n)
+    k = max(0, int(rounds / 2 - 0.98 * rounds ** 0.5))
+    lo, hi = ratios[max(0, k - 1)], ratios[min(rounds - 1, rounds - k)]
+    return {"rounds": rounds, "batch": batch, "allocate_p50_us": round(statistics.median(alloc_p50) * 1e6, 2),
+            "floor_spin_p50_us": round(statistics.median(floor_p50) * 1e6, 2),
+            "ratio_median": round(statistics.median(ratios), 3), "ratio_ci95": [round(lo, 3), round(hi, 3)]}
 
 
 def _placement_stats(batches, trace, topo_cpus: dict, rpc_allocate: int) -> dict:
@@ -678,9 +712,9 @@ def main() -> int:
     def step(rec):
         a, p, s, an, pn, tl = rec
         phase_sync()
-        starts, lat, cpus, pre = h2.bench_unary_ts(v1beta1.METHOD_ALLOCATE, alloc_req, ALLOCS)
+        starts, lat, cpus, pre, tail = h2.bench_unary_ts(v1beta1.METHOD_ALLOCATE, alloc_req, ALLOCS)
         an.extend(lat)
-        tl.append((starts, lat, cpus, pre))
+        tl.append((starts, lat, cpus, pre, tail))
         pn.extend(h2.bench_unary(v1beta1.METHOD_GET_PREFERRED, pref_req, PREFS))
         for _ in range(ALLOCS):
             t0 = perf()
@@ -744,6 +778,9 @@ def main() -> int:
     bf = nb.uds_pingpong_batched(args.steps, ALLOCS, int(SCRAPE_S * 1e6), *sizes,
                                  server_poll_us=args.busy_poll_us if args.busy_poll_us is not None else 50)
     mine["uds_floor_batched"] = (_pct(bf, 0.5), _pct(bf, 0.99), _pct(bf, 0.999), max(bf))
+    # Allocate against the spin floor paired in time: batches of each alternate, so a busy
+    # moment on the shared host lands on both (the floor above runs after the timed loop)
+    mine["paired"] = paired_floor(h2, nb, v1beta1.METHOD_ALLOCATE, alloc_req, sizes)
     # kubelet-like sparse calls: 1 ms apart, every one meets a sleeping server thread
     mine["alloc_cold"] = h2.bench_unary(v1beta1.METHOD_ALLOCATE, alloc_req, 400, 1000)
     # ... and the bare exchange with the same 1 ms idle gap (cold caches, idle CPU states)
@@ -811,6 +848,8 @@ def main() -> int:
             "uds_roundtrip_floor_spin_p999_us": round(gathered[0]["uds_floor_spin_p999"] * 1e6, 2),
             # the bare exchange timed in the same batches as Allocate (p50, p99, p99.9, max)
             "uds_roundtrip_floor_batched_us": [round(x * 1e6, 2) for x in gathered[0]["uds_floor_batched"]],
+            # Allocate and the spin floor in alternating batches after the timed loop (rank 0)
+            "allocate_vs_spin_floor_paired": gathered[0].get("paired"),
             "preferred_allocator_8gpu_size4_p50_us": _allocator_probe(n),
             "allocate_server_mean_us": (round(gathered[0]["server_allocate_mean_s"] * 1e6, 3)
                                         if gathered[0].get("server_allocate_mean_s") else None),

@@ -133,7 +133,8 @@ def main(argv=None) -> int:
     try:
         web.start()
         mt.start()
-        while not done.wait(0.5):
+        # (signals interrupt the wait; the parent check is the only reason to poll)
+        while not done.wait(0.5 if parent else 5.0):
             if parent and os.getppid() != parent:  # the harness is gone (PDEATHSIG backstop)
                 reason["why"] = "parent process %d exited, exiting gracefully..." % parent
                 break

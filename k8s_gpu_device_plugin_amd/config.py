@@ -154,7 +154,7 @@ class GrpcConfig:
     idleWakeMs: int = 1
     # native server: idleWakeMs and keepWarmMs run only this long after a worker's last
     # kubelet RPC (0 = always).  Outside this admission window the workers sleep: an idle
-    # node pays ~1 wake-up per worker per second for the plugin's gRPC server
+    # node pays ~1 wake-up per worker every 5 s for the plugin's gRPC server
     activeWindowMs: int = 10000
     keepWarmFull: bool = True    # ... through the whole request path of an in-memory connection (else HPACK + table)
     # native server: per-call trace of unary RPCs in a file-backed ring ("" = off), read by

@@ -931,8 +931,10 @@ class PluginManager:
         index has been advertised it stays pinned to that GPU's identity: a
         GPU that drops off the bus leaves its index empty (the selection does not take in
         the next GPU), and one that appears later with a lower BDF does not push a served
-        GPU - which pods may hold - out of the selection; it is logged and counted
-        (``devices_index_conflicts``) instead.  Indices never resolved are filled as GPUs
+        GPU that a pod holds out of the selection; it is logged and counted
+        (``devices_index_conflicts``) instead.  While no pod holds the pinned GPU the late
+        one takes its index back (``devices_index_reresolved``): a GPU missing
+        from the first discovery does not lose its index for the life of the process.  Indices never resolved are filled as GPUs
         appear.  UUIDs and BDFs are matched as given, and ``hip:<n>`` selects the GPU a
         HIP ordinal opens."""
         sel = parse_device_selector(self.cfg.devices)
@@ -953,6 +955,18 @@ class PluginManager:
         for i in sorted(indices):
             at_rank = [g for g in gpus if rank.get((g.bdf or "").lower(), -1) == i]
             pinned = self._pinned_index.get(i)
+            if pinned is not None and at_rank and self._identity(at_rank[0]) != pinned:
+                newk = self._identity(at_rank[0])
+                if newk not in self._pinned_index.values() and not self._pinned_gpu_in_use(pinned):
+                    # a GPU that enumerated late (missing from an earlier discovery) takes
+                    # its index back while no pod holds the GPU that stood in for it
+                    # 
+                    self._pinned_index[i] = newk
+                    picked.add(newk)
+                    self.counters["devices_index_reresolved"] = self.counters.get("devices_index_reresolved", 0) + 1
+                    log.warning("devices %r: index %d now names %s (ranks %d by BDF); %s, which held it, is "
+                                "not allocated to any pod", self.cfg.devices, i, newk, i, pinned)
+                    continue
             if pinned is not None:
                 if pinned in by_key:
                     picked.add(pinned)
@@ -961,9 +975,9 @@ class PluginManager:
                     if moved not in self._index_conflicts:
                         self._index_conflicts.add(moved)
                         self.counters["devices_index_conflicts"] = self.counters.get("devices_index_conflicts", 0) + 1
-                        log.warning("devices %r: index %d is pinned to %s, which this process advertised; %s now "
-                                    "ranks %d by BDF and is not selected (restart the plugin to re-resolve indices)",
-                                    self.cfg.devices, i, pinned, moved[1], i)
+                        log.warning("devices %r: index %d is pinned to %s, which a pod holds; %s now ranks %d by "
+                                    "BDF and is not selected until no pod holds %s", self.cfg.devices, i, pinned,
+                                    moved[1], i, pinned)
                 continue
             if at_rank:
                 k = self._identity(at_rank[0])
@@ -978,6 +992,14 @@ class PluginManager:
             log.info("devices %r selects %s", self.cfg.devices, ", ".join(chosen) or "nothing (yet)")
             self._selection = chosen
         return out
+
+    def _pinned_gpu_in_use(self, key: str) -> bool:
+        """Whether a pod holds a device of the advertised GPU ``key`` (PodResources when
+        polled, else kubelet's device checkpoint).  A GPU never advertised is not held."""
+        idx = self._index_of.get(key)
+        if idx is None or not self.device_map:
+            return False
+        return any(g == idx for g, _ in self._in_use_partitions(self.device_map))
 
     # ------------------------------------------------------------ health
     def _identity(self, g) -> str:
@@ -1428,10 +1450,12 @@ class PluginManager:
         self._watcher = watcher  # _shutdown wakes its read
 
         def watch_loop():
-            # a second per read: an idle node pays one wake-up a second for it, and
-            # _shutdown cuts the read short (DirWatcher.wake)
+            # long reads (inotify wakes it for every change in the directory): an idle node
+            # pays one wake-up every 5 s for it, and _shutdown cuts the read short
+            # (DirWatcher.wake).  A directory removed and created again is noticed on the
+            # timeout, so within 5 s.
             while self._running.is_set() and watcher is not None:
-                for name, _mask, created, _removed in watcher.read(1000):
+                for name, _mask, created, _removed in watcher.read(5000):
                     if name == "kubelet.sock" and created:
                         self.events.put((EV_KUBELET,))
                     elif _removed and name.endswith(".sock") and name != "kubelet.sock":
@@ -1444,7 +1468,7 @@ class PluginManager:
                 if not self.monitor.running:
                     time.sleep(0.1)
                     continue
-                for u in self.monitor.pop(1000):  # (returns at once on an update or stop)
+                for u in self.monitor.pop(5000):  # (returns at once on an update or stop)
                     self.events.put((EV_HEALTH, u))
 
         def rediscover_loop():

@@ -613,6 +613,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
   // call trace (set_call_trace): when the events being handled were delivered, whether the
   // worker was polling then, and the records of this batch still waiting for their send
   int64_t wake_ts = 0;
+  int64_t recv_done = 0;  // (call trace) when the request's recv() returned
   bool wake_spin = false;
   int64_t wake_idle = 0;      // the worker's time without work before this wake-up
   uint16_t last_cpu = 0xFFFF;  // CPU of the worker's previous work
@@ -672,6 +673,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
                                       : m == kMOptions ? kRpcOptions : 255);
       e.spinning = wake_spin ? 1 : 0;
       e.idle_ns = wake_idle;
+      e.recv_ns = recv_done > wake_ts ? static_cast<uint32_t>(std::min<int64_t>(recv_done - wake_ts, 0xFFFFFFFF)) : 0;
       const int cpu = sched_getcpu();
       e.cpu = static_cast<uint16_t>(cpu < 0 ? 0xFFFF : cpu);
       e.prev_cpu = last_cpu;
@@ -1135,12 +1137,12 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
       // ticks, and a worker that holds a connection wakes at least every idle_wake_ms (keeps
       // its core out of deep idle states: what the first request after a long idle pays most
       // of).  Outside it: nothing runs; the worker sleeps until a request, a notify, a table
-      // swap or stop (all of which write its eventfd), with a 1 s safety tick.
+      // swap or stop (all of which write its eventfd), with a 5 s safety tick.
       const int window = active_window_ms_.load(std::memory_order_relaxed);
       const bool active = window == 0 || (last_rpc != 0 && mono_ns() - last_rpc < static_cast<int64_t>(window) * 1000000);
       const int warm = active ? keep_warm_ms_.load(std::memory_order_relaxed) : 0;
       const int wake = (!active || w->conns.empty()) ? 0 : idle_wake_ms_.load(std::memory_order_relaxed);
-      int timeout = warm > 0 ? std::min(warm, 100) : (active ? 100 : 1000);
+      int timeout = warm > 0 ? std::min(warm, 100) : (active ? 100 : 5000);
       if (wake > 0) timeout = std::min(timeout, wake);
       n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), timeout);
       if (n == 0) idle_wakeups_.fetch_add(1, std::memory_order_relaxed);
@@ -1296,6 +1298,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
             break;
           }
         }
+        if (trace_) recv_done = mono_ns();
         if (!process(*c)) c->closing = true;
         const int64_t window = admitting ? std::max(spin_ns, admission_ns) : spin_ns;
         if (window > 0) {
@@ -1403,23 +1406,31 @@ void H2Client::send_all(const std::string& s) {
   }
 }
 
-bool H2Client::read_frame(uint8_t* type, uint8_t* flags, uint32_t* sid, std::string* payload) {
+bool H2Client::read_frame(uint8_t* type, uint8_t* flags, uint32_t* sid, std::string_view* payload) {
+  // Frames are parsed in place: *payload views in_, valid until the next read_frame (every
+  // caller uses it before reading on), and the consumed prefix goes only when more bytes
+  // are needed - no per-frame copy or memmove on the response path.
   char buf[32768];
   for (;;) {
-    if (in_.size() >= 9) {
-      const uint8_t* h = reinterpret_cast<const uint8_t*>(in_.data());
+    const size_t avail = in_.size() - in_off_;
+    if (avail >= 9) {
+      const uint8_t* h = reinterpret_cast<const uint8_t*>(in_.data() + in_off_);
       const uint32_t len = (static_cast<uint32_t>(h[0]) << 16) | (static_cast<uint32_t>(h[1]) << 8) | h[2];
-      if (in_.size() >= 9 + len) {
+      if (avail >= 9 + static_cast<size_t>(len)) {
         *type = h[3];
         *flags = h[4];
         *sid = get_u32(h + 5) & 0x7FFFFFFFu;
-        payload->assign(in_.data() + 9, len);
-        in_.erase(0, 9 + len);
+        *payload = std::string_view(in_.data() + in_off_ + 9, len);
+        in_off_ += 9 + len;
         return true;
       }
     }
+    if (in_off_ == in_.size()) in_.clear();
+    else if (in_off_ > 0) in_.erase(0, in_off_);
+    in_off_ = 0;
     // blocking recv bounded by SO_RCVTIMEO: one syscall per response instead of poll + recv
     const ssize_t r = recv(fd_, buf, sizeof(buf), 0);
+    if (stamp_recv_) recv_ret_ns_ = mono_ns();
     if (r <= 0) {
       if (r < 0 && errno == EINTR) continue;
       if (r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK))
@@ -1431,7 +1442,7 @@ bool H2Client::read_frame(uint8_t* type, uint8_t* flags, uint32_t* sid, std::str
 }
 
 
-bool H2Client::handle_control(uint8_t type, uint8_t flags, uint32_t sid, const std::string& payload) {
+bool H2Client::handle_control(uint8_t type, uint8_t flags, uint32_t sid, std::string_view payload) {
   std::string ctl;
   if (type == kSettings) {
     if (!(flags & kAck)) {
@@ -1490,7 +1501,7 @@ void H2Client::send_request(uint32_t sid, std::string_view path, std::string_vie
       o.clear();
       uint8_t type, flags;
       uint32_t fsid;
-      std::string payload;
+      std::string_view payload;
       if (!read_frame(&type, &flags, &fsid, &payload)) throw std::runtime_error("H2Client: connection closed");
       if (!handle_control(type, flags, fsid, payload) && fsid == sid && (type == kRstStream))
         throw std::runtime_error("H2Client: stream reset while sending");
@@ -1515,7 +1526,7 @@ int H2Client::unary(std::string_view path, std::string_view req, std::string* re
   int status = -1;
   uint8_t type, flags;
   uint32_t fsid;
-  std::string& payload = frame_buf_;
+  std::string_view payload;
   for (;;) {
     if (!read_frame(&type, &flags, &fsid, &payload)) throw std::runtime_error("H2Client: connection closed");
     if (handle_control(type, flags, fsid, payload)) continue;
@@ -1573,7 +1584,7 @@ int H2Client::first_stream_message(std::string_view path, std::string_view req, 
   std::string data;
   uint8_t type, flags;
   uint32_t fsid;
-  std::string payload;
+  std::string_view payload;
   for (;;) {
     if (!read_frame(&type, &flags, &fsid, &payload)) throw std::runtime_error("H2Client: connection closed");
     if (handle_control(type, flags, fsid, payload)) continue;
@@ -1609,7 +1620,7 @@ int H2Client::next_stream_message(std::string* resp, int timeout_ms) {
   } restore{this};
   uint8_t type, flags;
   uint32_t fsid;
-  std::string payload;
+  std::string_view payload;
   for (;;) {
     if (watch_buf_.size() >= 5) {
       const uint32_t len = get_u32(reinterpret_cast<const uint8_t*>(watch_buf_.data()) + 1);

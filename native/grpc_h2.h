@@ -44,7 +44,7 @@ struct CallTraceEntry {
   uint16_t cpu = 0;        // CPU the worker ran on at dispatch
   uint16_t prev_cpu = 0;   // CPU of the worker's previous work (0xFFFF: none yet)
   uint16_t pad0 = 0;
-  uint32_t pad1 = 0;
+  uint32_t recv_ns = 0;    // t_ready -> the connection's recv() returned (the rest to t_dispatch is parsing)
 };
 static_assert(sizeof(CallTraceEntry) == 56, "trace record layout is read by bench.py");
 struct CallTraceHeader {
@@ -120,9 +120,9 @@ class GrpcServer {
   void set_idle_wake_ms(int ms) { idle_wake_ms_.store(ms > 0 ? ms : 0); }
   // Admission window (grpc.activeWindowMs, 0 = always): idle wake-ups and keep-warm ticks
   // run only for this long after a worker's last kubelet RPC.  Outside it the worker sleeps
-  // in epoll_wait for up to a second at a time: an idle node pays nothing for the plugin,
+  // in epoll_wait for up to 5 s at a time: an idle node pays next to nothing for the plugin,
   // and a pod admission's first call (GetPreferredAllocation) opens the window for the
-  // Allocate that follows it.
+  // Allocate that follows it.  (Sleeping workers wake every 5 s.)
   void set_active_window_ms(int ms) { active_window_ms_.store(ms > 0 ? ms : 0); }
   // Epoll wake-ups of the workers that found nothing to do (timeouts), all workers.
   uint64_t idle_wakeups() const { return idle_wakeups_.load(); }
@@ -202,15 +202,19 @@ class H2Client {
   void open_stream(std::string_view path, std::string_view req);
   int next_stream_message(std::string* resp, int timeout_ms);
   void close();
+  // Benchmarks: stamp when each recv() returns (one clock read per recv), so a call's
+  // time after the response arrived (the client's own parsing) can be told from the wait.
+  void set_stamp_recv(bool on) { stamp_recv_ = on; }
+  int64_t last_recv_ns() const { return recv_ret_ns_; }
 
  private:
   void send_all(const std::string& s);
   void set_recv_timeout(int ms);
-  bool read_frame(uint8_t* type, uint8_t* flags, uint32_t* sid, std::string* payload);
+  bool read_frame(uint8_t* type, uint8_t* flags, uint32_t* sid, std::string_view* payload);
   // Sends HEADERS + gRPC-framed request DATA (split into frames, within flow control).
   void send_request(uint32_t sid, std::string_view path, std::string_view req);
   // Handles connection-level frames (SETTINGS/PING/WINDOW_UPDATE); true if consumed.
-  bool handle_control(uint8_t type, uint8_t flags, uint32_t sid, const std::string& payload);
+  bool handle_control(uint8_t type, uint8_t flags, uint32_t sid, std::string_view payload);
   int64_t send_window_ = 65535;          // connection send window
   int64_t stream_window_init_ = 65535;   // server's SETTINGS_INITIAL_WINDOW_SIZE
   int64_t stream_window_ = 0;            // current request stream's send window
@@ -220,13 +224,16 @@ class H2Client {
   uint32_t next_sid_ = 1;
   hpack::Decoder dec_;
   std::string in_;
+  size_t in_off_ = 0;  // bytes of in_ already parsed (read_frame)
+  bool stamp_recv_ = false;
+  int64_t recv_ret_ns_ = 0;
   int64_t conn_consumed_ = 0;
   uint32_t watch_sid_ = 0;
   std::string watch_buf_;
   int64_t watch_consumed_ = 0;
   int timeout_ms_;
   std::string hpath_, hblock_;  // last request path and its encoded header block
-  std::string out_buf_, body_buf_, data_buf_, frame_buf_;  // per-call scratch, capacity reused
+  std::string out_buf_, body_buf_, data_buf_;  // per-call scratch, capacity reused
 };
 
 

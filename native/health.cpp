@@ -90,9 +90,9 @@ void HealthMonitor::loop() {
     evs.clear();
     if (!backend_->delivers_events()) {
       // nothing armed (an unprivileged pod): health runs on polling; sleep until stop() or
-      // a second has passed (arming may happen later, after a re-initialisation)
+      // 5 s have passed (arming may happen later, after a re-initialisation)
       std::unique_lock<std::mutex> lk(mu_);
-      cv_wait_ms(cv_, lk, 1000, [&] { return stop_; });
+      cv_wait_ms(cv_, lk, 5000, [&] { return stop_; });
       continue;
     }
     // bounded wait so stop() is honoured within ~200 ms

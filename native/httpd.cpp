@@ -223,7 +223,7 @@ int HttpServer::start() {
   running_ = true;
   const int nthreads = std::max(1, cfg_.threads);
   // stop() writes this (never read: level-triggered, it wakes every worker at once), so the
-  // workers can sleep a second at a time when no scraper is around
+  // workers can sleep 5 s at a time when no scraper is around
   stop_efd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
   for (int t = 0; t < nthreads; ++t) {
     auto w = std::make_unique<Worker>();
@@ -413,7 +413,8 @@ int HttpServer::start() {
       const int64_t spin_ns = static_cast<int64_t>(std::max(0, std::min(cfg_.busy_poll_us, 100000))) * 1000;
       int64_t spin_until = 0;
       while (!stop_.load(std::memory_order_relaxed)) {
-        const int n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), spin_until ? 0 : 1000);
+        // 5 s: the idle-connection sweep below needs no finer grain (timeouts are 30-60 s)
+        const int n = epoll_wait(w->ep, evs.data(), static_cast<int>(evs.size()), spin_until ? 0 : 5000);
         const int64_t now = mono_ns();
         if (spin_until) {
           if (n == 0 && now < spin_until) {

@@ -269,10 +269,10 @@ void Exporter::watchdog_loop(std::shared_ptr<HealthMonitor> monitor, std::shared
     waker->sleep_ms(sleep_ms);
     if (stop_.load()) break;
     const int ms = stall_ms_.load();
-    // Checks an eighth of the stall threshold apart (25 ms .. 1 s; 1 s with no threshold),
-    // sooner when a call in flight is about to cross it: a 10 s threshold costs one
-    // wake-up a second on an idle node instead of forty.
-    const int64_t period = ms > 0 ? std::max<int64_t>(25, std::min<int64_t>(1000, ms / 8)) : 1000;
+    // Checks a quarter of the stall threshold apart (25 ms .. 5 s; 5 s with no threshold),
+    // sooner when a call in flight is about to cross it (then it wakes as it crosses): a
+    // 10 s threshold costs a wake-up every 2.5 s on an idle node instead of 40 a second.
+    const int64_t period = ms > 0 ? std::max<int64_t>(25, std::min<int64_t>(5000, ms / 4)) : 5000;
     sleep_ms = period;
     std::shared_ptr<Backend> be;
     {

@@ -178,7 +178,7 @@ class Daemon:
         self.starts = {"allocate": [], "preferred": []}  # client start (mono ns) of every timed call
 
         def timed(kind, method, req):
-            starts, lat, _, _ = self.h2.bench_unary_ts(method, req, 1)
+            starts, lat = self.h2.bench_unary_ts(method, req, 1)[:2]
             self.starts[kind].append(starts[0])
             return lat[0]
         self.allocate = lambda: timed("allocate", v1beta1.METHOD_ALLOCATE, self.alloc)

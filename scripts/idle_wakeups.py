@@ -120,7 +120,7 @@ def main() -> int:
         second = h2.bench_unary_ts(v1beta1.METHOD_ALLOCATE, req, 1)
         trace = bench.read_call_trace(os.path.join(workdir, "calltrace-%s.bin" % reg.resource_name.split("/")[-1]))
         calls = {}
-        for label, (starts, lats, _, _) in (("first_after_idle", first), ("one_second_later", second)):
+        for label, (starts, lats) in (("first_after_idle", first[:2]), ("one_second_later", second[:2])):
             e = bench.match_calls(starts, lats, trace, n.RPC_ALLOCATE)[0]
             seg = bench.segments(int(starts[0]), lats[0], e) if e is not None else None
             calls[label] = {"us": round(lats[0] * 1e6, 2),

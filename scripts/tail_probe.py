@@ -91,7 +91,7 @@ def run_variant(name, batches, overrides=None, pin=False, gap=True, idle_gap_s=0
             h2.bench_unary(v1beta1.METHOD_ALLOCATE, req, 2000)  # warm-up
             recs = []
             for _ in range(batches):
-                recs.append(h2.bench_unary_ts(v1beta1.METHOD_ALLOCATE, req, ALLOCS))
+                recs.append(h2.bench_unary_ts(v1beta1.METHOD_ALLOCATE, req, ALLOCS)[:4])
                 if idle_gap_s:
                     time.sleep(idle_gap_s)
                 elif gap:

@@ -52,14 +52,16 @@ PYBIND11_MODULE(_native_bench, m) {
   h2.def("bench_unary_ts",
          // Same as bench_unary, per call: (start, CLOCK_MONOTONIC ns; latency, s; the CPU the
          // client ran on when the answer arrived; involuntary context switches of the client
-         // thread during the call, read outside the timed interval) - for attributing the
+         // thread during the call, read outside the timed interval; ns from the last recv()
+         // returning to the call's end, the client's own parsing) - for attributing the
          // tail to idle gaps, CPU migrations, preemption or the server's handling (the
          // server's own per-call record: grpc.callTraceFile).
          [](H2Client& c, const std::string& path, const py::bytes& req, int n, int gap_us) {
            std::string r(req), resp, msg;
-           std::vector<int64_t> starts;
+           std::vector<int64_t> starts, tail_ns;
            std::vector<double> lat;
            std::vector<int> cpus, preempted;
+           c.set_stamp_recv(true);
            starts.reserve(static_cast<size_t>(n));
            lat.reserve(static_cast<size_t>(n));
            cpus.reserve(static_cast<size_t>(n));
@@ -73,8 +75,10 @@ PYBIND11_MODULE(_native_bench, m) {
                if (gap_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(gap_us));
                const int64_t t0 = mono_ns();
                const int st = c.unary(path, r, &resp, &msg);
-               lat.push_back((mono_ns() - t0) * 1e-9);
+               const int64_t t1 = mono_ns();
+               lat.push_back((t1 - t0) * 1e-9);
                starts.push_back(t0);
+               tail_ns.push_back(t1 - c.last_recv_ns());  // after the last recv returned
                cpus.push_back(sched_getcpu());
                getrusage(RUSAGE_THREAD, &ru);
                preempted.push_back(static_cast<int>(ru.ru_nivcsw - ivcsw));
@@ -82,7 +86,8 @@ PYBIND11_MODULE(_native_bench, m) {
                if (st != 0) throw std::runtime_error("grpc-status " + std::to_string(st) + ": " + msg);
              }
            }
-           return py::make_tuple(starts, lat, cpus, preempted);
+           c.set_stamp_recv(false);
+           return py::make_tuple(starts, lat, cpus, preempted, tail_ns);
          },
          py::arg("path"), py::arg("req"), py::arg("n"), py::arg("gap_us") = 0);
 

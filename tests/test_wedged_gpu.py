@@ -273,14 +273,34 @@ def test_devices_indices_wait_for_gpus_missing_at_first_discovery(make_cfg, plug
         be.set_gpu_present(3, True)  # GPU 1 still missing
         assert _wait(lambda: [g.uuid for g in m.gpus] == [uuids[0], uuids[2]], 5), [g.uuid for g in m.gpus]
         k.wait_for_registrations(1, timeout=5)
+        # a pod holds GPU 2 (kubelet's device checkpoint names its device)
+        dev2 = [d.id for p in m.plugins for d in p.devices() if d.gpu == 1][0]
+        _write_checkpoint(plugin_dir, [("amd.com/gpu", [dev2])])
         be.set_gpu_present(1, True)  # now it shows up, ranking 1 by BDF: GPU 2 keeps index 1
         assert _wait(lambda: m.counters.get("devices_index_conflicts", 0) == 1, 5)
         assert [g.uuid for g in m.gpus] == [uuids[0], uuids[2]]
+        # the pod goes: the late GPU takes its index back
+        _write_checkpoint(plugin_dir, [])
+        assert _wait(lambda: [g.uuid for g in m.gpus] == [uuids[0], uuids[1]], 5), [g.uuid for g in m.gpus]
+        assert m.counters.get("devices_index_reresolved") == 1
         # and a GPU that drops off the bus leaves its index empty (no neighbour moves in)
         be.set_gpu_present(0, False)
-        assert _wait(lambda: [g.uuid for g in m.gpus] == [uuids[2]], 5), [g.uuid for g in m.gpus]
+        assert _wait(lambda: [g.uuid for g in m.gpus] == [uuids[1]], 5), [g.uuid for g in m.gpus]
         time.sleep(0.3)
-        assert [g.uuid for g in m.gpus] == [uuids[2]]
+        assert [g.uuid for g in m.gpus] == [uuids[1]]
+
+
+def _write_checkpoint(plugin_dir, entries):
+    """kubelet's device-manager checkpoint: [(resource, [device ids])], one pod each."""
+    import json
+    data = {"Data": {"PodDeviceEntries": [{"PodUID": "pod-%d" % i, "ContainerName": "c", "ResourceName": res,
+                                           "DeviceIDs": {"-1": ids}, "AllocResp": ""}
+                                          for i, (res, ids) in enumerate(entries)],
+                     "RegisteredDevices": {}}, "Checksum": 0}
+    path = os.path.join(plugin_dir, "kubelet_internal_checkpoint")
+    with open(path + ".tmp", "w") as f:
+        json.dump(data, f)
+    os.replace(path + ".tmp", path)
 
 
 def test_sampler_refused_by_a_lane_stuck_in_discovery_shows_the_gpu_down(n):
