@@ -428,10 +428,18 @@ def _placement_stats(batches, trace, topo_cpus: dict, rpc_allocate: int) -> dict
     topo = cpu_topology(sorted(set(cpus) | {int(e["cpu"]) for e in matched if e is not None}))
     topo_cpus.update(topo)
     by = collections.defaultdict(list)
+    pairs = collections.defaultdict(list)
     for x, c, e in zip(lats, cpus, matched):
         if e is not None:
             by[cpu_relation(c, int(e["cpu"]), topo)].append(x)
-    return {rel: {"calls": len(v), "p50_us": round(_pct(v, 0.5) * 1e6, 2)} for rel, v in sorted(by.items())}
+            pairs[(c, int(e["cpu"]))].append(x)
+    out = {rel: {"calls": len(v), "p50_us": round(_pct(v, 0.5) * 1e6, 2)} for rel, v in sorted(by.items())}
+    # the (client CPU, worker CPU) pairs the calls ran on, busiest first, and each batch's p50
+    out["pairs"] = [{"client": c, "worker": w, "relation": cpu_relation(c, w, topo), "calls": len(v),
+                     "p50_us": round(_pct(v, 0.5) * 1e6, 2)}
+                    for (c, w), v in sorted(pairs.items(), key=lambda kv: -len(kv[1]))[:6]]
+    out["batch_p50_us"] = [round(_pct(list(b[1]), 0.5) * 1e6, 2) for b in batches]
+    return out
 
 
 def _server_mean(text: str, rpc: str):

@@ -106,9 +106,15 @@ FAMILIES = (
            "kubelet RPC latency (5 us .. 1 s buckets)"),
     Family("amdgpu_device_plugin_events_total", "counter", ("event",), "manager",
            "Lifecycle events: restarts (api/kubelet/retry), registrations, load failures, health events; "
-           "reloads and `table_swaps` (hitless reloads), `resets_observed` (GPU resets seen by polling the "
-           "firmware clock), `latches_restored`, `state_writes` / `state_write_errors` (`health.stateFile`), "
-           "start-up canary runs and skips, `reregistrations_stream_lost` (kubelet ended a ListAndWatch stream)"),
+           "reloads and `table_swaps` (hitless reloads), `resets_observed` (GPU resets seen by polling: the "
+           "kernel's reset count, a confirmed firmware clock restart, a UE counter started over), "
+           "`reset_candidates` (back from a telemetry outage with no reset confirmed), `latches_cleared_verified` "
+           "(a candidate the recovery canary passed), `health_clears` (`GET /health/clear`), `fw_clock_glitches` "
+           "(firmware clock readings that went back without being a restart), `latches_restored`, `state_writes` "
+           "/ `state_write_errors` (`health.stateFile`), start-up canary runs and skips, "
+           "`reregistrations_stream_lost` (kubelet ended a ListAndWatch stream), `reregistrations_restart` (a "
+           "`/restart` registered a kept plugin again), `stream_watch_socket_taken` (another instance bound the "
+           "socket path), `devices_index_conflicts` / `devices_index_reresolved`"),
     Family("amdgpu_device_plugin_devices", "gauge", ("resource", "health"), "manager",
            "Advertised devices per resource and health"),
     Family("amdgpu_device_plugin_registered", "gauge", ("resource",), "manager",

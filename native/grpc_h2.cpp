@@ -619,17 +619,30 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
   uint16_t last_cpu = 0xFFFF;  // CPU of the worker's previous work
   // Each worker writes its own slice of the ring with its own counter: one shared counter
   // was a cache line every traced call of every worker wrote (N ranks -> N cores)
-  std::vector<std::pair<uint64_t, uint32_t>> trace_pending;  // (slot, seq) awaiting the send
+  // Records are filled at dispatch and written to the ring after the response's send(),
+  // like the histogram observations below: nothing the bench's attribution needs sits on
+  // the request's critical path (a ring slot is a cache line missed once per lap)
+  std::vector<std::pair<uint64_t, CallTraceEntry>> trace_pending;  // (slot, record) awaiting the send
   const uint64_t trace_slice = trace_ ? std::max<uint64_t>(1, trace_hdr_->capacity / std::max(1, nthreads_)) : 1;
   const uint64_t trace_base = trace_ ? (static_cast<uint64_t>(w->index) * trace_slice) % trace_hdr_->capacity : 0;
   uint64_t trace_next = 0;
   auto stamp_sent = [&] {
     const int64_t t = mono_ns();
-    for (const auto& ps : trace_pending) {
-      CallTraceEntry& e = trace_[ps.first];
-      if (e.seq == ps.second) e.t_sent = t;
+    for (auto& ps : trace_pending) {
+      ps.second.t_sent = t;
+      trace_[ps.first] = ps.second;
     }
     trace_pending.clear();
+  };
+  struct PendingObs {
+    int rpc;
+    double dt;
+    bool err;
+  };
+  std::vector<PendingObs> pending_obs;  // RPC histogram observations, applied after the send
+  auto apply_observes = [&] {
+    for (const auto& o : pending_obs) table->observe(o.rpc, o.dt, o.err);
+    pending_obs.clear();
   };
   auto push_law = [&](Conn* c) {
     const uint64_t v = table->version();
@@ -646,7 +659,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
   };
   // the keep-warm connection's requests are not kubelet's: no counter or histogram sees them
   auto observe = [&](const Conn& c, int rpc, double dt, bool err) {
-    if (!c.internal) table->observe(rpc, dt, err);
+    if (!c.internal) pending_obs.push_back({rpc, dt, err});
   };
   auto dispatch = [&](Conn& c, uint32_t sid, Stream& s, std::string_view body) {
     if (s.dispatched) {  // END_STREAM seen twice (trailers or DATA after the request)
@@ -664,7 +677,8 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
     if (trace_ && !c.internal && m != kMLaw && m != kMPreStart) {
       const uint64_t idx = trace_next++;
       const uint64_t slot = trace_base + idx % trace_slice;
-      CallTraceEntry& e = trace_[slot];
+      trace_pending.emplace_back(slot, CallTraceEntry{});
+      CallTraceEntry& e = trace_pending.back().second;
       e.t_ready = wake_ts;
       e.t_dispatch = t0;
       e.t_sent = 0;
@@ -679,7 +693,6 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
       e.prev_cpu = last_cpu;
       last_cpu = e.cpu;
       e.seq = static_cast<uint32_t>(idx + 1);
-      trace_pending.emplace_back(slot, e.seq);
     }
     if (m == kMUnknown) {
       send_error(c, sid, s, 12, "unknown method " + s.path);  // UNIMPLEMENTED
@@ -1177,6 +1190,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
       wake_spin = polling;
     }
     bool law_tick = false;
+    bool got_input = false;  // this event carried input: (re)open the busy-poll window after the send
     for (int i = 0; i < n; ++i) {
       const int fd = evs[i].data.fd;
       if (fd == w->efd) {
@@ -1300,6 +1314,17 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
         }
         if (trace_) recv_done = mono_ns();
         if (!process(*c)) c->closing = true;
+        got_input = true;
+      }
+      if (c->out.size() - c->out_off > kMaxPendingOut) {  // e.g. a PING flood that is never read
+        close_conn(fd);
+        continue;
+      }
+      const bool alive = flush(c);  // the response goes out first; the bookkeeping follows
+      if (!trace_pending.empty()) stamp_sent();
+      if (!pending_obs.empty()) apply_observes();
+      if (got_input) {
+        got_input = false;
         const int64_t window = admitting ? std::max(spin_ns, admission_ns) : spin_ns;
         if (window > 0) {
           const int64_t now = mono_ns();
@@ -1314,15 +1339,10 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
         }
         admitting = false;
       }
-      if (c->out.size() - c->out_off > kMaxPendingOut) {  // e.g. a PING flood that is never read
-        close_conn(fd);
-        continue;
-      }
-      const bool alive = flush(c);
-      if (!trace_pending.empty()) stamp_sent();
       if (!alive) continue;
       if (peer_closed) close_conn(fd);
     }
+    if (!pending_obs.empty()) apply_observes();  // (a connection closed before its flush)
     // ListAndWatch: push on notify() and on any version change seen by the poll tick
     const uint64_t v = table->version();
     if (law_tick || v != seen_version) {

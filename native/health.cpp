@@ -360,6 +360,7 @@ void HealthMonitor::on_sample(int gpu, bool ok, const GpuSample& s) {
       //    process saw ticking for two, for two intervals otherwise: a frozen, garbage or
       //    one-off reading never clears a latch.
       bool jump_dropped = false;
+      bool too_close = false;
       if (s.fw_clock_s >= 0) {
         const double fw_boot = now_b - s.fw_clock_s;
         if (st.fw_clock >= 0 && s.fw_clock_s + 1.0 < st.fw_clock) {
@@ -378,7 +379,10 @@ void HealthMonitor::on_sample(int gpu, bool ok, const GpuSample& s) {
           st.fw_advancing = false;
         } else if (st.fw_clock >= 0) {
           const double dt = now_b - st.fw_read_at, dc = s.fw_clock_s - st.fw_clock;
-          if (dt >= 0.05) {  // (two readings closer than that say nothing about the rate)
+          // two readings closer than 20 ms say nothing about the rate: this one is skipped
+          // and the next is compared with the previous one (never with an unjudged reading)
+          too_close = dt < 0.02;
+          if (!too_close) {
             if (dc > 0 && dc / dt > 0.5 && dc / dt < 2.0) {
               ++st.fw_adv_n;
               st.fw_advancing = true;
@@ -397,8 +401,10 @@ void HealthMonitor::on_sample(int gpu, bool ok, const GpuSample& s) {
             }
           }
         }
-        st.fw_clock = s.fw_clock_s;
-        st.fw_read_at = now_b;
+        if (!too_close) {
+          st.fw_clock = s.fw_clock_s;
+          st.fw_read_at = now_b;
+        }
         if (st.fw_advancing) st.fw_boot = fw_boot;
         // a latch from a previous process: did the firmware start after it was recorded?
         // Judged once this process has seen the clock tick (a frozen clock never is).
