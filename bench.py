@@ -98,7 +98,7 @@ def _wait_http(port: int, timeout: float) -> None:
 
 TRACE_DTYPE = [("t_ready", "<i8"), ("t_dispatch", "<i8"), ("t_sent", "<i8"), ("conn", "<u8"), ("idle_ns", "<i8"),
                ("seq", "<u4"), ("method", "u1"), ("spinning", "u1"), ("cpu", "<u2"), ("prev_cpu", "<u2"),
-               ("pad0", "<u2"), ("recv_ns", "<u4")]  # native/grpc_h2.h CallTraceEntry (56 bytes)
+               ("handle_ns", "<u2"), ("recv_ns", "<u4")]  # native/grpc_h2.h CallTraceEntry (56 bytes)
 
 
 def read_call_trace(path: str):
@@ -192,13 +192,16 @@ def _tail_stats(batches, trace=None, rpc_allocate: int = 3) -> dict:
             rp = [int(e["t_dispatch"]) - int(e["t_ready"]) for e in matched if e is not None]
             hs = [int(e["t_sent"]) - int(e["t_dispatch"]) for e in matched if e is not None]
             rv = [int(e["recv_ns"]) for e in matched if e is not None]
+            hd = [int(e["handle_ns"]) for e in matched if e is not None]
             tails = [int(t) for b in batches if len(b) > 4 for t in b[4]]
             if tails:  # outbound = the client's wake-up and recv (kernel) + its own parsing after it
                 out["outbound_split_p50_us"] = {"client_parse": round(float(np.median(tails)) / 1e3, 2)}
             out["server_split_p50_us"] = {"recv_parse": round(float(np.median(rp)) / 1e3, 2),
                                           "recv": round(float(np.median(rv)) / 1e3, 2),
                                           "parse": round(float(np.median([a - b for a, b in zip(rp, rv)])) / 1e3, 2),
-                                          "handle_send": round(float(np.median(hs)) / 1e3, 2)}
+                                          "handle_send": round(float(np.median(hs)) / 1e3, 2),
+                                          "handle": round(float(np.median(hd)) / 1e3, 2),
+                                          "send": round(float(np.median([a - b for a, b in zip(hs, hd)])) / 1e3, 2)}
     causes = collections.Counter()
     excess = collections.defaultdict(list)
     slowest = []  # (latency s, cause, [inbound, server, outbound] us, worker was polling)
@@ -415,6 +418,49 @@ def paired_floor(h2, nb, method: str, req: bytes, sizes, rounds: int = 16, batch
             "ratio_median": round(statistics.median(ratios), 3), "ratio_ci95": [round(lo, 3), round(hi, 3)]}
 
 
+def _proc_stat_busy() -> dict:
+    """cpu -> (busy jiffies, total jiffies) from /proc/stat."""
+    out = {}
+    with open("/proc/stat") as f:
+        for line in f:
+            if not line.startswith("cpu") or line.startswith("cpu "):
+                continue
+            parts = line.split()
+            vals = [int(x) for x in parts[1:]]
+            idle = vals[3] + (vals[4] if len(vals) > 4 else 0)
+            out[int(parts[0][3:])] = (sum(vals) - idle, sum(vals))
+    return out
+
+
+def _busy_study(batches, trace, busy_log, rpc_allocate: int) -> list:
+    """Per timed batch: its p50, the client's and the worker's CPU, and how busy each of
+    those and their SMT siblings were during the batch (fraction of jiffies)."""
+    if not busy_log or trace is None:
+        return []
+    topo = cpu_topology(sorted(os.sched_getaffinity(0)))
+    rows = []
+    for b, (s0, s1) in zip(batches, busy_log):
+        m = match_calls([int(x) for x in b[0]], list(b[1]), trace, rpc_allocate)
+        workers = collections.Counter(int(e["cpu"]) for e in m if e is not None)
+        clients = collections.Counter(b[2])
+        if not workers or not clients:
+            continue
+        c, w = clients.most_common(1)[0][0], workers.most_common(1)[0][0]
+
+        def frac(cpu):
+            if cpu not in s0 or cpu not in s1 or s1[cpu][1] == s0[cpu][1]:
+                return None
+            return round((s1[cpu][0] - s0[cpu][0]) / (s1[cpu][1] - s0[cpu][1]), 2)
+
+        def sib(cpu):
+            t = topo.get(cpu)
+            return [x for x in (t["smt"] if t and t["smt"] else []) if x != cpu]
+        rows.append({"p50_us": round(_pct(list(b[1]), 0.5) * 1e6, 2), "client": c, "worker": w,
+                     "relation": cpu_relation(c, w, topo), "client_busy": frac(c), "worker_busy": frac(w),
+                     "client_sibling_busy": [frac(x) for x in sib(c)], "worker_sibling_busy": [frac(x) for x in sib(w)]})
+    return rows
+
+
 def _placement_stats(batches, trace, topo_cpus: dict, rpc_allocate: int) -> dict:
     """Allocate latency by where the daemon's worker ran relative to the client (the
     worker's CPU is in its call-trace record, the client's in bench_unary_ts)."""
@@ -602,6 +648,9 @@ def main() -> int:
     ap.add_argument("--fixture", default="", help="fixture node model of a fixture daemon (default: <N>gpu_spx)")
     ap.add_argument("--daemon-config", default="",
                     help='JSON config sections merged over the daemon\'s (A/B runs), e.g. {"grpc": {"keepWarmMs": 0}}')
+    ap.add_argument("--diag-cpu-busy", action="store_true",
+                    help="diagnostics: read /proc/stat around every compiled-client Allocate batch and report how "
+                         "busy the client's and the worker's CPUs and their SMT siblings were (placement study)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -720,7 +769,10 @@ def main() -> int:
     def step(rec):
         a, p, s, an, pn, tl = rec
         phase_sync()
+        busy0 = _proc_stat_busy() if args.diag_cpu_busy else None
         starts, lat, cpus, pre, tail = h2.bench_unary_ts(v1beta1.METHOD_ALLOCATE, alloc_req, ALLOCS)
+        if busy0 is not None:
+            busy_log.append((busy0, _proc_stat_busy()))
         an.extend(lat)
         tl.append((starts, lat, cpus, pre, tail))
         pn.extend(h2.bench_unary(v1beta1.METHOD_GET_PREFERRED, pref_req, PREFS))
@@ -739,9 +791,11 @@ def main() -> int:
         s.extend(r["latencies_s"])
         return r["elapsed_s"], r["bytes"] // max(1, r["ok"])
 
+    busy_log = []  # --diag-cpu-busy: (/proc/stat before, after) per timed batch
     junk = ([], [], [], [], [], [])
     for _ in range(args.warmup):
         step(junk)
+    busy_log.clear()
     barrier()
     rec = ([], [], [], [], [], [])
     scrape_time, body_len = 0.0, len(body)
@@ -761,6 +815,8 @@ def main() -> int:
     # where the client and the daemon's worker ran, per call, and what the host is (untimed)
     topo_cpus = {}
     mine["placement"] = _placement_stats(rec[5], trace, topo_cpus, n.RPC_ALLOCATE)
+    if args.diag_cpu_busy:
+        mine["placement"]["batch_cpu_busy"] = _busy_study(rec[5], trace, busy_log, n.RPC_ALLOCATE)
     client_cpus = collections.Counter(c for b in rec[5] for c in b[2])
     client_cpu = client_cpus.most_common(1)[0][0] if client_cpus else os.sched_getcpu()
     worker_cpus = collections.Counter(int(c) for c in trace["cpu"]) if trace is not None and len(trace) else {}
@@ -786,6 +842,7 @@ def main() -> int:
     bf = nb.uds_pingpong_batched(args.steps, ALLOCS, int(SCRAPE_S * 1e6), *sizes,
                                  server_poll_us=args.busy_poll_us if args.busy_poll_us is not None else 50)
     mine["uds_floor_batched"] = (_pct(bf, 0.5), _pct(bf, 0.99), _pct(bf, 0.999), max(bf))
+    mine["uds_floor_batched_batch_p50"] = [round(_pct(bf[i:i + ALLOCS], 0.5) * 1e6, 2) for i in range(0, len(bf), ALLOCS)]
     # Allocate against the spin floor paired in time: batches of each alternate, so a busy
     # moment on the shared host lands on both (the floor above runs after the timed loop)
     mine["paired"] = paired_floor(h2, nb, v1beta1.METHOD_ALLOCATE, alloc_req, sizes)
@@ -858,6 +915,9 @@ def main() -> int:
             "uds_roundtrip_floor_batched_us": [round(x * 1e6, 2) for x in gathered[0]["uds_floor_batched"]],
             # Allocate and the spin floor in alternating batches after the timed loop (rank 0)
             "allocate_vs_spin_floor_paired": gathered[0].get("paired"),
+            # per-batch p50 of the bare exchange timed in the loop's rhythm (rank 0): a host
+            # whose batches fall into a slow mode shows it here too
+            "uds_floor_batched_batch_p50_us": gathered[0].get("uds_floor_batched_batch_p50"),
             "preferred_allocator_8gpu_size4_p50_us": _allocator_probe(n),
             "allocate_server_mean_us": (round(gathered[0]["server_allocate_mean_s"] * 1e6, 3)
                                         if gathered[0].get("server_allocate_mean_s") else None),

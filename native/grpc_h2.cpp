@@ -626,10 +626,13 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
   const uint64_t trace_slice = trace_ ? std::max<uint64_t>(1, trace_hdr_->capacity / std::max(1, nthreads_)) : 1;
   const uint64_t trace_base = trace_ ? (static_cast<uint64_t>(w->index) * trace_slice) % trace_hdr_->capacity : 0;
   uint64_t trace_next = 0;
+  int64_t send_begin = 0;  // (call trace) when the flush that carries the responses began
   auto stamp_sent = [&] {
     const int64_t t = mono_ns();
     for (auto& ps : trace_pending) {
       ps.second.t_sent = t;
+      if (send_begin > ps.second.t_dispatch)
+        ps.second.handle_ns = static_cast<uint16_t>(std::min<int64_t>(send_begin - ps.second.t_dispatch, 0xFFFF));
       trace_[ps.first] = ps.second;
     }
     trace_pending.clear();
@@ -937,6 +940,40 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
           if (off + pad > len) {
             goaway(c, kProtocolError);
             return false;
+          }
+          // Fast unary path (every kubelet unary call): a complete header block for a new
+          // stream, followed in the buffer by the stream's one DATA frame with END_STREAM.
+          // Decoded and dispatched in place from the frames, on a stack Stream that enters
+          // the stream map only if it outlives the call (flow-controlled response,
+          // ListAndWatch, an asynchronous PreStartContainer).
+          if ((flags & (kEndHeaders | kEndStream)) == kEndHeaders && !c.cont_sid && (sid & 1) && sid > c.last_sid &&
+              c.streams.size() < kMaxStreams && c.in.size() - pos >= 9) {
+            const uint8_t* dh = reinterpret_cast<const uint8_t*>(c.in.data() + pos);
+            const uint32_t dlen = (static_cast<uint32_t>(dh[0]) << 16) | (static_cast<uint32_t>(dh[1]) << 8) | dh[2];
+            if (dh[3] == kData && (dh[4] & (kEndStream | kPadded)) == kEndStream && (get_u32(dh + 5) & 0x7FFFFFFFu) == sid &&
+                dlen <= kMaxFrame && c.in.size() - pos >= 9 + dlen) {
+              PathSink ps;
+              if (!c.dec.decode(p + off, len - off - pad, on_header, &ps)) {
+                goaway(c, kCompressionError);
+                return false;
+              }
+              c.last_sid = sid;
+              Stream s;
+              s.send_window = c.peer_init_window;
+              s.method = ps.method;
+              s.path = std::move(ps.unknown);
+              s.headers_done = true;
+              const char* body = reinterpret_cast<const char*>(dh + 9);
+              pos += 9 + dlen;
+              c.recv_unacked += dlen;
+              dispatch(c, sid, s, std::string_view(body, dlen));
+              if (!s.done || !s.pend.empty()) c.streams.emplace(sid, std::move(s));
+              if (c.recv_unacked > kLocalWindow / 2) {
+                window_update(&c.out, 0, static_cast<uint32_t>(c.recv_unacked));
+                c.recv_unacked = 0;
+              }
+              break;
+            }
           }
           c.hblock.assign(reinterpret_cast<const char*>(p + off), len - off - pad);
           if (flags & kEndHeaders) {
@@ -1320,6 +1357,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
         close_conn(fd);
         continue;
       }
+      if (!trace_pending.empty()) send_begin = mono_ns();
       const bool alive = flush(c);  // the response goes out first; the bookkeeping follows
       if (!trace_pending.empty()) stamp_sent();
       if (!pending_obs.empty()) apply_observes();

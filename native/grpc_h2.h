@@ -43,7 +43,7 @@ struct CallTraceEntry {
   uint8_t spinning = 0;    // 1: the worker was polling (busy-poll window), 0: it slept in epoll_wait
   uint16_t cpu = 0;        // CPU the worker ran on at dispatch
   uint16_t prev_cpu = 0;   // CPU of the worker's previous work (0xFFFF: none yet)
-  uint16_t pad0 = 0;
+  uint16_t handle_ns = 0;  // t_dispatch -> the response's send() began (capped at 65535)
   uint32_t recv_ns = 0;    // t_ready -> the connection's recv() returned (the rest to t_dispatch is parsing)
 };
 static_assert(sizeof(CallTraceEntry) == 56, "trace record layout is read by bench.py");
