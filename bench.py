@@ -836,6 +836,9 @@ def main() -> int:
     mine["uds_floor_spin_p50"] = _pct(spin, 0.5)
     mine["uds_floor_spin_p99"] = _pct(spin, 0.99)
     mine["uds_floor_spin_p999"] = _pct(spin, 0.999)
+    # ... and with the server consuming each request only after its answer (MSG_PEEK, the
+    # daemon's grpc.peekReads): the bare exchange without the client's spurious wake-up
+    mine["uds_floor_spin_peek_p50"] = _pct(nb.uds_pingpong(10000, 500, *sizes, server_spin=True, peek=True), 0.5)
     # ... and in the timed loop's own rhythm (batches of ALLOCS back-to-back exchanges, a
     # scrape phase apart) against a server with the plugin worker's polling policy: this
     # host's tail for that pattern, which Allocate's p99 / p99.9 are compared against
@@ -926,6 +929,7 @@ def main() -> int:
             "dist_backend": (dist.get_backend() if world > 1 else None),
             "uds_roundtrip_floor_p50_us": round(gathered[0]["uds_floor_p50"] * 1e6, 2),
             "uds_roundtrip_floor_spin_p50_us": round(gathered[0]["uds_floor_spin_p50"] * 1e6, 2),
+            "uds_roundtrip_floor_spin_peek_p50_us": round(gathered[0]["uds_floor_spin_peek_p50"] * 1e6, 2),
             "uds_roundtrip_floor_cold_p50_us": round(gathered[0]["uds_floor_cold_p50"] * 1e6, 2),
             "allocate_cold_p50_us": round(_pct([x for g in gathered for x in g["alloc_cold"]], 0.5) * 1e6, 2),
             "allocate_admission_p50_us": round(_pct([x for g in gathered for x in g["alloc_admission"]], 0.5) * 1e6, 2),

@@ -156,6 +156,12 @@ class GrpcConfig:
     # kubelet RPC (0 = always).  Outside this admission window the workers sleep: an idle
     # node pays ~1 wake-up per worker every 5 s for the plugin's gRPC server
     activeWindowMs: int = 10000
+    # native server: read requests with MSG_PEEK and consume them after the answer is sent
+    # (consuming the client's data wakes a client blocked in recv() for nothing).  Off: on
+    # the MI355X box the deferred wake-up only moved into send() and the client then woke
+    # from a deeper idle state - recv 0.21 vs 0.70 us, but send 0.85 vs 0.34 us and Allocate
+    # p50 2.8-3.5 vs 2.55 us (profiles/r6/ab_peek_*.json)
+    peekReads: bool = False
     keepWarmFull: bool = True    # ... through the whole request path of an in-memory connection (else HPACK + table)
     # native server: per-call trace of unary RPCs in a file-backed ring ("" = off), read by
     # bench.py to attribute slow calls; one record per call, callTraceEntries records

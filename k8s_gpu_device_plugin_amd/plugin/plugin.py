@@ -317,6 +317,7 @@ class AmdDevicePlugin:
             srv.set_keep_warm_full(bool(self.cfg.grpc.keepWarmFull))
             srv.set_idle_wake_ms(int(self.cfg.grpc.idleWakeMs))
             srv.set_active_window_ms(int(self.cfg.grpc.activeWindowMs))
+            srv.set_peek_reads(bool(self.cfg.grpc.peekReads))
             if self.cfg.grpc.callTraceFile:
                 srv.set_call_trace(self.cfg.grpc.callTraceFile.replace("{resource}", self.resource.get_resource_name()),
                                    int(self.cfg.grpc.callTraceEntries))

@@ -218,6 +218,14 @@ struct GrpcServer::Worker {
     bool closing = false;
     bool want_out = false;
     bool internal = false;  // the keep-warm tick's private connection: no fd, no accounting
+    // grpc.peekReads: requests are read with MSG_PEEK (SO_PEEK_OFF advances over what was
+    // read) and consumed only after the answers went out.  Consuming the client's data runs
+    // its socket's write-space callback, which wakes a client blocked in recv() on that
+    // socket (one wait queue for both directions) for nothing.  Measured on the MI355X box
+    // the early wake-up pays for itself: it keeps the client's CPU out of deeper idle states
+    // for the real one, so this is off by default (docs/ROUND6.md).
+    bool peek = false;
+    size_t peeked = 0;      // bytes read by peeking, still in the socket
   };
   std::unordered_map<int, std::unique_ptr<Conn>> conns;
   // Connections are spread over the workers: the one that accepts hands a new
@@ -573,6 +581,21 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
       w->conns.emplace(fd, std::move(c));
     }
     w->incoming.clear();
+  };
+  // Drops from the socket what was read by peeking (see Conn::peek), now that the answers
+  // are out; what cannot be dropped yet stays counted and goes with the next batch.
+  auto consume_peeked = [&](Conn* c) {
+    char sink[16384];
+    while (c->peeked > 0) {
+      const ssize_t n = recv(c->fd, sink, std::min(c->peeked, sizeof(sink)), MSG_DONTWAIT);
+      if (n > 0) {
+        c->peeked -= static_cast<size_t>(n);
+      } else if (n < 0 && errno == EINTR) {
+        continue;
+      } else {
+        break;
+      }
+    }
   };
   // returns false if the connection was closed
   auto flush = [&](Conn* c) -> bool {
@@ -1290,6 +1313,11 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
           Worker* t = pick_least_loaded(workers_, w);  // this one on a tie
           auto c = std::make_unique<Conn>();
           c->fd = cfd;
+          {
+            int zero = 0;  // peek offset 0: MSG_PEEK reads advance it, consuming reads take it back
+            c->peek = peek_reads_.load(std::memory_order_relaxed) &&
+                      setsockopt(cfd, SOL_SOCKET, SO_PEEK_OFF, &zero, sizeof(zero)) == 0;
+          }
           // server preface: SETTINGS(MAX_CONCURRENT_STREAMS, INITIAL_WINDOW_SIZE) + conn window
           frame(&c->out, 12, kSettings, 0, 0);
           c->out.push_back(0);
@@ -1335,9 +1363,10 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
       bool peer_closed = false;
       if (evs[i].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP)) {
         for (;;) {
-          const ssize_t r = recv(fd, rbuf, sizeof(rbuf), 0);
+          const ssize_t r = recv(fd, rbuf, sizeof(rbuf), c->peek ? MSG_PEEK : 0);
           if (r > 0) {
             c->in.append(rbuf, static_cast<size_t>(r));
+            if (c->peek) c->peeked += static_cast<size_t>(r);
             if (static_cast<size_t>(r) < sizeof(rbuf)) break;
           } else if (r == 0) {
             peer_closed = true;
@@ -1359,6 +1388,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
       }
       if (!trace_pending.empty()) send_begin = mono_ns();
       const bool alive = flush(c);  // the response goes out first; the bookkeeping follows
+      if (alive && c->peeked) consume_peeked(c);
       if (!trace_pending.empty()) stamp_sent();
       if (!pending_obs.empty()) apply_observes();
       if (got_input) {

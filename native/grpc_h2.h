@@ -124,6 +124,9 @@ class GrpcServer {
   // and a pod admission's first call (GetPreferredAllocation) opens the window for the
   // Allocate that follows it.  (Sleeping workers wake every 5 s.)
   void set_active_window_ms(int ms) { active_window_ms_.store(ms > 0 ? ms : 0); }
+  // Requests read with MSG_PEEK and consumed after the answer is sent (applies to
+  // connections accepted from now on; off by default, grpc.peekReads).  See Worker::Conn::peek.
+  void set_peek_reads(bool on) { peek_reads_.store(on); }
   // Epoll wake-ups of the workers that found nothing to do (timeouts), all workers.
   uint64_t idle_wakeups() const { return idle_wakeups_.load(); }
   std::vector<int> worker_connections() const;  // connections owned per worker thread
@@ -160,6 +163,7 @@ class GrpcServer {
   std::atomic<bool> keep_warm_full_{true};
   std::atomic<int> idle_wake_ms_{0};
   std::atomic<int> active_window_ms_{0};
+  std::atomic<bool> peek_reads_{false};
   std::atomic<uint64_t> idle_wakeups_{0};
   std::atomic<uint64_t> warm_ticks_{0};
   // table_ and table_gen_ change together under swap_mu_ (never held across anything else);

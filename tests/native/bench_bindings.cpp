@@ -131,13 +131,13 @@ PYBIND11_MODULE(_native_bench, m) {
       py::arg("backend"), py::arg("socket_path"), py::arg("gpu"), py::arg("events") = 60);
   m.def("uds_pingpong",
         [](int n, int warmup, int req_bytes, int resp_bytes, bool server_spin, bool tcp, int gap_us, int client_cpu,
-           int server_cpu) {
+           int server_cpu, bool peek) {
           py::gil_scoped_release rel;
-          return uds_pingpong(n, warmup, req_bytes, resp_bytes, server_spin, tcp, gap_us, client_cpu, server_cpu);
+          return uds_pingpong(n, warmup, req_bytes, resp_bytes, server_spin, tcp, gap_us, client_cpu, server_cpu, peek);
         },
         py::arg("n") = 10000, py::arg("warmup") = 500, py::arg("req_bytes") = 128, py::arg("resp_bytes") = 256,
         py::arg("server_spin") = false, py::arg("tcp") = false, py::arg("gap_us") = 0, py::arg("client_cpu") = -1,
-        py::arg("server_cpu") = -1);
+        py::arg("server_cpu") = -1, py::arg("peek") = false);
   m.def("core_ghz",
         [](int64_t iters, int reps) {
           py::gil_scoped_release rel;

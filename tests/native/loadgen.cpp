@@ -267,7 +267,7 @@ double core_ghz(int64_t iters, int reps) {
 }
 
 std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_bytes, bool server_spin, bool tcp,
-                                 int gap_us, int client_cpu, int server_cpu) {
+                                 int gap_us, int client_cpu, int server_cpu, bool peek) {
   if (n < 0 || warmup < 0 || gap_us < 0 || req_bytes <= 0 || resp_bytes <= 0 || req_bytes > (1 << 20) || resp_bytes > (4 << 20))
     throw std::invalid_argument("uds_pingpong: bad sizes");
   if (client_cpu >= CPU_SETSIZE || server_cpu >= CPU_SETSIZE) throw std::invalid_argument("uds_pingpong: bad cpu");
@@ -278,6 +278,10 @@ std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_byte
   fcntl(sfd, F_SETFL, fcntl(sfd, F_GETFL) | O_NONBLOCK);
   struct timeval tv {5, 0};  // a dead server thread ends the client's recv, not the process
   setsockopt(cfd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+  if (peek) {
+    int zero = 0;
+    if (tcp || setsockopt(sfd, SOL_SOCKET, SO_PEEK_OFF, &zero, sizeof(zero)) != 0) peek = false;
+  }
   const int ep = epoll_create1(EPOLL_CLOEXEC);
   struct epoll_event ev {};
   ev.events = EPOLLIN | EPOLLRDHUP;
@@ -287,6 +291,7 @@ std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_byte
   std::thread server([&] {  // the plugin server's syscall pattern: epoll_wait, recv, send
     server_pinned.store(pin_self(server_cpu, nullptr) ? 1 : 0);
     std::vector<char> in(static_cast<size_t>(req_bytes) + 65536), out(static_cast<size_t>(resp_bytes), 'r');
+    std::vector<char> sink(65536);
     size_t have = 0;
     epoll_event evs[4];
     for (;;) {
@@ -296,10 +301,12 @@ std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_byte
       if (k < 0 && errno != EINTR) return;
       if (k <= 0) continue;
       bool closed = false;
+      size_t peeked = 0;
       for (;;) {
-        const ssize_t r = recv(sfd, in.data() + have, in.size() - have, 0);
+        const ssize_t r = recv(sfd, in.data() + have, in.size() - have, peek ? MSG_PEEK : 0);
         if (r > 0) {
           have += static_cast<size_t>(r);
+          peeked += peek ? static_cast<size_t>(r) : 0;
           if (have >= in.size()) break;
         } else if (r < 0 && errno == EINTR) {
           continue;
@@ -320,6 +327,12 @@ std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_byte
           else
             return;
         }
+      }
+      while (peeked > 0) {  // consume what was peeked, after the answer went out
+        const ssize_t r = recv(sfd, sink.data(), std::min(peeked, sink.size()), MSG_DONTWAIT);
+        if (r > 0) peeked -= static_cast<size_t>(r);
+        else if (r < 0 && errno == EINTR) continue;
+        else break;
       }
       if (closed) return;
     }

@@ -41,8 +41,12 @@ LoadResult grpc_load(const std::string& socket_path, const std::string& method, 
 // client_cpu / server_cpu >= 0 pin the two threads (the calling thread's own affinity is
 // restored afterwards): the same exchange between two chosen CPUs - SMT siblings, two
 // cores of one L3, two L3 domains - is what says what a placement costs on this host.
+// peek: the server reads each request with MSG_PEEK and consumes it after its send (the
+// plugin's grpc.peekReads): the bare exchange without the write-space wake-up of the client
+// that consuming its data causes.
 std::vector<double> uds_pingpong(int n, int warmup, int req_bytes, int resp_bytes, bool server_spin = false,
-                                 bool tcp = false, int gap_us = 0, int client_cpu = -1, int server_cpu = -1);
+                                 bool tcp = false, int gap_us = 0, int client_cpu = -1, int server_cpu = -1,
+                                 bool peek = false);
 
 // Effective core clock of the calling thread, GHz: a chain of `iters` dependent integer
 // adds (one per cycle on x86-64) timed with CLOCK_MONOTONIC; the best of `reps`.  Tells a

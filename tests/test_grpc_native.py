@@ -842,3 +842,44 @@ def test_idle_daemon_threads_sleep(n, plugin_dir, make_cfg):
         m.stop()
         t.join(10)
     assert time.monotonic() - t0 < 3.0
+
+
+def test_peek_reads_serve_every_request_once(n, plugin_dir):
+    """grpc.peekReads (opt-in): requests read with MSG_PEEK and consumed after the answer -
+    back-to-back unary calls, a request spanning many frames and reads, and a stream all
+    see exactly one answer per request and nothing replayed."""
+    tc = n.TableConfig()
+    devs = [n.TableDevice("dev-%03d" % i, i // 8, i % 8, 0, -1, ["/dev/dri/renderD%d" % (128 + i)], True)
+            for i in range(64)]
+    table = n.DeviceTable(tc, devs, n.Topology(8))
+    path = os.path.join(plugin_dir, "amd-gpu.sock")
+    srv = n.GrpcServer(path, 2)
+    srv.set_peek_reads(True)
+    srv.set_table(table)
+    srv.start()
+    try:
+        c = n.H2Client(path)
+        for i in range(300):
+            req = v1beta1.AllocateRequest(container_requests=[v1beta1.ContainerAllocateRequest(
+                devices_ids=["dev-%03d" % (i % 64)])]).SerializeToString()
+            st, body, msg = c.unary(v1beta1.METHOD_ALLOCATE, req)
+            assert st == 0, msg
+            envs = v1beta1.AllocateResponse.FromString(body).container_responses[0].envs
+            assert envs["AMD_VISIBLE_DEVICES"] == "dev-%03d" % (i % 64)
+        ids = ["dev-%03d" % (i % 64) for i in range(12000)]  # ~200 KB: many frames, several reads
+        big = v1beta1.PreferredAllocationRequest(container_requests=[v1beta1.ContainerPreferredAllocationRequest(
+            available_deviceIDs=ids, allocation_size=4)]).SerializeToString()
+        for _ in range(4):
+            st, body, msg = c.unary(v1beta1.METHOD_GET_PREFERRED, big)
+            assert st == 0, msg
+        assert srv.requests == 304
+        c.open_stream(v1beta1.METHOD_LIST_AND_WATCH, b"")
+        first = c.next_stream_message(5.0)
+        assert len(v1beta1.ListAndWatchResponse.FromString(first).devices) == 64
+        table.set_gpu_health(1, -1, False)
+        srv.notify()
+        upd = v1beta1.ListAndWatchResponse.FromString(c.next_stream_message(5.0))
+        assert sum(d.health == "Unhealthy" for d in upd.devices) == 8
+        c.close()
+    finally:
+        srv.stop()

@@ -185,6 +185,9 @@ def test_restart_api_registers_again_on_the_running_socket(make_cfg, plugin_dir,
         time.sleep(0.3)
         m.restart()  # picks up GPU 1 in CPX: two resources from here on
         assert _wait(lambda: len(m.plugins) == 2, 10)
+        # that restart: the new resource registers, the kept one registers again
+        assert _wait(lambda: len(k.requests) == 3 and m.counters.get("reregistrations_restart") == 1, 10)
+        time.sleep(0.3)
         base = len(k.requests)
         idents = {p.resource: _socket_ident(p.socket) for p in m.plugins}
         old = k.watch(regs[0].endpoint)
