@@ -227,6 +227,9 @@ class AmdSmiBackend : public Backend {
   // takes the same lock) waits for an in-flight wait to return instead of stopping
   // notification underneath it, and a re-initialisation (gate closed) never waits on it.
   bool delivers_events() const override { return evt_live_.load() && !closed_.load(); }
+  // armed (a privileged or CDI-patched pod): one wake-up a second while nothing happens;
+  // stop() waits for at most that long
+  int event_wait_ms() const override { return 1000; }
 
   int wait_events(int timeout_ms, std::vector<HwEvent>* out) override {
     amdsmi_evt_notification_data_t data[16];

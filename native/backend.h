@@ -361,6 +361,9 @@ class Backend : public std::enable_shared_from_this<Backend> {
   // Whether wait_events has anything to wait on (armed sources, a fixture's scripts).  When
   // not, the health monitor's event thread sleeps a second at a time instead of calling it.
   virtual bool delivers_events() const { return true; }
+  // How long one wait_events call may block: the event thread's stop latency and its idle
+  // wake-up rate (a backend whose wait cannot be interrupted keeps this short).
+  virtual int event_wait_ms() const { return 200; }
   // Drop cached device handles so the next discover() enumerates afresh (a compute
   // partition change creates new processors).  Returns false when not possible.
   virtual bool reinit() { return true; }

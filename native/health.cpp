@@ -95,8 +95,9 @@ void HealthMonitor::loop() {
       cv_wait_ms(cv_, lk, 5000, [&] { return stop_; });
       continue;
     }
-    // bounded wait so stop() is honoured within ~200 ms
-    backend_->wait_events(200, &evs);
+    // bounded wait so stop() is honoured: 200 ms, a second for
+    // amdsmi (an idle node then pays one wake-up a second for event delivery)
+    backend_->wait_events(backend_->event_wait_ms(), &evs);
     for (const auto& e : evs) process(e);
   }
 }
