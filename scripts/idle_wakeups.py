@@ -10,8 +10,8 @@ kubelet stub and one compiled kubelet-like connection.  Phases:
   * ``idle``: after ``--settle`` seconds without an RPC, ``--window`` seconds more.
 
 Per phase: every thread's voluntary + involuntary context switches per second (from
-/proc/<pid>/task/<tid>/status) and CPU time (utime + stime from .../stat), grouped by
-thread name, and the daemon's totals.  Then the latency the idle phase costs: the first
+/proc/<pid>/task/<tid>/status) and CPU time (.../schedstat, ns; utime + stime where the
+kernel has no schedstat), grouped by thread name, and the daemon's totals.  Then the latency the idle phase costs: the first
 Allocate after the idle phase against an Allocate 1 s later (both single calls, the
 daemon's call trace splits them; inbound is the worker's wake-up).
 
@@ -38,7 +38,8 @@ CLK_TCK = os.sysconf("SC_CLK_TCK")
 
 
 def thread_stats(pid: int) -> dict:
-    """tid -> (name, context switches, cpu seconds)."""
+    """tid -> (name, context switches, cpu seconds).  CPU time from schedstat (ns on the
+    CPU, exact) where the kernel has it, else utime + stime (10 ms ticks)."""
     out = {}
     base = "/proc/%d/task" % pid
     for tid in os.listdir(base):
@@ -52,6 +53,11 @@ def thread_stats(pid: int) -> dict:
         name = stat[stat.index("(") + 1:stat.rindex(")")]
         fields = stat[stat.rindex(")") + 2:].split()
         cpu = (int(fields[11]) + int(fields[12])) / CLK_TCK
+        try:
+            with open("%s/%s/schedstat" % (base, tid)) as f:
+                cpu = int(f.read().split()[0]) * 1e-9
+        except (OSError, ValueError, IndexError):
+            pass
         cs = 0
         for line in st.splitlines():
             if line.startswith(("voluntary_ctxt_switches", "nonvoluntary_ctxt_switches")):
