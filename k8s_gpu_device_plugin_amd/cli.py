@@ -130,12 +130,14 @@ def main(argv=None) -> int:
     rc = 0
     import os
     parent = int(os.environ.get("AMDGPU_DP_PARENT_PID") or 0)
+    poll_parent = bool(parent) and not _watch_parent(parent, reason, done)
     try:
         web.start()
         mt.start()
-        # (signals interrupt the wait; the parent check is the only reason to poll)
-        while not done.wait(0.5 if parent else 5.0):
-            if parent and os.getppid() != parent:  # the harness is gone (PDEATHSIG backstop)
+        # (signals interrupt the wait; the parent check is the only reason to poll, and
+        # only where the kernel has no pidfd to wait on)
+        while not done.wait(0.5 if poll_parent else 5.0):
+            if poll_parent and os.getppid() != parent:  # the harness is gone (PDEATHSIG backstop)
                 reason["why"] = "parent process %d exited, exiting gracefully..." % parent
                 break
     except Exception as e:
@@ -152,6 +154,31 @@ def main(argv=None) -> int:
         rc = 1
     log.info("see you next time!")
     return rc
+
+
+def _watch_parent(parent: int, reason: dict, done: threading.Event) -> bool:
+    """A thread blocked on a pidfd of the harness process that started this daemon ends
+    the daemon when that process exits: no periodic wake-up for it.  False where the
+    kernel or Python has no pidfd (the caller polls getppid instead)."""
+    import os
+    import select
+    try:
+        fd = os.pidfd_open(parent)
+    except (AttributeError, OSError):
+        return False
+
+    def wait():
+        from .utils.util import name_os_thread
+        name_os_thread("parent-watch")
+        try:
+            select.select([fd], [], [])
+        finally:
+            os.close(fd)
+        reason["why"] = reason["why"] or "parent process %d exited, exiting gracefully..." % parent
+        done.set()
+
+    threading.Thread(target=wait, name="parent-watch", daemon=True).start()
+    return True
 
 
 if __name__ == "__main__":

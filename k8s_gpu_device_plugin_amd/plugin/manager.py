@@ -43,7 +43,7 @@ from ..device import build_device_map
 from ..device.backend import make_backend
 from ..resource import new_resources
 from ..utils.log import get_logger
-from ..utils.util import CloseOnce, parse_device_selector
+from ..utils.util import CloseOnce, name_os_thread, parse_device_selector
 from ..utils.version import APP_NAME, VERSION
 from .plugin import AmdDevicePlugin, _socket_ident
 from .state import HealthState
@@ -57,10 +57,15 @@ EV_SOCKET_GONE = "socket_gone"  # a *.sock other than kubelet.sock was removed f
 EV_DISCOVERED = "discovered"  # the discovery worker finished: (purpose, gpus, topo, report, error)
 EV_START_CANARY = "start_canary"  # a start-up canary verdict: (identity, partition, ok, why)
 EV_CLEAR = "clear"  # GET /health/clear: (gpu selector, concurrent.futures.Future)
+EV_SUPERVISE = "supervise"  # a native gRPC server faulted: run the supervision pass now
 EV_CANDIDATE_VERIFIED = "candidate_verified"  # recovery canary after a reset candidate: (identity, gen, ok)
 DISCOVERY_RELOAD, DISCOVERY_CHECK = "reload", "check"  # rebuild always / only if the inventory changed
 HEALTH_LOG_LEN = 4096
 SERVER_CHECK_S = 1.0  # gRPC server supervision poll
+# ... and once every plugin is registered with kubelet's stream open and readiness holds:
+# a quiet node's manager thread wakes every 5 s (a stream that ends is timed from its end,
+# so the re-registration below is as prompt as with the 1 s poll)
+SERVER_CHECK_QUIET_S = 5.0
 # kubelet holds one ListAndWatch stream per registered plugin for the plugin's life; when
 # it ends the stream (its side failed) it drops the endpoint and waits for a new Register.
 # A plugin whose stream has been gone this long, kubelet.sock still in place, registers again
@@ -156,6 +161,7 @@ def background_thread() -> None:
     """The calling helper thread runs SCHED_BATCH (config ``backgroundSched``): it never
     preempts a gRPC worker when it wakes.  Native servers started from it switch their
     workers back to SCHED_OTHER (``foreground_thread`` in native/common.cpp)."""
+    name_os_thread()
     if native.load().background_batch():
         try:
             os.sched_setscheduler(0, os.SCHED_BATCH, os.sched_param(0))  # 0: this thread
@@ -190,6 +196,8 @@ class PluginManager:
                                     int(cfg.health.pcieDebounceSamples))
         if hasattr(self.backend, "set_reset_query"):
             self.backend.set_reset_query(bool(cfg.health.resetQuery))
+        if hasattr(self.backend, "set_ecc_event_gate"):
+            self.backend.set_ecc_event_gate(bool(cfg.health.eccEventGate))
         self.events: "queue.Queue[tuple]" = queue.Queue()
         self.plugins: list[AmdDevicePlugin] = []
         self.gpus: list = []
@@ -374,6 +382,7 @@ class PluginManager:
 
     def start(self) -> None:
         """Runs the manager loop in the calling thread until ``stop()``."""
+        name_os_thread("manager")
         os.makedirs(self.cfg.pluginDir, exist_ok=True)
         self._running.set()
         try:
@@ -432,6 +441,19 @@ class PluginManager:
             self._publish_metrics()
         return True
 
+    def _check_period(self) -> float:
+        """Seconds to the next supervision pass: SERVER_CHECK_S while anything is in flux
+        (not ready, a discovery running, a plugin unregistered or without its stream, a
+        restart's Register pending, PodResources coverage to move on), else
+        SERVER_CHECK_QUIET_S."""
+        if (self.podres is not None or not self._readiness[0] or self._register_pending is not None
+                or (self._discoverer is not None and self._discoverer.pending())):
+            return SERVER_CHECK_S
+        for p in self.plugins:
+            if len(p) and (not p.registered or not p.serving or not p.law_had or p.law_lost_since is not None):
+                return SERVER_CHECK_S
+        return SERVER_CHECK_QUIET_S
+
     def _check_stream(self, p) -> bool:
         """Re-registers a plugin whose kubelet ListAndWatch stream ended and was not
         reopened within LAW_LOST_GRACE_S (kubelet dropped the endpoint without restarting:
@@ -450,8 +472,8 @@ class PluginManager:
         if not p.law_had:
             return False  # kubelet has not opened its stream since the last Register yet
         if p.law_lost_since is None:
-            p.law_lost_since = now
-            return False
+            closed = p.list_and_watch_closed_at()  # when the stream ended (the poll may be late)
+            p.law_lost_since = closed if 0 < closed <= now else now
         if now - p.law_lost_since < LAW_LOST_GRACE_S or not os.path.exists(self.cfg.kubelet_socket):
             return False
         if _socket_ident(p.socket) != p._sock_ident:
@@ -495,7 +517,7 @@ class PluginManager:
                 if self.podres is not None:  # PodResources' coverage moves on with every poll,
                     # changed map or not (its grace keeps a just-answered Allocate counted)
                     self.recent_allocations.set_covered_until(self.podres.covered_until())
-                next_check = now + SERVER_CHECK_S
+                next_check = now + self._check_period()
             try:
                 ev = self.events.get(timeout=max(0.0, next_check - now))
             except queue.Empty:
@@ -503,6 +525,9 @@ class PluginManager:
             if ev[0] == EV_STOP:
                 log.info("plugin server stopped")
                 return
+            if ev[0] == EV_SUPERVISE:
+                next_check = 0.0
+                continue
             self._handle(ev)
 
     # ------------------------------------------------------------ persisted latches
@@ -692,8 +717,10 @@ class PluginManager:
         held = self._canary_failed | self._start_pending
         failed = {(index_of[k], p) for k, p in held if k in index_of}
         plugins = [AmdDevicePlugin(name, devs, topo, self.cfg) for name, devs in device_map.items()]
+        events = self.events  # (the hook holds the queue only: no cycle through the server)
         for p in plugins:
             p.table.set_recent_allocations(self.recent_allocations)
+            p.on_server_fault = lambda: events.put((EV_SUPERVISE,))
         if self.cfg.health.canaryOnPreStart:
             for p in plugins:
                 p.prestart_check = self._prestart_check

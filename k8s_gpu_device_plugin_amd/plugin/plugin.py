@@ -33,6 +33,7 @@ from ..api import v1beta1
 from ..device import Devices
 from ..resource import ResourceName
 from ..utils.log import get_logger
+from ..utils.util import name_os_thread
 
 log = get_logger("plugin")
 
@@ -149,6 +150,9 @@ class AmdDevicePlugin:
         self._sock_ident = None  # (st_dev, st_ino) of the socket file this plugin bound
         # PreStartContainer verifier: fn(device ids) -> "" (pass) or an error message
         self.prestart_check = None
+        # called (on a native worker thread) when the native server faults: the manager
+        # supervises at once; must not hold this plugin (the server would keep it alive)
+        self.on_server_fault = None
         self._prestart_thread: threading.Thread | None = None
         self._prestart_pool: concurrent.futures.ThreadPoolExecutor | None = None
         self._retiring = False  # a successor took the server over (adopt)
@@ -157,7 +161,7 @@ class AmdDevicePlugin:
         self._front = [self]
         # ListAndWatch streams open on the grpcio server (the native server counts its own);
         # shared with a successor that adopts the server, like _front
-        self._law = [0]
+        self._law = [0, 0.0]  # [open streams, time.monotonic() when one last ended]
         # stream watchdog (PluginManager._check_stream): kubelet opened a stream since the
         # last Register, and since when none is open
         self.law_had = False
@@ -187,8 +191,9 @@ class AmdDevicePlugin:
     def _prestart_loop(self) -> None:
         """Pops PreStartContainer jobs from the table (either server enqueues them) and
         runs the verifier off the server threads; several containers verify in parallel."""
+        name_os_thread("prestart")
         while not self._stopping:
-            for job_id, ids in self.table.pop_prestart(200):
+            for job_id, ids in self.table.pop_prestart(5000):  # (a job or stop() wakes it)
                 self._prestart_pool.submit(self._run_prestart, job_id, ids)
             if self._retiring and self.table.prestart_pending == 0:
                 # a successor serves now and every check queued here has been answered
@@ -268,6 +273,7 @@ class AmdDevicePlugin:
             server.stop(grace=0.5).wait(2.0)
         if nserver is not None:
             nserver.stop()
+            nserver.set_failure_hook(None)
         if was_serving:
             log.info("Stopped serving", extra={"resourceName": str(self.resource), "socket": self.socket})
         _remove_if_ours(self.socket, self._sock_ident)
@@ -312,6 +318,8 @@ class AmdDevicePlugin:
                            self.cfg.grpc.busyPollUs if self.cfg is not None else 0,
                            self.cfg.grpc.admissionPollUs if self.cfg is not None else 0)
         srv.set_table(self.table)
+        if self.on_server_fault is not None:
+            srv.set_failure_hook(self.on_server_fault)
         if self.cfg is not None:
             srv.set_keep_warm_ms(int(self.cfg.grpc.keepWarmMs))
             srv.set_keep_warm_full(bool(self.cfg.grpc.keepWarmFull))
@@ -379,6 +387,7 @@ class AmdDevicePlugin:
         an unexpected termination restarts the server, >5 crashes within an hour is fatal.
         One thread per server: it acts for whichever plugin serves from it now (a
         successor that adopted the server is ``_front[0]``)."""
+        name_os_thread("grpcio-sup")
         front = self._front
         while True:
             server.wait_for_termination()
@@ -412,6 +421,13 @@ class AmdDevicePlugin:
             return srv.list_and_watch_streams()
         return self._law[0] if self._serving else 0
 
+    def list_and_watch_closed_at(self) -> float:
+        """time.monotonic() when a ListAndWatch stream of this server last ended (0: none)."""
+        srv = self._native_server
+        if srv is not None:
+            return srv.list_and_watch_closed_at()
+        return self._law[1]
+
     def register(self) -> None:
         """Registration.Register with kubelet (``plugin/plugin.go:139-162``).  Sent by the
         compiled HTTP/2 client when the native module has one (no grpcio import, no
@@ -423,11 +439,19 @@ class AmdDevicePlugin:
         n = native.load()
         if hasattr(n, "H2Client"):
             req = v1beta1.encode_register_request(os.path.basename(self.socket), str(self.resource), pre_start)
-            c = n.H2Client(self.kubelet_socket, DIAL_TIMEOUT_S)
-            try:
-                status, _, message = c.unary(v1beta1.METHOD_REGISTER, req)
-            finally:
-                c.close()
+            for attempt in (0, 1):
+                c = n.H2Client(self.kubelet_socket, DIAL_TIMEOUT_S)
+                try:
+                    status, _, message = c.unary(v1beta1.METHOD_REGISTER, req)
+                    break
+                except RuntimeError as e:
+                    # a GOAWAY that left the request unprocessed (kubelet's server going
+                    # away under it): safe to send once more on a new connection
+                    if attempt or "GOAWAY" not in str(e):
+                        raise
+                    log.info("Register with kubelet: %s; sending it again", e)
+                finally:
+                    c.close()
             if status != 0:
                 raise RuntimeError("Register with kubelet failed: grpc-status %d %s" % (status, message))
             self.registered, self.registered_at = True, time.monotonic()
@@ -550,6 +574,7 @@ class AmdDevicePlugin:
             finally:
                 with law_lock:
                     law[0] -= 1
+                    law[1] = time.monotonic()
 
         def _list_and_watch(ctx):
             plugin = front[0]

@@ -32,6 +32,24 @@ class CloseOnce:
         return self._ev.wait(timeout)
 
 
+_libc = None
+
+
+def name_os_thread(name: str | None = None) -> None:
+    """Gives the calling thread its Python name at the OS level too (``py-<name>``, 15
+    bytes at most), so ``top -H`` and /proc/<pid>/task/*/comm tell the daemon's Python
+    threads apart like its native ones (``dpgrpc-N``, ``dpsampler``, ...)."""
+    global _libc
+    try:
+        import ctypes
+        if _libc is None:
+            _libc = ctypes.CDLL(None, use_errno=True)
+        comm = ("py-" + (name or threading.current_thread().name)).encode()[:15]
+        _libc.prctl(15, ctypes.c_char_p(comm), 0, 0, 0)  # PR_SET_NAME
+    except Exception:
+        pass
+
+
 def new_id() -> str:
     """Random identifier (reference ``util.NewID``, uuid4 without dashes)."""
     return uuid.uuid4().hex

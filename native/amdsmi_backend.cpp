@@ -8,8 +8,14 @@
 // a call wedged in the driver stalls that GPU only; the library session is guarded by a
 // gate that a re-initialisation closes (SURVEY.md §7.5 hard part 6).
 #include <amd_smi/amdsmi.h>
+#include <dirent.h>
+#include <fcntl.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <cctype>
+#include <cerrno>
+#include <cstdlib>
 #include <atomic>
 #include <cmath>
 #include <ctime>
@@ -37,6 +43,35 @@ int g_init_refs = 0;
 // Probe-only callers pass keep=false, or drop an unadopted session with
 // amdsmi_release_probe(), so no process holds a session that nothing owns.
 bool g_probe_ref = false;
+
+// A sysfs attribute of the GPU's PCI device kept open: pread at offset 0 runs the
+// attribute's show() again without the path walk and open/close of a fresh read (4.1 us
+// -> 0.5 us for mem_info_vram_used on MI355X, scripts/sysfs_cost_probe.py).
+struct SysfsAttr {
+  int fd = -1;
+  explicit SysfsAttr(const std::string& path) : fd(::open(path.c_str(), O_RDONLY | O_CLOEXEC)) {}
+  ~SysfsAttr() {
+    if (fd >= 0) ::close(fd);
+  }
+  SysfsAttr(const SysfsAttr&) = delete;
+  SysfsAttr& operator=(const SysfsAttr&) = delete;
+  // bytes read into buf (NUL-terminated), -1 on error (a removed device: ENODEV)
+  ssize_t read(char* buf, size_t cap) const {
+    if (fd < 0 || cap == 0) return -1;
+    ssize_t r;
+    do {
+      r = ::pread(fd, buf, cap - 1, 0);
+    } while (r < 0 && errno == EINTR);
+    if (r >= 0) buf[r] = 0;
+    return r;
+  }
+};
+
+std::string pci_sysfs_dir(const std::string& bdf) {
+  std::string b = bdf;
+  for (auto& c : b) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+  return "/sys/bus/pci/devices/" + b;
+}
 
 std::string status_str(amdsmi_status_t st) {
   const char* s = nullptr;
@@ -213,6 +248,14 @@ class AmdSmiBackend : public Backend {
     // partitions whose busy figure came from the partition API vs the socket blob
     out.push_back({"partition_busy_from_partition_api", 0.0, part_from_api_.load()});
     out.push_back({"partition_busy_from_socket_blob", 0.0, part_from_blob_.load()});
+    // ECC totals asked of amdsmi vs reused (no RAS counter file changed / the RAS event
+    // state did not move); VRAM from sysfs vs amdsmi
+    out.push_back({"ecc_count_reads_library", 0.0, ecc_library_.load()});
+    out.push_back({"ecc_count_reads_unchanged", 0.0, ecc_unchanged_.load()});
+    out.push_back({"ecc_count_reads_event_gated", 0.0, ecc_gated_.load()});
+    out.push_back({"vram_reads_sysfs", 0.0, vram_sysfs_.load()});
+    out.push_back({"vram_reads_library", 0.0, vram_library_.load()});
+    out.push_back({"vram_reads_sysfs_disagreed", 0.0, vram_mismatch_.load()});
     return out;
   }
 
@@ -517,13 +560,18 @@ class AmdSmiBackend : public Backend {
     double used = 0, total = 0;
     bool have_vram = false;
     const bool shared_pool = inv.gpus[gpu].memory_partition == "NPS1";
-    for (size_t p = 0; p < ref.handles.size(); ++p) {
+    if (shared_pool && vram_direct(*ds, inv.gpus[gpu].bdf, h0, &used, &total)) {
+      have_vram = true;
+      s->partition_vram_used_bytes[0] = used;
+    }
+    for (size_t p = 0; p < ref.handles.size() && !have_vram; ++p) {
       amdsmi_vram_usage_t vu{};
       if (amdsmi_get_gpu_vram_usage(ref.handles[p], &vu) == AMDSMI_STATUS_SUCCESS) {
         have_vram = true;
         used += static_cast<double>(vu.vram_used) * 1048576.0;
         total += static_cast<double>(vu.vram_total) * 1048576.0;
         if (static_cast<int>(p) < kMaxPartitions) s->partition_vram_used_bytes[p] = static_cast<double>(vu.vram_used) * 1048576.0;
+        vram_library_.fetch_add(1, std::memory_order_relaxed);
         if (shared_pool) break;  // partitions share one VRAM pool in NPS1; do not double count
       }
     }
@@ -533,11 +581,7 @@ class AmdSmiBackend : public Backend {
       s->ok = true;
     }
     t = charge(kCallVram, t);
-    amdsmi_error_count_t ec{};
-    if (amdsmi_get_gpu_total_ecc_count(h0, &ec) == AMDSMI_STATUS_SUCCESS) {
-      s->ecc_correctable = static_cast<int64_t>(ec.correctable_count);
-      s->ecc_uncorrectable = static_cast<int64_t>(ec.uncorrectable_count);
-    }
+    ecc_totals(*ds, inv.gpus[gpu].bdf, h0, s);
     amdsmi_xgmi_status_t xs = AMDSMI_XGMI_STATUS_NO_ERRORS;
     if (amdsmi_gpu_xgmi_error_status(h0, &xs) == AMDSMI_STATUS_SUCCESS) s->xgmi_error_status = static_cast<int>(xs);
     t = charge(kCallEcc, t);
@@ -702,9 +746,44 @@ class AmdSmiBackend : public Backend {
     int64_t read_ns = 0;
     int64_t reserved = -1, pending = -1, unreservable = -1;
   };
+  // ECC totals (the health monitor's UE latch reads them).  amdsmi's total re-reads every
+  // RAS block's counter file, and the feature mask once per block: ~0.6 ms per GPU on
+  // MI355X, of which the kernel's own work is ~0.27 ms (the ras/aca_* reads query the
+  // firmware's error banks: 19-87 us each, scripts/sysfs_cost_probe.py).  The reported
+  // counts are always amdsmi's; what decides when to ask it again:
+  //  * eccEventGate (default) and ras/event_state present: that file (0.7 us) carries the
+  //    driver's RAS event sequence - fatal errors, poison creation and consumption, which
+  //    is how an uncorrectable error surfaces on MI300/MI350 - so amdsmi is asked when it
+  //    moved, and every kEccRefreshNs regardless (correctable counts, which raise no
+  //    event, are at most that old);
+  //  * otherwise the block files are kept open and read each sample, and amdsmi is asked
+  //    when any of them changed (and every kEccRefreshNs).
+  static constexpr int64_t kEccRefreshNs = 10'000'000'000LL;
+  struct EccWatch {
+    bool opened = false;
+    std::vector<std::unique_ptr<SysfsAttr>> files;  // ras/aca_* (MI355X) or ras/*_err_count
+    std::unique_ptr<SysfsAttr> events;              // ras/event_state
+    std::string seen, scratch;  // the files' contents at amdsmi's last read / this sample's
+    std::string events_seen;    // event_state at amdsmi's last read
+    int64_t read_ns = 0;
+    bool have = false;
+    int64_t ce = 0, ue = 0;
+  };
+  // VRAM usage of a GPU with one memory pool (NPS1): the kernel's mem_info_vram_used /
+  // mem_info_vram_total, the counters amdsmi's usage call reports in MiB (~85 us per call
+  // there, 0.5 us per pread here).  Checked against amdsmi on first use and every
+  // kVramVerifyNs; a disagreement switches the GPU back to amdsmi for good.
+  static constexpr int64_t kVramVerifyNs = 60'000'000'000LL;
+  struct VramDirect {
+    int state = 0;  // 0 untried, 1 agrees with amdsmi, -1 amdsmi only
+    std::unique_ptr<SysfsAttr> used, total;
+    int64_t verified_ns = 0;
+  };
   struct DevState {
     LinkCache links;
     BadPages pages;
+    EccWatch ecc;
+    VramDirect vram;
     std::unique_ptr<DrmResetWatch> reset_watch;  // the render node's amdgpu context (health.resetQuery)
     int partition_api = 0;  // amdsmi_get_gpu_partition_metrics_info: 0 untried, 1 answers, -1 not supported
   };
@@ -719,6 +798,122 @@ class AmdSmiBackend : public Backend {
     for (size_t i = 0; i < refs.size(); ++i)
       if (refs[i].order == order) return static_cast<int>(i);
     return -1;
+  }
+
+  void ecc_totals(DevState& ds, const std::string& bdf, amdsmi_processor_handle h, GpuSample* s) {
+    EccWatch& ew = ds.ecc;
+    if (!ew.opened) {
+      ew.opened = true;
+      const std::string ras = pci_sysfs_dir(bdf) + "/ras";
+      std::vector<std::string> names;
+      if (DIR* d = opendir(ras.c_str())) {
+        while (const dirent* e = readdir(d)) {
+          const std::string n = e->d_name;
+          if (n.rfind("aca_", 0) == 0 || (n.size() > 10 && n.compare(n.size() - 10, 10, "_err_count") == 0))
+            names.push_back(n);
+        }
+        closedir(d);
+      }
+      std::sort(names.begin(), names.end());
+      for (const auto& n : names) {
+        auto a = std::make_unique<SysfsAttr>(ras + "/" + n);
+        if (a->fd >= 0) ew.files.push_back(std::move(a));
+      }
+      auto ev = std::make_unique<SysfsAttr>(ras + "/event_state");
+      if (ev->fd >= 0) ew.events = std::move(ev);
+    }
+    const int64_t now = mono_ns();
+    char buf[512];
+    bool look = !ew.have || now - ew.read_ns >= kEccRefreshNs;
+    std::string events_now;
+    bool gated = false;
+    if (ecc_event_gate() && ew.events) {
+      const ssize_t r = ew.events->read(buf, sizeof(buf));
+      if (r >= 0) {
+        gated = true;
+        events_now.assign(buf, static_cast<size_t>(r));
+        look = look || events_now != ew.events_seen;
+      }
+    }
+    bool direct = false;
+    std::string& cur = ew.scratch;
+    cur.clear();
+    if (!gated) {  // the block files themselves (also read when looking: the next baseline)
+      direct = !ew.files.empty();
+      for (const auto& f : ew.files) {
+        const ssize_t r = f->read(buf, sizeof(buf));
+        if (r < 0) {
+          direct = false;
+          break;
+        }
+        cur.append(buf, static_cast<size_t>(r));
+        cur.push_back('\x1f');
+      }
+      look = look || !direct || cur != ew.seen;
+    }
+    if (look) {
+      amdsmi_error_count_t ec{};
+      ew.have = amdsmi_get_gpu_total_ecc_count(h, &ec) == AMDSMI_STATUS_SUCCESS;
+      if (ew.have) {
+        ew.ce = static_cast<int64_t>(ec.correctable_count);
+        ew.ue = static_cast<int64_t>(ec.uncorrectable_count);
+      }
+      ew.seen = direct ? cur : std::string();
+      ew.events_seen = gated ? events_now : std::string();
+      ew.read_ns = now;
+      ecc_library_.fetch_add(1, std::memory_order_relaxed);
+    } else {
+      (gated ? ecc_gated_ : ecc_unchanged_).fetch_add(1, std::memory_order_relaxed);
+    }
+    if (ew.have) {
+      s->ecc_correctable = ew.ce;
+      s->ecc_uncorrectable = ew.ue;
+    }
+  }
+
+  // bytes used / total of a one-pool GPU from sysfs; false: use amdsmi
+  bool vram_direct(DevState& ds, const std::string& bdf, amdsmi_processor_handle h, double* used, double* total) {
+    VramDirect& v = ds.vram;
+    if (v.state < 0) return false;
+    if (!v.used) {
+      const std::string dir = pci_sysfs_dir(bdf);
+      v.used = std::make_unique<SysfsAttr>(dir + "/mem_info_vram_used");
+      v.total = std::make_unique<SysfsAttr>(dir + "/mem_info_vram_total");
+    }
+    char b1[64], b2[64];
+    if (v.used->read(b1, sizeof(b1)) <= 0 || v.total->read(b2, sizeof(b2)) <= 0) {
+      v.state = -1;
+      return false;
+    }
+    char* e1 = nullptr;
+    char* e2 = nullptr;
+    const double u = std::strtod(b1, &e1), t = std::strtod(b2, &e2);
+    if (e1 == b1 || e2 == b2 || t <= 0) {
+      v.state = -1;
+      return false;
+    }
+    const int64_t now = mono_ns();
+    if (v.state == 0 || now - v.verified_ns >= kVramVerifyNs) {
+      amdsmi_vram_usage_t vu{};
+      if (amdsmi_get_gpu_vram_usage(h, &vu) != AMDSMI_STATUS_SUCCESS) {
+        v.state = -1;
+        return false;
+      }
+      const double mib = 1048576.0, lt = static_cast<double>(vu.vram_total) * mib,
+                   lu = static_cast<double>(vu.vram_used) * mib;
+      // totals agree to the MiB amdsmi rounds to; usage within what moves between two reads
+      if (std::fabs(lt - t) > 2 * mib || std::fabs(lu - u) > std::max(256 * mib, 0.05 * lt)) {
+        v.state = -1;
+        vram_mismatch_.fetch_add(1, std::memory_order_relaxed);
+        return false;
+      }
+      v.state = 1;
+      v.verified_ns = now;
+    }
+    *used = u;
+    *total = t;
+    vram_sysfs_.fetch_add(1, std::memory_order_relaxed);
+    return true;
   }
 
   void bad_pages(DevState& ds, amdsmi_processor_handle h, GpuSample* s) {
@@ -904,6 +1099,7 @@ class AmdSmiBackend : public Backend {
   std::atomic<int64_t> cost_ns_[kCallCount] = {};
   std::atomic<uint64_t> cost_n_[kCallCount] = {};
   std::atomic<uint64_t> link_fast_{0}, link_full_{0}, part_from_api_{0}, part_from_blob_{0};
+  std::atomic<uint64_t> ecc_library_{0}, ecc_unchanged_{0}, ecc_gated_{0}, vram_sysfs_{0}, vram_library_{0}, vram_mismatch_{0};
 
   std::mutex life_mu_;
   std::atomic<bool> closed_{false};

@@ -351,6 +351,11 @@ class Backend : public std::enable_shared_from_this<Backend> {
   // each GPU's render node (GpuSample::reset_count) where the node can be opened.
   void set_reset_query(bool on) { reset_query_.store(on); }
   bool reset_query() const { return reset_query_.load(); }
+  // health.eccEventGate: the ECC totals are re-read when the driver's RAS event state
+  // (fatal errors, poison creation / consumption) moved, and every 10 s otherwise,
+  // instead of every sample (amdsmi backend; where the kernel has that file).
+  void set_ecc_event_gate(bool on) { ecc_event_gate_.store(on); }
+  bool ecc_event_gate() const { return ecc_event_gate_.load(); }
 
   // Block up to timeout_ms for hardware events; append to *out.  Returns count.
   virtual int wait_events(int timeout_ms, std::vector<HwEvent>* out) = 0;
@@ -422,6 +427,7 @@ class Backend : public std::enable_shared_from_this<Backend> {
   SessionGate gate_;
   std::atomic<int> call_timeout_ms_{10000};
   std::atomic<bool> reset_query_{true};
+  std::atomic<bool> ecc_event_gate_{true};
   std::atomic<int> stall_ms_{0};
   std::atomic<int64_t> last_completion_ns_{0};
   // one discovery at a time (a flag + condition: libstdc++'s timed mutex waits are not

@@ -277,6 +277,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("call_timeout_ms", &Backend::call_timeout_ms)
       .def("set_stall_ms", &Backend::set_stall_ms)
       .def("set_reset_query", &Backend::set_reset_query, py::arg("on"))
+      .def("set_ecc_event_gate", &Backend::set_ecc_event_gate, py::arg("on"))
       .def_property_readonly("stall_ms", &Backend::stall_ms)
       .def("last_discovery",
            [](const Backend& b) {
@@ -760,9 +761,11 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("poll_windows_yielded", &GrpcServer::poll_windows_yielded)
       .def_property_readonly("connections", &GrpcServer::connections)
       .def("list_and_watch_streams", &GrpcServer::list_and_watch_streams, py::call_guard<py::gil_scoped_release>())
+      .def("list_and_watch_closed_at", &GrpcServer::list_and_watch_closed_at)
+      .def("set_failure_hook", &GrpcServer::set_failure_hook, py::arg("hook"))
       .def_property_readonly("worker_connections", &GrpcServer::worker_connections)
       .def_property_readonly("socket_path", &GrpcServer::socket_path)
-      .def("failure", &GrpcServer::failure)
+      .def("failure", &GrpcServer::failure, py::call_guard<py::gil_scoped_release>())
       .def("inject_fault", &GrpcServer::inject_fault)
       .def("set_keep_warm_ms", &GrpcServer::set_keep_warm_ms)
       .def("set_keep_warm_full", &GrpcServer::set_keep_warm_full)

@@ -363,6 +363,17 @@ void GrpcServer::set_call_trace(const std::string& path, int capacity) {
   trace_hdr_->magic = kCallTraceMagic;
 }
 
+void GrpcServer::law_closed(Worker* w) {
+  w->law_open.fetch_sub(1, std::memory_order_relaxed);
+  stamp_law_closed();
+}
+
+void GrpcServer::stamp_law_closed() {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  law_closed_ns_.store(static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec, std::memory_order_relaxed);
+}
+
 int GrpcServer::list_and_watch_streams() const {
   std::lock_guard<std::mutex> lk(mu_);  // workers_ changes only under it (start / stop)
   int n = 0;
@@ -503,9 +514,19 @@ void GrpcServer::stop() {
 }
 
 void GrpcServer::fail(const std::string& why) {
-  std::lock_guard<std::mutex> lk(fail_mu_);
-  if (failed_.exchange(true)) return;  // the first fault is the one reported
-  fail_reason_ = why;
+  std::shared_ptr<const std::function<void()>> hook;
+  {
+    std::lock_guard<std::mutex> lk(fail_mu_);
+    if (failed_.exchange(true)) return;  // the first fault is the one reported
+    fail_reason_ = why;
+    hook = fail_hook_;
+  }
+  if (hook && *hook) {
+    try {
+      (*hook)();  // (a Python callable takes the GIL itself; no lock of ours is held)
+    } catch (...) {  // the manager's poll still finds failure()
+    }
+  }
 }
 
 std::string GrpcServer::failure() const {
@@ -547,7 +568,7 @@ void GrpcServer::run_guarded(Worker* w, std::shared_ptr<DeviceTable> table, uint
     conns_.fetch_sub(1);
   }
   w->conns.clear();
-  w->law_open.store(0, std::memory_order_relaxed);
+  if (w->law_open.exchange(0, std::memory_order_relaxed) > 0) stamp_law_closed();  // kubelet's stream went too
   w->load.store(1 << 20, std::memory_order_relaxed);  // never picked for a new connection
   if (listen_fd_ >= 0) epoll_ctl(w->ep, EPOLL_CTL_DEL, listen_fd_, nullptr);
 }
@@ -568,7 +589,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
     auto ci = w->conns.find(fd);
     if (ci != w->conns.end())
       for (const auto& st : ci->second->streams)
-        if (st.second.law) w->law_open.fetch_sub(1, std::memory_order_relaxed);
+        if (st.second.law) law_closed(w);
     w->conns.erase(fd);
     conns_.fetch_sub(1);
     w->load.fetch_sub(1, std::memory_order_relaxed);
@@ -1071,7 +1092,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
           auto it = c.streams.find(sid);
           if (it != c.streams.end()) {
             drop_data(c, it->second);
-            if (it->second.law) w->law_open.fetch_sub(1, std::memory_order_relaxed);
+            if (it->second.law) law_closed(w);
             c.streams.erase(it);
           }
           break;
@@ -1087,7 +1108,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
     for (auto it = c.streams.begin(); it != c.streams.end();)
       if (it->second.done && it->second.pend.empty()) {
         drop_data(c, it->second);
-        if (it->second.law) w->law_open.fetch_sub(1, std::memory_order_relaxed);
+        if (it->second.law) law_closed(w);
         it = c.streams.erase(it);
       } else {
         ++it;
@@ -1557,7 +1578,16 @@ bool H2Client::handle_control(uint8_t type, uint8_t flags, uint32_t sid, std::st
     if (sid == 0) send_window_ += inc;
     else if (sid == cur_sid_) stream_window_ += inc;
   } else if (type == kGoaway) {
-    throw std::runtime_error("H2Client: GOAWAY");
+    // RFC 7540 6.8: streams up to last_stream_id may still be answered (a gRPC server
+    // shutting down gracefully sends last = 2^31-1 first); only a stream above it was
+    // not processed.  No new stream goes out on this connection afterwards.
+    const auto* g = reinterpret_cast<const uint8_t*>(payload.data());
+    const uint32_t last = payload.size() >= 8 ? get_u32(g) & 0x7FFFFFFFu : 0;
+    const uint32_t code = payload.size() >= 8 ? get_u32(g + 4) : 0;
+    goaway_ = true;
+    if (cur_sid_ > last || watch_sid_ > last)
+      throw std::runtime_error("H2Client: GOAWAY (error code " + std::to_string(code) + ", last stream " +
+                               std::to_string(last) + "): the request was not processed");
   } else {
     return false;
   }
@@ -1566,6 +1596,7 @@ bool H2Client::handle_control(uint8_t type, uint8_t flags, uint32_t sid, std::st
 }
 
 void H2Client::send_request(uint32_t sid, std::string_view path, std::string_view req) {
+  if (goaway_) throw std::runtime_error("H2Client: the server sent GOAWAY: open a new connection");
   cur_sid_ = sid;
   stream_window_ = stream_window_init_;
   std::string& o = out_buf_;  // capacity reused across calls

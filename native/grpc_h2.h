@@ -15,6 +15,7 @@
 #pragma once
 
 #include <atomic>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <sys/types.h>
@@ -88,8 +89,17 @@ class GrpcServer {
   // worker thread that died on an exception, or a listener that broke (accept errors,
   // EPOLLERR/HUP on the socket), leaves the server unable to serve.  failure() names
   // the first such fault ("" while healthy); the plugin manager polls it and restarts
-  // the server on a fresh socket.
+  // the server on a fresh socket.  The hook (set before start) runs once, on the thread
+  // that hit the fault, right after failure() names it: the manager checks at once
+  // instead of at its next poll.
   std::string failure() const;
+  // (held by shared_ptr: copying it under fail_mu_ must not copy a Python callable,
+  // whose copy takes the GIL - a thread polling failure() holds the GIL)
+  void set_failure_hook(std::function<void()> hook) {
+    auto h = hook ? std::make_shared<const std::function<void()>>(std::move(hook)) : nullptr;
+    std::lock_guard<std::mutex> lk(fail_mu_);
+    fail_hook_.swap(h);
+  }  // (the previous hook is released here, after the lock)
   // Test-only fault injection: "worker" (the next worker to wake throws) or "listener"
   // (the listening socket is shut down underneath the workers).
   void inject_fault(const std::string& kind);
@@ -103,6 +113,10 @@ class GrpcServer {
   // ListAndWatch streams open now (kubelet holds one per registered plugin; none while
   // registered means kubelet dropped the endpoint and waits for a new Register)
   int list_and_watch_streams() const;
+  // CLOCK_MONOTONIC seconds (Python's time.monotonic) when a ListAndWatch stream last
+  // ended, 0 if none has: the manager's stream watch times its grace from this, so it
+  // can look only every few seconds while the node is quiet
+  double list_and_watch_closed_at() const { return law_closed_ns_.load(std::memory_order_relaxed) * 1e-9; }
   // Keep-warm (grpc.keepWarmMs, 0 = off): a worker that holds a connection and has been
   // idle this long runs the request path on canned requests (HPACK decode of a typical
   // request header block, Allocate and GetPreferredAllocation through the table), so
@@ -148,12 +162,15 @@ class GrpcServer {
   // `table` is handed over at thread creation: a worker never takes mu_, which stop()
   // holds while it joins the workers (one not yet scheduled when stop() ran deadlocked)
   void run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t gen);
+  void law_closed(Worker* w);  // a ListAndWatch stream of w's ended
+  void stamp_law_closed();
   void run_guarded(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t gen);  // run() + fault capture
   void fail(const std::string& why);
   std::atomic<bool> failed_{false};
   std::atomic<int> inject_worker_fault_{0};
   mutable std::mutex fail_mu_;
   std::string fail_reason_;
+  std::shared_ptr<const std::function<void()>> fail_hook_;
   std::shared_ptr<Notifier> notifier_ = std::make_shared<Notifier>();
   std::string path_;
   int nthreads_;
@@ -182,6 +199,7 @@ class GrpcServer {
   ShardedCounter shed_;
   ShardedCounter admission_windows_, poll_windows_yielded_;
   std::atomic<int> conns_{0};
+  std::atomic<int64_t> law_closed_ns_{0};
   CallTraceHeader* trace_hdr_ = nullptr;  // mapped by set_call_trace (nullptr: off)
   CallTraceEntry* trace_ = nullptr;
   size_t trace_bytes_ = 0;
@@ -223,6 +241,7 @@ class H2Client {
   int64_t stream_window_init_ = 65535;   // server's SETTINGS_INITIAL_WINDOW_SIZE
   int64_t stream_window_ = 0;            // current request stream's send window
   uint32_t cur_sid_ = 0;
+  bool goaway_ = false;  // the server sent GOAWAY: no new streams on this connection
   uint32_t peer_max_frame_ = 16384;
   int fd_ = -1;
   uint32_t next_sid_ = 1;

@@ -99,20 +99,28 @@ def test_amdsmi_telemetry(amdsmi_backend):
 def test_amdsmi_sample_cost_breakdown(amdsmi_backend):
     """Where one telemetry pass spends its time (it runs once per GPU per tick, off the
     request path, but 8 GPUs x 8 partitions must fit a 1 s tick with room to spare)."""
-    amdsmi_backend.discover()
+    gpus, _ = amdsmi_backend.discover()
     before = amdsmi_backend.sample_costs()
     first = amdsmi_backend.sample(0)
     assert first.ok
     samples = [amdsmi_backend.sample(0) for _ in range(19)]
     assert all(x.ok for x in samples)
     after = amdsmi_backend.sample_costs()
-    per = {k: (after[k][0] - before[k][0]) / 20 * 1e6 for k in after
-           if not k.startswith(("xgmi_links_", "partition_busy_"))}
-    paths = {k: after[k][1] - before[k][1] for k in after if k.startswith(("xgmi_links_", "partition_busy_"))}
+    counts = ("xgmi_links_", "partition_busy_", "ecc_count_reads_", "vram_reads_")
+    per = {k: (after[k][0] - before[k][0]) / 20 * 1e6 for k in after if not k.startswith(counts)}
+    paths = {k: after[k][1] - before[k][1] for k in after if k.startswith(counts)}
     print("amdsmi sample cost per GPU (us):", {k: round(v, 1) for k, v in per.items()},
           "total %.1f us" % sum(per.values()), "link paths", paths)
     assert set(per) == {"gpu_metrics", "partition_metrics", "vram_usage", "ecc_count", "xgmi_links", "bad_pages"}
     assert sum(per.values()) < 50e3
+    # ECC totals: amdsmi is asked again only when the RAS event state moved (or every
+    # 10 s); one-pool VRAM is read from sysfs once it agreed with amdsmi
+    ras = "/sys/bus/pci/devices/%s/ras" % gpus[0].bdf.lower()
+    if os.path.exists(ras + "/event_state"):
+        assert paths["ecc_count_reads_event_gated"] >= 15, paths
+    assert paths["vram_reads_sysfs_disagreed"] == 0, paths
+    if gpus[0].memory_partition == "NPS1":
+        assert paths["vram_reads_sysfs"] == 20, paths
     # samples served from the gpu_metrics blob report the same links as the full path,
     # with byte counters that never run backwards
     for x in samples:
@@ -122,6 +130,30 @@ def test_amdsmi_sample_cost_breakdown(amdsmi_backend):
     for prev, cur in zip([first] + samples, samples):
         for a, b in zip(prev.links, cur.links):
             assert b[2] >= a[2] and b[3] >= a[3], (a, b)
+
+
+def test_ecc_totals_are_amdsmi_s_with_or_without_the_event_gate(amdsmi_backend):
+    """health.eccEventGate off: the RAS block files are read each sample and amdsmi is
+    asked only when one changed; on: only when ras/event_state moved.  Either way the
+    counts a sample carries are amdsmi's own totals."""
+    gpus, _ = amdsmi_backend.discover()
+    amdsmi_backend.set_ecc_event_gate(False)
+    try:
+        before = amdsmi_backend.sample_costs()
+        off = [amdsmi_backend.sample(0) for _ in range(10)]
+        after = amdsmi_backend.sample_costs()
+    finally:
+        amdsmi_backend.set_ecc_event_gate(True)
+    on = [amdsmi_backend.sample(0) for _ in range(10)]
+    reads = {k: after[k][1] - before[k][1] for k in after if k.startswith("ecc_count_reads_")}
+    print("gate off:", reads, "ecc", [(x.ecc_correctable, x.ecc_uncorrectable) for x in off[:2]],
+          "gate on:", [(x.ecc_correctable, x.ecc_uncorrectable) for x in on[:2]])
+    assert reads["ecc_count_reads_event_gated"] == 0
+    if os.path.isdir("/sys/bus/pci/devices/%s/ras" % gpus[0].bdf.lower()):
+        assert reads["ecc_count_reads_unchanged"] >= 8, reads
+    assert {(x.ecc_correctable, x.ecc_uncorrectable) for x in off} == {(x.ecc_correctable, x.ecc_uncorrectable)
+                                                                        for x in on}
+    assert off[0].ecc_uncorrectable >= 0
 
 
 def test_amdsmi_retired_pages(amdsmi_backend):

@@ -883,3 +883,63 @@ def test_peek_reads_serve_every_request_once(n, plugin_dir):
         c.close()
     finally:
         srv.stop()
+
+
+def _fake_h2_server(path, frames_after_request):
+    """One-connection HTTP/2 server: reads the client's preface, SETTINGS and request,
+    then writes ``frames_after_request`` (raw frames) and closes."""
+    lsock = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+    lsock.bind(path)
+    lsock.listen(1)
+
+    def run():
+        conn, _ = lsock.accept()
+        got = b""
+        conn.settimeout(5)
+        while b"\x00\x00\x05\x00\x01\x00\x00\x00\x01" not in got:  # the request's END_STREAM DATA
+            chunk = conn.recv(65536)
+            if not chunk:
+                break
+            got += chunk
+        conn.sendall(frames_after_request)
+        time.sleep(0.2)
+        conn.close()
+        lsock.close()
+    t = threading.Thread(target=run, daemon=True)
+    t.start()
+    return t
+
+
+def _frame(ftype, flags, sid, payload=b""):
+    return struct.pack(">I", len(payload))[1:] + bytes([ftype, flags]) + struct.pack(">I", sid) + payload
+
+
+def _lit(name, value):  # HPACK literal without indexing, new name
+    return b"\x00" + bytes([len(name)]) + name + bytes([len(value)]) + value
+
+
+@pytest.mark.parametrize("last_sid", [0x7FFFFFFF, 0])
+def test_client_honours_goaway_last_stream_id(n, tmp_path, last_sid):
+    """A GOAWAY that still covers the request (a gRPC server shutting down gracefully
+    sends last = 2^31-1 and then answers what it took) does not fail the call; one below
+    the request's stream says it was not processed, so the caller may send it again
+    (plugin.register does, once)."""
+    path = str(tmp_path / "h2.sock")
+    goaway = _frame(7, 0, 0, struct.pack(">II", last_sid, 0))
+    answer = (_frame(1, 0x4, 1, b"\x88" + _lit(b"content-type", b"application/grpc"))
+              + _frame(0, 0, 1, b"\x00\x00\x00\x00\x00")
+              + _frame(1, 0x5, 1, _lit(b"grpc-status", b"0")))
+    t = _fake_h2_server(path, _frame(4, 0, 0) + goaway + (answer if last_sid else b""))
+    c = n.H2Client(path)
+    try:
+        if last_sid:
+            status, payload, _ = c.unary(v1beta1.METHOD_ALLOCATE, b"")
+            assert status == 0 and payload == b""
+            with pytest.raises(RuntimeError, match="GOAWAY"):  # no new stream on it
+                c.unary(v1beta1.METHOD_ALLOCATE, b"")
+        else:
+            with pytest.raises(RuntimeError, match="not processed"):
+                c.unary(v1beta1.METHOD_ALLOCATE, b"")
+    finally:
+        c.close()
+        t.join(5)

@@ -594,7 +594,8 @@ def test_health_clear_route(make_cfg, plugin_dir, server):
                     for f in text_string_to_metric_families(get(port, "/metrics")[2].decode())
                     for s in f.samples if s.name == "echo_http_requests_total"}
             assert reqs[("/health/clear", "2xx")] == 1 and reqs[("/health/clear", "4xx")] >= 2
-            assert 'amdgpu_device_plugin_events_total{event="health_clears"}' in mgr.exporter.render()
+            # (the manager counts the clear, then publishes the metrics)
+            assert _wait_for(lambda: 'amdgpu_device_plugin_events_total{event="health_clears"}' in mgr.exporter.render())
         finally:
             w.stop()
             mgr.stop()

@@ -110,7 +110,13 @@ def test_plugin_dir_recreated_triggers_reregistration(make_cfg, plugin_dir, run_
         m = run_manager(make_cfg())
         k.wait_for_registrations(1)
         k.stop()
-        shutil.rmtree(plugin_dir)
+        # (the plugin serves its socket again when it sees it removed: it may land while
+        # the tree is being deleted)
+        for _ in range(20):
+            shutil.rmtree(plugin_dir, ignore_errors=True)
+            if not os.path.exists(plugin_dir):
+                break
+            time.sleep(0.05)
         time.sleep(0.3)
         k = KubeletStub(plugin_dir).start()  # recreates the directory and kubelet.sock
         k.wait_for_registrations(1, timeout=10)
@@ -138,7 +144,8 @@ def test_removed_plugin_socket_is_served_again(make_cfg, plugin_dir, run_manager
         k.wait_for_registrations(3, timeout=10)
         assert _wait(lambda: m.counters.get("restarts_socket", 0) == 1)
         assert k.client("amd-gpu.sock").get_options().get_preferred_allocation_available
-        assert 'amdgpu_device_plugin_events_total{event="restarts_socket"} 1' in m.exporter.render()
+        # (the handler counts the restart before it publishes the metrics)
+        assert _wait(lambda: 'amdgpu_device_plugin_events_total{event="restarts_socket"} 1' in m.exporter.render())
 
 
 @pytest.mark.parametrize("grpc_server", ["native", "python"])
@@ -1192,6 +1199,59 @@ def test_plugin_registers_again_when_kubelet_ends_its_stream(make_cfg, plugin_di
         w2.cancel()
 
 
+@pytest.mark.parametrize("grpc_server", ["native", "python"])
+def test_quiet_node_supervises_less_often_and_times_stream_loss_from_its_end(make_cfg, plugin_dir, run_manager,
+                                                                            grpc_server, monkeypatch):
+    """once every plugin is registered with kubelet's stream open, the
+    manager thread supervises every SERVER_CHECK_QUIET_S instead of every second.  A stream
+    that ends is timed from its end (the server stamps it), not from the late poll that
+    notices it, and the manager is back to 1 s passes until it is resolved."""
+    from k8s_gpu_device_plugin_amd.plugin import manager as manager_mod
+    monkeypatch.setattr(manager_mod, "SERVER_CHECK_QUIET_S", 3.0)
+    monkeypatch.setattr(manager_mod, "LAW_LOST_GRACE_S", 60.0)  # no re-registration in this test
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(grpc={"server": grpc_server}))
+        regs = k.wait_for_registrations(1)
+        assert m._check_period() == manager_mod.SERVER_CHECK_S  # no stream yet
+        w = k.watch(regs[0].endpoint)
+        w.next()
+        p = m.plugins[0]
+        assert _wait(lambda: p.law_had, timeout=3)
+        assert m._check_period() == 3.0
+        assert p.list_and_watch_closed_at() == 0
+        time.sleep(1.2)  # a poll falls due later than a 1 s one would
+        t_cancel = time.monotonic()
+        w.cancel()
+        assert _wait(lambda: p.list_and_watch_streams() == 0, timeout=5)
+        closed = p.list_and_watch_closed_at()
+        assert t_cancel - 0.05 <= closed <= time.monotonic()
+        assert _wait(lambda: p.law_lost_since is not None, timeout=5)
+        assert p.law_lost_since == closed  # timed from the stream's end
+        assert m._check_period() == manager_mod.SERVER_CHECK_S
+
+
+def test_native_server_fault_wakes_a_quiet_manager(make_cfg, plugin_dir, run_manager, monkeypatch):
+    """A native server fault runs the supervision pass at once (the server's failure hook
+    posts it) rather than at the quiet node's next poll."""
+    from k8s_gpu_device_plugin_amd.plugin import manager as manager_mod
+    monkeypatch.setattr(manager_mod, "SERVER_CHECK_QUIET_S", 60.0)
+    with KubeletStub(plugin_dir) as k:
+        m = run_manager(make_cfg(grpc={"server": "native"}))
+        regs = k.wait_for_registrations(1)
+        k.watch(regs[0].endpoint).next()
+        p = m.plugins[0]
+        assert _wait(lambda: p.law_had, timeout=3)
+        assert _wait(lambda: m._check_period() == 60.0, timeout=3)
+        time.sleep(1.5)  # the manager is now waiting out its 60 s quiet period
+        srv = p._native_server
+        t0 = time.monotonic()
+        srv.inject_fault("worker")
+        k.wait_for_registrations(2, timeout=10)
+        assert time.monotonic() - t0 < 5.0
+        assert _wait(lambda: m.counters.get("restarts_server", 0) == 1)
+        assert p._native_server is not srv and not p._native_server.failure()
+
+
 def test_stream_watchdog_leaves_a_socket_another_instance_took(make_cfg, plugin_dir, run_manager, monkeypatch):
     """an overlapping new instance re-bound the plugin's socket path and kubelet's
     stream went to it.  The old process must not re-register every grace period (kubelet
@@ -1206,11 +1266,12 @@ def test_stream_watchdog_leaves_a_socket_another_instance_took(make_cfg, plugin_
         w.next()
         p = m.plugins[0]
         assert _wait(lambda: p.law_had, timeout=3)
-        # the "new pod": binds its own socket at the same path (unlink + bind)
-        os.remove(p.socket)
+        # the "new pod": its own socket at the same path (bound aside and renamed over it,
+        # so the manager's socket-removed handler never sees the path missing)
         other = socket_mod.socket(socket_mod.AF_UNIX, socket_mod.SOCK_STREAM)
-        other.bind(p.socket)
+        other.bind(p.socket + ".new")
         other.listen(4)
+        os.rename(p.socket + ".new", p.socket)
         try:
             w.cancel()
             assert _wait(lambda: m.counters.get("stream_watch_socket_taken", 0) == 1, timeout=10)
