@@ -110,8 +110,11 @@ def main(argv=None) -> int:
     reason = {"why": ""}
 
     def on_signal(signum, _frame):
-        reason["why"] = "messaged %s, exiting gracefully..." % signal.Signals(signum).name
-        done.set()
+        reason["why"] = reason["why"] or "messaged %s, exiting gracefully..." % signal.Signals(signum).name
+        # not done.set() here: the handler runs on the main thread between any two
+        # bytecodes, also while that thread holds done's lock inside done.wait() (e.g.
+        # just woken by the parent watch's set), and the lock is not re-entrant
+        threading.Thread(target=done.set, name="signal", daemon=True).start()
 
     for s in (signal.SIGHUP, signal.SIGINT, signal.SIGQUIT, signal.SIGTERM):
         signal.signal(s, on_signal)

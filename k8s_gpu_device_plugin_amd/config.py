@@ -67,6 +67,11 @@ class SharingConfig:
 class TelemetryConfig:
     enabled: bool = True
     intervalMs: int = 1000
+    # while nothing has read the GPU metrics (/metrics, /gpu/metrics) for activeWindowS and
+    # every GPU's health is settled, sample every idleIntervalMs instead (0 = never slow
+    # down); the first read after that wakes the sampler and restores intervalMs
+    idleIntervalMs: int = 5000
+    activeWindowS: float = 120.0
 
 
 @dataclass
@@ -415,6 +420,10 @@ def validate(cfg: Config) -> Config:
         raise ConfigError("backgroundSched must be batch|normal, got %r" % cfg.backgroundSched)
     if cfg.telemetry.intervalMs < 10:
         raise ConfigError("telemetry.intervalMs must be >= 10")
+    if cfg.telemetry.idleIntervalMs < 0 or cfg.telemetry.idleIntervalMs > 3600000:
+        raise ConfigError("telemetry.idleIntervalMs must be within 0..3600000")
+    if cfg.telemetry.activeWindowS < 0:
+        raise ConfigError("telemetry.activeWindowS must be >= 0")
     if not cfg.resourcePrefix or "/" in cfg.resourcePrefix:
         raise ConfigError("resourcePrefix must be a DNS-like prefix without '/'")
     # extended resource prefixes are DNS subdomains (RFC 1123, at most 253 characters);

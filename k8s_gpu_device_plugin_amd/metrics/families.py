@@ -88,6 +88,9 @@ FAMILIES = (
     Family("amdgpu_telemetry_samples_total", "counter", (), "exporter", "Sampling passes"),
     Family("amdgpu_telemetry_sample_errors_total", "counter", (), "exporter", "Per-GPU sample failures"),
     Family("amdgpu_telemetry_sample_duration_seconds", "histogram", (), "exporter", "One sampling pass"),
+    Family("amdgpu_telemetry_interval_seconds", "gauge", (), "exporter",
+           "The sampler's current period: telemetry.intervalMs, or telemetry.idleIntervalMs while nothing "
+           "reads the GPU metrics and health is settled"),
     Family("amdgpu_telemetry_last_pass_age_seconds", "gauge", (), "exporter",
            "Seconds since the sampler last completed a pass (passes go on while one GPU's call hangs: "
            "it holds that GPU's lane only)"),

@@ -1524,6 +1524,8 @@ class PluginManager:
                             "health falls back to telemetry polling): check access to /dev/kfd")
         if self.cfg.telemetry.enabled:
             self.exporter.set_stall_ms(int(self.cfg.health.sampleStallS * 1000) if self.cfg.health.enabled else 0)
+            self.exporter.set_idle_interval(int(self.cfg.telemetry.idleIntervalMs),
+                                            int(self.cfg.telemetry.activeWindowS * 1000))
             self.exporter.start(self.backend, self.cfg.telemetry.intervalMs,
                                 self.monitor if self.cfg.health.enabled else None)
         self._publish_metrics()

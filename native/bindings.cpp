@@ -623,6 +623,9 @@ PYBIND11_MODULE(_native, m) {
 
   py::class_<Exporter, std::shared_ptr<Exporter>>(m, "Exporter")
       .def("set_stall_ms", &Exporter::set_stall_ms)
+      .def("set_idle_interval", &Exporter::set_idle_interval, py::arg("idle_ms"), py::arg("window_ms"))
+      .def_property_readonly("current_interval_ms", &Exporter::current_interval_ms)
+      .def_property_readonly("idle_passes", &Exporter::idle_passes)
       .def_property_readonly("stalled_gpu", &Exporter::stalled_gpu)
       .def_property_readonly("stalled_gpus", &Exporter::stalled_gpus)
       .def_property_readonly("blocked_gpus", &Exporter::blocked_gpus)

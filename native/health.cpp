@@ -703,6 +703,17 @@ std::vector<std::string> HealthMonitor::clear_latches(const std::string& key, co
   return out;
 }
 
+bool HealthMonitor::settling() const {
+  std::lock_guard<std::mutex> lk(mu_);
+  for (const auto& kv : state_) {
+    const GpuState& st = kv.second;
+    if (st.failures > 0 || st.lost || st.resetting || st.fw_jump_pending || st.candidate || st.outage_unresolved ||
+        st.pcie_low > 0 || (st.pcie_bad && st.pcie_ok > 0))
+      return true;
+  }
+  return false;
+}
+
 std::vector<std::string> HealthMonitor::holds(const std::string& key) const {
   std::lock_guard<std::mutex> lk(mu_);
   std::vector<std::string> out;

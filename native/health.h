@@ -168,6 +168,10 @@ class HealthMonitor {
   // What holds GPU `key` Unhealthy now ("reset_in_progress", "uncorrectable_ecc",
   // "telemetry_lost", "retired_pages", "pcie_link"), checks turned off included.
   std::vector<std::string> holds(const std::string& key) const;
+  // True while any GPU's health is in flux (failing or lost, a reset being confirmed,
+  // a candidate unresolved, PCIe or a resetting latch set): the sampler keeps its
+  // active cadence then (telemetry.idleIntervalMs).
+  bool settling() const;
   // Partitions a recovery must leave Unhealthy (identity -> partition indices; -1 = the
   // whole GPU): failed or pending canary verdicts the manager keeps.  The fast path of a
   // Healthy transition writes the other devices of the GPU only, in one table update.

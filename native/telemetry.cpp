@@ -154,14 +154,18 @@ void Exporter::start(std::shared_ptr<Backend> backend, int interval_ms, std::sha
   }
   stop_ = false;
   running_ = true;
+  started_ns_.store(mono_ns());
+  idle_mode_.store(false);
+  poke_.store(false);
+  current_interval_ms_.store(interval);
   {
     std::lock_guard<std::mutex> lk(first_mu_);
     first_done_ = false;
   }
   sampler_exit_ = std::make_shared<ThreadExit>();
-  waker_ = std::make_shared<Waker>();
   {
     std::lock_guard<std::mutex> lk(run_mu_);
+    waker_ = std::make_shared<Waker>();  // (under run_mu_: a scrape's note_read reads it)
     watchdog_ = std::thread([this, m = monitor_, wk = waker_] { watchdog_loop(m, wk); });  // before the first call
   }
   thread_ = std::thread(sampler_main, std::move(weak), sampler_exit_, waker_, gen, interval);
@@ -175,9 +179,18 @@ void Exporter::start(std::shared_ptr<Backend> backend, int interval_ms, std::sha
   cv_wait_ms(first_cv_, lk, ms > 0 ? ms : 10000, [&] { return first_done_; });
 }
 
-void Exporter::Waker::sleep_ms(int64_t ms) {
+void Exporter::Waker::sleep_ms(int64_t ms, bool pokeable) {
   std::unique_lock<std::mutex> lk(mu);
-  cv_wait_ms(cv, lk, static_cast<int>(std::min<int64_t>(ms, 3600000)), [&] { return stopping; });
+  cv_wait_ms(cv, lk, static_cast<int>(std::min<int64_t>(ms, 3600000)), [&] { return stopping || (pokeable && poked); });
+  if (pokeable) poked = false;
+}
+
+void Exporter::Waker::poke() {
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    poked = true;
+  }
+  cv.notify_all();
 }
 
 void Exporter::Waker::wake() {
@@ -373,7 +386,7 @@ void Exporter::sampler_main(std::weak_ptr<Exporter> weak, std::shared_ptr<Thread
       sleep_ms = self->sampler_step(&next, gen, interval_ms);
     }
     if (sleep_ms < 0) break;
-    if (sleep_ms > 0) waker->sleep_ms(sleep_ms);  // until the next pass, or stop()
+    if (sleep_ms > 0) waker->sleep_ms(sleep_ms, true);  // until the next pass, a poke, or stop()
   }
   exit->mark();
 }
@@ -381,6 +394,12 @@ void Exporter::sampler_main(std::weak_ptr<Exporter> weak, std::shared_ptr<Thread
 int Exporter::sampler_step(int64_t* next, uint64_t gen, int interval_ms) {
   if (stop_.load() || sampler_gen_.load() != gen) return -1;
   const int64_t now = mono_ns();
+  if (*next != 0 && now < *next && poke_.exchange(false)) {
+    // the GPU metrics were read while the sampler idled: the next pass is due one
+    // interval after the last, as if it had never slowed down
+    const int64_t due = last_pass_ns_.load() + static_cast<int64_t>(interval_ms) * 1000000;
+    if (due < *next) *next = due;
+  }
   if (*next != 0 && now < *next)  // (stop() cuts the sleep short)
     return static_cast<int>((*next - now) / 1000000 + 1);
   const bool first = *next == 0;
@@ -393,9 +412,48 @@ int Exporter::sampler_step(int64_t* next, uint64_t gen, int interval_ms) {
     first_cv_.notify_all();
     *next = mono_ns();
   }
-  *next += static_cast<int64_t>(interval_ms) * 1000000;  // fixed cadence, no drift
-  if (*next < mono_ns()) *next = mono_ns() + static_cast<int64_t>(interval_ms) * 1000000;
+  const int step = next_interval_ms(interval_ms);
+  *next += static_cast<int64_t>(step) * 1000000;  // fixed cadence, no drift
+  if (*next < mono_ns()) *next = mono_ns() + static_cast<int64_t>(step) * 1000000;
   return 0;
+}
+
+int Exporter::next_interval_ms(int interval_ms) {
+  const int idle = idle_interval_ms_.load();
+  bool active = idle <= interval_ms;
+  if (!active) {
+    const int64_t now = mono_ns(), window = static_cast<int64_t>(active_window_ms_.load()) * 1000000;
+    active = now - started_ns_.load() < window || now - last_read_ns_.load(std::memory_order_relaxed) < window;
+  }
+  if (!active) {
+    std::shared_ptr<HealthMonitor> mon;
+    {
+      std::lock_guard<std::mutex> lk(run_mu_);
+      mon = monitor_;
+    }
+    active = mon && mon->settling();
+  }
+  idle_mode_.store(!active);
+  if (!active) idle_passes_.fetch_add(1, std::memory_order_relaxed);
+  const int step = active ? interval_ms : idle;
+  current_interval_ms_.store(step);
+  return step;
+}
+
+void Exporter::note_read() const {
+  // (every scrape comes here: one relaxed load in the common case, a store at most every
+  // 100 ms, the sampler woken only on the first read after it slowed down)
+  const int64_t now = mono_ns();
+  if (now - last_read_ns_.load(std::memory_order_relaxed) < 100000000) return;
+  last_read_ns_.store(now, std::memory_order_relaxed);
+  if (idle_mode_.load(std::memory_order_relaxed) && !poke_.exchange(true)) {
+    std::shared_ptr<Waker> w;
+    {
+      std::lock_guard<std::mutex> lk(run_mu_);
+      w = waker_;
+    }
+    if (w) w->poke();
+  }
 }
 
 void Exporter::sample_once(uint64_t sampler_gen) {
@@ -901,6 +959,7 @@ void Exporter::render_process(std::string* out) const {
 void Exporter::render_parts(std::string_view* head, std::string* counters, std::string_view* health,
                             std::string* tail, std::shared_ptr<const std::string>* head_sp,
                             std::shared_ptr<const std::string>* health_sp) const {
+  note_read();
   TlCache& c = tl_cache();
   const uint64_t gen = view_gen_.load(std::memory_order_acquire);
   if (!c.view || c.view_gen != gen) {
@@ -919,6 +978,14 @@ void Exporter::render_parts(std::string_view* head, std::string* counters, std::
   counters->append("amdgpu_telemetry_sample_errors_total ");
   append_u64(counters, sample_errors_.load());
   counters->push_back('\n');
+  if (const int cur = current_interval_ms_.load()) {
+    append_header(counters, "amdgpu_telemetry_interval_seconds",
+                  "The sampler's current period (telemetry.intervalMs, or idleIntervalMs while unread and settled).",
+                  "gauge");
+    counters->append("amdgpu_telemetry_interval_seconds ");
+    append_float(counters, cur * 1e-3);
+    counters->push_back('\n');
+  }
   if (const int64_t last = last_pass_ns_.load()) {
     append_header(counters, "amdgpu_telemetry_last_pass_age_seconds",
                   "Seconds since the sampler last completed a pass over all GPUs.", "gauge");

@@ -83,6 +83,19 @@ class Exporter : public std::enable_shared_from_this<Exporter> {
   // completed after its own began (the library is not serialised behind the first
   // wedge), otherwise it is "blocked" behind it and stays Healthy.
   void set_stall_ms(int ms) { stall_ms_.store(ms > 0 ? ms : 0); }
+  // Adaptive cadence (telemetry.idleIntervalMs / activeWindowS): the sampler runs every
+  // idle_ms instead of the start() interval while nothing has read the GPU metrics for
+  // window_ms, the health monitor is settled (HealthMonitor::settling) and the first
+  // window_ms after start() are over.  A scrape in that state wakes the sampler at once
+  // and restores the interval.  A sample costs ~1 ms of CPU per MI355X, most of it the
+  // kernel fetching the firmware's metrics table (scripts/sysfs_cost_probe.py).
+  // idle_ms <= the interval: always the interval.
+  void set_idle_interval(int idle_ms, int window_ms) {
+    idle_interval_ms_.store(idle_ms > 0 ? idle_ms : 0);
+    active_window_ms_.store(window_ms > 0 ? window_ms : 0);
+  }
+  int current_interval_ms() const { return current_interval_ms_.load(); }
+  uint64_t idle_passes() const { return idle_passes_.load(); }
   int stalled_gpu() const;                 // lowest stalled GPU index, -1 = none
   std::vector<int> stalled_gpus() const;   // reported lost by the watchdog
   std::vector<int> blocked_gpus() const;   // stuck behind another GPU's call
@@ -117,8 +130,10 @@ class Exporter : public std::enable_shared_from_this<Exporter> {
     std::mutex mu;
     std::condition_variable cv;
     bool stopping = false;
-    void sleep_ms(int64_t ms);
+    bool poked = false;  // the sampler's sleep only (a scrape while idle)
+    void sleep_ms(int64_t ms, bool pokeable = false);
     void wake();
+    void poke();
   };
   static void sampler_main(std::weak_ptr<Exporter> weak, std::shared_ptr<ThreadExit> exit,
                            std::shared_ptr<Waker> waker, uint64_t gen, int interval_ms);
@@ -210,7 +225,7 @@ class Exporter : public std::enable_shared_from_this<Exporter> {
   std::shared_ptr<const std::string> extra_;
   std::shared_ptr<const std::string> gpu_text_;
 
-  std::mutex run_mu_;  // backend_, monitor_, interval_ms_: set by start(), copied by each pass
+  mutable std::mutex run_mu_;  // backend_, monitor_, interval_ms_, waker_: set by start(), copied by each pass
   std::shared_ptr<Backend> backend_;
   std::shared_ptr<HealthMonitor> monitor_;
   int interval_ms_ = 1000;
@@ -232,6 +247,15 @@ class Exporter : public std::enable_shared_from_this<Exporter> {
   std::atomic<int> stall_ms_{0};
   std::atomic<int64_t> last_pass_ns_{0};    // end of the last complete pass (mono ns)
   int64_t start_time_s_ = 0;
+  // adaptive cadence (set_idle_interval)
+  int next_interval_ms(int interval_ms);
+  void note_read() const;
+  std::atomic<int> idle_interval_ms_{0}, active_window_ms_{120000}, current_interval_ms_{0};
+  mutable std::atomic<int64_t> last_read_ns_{0};
+  std::atomic<int64_t> started_ns_{0};
+  std::atomic<bool> idle_mode_{false};
+  mutable std::atomic<bool> poke_{false};
+  std::atomic<uint64_t> idle_passes_{0};
 
   // gzip members cached against the exact segment objects they were compressed from
   mutable std::mutex gz_mu_;

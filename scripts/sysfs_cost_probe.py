@@ -132,13 +132,17 @@ def main() -> int:
                                          "cpu": round((time.process_time_ns() - c0) / a.reps / 1e3, 1)}
     # as the daemon runs it: one sample a second, caches cold in between
     cold = []
+    c_before = be.sample_costs()
     for _ in range(8):
         time.sleep(1.0)
         w0, c0 = time.perf_counter_ns(), time.process_time_ns()
         be.sample(0)
         cold.append(((time.perf_counter_ns() - w0) / 1e3, (time.process_time_ns() - c0) / 1e3))
+    c_after = be.sample_costs()
     res["sample_once_a_second_us"] = {"wall": round(sorted(x for x, _ in cold)[4], 1),
                                       "cpu": round(sorted(y for _, y in cold)[4], 1)}
+    res["sample_once_a_second_split_wall_us"] = {k: round((c_after[k][0] - c_before[k][0]) / 8 * 1e6, 1)
+                                                 for k in c_after if c_after[k][0] > 0}
     be.set_reset_query(False)
     res["sample_split_wall_us"] = {k: round((after[k][0] - before[k][0]) / a.reps * 1e6, 1) for k in after
                                    if not k.startswith(("xgmi_links_", "partition_busy_"))}

@@ -246,8 +246,21 @@ def test_bench_daemon_exits_with_a_harness_that_dies(tmp_path):
             return
         time.sleep(0.1)
     with open("/proc/%d/status" % pid) as f:
-        status = f.read()
+        status = [ln for ln in f.read().splitlines() if ln.startswith(("State", "PPid", "Threads", "Sig", "Shd"))]
+    threads = []
+    for tid in sorted(os.listdir("/proc/%d/task" % pid)):
+        try:
+            with open("/proc/%d/task/%s/comm" % (pid, tid)) as f:
+                comm = f.read().strip()
+            with open("/proc/%d/task/%s/wchan" % (pid, tid)) as f:
+                wchan = f.read().strip()
+            with open("/proc/%d/task/%s/status" % (pid, tid)) as f:
+                sig = [ln.split()[1] for ln in f.read().splitlines() if ln.startswith(("SigPnd", "SigBlk"))]
+            threads.append("%s %s %s pnd/blk=%s" % (tid, comm, wchan, "/".join(sig)))
+        except OSError:
+            pass
     os.kill(pid, signal.SIGKILL)
     with open(tmp_path / "daemon.log") as f:
         tail = f.read()[-3000:]
-    raise AssertionError("daemon %d outlived its harness\n%s\n%s" % (pid, status[:600], tail))
+    raise AssertionError("daemon %d outlived its harness\n%s\n%s\n%s" % (pid, "\n".join(status), "\n".join(threads),
+                                                                          tail))

@@ -702,3 +702,59 @@ def test_pcie_floor_from_config(make_cfg, plugin_dir):
         finally:
             m.stop()
             t.join(10)
+
+
+def test_sampler_slows_down_while_unread_and_settled(n):
+    """VERDICT r5 item 4 (telemetry.idleIntervalMs): once the start window is over, nothing
+    has read the GPU metrics for activeWindowS and health is settled, the sampler runs at
+    the idle period; the first read wakes it at once and restores the interval; a failing
+    GPU keeps it at the interval while it fails."""
+    be = fixtures.build_backend("2gpu_spx")
+    m = n.HealthMonitor(be, 3)
+    m.set_gpu_count(2)
+    ex = n.Exporter()
+    gpus, _ = be.discover()
+    ex.set_inventory(gpus)
+    ex.set_idle_interval(600, 300)
+    ex.start(be, 30, m)
+    try:
+        assert ex.current_interval_ms == 30
+        assert _wait_for(lambda: ex.current_interval_ms == 600, timeout=3)
+        assert ex.idle_passes >= 1
+        n0, t0 = ex.samples_total, time.monotonic()
+        time.sleep(0.9)  # idle: one or two passes, not thirty
+        assert ex.samples_total - n0 <= 3
+        text = ex.render()  # a scrape: the sampler wakes now, not at its next idle tick
+        assert "amdgpu_telemetry_interval_seconds 0.6" in text
+        n1, t1 = ex.samples_total, time.monotonic()
+        assert _wait_for(lambda: ex.samples_total > n1, timeout=0.4)
+        assert time.monotonic() - t1 < 0.4
+        assert _wait_for(lambda: ex.current_interval_ms == 30, timeout=1)
+        assert "amdgpu_telemetry_interval_seconds 0.03" in ex.render()
+        # unread again, but a GPU's samples fail: health is not settled, the cadence holds
+        assert _wait_for(lambda: ex.current_interval_ms == 600, timeout=3)
+        be.set_sample_fail(1, True)
+        ex.render()  # (wake it: the failure is seen on the next pass)
+        assert _wait_for(lambda: not m.gpu_healthy(1), timeout=3)
+        time.sleep(0.6)  # past the read window
+        assert ex.current_interval_ms == 30
+        be.set_sample_fail(1, False)
+        assert _wait_for(lambda: m.gpu_healthy(1), timeout=3)
+        assert _wait_for(lambda: ex.current_interval_ms == 600, timeout=3)
+    finally:
+        ex.stop()
+
+
+def test_idle_interval_off_or_below_the_interval_keeps_the_interval(n):
+    be = fixtures.build_backend("2gpu_spx")
+    ex = n.Exporter()
+    gpus, _ = be.discover()
+    ex.set_inventory(gpus)
+    for idle in (0, 20):
+        ex.set_idle_interval(idle, 50)
+        ex.start(be, 30, None)
+        try:
+            time.sleep(0.3)
+            assert ex.current_interval_ms == 30 and ex.idle_passes == 0
+        finally:
+            ex.stop()
