@@ -24,7 +24,7 @@ done
 echo "=== reset query probe ($(date +%T))"
 timeout -k 10 120 python scripts/reset_query_probe.py --out "$OUT/${tag}_reset_query_probe.json" > /dev/null 2>&1 || exit $?
 echo "=== idle cost ($(date +%T))"
-timeout -k 10 120 python scripts/idle_wakeups.py --out "$OUT/${tag}_idle_wakeups.json" > "$OUT/${tag}_idle_wakeups.log" 2>&1 || exit $?
+timeout -k 10 240 python scripts/idle_wakeups.py --settle 130 --out "$OUT/${tag}_idle_wakeups.json" > "$OUT/${tag}_idle_wakeups.log" 2>&1 || exit $?
 tail -3 "$OUT/${tag}_idle_wakeups.log" | head -2
 echo "=== rocprofv3 smoke ($(date +%T))"
 cd /tmp && export TMPDIR=/tmp
