@@ -172,6 +172,8 @@ class GrpcConfig:
     # from a deeper idle state - recv 0.21 vs 0.70 us, but send 0.85 vs 0.34 us and Allocate
     # p50 2.8-3.5 vs 2.55 us (profiles/r6/ab_peek_*.json)
     peekReads: bool = False
+    # busy-poll spacing: PAUSE for this long between two empty polls (0 = one PAUSE)
+    pollGapNs: int = 0
     keepWarmFull: bool = True    # ... through the whole request path of an in-memory connection (else HPACK + table)
     # native server: per-call trace of unary RPCs in a file-backed ring ("" = off), read by
     # bench.py to attribute slow calls; one record per call, callTraceEntries records
@@ -407,6 +409,8 @@ def validate(cfg: Config) -> Config:
             raise ConfigError("grpc.%s must be within 0..100000 (0 = off)" % key)
     if not 0 <= cfg.grpc.activeWindowMs <= 86400000:
         raise ConfigError("grpc.activeWindowMs must be within 0..86400000 (0 = always)")
+    if not 0 <= cfg.grpc.pollGapNs <= 100000:
+        raise ConfigError("grpc.pollGapNs must be within 0..100000")
     if cfg.grpc.callTraceFile and not 1 <= cfg.grpc.callTraceEntries <= (1 << 26):
         raise ConfigError("grpc.callTraceEntries must be within 1..%d" % (1 << 26))
     for sect in ("grpc", "http"):

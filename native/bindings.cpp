@@ -752,6 +752,7 @@ PYBIND11_MODULE(_native, m) {
       .def("set_idle_wake_ms", &GrpcServer::set_idle_wake_ms, py::arg("ms"))
       .def("set_active_window_ms", &GrpcServer::set_active_window_ms, py::arg("ms"))
       .def("set_peek_reads", &GrpcServer::set_peek_reads, py::arg("on"))
+      .def("set_poll_gap_ns", &GrpcServer::set_poll_gap_ns, py::arg("ns"))
       .def_property_readonly("idle_wakeups", &GrpcServer::idle_wakeups)
       .def("add_table", &GrpcServer::set_table)
       .def("start", &GrpcServer::start, py::call_guard<py::gil_scoped_release>())

@@ -1217,7 +1217,15 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
         if (now >= spin_until) {
           spin_until = 0;
         } else if (!polite) {
-          cpu_relax();
+          const int gap = poll_gap_ns_.load(std::memory_order_relaxed);
+          if (gap > 0) {
+            const int64_t until = now + gap;
+            do {
+              cpu_relax();
+            } while (mono_ns() < until);
+          } else {
+            cpu_relax();
+          }
         } else if (!guard.keep_polling(now)) {  // preempted: the CPU is wanted (maybe by the client)
           spin_until = 0;
           poll_windows_yielded_.add();

@@ -141,6 +141,10 @@ class GrpcServer {
   // Requests read with MSG_PEEK and consumed after the answer is sent (applies to
   // connections accepted from now on; off by default, grpc.peekReads).  See Worker::Conn::peek.
   void set_peek_reads(bool on) { peek_reads_.store(on); }
+  // Busy-poll spacing (grpc.pollGapNs): between two empty polls of an open busy-poll
+  // window the worker pauses this long (PAUSE instructions) instead of one PAUSE, so a
+  // client on the worker's SMT sibling gets most of the core.  0 = one PAUSE.
+  void set_poll_gap_ns(int ns) { poll_gap_ns_.store(std::max(0, std::min(ns, 100000))); }
   // Epoll wake-ups of the workers that found nothing to do (timeouts), all workers.
   uint64_t idle_wakeups() const { return idle_wakeups_.load(); }
   std::vector<int> worker_connections() const;  // connections owned per worker thread
@@ -181,6 +185,7 @@ class GrpcServer {
   std::atomic<int> idle_wake_ms_{0};
   std::atomic<int> active_window_ms_{0};
   std::atomic<bool> peek_reads_{false};
+  std::atomic<int> poll_gap_ns_{0};
   std::atomic<uint64_t> idle_wakeups_{0};
   std::atomic<uint64_t> warm_ticks_{0};
   // table_ and table_gen_ change together under swap_mu_ (never held across anything else);
