@@ -9,6 +9,7 @@ batch by batch (rounds), so every value meets the same moments of the host.  The
 spin exchange between the same CPU pairs is the floor.
 
     python scripts/smt_probe.py [--gaps 0,200,500] [--rounds 8] [--batch 512] [--out FILE]
+    python scripts/smt_probe.py --arms '{"base": {}, "peek": {"grpc": {"peekReads": true}}}'
 """
 from __future__ import annotations
 
@@ -57,6 +58,7 @@ def worker_tids(pid):
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gaps", default="0,200,500")
+    ap.add_argument("--arms", default="", help="JSON {name: daemon config overrides}; replaces --gaps")
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--out", default="")
@@ -73,13 +75,16 @@ def main() -> int:
     from k8s_gpu_device_plugin_amd.api import v1beta1
     n = native.load()
     nb = native.load_bench()
-    gaps = [int(g) for g in a.gaps.split(",")]
+    if a.arms:
+        arms = json.loads(a.arms)
+    else:
+        arms = {"pollGapNs=%d" % int(g): {"grpc": {"pollGapNs": int(g)}} for g in a.gaps.split(",")}
+    gaps = list(arms)
     daemons = []
     try:
         for g in gaps:
             wd = tempfile.mkdtemp(prefix="amdgpu-dp-smt-")
-            proc, kubelet, _port, reg, backend = bench.start_daemon(1, "native", wd,
-                                                                    overrides={"grpc": {"pollGapNs": g}})
+            proc, kubelet, _port, reg, backend = bench.start_daemon(1, "native", wd, overrides=arms[g])
             h2 = n.H2Client(os.path.join(wd, "device-plugins", reg.endpoint))
             law = kubelet.watch(reg.endpoint)
             _, devs = law.next(timeout=10)
@@ -106,18 +111,21 @@ def main() -> int:
                     lat = d["h2"].bench_unary(v1beta1.METHOD_ALLOCATE, d["req"], a.batch)
                     got[(d["gap"], where)].append(round(statistics.median(lat) * 1e6, 3))
         sizes = (9 + 80 + 9 + 5 + len(daemons[0]["req"]), 9 + 20 + 9 + 5 + 60 + 9 + 16)
-        floors = {}
+        floors, floors_peek = {}, {}
         for where, cpu in (("smt_sibling", sib), ("same_l3", other)):
             lat = nb.uds_pingpong(4000, 300, *sizes, server_spin=True, client_cpu=client, server_cpu=cpu)
             floors[where] = round(statistics.median(lat) * 1e6, 3)
+            lat = nb.uds_pingpong(4000, 300, *sizes, server_spin=True, client_cpu=client, server_cpu=cpu, peek=True)
+            floors_peek[where] = round(statistics.median(lat) * 1e6, 3)
         res["floor_spin_p50_us"] = floors
+        res["floor_spin_peek_p50_us"] = floors_peek
         res["allocate"] = {}
         for g in gaps:
             row = {}
             for where in ("smt_sibling", "same_l3"):
                 xs = got[(g, where)]
                 row[where] = {"p50_of_batches_us": round(statistics.median(xs), 3), "batches_us": xs}
-            res["allocate"]["pollGapNs=%d" % g] = row
+            res["allocate"][g] = row
     finally:
         for d in daemons:
             try:
