@@ -174,7 +174,10 @@ def _watch_parent(parent: int, reason: dict, done: threading.Event) -> bool:
         from .utils.util import name_os_thread
         name_os_thread("parent-watch")
         try:
-            select.select([fd], [], [])
+            p = select.poll()  # (not select(): no FD_SETSIZE limit on the descriptor)
+            p.register(fd, select.POLLIN)
+            while not p.poll():
+                pass
         finally:
             os.close(fd)
         reason["why"] = reason["why"] or "parent process %d exited, exiting gracefully..." % parent

@@ -264,3 +264,23 @@ def test_bench_daemon_exits_with_a_harness_that_dies(tmp_path):
         tail = f.read()[-3000:]
     raise AssertionError("daemon %d outlived its harness\n%s\n%s\n%s" % (pid, "\n".join(status), "\n".join(threads),
                                                                           tail))
+
+
+def test_parent_watch_ends_the_daemon_when_its_harness_exits():
+    """The pidfd watch (cli._watch_parent) sets the daemon's done event when the process it
+    watches exits, with no periodic wake-up while it lives."""
+    import threading
+    from k8s_gpu_device_plugin_amd import cli
+    child = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(60)"])
+    try:
+        reason, done = {"why": ""}, threading.Event()
+        if not cli._watch_parent(child.pid, reason, done):
+            pytest.skip("no pidfd_open on this kernel")
+        assert not done.wait(0.3)
+        child.kill()
+        child.wait(10)
+        assert done.wait(5)
+        assert "parent process %d exited" % child.pid in reason["why"]
+    finally:
+        if child.poll() is None:
+            child.kill()
