@@ -46,6 +46,7 @@ CORE_SOURCES = [
     "fixture_backend.cpp",
     "amdsmi_backend.cpp",
     "drm_reset.cpp",
+    "core_escape.cpp",
     "allocator.cpp",
     "device_table.cpp",
     "health.cpp",

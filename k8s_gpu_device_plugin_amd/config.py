@@ -174,6 +174,9 @@ class GrpcConfig:
     peekReads: bool = False
     # busy-poll spacing: PAUSE for this long between two empty polls (0 = one PAUSE)
     pollGapNs: int = 0
+    # a worker whose calls in a busy-poll window run 35 % over its own best (another busy
+    # hardware thread on its core, e.g. the client's) moves to another core of its L3
+    coreEscape: bool = False
     keepWarmFull: bool = True    # ... through the whole request path of an in-memory connection (else HPACK + table)
     # native server: per-call trace of unary RPCs in a file-backed ring ("" = off), read by
     # bench.py to attribute slow calls; one record per call, callTraceEntries records

@@ -327,6 +327,7 @@ class AmdDevicePlugin:
             srv.set_active_window_ms(int(self.cfg.grpc.activeWindowMs))
             srv.set_peek_reads(bool(self.cfg.grpc.peekReads))
             srv.set_poll_gap_ns(int(self.cfg.grpc.pollGapNs))
+            srv.set_core_escape(bool(self.cfg.grpc.coreEscape))
             if self.cfg.grpc.callTraceFile:
                 srv.set_call_trace(self.cfg.grpc.callTraceFile.replace("{resource}", self.resource.get_resource_name()),
                                    int(self.cfg.grpc.callTraceEntries))

@@ -11,6 +11,7 @@
 
 #include "allocator.h"
 #include "backend.h"
+#include "core_escape.h"
 #include "device_table.h"
 #include "fixture_backend.h"
 #include "grpc_h2.h"
@@ -453,6 +454,12 @@ PYBIND11_MODULE(_native, m) {
   m.attr("RPC_ALLOCATE") = static_cast<int>(kRpcAllocate);
   m.attr("RPC_PRE_START") = static_cast<int>(kRpcPreStart);
 
+  py::class_<ContentionDetector>(m, "ContentionDetector")  // grpc.coreEscape's decision (tests)
+      .def(py::init<>())
+      .def("note", &ContentionDetector::note, py::arg("svc_ns"), py::arg("now_ns"))
+      .def_property_readonly("best_ns", &ContentionDetector::best_ns)
+      .def_property_readonly("last_median_ns", &ContentionDetector::last_median_ns);
+  m.def("parse_cpu_list", [](const std::string& s) { return parse_cpu_list(s.c_str()); });
   py::class_<DeviceTable, std::shared_ptr<DeviceTable>>(m, "DeviceTable")
       .def("inherit_stats", &DeviceTable::inherit_stats, py::arg("prev"))
       .def("wait_change", &DeviceTable::wait_change, py::call_guard<py::gil_scoped_release>(), py::arg("seen"),
@@ -753,6 +760,8 @@ PYBIND11_MODULE(_native, m) {
       .def("set_active_window_ms", &GrpcServer::set_active_window_ms, py::arg("ms"))
       .def("set_peek_reads", &GrpcServer::set_peek_reads, py::arg("on"))
       .def("set_poll_gap_ns", &GrpcServer::set_poll_gap_ns, py::arg("ns"))
+      .def("set_core_escape", &GrpcServer::set_core_escape, py::arg("on"))
+      .def_property_readonly("core_escapes", &GrpcServer::core_escapes)
       .def_property_readonly("idle_wakeups", &GrpcServer::idle_wakeups)
       .def("add_table", &GrpcServer::set_table)
       .def("start", &GrpcServer::start, py::call_guard<py::gil_scoped_release>())

@@ -1,0 +1,110 @@
+#include "core_escape.h"
+
+#include <fcntl.h>
+#include <sched.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+
+namespace amdgpu_dp {
+
+bool ContentionDetector::note(int64_t svc_ns, int64_t now_ns) {
+  ring_[n_++] = svc_ns;
+  if (n_ < kWindow) return false;
+  n_ = 0;
+  int64_t w[kWindow];
+  std::copy(ring_, ring_ + kWindow, w);
+  std::nth_element(w, w + kWindow / 2, w + kWindow);
+  const int64_t m = w[kWindow / 2];
+  last_median_ = m;
+  if (best_ == 0 || m < best_) {
+    best_ = m;
+  } else {
+    best_ = std::min(m, best_ + best_ / 256);  // drifts up 0.4 % a window: a host that got slower is learnt
+  }
+  if (m * 100 > best_ * kRatioPct) {
+    ++strikes_;
+  } else {
+    strikes_ = 0;
+  }
+  if (strikes_ < kStrikes || now_ns - last_move_ < kMinGapNs) return false;
+  strikes_ = 0;
+  last_move_ = now_ns;
+  return true;
+}
+
+std::vector<int> parse_cpu_list(const char* s) {
+  std::vector<int> out;
+  while (s && *s) {
+    char* end = nullptr;
+    const long a = std::strtol(s, &end, 10);
+    if (end == s) break;
+    long b = a;
+    s = end;
+    if (*s == '-') {
+      ++s;
+      b = std::strtol(s, &end, 10);
+      if (end == s) break;
+      s = end;
+    }
+    for (long c = a; c <= b && c - a < 4096; ++c) out.push_back(static_cast<int>(c));
+    while (*s == ',' || *s == '\n' || *s == ' ') ++s;
+  }
+  return out;
+}
+
+namespace {
+
+std::vector<int> read_list(const std::string& path) {
+  char buf[4096];
+  const int fd = ::open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return {};
+  const ssize_t r = ::read(fd, buf, sizeof(buf) - 1);
+  ::close(fd);
+  if (r <= 0) return {};
+  buf[r] = 0;
+  return parse_cpu_list(buf);
+}
+
+std::vector<int> l3_of(int cpu) {
+  const std::string base = "/sys/devices/system/cpu/cpu" + std::to_string(cpu) + "/cache/index";
+  for (int i = 0; i < 8; ++i) {
+    char lvl[8] = {};
+    const int fd = ::open((base + std::to_string(i) + "/level").c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) continue;
+    const ssize_t r = ::read(fd, lvl, sizeof(lvl) - 1);
+    ::close(fd);
+    if (r > 0 && lvl[0] == '3') return read_list(base + std::to_string(i) + "/shared_cpu_list");
+  }
+  return {};
+}
+
+}  // namespace
+
+int escape_core(unsigned rotate) {
+  const int cpu = sched_getcpu();
+  if (cpu < 0) return -1;
+  const std::vector<int> sib =
+      read_list("/sys/devices/system/cpu/cpu" + std::to_string(cpu) + "/topology/thread_siblings_list");
+  if (sib.size() < 2) return -1;  // no SMT: no core to share
+  cpu_set_t allowed;
+  CPU_ZERO(&allowed);
+  if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return -1;
+  std::vector<int> cand;
+  for (const int c : l3_of(cpu))
+    if (c >= 0 && c < CPU_SETSIZE && CPU_ISSET(c, &allowed) && std::find(sib.begin(), sib.end(), c) == sib.end())
+      cand.push_back(c);
+  if (cand.empty()) return -1;
+  const int target = cand[rotate % cand.size()];
+  cpu_set_t one;
+  CPU_ZERO(&one);
+  CPU_SET(target, &one);
+  if (sched_setaffinity(0, sizeof(one), &one) != 0) return -1;  // moves this thread now
+  (void)!sched_setaffinity(0, sizeof(allowed), &allowed);       // and leaves it there
+  return target;
+}
+
+}  // namespace amdgpu_dp

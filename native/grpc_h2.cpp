@@ -1,5 +1,6 @@
 #include "grpc_h2.h"
 
+#include "core_escape.h"
 #include "hpack.h"
 #include "pbwire.h"
 
@@ -1187,6 +1188,8 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
   int64_t spin_until = 0;  // busy-poll window end (mono ns); 0 = closed
   SpinGuard guard;
   bool polite = false;  // the open window gives way to other threads (see SpinGuard)
+  ContentionDetector contention;  // grpc.coreEscape
+  unsigned escape_rotate = static_cast<unsigned>(w->index);
   while (!stop_.load(std::memory_order_relaxed)) {
     if (table_gen_.load(std::memory_order_acquire) != table_gen) {
       // hot table swap (set_table): serve from the new table from here on and send every
@@ -1417,9 +1420,14 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
       }
       if (!trace_pending.empty()) send_begin = mono_ns();
       const bool alive = flush(c);  // the response goes out first; the bookkeeping follows
+      // (a call answered inside a busy-poll window: its service time feeds the core
+      // contention check, grpc.coreEscape)
+      const int64_t sent_at = got_input && wake_spin && core_escape_.load(std::memory_order_relaxed) ? mono_ns() : 0;
       if (alive && c->peeked) consume_peeked(c);
       if (!trace_pending.empty()) stamp_sent();
       if (!pending_obs.empty()) apply_observes();
+      if (sent_at && contention.note(sent_at - wake_ts, sent_at) && escape_core(escape_rotate++) >= 0)
+        core_escapes_.fetch_add(1, std::memory_order_relaxed);
       if (got_input) {
         got_input = false;
         const int64_t window = admitting ? std::max(spin_ns, admission_ns) : spin_ns;

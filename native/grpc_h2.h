@@ -145,6 +145,10 @@ class GrpcServer {
   // window the worker pauses this long (PAUSE instructions) instead of one PAUSE, so a
   // client on the worker's SMT sibling gets most of the core.  0 = one PAUSE.
   void set_poll_gap_ns(int ns) { poll_gap_ns_.store(std::max(0, std::min(ns, 100000))); }
+  // grpc.coreEscape: a worker whose calls inside a busy-poll window run 35 % slower than
+  // its own best moves to another core of its L3 (core_escape.h).  core_escapes(): moves.
+  void set_core_escape(bool on) { core_escape_.store(on); }
+  uint64_t core_escapes() const { return core_escapes_.load(); }
   // Epoll wake-ups of the workers that found nothing to do (timeouts), all workers.
   uint64_t idle_wakeups() const { return idle_wakeups_.load(); }
   std::vector<int> worker_connections() const;  // connections owned per worker thread
@@ -186,6 +190,8 @@ class GrpcServer {
   std::atomic<int> active_window_ms_{0};
   std::atomic<bool> peek_reads_{false};
   std::atomic<int> poll_gap_ns_{0};
+  std::atomic<bool> core_escape_{false};
+  std::atomic<uint64_t> core_escapes_{0};
   std::atomic<uint64_t> idle_wakeups_{0};
   std::atomic<uint64_t> warm_ticks_{0};
   // table_ and table_gen_ change together under swap_mu_ (never held across anything else);

@@ -4,7 +4,9 @@ On a shared host the scheduler sometimes runs the gRPC worker on the SMT sibling
 client's CPU, and those batches take ~4.5 us instead of ~2.6 (bench.py `placement`): the
 worker's busy-poll loop and the client share one core.  This probe pins the client thread
 to one CPU and the daemon's gRPC workers either to its SMT sibling or to another core of
-the same L3, for one daemon per pollGapNs value, and alternates daemons and placements
+the same L3, or starts them on the sibling and then lets them go anywhere (what a busy
+host's scheduler does; grpc.coreEscape is then free to move them), for one daemon per
+pollGapNs value (or per --arms entry), and alternates daemons and placements
 batch by batch (rounds), so every value meets the same moments of the host.  The bare
 spin exchange between the same CPU pairs is the floor.
 
@@ -55,6 +57,14 @@ def worker_tids(pid):
     return out
 
 
+def _last_cpu(pid, tid):
+    try:
+        with open("/proc/%d/task/%d/stat" % (pid, tid)) as f:
+            return int(f.read().rsplit(")", 1)[1].split()[36])  # field 39: processor
+    except (OSError, ValueError, IndexError):
+        return -1
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gaps", default="0,200,500")
@@ -96,20 +106,35 @@ def main() -> int:
         os.sched_setaffinity(0, {client})  # this thread is the client
         for d in daemons:
             d["h2"].bench_unary(v1beta1.METHOD_ALLOCATE, d["req"], 2000)  # warm
-        got = {(d["gap"], w): [] for d in daemons for w in ("smt_sibling", "same_l3")}
+        wheres = ("smt_sibling", "same_l3", "sibling_start")
+        got = {(d["gap"], w): [] for d in daemons for w in wheres}
+        ended = {(d["gap"], "sibling_start"): [] for d in daemons}
         for r in range(a.rounds):
             order = daemons if r % 2 == 0 else list(reversed(daemons))
             for d in order:
-                places = (("smt_sibling", sib), ("same_l3", other))
-                for where, cpu in (places if r % 2 == 0 else tuple(reversed(places))):
+                full = os.sched_getaffinity(d["proc"].pid)
+                # pinned to the client's sibling / to another core; or started on the sibling
+                # and then free to go anywhere (what the scheduler does on a busy host)
+                places = (("smt_sibling", sib, None), ("same_l3", other, None), ("sibling_start", sib, full))
+                for where, cpu, then in (places if r % 2 == 0 else tuple(reversed(places))):
                     for tid in d["workers"]:
                         try:
                             os.sched_setaffinity(tid, {cpu})
                         except OSError:
                             pass
-                    time.sleep(0.005)
+                    # (a sibling start waits out the escape's 100 ms gap that a pinned batch's
+                    # failed attempt may have started)
+                    time.sleep(0.15 if then is not None else 0.005)
+                    if then is not None:
+                        for tid in d["workers"]:
+                            try:
+                                os.sched_setaffinity(tid, then)
+                            except OSError:
+                                pass
                     lat = d["h2"].bench_unary(v1beta1.METHOD_ALLOCATE, d["req"], a.batch)
                     got[(d["gap"], where)].append(round(statistics.median(lat) * 1e6, 3))
+                    if then is not None:
+                        ended[(d["gap"], where)].append(sorted({_last_cpu(d["proc"].pid, t) for t in d["workers"]}))
         sizes = (9 + 80 + 9 + 5 + len(daemons[0]["req"]), 9 + 20 + 9 + 5 + 60 + 9 + 16)
         floors, floors_peek = {}, {}
         for where, cpu in (("smt_sibling", sib), ("same_l3", other)):
@@ -122,9 +147,10 @@ def main() -> int:
         res["allocate"] = {}
         for g in gaps:
             row = {}
-            for where in ("smt_sibling", "same_l3"):
+            for where in wheres:
                 xs = got[(g, where)]
                 row[where] = {"p50_of_batches_us": round(statistics.median(xs), 3), "batches_us": xs}
+            row["sibling_start"]["worker_cpus_after"] = ended[(g, "sibling_start")]
             res["allocate"][g] = row
     finally:
         for d in daemons:

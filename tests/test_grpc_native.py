@@ -943,3 +943,52 @@ def test_client_honours_goaway_last_stream_id(n, tmp_path, last_sid):
     finally:
         c.close()
         t.join(5)
+
+
+def test_contention_detector_moves_only_on_a_sustained_slowdown(n):
+    """grpc.coreEscape's decision: 32-call windows against the worker's own best window;
+    two windows in a row 35 % over it ask for a move, at most once per 100 ms; a slow
+    host is learnt (the best drifts up 0.4 % a window)."""
+    d = n.ContentionDetector()
+    t = 0
+    moves = []
+
+    def feed(svc_ns, windows):
+        nonlocal t
+        for _ in range(32 * windows):
+            t += 3000
+            if d.note(svc_ns, t):
+                moves.append(t)
+    feed(1360, 5)
+    assert d.best_ns == 1360 and not moves
+    feed(1700, 2)  # 25 % over: noise, not contention
+    assert not moves
+    feed(1970, 1)  # one slow window: not yet
+    assert not moves
+    feed(1970, 1)  # the second in a row
+    assert len(moves) == 1
+    feed(1970, 4)  # still slow, but within 100 ms of the move
+    assert len(moves) == 1
+    t += 200_000_000
+    feed(1970, 2)
+    assert len(moves) == 2
+    # a host that got slower for good: the best drifts up until nothing is "over" it
+    e = n.ContentionDetector()
+    for _ in range(32):
+        e.note(1000, 1)
+    for _ in range(32 * 80):
+        e.note(1300, 1)
+    assert 1300 * 100 <= e.best_ns * 135 and e.best_ns <= 1300
+
+
+def test_parse_cpu_list(n):
+    assert n.parse_cpu_list("0-3,8,10-11\n") == [0, 1, 2, 3, 8, 10, 11]
+    assert n.parse_cpu_list("5") == [5]
+    assert n.parse_cpu_list("") == []
+
+
+def test_core_escape_is_off_by_default_and_counts(n, plugin_dir):
+    srv = n.GrpcServer(os.path.join(plugin_dir, "esc.sock"), 2)
+    assert srv.core_escapes == 0
+    srv.set_core_escape(True)
+    srv.set_core_escape(False)
