@@ -1,12 +1,15 @@
 #include "core_escape.h"
 
+#include <dirent.h>
 #include <fcntl.h>
 #include <sched.h>
+#include <sys/socket.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 
 namespace amdgpu_dp {
@@ -83,6 +86,50 @@ std::vector<int> l3_of(int cpu) {
 }
 
 }  // namespace
+
+bool peer_on_sibling(int fd, int cpu) {
+  if (fd < 0 || cpu < 0) return false;
+  struct ucred cr {};
+  socklen_t len = sizeof(cr);
+  if (getsockopt(fd, SOL_SOCKET, SO_PEERCRED, &cr, &len) != 0 || cr.pid <= 0) return false;
+  std::vector<int> sib = read_list("/sys/devices/system/cpu/cpu" + std::to_string(cpu) + "/topology/thread_siblings_list");
+  sib.erase(std::remove(sib.begin(), sib.end(), cpu), sib.end());
+  if (sib.empty()) return false;
+  const std::string base = "/proc/" + std::to_string(cr.pid) + "/task";
+  DIR* d = opendir(base.c_str());
+  if (!d) return false;
+  bool found = false;
+  int seen = 0;
+  while (const dirent* e = readdir(d)) {
+    if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
+    if (++seen > 1024) break;
+    char buf[1024];
+    const int sfd = ::open((base + "/" + e->d_name + "/stat").c_str(), O_RDONLY | O_CLOEXEC);
+    if (sfd < 0) continue;
+    const ssize_t r = ::read(sfd, buf, sizeof(buf) - 1);
+    ::close(sfd);
+    if (r <= 0) continue;
+    buf[r] = 0;
+    const char* p = std::strrchr(buf, ')');  // the command name may hold spaces
+    if (!p) continue;
+    // fields after the name: state is field 3, the CPU it last ran on field 39
+    int field = 2;
+    long last_cpu = -1;
+    for (const char* q = p + 1; *q; ++q) {
+      if (*q != ' ') continue;
+      if (++field == 39) {
+        last_cpu = std::strtol(q + 1, nullptr, 10);
+        break;
+      }
+    }
+    if (last_cpu >= 0 && std::find(sib.begin(), sib.end(), static_cast<int>(last_cpu)) != sib.end()) {
+      found = true;
+      break;
+    }
+  }
+  closedir(d);
+  return found;
+}
 
 int escape_core(unsigned rotate) {
   const int cpu = sched_getcpu();

@@ -7,9 +7,10 @@
 // service time (request read -> answer sent) grow.  ContentionDetector watches it per
 // 32-call window against the worker's own best window (which drifts up 0.4 % a window, so a
 // host that got slower for good is learnt); two windows in a row 35 % over
-// it, on a CPU that has an SMT sibling, and the worker moves itself to another core of
-// its L3 (escape_core): pinned there for the move, then given its whole allowed set back,
-// which leaves it where it is.  At most one move per 100 ms.
+// it, and peer_on_sibling checks whether the worker's SMT sibling is where its client
+// runs; only then does the worker move itself to another core of its L3
+// (escape_core): pinned there for the move, then given its whole allowed set back, which
+// leaves it where it is.  At most one check per 100 ms.
 #pragma once
 
 #include <cstdint>
@@ -36,6 +37,12 @@ class ContentionDetector {
   int strikes_ = 0;
   int64_t last_move_ = -kMinGapNs;  // (the first move is never held back)
 };
+
+// Tells the client's SMT sibling apart from other slowdowns before a move: does a thread
+// of the process at the other end of unix socket `fd` (SO_PEERCRED) last run on an SMT
+// sibling of `cpu`?  False when the peer is not visible in this PID namespace (kubelet
+// seen from an unprivileged pod), so the check, and the move, never happen there.
+bool peer_on_sibling(int fd, int cpu);
 
 // Moves the calling thread to another core of its current CPU's L3 (an allowed CPU that
 // is not an SMT sibling of the current one; `rotate` picks among them).  Returns the CPU

@@ -992,3 +992,22 @@ def test_core_escape_is_off_by_default_and_counts(n, plugin_dir):
     assert srv.core_escapes == 0
     srv.set_core_escape(True)
     srv.set_core_escape(False)
+
+
+def test_peer_on_sibling_reads_the_peer_threads_cpus(n, tmp_path):
+    """The escape's check: SO_PEERCRED names the client process, whose threads' last CPUs
+    (/proc/<pid>/task/*/stat field 39) are compared with the SMT siblings of a CPU.  On a
+    host without SMT there is never a sibling."""
+    import socket as socket_mod
+    a, b = socket_mod.socketpair(socket_mod.AF_UNIX, socket_mod.SOCK_STREAM)
+    try:
+        cpu = os.sched_getaffinity(0).pop()
+        sib_path = "/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list" % cpu
+        sibs = n.parse_cpu_list(open(sib_path).read()) if os.path.exists(sib_path) else [cpu]
+        got = n.peer_on_sibling(b.fileno(), cpu)
+        if len(sibs) < 2:
+            assert got is False
+        assert n.peer_on_sibling(-1, cpu) is False
+    finally:
+        a.close()
+        b.close()
