@@ -460,7 +460,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("best_ns", &ContentionDetector::best_ns)
       .def_property_readonly("last_median_ns", &ContentionDetector::last_median_ns);
   m.def("parse_cpu_list", [](const std::string& s) { return parse_cpu_list(s.c_str()); });
-  m.def("peer_on_sibling", &peer_on_sibling, py::arg("fd"), py::arg("cpu"));
+  m.def("peer_on_sibling", &peer_on_sibling, py::arg("fd"), py::arg("cpu"), py::arg("now_ns") = 0);
   py::class_<DeviceTable, std::shared_ptr<DeviceTable>>(m, "DeviceTable")
       .def("inherit_stats", &DeviceTable::inherit_stats, py::arg("prev"))
       .def("wait_change", &DeviceTable::wait_change, py::call_guard<py::gil_scoped_release>(), py::arg("seen"),

@@ -87,7 +87,29 @@ std::vector<int> l3_of(int cpu) {
 
 }  // namespace
 
-bool peer_on_sibling(int fd, int cpu) {
+namespace {
+
+// the CPU thread `tid` of `pid` last ran on (field 39 of its stat), -1 unknown
+long last_cpu_of(const std::string& task_dir) {
+  char buf[1024];
+  const int sfd = ::open((task_dir + "/stat").c_str(), O_RDONLY | O_CLOEXEC);
+  if (sfd < 0) return -1;
+  const ssize_t r = ::read(sfd, buf, sizeof(buf) - 1);
+  ::close(sfd);
+  if (r <= 0) return -1;
+  buf[r] = 0;
+  const char* p = std::strrchr(buf, ')');  // the command name may hold spaces
+  if (!p) return -1;
+  int field = 2;  // state is field 3
+  for (const char* q = p + 1; *q; ++q)
+    if (*q == ' ' && ++field == 39) return std::strtol(q + 1, nullptr, 10);
+  return -1;
+}
+
+}  // namespace
+
+bool peer_on_sibling(int fd, int cpu, int64_t now_ns) {
+  thread_local int64_t last_scan = -1'000'000'000'000LL;
   if (fd < 0 || cpu < 0) return false;
   struct ucred cr {};
   socklen_t len = sizeof(cr);
@@ -95,7 +117,11 @@ bool peer_on_sibling(int fd, int cpu) {
   std::vector<int> sib = read_list("/sys/devices/system/cpu/cpu" + std::to_string(cpu) + "/topology/thread_siblings_list");
   sib.erase(std::remove(sib.begin(), sib.end(), cpu), sib.end());
   if (sib.empty()) return false;
+  auto on_sib = [&](long c) { return c >= 0 && std::find(sib.begin(), sib.end(), static_cast<int>(c)) != sib.end(); };
   const std::string base = "/proc/" + std::to_string(cr.pid) + "/task";
+  if (on_sib(last_cpu_of(base + "/" + std::to_string(cr.pid)))) return true;  // the main thread
+  if (now_ns != 0 && now_ns - last_scan < 100'000'000) return false;
+  last_scan = now_ns;
   DIR* d = opendir(base.c_str());
   if (!d) return false;
   bool found = false;
@@ -103,26 +129,7 @@ bool peer_on_sibling(int fd, int cpu) {
   while (const dirent* e = readdir(d)) {
     if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
     if (++seen > 1024) break;
-    char buf[1024];
-    const int sfd = ::open((base + "/" + e->d_name + "/stat").c_str(), O_RDONLY | O_CLOEXEC);
-    if (sfd < 0) continue;
-    const ssize_t r = ::read(sfd, buf, sizeof(buf) - 1);
-    ::close(sfd);
-    if (r <= 0) continue;
-    buf[r] = 0;
-    const char* p = std::strrchr(buf, ')');  // the command name may hold spaces
-    if (!p) continue;
-    // fields after the name: state is field 3, the CPU it last ran on field 39
-    int field = 2;
-    long last_cpu = -1;
-    for (const char* q = p + 1; *q; ++q) {
-      if (*q != ' ') continue;
-      if (++field == 39) {
-        last_cpu = std::strtol(q + 1, nullptr, 10);
-        break;
-      }
-    }
-    if (last_cpu >= 0 && std::find(sib.begin(), sib.end(), static_cast<int>(last_cpu)) != sib.end()) {
+    if (on_sib(last_cpu_of(base + "/" + e->d_name))) {
       found = true;
       break;
     }

@@ -10,7 +10,9 @@
 // it, and peer_on_sibling checks whether the worker's SMT sibling is where its client
 // runs; only then does the worker move itself to another core of its L3
 // (escape_core): pinned there for the move, then given its whole allowed set back, which
-// leaves it where it is.  At most one check per 100 ms.
+// leaves it where it is.  At most one check per 10 ms; the peer's other threads are
+// scanned at most once per 100 ms (its main thread, a closed-loop client's usual caller,
+// every time).
 #pragma once
 
 #include <cstdint>
@@ -23,7 +25,7 @@ class ContentionDetector {
   static constexpr int kWindow = 32;
   static constexpr int kRatioPct = 135;
   static constexpr int kStrikes = 2;
-  static constexpr int64_t kMinGapNs = 100'000'000;
+  static constexpr int64_t kMinGapNs = 10'000'000;
   // One call's service time; true when the worker should move now.
   bool note(int64_t svc_ns, int64_t now_ns);
   int64_t best_ns() const { return best_; }
@@ -42,7 +44,7 @@ class ContentionDetector {
 // of the process at the other end of unix socket `fd` (SO_PEERCRED) last run on an SMT
 // sibling of `cpu`?  False when the peer is not visible in this PID namespace (kubelet
 // seen from an unprivileged pod), so the check, and the move, never happen there.
-bool peer_on_sibling(int fd, int cpu);
+bool peer_on_sibling(int fd, int cpu, int64_t now_ns = 0);
 
 // Moves the calling thread to another core of its current CPU's L3 (an allowed CPU that
 // is not an SMT sibling of the current one; `rotate` picks among them).  Returns the CPU

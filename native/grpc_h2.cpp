@@ -1426,7 +1426,7 @@ void GrpcServer::run(Worker* w, std::shared_ptr<DeviceTable> table, uint64_t tab
       if (alive && c->peeked) consume_peeked(c);
       if (!trace_pending.empty()) stamp_sent();
       if (!pending_obs.empty()) apply_observes();
-      if (sent_at && alive && contention.note(sent_at - wake_ts, sent_at) && peer_on_sibling(c->fd, sched_getcpu()) &&
+      if (sent_at && alive && contention.note(sent_at - wake_ts, sent_at) && peer_on_sibling(c->fd, sched_getcpu(), sent_at) &&
           escape_core(escape_rotate++) >= 0)
         core_escapes_.fetch_add(1, std::memory_order_relaxed);
       if (got_input) {

@@ -947,7 +947,7 @@ def test_client_honours_goaway_last_stream_id(n, tmp_path, last_sid):
 
 def test_contention_detector_moves_only_on_a_sustained_slowdown(n):
     """grpc.coreEscape's decision: 32-call windows against the worker's own best window;
-    two windows in a row 35 % over it ask for a move, at most once per 100 ms; a slow
+    two windows in a row 35 % over it ask for a move, at most once per 10 ms; a slow
     host is learnt (the best drifts up 0.4 % a window)."""
     d = n.ContentionDetector()
     t = 0
@@ -967,9 +967,9 @@ def test_contention_detector_moves_only_on_a_sustained_slowdown(n):
     assert not moves
     feed(1970, 1)  # the second in a row
     assert len(moves) == 1
-    feed(1970, 4)  # still slow, but within 100 ms of the move
+    feed(1970, 4)  # still slow, but within 10 ms of the move
     assert len(moves) == 1
-    t += 200_000_000
+    t += 20_000_000
     feed(1970, 2)
     assert len(moves) == 2
     # a host that got slower for good: the best drifts up until nothing is "over" it
