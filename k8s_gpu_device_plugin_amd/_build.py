@@ -30,6 +30,7 @@ import shutil
 import subprocess
 import sys
 import sysconfig
+import time
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG_DIR)
@@ -141,7 +142,11 @@ def _compile_objects(sources, obj_dir, extra_flags, force, jobs, cxx=None, src_d
 
     def one(pair):
         src, obj = pair
+        started = time.time()
         _run([cxx] + extra_flags + ["-c", src, "-o", obj], "compile " + os.path.basename(src))
+        # the object is as old as the sources it read: one edited while it compiled (a
+        # header changed under a long ASan build) leaves it stale for the next build
+        os.utime(obj, (started, started))
 
     if todo:
         with concurrent.futures.ThreadPoolExecutor(max_workers=jobs) as ex:

@@ -120,7 +120,7 @@ class HealthConfig:
     # clears the uncorrectable-ECC latch without amdsmi event notification
     resetQuery: bool = True
     # amdsmi backend: re-read the ECC totals when the driver's RAS event state (fatal error,
-    # poison creation / consumption) moved and every 10 s otherwise, instead of every sample
+    # poison creation / consumption) moved and every 30 s otherwise, instead of every sample
     # (the per-block reads query the firmware's error banks: ~0.27 ms of CPU per GPU per
     # sample on MI355X).  false = every sample, gated by the block files changing
     eccEventGate: bool = True

@@ -729,7 +729,9 @@ class AmdSmiBackend : public Backend {
   // skew of the blob's and, separately, blob status equal to the link-status call.
   // Between refreshes a verified GPU takes counters (and, if verified, status) from the
   // blob and peers / rates from the cache; an unverified one takes the full path.
-  static constexpr int64_t kLinkRefreshNs = 10'000'000'000;
+  // (60 s: with the sampler's 5 s idle period a shorter one made every other idle sample
+  // take the ~1 ms full path)
+  static constexpr int64_t kLinkRefreshNs = 60'000'000'000;
   struct LinkCache {
     int64_t read_ns = 0;
     bool counters_ok = false;  // blob counters line up with link_metrics
@@ -741,7 +743,7 @@ class AmdSmiBackend : public Backend {
   };
   // RAS retired-page records change only when the driver retires a page: re-read them
   // every kBadPageRefreshNs and report the cached counts in between.
-  static constexpr int64_t kBadPageRefreshNs = 10'000'000'000LL;
+  static constexpr int64_t kBadPageRefreshNs = 60'000'000'000LL;
   struct BadPages {
     int64_t read_ns = 0;
     int64_t reserved = -1, pending = -1, unreservable = -1;
@@ -758,7 +760,7 @@ class AmdSmiBackend : public Backend {
   //    event, are at most that old);
   //  * otherwise the block files are kept open and read each sample, and amdsmi is asked
   //    when any of them changed (and every kEccRefreshNs).
-  static constexpr int64_t kEccRefreshNs = 10'000'000'000LL;
+  static constexpr int64_t kEccRefreshNs = 30'000'000'000LL;
   struct EccWatch {
     bool opened = false;
     std::vector<std::unique_ptr<SysfsAttr>> files;  // ras/aca_* (MI355X) or ras/*_err_count

@@ -352,7 +352,7 @@ class Backend : public std::enable_shared_from_this<Backend> {
   void set_reset_query(bool on) { reset_query_.store(on); }
   bool reset_query() const { return reset_query_.load(); }
   // health.eccEventGate: the ECC totals are re-read when the driver's RAS event state
-  // (fatal errors, poison creation / consumption) moved, and every 10 s otherwise,
+  // (fatal errors, poison creation / consumption) moved, and every 30 s otherwise,
   // instead of every sample (amdsmi backend; where the kernel has that file).
   void set_ecc_event_gate(bool on) { ecc_event_gate_.store(on); }
   bool ecc_event_gate() const { return ecc_event_gate_.load(); }

@@ -114,7 +114,7 @@ def test_amdsmi_sample_cost_breakdown(amdsmi_backend):
     assert set(per) == {"gpu_metrics", "partition_metrics", "vram_usage", "ecc_count", "xgmi_links", "bad_pages"}
     assert sum(per.values()) < 50e3
     # ECC totals: amdsmi is asked again only when the RAS event state moved (or every
-    # 10 s); one-pool VRAM is read from sysfs once it agreed with amdsmi
+    # 30 s); one-pool VRAM is read from sysfs once it agreed with amdsmi
     ras = "/sys/bus/pci/devices/%s/ras" % gpus[0].bdf.lower()
     if os.path.exists(ras + "/event_state"):
         assert paths["ecc_count_reads_event_gated"] >= 15, paths
