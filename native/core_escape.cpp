@@ -85,11 +85,8 @@ std::vector<int> l3_of(int cpu) {
   return {};
 }
 
-}  // namespace
-
-namespace {
-
-// the CPU thread `tid` of `pid` last ran on (field 39 of its stat), -1 unknown
+// the CPU a thread (its /proc/<pid>/task/<tid> directory) last ran on: field 39 of its
+// stat, -1 unknown
 long last_cpu_of(const std::string& task_dir) {
   char buf[1024];
   const int sfd = ::open((task_dir + "/stat").c_str(), O_RDONLY | O_CLOEXEC);
@@ -120,6 +117,7 @@ bool peer_on_sibling(int fd, int cpu, int64_t now_ns) {
   auto on_sib = [&](long c) { return c >= 0 && std::find(sib.begin(), sib.end(), static_cast<int>(c)) != sib.end(); };
   const std::string base = "/proc/" + std::to_string(cr.pid) + "/task";
   if (on_sib(last_cpu_of(base + "/" + std::to_string(cr.pid)))) return true;  // the main thread
+  // every thread (kubelet-like clients call from any of theirs): at most every 100 ms
   if (now_ns != 0 && now_ns - last_scan < 100'000'000) return false;
   last_scan = now_ns;
   DIR* d = opendir(base.c_str());

@@ -1,18 +1,16 @@
-// Core-contention escape for the gRPC workers (grpc.coreEscape).
+// Core-contention escape for the gRPC workers (grpc.coreEscape, off by default).
 //
 // A busy-polling worker that the scheduler woke on the SMT sibling of its client's CPU
 // shares one core with it for the rest of the burst: on the MI355X hosts an Allocate then
 // takes ~4.6 us instead of ~2.6, and the bare exchange 2.7 instead of 2.2
-// (scripts/smt_probe.py).  The worker cannot see kubelet's CPU, but it sees its own
-// service time (request read -> answer sent) grow.  ContentionDetector watches it per
-// 32-call window against the worker's own best window (which drifts up 0.4 % a window, so a
-// host that got slower for good is learnt); two windows in a row 35 % over
-// it, and peer_on_sibling checks whether the worker's SMT sibling is where its client
-// runs; only then does the worker move itself to another core of its L3
-// (escape_core): pinned there for the move, then given its whole allowed set back, which
-// leaves it where it is.  At most one check per 10 ms; the peer's other threads are
-// scanned at most once per 100 ms (its main thread, a closed-loop client's usual caller,
-// every time).
+// (scripts/smt_probe.py).  ContentionDetector watches the worker's service time (request
+// read -> answer sent) per 32-call window against its own best window, which drifts up
+// 0.4 % a window so that a host that got slower for good is learnt.  Two windows in a row
+// 35 % over it, at most once per 10 ms, and peer_on_sibling checks whether a thread of
+// the client process last ran on the worker's SMT sibling; only then does the worker
+// move itself to another core of its L3 (escape_core): pinned there for the move, then
+// given its whole allowed set back, which leaves it where it is.  docs/ROUND6.md has the
+// measurements, and why it stays off.
 #pragma once
 
 #include <cstdint>
