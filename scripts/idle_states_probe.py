@@ -1,3 +1,12 @@
+"""Does a ping-pong client's CPU enter cpuidle once per call?  (It does not: the check
+tried first for grpc.coreEscape's "is the client on my SMT sibling" question.)
+
+Pins the bare unix-socket exchange (the plugin's syscall pattern, tests/native/loadgen.cpp)
+between CPU 0 and its SMT sibling (128 on the MI355X hosts), then CPU 0 and CPU 1, and
+prints how often each CPU entered each cpuidle state during 10000 calls.
+
+    python scripts/idle_states_probe.py
+"""
 import os, sys, json, glob
 sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "/root/repo"))
 from k8s_gpu_device_plugin_amd import native
