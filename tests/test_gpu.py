@@ -151,8 +151,11 @@ def test_ecc_totals_are_amdsmi_s_with_or_without_the_event_gate(amdsmi_backend):
     assert reads["ecc_count_reads_event_gated"] == 0
     if os.path.isdir("/sys/bus/pci/devices/%s/ras" % gpus[0].bdf.lower()):
         assert reads["ecc_count_reads_unchanged"] >= 8, reads
-    assert {(x.ecc_correctable, x.ecc_uncorrectable) for x in off} == {(x.ecc_correctable, x.ecc_uncorrectable)
-                                                                        for x in on}
+    # the same counters either way (correctable errors may still be counted meanwhile: they
+    # only ever grow)
+    assert {x.ecc_uncorrectable for x in off} == {x.ecc_uncorrectable for x in on}
+    seq = [x.ecc_correctable for x in off + on]
+    assert seq == sorted(seq)
     assert off[0].ecc_uncorrectable >= 0
 
 
