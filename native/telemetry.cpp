@@ -420,22 +420,34 @@ int Exporter::sampler_step(int64_t* next, uint64_t gen, int interval_ms) {
 
 int Exporter::next_interval_ms(int interval_ms) {
   const int idle = idle_interval_ms_.load();
-  bool active = idle <= interval_ms;
-  if (!active) {
+  int step = interval_ms;
+  bool unread = false;
+  if (idle > interval_ms) {
     const int64_t now = mono_ns(), window = static_cast<int64_t>(active_window_ms_.load()) * 1000000;
-    active = now - started_ns_.load() < window || now - last_read_ns_.load(std::memory_order_relaxed) < window;
-  }
-  if (!active) {
-    std::shared_ptr<HealthMonitor> mon;
-    {
-      std::lock_guard<std::mutex> lk(run_mu_);
-      mon = monitor_;
+    const bool starting = now - started_ns_.load() < window;
+    const bool read = now - last_read_ns_.load(std::memory_order_relaxed) < window;
+    bool settling = false;
+    if (!starting) {
+      std::shared_ptr<HealthMonitor> mon;
+      {
+        std::lock_guard<std::mutex> lk(run_mu_);
+        mon = monitor_;
+      }
+      settling = mon && mon->settling();
     }
-    active = mon && mon->settling();
+    if (!starting && !settling) {
+      if (!read) {
+        step = idle;
+        unread = true;
+      } else if (const int64_t gap = read_gap_ns_.load(std::memory_order_relaxed); gap > 0) {
+        // scraped: about two samples per scrape interval, between the two periods (a
+        // Prometheus scraping every 15-30 s gets samples at most idleIntervalMs old)
+        step = static_cast<int>(std::max<int64_t>(interval_ms, std::min<int64_t>(idle, gap / 2000000)));
+      }
+    }
   }
-  idle_mode_.store(!active);
-  if (!active) idle_passes_.fetch_add(1, std::memory_order_relaxed);
-  const int step = active ? interval_ms : idle;
+  idle_mode_.store(unread);
+  if (step > interval_ms) idle_passes_.fetch_add(1, std::memory_order_relaxed);
   current_interval_ms_.store(step);
   return step;
 }
@@ -444,8 +456,10 @@ void Exporter::note_read() const {
   // (every scrape comes here: one relaxed load in the common case, a store at most every
   // 100 ms, the sampler woken only on the first read after it slowed down)
   const int64_t now = mono_ns();
-  if (now - last_read_ns_.load(std::memory_order_relaxed) < 100000000) return;
+  const int64_t prev = last_read_ns_.load(std::memory_order_relaxed);
+  if (now - prev < 100000000) return;
   last_read_ns_.store(now, std::memory_order_relaxed);
+  read_gap_ns_.store(prev != 0 ? now - prev : 0, std::memory_order_relaxed);
   if (idle_mode_.load(std::memory_order_relaxed) && !poke_.exchange(true)) {
     std::shared_ptr<Waker> w;
     {

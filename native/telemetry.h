@@ -86,8 +86,9 @@ class Exporter : public std::enable_shared_from_this<Exporter> {
   // Adaptive cadence (telemetry.idleIntervalMs / activeWindowS): the sampler runs every
   // idle_ms instead of the start() interval while nothing has read the GPU metrics for
   // window_ms, the health monitor is settled (HealthMonitor::settling) and the first
-  // window_ms after start() are over.  A scrape in that state wakes the sampler at once
-  // and restores the interval.  A sample costs ~1 ms of CPU per MI355X, most of it the
+  // window_ms after start() are over.  A scrape in that state wakes the sampler at once;
+  // while scraped (and settled) it samples about twice per scrape interval, never less
+  // often than idle_ms nor more often than the interval.  A sample costs ~1 ms of CPU per MI355X, most of it the
   // kernel fetching the firmware's metrics table (scripts/sysfs_cost_probe.py).
   // idle_ms <= the interval: always the interval.
   void set_idle_interval(int idle_ms, int window_ms) {
@@ -95,7 +96,7 @@ class Exporter : public std::enable_shared_from_this<Exporter> {
     active_window_ms_.store(window_ms > 0 ? window_ms : 0);
   }
   int current_interval_ms() const { return current_interval_ms_.load(); }
-  uint64_t idle_passes() const { return idle_passes_.load(); }
+  uint64_t idle_passes() const { return idle_passes_.load(); }  // passes slower than the interval
   int stalled_gpu() const;                 // lowest stalled GPU index, -1 = none
   std::vector<int> stalled_gpus() const;   // reported lost by the watchdog
   std::vector<int> blocked_gpus() const;   // stuck behind another GPU's call
@@ -252,6 +253,7 @@ class Exporter : public std::enable_shared_from_this<Exporter> {
   void note_read() const;
   std::atomic<int> idle_interval_ms_{0}, active_window_ms_{120000}, current_interval_ms_{0};
   mutable std::atomic<int64_t> last_read_ns_{0};
+  mutable std::atomic<int64_t> read_gap_ns_{0};  // between the last two recorded reads (0: one read)
   std::atomic<int64_t> started_ns_{0};
   std::atomic<bool> idle_mode_{false};
   mutable std::atomic<bool> poke_{false};

@@ -758,3 +758,33 @@ def test_idle_interval_off_or_below_the_interval_keeps_the_interval(n):
             assert ex.current_interval_ms == 30 and ex.idle_passes == 0
         finally:
             ex.stop()
+
+
+def test_sampler_follows_a_slow_scraper(n):
+    """While scraped and settled, the sampler runs about twice per scrape interval,
+    between telemetry.intervalMs and idleIntervalMs: a Prometheus scraping every 15-30 s
+    does not keep it at the 1 s interval."""
+    be = fixtures.build_backend("2gpu_spx")
+    m = n.HealthMonitor(be, 3)
+    m.set_gpu_count(2)
+    ex = n.Exporter()
+    gpus, _ = be.discover()
+    ex.set_inventory(gpus)
+    ex.set_idle_interval(800, 1500)
+    ex.start(be, 20, m)
+    try:
+        assert _wait_for(lambda: ex.current_interval_ms == 800, timeout=4)  # start window over, unread
+        for _ in range(4):  # a scraper every 300 ms
+            ex.render()
+            time.sleep(0.3)
+        assert _wait_for(lambda: 120 <= ex.current_interval_ms <= 180, timeout=2), ex.current_interval_ms
+        for _ in range(3):  # one every 1.2 s: samples every 600 ms
+            ex.render()
+            time.sleep(1.2)
+        assert 500 <= ex.current_interval_ms <= 700, ex.current_interval_ms
+        for _ in range(8):  # fast scrapes never push it below the interval
+            ex.render()
+            time.sleep(0.11)
+        assert _wait_for(lambda: 20 <= ex.current_interval_ms <= 60, timeout=2), ex.current_interval_ms
+    finally:
+        ex.stop()
