@@ -67,9 +67,10 @@ class SharingConfig:
 class TelemetryConfig:
     enabled: bool = True
     intervalMs: int = 1000
-    # while nothing has read the GPU metrics (/metrics, /gpu/metrics) for activeWindowS and
-    # every GPU's health is settled, sample every idleIntervalMs instead (0 = never slow
-    # down); the first read after that wakes the sampler and restores intervalMs
+    # while nothing has read the GPU metrics (/metrics) for activeWindowS and every GPU's
+    # health is settled, sample every idleIntervalMs instead (0 = never slow down); the
+    # first read after that wakes the sampler, and while scraped it samples about twice
+    # per scrape interval, between intervalMs and idleIntervalMs
     idleIntervalMs: int = 5000
     activeWindowS: float = 120.0
 
